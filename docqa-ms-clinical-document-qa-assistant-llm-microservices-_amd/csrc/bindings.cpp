@@ -1,0 +1,273 @@
+// bindings.cpp -- registers the gfx950 kernels as torch operators (torch.ops.docqa.*).
+//
+// Ops allocate their outputs through the PyTorch caching allocator and launch on the
+// current HIP stream, so they run under torch.cuda.graph capture (HIP graphs) and on
+// the side streams the pipeline uses for embed/search/generate overlap.
+#include <torch/library.h>
+#include <ATen/ATen.h>
+#include <c10/hip/HIPStream.h>
+#include <c10/hip/HIPGuard.h>
+
+#include "docqa_kernels.h"
+
+namespace {
+
+hipStream_t stream() { return c10::hip::getCurrentHIPStream().stream(); }
+
+#define CHECK_GPU(t) TORCH_CHECK((t).is_cuda(), #t " must be a GPU tensor")
+#define CHECK_BF16(t) TORCH_CHECK((t).scalar_type() == at::kBFloat16, #t " must be bfloat16")
+#define CHECK_I32(t) TORCH_CHECK((t).scalar_type() == at::kInt, #t " must be int32")
+#define CHECK_CONTIG(t) TORCH_CHECK((t).is_contiguous(), #t " must be contiguous")
+#define CHECK_RC(rc, name) TORCH_CHECK((rc) == 0, "docqa kernel " name " failed with code ", (rc))
+
+at::Tensor rmsnorm(const at::Tensor& x, const at::Tensor& w, double eps) {
+  CHECK_GPU(x); CHECK_BF16(x); CHECK_BF16(w); CHECK_CONTIG(x); CHECK_CONTIG(w);
+  const int H = x.size(-1);
+  TORCH_CHECK(w.numel() == H, "rmsnorm weight size mismatch");
+  c10::hip::HIPGuard g(x.device());
+  auto out = at::empty_like(x);
+  const int rows = x.numel() / H;
+  CHECK_RC(docqa_rmsnorm(x.data_ptr(), w.data_ptr(), out.data_ptr(), rows, H, (float)eps, stream()), "rmsnorm");
+  return out;
+}
+
+at::Tensor add_rmsnorm(const at::Tensor& x, at::Tensor residual, const at::Tensor& w, double eps) {
+  CHECK_GPU(x); CHECK_BF16(x); CHECK_BF16(residual); CHECK_BF16(w);
+  CHECK_CONTIG(x); CHECK_CONTIG(residual);
+  TORCH_CHECK(x.sizes() == residual.sizes(), "add_rmsnorm shape mismatch");
+  const int H = x.size(-1);
+  c10::hip::HIPGuard g(x.device());
+  auto out = at::empty_like(x);
+  CHECK_RC(docqa_add_rmsnorm(x.data_ptr(), residual.data_ptr(), w.data_ptr(), out.data_ptr(),
+                             x.numel() / H, H, (float)eps, stream()), "add_rmsnorm");
+  return out;
+}
+
+at::Tensor layernorm(const at::Tensor& x, const c10::optional<at::Tensor>& residual,
+                     const at::Tensor& gamma, const at::Tensor& beta, double eps) {
+  CHECK_GPU(x); CHECK_BF16(x); CHECK_CONTIG(x); CHECK_BF16(gamma); CHECK_BF16(beta);
+  const int H = x.size(-1);
+  const void* rp = nullptr;
+  if (residual.has_value()) {
+    CHECK_BF16(*residual); CHECK_CONTIG(*residual);
+    TORCH_CHECK(residual->sizes() == x.sizes(), "layernorm residual shape mismatch");
+    rp = residual->data_ptr();
+  }
+  c10::hip::HIPGuard g(x.device());
+  auto out = at::empty_like(x);
+  CHECK_RC(docqa_layernorm(x.data_ptr(), rp, gamma.data_ptr(), beta.data_ptr(), out.data_ptr(),
+                           x.numel() / H, H, (float)eps, stream()), "layernorm");
+  return out;
+}
+
+void rope_cache(at::Tensor qkv, const at::Tensor& positions, const at::Tensor& cos_sin,
+                const c10::optional<at::Tensor>& slot_mapping, at::Tensor k_cache,
+                at::Tensor v_cache, int64_t Hq, int64_t Hkv, int64_t D) {
+  CHECK_GPU(qkv); CHECK_BF16(qkv); CHECK_I32(positions);
+  TORCH_CHECK(cos_sin.scalar_type() == at::kFloat, "cos_sin must be fp32");
+  TORCH_CHECK(qkv.stride(-1) == 1, "qkv rows must be contiguous");
+  TORCH_CHECK(qkv.size(-1) == (Hq + 2 * Hkv) * D, "qkv width mismatch");
+  const int T = qkv.numel() / qkv.size(-1);
+  const int* sm = nullptr;
+  int BS = 1;
+  if (slot_mapping.has_value()) {
+    CHECK_I32(*slot_mapping);
+    sm = slot_mapping->data_ptr<int>();
+    CHECK_BF16(k_cache); CHECK_BF16(v_cache);
+    BS = k_cache.size(2);  // [num_blocks, Hkv, BS, D]
+  }
+  c10::hip::HIPGuard g(qkv.device());
+  CHECK_RC(docqa_rope_cache(qkv.data_ptr(), positions.data_ptr<int>(), cos_sin.data_ptr<float>(),
+                            sm, sm ? k_cache.data_ptr() : nullptr, sm ? v_cache.data_ptr() : nullptr,
+                            T, Hq, Hkv, D, qkv.size(-1), BS, stream()), "rope_cache");
+}
+
+at::Tensor silu_mul(const at::Tensor& gu) {
+  CHECK_GPU(gu); CHECK_BF16(gu); CHECK_CONTIG(gu);
+  const int I2 = gu.size(-1);
+  auto sizes = gu.sizes().vec();
+  sizes.back() = I2 / 2;
+  c10::hip::HIPGuard g(gu.device());
+  auto out = at::empty(sizes, gu.options());
+  CHECK_RC(docqa_silu_mul(gu.data_ptr(), out.data_ptr(), gu.numel() / I2, I2 / 2, stream()), "silu_mul");
+  return out;
+}
+
+at::Tensor bias_act(const at::Tensor& x, const at::Tensor& bias,
+                    const c10::optional<at::Tensor>& residual, bool gelu) {
+  CHECK_GPU(x); CHECK_BF16(x); CHECK_CONTIG(x); CHECK_BF16(bias);
+  const int N = x.size(-1);
+  TORCH_CHECK(bias.numel() == N, "bias size mismatch");
+  const void* rp = nullptr;
+  if (residual.has_value()) { CHECK_BF16(*residual); CHECK_CONTIG(*residual); rp = residual->data_ptr(); }
+  c10::hip::HIPGuard g(x.device());
+  auto out = at::empty_like(x);
+  CHECK_RC(docqa_bias_act(x.data_ptr(), bias.data_ptr(), rp, out.data_ptr(), x.numel() / N, N,
+                          gelu ? 1 : 0, stream()), "bias_act");
+  return out;
+}
+
+at::Tensor embedding(const at::Tensor& ids, const at::Tensor& table) {
+  CHECK_GPU(ids); CHECK_I32(ids); CHECK_BF16(table); CHECK_CONTIG(table);
+  const int H = table.size(1);
+  auto sizes = ids.sizes().vec();
+  sizes.push_back(H);
+  c10::hip::HIPGuard g(ids.device());
+  auto out = at::empty(sizes, table.options());
+  CHECK_RC(docqa_embedding(ids.data_ptr<int>(), table.data_ptr(), out.data_ptr(), ids.numel(), H, stream()), "embedding");
+  return out;
+}
+
+at::Tensor bert_embed_ln(const at::Tensor& ids, const at::Tensor& pos,
+                         const c10::optional<at::Tensor>& token_type, const at::Tensor& wte,
+                         const at::Tensor& wpe, const at::Tensor& wtt, const at::Tensor& gamma,
+                         const at::Tensor& beta, double eps) {
+  CHECK_GPU(ids); CHECK_I32(ids); CHECK_I32(pos); CHECK_BF16(wte);
+  const int H = wte.size(1);
+  const int* tt = nullptr;
+  if (token_type.has_value()) { CHECK_I32(*token_type); tt = token_type->data_ptr<int>(); }
+  c10::hip::HIPGuard g(ids.device());
+  auto out = at::empty({ids.numel(), H}, wte.options());
+  CHECK_RC(docqa_bert_embed_ln(ids.data_ptr<int>(), pos.data_ptr<int>(), tt, wte.data_ptr(),
+                               wpe.data_ptr(), wtt.data_ptr(), gamma.data_ptr(), beta.data_ptr(),
+                               out.data_ptr(), ids.numel(), H, (float)eps, stream()), "bert_embed_ln");
+  return out;
+}
+
+at::Tensor argmax(const at::Tensor& logits) {
+  CHECK_GPU(logits);
+  TORCH_CHECK(logits.dim() == 2 && logits.stride(1) == 1, "argmax wants [rows, V] with unit stride");
+  const bool bf = logits.scalar_type() == at::kBFloat16;
+  TORCH_CHECK(bf || logits.scalar_type() == at::kFloat, "argmax: bf16 or fp32 logits");
+  const int rows = logits.size(0), V = logits.size(1);
+  int splits = (V + 8191) / 8192;
+  if (splits > 64) splits = 64;
+  if (splits < 1) splits = 1;
+  c10::hip::HIPGuard g(logits.device());
+  auto ws_v = at::empty({rows * splits}, logits.options().dtype(at::kFloat));
+  auto ws_i = at::empty({rows * splits}, logits.options().dtype(at::kInt));
+  auto out = at::empty({rows}, logits.options().dtype(at::kLong));
+  CHECK_RC(docqa_argmax(logits.data_ptr(), rows, V, logits.stride(0), bf ? 1 : 0,
+                        ws_v.data_ptr<float>(), ws_i.data_ptr<int>(), splits,
+                        out.data_ptr<int64_t>(), stream()), "argmax");
+  return out;
+}
+
+at::Tensor sample(const at::Tensor& logits, const at::Tensor& inv_temp, const at::Tensor& top_k,
+                  const at::Tensor& top_p, const at::Tensor& u) {
+  CHECK_GPU(logits);
+  TORCH_CHECK(logits.scalar_type() == at::kFloat && logits.dim() == 2 && logits.stride(1) == 1,
+              "sample wants fp32 [rows, V]");
+  CHECK_I32(top_k);
+  c10::hip::HIPGuard g(logits.device());
+  auto out = at::empty({logits.size(0)}, logits.options().dtype(at::kLong));
+  CHECK_RC(docqa_sample(logits.data_ptr<float>(), logits.size(0), logits.size(1), logits.stride(0),
+                        inv_temp.data_ptr<float>(), top_k.data_ptr<int>(), top_p.data_ptr<float>(),
+                        u.data_ptr<float>(), out.data_ptr<int64_t>(), stream()), "sample");
+  return out;
+}
+
+at::Tensor paged_decode(const at::Tensor& q, const at::Tensor& k_cache, const at::Tensor& v_cache,
+                        const at::Tensor& block_tables, const at::Tensor& context_lens,
+                        int64_t Hq, int64_t max_context, double scale) {
+  // q: [B, >= Hq*D] rows (e.g. the packed QKV buffer), caches [NB, Hkv, BS, D]
+  CHECK_GPU(q); CHECK_BF16(q); CHECK_BF16(k_cache); CHECK_BF16(v_cache);
+  CHECK_I32(block_tables); CHECK_I32(context_lens); CHECK_CONTIG(block_tables);
+  TORCH_CHECK(q.stride(-1) == 1, "q rows must be contiguous");
+  const int B = q.size(0);
+  const int Hkv = k_cache.size(1), BS = k_cache.size(2), D = k_cache.size(3);
+  const int part = docqa_decode_part_tokens();
+  const int max_parts = (max_context + part - 1) / part;
+  c10::hip::HIPGuard g(q.device());
+  auto out = at::empty({B, Hq * D}, q.options());
+  auto tmp_out = at::empty({B, Hq, max_parts, D}, q.options().dtype(at::kFloat));
+  auto tmp_ml = at::empty({B, Hq, max_parts, 2}, q.options().dtype(at::kFloat));
+  CHECK_RC(docqa_paged_decode(q.data_ptr(), q.stride(0), k_cache.data_ptr(), v_cache.data_ptr(),
+                              block_tables.data_ptr<int>(), block_tables.size(1),
+                              context_lens.data_ptr<int>(), out.data_ptr(), Hq * D,
+                              tmp_out.data_ptr<float>(), tmp_ml.data_ptr<float>(), B, Hq, Hkv, D,
+                              BS, max_parts, (float)scale, stream()), "paged_decode");
+  return out;
+}
+
+at::Tensor flash_prefill(const at::Tensor& qkv, const at::Tensor& cu_seqlens, int64_t max_len,
+                         int64_t Hq, int64_t Hkv, int64_t D, double scale, bool causal) {
+  CHECK_GPU(qkv); CHECK_BF16(qkv); CHECK_I32(cu_seqlens);
+  TORCH_CHECK(qkv.stride(-1) == 1 && qkv.size(-1) == (Hq + 2 * Hkv) * D, "qkv layout mismatch");
+  const int T = qkv.numel() / qkv.size(-1);
+  const int B = cu_seqlens.numel() - 1;
+  c10::hip::HIPGuard g(qkv.device());
+  auto out = at::empty({T, Hq * D}, qkv.options());
+  CHECK_RC(docqa_flash_prefill(qkv.data_ptr(), qkv.size(-1), cu_seqlens.data_ptr<int>(),
+                               out.data_ptr(), Hq * D, B, max_len, Hq, Hkv, D, (float)scale,
+                               causal ? 1 : 0, stream()), "flash_prefill");
+  return out;
+}
+
+std::tuple<at::Tensor, at::Tensor> knn(const at::Tensor& xb, const at::Tensor& xb_norms,
+                                       const at::Tensor& xq, int64_t k, bool inner_product,
+                                       int64_t id_offset) {
+  CHECK_GPU(xb); CHECK_CONTIG(xb); CHECK_CONTIG(xq);
+  TORCH_CHECK(xq.scalar_type() == at::kFloat, "queries must be fp32");
+  const bool bf = xb.scalar_type() == at::kBFloat16;
+  TORCH_CHECK(bf || xb.scalar_type() == at::kFloat, "database must be fp32 or bf16");
+  TORCH_CHECK(xb.size(1) == xq.size(1), "dimension mismatch");
+  TORCH_CHECK(k >= 1 && docqa_knn_kpad(k) > 0, "k must be in [1, 32]");
+  const int N = xb.size(0), d = xb.size(1), nq = xq.size(0);
+  c10::hip::HIPGuard g(xb.device());
+  auto out_d = at::empty({nq, k}, xq.options());
+  auto out_i = at::empty({nq, k}, xq.options().dtype(at::kLong));
+  if (N == 0 || nq == 0) {
+    out_d.fill_(inner_product ? -3.4028234663852886e38 : 3.4028234663852886e38);
+    out_i.fill_(-1);
+    return {out_d, out_i};
+  }
+  const int nblk = docqa_knn_workspace_blocks(N);
+  const int kp = docqa_knn_kpad(k);
+  auto ws_d = at::empty({nq, nblk, kp}, xq.options());
+  auto ws_i = at::empty({nq, nblk, kp}, xq.options().dtype(at::kInt));
+  const float* norms = inner_product ? nullptr : xb_norms.data_ptr<float>();
+  CHECK_RC(docqa_knn(xb.data_ptr(), norms, N, d, bf ? 1 : 0, xq.data_ptr<float>(), nq, k,
+                     inner_product ? 1 : 0, ws_d.data_ptr<float>(), ws_i.data_ptr<int>(), nblk,
+                     out_d.data_ptr<float>(), out_i.data_ptr<int64_t>(), id_offset, stream()), "knn");
+  return {out_d, out_i};
+}
+
+}  // namespace
+
+TORCH_LIBRARY(docqa, m) {
+  m.def("rmsnorm(Tensor x, Tensor w, float eps) -> Tensor");
+  m.def("add_rmsnorm(Tensor x, Tensor(a!) residual, Tensor w, float eps) -> Tensor");
+  m.def("layernorm(Tensor x, Tensor? residual, Tensor gamma, Tensor beta, float eps) -> Tensor");
+  m.def("rope_cache(Tensor(a!) qkv, Tensor positions, Tensor cos_sin, Tensor? slot_mapping, "
+        "Tensor(b!) k_cache, Tensor(c!) v_cache, int Hq, int Hkv, int D) -> ()");
+  m.def("silu_mul(Tensor gu) -> Tensor");
+  m.def("bias_act(Tensor x, Tensor bias, Tensor? residual, bool gelu) -> Tensor");
+  m.def("embedding(Tensor ids, Tensor table) -> Tensor");
+  m.def("bert_embed_ln(Tensor ids, Tensor pos, Tensor? token_type, Tensor wte, Tensor wpe, "
+        "Tensor wtt, Tensor gamma, Tensor beta, float eps) -> Tensor");
+  m.def("argmax(Tensor logits) -> Tensor");
+  m.def("sample(Tensor logits, Tensor inv_temp, Tensor top_k, Tensor top_p, Tensor u) -> Tensor");
+  m.def("paged_decode(Tensor q, Tensor k_cache, Tensor v_cache, Tensor block_tables, "
+        "Tensor context_lens, int Hq, int max_context, float scale) -> Tensor");
+  m.def("flash_prefill(Tensor qkv, Tensor cu_seqlens, int max_len, int Hq, int Hkv, int D, "
+        "float scale, bool causal) -> Tensor");
+  m.def("knn(Tensor xb, Tensor xb_norms, Tensor xq, int k, bool inner_product, int id_offset) "
+        "-> (Tensor, Tensor)");
+}
+
+TORCH_LIBRARY_IMPL(docqa, CUDA, m) {
+  m.impl("rmsnorm", &rmsnorm);
+  m.impl("add_rmsnorm", &add_rmsnorm);
+  m.impl("layernorm", &layernorm);
+  m.impl("rope_cache", &rope_cache);
+  m.impl("silu_mul", &silu_mul);
+  m.impl("bias_act", &bias_act);
+  m.impl("embedding", &embedding);
+  m.impl("bert_embed_ln", &bert_embed_ln);
+  m.impl("argmax", &argmax);
+  m.impl("sample", &sample);
+  m.impl("paged_decode", &paged_decode);
+  m.impl("flash_prefill", &flash_prefill);
+  m.impl("knn", &knn);
+}

@@ -1,0 +1,48 @@
+// docqa_kernels.h -- host launchers of the gfx950 kernels (raw pointers + stream).
+// Every launcher returns 0 on success, a negative value for an unsupported shape and a
+// hipError_t for a failed launch.  They allocate nothing and never synchronise, so they
+// can be captured into HIP graphs (cdna_hip_programming.md Guideline 9).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+int docqa_rmsnorm(const void* x, const void* w, void* out, int rows, int H, float eps,
+                  hipStream_t s);
+int docqa_add_rmsnorm(const void* x, void* residual, const void* w, void* out, int rows, int H,
+                      float eps, hipStream_t s);
+int docqa_layernorm(const void* x, const void* residual, const void* g, const void* b, void* out,
+                    int rows, int H, float eps, hipStream_t s);
+
+int docqa_rope_cache(void* qkv, const int* positions, const float* cos_sin,
+                     const int* slot_mapping, void* k_cache, void* v_cache, int T, int Hq,
+                     int Hkv, int D, int row_stride, int BS, hipStream_t s);
+
+int docqa_silu_mul(const void* gu, void* out, int T, int I, hipStream_t s);
+int docqa_bias_act(const void* x, const void* bias, const void* res, void* out, int T, int N,
+                   int gelu, hipStream_t s);
+
+int docqa_embedding(const int* ids, const void* table, void* out, int T, int H, hipStream_t s);
+int docqa_bert_embed_ln(const int* ids, const int* pos, const int* tt, const void* wte,
+                        const void* wpe, const void* wtt, const void* g, const void* b, void* out,
+                        int T, int H, float eps, hipStream_t s);
+int docqa_argmax(const void* logits, int rows, int V, int ld, int is_bf16, float* ws_v, int* ws_i,
+                 int splits, int64_t* out, hipStream_t s);
+int docqa_sample(const float* logits, int rows, int V, int ld, const float* inv_temp,
+                 const int* top_k, const float* top_p, const float* u, int64_t* out,
+                 hipStream_t s);
+
+int docqa_paged_decode(const void* q, int q_stride, const void* k_cache, const void* v_cache,
+                       const int* block_tables, int maxb, const int* context_lens, void* out,
+                       int out_stride, float* tmp_out, float* tmp_ml, int B, int Hq, int Hkv,
+                       int D, int BS, int max_parts, float scale, hipStream_t s);
+int docqa_decode_part_tokens();
+
+int docqa_flash_prefill(const void* qkv, int row_stride, const int* cu_seqlens, void* out,
+                        int o_stride, int B, int max_len, int Hq, int Hkv, int head_dim,
+                        float scale, int causal, hipStream_t s);
+
+int docqa_knn_workspace_blocks(int N);
+int docqa_knn_kpad(int k);
+int docqa_knn(const void* xb, const float* norms, int N, int d, int is_bf16, const float* xq,
+              int nq, int k, int metric_ip, float* ws_d, int* ws_i, int nblk, float* out_d,
+              int64_t* out_i, int64_t id_offset, hipStream_t s);

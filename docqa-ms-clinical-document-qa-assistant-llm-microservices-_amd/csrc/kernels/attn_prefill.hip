@@ -1,0 +1,261 @@
+// attn_prefill.hip -- causal varlen flash-attention forward on MFMA for the Llama-3
+// prefill (and, with causal=0, the bidirectional BERT encoders).
+//
+// Structure (cdna_hip_programming.md App. B "Fused attention prefill", §3 "An
+// accumulator tile as the next MFMA's operand", T10 tr-read, T2 swizzle, T14 split):
+//  * workgroup = 4 waves = 128 query rows of one (sequence, query head); each wave owns
+//    32 query rows.  KV tiles of 64 keys are staged HBM -> registers -> LDS once per
+//    workgroup and shared by the 4 waves.
+//  * swapped QK^T: X = S^T = K . Q^T on v_mfma_f32_32x32x16_bf16, so each lane holds one
+//    query's scores for 16 keys in registers -> the row max / row sum of the online
+//    softmax are in-register plus one cross-half shuffle (no LDS round trip for P).
+//  * O^T = V^T . P^T: P^T is exactly X converted to bf16 (the accumulator IS the next
+//    MFMA's B operand, no lane movement); V^T fragments come from the row-major V tile
+//    with ds_read_b64_tr_b16 (hardware transpose read), XOR-swizzled so the reads are
+//    bank-conflict-free.  K is read row-wise with ds_read_b128, swizzled chunk ^ (row&15).
+//  * next KV tile's global loads are issued before the current tile's MFMAs and written
+//    to LDS after the trailing barrier (async-STAGE split).
+//
+// Q/K/V are read straight from the packed post-RoPE QKV projection buffer
+// [T, (Hq + 2*Hkv) * D]; output is [T, Hq, D] (row stride o_stride).
+//
+// Reference parity: prefill is inside llama.cpp behind Ollama (llm-qa/main.py:69,117)
+// and the MiniLM encoder attention inside sentence-transformers
+// (semantic-indexer/indexer.py:37).
+#include "docqa_common.h"
+#include <float.h>
+
+using namespace docqa;
+
+namespace {
+constexpr int QB = 128;   // query rows per workgroup
+constexpr int KB = 64;    // keys per tile
+constexpr float kLog2e = 1.4426950408889634f;
+
+typedef __attribute__((address_space(3))) i16x4 lds_i16x4;
+
+// element offset of 16-B chunk `ch` of row `row` in the K / V tiles (XOR swizzles, see
+// header; for D=128 both are bank-conflict-free for their read pattern)
+template <int D>
+__device__ __forceinline__ int k_off(int row, int ch) {
+  return row * D + ((ch ^ (row & (D / 8 - 1))) << 3);
+}
+template <int D>
+__device__ __forceinline__ int v_off(int row, int ch) {
+  return row * D + ((ch ^ (((row & 3) << 2) & (D / 8 - 1))) << 3);
+}
+
+template <int D, bool CAUSAL>
+__global__ __launch_bounds__(256) void flash_prefill_kernel(
+    const uint16_t* __restrict__ qkv, int row_stride, const int* __restrict__ cu_seqlens,
+    uint16_t* __restrict__ out, int o_stride, int Hq, int Hkv, float scale) {
+  __shared__ __attribute__((aligned(16))) uint16_t smem[2 * KB * D];
+  uint16_t* sK = smem;
+  uint16_t* sV = smem + KB * D;
+
+  const int qt = blockIdx.x, h = blockIdx.y, b = blockIdx.z;
+  const int seq0 = cu_seqlens[b];
+  const int L = cu_seqlens[b + 1] - seq0;
+  const int q_start = qt * QB;
+  if (q_start >= L) return;
+  const int kvh = h / (Hq / Hkv);
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int l32 = lane & 31, hh = lane >> 5;
+  const int q_wave = q_start + wave * 32;       // first query row of this wave
+  const int my_q = q_wave + l32;                // this lane's query row (column of X)
+
+  // ---- Q fragments (B operand of S^T = K Q^T): lane holds Q[my_q][16ks + 8hh + j]
+  constexpr int NKS = D / 16;   // k-steps of the QK^T product
+  constexpr int NDT = D / 32;   // 32-wide dim tiles of O^T
+  constexpr int NCH = D / 8;    // 16-B chunks per row
+  constexpr int CPT = KB * NCH / 256;  // staged chunks per thread per tensor
+  bf16x8 qf[NKS];
+  {
+    const bool ok = my_q < L;
+    const uint16_t* qp = qkv + (size_t)(seq0 + (ok ? my_q : 0)) * row_stride + (size_t)h * D;
+#pragma unroll
+    for (int ks = 0; ks < NKS; ++ks) {
+      uint4 v = ok ? *reinterpret_cast<const uint4*>(qp + ks * 16 + hh * 8) : make_uint4(0, 0, 0, 0);
+      qf[ks] = *reinterpret_cast<bf16x8*>(&v);
+    }
+  }
+
+  f32x16 o[NDT];
+#pragma unroll
+  for (int i = 0; i < NDT; ++i)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) o[i][r] = 0.f;
+  float m_run = -FLT_MAX, l_run = 0.f;
+  const float sl2 = scale * kLog2e;
+
+  const int kv_end = CAUSAL ? min(L, q_start + QB) : L;
+  const int ntiles = (kv_end + KB - 1) / KB;
+  const uint16_t* kbase = qkv + (size_t)seq0 * row_stride + (size_t)(Hq + kvh) * D;
+  const uint16_t* vbase = qkv + (size_t)seq0 * row_stride + (size_t)(Hq + Hkv + kvh) * D;
+
+  // staging: KB rows x NCH chunks per tensor, CPT per thread per tensor
+  uint4 rk[CPT], rv[CPT];
+  auto load_tile = [&](int t) {
+#pragma unroll
+    for (int i = 0; i < CPT; ++i) {
+      const int idx = tid + 256 * i;
+      const int row = idx / NCH, ch = idx % NCH;
+      const int key = t * KB + row;
+      if (key < L) {
+        rk[i] = *reinterpret_cast<const uint4*>(kbase + (size_t)key * row_stride + ch * 8);
+        rv[i] = *reinterpret_cast<const uint4*>(vbase + (size_t)key * row_stride + ch * 8);
+      } else {
+        rk[i] = make_uint4(0, 0, 0, 0);
+        rv[i] = make_uint4(0, 0, 0, 0);
+      }
+    }
+  };
+  auto store_tile = [&]() {
+#pragma unroll
+    for (int i = 0; i < CPT; ++i) {
+      const int idx = tid + 256 * i;
+      const int row = idx / NCH, ch = idx % NCH;
+      *reinterpret_cast<uint4*>(sK + k_off<D>(row, ch)) = rk[i];
+      *reinterpret_cast<uint4*>(sV + v_off<D>(row, ch)) = rv[i];
+    }
+  };
+
+  load_tile(0);
+  store_tile();
+  __syncthreads();
+
+  // tr-read lane geometry (see header): group gi = lane>>4, q = (lane&15)>>2, p = lane&3
+  const int gi = lane >> 4, tq = (lane & 15) >> 2, tp = lane & 3;
+
+  for (int t = 0; t < ntiles; ++t) {
+    if (t + 1 < ntiles) load_tile(t + 1);
+    const int kb = t * KB;
+    // a wave whose rows all precede this tile's first key contributes nothing (causal)
+    const bool active = !CAUSAL || (kb <= q_wave + 31);
+    if (active) {
+      // ---- S^T for the two 32-key sub-tiles
+      f32x16 x[2];
+#pragma unroll
+      for (int kt = 0; kt < 2; ++kt) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) x[kt][r] = 0.f;
+        const int row = kt * 32 + l32;
+#pragma unroll
+        for (int ks = 0; ks < NKS; ++ks) {
+          const bf16x8 a = *reinterpret_cast<const bf16x8*>(sK + k_off<D>(row, ks * 2 + hh));
+          x[kt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, qf[ks], x[kt], 0, 0, 0);
+        }
+      }
+      // ---- online softmax (log2 domain); keys on registers, query on lane
+      float mx = -FLT_MAX;
+#pragma unroll
+      for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int key = kb + kt * 32 + (r & 3) + 8 * (r >> 2) + 4 * hh;
+          float s = x[kt][r] * sl2;
+          const bool masked = (key >= L) || (CAUSAL && key > my_q);
+          s = masked ? -FLT_MAX : s;
+          x[kt][r] = s;
+          mx = fmaxf(mx, s);
+        }
+      mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+      const float m_new = fmaxf(m_run, mx);
+      const bool dead = (m_new == -FLT_MAX);       // every key so far masked
+      const float alpha = dead ? 1.f : exp2f(m_run - m_new);
+      float rs = 0.f;
+#pragma unroll
+      for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const float p = (dead || x[kt][r] == -FLT_MAX) ? 0.f : exp2f(x[kt][r] - m_new);
+          x[kt][r] = p;
+          rs += p;
+        }
+      rs += __shfl_xor(rs, 32, 64);
+      l_run = l_run * alpha + rs;
+      m_run = m_new;
+#pragma unroll
+      for (int i = 0; i < NDT; ++i)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) o[i][r] *= alpha;
+
+      // ---- O^T += V^T P^T
+#pragma unroll
+      for (int kt = 0; kt < 2; ++kt) {
+#pragma unroll
+        for (int s = 0; s < 2; ++s) {
+          bf16x8 pb;
+#pragma unroll
+          for (int j = 0; j < 8; ++j) pb[j] = (__bf16)x[kt][8 * s + j];
+          const int krow = kt * 32 + 16 * s + 4 * hh + tq;  // key row for tr-read (first 4)
+#pragma unroll
+          for (int dt = 0; dt < NDT; ++dt) {
+            const int col = dt * 32 + 16 * (gi & 1) + 4 * tp;  // dim column
+            const int ch = col >> 3, half = (col & 7);
+            const i16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+                (lds_i16x4*)(sV + v_off<D>(krow, ch) + half));
+            const i16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+                (lds_i16x4*)(sV + v_off<D>(krow + 8, ch) + half));
+            bf16x8 a;
+            const __bf16* lp = reinterpret_cast<const __bf16*>(&lo);
+            const __bf16* hp = reinterpret_cast<const __bf16*>(&hi);
+#pragma unroll
+            for (int j = 0; j < 4; ++j) { a[j] = lp[j]; a[4 + j] = hp[j]; }
+            o[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, pb, o[dt], 0, 0, 0);
+          }
+        }
+      }
+    }
+    __syncthreads();
+    if (t + 1 < ntiles) {
+      store_tile();
+      __syncthreads();
+    }
+  }
+
+  // ---- epilogue: O[q][dim] = O^T[dim][q] / l
+  if (my_q < L) {
+    const float inv = l_run > 0.f ? 1.f / l_run : 0.f;
+    uint16_t* op = out + (size_t)(seq0 + my_q) * o_stride + (size_t)h * D;
+#pragma unroll
+    for (int dt = 0; dt < NDT; ++dt)
+#pragma unroll
+      for (int g4 = 0; g4 < 4; ++g4) {
+        const int d0 = dt * 32 + 8 * g4 + 4 * hh;
+        uint2 v;
+        v.x = pack2(o[dt][4 * g4 + 0] * inv, o[dt][4 * g4 + 1] * inv);
+        v.y = pack2(o[dt][4 * g4 + 2] * inv, o[dt][4 * g4 + 3] * inv);
+        *reinterpret_cast<uint2*>(op + d0) = v;
+      }
+  }
+}
+}  // namespace
+
+template <int D>
+static void launch_prefill(dim3 grid, hipStream_t s, int causal, const void* qkv, int row_stride,
+                           const int* cu, void* out, int o_stride, int Hq, int Hkv, float scale) {
+  if (causal)
+    flash_prefill_kernel<D, true><<<grid, 256, 0, s>>>((const uint16_t*)qkv, row_stride, cu,
+                                                       (uint16_t*)out, o_stride, Hq, Hkv, scale);
+  else
+    flash_prefill_kernel<D, false><<<grid, 256, 0, s>>>((const uint16_t*)qkv, row_stride, cu,
+                                                        (uint16_t*)out, o_stride, Hq, Hkv, scale);
+}
+
+int docqa_flash_prefill(const void* qkv, int row_stride, const int* cu_seqlens, void* out,
+                        int o_stride, int B, int max_len, int Hq, int Hkv, int head_dim,
+                        float scale, int causal, hipStream_t s) {
+  if (B == 0 || max_len == 0) return 0;
+  if (Hq % Hkv != 0) return -1;
+  dim3 grid((max_len + QB - 1) / QB, Hq, B);
+  switch (head_dim) {
+    case 32: launch_prefill<32>(grid, s, causal, qkv, row_stride, cu_seqlens, out, o_stride, Hq, Hkv, scale); break;
+    case 64: launch_prefill<64>(grid, s, causal, qkv, row_stride, cu_seqlens, out, o_stride, Hq, Hkv, scale); break;
+    case 128: launch_prefill<128>(grid, s, causal, qkv, row_stride, cu_seqlens, out, o_stride, Hq, Hkv, scale); break;
+    default: return -1;
+  }
+  DOCQA_CHECK_LAUNCH();
+  return 0;
+}

@@ -1,0 +1,87 @@
+// rope_cache.hip -- fused rotary embedding + paged KV-cache write for the Llama-3
+// generator.  One launch per layer replaces three (rope q, rope k, cache scatter):
+// it reads the packed QKV projection output once, rotates Q and K in place (the
+// prefill attention then reads Q/K/V straight from the packed buffer) and scatters
+// the rotated K and the V head into the paged cache
+//   k_cache/v_cache : [num_blocks, Hkv, BS, D]  (one (block, head) = BS*D contiguous)
+// slot = slot_mapping[token] (block = slot / BS, offset = slot % BS, -1 = padding).
+//
+// Rotation is Llama's rotate-half form: for i < D/2,
+//   x'[i] = x[i]*cos - x[i+D/2]*sin ;  x'[i+D/2] = x[i+D/2]*cos + x[i]*sin
+// with cos/sin precomputed in fp32 on the host ([max_pos][D/2 cos | D/2 sin]) so the
+// kernel stays memory-bound instead of trig-bound (cdna_hip_programming.md App. B,
+// "Element-wise").  Thread mapping: D/8 threads per head, each owning 4 rotation
+// pairs (two 8-byte loads); V heads move as one 16-byte chunk per thread.
+//
+// Reference parity: RoPE lives inside the llama.cpp Mistral served through Ollama
+// (llm-qa/main.py:66-69); this is its MI355X-native replacement.
+#include "docqa_common.h"
+
+using namespace docqa;
+
+__global__ __launch_bounds__(256) void rope_cache_kernel(
+    uint16_t* __restrict__ qkv, const int* __restrict__ positions,
+    const float* __restrict__ cos_sin, const int* __restrict__ slot_mapping,
+    uint16_t* __restrict__ k_cache, uint16_t* __restrict__ v_cache, int Hq, int Hkv, int D,
+    int row_stride, int BS) {
+  const int t = blockIdx.x;
+  const int tph = D >> 3;                 // threads per head
+  const int heads_per_pass = 256 / tph;
+  const int sub = threadIdx.x % tph;
+  const int pos = positions[t];
+  const int slot = slot_mapping ? slot_mapping[t] : -1;
+  const int half = D >> 1;
+  uint16_t* row = qkv + (size_t)t * row_stride;
+  const float* cs = cos_sin + (size_t)pos * D;
+  const int total = Hq + 2 * Hkv;
+  for (int h = threadIdx.x / tph; h < total; h += heads_per_pass) {
+    uint16_t* hp = row + h * D;
+    if (h < Hq + Hkv) {
+      const int i0 = sub * 4;
+      uint2 a = *reinterpret_cast<const uint2*>(hp + i0);
+      uint2 b = *reinterpret_cast<const uint2*>(hp + half + i0);
+      const float4 c = *reinterpret_cast<const float4*>(cs + i0);
+      const float4 s = *reinterpret_cast<const float4*>(cs + half + i0);
+      float x1[4] = {__uint_as_float(a.x << 16), __uint_as_float(a.x & 0xffff0000u),
+                     __uint_as_float(a.y << 16), __uint_as_float(a.y & 0xffff0000u)};
+      float x2[4] = {__uint_as_float(b.x << 16), __uint_as_float(b.x & 0xffff0000u),
+                     __uint_as_float(b.y << 16), __uint_as_float(b.y & 0xffff0000u)};
+      const float cc[4] = {c.x, c.y, c.z, c.w}, ss[4] = {s.x, s.y, s.z, s.w};
+      float o1[4], o2[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        o1[j] = x1[j] * cc[j] - x2[j] * ss[j];
+        o2[j] = x2[j] * cc[j] + x1[j] * ss[j];
+      }
+      uint2 oa, ob;
+      oa.x = pack2(o1[0], o1[1]); oa.y = pack2(o1[2], o1[3]);
+      ob.x = pack2(o2[0], o2[1]); ob.y = pack2(o2[2], o2[3]);
+      *reinterpret_cast<uint2*>(hp + i0) = oa;
+      *reinterpret_cast<uint2*>(hp + half + i0) = ob;
+      if (h >= Hq && slot >= 0) {
+        const int kh = h - Hq;
+        const int blk = slot / BS, off = slot - blk * BS;
+        uint16_t* dst = k_cache + (((size_t)blk * Hkv + kh) * BS + off) * D;
+        *reinterpret_cast<uint2*>(dst + i0) = oa;
+        *reinterpret_cast<uint2*>(dst + half + i0) = ob;
+      }
+    } else if (slot >= 0) {
+      const int vh = h - Hq - Hkv;
+      const int blk = slot / BS, off = slot - blk * BS;
+      uint16_t* dst = v_cache + (((size_t)blk * Hkv + vh) * BS + off) * D;
+      *reinterpret_cast<uint4*>(dst + sub * 8) = *reinterpret_cast<const uint4*>(hp + sub * 8);
+    }
+  }
+}
+
+int docqa_rope_cache(void* qkv, const int* positions, const float* cos_sin,
+                     const int* slot_mapping, void* k_cache, void* v_cache, int T, int Hq,
+                     int Hkv, int D, int row_stride, int BS, hipStream_t s) {
+  if (T == 0) return 0;
+  if (D % 8 != 0 || (256 % (D / 8)) != 0) return -1;
+  rope_cache_kernel<<<T, 256, 0, s>>>((uint16_t*)qkv, positions, cos_sin, slot_mapping,
+                                      (uint16_t*)k_cache, (uint16_t*)v_cache, Hq, Hkv, D,
+                                      row_stride, BS);
+  DOCQA_CHECK_LAUNCH();
+  return 0;
+}

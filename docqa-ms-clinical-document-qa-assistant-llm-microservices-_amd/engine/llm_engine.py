@@ -1,0 +1,248 @@
+"""Generation engine for the llm-qa service: batched varlen prefill + HIP-graph decode.
+
+One decode step for a batch bucket is captured once into a HIP graph (torch.cuda.graph
+on ROCm) that contains the whole step: slot computation from the block table, the 32/80
+layer forward, greedy/top-k/top-p sampling and the in-place advance of the step state
+(positions, context lengths, next input token).  The host therefore only enqueues
+``graph.replay()`` per token -- no per-layer launches, no host<->device syncs inside the
+decode loop (a Llama-3-8B step is ~230 kernels; eager launch overhead would otherwise
+dominate at small batch: MI355X_MICROARCH.md "graph-replay-floor").
+
+Prefill packs all prompts of a batch into one varlen token stream (cu_seqlens), split
+into sub-batches of at most ``max_prefill_tokens`` tokens; only the last position of
+each prompt is projected through the LM head.
+
+Reference parity: this is what ``RetrievalQA.invoke`` -> ``ChatOllama`` does per
+request in the reference (llm-qa/main.py:117, one request at a time, greedy at T=0).
+"""
+from __future__ import annotations
+
+import math
+import time
+from dataclasses import dataclass
+
+import torch
+
+from ..models.llama import AttnMeta, LlamaModel
+from .kv_cache import KVCache
+
+
+@dataclass
+class SamplingParams:
+    max_new_tokens: int = 128
+    temperature: float = 0.0      # 0 -> greedy (the reference's ChatOllama temperature=0)
+    top_k: int = 0
+    top_p: float = 1.0
+    stop_on_eos: bool = True
+    seed: int = 0
+
+
+@dataclass
+class GenStats:
+    prefill_s: float = 0.0
+    decode_s: float = 0.0
+    prompt_tokens: int = 0
+    generated_tokens: int = 0
+
+
+def _bucket(n: int, cap: int) -> int:
+    b = 1
+    while b < n:
+        b *= 2
+    return min(b, cap)
+
+
+class _DecodeGraph:
+    """Static buffers + captured graph for one batch bucket."""
+
+    def __init__(self, eng: "LLMEngine", bp: int):
+        dev = eng.device
+        self.bp = bp
+        self.tokens = torch.zeros(bp, dtype=torch.int32, device=dev)
+        self.positions = torch.zeros(bp, dtype=torch.int32, device=dev)
+        self.context_lens = torch.zeros(bp, dtype=torch.int32, device=dev)
+        self.valid = torch.zeros(bp, dtype=torch.int32, device=dev)
+        self.block_tables = torch.zeros(bp, eng.max_blocks_per_seq, dtype=torch.int32, device=dev)
+        self.inv_temp = torch.ones(bp, dtype=torch.float32, device=dev)
+        self.top_k = torch.zeros(bp, dtype=torch.int32, device=dev)
+        self.top_p = torch.ones(bp, dtype=torch.float32, device=dev)
+        self.out = torch.zeros(bp, dtype=torch.long, device=dev)
+        self.greedy = True
+        self.graph = None
+
+
+class LLMEngine:
+    def __init__(self, model: LlamaModel, max_batch: int = 64, max_context: int = 2048,
+                 block_size: int = 64, num_blocks: int | None = None, use_graphs: bool = True,
+                 max_prefill_tokens: int = 65536):
+        self.model = model
+        self.cfg = model.cfg
+        self.device = model.device
+        self.max_batch = max_batch
+        self.block_size = block_size
+        self.max_blocks_per_seq = (max_context + block_size - 1) // block_size
+        self.max_context = self.max_blocks_per_seq * block_size
+        self.max_prefill_tokens = max_prefill_tokens
+        if num_blocks is None:
+            num_blocks = max_batch * self.max_blocks_per_seq + 1
+        self.kv = KVCache(self.cfg.layers, num_blocks, model.hkv, self.cfg.head_dim, block_size,
+                          self.device, model.dtype)
+        self.use_graphs = use_graphs and self.device.type == "cuda"
+        self._graphs: dict[int, _DecodeGraph] = {}
+        self._pool = None
+        self.stats = GenStats()
+
+    # ------------------------------------------------------------------ prefill
+    def _prefill(self, prompts: list[list[int]], tables: list[list[int]]) -> torch.Tensor:
+        dev, BS = self.device, self.block_size
+        firsts = []
+        i = 0
+        while i < len(prompts):
+            j, tok = i, 0
+            while j < len(prompts) and (j == i or tok + len(prompts[j]) <= self.max_prefill_tokens):
+                tok += len(prompts[j])
+                j += 1
+            ids, pos, slots, cu = [], [], [], [0]
+            for p, tb in zip(prompts[i:j], tables[i:j]):
+                n = len(p)
+                ids.extend(p)
+                pos.extend(range(n))
+                slots.extend(tb[t // BS] * BS + t % BS for t in range(n))
+                cu.append(cu[-1] + n)
+            t_ids = torch.tensor(ids, dtype=torch.int32).to(dev, non_blocking=True)
+            meta = AttnMeta(
+                prefill=True,
+                positions=torch.tensor(pos, dtype=torch.int32).to(dev, non_blocking=True),
+                slot_mapping=torch.tensor(slots, dtype=torch.int32).to(dev, non_blocking=True),
+                cu_seqlens=torch.tensor(cu, dtype=torch.int32).to(dev, non_blocking=True),
+                max_len=max(len(p) for p in prompts[i:j]))
+            last = torch.tensor(cu[1:], dtype=torch.int64).to(dev, non_blocking=True) - 1
+            logits = self.model.forward(t_ids, meta, self.kv.caches, logits_index=last)
+            firsts.append(logits)
+            i = j
+        return torch.cat(firsts, 0)
+
+    # ------------------------------------------------------------------ decode step
+    def _step_body(self, g: _DecodeGraph) -> None:
+        BS = self.block_size
+        valid = g.valid.bool()
+        blk = torch.gather(g.block_tables, 1, (g.positions // BS).long()[:, None])[:, 0]
+        slots = torch.where(valid, blk * BS + g.positions % BS, torch.full_like(blk, -1))
+        meta = AttnMeta(prefill=False, positions=g.positions, slot_mapping=slots.int(),
+                        block_tables=g.block_tables, context_lens=g.context_lens,
+                        max_context=self.max_context)
+        logits = self.model.forward(g.tokens, meta, self.kv.caches)
+        nxt = self._select(logits, g)
+        g.out.copy_(nxt)
+        g.tokens.copy_(nxt.int())
+        g.positions.add_(g.valid)
+        g.context_lens.add_(g.valid)
+
+    def _select(self, logits, g: _DecodeGraph):
+        from .. import ops
+
+        if g.greedy:
+            return self.model.greedy(logits)
+        full = self.model.full_logits(logits).float()
+        u = torch.rand(full.shape[0], device=full.device)
+        return ops.sample(full, g.inv_temp, g.top_k, g.top_p, u)
+
+    def _get_graph(self, bp: int, greedy: bool) -> _DecodeGraph:
+        key = bp * 2 + int(greedy)
+        g = self._graphs.get(key)
+        if g is None:
+            g = _DecodeGraph(self, bp)
+            g.greedy = greedy
+            self._graphs[key] = g
+        return g
+
+    def _capture(self, g: _DecodeGraph) -> None:
+        # warm up on a side stream (allocator + hipBLASLt heuristics), then capture.
+        saved = [t.clone() for t in (g.tokens, g.positions, g.context_lens)]
+        s = torch.cuda.Stream()
+        s.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(s):
+            self._step_body(g)
+        torch.cuda.current_stream().wait_stream(s)
+        for t, v in zip((g.tokens, g.positions, g.context_lens), saved):
+            t.copy_(v)
+        graph = torch.cuda.CUDAGraph()
+        if self._pool is None:
+            self._pool = torch.cuda.graph_pool_handle()
+        with torch.cuda.graph(graph, pool=self._pool):
+            self._step_body(g)
+        for t, v in zip((g.tokens, g.positions, g.context_lens), saved):
+            t.copy_(v)
+        g.graph = graph
+
+    # ------------------------------------------------------------------ generate
+    @torch.inference_mode()
+    def generate(self, prompts: list[list[int]], params: SamplingParams | None = None) -> list[list[int]]:
+        params = params or SamplingParams()
+        out: list[list[int]] = []
+        for i in range(0, len(prompts), self.max_batch):
+            out.extend(self._generate_batch(prompts[i:i + self.max_batch], params))
+        return out
+
+    def _generate_batch(self, prompts: list[list[int]], params: SamplingParams) -> list[list[int]]:
+        B = len(prompts)
+        dev = self.device
+        lens = [len(p) for p in prompts]
+        need = max(lens) + params.max_new_tokens
+        if need > self.max_context:
+            raise ValueError(f"prompt+generation {need} exceeds max_context {self.max_context}")
+        alloc = self.kv.allocator
+        tables = [alloc.alloc(self.kv.blocks_for(n + params.max_new_tokens)) for n in lens]
+        try:
+            greedy = params.temperature <= 0.0
+            t0 = time.perf_counter()
+            logits = self._prefill(prompts, tables)
+            g = self._get_graph(_bucket(B, self.max_batch) if self.use_graphs else B, greedy)
+            # state for the first decode step
+            bt = torch.zeros(g.bp, self.max_blocks_per_seq, dtype=torch.int32)
+            for r, tb in enumerate(tables):
+                bt[r, :len(tb)] = torch.tensor(tb, dtype=torch.int32)
+            g.block_tables.copy_(bt.to(dev))
+            vl = torch.zeros(g.bp, dtype=torch.int32)
+            vl[:B] = 1
+            g.valid.copy_(vl.to(dev))
+            pos = torch.zeros(g.bp, dtype=torch.int32)
+            pos[:B] = torch.tensor(lens, dtype=torch.int32)
+            g.positions.copy_(pos.to(dev))
+            g.context_lens.copy_((pos + vl).to(dev))
+            if not greedy:
+                g.inv_temp.fill_(1.0 / params.temperature)
+                g.top_k.fill_(params.top_k)
+                g.top_p.fill_(params.top_p)
+                if params.seed:
+                    torch.manual_seed(params.seed)
+            first = self._select(logits, g) if greedy else self._select(logits, g)
+            gen = torch.empty(B, params.max_new_tokens, dtype=torch.long, device=dev)
+            gen[:, 0] = first
+            tok = torch.zeros(g.bp, dtype=torch.int32, device=dev)
+            tok[:B] = first.int()
+            g.tokens.copy_(tok)
+            if dev.type == "cuda":
+                torch.cuda.synchronize()
+            t1 = time.perf_counter()
+            if self.use_graphs and g.graph is None and params.max_new_tokens > 1:
+                self._capture(g)
+            for step in range(1, params.max_new_tokens):
+                if g.graph is not None:
+                    g.graph.replay()
+                else:
+                    self._step_body(g)
+                gen[:, step] = g.out[:B]
+            result = gen.tolist()  # the one host sync of the decode loop
+            t2 = time.perf_counter()
+            self.stats.prefill_s += t1 - t0
+            self.stats.decode_s += t2 - t1
+            self.stats.prompt_tokens += sum(lens)
+            self.stats.generated_tokens += B * params.max_new_tokens
+        finally:
+            for tb in tables:
+                alloc.free(tb)
+        if params.stop_on_eos:
+            eos = self.cfg.eos_token_id
+            result = [r[: r.index(eos) + 1] if eos in r else r for r in result]
+        return result

@@ -1,0 +1,221 @@
+"""Llama-3 decoder (8B / 70B / test sizes) for the llm-qa generator.
+
+MI355X-first layout:
+  * fused projections: one [(Hq + 2*Hkv)*D, H] QKV GEMM and one [2I, H] gate|up GEMM
+    per layer (fewer, larger hipBLASLt launches; the GEMM output is consumed in place by
+    the fused RoPE+KV-cache kernel and the SwiGLU kernel);
+  * the residual stream is updated inside the fused add+RMSNorm kernel, so each layer
+    costs 2 GEMM-epilogue-free passes over the hidden state instead of 4;
+  * attention reads Q/K/V straight out of the packed QKV buffer (prefill: MFMA flash
+    kernel; decode: paged split-K GQA kernel over a [blocks, Hkv, BS, D] cache);
+  * tensor parallelism is Megatron-style: column-parallel QKV / gate|up, row-parallel
+    O / down followed by one all-reduce each (RCCL over xGMI), vocab-parallel LM head
+    whose argmax is resolved with a [B, 2] all-gather instead of gathering logits;
+  * with 288 GB of HBM per GPU the 8B model (16 GB bf16) is replicated per GPU (TP=1,
+    request-level data parallel) and 70B (140 GB) runs TP=8 (17.6 GB/GPU).
+
+Weights are random-initialised on the device (no checkpoints are reachable offline);
+``load_safetensors`` maps Hugging Face Llama checkpoints when one is available.
+
+Reference parity: replaces the Ollama/llama.cpp Mistral-7B generator behind
+``ChatOllama(model="mistral", temperature=0)`` (llm-qa/main.py:66-69).
+"""
+from __future__ import annotations
+
+import math
+from dataclasses import dataclass, field
+
+import torch
+import torch.nn.functional as F
+
+from .. import ops
+from ..parallel import comm
+
+
+@dataclass
+class LlamaConfig:
+    name: str = "llama3-8b"
+    vocab_size: int = 128256
+    hidden: int = 4096
+    intermediate: int = 14336
+    layers: int = 32
+    heads: int = 32
+    kv_heads: int = 8
+    head_dim: int = 128
+    rope_theta: float = 500000.0
+    rms_eps: float = 1e-5
+    max_position: int = 8192
+    bos_token_id: int = 128000
+    eos_token_id: int = 128009
+
+    @staticmethod
+    def preset(name: str) -> "LlamaConfig":
+        if name in ("llama3-8b", "llama-3-8b", "8b"):
+            return LlamaConfig()
+        if name in ("llama3-70b", "llama-3-70b", "70b"):
+            return LlamaConfig(name="llama3-70b", hidden=8192, intermediate=28672, layers=80,
+                               heads=64, kv_heads=8)
+        if name == "llama3-1b-test":  # mid-size config for kernel/engine tests on GPU
+            return LlamaConfig(name=name, vocab_size=32000, hidden=2048, intermediate=8192,
+                               layers=4, heads=16, kv_heads=4, max_position=4096,
+                               bos_token_id=1, eos_token_id=2)
+        if name == "tiny":
+            return LlamaConfig(name="tiny", vocab_size=512, hidden=256, intermediate=512,
+                               layers=2, heads=4, kv_heads=2, head_dim=128, max_position=2048,
+                               bos_token_id=1, eos_token_id=2)
+        raise ValueError(f"unknown llama preset {name}")
+
+    def num_params(self) -> int:
+        H, I, D = self.hidden, self.intermediate, self.head_dim
+        per_layer = H * (self.heads + 2 * self.kv_heads) * D + self.heads * D * H + 3 * H * I + 2 * H
+        return self.layers * per_layer + 2 * self.vocab_size * H + H
+
+
+@dataclass
+class AttnMeta:
+    """Per-forward attention metadata (all int32 device tensors)."""
+    prefill: bool
+    positions: torch.Tensor                 # [T]
+    slot_mapping: torch.Tensor              # [T]
+    cu_seqlens: torch.Tensor | None = None  # [B+1] (prefill)
+    max_len: int = 0                        # (prefill)
+    block_tables: torch.Tensor | None = None  # [B, maxb] (decode)
+    context_lens: torch.Tensor | None = None  # [B] (decode; includes the new token)
+    max_context: int = 0                    # (decode) graph-capture bound
+
+
+class LlamaModel:
+    def __init__(self, cfg: LlamaConfig, device="cuda", dtype=torch.bfloat16, seed: int = 0,
+                 init: bool = True):
+        self.cfg = cfg
+        self.device = torch.device(device)
+        self.dtype = dtype
+        ps = comm.state()
+        self.tp = ps.tp_size
+        self.tp_rank = ps.tp_rank
+        if cfg.heads % self.tp or cfg.kv_heads % self.tp or cfg.intermediate % self.tp:
+            raise ValueError("heads / kv_heads / intermediate must divide the TP size")
+        self.hq = cfg.heads // self.tp
+        self.hkv = cfg.kv_heads // self.tp
+        self.inter = cfg.intermediate // self.tp
+        self.vocab_shard = (cfg.vocab_size + self.tp - 1) // self.tp
+        self.vocab_start = self.tp_rank * self.vocab_shard
+        self.scale = 1.0 / math.sqrt(cfg.head_dim)
+        self.cos_sin = ops.rope_cos_sin(cfg.max_position, cfg.head_dim, cfg.rope_theta, self.device)
+        self.layers: list[dict] = []
+        if init:
+            self._random_init(seed)
+
+    # ------------------------------------------------------------------ weights
+    def _random_init(self, seed: int) -> None:
+        cfg, dev, dt = self.cfg, self.device, self.dtype
+        g = torch.Generator(device=dev)
+        g.manual_seed(seed * 7919 + self.tp_rank)
+        std = 0.02
+
+        def w(*shape, s=std):
+            t = torch.empty(*shape, device=dev, dtype=dt)
+            t.normal_(0.0, s, generator=g)
+            return t
+
+        H, D = cfg.hidden, cfg.head_dim
+        self.embed = w(cfg.vocab_size, H)
+        self.final_norm = torch.ones(H, device=dev, dtype=dt)
+        self.lm_head = w(self.vocab_shard, H)
+        out_std = std / math.sqrt(2 * cfg.layers)
+        for _ in range(cfg.layers):
+            self.layers.append({
+                "in_norm": torch.ones(H, device=dev, dtype=dt),
+                "qkv": w((self.hq + 2 * self.hkv) * D, H),
+                "o": w(H, self.hq * D, s=out_std),
+                "post_norm": torch.ones(H, device=dev, dtype=dt),
+                "gate_up": w(2 * self.inter, H),
+                "down": w(H, self.inter, s=out_std),
+            })
+
+    def load_state_dict_hf(self, sd: dict) -> None:
+        """Map a Hugging Face LlamaForCausalLM state dict (full, un-sharded) onto this
+        rank's shards."""
+        cfg, D, r, tp = self.cfg, self.cfg.head_dim, self.tp_rank, self.tp
+        dev, dt = self.device, self.dtype
+
+        def get(k):
+            return sd[k].to(device=dev, dtype=dt)
+
+        self.embed = get("model.embed_tokens.weight")
+        self.final_norm = get("model.norm.weight")
+        lm = get("lm_head.weight") if "lm_head.weight" in sd else self.embed
+        pad = self.vocab_shard * tp - lm.shape[0]
+        if pad:
+            lm = torch.cat([lm, lm.new_zeros(pad, lm.shape[1])])
+        self.lm_head = lm[r * self.vocab_shard:(r + 1) * self.vocab_shard].contiguous()
+        self.layers = []
+        for i in range(cfg.layers):
+            p = f"model.layers.{i}."
+            q = get(p + "self_attn.q_proj.weight").view(cfg.heads, D, -1)[r * self.hq:(r + 1) * self.hq]
+            k = get(p + "self_attn.k_proj.weight").view(cfg.kv_heads, D, -1)[r * self.hkv:(r + 1) * self.hkv]
+            v = get(p + "self_attn.v_proj.weight").view(cfg.kv_heads, D, -1)[r * self.hkv:(r + 1) * self.hkv]
+            o = get(p + "self_attn.o_proj.weight")[:, r * self.hq * D:(r + 1) * self.hq * D]
+            gt = get(p + "mlp.gate_proj.weight")[r * self.inter:(r + 1) * self.inter]
+            up = get(p + "mlp.up_proj.weight")[r * self.inter:(r + 1) * self.inter]
+            dn = get(p + "mlp.down_proj.weight")[:, r * self.inter:(r + 1) * self.inter]
+            self.layers.append({
+                "in_norm": get(p + "input_layernorm.weight"),
+                "qkv": torch.cat([q.reshape(-1, cfg.hidden), k.reshape(-1, cfg.hidden),
+                                  v.reshape(-1, cfg.hidden)]).contiguous(),
+                "o": o.contiguous(),
+                "post_norm": get(p + "post_attention_layernorm.weight"),
+                "gate_up": torch.cat([gt, up]).contiguous(),
+                "down": dn.contiguous(),
+            })
+
+    def weight_bytes(self) -> int:
+        n = self.embed.numel() + self.lm_head.numel() + self.final_norm.numel()
+        for L in self.layers:
+            n += sum(t.numel() for t in L.values())
+        return n * self.embed.element_size()
+
+    # ------------------------------------------------------------------ forward
+    def forward(self, input_ids: torch.Tensor, meta: AttnMeta, kv_caches: list,
+                logits_index: torch.Tensor | None = None) -> torch.Tensor:
+        """input_ids [T] int32 -> logits fp32 [R, vocab_shard] for the rows selected by
+        ``logits_index`` (all rows if None).  kv_caches: list of (k_cache, v_cache)."""
+        cfg = self.cfg
+        D, hq, hkv, eps = cfg.head_dim, self.hq, self.hkv, cfg.rms_eps
+        h = ops.embedding(input_ids, self.embed)
+        residual = h
+        x = ops.rmsnorm(h, self.layers[0]["in_norm"], eps)
+        nl = len(self.layers)
+        for i, L in enumerate(self.layers):
+            kc, vc = kv_caches[i]
+            qkv = F.linear(x, L["qkv"])
+            ops.rope_cache(qkv, meta.positions, self.cos_sin, meta.slot_mapping, kc, vc, hq, hkv, D)
+            if meta.prefill:
+                a = ops.flash_prefill(qkv, meta.cu_seqlens, meta.max_len, hq, hkv, D, self.scale, True)
+            else:
+                a = ops.paged_decode(qkv, kc, vc, meta.block_tables, meta.context_lens, hq,
+                                     meta.max_context, self.scale)
+            o = comm.tp_all_reduce(F.linear(a, L["o"]))
+            x = ops.add_rmsnorm(o, residual, L["post_norm"], eps)
+            m = F.linear(ops.silu_mul(F.linear(x, L["gate_up"])), L["down"])
+            m = comm.tp_all_reduce(m)
+            nxt = self.layers[i + 1]["in_norm"] if i + 1 < nl else self.final_norm
+            x = ops.add_rmsnorm(m, residual, nxt, eps)
+        if logits_index is not None:
+            x = x.index_select(0, logits_index)
+        return F.linear(x, self.lm_head)
+
+    def greedy(self, logits: torch.Tensor) -> torch.Tensor:
+        """argmax over the (possibly vocab-parallel) logits -> int64 [R]."""
+        if self.tp == 1:
+            return ops.argmax(logits)
+        idx = ops.argmax(logits)
+        val = logits.gather(1, idx[:, None]).float()
+        pair = torch.cat([val, (idx + self.vocab_start).float()[:, None]], dim=1)  # [R, 2]
+        allp = comm.tp_all_gather_last(pair).view(pair.shape[0], self.tp, 2)
+        best = allp[..., 0].argmax(dim=1)
+        return allp[torch.arange(pair.shape[0], device=pair.device), best, 1].long()
+
+    def full_logits(self, logits: torch.Tensor) -> torch.Tensor:
+        full = comm.tp_all_gather_last(logits)
+        return full[:, : self.cfg.vocab_size]

@@ -1,0 +1,163 @@
+"""Operator dispatch: GPU tensors -> hand-written gfx950 HIP kernels (torch.ops.docqa.*),
+CPU tensors -> the fp32 PyTorch reference in :mod:`docqa_amd.ops.reference`.
+
+The native library is built in-tree by :mod:`docqa_amd.ops.build` into
+``ops/_docqa_C.so``.  On a GPU tensor there is deliberately NO silent fallback: if the
+extension is missing the op raises, so a GPU run can never pass on eager PyTorch by
+accident.  Set ``DOCQA_FORCE_REFERENCE=1`` to route GPU tensors through the reference
+(numerics debugging only).
+"""
+from __future__ import annotations
+
+import os
+import threading
+from pathlib import Path
+
+import torch
+
+from . import reference as ref
+
+_LIB_PATH = Path(__file__).resolve().parent / "_docqa_C.so"
+_lock = threading.Lock()
+_loaded = False
+_load_error: str | None = None
+_FORCE_REF = os.environ.get("DOCQA_FORCE_REFERENCE", "0") == "1"
+
+
+def library_path() -> Path:
+    return _LIB_PATH
+
+
+def load_native(build_if_missing: bool = False) -> bool:
+    """Load ``_docqa_C.so`` (optionally building it first). Returns True on success."""
+    global _loaded, _load_error
+    if _loaded:
+        return True
+    with _lock:
+        if _loaded:
+            return True
+        if not _LIB_PATH.exists() and build_if_missing:
+            from .build import build
+
+            build(verbose=False)
+        if not _LIB_PATH.exists():
+            _load_error = f"native library not built: {_LIB_PATH} (run python -m docqa_amd.ops.build)"
+            return False
+        try:
+            torch.ops.load_library(str(_LIB_PATH))
+            _loaded = True
+        except Exception as e:  # pragma: no cover - surfaced by native()
+            _load_error = f"failed to load {_LIB_PATH}: {e}"
+        return _loaded
+
+
+def native_loaded() -> bool:
+    return _loaded
+
+
+def _native():
+    if not _loaded and not load_native():
+        raise RuntimeError(f"docqa native kernels unavailable on a GPU tensor: {_load_error}")
+    return torch.ops.docqa
+
+
+def _gpu(t: torch.Tensor) -> bool:
+    return t.is_cuda and not _FORCE_REF
+
+
+# ----------------------------------------------------------------------------- norms
+def rmsnorm(x, w, eps: float):
+    if _gpu(x):
+        return _native().rmsnorm(x.contiguous(), w, eps)
+    return ref.rmsnorm(x, w, eps)
+
+
+def add_rmsnorm(x, residual, w, eps: float):
+    """residual <- residual + x (in place, bf16); returns rmsnorm(residual) * w."""
+    if _gpu(x):
+        return _native().add_rmsnorm(x.contiguous(), residual, w, eps)
+    return ref.add_rmsnorm(x, residual, w, eps)
+
+
+def layernorm(x, residual, gamma, beta, eps: float):
+    if _gpu(x):
+        return _native().layernorm(x.contiguous(), residual, gamma, beta, eps)
+    return ref.layernorm(x, residual, gamma, beta, eps)
+
+
+# ----------------------------------------------------------------------------- rope / kv
+def rope_cache(qkv, positions, cos_sin, slot_mapping, k_cache, v_cache, Hq, Hkv, D):
+    if _gpu(qkv):
+        if slot_mapping is None:
+            k_cache = v_cache = qkv  # unused placeholders
+        _native().rope_cache(qkv, positions, cos_sin, slot_mapping, k_cache, v_cache, Hq, Hkv, D)
+        return
+    ref.rope_cache(qkv, positions, cos_sin, slot_mapping, k_cache, v_cache, Hq, Hkv, D)
+
+
+rope_cos_sin = ref.rope_cos_sin
+
+
+# ----------------------------------------------------------------------------- activations
+def silu_mul(gu):
+    if _gpu(gu):
+        return _native().silu_mul(gu.contiguous())
+    return ref.silu_mul(gu)
+
+
+def bias_act(x, bias, residual=None, gelu: bool = False):
+    if _gpu(x):
+        return _native().bias_act(x.contiguous(), bias, residual, gelu)
+    return ref.bias_act(x, bias, residual, gelu)
+
+
+# ----------------------------------------------------------------------------- embeddings
+def embedding(ids, table):
+    if _gpu(table):
+        return _native().embedding(ids, table)
+    return ref.embedding(ids, table)
+
+
+def bert_embed_ln(ids, pos, token_type, wte, wpe, wtt, gamma, beta, eps):
+    if _gpu(wte):
+        return _native().bert_embed_ln(ids, pos, token_type, wte, wpe, wtt, gamma, beta, eps)
+    return ref.bert_embed_ln(ids, pos, token_type, wte, wpe, wtt, gamma, beta, eps)
+
+
+# ----------------------------------------------------------------------------- sampling
+def argmax(logits):
+    if _gpu(logits):
+        return _native().argmax(logits)
+    return ref.argmax(logits)
+
+
+def sample(logits, inv_temp, top_k, top_p, u):
+    if _gpu(logits):
+        return _native().sample(logits.float().contiguous(), inv_temp, top_k, top_p, u)
+    return ref.sample(logits, inv_temp, top_k, top_p, u)
+
+
+# ----------------------------------------------------------------------------- attention
+def paged_decode(q, k_cache, v_cache, block_tables, context_lens, Hq, max_context, scale):
+    if _gpu(q):
+        return _native().paged_decode(q, k_cache, v_cache, block_tables, context_lens, Hq,
+                                      max_context, scale)
+    return ref.paged_decode(q, k_cache, v_cache, block_tables, context_lens, Hq, max_context, scale)
+
+
+def flash_prefill(qkv, cu_seqlens, max_len, Hq, Hkv, D, scale, causal=True):
+    if _gpu(qkv):
+        return _native().flash_prefill(qkv, cu_seqlens, max_len, Hq, Hkv, D, scale, causal)
+    return ref.flash_prefill(qkv, cu_seqlens, max_len, Hq, Hkv, D, scale, causal)
+
+
+# ----------------------------------------------------------------------------- search
+def knn(xb, xb_norms, xq, k: int, inner_product: bool = False, id_offset: int = 0):
+    if _gpu(xb):
+        return _native().knn(xb, xb_norms, xq.float().contiguous(), k, inner_product, id_offset)
+    return ref.knn(xb, xb_norms, xq, k, inner_product, id_offset)
+
+
+# eager-load when a GPU is present so an import on the box fails loudly if unbuilt
+if torch.cuda.is_available() and not _FORCE_REF:
+    load_native()

@@ -1,0 +1,138 @@
+"""Process-group plumbing: one process per GPU, torch.distributed over RCCL ("nccl"
+backend on ROCm = RCCL over xGMI) on the GPU box, gloo on CPU for CI.
+
+Topology on one MI355X node: 8 GPUs fully connected by xGMI (7 point-to-point links
+per GPU).  We split WORLD into
+
+  * tensor-parallel groups (contiguous ranks, TP in {1, 2, 4, 8}) for the generator's
+    per-layer all-reduces, and
+  * data-parallel groups (ranks with equal TP index) for request-level replicas and
+    the sharded vector index (all-gather of per-shard top-k).
+
+Reference parity: the reference has no collectives at all; scale-out
+there is competing AMQP consumers (deid-service/anonymizer.py:97).
+"""
+from __future__ import annotations
+
+import datetime
+import os
+from dataclasses import dataclass
+
+import torch
+import torch.distributed as dist
+
+
+@dataclass
+class ParallelState:
+    rank: int = 0
+    world_size: int = 1
+    local_rank: int = 0
+    tp_size: int = 1
+    tp_rank: int = 0
+    dp_size: int = 1
+    dp_rank: int = 0
+    tp_group: object = None
+    dp_group: object = None
+    backend: str = "none"
+
+    @property
+    def is_distributed(self) -> bool:
+        return self.world_size > 1
+
+
+_STATE = ParallelState()
+
+
+def state() -> ParallelState:
+    return _STATE
+
+
+def init_distributed(tp_size: int = 1, backend: str | None = None, timeout_s: int = 600) -> ParallelState:
+    """Initialise torch.distributed from torchrun env vars (RANK/WORLD_SIZE/MASTER_*).
+
+    Safe to call without a launcher: falls back to a single-process state.
+    """
+    global _STATE
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world == 1 and not dist.is_initialized():
+        _STATE = ParallelState(tp_size=1, backend="none")
+        return _STATE
+    if backend is None:
+        backend = "nccl" if torch.cuda.is_available() else "gloo"
+    os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+    os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    if backend == "nccl":
+        torch.cuda.set_device(local_rank)
+    if not dist.is_initialized():
+        kw = {}
+        if backend == "nccl":
+            kw["device_id"] = torch.device("cuda", local_rank)
+        dist.init_process_group(backend=backend, rank=rank, world_size=world,
+                                timeout=datetime.timedelta(seconds=timeout_s), **kw)
+    if world % tp_size != 0:
+        raise ValueError(f"world size {world} not divisible by tp {tp_size}")
+    dp_size = world // tp_size
+    tp_group = dp_group = None
+    # every rank must create every group in the same order
+    for d in range(dp_size):
+        ranks = list(range(d * tp_size, (d + 1) * tp_size))
+        g = dist.new_group(ranks) if tp_size > 1 else None
+        if rank in ranks:
+            tp_group = g
+    for t in range(tp_size):
+        ranks = list(range(t, world, tp_size))
+        g = dist.new_group(ranks) if dp_size > 1 else None
+        if rank in ranks:
+            dp_group = g
+    _STATE = ParallelState(rank=rank, world_size=world, local_rank=local_rank, tp_size=tp_size,
+                           tp_rank=rank % tp_size, dp_size=dp_size, dp_rank=rank // tp_size,
+                           tp_group=tp_group, dp_group=dp_group, backend=backend)
+    return _STATE
+
+
+def set_state(s: ParallelState) -> None:
+    global _STATE
+    _STATE = s
+
+
+def tp_all_reduce(t: torch.Tensor) -> torch.Tensor:
+    s = _STATE
+    if s.tp_size > 1:
+        dist.all_reduce(t, group=s.tp_group)
+    return t
+
+
+def tp_all_gather_last(t: torch.Tensor) -> torch.Tensor:
+    """All-gather along the last dim across the TP group (vocab-parallel logits)."""
+    s = _STATE
+    if s.tp_size == 1:
+        return t
+    parts = [torch.empty_like(t) for _ in range(s.tp_size)]
+    dist.all_gather(parts, t.contiguous(), group=s.tp_group)
+    return torch.cat(parts, dim=-1)
+
+
+def dp_all_gather(t: torch.Tensor) -> list[torch.Tensor]:
+    s = _STATE
+    if s.dp_size == 1:
+        return [t]
+    parts = [torch.empty_like(t) for _ in range(s.dp_size)]
+    dist.all_gather(parts, t.contiguous(), group=s.dp_group)
+    return parts
+
+
+def barrier() -> None:
+    if dist.is_initialized():
+        if _STATE.backend == "nccl":
+            dist.barrier(device_ids=[torch.cuda.current_device()])
+        else:
+            dist.barrier()
+
+
+def destroy() -> None:
+    global _STATE
+    if dist.is_initialized():
+        dist.destroy_process_group()
+    _STATE = ParallelState()
