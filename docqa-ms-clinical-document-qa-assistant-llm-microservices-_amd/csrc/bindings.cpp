@@ -6,7 +6,7 @@
 #include <torch/library.h>
 #include <ATen/ATen.h>
 #include <c10/hip/HIPStream.h>
-#include <c10/hip/HIPGuard.h>
+#include <c10/core/DeviceGuard.h>
 
 #include "docqa_kernels.h"
 
@@ -24,7 +24,7 @@ at::Tensor rmsnorm(const at::Tensor& x, const at::Tensor& w, double eps) {
   CHECK_GPU(x); CHECK_BF16(x); CHECK_BF16(w); CHECK_CONTIG(x); CHECK_CONTIG(w);
   const int H = x.size(-1);
   TORCH_CHECK(w.numel() == H, "rmsnorm weight size mismatch");
-  c10::hip::HIPGuard g(x.device());
+  c10::DeviceGuard g(x.device());
   auto out = at::empty_like(x);
   const int rows = x.numel() / H;
   CHECK_RC(docqa_rmsnorm(x.data_ptr(), w.data_ptr(), out.data_ptr(), rows, H, (float)eps, stream()), "rmsnorm");
@@ -36,7 +36,7 @@ at::Tensor add_rmsnorm(const at::Tensor& x, at::Tensor residual, const at::Tenso
   CHECK_CONTIG(x); CHECK_CONTIG(residual);
   TORCH_CHECK(x.sizes() == residual.sizes(), "add_rmsnorm shape mismatch");
   const int H = x.size(-1);
-  c10::hip::HIPGuard g(x.device());
+  c10::DeviceGuard g(x.device());
   auto out = at::empty_like(x);
   CHECK_RC(docqa_add_rmsnorm(x.data_ptr(), residual.data_ptr(), w.data_ptr(), out.data_ptr(),
                              x.numel() / H, H, (float)eps, stream()), "add_rmsnorm");
@@ -53,7 +53,7 @@ at::Tensor layernorm(const at::Tensor& x, const c10::optional<at::Tensor>& resid
     TORCH_CHECK(residual->sizes() == x.sizes(), "layernorm residual shape mismatch");
     rp = residual->data_ptr();
   }
-  c10::hip::HIPGuard g(x.device());
+  c10::DeviceGuard g(x.device());
   auto out = at::empty_like(x);
   CHECK_RC(docqa_layernorm(x.data_ptr(), rp, gamma.data_ptr(), beta.data_ptr(), out.data_ptr(),
                            x.numel() / H, H, (float)eps, stream()), "layernorm");
@@ -76,7 +76,7 @@ void rope_cache(at::Tensor qkv, const at::Tensor& positions, const at::Tensor& c
     CHECK_BF16(k_cache); CHECK_BF16(v_cache);
     BS = k_cache.size(2);  // [num_blocks, Hkv, BS, D]
   }
-  c10::hip::HIPGuard g(qkv.device());
+  c10::DeviceGuard g(qkv.device());
   CHECK_RC(docqa_rope_cache(qkv.data_ptr(), positions.data_ptr<int>(), cos_sin.data_ptr<float>(),
                             sm, sm ? k_cache.data_ptr() : nullptr, sm ? v_cache.data_ptr() : nullptr,
                             T, Hq, Hkv, D, qkv.size(-1), BS, stream()), "rope_cache");
@@ -87,7 +87,7 @@ at::Tensor silu_mul(const at::Tensor& gu) {
   const int I2 = gu.size(-1);
   auto sizes = gu.sizes().vec();
   sizes.back() = I2 / 2;
-  c10::hip::HIPGuard g(gu.device());
+  c10::DeviceGuard g(gu.device());
   auto out = at::empty(sizes, gu.options());
   CHECK_RC(docqa_silu_mul(gu.data_ptr(), out.data_ptr(), gu.numel() / I2, I2 / 2, stream()), "silu_mul");
   return out;
@@ -100,7 +100,7 @@ at::Tensor bias_act(const at::Tensor& x, const at::Tensor& bias,
   TORCH_CHECK(bias.numel() == N, "bias size mismatch");
   const void* rp = nullptr;
   if (residual.has_value()) { CHECK_BF16(*residual); CHECK_CONTIG(*residual); rp = residual->data_ptr(); }
-  c10::hip::HIPGuard g(x.device());
+  c10::DeviceGuard g(x.device());
   auto out = at::empty_like(x);
   CHECK_RC(docqa_bias_act(x.data_ptr(), bias.data_ptr(), rp, out.data_ptr(), x.numel() / N, N,
                           gelu ? 1 : 0, stream()), "bias_act");
@@ -112,7 +112,7 @@ at::Tensor embedding(const at::Tensor& ids, const at::Tensor& table) {
   const int H = table.size(1);
   auto sizes = ids.sizes().vec();
   sizes.push_back(H);
-  c10::hip::HIPGuard g(ids.device());
+  c10::DeviceGuard g(ids.device());
   auto out = at::empty(sizes, table.options());
   CHECK_RC(docqa_embedding(ids.data_ptr<int>(), table.data_ptr(), out.data_ptr(), ids.numel(), H, stream()), "embedding");
   return out;
@@ -126,7 +126,7 @@ at::Tensor bert_embed_ln(const at::Tensor& ids, const at::Tensor& pos,
   const int H = wte.size(1);
   const int* tt = nullptr;
   if (token_type.has_value()) { CHECK_I32(*token_type); tt = token_type->data_ptr<int>(); }
-  c10::hip::HIPGuard g(ids.device());
+  c10::DeviceGuard g(ids.device());
   auto out = at::empty({ids.numel(), H}, wte.options());
   CHECK_RC(docqa_bert_embed_ln(ids.data_ptr<int>(), pos.data_ptr<int>(), tt, wte.data_ptr(),
                                wpe.data_ptr(), wtt.data_ptr(), gamma.data_ptr(), beta.data_ptr(),
@@ -143,7 +143,7 @@ at::Tensor argmax(const at::Tensor& logits) {
   int splits = (V + 8191) / 8192;
   if (splits > 64) splits = 64;
   if (splits < 1) splits = 1;
-  c10::hip::HIPGuard g(logits.device());
+  c10::DeviceGuard g(logits.device());
   auto ws_v = at::empty({rows * splits}, logits.options().dtype(at::kFloat));
   auto ws_i = at::empty({rows * splits}, logits.options().dtype(at::kInt));
   auto out = at::empty({rows}, logits.options().dtype(at::kLong));
@@ -159,7 +159,7 @@ at::Tensor sample(const at::Tensor& logits, const at::Tensor& inv_temp, const at
   TORCH_CHECK(logits.scalar_type() == at::kFloat && logits.dim() == 2 && logits.stride(1) == 1,
               "sample wants fp32 [rows, V]");
   CHECK_I32(top_k);
-  c10::hip::HIPGuard g(logits.device());
+  c10::DeviceGuard g(logits.device());
   auto out = at::empty({logits.size(0)}, logits.options().dtype(at::kLong));
   CHECK_RC(docqa_sample(logits.data_ptr<float>(), logits.size(0), logits.size(1), logits.stride(0),
                         inv_temp.data_ptr<float>(), top_k.data_ptr<int>(), top_p.data_ptr<float>(),
@@ -178,7 +178,7 @@ at::Tensor paged_decode(const at::Tensor& q, const at::Tensor& k_cache, const at
   const int Hkv = k_cache.size(1), BS = k_cache.size(2), D = k_cache.size(3);
   const int part = docqa_decode_part_tokens();
   const int max_parts = (max_context + part - 1) / part;
-  c10::hip::HIPGuard g(q.device());
+  c10::DeviceGuard g(q.device());
   auto out = at::empty({B, Hq * D}, q.options());
   auto tmp_out = at::empty({B, Hq, max_parts, D}, q.options().dtype(at::kFloat));
   auto tmp_ml = at::empty({B, Hq, max_parts, 2}, q.options().dtype(at::kFloat));
@@ -196,7 +196,7 @@ at::Tensor flash_prefill(const at::Tensor& qkv, const at::Tensor& cu_seqlens, in
   TORCH_CHECK(qkv.stride(-1) == 1 && qkv.size(-1) == (Hq + 2 * Hkv) * D, "qkv layout mismatch");
   const int T = qkv.numel() / qkv.size(-1);
   const int B = cu_seqlens.numel() - 1;
-  c10::hip::HIPGuard g(qkv.device());
+  c10::DeviceGuard g(qkv.device());
   auto out = at::empty({T, Hq * D}, qkv.options());
   CHECK_RC(docqa_flash_prefill(qkv.data_ptr(), qkv.size(-1), cu_seqlens.data_ptr<int>(),
                                out.data_ptr(), Hq * D, B, max_len, Hq, Hkv, D, (float)scale,
@@ -214,7 +214,7 @@ std::tuple<at::Tensor, at::Tensor> knn(const at::Tensor& xb, const at::Tensor& x
   TORCH_CHECK(xb.size(1) == xq.size(1), "dimension mismatch");
   TORCH_CHECK(k >= 1 && docqa_knn_kpad(k) > 0, "k must be in [1, 32]");
   const int N = xb.size(0), d = xb.size(1), nq = xq.size(0);
-  c10::hip::HIPGuard g(xb.device());
+  c10::DeviceGuard g(xb.device());
   auto out_d = at::empty({nq, k}, xq.options());
   auto out_i = at::empty({nq, k}, xq.options().dtype(at::kLong));
   if (N == 0 || nq == 0) {
@@ -231,6 +231,17 @@ std::tuple<at::Tensor, at::Tensor> knn(const at::Tensor& xb, const at::Tensor& x
                      inner_product ? 1 : 0, ws_d.data_ptr<float>(), ws_i.data_ptr<int>(), nblk,
                      out_d.data_ptr<float>(), out_i.data_ptr<int64_t>(), id_offset, stream()), "knn");
   return {out_d, out_i};
+}
+
+at::Tensor pool_l2(const at::Tensor& h, const at::Tensor& cu_seqlens, bool mean, bool normalize) {
+  CHECK_GPU(h); CHECK_BF16(h); CHECK_CONTIG(h); CHECK_I32(cu_seqlens);
+  const int H = h.size(-1);
+  const int B = cu_seqlens.numel() - 1;
+  c10::DeviceGuard g(h.device());
+  auto out = at::empty({B, H}, h.options().dtype(at::kFloat));
+  CHECK_RC(docqa_pool_l2(h.data_ptr(), cu_seqlens.data_ptr<int>(), B, H, mean ? 1 : 0,
+                         normalize ? 1 : 0, out.data_ptr<float>(), stream()), "pool_l2");
+  return out;
 }
 
 }  // namespace
@@ -254,6 +265,7 @@ TORCH_LIBRARY(docqa, m) {
         "float scale, bool causal) -> Tensor");
   m.def("knn(Tensor xb, Tensor xb_norms, Tensor xq, int k, bool inner_product, int id_offset) "
         "-> (Tensor, Tensor)");
+  m.def("pool_l2(Tensor h, Tensor cu_seqlens, bool mean, bool normalize) -> Tensor");
 }
 
 TORCH_LIBRARY_IMPL(docqa, CUDA, m) {
@@ -270,4 +282,5 @@ TORCH_LIBRARY_IMPL(docqa, CUDA, m) {
   m.impl("paged_decode", &paged_decode);
   m.impl("flash_prefill", &flash_prefill);
   m.impl("knn", &knn);
+  m.impl("pool_l2", &pool_l2);
 }

@@ -46,3 +46,6 @@ int docqa_knn_kpad(int k);
 int docqa_knn(const void* xb, const float* norms, int N, int d, int is_bf16, const float* xq,
               int nq, int k, int metric_ip, float* ws_d, int* ws_i, int nblk, float* out_d,
               int64_t* out_i, int64_t id_offset, hipStream_t s);
+
+int docqa_pool_l2(const void* h, const int* cu, int B, int H, int mean, int normalize, float* out,
+                  hipStream_t s);

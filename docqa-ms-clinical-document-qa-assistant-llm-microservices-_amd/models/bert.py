@@ -1,0 +1,214 @@
+"""BERT-family encoders: the semantic-indexer / llm-qa bi-encoder (all-MiniLM-L6-v2,
+bge-base-en) and the deid-service token classifier (clinical-BERT NER).
+
+Execution is packed varlen (no padding): a batch of B texts is one token stream of T
+tokens with ``cu_seqlens`` -- every kernel works on [T, H] rows, attention is the MFMA
+flash kernel with ``causal=False`` and per-sequence bounds, so a 40-token query and a
+256-token chunk cost what they contain.
+
+Per layer: one fused QKV GEMM (bias in the hipBLASLt epilogue), the bidirectional
+flash kernel reading Q/K/V from the packed buffer, O-proj, fused residual+LayerNorm
+kernel, FFN-up GEMM + fused bias+GELU(erf) kernel, FFN-down, fused residual+LayerNorm.
+Embeddings are one fused gather+add+LayerNorm kernel; pooling one fused
+mean/CLS-pool + L2-normalise kernel.
+
+Reference parity:
+  * ``SentenceTransformer('all-MiniLM-L6-v2').encode([text])`` at
+    semantic-indexer/indexer.py:21,37 and ``HuggingFaceEmbeddings`` at llm-qa/main.py:25
+    (6 layers, hidden 384, 12 heads x 32, FFN 1536, mean pooling, L2 normalised);
+  * ``bge-base-en`` for the 10M-vector config (12 x 768, CLS pooling);
+  * the spaCy/Presidio NER of deid-service/anonymizer.py:29,41-45 is replaced by a
+    BERT token classifier (:class:`BertTokenClassifier`).
+"""
+from __future__ import annotations
+
+import math
+from dataclasses import dataclass
+
+import torch
+import torch.nn.functional as F
+
+from .. import ops
+
+
+@dataclass
+class BertConfig:
+    name: str = "minilm-l6"
+    vocab_size: int = 30522
+    hidden: int = 384
+    layers: int = 6
+    heads: int = 12
+    intermediate: int = 1536
+    max_position: int = 512
+    type_vocab: int = 2
+    eps: float = 1e-12
+    pooling: str = "mean"      # "mean" | "cls"
+    normalize: bool = True
+    max_seq_len: int = 256     # sentence-transformers truncation for MiniLM
+
+    @property
+    def head_dim(self) -> int:
+        return self.hidden // self.heads
+
+    @staticmethod
+    def preset(name: str) -> "BertConfig":
+        if name in ("minilm-l6", "all-MiniLM-L6-v2"):
+            return BertConfig()
+        if name in ("bge-base", "bge-base-en"):
+            return BertConfig(name="bge-base", hidden=768, layers=12, heads=12, intermediate=3072,
+                              pooling="cls", max_seq_len=512)
+        if name in ("clinical-bert", "bert-base"):
+            return BertConfig(name="clinical-bert", vocab_size=28996, hidden=768, layers=12,
+                              heads=12, intermediate=3072, pooling="cls", normalize=False,
+                              max_seq_len=512)
+        if name == "tiny-bert":
+            return BertConfig(name="tiny-bert", vocab_size=1000, hidden=128, layers=2, heads=4,
+                              intermediate=256, max_position=256, max_seq_len=128)
+        raise ValueError(f"unknown bert preset {name}")
+
+
+class BertEncoder:
+    def __init__(self, cfg: BertConfig, device="cuda", dtype=torch.bfloat16, seed: int = 0):
+        self.cfg = cfg
+        self.device = torch.device(device)
+        self.dtype = dtype
+        self.scale = 1.0 / math.sqrt(cfg.head_dim)
+        self._random_init(seed)
+
+    def _random_init(self, seed: int) -> None:
+        cfg, dev, dt = self.cfg, self.device, self.dtype
+        g = torch.Generator(device=dev)
+        g.manual_seed(seed + 1234)
+
+        def w(*shape, s=0.02):
+            t = torch.empty(*shape, device=dev, dtype=dt)
+            t.normal_(0.0, s, generator=g)
+            return t
+
+        def ones(n):
+            return torch.ones(n, device=dev, dtype=dt)
+
+        def zeros(n):
+            return torch.zeros(n, device=dev, dtype=dt)
+
+        H, I = cfg.hidden, cfg.intermediate
+        self.wte = w(cfg.vocab_size, H)
+        self.wpe = w(cfg.max_position, H)
+        self.wtt = w(cfg.type_vocab, H)
+        self.emb_g, self.emb_b = ones(H), zeros(H)
+        self.layers = []
+        for _ in range(cfg.layers):
+            self.layers.append({
+                "qkv_w": w(3 * H, H), "qkv_b": w(3 * H, s=0.01),
+                "o_w": w(H, H), "o_b": w(H, s=0.01),
+                "ln1_g": ones(H), "ln1_b": zeros(H),
+                "up_w": w(I, H), "up_b": w(I, s=0.01),
+                "down_w": w(H, I), "down_b": w(H, s=0.01),
+                "ln2_g": ones(H), "ln2_b": zeros(H),
+            })
+
+    def load_state_dict_hf(self, sd: dict, prefix: str = "") -> None:
+        """Map a Hugging Face BertModel state dict (e.g. sentence-transformers MiniLM)."""
+        dev, dt = self.device, self.dtype
+
+        def get(k):
+            return sd[prefix + k].to(device=dev, dtype=dt).contiguous()
+
+        self.wte = get("embeddings.word_embeddings.weight")
+        self.wpe = get("embeddings.position_embeddings.weight")
+        self.wtt = get("embeddings.token_type_embeddings.weight")
+        self.emb_g = get("embeddings.LayerNorm.weight")
+        self.emb_b = get("embeddings.LayerNorm.bias")
+        self.layers = []
+        for i in range(self.cfg.layers):
+            p = f"encoder.layer.{i}."
+            self.layers.append({
+                "qkv_w": torch.cat([get(p + f"attention.self.{n}.weight") for n in ("query", "key", "value")]),
+                "qkv_b": torch.cat([get(p + f"attention.self.{n}.bias") for n in ("query", "key", "value")]),
+                "o_w": get(p + "attention.output.dense.weight"), "o_b": get(p + "attention.output.dense.bias"),
+                "ln1_g": get(p + "attention.output.LayerNorm.weight"),
+                "ln1_b": get(p + "attention.output.LayerNorm.bias"),
+                "up_w": get(p + "intermediate.dense.weight"), "up_b": get(p + "intermediate.dense.bias"),
+                "down_w": get(p + "output.dense.weight"), "down_b": get(p + "output.dense.bias"),
+                "ln2_g": get(p + "output.LayerNorm.weight"), "ln2_b": get(p + "output.LayerNorm.bias"),
+            })
+
+    # ------------------------------------------------------------------ forward
+    def hidden_states(self, ids: torch.Tensor, cu_seqlens: torch.Tensor, max_len: int,
+                      positions: torch.Tensor | None = None) -> torch.Tensor:
+        """ids int32 [T] (packed), cu_seqlens int32 [B+1] -> last hidden [T, H] bf16."""
+        cfg = self.cfg
+        if positions is None:
+            positions = packed_positions(cu_seqlens, ids.shape[0])
+        h = ops.bert_embed_ln(ids, positions, None, self.wte, self.wpe, self.wtt, self.emb_g,
+                              self.emb_b, cfg.eps)
+        nh, hd = cfg.heads, cfg.head_dim
+        for L in self.layers:
+            qkv = F.linear(h, L["qkv_w"], L["qkv_b"])
+            a = ops.flash_prefill(qkv, cu_seqlens, max_len, nh, nh, hd, self.scale, False)
+            o = F.linear(a, L["o_w"], L["o_b"])
+            h = ops.layernorm(o, h, L["ln1_g"], L["ln1_b"], cfg.eps)
+            u = ops.bias_act(F.linear(h, L["up_w"]), L["up_b"], None, True)
+            d = F.linear(u, L["down_w"], L["down_b"])
+            h = ops.layernorm(d, h, L["ln2_g"], L["ln2_b"], cfg.eps)
+        return h
+
+    def encode_packed(self, ids, cu_seqlens, max_len) -> torch.Tensor:
+        h = self.hidden_states(ids, cu_seqlens, max_len)
+        return ops.pool_l2(h, cu_seqlens, self.cfg.pooling == "mean", self.cfg.normalize)
+
+    @torch.inference_mode()
+    def encode(self, token_lists: list[list[int]]) -> torch.Tensor:
+        """list of token-id lists -> fp32 [B, H] sentence embeddings."""
+        ids, cu, max_len = pack(token_lists, self.cfg.max_seq_len, self.device)
+        return self.encode_packed(ids, cu, max_len)
+
+
+def packed_positions(cu_seqlens: torch.Tensor, T: int) -> torch.Tensor:
+    cu = cu_seqlens.long()
+    seg = torch.repeat_interleave(torch.arange(cu.numel() - 1, device=cu.device), cu[1:] - cu[:-1],
+                                  output_size=T)
+    return (torch.arange(T, device=cu.device) - cu[seg]).int()
+
+
+def pack(token_lists: list[list[int]], max_seq_len: int, device) -> tuple[torch.Tensor, torch.Tensor, int]:
+    flat, cu = [], [0]
+    for t in token_lists:
+        t = t[:max_seq_len]
+        flat.extend(t)
+        cu.append(cu[-1] + len(t))
+    max_len = max((cu[i + 1] - cu[i] for i in range(len(token_lists))), default=0)
+    ids = torch.tensor(flat, dtype=torch.int32).to(device, non_blocking=True)
+    cut = torch.tensor(cu, dtype=torch.int32).to(device, non_blocking=True)
+    return ids, cut, max_len
+
+
+class BertTokenClassifier(BertEncoder):
+    """Token-classification head (linear [num_labels, H]) on the encoder: the NER model
+    of the deid-service (labels: BIO tags over PERSON, DATE_TIME, LOCATION, NRP, ...)."""
+
+    def __init__(self, cfg: BertConfig, labels: list[str], device="cuda", dtype=torch.bfloat16,
+                 seed: int = 0):
+        super().__init__(cfg, device, dtype, seed)
+        self.labels = list(labels)
+        g = torch.Generator(device=self.device)
+        g.manual_seed(seed + 99)
+        n = len(self.labels)
+        npad = (n + 7) // 8 * 8
+        self.cls_w = torch.zeros(npad, cfg.hidden, device=self.device, dtype=dtype)
+        self.cls_w[:n].normal_(0.0, 0.02, generator=g)
+        self.cls_b = torch.zeros(npad, device=self.device, dtype=dtype)
+        self.cls_b[n:] = -1e4  # padded label columns never win the argmax
+
+    @torch.inference_mode()
+    def predict_packed(self, ids, cu_seqlens, max_len) -> torch.Tensor:
+        h = self.hidden_states(ids, cu_seqlens, max_len)
+        logits = F.linear(h, self.cls_w, self.cls_b)
+        return ops.argmax(logits)  # [T] label ids
+
+    @torch.inference_mode()
+    def predict(self, token_lists: list[list[int]]) -> list[list[int]]:
+        ids, cu, max_len = pack(token_lists, self.cfg.max_seq_len, self.device)
+        lab = self.predict_packed(ids, cu, max_len).tolist()
+        cl = cu.tolist()
+        return [lab[cl[i]:cl[i + 1]] for i in range(len(token_lists))]

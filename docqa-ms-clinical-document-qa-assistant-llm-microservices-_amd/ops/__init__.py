@@ -65,6 +65,22 @@ def _gpu(t: torch.Tensor) -> bool:
     return t.is_cuda and not _FORCE_REF
 
 
+class use_reference:
+    """Context manager: route GPU tensors through the PyTorch reference (model-level
+    numerics tests compare a whole forward on native vs reference ops)."""
+
+    def __enter__(self):
+        global _FORCE_REF
+        self._prev = _FORCE_REF
+        _FORCE_REF = True
+        return self
+
+    def __exit__(self, *exc):
+        global _FORCE_REF
+        _FORCE_REF = self._prev
+        return False
+
+
 # ----------------------------------------------------------------------------- norms
 def rmsnorm(x, w, eps: float):
     if _gpu(x):
@@ -156,6 +172,13 @@ def knn(xb, xb_norms, xq, k: int, inner_product: bool = False, id_offset: int = 
     if _gpu(xb):
         return _native().knn(xb, xb_norms, xq.float().contiguous(), k, inner_product, id_offset)
     return ref.knn(xb, xb_norms, xq, k, inner_product, id_offset)
+
+
+# ----------------------------------------------------------------------------- pooling
+def pool_l2(h, cu_seqlens, mean: bool = True, normalize: bool = True):
+    if _gpu(h):
+        return _native().pool_l2(h.contiguous(), cu_seqlens, mean, normalize)
+    return ref.pool_l2(h, cu_seqlens, mean, normalize)
 
 
 # eager-load when a GPU is present so an import on the box fails loudly if unbuilt

@@ -181,3 +181,15 @@ def knn(xb, xb_norms, xq, k, inner_product, id_offset):
     D[:, : vals.shape[1]] = vals
     I[:, : idx.shape[1]] = idx + id_offset
     return D, I
+
+
+def pool_l2(h, cu_seqlens, mean, normalize):
+    cu = cu_seqlens.tolist()
+    out = torch.zeros(len(cu) - 1, h.shape[-1], dtype=torch.float32, device=h.device)
+    for b in range(len(cu) - 1):
+        s0, s1 = cu[b], cu[b + 1]
+        if s1 > s0:
+            out[b] = h[s0:s1].float().mean(0) if mean else h[s0].float()
+    if normalize:
+        out = F.normalize(out, dim=-1, eps=1e-12)
+    return out

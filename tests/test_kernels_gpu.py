@@ -225,3 +225,13 @@ def test_knn_self_query_shipped_index(native):
     norms = (xb ** 2).sum(1)
     D, I = native.knn(xb, norms, xb[:64].clone(), 1, False, 0)
     assert (D[:, 0].abs() < 1e-4).all()
+
+
+@pytest.mark.parametrize("mean", [True, False])
+def test_pool_l2(native, mean):
+    from docqa_amd.ops import reference as R
+
+    lens = [1, 7, 256, 33]
+    cu = torch.tensor([0] + list(torch.tensor(lens).cumsum(0)), device="cuda", dtype=torch.int32)
+    h = torch.randn(sum(lens), 768, device="cuda", dtype=torch.bfloat16)
+    _close(native.pool_l2(h, cu, mean, True), R.pool_l2(h, cu, mean, True), 1e-4)
