@@ -1,0 +1,137 @@
+"""Headline benchmark: end-to-end RAG QA throughput (embed + kNN + generate) and p50
+answer latency with a Llama-3-8B generator (BASELINE.json metric / config 4, scaled
+data-parallel over 1-8 MI355X with the vector index sharded across the GPUs).
+
+One step = one batch of ``--batch`` clinical questions per data-parallel rank, pushed
+through the whole llm-qa path: WordPiece tokenise -> MiniLM-L6 embed (HIP encoder
+kernels) -> kNN top-3 over the sharded flat L2 index (HIP MFMA distance+top-k, RCCL
+all-gathers across ranks) -> stuff prompt -> Llama-3-8B bf16 prefill + greedy decode
+of ``--max-new-tokens`` tokens (HIP attention/norm/rope kernels, hipBLASLt GEMMs,
+HIP-graph decode loop) -> detokenise.  Synthetic clinical notes + random-init weights
+of the named architectures (no checkpoints or datasets are reachable).
+
+Usage: python bench.py [--gpus N] [--steps K] [--warmup W]
+       (N>1: launched by torchrun, one rank per GPU, RANK/WORLD_SIZE from the env)
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import statistics
+import sys
+import time
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parent
+sys.path.insert(0, str(ROOT))
+os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+
+
+def main() -> None:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--batch", type=int, default=64, help="questions per data-parallel rank per step")
+    ap.add_argument("--max-new-tokens", type=int, default=128)
+    ap.add_argument("--llm", default="llama3-8b")
+    ap.add_argument("--embed", default="minilm-l6")
+    ap.add_argument("--notes", type=int, default=1000)
+    ap.add_argument("--tp", type=int, default=1)
+    ap.add_argument("--k", type=int, default=3)
+    ap.add_argument("--max-context", type=int, default=2048)
+    ap.add_argument("--no-graphs", action="store_true")
+    a = ap.parse_args()
+
+    import torch
+    import torch.distributed as dist
+
+    from docqa_amd import ops
+    from docqa_amd.engine.llm_engine import SamplingParams
+    from docqa_amd.parallel import comm
+    from docqa_amd.pipeline.builder import StackConfig, build_stack
+    from docqa_amd.text.synthetic import synthetic_questions
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world != a.gpus:
+        print(f"[bench] warning: --gpus {a.gpus} but WORLD_SIZE {world}", file=sys.stderr)
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local_rank)
+    ps = comm.init_distributed(tp_size=a.tp)
+    assert ops.load_native(), "native HIP kernels not built (python -m docqa_amd.ops.build)"
+    dev = f"cuda:{local_rank}"
+
+    sc = StackConfig(llm=a.llm, embed=a.embed, n_notes=a.notes, max_batch=a.batch,
+                     max_context=a.max_context, k=a.k, use_graphs=not a.no_graphs)
+    pipe, info = build_stack(sc, device=dev)
+    params = SamplingParams(max_new_tokens=a.max_new_tokens, temperature=0.0, stop_on_eos=False)
+
+    # distinct questions per (step, dp rank); identical within a TP group
+    total_steps = a.warmup + a.steps
+    qs = synthetic_questions(total_steps * ps.dp_size * a.batch, seed=123)
+
+    def batch_for(step: int) -> list[str]:
+        base = (step * ps.dp_size + ps.dp_rank) * a.batch
+        return qs[base:base + a.batch]
+
+    for w in range(a.warmup):
+        pipe.answer_batch(batch_for(w), params)
+    torch.cuda.synchronize()
+    comm.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    step_times, stages = [], []
+    for s in range(a.steps):
+        ts = time.perf_counter()
+        ans = pipe.answer_batch(batch_for(a.warmup + s), params)
+        step_times.append(time.perf_counter() - ts)
+        stages.append(pipe.last_times)
+    torch.cuda.synchronize()
+    comm.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+
+    t = torch.tensor([elapsed] + step_times, dtype=torch.float64, device=dev)
+    if dist.is_initialized():
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    elapsed_max = float(t[0])
+    steps_max = [float(x) for x in t[1:]]
+    queries = ps.dp_size * a.batch * a.steps
+    qps = queries / elapsed_max
+    eng = pipe.engine
+    if ps.rank == 0:
+        st = {k: round(1e3 * statistics.mean(getattr(x, k) for x in stages), 2)
+              for k in ("embed_s", "search_s", "prompt_s", "generate_s")}
+        out = {
+            "metric": "e2e_qa_queries_per_sec",
+            "value": round(qps, 3),
+            "unit": "queries/s",
+            "n_gpus": ps.world_size,
+            "steps": a.steps,
+            "warmup": a.warmup,
+            "ms_per_step": round(1e3 * elapsed_max / a.steps, 2),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "bf16",
+            "data": "synthetic clinical notes + questions, random-init weights",
+            "p50_latency_ms": round(1e3 * statistics.median(steps_max), 2),
+            "config": {
+                "model": f"{a.llm} generator + {a.embed} embedder + flat-L2 kNN (k={a.k})",
+                "global_batch": ps.dp_size * a.batch,
+                "seq_len": a.max_context,
+                "max_new_tokens": a.max_new_tokens,
+                "parallelism": f"dp{ps.dp_size}" + (f"xtp{a.tp}" if a.tp > 1 else ""),
+                "index_vectors": info.get("index_vectors"),
+            },
+            "stage_ms_mean": st,
+            "gen_tokens_per_sec": round(ps.dp_size * a.batch * a.max_new_tokens * a.steps / elapsed_max, 1),
+            "avg_prompt_tokens": round(eng.stats.prompt_tokens / max(1, (a.warmup + a.steps) * a.batch), 1),
+        }
+        print(json.dumps(out), flush=True)
+    comm.destroy()
+
+
+if __name__ == "__main__":
+    main()

@@ -62,7 +62,7 @@ class BertConfig:
                               heads=12, intermediate=3072, pooling="cls", normalize=False,
                               max_seq_len=512)
         if name == "tiny-bert":
-            return BertConfig(name="tiny-bert", vocab_size=1000, hidden=128, layers=2, heads=4,
+            return BertConfig(name="tiny-bert", vocab_size=4096, hidden=128, layers=2, heads=4,
                               intermediate=256, max_position=256, max_seq_len=128)
         raise ValueError(f"unknown bert preset {name}")
 

@@ -60,7 +60,7 @@ class LlamaConfig:
                                layers=4, heads=16, kv_heads=4, max_position=4096,
                                bos_token_id=1, eos_token_id=2)
         if name == "tiny":
-            return LlamaConfig(name="tiny", vocab_size=512, hidden=256, intermediate=512,
+            return LlamaConfig(name="tiny", vocab_size=4096, hidden=256, intermediate=512,
                                layers=2, heads=4, kv_heads=2, head_dim=128, max_position=2048,
                                bos_token_id=1, eos_token_id=2)
         raise ValueError(f"unknown llama preset {name}")

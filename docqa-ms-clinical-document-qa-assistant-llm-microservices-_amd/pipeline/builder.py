@@ -1,0 +1,61 @@
+"""Assemble the QA stack (encoder + index + generator) for services, bench and smoke."""
+from __future__ import annotations
+
+import time
+from dataclasses import dataclass
+
+import torch
+
+from ..engine.llm_engine import LLMEngine
+from ..index.flat import FlatIndex
+from ..index.sharded import ShardedFlatIndex
+from ..models.bert import BertConfig, BertEncoder
+from ..models.llama import LlamaConfig, LlamaModel
+from ..parallel import comm
+from ..text.tokenizer import ChatTokenizer, WordPieceTokenizer
+from .corpus import build_corpus, embed_records
+from .rag import RAGPipeline
+
+
+@dataclass
+class StackConfig:
+    llm: str = "llama3-8b"
+    embed: str = "minilm-l6"
+    n_notes: int = 1000
+    kb_dir: str | None = None
+    max_batch: int = 64
+    max_context: int = 2048
+    k: int = 3
+    storage_dtype: torch.dtype = torch.float32
+    use_graphs: bool = True
+    seed: int = 0
+
+
+def build_stack(sc: StackConfig, device="cuda", log=print) -> tuple[RAGPipeline, dict]:
+    info = {}
+    t0 = time.perf_counter()
+    s = comm.state()
+    llm_cfg = LlamaConfig.preset(sc.llm)
+    enc_tok = WordPieceTokenizer()
+    chat_tok = ChatTokenizer(model_vocab=llm_cfg.vocab_size)
+    encoder = BertEncoder(BertConfig.preset(sc.embed), device=device, seed=sc.seed)
+    records = build_corpus(sc.n_notes, sc.kb_dir, sc.seed)
+    # contiguous shard per data-parallel rank: global ids = shard offset + local row
+    n = len(records)
+    lo = n * s.dp_rank // s.dp_size
+    hi = n * (s.dp_rank + 1) // s.dp_size
+    emb = embed_records(encoder, enc_tok, records[lo:hi])
+    local = FlatIndex(encoder.cfg.hidden, "l2", device, sc.storage_dtype, capacity=max(1024, hi - lo))
+    local.add(emb)
+    index = ShardedFlatIndex(local) if s.dp_size > 1 else local
+    if device != "cpu" and torch.device(device).type == "cuda":
+        torch.cuda.synchronize()
+    info["index_build_s"] = time.perf_counter() - t0
+    info["index_vectors"] = n
+    model = LlamaModel(llm_cfg, device=device, seed=sc.seed)
+    engine = LLMEngine(model, max_batch=sc.max_batch, max_context=sc.max_context,
+                       use_graphs=sc.use_graphs)
+    pipe = RAGPipeline(encoder, enc_tok, index, records, engine, chat_tok, k=sc.k,
+                       max_prompt_tokens=sc.max_context - 256)
+    info["setup_s"] = time.perf_counter() - t0
+    return pipe, info

@@ -1,0 +1,125 @@
+"""Retrieval-augmented QA: question -> embed -> kNN top-k -> "stuff" prompt -> generate.
+
+Batched and device-resident end to end: a batch of questions is embedded in one packed
+varlen encoder forward, searched in one fused distance+top-k launch (or the sharded
+all-gather search across GPUs), and all prompts are generated together by the HIP-graph
+decode engine.  Per-stage wall times are recorded for the latency breakdown.
+
+Reference parity (llm-qa/main.py:71-122): ``RetrievalQA.from_chain_type(chain_type=
+"stuff", k=3, return_source_documents=True)`` -> contexts joined with a blank line into
+the prompt's ``{context}``, the user question into ``{question}``; the response carries
+``answer`` and the ``source`` metadata of the k retrieved chunks (duplicates allowed).
+The reference serves one request at a time; here every stage is batched.
+"""
+from __future__ import annotations
+
+import time
+from dataclasses import dataclass, field
+
+import torch
+
+from ..engine.llm_engine import LLMEngine, SamplingParams
+
+# Expert-assistant prompt with the same slots/structure as the reference's
+# QA_CHAIN_PROMPT (context block, strict instructions, practitioner question).
+DEFAULT_TEMPLATE = """Vous êtes un expert en pharmacopée chinoise (MTC) assistant un praticien.
+Les extraits ci-dessous proviennent de la base de connaissances et des dossiers patients ;
+chaque plante y est accompagnée d'un score de pertinence.
+
+EXTRAITS (base MTC et dossier patient) :
+{context}
+
+CONSIGNES :
+1. Repérez le syndrome du patient dans les extraits.
+2. Relevez les plantes associées à ce syndrome.
+3. Ordonnez-les par score de pertinence décroissant (10 = plante Empereur, 7 = plante Ministre).
+4. Répondez par une liste numérotée en justifiant chaque plante par son score et son rôle,
+   par exemple : "1. [Plante] (score 10, Empereur) : recommandée parce que ...".
+
+QUESTION DU PRATICIEN :
+{question}
+
+RÉPONSE DE L'EXPERT :
+"""
+
+
+@dataclass
+class StageTimes:
+    embed_s: float = 0.0
+    search_s: float = 0.0
+    prompt_s: float = 0.0
+    generate_s: float = 0.0
+
+    def total(self) -> float:
+        return self.embed_s + self.search_s + self.prompt_s + self.generate_s
+
+
+@dataclass
+class Answer:
+    answer: str
+    sources: list
+    token_ids: list = field(default_factory=list)
+
+
+class RAGPipeline:
+    def __init__(self, encoder, enc_tokenizer, index, metadata: list[dict], engine: LLMEngine,
+                 chat_tokenizer, k: int = 3, template: str = DEFAULT_TEMPLATE,
+                 max_prompt_tokens: int | None = None):
+        self.encoder = encoder
+        self.enc_tok = enc_tokenizer
+        self.index = index
+        self.metadata = metadata
+        self.engine = engine
+        self.chat_tok = chat_tokenizer
+        self.k = k
+        self.template = template
+        self.max_prompt_tokens = max_prompt_tokens
+        self.last_times = StageTimes()
+
+    def _sync(self):
+        if self.engine.device.type == "cuda":
+            torch.cuda.synchronize()
+
+    def embed(self, texts: list[str]) -> torch.Tensor:
+        return self.encoder.encode(self.enc_tok.encode_batch(texts))
+
+    def retrieve(self, questions: list[str]):
+        q = self.embed(questions)
+        D, I = self.index.search(q, self.k)
+        return D, I
+
+    def build_prompts(self, questions: list[str], I: list[list[int]]) -> list[list[int]]:
+        prompts = []
+        for qtext, ids in zip(questions, I):
+            ctx = "\n\n".join(self.metadata[i]["text_content"] for i in ids if 0 <= i < len(self.metadata))
+            p = self.chat_tok.chat_prompt(self.template.format(context=ctx, question=qtext))
+            if self.max_prompt_tokens and len(p) > self.max_prompt_tokens:
+                p = p[: self.max_prompt_tokens // 2] + p[-self.max_prompt_tokens // 2:]
+            prompts.append(p)
+        return prompts
+
+    @torch.inference_mode()
+    def answer_batch(self, questions: list[str], params: SamplingParams | None = None) -> list[Answer]:
+        params = params or SamplingParams(stop_on_eos=True)
+        t = StageTimes()
+        t0 = time.perf_counter()
+        qemb = self.embed(questions)
+        self._sync()
+        t1 = time.perf_counter()
+        D, I = self.index.search(qemb, self.k)
+        I = I.tolist()  # host needs ids to assemble the prompts
+        t2 = time.perf_counter()
+        prompts = self.build_prompts(questions, I)
+        t3 = time.perf_counter()
+        outs = self.engine.generate(prompts, params)
+        t4 = time.perf_counter()
+        t.embed_s, t.search_s, t.prompt_s, t.generate_s = t1 - t0, t2 - t1, t3 - t2, t4 - t3
+        self.last_times = t
+        res = []
+        for ids, toks in zip(I, outs):
+            srcs = [self.metadata[i].get("source") for i in ids if 0 <= i < len(self.metadata)]
+            res.append(Answer(answer=self.chat_tok.decode(toks), sources=srcs, token_ids=toks))
+        return res
+
+    def answer(self, question: str, params: SamplingParams | None = None) -> Answer:
+        return self.answer_batch([question], params)[0]
