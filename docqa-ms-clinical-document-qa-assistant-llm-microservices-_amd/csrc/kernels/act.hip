@@ -16,12 +16,14 @@ __device__ __forceinline__ float gelu_erf(float x) { return 0.5f * x * (1.f + er
 
 __global__ __launch_bounds__(256) void silu_mul_kernel(const uint16_t* __restrict__ gu,
                                                        uint16_t* __restrict__ out, int T, int I) {
+  // 32-bit index math (T * I / 8 < 2^31 is checked by the launcher): 64-bit integer
+  // division is a ~100-instruction software sequence on CDNA.
   const int cpr = I >> 3;  // chunks per row
-  const size_t total = (size_t)T * cpr;
-  for (size_t idx = (size_t)blockIdx.x * blockDim.x + threadIdx.x; idx < total;
-       idx += (size_t)gridDim.x * blockDim.x) {
-    const size_t t = idx / cpr;
-    const int c = (int)(idx - t * cpr);
+  const int total = T * cpr;
+  for (int idx = blockIdx.x * blockDim.x + threadIdx.x; idx < total;
+       idx += gridDim.x * blockDim.x) {
+    const int t = idx / cpr;
+    const int c = idx - t * cpr;
     const uint4* row = reinterpret_cast<const uint4*>(gu + t * (size_t)(2 * I));
     float g[8], u[8], o[8];
     unpack8(row[c], g);
@@ -38,10 +40,10 @@ __global__ __launch_bounds__(256) void bias_act_kernel(const uint16_t* __restric
                                                        const uint16_t* __restrict__ res,
                                                        uint16_t* __restrict__ out, int T, int N) {
   const int cpr = N >> 3;
-  const size_t total = (size_t)T * cpr;
-  for (size_t idx = (size_t)blockIdx.x * blockDim.x + threadIdx.x; idx < total;
-       idx += (size_t)gridDim.x * blockDim.x) {
-    const int c = (int)(idx % cpr);
+  const int total = T * cpr;
+  for (int idx = blockIdx.x * blockDim.x + threadIdx.x; idx < total;
+       idx += gridDim.x * blockDim.x) {
+    const int c = idx % cpr;
     float v[8], b[8];
     unpack8(reinterpret_cast<const uint4*>(x)[idx], v);
     unpack8(reinterpret_cast<const uint4*>(bias)[c], b);
@@ -63,7 +65,7 @@ static inline int grid_for(size_t work) {
 }
 
 int docqa_silu_mul(const void* gu, void* out, int T, int I, hipStream_t s) {
-  if (I % 8 != 0) return -1;
+  if (I % 8 != 0 || (long long)T * (I / 8) >= (1LL << 31)) return -1;
   if (T == 0) return 0;
   silu_mul_kernel<<<grid_for((size_t)T * (I / 8)), 256, 0, s>>>((const uint16_t*)gu,
                                                                 (uint16_t*)out, T, I);
@@ -73,7 +75,7 @@ int docqa_silu_mul(const void* gu, void* out, int T, int I, hipStream_t s) {
 
 int docqa_bias_act(const void* x, const void* bias, const void* res, void* out, int T, int N,
                    int gelu, hipStream_t s) {
-  if (N % 8 != 0) return -1;
+  if (N % 8 != 0 || (long long)T * (N / 8) >= (1LL << 31)) return -1;
   if (T == 0) return 0;
   const int g = grid_for((size_t)T * (N / 8));
   const uint16_t *xp = (const uint16_t*)x, *bp = (const uint16_t*)bias, *rp = (const uint16_t*)res;

@@ -4,15 +4,18 @@
 // Cache layout: k_cache/v_cache [num_blocks, Hkv, BS, D] bf16; block_tables [B, maxb].
 //
 // Kernel 1, grid (max_parts, Hkv, B), 256 threads: one workgroup owns one KV head of one
-// sequence over a P=256-token partition and serves all G = Hq/Hkv query heads of that
-// group, so every K/V byte is read from HBM exactly once per step (decode attention is
-// a KV-streaming op: ~4 FLOP/byte, far below the VALU roof -- no MFMA needed;
-// cdna_hip_programming.md App. B "Attention decode": K/V straight to VGPRs).
-//   lane = 16 lanes x 16 B per 256-B K row (D=128), so one wave instruction reads four
-//   consecutive tokens = 1 KiB contiguous in the (block, head) slab.
-//   phase 1: scores s[g][t] = q_g . k_t  (16-lane shuffle reduce) -> LDS
-//   phase 2: per-head max / exp2 / sum over the partition (LDS, whole workgroup)
-//   phase 3: acc[g][8 dims] += p[g][t] * v_t, reduced over token groups and waves
+// sequence over a P=256-token partition and serves all G = Hq/Hkv query heads of the
+// group, so every K/V byte is read from HBM exactly once per step.  Decode attention is a
+// KV-streaming op (~4 FLOP/byte, far below the VALU roof): no MFMA, K/V go straight to
+// VGPRs (cdna_hip_programming.md App. B "Attention decode"; the "GEMV / M <= 16" row of
+// §5: no LDS round trip), and the whole design is about keeping HBM requests in flight:
+//   * a 16-lane group owns one token row (16 lanes x 16 B = one 256-B K row), a wave
+//     reads 4 consecutive tokens = 1 KiB contiguous per instruction;
+//   * each of the 16 lane groups of the workgroup is an independent stream with its own
+//     online-softmax state (m, l, acc[G][8 dims]) -- no barrier inside the token loop;
+//   * U=4 tokens per iteration: 4 K rows + 4 V rows (8 x 16-B loads) are issued before
+//     any of them is consumed;
+//   * the 16 streams merge at the end: 4 lane groups by two xor-shuffles, 4 waves via LDS.
 // Output per partition: un-normalised acc + (max, sum) in fp32 workspaces.
 // Kernel 2, grid (Hq, B): log-sum-exp merge of the partitions -> bf16 [B, Hq, D].
 //
@@ -29,7 +32,7 @@ using namespace docqa;
 constexpr int kPart = 256;   // tokens per partition
 constexpr float kLog2e = 1.4426950408889634f;
 
-template <int G, int D>
+template <int G, int D, int U>
 __global__ __launch_bounds__(256) void paged_decode_kernel(
     const uint16_t* __restrict__ q, int q_stride, const uint16_t* __restrict__ k_cache,
     const uint16_t* __restrict__ v_cache, const int* __restrict__ block_tables, int maxb,
@@ -40,18 +43,15 @@ __global__ __launch_bounds__(256) void paged_decode_kernel(
   const int L = context_lens[b];
   const int start = part * kPart;
   if (start >= L) return;
-  const int end = min(L, start + kPart);
-  const int n = end - start;
+  const int n = min(L - start, kPart);
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int chunk = lane & 15;        // 8-dim chunk of the head
-  const int tg = lane >> 4;           // token sub-group inside the wave (0..3)
+  const int tg = lane >> 4;           // lane group = token stream inside the wave
 
-  __shared__ float s_p[G][kPart];
-  __shared__ float s_red[4][G][D];
-  __shared__ float s_stat[2][4][G];
+  __shared__ float s_acc[4][G][D];
+  __shared__ float s_m[4][G], s_l[4][G];
 
-  // q for the G heads of this group, pre-scaled so exp2 can be used
   float qv[G][8];
   const float qs = scale * kLog2e;
 #pragma unroll
@@ -62,135 +62,119 @@ __global__ __launch_bounds__(256) void paged_decode_kernel(
     for (int j = 0; j < 8; ++j) qv[g][j] *= qs;
   }
   const int* bt = block_tables + (size_t)b * maxb;
-  const size_t head_off = (size_t)kvh * BS * D;
+  const size_t head_off = (size_t)kvh * BS * D + chunk * 8;
   const size_t blk_stride = (size_t)Hkv * BS * D;
 
-  // ---- phase 1: scores.  Each wave covers 4 tokens per step, 16 tokens per WG step.
-  for (int base = wave * 4; base < n; base += 16 * 2) {
-    uint4 kv[2];
-    int tok[2];
+  float m[G], l[G], acc[G][8];
 #pragma unroll
-    for (int u = 0; u < 2; ++u) {
-      tok[u] = base + u * 16 + tg;
-      if (tok[u] < n) {
-        const int t = start + tok[u];
-        const int blk = bt[t >> log2BS];
-        const int off = t & (BS - 1);
-        kv[u] = reinterpret_cast<const uint4*>(k_cache + blk * blk_stride + head_off +
-                                               (size_t)off * D)[chunk];
+  for (int g = 0; g < G; ++g) {
+    m[g] = -FLT_MAX;
+    l[g] = 0.f;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[g][j] = 0.f;
+  }
+
+  for (int base = wave * 4 + tg; base < n; base += 16 * U) {
+    uint4 kr[U], vr[U];
+    bool ok[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int tok = base + 16 * u;
+      ok[u] = tok < n;
+      if (ok[u]) {
+        const int t = start + tok;
+        const size_t off = (size_t)bt[t >> log2BS] * blk_stride + head_off +
+                           (size_t)(t & (BS - 1)) * D;
+        kr[u] = *reinterpret_cast<const uint4*>(k_cache + off);
+        vr[u] = *reinterpret_cast<const uint4*>(v_cache + off);
       }
     }
+    float s[U][G];
 #pragma unroll
-    for (int u = 0; u < 2; ++u) {
+    for (int u = 0; u < U; ++u) {
       float kf[8];
-      if (tok[u] < n) unpack8(kv[u], kf);
-      else {
-#pragma unroll
-        for (int j = 0; j < 8; ++j) kf[j] = 0.f;
-      }
+      unpack8(kr[u], kf);
 #pragma unroll
       for (int g = 0; g < G; ++g) {
         float d = 0.f;
 #pragma unroll
         for (int j = 0; j < 8; ++j) d += qv[g][j] * kf[j];
         d = group_sum<16>(d);
-        if (chunk == 0 && tok[u] < n) s_p[g][tok[u]] = d;
-      }
-    }
-  }
-  __syncthreads();
-
-  // ---- phase 2: softmax statistics per head (log2 domain)
-  float m[G], l[G];
-#pragma unroll
-  for (int g = 0; g < G; ++g) {
-    float mx = -FLT_MAX;
-    for (int i = tid; i < n; i += 256) mx = fmaxf(mx, s_p[g][i]);
-    mx = wave_max(mx);
-    if (lane == 0) s_stat[0][wave][g] = mx;
-  }
-  __syncthreads();
-#pragma unroll
-  for (int g = 0; g < G; ++g)
-    m[g] = fmaxf(fmaxf(s_stat[0][0][g], s_stat[0][1][g]), fmaxf(s_stat[0][2][g], s_stat[0][3][g]));
-#pragma unroll
-  for (int g = 0; g < G; ++g) {
-    float sum = 0.f;
-    for (int i = tid; i < n; i += 256) {
-      const float p = exp2f(s_p[g][i] - m[g]);
-      s_p[g][i] = p;
-      sum += p;
-    }
-    sum = wave_sum(sum);
-    if (lane == 0) s_stat[1][wave][g] = sum;
-  }
-  __syncthreads();
-#pragma unroll
-  for (int g = 0; g < G; ++g)
-    l[g] = s_stat[1][0][g] + s_stat[1][1][g] + s_stat[1][2][g] + s_stat[1][3][g];
-
-  // ---- phase 3: P.V
-  float acc[G][8];
-#pragma unroll
-  for (int g = 0; g < G; ++g)
-#pragma unroll
-    for (int j = 0; j < 8; ++j) acc[g][j] = 0.f;
-  for (int base = wave * 4; base < n; base += 16 * 2) {
-    uint4 vv[2];
-    int tok[2];
-#pragma unroll
-    for (int u = 0; u < 2; ++u) {
-      tok[u] = base + u * 16 + tg;
-      if (tok[u] < n) {
-        const int t = start + tok[u];
-        const int blk = bt[t >> log2BS];
-        const int off = t & (BS - 1);
-        vv[u] = reinterpret_cast<const uint4*>(v_cache + blk * blk_stride + head_off +
-                                               (size_t)off * D)[chunk];
+        s[u][g] = ok[u] ? d : -FLT_MAX;
       }
     }
 #pragma unroll
-    for (int u = 0; u < 2; ++u) {
-      if (tok[u] < n) {
+    for (int g = 0; g < G; ++g) {
+      float mx = m[g];
+#pragma unroll
+      for (int u = 0; u < U; ++u) mx = fmaxf(mx, s[u][g]);
+      const float corr = exp2f(m[g] - mx);
+      m[g] = mx;
+      l[g] *= corr;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) acc[g][j] *= corr;
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      if (ok[u]) {
         float vf[8];
-        unpack8(vv[u], vf);
+        unpack8(vr[u], vf);
 #pragma unroll
         for (int g = 0; g < G; ++g) {
-          const float p = s_p[g][tok[u]];
+          const float p = exp2f(s[u][g] - m[g]);
+          l[g] += p;
 #pragma unroll
           for (int j = 0; j < 8; ++j) acc[g][j] += p * vf[j];
         }
       }
     }
   }
-  // reduce over the 4 token sub-groups of the wave (lanes differing in bits 4,5)
+
+  // ---- merge the 4 lane-group streams of the wave (lanes l, l^16, l^32, l^48)
 #pragma unroll
-  for (int g = 0; g < G; ++g)
+  for (int g = 0; g < G; ++g) {
+    float M = fmaxf(m[g], __shfl_xor(m[g], 16, 64));
+    M = fmaxf(M, __shfl_xor(M, 32, 64));
+    const float f = (m[g] == -FLT_MAX) ? 0.f : exp2f(m[g] - M);
+    float lv = l[g] * f;
+    lv += __shfl_xor(lv, 16, 64);
+    lv += __shfl_xor(lv, 32, 64);
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
-      float v = acc[g][j];
-      v += __shfl_xor(v, 16, 64);
-      v += __shfl_xor(v, 32, 64);
-      acc[g][j] = v;
+      float a = acc[g][j] * f;
+      a += __shfl_xor(a, 16, 64);
+      a += __shfl_xor(a, 32, 64);
+      acc[g][j] = a;
     }
+    m[g] = M;
+    l[g] = lv;
+  }
   if (tg == 0) {
 #pragma unroll
-    for (int g = 0; g < G; ++g)
+    for (int g = 0; g < G; ++g) {
 #pragma unroll
-      for (int j = 0; j < 8; ++j) s_red[wave][g][chunk * 8 + j] = acc[g][j];
+      for (int j = 0; j < 8; ++j) s_acc[wave][g][chunk * 8 + j] = acc[g][j];
+      if (chunk == 0) { s_m[wave][g] = m[g]; s_l[wave][g] = l[g]; }
+    }
   }
   __syncthreads();
-  // write partition result: G*D values, 256 threads
-  const int nparts_stride = max_parts;
+  // ---- merge the 4 waves, write the partition result
   for (int i = tid; i < G * D; i += 256) {
     const int g = i / D, d = i % D;
-    const float v = s_red[0][g][d] + s_red[1][g][d] + s_red[2][g][d] + s_red[3][g][d];
+    float M = fmaxf(fmaxf(s_m[0][g], s_m[1][g]), fmaxf(s_m[2][g], s_m[3][g]));
+    float v = 0.f, lsum = 0.f;
+#pragma unroll
+    for (int w = 0; w < 4; ++w) {
+      const float f = (s_m[w][g] == -FLT_MAX) ? 0.f : exp2f(s_m[w][g] - M);
+      v += s_acc[w][g][d] * f;
+      lsum += s_l[w][g] * f;
+    }
     const int h = kvh * G + g;
-    const size_t o = (((size_t)b * (Hkv * G) + h) * nparts_stride + part);
+    const size_t o = ((size_t)b * (Hkv * G) + h) * max_parts + part;
     tmp_out[o * D + d] = v;
     if (d == 0) {
-      tmp_ml[o * 2 + 0] = m[g];
-      tmp_ml[o * 2 + 1] = l[g];
+      tmp_ml[o * 2 + 0] = M;
+      tmp_ml[o * 2 + 1] = lsum;
     }
   }
 }
@@ -213,7 +197,7 @@ __global__ __launch_bounds__(D) void paged_decode_reduce(const float* __restrict
     num += w * tmp_out[(base + p) * D + d];
     den += w * tmp_ml[(base + p) * 2 + 1];
   }
-  out[(size_t)b * out_stride + (size_t)h * D + d] = f2bf(L > 0 ? num / den : 0.f);
+  out[(size_t)b * out_stride + (size_t)h * D + d] = f2bf(den > 0.f ? num / den : 0.f);
 }
 
 int docqa_paged_decode(const void* q, int q_stride, const void* k_cache, const void* v_cache,
@@ -226,15 +210,15 @@ int docqa_paged_decode(const void* q, int q_stride, const void* k_cache, const v
   while ((1 << log2BS) < BS) ++log2BS;
   const int G = Hq / Hkv;
   dim3 grid(max_parts, Hkv, B);
-#define DEC(GG)                                                                             \
-  paged_decode_kernel<GG, 128><<<grid, 256, 0, s>>>(                                        \
+#define DEC(GG, UU)                                                                         \
+  paged_decode_kernel<GG, 128, UU><<<grid, 256, 0, s>>>(                                    \
       (const uint16_t*)q, q_stride, (const uint16_t*)k_cache, (const uint16_t*)v_cache,     \
       block_tables, maxb, context_lens, tmp_out, tmp_ml, Hkv, BS, log2BS, max_parts, scale)
   switch (G) {
-    case 1: DEC(1); break;
-    case 2: DEC(2); break;
-    case 4: DEC(4); break;
-    case 8: DEC(8); break;
+    case 1: DEC(1, 4); break;
+    case 2: DEC(2, 4); break;
+    case 4: DEC(4, 4); break;
+    case 8: DEC(8, 2); break;
     default: return -1;
   }
 #undef DEC

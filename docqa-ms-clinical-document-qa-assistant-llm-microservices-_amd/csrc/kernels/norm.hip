@@ -62,6 +62,59 @@ __global__ __launch_bounds__(256) void rmsnorm_kernel(const uint16_t* __restrict
   }
 }
 
+// Few-row variant (decode: rows = batch <= a few thousand): one 256-thread workgroup per
+// row so a 64-row step still spreads over 64 CUs with 2 chunks per lane, instead of 16
+// workgroups each walking four whole rows.
+template <int NV, bool ADD>
+__global__ __launch_bounds__(256) void rmsnorm_row_kernel(const uint16_t* __restrict__ x,
+                                                          uint16_t* __restrict__ residual,
+                                                          const uint16_t* __restrict__ w,
+                                                          uint16_t* __restrict__ out, int H,
+                                                          float eps) {
+  const int row = blockIdx.x;
+  const int tid = threadIdx.x;
+  const int nchunk = H >> 3;
+  const uint4* xr = reinterpret_cast<const uint4*>(x + (size_t)row * H);
+  uint4* rr = reinterpret_cast<uint4*>(residual + (size_t)row * H);
+  float v[NV][8];
+  float ss = 0.f;
+#pragma unroll
+  for (int i = 0; i < NV; ++i) {
+    const int c = tid + 256 * i;
+    if (c < nchunk) {
+      unpack8(xr[c], v[i]);
+      if constexpr (ADD) {
+        float r[8];
+        unpack8(rr[c], r);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[i][j] = bf2f(f2bf(v[i][j] + r[j]));
+        rr[c] = pack8(v[i]);
+      }
+#pragma unroll
+      for (int j = 0; j < 8; ++j) ss += v[i][j] * v[i][j];
+    }
+  }
+  __shared__ float red[4];
+  ss = wave_sum(ss);
+  if ((tid & 63) == 0) red[tid >> 6] = ss;
+  __syncthreads();
+  ss = red[0] + red[1] + red[2] + red[3];
+  const float inv = rsqrtf(ss / (float)H + eps);
+  const uint4* wr = reinterpret_cast<const uint4*>(w);
+  uint4* orow = reinterpret_cast<uint4*>(out + (size_t)row * H);
+#pragma unroll
+  for (int i = 0; i < NV; ++i) {
+    const int c = tid + 256 * i;
+    if (c < nchunk) {
+      float g[8], o[8];
+      unpack8(wr[c], g);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) o[j] = v[i][j] * inv * g[j];
+      orow[c] = pack8(o);
+    }
+  }
+}
+
 // LayerNorm(x [+ residual]) * gamma + beta; optional residual may alias nothing.
 template <int NV, bool ADD>
 __global__ __launch_bounds__(256) void layernorm_kernel(const uint16_t* __restrict__ x,
@@ -131,6 +184,15 @@ static int launch_rms(const void* x, void* res, const void* w, void* out, int ro
   const int nv = (H / 8 + 63) / 64;
   const uint16_t *xp = (const uint16_t*)x, *wp = (const uint16_t*)w;
   uint16_t *rp = (uint16_t*)res, *op = (uint16_t*)out;
+  if (rows <= 2048 && H >= 1024) {  // few rows: one workgroup per row
+    const int nvr = (H / 8 + 255) / 256;
+    if (nvr <= 1) rmsnorm_row_kernel<1, ADD><<<rows, 256, 0, s>>>(xp, rp, wp, op, H, eps);
+    else if (nvr <= 2) rmsnorm_row_kernel<2, ADD><<<rows, 256, 0, s>>>(xp, rp, wp, op, H, eps);
+    else if (nvr <= 4) rmsnorm_row_kernel<4, ADD><<<rows, 256, 0, s>>>(xp, rp, wp, op, H, eps);
+    else return -1;
+    DOCQA_CHECK_LAUNCH();
+    return 0;
+  }
   if (nv <= 1) rmsnorm_kernel<1, ADD><<<grid, block, 0, s>>>(xp, rp, wp, op, rows, H, eps);
   else if (nv <= 2) rmsnorm_kernel<2, ADD><<<grid, block, 0, s>>>(xp, rp, wp, op, rows, H, eps);
   else if (nv <= 4) rmsnorm_kernel<4, ADD><<<grid, block, 0, s>>>(xp, rp, wp, op, rows, H, eps);

@@ -18,6 +18,7 @@ request in the reference (llm-qa/main.py:117, one request at a time, greedy at T
 from __future__ import annotations
 
 import math
+import os
 import time
 from dataclasses import dataclass
 
@@ -88,6 +89,7 @@ class LLMEngine:
         self.kv = KVCache(self.cfg.layers, num_blocks, model.hkv, self.cfg.head_dim, block_size,
                           self.device, model.dtype)
         self.use_graphs = use_graphs and self.device.type == "cuda"
+        self.tune_decode_gemms = os.environ.get("DOCQA_TUNE_DECODE", "1") == "1"
         self._graphs: dict[int, _DecodeGraph] = {}
         self._pool = None
         self.stats = GenStats()
@@ -158,19 +160,34 @@ class LLMEngine:
 
     def _capture(self, g: _DecodeGraph) -> None:
         # warm up on a side stream (allocator + hipBLASLt heuristics), then capture.
+        # Decode GEMMs are skinny (M = batch bucket) and their shapes are fixed per bucket,
+        # so they are worth an exhaustive hipBLASLt/rocBLAS solution search (PyTorch
+        # TunableOp) during the eager warm-up; the winners are baked into the graph.
+        # Prefill shapes vary per batch and keep the default heuristics.
+        tune = self.tune_decode_gemms
+        tunable = getattr(torch.cuda, "tunable", None)
+        if tune and tunable is not None:
+            tunable.enable(True)
+            tunable.tuning_enable(True)
         saved = [t.clone() for t in (g.tokens, g.positions, g.context_lens)]
-        s = torch.cuda.Stream()
-        s.wait_stream(torch.cuda.current_stream())
-        with torch.cuda.stream(s):
-            self._step_body(g)
-        torch.cuda.current_stream().wait_stream(s)
-        for t, v in zip((g.tokens, g.positions, g.context_lens), saved):
-            t.copy_(v)
-        graph = torch.cuda.CUDAGraph()
-        if self._pool is None:
-            self._pool = torch.cuda.graph_pool_handle()
-        with torch.cuda.graph(graph, pool=self._pool):
-            self._step_body(g)
+        try:
+            s = torch.cuda.Stream()
+            s.wait_stream(torch.cuda.current_stream())
+            with torch.cuda.stream(s):
+                self._step_body(g)
+            torch.cuda.current_stream().wait_stream(s)
+            for t, v in zip((g.tokens, g.positions, g.context_lens), saved):
+                t.copy_(v)
+            if tune and tunable is not None:
+                tunable.tuning_enable(False)
+            graph = torch.cuda.CUDAGraph()
+            if self._pool is None:
+                self._pool = torch.cuda.graph_pool_handle()
+            with torch.cuda.graph(graph, pool=self._pool):
+                self._step_body(g)
+        finally:
+            if tune and tunable is not None:
+                tunable.enable(False)
         for t, v in zip((g.tokens, g.positions, g.context_lens), saved):
             t.copy_(v)
         g.graph = graph

@@ -14,6 +14,14 @@ if [ -n "$PROBE_ARGS" ]; then
   timeout -k 10 600 python scripts/gen_probe.py $PROBE_ARGS > gpurun_out/gen_probe.log 2>&1
   rc=$?; echo "probe rc=$rc"; [ $rc -eq 0 ] || exit $rc
 fi
+if [ -n "$BENCH_ARGS" ]; then
+  timeout -k 10 900 python bench.py $BENCH_ARGS > gpurun_out/bench.log 2>&1
+  rc=$?; echo "bench rc=$rc"; tail -1 gpurun_out/bench.log; [ $rc -eq 0 ] || exit $rc
+fi
+if [ -n "$SMOKE" ]; then
+  timeout -k 10 600 python -c "from __graft_entry__ import smoke; smoke()" > gpurun_out/smoke.log 2>&1
+  rc=$?; echo "smoke rc=$rc"; [ $rc -eq 0 ] || exit $rc
+fi
 if [ -n "$PROF_ARGS" ]; then
   cd /tmp && export TMPDIR=/tmp
   timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$GRAFT_REPO_ROOT/gpurun_out/prof" -o run --output-format csv -- python3 "$GRAFT_REPO_ROOT/scripts/gen_probe.py" $PROF_ARGS > "$GRAFT_REPO_ROOT/gpurun_out/prof.log" 2>&1
