@@ -1,0 +1,87 @@
+"""Environment-variable configuration.
+
+Names and defaults follow the reference so existing deployments keep
+working; the hard-coded constants of the reference are exposed as variables too, plus
+the MI355X knobs of this framework.
+
+| variable | default | reference site |
+|---|---|---|
+| RABBITMQ_HOST | localhost | doc-ingestor/processing.py:7, deid-service/anonymizer.py:20 |
+| DB_HOST / DB_PORT | localhost / 5433 | doc-ingestor/database.py:7-8 |
+| INPUT_QUEUE / OUTPUT_QUEUE | raw_documents_queue / clean_documents_queue | deid-service/anonymizer.py:21-22 |
+| NLP_LANG | en | deid-service/anonymizer.py:24 |
+| OLLAMA_BASE_URL | http://localhost:11434 | llm-qa/main.py:66 (unused: generation is in-process) |
+| SEMANTIC_INDEXER_URL | http://semantic-indexer:8003 | synthese-comparative/core/config.py:10-13 |
+| LLM_QA_URL | http://llm-qa:8004 | synthese-comparative/core/config.py:16-19 |
+| USE_FAKE_RETRIEVAL / USE_FAKE_LLM | true / true | synthese-comparative/core/config.py:22-23 |
+"""
+from __future__ import annotations
+
+import os
+from dataclasses import dataclass, field
+
+
+def env_bool(name: str, default: str = "true") -> bool:
+    """The reference's ``_env_bool``: "1/true/yes/y" (case-insensitive) are true."""
+    return os.getenv(name, default).lower() in ("1", "true", "yes", "y")
+
+
+def env_int(name: str, default: int) -> int:
+    try:
+        return int(os.getenv(name, str(default)))
+    except ValueError:
+        return default
+
+
+@dataclass
+class Settings:
+    # transport / infra (reference names)
+    rabbitmq_host: str = field(default_factory=lambda: os.getenv("RABBITMQ_HOST", "localhost"))
+    bus_backend: str = field(default_factory=lambda: os.getenv("DOCQA_BUS", "inproc"))  # inproc | amqp
+    bus_journal_dir: str = field(default_factory=lambda: os.getenv("DOCQA_BUS_JOURNAL", ""))
+    db_host: str = field(default_factory=lambda: os.getenv("DB_HOST", "localhost"))
+    db_port: str = field(default_factory=lambda: os.getenv("DB_PORT", "5433"))
+    database_url: str = field(default_factory=lambda: os.getenv("DATABASE_URL", "sqlite:///docqa_documents.db"))
+    raw_queue: str = field(default_factory=lambda: os.getenv("INPUT_QUEUE", "raw_documents_queue"))
+    clean_queue: str = field(default_factory=lambda: os.getenv("OUTPUT_QUEUE", "clean_documents_queue"))
+    nlp_lang: str = field(default_factory=lambda: os.getenv("NLP_LANG", "en"))
+    tika_url: str = field(default_factory=lambda: os.getenv("TIKA_URL", ""))  # empty: native extractors
+    upload_dir: str = field(default_factory=lambda: os.getenv("UPLOAD_DIR", "temp_uploads"))
+    # indexer
+    index_dir: str = field(default_factory=lambda: os.getenv("INDEX_DIR", "."))
+    index_file: str = field(default_factory=lambda: os.getenv("INDEX_FILE", "vector_store.faiss"))
+    metadata_file: str = field(default_factory=lambda: os.getenv("METADATA_FILE", "metadata_store.pkl"))
+    default_data_dir: str = field(default_factory=lambda: os.getenv("DEFAULT_DATA_DIR", "default_data"))
+    chunk_size: int = field(default_factory=lambda: env_int("CHUNK_SIZE", 500))
+    embed_model: str = field(default_factory=lambda: os.getenv("EMBED_MODEL", "minilm-l6"))
+    # llm-qa
+    llm_model: str = field(default_factory=lambda: os.getenv("LLM_MODEL", "llama3-8b"))
+    top_k: int = field(default_factory=lambda: env_int("TOP_K", 3))
+    max_new_tokens: int = field(default_factory=lambda: env_int("MAX_NEW_TOKENS", 256))
+    temperature: float = field(default_factory=lambda: float(os.getenv("TEMPERATURE", "0")))
+    max_batch: int = field(default_factory=lambda: env_int("MAX_BATCH", 64))
+    batch_window_ms: int = field(default_factory=lambda: env_int("BATCH_WINDOW_MS", 5))
+    tp_size: int = field(default_factory=lambda: env_int("TP_SIZE", 1))
+    device: str = field(default_factory=lambda: os.getenv("DOCQA_DEVICE", "auto"))
+    # synthese
+    semantic_indexer_url: str = field(default_factory=lambda: os.getenv("SEMANTIC_INDEXER_URL", "http://semantic-indexer:8003"))
+    llm_qa_url: str = field(default_factory=lambda: os.getenv("LLM_QA_URL", "http://llm-qa:8004"))
+    use_fake_retrieval: bool = field(default_factory=lambda: env_bool("USE_FAKE_RETRIEVAL", "true"))
+    use_fake_llm: bool = field(default_factory=lambda: env_bool("USE_FAKE_LLM", "true"))
+    fake_max_chars: int = 1200
+    llm_timeout_s: float = 60.0
+    retrieval_timeout_s: float = 30.0
+
+    def resolved_device(self) -> str:
+        if self.device != "auto":
+            return self.device
+        try:
+            import torch
+
+            return "cuda" if torch.cuda.is_available() else "cpu"
+        except Exception:
+            return "cpu"
+
+
+def settings() -> Settings:
+    return Settings()

@@ -1,5 +1,9 @@
 """Model-level numerics: whole forwards on the native gfx950 kernels vs the same forward
-routed through the fp32 PyTorch reference ops (same weights, same GPU)."""
+routed through the fp32 PyTorch reference ops (same weights, same GPU).
+
+Random-init decoders have nearly flat logits, so greedy token streams are compared only
+where kernels are identical (graph vs eager); across kernel implementations the tests
+compare logits (teacher forcing), which is what numerics parity means."""
 import pytest
 import torch
 
@@ -12,6 +16,11 @@ def native():
 
     assert ops.load_native(build_if_missing=True)
     return ops
+
+
+def _rel(a, b):
+    a, b = a.float(), b.float()
+    return ((a - b).abs().max() / b.abs().max()).item()
 
 
 @pytest.mark.parametrize("preset", ["minilm-l6", "bge-base"])
@@ -28,26 +37,70 @@ def test_bert_encoder_native_vs_reference(native, preset):
     assert cos.min().item() > 0.995, cos
 
 
-def test_llama_prefill_decode_native_vs_reference(native):
-    from docqa_amd.engine.llm_engine import LLMEngine, SamplingParams
+def _prefill_logits(m, kv, prompts, BS):
+    from docqa_amd.models.llama import AttnMeta
+
+    ids, pos, slots, cu = [], [], [], [0]
+    nb = 0
+    tables = []
+    for p in prompts:
+        n = len(p)
+        blocks = list(range(nb, nb + (n + BS) // BS + 1))
+        nb += len(blocks)
+        tables.append(blocks)
+        ids += p
+        pos += list(range(n))
+        slots += [blocks[t // BS] * BS + t % BS for t in range(n)]
+        cu.append(cu[-1] + n)
+    meta = AttnMeta(prefill=True, positions=torch.tensor(pos, dtype=torch.int32, device="cuda"),
+                    slot_mapping=torch.tensor(slots, dtype=torch.int32, device="cuda"),
+                    cu_seqlens=torch.tensor(cu, dtype=torch.int32, device="cuda"),
+                    max_len=max(len(p) for p in prompts))
+    last = torch.tensor(cu[1:], device="cuda") - 1
+    logits = m.forward(torch.tensor(ids, dtype=torch.int32, device="cuda"), meta, kv, last)
+    return logits, tables
+
+
+def _decode_logits(m, kv, prompts, tables, next_tok, BS):
+    from docqa_amd.models.llama import AttnMeta
+
+    B = len(prompts)
+    maxb = max(len(t) for t in tables)
+    bt = torch.zeros(B, maxb, dtype=torch.int32)
+    for i, t in enumerate(tables):
+        bt[i, :len(t)] = torch.tensor(t)
+    lens = [len(p) for p in prompts]
+    slots = [tables[i][lens[i] // BS] * BS + lens[i] % BS for i in range(B)]
+    meta = AttnMeta(prefill=False, positions=torch.tensor(lens, dtype=torch.int32, device="cuda"),
+                    slot_mapping=torch.tensor(slots, dtype=torch.int32, device="cuda"),
+                    block_tables=bt.cuda(),
+                    context_lens=torch.tensor([n + 1 for n in lens], dtype=torch.int32, device="cuda"),
+                    max_context=maxb * BS)
+    return m.forward(torch.tensor(next_tok, dtype=torch.int32, device="cuda"), meta, kv)
+
+
+def test_llama_prefill_decode_logits_native_vs_reference(native):
+    from docqa_amd.engine.kv_cache import KVCache
     from docqa_amd.models.llama import LlamaConfig, LlamaModel
 
     m = LlamaModel(LlamaConfig.preset("llama3-1b-test"), device="cuda")
     g = torch.Generator().manual_seed(1)
     prompts = [torch.randint(0, 32000, (n,), generator=g).tolist() for n in (9, 130, 300)]
-    eng = LLMEngine(m, max_batch=4, max_context=512, use_graphs=True)
-    sp = SamplingParams(max_new_tokens=12, stop_on_eos=False)
-    out_native = eng.generate(prompts, sp)
-    eng_ref = LLMEngine(m, max_batch=4, max_context=512, use_graphs=False)
+    BS = 64
+    nxt = [5, 6, 7]
+    kv1 = KVCache(m.cfg.layers, 64, m.hkv, m.cfg.head_dim, BS).caches
+    kv2 = KVCache(m.cfg.layers, 64, m.hkv, m.cfg.head_dim, BS).caches
+    p1, tables = _prefill_logits(m, kv1, prompts, BS)
+    d1 = _decode_logits(m, kv1, prompts, tables, nxt, BS)
     with native.use_reference():
-        out_ref = eng_ref.generate(prompts, sp)
-    # greedy over random weights: the first tokens must agree; allow late divergence
-    # from bf16 near-ties
-    agree = sum(a[:4] == b[:4] for a, b in zip(out_native, out_ref))
-    assert agree >= 2, (out_native, out_ref)
+        p2, _ = _prefill_logits(m, kv2, prompts, BS)
+        d2 = _decode_logits(m, kv2, prompts, tables, nxt, BS)
+    assert _rel(p1, p2) < 0.03
+    assert _rel(d1, d2) < 0.03
 
 
-def test_llama_graph_vs_eager(native):
+def test_llama_graph_vs_eager(native, monkeypatch):
+    monkeypatch.setenv("DOCQA_TUNE_DECODE", "0")  # same GEMM kernels on both paths
     from docqa_amd.engine.llm_engine import LLMEngine, SamplingParams
     from docqa_amd.models.llama import LlamaConfig, LlamaModel
 
@@ -60,17 +113,37 @@ def test_llama_graph_vs_eager(native):
     assert a == b
 
 
-def test_llama_batch_invariance(native):
-    """A prompt decodes to the same tokens alone and inside a batch (paging correctness)."""
-    from docqa_amd.engine.llm_engine import LLMEngine, SamplingParams
+def test_llama_batch_invariance_logits(native):
+    """A prompt's prefill+decode logits are the same alone and inside a batch (paging and
+    varlen packing correctness)."""
+    from docqa_amd.engine.kv_cache import KVCache
     from docqa_amd.models.llama import LlamaConfig, LlamaModel
 
     m = LlamaModel(LlamaConfig.preset("llama3-1b-test"), device="cuda", seed=5)
     g = torch.Generator().manual_seed(3)
     prompts = [torch.randint(0, 32000, (n,), generator=g).tolist() for n in (50, 200, 3, 90)]
-    sp = SamplingParams(max_new_tokens=10, stop_on_eos=False)
-    eng = LLMEngine(m, max_batch=8, max_context=512)
-    batch = eng.generate(prompts, sp)
-    single = [eng.generate([p], sp)[0] for p in prompts]
-    same = sum(x[:6] == y[:6] for x, y in zip(batch, single))
-    assert same >= 3, (batch, single)
+    BS = 64
+    kv = KVCache(m.cfg.layers, 64, m.hkv, m.cfg.head_dim, BS).caches
+    pb, tb = _prefill_logits(m, kv, prompts, BS)
+    db = _decode_logits(m, kv, prompts, tb, [11, 12, 13, 14], BS)
+    for i, p in enumerate(prompts):
+        kv1 = KVCache(m.cfg.layers, 16, m.hkv, m.cfg.head_dim, BS).caches
+        ps, ts = _prefill_logits(m, kv1, [p], BS)
+        ds = _decode_logits(m, kv1, [p], ts, [11 + i], BS)
+        assert _rel(ps[0], pb[i]) < 0.02
+        assert _rel(ds[0], db[i]) < 0.02
+
+
+def test_engine_greedy_matches_argmax_of_logits(native):
+    """The engine's first generated token is the argmax of the prefill logits."""
+    from docqa_amd.engine.llm_engine import LLMEngine, SamplingParams
+    from docqa_amd.engine.kv_cache import KVCache
+    from docqa_amd.models.llama import LlamaConfig, LlamaModel
+
+    m = LlamaModel(LlamaConfig.preset("llama3-1b-test"), device="cuda", seed=9)
+    g = torch.Generator().manual_seed(4)
+    prompts = [torch.randint(0, 32000, (n,), generator=g).tolist() for n in (33, 70)]
+    kv = KVCache(m.cfg.layers, 16, m.hkv, m.cfg.head_dim, 64).caches
+    logits, _ = _prefill_logits(m, kv, prompts, 64)
+    out = LLMEngine(m, max_batch=2, max_context=256).generate(prompts, SamplingParams(max_new_tokens=2, stop_on_eos=False))
+    assert [o[0] for o in out] == logits.float().argmax(-1).tolist()
