@@ -176,8 +176,7 @@ at::Tensor paged_decode(const at::Tensor& q, const at::Tensor& k_cache, const at
   TORCH_CHECK(q.stride(-1) == 1, "q rows must be contiguous");
   const int B = q.size(0);
   const int Hkv = k_cache.size(1), BS = k_cache.size(2), D = k_cache.size(3);
-  const int part = docqa_decode_part_tokens();
-  const int max_parts = (max_context + part - 1) / part;
+  const int max_parts = docqa_decode_splits(B, Hkv, max_context);
   c10::DeviceGuard g(q.device());
   auto out = at::empty({B, Hq * D}, q.options());
   auto tmp_out = at::empty({B, Hq, max_parts, D}, q.options().dtype(at::kFloat));

@@ -4,7 +4,7 @@
 // Cache layout: k_cache/v_cache [num_blocks, Hkv, BS, D] bf16; block_tables [B, maxb].
 //
 // Kernel 1, grid (max_parts, Hkv, B), 256 threads: one workgroup owns one KV head of one
-// sequence over a P=256-token partition and serves all G = Hq/Hkv query heads of the
+// sequence over one context slice (adaptive split, below) and serves all G = Hq/Hkv query heads of the
 // group, so every K/V byte is read from HBM exactly once per step.  Decode attention is a
 // KV-streaming op (~4 FLOP/byte, far below the VALU roof): no MFMA, K/V go straight to
 // VGPRs (cdna_hip_programming.md App. B "Attention decode"; the "GEMV / M <= 16" row of
@@ -19,8 +19,9 @@
 // Output per partition: un-normalised acc + (max, sum) in fp32 workspaces.
 // Kernel 2, grid (Hq, B): log-sum-exp merge of the partitions -> bf16 [B, Hq, D].
 //
-// Graph capture: the grid is sized for the maximum context, so a captured replay works
-// for any context <= max; partitions past the sequence's length exit immediately.
+// Graph capture: the split count is a function of (batch, Hkv, max context) only, so a
+// captured replay serves every step; the per-sequence slice length is computed on the
+// device from the live context length.
 //
 // Reference parity: decode attention is inside llama.cpp behind Ollama
 // (llm-qa/main.py:69, greedy decode loop of RetrievalQA.invoke at llm-qa/main.py:117).
@@ -29,8 +30,20 @@
 
 using namespace docqa;
 
-constexpr int kPart = 256;   // tokens per partition
+constexpr int kMinChunk = 64;   // smallest context slice worth a workgroup
 constexpr float kLog2e = 1.4426950408889634f;
+
+// Adaptive split: the grid has a fixed number of splits per (sequence, kv head) --
+// fixed so a HIP graph captured once serves every step -- and each sequence's context
+// is cut into that many equal slices (multiples of 64 tokens), so no workgroup is
+// launched for a partition past the end of a short context and long contexts simply get
+// longer slices.  The launcher picks the split count from the batch size so that
+// B x Hkv x splits fills the 256 CUs (batch 1: many splits; batch 64: few).
+__device__ __forceinline__ int split_chunk(int L, int nsplit) {
+  int c = (L + nsplit - 1) / nsplit;
+  c = (c + kMinChunk - 1) / kMinChunk * kMinChunk;
+  return c < kMinChunk ? kMinChunk : c;
+}
 
 template <int G, int D, int U>
 __global__ __launch_bounds__(256) void paged_decode_kernel(
@@ -41,9 +54,10 @@ __global__ __launch_bounds__(256) void paged_decode_kernel(
   static_assert(D == 128, "decode kernel is specialised for head_dim 128");
   const int part = blockIdx.x, kvh = blockIdx.y, b = blockIdx.z;
   const int L = context_lens[b];
-  const int start = part * kPart;
+  const int slice = split_chunk(L, max_parts);
+  const int start = part * slice;
   if (start >= L) return;
-  const int n = min(L - start, kPart);
+  const int n = min(L - start, slice);
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int chunk = lane & 15;        // 8-dim chunk of the head
@@ -187,7 +201,8 @@ __global__ __launch_bounds__(D) void paged_decode_reduce(const float* __restrict
                                                          int out_stride, int Hq, int max_parts) {
   const int h = blockIdx.x, b = blockIdx.y, d = threadIdx.x;
   const int L = context_lens[b];
-  const int np = (L + kPart - 1) / kPart;
+  const int chunk = split_chunk(L, max_parts);
+  const int np = min(max_parts, (L + chunk - 1) / chunk);
   const size_t base = ((size_t)b * Hq + h) * max_parts;
   float M = -FLT_MAX;
   for (int p = 0; p < np; ++p) M = fmaxf(M, tmp_ml[(base + p) * 2]);
@@ -229,4 +244,11 @@ int docqa_paged_decode(const void* q, int q_stride, const void* k_cache, const v
   return 0;
 }
 
-int docqa_decode_part_tokens() { return kPart; }
+// splits per (sequence, kv head): enough workgroups to cover the chip ~4x, at most 64
+int docqa_decode_splits(int B, int Hkv, int max_context) {
+  int s = (4 * 256 + B * Hkv - 1) / (B * Hkv);
+  const int by_len = (max_context + kMinChunk - 1) / kMinChunk;
+  if (s > by_len) s = by_len;
+  if (s > 64) s = 64;
+  return s < 1 ? 1 : s;
+}

@@ -1,0 +1,121 @@
+"""De-identification engine: analyze -> resolve -> replace with ``<ENTITY_TYPE>``.
+
+Reference behaviour (deid-service/anonymizer.py:37-48): empty/None -> ``""``; otherwise
+Presidio analyze over six entity types followed by the default ``replace`` operator, so
+every detected span becomes ``<ENTITY_TYPE>`` (confirmed by the shipped metadata rows
+647-648 containing ``<NRP>`` and ``<PERSON>``).
+
+The learned recognizer is the BERT token classifier on the MI355X (packed varlen batch of
+documents, native encoder kernels, GPU argmax) whose BIO labels are decoded back to
+character spans through the WordPiece offsets.  Pattern and context recognizers run on
+the CPU.  Documents longer than the encoder window are split into overlapping windows.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+
+from .recognizers import ENTITIES, Span, context_spans, pattern_spans, resolve_overlaps
+
+NER_LABELS = ["O", "B-PER", "I-PER", "B-LOC", "I-LOC", "B-NRP", "I-NRP", "B-DATE", "I-DATE"]
+_LABEL_ENTITY = {"PER": "PERSON", "LOC": "LOCATION", "NRP": "NRP", "DATE": "DATE_TIME"}
+
+
+def bio_to_spans(labels: list[str], offsets: list[tuple[int, int]], score: float = 0.85) -> list[Span]:
+    """BIO tag sequence + token char offsets -> entity spans (I- without B- opens a span)."""
+    spans: list[Span] = []
+    cur_type, cur_start, cur_end = None, 0, 0
+    for lab, (s, e) in zip(labels, offsets):
+        if s == e:  # special token
+            continue
+        if lab == "O":
+            if cur_type:
+                spans.append(Span(cur_start, cur_end, _LABEL_ENTITY[cur_type], score))
+                cur_type = None
+            continue
+        tag, typ = lab.split("-", 1)
+        if tag == "B" or typ != cur_type:
+            if cur_type:
+                spans.append(Span(cur_start, cur_end, _LABEL_ENTITY[cur_type], score))
+            cur_type, cur_start, cur_end = typ, s, e
+        else:
+            cur_end = e
+    if cur_type:
+        spans.append(Span(cur_start, cur_end, _LABEL_ENTITY[cur_type], score))
+    return spans
+
+
+@dataclass
+class AnalyzerResult:
+    entity_type: str
+    start: int
+    end: int
+    score: float
+
+
+class DeidEngine:
+    def __init__(self, ner_model=None, tokenizer=None, use_model: bool = False,
+                 window: int = 256, stride: int = 192):
+        self.ner = ner_model
+        self.tok = tokenizer
+        self.use_model = use_model and ner_model is not None and tokenizer is not None
+        self.window = window
+        self.stride = stride
+
+    # ------------------------------------------------------------------ analyze
+    def _model_spans_batch(self, texts: list[str]) -> list[list[Span]]:
+        """Token-classify every window of every text in ONE packed GPU forward."""
+        encs = [self.tok.tok.encode(t, add_special_tokens=False) for t in texts]
+        windows, owners = [], []
+        for di, e in enumerate(encs):
+            n = len(e.ids)
+            w = self.window - 2
+            starts = list(range(0, max(1, n - w + self.stride), self.stride)) or [0]
+            for s0 in starts:
+                windows.append((e.ids[s0:s0 + w], e.offsets[s0:s0 + w]))
+                owners.append(di)
+                if s0 + w >= n:
+                    break
+        cls = self.tok.tok.token_to_id("[CLS]") or 2
+        sep = self.tok.tok.token_to_id("[SEP]") or 3
+        toks = [[cls] + ids + [sep] for ids, _ in windows]
+        preds = self.ner.predict(toks) if toks else []
+        out: list[list[Span]] = [[] for _ in texts]
+        for (ids, offs), owner, p in zip(windows, owners, preds):
+            labels = [self.ner.labels[i] if i < len(self.ner.labels) else "O" for i in p[1:-1]]
+            out[owner] += bio_to_spans(labels, list(offs))
+        return out
+
+    def analyze_batch(self, texts: list[str], entities=None) -> list[list[AnalyzerResult]]:
+        ents = list(entities or ENTITIES)
+        model = self._model_spans_batch(texts) if self.use_model else [[] for _ in texts]
+        res = []
+        for t, ms in zip(texts, model):
+            spans = pattern_spans(t, ents) + context_spans(t, ents) + [s for s in ms if s.entity_type in ents]
+            res.append([AnalyzerResult(s.entity_type, s.start, s.end, s.score) for s in resolve_overlaps(spans)])
+        return res
+
+    def analyze(self, text: str, entities=None, language: str = "en") -> list[AnalyzerResult]:
+        return self.analyze_batch([text], entities)[0]
+
+    # ------------------------------------------------------------------ anonymize
+    @staticmethod
+    def anonymize(text: str, results: list[AnalyzerResult]) -> str:
+        out, last = [], 0
+        for r in sorted(results, key=lambda r: r.start):
+            if r.start < last:
+                continue
+            out.append(text[last:r.start])
+            out.append(f"<{r.entity_type}>")
+            last = r.end
+        out.append(text[last:])
+        return "".join(out)
+
+    def process_batch(self, texts: list[str], entities=None) -> list[str]:
+        res = self.analyze_batch([t or "" for t in texts], entities)
+        return ["" if not t else self.anonymize(t, r) for t, r in zip(texts, res)]
+
+    def process_text_anonymization(self, text, entities=None) -> str:
+        """Reference-compatible entry point (deid-service/anonymizer.py:37-48)."""
+        if not text:
+            return ""
+        return self.process_batch([text], entities)[0]

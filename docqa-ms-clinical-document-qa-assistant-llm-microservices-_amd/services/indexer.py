@@ -1,0 +1,204 @@
+"""semantic-indexer service: clean_documents_queue consumer + search HTTP API (port 8003).
+
+Reference (semantic-indexer/indexer.py:11-143):
+  * startup: load ``vector_store.faiss`` + ``metadata_store.pkl`` if both exist (resume),
+    else build from the ``default_data`` CSVs and save;
+  * consume clean documents (prefetch 1): ``text[i:i+500]`` chunks labelled
+    ``"Dossier Patient {doc_id}"`` / ``"patient_file"``, add, save, ack;
+  * ``add_to_index`` skips blank text.
+Fixes, each covered by tests: the whole document is embedded in one packed GPU batch
+instead of one encode per chunk; snapshots are atomic (temp + rename, index before
+metadata) so a reader never sees mismatched lengths; one writer lock serialises index
+mutation (multiple consumers are safe); the QA side shares the live index object in
+process (no restart needed to see new documents); metadata ``doc_id`` is the real
+document id.
+HTTP (the endpoint the reference's synthese-comparative expects but nobody served,
+synthese-comparative/core/retrieval_client.py:72-91):
+  GET  /api/search/patient-snippets?patient_id&from_date&to_date&focus -> [{doc_id, text}]
+  POST /api/search {"query", "k"} -> hits;  GET /api/index/stats;  GET /health
+"""
+from __future__ import annotations
+
+import json
+import logging
+import threading
+import time
+from pathlib import Path
+
+import torch
+from fastapi import FastAPI
+from fastapi.responses import JSONResponse
+
+from ..bus.broker import get_broker
+from ..config import Settings
+from ..index import faiss_io
+from ..index.flat import FlatIndex
+from ..pipeline.corpus import embed_records
+from ..schemas import SearchRequest
+from ..store import metadata_io
+from ..text.chunking import chunk_chars
+from ..text.kb import kb_records_from_dir, synthetic_kb_records
+
+logger = logging.getLogger("semantic-indexer")
+
+
+class SemanticIndexer:
+    def __init__(self, encoder, tokenizer, settings: Settings | None = None, index: FlatIndex | None = None,
+                 metadata: list | None = None, device: str = "cuda", on_indexed=None):
+        self.st = settings or Settings()
+        self.encoder = encoder
+        self.tok = tokenizer
+        self.device = device
+        self.index = index
+        self.metadata: list[dict] = metadata if metadata is not None else []
+        self.lock = threading.RLock()
+        self.on_indexed = on_indexed  # callback(doc_id) e.g. docs DB status -> INDEXED
+        self._ch = None
+        self.version = 0
+
+    # ------------------------------------------------------------------ paths
+    @property
+    def index_path(self) -> Path:
+        return Path(self.st.index_dir) / self.st.index_file
+
+    @property
+    def meta_path(self) -> Path:
+        return Path(self.st.index_dir) / self.st.metadata_file
+
+    # ------------------------------------------------------------------ lifecycle
+    def startup(self, build_if_missing: bool = True) -> "SemanticIndexer":
+        with self.lock:
+            if self.index_path.exists() and self.meta_path.exists():
+                self.index = FlatIndex.load(self.index_path, device=self.device)
+                self.metadata = metadata_io.read_metadata(self.meta_path)
+                if len(self.metadata) != self.index.ntotal:
+                    raise RuntimeError(f"index/metadata mismatch: {self.index.ntotal} vs {len(self.metadata)}")
+                logger.info("resumed index (%d vectors)", self.index.ntotal)
+            else:
+                self.index = FlatIndex(self.encoder.cfg.hidden, "l2", self.device)
+                self.metadata = []
+                if build_if_missing:
+                    recs = kb_records_from_dir(self.st.default_data_dir) or synthetic_kb_records()
+                    self.add_records(recs)
+                    self.save_state()
+        return self
+
+    def save_state(self) -> None:
+        with self.lock:
+            Path(self.st.index_dir).mkdir(parents=True, exist_ok=True)
+            self.index.save(self.index_path)            # atomic
+            metadata_io.write_metadata(self.meta_path, self.metadata)  # atomic
+
+    # ------------------------------------------------------------------ mutation
+    def add_records(self, records: list[dict]) -> int:
+        recs = [r for r in records if r.get("text_content", "").strip()]
+        if not recs:
+            return 0
+        emb = embed_records(self.encoder, self.tok, recs)
+        with self.lock:
+            if self.index is None:
+                self.index = FlatIndex(self.encoder.cfg.hidden, "l2", self.device)
+            self.index.add(emb)
+            self.metadata.extend(recs)
+            self.version += 1
+        return len(recs)
+
+    def add_to_index(self, text: str, source_name: str, doc_type: str = "knowledge_base", doc_id: str = "KB") -> bool:
+        """Reference-compatible single add (blank text skipped)."""
+        return self.add_records([{"doc_id": doc_id, "text_content": text, "source": source_name,
+                                  "type": doc_type}]) == 1
+
+    def index_document(self, doc_id, text: str, metadata: dict | None = None) -> int:
+        md = metadata or {}
+        recs = [{"doc_id": str(doc_id), "text_content": c, "source": f"Dossier Patient {doc_id}",
+                 "type": "patient_file", "patient_id": md.get("patient_id", str(doc_id)),
+                 "filename": md.get("filename")}
+                for c in chunk_chars(text or "", self.st.chunk_size)]
+        return self.add_records(recs)
+
+    # ------------------------------------------------------------------ queue
+    def callback(self, ch, method, properties, body):
+        try:
+            msg = json.loads(body)
+            doc_id = msg.get("doc_id")
+            n = self.index_document(doc_id, msg.get("original_text_masked", ""), msg.get("metadata"))
+            self.save_state()
+            ch.basic_ack(delivery_tag=method.delivery_tag)
+            logger.info("indexed doc %s (%d chunks)", doc_id, n)
+            if self.on_indexed is not None and isinstance(doc_id, int):
+                self.on_indexed(doc_id)
+        except Exception as e:  # noqa: BLE001
+            logger.error("indexing error: %s", e)
+            ch.basic_nack(delivery_tag=method.delivery_tag, requeue=False)
+
+    def start_consumer(self, broker=None) -> threading.Thread:
+        broker = broker or get_broker(self.st)
+        ch = broker.channel()
+        self._ch = ch
+        ch.queue_declare(queue=self.st.clean_queue, durable=True)
+        ch.basic_qos(prefetch_count=1)
+        ch.basic_consume(queue=self.st.clean_queue, on_message_callback=self.callback)
+        t = threading.Thread(target=ch.start_consuming, name="indexer-consumer", daemon=True)
+        t.start()
+        return t
+
+    def stop_consumer(self) -> None:
+        if self._ch is not None:
+            self._ch.stop_consuming()
+
+    # ------------------------------------------------------------------ query
+    @torch.inference_mode()
+    def search(self, query: str, k: int = 3) -> list[dict]:
+        q = self.encoder.encode(self.tok.encode_batch([query]))
+        with self.lock:
+            D, I = self.index.search(q, k)
+            out = []
+            for d, i in zip(D[0].tolist(), I[0].tolist()):
+                if 0 <= i < len(self.metadata):
+                    m = self.metadata[i]
+                    out.append({"id": i, "score": d, "text": m.get("text_content", ""), "source": m.get("source"),
+                                "type": m.get("type"), "doc_id": str(m.get("doc_id"))})
+            return out
+
+    def patient_snippets(self, patient_id: str, from_date=None, to_date=None, focus=None, limit: int = 20) -> list[dict]:
+        pid = str(patient_id)
+        with self.lock:
+            rows = [(i, m) for i, m in enumerate(self.metadata)
+                    if m.get("type") == "patient_file" and (str(m.get("patient_id")) == pid or str(m.get("doc_id")) == pid)]
+        if focus and rows:
+            q = self.encoder.encode(self.tok.encode_batch([focus]))
+            ids = torch.tensor([i for i, _ in rows], device=self.index.xb.device)
+            with self.lock:
+                xb = self.index.xb.index_select(0, ids).float()
+            d = ((xb - q.to(xb.device)) ** 2).sum(1)
+            order = d.argsort().tolist()
+            rows = [rows[j] for j in order]
+        return [{"doc_id": str(m.get("doc_id")), "text": m.get("text_content", "")} for _, m in rows[:limit]]
+
+
+def create_app(indexer: SemanticIndexer) -> FastAPI:
+    app = FastAPI(title="Semantic Indexer (MI355X)")
+    app.state.indexer = indexer
+
+    @app.get("/health")
+    def health():
+        return {"status": "ok", "service": "semantic-indexer"}
+
+    @app.get("/api/index/stats")
+    def stats():
+        idx = indexer.index
+        return {"ntotal": idx.ntotal if idx is not None else 0, "dim": idx.d if idx is not None else None,
+                "metric": idx.metric if idx is not None else None, "version": indexer.version}
+
+    @app.post("/api/search")
+    def search(req: SearchRequest):
+        if indexer.index is None:
+            return JSONResponse(status_code=503, content={"detail": "Index non chargé."})
+        return indexer.search(req.query, req.k)
+
+    @app.get("/api/search/patient-snippets")
+    def patient_snippets(patient_id: str, from_date: str | None = None, to_date: str | None = None,
+                         focus: str | None = None):
+        return indexer.patient_snippets(patient_id, from_date, to_date, focus)
+
+    return app

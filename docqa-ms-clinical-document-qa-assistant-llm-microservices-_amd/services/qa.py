@@ -1,0 +1,136 @@
+"""llm-qa service (FastAPI, port 8001; 8004 in the synthese deployment).
+
+Contract (llm-qa/main.py:108-126 and synthese-comparative/core/llm_client.py:42-54):
+  POST /ask/                {"question"} -> {"answer", "sources": [source x k]}
+                            503 {"detail": "Index non chargé."} when no index is loaded
+  POST /api/llm/summarize   {"prompt"}   -> {"summary"}   (expected by synthese, missing
+                            in the reference; served here)
+  GET  /health              {"status": "ok", "service": "llm-qa"}
+  GET  /metrics             Prometheus text (requests, batch sizes, stage latencies)
+
+Serving model: the reference answers one blocking request at a time per process
+(llm-qa/main.py:111-117).  Here a dynamic batcher thread drains the request queue every
+``BATCH_WINDOW_MS`` (or as soon as ``MAX_BATCH`` requests wait) and runs the whole batch
+through the RAG pipeline -- one packed embed, one kNN launch, one batched prefill and a
+HIP-graph decode loop -- while the event loop keeps accepting requests.
+"""
+from __future__ import annotations
+
+import asyncio
+import concurrent.futures as cf
+import queue
+import threading
+import time
+
+from fastapi import FastAPI
+from fastapi.responses import JSONResponse, PlainTextResponse
+
+from ..config import Settings
+from ..engine.llm_engine import SamplingParams
+from ..schemas import AskResponse, Query, SummarizeRequest, SummarizeResponse
+from ..utils.metrics import Metrics
+
+
+class DynamicBatcher:
+    def __init__(self, pipeline, settings: Settings, metrics: Metrics):
+        self.pipe = pipeline
+        self.st = settings
+        self.metrics = metrics
+        self.q: queue.Queue = queue.Queue()
+        self._stop = threading.Event()
+        self._t = threading.Thread(target=self._loop, name="qa-batcher", daemon=True)
+        self._t.start()
+
+    def submit(self, kind: str, payload: str) -> cf.Future:
+        f: cf.Future = cf.Future()
+        self.q.put((kind, payload, f, time.perf_counter()))
+        return f
+
+    def _params(self) -> SamplingParams:
+        return SamplingParams(max_new_tokens=self.st.max_new_tokens, temperature=self.st.temperature,
+                              stop_on_eos=True)
+
+    def _loop(self) -> None:
+        while not self._stop.is_set():
+            try:
+                first = self.q.get(timeout=0.1)
+            except queue.Empty:
+                continue
+            batch = [first]
+            deadline = time.perf_counter() + self.st.batch_window_ms / 1e3
+            while len(batch) < self.st.max_batch:
+                rem = deadline - time.perf_counter()
+                if rem <= 0:
+                    break
+                try:
+                    batch.append(self.q.get(timeout=rem))
+                except queue.Empty:
+                    break
+            self._run(batch)
+
+    def _run(self, batch) -> None:
+        asks = [b for b in batch if b[0] == "ask"]
+        sums = [b for b in batch if b[0] == "summarize"]
+        try:
+            if asks:
+                res = self.pipe.answer_batch([b[1] for b in asks], self._params())
+                for (_, _, f, t0), r in zip(asks, res):
+                    self.metrics.observe("ask_latency_s", time.perf_counter() - t0)
+                    f.set_result({"answer": r.answer, "sources": r.sources})
+                self.metrics.observe("ask_batch_size", len(asks))
+                for k, v in vars(self.pipe.last_times).items():
+                    self.metrics.observe(f"stage_{k}", v)
+            if sums:
+                prompts = [self.pipe.chat_tok.chat_prompt(b[1]) for b in sums]
+                lim = self.pipe.max_prompt_tokens
+                if lim:
+                    prompts = [p if len(p) <= lim else p[: lim // 2] + p[-lim // 2:] for p in prompts]
+                outs = self.pipe.engine.generate(prompts, self._params())
+                for (_, _, f, t0), o in zip(sums, outs):
+                    self.metrics.observe("summarize_latency_s", time.perf_counter() - t0)
+                    f.set_result({"summary": self.pipe.chat_tok.decode(o)})
+        except Exception as e:  # noqa: BLE001 - fail every waiter of the batch
+            for b in batch:
+                if not b[2].done():
+                    b[2].set_exception(e)
+
+    def stop(self) -> None:
+        self._stop.set()
+
+
+def create_app(pipeline=None, settings: Settings | None = None) -> FastAPI:
+    st = settings or Settings()
+    metrics = Metrics("llm_qa")
+    app = FastAPI(title="Health LLM Assistant (MI355X)")
+    app.state.pipeline = pipeline
+    app.state.batcher = DynamicBatcher(pipeline, st, metrics) if pipeline is not None else None
+
+    def ready() -> bool:
+        p = app.state.pipeline
+        return p is not None and p.index is not None and p.index.ntotal > 0
+
+    @app.post("/ask/", response_model=AskResponse)
+    async def ask_question(query: Query):
+        if not ready():
+            return JSONResponse(status_code=503, content={"detail": "Index non chargé."})
+        metrics.inc("ask_requests")
+        fut = app.state.batcher.submit("ask", query.question)
+        return await asyncio.wrap_future(fut)
+
+    @app.post("/api/llm/summarize", response_model=SummarizeResponse)
+    async def summarize(req: SummarizeRequest):
+        if app.state.batcher is None:
+            return JSONResponse(status_code=503, content={"detail": "LLM non chargé."})
+        metrics.inc("summarize_requests")
+        fut = app.state.batcher.submit("summarize", req.prompt)
+        return await asyncio.wrap_future(fut)
+
+    @app.get("/health")
+    def health():
+        return {"status": "ok", "service": "llm-qa"}
+
+    @app.get("/metrics")
+    def prom():
+        return PlainTextResponse(metrics.render())
+
+    return app

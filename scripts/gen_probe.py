@@ -21,6 +21,7 @@ def main():
     ap.add_argument("--gen", type=int, default=128)
     ap.add_argument("--iters", type=int, default=2)
     ap.add_argument("--no-graph", action="store_true")
+    ap.add_argument("--max-context", type=int, default=0)
     a = ap.parse_args()
     assert ops.load_native()
     cfg = LlamaConfig.preset(a.model)
@@ -28,7 +29,8 @@ def main():
     m = LlamaModel(cfg, device="cuda")
     torch.cuda.synchronize()
     print(f"init {time.time()-t:.1f}s weights {m.weight_bytes()/1e9:.1f} GB", flush=True)
-    eng = LLMEngine(m, max_batch=a.batch, max_context=a.prompt + a.gen + 64, use_graphs=not a.no_graph)
+    eng = LLMEngine(m, max_batch=a.batch, max_context=a.max_context or (a.prompt + a.gen + 64),
+                    use_graphs=not a.no_graph)
     g = torch.Generator().manual_seed(0)
     prompts = [torch.randint(0, cfg.vocab_size, (a.prompt,), generator=g).tolist() for _ in range(a.batch)]
     sp = SamplingParams(max_new_tokens=a.gen, stop_on_eos=False)

@@ -26,5 +26,6 @@ if [ -n "$PROF_ARGS" ]; then
   cd /tmp && export TMPDIR=/tmp
   timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$GRAFT_REPO_ROOT/gpurun_out/prof" -o run --output-format csv -- python3 "$GRAFT_REPO_ROOT/${PROF_SCRIPT:-scripts/gen_probe.py}" $PROF_ARGS > "$GRAFT_REPO_ROOT/gpurun_out/prof.log" 2>&1
   rc=$?; echo "prof rc=$rc"
+  rm -f "$GRAFT_REPO_ROOT"/gpurun_out/prof/*kernel_trace.csv
 fi
 exit 0

@@ -141,7 +141,7 @@ def test_sample_distribution(native):
 
 
 @pytest.mark.parametrize("G", [1, 4, 8])
-@pytest.mark.parametrize("lens", [[1, 17, 300, 1000], [64], [513, 2]])
+@pytest.mark.parametrize("lens", [[1, 17, 300, 1000], [64], [513, 2], [2000], [65] * 24])
 def test_paged_decode(native, G, lens):
     from docqa_amd.ops import reference as R
 
