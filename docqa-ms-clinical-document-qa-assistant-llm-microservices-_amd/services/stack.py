@@ -1,0 +1,106 @@
+"""The whole DocQA stack in one process (one MI355X, or CPU with tiny models).
+
+Wiring (SURVEY.md §1 data flow, with the process boundaries that carried no compute
+removed): doc-ingestor -> bus(raw_documents_queue) -> deid worker (NER on the GPU) ->
+bus(clean_documents_queue) -> semantic indexer (encoder + HBM index) -> the llm-qa RAG
+pipeline shares the *live* index object, so a document is answerable as soon as its
+status turns INDEXED.  synthese-comparative is wired in REAL mode to the in-process
+retrieval and LLM when ``real_synthese`` is set.  ``launch.py`` serves each app on the
+reference's port.
+"""
+from __future__ import annotations
+
+import logging
+import tempfile
+from dataclasses import dataclass
+
+from ..bus.broker import InProcBroker
+from ..config import Settings
+from ..deid.engine import NER_LABELS, DeidEngine
+from ..engine.llm_engine import LLMEngine
+from ..models.bert import BertConfig, BertEncoder, BertTokenClassifier
+from ..models.llama import LlamaConfig, LlamaModel
+from ..pipeline.rag import RAGPipeline
+from ..store import docs_db
+from ..text.tokenizer import ChatTokenizer, WordPieceTokenizer
+from . import deid_worker, indexer as indexer_mod, ingest, qa, synthese, ui
+
+log = logging.getLogger("docqa.stack")
+
+
+@dataclass
+class StackOptions:
+    llm: str = "llama3-8b"
+    embed: str = "minilm-l6"
+    ner: str = "clinical-bert"
+    device: str = "cuda"
+    max_batch: int = 64
+    max_context: int = 4096
+    use_graphs: bool = True
+    ner_in_loop: bool = False     # run the (random-init) NER model inside de-identification
+    real_synthese: bool = False
+
+
+class _LocalRetrieval(synthese.RetrievalClient):
+    def __init__(self, idx, st):
+        super().__init__(settings=st)
+        self.idx = idx
+
+    async def get_patient_documents(self, patient_id, from_date=None, to_date=None, focus=None):
+        return self.idx.patient_snippets(patient_id, from_date, to_date, focus)
+
+
+class _LocalLLM(synthese.LLMClient):
+    def __init__(self, batcher, st):
+        super().__init__(settings=st)
+        self.batcher = batcher
+
+    def summarize(self, prompt: str, max_chars: int = 1200) -> str:
+        try:
+            out = self.batcher.submit("summarize", prompt).result(timeout=self.st.llm_timeout_s)["summary"]
+            return out or self._summarize_fake(prompt, max_chars)
+        except Exception:  # noqa: BLE001 - same fallback as the HTTP client
+            return self._summarize_fake(prompt, max_chars)
+
+
+class DocQAStack:
+    def __init__(self, opts: StackOptions, settings: Settings | None = None):
+        self.opts = opts
+        self.st = settings or Settings()
+        if not self.st.upload_dir or self.st.upload_dir == "temp_uploads":
+            self.st.upload_dir = tempfile.mkdtemp(prefix="docqa_uploads_")
+        dev = opts.device
+        self.broker = InProcBroker(self.st.bus_journal_dir or None)
+        self.db = docs_db.DocsDB(self.st.database_url)
+        self.enc_tok = WordPieceTokenizer()
+        llm_cfg = LlamaConfig.preset(opts.llm)
+        self.chat_tok = ChatTokenizer(model_vocab=llm_cfg.vocab_size)
+        self.encoder = BertEncoder(BertConfig.preset(opts.embed), device=dev)
+        ner_model = BertTokenClassifier(BertConfig.preset(opts.ner), NER_LABELS, device=dev) if opts.ner_in_loop else None
+        self.deid_engine = DeidEngine(ner_model, self.enc_tok, use_model=opts.ner_in_loop)
+        self.indexer = indexer_mod.SemanticIndexer(
+            self.encoder, self.enc_tok, self.st, device=dev,
+            on_indexed=lambda i: self.db.set_status(i, docs_db.STATUS_INDEXED)).startup()
+        self.model = LlamaModel(llm_cfg, device=dev)
+        self.engine = LLMEngine(self.model, max_batch=opts.max_batch, max_context=opts.max_context,
+                                use_graphs=opts.use_graphs)
+        self.pipeline = RAGPipeline(self.encoder, self.enc_tok, self.indexer.index, self.indexer.metadata,
+                                    self.engine, self.chat_tok, k=self.st.top_k,
+                                    max_prompt_tokens=opts.max_context - self.st.max_new_tokens - 8)
+        self.deid = deid_worker.DeidWorker(self.deid_engine, self.st, self.broker).start()
+        self.indexer.start_consumer(self.broker)
+        self.ingest_app = ingest.create_app(self.st, self.db, self.broker)
+        self.qa_app = qa.create_app(self.pipeline, self.st)
+        self.indexer_app = indexer_mod.create_app(self.indexer)
+        if opts.real_synthese:
+            self.synthese_app = synthese.create_app(
+                self.st, _LocalLLM(self.qa_app.state.batcher, self.st), _LocalRetrieval(self.indexer, self.st))
+        else:
+            self.synthese_app = synthese.create_app(self.st)
+        self.ui_app = ui.create_app()
+
+    def close(self) -> None:
+        self.deid.stop()
+        self.indexer.stop_consumer()
+        if self.qa_app.state.batcher is not None:
+            self.qa_app.state.batcher.stop()

@@ -1,0 +1,270 @@
+"""Service contracts on CPU (tiny random models, in-process bus).  Mirrors the
+reference's per-service unit tests (doc-ingestor/tests/test_processing.py,
+deid-service/tests/test_anonymizer.py, semantic-indexer/tests/test_indexer.py,
+synthese-comparative/tests/test_llm_client.py) and adds end-to-end pipeline tests the
+reference never had (ingest -> deid -> index -> ask / synthese)."""
+import json
+import time
+from unittest.mock import MagicMock, patch
+
+import pytest
+from fastapi.testclient import TestClient
+
+from docqa_amd.bus.broker import InProcBroker
+from docqa_amd.config import Settings
+from docqa_amd.services.multipart import FilePart, encode_multipart
+
+
+# ------------------------------------------------------------------ doc-ingestor
+def test_extract_text_strip_and_none(tmp_path):
+    from docqa_amd.text.extraction import extract_text_from_file
+
+    p = tmp_path / "a.txt"
+    p.write_text("\n  Extracted Text  \n", encoding="utf-8")
+    assert extract_text_from_file(str(p)) == "Extracted Text"
+    assert extract_text_from_file(str(tmp_path / "missing.pdf")) is None
+
+
+def test_extract_pdf_and_docx(tmp_path):
+    from docqa_amd.text.extraction import extract_text_from_file, make_docx, make_pdf
+
+    txt = "Patient : Jean Martin\nTraitement par (warfarine) 5 mg"
+    for name, data in (("a.pdf", make_pdf(txt)), ("b.pdf", make_pdf(txt, compress=False)),
+                       ("c.docx", make_docx(txt))):
+        p = tmp_path / name
+        p.write_bytes(data)
+        out = extract_text_from_file(str(p))
+        assert "Jean Martin" in out and "(warfarine) 5 mg" in out, (name, out)
+
+
+def test_publish_to_queue_body_and_queue():
+    from docqa_amd.services.ingest import publish_to_queue
+
+    b = InProcBroker()
+    publish_to_queue(b, "raw_documents_queue", 123, "Sample text", {"type": "report"})
+    body = b.get_nowait("raw_documents_queue")
+    assert body == json.dumps({"doc_id": 123, "text": "Sample text", "metadata": {"type": "report"}}).encode()
+
+
+def _ingest_app(tmp_path):
+    from docqa_amd.services import ingest
+    from docqa_amd.store.docs_db import DocsDB
+
+    st = Settings()
+    st.upload_dir = str(tmp_path / "up")
+    b = InProcBroker()
+    return ingest.create_app(st, DocsDB("sqlite://"), b), b
+
+
+def test_ingest_success_error_and_listing(tmp_path):
+    app, broker = _ingest_app(tmp_path)
+    c = TestClient(app)
+    body, ct = encode_multipart({"file": FilePart("note.txt", "text/plain", "Bonjour docteur".encode()),
+                                 "doc_type": "compte-rendu"})
+    r = c.post("/ingest/", content=body, headers={"content-type": ct})
+    assert r.status_code == 200 and r.json() == {"message": "Ingestion réussie", "doc_id": 1}
+    msg = json.loads(broker.get_nowait("raw_documents_queue"))
+    assert list(msg) == ["doc_id", "text", "metadata"]
+    assert msg["metadata"] == {"filename": "note.txt", "type": "compte-rendu"}
+    body, ct = encode_multipart({"file": FilePart("empty.txt", "text/plain", b"   "), "doc_type": "x"})
+    r = c.post("/ingest/", content=body, headers={"content-type": ct})
+    assert r.status_code == 200 and r.json() == {"error": "Impossible d'extraire le texte"}
+    docs = c.get("/documents/").json()
+    assert [d["status"] for d in docs] == ["PROCESSED", "ERROR_EXTRACTION"]
+    assert set(docs[0]) == {"id", "filename", "upload_date", "status", "doc_type"}
+    body, ct = encode_multipart({"file": FilePart("n.txt", "text/plain", b"x")})
+    assert c.post("/ingest/", content=body, headers={"content-type": ct}).status_code == 422
+    assert c.get("/health").json() == {"status": "ok", "service": "doc-ingestor"}
+
+
+def test_ingest_queue_failure_sets_error_queue(tmp_path):
+    app, broker = _ingest_app(tmp_path)
+    broker.publish = MagicMock(side_effect=RuntimeError("broker down"))
+    c = TestClient(app)
+    body, ct = encode_multipart({"file": FilePart("n.txt", "text/plain", b"texte"), "doc_type": "x"})
+    r = c.post("/ingest/", content=body, headers={"content-type": ct})
+    assert r.json() == {"error": "broker down"}
+    assert c.get("/documents/").json()[0]["status"] == "ERROR_QUEUE"
+
+
+# ------------------------------------------------------------------ deid
+def test_anonymizer_empty_and_none():
+    from docqa_amd.deid.engine import DeidEngine
+
+    e = DeidEngine()
+    assert e.process_text_anonymization("") == ""
+    assert e.process_text_anonymization(None) == ""
+
+
+def test_anonymizer_masks_pii():
+    from docqa_amd.deid.engine import DeidEngine
+
+    text = ("Patient : Jean Martin, né le 12/03/1980 à Lyon, nationalité française. "
+            "Tél 06 12 34 56 78, mail jean.martin@example.com. Suivi par Dr Sophie Durand.")
+    out = DeidEngine().process_text_anonymization(text)
+    for pii in ("Jean Martin", "12/03/1980", "Lyon", "française", "06 12 34 56 78",
+                "jean.martin@example.com", "Sophie Durand"):
+        assert pii not in out, (pii, out)
+    for tag in ("<PERSON>", "<DATE_TIME>", "<LOCATION>", "<NRP>", "<PHONE_NUMBER>", "<EMAIL_ADDRESS>"):
+        assert tag in out, (tag, out)
+
+
+def test_overlap_resolution_prefers_score_then_length():
+    from docqa_amd.deid.recognizers import Span, resolve_overlaps
+
+    spans = [Span(0, 10, "PERSON", 0.85), Span(2, 5, "DATE_TIME", 0.85), Span(8, 20, "EMAIL_ADDRESS", 1.0)]
+    kept = resolve_overlaps(spans)
+    assert [(s.entity_type, s.start) for s in kept] == [("DATE_TIME", 2), ("EMAIL_ADDRESS", 8)]
+
+
+def test_bio_decoding():
+    from docqa_amd.deid.engine import bio_to_spans
+
+    labels = ["O", "B-PER", "I-PER", "O", "I-LOC", "B-NRP"]
+    offs = [(0, 0), (0, 4), (5, 10), (11, 13), (14, 18), (19, 25)]
+    sp = bio_to_spans(labels, offs)
+    assert [(s.entity_type, s.start, s.end) for s in sp] == [("PERSON", 0, 10), ("LOCATION", 14, 18), ("NRP", 19, 25)]
+
+
+def test_deid_worker_callback_ack_nack():
+    from docqa_amd.services.deid_worker import DeidWorker
+
+    b = InProcBroker()
+    w = DeidWorker(broker=b)
+    ch = b.channel()
+    method = MagicMock(delivery_tag=1)
+    ch._unacked[1] = ("raw_documents_queue", "m1", b"")
+    w.callback(ch, method, None, json.dumps({"doc_id": 7, "text": "Patient : Jean Martin", "metadata": {"a": 1}}))
+    out = json.loads(b.get_nowait("clean_documents_queue"))
+    assert out["doc_id"] == 7 and out["metadata"] == {"a": 1} and "<PERSON>" in out["original_text_masked"]
+    assert isinstance(out["processed_at"], float)
+    ch._unacked[2] = ("raw_documents_queue", "m2", b"not json")
+    w.callback(ch, MagicMock(delivery_tag=2), None, b"not json")
+    assert b.get_nowait("raw_documents_queue.dlq") == b"not json"  # dead-lettered, not lost
+
+
+# ------------------------------------------------------------------ bus
+def test_broker_prefetch_ack_and_journal_redelivery(tmp_path):
+    b = InProcBroker(str(tmp_path / "j"))
+    b.publish("q", b"m1")
+    b.publish("q", b"m2")
+    ch = b.channel()
+    ch.basic_qos(prefetch_count=1)
+    seen = []
+    ch.basic_consume("q", lambda c, m, p, body: seen.append((m.delivery_tag, body)))
+    assert ch._dispatch_one(0.01) and not ch._dispatch_one(0.01)  # prefetch=1 blocks the 2nd
+    ch.basic_ack(seen[0][0])
+    assert ch._dispatch_one(0.01) and seen[1][1] == b"m2"
+    # crash before acking m2: a new broker on the same journal redelivers it
+    b2 = InProcBroker(str(tmp_path / "j"))
+    got = b2._get("q", 0.01)
+    assert got is not None and got[1] == b"m2" and got[2] is True
+
+
+# ------------------------------------------------------------------ synthese
+def test_llm_client_fake_and_fallback():
+    from docqa_amd.services.synthese import LLMClient
+
+    c = LLMClient(base_url="http://fake-url")
+    assert c._summarize_fake("Short text", max_chars=100) == "Short text"
+    assert c._summarize_fake("Hello World", max_chars=5) == "World"
+    with patch("docqa_amd.services.synthese.httpx.Client") as cls:
+        inst = cls.return_value.__enter__.return_value
+        resp = MagicMock()
+        resp.json.return_value = {"summary": "Summarized text"}
+        inst.post.return_value = resp
+        assert c._call_llm_qa_sync("Prompt") == "Summarized text"
+        inst.post.assert_called_once()
+    with patch.object(LLMClient, "_call_llm_qa_sync", return_value="Remote summary"):
+        assert c._summarize_remote("Prompt") == "Remote summary"
+    with patch.object(LLMClient, "_call_llm_qa_sync", side_effect=Exception("Network error")):
+        assert c._summarize_remote("This is a fallback text") == "This is a fallback text"
+
+
+def test_env_bool_semantics(monkeypatch):
+    from docqa_amd.config import env_bool
+
+    for v, exp in (("1", True), ("TRUE", True), ("y", True), ("no", False), ("0", False)):
+        monkeypatch.setenv("X_FLAG", v)
+        assert env_bool("X_FLAG") is exp
+
+
+def test_synthese_routes_fake_mode():
+    from docqa_amd.services.synthese import create_app
+
+    c = TestClient(create_app())
+    assert c.get("/api/status").json() == {"status": "SyntheseComparative is running"}
+    r = c.post("/api/synthese/patient", json={"patient_id": "P1", "focus": "anticoagulant"}).json()
+    assert r["type"] == "single_patient_summary" and r["patient_alias"] == "PATIENT_P1"
+    assert r["sections"][0]["title"] == "Synthèse clinique" and len(r["sources"]) == 2
+    assert all(len(s["snippet"]) <= 300 for s in r["sources"])
+    assert c.post("/api/synthese/comparaison", json={"patient_ids": ["A"]}).status_code == 400
+    r = c.post("/api/synthese/comparaison", json={"patient_ids": ["A", "B", "C"]}).json()
+    assert r["type"] == "multi_patient_comparison" and r["patients"] == ["PATIENT_A", "PATIENT_B", "PATIENT_C"]
+    assert len(r["sources"]) == 6 and r["comparison_table"][0]["dimension"]
+
+
+def test_synthese_404_when_no_docs():
+    from docqa_amd.services.synthese import RetrievalClient, create_app
+
+    class Empty(RetrievalClient):
+        async def get_patient_documents(self, *a, **k):
+            return []
+
+    c = TestClient(create_app(retrieval_client=Empty()))
+    assert c.post("/api/synthese/patient", json={"patient_id": "X"}).status_code == 404
+
+
+# ------------------------------------------------------------------ full stack (tiny models)
+@pytest.fixture(scope="module")
+def stack(tmp_path_factory):
+    from docqa_amd.services.stack import DocQAStack, StackOptions
+
+    d = tmp_path_factory.mktemp("stack")
+    st = Settings()
+    st.index_dir = str(d)
+    st.default_data_dir = str(d / "nodata")
+    st.database_url = "sqlite://"
+    st.max_new_tokens = 4
+    s = DocQAStack(StackOptions(llm="tiny", embed="tiny-bert", ner="tiny-bert", device="cpu",
+                                max_batch=4, max_context=1024, use_graphs=False, real_synthese=True), st)
+    yield s
+    s.close()
+
+
+def test_stack_ingest_to_answer(stack):
+    ing = TestClient(stack.ingest_app)
+    note = "Patient : Jean Martin, né le 01/02/1970. Syndrome Vide de Qi de la Rate. " * 12
+    body, ct = encode_multipart({"file": FilePart("n.txt", "text/plain", note.encode()), "doc_type": "compte-rendu"})
+    doc_id = ing.post("/ingest/", content=body, headers={"content-type": ct}).json()["doc_id"]
+    for _ in range(200):
+        if ing.get(f"/documents/{doc_id}").json()["status"] == "INDEXED":
+            break
+        time.sleep(0.05)
+    assert ing.get(f"/documents/{doc_id}").json()["status"] == "INDEXED"
+    rows = [m for m in stack.indexer.metadata if m["source"] == f"Dossier Patient {doc_id}"]
+    assert len(rows) == (len(note) + 499) // 500          # 500-char chunks
+    assert all("Jean Martin" not in m["text_content"] for m in rows)  # de-identified before indexing
+    idx = TestClient(stack.indexer_app)
+    snips = idx.get("/api/search/patient-snippets", params={"patient_id": str(doc_id)}).json()
+    assert len(snips) == len(rows) and snips[0]["doc_id"] == str(doc_id)
+    qa = TestClient(stack.qa_app)
+    r = qa.post("/ask/", json={"question": "Quelles plantes pour un Vide de Qi ?"})
+    assert r.status_code == 200
+    j = r.json()
+    assert set(j) == {"answer", "sources"} and len(j["sources"]) == 3
+    s = qa.post("/api/llm/summarize", json={"prompt": "Résume ce dossier."}).json()
+    assert isinstance(s["summary"], str)
+    syn = TestClient(stack.synthese_app).post("/api/synthese/patient", json={"patient_id": str(doc_id)}).json()
+    assert syn["sources"] and syn["sources"][0]["doc_id"] == str(doc_id)
+    assert "llm_qa_ask_requests" in qa.get("/metrics").text
+
+
+def test_stack_persistence_resume(stack, tmp_path):
+    from docqa_amd.index.faiss_io import read_index
+    from docqa_amd.store.metadata_io import read_metadata
+
+    stack.indexer.save_state()
+    idx = read_index(stack.indexer.index_path)
+    meta = read_metadata(stack.indexer.meta_path)
+    assert idx.ntotal == len(meta) == stack.indexer.index.ntotal
