@@ -169,6 +169,25 @@ class LlamaModel:
                 "down": dn.contiguous(),
             })
 
+    def export_state_dict_hf(self) -> dict:
+        """Inverse of :meth:`load_state_dict_hf` for an un-sharded (TP=1) model."""
+        if self.tp != 1:
+            raise ValueError("export requires TP=1")
+        cfg, D = self.cfg, self.cfg.head_dim
+        sd = {"model.embed_tokens.weight": self.embed, "model.norm.weight": self.final_norm,
+              "lm_head.weight": self.lm_head[: cfg.vocab_size]}
+        for i, L in enumerate(self.layers):
+            p = f"model.layers.{i}."
+            q, k, v = L["qkv"].split([self.hq * D, self.hkv * D, self.hkv * D])
+            g, u = L["gate_up"].split([self.inter, self.inter])
+            sd.update({p + "self_attn.q_proj.weight": q, p + "self_attn.k_proj.weight": k,
+                       p + "self_attn.v_proj.weight": v, p + "self_attn.o_proj.weight": L["o"],
+                       p + "mlp.gate_proj.weight": g, p + "mlp.up_proj.weight": u,
+                       p + "mlp.down_proj.weight": L["down"],
+                       p + "input_layernorm.weight": L["in_norm"],
+                       p + "post_attention_layernorm.weight": L["post_norm"]})
+        return {k: t.detach().cpu() for k, t in sd.items()}
+
     def weight_bytes(self) -> int:
         n = self.embed.numel() + self.lm_head.numel() + self.final_norm.numel()
         for L in self.layers:
