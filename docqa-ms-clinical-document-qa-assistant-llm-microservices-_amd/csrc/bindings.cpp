@@ -243,6 +243,47 @@ at::Tensor pool_l2(const at::Tensor& h, const at::Tensor& cu_seqlens, bool mean,
   return out;
 }
 
+std::tuple<at::Tensor, at::Tensor> ivfpq_search(const at::Tensor& xq, const at::Tensor& centroids,
+                                                const at::Tensor& pq, const at::Tensor& codes,
+                                                const at::Tensor& ids, const at::Tensor& list_off,
+                                                const at::Tensor& probes, int64_t k) {
+  CHECK_GPU(xq); CHECK_CONTIG(xq); CHECK_CONTIG(centroids); CHECK_CONTIG(pq); CHECK_CONTIG(codes);
+  CHECK_CONTIG(probes);
+  TORCH_CHECK(xq.scalar_type() == at::kFloat && centroids.scalar_type() == at::kFloat &&
+              pq.scalar_type() == at::kFloat, "ivfpq: fp32 queries / centroids / codebook");
+  TORCH_CHECK(codes.scalar_type() == at::kByte, "codes must be uint8");
+  TORCH_CHECK(ids.scalar_type() == at::kLong && list_off.scalar_type() == at::kLong &&
+              probes.scalar_type() == at::kLong, "ids / list offsets / probes must be int64");
+  const int nq = xq.size(0), d = xq.size(1), nprobe = probes.size(1), M = pq.size(0);
+  TORCH_CHECK(pq.size(1) == 256 && pq.size(2) * M == d, "pq codebook must be [M, 256, d/M]");
+  TORCH_CHECK(codes.size(1) == M, "codes must be [N, M]");
+  TORCH_CHECK(k >= 1 && k <= 32, "k must be in [1, 32]");
+  const int kp = k <= 4 ? 4 : k <= 8 ? 8 : k <= 16 ? 16 : 32;
+  c10::DeviceGuard g(xq.device());
+  auto out_d = at::empty({nq, k}, xq.options());
+  auto out_i = at::empty({nq, k}, xq.options().dtype(at::kLong));
+  auto ws_d = at::empty({nq, nprobe, kp}, xq.options());
+  auto ws_i = at::empty({nq, nprobe, kp}, xq.options().dtype(at::kInt));
+  CHECK_RC(docqa_ivfpq_search(xq.data_ptr<float>(), centroids.data_ptr<float>(), pq.data_ptr<float>(),
+                              codes.data_ptr<uint8_t>(), ids.data_ptr<int64_t>(),
+                              list_off.data_ptr<int64_t>(), probes.data_ptr<int64_t>(), nq, nprobe, d,
+                              M, k, ws_d.data_ptr<float>(), ws_i.data_ptr<int>(),
+                              out_d.data_ptr<float>(), out_i.data_ptr<int64_t>(), stream()), "ivfpq_search");
+  return {out_d, out_i};
+}
+
+at::Tensor pq_encode(const at::Tensor& x, const at::Tensor& centroids, const at::Tensor& assign,
+                     const at::Tensor& pq) {
+  CHECK_GPU(x); CHECK_CONTIG(x); CHECK_CONTIG(centroids); CHECK_CONTIG(pq); CHECK_CONTIG(assign);
+  TORCH_CHECK(assign.scalar_type() == at::kLong, "assign must be int64");
+  const int n = x.size(0), d = x.size(1), M = pq.size(0);
+  c10::DeviceGuard g(x.device());
+  auto codes = at::empty({n, M}, x.options().dtype(at::kByte));
+  CHECK_RC(docqa_pq_encode(x.data_ptr<float>(), centroids.data_ptr<float>(), assign.data_ptr<int64_t>(),
+                           pq.data_ptr<float>(), n, d, M, codes.data_ptr<uint8_t>(), stream()), "pq_encode");
+  return codes;
+}
+
 }  // namespace
 
 TORCH_LIBRARY(docqa, m) {
@@ -265,6 +306,9 @@ TORCH_LIBRARY(docqa, m) {
   m.def("knn(Tensor xb, Tensor xb_norms, Tensor xq, int k, bool inner_product, int id_offset) "
         "-> (Tensor, Tensor)");
   m.def("pool_l2(Tensor h, Tensor cu_seqlens, bool mean, bool normalize) -> Tensor");
+  m.def("ivfpq_search(Tensor xq, Tensor centroids, Tensor pq, Tensor codes, Tensor ids, "
+        "Tensor list_off, Tensor probes, int k) -> (Tensor, Tensor)");
+  m.def("pq_encode(Tensor x, Tensor centroids, Tensor assign, Tensor pq) -> Tensor");
 }
 
 TORCH_LIBRARY_IMPL(docqa, CUDA, m) {
@@ -282,4 +326,6 @@ TORCH_LIBRARY_IMPL(docqa, CUDA, m) {
   m.impl("flash_prefill", &flash_prefill);
   m.impl("knn", &knn);
   m.impl("pool_l2", &pool_l2);
+  m.impl("ivfpq_search", &ivfpq_search);
+  m.impl("pq_encode", &pq_encode);
 }

@@ -47,5 +47,12 @@ int docqa_knn(const void* xb, const float* norms, int N, int d, int is_bf16, con
               int nq, int k, int metric_ip, float* ws_d, int* ws_i, int nblk, float* out_d,
               int64_t* out_i, int64_t id_offset, hipStream_t s);
 
+int docqa_ivfpq_search(const float* xq, const float* centroids, const float* pq,
+                       const uint8_t* codes, const int64_t* ids, const int64_t* list_off,
+                       const int64_t* probes, int nq, int nprobe, int d, int M, int k,
+                       float* ws_d, int* ws_i, float* out_d, int64_t* out_i, hipStream_t s);
+int docqa_pq_encode(const float* x, const float* centroids, const int64_t* assign, const float* pq,
+                    int n, int d, int M, uint8_t* codes, hipStream_t s);
+
 int docqa_pool_l2(const void* h, const int* cu, int B, int H, int mean, int normalize, float* out,
                   hipStream_t s);

@@ -21,25 +21,12 @@
 //     top-K per (query, row-block) -> workspace.
 // Kernel 2 (grid nq): merges the row-block lists -> final (D, I) per query.
 #include "docqa_common.h"
+#include "docqa_topk.h"
 #include <float.h>
 
 using namespace docqa;
 
 namespace {
-
-template <int K>
-__device__ __forceinline__ void topk_insert(float (&td)[K], int (&ti)[K], float d, int id) {
-#pragma unroll
-  for (int i = 0; i < K; ++i) {
-    const bool sw = d < td[i] || (d == td[i] && id < ti[i]);
-    const float nd = sw ? td[i] : d;
-    const int ni = sw ? ti[i] : id;
-    td[i] = sw ? d : td[i];
-    ti[i] = sw ? id : ti[i];
-    d = nd;
-    id = ni;
-  }
-}
 
 template <int K, bool IP, bool BF16>
 __global__ __launch_bounds__(256) void knn_tile_kernel(
@@ -158,56 +145,6 @@ __global__ __launch_bounds__(256) void knn_tile_kernel(
   }
 }
 
-template <int K, bool IP>
-__global__ __launch_bounds__(256) void knn_merge_kernel(const float* __restrict__ ws_d,
-                                                        const int* __restrict__ ws_i, int nblk,
-                                                        const float* __restrict__ xq, int d,
-                                                        int k_out, float* __restrict__ out_d,
-                                                        int64_t* __restrict__ out_i,
-                                                        int64_t id_offset) {
-  __shared__ float sd[256 * K];
-  __shared__ int si[256 * K];
-  __shared__ float qn;
-  const int q = blockIdx.x, tid = threadIdx.x;
-  float td[K];
-  int ti[K];
-#pragma unroll
-  for (int i = 0; i < K; ++i) { td[i] = FLT_MAX; ti[i] = -1; }
-  const size_t base = (size_t)q * nblk * K;
-  for (int c = tid; c < nblk * K; c += 256) {
-    const float v = ws_d[base + c];
-    if (v < td[K - 1]) topk_insert<K>(td, ti, v, ws_i[base + c]);
-  }
-#pragma unroll
-  for (int i = 0; i < K; ++i) { sd[tid * K + i] = td[i]; si[tid * K + i] = ti[i]; }
-  if (!IP && tid == 0) {
-    float s = 0.f;
-    for (int c = 0; c < d; ++c) s += xq[(size_t)q * d + c] * xq[(size_t)q * d + c];
-    qn = s;
-  }
-  __syncthreads();
-  for (int stride = 128; stride > 0; stride >>= 1) {
-    if (tid < stride) {
-      const int o = tid + stride;
-#pragma unroll
-      for (int i = 0; i < K; ++i) {
-        const float v = sd[o * K + i];
-        if (v < td[K - 1]) topk_insert<K>(td, ti, v, si[o * K + i]);
-      }
-#pragma unroll
-      for (int i = 0; i < K; ++i) { sd[tid * K + i] = td[i]; si[tid * K + i] = ti[i]; }
-    }
-    __syncthreads();
-  }
-  if (tid == 0) {
-    for (int i = 0; i < k_out; ++i) {
-      const bool valid = ti[i] >= 0 && td[i] != FLT_MAX;
-      out_d[(size_t)q * k_out + i] = valid ? (IP ? -td[i] : td[i] + qn) : (IP ? -FLT_MAX : FLT_MAX);
-      out_i[(size_t)q * k_out + i] = valid ? (int64_t)ti[i] + id_offset : -1;
-    }
-  }
-}
-
 }  // namespace
 
 int docqa_knn_workspace_blocks(int N) {
@@ -228,7 +165,7 @@ static int launch_knn(const void* xb, const float* norms, int N, int d, const fl
   if (lds > 160 * 1024) return -2;
   dim3 g1(nblk, (nq + 31) / 32);
   knn_tile_kernel<K, IP, BF16><<<g1, 256, lds, s>>>(xb, norms, N, d, xq, nq, rpb, ws_d, ws_i, nblk);
-  knn_merge_kernel<K, IP><<<nq, 256, 0, s>>>(ws_d, ws_i, nblk, xq, d, k, out_d, out_i, id_offset);
+  topk_merge_kernel<K, IP><<<nq, 256, 0, s>>>(ws_d, ws_i, nblk, xq, d, k, out_d, out_i, id_offset, nullptr);
   DOCQA_CHECK_LAUNCH();
   return 0;
 }

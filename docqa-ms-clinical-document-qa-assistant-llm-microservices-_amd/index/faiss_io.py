@@ -111,7 +111,7 @@ def read_index(path) -> object:
     fourcc = r.read(4)
     if fourcc in (b"IxF2", b"IxFI", b"IxFl"):
         return read_flat(r, fourcc)
-    if fourcc == b"IwPQ":
+    if fourcc in (b"IvPQ", b"IwPQ"):
         from .ivfpq import read_ivfpq_body
 
         return read_ivfpq_body(r)
