@@ -46,11 +46,11 @@ class PyBlockAllocator:
                 raise RuntimeError(f"double free of KV block {b}")
 
 
-def make_allocator(num_blocks: int):
+def make_allocator(num_blocks: int, block_size: int = 64):
     try:
         from ..runtime import native_block_allocator
 
-        a = native_block_allocator(num_blocks)
+        a = native_block_allocator(num_blocks, block_size)
         if a is not None:
             return a
     except Exception:
@@ -68,7 +68,7 @@ class KVCache:
         shape = (num_blocks, kv_heads, block_size, head_dim)
         self.caches = [(torch.empty(shape, device=device, dtype=dtype),
                         torch.empty(shape, device=device, dtype=dtype)) for _ in range(layers)]
-        self.allocator = make_allocator(num_blocks)
+        self.allocator = make_allocator(num_blocks, block_size)
 
     @staticmethod
     def bytes_per_block(layers, kv_heads, head_dim, block_size, dtype_bytes=2) -> int:

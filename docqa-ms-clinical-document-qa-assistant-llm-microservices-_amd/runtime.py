@@ -1,0 +1,54 @@
+"""Handles to the native (C++) runtime objects compiled into ``ops/_docqa_C.so``.
+
+* ``torch.classes.docqa_rt.BlockManager`` -- paged-KV block allocator with refcounts
+  and a content-hashed prompt-prefix cache (csrc/runtime/block_manager.cpp).
+"""
+from __future__ import annotations
+
+import torch
+
+from . import ops
+
+
+class NativeBlockAllocator:
+    """Python-facing wrapper with the :class:`engine.kv_cache.PyBlockAllocator` API."""
+
+    def __init__(self, num_blocks: int, block_size: int = 64):
+        self._m = torch.classes.docqa_rt.BlockManager(num_blocks, block_size)
+        self.num_blocks = num_blocks
+        self.block_size = block_size
+
+    def num_free(self) -> int:
+        return int(self._m.num_free())
+
+    def alloc(self, n: int) -> list[int]:
+        try:
+            return list(self._m.alloc(n))
+        except RuntimeError as e:
+            raise MemoryError(str(e)) from e
+
+    def share(self, blocks: list[int]) -> None:
+        self._m.share(list(blocks))
+
+    def free(self, blocks: list[int]) -> None:
+        self._m.free(list(blocks))
+
+    def match_prefix(self, tokens: list[int]) -> list[int]:
+        return list(self._m.match_prefix(list(tokens)))
+
+    def register_prefix(self, tokens: list[int], blocks: list[int]) -> None:
+        self._m.register_prefix(list(tokens), list(blocks))
+
+    def stats(self) -> dict:
+        f, lru, cached, lookups, hits = self._m.stats()
+        return {"free": f, "evictable": lru, "cached_blocks": cached, "lookups": lookups,
+                "hit_blocks": hits}
+
+
+def native_block_allocator(num_blocks: int, block_size: int = 64):
+    if not ops.load_native():
+        return None
+    try:
+        return NativeBlockAllocator(num_blocks, block_size)
+    except Exception:
+        return None
