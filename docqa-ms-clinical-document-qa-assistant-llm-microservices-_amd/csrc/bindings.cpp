@@ -203,6 +203,27 @@ at::Tensor flash_prefill(const at::Tensor& qkv, const at::Tensor& cu_seqlens, in
   return out;
 }
 
+at::Tensor flash_prefill_paged(const at::Tensor& qkv, const at::Tensor& cu_seqlens, int64_t max_len,
+                               int64_t Hq, int64_t Hkv, int64_t D, double scale,
+                               const at::Tensor& k_cache, const at::Tensor& v_cache,
+                               const at::Tensor& block_tables, const at::Tensor& ctx_start) {
+  CHECK_GPU(qkv); CHECK_BF16(qkv); CHECK_I32(cu_seqlens); CHECK_BF16(k_cache); CHECK_BF16(v_cache);
+  CHECK_I32(block_tables); CHECK_I32(ctx_start); CHECK_CONTIG(block_tables);
+  TORCH_CHECK(qkv.stride(-1) == 1 && qkv.size(-1) == (Hq + 2 * Hkv) * D, "qkv layout mismatch");
+  TORCH_CHECK(k_cache.size(1) == Hkv && k_cache.size(3) == D, "cache layout mismatch");
+  const int T = qkv.numel() / qkv.size(-1);
+  const int B = cu_seqlens.numel() - 1;
+  TORCH_CHECK(block_tables.size(0) == B && ctx_start.numel() == B, "per-sequence metadata mismatch");
+  c10::DeviceGuard g(qkv.device());
+  auto out = at::empty({T, Hq * D}, qkv.options());
+  CHECK_RC(docqa_flash_prefill_paged(qkv.data_ptr(), qkv.size(-1), cu_seqlens.data_ptr<int>(),
+                                     out.data_ptr(), Hq * D, B, max_len, Hq, Hkv, D, (float)scale,
+                                     k_cache.data_ptr(), v_cache.data_ptr(), block_tables.data_ptr<int>(),
+                                     block_tables.size(1), ctx_start.data_ptr<int>(), k_cache.size(2),
+                                     stream()), "flash_prefill_paged");
+  return out;
+}
+
 std::tuple<at::Tensor, at::Tensor> knn(const at::Tensor& xb, const at::Tensor& xb_norms,
                                        const at::Tensor& xq, int64_t k, bool inner_product,
                                        int64_t id_offset) {
@@ -309,6 +330,8 @@ TORCH_LIBRARY(docqa, m) {
   m.def("ivfpq_search(Tensor xq, Tensor centroids, Tensor pq, Tensor codes, Tensor ids, "
         "Tensor list_off, Tensor probes, int k) -> (Tensor, Tensor)");
   m.def("pq_encode(Tensor x, Tensor centroids, Tensor assign, Tensor pq) -> Tensor");
+  m.def("flash_prefill_paged(Tensor qkv, Tensor cu_seqlens, int max_len, int Hq, int Hkv, int D, "
+        "float scale, Tensor k_cache, Tensor v_cache, Tensor block_tables, Tensor ctx_start) -> Tensor");
 }
 
 TORCH_LIBRARY_IMPL(docqa, CUDA, m) {
@@ -328,4 +351,5 @@ TORCH_LIBRARY_IMPL(docqa, CUDA, m) {
   m.impl("pool_l2", &pool_l2);
   m.impl("ivfpq_search", &ivfpq_search);
   m.impl("pq_encode", &pq_encode);
+  m.impl("flash_prefill_paged", &flash_prefill_paged);
 }

@@ -41,6 +41,12 @@ int docqa_flash_prefill(const void* qkv, int row_stride, const int* cu_seqlens, 
                         int o_stride, int B, int max_len, int Hq, int Hkv, int head_dim,
                         float scale, int causal, hipStream_t s);
 
+int docqa_flash_prefill_paged(const void* qkv, int row_stride, const int* cu_seqlens, void* out,
+                              int o_stride, int B, int max_len, int Hq, int Hkv, int head_dim,
+                              float scale, const void* k_cache, const void* v_cache,
+                              const int* block_tables, int maxb, const int* ctx_start, int BS,
+                              hipStream_t s);
+
 int docqa_knn_workspace_blocks(int N);
 int docqa_knn_kpad(int k);
 int docqa_knn(const void* xb, const float* norms, int N, int d, int is_bf16, const float* xq,

@@ -45,10 +45,24 @@ __device__ __forceinline__ int v_off(int row, int ch) {
   return row * D + ((ch ^ (((row & 3) << 2) & (D / 8 - 1))) << 3);
 }
 
-template <int D, bool CAUSAL>
+// Paged K/V source for prefix-cached prefill: keys [0, ctx_start[b]) were computed by an
+// earlier request (shared prompt prefix, prefix-cache hit) and keys
+// [ctx_start[b], ctx_start[b] + L) were just written by the fused RoPE/cache kernel, so
+// every key of the sequence is read through the block table from the paged cache.
+struct PagedKV {
+  const uint16_t* k;
+  const uint16_t* v;
+  const int* block_tables;
+  int maxb;
+  const int* ctx_start;
+  int BS;
+  int log2BS;
+};
+
+template <int D, bool CAUSAL, bool PAGED>
 __global__ __launch_bounds__(256) void flash_prefill_kernel(
     const uint16_t* __restrict__ qkv, int row_stride, const int* __restrict__ cu_seqlens,
-    uint16_t* __restrict__ out, int o_stride, int Hq, int Hkv, float scale) {
+    uint16_t* __restrict__ out, int o_stride, int Hq, int Hkv, float scale, PagedKV pk) {
   __shared__ __attribute__((aligned(16))) uint16_t smem[2 * KB * D];
   uint16_t* sK = smem;
   uint16_t* sV = smem + KB * D;
@@ -59,6 +73,8 @@ __global__ __launch_bounds__(256) void flash_prefill_kernel(
   const int q_start = qt * QB;
   if (q_start >= L) return;
   const int kvh = h / (Hq / Hkv);
+  const int P0 = PAGED ? pk.ctx_start[b] : 0;   // absolute position of query row 0
+  const int Lk = P0 + L;                         // keys visible to this sequence
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int l32 = lane & 31, hh = lane >> 5;
@@ -89,7 +105,7 @@ __global__ __launch_bounds__(256) void flash_prefill_kernel(
   float m_run = -FLT_MAX, l_run = 0.f;
   const float sl2 = scale * kLog2e;
 
-  const int kv_end = CAUSAL ? min(L, q_start + QB) : L;
+  const int kv_end = CAUSAL ? min(Lk, P0 + q_start + QB) : Lk;
   const int ntiles = (kv_end + KB - 1) / KB;
   const uint16_t* kbase = qkv + (size_t)seq0 * row_stride + (size_t)(Hq + kvh) * D;
   const uint16_t* vbase = qkv + (size_t)seq0 * row_stride + (size_t)(Hq + Hkv + kvh) * D;
@@ -102,9 +118,16 @@ __global__ __launch_bounds__(256) void flash_prefill_kernel(
       const int idx = tid + 256 * i;
       const int row = idx / NCH, ch = idx % NCH;
       const int key = t * KB + row;
-      if (key < L) {
-        rk[i] = *reinterpret_cast<const uint4*>(kbase + (size_t)key * row_stride + ch * 8);
-        rv[i] = *reinterpret_cast<const uint4*>(vbase + (size_t)key * row_stride + ch * 8);
+      if (key < Lk) {
+        if constexpr (PAGED) {
+          const int blk = pk.block_tables[(size_t)b * pk.maxb + (key >> pk.log2BS)];
+          const size_t off = (((size_t)blk * Hkv + kvh) * pk.BS + (key & (pk.BS - 1))) * D + ch * 8;
+          rk[i] = *reinterpret_cast<const uint4*>(pk.k + off);
+          rv[i] = *reinterpret_cast<const uint4*>(pk.v + off);
+        } else {
+          rk[i] = *reinterpret_cast<const uint4*>(kbase + (size_t)key * row_stride + ch * 8);
+          rv[i] = *reinterpret_cast<const uint4*>(vbase + (size_t)key * row_stride + ch * 8);
+        }
       } else {
         rk[i] = make_uint4(0, 0, 0, 0);
         rv[i] = make_uint4(0, 0, 0, 0);
@@ -132,7 +155,7 @@ __global__ __launch_bounds__(256) void flash_prefill_kernel(
     if (t + 1 < ntiles) load_tile(t + 1);
     const int kb = t * KB;
     // a wave whose rows all precede this tile's first key contributes nothing (causal)
-    const bool active = !CAUSAL || (kb <= q_wave + 31);
+    const bool active = !CAUSAL || (kb <= P0 + q_wave + 31);
     if (active) {
       // ---- S^T for the two 32-key sub-tiles
       f32x16 x[2];
@@ -155,7 +178,7 @@ __global__ __launch_bounds__(256) void flash_prefill_kernel(
         for (int r = 0; r < 16; ++r) {
           const int key = kb + kt * 32 + (r & 3) + 8 * (r >> 2) + 4 * hh;
           float s = x[kt][r] * sl2;
-          const bool masked = (key >= L) || (CAUSAL && key > my_q);
+          const bool masked = (key >= Lk) || (CAUSAL && key > P0 + my_q);
           s = masked ? -FLT_MAX : s;
           x[kt][r] = s;
           mx = fmaxf(mx, s);
@@ -235,13 +258,30 @@ __global__ __launch_bounds__(256) void flash_prefill_kernel(
 
 template <int D>
 static void launch_prefill(dim3 grid, hipStream_t s, int causal, const void* qkv, int row_stride,
-                           const int* cu, void* out, int o_stride, int Hq, int Hkv, float scale) {
-  if (causal)
-    flash_prefill_kernel<D, true><<<grid, 256, 0, s>>>((const uint16_t*)qkv, row_stride, cu,
-                                                       (uint16_t*)out, o_stride, Hq, Hkv, scale);
-  else
-    flash_prefill_kernel<D, false><<<grid, 256, 0, s>>>((const uint16_t*)qkv, row_stride, cu,
-                                                        (uint16_t*)out, o_stride, Hq, Hkv, scale);
+                           const int* cu, void* out, int o_stride, int Hq, int Hkv, float scale,
+                           const PagedKV& pk) {
+  const uint16_t* q = (const uint16_t*)qkv;
+  uint16_t* o = (uint16_t*)out;
+  if (pk.k) {
+    flash_prefill_kernel<D, true, true><<<grid, 256, 0, s>>>(q, row_stride, cu, o, o_stride, Hq, Hkv, scale, pk);
+  } else if (causal) {
+    flash_prefill_kernel<D, true, false><<<grid, 256, 0, s>>>(q, row_stride, cu, o, o_stride, Hq, Hkv, scale, pk);
+  } else {
+    flash_prefill_kernel<D, false, false><<<grid, 256, 0, s>>>(q, row_stride, cu, o, o_stride, Hq, Hkv, scale, pk);
+  }
+}
+
+static int prefill_dispatch(dim3 grid, hipStream_t s, int head_dim, int causal, const void* qkv,
+                            int row_stride, const int* cu, void* out, int o_stride, int Hq, int Hkv,
+                            float scale, const PagedKV& pk) {
+  switch (head_dim) {
+    case 32: launch_prefill<32>(grid, s, causal, qkv, row_stride, cu, out, o_stride, Hq, Hkv, scale, pk); break;
+    case 64: launch_prefill<64>(grid, s, causal, qkv, row_stride, cu, out, o_stride, Hq, Hkv, scale, pk); break;
+    case 128: launch_prefill<128>(grid, s, causal, qkv, row_stride, cu, out, o_stride, Hq, Hkv, scale, pk); break;
+    default: return -1;
+  }
+  DOCQA_CHECK_LAUNCH();
+  return 0;
 }
 
 int docqa_flash_prefill(const void* qkv, int row_stride, const int* cu_seqlens, void* out,
@@ -250,12 +290,23 @@ int docqa_flash_prefill(const void* qkv, int row_stride, const int* cu_seqlens, 
   if (B == 0 || max_len == 0) return 0;
   if (Hq % Hkv != 0) return -1;
   dim3 grid((max_len + QB - 1) / QB, Hq, B);
-  switch (head_dim) {
-    case 32: launch_prefill<32>(grid, s, causal, qkv, row_stride, cu_seqlens, out, o_stride, Hq, Hkv, scale); break;
-    case 64: launch_prefill<64>(grid, s, causal, qkv, row_stride, cu_seqlens, out, o_stride, Hq, Hkv, scale); break;
-    case 128: launch_prefill<128>(grid, s, causal, qkv, row_stride, cu_seqlens, out, o_stride, Hq, Hkv, scale); break;
-    default: return -1;
-  }
-  DOCQA_CHECK_LAUNCH();
-  return 0;
+  PagedKV pk{nullptr, nullptr, nullptr, 0, nullptr, 1, 0};
+  return prefill_dispatch(grid, s, head_dim, causal, qkv, row_stride, cu_seqlens, out, o_stride, Hq,
+                          Hkv, scale, pk);
+}
+
+// Causal prefill of new tokens whose keys (prefix + new) live in the paged cache.
+int docqa_flash_prefill_paged(const void* qkv, int row_stride, const int* cu_seqlens, void* out,
+                              int o_stride, int B, int max_len, int Hq, int Hkv, int head_dim,
+                              float scale, const void* k_cache, const void* v_cache,
+                              const int* block_tables, int maxb, const int* ctx_start, int BS,
+                              hipStream_t s) {
+  if (B == 0 || max_len == 0) return 0;
+  if (Hq % Hkv != 0 || (BS & (BS - 1)) != 0 || head_dim != 128) return -1;
+  int log2BS = 0;
+  while ((1 << log2BS) < BS) ++log2BS;
+  dim3 grid((max_len + QB - 1) / QB, Hq, B);
+  PagedKV pk{(const uint16_t*)k_cache, (const uint16_t*)v_cache, block_tables, maxb, ctx_start, BS, log2BS};
+  return prefill_dispatch(grid, s, head_dim, 1, qkv, row_stride, cu_seqlens, out, o_stride, Hq, Hkv,
+                          scale, pk);
 }

@@ -44,6 +44,7 @@ class GenStats:
     decode_s: float = 0.0
     prompt_tokens: int = 0
     generated_tokens: int = 0
+    cached_tokens: int = 0     # prompt tokens served from the prefix cache
 
 
 def _bucket(n: int, cap: int) -> int:
@@ -75,7 +76,7 @@ class _DecodeGraph:
 class LLMEngine:
     def __init__(self, model: LlamaModel, max_batch: int = 64, max_context: int = 2048,
                  block_size: int = 64, num_blocks: int | None = None, use_graphs: bool = True,
-                 max_prefill_tokens: int = 65536):
+                 max_prefill_tokens: int = 65536, prefix_cache: bool = True):
         self.model = model
         self.cfg = model.cfg
         self.device = model.device
@@ -90,34 +91,47 @@ class LLMEngine:
                           self.device, model.dtype)
         self.use_graphs = use_graphs and self.device.type == "cuda"
         self.tune_decode_gemms = os.environ.get("DOCQA_TUNE_DECODE", "1") == "1"
+        # reuse KV blocks of shared prompt prefixes (the fixed RAG instruction template)
+        self.prefix_cache = prefix_cache and os.environ.get("DOCQA_PREFIX_CACHE", "1") == "1"
         self._graphs: dict[int, _DecodeGraph] = {}
         self._pool = None
         self.stats = GenStats()
 
     # ------------------------------------------------------------------ prefill
-    def _prefill(self, prompts: list[list[int]], tables: list[list[int]]) -> torch.Tensor:
+    def _prefill(self, prompts: list[list[int]], tables: list[list[int]],
+                 cached: list[int] | None = None) -> torch.Tensor:
+        """Prefill prompt tokens [cached[i], len) of each prompt (the first cached[i]
+        tokens are prefix-cache hits already in the paged KV cache)."""
         dev, BS = self.device, self.block_size
+        cached = cached or [0] * len(prompts)
         firsts = []
         i = 0
         while i < len(prompts):
             j, tok = i, 0
-            while j < len(prompts) and (j == i or tok + len(prompts[j]) <= self.max_prefill_tokens):
-                tok += len(prompts[j])
+            while j < len(prompts) and (j == i or tok + len(prompts[j]) - cached[j] <= self.max_prefill_tokens):
+                tok += len(prompts[j]) - cached[j]
                 j += 1
             ids, pos, slots, cu = [], [], [], [0]
-            for p, tb in zip(prompts[i:j], tables[i:j]):
+            for p, tb, c in zip(prompts[i:j], tables[i:j], cached[i:j]):
                 n = len(p)
-                ids.extend(p)
-                pos.extend(range(n))
-                slots.extend(tb[t // BS] * BS + t % BS for t in range(n))
-                cu.append(cu[-1] + n)
+                ids.extend(p[c:])
+                pos.extend(range(c, n))
+                slots.extend(tb[t // BS] * BS + t % BS for t in range(c, n))
+                cu.append(cu[-1] + n - c)
             t_ids = torch.tensor(ids, dtype=torch.int32).to(dev, non_blocking=True)
             meta = AttnMeta(
                 prefill=True,
                 positions=torch.tensor(pos, dtype=torch.int32).to(dev, non_blocking=True),
                 slot_mapping=torch.tensor(slots, dtype=torch.int32).to(dev, non_blocking=True),
                 cu_seqlens=torch.tensor(cu, dtype=torch.int32).to(dev, non_blocking=True),
-                max_len=max(len(p) for p in prompts[i:j]))
+                max_len=max(len(p) - c for p, c in zip(prompts[i:j], cached[i:j])))
+            if any(cached[i:j]):
+                maxb = max(len(tb) for tb in tables[i:j])
+                bt = torch.zeros(j - i, maxb, dtype=torch.int32)
+                for r, tb in enumerate(tables[i:j]):
+                    bt[r, :len(tb)] = torch.tensor(tb, dtype=torch.int32)
+                meta.block_tables = bt.to(dev, non_blocking=True)
+                meta.prefix_lens = torch.tensor(cached[i:j], dtype=torch.int32).to(dev, non_blocking=True)
             last = torch.tensor(cu[1:], dtype=torch.int64).to(dev, non_blocking=True) - 1
             logits = self.model.forward(t_ids, meta, self.kv.caches, logits_index=last)
             firsts.append(logits)
@@ -209,11 +223,29 @@ class LLMEngine:
         if need > self.max_context:
             raise ValueError(f"prompt+generation {need} exceeds max_context {self.max_context}")
         alloc = self.kv.allocator
-        tables = [alloc.alloc(self.kv.blocks_for(n + params.max_new_tokens)) for n in lens]
+        use_pc = self.prefix_cache and hasattr(alloc, "match_prefix")
+        tables, cached = [], []
+        try:
+            for p in prompts:
+                hit = alloc.match_prefix(p) if use_pc else []
+                if hit and len(hit) * self.block_size >= len(p):
+                    alloc.free([hit[-1]])  # always recompute >= 1 token (its logits seed decode)
+                    hit = hit[:-1]
+                tables.append(hit)
+                cached.append(len(hit) * self.block_size)
+                tables[-1] = hit + alloc.alloc(self.kv.blocks_for(len(p) + params.max_new_tokens) - len(hit))
+        except MemoryError:
+            for tb in tables:
+                alloc.free(tb)
+            raise
         try:
             greedy = params.temperature <= 0.0
             t0 = time.perf_counter()
-            logits = self._prefill(prompts, tables)
+            logits = self._prefill(prompts, tables, cached)
+            if use_pc:
+                for p, tb in zip(prompts, tables):
+                    alloc.register_prefix(p, tb)
+            self.stats.cached_tokens += sum(cached)
             g = self._get_graph(_bucket(B, self.max_batch) if self.use_graphs else B, greedy)
             # state for the first decode step
             bt = torch.zeros(g.bp, self.max_blocks_per_seq, dtype=torch.int32)

@@ -82,6 +82,7 @@ class AttnMeta:
     block_tables: torch.Tensor | None = None  # [B, maxb] (decode)
     context_lens: torch.Tensor | None = None  # [B] (decode; includes the new token)
     max_context: int = 0                    # (decode) graph-capture bound
+    prefix_lens: torch.Tensor | None = None  # [B] (prefill with prefix-cache hits)
 
 
 class LlamaModel:
@@ -209,7 +210,11 @@ class LlamaModel:
             kc, vc = kv_caches[i]
             qkv = F.linear(x, L["qkv"])
             ops.rope_cache(qkv, meta.positions, self.cos_sin, meta.slot_mapping, kc, vc, hq, hkv, D)
-            if meta.prefill:
+            if meta.prefill and meta.prefix_lens is not None:
+                # prompt prefix already in the paged cache: attend over cache (prefix + new)
+                a = ops.flash_prefill_paged(qkv, meta.cu_seqlens, meta.max_len, hq, hkv, D, self.scale,
+                                            kc, vc, meta.block_tables, meta.prefix_lens)
+            elif meta.prefill:
                 a = ops.flash_prefill(qkv, meta.cu_seqlens, meta.max_len, hq, hkv, D, self.scale, True)
             else:
                 a = ops.paged_decode(qkv, kc, vc, meta.block_tables, meta.context_lens, hq,

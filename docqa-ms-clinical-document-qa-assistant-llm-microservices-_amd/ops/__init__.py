@@ -167,6 +167,15 @@ def flash_prefill(qkv, cu_seqlens, max_len, Hq, Hkv, D, scale, causal=True):
     return ref.flash_prefill(qkv, cu_seqlens, max_len, Hq, Hkv, D, scale, causal)
 
 
+def flash_prefill_paged(qkv, cu_seqlens, max_len, Hq, Hkv, D, scale, k_cache, v_cache,
+                        block_tables, ctx_start):
+    if _gpu(qkv):
+        return _native().flash_prefill_paged(qkv, cu_seqlens, max_len, Hq, Hkv, D, scale, k_cache,
+                                             v_cache, block_tables, ctx_start)
+    return ref.flash_prefill_paged(qkv, cu_seqlens, max_len, Hq, Hkv, D, scale, k_cache, v_cache,
+                                   block_tables, ctx_start)
+
+
 # ----------------------------------------------------------------------------- search
 def knn(xb, xb_norms, xq, k: int, inner_product: bool = False, id_offset: int = 0):
     if _gpu(xb):

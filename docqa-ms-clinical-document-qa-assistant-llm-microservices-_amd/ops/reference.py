@@ -160,6 +160,39 @@ def flash_prefill(qkv, cu_seqlens, max_len, Hq, Hkv, D, scale, causal):
     return out
 
 
+def flash_prefill_paged(qkv, cu_seqlens, max_len, Hq, Hkv, D, scale, k_cache, v_cache,
+                        block_tables, ctx_start):
+    """Causal attention of the new tokens over (cached prefix + new) keys read from the
+    paged cache (the new keys must already be written there)."""
+    T = qkv.shape[0]
+    x = qkv.view(T, Hq + 2 * Hkv, D)
+    G = Hq // Hkv
+    BS = k_cache.shape[2]
+    out = torch.empty(T, Hq * D, dtype=qkv.dtype, device=qkv.device)
+    cu = cu_seqlens.tolist()
+    for b in range(len(cu) - 1):
+        s0, s1 = cu[b], cu[b + 1]
+        L = s1 - s0
+        if L == 0:
+            continue
+        P0 = int(ctx_start[b])
+        Lk = P0 + L
+        nblk = (Lk + BS - 1) // BS
+        blocks = block_tables[b, :nblk].long()
+        k = k_cache[blocks].permute(1, 0, 2, 3).reshape(Hkv, nblk * BS, D)[:, :Lk].float()
+        v = v_cache[blocks].permute(1, 0, 2, 3).reshape(Hkv, nblk * BS, D)[:, :Lk].float()
+        k = k.repeat_interleave(G, 0)
+        v = v.repeat_interleave(G, 0)
+        q = x[s0:s1, :Hq].float().transpose(0, 1)
+        s = torch.einsum("hld,hmd->hlm", q, k) * scale
+        qpos = torch.arange(P0, Lk, device=qkv.device)[:, None]
+        kpos = torch.arange(Lk, device=qkv.device)[None, :]
+        s = s.masked_fill(kpos > qpos, -math.inf)
+        o = torch.einsum("hlm,hmd->hld", torch.softmax(s, -1), v)
+        out[s0:s1] = o.transpose(0, 1).reshape(L, Hq * D).to(qkv.dtype)
+    return out
+
+
 def knn(xb, xb_norms, xq, k, inner_product, id_offset):
     """FAISS IndexFlat semantics: L2 -> ascending squared distances, IP -> descending."""
     nq = xq.shape[0]

@@ -20,14 +20,14 @@ import torch
 
 from ..engine.llm_engine import LLMEngine, SamplingParams
 
-# Expert-assistant prompt with the same slots/structure as the reference's
-# QA_CHAIN_PROMPT (context block, strict instructions, practitioner question).
+# Expert-assistant prompt with the same slots as the reference's QA_CHAIN_PROMPT
+# (instructions, context block, practitioner question).  All fixed text comes FIRST so
+# every request shares a long token prefix: the engine's prefix cache then serves those
+# KV blocks from HBM instead of recomputing them (the reference puts the context in the
+# middle, which would make every prompt unique after ~30 tokens).
 DEFAULT_TEMPLATE = """Vous êtes un expert en pharmacopée chinoise (MTC) assistant un praticien.
-Les extraits ci-dessous proviennent de la base de connaissances et des dossiers patients ;
-chaque plante y est accompagnée d'un score de pertinence.
-
-EXTRAITS (base MTC et dossier patient) :
-{context}
+Vous recevez des extraits de la base de connaissances et des dossiers patients ; chaque
+plante y est accompagnée d'un score de pertinence.
 
 CONSIGNES :
 1. Repérez le syndrome du patient dans les extraits.
@@ -35,6 +35,10 @@ CONSIGNES :
 3. Ordonnez-les par score de pertinence décroissant (10 = plante Empereur, 7 = plante Ministre).
 4. Répondez par une liste numérotée en justifiant chaque plante par son score et son rôle,
    par exemple : "1. [Plante] (score 10, Empereur) : recommandée parce que ...".
+5. N'utilisez que les informations des extraits ; si elles sont insuffisantes, dites-le.
+
+EXTRAITS (base MTC et dossier patient) :
+{context}
 
 QUESTION DU PRATICIEN :
 {question}

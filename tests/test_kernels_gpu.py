@@ -177,6 +177,26 @@ def test_flash_prefill(native, D, causal):
     _close(o1, o2, 3e-2, 1e-2)
 
 
+@pytest.mark.parametrize("prefix", [[0, 64, 128, 320], [256, 0, 64, 1000]])
+def test_flash_prefill_paged(native, prefix):
+    """Prefix-cached prefill: keys = cached prefix + new tokens, read via block tables."""
+    from docqa_amd.ops import reference as R
+
+    Hq, Hkv, D, BS = 8, 2, 128, 64
+    new = [5, 130, 64, 200]
+    B = len(new)
+    maxb = 32
+    kc = torch.randn(B * maxb, Hkv, BS, D, device="cuda", dtype=torch.bfloat16)
+    vc = torch.randn(B * maxb, Hkv, BS, D, device="cuda", dtype=torch.bfloat16)
+    bt = torch.randperm(B * maxb, device="cuda").int().view(B, maxb)
+    cu = torch.tensor([0] + list(torch.tensor(new).cumsum(0)), device="cuda", dtype=torch.int32)
+    qkv = torch.randn(sum(new), (Hq + 2 * Hkv) * D, device="cuda", dtype=torch.bfloat16)
+    cs = torch.tensor(prefix, device="cuda", dtype=torch.int32)
+    o1 = native.flash_prefill_paged(qkv, cu, max(new), Hq, Hkv, D, 1 / math.sqrt(D), kc, vc, bt, cs)
+    o2 = R.flash_prefill_paged(qkv, cu, max(new), Hq, Hkv, D, 1 / math.sqrt(D), kc, vc, bt, cs)
+    _close(o1, o2, 3e-2, 1e-2)
+
+
 def test_flash_prefill_spike(native):
     """Force the online-softmax rescale branch: one huge key late in the sequence."""
     from docqa_amd.ops import reference as R
