@@ -19,6 +19,7 @@
 #include "docqa_common.h"
 #include "docqa_topk.h"
 #include <float.h>
+#include <algorithm>
 
 using namespace docqa;
 
@@ -121,10 +122,13 @@ __global__ __launch_bounds__(256) void pq_encode_kernel(const float* __restrict_
                                                         const int64_t* __restrict__ assign,
                                                         const float* __restrict__ pq, int n, int d,
                                                         int M, int dsub, uint8_t* __restrict__ codes) {
-  const int wave = (blockIdx.x * 256 + threadIdx.x) >> 6;
   const int lane = threadIdx.x & 63;
-  const int i = wave / M, m = wave % M;
-  if (i >= n) return;
+  const long long total = (long long)n * M;
+  const long long nwaves = (long long)gridDim.x * 4;
+  // grid-stride over (vector, sub-quantizer) pairs: a 10M x 64 encode is 640M wave-tasks,
+  // past HIP's 2^32 work-item launch limit if launched flat
+  for (long long wave = (long long)blockIdx.x * 4 + (threadIdx.x >> 6); wave < total; wave += nwaves) {
+  const int i = (int)(wave / M), m = (int)(wave % M);
   const float* xr = x + (size_t)i * d + m * dsub;
   const float* cr = centroids + (size_t)assign[i] * d + m * dsub;
   float best = FLT_MAX;
@@ -145,6 +149,7 @@ __global__ __launch_bounds__(256) void pq_encode_kernel(const float* __restrict_
     if (ob < best || (ob == best && oi < bi)) { best = ob; bi = oi; }
   }
   if (lane == 0) codes[(size_t)i * M + m] = (uint8_t)bi;
+  }
 }
 
 }  // namespace
@@ -199,7 +204,7 @@ int docqa_pq_encode(const float* x, const float* centroids, const int64_t* assig
   if (n == 0) return 0;
   if (d % M != 0) return -1;
   const long long waves = (long long)n * M;
-  const int blocks = (int)((waves + 3) / 4);
+  const int blocks = (int)std::min<long long>((waves + 3) / 4, 1 << 16);
   pq_encode_kernel<<<blocks, 256, 0, s>>>(x, centroids, assign, pq, n, d, M, d / M, codes);
   DOCQA_CHECK_LAUNCH();
   return 0;
