@@ -224,6 +224,25 @@ at::Tensor flash_prefill_paged(const at::Tensor& qkv, const at::Tensor& cu_seqle
   return out;
 }
 
+// epilogue: 0 none, 1 bias, 2 bias+gelu, 3 bias+residual
+at::Tensor gemm(const at::Tensor& a, const at::Tensor& w, const c10::optional<at::Tensor>& bias,
+                const c10::optional<at::Tensor>& residual, int64_t epi) {
+  CHECK_GPU(a); CHECK_BF16(a); CHECK_BF16(w); CHECK_CONTIG(a); CHECK_CONTIG(w);
+  const int K = a.size(-1), N = w.size(0);
+  TORCH_CHECK(w.size(1) == K, "gemm: K mismatch");
+  const int M = a.numel() / K;
+  const void* bp = nullptr;
+  const void* rp = nullptr;
+  if (bias.has_value()) { CHECK_BF16(*bias); TORCH_CHECK(bias->numel() == N, "bias size"); bp = bias->data_ptr(); }
+  if (residual.has_value()) { CHECK_BF16(*residual); CHECK_CONTIG(*residual); rp = residual->data_ptr(); }
+  auto sizes = a.sizes().vec();
+  sizes.back() = N;
+  c10::DeviceGuard g(a.device());
+  auto out = at::empty(sizes, a.options());
+  CHECK_RC(docqa_gemm(a.data_ptr(), w.data_ptr(), bp, rp, out.data_ptr(), M, N, K, (int)epi, stream()), "gemm");
+  return out;
+}
+
 std::tuple<at::Tensor, at::Tensor> knn(const at::Tensor& xb, const at::Tensor& xb_norms,
                                        const at::Tensor& xq, int64_t k, bool inner_product,
                                        int64_t id_offset) {
@@ -330,6 +349,7 @@ TORCH_LIBRARY(docqa, m) {
   m.def("ivfpq_search(Tensor xq, Tensor centroids, Tensor pq, Tensor codes, Tensor ids, "
         "Tensor list_off, Tensor probes, int k) -> (Tensor, Tensor)");
   m.def("pq_encode(Tensor x, Tensor centroids, Tensor assign, Tensor pq) -> Tensor");
+  m.def("gemm(Tensor a, Tensor w, Tensor? bias, Tensor? residual, int epi) -> Tensor");
   m.def("flash_prefill_paged(Tensor qkv, Tensor cu_seqlens, int max_len, int Hq, int Hkv, int D, "
         "float scale, Tensor k_cache, Tensor v_cache, Tensor block_tables, Tensor ctx_start) -> Tensor");
 }
@@ -351,5 +371,6 @@ TORCH_LIBRARY_IMPL(docqa, CUDA, m) {
   m.impl("pool_l2", &pool_l2);
   m.impl("ivfpq_search", &ivfpq_search);
   m.impl("pq_encode", &pq_encode);
+  m.impl("gemm", &gemm);
   m.impl("flash_prefill_paged", &flash_prefill_paged);
 }

@@ -47,6 +47,9 @@ int docqa_flash_prefill_paged(const void* qkv, int row_stride, const int* cu_seq
                               const int* block_tables, int maxb, const int* ctx_start, int BS,
                               hipStream_t s);
 
+int docqa_gemm(const void* A, const void* W, const void* bias, const void* res, void* C, int M,
+               int N, int K, int epi, hipStream_t s);
+
 int docqa_knn_workspace_blocks(int N);
 int docqa_knn_kpad(int k);
 int docqa_knn(const void* xb, const float* norms, int N, int d, int is_bf16, const float* xq,

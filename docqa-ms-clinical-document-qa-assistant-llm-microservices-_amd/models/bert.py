@@ -144,13 +144,13 @@ class BertEncoder:
                               self.emb_b, cfg.eps)
         nh, hd = cfg.heads, cfg.head_dim
         for L in self.layers:
-            qkv = F.linear(h, L["qkv_w"], L["qkv_b"])
+            qkv = ops.linear_fused(h, L["qkv_w"], L["qkv_b"], None, ops.EPI_BIAS)
             a = ops.flash_prefill(qkv, cu_seqlens, max_len, nh, nh, hd, self.scale, False)
-            o = F.linear(a, L["o_w"], L["o_b"])
-            h = ops.layernorm(o, h, L["ln1_g"], L["ln1_b"], cfg.eps)
-            u = ops.bias_act(F.linear(h, L["up_w"]), L["up_b"], None, True)
-            d = F.linear(u, L["down_w"], L["down_b"])
-            h = ops.layernorm(d, h, L["ln2_g"], L["ln2_b"], cfg.eps)
+            o = ops.linear_fused(a, L["o_w"], L["o_b"], h, ops.EPI_BIAS_RES)     # + residual
+            h = ops.layernorm(o, None, L["ln1_g"], L["ln1_b"], cfg.eps)
+            u = ops.linear_fused(h, L["up_w"], L["up_b"], None, ops.EPI_BIAS_GELU)
+            d = ops.linear_fused(u, L["down_w"], L["down_b"], h, ops.EPI_BIAS_RES)
+            h = ops.layernorm(d, None, L["ln2_g"], L["ln2_b"], cfg.eps)
         return h
 
     def encode_packed(self, ids, cu_seqlens, max_len) -> torch.Tensor:

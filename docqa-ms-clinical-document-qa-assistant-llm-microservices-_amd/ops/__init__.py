@@ -127,6 +127,24 @@ def bias_act(x, bias, residual=None, gelu: bool = False):
     return ref.bias_act(x, bias, residual, gelu)
 
 
+# ----------------------------------------------------------------------------- fused GEMM
+EPI_NONE, EPI_BIAS, EPI_BIAS_GELU, EPI_BIAS_RES = 0, 1, 2, 3
+
+
+def linear_fused(x, w, bias=None, residual=None, epi: int = EPI_BIAS):
+    """act(x @ w^T + bias) (+ residual) on the hand-written MFMA GEMM (N % 128 == 0,
+    K % 64 == 0); other shapes fall back to hipBLASLt + the element-wise kernel."""
+    if _gpu(x):
+        N, K = w.shape
+        if N % 128 == 0 and K % 64 == 0:
+            return _native().gemm(x.contiguous(), w, bias, residual, epi)
+        y = torch.nn.functional.linear(x, w)
+        if epi == EPI_NONE:
+            return y
+        return bias_act(y, bias, residual if epi == EPI_BIAS_RES else None, epi == EPI_BIAS_GELU)
+    return ref.linear_fused(x, w, bias, residual, epi)
+
+
 # ----------------------------------------------------------------------------- embeddings
 def embedding(ids, table):
     if _gpu(table):

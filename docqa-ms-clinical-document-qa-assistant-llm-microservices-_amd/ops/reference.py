@@ -81,6 +81,18 @@ def bias_act(x, bias, residual, gelu):
     return y.to(x.dtype)
 
 
+def linear_fused(x, w, bias, residual, epi):
+    """epi: 0 none, 1 bias, 2 bias+gelu, 3 bias+residual (fp32 accumulate, bf16 out)."""
+    y = x.float() @ w.float().T
+    if epi >= 1:
+        y = y + bias.float()
+    if epi == 2:
+        y = F.gelu(y)
+    if epi == 3:
+        y = y + residual.float()
+    return y.to(x.dtype)
+
+
 def embedding(ids, table):
     return table[ids.long()]
 

@@ -197,6 +197,34 @@ def test_flash_prefill_paged(native, prefix):
     _close(o1, o2, 3e-2, 1e-2)
 
 
+@pytest.mark.parametrize("M,N,K", [(1, 128, 64), (77, 384, 384), (300, 1536, 384), (1000, 384, 1536),
+                                   (2048, 3072, 768), (129, 1152, 384)])
+@pytest.mark.parametrize("epi", [0, 1, 2, 3])
+def test_gemm_fused(native, M, N, K, epi):
+    from docqa_amd.ops import reference as R
+
+    a = torch.randn(M, K, device="cuda", dtype=torch.bfloat16)
+    w = (torch.randn(N, K, device="cuda") / K ** 0.5).bfloat16()
+    b = torch.randn(N, device="cuda", dtype=torch.bfloat16)
+    r = torch.randn(M, N, device="cuda", dtype=torch.bfloat16)
+    bias = b if epi else None
+    res = r if epi == 3 else None
+    o1 = native.gemm(a, w, bias, res, epi)
+    o2 = R.linear_fused(a, w, bias, res, epi)
+    _close(o1, o2, 3e-2, 1e-2)
+
+
+def test_gemm_asymmetric_identity(native):
+    """A = I with an asymmetric W catches a transposed C write (guide §3)."""
+    n = 128
+    a = torch.eye(n, device="cuda", dtype=torch.bfloat16)
+    w = (torch.arange(n * 64, device="cuda").view(n, 64) % 97).bfloat16()
+    a64 = torch.zeros(n, 64, device="cuda", dtype=torch.bfloat16)
+    a64[:, :64] = a[:, :64]
+    o = native.gemm(a64, w, None, None, 0).float()
+    assert torch.equal(o[:64, :], w.float()[:, :64].T[:64, :])
+
+
 def test_flash_prefill_spike(native):
     """Force the online-softmax rescale branch: one huge key late in the sequence."""
     from docqa_amd.ops import reference as R
