@@ -59,38 +59,35 @@ __global__ __launch_bounds__(256) void gemm_kernel(const uint16_t* __restrict__ 
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  // staging: each tensor tile = 128 rows x 8 chunks = 1024 chunks, 4 per thread
-  uint4 ra[4], rw[4];
-  auto load = [&](int kt) {
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int idx = tid + 256 * i;
-      const int r = idx >> 3, ch = idx & 7;
-      const int gr = row0 + r;
-      ra[i] = gr < M ? *reinterpret_cast<const uint4*>(A + (size_t)gr * K + kt * BK + ch * 8)
-                     : make_uint4(0, 0, 0, 0);
-      rw[i] = *reinterpret_cast<const uint4*>(W + (size_t)(col0 + r) * K + kt * BK + ch * 8);
-    }
-  };
-  auto store = [&](int buf) {
+  // staging by LDS-DMA (global_load_lds, 16 B per lane): each tensor tile is 128 rows x
+  // 8 chunks = 16 wave-instructions of 1 KiB, 4 per wave per tensor.  The LDS image is
+  // lane-linear, so the XOR swizzle is applied to the per-lane SOURCE address (rule 21):
+  // physical chunk p of the image receives logical chunk (p&7) ^ ((row>>1)&7) of its row.
+  typedef __attribute__((address_space(3))) void lds_void;
+  auto stage = [&](int kt, int buf) {
     uint16_t* sa = smem + buf * (2 * BM * BK);
     uint16_t* sw = sa + BM * BK;
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-      const int idx = tid + 256 * i;
-      const int r = idx >> 3, ch = idx & 7;
-      *reinterpret_cast<uint4*>(sa + sw_off(r, ch)) = ra[i];
-      *reinterpret_cast<uint4*>(sw + sw_off(r, ch)) = rw[i];
+      const int p0 = (i * 4 + wave) * 64;          // first physical chunk of this issue
+      const int p = p0 + lane;
+      const int r = p >> 3;
+      const int ch = (p & 7) ^ ((r >> 1) & 7);
+      const int gr = min(row0 + r, M - 1);         // tail rows: valid memory, never stored
+      __builtin_amdgcn_global_load_lds(A + (size_t)gr * K + kt * BK + ch * 8,
+                                       (lds_void*)(sa + p0 * 8), 16, 0, 0);
+      __builtin_amdgcn_global_load_lds(W + (size_t)(col0 + r) * K + kt * BK + ch * 8,
+                                       (lds_void*)(sw + p0 * 8), 16, 0, 0);
     }
   };
 
   const int nk = K / BK;
-  load(0);
-  store(0);
+  stage(0, 0);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   for (int kt = 0; kt < nk; ++kt) {
     const int buf = kt & 1;
-    if (kt + 1 < nk) load(kt + 1);
+    if (kt + 1 < nk) stage(kt + 1, buf ^ 1);   // DMA of tile t+1 overlaps MFMAs of tile t
     const uint16_t* sa = smem + buf * (2 * BM * BK);
     const uint16_t* sw = sa + BM * BK;
 #pragma unroll
@@ -109,7 +106,7 @@ __global__ __launch_bounds__(256) void gemm_kernel(const uint16_t* __restrict__ 
         for (int j = 0; j < 4; ++j)
           acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bf[j], acc[i][j], 0, 0, 0);
     }
-    if (kt + 1 < nk) store(buf ^ 1);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
   }
 
