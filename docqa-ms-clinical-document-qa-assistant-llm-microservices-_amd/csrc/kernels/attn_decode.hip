@@ -27,6 +27,7 @@
 // (llm-qa/main.py:69, greedy decode loop of RetrievalQA.invoke at llm-qa/main.py:117).
 #include "docqa_common.h"
 #include <float.h>
+#include <stdlib.h>
 
 using namespace docqa;
 
@@ -244,9 +245,16 @@ int docqa_paged_decode(const void* q, int q_stride, const void* k_cache, const v
   return 0;
 }
 
-// splits per (sequence, kv head): enough workgroups to cover the chip ~4x, at most 64
+// splits per (sequence, kv head): about `target` workgroups in total (default 512 = two
+// per CU, all resident at once at this kernel's 3 waves/SIMD -- a second partial round of
+// workgroups would leave most CUs idle at the tail), at most 64 splits
 int docqa_decode_splits(int B, int Hkv, int max_context) {
-  int s = (4 * 256 + B * Hkv - 1) / (B * Hkv);
+  static int target = [] {
+    const char* e = getenv("DOCQA_DECODE_WG_TARGET");
+    const int v = e ? atoi(e) : 0;
+    return v > 0 ? v : 512;
+  }();
+  int s = (target + B * Hkv - 1) / (B * Hkv);
   const int by_len = (max_context + kMinChunk - 1) / kMinChunk;
   if (s > by_len) s = by_len;
   if (s > 64) s = 64;
