@@ -78,18 +78,20 @@ def main() -> None:
         base = (step * ps.dp_size + ps.dp_rank) * a.batch
         return qs[base:base + a.batch]
 
-    for w in range(a.warmup):
-        pipe.answer_batch(batch_for(w), params)
+    # Warm-up and timed runs are separate pipelines, so the timed region contains exactly
+    # K batches' worth of embed + search + prompt assembly + generation (batch i+1's
+    # embed/search run on a side HIP stream and its prompt assembly on a helper thread
+    # while batch i generates) and no collective is pending at the barriers.
+    for _ in pipe.answer_pipelined([batch_for(w) for w in range(a.warmup)], params):
+        pass
     torch.cuda.synchronize()
     comm.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     step_times, stages = [], []
-    for s in range(a.steps):
-        ts = time.perf_counter()
-        ans = pipe.answer_batch(batch_for(a.warmup + s), params)
-        step_times.append(time.perf_counter() - ts)
-        stages.append(pipe.last_times)
+    for ans, st, lat in pipe.answer_pipelined([batch_for(a.warmup + s) for s in range(a.steps)], params):
+        step_times.append(lat)   # per-batch answer latency: prepare start -> answers ready
+        stages.append(st)
     torch.cuda.synchronize()
     comm.barrier()
     torch.cuda.synchronize()

@@ -89,9 +89,10 @@ __global__ __launch_bounds__(256) void paged_decode_kernel(
     for (int j = 0; j < 8; ++j) acc[g][j] = 0.f;
   }
 
-  for (int base = wave * 4 + tg; base < n; base += 16 * U) {
-    uint4 kr[U], vr[U];
-    bool ok[U];
+  // Software pipeline (register double buffer): the K/V rows of step i+1 are in flight
+  // while step i's dot products / online softmax / P.V run, so HBM latency is hidden by
+  // this wave's own compute instead of only by other waves.
+  auto load = [&](uint4 (&kr)[U], uint4 (&vr)[U], bool (&ok)[U], int base) {
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const int tok = base + 16 * u;
@@ -104,6 +105,8 @@ __global__ __launch_bounds__(256) void paged_decode_kernel(
         vr[u] = *reinterpret_cast<const uint4*>(v_cache + off);
       }
     }
+  };
+  auto compute = [&](const uint4 (&kr)[U], const uint4 (&vr)[U], const bool (&ok)[U]) {
     float s[U][G];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
@@ -143,6 +146,21 @@ __global__ __launch_bounds__(256) void paged_decode_kernel(
         }
       }
     }
+  };
+
+  uint4 kA[U], vA[U], kB[U], vB[U];
+  bool okA[U], okB[U];
+  int base = wave * 4 + tg;
+  if (base < n) load(kA, vA, okA, base);
+  while (base < n) {
+    const int nb = base + 16 * U;
+    if (nb < n) load(kB, vB, okB, nb);
+    compute(kA, vA, okA);
+    if (nb >= n) break;
+    const int nb2 = nb + 16 * U;
+    if (nb2 < n) load(kA, vA, okA, nb2);
+    compute(kB, vB, okB);
+    base = nb2;
   }
 
   // ---- merge the 4 lane-group streams of the wave (lanes l, l^16, l^32, l^48)
@@ -233,8 +251,8 @@ int docqa_paged_decode(const void* q, int q_stride, const void* k_cache, const v
   switch (G) {
     case 1: DEC(1, 4); break;
     case 2: DEC(2, 4); break;
-    case 4: DEC(4, 4); break;
-    case 8: DEC(8, 2); break;
+    case 4: DEC(4, 2); break;
+    case 8: DEC(8, 1); break;
     default: return -1;
   }
 #undef DEC

@@ -271,8 +271,8 @@ class LLMEngine:
             tok = torch.zeros(g.bp, dtype=torch.int32, device=dev)
             tok[:B] = first.int()
             g.tokens.copy_(tok)
-            if dev.type == "cuda":
-                torch.cuda.synchronize()
+            if dev.type == "cuda":  # this stream only: a pipelined prep stream keeps running
+                torch.cuda.current_stream().synchronize()
             t1 = time.perf_counter()
             if self.use_graphs and g.graph is None and params.max_new_tokens > 1:
                 self._capture(g)

@@ -127,3 +127,50 @@ class RAGPipeline:
 
     def answer(self, question: str, params: SamplingParams | None = None) -> Answer:
         return self.answer_batch([question], params)[0]
+
+    # ------------------------------------------------------------------ pipelined
+    def _prepare(self, questions: list[str], stream):
+        """embed + kNN on a side HIP stream, then host-side prompt assembly."""
+        t0 = time.perf_counter()
+        ctx = torch.cuda.stream(stream) if stream is not None else _nullctx()
+        with ctx:
+            qemb = self.embed(questions)
+            _, I = self.index.search(qemb, self.k)
+            I = I.tolist()       # waits for this side stream only
+        t1 = time.perf_counter()
+        prompts = self.build_prompts(questions, I)
+        return questions, I, prompts, t0, t1, time.perf_counter()
+
+    @torch.inference_mode()
+    def answer_pipelined(self, batches: list[list[str]], params: SamplingParams | None = None):
+        """Yield (answers, StageTimes, latency_s) per batch while overlapping batch i+1's
+        embedding, kNN search (side HIP stream) and prompt assembly (helper thread) with
+        batch i's generation on the main stream -- the embed/search/generate overlap of
+        the serving path.  Latency = prepare start -> answers ready."""
+        import concurrent.futures as cf
+
+        params = params or SamplingParams(stop_on_eos=True)
+        stream = torch.cuda.Stream() if self.engine.device.type == "cuda" else None
+        with cf.ThreadPoolExecutor(1, thread_name_prefix="rag-prep") as ex:
+            fut = ex.submit(self._prepare, batches[0], stream) if batches else None
+            for i in range(len(batches)):
+                questions, I, prompts, t0, t1, t2 = fut.result()
+                if i + 1 < len(batches):
+                    fut = ex.submit(self._prepare, batches[i + 1], stream)
+                t3 = time.perf_counter()
+                outs = self.engine.generate(prompts, params)
+                t4 = time.perf_counter()
+                st = StageTimes(embed_s=t1 - t0, search_s=0.0, prompt_s=t2 - t1, generate_s=t4 - t3)
+                self.last_times = st
+                res = [Answer(answer=self.chat_tok.decode(toks),
+                              sources=[self.metadata[j].get("source") for j in ids if 0 <= j < len(self.metadata)],
+                              token_ids=toks) for ids, toks in zip(I, outs)]
+                yield res, st, t4 - t0
+
+
+class _nullctx:
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        return False

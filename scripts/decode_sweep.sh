@@ -1,7 +1,7 @@
 #!/bin/bash
 # sweep the decode split target on the kernel micro-benchmark (one process per setting)
 cd "${GRAFT_REPO_ROOT:-/root/repo}"; mkdir -p gpurun_out
-for t in 256 512 768 1024; do
+for t in ${SWEEP_TARGETS:-512}; do
   DOCQA_DECODE_WG_TARGET=$t timeout -k 10 300 python -c "
 import json, math, torch, sys
 sys.path.insert(0, '.')
