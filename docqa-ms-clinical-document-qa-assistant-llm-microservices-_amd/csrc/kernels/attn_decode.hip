@@ -92,18 +92,19 @@ __global__ __launch_bounds__(256) void paged_decode_kernel(
   // Software pipeline (register double buffer): the K/V rows of step i+1 are in flight
   // while step i's dot products / online softmax / P.V run, so HBM latency is hidden by
   // this wave's own compute instead of only by other waves.
+  // Loads are unconditional (tail tokens re-read the slice's last valid row and are
+  // masked in compute): a per-element "load or skip" branch makes hipcc wait vmcnt(0)
+  // around every load and serialises the stream (guide §5 trap (c)).
   auto load = [&](uint4 (&kr)[U], uint4 (&vr)[U], bool (&ok)[U], int base) {
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const int tok = base + 16 * u;
       ok[u] = tok < n;
-      if (ok[u]) {
-        const int t = start + tok;
-        const size_t off = (size_t)bt[t >> log2BS] * blk_stride + head_off +
-                           (size_t)(t & (BS - 1)) * D;
-        kr[u] = *reinterpret_cast<const uint4*>(k_cache + off);
-        vr[u] = *reinterpret_cast<const uint4*>(v_cache + off);
-      }
+      const int t = start + min(tok, n - 1);
+      const size_t off = (size_t)bt[t >> log2BS] * blk_stride + head_off +
+                         (size_t)(t & (BS - 1)) * D;
+      kr[u] = *reinterpret_cast<const uint4*>(k_cache + off);
+      vr[u] = *reinterpret_cast<const uint4*>(v_cache + off);
     }
   };
   auto compute = [&](const uint4 (&kr)[U], const uint4 (&vr)[U], const bool (&ok)[U]) {

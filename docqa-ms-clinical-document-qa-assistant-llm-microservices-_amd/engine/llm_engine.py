@@ -208,14 +208,19 @@ class LLMEngine:
 
     # ------------------------------------------------------------------ generate
     @torch.inference_mode()
-    def generate(self, prompts: list[list[int]], params: SamplingParams | None = None) -> list[list[int]]:
+    def generate(self, prompts: list[list[int]], params: SamplingParams | None = None,
+                 on_step=None) -> list[list[int]]:
+        """``on_step(step, total)`` is called from the host decode loop after each step is
+        enqueued (the serving pipeline uses it to start the next batch's preparation a few
+        steps before this one ends)."""
         params = params or SamplingParams()
         out: list[list[int]] = []
         for i in range(0, len(prompts), self.max_batch):
-            out.extend(self._generate_batch(prompts[i:i + self.max_batch], params))
+            out.extend(self._generate_batch(prompts[i:i + self.max_batch], params, on_step))
         return out
 
-    def _generate_batch(self, prompts: list[list[int]], params: SamplingParams) -> list[list[int]]:
+    def _generate_batch(self, prompts: list[list[int]], params: SamplingParams,
+                        on_step=None) -> list[list[int]]:
         B = len(prompts)
         dev = self.device
         lens = [len(p) for p in prompts]
@@ -277,6 +282,8 @@ class LLMEngine:
             if self.use_graphs and g.graph is None and params.max_new_tokens > 1:
                 self._capture(g)
             for step in range(1, params.max_new_tokens):
+                if on_step is not None:
+                    on_step(step, params.max_new_tokens)
                 if g.graph is not None:
                     g.graph.replay()
                 else:

@@ -129,43 +129,77 @@ class RAGPipeline:
         return self.answer_batch([question], params)[0]
 
     # ------------------------------------------------------------------ pipelined
-    def _prepare(self, questions: list[str], stream):
-        """embed + kNN on a side HIP stream, then host-side prompt assembly."""
+    @torch.inference_mode()
+    def _prepare(self, questions: list[str], stream, gate):
+        """embed + kNN on a side HIP stream (held back by ``gate`` until the running
+        generation is ``lead_steps`` from its end), then host-side prompt assembly."""
         t0 = time.perf_counter()
-        ctx = torch.cuda.stream(stream) if stream is not None else _nullctx()
-        with ctx:
+        ev_start = None
+        if stream is not None:
+            with torch.cuda.stream(stream):
+                if gate is not None:
+                    stream.wait_event(gate)
+                ev_start = torch.cuda.Event(enable_timing=True)
+                ev_start.record(stream)
+                qemb = self.embed(questions)
+                _, I = self.index.search(qemb, self.k)
+                I = I.tolist()       # waits for this side stream only
+        else:
             qemb = self.embed(questions)
             _, I = self.index.search(qemb, self.k)
-            I = I.tolist()       # waits for this side stream only
+            I = I.tolist()
         t1 = time.perf_counter()
         prompts = self.build_prompts(questions, I)
-        return questions, I, prompts, t0, t1, time.perf_counter()
+        return questions, I, prompts, ev_start, t0, t1, time.perf_counter()
 
     @torch.inference_mode()
-    def answer_pipelined(self, batches: list[list[str]], params: SamplingParams | None = None):
-        """Yield (answers, StageTimes, latency_s) per batch while overlapping batch i+1's
-        embedding, kNN search (side HIP stream) and prompt assembly (helper thread) with
-        batch i's generation on the main stream -- the embed/search/generate overlap of
-        the serving path.  Latency = prepare start -> answers ready."""
+    def answer_pipelined(self, batches: list[list[str]], params: SamplingParams | None = None,
+                         lead_steps: int = 12):
+        """Yield (answers, StageTimes, latency_s) per batch.  Batch i+1's embedding and
+        kNN search run on a side HIP stream and its prompt assembly on a helper thread,
+        released when batch i's decode is ``lead_steps`` steps from its end, so they
+        overlap the tail of batch i's generation (embed/search/generate overlap).
+        Latency is measured on the GPU clock from the moment batch i+1's embedding may
+        start to its answers being ready."""
         import concurrent.futures as cf
 
         params = params or SamplingParams(stop_on_eos=True)
-        stream = torch.cuda.Stream() if self.engine.device.type == "cuda" else None
+        cuda = self.engine.device.type == "cuda"
+        stream = torch.cuda.Stream() if cuda else None
         with cf.ThreadPoolExecutor(1, thread_name_prefix="rag-prep") as ex:
-            fut = ex.submit(self._prepare, batches[0], stream) if batches else None
+            fut = ex.submit(self._prepare, batches[0], stream, None) if batches else None
             for i in range(len(batches)):
-                questions, I, prompts, t0, t1, t2 = fut.result()
-                if i + 1 < len(batches):
-                    fut = ex.submit(self._prepare, batches[i + 1], stream)
+                questions, I, prompts, ev_start, t0, t1, t2 = fut.result()
+                fut = None
+                nxt = batches[i + 1] if i + 1 < len(batches) else None
+
+                def on_step(step, total, nxt=nxt):
+                    nonlocal fut
+                    if nxt is not None and fut is None and step >= max(1, total - lead_steps):
+                        gate = None
+                        if cuda:
+                            gate = torch.cuda.Event()
+                            gate.record()
+                        fut = ex.submit(self._prepare, nxt, stream, gate)
+
                 t3 = time.perf_counter()
-                outs = self.engine.generate(prompts, params)
+                outs = self.engine.generate(prompts, params, on_step=on_step)
                 t4 = time.perf_counter()
+                if nxt is not None and fut is None:   # single-step generations
+                    fut = ex.submit(self._prepare, nxt, stream, None)
+                if cuda:
+                    ev_done = torch.cuda.Event(enable_timing=True)
+                    ev_done.record()
+                    ev_done.synchronize()
+                    latency = ev_start.elapsed_time(ev_done) / 1e3
+                else:
+                    latency = t4 - t0
                 st = StageTimes(embed_s=t1 - t0, search_s=0.0, prompt_s=t2 - t1, generate_s=t4 - t3)
                 self.last_times = st
                 res = [Answer(answer=self.chat_tok.decode(toks),
                               sources=[self.metadata[j].get("source") for j in ids if 0 <= j < len(self.metadata)],
                               token_ids=toks) for ids, toks in zip(I, outs)]
-                yield res, st, t4 - t0
+                yield res, st, latency
 
 
 class _nullctx:
