@@ -45,6 +45,7 @@ def main() -> None:
     ap.add_argument("--k", type=int, default=3)
     ap.add_argument("--max-context", type=int, default=2048)
     ap.add_argument("--no-graphs", action="store_true")
+    ap.add_argument("--device", default="cuda", help="cuda (MI355X) | cpu (CI rehearsal of the DP path with gloo)")
     a = ap.parse_args()
 
     import torch
@@ -60,13 +61,20 @@ def main() -> None:
     if world != a.gpus:
         print(f"[bench] warning: --gpus {a.gpus} but WORLD_SIZE {world}", file=sys.stderr)
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    torch.cuda.set_device(local_rank)
-    ps = comm.init_distributed(tp_size=a.tp)
-    assert ops.load_native(), "native HIP kernels not built (python -m docqa_amd.ops.build)"
-    dev = f"cuda:{local_rank}"
+    cuda = a.device == "cuda"
+    if cuda:
+        torch.cuda.set_device(local_rank)
+    ps = comm.init_distributed(tp_size=a.tp, backend=None if cuda else "gloo")
+    if cuda:
+        assert ops.load_native(), "native HIP kernels not built (python -m docqa_amd.ops.build)"
+    dev = f"cuda:{local_rank}" if cuda else "cpu"
+
+    def sync():
+        if cuda:
+            torch.cuda.synchronize()
 
     sc = StackConfig(llm=a.llm, embed=a.embed, n_notes=a.notes, max_batch=a.batch,
-                     max_context=a.max_context, k=a.k, use_graphs=not a.no_graphs)
+                     max_context=a.max_context, k=a.k, use_graphs=(not a.no_graphs) and cuda)
     pipe, info = build_stack(sc, device=dev)
     params = SamplingParams(max_new_tokens=a.max_new_tokens, temperature=0.0, stop_on_eos=False)
 
@@ -84,17 +92,17 @@ def main() -> None:
     # while batch i generates) and no collective is pending at the barriers.
     for _ in pipe.answer_pipelined([batch_for(w) for w in range(a.warmup)], params):
         pass
-    torch.cuda.synchronize()
+    sync()
     comm.barrier()
-    torch.cuda.synchronize()
+    sync()
     t0 = time.perf_counter()
     step_times, stages = [], []
     for ans, st, lat in pipe.answer_pipelined([batch_for(a.warmup + s) for s in range(a.steps)], params):
         step_times.append(lat)   # per-batch answer latency: prepare start -> answers ready
         stages.append(st)
-    torch.cuda.synchronize()
+    sync()
     comm.barrier()
-    torch.cuda.synchronize()
+    sync()
     elapsed = time.perf_counter() - t0
 
     t = torch.tensor([elapsed] + step_times, dtype=torch.float64, device=dev)

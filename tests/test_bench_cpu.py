@@ -1,0 +1,51 @@
+"""Rehearse the driver's bench.py contract on CPU: single process and a 2-rank torchrun
+(gloo) with the index sharded across ranks, tiny models.  Checks the one-JSON-line output
+and its required keys, so the round-end multi-GPU scaling run cannot fail on plumbing."""
+import json
+import os
+import socket
+import subprocess
+import sys
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parents[1]
+KEYS = {"metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better",
+        "scaling", "vs_baseline", "dtype", "data", "config"}
+ARGS = ["--device", "cpu", "--llm", "tiny", "--embed", "tiny-bert", "--notes", "8", "--batch", "3",
+        "--max-new-tokens", "3", "--steps", "2", "--warmup", "1", "--max-context", "1024"]
+
+
+def _port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _last_json(out: str) -> dict:
+    lines = [l for l in out.strip().splitlines() if l.startswith("{")]
+    assert len(lines) == 1, out
+    return json.loads(lines[0])
+
+
+def test_bench_single_process_cpu():
+    env = dict(os.environ, WORLD_SIZE="1")
+    r = subprocess.run([sys.executable, str(ROOT / "bench.py"), "--gpus", "1", *ARGS], cwd=ROOT,
+                       capture_output=True, text=True, timeout=600, env=env)
+    assert r.returncode == 0, r.stderr[-3000:]
+    d = _last_json(r.stdout)
+    assert KEYS <= set(d) and d["n_gpus"] == 1 and d["value"] > 0
+
+
+def test_bench_two_ranks_gloo_sharded_index():
+    env = dict(os.environ)
+    for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
+        env.pop(k, None)
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", str(_port()), str(ROOT / "bench.py"),
+           "--gpus", "2", *ARGS]
+    r = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=900, env=env)
+    assert r.returncode == 0, r.stderr[-3000:]
+    d = _last_json(r.stdout)
+    assert d["n_gpus"] == 2 and d["config"]["global_batch"] == 6 and d["config"]["parallelism"] == "dp2"
