@@ -82,6 +82,46 @@ void rope_cache(at::Tensor qkv, const at::Tensor& positions, const at::Tensor& c
                             T, Hq, Hkv, D, qkv.size(-1), BS, stream()), "rope_cache");
 }
 
+// split-K partial slabs P [S, rows, H] fp32 -> residual += bf16(sum P); rmsnorm(residual) * w
+at::Tensor add_rmsnorm_splitk(const at::Tensor& P, at::Tensor residual, const at::Tensor& w, double eps) {
+  CHECK_GPU(P); CHECK_CONTIG(P); CHECK_BF16(residual); CHECK_CONTIG(residual); CHECK_BF16(w);
+  TORCH_CHECK(P.scalar_type() == at::kFloat && P.dim() == 3, "partials must be fp32 [S, rows, H]");
+  TORCH_CHECK(P.size(1) * P.size(2) == residual.numel() && P.size(2) == residual.size(-1),
+              "add_rmsnorm_splitk shape mismatch");
+  c10::DeviceGuard g(P.device());
+  auto out = at::empty_like(residual);
+  CHECK_RC(docqa_add_rmsnorm_splitk(P.data_ptr<float>(), P.size(0), residual.data_ptr(), w.data_ptr(),
+                                    out.data_ptr(), P.size(1), P.size(2), (float)eps, stream()),
+           "add_rmsnorm_splitk");
+  return out;
+}
+
+// split-K partial slabs P [S, T, (Hq+2Hkv)*D] fp32 -> packed bf16 qkv (rotated) + cache write
+at::Tensor rope_cache_splitk(const at::Tensor& P, const at::Tensor& positions, const at::Tensor& cos_sin,
+                             const c10::optional<at::Tensor>& slot_mapping, at::Tensor k_cache,
+                             at::Tensor v_cache, int64_t Hq, int64_t Hkv, int64_t D) {
+  CHECK_GPU(P); CHECK_CONTIG(P); CHECK_I32(positions);
+  TORCH_CHECK(P.scalar_type() == at::kFloat && P.dim() == 3, "partials must be fp32 [S, T, width]");
+  TORCH_CHECK(cos_sin.scalar_type() == at::kFloat, "cos_sin must be fp32");
+  TORCH_CHECK(P.size(2) == (Hq + 2 * Hkv) * D, "qkv width mismatch");
+  const int T = P.size(1);
+  const int* sm = nullptr;
+  int BS = 1;
+  if (slot_mapping.has_value()) {
+    CHECK_I32(*slot_mapping);
+    sm = slot_mapping->data_ptr<int>();
+    CHECK_BF16(k_cache); CHECK_BF16(v_cache);
+    BS = k_cache.size(2);
+  }
+  c10::DeviceGuard g(P.device());
+  auto qkv = at::empty({T, P.size(2)}, P.options().dtype(at::kBFloat16));
+  CHECK_RC(docqa_rope_cache_splitk(P.data_ptr<float>(), P.size(0), qkv.data_ptr(), positions.data_ptr<int>(),
+                                   cos_sin.data_ptr<float>(), sm, sm ? k_cache.data_ptr() : nullptr,
+                                   sm ? v_cache.data_ptr() : nullptr, T, Hq, Hkv, D, P.size(2), BS,
+                                   stream()), "rope_cache_splitk");
+  return qkv;
+}
+
 at::Tensor silu_mul(const at::Tensor& gu) {
   CHECK_GPU(gu); CHECK_BF16(gu); CHECK_CONTIG(gu);
   const int I2 = gu.size(-1);
@@ -243,6 +283,39 @@ at::Tensor gemm(const at::Tensor& a, const at::Tensor& w, const c10::optional<at
   return out;
 }
 
+// skinny decode projection Y = X . W^T for M <= 64 rows (splits = 0: auto split-K)
+// split-K partial slabs only: [S, M, N] fp32 (S >= 1), combine fused into the consumer
+at::Tensor dgemm_partial(const at::Tensor& x, const at::Tensor& w, int64_t splits) {
+  CHECK_GPU(x); CHECK_BF16(x); CHECK_BF16(w); CHECK_CONTIG(x); CHECK_CONTIG(w);
+  const int K = x.size(-1), N = w.size(0);
+  TORCH_CHECK(w.size(1) == K, "dgemm_partial: K mismatch");
+  const int M = x.numel() / K;
+  TORCH_CHECK(M <= 64 && splits >= 1, "dgemm_partial: at most 64 rows, splits >= 1");
+  c10::DeviceGuard g(x.device());
+  auto part = at::empty({splits, M, N}, x.options().dtype(at::kFloat));
+  CHECK_RC(docqa_dgemm_partial(x.data_ptr(), w.data_ptr(), part.data_ptr<float>(), M, N, K, (int)splits,
+                               stream()), "dgemm_partial");
+  return part;
+}
+
+at::Tensor dgemm(const at::Tensor& x, const at::Tensor& w, int64_t splits) {
+  CHECK_GPU(x); CHECK_BF16(x); CHECK_BF16(w); CHECK_CONTIG(x); CHECK_CONTIG(w);
+  const int K = x.size(-1), N = w.size(0);
+  TORCH_CHECK(w.size(1) == K, "dgemm: K mismatch");
+  const int M = x.numel() / K;
+  TORCH_CHECK(M <= 64, "dgemm: at most 64 rows");
+  const int S = splits > 0 ? (int)splits : docqa_dgemm_splits(N, K);
+  auto sizes = x.sizes().vec();
+  sizes.back() = N;
+  c10::DeviceGuard g(x.device());
+  auto out = at::empty(sizes, x.options());
+  at::Tensor part;
+  if (S > 1) part = at::empty({S, M, N}, x.options().dtype(at::kFloat));
+  CHECK_RC(docqa_dgemm(x.data_ptr(), w.data_ptr(), out.data_ptr(), S > 1 ? part.data_ptr<float>() : nullptr,
+                       M, N, K, S, stream()), "dgemm");
+  return out;
+}
+
 std::tuple<at::Tensor, at::Tensor> knn(const at::Tensor& xb, const at::Tensor& xb_norms,
                                        const at::Tensor& xq, int64_t k, bool inner_product,
                                        int64_t id_offset) {
@@ -352,6 +425,11 @@ TORCH_LIBRARY(docqa, m) {
   m.def("gemm(Tensor a, Tensor w, Tensor? bias, Tensor? residual, int epi) -> Tensor");
   m.def("flash_prefill_paged(Tensor qkv, Tensor cu_seqlens, int max_len, int Hq, int Hkv, int D, "
         "float scale, Tensor k_cache, Tensor v_cache, Tensor block_tables, Tensor ctx_start) -> Tensor");
+  m.def("dgemm(Tensor x, Tensor w, int splits) -> Tensor");
+  m.def("dgemm_partial(Tensor x, Tensor w, int splits) -> Tensor");
+  m.def("add_rmsnorm_splitk(Tensor P, Tensor(a!) residual, Tensor w, float eps) -> Tensor");
+  m.def("rope_cache_splitk(Tensor P, Tensor positions, Tensor cos_sin, Tensor? slot_mapping, "
+        "Tensor(b!) k_cache, Tensor(c!) v_cache, int Hq, int Hkv, int D) -> Tensor");
 }
 
 TORCH_LIBRARY_IMPL(docqa, CUDA, m) {
@@ -373,4 +451,8 @@ TORCH_LIBRARY_IMPL(docqa, CUDA, m) {
   m.impl("pq_encode", &pq_encode);
   m.impl("gemm", &gemm);
   m.impl("flash_prefill_paged", &flash_prefill_paged);
+  m.impl("dgemm", &dgemm);
+  m.impl("dgemm_partial", &dgemm_partial);
+  m.impl("add_rmsnorm_splitk", &add_rmsnorm_splitk);
+  m.impl("rope_cache_splitk", &rope_cache_splitk);
 }

@@ -47,6 +47,17 @@ int docqa_flash_prefill_paged(const void* qkv, int row_stride, const int* cu_seq
                               const int* block_tables, int maxb, const int* ctx_start, int BS,
                               hipStream_t s);
 
+int docqa_dgemm_partial(const void* X, const void* W, float* P, int M, int N, int K, int S,
+                        hipStream_t s);
+int docqa_add_rmsnorm_splitk(const float* P, int S, void* residual, const void* w, void* out,
+                             int rows, int H, float eps, hipStream_t s);
+int docqa_rope_cache_splitk(const float* P, int S, void* qkv_out, const int* positions,
+                            const float* cos_sin, const int* slot_mapping, void* k_cache,
+                            void* v_cache, int T, int Hq, int Hkv, int D, int row_stride, int BS,
+                            hipStream_t s);
+int docqa_dgemm_splits(int N, int K);
+int docqa_dgemm(const void* X, const void* W, void* Y, float* partial, int M, int N, int K, int S,
+                hipStream_t s);
 int docqa_gemm(const void* A, const void* W, const void* bias, const void* res, void* C, int M,
                int N, int K, int epi, hipStream_t s);
 

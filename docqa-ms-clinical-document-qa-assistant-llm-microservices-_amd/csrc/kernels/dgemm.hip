@@ -1,0 +1,273 @@
+// dgemm.hip -- skinny "decode GEMM" for the Llama generator's per-token projections:
+//   Y[M, N] = X[M, K] . W[N, K]^T,   M = decode batch (<= 64), weights streamed once.
+//
+// At M <= 64 a projection is a weight-streaming problem (<= 64 FLOP per weight byte, far
+// below the MFMA roof), so the design is about HBM bytes in flight (Little's law: ~8 TB/s x
+// a few us of loaded latency = tens of KB per CU), not about tiles:
+//   * workgroup = 64 weight rows x all M rows x one K slice.  W streams HBM -> LDS through
+//     a 4-stage ring of 128-deep k-blocks filled by LDS-DMA (global_load_lds 16 B, source
+//     XOR swizzle so the 16-row B-fragment reads are bank-conflict-free).  In-flight bytes
+//     then cost LDS, not VGPRs: 2 workgroups x 3 stages x 16 KB per CU, while a register
+//     double buffer (the first version of this kernel) capped M=64 at ~4.2 TB/s;
+//   * X (tiny, L2-resident) goes straight to VGPRs, one k-block ahead; each wave owns a
+//     disjoint (16 X rows x k-range) piece: 4 m-tiles at M=64, or 1-2 m-tiles with the
+//     k-range split across waves (partials summed through LDS at the end);
+//   * v_mfma_f32_16x16x32_bf16: A = X fragment, B = 4 weight n-tiles from the ring;
+//   * split-K over the grid's y dimension gives >= 256 workgroups for the narrow
+//     projections (O: N=4096); slices write fp32 partials reduced by a tiny second kernel,
+//     S = 1 writes bf16 directly (gate|up, LM head).
+// Shapes: N % 64 == 0, (K / S) % 512 == 0 (whole 4-stage ring turns), M <= 64.
+#include "docqa_common.h"
+
+using namespace docqa;
+
+namespace {
+constexpr int BN = 64, BKD = 128, NS = 4, MR = 64;
+constexpr int KSTEPS = BKD / 32;               // 16x16x32 k-steps per stage
+constexpr int STAGE = BN * BKD;                // elements of one W stage (16 KB)
+typedef __attribute__((address_space(3))) void lds_void;
+
+// All vector-memory traffic of the main loop is inline asm, so hipcc's waitcnt pass sees
+// none of it: with the LDS-DMA / X loads as builtins it drained everything (vmcnt(0)) at
+// the loop header and before the first MFMA (an LDS-DMA is a pending LDS write to it, and
+// its loop-carried bookkeeping is conservative), which collapsed the ring to one stage.
+// The counted waits below are the only ones (cdna_hip_programming.md §5.7).
+__device__ __forceinline__ void ring_barrier() { asm volatile("s_barrier" ::: "memory"); }
+
+__device__ __forceinline__ uint32_t lds_u32(const void* p) {
+  return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) char*)p;
+}
+
+// one 16-B-per-lane LDS-DMA wave-instruction: lanes write dst_base + 16 * lane.  `nt`:
+// decode weights are read once per step (16 GB per step >> the 256 MB MALL), and the
+// non-temporal policy lands them ~4 % sooner (MI355X_MICROARCH.md nt-weights).
+__device__ __forceinline__ void glds16(const void* gsrc, uint32_t dst_base) {
+  unsigned keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off nt\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep) : "v"(gsrc), "s"(dst_base) : "memory");
+}
+
+template <int OFF>
+__device__ __forceinline__ void gload16(bf16x8& d, const void* p) {
+  asm volatile("global_load_dwordx4 %0, %1, off offset:%2" : "=v"(d) : "v"(p), "i"(OFF) : "memory");
+}
+
+// wait until at most N vector-memory ops are outstanding, naming the registers that
+// become valid so nothing reading them is scheduled above the wait
+template <int N, int SPW>
+__device__ __forceinline__ void wait_vm_n(bf16x8 (&x)[SPW]) {
+  if constexpr (SPW == 1)
+    asm volatile("s_waitcnt vmcnt(%1)" : "+v"(x[0]) : "i"(N) : "memory");
+  else if constexpr (SPW == 2)
+    asm volatile("s_waitcnt vmcnt(%2)" : "+v"(x[0]), "+v"(x[1]) : "i"(N) : "memory");
+  else
+    asm volatile("s_waitcnt vmcnt(%4)" : "+v"(x[0]), "+v"(x[1]), "+v"(x[2]), "+v"(x[3]) : "i"(N) : "memory");
+}
+
+// keep x's registers allocated up to this point (for loads that are drained, never read)
+template <int SPW>
+__device__ __forceinline__ void keep_live(bf16x8 (&x)[SPW]) {
+#pragma unroll
+  for (int s = 0; s < SPW; ++s) asm volatile("" : "+v"(x[s]));
+}
+
+__device__ __forceinline__ int w_off(int row, int ch) {  // [64][128] stage, 16 chunks per row
+  return row * BKD + ((ch ^ (row & 15)) << 3);
+}
+
+// Wave roles: MT m-tiles of 16 X rows; the 4 waves split as (m-tile = wave % MT,
+// k-group = wave / MT) so every wave owns a disjoint (rows x k) piece of the product and
+// the W stage in LDS is shared by all of them.  KW = 4 / MT k-groups are summed at the end.
+template <bool SPLIT, int MT>
+__global__ __launch_bounds__(256) void dgemm_kernel(const uint16_t* __restrict__ X,
+                                                    const uint16_t* __restrict__ W,
+                                                    uint16_t* __restrict__ Y,
+                                                    float* __restrict__ P, int M, int N, int K,
+                                                    int Ks) {
+  constexpr int KW = 4 / MT, SPW = KSTEPS / KW;
+  __shared__ __attribute__((aligned(16))) uint16_t sw[NS * STAGE];   // 64 KB W ring
+  const int n0 = blockIdx.x * BN;
+  const int slice = blockIdx.y;
+  const int kbeg = slice * Ks;
+  const int nkb = Ks / BKD;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int fr = lane & 15, fq = lane >> 4;
+  const int mt = wave % MT, kg = wave / MT;
+  const int xr = min(mt * 16 + fr, M - 1);
+  const uint16_t* xrow = X + (size_t)xr * K + kbeg + kg * SPW * 32 + fq * 8;
+  const uint32_t ring = lds_u32(sw);
+
+  f32x4 acc[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) acc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  // W stage j -> ring slot j % NS: 16 wave-instructions of 64 lanes x 16 B, 4 per wave,
+  // source XOR-swizzled (the DMA destination is lane-linear).  Past the last stage the
+  // sources are clamped (L2 hits into free slots / dead X buffers) so that every step
+  // issues the same loads unconditionally: a load whose destination is live on one path
+  // and not on another lets hipcc hand its registers to other values while the data is
+  // still in flight.
+  const uint16_t* wsrc[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int p = (i * 4 + wave) * 64 + lane;
+    const int r = p >> 4;
+    wsrc[i] = W + (size_t)(n0 + r) * K + kbeg + (((p & 15) ^ (r & 15)) << 3);
+  }
+  auto stage_w = [&](int j) {
+    const int koff = min(j, nkb - 1) * BKD;
+    const uint32_t dst = ring + (uint32_t)((j % NS) * STAGE * 2);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) glds16(wsrc[i] + koff, dst + (uint32_t)((i * 4 + wave) * 1024));
+  };
+  auto load_x = [&](bf16x8 (&x)[SPW], int j) {
+    const uint16_t* src = xrow + min(j, nkb - 1) * BKD;
+    gload16<0>(x[0], src);
+    if constexpr (SPW > 1) gload16<64>(x[1], src);
+    if constexpr (SPW > 2) { gload16<128>(x[2], src); gload16<192>(x[3], src); }
+  };
+  auto mma = [&](const bf16x8 (&x)[SPW], int j) {
+    const uint16_t* src = sw + (j % NS) * STAGE;
+#pragma unroll
+    for (int s = 0; s < SPW; ++s) {
+      const bf16x8 a = x[s];
+      const int ch = (kg * SPW + s) * 4 + fq;
+#pragma unroll
+      for (int nt = 0; nt < 4; ++nt) {
+        const bf16x8 b = *reinterpret_cast<const bf16x8*>(src + w_off(nt * 16 + fr, ch));
+        acc[nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, acc[nt], 0, 0, 0);
+      }
+    }
+  };
+  // Issue order per wave: W0 X0 W1 X1 W2 | step i: X(i+2) W(i+3).  At the top of step i
+  // the ops issued after X(i) are W(i+1), X(i+1), W(i+2), so vmcnt(8 + SPW) retires X(i)
+  // and (issued before it) W(i) while two W stages stay in flight; the barrier then
+  // publishes stage i to every wave and frees slot (i-1) % NS for W(i+3).
+  bf16x8 x0[SPW], x1[SPW], x2[SPW], x3[SPW];
+  stage_w(0);
+  load_x(x0, 0);
+  stage_w(1);
+  load_x(x1, 1);
+  stage_w(2);
+#define RING_STEP(I, XC, XN)                                                            \
+  wait_vm_n<8 + SPW>(XC);                                                               \
+  ring_barrier();                                                                       \
+  load_x(XN, (I) + 2);                                                                  \
+  stage_w((I) + 3);                                                                     \
+  mma(XC, I);
+  // nkb % 4 == 0: a break-free 4-step body keeps each X buffer in one register set (an
+  // early exit makes hipcc merge buffers with register copies that read in-flight data)
+  for (int i = 0; i < nkb; i += 4) {
+    RING_STEP(i, x0, x2)
+    RING_STEP(i + 1, x1, x3)
+    RING_STEP(i + 2, x2, x0)
+    RING_STEP(i + 3, x3, x1)
+  }
+#undef RING_STEP
+  // drain the clamped tail loads; naming every X buffer keeps their registers reserved
+  // until the data has landed
+  wait_vm_n<0>(x0);
+  keep_live(x1);
+  keep_live(x2);
+  keep_live(x3);
+
+  // C/D map of 16x16x32: col = lane & 15 (weight row), row = 4 * (lane >> 4) + r (X row)
+  if constexpr (KW == 1) {
+#pragma unroll
+    for (int nt = 0; nt < 4; ++nt)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = mt * 16 + fq * 4 + r, col = n0 + nt * 16 + fr;
+        if (row < M) {
+          if constexpr (SPLIT) P[((size_t)slice * M + row) * N + col] = acc[nt][r];
+          else Y[(size_t)row * N + col] = f2bf(acc[nt][r]);
+        }
+      }
+  } else {
+    // sum the KW k-groups through LDS (ring is free after the last barrier + wait)
+    __syncthreads();
+    f32x4* red = reinterpret_cast<f32x4*>(sw);   // 16 KB = one slot        // [wave][nt][lane]
+#pragma unroll
+    for (int nt = 0; nt < 4; ++nt) red[(wave * 4 + nt) * 64 + lane] = acc[nt];
+    __syncthreads();
+    const float* rf = reinterpret_cast<const float*>(sw);
+#pragma unroll
+    for (int e = 0; e < MT * 4; ++e) {
+      const int idx = e * 256 + tid;                 // (m-tile, nt, lane, r)
+      const int r = idx & 3, ln = (idx >> 2) & 63, nt = (idx >> 8) & 3, m = idx >> 10;
+      float v = 0.f;
+#pragma unroll
+      for (int g = 0; g < KW; ++g) v += rf[(((g * MT + m) * 4 + nt) * 64 + ln) * 4 + r];
+      const int row = m * 16 + (ln >> 4) * 4 + r, col = n0 + nt * 16 + (ln & 15);
+      if (row < M) {
+        if constexpr (SPLIT) P[((size_t)slice * M + row) * N + col] = v;
+        else Y[(size_t)row * N + col] = f2bf(v);
+      }
+    }
+  }
+}
+
+__global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* __restrict__ P,
+                                                            uint16_t* __restrict__ Y, int MN, int S) {
+  const int i = (blockIdx.x * 256 + threadIdx.x) * 4;
+  if (i >= MN) return;
+  float4 acc = *reinterpret_cast<const float4*>(P + i);
+  for (int s = 1; s < S; ++s) {
+    const float4 v = *reinterpret_cast<const float4*>(P + (size_t)s * MN + i);
+    acc.x += v.x; acc.y += v.y; acc.z += v.z; acc.w += v.w;
+  }
+  uint2 o;
+  o.x = pack2(acc.x, acc.y);
+  o.y = pack2(acc.z, acc.w);
+  *reinterpret_cast<uint2*>(Y + i) = o;
+}
+}  // namespace
+
+// split count: enough workgroups for the chip (>= 256), K slices of whole k-blocks
+int docqa_dgemm_splits(int N, int K) {
+  const int tiles = N / BN;
+  int s = 1;
+  while (tiles * s < 256 && K % (s * 2) == 0 && (K / (s * 2)) % (NS * BKD) == 0)
+    s *= 2;
+  return s;
+}
+
+int docqa_dgemm(const void* X, const void* W, void* Y, float* partial, int M, int N, int K,
+                int S, hipStream_t s) {
+  if (M == 0) return 0;
+  if (M > MR || N % BN != 0 || K % S != 0 || (K / S) % (NS * BKD) != 0) return -1;
+  dim3 grid(N / BN, S);
+  const int mt = (M + 15) / 16;
+  const uint16_t* x = (const uint16_t*)X;
+  const uint16_t* w = (const uint16_t*)W;
+  if (S > 1 && !partial) return -1;
+#define DG(MTV)                                                                                 \
+  if (S == 1) dgemm_kernel<false, MTV><<<grid, 256, 0, s>>>(x, w, (uint16_t*)Y, nullptr, M, N, K, K); \
+  else dgemm_kernel<true, MTV><<<grid, 256, 0, s>>>(x, w, nullptr, partial, M, N, K, K / S);
+  if (mt == 1) { DG(1) } else if (mt == 2) { DG(2) } else { DG(4) }
+#undef DG
+  if (S > 1) {
+    const int MN = M * N;  // multiple of 4 (N % 64 == 0)
+    splitk_reduce_kernel<<<(MN / 4 + 255) / 256, 256, 0, s>>>(partial, (uint16_t*)Y, MN, S);
+  }
+  DOCQA_CHECK_LAUNCH();
+  return 0;
+}
+
+// split-K partial slabs only (S >= 1, P: [S, M, N] fp32): the combine is fused into the
+// consumer (add_rmsnorm_splitk / rope_cache_splitk)
+int docqa_dgemm_partial(const void* X, const void* W, float* P, int M, int N, int K, int S,
+                        hipStream_t s) {
+  if (M == 0) return 0;
+  if (M > MR || N % BN != 0 || S < 1 || K % S != 0 || (K / S) % (NS * BKD) != 0 || !P) return -1;
+  dim3 grid(N / BN, S);
+  const int mt = (M + 15) / 16;
+  const uint16_t* x = (const uint16_t*)X;
+  const uint16_t* w = (const uint16_t*)W;
+  if (mt == 1) dgemm_kernel<true, 1><<<grid, 256, 0, s>>>(x, w, nullptr, P, M, N, K, K / S);
+  else if (mt == 2) dgemm_kernel<true, 2><<<grid, 256, 0, s>>>(x, w, nullptr, P, M, N, K, K / S);
+  else dgemm_kernel<true, 4><<<grid, 256, 0, s>>>(x, w, nullptr, P, M, N, K, K / S);
+  DOCQA_CHECK_LAUNCH();
+  return 0;
+}

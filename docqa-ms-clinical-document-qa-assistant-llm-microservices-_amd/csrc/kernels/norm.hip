@@ -115,6 +115,67 @@ __global__ __launch_bounds__(256) void rmsnorm_row_kernel(const uint16_t* __rest
   }
 }
 
+// Decode add_rmsnorm fed straight by a split-K projection: x = sum of S fp32 partial slabs
+// P[s][row][:] (the skinny GEMM's split-K combine fused here instead of a separate
+// reduce launch + bf16 round trip).  x is rounded to bf16 before the residual add so the
+// result matches projection -> bf16 -> add_rmsnorm bit for bit.
+template <int NV>
+__global__ __launch_bounds__(256) void add_rmsnorm_splitk_kernel(const float* __restrict__ P,
+                                                                 int S, size_t slab,
+                                                                 uint16_t* __restrict__ residual,
+                                                                 const uint16_t* __restrict__ w,
+                                                                 uint16_t* __restrict__ out,
+                                                                 int H, float eps) {
+  const int row = blockIdx.x;
+  const int tid = threadIdx.x;
+  const int nchunk = H >> 3;
+  uint4* rr = reinterpret_cast<uint4*>(residual + (size_t)row * H);
+  float v[NV][8];
+  float ss = 0.f;
+#pragma unroll
+  for (int i = 0; i < NV; ++i) {
+    const int c = tid + 256 * i;
+    if (c < nchunk) {
+      const float* pr = P + (size_t)row * H + c * 8;
+      float4 a = *reinterpret_cast<const float4*>(pr);
+      float4 b = *reinterpret_cast<const float4*>(pr + 4);
+      for (int sl = 1; sl < S; ++sl) {
+        const float4 a2 = *reinterpret_cast<const float4*>(pr + sl * slab);
+        const float4 b2 = *reinterpret_cast<const float4*>(pr + sl * slab + 4);
+        a.x += a2.x; a.y += a2.y; a.z += a2.z; a.w += a2.w;
+        b.x += b2.x; b.y += b2.y; b.z += b2.z; b.w += b2.w;
+      }
+      const float x8[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+      float r[8];
+      unpack8(rr[c], r);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[i][j] = bf2f(f2bf(bf2f(f2bf(x8[j])) + r[j]));
+      rr[c] = pack8(v[i]);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) ss += v[i][j] * v[i][j];
+    }
+  }
+  __shared__ float red[4];
+  ss = wave_sum(ss);
+  if ((tid & 63) == 0) red[tid >> 6] = ss;
+  __syncthreads();
+  ss = red[0] + red[1] + red[2] + red[3];
+  const float inv = rsqrtf(ss / (float)H + eps);
+  const uint4* wr = reinterpret_cast<const uint4*>(w);
+  uint4* orow = reinterpret_cast<uint4*>(out + (size_t)row * H);
+#pragma unroll
+  for (int i = 0; i < NV; ++i) {
+    const int c = tid + 256 * i;
+    if (c < nchunk) {
+      float g[8], o[8];
+      unpack8(wr[c], g);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) o[j] = v[i][j] * inv * g[j];
+      orow[c] = pack8(o);
+    }
+  }
+}
+
 // LayerNorm(x [+ residual]) * gamma + beta; optional residual may alias nothing.
 template <int NV, bool ADD>
 __global__ __launch_bounds__(256) void layernorm_kernel(const uint16_t* __restrict__ x,
@@ -213,6 +274,22 @@ int docqa_add_rmsnorm(const void* x, void* residual, const void* w, void* out, i
                       float eps, hipStream_t s) {
   if (H % 8 != 0 || rows <= 0) return rows == 0 ? 0 : -1;
   return launch_rms<true>(x, residual, w, out, rows, H, eps, s);
+}
+
+int docqa_add_rmsnorm_splitk(const float* P, int S, void* residual, const void* w, void* out,
+                             int rows, int H, float eps, hipStream_t s) {
+  if (rows == 0) return 0;
+  if (H % 8 != 0 || S < 1) return -1;
+  const size_t slab = (size_t)rows * H;
+  const int nvr = (H / 8 + 255) / 256;
+  uint16_t *rp = (uint16_t*)residual, *op = (uint16_t*)out;
+  const uint16_t* wp = (const uint16_t*)w;
+  if (nvr <= 1) add_rmsnorm_splitk_kernel<1><<<rows, 256, 0, s>>>(P, S, slab, rp, wp, op, H, eps);
+  else if (nvr <= 2) add_rmsnorm_splitk_kernel<2><<<rows, 256, 0, s>>>(P, S, slab, rp, wp, op, H, eps);
+  else if (nvr <= 4) add_rmsnorm_splitk_kernel<4><<<rows, 256, 0, s>>>(P, S, slab, rp, wp, op, H, eps);
+  else return -1;
+  DOCQA_CHECK_LAUNCH();
+  return 0;
 }
 
 int docqa_layernorm(const void* x, const void* residual, const void* g, const void* b, void* out,

@@ -19,11 +19,30 @@
 
 using namespace docqa;
 
+// sum of S fp32 split-K partial slabs at element offset `off`, rounded to bf16 (as the
+// unfused projection -> bf16 path would), n = 4 or 8 values
+template <int N>
+__device__ __forceinline__ void load_partials(const float* P, int S, size_t slab, size_t off, float* x) {
+#pragma unroll
+  for (int j = 0; j < N; j += 4) {
+    float4 a = *reinterpret_cast<const float4*>(P + off + j);
+    for (int sl = 1; sl < S; ++sl) {
+      const float4 b = *reinterpret_cast<const float4*>(P + sl * slab + off + j);
+      a.x += b.x; a.y += b.y; a.z += b.z; a.w += b.w;
+    }
+    x[j] = bf2f(f2bf(a.x)); x[j + 1] = bf2f(f2bf(a.y));
+    x[j + 2] = bf2f(f2bf(a.z)); x[j + 3] = bf2f(f2bf(a.w));
+  }
+}
+
+// SPLIT: the packed QKV row comes from a split-K decode projection as S fp32 partial slabs
+// P[s][t][:] and is written (rotated) into `qkv` -- the combine fused into this pass.
+template <bool SPLIT>
 __global__ __launch_bounds__(256) void rope_cache_kernel(
     uint16_t* __restrict__ qkv, const int* __restrict__ positions,
     const float* __restrict__ cos_sin, const int* __restrict__ slot_mapping,
     uint16_t* __restrict__ k_cache, uint16_t* __restrict__ v_cache, int Hq, int Hkv, int D,
-    int row_stride, int BS) {
+    int row_stride, int BS, const float* __restrict__ P, int S, size_t slab) {
   const int t = blockIdx.x;
   const int tph = D >> 3;                 // threads per head
   const int heads_per_pass = 256 / tph;
@@ -38,14 +57,21 @@ __global__ __launch_bounds__(256) void rope_cache_kernel(
     uint16_t* hp = row + h * D;
     if (h < Hq + Hkv) {
       const int i0 = sub * 4;
-      uint2 a = *reinterpret_cast<const uint2*>(hp + i0);
-      uint2 b = *reinterpret_cast<const uint2*>(hp + half + i0);
       const float4 c = *reinterpret_cast<const float4*>(cs + i0);
       const float4 s = *reinterpret_cast<const float4*>(cs + half + i0);
-      float x1[4] = {__uint_as_float(a.x << 16), __uint_as_float(a.x & 0xffff0000u),
-                     __uint_as_float(a.y << 16), __uint_as_float(a.y & 0xffff0000u)};
-      float x2[4] = {__uint_as_float(b.x << 16), __uint_as_float(b.x & 0xffff0000u),
-                     __uint_as_float(b.y << 16), __uint_as_float(b.y & 0xffff0000u)};
+      float x1[4], x2[4];
+      if constexpr (SPLIT) {
+        const size_t base = (size_t)t * row_stride + h * D;
+        load_partials<4>(P, S, slab, base + i0, x1);
+        load_partials<4>(P, S, slab, base + half + i0, x2);
+      } else {
+        const uint2 a = *reinterpret_cast<const uint2*>(hp + i0);
+        const uint2 b = *reinterpret_cast<const uint2*>(hp + half + i0);
+        x1[0] = __uint_as_float(a.x << 16); x1[1] = __uint_as_float(a.x & 0xffff0000u);
+        x1[2] = __uint_as_float(a.y << 16); x1[3] = __uint_as_float(a.y & 0xffff0000u);
+        x2[0] = __uint_as_float(b.x << 16); x2[1] = __uint_as_float(b.x & 0xffff0000u);
+        x2[2] = __uint_as_float(b.y << 16); x2[3] = __uint_as_float(b.y & 0xffff0000u);
+      }
       const float cc[4] = {c.x, c.y, c.z, c.w}, ss[4] = {s.x, s.y, s.z, s.w};
       float o1[4], o2[4];
 #pragma unroll
@@ -65,11 +91,23 @@ __global__ __launch_bounds__(256) void rope_cache_kernel(
         *reinterpret_cast<uint2*>(dst + i0) = oa;
         *reinterpret_cast<uint2*>(dst + half + i0) = ob;
       }
-    } else if (slot >= 0) {
-      const int vh = h - Hq - Hkv;
-      const int blk = slot / BS, off = slot - blk * BS;
-      uint16_t* dst = v_cache + (((size_t)blk * Hkv + vh) * BS + off) * D;
-      *reinterpret_cast<uint4*>(dst + sub * 8) = *reinterpret_cast<const uint4*>(hp + sub * 8);
+    } else {
+      uint4 vv;
+      if constexpr (SPLIT) {
+        float x8[8];
+        load_partials<8>(P, S, slab, (size_t)t * row_stride + h * D + sub * 8, x8);
+        vv = pack8(x8);
+        *reinterpret_cast<uint4*>(hp + sub * 8) = vv;
+      } else {
+        if (slot < 0) continue;
+        vv = *reinterpret_cast<const uint4*>(hp + sub * 8);
+      }
+      if (slot >= 0) {
+        const int vh = h - Hq - Hkv;
+        const int blk = slot / BS, off = slot - blk * BS;
+        uint16_t* dst = v_cache + (((size_t)blk * Hkv + vh) * BS + off) * D;
+        *reinterpret_cast<uint4*>(dst + sub * 8) = vv;
+      }
     }
   }
 }
@@ -79,9 +117,23 @@ int docqa_rope_cache(void* qkv, const int* positions, const float* cos_sin,
                      int Hkv, int D, int row_stride, int BS, hipStream_t s) {
   if (T == 0) return 0;
   if (D % 8 != 0 || (256 % (D / 8)) != 0) return -1;
-  rope_cache_kernel<<<T, 256, 0, s>>>((uint16_t*)qkv, positions, cos_sin, slot_mapping,
-                                      (uint16_t*)k_cache, (uint16_t*)v_cache, Hq, Hkv, D,
-                                      row_stride, BS);
+  rope_cache_kernel<false><<<T, 256, 0, s>>>((uint16_t*)qkv, positions, cos_sin, slot_mapping,
+                                             (uint16_t*)k_cache, (uint16_t*)v_cache, Hq, Hkv, D,
+                                             row_stride, BS, nullptr, 0, 0);
+  DOCQA_CHECK_LAUNCH();
+  return 0;
+}
+
+// qkv_out [T, row_stride] bf16 <- rope(sum_s P[s]) ; P: [S, T, row_stride] fp32
+int docqa_rope_cache_splitk(const float* P, int S, void* qkv_out, const int* positions,
+                            const float* cos_sin, const int* slot_mapping, void* k_cache,
+                            void* v_cache, int T, int Hq, int Hkv, int D, int row_stride, int BS,
+                            hipStream_t s) {
+  if (T == 0) return 0;
+  if (D % 8 != 0 || (256 % (D / 8)) != 0 || S < 1 || row_stride % 4 != 0) return -1;
+  rope_cache_kernel<true><<<T, 256, 0, s>>>((uint16_t*)qkv_out, positions, cos_sin, slot_mapping,
+                                            (uint16_t*)k_cache, (uint16_t*)v_cache, Hq, Hkv, D,
+                                            row_stride, BS, P, S, (size_t)T * row_stride);
   DOCQA_CHECK_LAUNCH();
   return 0;
 }

@@ -206,10 +206,26 @@ class LlamaModel:
         residual = h
         x = ops.rmsnorm(h, self.layers[0]["in_norm"], eps)
         nl = len(self.layers)
+        # decode steps stream every weight once for <= 64 rows: skinny ring GEMM; at TP=1
+        # its split-K combine is fused into the consumer (rope / add_rmsnorm), so QKV, O
+        # and down leave fp32 partial slabs instead of a bf16 tensor + a reduce launch
+        decode = not meta.prefill
+        lin = ops.decode_linear if decode else F.linear
+        M = x.shape[0]
+        sq = so = sd = 0
+        if decode and self.tp == 1 and self.layers:
+            L0 = self.layers[0]
+            sq = ops.decode_splits(M, *L0["qkv"].shape)
+            so = ops.decode_splits(M, *L0["o"].shape)
+            sd = ops.decode_splits(M, *L0["down"].shape)
         for i, L in enumerate(self.layers):
             kc, vc = kv_caches[i]
-            qkv = F.linear(x, L["qkv"])
-            ops.rope_cache(qkv, meta.positions, self.cos_sin, meta.slot_mapping, kc, vc, hq, hkv, D)
+            if sq:
+                qkv = ops.rope_cache_splitk(ops.dgemm_partial(x, L["qkv"], sq), meta.positions, self.cos_sin,
+                                            meta.slot_mapping, kc, vc, hq, hkv, D)
+            else:
+                qkv = lin(x, L["qkv"])
+                ops.rope_cache(qkv, meta.positions, self.cos_sin, meta.slot_mapping, kc, vc, hq, hkv, D)
             if meta.prefill and meta.prefix_lens is not None:
                 # prompt prefix already in the paged cache: attend over cache (prefix + new)
                 a = ops.flash_prefill_paged(qkv, meta.cu_seqlens, meta.max_len, hq, hkv, D, self.scale,
@@ -219,12 +235,18 @@ class LlamaModel:
             else:
                 a = ops.paged_decode(qkv, kc, vc, meta.block_tables, meta.context_lens, hq,
                                      meta.max_context, self.scale)
-            o = comm.tp_all_reduce(F.linear(a, L["o"]))
-            x = ops.add_rmsnorm(o, residual, L["post_norm"], eps)
-            m = F.linear(ops.silu_mul(F.linear(x, L["gate_up"])), L["down"])
-            m = comm.tp_all_reduce(m)
+            if so:
+                x = ops.add_rmsnorm_splitk(ops.dgemm_partial(a, L["o"], so), residual, L["post_norm"], eps)
+            else:
+                o = comm.tp_all_reduce(lin(a, L["o"]))
+                x = ops.add_rmsnorm(o, residual, L["post_norm"], eps)
+            g = ops.silu_mul(lin(x, L["gate_up"]))
             nxt = self.layers[i + 1]["in_norm"] if i + 1 < nl else self.final_norm
-            x = ops.add_rmsnorm(m, residual, nxt, eps)
+            if sd:
+                x = ops.add_rmsnorm_splitk(ops.dgemm_partial(g, L["down"], sd), residual, nxt, eps)
+            else:
+                m = comm.tp_all_reduce(lin(g, L["down"]))
+                x = ops.add_rmsnorm(m, residual, nxt, eps)
         if logits_index is not None:
             x = x.index_select(0, logits_index)
         return F.linear(x, self.lm_head)

@@ -145,6 +145,60 @@ def linear_fused(x, w, bias=None, residual=None, epi: int = EPI_BIAS):
     return ref.linear_fused(x, w, bias, residual, epi)
 
 
+def decode_splits(M: int, N: int, K: int) -> int:
+    """Split-K count for the skinny decode GEMM (csrc/kernels/dgemm.hip) on an [M, K] x
+    [N, K]^T projection, or 0 where hipBLASLt is faster / the shape is unsupported.
+    Measured per projection at M = 64 (profiles/r1_bench_kernels_dgemm.json): the LM head
+    and, above 32 rows, gate|up stay on hipBLASLt; QKV / O / down use the ring kernel with
+    the smallest split giving >= 192 workgroups."""
+    if M > 64 or N % 64 or N >= 65536 or (N >= 16384 and M > 32):
+        return 0
+    tiles, S = N // 64, 1
+    while tiles * S < 192 and K % (2 * S) == 0 and (K // (2 * S)) % 512 == 0:
+        S *= 2
+    return S if K % S == 0 and (K // S) % 512 == 0 else 0
+
+
+def decode_linear(x, w):
+    """x @ w^T for a decode step (<= 64 rows): the skinny weight-streaming MFMA kernel
+    where it beats hipBLASLt on MI355X, else F.linear."""
+    if _gpu(x):
+        N, K = w.shape
+        S = decode_splits(x.numel() // K, N, K)
+        if S:
+            return _native().dgemm(x.contiguous(), w, S)
+    return torch.nn.functional.linear(x, w)
+
+
+def dgemm_partial(x, w, splits: int):
+    """Split-K partial slabs [S, M, N] fp32 of x @ w^T (combine fused into the consumer:
+    add_rmsnorm_splitk / rope_cache_splitk)."""
+    if _gpu(x):
+        return _native().dgemm_partial(x.contiguous(), w, splits)
+    K = w.shape[1]
+    xs = x.float().reshape(-1, splits, K // splits)
+    ws = w.float().reshape(-1, splits, K // splits)
+    return torch.einsum("msk,nsk->smn", xs, ws).contiguous()
+
+
+def add_rmsnorm_splitk(P, residual, w, eps: float):
+    """residual <- residual + bf16(sum_s P[s]); returns rmsnorm(residual) * w."""
+    if _gpu(P):
+        return _native().add_rmsnorm_splitk(P, residual, w, eps)
+    return ref.add_rmsnorm(P.sum(0).to(residual.dtype).view_as(residual), residual, w, eps)
+
+
+def rope_cache_splitk(P, positions, cos_sin, slot_mapping, k_cache, v_cache, Hq, Hkv, D):
+    """Packed bf16 QKV <- rope(bf16(sum_s P[s])) with the paged-cache write (rope_cache)."""
+    if _gpu(P):
+        if slot_mapping is None:
+            k_cache = v_cache = P
+        return _native().rope_cache_splitk(P, positions, cos_sin, slot_mapping, k_cache, v_cache, Hq, Hkv, D)
+    qkv = P.sum(0).to(torch.bfloat16)
+    ref.rope_cache(qkv, positions, cos_sin, slot_mapping, k_cache, v_cache, Hq, Hkv, D)
+    return qkv
+
+
 # ----------------------------------------------------------------------------- embeddings
 def embedding(ids, table):
     if _gpu(table):

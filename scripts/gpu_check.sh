@@ -4,11 +4,14 @@
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
 mkdir -p gpurun_out
 export HSA_ENABLE_IPC_MODE_LEGACY=0
-ok() { local rc=$1; [ $rc -eq 0 ] || [ $rc -eq 1 ]; }
 timeout -k 10 400 python -c "from __graft_entry__ import build; build()" > gpurun_out/build.log 2>&1 || exit 3
 if [ "$SKIP_PYTEST" != "1" ]; then
   timeout -k 10 900 python -m pytest tests -m gpu -q ${PYTEST_ARGS} > gpurun_out/pytest_gpu.log 2>&1
-  rc=$?; echo "pytest rc=$rc"; ok $rc || exit $rc
+  rc=$?; echo "pytest rc=$rc"; [ $rc -eq 0 ] || exit $rc
+fi
+if [ -n "$KBENCH_ARGS" ]; then
+  timeout -k 10 600 python benchmarks/bench_kernels.py $KBENCH_ARGS > gpurun_out/kbench.log 2>&1
+  rc=$?; echo "kbench rc=$rc"; [ $rc -eq 0 ] || exit $rc
 fi
 if [ -n "$PROBE_ARGS" ]; then
   timeout -k 10 600 python scripts/gen_probe.py $PROBE_ARGS > gpurun_out/gen_probe.log 2>&1

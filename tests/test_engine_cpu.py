@@ -91,3 +91,27 @@ def test_sampling_reference_topk1_is_greedy():
     x = torch.randn(4, 50)
     out = R.sample(x, torch.ones(4), torch.ones(4, dtype=torch.int32), torch.ones(4), torch.rand(4))
     assert torch.equal(out, x.argmax(-1))
+
+
+def test_splitk_reference_ops_cpu():
+    """CPU references of the fused split-K decode path: partial slabs sum to x @ w^T and
+    the consumers see bf16(sum) exactly like the unfused projection."""
+    import torch
+
+    from docqa_amd import ops
+    from docqa_amd.ops import reference as R
+
+    torch.manual_seed(0)
+    x = torch.randn(5, 1024).bfloat16()
+    w = torch.randn(256, 1024).bfloat16()
+    P = ops.dgemm_partial(x, w, 4)
+    assert P.shape == (4, 5, 256)
+    assert torch.allclose(P.sum(0), x.float() @ w.float().T, atol=1e-3, rtol=1e-4)
+    assert ops.decode_splits(64, 6144, 4096) == 2 and ops.decode_splits(64, 4096, 14336) == 4
+    assert ops.decode_splits(64, 28672, 4096) == 0 and ops.decode_splits(64, 128256, 4096) == 0
+    r1 = torch.randn(5, 256).bfloat16()
+    r2 = r1.clone()
+    g = torch.ones(256).bfloat16()
+    o1 = ops.add_rmsnorm_splitk(P, r1, g, 1e-5)
+    o2 = R.add_rmsnorm(P.sum(0).bfloat16(), r2, g, 1e-5)
+    assert torch.equal(r1, r2) and torch.equal(o1, o2)

@@ -225,6 +225,66 @@ def test_gemm_asymmetric_identity(native):
     assert torch.equal(o[:64, :], w.float()[:, :64].T[:64, :])
 
 
+@pytest.mark.parametrize("M", [1, 5, 16, 31, 64])
+@pytest.mark.parametrize("N,K,S", [(6144, 4096, 0), (4096, 4096, 0), (4096, 14336, 0), (28672, 4096, 0),
+                                   (512, 1024, 1), (512, 1024, 2), (640, 3584, 7)])
+def test_dgemm(native, M, N, K, S):
+    """Skinny decode projection (split-K / direct) vs the fp32 reference."""
+    x = torch.randn(M, K, device="cuda", dtype=torch.bfloat16)
+    w = (torch.randn(N, K, device="cuda") / K ** 0.5).bfloat16()
+    o2 = (x.float() @ w.float().T)
+    for _ in range(3):   # a ring-pipeline race shows up intermittently, not on every call
+        o1 = torch.ops.docqa.dgemm(x, w, S)
+        _close(o1, o2, 2e-2, 1e-2)
+
+
+@pytest.mark.parametrize("S", [1, 4])
+def test_splitk_fused_consumers(native, S):
+    """dgemm_partial + add_rmsnorm_splitk / rope_cache_splitk == reference on bf16(sum P)."""
+    from docqa_amd.ops import reference as R
+
+    M, H = 37, 4096
+    x = torch.randn(M, 4096, device="cuda", dtype=torch.bfloat16)
+    w = (torch.randn(H, 4096, device="cuda") / 64).bfloat16()
+    P = torch.ops.docqa.dgemm_partial(x, w, S)
+    assert P.shape == (S, M, H)
+    _close(P.sum(0), x.float() @ w.float().T, 2e-2, 1e-2)
+    r1 = torch.randn(M, H, device="cuda", dtype=torch.bfloat16)
+    r2 = r1.clone()
+    g = (torch.rand(H, device="cuda") + 0.5).bfloat16()
+    o1 = torch.ops.docqa.add_rmsnorm_splitk(P, r1, g, 1e-5)
+    o2 = R.add_rmsnorm(P.sum(0).bfloat16(), r2, g, 1e-5)
+    _close(r1, r2, 1e-2, 1e-2)
+    _close(o1, o2, 3e-2, 1e-2)
+    # packed QKV: 8 q + 2 k + 2 v heads of 128
+    Hq, Hkv, D, BS, T = 8, 2, 128, 16, M
+    Pq = torch.randn(S, T, (Hq + 2 * Hkv) * D, device="cuda")
+    cs = R.rope_cos_sin(1024, D, 500000.0, "cuda")
+    pos = torch.randint(0, 1000, (T,), device="cuda", dtype=torch.int32)
+    slots = torch.randperm(8 * BS, device="cuda")[:T].int()
+    slots[3] = -1
+    kc1 = torch.zeros(8, Hkv, BS, D, device="cuda", dtype=torch.bfloat16)
+    vc1 = torch.zeros_like(kc1)
+    kc2, vc2 = kc1.clone(), vc1.clone()
+    q1 = torch.ops.docqa.rope_cache_splitk(Pq, pos, cs, slots, kc1, vc1, Hq, Hkv, D)
+    q2 = Pq.sum(0).bfloat16()
+    R.rope_cache(q2, pos, cs, slots, kc2, vc2, Hq, Hkv, D)
+    _close(q1, q2, 2e-2, 1e-2)
+    _close(kc1, kc2, 2e-2, 1e-2)
+    _close(vc1, vc2, 1e-2)
+
+
+def test_dgemm_asymmetric_identity(native):
+    """X = I rows against an asymmetric W: Y must be W's columns, catches transposed writes."""
+    M, N, K = 48, 128, 512
+    x = torch.zeros(M, K, device="cuda", dtype=torch.bfloat16)
+    x[torch.arange(M), torch.arange(M) * 3] = 1
+    w = (torch.arange(N * K, device="cuda").view(N, K) % 97).bfloat16()
+    for S in (1, 0):
+        o = torch.ops.docqa.dgemm(x, w, S).float()
+        assert torch.equal(o, w.float()[:, torch.arange(M, device="cuda") * 3].T)
+
+
 def test_flash_prefill_spike(native):
     """Force the online-softmax rescale branch: one huge key late in the sequence."""
     from docqa_amd.ops import reference as R
