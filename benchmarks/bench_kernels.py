@@ -45,6 +45,14 @@ def bench_dgemm(nat):
             rows.append({"proj": name, "M": M, "N": N, "K": K, "ours_us": round(t_ours, 1),
                          "hipblaslt_us": round(t_lib, 1), "ours_TBps": round(nb / t_ours / 1e6, 2),
                          "hipblaslt_TBps": round(nb / t_lib / 1e6, 2)})
+        if name == "gate_up":   # fused SwiGLU decode GEMM vs hipBLASLt + silu_mul kernel
+            for M in (1, 16, 32, 64):
+                x = torch.randn(M, K, device="cuda", dtype=torch.bfloat16)
+                it = iter(range(1 << 30))
+                t_ours = timeit(lambda: nat.dgemm_glu(x, ws[next(it) % copies]), iters=4 * copies)
+                t_lib = timeit(lambda: nat.silu_mul(F.linear(x, ws[next(it) % copies]), True), iters=4 * copies)
+                rows.append({"proj": "gate_up+swiglu", "M": M, "N": N, "K": K, "ours_us": round(t_ours, 1),
+                             "hipblaslt_plus_silu_us": round(t_lib, 1), "ours_TBps": round(nb / t_ours / 1e6, 2)})
         if "--sweep" in sys.argv and N <= 8192:
             x = torch.randn(64, K, device="cuda", dtype=torch.bfloat16)
             for S in (1, 2, 4, 8, 16):

@@ -122,14 +122,15 @@ at::Tensor rope_cache_splitk(const at::Tensor& P, const at::Tensor& positions, c
   return qkv;
 }
 
-at::Tensor silu_mul(const at::Tensor& gu) {
+at::Tensor silu_mul(const at::Tensor& gu, bool interleaved) {
   CHECK_GPU(gu); CHECK_BF16(gu); CHECK_CONTIG(gu);
   const int I2 = gu.size(-1);
   auto sizes = gu.sizes().vec();
   sizes.back() = I2 / 2;
   c10::DeviceGuard g(gu.device());
   auto out = at::empty(sizes, gu.options());
-  CHECK_RC(docqa_silu_mul(gu.data_ptr(), out.data_ptr(), gu.numel() / I2, I2 / 2, stream()), "silu_mul");
+  CHECK_RC(docqa_silu_mul(gu.data_ptr(), out.data_ptr(), gu.numel() / I2, I2 / 2, interleaved ? 1 : 0,
+                          stream()), "silu_mul");
   return out;
 }
 
@@ -284,6 +285,21 @@ at::Tensor gemm(const at::Tensor& a, const at::Tensor& w, const c10::optional<at
 }
 
 // skinny decode projection Y = X . W^T for M <= 64 rows (splits = 0: auto split-K)
+// decode gate|up projection with fused SwiGLU: x [M, K], w [2I, K] (8-interleaved) -> [M, I]
+at::Tensor dgemm_glu(const at::Tensor& x, const at::Tensor& w) {
+  CHECK_GPU(x); CHECK_BF16(x); CHECK_BF16(w); CHECK_CONTIG(x); CHECK_CONTIG(w);
+  const int K = x.size(-1), N = w.size(0);
+  TORCH_CHECK(w.size(1) == K && N % 16 == 0, "dgemm_glu: shape mismatch");
+  const int M = x.numel() / K;
+  TORCH_CHECK(M <= 64, "dgemm_glu: at most 64 rows");
+  auto sizes = x.sizes().vec();
+  sizes.back() = N / 2;
+  c10::DeviceGuard g(x.device());
+  auto out = at::empty(sizes, x.options());
+  CHECK_RC(docqa_dgemm_glu(x.data_ptr(), w.data_ptr(), out.data_ptr(), M, N, K, stream()), "dgemm_glu");
+  return out;
+}
+
 // split-K partial slabs only: [S, M, N] fp32 (S >= 1), combine fused into the consumer
 at::Tensor dgemm_partial(const at::Tensor& x, const at::Tensor& w, int64_t splits) {
   CHECK_GPU(x); CHECK_BF16(x); CHECK_BF16(w); CHECK_CONTIG(x); CHECK_CONTIG(w);
@@ -405,7 +421,7 @@ TORCH_LIBRARY(docqa, m) {
   m.def("layernorm(Tensor x, Tensor? residual, Tensor gamma, Tensor beta, float eps) -> Tensor");
   m.def("rope_cache(Tensor(a!) qkv, Tensor positions, Tensor cos_sin, Tensor? slot_mapping, "
         "Tensor(b!) k_cache, Tensor(c!) v_cache, int Hq, int Hkv, int D) -> ()");
-  m.def("silu_mul(Tensor gu) -> Tensor");
+  m.def("silu_mul(Tensor gu, bool interleaved=False) -> Tensor");
   m.def("bias_act(Tensor x, Tensor bias, Tensor? residual, bool gelu) -> Tensor");
   m.def("embedding(Tensor ids, Tensor table) -> Tensor");
   m.def("bert_embed_ln(Tensor ids, Tensor pos, Tensor? token_type, Tensor wte, Tensor wpe, "
@@ -427,6 +443,7 @@ TORCH_LIBRARY(docqa, m) {
         "float scale, Tensor k_cache, Tensor v_cache, Tensor block_tables, Tensor ctx_start) -> Tensor");
   m.def("dgemm(Tensor x, Tensor w, int splits) -> Tensor");
   m.def("dgemm_partial(Tensor x, Tensor w, int splits) -> Tensor");
+  m.def("dgemm_glu(Tensor x, Tensor w) -> Tensor");
   m.def("add_rmsnorm_splitk(Tensor P, Tensor(a!) residual, Tensor w, float eps) -> Tensor");
   m.def("rope_cache_splitk(Tensor P, Tensor positions, Tensor cos_sin, Tensor? slot_mapping, "
         "Tensor(b!) k_cache, Tensor(c!) v_cache, int Hq, int Hkv, int D) -> Tensor");
@@ -453,6 +470,7 @@ TORCH_LIBRARY_IMPL(docqa, CUDA, m) {
   m.impl("flash_prefill_paged", &flash_prefill_paged);
   m.impl("dgemm", &dgemm);
   m.impl("dgemm_partial", &dgemm_partial);
+  m.impl("dgemm_glu", &dgemm_glu);
   m.impl("add_rmsnorm_splitk", &add_rmsnorm_splitk);
   m.impl("rope_cache_splitk", &rope_cache_splitk);
 }

@@ -17,7 +17,7 @@ int docqa_rope_cache(void* qkv, const int* positions, const float* cos_sin,
                      const int* slot_mapping, void* k_cache, void* v_cache, int T, int Hq,
                      int Hkv, int D, int row_stride, int BS, hipStream_t s);
 
-int docqa_silu_mul(const void* gu, void* out, int T, int I, hipStream_t s);
+int docqa_silu_mul(const void* gu, void* out, int T, int I, int interleaved, hipStream_t s);
 int docqa_bias_act(const void* x, const void* bias, const void* res, void* out, int T, int N,
                    int gelu, hipStream_t s);
 
@@ -56,6 +56,7 @@ int docqa_rope_cache_splitk(const float* P, int S, void* qkv_out, const int* pos
                             void* v_cache, int T, int Hq, int Hkv, int D, int row_stride, int BS,
                             hipStream_t s);
 int docqa_dgemm_splits(int N, int K);
+int docqa_dgemm_glu(const void* X, const void* W, void* Y, int M, int N, int K, hipStream_t s);
 int docqa_dgemm(const void* X, const void* W, void* Y, float* partial, int M, int N, int K, int S,
                 hipStream_t s);
 int docqa_gemm(const void* A, const void* W, const void* bias, const void* res, void* C, int M,

@@ -14,6 +14,9 @@ using namespace docqa;
 __device__ __forceinline__ float silu(float x) { return x / (1.f + __expf(-x)); }
 __device__ __forceinline__ float gelu_erf(float x) { return 0.5f * x * (1.f + erff(x * 0.70710678118654752f)); }
 
+// IL: gate|up rows interleaved in blocks of 8 (the layout the decode GEMM's fused SwiGLU
+// epilogue reads): output chunk c = silu(chunk 2c) * chunk 2c+1 of the row.
+template <bool IL>
 __global__ __launch_bounds__(256) void silu_mul_kernel(const uint16_t* __restrict__ gu,
                                                        uint16_t* __restrict__ out, int T, int I) {
   // 32-bit index math (T * I / 8 < 2^31 is checked by the launcher): 64-bit integer
@@ -26,8 +29,8 @@ __global__ __launch_bounds__(256) void silu_mul_kernel(const uint16_t* __restric
     const int c = idx - t * cpr;
     const uint4* row = reinterpret_cast<const uint4*>(gu + t * (size_t)(2 * I));
     float g[8], u[8], o[8];
-    unpack8(row[c], g);
-    unpack8(row[cpr + c], u);
+    unpack8(row[IL ? 2 * c : c], g);
+    unpack8(row[IL ? 2 * c + 1 : cpr + c], u);
 #pragma unroll
     for (int j = 0; j < 8; ++j) o[j] = silu(g[j]) * u[j];
     reinterpret_cast<uint4*>(out + t * (size_t)I)[c] = pack8(o);
@@ -64,11 +67,15 @@ static inline int grid_for(size_t work) {
   return (int)(g > 2048 ? 2048 : (g == 0 ? 1 : g));
 }
 
-int docqa_silu_mul(const void* gu, void* out, int T, int I, hipStream_t s) {
+int docqa_silu_mul(const void* gu, void* out, int T, int I, int interleaved, hipStream_t s) {
   if (I % 8 != 0 || (long long)T * (I / 8) >= (1LL << 31)) return -1;
   if (T == 0) return 0;
-  silu_mul_kernel<<<grid_for((size_t)T * (I / 8)), 256, 0, s>>>((const uint16_t*)gu,
-                                                                (uint16_t*)out, T, I);
+  if (interleaved)
+    silu_mul_kernel<true><<<grid_for((size_t)T * (I / 8)), 256, 0, s>>>((const uint16_t*)gu,
+                                                                       (uint16_t*)out, T, I);
+  else
+    silu_mul_kernel<false><<<grid_for((size_t)T * (I / 8)), 256, 0, s>>>((const uint16_t*)gu,
+                                                                        (uint16_t*)out, T, I);
   DOCQA_CHECK_LAUNCH();
   return 0;
 }

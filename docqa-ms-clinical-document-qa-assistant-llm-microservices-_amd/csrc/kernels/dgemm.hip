@@ -16,7 +16,14 @@
 //   * split-K over the grid's y dimension gives >= 256 workgroups for the narrow
 //     projections (O: N=4096); slices write fp32 partials reduced by a tiny second kernel,
 //     S = 1 writes bf16 directly (gate|up, LM head).
-// Shapes: N % 64 == 0, (K / S) % 512 == 0 (whole 4-stage ring turns), M <= 64.
+//   * EPI_GLU: the Llama gate|up projection with SwiGLU fused into the epilogue.  The
+//     weight rows are interleaved in blocks of 8 (gate 8b..8b+7, then up 8b..8b+7), so one
+//     16-wide MFMA n-tile holds matching gate and up columns 8 lanes apart: a DPP row
+//     rotate by 8 pairs them and silu(g) * u is written directly -- no [M, 2I] round trip
+//     and no separate silu_mul launch.  7 n-tiles per workgroup (112 rows) make the Llama-3-8B
+//     shape exactly 256 workgroups = one per CU, and halve the L2 traffic of re-reading X
+//     per workgroup (at M = 64 that X traffic, not HBM, was the limiter).
+// Shapes: N % (16 NT) == 0, (K / S) % 512 == 0 (whole 4-stage ring turns), M <= 64.
 #include "docqa_common.h"
 
 using namespace docqa;
@@ -24,7 +31,7 @@ using namespace docqa;
 namespace {
 constexpr int BN = 64, BKD = 128, NS = 4, MR = 64;
 constexpr int KSTEPS = BKD / 32;               // 16x16x32 k-steps per stage
-constexpr int STAGE = BN * BKD;                // elements of one W stage (16 KB)
+enum { EPI_BF16 = 0, EPI_PARTIAL = 1, EPI_GLU = 2 };
 typedef __attribute__((address_space(3))) void lds_void;
 
 // All vector-memory traffic of the main loop is inline asm, so hipcc's waitcnt pass sees
@@ -71,22 +78,31 @@ __device__ __forceinline__ void keep_live(bf16x8 (&x)[SPW]) {
   for (int s = 0; s < SPW; ++s) asm volatile("" : "+v"(x[s]));
 }
 
-__device__ __forceinline__ int w_off(int row, int ch) {  // [64][128] stage, 16 chunks per row
+__device__ __forceinline__ int w_off(int row, int ch) {  // [rows][128] stage, 16 chunks per row
   return row * BKD + ((ch ^ (row & 15)) << 3);
+}
+
+__device__ __forceinline__ float silu_f(float x) { return x / (1.f + __expf(-x)); }
+
+// value of the lane 8 positions away inside each 16-lane row (DPP row_ror:8)
+__device__ __forceinline__ float row_swap8(float v) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x128, 0xf, 0xf, false));
 }
 
 // Wave roles: MT m-tiles of 16 X rows; the 4 waves split as (m-tile = wave % MT,
 // k-group = wave / MT) so every wave owns a disjoint (rows x k) piece of the product and
-// the W stage in LDS is shared by all of them.  KW = 4 / MT k-groups are summed at the end.
-template <bool SPLIT, int MT>
+// the W stage in LDS (NT 16-row n-tiles) is shared by all of them.  KW = 4 / MT k-groups
+// are summed through LDS at the end.
+template <int EPI, int MT, int NT>
 __global__ __launch_bounds__(256) void dgemm_kernel(const uint16_t* __restrict__ X,
                                                     const uint16_t* __restrict__ W,
                                                     uint16_t* __restrict__ Y,
                                                     float* __restrict__ P, int M, int N, int K,
                                                     int Ks) {
   constexpr int KW = 4 / MT, SPW = KSTEPS / KW;
-  __shared__ __attribute__((aligned(16))) uint16_t sw[NS * STAGE];   // 64 KB W ring
-  const int n0 = blockIdx.x * BN;
+  constexpr int STAGE = NT * 16 * BKD;         // elements of one W stage (NT x 4 KB)
+  __shared__ __attribute__((aligned(16))) uint16_t sw[NS * STAGE];   // W ring
+  const int n0 = blockIdx.x * NT * 16;
   const int slice = blockIdx.y;
   const int kbeg = slice * Ks;
   const int nkb = Ks / BKD;
@@ -98,19 +114,19 @@ __global__ __launch_bounds__(256) void dgemm_kernel(const uint16_t* __restrict__
   const uint16_t* xrow = X + (size_t)xr * K + kbeg + kg * SPW * 32 + fq * 8;
   const uint32_t ring = lds_u32(sw);
 
-  f32x4 acc[4];
+  f32x4 acc[NT];
 #pragma unroll
-  for (int i = 0; i < 4; ++i) acc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+  for (int i = 0; i < NT; ++i) acc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  // W stage j -> ring slot j % NS: 16 wave-instructions of 64 lanes x 16 B, 4 per wave,
+  // W stage j -> ring slot j % NS: 4 NT wave-instructions of 64 lanes x 16 B, NT per wave,
   // source XOR-swizzled (the DMA destination is lane-linear).  Past the last stage the
   // sources are clamped (L2 hits into free slots / dead X buffers) so that every step
   // issues the same loads unconditionally: a load whose destination is live on one path
   // and not on another lets hipcc hand its registers to other values while the data is
   // still in flight.
-  const uint16_t* wsrc[4];
+  const uint16_t* wsrc[NT];
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
+  for (int i = 0; i < NT; ++i) {
     const int p = (i * 4 + wave) * 64 + lane;
     const int r = p >> 4;
     wsrc[i] = W + (size_t)(n0 + r) * K + kbeg + (((p & 15) ^ (r & 15)) << 3);
@@ -119,7 +135,7 @@ __global__ __launch_bounds__(256) void dgemm_kernel(const uint16_t* __restrict__
     const int koff = min(j, nkb - 1) * BKD;
     const uint32_t dst = ring + (uint32_t)((j % NS) * STAGE * 2);
 #pragma unroll
-    for (int i = 0; i < 4; ++i) glds16(wsrc[i] + koff, dst + (uint32_t)((i * 4 + wave) * 1024));
+    for (int i = 0; i < NT; ++i) glds16(wsrc[i] + koff, dst + (uint32_t)((i * 4 + wave) * 1024));
   };
   auto load_x = [&](bf16x8 (&x)[SPW], int j) {
     const uint16_t* src = xrow + min(j, nkb - 1) * BKD;
@@ -134,15 +150,15 @@ __global__ __launch_bounds__(256) void dgemm_kernel(const uint16_t* __restrict__
       const bf16x8 a = x[s];
       const int ch = (kg * SPW + s) * 4 + fq;
 #pragma unroll
-      for (int nt = 0; nt < 4; ++nt) {
+      for (int nt = 0; nt < NT; ++nt) {
         const bf16x8 b = *reinterpret_cast<const bf16x8*>(src + w_off(nt * 16 + fr, ch));
         acc[nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, acc[nt], 0, 0, 0);
       }
     }
   };
   // Issue order per wave: W0 X0 W1 X1 W2 | step i: X(i+2) W(i+3).  At the top of step i
-  // the ops issued after X(i) are W(i+1), X(i+1), W(i+2), so vmcnt(8 + SPW) retires X(i)
-  // and (issued before it) W(i) while two W stages stay in flight; the barrier then
+  // the ops issued after X(i) are W(i+1), X(i+1), W(i+2), so vmcnt(2 NT + SPW) retires
+  // X(i) and (issued before it) W(i) while two W stages stay in flight; the barrier then
   // publishes stage i to every wave and frees slot (i-1) % NS for W(i+3).
   bf16x8 x0[SPW], x1[SPW], x2[SPW], x3[SPW];
   stage_w(0);
@@ -151,7 +167,7 @@ __global__ __launch_bounds__(256) void dgemm_kernel(const uint16_t* __restrict__
   load_x(x1, 1);
   stage_w(2);
 #define RING_STEP(I, XC, XN)                                                            \
-  wait_vm_n<8 + SPW>(XC);                                                               \
+  wait_vm_n<2 * NT + SPW>(XC);                                                          \
   ring_barrier();                                                                       \
   load_x(XN, (I) + 2);                                                                  \
   stage_w((I) + 3);                                                                     \
@@ -173,36 +189,53 @@ __global__ __launch_bounds__(256) void dgemm_kernel(const uint16_t* __restrict__
   keep_live(x3);
 
   // C/D map of 16x16x32: col = lane & 15 (weight row), row = 4 * (lane >> 4) + r (X row)
+  auto store = [&](int row, int col, float v) {
+    if constexpr (EPI == EPI_PARTIAL) P[((size_t)slice * M + row) * N + col] = v;
+    else Y[(size_t)row * N + col] = f2bf(v);
+  };
+  // SwiGLU pair: gate value at an 8-block's low half, up value 8 columns later
+  auto store_glu = [&](int row, int col, float g, float u) {
+    const float gb = bf2f(f2bf(g)), ub = bf2f(f2bf(u));   // as the unfused bf16 GEMM output
+    Y[(size_t)row * (N >> 1) + ((col >> 4) << 3) + (col & 7)] = f2bf(silu_f(gb) * ub);
+  };
   if constexpr (KW == 1) {
 #pragma unroll
-    for (int nt = 0; nt < 4; ++nt)
+    for (int nt = 0; nt < NT; ++nt)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int row = mt * 16 + fq * 4 + r, col = n0 + nt * 16 + fr;
-        if (row < M) {
-          if constexpr (SPLIT) P[((size_t)slice * M + row) * N + col] = acc[nt][r];
-          else Y[(size_t)row * N + col] = f2bf(acc[nt][r]);
+        if constexpr (EPI == EPI_GLU) {
+          const float u = row_swap8(acc[nt][r]);
+          if (row < M && (fr & 8) == 0) store_glu(row, col, acc[nt][r], u);
+        } else if (row < M) {
+          store(row, col, acc[nt][r]);
         }
       }
   } else {
     // sum the KW k-groups through LDS (ring is free after the last barrier + wait)
     __syncthreads();
-    f32x4* red = reinterpret_cast<f32x4*>(sw);   // 16 KB = one slot        // [wave][nt][lane]
+    f32x4* red = reinterpret_cast<f32x4*>(sw);        // [wave][nt][lane] = one slot
 #pragma unroll
-    for (int nt = 0; nt < 4; ++nt) red[(wave * 4 + nt) * 64 + lane] = acc[nt];
+    for (int nt = 0; nt < NT; ++nt) red[(wave * NT + nt) * 64 + lane] = acc[nt];
     __syncthreads();
     const float* rf = reinterpret_cast<const float*>(sw);
-#pragma unroll
-    for (int e = 0; e < MT * 4; ++e) {
-      const int idx = e * 256 + tid;                 // (m-tile, nt, lane, r)
-      const int r = idx & 3, ln = (idx >> 2) & 63, nt = (idx >> 8) & 3, m = idx >> 10;
+    auto sum_k = [&](int m, int nt, int ln, int r) {
       float v = 0.f;
 #pragma unroll
-      for (int g = 0; g < KW; ++g) v += rf[(((g * MT + m) * 4 + nt) * 64 + ln) * 4 + r];
+      for (int g = 0; g < KW; ++g) v += rf[(((g * MT + m) * NT + nt) * 64 + ln) * 4 + r];
+      return v;
+    };
+#pragma unroll
+    for (int e = 0; e < MT * NT; ++e) {
+      const int idx = e * 256 + tid;                 // (m-tile, nt, lane, r)
+      const int r = idx & 3, ln = (idx >> 2) & 63, q = idx >> 8;
+      const int nt = q % NT, m = q / NT;
       const int row = m * 16 + (ln >> 4) * 4 + r, col = n0 + nt * 16 + (ln & 15);
-      if (row < M) {
-        if constexpr (SPLIT) P[((size_t)slice * M + row) * N + col] = v;
-        else Y[(size_t)row * N + col] = f2bf(v);
+      if (row >= M) continue;
+      if constexpr (EPI == EPI_GLU) {
+        if ((ln & 8) == 0) store_glu(row, col, sum_k(m, nt, ln, r), sum_k(m, nt, ln + 8, r));
+      } else {
+        store(row, col, sum_k(m, nt, ln, r));
       }
     }
   }
@@ -224,7 +257,7 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* __restr
 }
 }  // namespace
 
-// split count: enough workgroups for the chip (>= 256), K slices of whole k-blocks
+// split count: enough workgroups for the chip (>= 256), K slices of whole ring turns
 int docqa_dgemm_splits(int N, int K) {
   const int tiles = N / BN;
   int s = 1;
@@ -233,21 +266,30 @@ int docqa_dgemm_splits(int N, int K) {
   return s;
 }
 
+template <int EPI, int NT>
+static void launch_mt(int mt, dim3 grid, hipStream_t s, const uint16_t* x, const uint16_t* w,
+                      uint16_t* y, float* p, int M, int N, int K, int Ks) {
+  if (mt == 1) dgemm_kernel<EPI, 1, NT><<<grid, 256, 0, s>>>(x, w, y, p, M, N, K, Ks);
+  else if (mt == 2) dgemm_kernel<EPI, 2, NT><<<grid, 256, 0, s>>>(x, w, y, p, M, N, K, Ks);
+  else dgemm_kernel<EPI, 4, NT><<<grid, 256, 0, s>>>(x, w, y, p, M, N, K, Ks);
+}
+
+static bool shape_ok(int M, int N, int K, int S, int bn) {
+  return M <= MR && N % bn == 0 && S >= 1 && K % S == 0 && (K / S) % (NS * BKD) == 0;
+}
+
 int docqa_dgemm(const void* X, const void* W, void* Y, float* partial, int M, int N, int K,
                 int S, hipStream_t s) {
   if (M == 0) return 0;
-  if (M > MR || N % BN != 0 || K % S != 0 || (K / S) % (NS * BKD) != 0) return -1;
+  if (!shape_ok(M, N, K, S, BN) || (S > 1 && !partial)) return -1;
   dim3 grid(N / BN, S);
   const int mt = (M + 15) / 16;
   const uint16_t* x = (const uint16_t*)X;
   const uint16_t* w = (const uint16_t*)W;
-  if (S > 1 && !partial) return -1;
-#define DG(MTV)                                                                                 \
-  if (S == 1) dgemm_kernel<false, MTV><<<grid, 256, 0, s>>>(x, w, (uint16_t*)Y, nullptr, M, N, K, K); \
-  else dgemm_kernel<true, MTV><<<grid, 256, 0, s>>>(x, w, nullptr, partial, M, N, K, K / S);
-  if (mt == 1) { DG(1) } else if (mt == 2) { DG(2) } else { DG(4) }
-#undef DG
-  if (S > 1) {
+  if (S == 1) {
+    launch_mt<EPI_BF16, 4>(mt, grid, s, x, w, (uint16_t*)Y, nullptr, M, N, K, K);
+  } else {
+    launch_mt<EPI_PARTIAL, 4>(mt, grid, s, x, w, nullptr, partial, M, N, K, K / S);
     const int MN = M * N;  // multiple of 4 (N % 64 == 0)
     splitk_reduce_kernel<<<(MN / 4 + 255) / 256, 256, 0, s>>>(partial, (uint16_t*)Y, MN, S);
   }
@@ -260,14 +302,26 @@ int docqa_dgemm(const void* X, const void* W, void* Y, float* partial, int M, in
 int docqa_dgemm_partial(const void* X, const void* W, float* P, int M, int N, int K, int S,
                         hipStream_t s) {
   if (M == 0) return 0;
-  if (M > MR || N % BN != 0 || S < 1 || K % S != 0 || (K / S) % (NS * BKD) != 0 || !P) return -1;
-  dim3 grid(N / BN, S);
+  if (!shape_ok(M, N, K, S, BN) || !P) return -1;
+  launch_mt<EPI_PARTIAL, 4>((M + 15) / 16, dim3(N / BN, S), s, (const uint16_t*)X,
+                            (const uint16_t*)W, nullptr, P, M, N, K, K / S);
+  DOCQA_CHECK_LAUNCH();
+  return 0;
+}
+
+// Y[M, N/2] = silu(gate) * up for the 8-interleaved gate|up weight W [N, K] (N = 2 I)
+int docqa_dgemm_glu(const void* X, const void* W, void* Y, int M, int N, int K, hipStream_t s) {
+  if (M == 0) return 0;
   const int mt = (M + 15) / 16;
   const uint16_t* x = (const uint16_t*)X;
   const uint16_t* w = (const uint16_t*)W;
-  if (mt == 1) dgemm_kernel<true, 1><<<grid, 256, 0, s>>>(x, w, nullptr, P, M, N, K, K / S);
-  else if (mt == 2) dgemm_kernel<true, 2><<<grid, 256, 0, s>>>(x, w, nullptr, P, M, N, K, K / S);
-  else dgemm_kernel<true, 4><<<grid, 256, 0, s>>>(x, w, nullptr, P, M, N, K, K / S);
+  if (shape_ok(M, N, K, 1, 112) && N / 112 >= 192) {
+    launch_mt<EPI_GLU, 7>(mt, dim3(N / 112), s, x, w, (uint16_t*)Y, nullptr, M, N, K, K);
+  } else if (shape_ok(M, N, K, 1, 64)) {
+    launch_mt<EPI_GLU, 4>(mt, dim3(N / 64), s, x, w, (uint16_t*)Y, nullptr, M, N, K, K);
+  } else {
+    return -1;
+  }
   DOCQA_CHECK_LAUNCH();
   return 0;
 }

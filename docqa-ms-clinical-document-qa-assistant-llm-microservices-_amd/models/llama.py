@@ -166,7 +166,9 @@ class LlamaModel:
                                   v.reshape(-1, cfg.hidden)]).contiguous(),
                 "o": o.contiguous(),
                 "post_norm": get(p + "post_attention_layernorm.weight"),
-                "gate_up": torch.cat([gt, up]).contiguous(),
+                # rows interleaved in blocks of 8 (gate, up): the decode GEMM's fused SwiGLU
+                # epilogue pairs them inside one MFMA tile (csrc/kernels/dgemm.hip)
+                "gate_up": ops.glu_interleave(gt, up).contiguous(),
                 "down": dn.contiguous(),
             })
 
@@ -180,7 +182,7 @@ class LlamaModel:
         for i, L in enumerate(self.layers):
             p = f"model.layers.{i}."
             q, k, v = L["qkv"].split([self.hq * D, self.hkv * D, self.hkv * D])
-            g, u = L["gate_up"].split([self.inter, self.inter])
+            g, u = ops.glu_split(L["gate_up"])
             sd.update({p + "self_attn.q_proj.weight": q, p + "self_attn.k_proj.weight": k,
                        p + "self_attn.v_proj.weight": v, p + "self_attn.o_proj.weight": L["o"],
                        p + "mlp.gate_proj.weight": g, p + "mlp.up_proj.weight": u,
@@ -240,7 +242,10 @@ class LlamaModel:
             else:
                 o = comm.tp_all_reduce(lin(a, L["o"]))
                 x = ops.add_rmsnorm(o, residual, L["post_norm"], eps)
-            g = ops.silu_mul(lin(x, L["gate_up"]))
+            if decode:
+                g = ops.glu_linear(x, L["gate_up"])
+            else:
+                g = ops.silu_mul(F.linear(x, L["gate_up"]), interleaved=True)
             nxt = self.layers[i + 1]["in_norm"] if i + 1 < nl else self.final_norm
             if sd:
                 x = ops.add_rmsnorm_splitk(ops.dgemm_partial(g, L["down"], sd), residual, nxt, eps)

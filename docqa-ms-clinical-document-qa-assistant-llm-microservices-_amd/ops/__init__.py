@@ -115,10 +115,23 @@ rope_cos_sin = ref.rope_cos_sin
 
 
 # ----------------------------------------------------------------------------- activations
-def silu_mul(gu):
+def silu_mul(gu, interleaved: bool = False):
     if _gpu(gu):
-        return _native().silu_mul(gu.contiguous())
-    return ref.silu_mul(gu)
+        return _native().silu_mul(gu.contiguous(), interleaved)
+    return ref.silu_mul(gu, interleaved)
+
+
+glu_interleave, glu_split = ref.glu_interleave, ref.glu_split
+
+
+def glu_linear(x, w_il):
+    """silu(x Wg^T) * (x Wu^T) for 8-interleaved gate|up weights: the fused SwiGLU decode
+    GEMM for <= 64 rows, else hipBLASLt + the interleaved silu_mul kernel."""
+    if _gpu(x):
+        N, K = w_il.shape
+        if x.numel() // K <= 64 and N % 64 == 0 and K % 512 == 0:
+            return _native().dgemm_glu(x.contiguous(), w_il)
+    return silu_mul(torch.nn.functional.linear(x, w_il), interleaved=True)
 
 
 def bias_act(x, bias, residual=None, gelu: bool = False):

@@ -66,9 +66,26 @@ def rope_cache(qkv, positions, cos_sin, slot_mapping, k_cache, v_cache, Hq, Hkv,
         v_cache[blk, :, off] = v
 
 
-def silu_mul(gu):
-    g, u = gu.float().chunk(2, dim=-1)
+def silu_mul(gu, interleaved: bool = False):
+    """SwiGLU; ``interleaved``: gate|up rows in blocks of 8 (glu_interleave layout)."""
+    if interleaved:
+        v = gu.float().unflatten(-1, (-1, 2, 8))
+        g, u = v[..., 0, :].flatten(-2), v[..., 1, :].flatten(-2)
+    else:
+        g, u = gu.float().chunk(2, dim=-1)
     return (F.silu(g) * u).to(gu.dtype)
+
+
+def glu_interleave(gate, up):
+    """[I, K] gate and up -> [2I, K] with rows in blocks of 8: g0..g7 u0..u7 g8..g15 ..."""
+    I, K = gate.shape
+    return torch.stack([gate.view(I // 8, 8, K), up.view(I // 8, 8, K)], 1).reshape(2 * I, K)
+
+
+def glu_split(gu):
+    """Inverse of :func:`glu_interleave`."""
+    v = gu.view(-1, 2, 8, gu.shape[-1])
+    return v[:, 0].reshape(-1, gu.shape[-1]), v[:, 1].reshape(-1, gu.shape[-1])
 
 
 def bias_act(x, bias, residual, gelu):

@@ -115,3 +115,19 @@ def test_splitk_reference_ops_cpu():
     o1 = ops.add_rmsnorm_splitk(P, r1, g, 1e-5)
     o2 = R.add_rmsnorm(P.sum(0).bfloat16(), r2, g, 1e-5)
     assert torch.equal(r1, r2) and torch.equal(o1, o2)
+
+
+def test_glu_interleave_roundtrip_cpu():
+    import torch
+
+    from docqa_amd.ops import reference as R
+
+    g, u = torch.randn(32, 24), torch.randn(32, 24)
+    il = R.glu_interleave(g, u)
+    assert torch.equal(il[:8], g[:8]) and torch.equal(il[8:16], u[:8]) and torch.equal(il[16:24], g[8:16])
+    g2, u2 = R.glu_split(il)
+    assert torch.equal(g, g2) and torch.equal(u, u2)
+    x = torch.randn(3, 24)
+    a = R.silu_mul(torch.cat([x @ g.T, x @ u.T], -1))
+    b = R.silu_mul(x @ il.T, interleaved=True)
+    assert torch.allclose(a, b, atol=1e-5)

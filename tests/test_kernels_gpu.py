@@ -274,6 +274,22 @@ def test_splitk_fused_consumers(native, S):
     _close(vc1, vc2, 1e-2)
 
 
+@pytest.mark.parametrize("M", [1, 16, 33, 64])
+@pytest.mark.parametrize("N,K", [(28672, 4096), (1024, 512)])
+def test_dgemm_glu(native, M, N, K):
+    """Fused SwiGLU decode GEMM (8-interleaved gate|up) vs fp32 GEMM + reference SwiGLU."""
+    from docqa_amd.ops import reference as R
+
+    x = torch.randn(M, K, device="cuda", dtype=torch.bfloat16)
+    w = (torch.randn(N, K, device="cuda") / K ** 0.5).bfloat16()
+    ref = R.silu_mul((x.float() @ w.float().T).bfloat16(), interleaved=True)
+    for _ in range(3):
+        _close(torch.ops.docqa.dgemm_glu(x, w), ref, 2e-2, 1e-2)
+    # interleaved silu_mul kernel (prefill path) on the same GEMM output
+    gu = (x.float() @ w.float().T).bfloat16()
+    _close(native.silu_mul(gu, interleaved=True), R.silu_mul(gu, interleaved=True), 2e-2, 1e-2)
+
+
 def test_dgemm_asymmetric_identity(native):
     """X = I rows against an asymmetric W: Y must be W's columns, catches transposed writes."""
     M, N, K = 48, 128, 512
