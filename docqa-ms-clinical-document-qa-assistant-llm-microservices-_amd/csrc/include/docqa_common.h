@@ -55,12 +55,28 @@ __device__ __forceinline__ float wave_max(float v) {
   for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
   return v;
 }
-// reduction over an aligned group of `W` lanes (W power of two <= 64)
+// value of the lane `N` positions up inside its 16-lane DPP row (row_ror:N), no LDS trip
+template <int N>
+__device__ __forceinline__ float row_ror(float v) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x120 + N, 0xf, 0xf, false));
+}
+
+// reduction over an aligned group of `W` lanes (W power of two <= 64).  W <= 16 stays in
+// the DPP row (rotations by W/2 .. 1 leave every lane with the group sum) instead of
+// ds_bpermute round trips through the LDS crossbar.
 template <int W>
 __device__ __forceinline__ float group_sum(float v) {
+  if constexpr (W == 16) {
+    v += row_ror<8>(v);
+    v += row_ror<4>(v);
+    v += row_ror<2>(v);
+    v += row_ror<1>(v);
+    return v;
+  } else {
 #pragma unroll
-  for (int o = W / 2; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-  return v;
+    for (int o = W / 2; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
+  }
 }
 template <int W>
 __device__ __forceinline__ float group_max(float v) {

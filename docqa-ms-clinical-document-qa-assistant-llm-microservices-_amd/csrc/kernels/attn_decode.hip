@@ -249,10 +249,19 @@ int docqa_paged_decode(const void* q, int q_stride, const void* k_cache, const v
   paged_decode_kernel<GG, 128, UU><<<grid, 256, 0, s>>>(                                    \
       (const uint16_t*)q, q_stride, (const uint16_t*)k_cache, (const uint16_t*)v_cache,     \
       block_tables, maxb, context_lens, tmp_out, tmp_ml, Hkv, BS, log2BS, max_parts, scale)
+  // tokens in flight per lane group per buffer (U): DOCQA_DECODE_U overrides (tuning knob)
+  static const int u_env = [] {
+    const char* e = getenv("DOCQA_DECODE_U");
+    return e ? atoi(e) : 0;
+  }();
   switch (G) {
     case 1: DEC(1, 4); break;
     case 2: DEC(2, 4); break;
-    case 4: DEC(4, 2); break;
+    case 4:  // U = 4 measured best on HBM-resident caches (benchmarks/bench_decode_attn.py)
+      if (u_env == 2) DEC(4, 2);
+      else if (u_env == 1) DEC(4, 1);
+      else DEC(4, 4);
+      break;
     case 8: DEC(8, 1); break;
     default: return -1;
   }
