@@ -103,7 +103,17 @@ class LLMEngine:
         """Prefill prompt tokens [cached[i], len) of each prompt (the first cached[i]
         tokens are prefix-cache hits already in the paged KV cache)."""
         dev, BS = self.device, self.block_size
-        cached = cached or [0] * len(prompts)
+        cached = list(cached or [0] * len(prompts))
+        # chunked prefill: a prompt longer than the token budget is fed in budget-sized
+        # pieces; each piece attends to the earlier ones through the paged cache (the
+        # prefix-cache attention path), so activation memory stays bounded for the long
+        # multi-patient synthese prompts (SURVEY.md §5.7)
+        budget = max(BS, self.max_prefill_tokens // BS * BS)
+        for k, (p, tb) in enumerate(zip(prompts, tables)):
+            while len(p) - cached[k] > budget:
+                end = cached[k] + budget
+                self._prefill([p[:end]], [tb], [cached[k]])
+                cached[k] = end
         firsts = []
         i = 0
         while i < len(prompts):

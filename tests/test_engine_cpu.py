@@ -131,3 +131,17 @@ def test_glu_interleave_roundtrip_cpu():
     a = R.silu_mul(torch.cat([x @ g.T, x @ u.T], -1))
     b = R.silu_mul(x @ il.T, interleaved=True)
     assert torch.allclose(a, b, atol=1e-5)
+
+
+def test_chunked_prefill_matches_single_pass():
+    """A prompt longer than max_prefill_tokens is prefilled in pieces through the paged
+    prefix attention; the greedy continuation must equal the one-pass prefill's."""
+    m = _model()
+    prompts = [list(range(3, 103)), [5, 6, 7], list(range(200, 150, -1))]
+    sp = SamplingParams(max_new_tokens=6, stop_on_eos=False)
+    one = LLMEngine(m, max_batch=4, max_context=256, block_size=16, use_graphs=False,
+                    prefix_cache=False).generate(prompts, sp)
+    chunked = LLMEngine(m, max_batch=4, max_context=256, block_size=16, use_graphs=False,
+                        max_prefill_tokens=32, prefix_cache=False).generate(prompts, sp)
+    assert one == chunked
+    assert one[0] == _naive_greedy(m, prompts[0], 6)
