@@ -95,6 +95,8 @@ def main() -> None:
     sync()
     comm.barrier()
     sync()
+    eng = pipe.engine
+    s0 = (eng.stats.prefill_s, eng.stats.decode_s, eng.stats.prompt_tokens, eng.stats.cached_tokens)
     t0 = time.perf_counter()
     step_times, stages = [], []
     for ans, st, lat in pipe.answer_pipelined([batch_for(a.warmup + s) for s in range(a.steps)], params):
@@ -112,7 +114,7 @@ def main() -> None:
     steps_max = [float(x) for x in t[1:]]
     queries = ps.dp_size * a.batch * a.steps
     qps = queries / elapsed_max
-    eng = pipe.engine
+    s1 = (eng.stats.prefill_s, eng.stats.decode_s, eng.stats.prompt_tokens, eng.stats.cached_tokens)
     if ps.rank == 0:
         st = {k: round(1e3 * statistics.mean(getattr(x, k) for x in stages), 2)
               for k in ("embed_s", "search_s", "prompt_s", "generate_s")}
@@ -141,6 +143,9 @@ def main() -> None:
             "stage_ms_mean": st,
             "gen_tokens_per_sec": round(ps.dp_size * a.batch * a.max_new_tokens * a.steps / elapsed_max, 1),
             "avg_prompt_tokens": round(eng.stats.prompt_tokens / max(1, (a.warmup + a.steps) * a.batch), 1),
+            "engine_ms_per_batch": {"prefill": round(1e3 * (s1[0] - s0[0]) / a.steps, 2),
+                                    "decode": round(1e3 * (s1[1] - s0[1]) / a.steps, 2)},
+            "prefix_cached_frac": round((s1[3] - s0[3]) / max(1, s1[2] - s0[2]), 3),
         }
         print(json.dumps(out), flush=True)
     comm.destroy()

@@ -301,7 +301,7 @@ at::Tensor dgemm_glu(const at::Tensor& x, const at::Tensor& w) {
 }
 
 // split-K partial slabs only: [S, M, N] fp32 (S >= 1), combine fused into the consumer
-at::Tensor dgemm_partial(const at::Tensor& x, const at::Tensor& w, int64_t splits) {
+at::Tensor dgemm_partial(const at::Tensor& x, const at::Tensor& w, int64_t splits, int64_t tile_rows) {
   CHECK_GPU(x); CHECK_BF16(x); CHECK_BF16(w); CHECK_CONTIG(x); CHECK_CONTIG(w);
   const int K = x.size(-1), N = w.size(0);
   TORCH_CHECK(w.size(1) == K, "dgemm_partial: K mismatch");
@@ -310,7 +310,7 @@ at::Tensor dgemm_partial(const at::Tensor& x, const at::Tensor& w, int64_t split
   c10::DeviceGuard g(x.device());
   auto part = at::empty({splits, M, N}, x.options().dtype(at::kFloat));
   CHECK_RC(docqa_dgemm_partial(x.data_ptr(), w.data_ptr(), part.data_ptr<float>(), M, N, K, (int)splits,
-                               stream()), "dgemm_partial");
+                               (int)tile_rows, stream()), "dgemm_partial");
   return part;
 }
 
@@ -442,7 +442,7 @@ TORCH_LIBRARY(docqa, m) {
   m.def("flash_prefill_paged(Tensor qkv, Tensor cu_seqlens, int max_len, int Hq, int Hkv, int D, "
         "float scale, Tensor k_cache, Tensor v_cache, Tensor block_tables, Tensor ctx_start) -> Tensor");
   m.def("dgemm(Tensor x, Tensor w, int splits) -> Tensor");
-  m.def("dgemm_partial(Tensor x, Tensor w, int splits) -> Tensor");
+  m.def("dgemm_partial(Tensor x, Tensor w, int splits, int tile_rows=64) -> Tensor");
   m.def("dgemm_glu(Tensor x, Tensor w) -> Tensor");
   m.def("add_rmsnorm_splitk(Tensor P, Tensor(a!) residual, Tensor w, float eps) -> Tensor");
   m.def("rope_cache_splitk(Tensor P, Tensor positions, Tensor cos_sin, Tensor? slot_mapping, "

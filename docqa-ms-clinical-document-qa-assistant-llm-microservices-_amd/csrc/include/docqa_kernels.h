@@ -48,7 +48,7 @@ int docqa_flash_prefill_paged(const void* qkv, int row_stride, const int* cu_seq
                               hipStream_t s);
 
 int docqa_dgemm_partial(const void* X, const void* W, float* P, int M, int N, int K, int S,
-                        hipStream_t s);
+                        int tile_rows, hipStream_t s);
 int docqa_add_rmsnorm_splitk(const float* P, int S, void* residual, const void* w, void* out,
                              int rows, int H, float eps, hipStream_t s);
 int docqa_rope_cache_splitk(const float* P, int S, void* qkv_out, const int* positions,

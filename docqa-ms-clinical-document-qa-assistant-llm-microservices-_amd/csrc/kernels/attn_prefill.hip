@@ -3,9 +3,13 @@
 //
 // Structure (cdna_hip_programming.md App. B "Fused attention prefill", §3 "An
 // accumulator tile as the next MFMA's operand", T10 tr-read, T2 swizzle, T14 split):
-//  * workgroup = 4 waves = 128 query rows of one (sequence, query head); each wave owns
-//    32 query rows.  KV tiles of 64 keys are staged HBM -> registers -> LDS once per
-//    workgroup and shared by the 4 waves.
+//  * workgroup = G query heads (one GQA group sharing a KV head) x WPH waves per head,
+//    each wave owning 32 query rows of one head.  KV tiles of 64 keys are staged
+//    HBM -> registers -> LDS once per workgroup and shared by all G x WPH waves, so with
+//    GQA (Llama-3: 4 query heads per KV head) every K/V tile is fetched once per group
+//    instead of once per query head: the prefix-cached RAG prefill (~140 new tokens
+//    against ~570 cached keys) was bound by exactly that re-fetch.  Encoders (no GQA):
+//    G = 1, WPH = 4 (128 rows of one head).
 //  * swapped QK^T: X = S^T = K . Q^T on v_mfma_f32_32x32x16_bf16, so each lane holds one
 //    query's scores for 16 keys in registers -> the row max / row sum of the online
 //    softmax are in-register plus one cross-half shuffle (no LDS round trip for P).
@@ -59,33 +63,37 @@ struct PagedKV {
   int log2BS;
 };
 
-template <int D, bool CAUSAL, bool PAGED>
-__global__ __launch_bounds__(256) void flash_prefill_kernel(
+template <int D, bool CAUSAL, bool PAGED, int G, int WPH>
+__global__ __launch_bounds__(64 * G * WPH) void flash_prefill_kernel(
     const uint16_t* __restrict__ qkv, int row_stride, const int* __restrict__ cu_seqlens,
     uint16_t* __restrict__ out, int o_stride, int Hq, int Hkv, float scale, PagedKV pk) {
+  constexpr int NT = 64 * G * WPH;              // threads
+  constexpr int QBW = 32 * WPH;                 // query rows per workgroup
   __shared__ __attribute__((aligned(16))) uint16_t smem[2 * KB * D];
   uint16_t* sK = smem;
   uint16_t* sV = smem + KB * D;
 
-  const int qt = blockIdx.x, h = blockIdx.y, b = blockIdx.z;
+  const int qt = blockIdx.x, hb = blockIdx.y, b = blockIdx.z;
   const int seq0 = cu_seqlens[b];
   const int L = cu_seqlens[b + 1] - seq0;
-  const int q_start = qt * QB;
+  const int q_start = qt * QBW;
   if (q_start >= L) return;
-  const int kvh = h / (Hq / Hkv);
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  // G > 1: blockIdx.y is the KV head and wave / WPH picks the query head of its group
+  const int h = G > 1 ? hb * G + wave / WPH : hb;
+  const int kvh = G > 1 ? hb : h / (Hq / Hkv);
   const int P0 = PAGED ? pk.ctx_start[b] : 0;   // absolute position of query row 0
   const int Lk = P0 + L;                         // keys visible to this sequence
 
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int l32 = lane & 31, hh = lane >> 5;
-  const int q_wave = q_start + wave * 32;       // first query row of this wave
+  const int q_wave = q_start + (wave % WPH) * 32;   // first query row of this wave
   const int my_q = q_wave + l32;                // this lane's query row (column of X)
 
   // ---- Q fragments (B operand of S^T = K Q^T): lane holds Q[my_q][16ks + 8hh + j]
   constexpr int NKS = D / 16;   // k-steps of the QK^T product
   constexpr int NDT = D / 32;   // 32-wide dim tiles of O^T
   constexpr int NCH = D / 8;    // 16-B chunks per row
-  constexpr int CPT = KB * NCH / 256;  // staged chunks per thread per tensor
+  constexpr int CPT = (KB * NCH + NT - 1) / NT;  // staged chunks per thread per tensor
   bf16x8 qf[NKS];
   {
     const bool ok = my_q < L;
@@ -105,7 +113,7 @@ __global__ __launch_bounds__(256) void flash_prefill_kernel(
   float m_run = -FLT_MAX, l_run = 0.f;
   const float sl2 = scale * kLog2e;
 
-  const int kv_end = CAUSAL ? min(Lk, P0 + q_start + QB) : Lk;
+  const int kv_end = CAUSAL ? min(Lk, P0 + q_start + QBW) : Lk;
   const int ntiles = (kv_end + KB - 1) / KB;
   const uint16_t* kbase = qkv + (size_t)seq0 * row_stride + (size_t)(Hq + kvh) * D;
   const uint16_t* vbase = qkv + (size_t)seq0 * row_stride + (size_t)(Hq + Hkv + kvh) * D;
@@ -115,10 +123,10 @@ __global__ __launch_bounds__(256) void flash_prefill_kernel(
   auto load_tile = [&](int t) {
 #pragma unroll
     for (int i = 0; i < CPT; ++i) {
-      const int idx = tid + 256 * i;
+      const int idx = tid + NT * i;
       const int row = idx / NCH, ch = idx % NCH;
       const int key = t * KB + row;
-      if (key < Lk) {
+      if (idx < KB * NCH && key < Lk) {
         if constexpr (PAGED) {
           const int blk = pk.block_tables[(size_t)b * pk.maxb + (key >> pk.log2BS)];
           const size_t off = (((size_t)blk * Hkv + kvh) * pk.BS + (key & (pk.BS - 1))) * D + ch * 8;
@@ -137,7 +145,8 @@ __global__ __launch_bounds__(256) void flash_prefill_kernel(
   auto store_tile = [&]() {
 #pragma unroll
     for (int i = 0; i < CPT; ++i) {
-      const int idx = tid + 256 * i;
+      const int idx = tid + NT * i;
+      if (idx >= KB * NCH) break;
       const int row = idx / NCH, ch = idx % NCH;
       *reinterpret_cast<uint4*>(sK + k_off<D>(row, ch)) = rk[i];
       *reinterpret_cast<uint4*>(sV + v_off<D>(row, ch)) = rv[i];
@@ -154,8 +163,9 @@ __global__ __launch_bounds__(256) void flash_prefill_kernel(
   for (int t = 0; t < ntiles; ++t) {
     if (t + 1 < ntiles) load_tile(t + 1);
     const int kb = t * KB;
-    // a wave whose rows all precede this tile's first key contributes nothing (causal)
-    const bool active = !CAUSAL || (kb <= P0 + q_wave + 31);
+    // a wave whose rows all precede this tile's first key contributes nothing (causal),
+    // nor does a wave whose rows all lie past the end of the sequence
+    const bool active = (!CAUSAL || (kb <= P0 + q_wave + 31)) && q_wave < L;
     if (active) {
       // ---- S^T for the two 32-key sub-tiles
       f32x16 x[2];
@@ -256,29 +266,39 @@ __global__ __launch_bounds__(256) void flash_prefill_kernel(
 }
 }  // namespace
 
-template <int D>
+template <int D, int G, int WPH>
 static void launch_prefill(dim3 grid, hipStream_t s, int causal, const void* qkv, int row_stride,
                            const int* cu, void* out, int o_stride, int Hq, int Hkv, float scale,
                            const PagedKV& pk) {
   const uint16_t* q = (const uint16_t*)qkv;
   uint16_t* o = (uint16_t*)out;
+  constexpr int NT = 64 * G * WPH;
   if (pk.k) {
-    flash_prefill_kernel<D, true, true><<<grid, 256, 0, s>>>(q, row_stride, cu, o, o_stride, Hq, Hkv, scale, pk);
+    flash_prefill_kernel<D, true, true, G, WPH><<<grid, NT, 0, s>>>(q, row_stride, cu, o, o_stride, Hq, Hkv, scale, pk);
   } else if (causal) {
-    flash_prefill_kernel<D, true, false><<<grid, 256, 0, s>>>(q, row_stride, cu, o, o_stride, Hq, Hkv, scale, pk);
+    flash_prefill_kernel<D, true, false, G, WPH><<<grid, NT, 0, s>>>(q, row_stride, cu, o, o_stride, Hq, Hkv, scale, pk);
   } else {
-    flash_prefill_kernel<D, false, false><<<grid, 256, 0, s>>>(q, row_stride, cu, o, o_stride, Hq, Hkv, scale, pk);
+    flash_prefill_kernel<D, false, false, G, WPH><<<grid, NT, 0, s>>>(q, row_stride, cu, o, o_stride, Hq, Hkv, scale, pk);
   }
 }
 
-static int prefill_dispatch(dim3 grid, hipStream_t s, int head_dim, int causal, const void* qkv,
+// G = 4 query heads per KV head (Llama-3 GQA): one workgroup per (64 query rows, KV head)
+// with 8 waves; otherwise one workgroup per (128 rows, query head) with 4 waves
+static int prefill_dispatch(hipStream_t s, int B, int max_len, int head_dim, int causal, const void* qkv,
                             int row_stride, const int* cu, void* out, int o_stride, int Hq, int Hkv,
                             float scale, const PagedKV& pk) {
-  switch (head_dim) {
-    case 32: launch_prefill<32>(grid, s, causal, qkv, row_stride, cu, out, o_stride, Hq, Hkv, scale, pk); break;
-    case 64: launch_prefill<64>(grid, s, causal, qkv, row_stride, cu, out, o_stride, Hq, Hkv, scale, pk); break;
-    case 128: launch_prefill<128>(grid, s, causal, qkv, row_stride, cu, out, o_stride, Hq, Hkv, scale, pk); break;
-    default: return -1;
+  const bool gqa4 = head_dim == 128 && Hq == 4 * Hkv;
+  if (gqa4) {
+    dim3 grid((max_len + 63) / 64, Hkv, B);
+    launch_prefill<128, 4, 2>(grid, s, causal, qkv, row_stride, cu, out, o_stride, Hq, Hkv, scale, pk);
+  } else {
+    dim3 grid((max_len + QB - 1) / QB, Hq, B);
+    switch (head_dim) {
+      case 32: launch_prefill<32, 1, 4>(grid, s, causal, qkv, row_stride, cu, out, o_stride, Hq, Hkv, scale, pk); break;
+      case 64: launch_prefill<64, 1, 4>(grid, s, causal, qkv, row_stride, cu, out, o_stride, Hq, Hkv, scale, pk); break;
+      case 128: launch_prefill<128, 1, 4>(grid, s, causal, qkv, row_stride, cu, out, o_stride, Hq, Hkv, scale, pk); break;
+      default: return -1;
+    }
   }
   DOCQA_CHECK_LAUNCH();
   return 0;
@@ -289,9 +309,8 @@ int docqa_flash_prefill(const void* qkv, int row_stride, const int* cu_seqlens, 
                         float scale, int causal, hipStream_t s) {
   if (B == 0 || max_len == 0) return 0;
   if (Hq % Hkv != 0) return -1;
-  dim3 grid((max_len + QB - 1) / QB, Hq, B);
   PagedKV pk{nullptr, nullptr, nullptr, 0, nullptr, 1, 0};
-  return prefill_dispatch(grid, s, head_dim, causal, qkv, row_stride, cu_seqlens, out, o_stride, Hq,
+  return prefill_dispatch(s, B, max_len, head_dim, causal, qkv, row_stride, cu_seqlens, out, o_stride, Hq,
                           Hkv, scale, pk);
 }
 
@@ -305,8 +324,7 @@ int docqa_flash_prefill_paged(const void* qkv, int row_stride, const int* cu_seq
   if (Hq % Hkv != 0 || (BS & (BS - 1)) != 0 || head_dim != 128) return -1;
   int log2BS = 0;
   while ((1 << log2BS) < BS) ++log2BS;
-  dim3 grid((max_len + QB - 1) / QB, Hq, B);
   PagedKV pk{(const uint16_t*)k_cache, (const uint16_t*)v_cache, block_tables, maxb, ctx_start, BS, log2BS};
-  return prefill_dispatch(grid, s, head_dim, 1, qkv, row_stride, cu_seqlens, out, o_stride, Hq, Hkv,
+  return prefill_dispatch(s, B, max_len, head_dim, 1, qkv, row_stride, cu_seqlens, out, o_stride, Hq, Hkv,
                           scale, pk);
 }

@@ -300,11 +300,16 @@ int docqa_dgemm(const void* X, const void* W, void* Y, float* partial, int M, in
 // split-K partial slabs only (S >= 1, P: [S, M, N] fp32): the combine is fused into the
 // consumer (add_rmsnorm_splitk / rope_cache_splitk)
 int docqa_dgemm_partial(const void* X, const void* W, float* P, int M, int N, int K, int S,
-                        hipStream_t s) {
+                        int tile_rows, hipStream_t s) {
   if (M == 0) return 0;
-  if (!shape_ok(M, N, K, S, BN) || !P) return -1;
-  launch_mt<EPI_PARTIAL, 4>((M + 15) / 16, dim3(N / BN, S), s, (const uint16_t*)X,
-                            (const uint16_t*)W, nullptr, P, M, N, K, K / S);
+  if (!P || (tile_rows != 64 && tile_rows != 128) || !shape_ok(M, N, K, S, tile_rows)) return -1;
+  const int mt = (M + 15) / 16;
+  const uint16_t* x = (const uint16_t*)X;
+  const uint16_t* w = (const uint16_t*)W;
+  if (tile_rows == 128)   // 1 workgroup per CU (128 KB ring), X re-read half as often
+    launch_mt<EPI_PARTIAL, 8>(mt, dim3(N / 128, S), s, x, w, nullptr, P, M, N, K, K / S);
+  else
+    launch_mt<EPI_PARTIAL, 4>(mt, dim3(N / 64, S), s, x, w, nullptr, P, M, N, K, K / S);
   DOCQA_CHECK_LAUNCH();
   return 0;
 }

@@ -183,11 +183,11 @@ def decode_linear(x, w):
     return torch.nn.functional.linear(x, w)
 
 
-def dgemm_partial(x, w, splits: int):
+def dgemm_partial(x, w, splits: int, tile_rows: int = 64):
     """Split-K partial slabs [S, M, N] fp32 of x @ w^T (combine fused into the consumer:
-    add_rmsnorm_splitk / rope_cache_splitk)."""
+    add_rmsnorm_splitk / rope_cache_splitk); tile_rows 64 or 128 weight rows per workgroup."""
     if _gpu(x):
-        return _native().dgemm_partial(x.contiguous(), w, splits)
+        return _native().dgemm_partial(x.contiguous(), w, splits, tile_rows)
     K = w.shape[1]
     xs = x.float().reshape(-1, splits, K // splits)
     ws = w.float().reshape(-1, splits, K // splits)
