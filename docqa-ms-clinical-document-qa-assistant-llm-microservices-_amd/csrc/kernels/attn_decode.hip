@@ -46,12 +46,16 @@ __device__ __forceinline__ int split_chunk(int L, int nsplit) {
   return c < kMinChunk ? kMinChunk : c;
 }
 
-template <int G, int D, int U>
+// DIRECT (one partition per sequence, the batch-64 serving case): the workgroup already
+// holds the whole softmax, so it writes the normalised bf16 output itself and the
+// partition-merge launch is skipped (one kernel boundary less per layer).
+template <int G, int D, int U, bool DIRECT>
 __global__ __launch_bounds__(256) void paged_decode_kernel(
     const uint16_t* __restrict__ q, int q_stride, const uint16_t* __restrict__ k_cache,
     const uint16_t* __restrict__ v_cache, const int* __restrict__ block_tables, int maxb,
     const int* __restrict__ context_lens, float* __restrict__ tmp_out,
-    float* __restrict__ tmp_ml, int Hkv, int BS, int log2BS, int max_parts, float scale) {
+    float* __restrict__ tmp_ml, int Hkv, int BS, int log2BS, int max_parts, float scale,
+    uint16_t* __restrict__ out, int out_stride) {
   static_assert(D == 128, "decode kernel is specialised for head_dim 128");
   const int part = blockIdx.x, kvh = blockIdx.y, b = blockIdx.z;
   const int L = context_lens[b];
@@ -204,11 +208,15 @@ __global__ __launch_bounds__(256) void paged_decode_kernel(
       lsum += s_l[w][g] * f;
     }
     const int h = kvh * G + g;
-    const size_t o = ((size_t)b * (Hkv * G) + h) * max_parts + part;
-    tmp_out[o * D + d] = v;
-    if (d == 0) {
-      tmp_ml[o * 2 + 0] = M;
-      tmp_ml[o * 2 + 1] = lsum;
+    if constexpr (DIRECT) {
+      out[(size_t)b * out_stride + (size_t)h * D + d] = f2bf(lsum > 0.f ? v / lsum : 0.f);
+    } else {
+      const size_t o = ((size_t)b * (Hkv * G) + h) * max_parts + part;
+      tmp_out[o * D + d] = v;
+      if (d == 0) {
+        tmp_ml[o * 2 + 0] = M;
+        tmp_ml[o * 2 + 1] = lsum;
+      }
     }
   }
 }
@@ -245,10 +253,20 @@ int docqa_paged_decode(const void* q, int q_stride, const void* k_cache, const v
   while ((1 << log2BS) < BS) ++log2BS;
   const int G = Hq / Hkv;
   dim3 grid(max_parts, Hkv, B);
-#define DEC(GG, UU)                                                                         \
-  paged_decode_kernel<GG, 128, UU><<<grid, 256, 0, s>>>(                                    \
-      (const uint16_t*)q, q_stride, (const uint16_t*)k_cache, (const uint16_t*)v_cache,     \
-      block_tables, maxb, context_lens, tmp_out, tmp_ml, Hkv, BS, log2BS, max_parts, scale)
+  const bool direct = max_parts == 1;
+#define DEC(GG, UU)                                                                           \
+  do {                                                                                        \
+  if (direct)                                                                                 \
+    paged_decode_kernel<GG, 128, UU, true><<<grid, 256, 0, s>>>(                              \
+        (const uint16_t*)q, q_stride, (const uint16_t*)k_cache, (const uint16_t*)v_cache,     \
+        block_tables, maxb, context_lens, tmp_out, tmp_ml, Hkv, BS, log2BS, max_parts, scale, \
+        (uint16_t*)out, out_stride);                                                          \
+  else                                                                                        \
+    paged_decode_kernel<GG, 128, UU, false><<<grid, 256, 0, s>>>(                             \
+        (const uint16_t*)q, q_stride, (const uint16_t*)k_cache, (const uint16_t*)v_cache,     \
+        block_tables, maxb, context_lens, tmp_out, tmp_ml, Hkv, BS, log2BS, max_parts, scale, \
+        (uint16_t*)out, out_stride);                                                          \
+  } while (0)
   // tokens in flight per lane group per buffer (U): DOCQA_DECODE_U overrides (tuning knob)
   static const int u_env = [] {
     const char* e = getenv("DOCQA_DECODE_U");
@@ -266,9 +284,10 @@ int docqa_paged_decode(const void* q, int q_stride, const void* k_cache, const v
     default: return -1;
   }
 #undef DEC
-  paged_decode_reduce<128><<<dim3(Hq, B), 128, 0, s>>>(tmp_out, tmp_ml, context_lens,
-                                                       (uint16_t*)out, out_stride, Hq,
-                                                       max_parts);
+  if (!direct)
+    paged_decode_reduce<128><<<dim3(Hq, B), 128, 0, s>>>(tmp_out, tmp_ml, context_lens,
+                                                         (uint16_t*)out, out_stride, Hq,
+                                                         max_parts);
   DOCQA_CHECK_LAUNCH();
   return 0;
 }

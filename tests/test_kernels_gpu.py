@@ -161,6 +161,25 @@ def test_paged_decode(native, G, lens):
     _close(o1, o2, 2e-2, 1e-2)
 
 
+def test_paged_decode_single_partition(native):
+    """Batch 64 x 8 KV heads fills the chip with one partition per sequence: the kernel
+    writes the normalised output directly (no merge launch)."""
+    from docqa_amd.ops import reference as R
+
+    B, Hkv, G, D, BS = 64, 8, 4, 128, 64
+    Hq = Hkv * G
+    lens = torch.randint(1, 700, (B,)).tolist()
+    maxb = 12
+    kc = torch.randn(B * maxb, Hkv, BS, D, device="cuda", dtype=torch.bfloat16)
+    vc = torch.randn_like(kc)
+    bt = torch.randperm(B * maxb, device="cuda").int().view(B, maxb)
+    cl = torch.tensor(lens, device="cuda", dtype=torch.int32)
+    q = torch.randn(B, (Hq + 2 * Hkv) * D, device="cuda", dtype=torch.bfloat16)
+    o1 = native.paged_decode(q, kc, vc, bt, cl, Hq, maxb * BS, 1 / math.sqrt(D))
+    o2 = R.paged_decode(q, kc, vc, bt, cl, Hq, maxb * BS, 1 / math.sqrt(D))
+    _close(o1, o2, 2e-2, 1e-2)
+
+
 @pytest.mark.parametrize("D", [128, 64, 32])
 @pytest.mark.parametrize("causal", [True, False])
 def test_flash_prefill(native, D, causal):
