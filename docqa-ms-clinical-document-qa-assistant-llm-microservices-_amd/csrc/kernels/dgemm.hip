@@ -25,11 +25,12 @@
 //     per workgroup (at M = 64 that X traffic, not HBM, was the limiter).
 // Shapes: N % (16 NT) == 0, (K / S) % 512 == 0 (whole 4-stage ring turns), M <= 64.
 #include "docqa_common.h"
+#include <stdlib.h>
 
 using namespace docqa;
 
 namespace {
-constexpr int BN = 64, BKD = 128, NS = 4, MR = 64;
+constexpr int BN = 64, BKD = 128, NS = 4, MR = 64;   // NS: default ring slots, K granule 4 stages
 constexpr int KSTEPS = BKD / 32;               // 16x16x32 k-steps per stage
 enum { EPI_BF16 = 0, EPI_PARTIAL = 1, EPI_GLU = 2 };
 typedef __attribute__((address_space(3))) void lds_void;
@@ -93,7 +94,7 @@ __device__ __forceinline__ float row_swap8(float v) {
 // k-group = wave / MT) so every wave owns a disjoint (rows x k) piece of the product and
 // the W stage in LDS (NT 16-row n-tiles) is shared by all of them.  KW = 4 / MT k-groups
 // are summed through LDS at the end.
-template <int EPI, int MT, int NT>
+template <int EPI, int MT, int NT, int NSR>
 __global__ __launch_bounds__(256) void dgemm_kernel(const uint16_t* __restrict__ X,
                                                     const uint16_t* __restrict__ W,
                                                     uint16_t* __restrict__ Y,
@@ -101,7 +102,8 @@ __global__ __launch_bounds__(256) void dgemm_kernel(const uint16_t* __restrict__
                                                     int Ks) {
   constexpr int KW = 4 / MT, SPW = KSTEPS / KW;
   constexpr int STAGE = NT * 16 * BKD;         // elements of one W stage (NT x 4 KB)
-  __shared__ __attribute__((aligned(16))) uint16_t sw[NS * STAGE];   // W ring
+  static_assert(NSR >= 4, "ring needs >= 4 slots");
+  __shared__ __attribute__((aligned(16))) uint16_t sw[NSR * STAGE];   // W ring
   const int n0 = blockIdx.x * NT * 16;
   const int slice = blockIdx.y;
   const int kbeg = slice * Ks;
@@ -133,7 +135,7 @@ __global__ __launch_bounds__(256) void dgemm_kernel(const uint16_t* __restrict__
   }
   auto stage_w = [&](int j) {
     const int koff = min(j, nkb - 1) * BKD;
-    const uint32_t dst = ring + (uint32_t)((j % NS) * STAGE * 2);
+    const uint32_t dst = ring + (uint32_t)((j % NSR) * STAGE * 2);
 #pragma unroll
     for (int i = 0; i < NT; ++i) glds16(wsrc[i] + koff, dst + (uint32_t)((i * 4 + wave) * 1024));
   };
@@ -144,7 +146,7 @@ __global__ __launch_bounds__(256) void dgemm_kernel(const uint16_t* __restrict__
     if constexpr (SPW > 2) { gload16<128>(x[2], src); gload16<192>(x[3], src); }
   };
   auto mma = [&](const bf16x8 (&x)[SPW], int j) {
-    const uint16_t* src = sw + (j % NS) * STAGE;
+    const uint16_t* src = sw + (j % NSR) * STAGE;
 #pragma unroll
     for (int s = 0; s < SPW; ++s) {
       const bf16x8 a = x[s];
@@ -156,21 +158,23 @@ __global__ __launch_bounds__(256) void dgemm_kernel(const uint16_t* __restrict__
       }
     }
   };
-  // Issue order per wave: W0 X0 W1 X1 W2 | step i: X(i+2) W(i+3).  At the top of step i
-  // the ops issued after X(i) are W(i+1), X(i+1), W(i+2), so vmcnt(2 NT + SPW) retires
-  // X(i) and (issued before it) W(i) while two W stages stay in flight; the barrier then
-  // publishes stage i to every wave and frees slot (i-1) % NS for W(i+3).
+  // Issue order per wave (R = NSR): W0 .. W(R-4) X0 W(R-3) X1 W(R-2) | step i: X(i+2)
+  // W(i+R-1).  At the top of step i the ops issued after X(i) are one W group, X(i+1) and
+  // one more W group, so vmcnt(2 NT + SPW) retires X(i) and (issued before it) W(i)
+  // while R-2 W stages stay in flight; the barrier then publishes stage i to every wave
+  // and frees slot (i-1) % R for W(i+R-1).
   bf16x8 x0[SPW], x1[SPW], x2[SPW], x3[SPW];
-  stage_w(0);
+#pragma unroll
+  for (int j = 0; j <= NSR - 4; ++j) stage_w(j);
   load_x(x0, 0);
-  stage_w(1);
+  stage_w(NSR - 3);
   load_x(x1, 1);
-  stage_w(2);
+  stage_w(NSR - 2);
 #define RING_STEP(I, XC, XN)                                                            \
   wait_vm_n<2 * NT + SPW>(XC);                                                          \
   ring_barrier();                                                                       \
   load_x(XN, (I) + 2);                                                                  \
-  stage_w((I) + 3);                                                                     \
+  stage_w((I) + NSR - 1);                                                               \
   mma(XC, I);
   // nkb % 4 == 0: a break-free 4-step body keeps each X buffer in one register set (an
   // early exit makes hipcc merge buffers with register copies that read in-flight data)
@@ -266,12 +270,12 @@ int docqa_dgemm_splits(int N, int K) {
   return s;
 }
 
-template <int EPI, int NT>
+template <int EPI, int NT, int NSR = NS>
 static void launch_mt(int mt, dim3 grid, hipStream_t s, const uint16_t* x, const uint16_t* w,
                       uint16_t* y, float* p, int M, int N, int K, int Ks) {
-  if (mt == 1) dgemm_kernel<EPI, 1, NT><<<grid, 256, 0, s>>>(x, w, y, p, M, N, K, Ks);
-  else if (mt == 2) dgemm_kernel<EPI, 2, NT><<<grid, 256, 0, s>>>(x, w, y, p, M, N, K, Ks);
-  else dgemm_kernel<EPI, 4, NT><<<grid, 256, 0, s>>>(x, w, y, p, M, N, K, Ks);
+  if (mt == 1) dgemm_kernel<EPI, 1, NT, NSR><<<grid, 256, 0, s>>>(x, w, y, p, M, N, K, Ks);
+  else if (mt == 2) dgemm_kernel<EPI, 2, NT, NSR><<<grid, 256, 0, s>>>(x, w, y, p, M, N, K, Ks);
+  else dgemm_kernel<EPI, 4, NT, NSR><<<grid, 256, 0, s>>>(x, w, y, p, M, N, K, Ks);
 }
 
 static bool shape_ok(int M, int N, int K, int S, int bn) {
@@ -306,8 +310,16 @@ int docqa_dgemm_partial(const void* X, const void* W, float* P, int M, int N, in
   const int mt = (M + 15) / 16;
   const uint16_t* x = (const uint16_t*)X;
   const uint16_t* w = (const uint16_t*)W;
+  static const int ns_env = [] {   // ring depth knob (tuning experiments)
+    const char* e = getenv("DOCQA_DGEMM_NS");
+    return e ? atoi(e) : 0;
+  }();
   if (tile_rows == 128)   // 1 workgroup per CU (128 KB ring), X re-read half as often
     launch_mt<EPI_PARTIAL, 8>(mt, dim3(N / 128, S), s, x, w, nullptr, P, M, N, K, K / S);
+  else if (ns_env == 6)
+    launch_mt<EPI_PARTIAL, 4, 6>(mt, dim3(N / 64, S), s, x, w, nullptr, P, M, N, K, K / S);
+  else if (ns_env == 8)
+    launch_mt<EPI_PARTIAL, 4, 8>(mt, dim3(N / 64, S), s, x, w, nullptr, P, M, N, K, K / S);
   else
     launch_mt<EPI_PARTIAL, 4>(mt, dim3(N / 64, S), s, x, w, nullptr, P, M, N, K, K / S);
   DOCQA_CHECK_LAUNCH();
