@@ -67,6 +67,8 @@ def main() -> None:
     ps = comm.init_distributed(tp_size=a.tp, backend=None if cuda else "gloo")
     if cuda:
         assert ops.load_native(), "native HIP kernels not built (python -m docqa_amd.ops.build)"
+        if a.tp > 1 and os.environ.get("DOCQA_CUSTOM_AR", "0") == "1":
+            comm.enable_custom_all_reduce()
     dev = f"cuda:{local_rank}" if cuda else "cpu"
 
     def sync():

@@ -413,6 +413,48 @@ at::Tensor pq_encode(const at::Tensor& x, const at::Tensor& centroids, const at:
   return codes;
 }
 
+// ---- one-shot IPC all-reduce (kernels/allreduce.hip): raw device pointers travel as int64
+int64_t ar_region_bytes(int64_t max_elems) { return (int64_t)docqa_ar_region_bytes((size_t)max_elems); }
+
+int64_t ar_alloc(int64_t bytes) {
+  void* p = nullptr;
+  TORCH_CHECK(docqa_ar_alloc((size_t)bytes, &p) == 0, "ar_alloc: hipExtMallocWithFlags(uncached) failed");
+  return (int64_t)(uintptr_t)p;
+}
+
+void ar_free(int64_t ptr) { TORCH_CHECK(docqa_ar_free((void*)(uintptr_t)ptr) == 0, "ar_free failed"); }
+
+at::Tensor ar_ipc_handle(int64_t ptr) {
+  auto h = at::empty({64}, at::TensorOptions().dtype(at::kByte));
+  TORCH_CHECK(docqa_ar_ipc_handle((void*)(uintptr_t)ptr, h.data_ptr()) == 0, "hipIpcGetMemHandle failed");
+  return h;
+}
+
+int64_t ar_ipc_open(const at::Tensor& handle) {
+  TORCH_CHECK(handle.numel() == 64 && handle.scalar_type() == at::kByte && !handle.is_cuda(),
+              "ipc handle must be 64 host bytes");
+  void* p = nullptr;
+  TORCH_CHECK(docqa_ar_ipc_open(handle.contiguous().data_ptr(), &p) == 0, "hipIpcOpenMemHandle failed");
+  return (int64_t)(uintptr_t)p;
+}
+
+void ar_ipc_close(int64_t ptr) { TORCH_CHECK(docqa_ar_ipc_close((void*)(uintptr_t)ptr) == 0, "ipc close failed"); }
+
+at::Tensor ar_oneshot(const at::Tensor& in, int64_t rank, std::vector<int64_t> regions, int64_t max_elems,
+                      at::Tensor epochs, at::Tensor err) {
+  CHECK_GPU(in); CHECK_BF16(in); CHECK_CONTIG(in);
+  TORCH_CHECK(epochs.scalar_type() == at::kInt && err.scalar_type() == at::kInt, "epochs/err must be int32");
+  TORCH_CHECK(regions.size() >= 1 && regions.size() <= 8, "1..8 ranks");
+  std::vector<void*> ptrs;
+  for (auto r : regions) ptrs.push_back((void*)(uintptr_t)r);
+  c10::DeviceGuard g(in.device());
+  auto out = at::empty_like(in);
+  CHECK_RC(docqa_ar_oneshot(in.data_ptr(), out.data_ptr(), in.numel(), (int)rank, (int)regions.size(),
+                            ptrs.data(), (size_t)max_elems, (unsigned*)epochs.data_ptr(),
+                            (unsigned*)err.data_ptr(), stream()), "ar_oneshot");
+  return out;
+}
+
 }  // namespace
 
 TORCH_LIBRARY(docqa, m) {
@@ -444,6 +486,13 @@ TORCH_LIBRARY(docqa, m) {
   m.def("dgemm(Tensor x, Tensor w, int splits) -> Tensor");
   m.def("dgemm_partial(Tensor x, Tensor w, int splits, int tile_rows=64) -> Tensor");
   m.def("dgemm_glu(Tensor x, Tensor w) -> Tensor");
+  m.def("ar_oneshot(Tensor x, int rank, int[] regions, int max_elems, Tensor(a!) epochs, Tensor(b!) err) -> Tensor");
+  m.def("ar_region_bytes(int max_elems) -> int", &ar_region_bytes);
+  m.def("ar_alloc(int bytes) -> int", &ar_alloc);
+  m.def("ar_free(int ptr) -> ()", &ar_free);
+  m.def("ar_ipc_handle(int ptr) -> Tensor", &ar_ipc_handle);
+  m.def("ar_ipc_open(Tensor handle) -> int", &ar_ipc_open);
+  m.def("ar_ipc_close(int ptr) -> ()", &ar_ipc_close);
   m.def("add_rmsnorm_splitk(Tensor P, Tensor(a!) residual, Tensor w, float eps) -> Tensor");
   m.def("rope_cache_splitk(Tensor P, Tensor positions, Tensor cos_sin, Tensor? slot_mapping, "
         "Tensor(b!) k_cache, Tensor(c!) v_cache, int Hq, int Hkv, int D) -> Tensor");
@@ -471,6 +520,7 @@ TORCH_LIBRARY_IMPL(docqa, CUDA, m) {
   m.impl("dgemm", &dgemm);
   m.impl("dgemm_partial", &dgemm_partial);
   m.impl("dgemm_glu", &dgemm_glu);
+  m.impl("ar_oneshot", &ar_oneshot);
   m.impl("add_rmsnorm_splitk", &add_rmsnorm_splitk);
   m.impl("rope_cache_splitk", &rope_cache_splitk);
 }

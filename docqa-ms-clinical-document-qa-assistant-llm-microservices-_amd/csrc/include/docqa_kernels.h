@@ -55,6 +55,14 @@ int docqa_rope_cache_splitk(const float* P, int S, void* qkv_out, const int* pos
                             const float* cos_sin, const int* slot_mapping, void* k_cache,
                             void* v_cache, int T, int Hq, int Hkv, int D, int row_stride, int BS,
                             hipStream_t s);
+size_t docqa_ar_region_bytes(size_t max_elems);
+int docqa_ar_alloc(size_t bytes, void** ptr);
+int docqa_ar_free(void* ptr);
+int docqa_ar_ipc_handle(void* ptr, void* handle_out);
+int docqa_ar_ipc_open(const void* handle, void** ptr);
+int docqa_ar_ipc_close(void* ptr);
+int docqa_ar_oneshot(const void* in, void* out, int n, int rank, int nranks, void* const* regions,
+                     size_t max_elems, unsigned* epochs, unsigned* err, hipStream_t s);
 int docqa_dgemm_splits(int N, int K);
 int docqa_dgemm_glu(const void* X, const void* W, void* Y, int M, int N, int K, hipStream_t s);
 int docqa_dgemm(const void* X, const void* W, void* Y, float* partial, int M, int N, int K, int S,

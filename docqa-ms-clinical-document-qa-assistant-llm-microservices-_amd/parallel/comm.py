@@ -97,9 +97,27 @@ def set_state(s: ParallelState) -> None:
     _STATE = s
 
 
+_CUSTOM_AR = None
+
+
+def enable_custom_all_reduce(max_bytes: int = 8 << 20):
+    """Use the one-shot IPC all-reduce (parallel/custom_ar.py) for TP all-reduces that fit
+    ``max_bytes`` (bf16, contiguous); RCCL keeps everything else.  Opt-in
+    (DOCQA_CUSTOM_AR=1 in bench.py): validated 2-rank on one GPU, not yet on a multi-GPU
+    node."""
+    global _CUSTOM_AR
+    s = _STATE
+    if s.tp_size > 1 and s.backend == "nccl" and _CUSTOM_AR is None:
+        from .custom_ar import CustomAllReduce
+        _CUSTOM_AR = CustomAllReduce(group=s.tp_group, max_bytes=max_bytes)
+    return _CUSTOM_AR
+
+
 def tp_all_reduce(t: torch.Tensor) -> torch.Tensor:
     s = _STATE
     if s.tp_size > 1:
+        if _CUSTOM_AR is not None and _CUSTOM_AR.supports(t):
+            return _CUSTOM_AR.all_reduce(t)
         dist.all_reduce(t, group=s.tp_group)
     return t
 
@@ -132,7 +150,10 @@ def barrier() -> None:
 
 
 def destroy() -> None:
-    global _STATE
+    global _STATE, _CUSTOM_AR
+    if _CUSTOM_AR is not None:
+        _CUSTOM_AR.close()
+        _CUSTOM_AR = None
     if dist.is_initialized():
         dist.destroy_process_group()
     _STATE = ParallelState()
