@@ -49,8 +49,8 @@ __device__ __forceinline__ int split_chunk(int L, int nsplit) {
 // DIRECT (one partition per sequence, the batch-64 serving case): the workgroup already
 // holds the whole softmax, so it writes the normalised bf16 output itself and the
 // partition-merge launch is skipped (one kernel boundary less per layer).
-template <int G, int D, int U, bool DIRECT>
-__global__ __launch_bounds__(256) void paged_decode_kernel(
+template <int G, int D, int U, bool DIRECT, int OCC = 2>
+__global__ __launch_bounds__(256, OCC) void paged_decode_kernel(
     const uint16_t* __restrict__ q, int q_stride, const uint16_t* __restrict__ k_cache,
     const uint16_t* __restrict__ v_cache, const int* __restrict__ block_tables, int maxb,
     const int* __restrict__ context_lens, float* __restrict__ tmp_out,
@@ -71,14 +71,19 @@ __global__ __launch_bounds__(256) void paged_decode_kernel(
   __shared__ float s_acc[4][G][D];
   __shared__ float s_m[4][G], s_l[4][G];
 
-  float qv[G][8];
+  // q stays packed bf16: q.k runs on v_dot2c_f32_bf16 straight from the packed K row
+  // (no bf16 -> fp32 unpack of K, half the VALU ops of fp32 FMAs); the softmax scale is
+  // applied to the reduced score
+  bf16x2 qv[G][4];
   const float qs = scale * kLog2e;
 #pragma unroll
   for (int g = 0; g < G; ++g) {
     const uint16_t* qp = q + (size_t)b * q_stride + (size_t)(kvh * G + g) * D;
-    unpack8(reinterpret_cast<const uint4*>(qp)[chunk], qv[g]);
-#pragma unroll
-    for (int j = 0; j < 8; ++j) qv[g][j] *= qs;
+    const uint4 qq = reinterpret_cast<const uint4*>(qp)[chunk];
+    qv[g][0] = __builtin_bit_cast(bf16x2, qq.x);
+    qv[g][1] = __builtin_bit_cast(bf16x2, qq.y);
+    qv[g][2] = __builtin_bit_cast(bf16x2, qq.z);
+    qv[g][3] = __builtin_bit_cast(bf16x2, qq.w);
   }
   const int* bt = block_tables + (size_t)b * maxb;
   const size_t head_off = (size_t)kvh * BS * D + chunk * 8;
@@ -115,14 +120,15 @@ __global__ __launch_bounds__(256) void paged_decode_kernel(
     float s[U][G];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
-      float kf[8];
-      unpack8(kr[u], kf);
+      const bf16x2 k0 = __builtin_bit_cast(bf16x2, kr[u].x), k1 = __builtin_bit_cast(bf16x2, kr[u].y);
+      const bf16x2 k2 = __builtin_bit_cast(bf16x2, kr[u].z), k3 = __builtin_bit_cast(bf16x2, kr[u].w);
 #pragma unroll
       for (int g = 0; g < G; ++g) {
-        float d = 0.f;
-#pragma unroll
-        for (int j = 0; j < 8; ++j) d += qv[g][j] * kf[j];
-        d = group_sum<16>(d);
+        float d0 = __builtin_amdgcn_fdot2_f32_bf16(k0, qv[g][0], 0.f, false);
+        float d1 = __builtin_amdgcn_fdot2_f32_bf16(k2, qv[g][2], 0.f, false);
+        d0 = __builtin_amdgcn_fdot2_f32_bf16(k1, qv[g][1], d0, false);
+        d1 = __builtin_amdgcn_fdot2_f32_bf16(k3, qv[g][3], d1, false);
+        const float d = group_sum<16>(d0 + d1) * qs;
         s[u][g] = ok[u] ? d : -FLT_MAX;
       }
     }
@@ -254,36 +260,36 @@ int docqa_paged_decode(const void* q, int q_stride, const void* k_cache, const v
   const int G = Hq / Hkv;
   dim3 grid(max_parts, Hkv, B);
   const bool direct = max_parts == 1;
-#define DEC(GG, UU)                                                                           \
-  do {                                                                                        \
-  if (direct)                                                                                 \
-    paged_decode_kernel<GG, 128, UU, true><<<grid, 256, 0, s>>>(                              \
-        (const uint16_t*)q, q_stride, (const uint16_t*)k_cache, (const uint16_t*)v_cache,     \
-        block_tables, maxb, context_lens, tmp_out, tmp_ml, Hkv, BS, log2BS, max_parts, scale, \
-        (uint16_t*)out, out_stride);                                                          \
-  else                                                                                        \
-    paged_decode_kernel<GG, 128, UU, false><<<grid, 256, 0, s>>>(                             \
-        (const uint16_t*)q, q_stride, (const uint16_t*)k_cache, (const uint16_t*)v_cache,     \
-        block_tables, maxb, context_lens, tmp_out, tmp_ml, Hkv, BS, log2BS, max_parts, scale, \
-        (uint16_t*)out, out_stride);                                                          \
-  } while (0)
-  // tokens in flight per lane group per buffer (U): DOCQA_DECODE_U overrides (tuning knob)
+  // U (tokens in flight per lane group per buffer) and occupancy: measured on HBM-resident
+  // caches (benchmarks/bench_decode_attn.py, profiles/r1_decode_attention_sweep_hbm.log):
+  // U=4 at 2 waves/SIMD beats U=3/3 and U=2/4 -- all keep ~64 wave-loads in flight per
+  // CU, which at the loaded HBM latency caps one CU near 17 GB/s.  DOCQA_DECODE_U=2 knob.
   static const int u_env = [] {
     const char* e = getenv("DOCQA_DECODE_U");
     return e ? atoi(e) : 0;
   }();
+#define DEC_K(GG, UU, DIR)                                                                    \
+  paged_decode_kernel<GG, 128, UU, DIR><<<grid, 256, 0, s>>>(                                 \
+      (const uint16_t*)q, q_stride, (const uint16_t*)k_cache, (const uint16_t*)v_cache,       \
+      block_tables, maxb, context_lens, tmp_out, tmp_ml, Hkv, BS, log2BS, max_parts, scale,   \
+      (uint16_t*)out, out_stride)
+#define DEC(GG, UU)                                                                           \
+  do {                                                                                        \
+    if (direct) DEC_K(GG, UU, true);                                                          \
+    else DEC_K(GG, UU, false);                                                                \
+  } while (0)
   switch (G) {
     case 1: DEC(1, 4); break;
     case 2: DEC(2, 4); break;
-    case 4:  // U = 4 measured best on HBM-resident caches (benchmarks/bench_decode_attn.py)
+    case 4:
       if (u_env == 2) DEC(4, 2);
-      else if (u_env == 1) DEC(4, 1);
       else DEC(4, 4);
       break;
     case 8: DEC(8, 1); break;
     default: return -1;
   }
 #undef DEC
+#undef DEC_K
   if (!direct)
     paged_decode_reduce<128><<<dim3(Hq, B), 128, 0, s>>>(tmp_out, tmp_ml, context_lens,
                                                          (uint16_t*)out, out_stride, Hq,
