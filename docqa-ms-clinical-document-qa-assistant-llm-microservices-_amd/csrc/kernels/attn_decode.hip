@@ -26,6 +26,7 @@
 // Reference parity: decode attention is inside llama.cpp behind Ollama
 // (llm-qa/main.py:69, greedy decode loop of RetrievalQA.invoke at llm-qa/main.py:117).
 #include "docqa_common.h"
+#include "docqa_asm.h"
 #include <float.h>
 #include <stdlib.h>
 
@@ -44,6 +45,117 @@ __device__ __forceinline__ int split_chunk(int L, int nsplit) {
   int c = (L + nsplit - 1) / nsplit;
   c = (c + kMinChunk - 1) / kMinChunk * kMinChunk;
   return c < kMinChunk ? kMinChunk : c;
+}
+
+// Online-softmax attention of one lane group's U token rows (16 lanes x 8 dims each): q.k
+// on v_dot2c_f32_bf16 + DPP row reduction, rescale, P.V accumulate in fp32.
+template <int G, int U>
+__device__ __forceinline__ void attend_rows(const uint4 (&kr)[U], const uint4 (&vr)[U],
+                                            const bool (&ok)[U], const bf16x2 (&qv)[G][4],
+                                            float qs, float (&m)[G], float (&l)[G],
+                                            float (&acc)[G][8]) {
+    float s[U][G];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const bf16x2 k0 = __builtin_bit_cast(bf16x2, kr[u].x), k1 = __builtin_bit_cast(bf16x2, kr[u].y);
+      const bf16x2 k2 = __builtin_bit_cast(bf16x2, kr[u].z), k3 = __builtin_bit_cast(bf16x2, kr[u].w);
+#pragma unroll
+      for (int g = 0; g < G; ++g) {
+        float d0 = __builtin_amdgcn_fdot2_f32_bf16(k0, qv[g][0], 0.f, false);
+        float d1 = __builtin_amdgcn_fdot2_f32_bf16(k2, qv[g][2], 0.f, false);
+        d0 = __builtin_amdgcn_fdot2_f32_bf16(k1, qv[g][1], d0, false);
+        d1 = __builtin_amdgcn_fdot2_f32_bf16(k3, qv[g][3], d1, false);
+        const float d = group_sum<16>(d0 + d1) * qs;
+        s[u][g] = ok[u] ? d : -FLT_MAX;
+      }
+    }
+#pragma unroll
+    for (int g = 0; g < G; ++g) {
+      float mx = m[g];
+#pragma unroll
+      for (int u = 0; u < U; ++u) mx = fmaxf(mx, s[u][g]);
+      const float corr = exp2f(m[g] - mx);
+      m[g] = mx;
+      l[g] *= corr;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) acc[g][j] *= corr;
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      if (ok[u]) {
+        float vf[8];
+        unpack8(vr[u], vf);
+#pragma unroll
+        for (int g = 0; g < G; ++g) {
+          const float p = exp2f(s[u][g] - m[g]);
+          l[g] += p;
+#pragma unroll
+          for (int j = 0; j < 8; ++j) acc[g][j] += p * vf[j];
+        }
+      }
+    }
+  }
+
+// Merge the 16 lane-group streams of a workgroup (4 per wave via xor-shuffles, 4 waves
+// through LDS) and write the partition result: normalised bf16 output (DIRECT) or the
+// un-normalised accumulator + (max, sum) for the merge kernel.
+template <int G, int D, bool DIRECT>
+__device__ __forceinline__ void finish_partition(
+    float (&m)[G], float (&l)[G], float (&acc)[G][8], float (*s_acc)[G][D], float (*s_m)[G],
+    float (*s_l)[G], int tid, int wave, int tg, int chunk, int b, int kvh, int part, int Hkv,
+    int max_parts, float* __restrict__ tmp_out, float* __restrict__ tmp_ml,
+    uint16_t* __restrict__ out, int out_stride) {
+  // ---- merge the 4 lane-group streams of the wave (lanes l, l^16, l^32, l^48)
+#pragma unroll
+  for (int g = 0; g < G; ++g) {
+    float M = fmaxf(m[g], __shfl_xor(m[g], 16, 64));
+    M = fmaxf(M, __shfl_xor(M, 32, 64));
+    const float f = (m[g] == -FLT_MAX) ? 0.f : exp2f(m[g] - M);
+    float lv = l[g] * f;
+    lv += __shfl_xor(lv, 16, 64);
+    lv += __shfl_xor(lv, 32, 64);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      float a = acc[g][j] * f;
+      a += __shfl_xor(a, 16, 64);
+      a += __shfl_xor(a, 32, 64);
+      acc[g][j] = a;
+    }
+    m[g] = M;
+    l[g] = lv;
+  }
+  if (tg == 0) {
+#pragma unroll
+    for (int g = 0; g < G; ++g) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) s_acc[wave][g][chunk * 8 + j] = acc[g][j];
+      if (chunk == 0) { s_m[wave][g] = m[g]; s_l[wave][g] = l[g]; }
+    }
+  }
+  __syncthreads();
+  // ---- merge the 4 waves, write the partition result
+  for (int i = tid; i < G * D; i += 256) {
+    const int g = i / D, d = i % D;
+    float M = fmaxf(fmaxf(s_m[0][g], s_m[1][g]), fmaxf(s_m[2][g], s_m[3][g]));
+    float v = 0.f, lsum = 0.f;
+#pragma unroll
+    for (int w = 0; w < 4; ++w) {
+      const float f = (s_m[w][g] == -FLT_MAX) ? 0.f : exp2f(s_m[w][g] - M);
+      v += s_acc[w][g][d] * f;
+      lsum += s_l[w][g] * f;
+    }
+    const int h = kvh * G + g;
+    if constexpr (DIRECT) {
+      out[(size_t)b * out_stride + (size_t)h * D + d] = f2bf(lsum > 0.f ? v / lsum : 0.f);
+    } else {
+      const size_t o = ((size_t)b * (Hkv * G) + h) * max_parts + part;
+      tmp_out[o * D + d] = v;
+      if (d == 0) {
+        tmp_ml[o * 2 + 0] = M;
+        tmp_ml[o * 2 + 1] = lsum;
+      }
+    }
+  }
 }
 
 // DIRECT (one partition per sequence, the batch-64 serving case): the workgroup already
@@ -117,46 +229,7 @@ __global__ __launch_bounds__(256, OCC) void paged_decode_kernel(
     }
   };
   auto compute = [&](const uint4 (&kr)[U], const uint4 (&vr)[U], const bool (&ok)[U]) {
-    float s[U][G];
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const bf16x2 k0 = __builtin_bit_cast(bf16x2, kr[u].x), k1 = __builtin_bit_cast(bf16x2, kr[u].y);
-      const bf16x2 k2 = __builtin_bit_cast(bf16x2, kr[u].z), k3 = __builtin_bit_cast(bf16x2, kr[u].w);
-#pragma unroll
-      for (int g = 0; g < G; ++g) {
-        float d0 = __builtin_amdgcn_fdot2_f32_bf16(k0, qv[g][0], 0.f, false);
-        float d1 = __builtin_amdgcn_fdot2_f32_bf16(k2, qv[g][2], 0.f, false);
-        d0 = __builtin_amdgcn_fdot2_f32_bf16(k1, qv[g][1], d0, false);
-        d1 = __builtin_amdgcn_fdot2_f32_bf16(k3, qv[g][3], d1, false);
-        const float d = group_sum<16>(d0 + d1) * qs;
-        s[u][g] = ok[u] ? d : -FLT_MAX;
-      }
-    }
-#pragma unroll
-    for (int g = 0; g < G; ++g) {
-      float mx = m[g];
-#pragma unroll
-      for (int u = 0; u < U; ++u) mx = fmaxf(mx, s[u][g]);
-      const float corr = exp2f(m[g] - mx);
-      m[g] = mx;
-      l[g] *= corr;
-#pragma unroll
-      for (int j = 0; j < 8; ++j) acc[g][j] *= corr;
-    }
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      if (ok[u]) {
-        float vf[8];
-        unpack8(vr[u], vf);
-#pragma unroll
-        for (int g = 0; g < G; ++g) {
-          const float p = exp2f(s[u][g] - m[g]);
-          l[g] += p;
-#pragma unroll
-          for (int j = 0; j < 8; ++j) acc[g][j] += p * vf[j];
-        }
-      }
-    }
+    attend_rows<G, U>(kr, vr, ok, qv, qs, m, l, acc);
   };
 
   uint4 kA[U], vA[U], kB[U], vB[U];
@@ -174,57 +247,112 @@ __global__ __launch_bounds__(256, OCC) void paged_decode_kernel(
     base = nb2;
   }
 
-  // ---- merge the 4 lane-group streams of the wave (lanes l, l^16, l^32, l^48)
+  finish_partition<G, D, DIRECT>(m, l, acc, s_acc, s_m, s_l, tid, wave, tg, chunk, b, kvh, part,
+                                 Hkv, max_parts, tmp_out, tmp_ml, out, out_stride);
+}
+
+// LDS-DMA ring variant (BS = 64, D = 128).  The register kernel above is capped by the
+// wave-loads a CU can keep in flight (~64 x 1 KB at 2 waves/SIMD, ~17 GB/s per CU at the
+// loaded HBM latency).  Here K/V move HBM -> LDS by LDS-DMA (global_load_lds, no VGPR
+// cost), 32-token tiles (8 KB K + 8 KB V) through a 4-slot ring with three tiles in
+// flight per workgroup, two workgroups per CU; lane groups then read their token rows
+// from LDS (ds_read_b128, 1 KB contiguous per wave-instruction: conflict-free) and run the
+// same online-softmax math.  Counted vmcnt waits + raw s_barrier as in dgemm.hip.
+template <int G, bool DIRECT>
+__global__ __launch_bounds__(256) void paged_decode_ring_kernel(
+    const uint16_t* __restrict__ q, int q_stride, const uint16_t* __restrict__ k_cache,
+    const uint16_t* __restrict__ v_cache, const int* __restrict__ block_tables, int maxb,
+    const int* __restrict__ context_lens, float* __restrict__ tmp_out,
+    float* __restrict__ tmp_ml, int Hkv, int max_parts, float scale,
+    uint16_t* __restrict__ out, int out_stride) {
+  constexpr int D = 128, TT = 32, NSR = 4, U = 2;
+  constexpr int TILE = TT * D;                   // elements of one K (or V) tile: 8 KB
+  __shared__ __attribute__((aligned(16))) uint16_t ring[NSR * 2 * TILE];   // 64 KB
+  __shared__ float s_acc[4][G][D];
+  __shared__ float s_m[4][G], s_l[4][G];
+  __shared__ int s_bt[256];                      // block ids of the slice (<= 16k tokens)
+
+  const int part = blockIdx.x, kvh = blockIdx.y, b = blockIdx.z;
+  const int L = context_lens[b];
+  const int slice = split_chunk(L, max_parts);   // multiple of 64
+  const int start = part * slice;
+  if (start >= L) return;
+  const int n = min(L - start, slice);
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int chunk = lane & 15, tg = lane >> 4;
+
+  // this slice's block ids -> LDS (ring addressing then needs no vector-memory loads)
+  const int nblk = (n + 63) >> 6;
+  for (int i = tid; i < nblk; i += 256) s_bt[i] = block_tables[(size_t)b * maxb + (start >> 6) + i];
+
+  bf16x2 qv[G][4];
+  const float qs = scale * kLog2e;
 #pragma unroll
   for (int g = 0; g < G; ++g) {
-    float M = fmaxf(m[g], __shfl_xor(m[g], 16, 64));
-    M = fmaxf(M, __shfl_xor(M, 32, 64));
-    const float f = (m[g] == -FLT_MAX) ? 0.f : exp2f(m[g] - M);
-    float lv = l[g] * f;
-    lv += __shfl_xor(lv, 16, 64);
-    lv += __shfl_xor(lv, 32, 64);
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      float a = acc[g][j] * f;
-      a += __shfl_xor(a, 16, 64);
-      a += __shfl_xor(a, 32, 64);
-      acc[g][j] = a;
-    }
-    m[g] = M;
-    l[g] = lv;
-  }
-  if (tg == 0) {
-#pragma unroll
-    for (int g = 0; g < G; ++g) {
-#pragma unroll
-      for (int j = 0; j < 8; ++j) s_acc[wave][g][chunk * 8 + j] = acc[g][j];
-      if (chunk == 0) { s_m[wave][g] = m[g]; s_l[wave][g] = l[g]; }
-    }
+    const uint16_t* qp = q + (size_t)b * q_stride + (size_t)(kvh * G + g) * D;
+    const uint4 qq = reinterpret_cast<const uint4*>(qp)[chunk];
+    asm volatile("" :: "v"(qq.x), "v"(qq.y), "v"(qq.z), "v"(qq.w));   // land q before the ring
+    qv[g][0] = __builtin_bit_cast(bf16x2, qq.x);
+    qv[g][1] = __builtin_bit_cast(bf16x2, qq.y);
+    qv[g][2] = __builtin_bit_cast(bf16x2, qq.z);
+    qv[g][3] = __builtin_bit_cast(bf16x2, qq.w);
   }
   __syncthreads();
-  // ---- merge the 4 waves, write the partition result
-  for (int i = tid; i < G * D; i += 256) {
-    const int g = i / D, d = i % D;
-    float M = fmaxf(fmaxf(s_m[0][g], s_m[1][g]), fmaxf(s_m[2][g], s_m[3][g]));
-    float v = 0.f, lsum = 0.f;
+
+  float m[G], l[G], acc[G][8];
 #pragma unroll
-    for (int w = 0; w < 4; ++w) {
-      const float f = (s_m[w][g] == -FLT_MAX) ? 0.f : exp2f(s_m[w][g] - M);
-      v += s_acc[w][g][d] * f;
-      lsum += s_l[w][g] * f;
-    }
-    const int h = kvh * G + g;
-    if constexpr (DIRECT) {
-      out[(size_t)b * out_stride + (size_t)h * D + d] = f2bf(lsum > 0.f ? v / lsum : 0.f);
-    } else {
-      const size_t o = ((size_t)b * (Hkv * G) + h) * max_parts + part;
-      tmp_out[o * D + d] = v;
-      if (d == 0) {
-        tmp_ml[o * 2 + 0] = M;
-        tmp_ml[o * 2 + 1] = lsum;
-      }
-    }
+  for (int g = 0; g < G; ++g) {
+    m[g] = -FLT_MAX;
+    l[g] = 0.f;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[g][j] = 0.f;
   }
+
+  const int ntile = (n + TT - 1) / TT;
+  const uint32_t ring_base = lds_u32(ring);
+  const size_t head_rows = (size_t)kvh * 64;     // row offset of this head inside a block
+  // tile j -> slot j % NSR: 8 KB of K + 8 KB of V = 16 wave-instructions, 4 per wave.
+  // Past the last tile the source is clamped (L2 hit into a free slot): every step issues
+  // the same number of DMAs, so the counted wait below needs no tail cases.
+  auto stage = [&](int j) {
+    const int jj = min(j, ntile - 1);
+    const int tok0 = jj * TT;                    // start is a multiple of 64
+    const size_t row = ((size_t)s_bt[tok0 >> 6] * Hkv) * 64 + head_rows + (tok0 & 63);
+    const uint16_t* kp = k_cache + row * D;
+    const uint16_t* vp = v_cache + row * D;
+    const uint32_t dst = ring_base + (uint32_t)((j % NSR) * 2 * TILE * 2);
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int c = i * 4 + wave;                // 1 KB piece of the 8 KB tile
+      glds16<true>(kp + c * 512 + lane * 8, dst + c * 1024);
+      glds16<true>(vp + c * 512 + lane * 8, dst + TILE * 2 + c * 1024);
+    }
+  };
+  stage(0);
+  stage(1);
+  stage(2);
+  for (int i = 0; i < ntile; ++i) {
+    wait_vmcnt<8>();                             // tiles i+1, i+2 (4 DMAs each) may fly
+    ring_barrier();                              // tile i visible; slot (i-1) % NSR free
+    stage(i + 3);
+    const uint16_t* kt = ring + (i % NSR) * 2 * TILE;
+    const uint16_t* vt = kt + TILE;
+    uint4 kr[U], vr[U];
+    bool ok[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int r = wave * 8 + 4 * u + tg;       // token row of the tile
+      ok[u] = i * TT + r < n;
+      kr[u] = *reinterpret_cast<const uint4*>(kt + r * D + chunk * 8);
+      vr[u] = *reinterpret_cast<const uint4*>(vt + r * D + chunk * 8);
+    }
+    attend_rows<G, U>(kr, vr, ok, qv, qs, m, l, acc);
+  }
+  wait_vmcnt<0>();                               // drain the clamped tail DMAs
+
+  finish_partition<G, D, DIRECT>(m, l, acc, s_acc, s_m, s_l, tid, wave, tg, chunk, b, kvh, part,
+                                 Hkv, max_parts, tmp_out, tmp_ml, out, out_stride);
 }
 
 template <int D>
@@ -278,6 +406,39 @@ int docqa_paged_decode(const void* q, int q_stride, const void* k_cache, const v
     if (direct) DEC_K(GG, UU, true);                                                          \
     else DEC_K(GG, UU, false);                                                                \
   } while (0)
+  static const bool ring_env = [] {
+    const char* e = getenv("DOCQA_DECODE_RING");
+    return !(e && atoi(e) == 0);
+  }();
+  if (ring_env && BS == 64 && maxb <= 256) {
+#define DRING(GG)                                                                             \
+    do {                                                                                      \
+      if (direct)                                                                             \
+        paged_decode_ring_kernel<GG, true><<<grid, 256, 0, s>>>(                              \
+            (const uint16_t*)q, q_stride, (const uint16_t*)k_cache, (const uint16_t*)v_cache, \
+            block_tables, maxb, context_lens, tmp_out, tmp_ml, Hkv, max_parts, scale,         \
+            (uint16_t*)out, out_stride);                                                      \
+      else                                                                                    \
+        paged_decode_ring_kernel<GG, false><<<grid, 256, 0, s>>>(                             \
+            (const uint16_t*)q, q_stride, (const uint16_t*)k_cache, (const uint16_t*)v_cache, \
+            block_tables, maxb, context_lens, tmp_out, tmp_ml, Hkv, max_parts, scale,         \
+            (uint16_t*)out, out_stride);                                                      \
+    } while (0)
+    switch (G) {
+      case 1: DRING(1); break;
+      case 2: DRING(2); break;
+      case 4: DRING(4); break;
+      case 8: DRING(8); break;
+      default: return -1;
+    }
+#undef DRING
+    if (!direct)
+      paged_decode_reduce<128><<<dim3(Hq, B), 128, 0, s>>>(tmp_out, tmp_ml, context_lens,
+                                                           (uint16_t*)out, out_stride, Hq,
+                                                           max_parts);
+    DOCQA_CHECK_LAUNCH();
+    return 0;
+  }
   switch (G) {
     case 1: DEC(1, 4); break;
     case 2: DEC(2, 4); break;

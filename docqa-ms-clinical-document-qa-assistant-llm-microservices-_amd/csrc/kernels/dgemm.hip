@@ -25,6 +25,7 @@
 //     per workgroup (at M = 64 that X traffic, not HBM, was the limiter).
 // Shapes: N % (16 NT) == 0, (K / S) % 512 == 0 (whole 4-stage ring turns), M <= 64.
 #include "docqa_common.h"
+#include "docqa_asm.h"
 #include <stdlib.h>
 
 using namespace docqa;
@@ -35,25 +36,8 @@ constexpr int KSTEPS = BKD / 32;               // 16x16x32 k-steps per stage
 enum { EPI_BF16 = 0, EPI_PARTIAL = 1, EPI_GLU = 2 };
 typedef __attribute__((address_space(3))) void lds_void;
 
-// All vector-memory traffic of the main loop is inline asm, so hipcc's waitcnt pass sees
-// none of it: with the LDS-DMA / X loads as builtins it drained everything (vmcnt(0)) at
-// the loop header and before the first MFMA (an LDS-DMA is a pending LDS write to it, and
-// its loop-carried bookkeeping is conservative), which collapsed the ring to one stage.
-// The counted waits below are the only ones (cdna_hip_programming.md §5.7).
-__device__ __forceinline__ void ring_barrier() { asm volatile("s_barrier" ::: "memory"); }
-
-__device__ __forceinline__ uint32_t lds_u32(const void* p) {
-  return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) char*)p;
-}
-
-// one 16-B-per-lane LDS-DMA wave-instruction: lanes write dst_base + 16 * lane.  `nt`:
-// decode weights are read once per step (16 GB per step >> the 256 MB MALL), and the
-// non-temporal policy lands them ~4 % sooner (MI355X_MICROARCH.md nt-weights).
-__device__ __forceinline__ void glds16(const void* gsrc, uint32_t dst_base) {
-  unsigned keep;
-  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off nt\n\ts_mov_b32 m0, %0"
-               : "=&s"(keep) : "v"(gsrc), "s"(dst_base) : "memory");
-}
+// The ring's DMA / X loads are inline asm (docqa_asm.h): the counted waits below are the
+// only vmcnt waits of the main loop.
 
 template <int OFF>
 __device__ __forceinline__ void gload16(bf16x8& d, const void* p) {
@@ -137,7 +121,7 @@ __global__ __launch_bounds__(256) void dgemm_kernel(const uint16_t* __restrict__
     const int koff = min(j, nkb - 1) * BKD;
     const uint32_t dst = ring + (uint32_t)((j % NSR) * STAGE * 2);
 #pragma unroll
-    for (int i = 0; i < NT; ++i) glds16(wsrc[i] + koff, dst + (uint32_t)((i * 4 + wave) * 1024));
+    for (int i = 0; i < NT; ++i) glds16<true>(wsrc[i] + koff, dst + (uint32_t)((i * 4 + wave) * 1024));
   };
   auto load_x = [&](bf16x8 (&x)[SPW], int j) {
     const uint16_t* src = xrow + min(j, nkb - 1) * BKD;
