@@ -230,6 +230,34 @@ at::Tensor paged_decode(const at::Tensor& q, const at::Tensor& k_cache, const at
   return out;
 }
 
+// decode step attention fed by the QKV projection's split-K partial slabs: RoPE + cache
+// write of the new token + paged attention in one launch (ring kernel)
+at::Tensor paged_decode_fused(const at::Tensor& P, const at::Tensor& positions, const at::Tensor& cos_sin,
+                              const at::Tensor& slot_mapping, at::Tensor k_cache, at::Tensor v_cache,
+                              const at::Tensor& block_tables, const at::Tensor& context_lens,
+                              int64_t Hq, int64_t max_context, double scale) {
+  CHECK_GPU(P); CHECK_CONTIG(P); CHECK_BF16(k_cache); CHECK_BF16(v_cache);
+  CHECK_I32(positions); CHECK_I32(slot_mapping); CHECK_I32(block_tables); CHECK_I32(context_lens);
+  CHECK_CONTIG(block_tables);
+  TORCH_CHECK(P.scalar_type() == at::kFloat && P.dim() == 3, "partials must be fp32 [S, B, width]");
+  TORCH_CHECK(cos_sin.scalar_type() == at::kFloat, "cos_sin must be fp32");
+  const int B = P.size(1);
+  const int Hkv = k_cache.size(1), BS = k_cache.size(2), D = k_cache.size(3);
+  TORCH_CHECK(D == 128 && P.size(2) == (Hq + 2 * Hkv) * D, "fused decode: head_dim 128, packed QKV width");
+  const int max_parts = docqa_decode_splits(B, Hkv, max_context);
+  c10::DeviceGuard g(P.device());
+  auto out = at::empty({B, Hq * D}, P.options().dtype(at::kBFloat16));
+  auto tmp_out = at::empty({B, Hq, max_parts, D}, P.options());
+  auto tmp_ml = at::empty({B, Hq, max_parts, 2}, P.options());
+  CHECK_RC(docqa_paged_decode_fused(P.data_ptr<float>(), P.size(0), positions.data_ptr<int>(),
+                                    cos_sin.data_ptr<float>(), slot_mapping.data_ptr<int>(),
+                                    k_cache.data_ptr(), v_cache.data_ptr(), block_tables.data_ptr<int>(),
+                                    block_tables.size(1), context_lens.data_ptr<int>(), out.data_ptr(),
+                                    Hq * D, tmp_out.data_ptr<float>(), tmp_ml.data_ptr<float>(), B, Hq,
+                                    Hkv, BS, max_parts, (float)scale, stream()), "paged_decode_fused");
+  return out;
+}
+
 at::Tensor flash_prefill(const at::Tensor& qkv, const at::Tensor& cu_seqlens, int64_t max_len,
                          int64_t Hq, int64_t Hkv, int64_t D, double scale, bool causal) {
   CHECK_GPU(qkv); CHECK_BF16(qkv); CHECK_I32(cu_seqlens);
@@ -486,6 +514,9 @@ TORCH_LIBRARY(docqa, m) {
   m.def("dgemm(Tensor x, Tensor w, int splits) -> Tensor");
   m.def("dgemm_partial(Tensor x, Tensor w, int splits, int tile_rows=64) -> Tensor");
   m.def("dgemm_glu(Tensor x, Tensor w) -> Tensor");
+  m.def("paged_decode_fused(Tensor P, Tensor positions, Tensor cos_sin, Tensor slot_mapping, "
+        "Tensor(a!) k_cache, Tensor(b!) v_cache, Tensor block_tables, Tensor context_lens, int Hq, "
+        "int max_context, float scale) -> Tensor");
   m.def("ar_oneshot(Tensor x, int rank, int[] regions, int max_elems, Tensor(a!) epochs, Tensor(b!) err) -> Tensor");
   m.def("ar_region_bytes(int max_elems) -> int", &ar_region_bytes);
   m.def("ar_alloc(int bytes) -> int", &ar_alloc);
@@ -520,6 +551,7 @@ TORCH_LIBRARY_IMPL(docqa, CUDA, m) {
   m.impl("dgemm", &dgemm);
   m.impl("dgemm_partial", &dgemm_partial);
   m.impl("dgemm_glu", &dgemm_glu);
+  m.impl("paged_decode_fused", &paged_decode_fused);
   m.impl("ar_oneshot", &ar_oneshot);
   m.impl("add_rmsnorm_splitk", &add_rmsnorm_splitk);
   m.impl("rope_cache_splitk", &rope_cache_splitk);

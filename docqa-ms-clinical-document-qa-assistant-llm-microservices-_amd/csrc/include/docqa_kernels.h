@@ -63,6 +63,11 @@ int docqa_ar_ipc_open(const void* handle, void** ptr);
 int docqa_ar_ipc_close(void* ptr);
 int docqa_ar_oneshot(const void* in, void* out, int n, int rank, int nranks, void* const* regions,
                      size_t max_elems, unsigned* epochs, unsigned* err, hipStream_t s);
+int docqa_paged_decode_fused(const float* P, int S, const int* positions, const float* cos_sin,
+                             const int* slot_mapping, void* k_cache, void* v_cache,
+                             const int* block_tables, int maxb, const int* context_lens, void* out,
+                             int out_stride, float* tmp_out, float* tmp_ml, int B, int Hq, int Hkv,
+                             int BS, int max_parts, float scale, hipStream_t s);
 int docqa_dgemm_splits(int N, int K);
 int docqa_dgemm_glu(const void* X, const void* W, void* Y, int M, int N, int K, hipStream_t s);
 int docqa_dgemm(const void* X, const void* W, void* Y, float* partial, int M, int N, int K, int S,

@@ -258,13 +258,56 @@ __global__ __launch_bounds__(256, OCC) void paged_decode_kernel(
 // flight per workgroup, two workgroups per CU; lane groups then read their token rows
 // from LDS (ds_read_b128, 1 KB contiguous per wave-instruction: conflict-free) and run the
 // same online-softmax math.  Counted vmcnt waits + raw s_barrier as in dgemm.hip.
-template <int G, bool DIRECT>
+// FUSED: the step's packed QKV arrives as S fp32 split-K partial slabs of the decode
+// projection (FusedQKV); the workgroup sums its G query heads and its KV head, applies
+// RoPE (rotate-half partner = lane ^ 8 inside the 16-lane row, one DPP rotate), writes the
+// new token's K/V into the paged cache (the workgroup whose slice holds the last token)
+// and attends -- replacing the separate rope_cache_splitk launch and the bf16 QKV round
+// trip.
+struct FusedQKV {
+  const float* P;            // [S, B, (Hq + 2 Hkv) D]
+  int S;
+  const int* positions;      // [B]
+  const float* cos_sin;      // [max_pos, D] = [cos(D/2) | sin(D/2)]
+  const int* slot_mapping;   // [B], -1: no cache write
+  int Hq;
+};
+
+// sum of the S slabs of 8 consecutive values, rounded to bf16 like the unfused path
+__device__ __forceinline__ void sum_slabs8(const float* p, int S, size_t slab, float (&x)[8]) {
+  float4 a = *reinterpret_cast<const float4*>(p), b = *reinterpret_cast<const float4*>(p + 4);
+  for (int sl = 1; sl < S; ++sl) {
+    const float4 c = *reinterpret_cast<const float4*>(p + sl * slab);
+    const float4 d = *reinterpret_cast<const float4*>(p + sl * slab + 4);
+    a.x += c.x; a.y += c.y; a.z += c.z; a.w += c.w;
+    b.x += d.x; b.y += d.y; b.z += d.z; b.w += d.w;
+  }
+  const float v[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+#pragma unroll
+  for (int j = 0; j < 8; ++j) x[j] = bf2f(f2bf(v[j]));
+}
+
+// rotate-half RoPE of one 8-dim chunk (chunk index c of 16, D = 128): partner chunk c ^ 8
+// lives 8 lanes away in the same DPP row
+__device__ __forceinline__ void rope8(float (&x)[8], int c, const float* cs) {
+  float xp[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) xp[j] = row_ror<8>(x[j]);
+  const int i0 = (c & 7) * 8;                    // rotation index of dim 0 of this chunk
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const float co = cs[i0 + j], si = cs[64 + i0 + j];
+    x[j] = c < 8 ? x[j] * co - xp[j] * si : x[j] * co + xp[j] * si;
+  }
+}
+
+template <int G, bool DIRECT, bool FUSED = false>
 __global__ __launch_bounds__(256) void paged_decode_ring_kernel(
-    const uint16_t* __restrict__ q, int q_stride, const uint16_t* __restrict__ k_cache,
-    const uint16_t* __restrict__ v_cache, const int* __restrict__ block_tables, int maxb,
+    const uint16_t* __restrict__ q, int q_stride, uint16_t* __restrict__ k_cache,
+    uint16_t* __restrict__ v_cache, const int* __restrict__ block_tables, int maxb,
     const int* __restrict__ context_lens, float* __restrict__ tmp_out,
     float* __restrict__ tmp_ml, int Hkv, int max_parts, float scale,
-    uint16_t* __restrict__ out, int out_stride) {
+    uint16_t* __restrict__ out, int out_stride, FusedQKV fz) {
   constexpr int D = 128, TT = 32, NSR = 4, U = 2;
   constexpr int TILE = TT * D;                   // elements of one K (or V) tile: 8 KB
   __shared__ __attribute__((aligned(16))) uint16_t ring[NSR * 2 * TILE];   // 64 KB
@@ -288,15 +331,17 @@ __global__ __launch_bounds__(256) void paged_decode_ring_kernel(
 
   bf16x2 qv[G][4];
   const float qs = scale * kLog2e;
+  if constexpr (!FUSED) {
 #pragma unroll
-  for (int g = 0; g < G; ++g) {
-    const uint16_t* qp = q + (size_t)b * q_stride + (size_t)(kvh * G + g) * D;
-    const uint4 qq = reinterpret_cast<const uint4*>(qp)[chunk];
-    asm volatile("" :: "v"(qq.x), "v"(qq.y), "v"(qq.z), "v"(qq.w));   // land q before the ring
-    qv[g][0] = __builtin_bit_cast(bf16x2, qq.x);
-    qv[g][1] = __builtin_bit_cast(bf16x2, qq.y);
-    qv[g][2] = __builtin_bit_cast(bf16x2, qq.z);
-    qv[g][3] = __builtin_bit_cast(bf16x2, qq.w);
+    for (int g = 0; g < G; ++g) {
+      const uint16_t* qp = q + (size_t)b * q_stride + (size_t)(kvh * G + g) * D;
+      const uint4 qq = reinterpret_cast<const uint4*>(qp)[chunk];
+      asm volatile("" :: "v"(qq.x), "v"(qq.y), "v"(qq.z), "v"(qq.w));   // land q before the ring
+      qv[g][0] = __builtin_bit_cast(bf16x2, qq.x);
+      qv[g][1] = __builtin_bit_cast(bf16x2, qq.y);
+      qv[g][2] = __builtin_bit_cast(bf16x2, qq.z);
+      qv[g][3] = __builtin_bit_cast(bf16x2, qq.w);
+    }
   }
   __syncthreads();
 
@@ -309,7 +354,12 @@ __global__ __launch_bounds__(256) void paged_decode_ring_kernel(
     for (int j = 0; j < 8; ++j) acc[g][j] = 0.f;
   }
 
-  const int ntile = (n + TT - 1) / TT;
+  // FUSED: the step's new token (position L-1) is not read back from the cache -- the
+  // workgroup whose slice holds it attends to it from registers -- so the ring can start
+  // streaming before the QKV partials are even read
+  const bool owns_last = FUSED && (start <= L - 1) && (L - 1 < start + n);
+  const int n_ring = owns_last ? n - 1 : n;
+  const int ntile = (n_ring + TT - 1) / TT;
   const uint32_t ring_base = lds_u32(ring);
   const size_t head_rows = (size_t)kvh * 64;     // row offset of this head inside a block
   // tile j -> slot j % NSR: 8 KB of K + 8 KB of V = 16 wave-instructions, 4 per wave.
@@ -329,9 +379,46 @@ __global__ __launch_bounds__(256) void paged_decode_ring_kernel(
       glds16<true>(vp + c * 512 + lane * 8, dst + TILE * 2 + c * 1024);
     }
   };
-  stage(0);
-  stage(1);
-  stage(2);
+  if (ntile > 0) {
+    stage(0);
+    stage(1);
+    stage(2);
+  }
+
+  uint4 knew = make_uint4(0, 0, 0, 0), vnew = make_uint4(0, 0, 0, 0);
+  if constexpr (FUSED) {
+    // q for the G heads of the group and (slice owner) the new K/V: sum of the split-K
+    // partial slabs, rounded to bf16, RoPE; the new K/V row also goes to the paged cache
+    const int W = (fz.Hq + 2 * Hkv) * D;
+    const size_t slab = (size_t)gridDim.z * W;
+    const float* row = fz.P + (size_t)b * W;
+    const float* cs = fz.cos_sin + (size_t)fz.positions[b] * D;
+#pragma unroll
+    for (int g = 0; g < G; ++g) {
+      float x[8];
+      sum_slabs8(row + (size_t)(kvh * G + g) * D + chunk * 8, fz.S, slab, x);
+      rope8(x, chunk, cs);
+      qv[g][0] = __builtin_bit_cast(bf16x2, pack2(x[0], x[1]));
+      qv[g][1] = __builtin_bit_cast(bf16x2, pack2(x[2], x[3]));
+      qv[g][2] = __builtin_bit_cast(bf16x2, pack2(x[4], x[5]));
+      qv[g][3] = __builtin_bit_cast(bf16x2, pack2(x[6], x[7]));
+    }
+    if (owns_last && wave == 0 && tg == 0) {
+      float kx[8], vx[8];
+      sum_slabs8(row + (size_t)(fz.Hq + kvh) * D + chunk * 8, fz.S, slab, kx);
+      rope8(kx, chunk, cs);
+      sum_slabs8(row + (size_t)(fz.Hq + Hkv + kvh) * D + chunk * 8, fz.S, slab, vx);
+      knew = pack8(kx);
+      vnew = pack8(vx);
+      const int slot = fz.slot_mapping[b];
+      if (slot >= 0) {
+        const size_t off = (((size_t)(slot >> 6) * Hkv + kvh) * 64 + (slot & 63)) * D + chunk * 8;
+        *reinterpret_cast<uint4*>(k_cache + off) = knew;
+        *reinterpret_cast<uint4*>(v_cache + off) = vnew;
+      }
+    }
+  }
+
   for (int i = 0; i < ntile; ++i) {
     wait_vmcnt<8>();                             // tiles i+1, i+2 (4 DMAs each) may fly
     ring_barrier();                              // tile i visible; slot (i-1) % NSR free
@@ -343,11 +430,16 @@ __global__ __launch_bounds__(256) void paged_decode_ring_kernel(
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const int r = wave * 8 + 4 * u + tg;       // token row of the tile
-      ok[u] = i * TT + r < n;
+      ok[u] = i * TT + r < n_ring;
       kr[u] = *reinterpret_cast<const uint4*>(kt + r * D + chunk * 8);
       vr[u] = *reinterpret_cast<const uint4*>(vt + r * D + chunk * 8);
     }
     attend_rows<G, U>(kr, vr, ok, qv, qs, m, l, acc);
+  }
+  if (owns_last && wave == 0 && tg == 0) {       // the new token, from registers
+    const uint4 kr1[1] = {knew}, vr1[1] = {vnew};
+    const bool ok1[1] = {true};
+    attend_rows<G, 1>(kr1, vr1, ok1, qv, qs, m, l, acc);
   }
   wait_vmcnt<0>();                               // drain the clamped tail DMAs
 
@@ -415,14 +507,14 @@ int docqa_paged_decode(const void* q, int q_stride, const void* k_cache, const v
     do {                                                                                      \
       if (direct)                                                                             \
         paged_decode_ring_kernel<GG, true><<<grid, 256, 0, s>>>(                              \
-            (const uint16_t*)q, q_stride, (const uint16_t*)k_cache, (const uint16_t*)v_cache, \
+            (const uint16_t*)q, q_stride, (uint16_t*)k_cache, (uint16_t*)v_cache,             \
             block_tables, maxb, context_lens, tmp_out, tmp_ml, Hkv, max_parts, scale,         \
-            (uint16_t*)out, out_stride);                                                      \
+            (uint16_t*)out, out_stride, FusedQKV{});                                          \
       else                                                                                    \
         paged_decode_ring_kernel<GG, false><<<grid, 256, 0, s>>>(                             \
-            (const uint16_t*)q, q_stride, (const uint16_t*)k_cache, (const uint16_t*)v_cache, \
+            (const uint16_t*)q, q_stride, (uint16_t*)k_cache, (uint16_t*)v_cache,             \
             block_tables, maxb, context_lens, tmp_out, tmp_ml, Hkv, max_parts, scale,         \
-            (uint16_t*)out, out_stride);                                                      \
+            (uint16_t*)out, out_stride, FusedQKV{});                                          \
     } while (0)
     switch (G) {
       case 1: DRING(1); break;
@@ -473,4 +565,43 @@ int docqa_decode_splits(int B, int Hkv, int max_context) {
   if (s > by_len) s = by_len;
   if (s > 64) s = 64;
   return s < 1 ? 1 : s;
+}
+
+// Fused decode step attention: QKV split-K partials [S, B, (Hq + 2 Hkv) * 128] fp32 ->
+// RoPE + paged-cache write of the new token + attention (ring kernel, FUSED mode).
+int docqa_paged_decode_fused(const float* P, int S, const int* positions, const float* cos_sin,
+                             const int* slot_mapping, void* k_cache, void* v_cache,
+                             const int* block_tables, int maxb, const int* context_lens, void* out,
+                             int out_stride, float* tmp_out, float* tmp_ml, int B, int Hq, int Hkv,
+                             int BS, int max_parts, float scale, hipStream_t s) {
+  if (B == 0) return 0;
+  if (BS != 64 || maxb > 256 || Hq % Hkv != 0 || S < 1) return -1;
+  const int G = Hq / Hkv;
+  dim3 grid(max_parts, Hkv, B);
+  const bool direct = max_parts == 1;
+  FusedQKV fz{P, S, positions, cos_sin, slot_mapping, Hq};
+#define DFUSED(GG)                                                                            \
+  do {                                                                                        \
+    if (direct)                                                                               \
+      paged_decode_ring_kernel<GG, true, true><<<grid, 256, 0, s>>>(                          \
+          nullptr, 0, (uint16_t*)k_cache, (uint16_t*)v_cache, block_tables, maxb,             \
+          context_lens, tmp_out, tmp_ml, Hkv, max_parts, scale, (uint16_t*)out, out_stride, fz); \
+    else                                                                                      \
+      paged_decode_ring_kernel<GG, false, true><<<grid, 256, 0, s>>>(                         \
+          nullptr, 0, (uint16_t*)k_cache, (uint16_t*)v_cache, block_tables, maxb,             \
+          context_lens, tmp_out, tmp_ml, Hkv, max_parts, scale, (uint16_t*)out, out_stride, fz); \
+  } while (0)
+  switch (G) {
+    case 1: DFUSED(1); break;
+    case 2: DFUSED(2); break;
+    case 4: DFUSED(4); break;
+    case 8: DFUSED(8); break;
+    default: return -1;
+  }
+#undef DFUSED
+  if (!direct)
+    paged_decode_reduce<128><<<dim3(Hq, B), 128, 0, s>>>(tmp_out, tmp_ml, context_lens,
+                                                         (uint16_t*)out, out_stride, Hq, max_parts);
+  DOCQA_CHECK_LAUNCH();
+  return 0;
 }

@@ -222,13 +222,21 @@ class LlamaModel:
             sd = ops.decode_splits(M, *L0["down"].shape)
         for i, L in enumerate(self.layers):
             kc, vc = kv_caches[i]
-            if sq:
+            if sq and ops.fused_decode_ok(kc, meta.block_tables):
+                # QKV partials -> RoPE + new-token cache write + attention, one launch
+                a = ops.paged_decode_fused(ops.dgemm_partial(x, L["qkv"], sq), meta.positions, self.cos_sin,
+                                           meta.slot_mapping, kc, vc, meta.block_tables, meta.context_lens,
+                                           hq, meta.max_context, self.scale)
+                qkv = None
+            elif sq:
                 qkv = ops.rope_cache_splitk(ops.dgemm_partial(x, L["qkv"], sq), meta.positions, self.cos_sin,
                                             meta.slot_mapping, kc, vc, hq, hkv, D)
             else:
                 qkv = lin(x, L["qkv"])
                 ops.rope_cache(qkv, meta.positions, self.cos_sin, meta.slot_mapping, kc, vc, hq, hkv, D)
-            if meta.prefill and meta.prefix_lens is not None:
+            if qkv is None:
+                pass
+            elif meta.prefill and meta.prefix_lens is not None:
                 # prompt prefix already in the paged cache: attend over cache (prefix + new)
                 a = ops.flash_prefill_paged(qkv, meta.cu_seqlens, meta.max_len, hq, hkv, D, self.scale,
                                             kc, vc, meta.block_tables, meta.prefix_lens)

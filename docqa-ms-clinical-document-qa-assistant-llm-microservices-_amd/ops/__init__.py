@@ -201,6 +201,25 @@ def add_rmsnorm_splitk(P, residual, w, eps: float):
     return ref.add_rmsnorm(P.sum(0).to(residual.dtype).view_as(residual), residual, w, eps)
 
 
+def paged_decode_fused(P, positions, cos_sin, slot_mapping, k_cache, v_cache, block_tables,
+                       context_lens, Hq, max_context, scale):
+    """Decode attention straight from the QKV projection's split-K partial slabs: RoPE,
+    paged-cache write of the new token and attention in one launch (attn_decode.hip ring
+    kernel, FUSED mode).  Same result as rope_cache_splitk + paged_decode."""
+    if _gpu(P):
+        return _native().paged_decode_fused(P, positions, cos_sin, slot_mapping, k_cache, v_cache,
+                                            block_tables, context_lens, Hq, max_context, scale)
+    Hkv, D = k_cache.shape[1], k_cache.shape[3]
+    qkv = rope_cache_splitk(P, positions, cos_sin, slot_mapping, k_cache, v_cache, Hq, Hkv, D)
+    return ref.paged_decode(qkv, k_cache, v_cache, block_tables, context_lens, Hq, max_context, scale)
+
+
+def fused_decode_ok(k_cache, block_tables) -> bool:
+    """Shapes the fused decode attention kernel supports (head_dim 128, 64-token blocks,
+    <= 256 blocks per sequence)."""
+    return k_cache.shape[2] == 64 and k_cache.shape[3] == 128 and block_tables.shape[1] <= 256
+
+
 def rope_cache_splitk(P, positions, cos_sin, slot_mapping, k_cache, v_cache, Hq, Hkv, D):
     """Packed bf16 QKV <- rope(bf16(sum_s P[s])) with the paged-cache write (rope_cache)."""
     if _gpu(P):

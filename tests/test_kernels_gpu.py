@@ -309,6 +309,37 @@ def test_dgemm_glu(native, M, N, K):
     _close(native.silu_mul(gu, interleaved=True), R.silu_mul(gu, interleaved=True), 2e-2, 1e-2)
 
 
+@pytest.mark.parametrize("B,Hkv,S", [(64, 8, 2), (5, 8, 1), (3, 2, 4)])
+def test_paged_decode_fused(native, B, Hkv, S):
+    """RoPE + new-token cache write + attention from QKV split-K partials == the unfused
+    rope_cache_splitk + paged_decode (outputs and cache contents)."""
+    from docqa_amd.ops import reference as R
+
+    G, D, BS, maxb = 4, 128, 64, 16
+    Hq = G * Hkv
+    W = (Hq + 2 * Hkv) * D
+    P = torch.randn(S, B, W, device="cuda") * 0.5
+    pos = torch.randint(0, maxb * BS - 1, (B,), device="cuda", dtype=torch.int32)
+    bt = torch.randperm(B * maxb, device="cuda").int().view(B, maxb)
+    slots = (bt.gather(1, (pos // BS).long()[:, None])[:, 0] * BS + pos % BS).int()
+    slots[B // 2] = -1 if B > 2 else slots[B // 2]
+    cl = pos + 1
+    kc1 = torch.randn(B * maxb, Hkv, BS, D, device="cuda", dtype=torch.bfloat16)
+    vc1 = torch.randn_like(kc1)
+    kc2, vc2 = kc1.clone(), vc1.clone()
+    cs = R.rope_cos_sin(maxb * BS, D, 500000.0, "cuda")
+    scale = 1 / math.sqrt(D)
+    o1 = native.paged_decode_fused(P, pos, cs, slots, kc1, vc1, bt, cl, Hq, maxb * BS, scale)
+    qkv = native.rope_cache_splitk(P, pos, cs, slots, kc2, vc2, Hq, Hkv, D)
+    o2 = native.paged_decode(qkv, kc2, vc2, bt, cl, Hq, maxb * BS, scale)
+    _close(kc1, kc2, 0.0)
+    _close(vc1, vc2, 0.0)
+    # a slot of -1 marks a padded batch row: the unfused path then attends to the stale
+    # cache row, the fused one to the computed token -- only valid rows are compared
+    valid = slots >= 0
+    _close(o1[valid], o2[valid], 2e-2, 1e-2)
+
+
 def test_dgemm_asymmetric_identity(native):
     """X = I rows against an asymmetric W: Y must be W's columns, catches transposed writes."""
     M, N, K = 48, 128, 512
