@@ -100,14 +100,14 @@ def set_state(s: ParallelState) -> None:
 _CUSTOM_AR = None
 
 
-def enable_custom_all_reduce(max_bytes: int = 8 << 20):
+def enable_custom_all_reduce(max_bytes: int = 8 << 20, force: bool = False):
     """Use the one-shot IPC all-reduce (parallel/custom_ar.py) for TP all-reduces that fit
     ``max_bytes`` (bf16, contiguous); RCCL keeps everything else.  Opt-in
     (DOCQA_CUSTOM_AR=1 in bench.py): validated 2-rank on one GPU, not yet on a multi-GPU
     node."""
     global _CUSTOM_AR
     s = _STATE
-    if s.tp_size > 1 and s.backend == "nccl" and _CUSTOM_AR is None:
+    if s.tp_size > 1 and (s.backend == "nccl" or force) and _CUSTOM_AR is None:
         from .custom_ar import CustomAllReduce
         _CUSTOM_AR = CustomAllReduce(group=s.tp_group, max_bytes=max_bytes)
     return _CUSTOM_AR
