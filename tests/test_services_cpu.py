@@ -268,3 +268,43 @@ def test_stack_persistence_resume(stack, tmp_path):
     idx = read_index(stack.indexer.index_path)
     meta = read_metadata(stack.indexer.meta_path)
     assert idx.ntotal == len(meta) == stack.indexer.index.ntotal
+
+
+def test_indexer_group_commit_burst(tmp_path, monkeypatch):
+    """A burst of clean documents is embedded, snapshotted and acked in groups (fewer
+    index snapshots than documents); every document still ends INDEXED, chunked at 500
+    characters, and an idle queue flushes a lone document immediately."""
+    import json as _json
+
+    from docqa_amd.bus.broker import InProcBroker
+    from docqa_amd.config import Settings
+    from docqa_amd.models.bert import BertConfig, BertEncoder
+    from docqa_amd.services.indexer import SemanticIndexer
+    from docqa_amd.text.tokenizer import WordPieceTokenizer
+
+    st = Settings()
+    st.index_dir = str(tmp_path)
+    enc = BertEncoder(BertConfig.preset("tiny-bert"), device="cpu")
+    done = []
+    idx = SemanticIndexer(enc, WordPieceTokenizer(), st, device="cpu", on_indexed=done.append).startup(build_if_missing=False)
+    saves = []
+    orig = idx.save_state
+    monkeypatch.setattr(idx, "save_state", lambda: (saves.append(1), orig())[1])
+    broker = InProcBroker()
+    for i in range(1, 21):
+        broker.publish(st.clean_queue, _json.dumps({"doc_id": i, "original_text_masked": "x" * 1200,
+                                                    "metadata": {}}).encode())
+    idx.start_consumer(broker)
+    for _ in range(400):
+        if len(done) == 20:
+            break
+        time.sleep(0.05)
+    assert sorted(done) == list(range(1, 21))
+    assert idx.index.ntotal == 20 * 3 and len(saves) < 20
+    broker.publish(st.clean_queue, _json.dumps({"doc_id": 21, "original_text_masked": "y" * 10}).encode())
+    for _ in range(200):
+        if 21 in done:
+            break
+        time.sleep(0.05)
+    assert 21 in done and idx.index.ntotal == 61
+    idx.stop_consumer()
