@@ -230,6 +230,41 @@ at::Tensor paged_decode(const at::Tensor& q, const at::Tensor& k_cache, const at
   return out;
 }
 
+// cascade decode attention: the prompt prefix shared by every sequence of the batch
+// (prefix_table: its block ids, prefix_len: device scalar, multiple of 64) is attended once
+// for all rows by the MFMA prefix kernel; each sequence's suffix by the ring kernel
+at::Tensor paged_decode_cascade(const at::Tensor& q, at::Tensor k_cache, at::Tensor v_cache,
+                                const at::Tensor& block_tables, const at::Tensor& context_lens,
+                                int64_t Hq, int64_t max_context, double scale,
+                                const at::Tensor& prefix_table, const at::Tensor& prefix_len,
+                                int64_t nchunk) {
+  CHECK_GPU(q); CHECK_BF16(q); CHECK_BF16(k_cache); CHECK_BF16(v_cache);
+  CHECK_I32(block_tables); CHECK_I32(context_lens); CHECK_CONTIG(block_tables);
+  CHECK_I32(prefix_table); CHECK_I32(prefix_len); CHECK_CONTIG(prefix_table);
+  TORCH_CHECK(q.stride(-1) == 1, "q rows must be contiguous");
+  const int B = q.size(0);
+  const int Hkv = k_cache.size(1), BS = k_cache.size(2), D = k_cache.size(3);
+  TORCH_CHECK(D == 128 && BS == 64 && Hq == 4 * Hkv, "cascade decode: head_dim 128, 64-token blocks, GQA 4");
+  TORCH_CHECK(block_tables.size(1) <= 256, "cascade decode: <= 256 blocks per sequence");
+  TORCH_CHECK(prefix_table.numel() >= 1 && prefix_len.numel() == 1, "cascade decode: prefix table / length");
+  const int max_parts = docqa_decode_splits(B, Hkv, max_context);
+  c10::DeviceGuard g(q.device());
+  auto out = at::empty({B, Hq * D}, q.options());
+  auto f32 = q.options().dtype(at::kFloat);
+  auto tmp_out = at::empty({B, Hq, max_parts, D}, f32);
+  auto tmp_ml = at::empty({B, Hq, max_parts, 2}, f32);
+  auto pacc = at::empty({nchunk, B, Hq, D}, f32);
+  auto pml = at::empty({nchunk, B, Hq, 2}, f32);
+  CHECK_RC(docqa_paged_decode_cascade(q.data_ptr(), q.stride(0), k_cache.data_ptr(), v_cache.data_ptr(),
+                                      block_tables.data_ptr<int>(), block_tables.size(1),
+                                      context_lens.data_ptr<int>(), out.data_ptr(), Hq * D,
+                                      tmp_out.data_ptr<float>(), tmp_ml.data_ptr<float>(), B, Hq, Hkv, BS,
+                                      max_parts, (float)scale, prefix_table.data_ptr<int>(),
+                                      prefix_len.data_ptr<int>(), (int)nchunk, pacc.data_ptr<float>(),
+                                      pml.data_ptr<float>(), stream()), "paged_decode_cascade");
+  return out;
+}
+
 // decode step attention fed by the QKV projection's split-K partial slabs: RoPE + cache
 // write of the new token + paged attention in one launch (ring kernel)
 at::Tensor paged_decode_fused(const at::Tensor& P, const at::Tensor& positions, const at::Tensor& cos_sin,
@@ -312,14 +347,14 @@ at::Tensor gemm(const at::Tensor& a, const at::Tensor& w, const c10::optional<at
   return out;
 }
 
-// skinny decode projection Y = X . W^T for M <= 64 rows (splits = 0: auto split-K)
+// skinny decode projection Y = X . W^T for M <= 128 rows (splits = 0: auto split-K)
 // decode gate|up projection with fused SwiGLU: x [M, K], w [2I, K] (8-interleaved) -> [M, I]
 at::Tensor dgemm_glu(const at::Tensor& x, const at::Tensor& w) {
   CHECK_GPU(x); CHECK_BF16(x); CHECK_BF16(w); CHECK_CONTIG(x); CHECK_CONTIG(w);
   const int K = x.size(-1), N = w.size(0);
   TORCH_CHECK(w.size(1) == K && N % 16 == 0, "dgemm_glu: shape mismatch");
   const int M = x.numel() / K;
-  TORCH_CHECK(M <= 64, "dgemm_glu: at most 64 rows");
+  TORCH_CHECK(M <= 128, "dgemm_glu: at most 128 rows");
   auto sizes = x.sizes().vec();
   sizes.back() = N / 2;
   c10::DeviceGuard g(x.device());
@@ -334,7 +369,7 @@ at::Tensor dgemm_partial(const at::Tensor& x, const at::Tensor& w, int64_t split
   const int K = x.size(-1), N = w.size(0);
   TORCH_CHECK(w.size(1) == K, "dgemm_partial: K mismatch");
   const int M = x.numel() / K;
-  TORCH_CHECK(M <= 64 && splits >= 1, "dgemm_partial: at most 64 rows, splits >= 1");
+  TORCH_CHECK(M <= 128 && splits >= 1, "dgemm_partial: at most 128 rows, splits >= 1");
   c10::DeviceGuard g(x.device());
   auto part = at::empty({splits, M, N}, x.options().dtype(at::kFloat));
   CHECK_RC(docqa_dgemm_partial(x.data_ptr(), w.data_ptr(), part.data_ptr<float>(), M, N, K, (int)splits,
@@ -347,7 +382,7 @@ at::Tensor dgemm(const at::Tensor& x, const at::Tensor& w, int64_t splits) {
   const int K = x.size(-1), N = w.size(0);
   TORCH_CHECK(w.size(1) == K, "dgemm: K mismatch");
   const int M = x.numel() / K;
-  TORCH_CHECK(M <= 64, "dgemm: at most 64 rows");
+  TORCH_CHECK(M <= 128, "dgemm: at most 128 rows");
   const int S = splits > 0 ? (int)splits : docqa_dgemm_splits(N, K);
   auto sizes = x.sizes().vec();
   sizes.back() = N;
@@ -514,6 +549,9 @@ TORCH_LIBRARY(docqa, m) {
   m.def("dgemm(Tensor x, Tensor w, int splits) -> Tensor");
   m.def("dgemm_partial(Tensor x, Tensor w, int splits, int tile_rows=64) -> Tensor");
   m.def("dgemm_glu(Tensor x, Tensor w) -> Tensor");
+  m.def("paged_decode_cascade(Tensor q, Tensor k_cache, Tensor v_cache, Tensor block_tables, "
+        "Tensor context_lens, int Hq, int max_context, float scale, Tensor prefix_table, Tensor prefix_len, "
+        "int nchunk) -> Tensor");
   m.def("paged_decode_fused(Tensor P, Tensor positions, Tensor cos_sin, Tensor slot_mapping, "
         "Tensor(a!) k_cache, Tensor(b!) v_cache, Tensor block_tables, Tensor context_lens, int Hq, "
         "int max_context, float scale) -> Tensor");
@@ -552,6 +590,7 @@ TORCH_LIBRARY_IMPL(docqa, CUDA, m) {
   m.impl("dgemm_partial", &dgemm_partial);
   m.impl("dgemm_glu", &dgemm_glu);
   m.impl("paged_decode_fused", &paged_decode_fused);
+  m.impl("paged_decode_cascade", &paged_decode_cascade);
   m.impl("ar_oneshot", &ar_oneshot);
   m.impl("add_rmsnorm_splitk", &add_rmsnorm_splitk);
   m.impl("rope_cache_splitk", &rope_cache_splitk);

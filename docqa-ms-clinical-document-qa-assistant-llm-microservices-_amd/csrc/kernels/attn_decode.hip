@@ -27,6 +27,7 @@
 // (llm-qa/main.py:69, greedy decode loop of RetrievalQA.invoke at llm-qa/main.py:117).
 #include "docqa_common.h"
 #include "docqa_asm.h"
+#include "docqa_cascade.h"
 #include <float.h>
 #include <stdlib.h>
 
@@ -104,7 +105,7 @@ __device__ __forceinline__ void finish_partition(
     float (&m)[G], float (&l)[G], float (&acc)[G][8], float (*s_acc)[G][D], float (*s_m)[G],
     float (*s_l)[G], int tid, int wave, int tg, int chunk, int b, int kvh, int part, int Hkv,
     int max_parts, float* __restrict__ tmp_out, float* __restrict__ tmp_ml,
-    uint16_t* __restrict__ out, int out_stride) {
+    uint16_t* __restrict__ out, int out_stride, const CascadeIn& ci) {
   // ---- merge the 4 lane-group streams of the wave (lanes l, l^16, l^32, l^48)
 #pragma unroll
   for (int g = 0; g < G; ++g) {
@@ -146,6 +147,33 @@ __device__ __forceinline__ void finish_partition(
     }
     const int h = kvh * G + g;
     if constexpr (DIRECT) {
+      const int np = ci.plen ? cascade_parts(*ci.plen, ci.nchunk) : 0;
+      if (np > 0) {   // cascade: fold in the shared-prefix chunk partials
+        // every chunk's (max, sum, acc) load is issued before the first is used (indices
+        // clamped, extra chunks weighted 0): one memory latency, not 2 x np dependent ones
+        const size_t B = gridDim.z, Hq = (size_t)Hkv * G;
+        float pm[kCascadeMaxChunks], pl[kCascadeMaxChunks], pa[kCascadeMaxChunks];
+#pragma unroll
+        for (int c = 0; c < kCascadeMaxChunks; ++c) {
+          const size_t r = ((size_t)min(c, np - 1) * B + b) * Hq + h;
+          const float2 mlv = *reinterpret_cast<const float2*>(ci.ml + r * 2);
+          pm[c] = c < np ? mlv.x : -FLT_MAX;
+          pl[c] = mlv.y;
+          pa[c] = ci.acc[r * D + d];
+        }
+        float M2 = M;
+#pragma unroll
+        for (int c = 0; c < kCascadeMaxChunks; ++c) M2 = fmaxf(M2, pm[c]);
+        const float f0 = (M == -FLT_MAX) ? 0.f : exp2f(M - M2);
+        v *= f0;
+        lsum *= f0;
+#pragma unroll
+        for (int c = 0; c < kCascadeMaxChunks; ++c) {
+          const float f = (pm[c] == -FLT_MAX) ? 0.f : exp2f(pm[c] - M2);
+          v += f * pa[c];
+          lsum += f * pl[c];
+        }
+      }
       out[(size_t)b * out_stride + (size_t)h * D + d] = f2bf(lsum > 0.f ? v / lsum : 0.f);
     } else {
       const size_t o = ((size_t)b * (Hkv * G) + h) * max_parts + part;
@@ -248,7 +276,7 @@ __global__ __launch_bounds__(256, OCC) void paged_decode_kernel(
   }
 
   finish_partition<G, D, DIRECT>(m, l, acc, s_acc, s_m, s_l, tid, wave, tg, chunk, b, kvh, part,
-                                 Hkv, max_parts, tmp_out, tmp_ml, out, out_stride);
+                                 Hkv, max_parts, tmp_out, tmp_ml, out, out_stride, CascadeIn{});
 }
 
 // LDS-DMA ring variant (BS = 64, D = 128).  The register kernel above is capped by the
@@ -307,7 +335,7 @@ __global__ __launch_bounds__(256) void paged_decode_ring_kernel(
     uint16_t* __restrict__ v_cache, const int* __restrict__ block_tables, int maxb,
     const int* __restrict__ context_lens, float* __restrict__ tmp_out,
     float* __restrict__ tmp_ml, int Hkv, int max_parts, float scale,
-    uint16_t* __restrict__ out, int out_stride, FusedQKV fz) {
+    uint16_t* __restrict__ out, int out_stride, FusedQKV fz, CascadeIn ci) {
   constexpr int D = 128, TT = 32, NSR = 4, U = 2;
   constexpr int TILE = TT * D;                   // elements of one K (or V) tile: 8 KB
   __shared__ __attribute__((aligned(16))) uint16_t ring[NSR * 2 * TILE];   // 64 KB
@@ -317,8 +345,11 @@ __global__ __launch_bounds__(256) void paged_decode_ring_kernel(
 
   const int part = blockIdx.x, kvh = blockIdx.y, b = blockIdx.z;
   const int L = context_lens[b];
-  const int slice = split_chunk(L, max_parts);   // multiple of 64
-  const int start = part * slice;
+  // cascade: keys [0, P) are the shared prefix (attended by the prefix kernel), this
+  // kernel covers the sequence's own suffix [P, L); P is a multiple of 64
+  const int P = ci.plen ? *ci.plen : 0;
+  const int slice = split_chunk(L - P, max_parts);   // multiple of 64
+  const int start = P + part * slice;
   if (start >= L) return;
   const int n = min(L - start, slice);
   const int tid = threadIdx.x, lane = tid & 63;
@@ -444,27 +475,42 @@ __global__ __launch_bounds__(256) void paged_decode_ring_kernel(
   wait_vmcnt<0>();                               // drain the clamped tail DMAs
 
   finish_partition<G, D, DIRECT>(m, l, acc, s_acc, s_m, s_l, tid, wave, tg, chunk, b, kvh, part,
-                                 Hkv, max_parts, tmp_out, tmp_ml, out, out_stride);
+                                 Hkv, max_parts, tmp_out, tmp_ml, out, out_stride, ci);
 }
 
+// log-sum-exp merge of a sequence's context partitions (and, cascade, of the shared-prefix
+// chunk partials) -> normalised bf16 output
 template <int D>
 __global__ __launch_bounds__(D) void paged_decode_reduce(const float* __restrict__ tmp_out,
                                                          const float* __restrict__ tmp_ml,
                                                          const int* __restrict__ context_lens,
                                                          uint16_t* __restrict__ out,
-                                                         int out_stride, int Hq, int max_parts) {
+                                                         int out_stride, int Hq, int max_parts,
+                                                         CascadeIn ci = CascadeIn{}) {
   const int h = blockIdx.x, b = blockIdx.y, d = threadIdx.x;
-  const int L = context_lens[b];
+  const int P = ci.plen ? *ci.plen : 0;
+  const int L = context_lens[b] - P;
+  if (L <= 0) return;
   const int chunk = split_chunk(L, max_parts);
   const int np = min(max_parts, (L + chunk - 1) / chunk);
+  const int nc = ci.plen ? cascade_parts(P, ci.nchunk) : 0;
   const size_t base = ((size_t)b * Hq + h) * max_parts;
+  const size_t B = gridDim.y;
   float M = -FLT_MAX;
   for (int p = 0; p < np; ++p) M = fmaxf(M, tmp_ml[(base + p) * 2]);
+  for (int c = 0; c < nc; ++c) M = fmaxf(M, ci.ml[((c * B + b) * Hq + h) * 2]);
   float num = 0.f, den = 0.f;
   for (int p = 0; p < np; ++p) {
     const float w = exp2f(tmp_ml[(base + p) * 2] - M);
     num += w * tmp_out[(base + p) * D + d];
     den += w * tmp_ml[(base + p) * 2 + 1];
+  }
+  for (int c = 0; c < nc; ++c) {
+    const size_t r = (c * B + b) * Hq + h;
+    const float pm = ci.ml[r * 2];
+    const float w = (pm == -FLT_MAX) ? 0.f : exp2f(pm - M);
+    num += w * ci.acc[r * D + d];
+    den += w * ci.ml[r * 2 + 1];
   }
   out[(size_t)b * out_stride + (size_t)h * D + d] = f2bf(den > 0.f ? num / den : 0.f);
 }
@@ -509,12 +555,12 @@ int docqa_paged_decode(const void* q, int q_stride, const void* k_cache, const v
         paged_decode_ring_kernel<GG, true><<<grid, 256, 0, s>>>(                              \
             (const uint16_t*)q, q_stride, (uint16_t*)k_cache, (uint16_t*)v_cache,             \
             block_tables, maxb, context_lens, tmp_out, tmp_ml, Hkv, max_parts, scale,         \
-            (uint16_t*)out, out_stride, FusedQKV{});                                          \
+            (uint16_t*)out, out_stride, FusedQKV{}, CascadeIn{});                                          \
       else                                                                                    \
         paged_decode_ring_kernel<GG, false><<<grid, 256, 0, s>>>(                             \
             (const uint16_t*)q, q_stride, (uint16_t*)k_cache, (uint16_t*)v_cache,             \
             block_tables, maxb, context_lens, tmp_out, tmp_ml, Hkv, max_parts, scale,         \
-            (uint16_t*)out, out_stride, FusedQKV{});                                          \
+            (uint16_t*)out, out_stride, FusedQKV{}, CascadeIn{});                                          \
     } while (0)
     switch (G) {
       case 1: DRING(1); break;
@@ -585,11 +631,11 @@ int docqa_paged_decode_fused(const float* P, int S, const int* positions, const 
     if (direct)                                                                               \
       paged_decode_ring_kernel<GG, true, true><<<grid, 256, 0, s>>>(                          \
           nullptr, 0, (uint16_t*)k_cache, (uint16_t*)v_cache, block_tables, maxb,             \
-          context_lens, tmp_out, tmp_ml, Hkv, max_parts, scale, (uint16_t*)out, out_stride, fz); \
+          context_lens, tmp_out, tmp_ml, Hkv, max_parts, scale, (uint16_t*)out, out_stride, fz, CascadeIn{}); \
     else                                                                                      \
       paged_decode_ring_kernel<GG, false, true><<<grid, 256, 0, s>>>(                         \
           nullptr, 0, (uint16_t*)k_cache, (uint16_t*)v_cache, block_tables, maxb,             \
-          context_lens, tmp_out, tmp_ml, Hkv, max_parts, scale, (uint16_t*)out, out_stride, fz); \
+          context_lens, tmp_out, tmp_ml, Hkv, max_parts, scale, (uint16_t*)out, out_stride, fz, CascadeIn{}); \
   } while (0)
   switch (G) {
     case 1: DFUSED(1); break;
@@ -602,6 +648,41 @@ int docqa_paged_decode_fused(const float* P, int S, const int* positions, const 
   if (!direct)
     paged_decode_reduce<128><<<dim3(Hq, B), 128, 0, s>>>(tmp_out, tmp_ml, context_lens,
                                                          (uint16_t*)out, out_stride, Hq, max_parts);
+  DOCQA_CHECK_LAUNCH();
+  return 0;
+}
+
+int docqa_cascade_prefix(const void* qkv, int row_stride, int rows, int Hq, int Hkv, float scale,
+                         const void* k_cache, const void* v_cache, const int* prefix_table,
+                         const int* plen, int BS, int nchunk, float* acc, float* ml, hipStream_t s);
+
+// Cascade decode attention (docqa_cascade.h): MFMA prefix partials over the shared prompt
+// prefix [0, *plen) for all B rows, then the ring kernel over each suffix [*plen, L) with
+// the prefix partials merged before normalisation.  q: post-RoPE rows of the packed QKV
+// buffer (row stride q_stride), the step's new K/V already in the cache.
+int docqa_paged_decode_cascade(const void* q, int q_stride, void* k_cache, void* v_cache,
+                               const int* block_tables, int maxb, const int* context_lens, void* out,
+                               int out_stride, float* tmp_out, float* tmp_ml, int B, int Hq, int Hkv,
+                               int BS, int max_parts, float scale, const int* prefix_table,
+                               const int* plen, int nchunk, float* pacc, float* pml, hipStream_t s) {
+  if (B == 0) return 0;
+  if (BS != 64 || maxb > 256 || Hq != 4 * Hkv || nchunk < 1 || nchunk > kCascadeMaxChunks) return -1;
+  int rc = docqa_cascade_prefix(q, q_stride, B, Hq, Hkv, scale, k_cache, v_cache, prefix_table, plen,
+                                BS, nchunk, pacc, pml, s);
+  if (rc) return rc;
+  const CascadeIn ci{pacc, pml, plen, nchunk};
+  dim3 grid(max_parts, Hkv, B);
+  if (max_parts == 1)
+    paged_decode_ring_kernel<4, true><<<grid, 256, 0, s>>>(
+        (const uint16_t*)q, q_stride, (uint16_t*)k_cache, (uint16_t*)v_cache, block_tables, maxb,
+        context_lens, tmp_out, tmp_ml, Hkv, max_parts, scale, (uint16_t*)out, out_stride, FusedQKV{}, ci);
+  else {
+    paged_decode_ring_kernel<4, false><<<grid, 256, 0, s>>>(
+        (const uint16_t*)q, q_stride, (uint16_t*)k_cache, (uint16_t*)v_cache, block_tables, maxb,
+        context_lens, tmp_out, tmp_ml, Hkv, max_parts, scale, (uint16_t*)out, out_stride, FusedQKV{}, ci);
+    paged_decode_reduce<128><<<dim3(Hq, B), 128, 0, s>>>(tmp_out, tmp_ml, context_lens, (uint16_t*)out,
+                                                         out_stride, Hq, max_parts, ci);
+  }
   DOCQA_CHECK_LAUNCH();
   return 0;
 }

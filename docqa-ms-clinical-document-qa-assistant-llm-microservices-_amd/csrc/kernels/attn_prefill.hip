@@ -27,6 +27,7 @@
 // and the MiniLM encoder attention inside sentence-transformers
 // (semantic-indexer/indexer.py:37).
 #include "docqa_common.h"
+#include "docqa_cascade.h"
 #include <float.h>
 
 using namespace docqa;
@@ -63,10 +64,16 @@ struct PagedKV {
   int log2BS;
 };
 
-template <int D, bool CAUSAL, bool PAGED, int G, int WPH>
+// PFX (cascade decode, docqa_cascade.h): the query rows are the B sequences of a decode
+// step (one new token each, rows of the packed QKV buffer), the keys are one chunk
+// (blockIdx.z) of the prompt prefix they all share, read through the shared block table
+// (row 0 of pk.block_tables), no causal mask; the epilogue writes the un-normalised
+// accumulator and (max, sum) of the chunk instead of normalised bf16 rows.
+template <int D, bool CAUSAL, bool PAGED, int G, int WPH, bool PFX = false>
 __global__ __launch_bounds__(64 * G * WPH) void flash_prefill_kernel(
     const uint16_t* __restrict__ qkv, int row_stride, const int* __restrict__ cu_seqlens,
-    uint16_t* __restrict__ out, int o_stride, int Hq, int Hkv, float scale, PagedKV pk) {
+    uint16_t* __restrict__ out, int o_stride, int Hq, int Hkv, float scale, PagedKV pk,
+    CascadeOut co) {
   constexpr int NT = 64 * G * WPH;              // threads
   constexpr int QBW = 32 * WPH;                 // query rows per workgroup
   __shared__ __attribute__((aligned(16))) uint16_t smem[2 * KB * D];
@@ -74,16 +81,27 @@ __global__ __launch_bounds__(64 * G * WPH) void flash_prefill_kernel(
   uint16_t* sV = smem + KB * D;
 
   const int qt = blockIdx.x, hb = blockIdx.y, b = blockIdx.z;
-  const int seq0 = cu_seqlens[b];
-  const int L = cu_seqlens[b + 1] - seq0;
+  int seq0, L, kv_beg = 0, pfx_end = 0;
+  if constexpr (PFX) {
+    seq0 = 0;
+    L = co.rows;
+    const int Lp = *co.plen;
+    const int ck = cascade_chunk(Lp, co.nchunk);
+    kv_beg = b * ck;                              // this chunk's keys: [kv_beg, pfx_end)
+    if (kv_beg >= Lp) return;
+    pfx_end = min(Lp, kv_beg + ck);
+  } else {
+    seq0 = cu_seqlens[b];
+    L = cu_seqlens[b + 1] - seq0;
+  }
   const int q_start = qt * QBW;
   if (q_start >= L) return;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   // G > 1: blockIdx.y is the KV head and wave / WPH picks the query head of its group
   const int h = G > 1 ? hb * G + wave / WPH : hb;
   const int kvh = G > 1 ? hb : h / (Hq / Hkv);
-  const int P0 = PAGED ? pk.ctx_start[b] : 0;   // absolute position of query row 0
-  const int Lk = P0 + L;                         // keys visible to this sequence
+  const int P0 = (PAGED && !PFX) ? pk.ctx_start[b] : 0;   // absolute position of query row 0
+  const int Lk = PFX ? pfx_end : P0 + L;         // keys visible to this sequence
 
   const int l32 = lane & 31, hh = lane >> 5;
   const int q_wave = q_start + (wave % WPH) * 32;   // first query row of this wave
@@ -115,6 +133,7 @@ __global__ __launch_bounds__(64 * G * WPH) void flash_prefill_kernel(
 
   const int kv_end = CAUSAL ? min(Lk, P0 + q_start + QBW) : Lk;
   const int ntiles = (kv_end + KB - 1) / KB;
+  const int t_beg = kv_beg / KB;
   const uint16_t* kbase = qkv + (size_t)seq0 * row_stride + (size_t)(Hq + kvh) * D;
   const uint16_t* vbase = qkv + (size_t)seq0 * row_stride + (size_t)(Hq + Hkv + kvh) * D;
 
@@ -128,7 +147,7 @@ __global__ __launch_bounds__(64 * G * WPH) void flash_prefill_kernel(
       const int key = t * KB + row;
       if (idx < KB * NCH && key < Lk) {
         if constexpr (PAGED) {
-          const int blk = pk.block_tables[(size_t)b * pk.maxb + (key >> pk.log2BS)];
+          const int blk = pk.block_tables[(size_t)(PFX ? 0 : b) * pk.maxb + (key >> pk.log2BS)];
           const size_t off = (((size_t)blk * Hkv + kvh) * pk.BS + (key & (pk.BS - 1))) * D + ch * 8;
           rk[i] = *reinterpret_cast<const uint4*>(pk.k + off);
           rv[i] = *reinterpret_cast<const uint4*>(pk.v + off);
@@ -153,14 +172,14 @@ __global__ __launch_bounds__(64 * G * WPH) void flash_prefill_kernel(
     }
   };
 
-  load_tile(0);
+  load_tile(t_beg);
   store_tile();
   __syncthreads();
 
   // tr-read lane geometry (see header): group gi = lane>>4, q = (lane&15)>>2, p = lane&3
   const int gi = lane >> 4, tq = (lane & 15) >> 2, tp = lane & 3;
 
-  for (int t = 0; t < ntiles; ++t) {
+  for (int t = t_beg; t < ntiles; ++t) {
     if (t + 1 < ntiles) load_tile(t + 1);
     const int kb = t * KB;
     // a wave whose rows all precede this tile's first key contributes nothing (causal),
@@ -248,6 +267,22 @@ __global__ __launch_bounds__(64 * G * WPH) void flash_prefill_kernel(
     }
   }
 
+  if constexpr (PFX) {   // chunk partial: un-normalised O and (max, sum) per (row, head)
+    if (my_q < L) {
+      const size_t r = ((size_t)b * L + my_q) * Hq + h;
+      float* ap = co.acc + r * D;
+#pragma unroll
+      for (int dt = 0; dt < NDT; ++dt)
+#pragma unroll
+        for (int g4 = 0; g4 < 4; ++g4) {
+          const int d0 = dt * 32 + 8 * g4 + 4 * hh;
+          *reinterpret_cast<float4*>(ap + d0) =
+              make_float4(o[dt][4 * g4 + 0], o[dt][4 * g4 + 1], o[dt][4 * g4 + 2], o[dt][4 * g4 + 3]);
+        }
+      if (hh == 0) *reinterpret_cast<float2*>(co.ml + r * 2) = make_float2(m_run, l_run);
+    }
+    return;
+  }
   // ---- epilogue: O[q][dim] = O^T[dim][q] / l
   if (my_q < L) {
     const float inv = l_run > 0.f ? 1.f / l_run : 0.f;
@@ -273,12 +308,13 @@ static void launch_prefill(dim3 grid, hipStream_t s, int causal, const void* qkv
   const uint16_t* q = (const uint16_t*)qkv;
   uint16_t* o = (uint16_t*)out;
   constexpr int NT = 64 * G * WPH;
+  const CascadeOut co{};
   if (pk.k) {
-    flash_prefill_kernel<D, true, true, G, WPH><<<grid, NT, 0, s>>>(q, row_stride, cu, o, o_stride, Hq, Hkv, scale, pk);
+    flash_prefill_kernel<D, true, true, G, WPH><<<grid, NT, 0, s>>>(q, row_stride, cu, o, o_stride, Hq, Hkv, scale, pk, co);
   } else if (causal) {
-    flash_prefill_kernel<D, true, false, G, WPH><<<grid, NT, 0, s>>>(q, row_stride, cu, o, o_stride, Hq, Hkv, scale, pk);
+    flash_prefill_kernel<D, true, false, G, WPH><<<grid, NT, 0, s>>>(q, row_stride, cu, o, o_stride, Hq, Hkv, scale, pk, co);
   } else {
-    flash_prefill_kernel<D, false, false, G, WPH><<<grid, NT, 0, s>>>(q, row_stride, cu, o, o_stride, Hq, Hkv, scale, pk);
+    flash_prefill_kernel<D, false, false, G, WPH><<<grid, NT, 0, s>>>(q, row_stride, cu, o, o_stride, Hq, Hkv, scale, pk, co);
   }
 }
 
@@ -327,4 +363,22 @@ int docqa_flash_prefill_paged(const void* qkv, int row_stride, const int* cu_seq
   PagedKV pk{(const uint16_t*)k_cache, (const uint16_t*)v_cache, block_tables, maxb, ctx_start, BS, log2BS};
   return prefill_dispatch(s, B, max_len, head_dim, 1, qkv, row_stride, cu_seqlens, out, o_stride, Hq, Hkv,
                           scale, pk);
+}
+
+// Cascade decode, prefix part: chunk partials of the B decode queries (rows of the packed
+// QKV buffer, post-RoPE) against the shared prompt prefix [0, *plen) of the 64-token
+// blocks listed in prefix_table.  Llama-3 GQA shape only (head_dim 128, 4 query heads per
+// KV head): one workgroup per (64 rows, KV head, key chunk), 8 waves.
+int docqa_cascade_prefix(const void* qkv, int row_stride, int rows, int Hq, int Hkv, float scale,
+                         const void* k_cache, const void* v_cache, const int* prefix_table,
+                         const int* plen, int BS, int nchunk, float* acc, float* ml, hipStream_t s) {
+  if (rows == 0) return 0;
+  if (Hq != 4 * Hkv || BS != 64 || nchunk < 1) return -1;
+  PagedKV pk{(const uint16_t*)k_cache, (const uint16_t*)v_cache, prefix_table, 0, nullptr, BS, 6};
+  const CascadeOut co{acc, ml, plen, nchunk, rows};
+  dim3 grid((rows + 63) / 64, Hkv, nchunk);
+  flash_prefill_kernel<128, false, true, 4, 2, true><<<grid, 512, 0, s>>>(
+      (const uint16_t*)qkv, row_stride, nullptr, nullptr, 0, Hq, Hkv, scale, pk, co);
+  DOCQA_CHECK_LAUNCH();
+  return 0;
 }

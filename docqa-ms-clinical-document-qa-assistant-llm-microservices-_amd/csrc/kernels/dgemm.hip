@@ -1,5 +1,5 @@
 // dgemm.hip -- skinny "decode GEMM" for the Llama generator's per-token projections:
-//   Y[M, N] = X[M, K] . W[N, K]^T,   M = decode batch (<= 64), weights streamed once.
+//   Y[M, N] = X[M, K] . W[N, K]^T,   M = decode batch (<= 128), weights streamed once.
 //
 // At M <= 64 a projection is a weight-streaming problem (<= 64 FLOP per weight byte, far
 // below the MFMA roof), so the design is about HBM bytes in flight (Little's law: ~8 TB/s x
@@ -23,7 +23,10 @@
 //     and no separate silu_mul launch.  7 n-tiles per workgroup (112 rows) make the Llama-3-8B
 //     shape exactly 256 workgroups = one per CU, and halve the L2 traffic of re-reading X
 //     per workgroup (at M = 64 that X traffic, not HBM, was the limiter).
-// Shapes: N % (16 NT) == 0, (K / S) % 512 == 0 (whole 4-stage ring turns), M <= 64.
+//   * 65..128 rows: each wave owns two 16-row m-tiles over the whole k-block, so every
+//     B fragment read from the LDS ring feeds two MFMAs and the weights still stream from
+//     HBM exactly once (a second pass over 64-row halves would read them twice).
+// Shapes: N % (16 NT) == 0, (K / S) % 512 == 0 (whole 4-stage ring turns), M <= 128.
 #include "docqa_common.h"
 #include "docqa_asm.h"
 #include <stdlib.h>
@@ -31,7 +34,7 @@
 using namespace docqa;
 
 namespace {
-constexpr int BN = 64, BKD = 128, NS = 4, MR = 64;   // NS: default ring slots, K granule 4 stages
+constexpr int BN = 64, BKD = 128, NS = 4, MR = 128;   // NS: default ring slots, K granule 4 stages
 constexpr int KSTEPS = BKD / 32;               // 16x16x32 k-steps per stage
 enum { EPI_BF16 = 0, EPI_PARTIAL = 1, EPI_GLU = 2 };
 typedef __attribute__((address_space(3))) void lds_void;
@@ -52,8 +55,11 @@ __device__ __forceinline__ void wait_vm_n(bf16x8 (&x)[SPW]) {
     asm volatile("s_waitcnt vmcnt(%1)" : "+v"(x[0]) : "i"(N) : "memory");
   else if constexpr (SPW == 2)
     asm volatile("s_waitcnt vmcnt(%2)" : "+v"(x[0]), "+v"(x[1]) : "i"(N) : "memory");
-  else
+  else if constexpr (SPW == 4)
     asm volatile("s_waitcnt vmcnt(%4)" : "+v"(x[0]), "+v"(x[1]), "+v"(x[2]), "+v"(x[3]) : "i"(N) : "memory");
+  else
+    asm volatile("s_waitcnt vmcnt(%8)" : "+v"(x[0]), "+v"(x[1]), "+v"(x[2]), "+v"(x[3]), "+v"(x[4]), "+v"(x[5]),
+                 "+v"(x[6]), "+v"(x[7]) : "i"(N) : "memory");
 }
 
 // keep x's registers allocated up to this point (for loads that are drained, never read)
@@ -74,19 +80,24 @@ __device__ __forceinline__ float row_swap8(float v) {
   return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x128, 0xf, 0xf, false));
 }
 
-// Wave roles: MT m-tiles of 16 X rows; the 4 waves split as (m-tile = wave % MT,
+// Wave roles: MT m-tiles of 16 X rows.  MT <= 4: the 4 waves split as (m-tile = wave % MT,
 // k-group = wave / MT) so every wave owns a disjoint (rows x k) piece of the product and
-// the W stage in LDS (NT 16-row n-tiles) is shared by all of them.  KW = 4 / MT k-groups
-// are summed through LDS at the end.
+// the W stage in LDS (NT 16-row n-tiles) is shared by all of them; KW = 4 / MT k-groups
+// are summed through LDS at the end.  MT = 8: wave w owns m-tiles 2w, 2w+1 (MPW = 2) over
+// the whole k-block (KW = 1).
 template <int EPI, int MT, int NT, int NSR>
 __global__ __launch_bounds__(256) void dgemm_kernel(const uint16_t* __restrict__ X,
                                                     const uint16_t* __restrict__ W,
                                                     uint16_t* __restrict__ Y,
                                                     float* __restrict__ P, int M, int N, int K,
                                                     int Ks) {
-  constexpr int KW = 4 / MT, SPW = KSTEPS / KW;
-  constexpr int STAGE = NT * 16 * BKD;         // elements of one W stage (NT x 4 KB)
+  constexpr int MPW = MT > 4 ? MT / 4 : 1;       // m-tiles per wave
+  constexpr int MTW = MT > 4 ? 4 : MT;           // wave groups along m
+  constexpr int KW = 4 / MTW, SPW = KSTEPS / KW;
+  constexpr int XR = MPW * SPW;                  // X fragments per wave per stage
+  constexpr int STAGE = NT * 16 * BKD;           // elements of one W stage (NT x 4 KB)
   static_assert(NSR >= 4, "ring needs >= 4 slots");
+  static_assert(MT <= 4 || MT == 8, "MT in {1, 2, 4, 8}");
   __shared__ __attribute__((aligned(16))) uint16_t sw[NSR * STAGE];   // W ring
   const int n0 = blockIdx.x * NT * 16;
   const int slice = blockIdx.y;
@@ -95,14 +106,20 @@ __global__ __launch_bounds__(256) void dgemm_kernel(const uint16_t* __restrict__
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int fr = lane & 15, fq = lane >> 4;
-  const int mt = wave % MT, kg = wave / MT;
-  const int xr = min(mt * 16 + fr, M - 1);
-  const uint16_t* xrow = X + (size_t)xr * K + kbeg + kg * SPW * 32 + fq * 8;
+  const int mt = wave % MTW, kg = wave / MTW;
+  const uint16_t* xrow[MPW];
+#pragma unroll
+  for (int mi = 0; mi < MPW; ++mi) {
+    const int xr = min((mt * MPW + mi) * 16 + fr, M - 1);
+    xrow[mi] = X + (size_t)xr * K + kbeg + kg * SPW * 32 + fq * 8;
+  }
   const uint32_t ring = lds_u32(sw);
 
-  f32x4 acc[NT];
+  f32x4 acc[MPW][NT];
 #pragma unroll
-  for (int i = 0; i < NT; ++i) acc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+  for (int mi = 0; mi < MPW; ++mi)
+#pragma unroll
+    for (int i = 0; i < NT; ++i) acc[mi][i] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   // W stage j -> ring slot j % NS: 4 NT wave-instructions of 64 lanes x 16 B, NT per wave,
   // source XOR-swizzled (the DMA destination is lane-linear).  Past the last stage the
@@ -123,31 +140,35 @@ __global__ __launch_bounds__(256) void dgemm_kernel(const uint16_t* __restrict__
 #pragma unroll
     for (int i = 0; i < NT; ++i) glds16<true>(wsrc[i] + koff, dst + (uint32_t)((i * 4 + wave) * 1024));
   };
-  auto load_x = [&](bf16x8 (&x)[SPW], int j) {
-    const uint16_t* src = xrow + min(j, nkb - 1) * BKD;
-    gload16<0>(x[0], src);
-    if constexpr (SPW > 1) gload16<64>(x[1], src);
-    if constexpr (SPW > 2) { gload16<128>(x[2], src); gload16<192>(x[3], src); }
+  auto load_x = [&](bf16x8 (&x)[XR], int j) {
+#pragma unroll
+    for (int mi = 0; mi < MPW; ++mi) {
+      const uint16_t* src = xrow[mi] + min(j, nkb - 1) * BKD;
+      gload16<0>(x[mi * SPW], src);
+      if constexpr (SPW > 1) gload16<64>(x[mi * SPW + 1], src);
+      if constexpr (SPW > 2) { gload16<128>(x[mi * SPW + 2], src); gload16<192>(x[mi * SPW + 3], src); }
+    }
   };
-  auto mma = [&](const bf16x8 (&x)[SPW], int j) {
+  auto mma = [&](const bf16x8 (&x)[XR], int j) {
     const uint16_t* src = sw + (j % NSR) * STAGE;
 #pragma unroll
     for (int s = 0; s < SPW; ++s) {
-      const bf16x8 a = x[s];
       const int ch = (kg * SPW + s) * 4 + fq;
 #pragma unroll
       for (int nt = 0; nt < NT; ++nt) {
         const bf16x8 b = *reinterpret_cast<const bf16x8*>(src + w_off(nt * 16 + fr, ch));
-        acc[nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, acc[nt], 0, 0, 0);
+#pragma unroll
+        for (int mi = 0; mi < MPW; ++mi)
+          acc[mi][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(x[mi * SPW + s], b, acc[mi][nt], 0, 0, 0);
       }
     }
   };
   // Issue order per wave (R = NSR): W0 .. W(R-4) X0 W(R-3) X1 W(R-2) | step i: X(i+2)
   // W(i+R-1).  At the top of step i the ops issued after X(i) are one W group, X(i+1) and
-  // one more W group, so vmcnt(2 NT + SPW) retires X(i) and (issued before it) W(i)
+  // one more W group, so vmcnt(2 NT + XR) retires X(i) and (issued before it) W(i)
   // while R-2 W stages stay in flight; the barrier then publishes stage i to every wave
   // and frees slot (i-1) % R for W(i+R-1).
-  bf16x8 x0[SPW], x1[SPW], x2[SPW], x3[SPW];
+  bf16x8 x0[XR], x1[XR], x2[XR], x3[XR];
 #pragma unroll
   for (int j = 0; j <= NSR - 4; ++j) stage_w(j);
   load_x(x0, 0);
@@ -155,7 +176,7 @@ __global__ __launch_bounds__(256) void dgemm_kernel(const uint16_t* __restrict__
   load_x(x1, 1);
   stage_w(NSR - 2);
 #define RING_STEP(I, XC, XN)                                                            \
-  wait_vm_n<2 * NT + SPW>(XC);                                                          \
+  wait_vm_n<2 * NT + XR>(XC);                                                           \
   ring_barrier();                                                                       \
   load_x(XN, (I) + 2);                                                                  \
   stage_w((I) + NSR - 1);                                                               \
@@ -188,23 +209,25 @@ __global__ __launch_bounds__(256) void dgemm_kernel(const uint16_t* __restrict__
   };
   if constexpr (KW == 1) {
 #pragma unroll
-    for (int nt = 0; nt < NT; ++nt)
+    for (int mi = 0; mi < MPW; ++mi)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int row = mt * 16 + fq * 4 + r, col = n0 + nt * 16 + fr;
-        if constexpr (EPI == EPI_GLU) {
-          const float u = row_swap8(acc[nt][r]);
-          if (row < M && (fr & 8) == 0) store_glu(row, col, acc[nt][r], u);
-        } else if (row < M) {
-          store(row, col, acc[nt][r]);
+      for (int nt = 0; nt < NT; ++nt)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int row = (mt * MPW + mi) * 16 + fq * 4 + r, col = n0 + nt * 16 + fr;
+          if constexpr (EPI == EPI_GLU) {
+            const float u = row_swap8(acc[mi][nt][r]);
+            if (row < M && (fr & 8) == 0) store_glu(row, col, acc[mi][nt][r], u);
+          } else if (row < M) {
+            store(row, col, acc[mi][nt][r]);
+          }
         }
-      }
   } else {
     // sum the KW k-groups through LDS (ring is free after the last barrier + wait)
     __syncthreads();
     f32x4* red = reinterpret_cast<f32x4*>(sw);        // [wave][nt][lane] = one slot
 #pragma unroll
-    for (int nt = 0; nt < NT; ++nt) red[(wave * NT + nt) * 64 + lane] = acc[nt];
+    for (int nt = 0; nt < NT; ++nt) red[(wave * NT + nt) * 64 + lane] = acc[0][nt];
     __syncthreads();
     const float* rf = reinterpret_cast<const float*>(sw);
     auto sum_k = [&](int m, int nt, int ln, int r) {
@@ -259,7 +282,8 @@ static void launch_mt(int mt, dim3 grid, hipStream_t s, const uint16_t* x, const
                       uint16_t* y, float* p, int M, int N, int K, int Ks) {
   if (mt == 1) dgemm_kernel<EPI, 1, NT, NSR><<<grid, 256, 0, s>>>(x, w, y, p, M, N, K, Ks);
   else if (mt == 2) dgemm_kernel<EPI, 2, NT, NSR><<<grid, 256, 0, s>>>(x, w, y, p, M, N, K, Ks);
-  else dgemm_kernel<EPI, 4, NT, NSR><<<grid, 256, 0, s>>>(x, w, y, p, M, N, K, Ks);
+  else if (mt <= 4) dgemm_kernel<EPI, 4, NT, NSR><<<grid, 256, 0, s>>>(x, w, y, p, M, N, K, Ks);
+  else dgemm_kernel<EPI, 8, NT, NSR><<<grid, 256, 0, s>>>(x, w, y, p, M, N, K, Ks);
 }
 
 static bool shape_ok(int M, int N, int K, int S, int bn) {

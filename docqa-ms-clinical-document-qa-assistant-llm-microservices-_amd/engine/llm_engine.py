@@ -24,6 +24,7 @@ from dataclasses import dataclass
 
 import torch
 
+from .. import ops
 from ..models.llama import AttnMeta, LlamaModel
 from .kv_cache import KVCache
 
@@ -69,6 +70,10 @@ class _DecodeGraph:
         self.top_k = torch.zeros(bp, dtype=torch.int32, device=dev)
         self.top_p = torch.ones(bp, dtype=torch.float32, device=dev)
         self.out = torch.zeros(bp, dtype=torch.long, device=dev)
+        # cascade decode: block ids / length of the prompt prefix every row shares
+        self.shared_table = torch.zeros(eng.max_blocks_per_seq, dtype=torch.int32, device=dev)
+        self.shared_len = torch.zeros(1, dtype=torch.int32, device=dev)
+        self.cascade = False
         self.greedy = True
         self.graph = None
 
@@ -93,7 +98,13 @@ class LLMEngine:
         self.tune_decode_gemms = os.environ.get("DOCQA_TUNE_DECODE", "1") == "1"
         # reuse KV blocks of shared prompt prefixes (the fixed RAG instruction template)
         self.prefix_cache = prefix_cache and os.environ.get("DOCQA_PREFIX_CACHE", "1") == "1"
-        self._graphs: dict[int, _DecodeGraph] = {}
+        # cascade decode attention (csrc/include/docqa_cascade.h): when every sequence of a
+        # batch starts with the same cached prompt-prefix blocks (the RAG instruction
+        # template), that prefix is attended once per step for the whole batch
+        self.cascade = os.environ.get("DOCQA_CASCADE", "1") == "1"
+        self.cascade_min_tokens = int(os.environ.get("DOCQA_CASCADE_MIN_TOKENS", "128"))
+        self.cascade_min_batch = int(os.environ.get("DOCQA_CASCADE_MIN_BATCH", "4"))
+        self._graphs: dict[tuple, _DecodeGraph] = {}
         self._pool = None
         self.stats = GenStats()
 
@@ -157,6 +168,9 @@ class LLMEngine:
         meta = AttnMeta(prefill=False, positions=g.positions, slot_mapping=slots.int(),
                         block_tables=g.block_tables, context_lens=g.context_lens,
                         max_context=self.max_context)
+        if g.cascade:
+            meta.shared_table, meta.shared_len = g.shared_table, g.shared_len
+            meta.cascade_chunks = self._cascade_chunks(g.bp)
         logits = self.model.forward(g.tokens, meta, self.kv.caches)
         nxt = self._select(logits, g)
         g.out.copy_(nxt)
@@ -173,14 +187,38 @@ class LLMEngine:
         u = torch.rand(full.shape[0], device=full.device)
         return ops.sample(full, g.inv_temp, g.top_k, g.top_p, u)
 
-    def _get_graph(self, bp: int, greedy: bool) -> _DecodeGraph:
-        key = bp * 2 + int(greedy)
+    def _get_graph(self, bp: int, greedy: bool, cascade: bool = False) -> _DecodeGraph:
+        key = (bp, greedy, cascade)
         g = self._graphs.get(key)
         if g is None:
             g = _DecodeGraph(self, bp)
             g.greedy = greedy
+            g.cascade = cascade
             self._graphs[key] = g
         return g
+
+    def _cascade_chunks(self, bp: int) -> int:
+        """Key chunks of the shared-prefix kernel: about 256 workgroups of (64 rows, KV
+        head, chunk) in total, 1..16 chunks (DOCQA_CASCADE_CHUNKS overrides)."""
+        env = int(os.environ.get("DOCQA_CASCADE_CHUNKS", "0"))
+        if env > 0:
+            return env
+        tiles = (bp + 63) // 64 * self.model.hkv
+        return max(1, min(16, 256 // max(1, tiles)))
+
+    def _shared_prefix_blocks(self, tables: list[list[int]], cached: list[int]) -> int:
+        """Number of leading prefix-cache blocks that are the SAME physical blocks in every
+        row of the batch (0 if cascade decode does not apply)."""
+        B, BS = len(tables), self.block_size
+        if (not self.cascade or B < self.cascade_min_batch
+                or not ops.cascade_ok(self.kv.caches[0][0], torch.empty(0, self.max_blocks_per_seq), self.model.hq)):
+            return 0
+        n = min(c // BS for c in cached)
+        first = tables[0]
+        k = 0
+        while k < n and all(t[k] == first[k] for t in tables):
+            k += 1
+        return k if k * BS >= self.cascade_min_tokens else 0
 
     def _capture(self, g: _DecodeGraph) -> None:
         # warm up on a side stream (allocator + hipBLASLt heuristics), then capture.
@@ -261,7 +299,13 @@ class LLMEngine:
                 for p, tb in zip(prompts, tables):
                     alloc.register_prefix(p, tb)
             self.stats.cached_tokens += sum(cached)
-            g = self._get_graph(_bucket(B, self.max_batch) if self.use_graphs else B, greedy)
+            nshared = self._shared_prefix_blocks(tables, cached)
+            g = self._get_graph(_bucket(B, self.max_batch) if self.use_graphs else B, greedy, nshared > 0)
+            if nshared:
+                st = torch.zeros(self.max_blocks_per_seq, dtype=torch.int32)
+                st[:nshared] = torch.tensor(tables[0][:nshared], dtype=torch.int32)
+                g.shared_table.copy_(st.to(dev))
+                g.shared_len.fill_(nshared * self.block_size)
             # state for the first decode step
             bt = torch.zeros(g.bp, self.max_blocks_per_seq, dtype=torch.int32)
             for r, tb in enumerate(tables):

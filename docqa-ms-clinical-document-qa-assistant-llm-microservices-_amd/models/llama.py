@@ -83,6 +83,11 @@ class AttnMeta:
     context_lens: torch.Tensor | None = None  # [B] (decode; includes the new token)
     max_context: int = 0                    # (decode) graph-capture bound
     prefix_lens: torch.Tensor | None = None  # [B] (prefill with prefix-cache hits)
+    # (decode, cascade) prompt prefix shared by every row: its block ids [maxb] and its
+    # length [1] (multiple of the block size), attended once for the whole batch
+    shared_table: torch.Tensor | None = None
+    shared_len: torch.Tensor | None = None
+    cascade_chunks: int = 8
 
 
 class LlamaModel:
@@ -208,28 +213,42 @@ class LlamaModel:
         residual = h
         x = ops.rmsnorm(h, self.layers[0]["in_norm"], eps)
         nl = len(self.layers)
-        # decode steps stream every weight once for <= 64 rows: skinny ring GEMM; at TP=1
+        # decode steps stream every weight once for <= 128 rows: skinny ring GEMM; at TP=1
         # its split-K combine is fused into the consumer (rope / add_rmsnorm), so QKV, O
         # and down leave fp32 partial slabs instead of a bf16 tensor + a reduce launch
         decode = not meta.prefill
         lin = ops.decode_linear if decode else F.linear
         M = x.shape[0]
         sq = so = sd = 0
+        tq = to = td = 64
         if decode and self.tp == 1 and self.layers:
             L0 = self.layers[0]
-            sq = ops.decode_splits(M, *L0["qkv"].shape)
-            so = ops.decode_splits(M, *L0["o"].shape)
-            sd = ops.decode_splits(M, *L0["down"].shape)
+            sq, tq = ops.decode_plan(M, *L0["qkv"].shape)
+            so, to = ops.decode_plan(M, *L0["o"].shape)
+            sd, td = ops.decode_plan(M, *L0["down"].shape)
+        cascade = decode and meta.shared_len is not None
         for i, L in enumerate(self.layers):
             kc, vc = kv_caches[i]
-            if sq and ops.fused_decode_ok(kc, meta.block_tables):
+            if cascade:
+                # shared-prefix decode: RoPE + cache write, then prefix-once + suffix attention
+                if sq:
+                    qkv = ops.rope_cache_splitk(ops.dgemm_partial(x, L["qkv"], sq, tq), meta.positions,
+                                                self.cos_sin, meta.slot_mapping, kc, vc, hq, hkv, D)
+                else:
+                    qkv = lin(x, L["qkv"])
+                    ops.rope_cache(qkv, meta.positions, self.cos_sin, meta.slot_mapping, kc, vc, hq, hkv, D)
+                a = ops.paged_decode_cascade(qkv, kc, vc, meta.block_tables, meta.context_lens, hq,
+                                             meta.max_context, self.scale, meta.shared_table,
+                                             meta.shared_len, meta.cascade_chunks)
+                qkv = None
+            elif sq and ops.fused_decode_ok(kc, meta.block_tables):
                 # QKV partials -> RoPE + new-token cache write + attention, one launch
-                a = ops.paged_decode_fused(ops.dgemm_partial(x, L["qkv"], sq), meta.positions, self.cos_sin,
+                a = ops.paged_decode_fused(ops.dgemm_partial(x, L["qkv"], sq, tq), meta.positions, self.cos_sin,
                                            meta.slot_mapping, kc, vc, meta.block_tables, meta.context_lens,
                                            hq, meta.max_context, self.scale)
                 qkv = None
             elif sq:
-                qkv = ops.rope_cache_splitk(ops.dgemm_partial(x, L["qkv"], sq), meta.positions, self.cos_sin,
+                qkv = ops.rope_cache_splitk(ops.dgemm_partial(x, L["qkv"], sq, tq), meta.positions, self.cos_sin,
                                             meta.slot_mapping, kc, vc, hq, hkv, D)
             else:
                 qkv = lin(x, L["qkv"])
@@ -246,7 +265,7 @@ class LlamaModel:
                 a = ops.paged_decode(qkv, kc, vc, meta.block_tables, meta.context_lens, hq,
                                      meta.max_context, self.scale)
             if so:
-                x = ops.add_rmsnorm_splitk(ops.dgemm_partial(a, L["o"], so), residual, L["post_norm"], eps)
+                x = ops.add_rmsnorm_splitk(ops.dgemm_partial(a, L["o"], so, to), residual, L["post_norm"], eps)
             else:
                 o = comm.tp_all_reduce(lin(a, L["o"]))
                 x = ops.add_rmsnorm(o, residual, L["post_norm"], eps)
@@ -256,7 +275,7 @@ class LlamaModel:
                 g = ops.silu_mul(F.linear(x, L["gate_up"]), interleaved=True)
             nxt = self.layers[i + 1]["in_norm"] if i + 1 < nl else self.final_norm
             if sd:
-                x = ops.add_rmsnorm_splitk(ops.dgemm_partial(g, L["down"], sd), residual, nxt, eps)
+                x = ops.add_rmsnorm_splitk(ops.dgemm_partial(g, L["down"], sd, td), residual, nxt, eps)
             else:
                 m = comm.tp_all_reduce(lin(g, L["down"]))
                 x = ops.add_rmsnorm(m, residual, nxt, eps)

@@ -158,22 +158,44 @@ def linear_fused(x, w, bias=None, residual=None, epi: int = EPI_BIAS):
     return ref.linear_fused(x, w, bias, residual, epi)
 
 
-def decode_splits(M: int, N: int, K: int) -> int:
-    """Split-K count for the skinny decode GEMM (csrc/kernels/dgemm.hip) on an [M, K] x
-    [N, K]^T projection, or 0 where hipBLASLt is faster / the shape is unsupported.
-    Measured per projection at M = 64 (profiles/r1_bench_kernels_dgemm.json): the LM head
-    and, above 32 rows, gate|up stay on hipBLASLt; QKV / O / down use the ring kernel with
-    the smallest split giving >= 192 workgroups."""
-    if M > 64 or N % 64 or N >= 65536 or (N >= 16384 and M > 32):
-        return 0
-    tiles, S = N // 64, 1
+def _splits_for(N: int, K: int, tile: int) -> int:
+    """Smallest split-K count giving >= 192 workgroups of ``tile`` weight rows (whole
+    512-deep ring turns per slice)."""
+    tiles, S = N // tile, 1
     while tiles * S < 192 and K % (2 * S) == 0 and (K // (2 * S)) % 512 == 0:
         S *= 2
     return S if K % S == 0 and (K // S) % 512 == 0 else 0
 
 
+def decode_plan(M: int, N: int, K: int) -> tuple[int, int]:
+    """(split-K count, weight rows per workgroup) of the skinny decode GEMM
+    (csrc/kernels/dgemm.hip) for an [M, K] x [N, K]^T projection; split 0 where hipBLASLt
+    is faster or the shape is unsupported.
+
+    Measured per Llama-3-8B projection (profiles/r1_bench_kernels_dgemm.json at M <= 64,
+    profiles/r1_dgemm_m128_sweep.log at 65-128 rows, weights rotated past the MALL): the
+    LM head and, above 32 rows, gate|up stay on hipBLASLt; at <= 64 rows QKV / O / down use
+    64-row tiles with the smallest split giving >= 192 workgroups; at 65-128 rows 128-row
+    tiles (X re-read from L2 half as often) where such a split exists (QKV S=4: 21.9 us vs
+    hipBLASLt 25.2 at M=128; O S=8: 17.2 vs 24.4), else 64-row tiles (down S=4: 40.7 vs 75.1)."""
+    if M > 128 or N % 64 or N >= 65536 or (N >= 16384 and M > 32):
+        return 0, 64
+    if M <= 64:
+        return _splits_for(N, K, 64), 64
+    if N % 128 == 0:
+        S = _splits_for(N, K, 128)
+        if S and (N // 128) * S >= 192:
+            return S, 128
+    return _splits_for(N, K, 64), 64
+
+
+def decode_splits(M: int, N: int, K: int) -> int:
+    """Split-K count of :func:`decode_plan` (0: use hipBLASLt)."""
+    return decode_plan(M, N, K)[0]
+
+
 def decode_linear(x, w):
-    """x @ w^T for a decode step (<= 64 rows): the skinny weight-streaming MFMA kernel
+    """x @ w^T for a decode step (<= 128 rows): the skinny weight-streaming MFMA kernel
     where it beats hipBLASLt on MI355X, else F.linear."""
     if _gpu(x):
         N, K = w.shape
@@ -263,6 +285,29 @@ def paged_decode(q, k_cache, v_cache, block_tables, context_lens, Hq, max_contex
         return _native().paged_decode(q, k_cache, v_cache, block_tables, context_lens, Hq,
                                       max_context, scale)
     return ref.paged_decode(q, k_cache, v_cache, block_tables, context_lens, Hq, max_context, scale)
+
+
+def cascade_ok(k_cache, block_tables, Hq: int) -> bool:
+    """Shapes the cascade (shared-prefix) decode path supports: Llama-3 GQA (4 query heads
+    per KV head), head_dim 128, 64-token blocks, <= 256 blocks per sequence (the CPU
+    reference path takes any GQA shape)."""
+    if not _gpu(k_cache):
+        return Hq % k_cache.shape[1] == 0
+    return (k_cache.shape[2] == 64 and k_cache.shape[3] == 128 and Hq == 4 * k_cache.shape[1]
+            and block_tables.shape[1] <= 256)
+
+
+def paged_decode_cascade(q, k_cache, v_cache, block_tables, context_lens, Hq, max_context, scale,
+                         prefix_table, prefix_len, nchunk: int = 8):
+    """Decode attention with the batch's shared prompt prefix attended once for all rows
+    (csrc/include/docqa_cascade.h): keys [0, prefix_len) from ``prefix_table``, keys
+    [prefix_len, L) from each row's block table.  Same result as :func:`paged_decode`
+    when the prefix blocks are the ones every row's table starts with."""
+    if _gpu(q):
+        return _native().paged_decode_cascade(q, k_cache, v_cache, block_tables, context_lens, Hq,
+                                              max_context, scale, prefix_table, prefix_len, nchunk)
+    return ref.paged_decode_cascade(q, k_cache, v_cache, block_tables, context_lens, Hq, max_context,
+                                    scale, prefix_table, prefix_len, nchunk)
 
 
 def flash_prefill(qkv, cu_seqlens, max_len, Hq, Hkv, D, scale, causal=True):

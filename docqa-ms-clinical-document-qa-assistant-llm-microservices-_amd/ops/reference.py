@@ -166,6 +166,33 @@ def paged_decode(q, k_cache, v_cache, block_tables, context_lens, Hq, max_contex
     return out
 
 
+def paged_decode_cascade(q, k_cache, v_cache, block_tables, context_lens, Hq, max_context, scale,
+                         prefix_table, prefix_len, nchunk=8):
+    """Cascade decode attention: keys [0, P) come from the shared ``prefix_table`` blocks,
+    keys [P, L) from each sequence's own block table (one softmax over both)."""
+    B = q.shape[0]
+    NB, Hkv, BS, D = k_cache.shape
+    G = Hq // Hkv
+    P = int(prefix_len.reshape(-1)[0])
+    pb = prefix_table.reshape(-1)[: P // BS].long()
+    kp = k_cache[pb].permute(1, 0, 2, 3).reshape(Hkv, -1, D).float()
+    vp = v_cache[pb].permute(1, 0, 2, 3).reshape(Hkv, -1, D).float()
+    out = torch.zeros(B, Hq * D, dtype=q.dtype, device=q.device)
+    for b in range(B):
+        L = int(context_lens[b])
+        if L <= P:
+            continue
+        nblk = (L + BS - 1) // BS
+        blocks = block_tables[b, P // BS:nblk].long()
+        ks = k_cache[blocks].permute(1, 0, 2, 3).reshape(Hkv, -1, D)[:, : L - P].float()
+        vs = v_cache[blocks].permute(1, 0, 2, 3).reshape(Hkv, -1, D)[:, : L - P].float()
+        k, v = torch.cat([kp, ks], 1), torch.cat([vp, vs], 1)
+        qb = q[b, : Hq * D].view(Hkv, G, D).float()
+        p = torch.softmax(torch.einsum("hgd,htd->hgt", qb, k) * scale, -1)
+        out[b] = torch.einsum("hgt,htd->hgd", p, v).reshape(-1).to(q.dtype)
+    return out
+
+
 def flash_prefill(qkv, cu_seqlens, max_len, Hq, Hkv, D, scale, causal):
     T = qkv.shape[0]
     x = qkv.view(T, Hq + 2 * Hkv, D)

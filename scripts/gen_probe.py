@@ -22,6 +22,7 @@ def main():
     ap.add_argument("--iters", type=int, default=2)
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--max-context", type=int, default=0)
+    ap.add_argument("--shared", type=int, default=0, help="leading prompt tokens shared by every request (RAG template)")
     a = ap.parse_args()
     assert ops.load_native()
     cfg = LlamaConfig.preset(a.model)
@@ -32,7 +33,9 @@ def main():
     eng = LLMEngine(m, max_batch=a.batch, max_context=a.max_context or (a.prompt + a.gen + 64),
                     use_graphs=not a.no_graph)
     g = torch.Generator().manual_seed(0)
-    prompts = [torch.randint(0, cfg.vocab_size, (a.prompt,), generator=g).tolist() for _ in range(a.batch)]
+    head = torch.randint(0, cfg.vocab_size, (a.shared,), generator=g).tolist()
+    prompts = [head + torch.randint(0, cfg.vocab_size, (a.prompt - a.shared,), generator=g).tolist()
+               for _ in range(a.batch)]
     sp = SamplingParams(max_new_tokens=a.gen, stop_on_eos=False)
     for it in range(a.iters + 1):
         eng.stats.__init__()
@@ -42,6 +45,8 @@ def main():
         torch.cuda.synchronize()
         dt = time.time() - t
         s = eng.stats
+        casc = any(k[2] for k in eng._graphs if isinstance(k, tuple))
+        print(f"cascade={casc} cached={s.cached_tokens} ", end="")
         print(f"iter {it}: total {dt*1e3:.0f} ms prefill {s.prefill_s*1e3:.0f} ms "
               f"({s.prompt_tokens/s.prefill_s:.0f} tok/s) decode {s.decode_s*1e3:.0f} ms "
               f"({(a.gen-1)} steps, {s.decode_s/(a.gen-1)*1e3:.2f} ms/step) "

@@ -244,7 +244,7 @@ def test_gemm_asymmetric_identity(native):
     assert torch.equal(o[:64, :], w.float()[:, :64].T[:64, :])
 
 
-@pytest.mark.parametrize("M", [1, 5, 16, 31, 64])
+@pytest.mark.parametrize("M", [1, 5, 16, 31, 64, 65, 100, 128])
 @pytest.mark.parametrize("N,K,S", [(6144, 4096, 0), (4096, 4096, 0), (4096, 14336, 0), (28672, 4096, 0),
                                    (512, 1024, 1), (512, 1024, 2), (640, 3584, 7)])
 def test_dgemm(native, M, N, K, S):
@@ -257,15 +257,15 @@ def test_dgemm(native, M, N, K, S):
         _close(o1, o2, 2e-2, 1e-2)
 
 
-@pytest.mark.parametrize("S", [1, 4])
-def test_splitk_fused_consumers(native, S):
+@pytest.mark.parametrize("S,M,tile", [(1, 37, 64), (4, 37, 64), (4, 100, 128), (8, 128, 128), (2, 128, 64)])
+def test_splitk_fused_consumers(native, S, M, tile):
     """dgemm_partial + add_rmsnorm_splitk / rope_cache_splitk == reference on bf16(sum P)."""
     from docqa_amd.ops import reference as R
 
-    M, H = 37, 4096
+    H = 4096
     x = torch.randn(M, 4096, device="cuda", dtype=torch.bfloat16)
     w = (torch.randn(H, 4096, device="cuda") / 64).bfloat16()
-    P = torch.ops.docqa.dgemm_partial(x, w, S)
+    P = torch.ops.docqa.dgemm_partial(x, w, S, tile)
     assert P.shape == (S, M, H)
     _close(P.sum(0), x.float() @ w.float().T, 2e-2, 1e-2)
     r1 = torch.randn(M, H, device="cuda", dtype=torch.bfloat16)
@@ -293,7 +293,7 @@ def test_splitk_fused_consumers(native, S):
     _close(vc1, vc2, 1e-2)
 
 
-@pytest.mark.parametrize("M", [1, 16, 33, 64])
+@pytest.mark.parametrize("M", [1, 16, 33, 64, 97, 128])
 @pytest.mark.parametrize("N,K", [(28672, 4096), (1024, 512)])
 def test_dgemm_glu(native, M, N, K):
     """Fused SwiGLU decode GEMM (8-interleaved gate|up) vs fp32 GEMM + reference SwiGLU."""
@@ -309,7 +309,7 @@ def test_dgemm_glu(native, M, N, K):
     _close(native.silu_mul(gu, interleaved=True), R.silu_mul(gu, interleaved=True), 2e-2, 1e-2)
 
 
-@pytest.mark.parametrize("B,Hkv,S", [(64, 8, 2), (5, 8, 1), (3, 2, 4)])
+@pytest.mark.parametrize("B,Hkv,S", [(64, 8, 2), (5, 8, 1), (3, 2, 4), (128, 8, 4)])
 def test_paged_decode_fused(native, B, Hkv, S):
     """RoPE + new-token cache write + attention from QKV split-K partials == the unfused
     rope_cache_splitk + paged_decode (outputs and cache contents)."""
@@ -409,3 +409,38 @@ def test_pool_l2(native, mean):
     cu = torch.tensor([0] + list(torch.tensor(lens).cumsum(0)), device="cuda", dtype=torch.int32)
     h = torch.randn(sum(lens), 768, device="cuda", dtype=torch.bfloat16)
     _close(native.pool_l2(h, cu, mean, True), R.pool_l2(h, cu, mean, True), 1e-4)
+
+
+@pytest.mark.parametrize("B,Lp,nchunk", [(5, 448, 4), (64, 448, 16), (128, 448, 16), (128, 960, 8),
+                                         (200, 192, 1), (64, 0, 8)])
+def test_paged_decode_cascade(native, B, Lp, nchunk):
+    """Shared-prefix (cascade) decode attention == plain paged decode over the same tables:
+    MFMA prefix partials in key chunks + ring suffix kernel + LSE merge, in the direct
+    (one partition) and the split (merge kernel) regimes."""
+    from docqa_amd.ops import reference as R
+
+    Hkv, G, D, BS, maxb = 8, 4, 128, 64, 40
+    Hq = G * Hkv
+    npb = Lp // BS
+    NB = npb + B * (maxb - npb) + 1
+    kc = torch.randn(NB, Hkv, BS, D, device="cuda", dtype=torch.bfloat16)
+    vc = torch.randn_like(kc)
+    shared = torch.randperm(NB, device="cuda")[:npb].int()
+    rest = torch.tensor([i for i in range(NB) if i not in set(shared.tolist())], device="cuda").int()
+    bt = torch.zeros(B, maxb, dtype=torch.int32, device="cuda")
+    for b in range(B):
+        bt[b, :npb] = shared
+        bt[b, npb:] = rest[b * (maxb - npb):(b + 1) * (maxb - npb)]
+    cl = (Lp + 1 + torch.randint(0, maxb * BS - Lp - 1, (B,), device="cuda")).int()
+    cl[0] = Lp + 1                                   # suffix of exactly the new token
+    q = (torch.randn(B, (Hq + 2 * Hkv) * D, device="cuda") * 0.5).bfloat16()
+    st = torch.zeros(maxb, dtype=torch.int32, device="cuda")
+    st[:npb] = shared
+    pl = torch.tensor([Lp], dtype=torch.int32, device="cuda")
+    scale = 1 / math.sqrt(D)
+    o1 = native.paged_decode_cascade(q, kc, vc, bt, cl, Hq, maxb * BS, scale, st, pl, nchunk)
+    o2 = native.paged_decode(q, kc, vc, bt, cl, Hq, maxb * BS, scale)
+    _close(o1, o2, 2e-2, 1e-2)
+    sel = torch.arange(0, B, max(1, B // 6), device="cuda")
+    o3 = R.paged_decode_cascade(q[sel], kc, vc, bt[sel], cl[sel], Hq, maxb * BS, scale, st, pl)
+    _close(o1[sel], o3, 2e-2, 1e-2)

@@ -32,3 +32,43 @@ def test_prefix_cache_eviction_under_pressure():
     for s in range(6):  # distinct prompts fill the cache; eviction must make room
         p = [s * 7 + i for i in range(60)]
         assert len(eng.generate([p], sp)[0]) == 4
+
+
+def test_cascade_decode_matches_plain_decode():
+    """Cascade decode (shared prompt prefix attended once for the batch, suffixes per row)
+    generates exactly the tokens of plain paged decode: a batch whose prompts share 5
+    cached blocks switches to the cascade path on its second run."""
+    cfg = LlamaConfig(name="tiny-gqa4", vocab_size=4096, hidden=256, intermediate=512, layers=2,
+                      heads=8, kv_heads=2, head_dim=128, max_position=2048, bos_token_id=1, eos_token_id=2)
+    m = LlamaModel(cfg, device="cpu", dtype=torch.float32, seed=5)
+    eng = LLMEngine(m, max_batch=8, max_context=512, block_size=16, use_graphs=False)
+    eng.cascade_min_tokens = 32
+    pre = list(range(200, 280))                    # 5 full shared blocks
+    ps = [pre + [11 + i, 7, 3 * i + 1][: 1 + i % 3] + list(range(i)) for i in range(6)]
+    sp = SamplingParams(max_new_tokens=20, stop_on_eos=False)   # crosses block boundaries
+    first = eng.generate(ps, sp)
+    assert not any(k[2] for k in eng._graphs)
+    second = eng.generate(ps, sp)
+    assert any(k[2] for k in eng._graphs), "second run must take the cascade path"
+    ref = LLMEngine(m, max_batch=8, max_context=512, block_size=16, use_graphs=False,
+                    prefix_cache=False).generate(ps, sp)
+    assert first == second == ref
+
+
+def test_cascade_reference_op_equals_paged_decode():
+    from docqa_amd.ops import reference as R
+
+    torch.manual_seed(0)
+    NB, Hkv, BS, D, Hq, B = 40, 2, 16, 128, 8, 5
+    kc, vc = torch.randn(NB, Hkv, BS, D), torch.randn(NB, Hkv, BS, D)
+    shared = [3, 7, 1]
+    bt = torch.zeros(B, 8, dtype=torch.int32)
+    for b in range(B):
+        bt[b, :3] = torch.tensor(shared)
+        bt[b, 3:] = torch.arange(10 + 5 * b, 15 + 5 * b)
+    cl = torch.tensor([49, 60, 80, 100, 120], dtype=torch.int32)
+    q = torch.randn(B, (Hq + 2 * Hkv) * D)
+    a = R.paged_decode(q, kc, vc, bt, cl, Hq, 128, 0.1)
+    c = R.paged_decode_cascade(q, kc, vc, bt, cl, Hq, 128, 0.1, torch.tensor(shared + [0] * 5, dtype=torch.int32),
+                               torch.tensor([48], dtype=torch.int32))
+    assert torch.allclose(a, c, atol=1e-5)
