@@ -36,7 +36,7 @@ def main() -> None:
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--batch", type=int, default=64, help="questions per data-parallel rank per step")
+    ap.add_argument("--batch", type=int, default=128, help="questions per data-parallel rank per step")
     ap.add_argument("--max-new-tokens", type=int, default=128)
     ap.add_argument("--llm", default="llama3-8b")
     ap.add_argument("--embed", default="minilm-l6")

@@ -25,9 +25,14 @@ from .flat import FlatIndex
 
 
 class ShardedFlatIndex:
-    def __init__(self, local: FlatIndex, group=None):
+    """``replicated=True``: every rank of ``group`` searches with the SAME queries (a
+    tensor-parallel group serving one request stream, config 5): the query all-gather is
+    skipped and each shard answers the batch once."""
+
+    def __init__(self, local: FlatIndex, group=None, replicated: bool = False):
         self.local = local
         self.group = group
+        self.replicated = replicated
         s = comm.state()
         self.world = s.dp_size if group is None else dist.get_world_size(group)
         self.rank = s.dp_rank if group is None else dist.get_rank(group)
@@ -67,6 +72,9 @@ class ShardedFlatIndex:
             return self.local.search(xq, k)
         nq = xq.shape[0]
         dev = xq.device
+        if self.replicated:
+            D, I = self.local.search(xq, k, id_offset=self._offset)
+            return self._merge(D, I, k, 0, nq)
         cnt = torch.tensor([nq], dtype=torch.long, device=dev)
         cnts = [torch.empty_like(cnt) for _ in range(self.world)]
         dist.all_gather(cnts, cnt, group=self.group)
@@ -78,7 +86,11 @@ class ShardedFlatIndex:
         dist.all_gather(allq, pad, group=self.group)
         Q = torch.cat([q[:c] for q, c in zip(allq, counts)], 0)
         D, I = self.local.search(Q, k, id_offset=self._offset)
-        tot = Q.shape[0]
+        return self._merge(D, I, k, sum(counts[: self.rank]), nq)
+
+    def _merge(self, D, I, k: int, start: int, nq: int):
+        """all-gather every shard's top-k (dist, id) and keep the global top-k of rows
+        [start, start + nq)."""
         allD = [torch.empty_like(D) for _ in range(self.world)]
         allI = [torch.empty_like(I) for _ in range(self.world)]
         dist.all_gather(allD, D.contiguous(), group=self.group)
@@ -88,6 +100,4 @@ class ShardedFlatIndex:
         largest = self.local.metric == "ip"
         vals, pos = torch.topk(Dc, k, dim=1, largest=largest)
         ids = torch.gather(Ic, 1, pos)
-        start = sum(counts[: self.rank])
-        del tot
         return vals[start:start + nq], ids[start:start + nq]

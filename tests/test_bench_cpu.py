@@ -49,3 +49,21 @@ def test_bench_two_ranks_gloo_sharded_index():
     assert r.returncode == 0, r.stderr[-3000:]
     d = _last_json(r.stdout)
     assert d["n_gpus"] == 2 and d["config"]["global_batch"] == 6 and d["config"]["parallelism"] == "dp2"
+
+
+def test_pipeline_bench_tp2_gloo_sharded_index():
+    """Config-5 pipeline benchmark (ingest -> deid -> embed -> sharded kNN -> TP generate)
+    as 2 gloo ranks: TP=2 generator, index sharded over both ranks with replicated queries."""
+    env = dict(os.environ)
+    for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
+        env.pop(k, None)
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", str(_port()),
+           str(ROOT / "benchmarks" / "bench_pipeline.py"), "--device", "cpu", "--llm", "tiny",
+           "--embed", "tiny-bert", "--ner", "tiny-bert", "--notes", "24", "--batch", "3",
+           "--steps", "1", "--warmup", "1", "--max-new-tokens", "3", "--max-context", "1024"]
+    r = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=900, env=env)
+    assert r.returncode == 0, r.stderr[-3000:]
+    d = _last_json(r.stdout)
+    assert d["n_gpus"] == 2 and d["config"]["parallelism"] == "tp2" and d["value"] > 0
+    assert d["ingest_docs_per_sec"] > 0 and d["config"]["index"] == "flat-L2 sharded x2"
