@@ -61,6 +61,9 @@ class Settings:
     temperature: float = field(default_factory=lambda: float(os.getenv("TEMPERATURE", "0")))
     max_batch: int = field(default_factory=lambda: env_int("MAX_BATCH", 64))
     batch_window_ms: int = field(default_factory=lambda: env_int("BATCH_WINDOW_MS", 5))
+    # llm-qa scheduling: "continuous" (requests join/leave the decode batch every step,
+    # engine/scheduler.py) or "batch" (static batches, one prefill + decode loop each)
+    serving_mode: str = field(default_factory=lambda: os.getenv("DOCQA_SERVING", "continuous"))
     tp_size: int = field(default_factory=lambda: env_int("TP_SIZE", 1))
     device: str = field(default_factory=lambda: os.getenv("DOCQA_DEVICE", "auto"))
     # synthese

@@ -155,7 +155,7 @@ at::Tensor embedding(const at::Tensor& ids, const at::Tensor& table) {
   sizes.push_back(H);
   c10::DeviceGuard g(ids.device());
   auto out = at::empty(sizes, table.options());
-  CHECK_RC(docqa_embedding(ids.data_ptr<int>(), table.data_ptr(), out.data_ptr(), ids.numel(), H, stream()), "embedding");
+  CHECK_RC(docqa_embedding(ids.data_ptr<int>(), table.data_ptr(), out.data_ptr(), ids.numel(), H, (int)table.size(0), stream()), "embedding");
   return out;
 }
 

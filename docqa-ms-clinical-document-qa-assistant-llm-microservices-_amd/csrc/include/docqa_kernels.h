@@ -21,7 +21,7 @@ int docqa_silu_mul(const void* gu, void* out, int T, int I, int interleaved, hip
 int docqa_bias_act(const void* x, const void* bias, const void* res, void* out, int T, int N,
                    int gelu, hipStream_t s);
 
-int docqa_embedding(const int* ids, const void* table, void* out, int T, int H, hipStream_t s);
+int docqa_embedding(const int* ids, const void* table, void* out, int T, int H, int V, hipStream_t s);
 int docqa_bert_embed_ln(const int* ids, const int* pos, const int* tt, const void* wte,
                         const void* wpe, const void* wtt, const void* g, const void* b, void* out,
                         int T, int H, float eps, hipStream_t s);

@@ -201,7 +201,11 @@ __global__ __launch_bounds__(256, OCC) void paged_decode_kernel(
   const int L = context_lens[b];
   const int slice = split_chunk(L, max_parts);
   const int start = part * slice;
-  if (start >= L) return;
+  if (start >= L) {
+    if (DIRECT && L <= 0)   // padded slot: defined (zero) output
+      for (int i = threadIdx.x; i < G * D; i += 256) out[(size_t)b * out_stride + (size_t)kvh * G * D + i] = 0;
+    return;
+  }
   const int n = min(L - start, slice);
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -350,7 +354,13 @@ __global__ __launch_bounds__(256) void paged_decode_ring_kernel(
   const int P = ci.plen ? *ci.plen : 0;
   const int slice = split_chunk(L - P, max_parts);   // multiple of 64
   const int start = P + part * slice;
-  if (start >= L) return;
+  if (start >= L) {
+    // a row with no keys of its own (a padded decode slot, L = 0) still gets a defined
+    // output: zeros, so nothing downstream ever consumes uninitialised memory
+    if (DIRECT && L <= P)
+      for (int i = threadIdx.x; i < G * D; i += 256) out[(size_t)b * out_stride + (size_t)kvh * G * D + i] = 0;
+    return;
+  }
   const int n = min(L - start, slice);
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -490,7 +500,10 @@ __global__ __launch_bounds__(D) void paged_decode_reduce(const float* __restrict
   const int h = blockIdx.x, b = blockIdx.y, d = threadIdx.x;
   const int P = ci.plen ? *ci.plen : 0;
   const int L = context_lens[b] - P;
-  if (L <= 0) return;
+  if (L <= 0) {   // padded slot: defined (zero) output
+    out[(size_t)b * out_stride + (size_t)h * D + d] = 0;
+    return;
+  }
   const int chunk = split_chunk(L, max_parts);
   const int np = min(max_parts, (L + chunk - 1) / chunk);
   const int nc = ci.plen ? cascade_parts(P, ci.nchunk) : 0;

@@ -16,9 +16,11 @@ using namespace docqa;
 
 __global__ __launch_bounds__(256) void embedding_gather_kernel(const int* __restrict__ ids,
                                                                const uint16_t* __restrict__ table,
-                                                               uint16_t* __restrict__ out, int H) {
+                                                               uint16_t* __restrict__ out, int H, int V) {
   const int t = blockIdx.x;
-  const uint4* src = reinterpret_cast<const uint4*>(table + (size_t)ids[t] * H);
+  // out-of-range ids (a padded decode slot's stale token) read row 0, never past the table
+  const int id = (unsigned)ids[t] < (unsigned)V ? ids[t] : 0;
+  const uint4* src = reinterpret_cast<const uint4*>(table + (size_t)id * H);
   uint4* dst = reinterpret_cast<uint4*>(out + (size_t)t * H);
   for (int c = threadIdx.x; c < (H >> 3); c += blockDim.x) dst[c] = src[c];
 }
@@ -144,7 +146,7 @@ __global__ __launch_bounds__(64) void argmax_pass2(const float* __restrict__ pv,
     const int oi = __shfl_xor(bi, o, 64);
     better(bv, bi, ov, oi);
   }
-  if (threadIdx.x == 0) out[row] = bi;
+  if (threadIdx.x == 0) out[row] = bi == 0x7fffffff ? 0 : bi;   // all-NaN row: a valid id
 }
 
 // ---------------------------------------------------------------------------------
@@ -254,10 +256,10 @@ __global__ __launch_bounds__(256) void sample_kernel(const float* __restrict__ l
   }
 }
 
-int docqa_embedding(const int* ids, const void* table, void* out, int T, int H, hipStream_t s) {
+int docqa_embedding(const int* ids, const void* table, void* out, int T, int H, int V, hipStream_t s) {
   if (T == 0) return 0;
   if (H % 8 != 0) return -1;
-  embedding_gather_kernel<<<T, 256, 0, s>>>(ids, (const uint16_t*)table, (uint16_t*)out, H);
+  embedding_gather_kernel<<<T, 256, 0, s>>>(ids, (const uint16_t*)table, (uint16_t*)out, H, V);
   DOCQA_CHECK_LAUNCH();
   return 0;
 }

@@ -77,6 +77,20 @@ class _DecodeGraph:
         self.greedy = True
         self.graph = None
 
+    @classmethod
+    def view_of(cls, master: "_DecodeGraph", bp: int) -> "_DecodeGraph":
+        """Buffers for bucket ``bp`` that are the first ``bp`` slots of ``master``: graphs
+        of every bucket then read/write ONE slot state, so a continuous-batching scheduler
+        can change bucket between steps without copying state."""
+        g = cls.__new__(cls)
+        g.bp = bp
+        for name in ("tokens", "positions", "context_lens", "valid", "block_tables", "inv_temp",
+                     "top_k", "top_p", "out"):
+            setattr(g, name, getattr(master, name)[:bp])
+        g.shared_table, g.shared_len = master.shared_table, master.shared_len
+        g.cascade, g.greedy, g.graph = False, True, None
+        return g
+
 
 class LLMEngine:
     def __init__(self, model: LlamaModel, max_batch: int = 64, max_context: int = 2048,
@@ -220,7 +234,9 @@ class LLMEngine:
             k += 1
         return k if k * BS >= self.cascade_min_tokens else 0
 
-    def _capture(self, g: _DecodeGraph) -> None:
+    def _capture(self, g: _DecodeGraph, pool=None) -> None:
+        """``pool``: graph memory pool handle (default: this engine's own); a scheduler
+        that owns its graphs passes its own so their lifetimes stay independent."""
         # warm up on a side stream (allocator + hipBLASLt heuristics), then capture.
         # Decode GEMMs are skinny (M = batch bucket) and their shapes are fixed per bucket,
         # so they are worth an exhaustive hipBLASLt/rocBLAS solution search (PyTorch
@@ -243,9 +259,11 @@ class LLMEngine:
             if tune and tunable is not None:
                 tunable.tuning_enable(False)
             graph = torch.cuda.CUDAGraph()
-            if self._pool is None:
-                self._pool = torch.cuda.graph_pool_handle()
-            with torch.cuda.graph(graph, pool=self._pool):
+            if pool is None:
+                if self._pool is None:
+                    self._pool = torch.cuda.graph_pool_handle()
+                pool = self._pool
+            with torch.cuda.graph(graph, pool=pool):
                 self._step_body(g)
         finally:
             if tune and tunable is not None:

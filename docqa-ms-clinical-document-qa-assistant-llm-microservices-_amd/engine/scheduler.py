@@ -1,0 +1,396 @@
+"""Continuous (iteration-level) batching on top of :class:`LLMEngine`.
+
+The static path (:meth:`LLMEngine.generate`) runs one batch from prefill to its last
+token; a request that arrives meanwhile waits for the whole batch, and a sequence that
+stops early (EOS) leaves its slot idle.  Here the decode batch is a set of SLOTS that
+requests join and leave between steps:
+
+  * admission: waiting requests are admitted while slots and KV blocks are free (prompt
+    + max_new_tokens blocks reserved up front, prompt-prefix cache hits reused), their
+    prompts prefilled together (one packed varlen forward, chunked past the token
+    budget) and their first tokens sampled;
+  * decode: one step for every running slot -- a HIP graph captured per (batch bucket,
+    greedy/sampled, cascade) whose buffers are VIEWS of one slot-state tensor set, so
+    moving between buckets as the batch grows and shrinks copies nothing;
+  * retirement: a slot whose request hit EOS / its token limit frees its blocks, resolves
+    its future, and the last slot moves into the hole (device-side row gather) so slots
+    stay dense and the smallest bucket covers them;
+  * cascade: when every running slot starts with the same cached prompt-prefix blocks
+    (the RAG template), the step attends that prefix once for the whole batch
+    (csrc/include/docqa_cascade.h);
+  * lagged readback: step t's tokens are copied to pinned host memory and read while
+    step t+1 already runs, so the GPU never idles on the host's bookkeeping (a finished
+    request rides one extra step inside its reserved blocks and that token is dropped);
+  * admission batching: under load, arrivals are admitted in groups (>= ``admit_min``
+    waiting or the oldest waiting ``admit_wait_s``), so one prefill pass over the weights
+    serves several new requests instead of stalling every decode step.
+
+Reference parity: the reference serves one blocking request at a time
+(llm-qa/main.py:111-117); its generator (Ollama) schedules requests internally.
+"""
+from __future__ import annotations
+
+import collections
+import concurrent.futures as cf
+import itertools
+import threading
+import time
+from dataclasses import dataclass, field
+
+import torch
+
+from .. import ops
+from .llm_engine import LLMEngine, SamplingParams, _bucket, _DecodeGraph
+
+
+@dataclass
+class Request:
+    rid: int
+    prompt: list[int]
+    params: SamplingParams
+    future: cf.Future
+    on_token: object = None          # callable(rid, token) for streaming
+    out: list[int] = field(default_factory=list)
+    blocks: list[int] = field(default_factory=list)
+    cached: int = 0
+    t_arrival: float = 0.0
+    t_first: float = 0.0
+    done: bool = False
+
+
+class ContinuousEngine:
+    def __init__(self, engine: LLMEngine, max_running: int | None = None):
+        self.eng = engine
+        self.max_running = min(max_running or engine.max_batch, engine.max_batch)
+        self.waiting: collections.deque[Request] = collections.deque()
+        self.running: list[Request] = []
+        self._cv = threading.Condition()
+        self._ids = itertools.count()
+        self._master = _DecodeGraph(engine, engine.max_batch)
+        self._graphs: dict[tuple, _DecodeGraph] = {}
+        self._nshared = 0
+        self._shared_head: list[int] = []
+        self._thread: threading.Thread | None = None
+        self._stop = threading.Event()
+        self.steps = 0
+        # decode over power-of-two slot buckets (padded slots: valid 0); on by default with
+        # graphs, settable on CPU to exercise the padded-slot paths of the reference ops
+        self.pad_buckets = engine.use_graphs
+        self.admit_min = max(1, self.max_running // 8)
+        self.admit_wait_s = 0.04
+        self._pool = None
+        self._pending = None               # (event, pinned host tokens, slot -> request) of the last step
+        self._host = None
+        self._flip = 0
+
+    # ------------------------------------------------------------------ client side
+    def submit(self, prompt: list[int], params: SamplingParams | None = None, on_token=None) -> cf.Future:
+        params = params or SamplingParams()
+        fut: cf.Future = cf.Future()
+        if len(prompt) + params.max_new_tokens > self.eng.max_context or not prompt:
+            fut.set_exception(ValueError(
+                f"prompt+generation {len(prompt) + params.max_new_tokens} exceeds max_context {self.eng.max_context}"))
+            return fut
+        r = Request(next(self._ids), list(prompt), params, fut, on_token, t_arrival=time.perf_counter())
+        with self._cv:
+            self.waiting.append(r)
+            self._cv.notify()
+        return fut
+
+    def has_work(self) -> bool:
+        return bool(self.waiting or self.running or self._pending)
+
+    def generate(self, prompts: list[list[int]], params: SamplingParams | None = None) -> list[list[int]]:
+        """Submit all prompts and drive the scheduler in this thread until they finish."""
+        futs = [self.submit(p, params) for p in prompts]
+        while not all(f.done() for f in futs):
+            self.step()
+        return [f.result() for f in futs]
+
+    @torch.inference_mode()
+    def warmup(self, buckets: list[int] | None = None, sampled: bool = False) -> None:
+        """Capture the decode graphs of every bucket (plain and cascade; greedy, and
+        sampled if asked) before serving, so no request pays a capture / GEMM-tuning
+        stall mid-stream.  Slots are empty (valid 0): the captured warm-up steps write
+        nothing to the KV cache."""
+        if not self.eng.use_graphs or self.running:
+            return
+        bs, b = [], 1
+        while b < self.eng.max_batch:
+            bs.append(b)
+            b *= 2
+        bs.append(self.eng.max_batch)
+        casc = [False, True] if self.eng.cascade else [False]
+        for bp in buckets or bs:
+            for greedy in ([True, False] if sampled else [True]):
+                for c in casc:
+                    g = self._graph(bp, greedy, c)
+                    if g.graph is None:
+                        if self._pool is None:
+                            self._pool = torch.cuda.graph_pool_handle()
+                        self.eng._capture(g, self._pool)
+
+    # ------------------------------------------------------------------ serving thread
+    def start(self) -> "ContinuousEngine":
+        if self._thread is None:
+            self._thread = threading.Thread(target=self._serve, name="llm-scheduler", daemon=True)
+            self._thread.start()
+        return self
+
+    def stop(self) -> None:
+        self._stop.set()
+        with self._cv:
+            self._cv.notify()
+        if self._thread is not None:
+            self._thread.join(timeout=30)
+            self._thread = None
+
+    def _serve(self) -> None:
+        while not self._stop.is_set():
+            with self._cv:
+                if not self.has_work():
+                    self._cv.wait(timeout=0.1)
+                    continue
+            try:
+                self.step()
+            except Exception as e:  # noqa: BLE001 - fail the affected requests, keep serving
+                self._fail_all(e)
+
+    def _fail_all(self, e: Exception) -> None:
+        self._pending = None
+        for r in self.running:
+            self.eng.kv.allocator.free(r.blocks)
+            if not r.future.done():
+                r.future.set_exception(e)
+        self.running = []
+        self._master.valid.zero_()
+        self._master.context_lens.zero_()
+
+    # ------------------------------------------------------------------ one iteration
+    @torch.inference_mode()
+    def step(self) -> None:
+        self._admit()
+        if self.running:
+            self._decode()
+        elif self._pending is not None:
+            p, self._pending = self._pending, None
+            self._process(p)
+
+    def _take_waiting(self) -> list[Request]:
+        eng, alloc = self.eng, self.eng.kv.allocator
+        use_pc = eng.prefix_cache and hasattr(alloc, "match_prefix")
+        admitted, budget = [], 0
+        with self._cv:
+            while self.waiting and len(self.running) + len(admitted) < self.max_running:
+                r = self.waiting[0]
+                hit = alloc.match_prefix(r.prompt) if use_pc else []
+                if hit and len(hit) * eng.block_size >= len(r.prompt):
+                    alloc.free([hit[-1]])        # recompute >= 1 token: its logits seed decode
+                    hit = hit[:-1]
+                need = eng.kv.blocks_for(len(r.prompt) + r.params.max_new_tokens) - len(hit)
+                try:
+                    new = alloc.alloc(need)
+                except MemoryError:
+                    alloc.free(hit)
+                    if not self.running and not admitted:   # can never fit: fail, don't stall
+                        self.waiting.popleft().future.set_exception(MemoryError(
+                            f"request needs {need} KV blocks, the cache has {alloc.num_free()} free"))
+                        continue
+                    break                        # retry after running requests retire
+                r.blocks, r.cached = hit + new, len(hit) * eng.block_size
+                admitted.append(self.waiting.popleft())
+                budget += len(r.prompt) - r.cached
+                if budget >= eng.max_prefill_tokens:
+                    break
+        return admitted
+
+    def _admit(self) -> None:
+        if self.running and self.waiting:
+            free = self.max_running - len(self.running)
+            age = time.perf_counter() - self.waiting[0].t_arrival
+            if len(self.waiting) < min(free, self.admit_min) and age < self.admit_wait_s:
+                return                         # gather a group: one prefill pass for several
+        adm = self._take_waiting()
+        if not adm:
+            return
+        eng, alloc = self.eng, self.eng.kv.allocator
+        t0 = time.perf_counter()
+        try:
+            logits = eng._prefill([r.prompt for r in adm], [r.blocks for r in adm], [r.cached for r in adm])
+            first = self._sample_rows(logits, [r.params for r in adm])
+        except Exception as e:  # noqa: BLE001
+            for r in adm:
+                alloc.free(r.blocks)
+                r.future.set_exception(e)
+            return
+        if eng.prefix_cache and hasattr(alloc, "register_prefix"):
+            for r in adm:
+                alloc.register_prefix(r.prompt, r.blocks)
+        now = time.perf_counter()
+        eng.stats.prefill_s += now - t0
+        eng.stats.prompt_tokens += sum(len(r.prompt) for r in adm)
+        eng.stats.cached_tokens += sum(r.cached for r in adm)
+        joined = []
+        for r, t in zip(adm, first):
+            r.t_first = now
+            self._emit(r, t)
+            if self._finished(r):
+                r.done = True
+                self._retire(r)
+            else:
+                joined.append(r)
+        if joined:
+            self._place(joined)
+        self._update_shared()
+
+    def _place(self, reqs: list[Request]) -> None:
+        """Write the decode state of newly joined requests into slots [n, n + k)."""
+        m, n, k = self._master, len(self.running), len(reqs)
+        maxb = self.eng.max_blocks_per_seq
+        bt = torch.zeros(k, maxb, dtype=torch.int32)
+        tok = torch.empty(k, dtype=torch.int32)
+        pos = torch.empty(k, dtype=torch.int32)
+        it = torch.ones(k, dtype=torch.float32)
+        tk = torch.zeros(k, dtype=torch.int32)
+        tp = torch.ones(k, dtype=torch.float32)
+        for i, r in enumerate(reqs):
+            bt[i, :len(r.blocks)] = torch.tensor(r.blocks, dtype=torch.int32)
+            tok[i] = r.out[-1]
+            pos[i] = len(r.prompt) + len(r.out) - 1
+            if r.params.temperature > 0:
+                it[i], tk[i], tp[i] = 1.0 / r.params.temperature, r.params.top_k, r.params.top_p
+            else:
+                tk[i] = 1                        # greedy row inside a sampled batch: argmax
+        dev = m.tokens.device
+        sl = slice(n, n + k)
+        m.block_tables[sl].copy_(bt.to(dev, non_blocking=True))
+        m.tokens[sl].copy_(tok.to(dev, non_blocking=True))
+        m.positions[sl].copy_(pos.to(dev, non_blocking=True))
+        m.context_lens[sl].copy_((pos + 1).to(dev, non_blocking=True))
+        m.valid[sl].fill_(1)
+        m.inv_temp[sl].copy_(it.to(dev, non_blocking=True))
+        m.top_k[sl].copy_(tk.to(dev, non_blocking=True))
+        m.top_p[sl].copy_(tp.to(dev, non_blocking=True))
+        self.running.extend(reqs)
+
+    def _sample_rows(self, logits: torch.Tensor, params: list[SamplingParams]) -> list[int]:
+        model = self.eng.model
+        if all(p.temperature <= 0 for p in params):
+            return model.greedy(logits).tolist()
+        full = model.full_logits(logits).float()
+        dev = full.device
+        it = torch.tensor([1.0 / p.temperature if p.temperature > 0 else 1.0 for p in params], device=dev)
+        tk = torch.tensor([p.top_k if p.temperature > 0 else 1 for p in params], dtype=torch.int32, device=dev)
+        tp = torch.tensor([p.top_p if p.temperature > 0 else 1.0 for p in params], device=dev)
+        u = torch.rand(full.shape[0], device=dev)
+        return ops.sample(full, it, tk, tp, u).tolist()
+
+    def _graph(self, bp: int, greedy: bool, cascade: bool) -> _DecodeGraph:
+        key = (bp, greedy, cascade)
+        g = self._graphs.get(key)
+        if g is None:
+            g = _DecodeGraph.view_of(self._master, bp)
+            g.greedy, g.cascade = greedy, cascade
+            self._graphs[key] = g
+        return g
+
+    def _decode(self) -> None:
+        eng = self.eng
+        n = len(self.running)
+        bp = _bucket(n, eng.max_batch) if self.pad_buckets else n
+        greedy = all(r.params.temperature <= 0 for r in self.running)
+        g = self._graph(bp, greedy, self._nshared > 0)
+        t0 = time.perf_counter()
+        if eng.use_graphs:
+            if g.graph is None:
+                if self._pool is None:
+                    self._pool = torch.cuda.graph_pool_handle()
+                eng._capture(g, self._pool)
+            g.graph.replay()
+        else:
+            eng._step_body(g)
+        eng.stats.generated_tokens += n
+        self.steps += 1
+        snap = list(self.running)
+        if g.out.device.type == "cuda":
+            if self._host is None:
+                self._host = [torch.empty(eng.max_batch, dtype=torch.long, pin_memory=True) for _ in range(2)]
+            host = self._host[self._flip]
+            self._flip ^= 1
+            host[:n].copy_(g.out[:n], non_blocking=True)
+            ev = torch.cuda.Event()
+            ev.record()
+            prev, self._pending = self._pending, (ev, host, snap)
+            if prev is not None:
+                self._process(prev)          # step t-1's tokens while step t runs
+        else:
+            self._process((None, g.out[:n].clone(), snap))
+        eng.stats.decode_s += time.perf_counter() - t0
+
+    def _process(self, pending) -> None:
+        ev, host, snap = pending
+        if ev is not None:
+            ev.synchronize()
+        toks = host[:len(snap)].tolist()
+        finished = []
+        for r, t in zip(snap, toks):
+            if r.done:
+                continue                      # the extra lagged step of a finished request
+            self._emit(r, t)
+            if self._finished(r):
+                r.done = True
+                finished.append(r)
+        if finished:
+            for r in finished:
+                self._retire(r)
+            keep = [i for i, r in enumerate(self.running) if not r.done]
+            self._compact(keep)
+            self._update_shared()
+
+    def _emit(self, r: Request, tok: int) -> None:
+        r.out.append(int(tok))
+        if r.on_token is not None:
+            try:
+                r.on_token(r.rid, int(tok))
+            except Exception:  # noqa: BLE001 - a client callback must not stop the engine
+                r.on_token = None
+
+    def _finished(self, r: Request) -> bool:
+        if len(r.out) >= r.params.max_new_tokens:
+            return True
+        return r.params.stop_on_eos and r.out[-1] == self.eng.cfg.eos_token_id
+
+    def _retire(self, r: Request) -> None:
+        self.eng.kv.allocator.free(r.blocks)
+        r.blocks = []
+        if not r.future.done():
+            r.future.set_result(list(r.out))
+
+    def _compact(self, keep: list[int]) -> None:
+        """Move the surviving slots to [0, len(keep)) (one row gather per state tensor)."""
+        m, n, k = self._master, len(self.running), len(keep)
+        if keep != list(range(k)):
+            idx = torch.tensor(keep, dtype=torch.long, device=m.tokens.device)
+            for name in ("tokens", "positions", "context_lens", "valid", "block_tables", "inv_temp",
+                         "top_k", "top_p"):
+                t = getattr(m, name)
+                t[:k] = t[idx]
+        m.valid[k:n].zero_()
+        m.context_lens[k:n].zero_()
+        m.positions[k:n].zero_()
+        m.tokens[k:n].zero_()
+        self.running = [self.running[i] for i in keep]
+
+    def _update_shared(self) -> None:
+        """Cascade decode applies when all running slots share leading cached blocks."""
+        rs = self.running
+        ns = self.eng._shared_prefix_blocks([r.blocks for r in rs], [r.cached for r in rs]) if rs else 0
+        if ns != self._nshared or (ns and self._shared_head != rs[0].blocks[:ns]):
+            m = self._master
+            if ns:
+                st = torch.zeros(self.eng.max_blocks_per_seq, dtype=torch.int32)
+                st[:ns] = torch.tensor(rs[0].blocks[:ns], dtype=torch.int32)
+                m.shared_table.copy_(st.to(m.shared_table.device))
+            m.shared_len.fill_(ns * self.eng.block_size)
+            self._nshared = ns
+            self._shared_head = rs[0].blocks[:ns] if ns else []

@@ -9,10 +9,13 @@ Contract (llm-qa/main.py:108-126 and synthese-comparative/core/llm_client.py:42-
   GET  /metrics             Prometheus text (requests, batch sizes, stage latencies)
 
 Serving model: the reference answers one blocking request at a time per process
-(llm-qa/main.py:111-117).  Here a dynamic batcher thread drains the request queue every
-``BATCH_WINDOW_MS`` (or as soon as ``MAX_BATCH`` requests wait) and runs the whole batch
-through the RAG pipeline -- one packed embed, one kNN launch, one batched prefill and a
-HIP-graph decode loop -- while the event loop keeps accepting requests.
+(llm-qa/main.py:111-117).  Here (``DOCQA_SERVING=continuous``, default) a scheduler thread
+owns the GPU: between two decode steps it takes every request that arrived, embeds and
+searches them as one batch, and hands their prompts to the continuous-batching engine
+(engine/scheduler.py), where they join the running decode batch at the next step and
+leave it when they finish -- no request waits for another batch to drain.
+``DOCQA_SERVING=batch`` keeps the static dynamic batcher: drain the queue every
+``BATCH_WINDOW_MS`` (or at ``MAX_BATCH``) and run the batch from prefill to last token.
 """
 from __future__ import annotations
 
@@ -96,6 +99,105 @@ class DynamicBatcher:
 
     def stop(self) -> None:
         self._stop.set()
+        self._t.join(timeout=60)
+
+
+class ContinuousBatcher:
+    """Scheduler thread: admit arrivals (batched embed + kNN + prompt assembly), then one
+    continuous-batching engine step; repeat."""
+
+    def __init__(self, pipeline, settings: Settings, metrics: Metrics):
+        from ..engine.scheduler import ContinuousEngine
+
+        self.pipe = pipeline
+        self.st = settings
+        self.metrics = metrics
+        self.engine = ContinuousEngine(pipeline.engine, max_running=settings.max_batch)
+        self.q: queue.Queue = queue.Queue()
+        self._stop = threading.Event()
+        self._t = threading.Thread(target=self._loop, name="qa-scheduler", daemon=True)
+        self._t.start()
+
+    def submit(self, kind: str, payload: str) -> cf.Future:
+        f: cf.Future = cf.Future()
+        self.q.put((kind, payload, f, time.perf_counter()))
+        return f
+
+    def _params(self) -> SamplingParams:
+        return SamplingParams(max_new_tokens=self.st.max_new_tokens, temperature=self.st.temperature,
+                              stop_on_eos=True)
+
+    def _drain(self) -> list:
+        items = []
+        try:
+            items.append(self.q.get(timeout=0 if self.engine.has_work() else 0.1))
+        except queue.Empty:
+            return items
+        while True:
+            try:
+                items.append(self.q.get_nowait())
+            except queue.Empty:
+                return items
+
+    def _loop(self) -> None:
+        import torch
+
+        while not self._stop.is_set():
+            items = self._drain()
+            if items:
+                try:
+                    with torch.inference_mode():
+                        self._admit(items)
+                except Exception as e:  # noqa: BLE001
+                    for it in items:
+                        if not it[2].done():
+                            it[2].set_exception(e)
+            if self.engine.has_work():
+                try:
+                    self.engine.step()
+                except Exception as e:  # noqa: BLE001
+                    self.engine._fail_all(e)
+
+    def _admit(self, items) -> None:
+        pipe, params = self.pipe, self._params()
+        asks = [it for it in items if it[0] == "ask"]
+        sums = [it for it in items if it[0] == "summarize"]
+        if asks:
+            qs = [it[1] for it in asks]
+            qemb = pipe.embed(qs)
+            _, I = pipe.index.search(qemb, pipe.k)
+            I = I.tolist()
+            prompts = pipe.build_prompts(qs, I)
+            self.metrics.observe("ask_batch_size", len(asks))
+            for (_, _, f, t0), ids, p in zip(asks, I, prompts):
+                srcs = [pipe.metadata[j].get("source") for j in ids if 0 <= j < len(pipe.metadata)]
+
+                def done(ef, f=f, t0=t0, srcs=srcs):
+                    if ef.exception() is not None:
+                        f.set_exception(ef.exception())
+                        return
+                    self.metrics.observe("ask_latency_s", time.perf_counter() - t0)
+                    f.set_result({"answer": pipe.chat_tok.decode(ef.result()), "sources": srcs})
+
+                self.engine.submit(p, params).add_done_callback(done)
+        for _, text, f, t0 in sums:
+            p = pipe.chat_tok.chat_prompt(text)
+            lim = pipe.max_prompt_tokens
+            if lim and len(p) > lim:
+                p = p[: lim // 2] + p[-lim // 2:]
+
+            def sdone(ef, f=f, t0=t0):
+                if ef.exception() is not None:
+                    f.set_exception(ef.exception())
+                    return
+                self.metrics.observe("summarize_latency_s", time.perf_counter() - t0)
+                f.set_result({"summary": pipe.chat_tok.decode(ef.result())})
+
+            self.engine.submit(p, params).add_done_callback(sdone)
+
+    def stop(self) -> None:
+        self._stop.set()
+        self._t.join(timeout=60)
 
 
 def create_app(pipeline=None, settings: Settings | None = None) -> FastAPI:
@@ -103,7 +205,8 @@ def create_app(pipeline=None, settings: Settings | None = None) -> FastAPI:
     metrics = Metrics("llm_qa")
     app = FastAPI(title="Health LLM Assistant (MI355X)")
     app.state.pipeline = pipeline
-    app.state.batcher = DynamicBatcher(pipeline, st, metrics) if pipeline is not None else None
+    batcher_cls = ContinuousBatcher if st.serving_mode == "continuous" else DynamicBatcher
+    app.state.batcher = batcher_cls(pipeline, st, metrics) if pipeline is not None else None
 
     def ready() -> bool:
         p = app.state.pipeline

@@ -21,6 +21,10 @@ class Metrics:
         with self._lock:
             self._o[name].append(float(v))
 
+    def values(self, name: str) -> list[float]:
+        with self._lock:
+            return list(self._o.get(name, ()))
+
     def quantile(self, name: str, q: float) -> float | None:
         with self._lock:
             xs = sorted(self._o.get(name, ()))

@@ -444,3 +444,32 @@ def test_paged_decode_cascade(native, B, Lp, nchunk):
     sel = torch.arange(0, B, max(1, B // 6), device="cuda")
     o3 = R.paged_decode_cascade(q[sel], kc, vc, bt[sel], cl[sel], Hq, maxb * BS, scale, st, pl)
     _close(o1[sel], o3, 2e-2, 1e-2)
+
+
+@pytest.mark.parametrize("B", [3, 96])
+def test_padded_slots_get_defined_outputs(native, B):
+    """Padded decode slots (context length 0) produce zero attention output in the split
+    (B=3) and direct (B=96) regimes and with cascade; an all-NaN logits row argmaxes to a
+    valid id; an out-of-range token id embeds as row 0 -- so a stale slot can never feed
+    an out-of-bounds id into the next graph replay."""
+    Hkv, G, D, BS, maxb = 8, 4, 128, 64, 8
+    Hq = G * Hkv
+    kc = torch.randn(B * maxb, Hkv, BS, D, device="cuda", dtype=torch.bfloat16)
+    vc = torch.randn_like(kc)
+    bt = torch.arange(B * maxb, device="cuda", dtype=torch.int32).view(B, maxb)
+    cl = torch.full((B,), 100, device="cuda", dtype=torch.int32)
+    cl[1] = 0
+    q = torch.randn(B, (Hq + 2 * Hkv) * D, device="cuda").bfloat16()
+    for _ in range(2):   # the output buffer may come back from the allocator dirty
+        o = native.paged_decode(q, kc, vc, bt, cl, Hq, maxb * BS, 0.1)
+        assert torch.isfinite(o.float()).all() and (o[1] == 0).all()
+        st = bt[0].clone()
+        oc = native.paged_decode_cascade(q, kc, vc, bt, cl, Hq, maxb * BS, 0.1, st,
+                                         torch.tensor([64], device="cuda", dtype=torch.int32), 4)
+        assert (oc[1] == 0).all()
+    lg = torch.randn(2, 1000, device="cuda")
+    lg[0] = float("nan")
+    assert 0 <= int(native.argmax(lg)[0]) < 1000
+    tab = torch.randn(50, 64, device="cuda").bfloat16()
+    e = native.embedding(torch.tensor([3, 2 ** 31 - 1, -5], device="cuda", dtype=torch.int32), tab)
+    assert torch.equal(e[1], tab[0]) and torch.equal(e[2], tab[0]) and torch.equal(e[0], tab[3])

@@ -1,0 +1,96 @@
+"""Continuous batching (engine/scheduler.py): requests that join and leave the decode
+batch between steps produce exactly the tokens of running each one alone, the batch
+shrinks/grows across buckets, cascade decode switches on for shared prefixes, and every
+KV block is returned."""
+import threading
+
+import torch
+
+from docqa_amd.engine.llm_engine import LLMEngine, SamplingParams
+from docqa_amd.engine.scheduler import ContinuousEngine
+from docqa_amd.models.llama import LlamaConfig, LlamaModel
+
+
+def _model(seed=7):
+    cfg = LlamaConfig(name="tiny-gqa4", vocab_size=4096, hidden=256, intermediate=512, layers=2,
+                      heads=8, kv_heads=2, head_dim=128, max_position=2048, bos_token_id=1, eos_token_id=2)
+    return LlamaModel(cfg, device="cpu", dtype=torch.float32, seed=seed)
+
+
+def _alone(m, p, n):
+    eng = LLMEngine(m, max_batch=4, max_context=512, block_size=16, use_graphs=False, prefix_cache=False)
+    return eng.generate([p], SamplingParams(max_new_tokens=n, stop_on_eos=False))[0]
+
+
+def test_staggered_arrivals_match_isolated_generation():
+    m = _model()
+    eng = LLMEngine(m, max_batch=4, max_context=512, block_size=16, use_graphs=False)
+    ce = ContinuousEngine(eng)
+    g = torch.Generator().manual_seed(0)
+    prompts = [torch.randint(3, 4096, (int(n),), generator=g).tolist() for n in (20, 35, 17, 50, 9, 28)]
+    lens = [6, 11, 3, 8, 14, 5]
+    futs = []
+    for i, (p, n) in enumerate(zip(prompts, lens)):
+        futs.append(ce.submit(p, SamplingParams(max_new_tokens=n, stop_on_eos=False)))
+        for _ in range(i % 3):          # requests arrive while others are mid-decode
+            ce.step()
+    while ce.has_work():
+        ce.step()
+    outs = [f.result() for f in futs]
+    for p, n, o in zip(prompts, lens, outs):
+        assert o == _alone(m, p, n)
+    st = eng.kv.allocator.stats()
+    assert st["free"] + st["evictable"] == eng.kv.num_blocks
+    assert not ce.running and not ce.waiting
+
+
+def test_more_requests_than_slots_and_eos():
+    m = _model(seed=11)
+    eng = LLMEngine(m, max_batch=2, max_context=256, block_size=16, use_graphs=False)
+    ce = ContinuousEngine(eng)
+    g = torch.Generator().manual_seed(1)
+    prompts = [torch.randint(3, 4096, (12 + i,), generator=g).tolist() for i in range(5)]
+    outs = ce.generate(prompts, SamplingParams(max_new_tokens=7, stop_on_eos=False))
+    assert [len(o) for o in outs] == [7] * 5
+    for p, o in zip(prompts, outs):
+        assert o == _alone(m, p, 7)
+    # EOS: force the model's first greedy token to be the stop token
+    eos = outs[0][0]
+    eng.cfg.eos_token_id = eos
+    r = ce.generate([prompts[0]], SamplingParams(max_new_tokens=7, stop_on_eos=True))[0]
+    assert r == [eos]
+
+
+def test_cascade_engages_for_shared_prefix_and_is_exact():
+    m = _model(seed=13)
+    eng = LLMEngine(m, max_batch=8, max_context=512, block_size=16, use_graphs=False)
+    eng.cascade_min_tokens = 32
+    ce = ContinuousEngine(eng)
+    pre = list(range(300, 380))
+    ps = [pre + [5 + i] * (1 + i) for i in range(5)]
+    sp = SamplingParams(max_new_tokens=9, stop_on_eos=False)
+    first = ce.generate(ps, sp)                   # registers the shared prefix
+    second = ce.generate(ps, sp)                  # every slot hits the same cached blocks
+    assert any(k[2] for k in ce._graphs), "cascade graph expected"
+    assert first == second == [_alone(m, p, 9) for p in ps]
+
+
+def test_serving_thread_resolves_concurrent_futures():
+    m = _model(seed=17)
+    eng = LLMEngine(m, max_batch=4, max_context=256, block_size=16, use_graphs=False)
+    ce = ContinuousEngine(eng).start()
+    try:
+        res = {}
+
+        def client(i):
+            p = list(range(10 + i, 30 + 2 * i))
+            res[i] = ce.submit(p, SamplingParams(max_new_tokens=4 + i, stop_on_eos=False)).result(timeout=120)
+
+        th = [threading.Thread(target=client, args=(i,)) for i in range(6)]
+        for t in th:
+            t.start()
+        for t in th:
+            t.join()
+        assert sorted(res) == list(range(6)) and all(len(res[i]) == 4 + i for i in range(6))
+    finally:
+        ce.stop()

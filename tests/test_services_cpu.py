@@ -308,3 +308,34 @@ def test_indexer_group_commit_burst(tmp_path, monkeypatch):
         time.sleep(0.05)
     assert 21 in done and idx.index.ntotal == 61
     idx.stop_consumer()
+
+
+@pytest.mark.parametrize("mode", ["continuous", "batch"])
+def test_qa_concurrent_asks_both_serving_modes(tmp_path, mode):
+    """Concurrent /ask/ and /api/llm/summarize requests through the continuous-batching
+    scheduler and the static batcher: every request answered with k sources."""
+    import concurrent.futures as cf
+
+    from docqa_amd.services.stack import DocQAStack, StackOptions
+
+    st = Settings()
+    st.index_dir = str(tmp_path)
+    st.default_data_dir = str(tmp_path / "nodata")
+    st.database_url = "sqlite://"
+    st.max_new_tokens = 5
+    st.serving_mode = mode
+    s = DocQAStack(StackOptions(llm="tiny", embed="tiny-bert", ner="tiny-bert", device="cpu",
+                                max_batch=4, max_context=1024, use_graphs=False), st)
+    try:
+        qa = TestClient(s.qa_app)
+        with cf.ThreadPoolExecutor(6) as ex:
+            asks = [ex.submit(qa.post, "/ask/", json={"question": f"Quelle plante pour le cas {i} ?"})
+                    for i in range(9)]
+            sums = [ex.submit(qa.post, "/api/llm/summarize", json={"prompt": f"Résumé {i}"}) for i in range(3)]
+            for f in asks:
+                r = f.result(timeout=300)
+                assert r.status_code == 200 and len(r.json()["sources"]) == 3
+            for f in sums:
+                assert isinstance(f.result(timeout=300).json()["summary"], str)
+    finally:
+        s.close()
