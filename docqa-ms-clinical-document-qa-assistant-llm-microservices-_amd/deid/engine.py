@@ -14,6 +14,7 @@ from __future__ import annotations
 
 from dataclasses import dataclass
 
+from ..utils import tracing
 from .recognizers import ENTITIES, Span, context_spans, pattern_spans, resolve_overlaps
 
 NER_LABELS = ["O", "B-PER", "I-PER", "B-LOC", "I-LOC", "B-NRP", "I-NRP", "B-DATE", "I-DATE"]
@@ -111,7 +112,8 @@ class DeidEngine:
         return "".join(out)
 
     def process_batch(self, texts: list[str], entities=None) -> list[str]:
-        res = self.analyze_batch([t or "" for t in texts], entities)
+        with tracing.span("deid.analyze", docs=len(texts), model=self.use_model):
+            res = self.analyze_batch([t or "" for t in texts], entities)
         return ["" if not t else self.anonymize(t, r) for t, r in zip(texts, res)]
 
     def process_text_anonymization(self, text, entities=None) -> str:

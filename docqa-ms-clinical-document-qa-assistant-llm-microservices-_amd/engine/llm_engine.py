@@ -25,6 +25,7 @@ from dataclasses import dataclass
 import torch
 
 from .. import ops
+from ..utils import tracing
 from ..models.llama import AttnMeta, LlamaModel
 from .kv_cache import KVCache
 
@@ -312,7 +313,8 @@ class LLMEngine:
         try:
             greedy = params.temperature <= 0.0
             t0 = time.perf_counter()
-            logits = self._prefill(prompts, tables, cached)
+            with tracing.span("engine.prefill", seqs=B, tokens=sum(lens) - sum(cached)):
+                logits = self._prefill(prompts, tables, cached)
             if use_pc:
                 for p, tb in zip(prompts, tables):
                     alloc.register_prefix(p, tb)

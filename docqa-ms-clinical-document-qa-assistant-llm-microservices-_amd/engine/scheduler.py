@@ -40,6 +40,7 @@ from dataclasses import dataclass, field
 import torch
 
 from .. import ops
+from ..utils import tracing
 from .llm_engine import LLMEngine, SamplingParams, _bucket, _DecodeGraph
 
 
@@ -216,8 +217,9 @@ class ContinuousEngine:
         eng, alloc = self.eng, self.eng.kv.allocator
         t0 = time.perf_counter()
         try:
-            logits = eng._prefill([r.prompt for r in adm], [r.blocks for r in adm], [r.cached for r in adm])
-            first = self._sample_rows(logits, [r.params for r in adm])
+            with tracing.span("sched.admit", seqs=len(adm), tokens=sum(len(r.prompt) - r.cached for r in adm)):
+                logits = eng._prefill([r.prompt for r in adm], [r.blocks for r in adm], [r.cached for r in adm])
+                first = self._sample_rows(logits, [r.params for r in adm])
         except Exception as e:  # noqa: BLE001
             for r in adm:
                 alloc.free(r.blocks)
@@ -301,14 +303,15 @@ class ContinuousEngine:
         greedy = all(r.params.temperature <= 0 for r in self.running)
         g = self._graph(bp, greedy, self._nshared > 0)
         t0 = time.perf_counter()
-        if eng.use_graphs:
-            if g.graph is None:
-                if self._pool is None:
-                    self._pool = torch.cuda.graph_pool_handle()
-                eng._capture(g, self._pool)
-            g.graph.replay()
-        else:
-            eng._step_body(g)
+        with tracing.span("sched.decode", running=n, bucket=bp, cascade=self._nshared > 0):
+            if eng.use_graphs:
+                if g.graph is None:
+                    if self._pool is None:
+                        self._pool = torch.cuda.graph_pool_handle()
+                    eng._capture(g, self._pool)
+                g.graph.replay()
+            else:
+                eng._step_body(g)
         eng.stats.generated_tokens += n
         self.steps += 1
         snap = list(self.running)

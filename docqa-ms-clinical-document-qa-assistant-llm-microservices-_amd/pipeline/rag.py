@@ -18,6 +18,7 @@ from dataclasses import dataclass, field
 
 import torch
 
+from ..utils import tracing
 from ..engine.llm_engine import LLMEngine, SamplingParams
 
 # Expert-assistant prompt with the same slots as the reference's QA_CHAIN_PROMPT
@@ -107,15 +108,19 @@ class RAGPipeline:
         params = params or SamplingParams(stop_on_eos=True)
         t = StageTimes()
         t0 = time.perf_counter()
-        qemb = self.embed(questions)
-        self._sync()
+        with tracing.span("rag.embed", n=len(questions)):
+            qemb = self.embed(questions)
+            self._sync()
         t1 = time.perf_counter()
-        D, I = self.index.search(qemb, self.k)
-        I = I.tolist()  # host needs ids to assemble the prompts
+        with tracing.span("rag.search", n=len(questions), k=self.k):
+            D, I = self.index.search(qemb, self.k)
+            I = I.tolist()  # host needs ids to assemble the prompts
         t2 = time.perf_counter()
-        prompts = self.build_prompts(questions, I)
+        with tracing.span("rag.prompt", n=len(questions)):
+            prompts = self.build_prompts(questions, I)
         t3 = time.perf_counter()
-        outs = self.engine.generate(prompts, params)
+        with tracing.span("rag.generate", n=len(prompts)):
+            outs = self.engine.generate(prompts, params)
         t4 = time.perf_counter()
         t.embed_s, t.search_s, t.prompt_s, t.generate_s = t1 - t0, t2 - t1, t3 - t2, t4 - t3
         self.last_times = t
@@ -135,6 +140,8 @@ class RAGPipeline:
         generation is ``lead_steps`` from its end), then host-side prompt assembly."""
         t0 = time.perf_counter()
         ev_start = None
+        sp = tracing.span("rag.prepare", n=len(questions))
+        sp.__enter__()
         if stream is not None:
             with torch.cuda.stream(stream):
                 if gate is not None:
@@ -150,6 +157,7 @@ class RAGPipeline:
             I = I.tolist()
         t1 = time.perf_counter()
         prompts = self.build_prompts(questions, I)
+        sp.__exit__(None, None, None)
         return questions, I, prompts, ev_start, t0, t1, time.perf_counter()
 
     @torch.inference_mode()

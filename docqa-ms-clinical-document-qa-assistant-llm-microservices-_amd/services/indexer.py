@@ -37,6 +37,7 @@ from ..pipeline.corpus import embed_records
 from ..schemas import SearchRequest
 from ..store import metadata_io
 from ..text.chunking import chunk_chars
+from ..utils import tracing
 from ..text.kb import kb_records_from_dir, synthetic_kb_records
 
 logger = logging.getLogger("semantic-indexer")
@@ -96,7 +97,8 @@ class SemanticIndexer:
         recs = [r for r in records if r.get("text_content", "").strip()]
         if not recs:
             return 0
-        emb = embed_records(self.encoder, self.tok, recs)
+        with tracing.span("indexer.embed", chunks=len(recs)):
+            emb = embed_records(self.encoder, self.tok, recs)
         with self.lock:
             if self.index is None:
                 self.index = FlatIndex(self.encoder.cfg.hidden, "l2", self.device)
@@ -215,6 +217,10 @@ def create_app(indexer: SemanticIndexer) -> FastAPI:
     @app.get("/health")
     def health():
         return {"status": "ok", "service": "semantic-indexer"}
+
+    @app.get("/debug/trace")
+    def trace_dump():
+        return tracing.chrome_trace()
 
     @app.get("/api/index/stats")
     def stats():

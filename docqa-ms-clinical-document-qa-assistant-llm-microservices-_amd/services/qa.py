@@ -31,6 +31,7 @@ from fastapi.responses import JSONResponse, PlainTextResponse
 from ..config import Settings
 from ..engine.llm_engine import SamplingParams
 from ..schemas import AskResponse, Query, SummarizeRequest, SummarizeResponse
+from ..utils import tracing
 from ..utils.metrics import Metrics
 
 
@@ -235,5 +236,14 @@ def create_app(pipeline=None, settings: Settings | None = None) -> FastAPI:
     @app.get("/metrics")
     def prom():
         return PlainTextResponse(metrics.render())
+
+    @app.get("/debug/trace")
+    def trace_dump():
+        """Chrome / Perfetto trace-event JSON of the recorded spans (DOCQA_TRACE=1)."""
+        return tracing.chrome_trace()
+
+    @app.get("/debug/trace/summary")
+    def trace_summary():
+        return {"enabled": tracing.enabled(), "spans": tracing.summary()}
 
     return app

@@ -339,3 +339,24 @@ def test_qa_concurrent_asks_both_serving_modes(tmp_path, mode):
                 assert isinstance(f.result(timeout=300).json()["summary"], str)
     finally:
         s.close()
+
+
+def test_tracing_spans_and_chrome_export(stack):
+    """DOCQA_TRACE spans around the RAG stages / engine / scheduler, exported as
+    trace-event JSON by the llm-qa service."""
+    from docqa_amd.utils import tracing
+
+    tracing.enable(True)
+    tracing.clear()
+    try:
+        qa = TestClient(stack.qa_app)
+        assert qa.post("/ask/", json={"question": "Quelles plantes pour un Vide de Qi ?"}).status_code == 200
+        names = {e["name"] for e in tracing.events()}
+        assert {"sched.admit", "sched.decode"} <= names or {"rag.embed", "rag.generate"} <= names
+        tr = qa.get("/debug/trace").json()
+        xs = [e for e in tr["traceEvents"] if e["ph"] == "X"]
+        assert xs and all(e["dur"] >= 0 and "ts" in e for e in xs)
+        summ = qa.get("/debug/trace/summary").json()
+        assert summ["enabled"] and summ["spans"]
+    finally:
+        tracing.enable(False)
