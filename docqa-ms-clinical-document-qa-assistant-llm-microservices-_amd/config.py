@@ -51,6 +51,10 @@ class Settings:
     index_dir: str = field(default_factory=lambda: os.getenv("INDEX_DIR", "."))
     index_file: str = field(default_factory=lambda: os.getenv("INDEX_FILE", "vector_store.faiss"))
     metadata_file: str = field(default_factory=lambda: os.getenv("METADATA_FILE", "metadata_store.pkl"))
+    # durability: every indexed batch is appended to <index>.wal (O(batch) bytes); the
+    # FAISS + pickle snapshot pair is rewritten every INDEX_SNAPSHOT_EVERY batches
+    index_wal: bool = field(default_factory=lambda: env_bool("INDEX_WAL", "true"))
+    snapshot_every: int = field(default_factory=lambda: env_int("INDEX_SNAPSHOT_EVERY", 16))
     default_data_dir: str = field(default_factory=lambda: os.getenv("DEFAULT_DATA_DIR", "default_data"))
     chunk_size: int = field(default_factory=lambda: env_int("CHUNK_SIZE", 500))
     embed_model: str = field(default_factory=lambda: os.getenv("EMBED_MODEL", "minilm-l6"))

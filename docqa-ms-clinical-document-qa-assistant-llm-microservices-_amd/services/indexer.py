@@ -7,8 +7,11 @@ Reference (semantic-indexer/indexer.py:11-143):
     ``"Dossier Patient {doc_id}"`` / ``"patient_file"``, add, save, ack;
   * ``add_to_index`` skips blank text.
 Fixes, each covered by tests: the whole document is embedded in one packed GPU batch
-instead of one encode per chunk; snapshots are atomic (temp + rename, index before
-metadata) so a reader never sees mismatched lengths; one writer lock serialises index
+instead of one encode per chunk; a batch is made durable by one append to a CRC-framed
+write-ahead log (store/segment_log.py) and acked, the full snapshot pair is rewritten
+only every ``INDEX_SNAPSHOT_EVERY`` batches (the reference rewrites O(N x d) bytes per
+document), resume = snapshot + WAL replay; snapshots are atomic (temp + rename, index
+before metadata) so a reader never sees mismatched lengths; one writer lock serialises index
 mutation (multiple consumers are safe); the QA side shares the live index object in
 process (no restart needed to see new documents); metadata ``doc_id`` is the real
 document id.
@@ -36,6 +39,7 @@ from ..index.flat import FlatIndex
 from ..pipeline.corpus import embed_records
 from ..schemas import SearchRequest
 from ..store import metadata_io
+from ..store.segment_log import SegmentLog, read_snapshot_marker, write_snapshot_marker
 from ..text.chunking import chunk_chars
 from ..utils import tracing
 from ..text.kb import kb_records_from_dir, synthetic_kb_records
@@ -58,6 +62,8 @@ class SemanticIndexer:
         self._depth = None          # broker queue-depth probe (group commit), None: per message
         self._pending: list = []
         self.version = 0
+        self.wal = SegmentLog(self.index_path.with_name(self.index_path.name + ".wal")) if self.st.index_wal else None
+        self._batches_since_snapshot = 0
 
     # ------------------------------------------------------------------ paths
     @property
@@ -69,21 +75,40 @@ class SemanticIndexer:
         return Path(self.st.index_dir) / self.st.metadata_file
 
     # ------------------------------------------------------------------ lifecycle
+    @property
+    def marker_path(self) -> Path:
+        return self.index_path.with_name(self.index_path.name + ".snapshot.json")
+
     def startup(self, build_if_missing: bool = True) -> "SemanticIndexer":
         with self.lock:
+            dirty = False
+            covered = 0
             if self.index_path.exists() and self.meta_path.exists():
                 self.index = FlatIndex.load(self.index_path, device=self.device)
                 self.metadata = metadata_io.read_metadata(self.meta_path)
                 if len(self.metadata) != self.index.ntotal:
                     raise RuntimeError(f"index/metadata mismatch: {self.index.ntotal} vs {len(self.metadata)}")
+                covered = read_snapshot_marker(self.marker_path)["wal_seq"]
                 logger.info("resumed index (%d vectors)", self.index.ntotal)
             else:
                 self.index = FlatIndex(self.encoder.cfg.hidden, "l2", self.device)
                 self.metadata = []
                 if build_if_missing:
                     recs = kb_records_from_dir(self.st.default_data_dir) or synthetic_kb_records()
-                    self.add_records(recs)
-                    self.save_state()
+                    self.add_records(recs, log=False)
+                    dirty = True
+            if self.wal is not None:   # batches made durable after the last snapshot
+                replayed = 0
+                for _, recs, vecs in self.wal.replay(after_seq=covered):
+                    self.index.add(torch.from_numpy(vecs.copy()))
+                    self.metadata.extend(recs)
+                    replayed += len(recs)
+                if replayed:
+                    logger.info("replayed %d vectors from the write-ahead log", replayed)
+                    self.version += 1
+                    dirty = True
+            if dirty:
+                self.save_state()
         return self
 
     def save_state(self) -> None:
@@ -91,9 +116,21 @@ class SemanticIndexer:
             Path(self.st.index_dir).mkdir(parents=True, exist_ok=True)
             self.index.save(self.index_path)            # atomic
             metadata_io.write_metadata(self.meta_path, self.metadata)  # atomic
+            if self.wal is not None:                    # snapshot covers the whole log
+                seq = self.wal.last_seq
+                write_snapshot_marker(self.marker_path, seq, self.index.ntotal)
+                self.wal.reset(seq)
+            self._batches_since_snapshot = 0
+
+    def commit(self) -> None:
+        """Make the batches indexed so far durable: a WAL append already did; take a
+        full snapshot every ``snapshot_every`` batches (always, without a WAL)."""
+        self._batches_since_snapshot += 1
+        if self.wal is None or self._batches_since_snapshot >= self.st.snapshot_every:
+            self.save_state()
 
     # ------------------------------------------------------------------ mutation
-    def add_records(self, records: list[dict]) -> int:
+    def add_records(self, records: list[dict], log: bool = True) -> int:
         recs = [r for r in records if r.get("text_content", "").strip()]
         if not recs:
             return 0
@@ -102,6 +139,8 @@ class SemanticIndexer:
         with self.lock:
             if self.index is None:
                 self.index = FlatIndex(self.encoder.cfg.hidden, "l2", self.device)
+            if log and self.wal is not None:           # durable before it is visible
+                self.wal.append(recs, emb.float().cpu().numpy())
             self.index.add(emb)
             self.metadata.extend(recs)
             self.version += 1
@@ -150,7 +189,7 @@ class SemanticIndexer:
                 c.basic_nack(delivery_tag=m.delivery_tag, requeue=False)
         try:
             n = self.add_records(recs)
-            self.save_state()
+            self.commit()
         except Exception as e:  # noqa: BLE001
             logger.error("indexing error: %s", e)
             for c, m, _ in done:
