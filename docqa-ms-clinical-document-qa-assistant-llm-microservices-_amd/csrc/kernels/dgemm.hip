@@ -85,12 +85,12 @@ __device__ __forceinline__ float row_swap8(float v) {
 // the W stage in LDS (NT 16-row n-tiles) is shared by all of them; KW = 4 / MT k-groups
 // are summed through LDS at the end.  MT = 8: wave w owns m-tiles 2w, 2w+1 (MPW = 2) over
 // the whole k-block (KW = 1).
-template <int EPI, int MT, int NT, int NSR>
+template <int EPI, int MT, int NT, int NSR, int XA = 2>
 __global__ __launch_bounds__(256) void dgemm_kernel(const uint16_t* __restrict__ X,
                                                     const uint16_t* __restrict__ W,
                                                     uint16_t* __restrict__ Y,
                                                     float* __restrict__ P, int M, int N, int K,
-                                                    int Ks) {
+                                                    int Ks, int xcd_remap) {
   constexpr int MPW = MT > 4 ? MT / 4 : 1;       // m-tiles per wave
   constexpr int MTW = MT > 4 ? 4 : MT;           // wave groups along m
   constexpr int KW = 4 / MTW, SPW = KSTEPS / KW;
@@ -99,8 +99,19 @@ __global__ __launch_bounds__(256) void dgemm_kernel(const uint16_t* __restrict__
   static_assert(NSR >= 4, "ring needs >= 4 slots");
   static_assert(MT <= 4 || MT == 8, "MT in {1, 2, 4, 8}");
   __shared__ __attribute__((aligned(16))) uint16_t sw[NSR * STAGE];   // W ring
-  const int n0 = blockIdx.x * NT * 16;
-  const int slice = blockIdx.y;
+  // XCD-aware split-K placement: workgroups are dealt to the 8 XCDs round-robin by linear
+  // id, so with the plain (tile, slice) grid every XCD sees every K slice and its 4 MB L2
+  // must hold all of X next to the weight stream.  Remapped, XCD x only runs slice x % S:
+  // its L2 holds 1/S of X and the re-reads of X by its workgroups hit there.
+  int tile = blockIdx.x, slice = blockIdx.y;
+  if (xcd_remap) {
+    const int S = gridDim.y;
+    const int L = blockIdx.x + blockIdx.y * gridDim.x;
+    const int xcd = L & 7, j = L >> 3;
+    slice = xcd % S;
+    tile = j * (8 / S) + xcd / S;
+  }
+  const int n0 = tile * NT * 16;
   const int kbeg = slice * Ks;
   const int nkb = Ks / BKD;
   const int tid = threadIdx.x, lane = tid & 63;
@@ -169,25 +180,44 @@ __global__ __launch_bounds__(256) void dgemm_kernel(const uint16_t* __restrict__
   // while R-2 W stages stay in flight; the barrier then publishes stage i to every wave
   // and frees slot (i-1) % R for W(i+R-1).
   bf16x8 x0[XR], x1[XR], x2[XR], x3[XR];
-#pragma unroll
-  for (int j = 0; j <= NSR - 4; ++j) stage_w(j);
-  load_x(x0, 0);
-  stage_w(NSR - 3);
-  load_x(x1, 1);
-  stage_w(NSR - 2);
-#define RING_STEP(I, XC, XN)                                                            \
-  wait_vm_n<2 * NT + XR>(XC);                                                           \
+#define RING_STEP(I, XC, XN, NW)                                                        \
+  wait_vm_n<NW>(XC);                                                                    \
   ring_barrier();                                                                       \
-  load_x(XN, (I) + 2);                                                                  \
+  load_x(XN, (I) + XA);                                                                 \
   stage_w((I) + NSR - 1);                                                               \
   mma(XC, I);
-  // nkb % 4 == 0: a break-free 4-step body keeps each X buffer in one register set (an
-  // early exit makes hipcc merge buffers with register copies that read in-flight data)
-  for (int i = 0; i < nkb; i += 4) {
-    RING_STEP(i, x0, x2)
-    RING_STEP(i + 1, x1, x3)
-    RING_STEP(i + 2, x2, x0)
-    RING_STEP(i + 3, x3, x1)
+  if constexpr (XA == 2) {
+#pragma unroll
+    for (int j = 0; j <= NSR - 4; ++j) stage_w(j);
+    load_x(x0, 0);
+    stage_w(NSR - 3);
+    load_x(x1, 1);
+    stage_w(NSR - 2);
+    // nkb % 4 == 0: a break-free 4-step body keeps each X buffer in one register set (an
+    // early exit makes hipcc merge buffers with register copies that read in-flight data)
+    for (int i = 0; i < nkb; i += 4) {
+      RING_STEP(i, x0, x2, 2 * NT + XR)
+      RING_STEP(i + 1, x1, x3, 2 * NT + XR)
+      RING_STEP(i + 2, x2, x0, 2 * NT + XR)
+      RING_STEP(i + 3, x3, x1, 2 * NT + XR)
+    }
+  } else {
+    // X three k-blocks ahead (the 65-128-row case, where X -- not W -- is the longer
+    // pole): issue W0 X0 W1 X1 W2 X2 | step i: X(i+3) W(i+3).  W(i) now follows X(i), and
+    // the ops after W(i) are X(i+1) W(i+1) X(i+2) W(i+2): vmcnt(2 (NT + XR)) retires both.
+    static_assert(NSR == 4, "X-ahead-3 schedule is written for a 4-slot ring");
+    stage_w(0);
+    load_x(x0, 0);
+    stage_w(1);
+    load_x(x1, 1);
+    stage_w(2);
+    load_x(x2, 2);
+    for (int i = 0; i < nkb; i += 4) {
+      RING_STEP(i, x0, x3, 2 * (NT + XR))
+      RING_STEP(i + 1, x1, x0, 2 * (NT + XR))
+      RING_STEP(i + 2, x2, x1, 2 * (NT + XR))
+      RING_STEP(i + 3, x3, x2, 2 * (NT + XR))
+    }
   }
 #undef RING_STEP
   // drain the clamped tail loads; naming every X buffer keeps their registers reserved
@@ -277,13 +307,36 @@ int docqa_dgemm_splits(int N, int K) {
   return s;
 }
 
+static int xa_knob() {   // X prefetch distance for 65-128 rows (tuning experiments)
+  static const int v = [] {
+    const char* e = getenv("DOCQA_DGEMM_XA");
+    return e ? atoi(e) : 0;
+  }();
+  return v;
+}
+
+static int xcd_knob() {   // XCD-aware slice placement (A/B experiments): 1 on, 0 off
+  static const int v = [] {
+    const char* e = getenv("DOCQA_DGEMM_XCD");
+    return e ? atoi(e) : 1;
+  }();
+  return v;
+}
+
 template <int EPI, int NT, int NSR = NS>
 static void launch_mt(int mt, dim3 grid, hipStream_t s, const uint16_t* x, const uint16_t* w,
                       uint16_t* y, float* p, int M, int N, int K, int Ks) {
-  if (mt == 1) dgemm_kernel<EPI, 1, NT, NSR><<<grid, 256, 0, s>>>(x, w, y, p, M, N, K, Ks);
-  else if (mt == 2) dgemm_kernel<EPI, 2, NT, NSR><<<grid, 256, 0, s>>>(x, w, y, p, M, N, K, Ks);
-  else if (mt <= 4) dgemm_kernel<EPI, 4, NT, NSR><<<grid, 256, 0, s>>>(x, w, y, p, M, N, K, Ks);
-  else dgemm_kernel<EPI, 8, NT, NSR><<<grid, 256, 0, s>>>(x, w, y, p, M, N, K, Ks);
+  const int S = grid.y;
+  const int xr = (xcd_knob() && S > 1 && 8 % S == 0 && (grid.x * S) % 8 == 0) ? 1 : 0;
+  if (mt == 1) dgemm_kernel<EPI, 1, NT, NSR><<<grid, 256, 0, s>>>(x, w, y, p, M, N, K, Ks, xr);
+  else if (mt == 2) dgemm_kernel<EPI, 2, NT, NSR><<<grid, 256, 0, s>>>(x, w, y, p, M, N, K, Ks, xr);
+  else if (mt <= 4) dgemm_kernel<EPI, 4, NT, NSR><<<grid, 256, 0, s>>>(x, w, y, p, M, N, K, Ks, xr);
+  else if constexpr (NSR == 4) {
+    if (xa_knob() == 3) dgemm_kernel<EPI, 8, NT, NSR, 3><<<grid, 256, 0, s>>>(x, w, y, p, M, N, K, Ks, xr);
+    else dgemm_kernel<EPI, 8, NT, NSR><<<grid, 256, 0, s>>>(x, w, y, p, M, N, K, Ks, xr);
+  } else {
+    dgemm_kernel<EPI, 8, NT, NSR><<<grid, 256, 0, s>>>(x, w, y, p, M, N, K, Ks, xr);
+  }
 }
 
 static bool shape_ok(int M, int N, int K, int S, int bn) {
@@ -340,7 +393,11 @@ int docqa_dgemm_glu(const void* X, const void* W, void* Y, int M, int N, int K, 
   const int mt = (M + 15) / 16;
   const uint16_t* x = (const uint16_t*)X;
   const uint16_t* w = (const uint16_t*)W;
-  if (shape_ok(M, N, K, 1, 112) && N / 112 >= 192) {
+  static const int glu_nt = [] {   // tile-width knob (tuning experiments): 4 -> 64-row tiles
+    const char* e = getenv("DOCQA_GLU_NT");
+    return e ? atoi(e) : 0;
+  }();
+  if (glu_nt != 4 && shape_ok(M, N, K, 1, 112) && N / 112 >= 192) {
     launch_mt<EPI_GLU, 7>(mt, dim3(N / 112), s, x, w, (uint16_t*)Y, nullptr, M, N, K, K);
   } else if (shape_ok(M, N, K, 1, 64)) {
     launch_mt<EPI_GLU, 4>(mt, dim3(N / 64), s, x, w, (uint16_t*)Y, nullptr, M, N, K, K);
