@@ -23,7 +23,10 @@ def main():
     nat = torch.ops.docqa
     res = []
     Hq, Hkv, D, BS = 32, 8, 128, 64
-    for (B, ctx) in [(64, 640), (64, 1024), (32, 640), (8, 1024), (1, 4096)]:
+    shapes = [(64, 640), (64, 1024), (32, 640), (8, 1024), (1, 4096)]
+    if os.environ.get("SHAPES"):
+        shapes = [tuple(int(v) for v in x.split("x")) for x in os.environ["SHAPES"].split(",")]
+    for (B, ctx) in shapes:
         maxb = (ctx + BS - 1) // BS
         nbytes = 2 * B * maxb * Hkv * BS * D * 2
         copies = max(2, (1 << 30) // nbytes + 1)
@@ -41,7 +44,8 @@ def main():
         res.append({"B": B, "ctx": ctx, "us": round(t, 1), "kv_TBps": round(2 * B * ctx * Hkv * D * 2 / t / 1e6, 2)})
         del caches
         torch.cuda.empty_cache()
-    print(json.dumps({"wg_target": os.environ.get("DOCQA_DECODE_WG_TARGET", "512"),
+    print(json.dumps({"mfma": os.environ.get("DOCQA_DECODE_MFMA", "1"), "nsr": os.environ.get("DOCQA_DECODE_NSR", "4"),
+                      "wg_target": os.environ.get("DOCQA_DECODE_WG_TARGET", "512"),
                       "U": os.environ.get("DOCQA_DECODE_U", "2"), "rows": res}), flush=True)
 
 

@@ -34,6 +34,39 @@
 using namespace docqa;
 
 constexpr int kMinChunk = 64;   // smallest context slice worth a workgroup
+typedef __attribute__((address_space(3))) i16x4 lds_i16x4;
+
+// KV heads per workgroup of the MFMA decode kernel in the one-partition regime (knob)
+static int hpw_knob() {
+  static const int v = [] {
+    const char* e = getenv("DOCQA_DECODE_HPW");
+    return e ? atoi(e) : 1;
+  }();
+  return v;
+}
+
+// ring slots of the MFMA decode kernel (knob): 3 -> 48 KB LDS, 3 workgroups per CU
+static int mfma_nsr() {
+  static const int v = [] {
+    const char* e = getenv("DOCQA_DECODE_NSR");
+    return e ? atoi(e) : 4;
+  }();
+  return v;
+}
+
+// MFMA vs VALU decode kernel.  Measured on HBM-resident caches
+// (benchmarks/bench_decode_attn.py, profiles/r1_decode_attention_mfma_ab.log): at G = 4 both
+// are LDS-DMA-stream bound (~4 TB/s at 320-640 tokens) and the VALU ring kernel is a few %
+// ahead; the MFMA kernel wins on long contexts (5.2 vs 4.6 TB/s at 2k tokens) and its
+// per-token cost does not grow with G, so it is the default for G >= 8 (Llama-3-70B).
+// DOCQA_DECODE_MFMA=1 / 0 forces it on / off.
+static bool mfma_decode_on(int G) {
+  static const int v = [] {
+    const char* e = getenv("DOCQA_DECODE_MFMA");
+    return e ? atoi(e) : -1;
+  }();
+  return v == 1 || (v < 0 && G >= 8);
+}
 constexpr float kLog2e = 1.4426950408889634f;
 
 // Adaptive split: the grid has a fixed number of splits per (sequence, kv head) --
@@ -488,6 +521,253 @@ __global__ __launch_bounds__(256) void paged_decode_ring_kernel(
                                  Hkv, max_parts, tmp_out, tmp_ml, out, out_stride, ci);
 }
 
+// ---------------------------------------------------------------------------------------
+// MFMA decode attention (GQA, G query heads per KV head, head_dim 128, 64-token blocks).
+// The VALU kernels above spend ~10 instructions per (token, head) on 16-lane dot-product
+// reductions and per-score exponentials, which leaves them VALU-bound once the context is
+// short (profiled: the ring kernel at 63 % VALU-active with 2 waves/SIMD on 340-token
+// suffixes).  Here each 32-token K/V tile (same LDS-DMA ring as the ring kernel) feeds:
+//   S^T[16 tok x 16 col] = K[16 tok x 128] . Q^T   -- 4 v_mfma_f32_16x16x32_bf16 per 16
+//     tokens; the G heads are columns 0..G-1 of the B operand (the rest zero);
+//   online softmax on the accumulator: each lane holds 4 tokens of ONE head, a head's 16
+//     tokens live on lanes l, l^16, l^32, l^48 (two xor-shuffles per reduction);
+//   O^T[dims x 16] += V^T . P^T -- v_mfma_f32_16x16x16_bf16 with P^T taken straight from
+//     the S^T accumulator (its layout IS the B operand) and V^T fragments from a
+//     ds_read_b64_tr_b16 transposed read of the row-major V tile (cdna_hip_programming.md
+//     T10; XOR-swizzled image (b) so the reads are conflict-free).
+// Every wave computes S for the whole tile (4 x cheaper than any cross-wave softmax merge)
+// and owns 32 of the 128 output dims, so the epilogue needs no LDS reduction at all.
+// K tiles are swizzled for the 16-lane ds_read_b128 row reads (slot = chunk ^ (row & 15)).
+__device__ __forceinline__ int vswz(int t) { return ((t & 3) << 2) | ((t >> 2) & 3); }
+
+template <int G, bool DIRECT, int HPW = 1, int NSR = 4>
+__global__ __launch_bounds__(256) void paged_decode_mfma_kernel(
+    const uint16_t* __restrict__ q, int q_stride, const uint16_t* __restrict__ k_cache,
+    const uint16_t* __restrict__ v_cache, const int* __restrict__ block_tables, int maxb,
+    const int* __restrict__ context_lens, float* __restrict__ tmp_out,
+    float* __restrict__ tmp_ml, int Hkv, int max_parts, float scale,
+    uint16_t* __restrict__ out, int out_stride, CascadeIn ci) {
+  static_assert(G <= 16, "heads are MFMA columns");
+  constexpr int D = 128, TT = 32;
+  static_assert(NSR == 3 || NSR == 4, "ring of 3 (48 KB: 3 workgroups/CU) or 4 slots");
+  constexpr int TILE = TT * D;                   // elements of one K (or V) tile: 8 KB
+  __shared__ __attribute__((aligned(16))) uint16_t ring[NSR * 2 * TILE];   // 48 / 64 KB
+  __shared__ int s_bt[256];
+
+  // HPW KV heads per workgroup, one after the other through the same ring (the K/V tile
+  // stream runs on across the head boundary): 1/HPW of the workgroups -- one launch round
+  // at batch 128 -- and the next head's ring fill overlaps the current head's tail.
+  const int part = blockIdx.x, kvh0 = blockIdx.y * HPW, b = blockIdx.z;
+  const int L = context_lens[b];
+  const int P = ci.plen ? *ci.plen : 0;
+  const int slice = split_chunk(L - P, max_parts);
+  const int start = P + part * slice;
+  if (start >= L) {
+    if (DIRECT && L <= P)
+      for (int i = threadIdx.x; i < HPW * G * D; i += 256) out[(size_t)b * out_stride + (size_t)kvh0 * G * D + i] = 0;
+    return;
+  }
+  const int n = min(L - start, slice);
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int hl = lane & 15, lg = lane >> 4;      // MFMA column (head) / lane group
+
+  const int nblk = (n + 63) >> 6;
+  for (int i = tid; i < nblk; i += 256) s_bt[i] = block_tables[(size_t)b * maxb + (start >> 6) + i];
+
+  // Q^T fragments (B operand of S^T = K Q^T): lane holds Q[head hl][32 ks + 8 lg + j]
+  bf16x8 qf[HPW][4];
+#pragma unroll
+  for (int e = 0; e < HPW; ++e) {
+    const uint16_t* qp = q + (size_t)b * q_stride + (size_t)((kvh0 + e) * G + (hl < G ? hl : 0)) * D + lg * 8;
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) {
+      uint4 v = hl < G ? *reinterpret_cast<const uint4*>(qp + ks * 32) : make_uint4(0, 0, 0, 0);
+      qf[e][ks] = __builtin_bit_cast(bf16x8, v);
+    }
+  }
+  __syncthreads();
+
+  const float qs = scale * kLog2e;
+  const int ntile = (n + TT - 1) / TT;           // tiles per head
+  const int ntot = HPW * ntile;                  // the workgroup's tile stream
+  const uint32_t ring_base = lds_u32(ring);
+  const int prow = lane >> 4, pslot = lane & 15;  // DMA piece geometry: 4 rows x 16 slots
+  auto stage = [&](int j) {
+    const int jj = min(j, ntot - 1);
+    const int e = HPW == 1 ? 0 : jj / ntile;
+    const int tok0 = (jj - e * ntile) * TT;
+    const size_t row0 = ((size_t)s_bt[tok0 >> 6] * Hkv) * 64 + (size_t)(kvh0 + e) * 64 + (tok0 & 63);
+    const uint16_t* kp = k_cache + row0 * D;
+    const uint16_t* vp = v_cache + row0 * D;
+    const uint32_t dst = ring_base + (uint32_t)((j % NSR) * 2 * TILE * 2);
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int c = i * 4 + wave;                // 1 KB piece = tile rows 4c .. 4c+3
+      const int t = 4 * c + prow;
+      glds16<true>(kp + t * D + ((pslot ^ (t & 15)) << 3), dst + c * 1024);
+      glds16<true>(vp + t * D + ((pslot ^ vswz(t)) << 3), dst + TILE * 2 + c * 1024);
+    }
+  };
+
+  // epilogue of one head: lane holds O^T[dim 16 dt + 4 lg + r][head hl], dt = 2 wave + dd
+  auto finish = [&](int e, float m, float l, const f32x4 (&acc)[2]) {
+    if (hl >= G) return;
+    const int h = (kvh0 + e) * G + hl;
+    if constexpr (DIRECT) {
+      float den = l;
+      float o[2][4];
+#pragma unroll
+      for (int dd = 0; dd < 2; ++dd)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) o[dd][r] = acc[dd][r];
+      const int np = ci.plen ? cascade_parts(P, ci.nchunk) : 0;
+      if (np > 0) {   // cascade: fold in the shared-prefix chunk partials
+        // (max, sum) of every chunk first (loads issued together), then the accumulators
+        // in groups of 4 chunks: bounded registers, 8 loads in flight per group
+        const size_t B = gridDim.z, Hq = (size_t)Hkv * G;
+        float pm[kCascadeMaxChunks], pl[kCascadeMaxChunks];
+#pragma unroll
+        for (int c = 0; c < kCascadeMaxChunks; ++c) {
+          const size_t r = ((size_t)min(c, np - 1) * B + b) * Hq + h;
+          const float2 mlv = *reinterpret_cast<const float2*>(ci.ml + r * 2);
+          pm[c] = c < np ? mlv.x : -FLT_MAX;
+          pl[c] = mlv.y;
+        }
+        float M2 = m;
+#pragma unroll
+        for (int c = 0; c < kCascadeMaxChunks; ++c) M2 = fmaxf(M2, pm[c]);
+        const float f0 = exp2f(m - M2);
+        den = l * f0;
+#pragma unroll
+        for (int dd = 0; dd < 2; ++dd)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) o[dd][r] *= f0;
+        for (int c0 = 0; c0 < np; c0 += 4) {
+          f32x4 pa[4][2];
+#pragma unroll
+          for (int cc = 0; cc < 4; ++cc) {
+            const size_t r = ((size_t)min(c0 + cc, np - 1) * B + b) * Hq + h;
+#pragma unroll
+            for (int dd = 0; dd < 2; ++dd)
+              pa[cc][dd] = *reinterpret_cast<const f32x4*>(ci.acc + r * D + 16 * (2 * wave + dd) + 4 * lg);
+          }
+#pragma unroll
+          for (int cc = 0; cc < 4; ++cc) {
+            float pmc = -FLT_MAX, plc = 0.f;
+#pragma unroll
+            for (int c = 0; c < kCascadeMaxChunks; ++c)
+              if (c == c0 + cc) { pmc = pm[c]; plc = pl[c]; }
+            const float f = pmc == -FLT_MAX ? 0.f : exp2f(pmc - M2);
+            den += f * plc;
+#pragma unroll
+            for (int dd = 0; dd < 2; ++dd)
+#pragma unroll
+              for (int r = 0; r < 4; ++r) o[dd][r] += f * pa[cc][dd][r];
+          }
+        }
+      }
+      const float inv = den > 0.f ? 1.f / den : 0.f;
+      uint16_t* op = out + (size_t)b * out_stride + (size_t)h * D;
+#pragma unroll
+      for (int dd = 0; dd < 2; ++dd) {
+        uint2 v;
+        v.x = pack2(o[dd][0] * inv, o[dd][1] * inv);
+        v.y = pack2(o[dd][2] * inv, o[dd][3] * inv);
+        *reinterpret_cast<uint2*>(op + 16 * (2 * wave + dd) + 4 * lg) = v;
+      }
+    } else {
+      const size_t o = ((size_t)b * (Hkv * G) + h) * max_parts + part;
+#pragma unroll
+      for (int dd = 0; dd < 2; ++dd)
+        *reinterpret_cast<f32x4*>(tmp_out + o * D + 16 * (2 * wave + dd) + 4 * lg) = acc[dd];
+      if (wave == 0 && lg == 0) *reinterpret_cast<float2*>(tmp_ml + o * 2) = make_float2(m, l);
+    }
+  };
+
+  if (ntot > 0) {
+    stage(0);
+    stage(1);
+    if constexpr (NSR == 4) stage(2);
+  }
+  float m = -FLT_MAX, l = 0.f;
+  f32x4 acc[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
+  for (int jt = 0; jt < ntot; ++jt) {
+    const int e = HPW == 1 ? 0 : jt / ntile;     // head of this tile
+    const int i = jt - e * ntile;                // tile within the head
+    wait_vmcnt<4 * (NSR - 2)>();                 // the next NSR-2 tiles (4 DMAs each) may fly
+    ring_barrier();                              // tile jt visible; slot (jt-1) % NSR free
+    stage(jt + NSR - 1);
+    const uint16_t* kt = ring + (jt % NSR) * 2 * TILE;
+    const uint16_t* vt = kt + TILE;
+    // ---- S^T for the two 16-token halves
+    f32x4 x[2];
+#pragma unroll
+    for (int c = 0; c < 2; ++c) {
+      x[c] = f32x4{0.f, 0.f, 0.f, 0.f};
+      const int t = 16 * c + hl;
+#pragma unroll
+      for (int ks = 0; ks < 4; ++ks) {
+        const bf16x8 a = *reinterpret_cast<const bf16x8*>(kt + t * D + (((4 * ks + lg) ^ (t & 15)) << 3));
+        x[c] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, qf[e][ks], x[c], 0, 0, 0);
+      }
+    }
+    // ---- online softmax: lane = 4 tokens (16c + 4 lg + r) of head hl
+    float mx = -FLT_MAX;
+#pragma unroll
+    for (int c = 0; c < 2; ++c)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int tok = i * TT + 16 * c + 4 * lg + r;
+        const float v = tok < n ? x[c][r] * qs : -FLT_MAX;
+        x[c][r] = v;
+        mx = fmaxf(mx, v);
+      }
+    mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
+    mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+    const float m_new = fmaxf(m, mx);            // a tile always holds >= 1 live token
+    const float alpha = exp2f(m - m_new);
+    float ps = 0.f;
+#pragma unroll
+    for (int c = 0; c < 2; ++c)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float p = x[c][r] == -FLT_MAX ? 0.f : exp2f(x[c][r] - m_new);
+        x[c][r] = p;
+        ps += p;
+      }
+    ps += __shfl_xor(ps, 16, 64);
+    ps += __shfl_xor(ps, 32, 64);
+    l = l * alpha + ps;
+    m = m_new;
+#pragma unroll
+    for (int dd = 0; dd < 2; ++dd) acc[dd] *= alpha;
+    // ---- O^T += V^T P^T (this wave's 32 dims)
+#pragma unroll
+    for (int c = 0; c < 2; ++c) {
+      i16x4 pb;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) pb[r] = (short)f2bf(x[c][r]);
+      const int row = 16 * c + 4 * lg + (hl >> 2), pp = hl & 3;
+#pragma unroll
+      for (int dd = 0; dd < 2; ++dd) {
+        const int ch = 2 * (2 * wave + dd) + (pp >> 1);
+        const uint16_t* va = vt + row * D + ((ch ^ vswz(row)) << 3) + 4 * (pp & 1);
+        const i16x4 a = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_i16x4*)va);
+        acc[dd] = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(a, pb, acc[dd], 0, 0, 0);
+      }
+    }
+    if (i == ntile - 1) {                        // head e done: write it, start the next
+      finish(e, m, l, acc);
+      m = -FLT_MAX;
+      l = 0.f;
+      acc[0] = f32x4{0.f, 0.f, 0.f, 0.f};
+      acc[1] = f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+  }
+  wait_vmcnt<0>();                               // drain the clamped tail DMAs
+}
+
 // log-sum-exp merge of a sequence's context partitions (and, cascade, of the shared-prefix
 // chunk partials) -> normalised bf16 output
 template <int D>
@@ -557,6 +837,35 @@ int docqa_paged_decode(const void* q, int q_stride, const void* k_cache, const v
     if (direct) DEC_K(GG, UU, true);                                                          \
     else DEC_K(GG, UU, false);                                                                \
   } while (0)
+  if (mfma_decode_on(G) && BS == 64 && maxb <= 256 && (G == 4 || G == 8)) {
+#define DMFMA(GG)                                                                             \
+    do {                                                                                      \
+      if (direct && Hkv % 2 == 0 && hpw_knob() == 2)                                          \
+        paged_decode_mfma_kernel<GG, true, 2><<<dim3(1, Hkv / 2, B), 256, 0, s>>>(            \
+            (const uint16_t*)q, q_stride, (const uint16_t*)k_cache, (const uint16_t*)v_cache, \
+            block_tables, maxb, context_lens, tmp_out, tmp_ml, Hkv, max_parts, scale,         \
+            (uint16_t*)out, out_stride, CascadeIn{});                                         \
+      else if (direct)                                                                        \
+        paged_decode_mfma_kernel<GG, true><<<grid, 256, 0, s>>>(                              \
+            (const uint16_t*)q, q_stride, (const uint16_t*)k_cache, (const uint16_t*)v_cache, \
+            block_tables, maxb, context_lens, tmp_out, tmp_ml, Hkv, max_parts, scale,         \
+            (uint16_t*)out, out_stride, CascadeIn{});                                         \
+      else                                                                                    \
+        paged_decode_mfma_kernel<GG, false><<<grid, 256, 0, s>>>(                             \
+            (const uint16_t*)q, q_stride, (const uint16_t*)k_cache, (const uint16_t*)v_cache, \
+            block_tables, maxb, context_lens, tmp_out, tmp_ml, Hkv, max_parts, scale,         \
+            (uint16_t*)out, out_stride, CascadeIn{});                                         \
+    } while (0)
+    if (G == 4) DMFMA(4);
+    else DMFMA(8);
+#undef DMFMA
+    if (!direct)
+      paged_decode_reduce<128><<<dim3(Hq, B), 128, 0, s>>>(tmp_out, tmp_ml, context_lens,
+                                                           (uint16_t*)out, out_stride, Hq,
+                                                           max_parts);
+    DOCQA_CHECK_LAUNCH();
+    return 0;
+  }
   static const bool ring_env = [] {
     const char* e = getenv("DOCQA_DECODE_RING");
     return !(e && atoi(e) == 0);
@@ -685,7 +994,27 @@ int docqa_paged_decode_cascade(const void* q, int q_stride, void* k_cache, void*
   if (rc) return rc;
   const CascadeIn ci{pacc, pml, plen, nchunk};
   dim3 grid(max_parts, Hkv, B);
-  if (max_parts == 1)
+  if (mfma_decode_on(Hq / Hkv)) {
+    if (max_parts == 1 && Hkv % 2 == 0 && hpw_knob() == 2)
+      paged_decode_mfma_kernel<4, true, 2><<<dim3(1, Hkv / 2, B), 256, 0, s>>>(
+          (const uint16_t*)q, q_stride, (const uint16_t*)k_cache, (const uint16_t*)v_cache, block_tables, maxb,
+          context_lens, tmp_out, tmp_ml, Hkv, max_parts, scale, (uint16_t*)out, out_stride, ci);
+    else if (max_parts == 1 && mfma_nsr() == 3)
+      paged_decode_mfma_kernel<4, true, 1, 3><<<grid, 256, 0, s>>>(
+          (const uint16_t*)q, q_stride, (const uint16_t*)k_cache, (const uint16_t*)v_cache, block_tables, maxb,
+          context_lens, tmp_out, tmp_ml, Hkv, max_parts, scale, (uint16_t*)out, out_stride, ci);
+    else if (max_parts == 1)
+      paged_decode_mfma_kernel<4, true><<<grid, 256, 0, s>>>(
+          (const uint16_t*)q, q_stride, (const uint16_t*)k_cache, (const uint16_t*)v_cache, block_tables, maxb,
+          context_lens, tmp_out, tmp_ml, Hkv, max_parts, scale, (uint16_t*)out, out_stride, ci);
+    else {
+      paged_decode_mfma_kernel<4, false><<<grid, 256, 0, s>>>(
+          (const uint16_t*)q, q_stride, (const uint16_t*)k_cache, (const uint16_t*)v_cache, block_tables, maxb,
+          context_lens, tmp_out, tmp_ml, Hkv, max_parts, scale, (uint16_t*)out, out_stride, ci);
+      paged_decode_reduce<128><<<dim3(Hq, B), 128, 0, s>>>(tmp_out, tmp_ml, context_lens, (uint16_t*)out,
+                                                           out_stride, Hq, max_parts, ci);
+    }
+  } else if (max_parts == 1)
     paged_decode_ring_kernel<4, true><<<grid, 256, 0, s>>>(
         (const uint16_t*)q, q_stride, (uint16_t*)k_cache, (uint16_t*)v_cache, block_tables, maxb,
         context_lens, tmp_out, tmp_ml, Hkv, max_parts, scale, (uint16_t*)out, out_stride, FusedQKV{}, ci);
