@@ -110,7 +110,7 @@ def test_splitk_reference_ops_cpu():
     assert ops.decode_splits(64, 6144, 4096) == 2 and ops.decode_splits(64, 4096, 14336) == 4
     assert ops.decode_splits(64, 28672, 4096) == 0 and ops.decode_splits(64, 128256, 4096) == 0
     # 65-128 rows: 128-row tiles where a split reaches 192 workgroups, else 64-row tiles
-    assert ops.decode_plan(128, 6144, 4096) == (4, 128) and ops.decode_plan(128, 4096, 4096) == (8, 128)
+    assert ops.decode_plan(128, 6144, 4096) == (4, 128) and ops.decode_plan(128, 4096, 4096) == (4, 64)
     assert ops.decode_plan(128, 4096, 14336) == (4, 64) and ops.decode_plan(100, 28672, 4096)[0] == 0
     assert ops.decode_plan(129, 6144, 4096)[0] == 0
     r1 = torch.randn(5, 256).bfloat16()
