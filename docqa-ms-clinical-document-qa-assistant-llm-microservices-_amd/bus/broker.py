@@ -11,6 +11,9 @@ semantic-indexer/indexer.py:112-137):
   durable-queue + persistent-message semantics of doc-ingestor/processing.py:27,40),
   and a dead-letter queue ``<queue>.dlq`` for ``nack(requeue=False)`` -- the reference
   silently drops poison messages.
+* :class:`SpoolBroker` (``DOCQA_BUS=spool``): the same semantics across PROCESSES on
+  a shared directory (atomic-rename claims), so each service can run as its own
+  process without a broker daemon;
 * :class:`AmqpBroker`: RabbitMQ through pika when it is installed (wire-compatible
   JSON bodies, default exchange, ``delivery_mode=2``).
 """
@@ -223,6 +226,138 @@ class InProcBroker:
         return got[1]
 
 
+class SpoolChannel(InProcChannel):
+    """Channel of a :class:`SpoolBroker` (same pika-shaped API and flow control)."""
+
+    def close(self):
+        self.stop_consuming()
+        with self._lock:
+            pending = list(self._unacked.values())
+            self._unacked.clear()
+        for q, mid, body in pending:
+            self.broker._requeue(q, mid, body)
+
+
+class SpoolBroker:
+    """Multi-process durable queues on a shared directory (no daemon): one file per
+    message, FIFO by name, claimed by an atomic ``rename`` so competing consumers in
+    different processes never receive the same delivery.
+
+        <root>/<queue>/new/<id>           ready
+        <root>/<queue>/cur/<pid>-<id>     delivered to a consumer process, unacked
+        <root>/<queue>/tmp/<id>           being written (renamed into new/ when complete)
+
+    ack deletes the claimed file, ``nack(requeue=True)`` renames it back (marked
+    redelivered), ``nack(requeue=False)`` moves it to ``<queue>.dlq``; deliveries held by
+    a process that died are re-queued when any process opens the queue.  This is the
+    single-node stand-in for RabbitMQ's durable queues + persistent messages + manual ack
+    (doc-ingestor/processing.py:27,40; deid-service/anonymizer.py:79-87) that lets every
+    service run in its own process, like the reference's start_all.bat, with no broker
+    to install."""
+
+    POLL_S = 0.01
+
+    def __init__(self, root: str, fsync: bool = False):
+        self.root = Path(root)
+        self.root.mkdir(parents=True, exist_ok=True)
+        self.fsync = fsync
+        self._tags = itertools.count(1)
+        self._ids = itertools.count(1)
+        self._declared: set[str] = set()
+        self._lock = threading.Lock()
+
+    def _dirs(self, q: str):
+        base = self.root / q
+        return base / "new", base / "cur", base / "tmp"
+
+    def declare(self, name: str, durable: bool = True):
+        with self._lock:
+            if name in self._declared:
+                return name
+            self._declared.add(name)
+        new, cur, tmp = self._dirs(name)
+        for d in (new, cur, tmp):
+            d.mkdir(parents=True, exist_ok=True)
+        self._recover(name)
+        return name
+
+    def _recover(self, q: str) -> None:
+        """Re-queue deliveries whose consumer process is gone."""
+        new, cur, _ = self._dirs(q)
+        for f in cur.iterdir():
+            pid_s, _, mid = f.name.partition("-")
+            try:
+                os.kill(int(pid_s), 0)
+                alive = True
+            except (ValueError, ProcessLookupError):
+                alive = False
+            except PermissionError:
+                alive = True
+            if not alive:
+                try:
+                    os.rename(f, new / (mid if mid.endswith(".r") else mid + ".r"))
+                except FileNotFoundError:
+                    pass
+
+    def publish(self, queue: str, body: bytes) -> None:
+        self.declare(queue)
+        new, _, tmp = self._dirs(queue)
+        mid = f"{time.time_ns():020d}-{os.getpid()}-{next(self._ids)}"
+        t = tmp / mid
+        with open(t, "wb") as f:
+            f.write(body)
+            if self.fsync:
+                f.flush()
+                os.fsync(f.fileno())
+        os.rename(t, new / mid)
+
+    def _get(self, queue: str, timeout: float):
+        self.declare(queue)
+        new, cur, _ = self._dirs(queue)
+        deadline = time.monotonic() + timeout
+        while True:
+            for name in sorted(os.listdir(new)):
+                claimed = cur / f"{os.getpid()}-{name}"
+                try:
+                    os.rename(new / name, claimed)
+                except FileNotFoundError:
+                    continue                      # another consumer won this one
+                body = claimed.read_bytes()
+                return claimed.name, body, name.endswith(".r")
+            if time.monotonic() >= deadline:
+                return None
+            time.sleep(min(self.POLL_S, max(0.0, deadline - time.monotonic())))
+
+    def _journal_ack(self, queue: str, mid: str) -> None:
+        _, cur, _ = self._dirs(queue)
+        try:
+            os.unlink(cur / mid)
+        except FileNotFoundError:
+            pass
+
+    def _requeue(self, queue: str, mid: str, body: bytes) -> None:
+        new, cur, _ = self._dirs(queue)
+        name = mid.partition("-")[2]
+        try:
+            os.rename(cur / mid, new / (name if name.endswith(".r") else name + ".r"))
+        except FileNotFoundError:
+            pass
+
+    def depth(self, queue: str) -> int:
+        self.declare(queue)
+        return len(os.listdir(self._dirs(queue)[0]))
+
+    def channel(self) -> SpoolChannel:
+        return SpoolChannel(self)
+
+    def get_nowait(self, queue: str):
+        got = self._get(queue, 0.0)
+        if got is None:
+            return None
+        self._journal_ack(queue, got[0])
+        return got[1]
+
+
 class AmqpBroker:
     """RabbitMQ via pika (only when pika is importable).  Opens one connection per
     publisher call like the reference (doc-ingestor/processing.py:21-44)."""
@@ -265,6 +400,8 @@ def get_broker(settings=None):
     st = settings or _s()
     if st.bus_backend == "amqp":
         return AmqpBroker(st.rabbitmq_host)
+    if st.bus_backend == "spool":
+        return SpoolBroker(st.spool_dir)
     with _dlock:
         if _default is None:
             _default = InProcBroker(st.bus_journal_dir or None)

@@ -37,8 +37,9 @@ def env_int(name: str, default: int) -> int:
 class Settings:
     # transport / infra (reference names)
     rabbitmq_host: str = field(default_factory=lambda: os.getenv("RABBITMQ_HOST", "localhost"))
-    bus_backend: str = field(default_factory=lambda: os.getenv("DOCQA_BUS", "inproc"))  # inproc | amqp
+    bus_backend: str = field(default_factory=lambda: os.getenv("DOCQA_BUS", "inproc"))  # inproc | spool | amqp
     bus_journal_dir: str = field(default_factory=lambda: os.getenv("DOCQA_BUS_JOURNAL", ""))
+    spool_dir: str = field(default_factory=lambda: os.getenv("DOCQA_SPOOL_DIR", "docqa_spool"))  # DOCQA_BUS=spool
     db_host: str = field(default_factory=lambda: os.getenv("DB_HOST", "localhost"))
     db_port: str = field(default_factory=lambda: os.getenv("DB_PORT", "5433"))
     database_url: str = field(default_factory=lambda: os.getenv("DATABASE_URL", "sqlite:///docqa_documents.db"))

@@ -1,7 +1,15 @@
-"""Run the DocQA stack: every service on the reference's port, one process per GPU.
+"""Run the DocQA stack: every service on the reference's port, one process per GPU, or
+one process per service like the reference's start_all.bat.
 
     python -m docqa_amd.services.launch                 # full stack on cuda:0
     python -m docqa_amd.services.launch --tiny --device cpu   # CPU demo with tiny models
+    # microservices, one process each (shared spool bus, SQLite file, index directory):
+    export DOCQA_BUS=spool DOCQA_SPOOL_DIR=/srv/docqa/spool INDEX_DIR=/srv/docqa/index \
+           DATABASE_URL=sqlite:////srv/docqa/docs.db
+    python -m docqa_amd.services.launch --services ingest
+    python -m docqa_amd.services.launch --services deid --device cuda:1
+    python -m docqa_amd.services.launch --services indexer --device cuda:2
+    python -m docqa_amd.services.launch --services qa,ui --device cuda:3
 
 Ports (start_all.bat:18,31; synthese Dockerfile:27,36; clinical-ui Streamlit default):
 doc-ingestor 8000, llm-qa 8001, semantic-indexer 8003, synthese-comparative 8005, UI 8501.
@@ -33,17 +41,28 @@ def main() -> None:
     ap.add_argument("--llm", default="llama3-8b")
     ap.add_argument("--embed", default="minilm-l6")
     ap.add_argument("--real-synthese", action="store_true")
+    ap.add_argument("--services", default="", help="comma list of ingest,deid,indexer,qa,synthese,ui (default all)")
+    ap.add_argument("--port-offset", type=int, default=0, help="added to every reference port (tests)")
     a = ap.parse_args()
     logging.basicConfig(level=logging.INFO)
     opts = StackOptions(llm="tiny" if a.tiny else a.llm, embed="tiny-bert" if a.tiny else a.embed,
                         ner="tiny-bert" if a.tiny else "clinical-bert", device=a.device,
                         use_graphs=a.device != "cpu", max_context=2048 if a.tiny else 4096,
-                        real_synthese=a.real_synthese)
+                        real_synthese=a.real_synthese,
+                        services=tuple(x for x in a.services.split(",") if x))
     stack = DocQAStack(opts)
-    threads = [serve(stack.ingest_app, 8000, a.host), serve(stack.qa_app, 8001, a.host),
-               serve(stack.indexer_app, 8003, a.host), serve(stack.synthese_app, 8005, a.host),
-               serve(stack.ui_app, 8501, a.host)]
-    print("DocQA stack up: ingest :8000, llm-qa :8001, indexer :8003, synthese :8005, ui :8501", flush=True)
+    o = a.port_offset
+    apps = [("ingest", stack.ingest_app, 8000), ("llm-qa", stack.qa_app, 8001),
+            ("indexer", stack.indexer_app, 8003), ("synthese", stack.synthese_app, 8005),
+            ("ui", stack.ui_app, 8501)]
+    threads = [serve(app, port + o, a.host) for _, app, port in apps if app is not None]
+    up = ", ".join(f"{n} :{port + o}" for n, app, port in apps if app is not None)
+    extra = " (+ deid worker)" if stack.deid is not None else ""
+    print(f"DocQA up: {up or 'no HTTP service'}{extra}", flush=True)
+    if not threads:   # worker-only process (deid): keep it alive
+        import time
+        while True:
+            time.sleep(3600)
     try:
         for t in threads:
             t.join()

@@ -14,7 +14,8 @@ import logging
 import tempfile
 from dataclasses import dataclass
 
-from ..bus.broker import InProcBroker
+from ..bus.broker import InProcBroker, get_broker
+from ..index.follower import IndexFollower
 from ..config import Settings
 from ..deid.engine import NER_LABELS, DeidEngine
 from ..engine.llm_engine import LLMEngine
@@ -39,6 +40,7 @@ class StackOptions:
     use_graphs: bool = True
     ner_in_loop: bool = False     # run the (random-init) NER model inside de-identification
     real_synthese: bool = False
+    services: tuple = ()          # subset of ALL_SERVICES hosted by this process (empty: all)
 
 
 class _LocalRetrieval(synthese.RetrievalClient):
@@ -63,44 +65,82 @@ class _LocalLLM(synthese.LLMClient):
             return self._summarize_fake(prompt, max_chars)
 
 
+ALL_SERVICES = ("ingest", "deid", "indexer", "qa", "synthese", "ui")
+
+
 class DocQAStack:
+    """Build the services named in ``opts.services`` (default: all, in one process).
+
+    Several processes can each host a subset -- the reference's deployment of one
+    process per service (start_all.bat) -- when the bus crosses processes
+    (``DOCQA_BUS=spool`` or ``amqp``), the documents DB is a shared URL (SQLite file or
+    Postgres), and the indexer directory is shared: a llm-qa process without the
+    indexer follows the indexer's snapshot + write-ahead log (index/follower.py) instead
+    of holding the live index object."""
+
     def __init__(self, opts: StackOptions, settings: Settings | None = None):
         self.opts = opts
         self.st = settings or Settings()
+        svc = set(opts.services or ALL_SERVICES)
+        unknown = svc - set(ALL_SERVICES)
+        if unknown:
+            raise ValueError(f"unknown services {sorted(unknown)}")
+        self.services = svc
         if not self.st.upload_dir or self.st.upload_dir == "temp_uploads":
             self.st.upload_dir = tempfile.mkdtemp(prefix="docqa_uploads_")
         dev = opts.device
-        self.broker = InProcBroker(self.st.bus_journal_dir or None)
-        self.db = docs_db.DocsDB(self.st.database_url)
+        self.broker = (get_broker(self.st) if self.st.bus_backend != "inproc"
+                       else InProcBroker(self.st.bus_journal_dir or None))
+        self.db = docs_db.DocsDB(self.st.database_url) if svc & {"ingest", "indexer"} else None
         self.enc_tok = WordPieceTokenizer()
         llm_cfg = LlamaConfig.preset(opts.llm)
         self.chat_tok = ChatTokenizer(model_vocab=llm_cfg.vocab_size)
-        self.encoder = BertEncoder(BertConfig.preset(opts.embed), device=dev)
-        ner_model = BertTokenClassifier(BertConfig.preset(opts.ner), NER_LABELS, device=dev) if opts.ner_in_loop else None
-        self.deid_engine = DeidEngine(ner_model, self.enc_tok, use_model=opts.ner_in_loop)
-        self.indexer = indexer_mod.SemanticIndexer(
-            self.encoder, self.enc_tok, self.st, device=dev,
-            on_indexed=lambda i: self.db.set_status(i, docs_db.STATUS_INDEXED)).startup()
-        self.model = LlamaModel(llm_cfg, device=dev)
-        self.engine = LLMEngine(self.model, max_batch=opts.max_batch, max_context=opts.max_context,
-                                use_graphs=opts.use_graphs)
-        self.pipeline = RAGPipeline(self.encoder, self.enc_tok, self.indexer.index, self.indexer.metadata,
-                                    self.engine, self.chat_tok, k=self.st.top_k,
-                                    max_prompt_tokens=opts.max_context - self.st.max_new_tokens - 8)
-        self.deid = deid_worker.DeidWorker(self.deid_engine, self.st, self.broker).start()
-        self.indexer.start_consumer(self.broker)
-        self.ingest_app = ingest.create_app(self.st, self.db, self.broker)
-        self.qa_app = qa.create_app(self.pipeline, self.st)
-        self.indexer_app = indexer_mod.create_app(self.indexer)
-        if opts.real_synthese:
-            self.synthese_app = synthese.create_app(
-                self.st, _LocalLLM(self.qa_app.state.batcher, self.st), _LocalRetrieval(self.indexer, self.st))
-        else:
-            self.synthese_app = synthese.create_app(self.st)
-        self.ui_app = ui.create_app()
+        self.encoder = BertEncoder(BertConfig.preset(opts.embed), device=dev) if svc & {"indexer", "qa"} else None
+        self.deid = self.indexer = self.follower = self.engine = self.pipeline = None
+        self.ingest_app = self.qa_app = self.indexer_app = self.synthese_app = self.ui_app = None
+        if "deid" in svc:
+            ner_model = (BertTokenClassifier(BertConfig.preset(opts.ner), NER_LABELS, device=dev)
+                         if opts.ner_in_loop else None)
+            self.deid_engine = DeidEngine(ner_model, self.enc_tok, use_model=opts.ner_in_loop)
+            self.deid = deid_worker.DeidWorker(self.deid_engine, self.st, self.broker).start()
+        if "indexer" in svc:
+            db = self.db
+            self.indexer = indexer_mod.SemanticIndexer(
+                self.encoder, self.enc_tok, self.st, device=dev,
+                on_indexed=lambda i: db.set_status(i, docs_db.STATUS_INDEXED)).startup()
+            self.indexer.start_consumer(self.broker)
+            self.indexer_app = indexer_mod.create_app(self.indexer)
+        if "qa" in svc:
+            if self.indexer is not None:
+                index, metadata = self.indexer.index, self.indexer.metadata
+            else:
+                self.follower = IndexFollower(self.st.index_dir, self.st.index_file, self.st.metadata_file,
+                                              d=self.encoder.cfg.hidden, device=dev).start()
+                index, metadata = self.follower.index, self.follower.metadata
+            self.model = LlamaModel(llm_cfg, device=dev)
+            self.engine = LLMEngine(self.model, max_batch=opts.max_batch, max_context=opts.max_context,
+                                    use_graphs=opts.use_graphs)
+            self.pipeline = RAGPipeline(self.encoder, self.enc_tok, index, metadata,
+                                        self.engine, self.chat_tok, k=self.st.top_k,
+                                        max_prompt_tokens=opts.max_context - self.st.max_new_tokens - 8)
+            self.qa_app = qa.create_app(self.pipeline, self.st)
+        if "ingest" in svc:
+            self.ingest_app = ingest.create_app(self.st, self.db, self.broker)
+        if "synthese" in svc:
+            if opts.real_synthese and self.qa_app is not None and self.indexer is not None:
+                self.synthese_app = synthese.create_app(
+                    self.st, _LocalLLM(self.qa_app.state.batcher, self.st), _LocalRetrieval(self.indexer, self.st))
+            else:   # FAKE / REAL-over-HTTP per USE_FAKE_* and the service URLs (reference behaviour)
+                self.synthese_app = synthese.create_app(self.st)
+        if "ui" in svc:
+            self.ui_app = ui.create_app()
 
     def close(self) -> None:
-        self.deid.stop()
-        self.indexer.stop_consumer()
-        if self.qa_app.state.batcher is not None:
+        if self.deid is not None:
+            self.deid.stop()
+        if self.indexer is not None:
+            self.indexer.stop_consumer()
+        if self.follower is not None:
+            self.follower.stop()
+        if self.qa_app is not None and self.qa_app.state.batcher is not None:
             self.qa_app.state.batcher.stop()

@@ -119,9 +119,38 @@ class SegmentLog:
         self.bytes = good_end
 
 
+def tail_frames(path, offset: int):
+    """Read intact frames from byte ``offset`` of a log another process is appending to:
+    returns ([(seq, records, vectors)], new_offset).  An incomplete frame at the end (the
+    writer is mid-append) is left for the next call -- never truncated here."""
+    p = Path(path)
+    out = []
+    if not p.exists():
+        return out, offset
+    with open(p, "rb") as f:
+        f.seek(offset)
+        while True:
+            h = f.read(_HDR.size)
+            if len(h) < _HDR.size:
+                break
+            magic, seq, n, d, mlen, crc = _HDR.unpack(h)
+            if magic != MAGIC:
+                break
+            meta = f.read(mlen)
+            body = f.read(n * d * 4)
+            if len(meta) < mlen or len(body) < n * d * 4 or zlib.crc32(body, zlib.crc32(meta)) != crc:
+                break
+            out.append((seq, json.loads(meta), np.frombuffer(body, dtype=np.float32).reshape(n, d)))
+            offset = f.tell()
+    return out, offset
+
+
 def write_snapshot_marker(path, seq: int, ntotal: int) -> None:
+    """``t`` makes every snapshot's marker distinct, so a follower notices each one."""
+    import time
+
     tmp = Path(str(path) + ".tmp")
-    tmp.write_text(json.dumps({"wal_seq": seq, "ntotal": ntotal}))
+    tmp.write_text(json.dumps({"wal_seq": seq, "ntotal": ntotal, "t": time.time_ns()}))
     os.replace(tmp, path)
 
 

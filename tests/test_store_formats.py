@@ -125,3 +125,40 @@ def test_indexer_wal_resume_without_snapshot(tmp_path):
     assert torch.allclose(b.index.xb.float(), a.index.xb.float())
     c = SemanticIndexer(enc, tok, st, device="cpu").startup()   # b snapshotted: nothing to replay
     assert c.index.ntotal == a.index.ntotal and c.wal.bytes == 0
+
+
+def test_index_follower_tails_writer_across_snapshots(tmp_path):
+    """A reader process's follower sees every batch the indexer makes durable (WAL tail),
+    keeps them across the writer's snapshot rotations, and reloads the snapshot when it
+    missed frames."""
+    import torch
+
+    from docqa_amd.config import Settings
+    from docqa_amd.index.follower import IndexFollower
+    from docqa_amd.models.bert import BertConfig, BertEncoder
+    from docqa_amd.services.indexer import SemanticIndexer
+    from docqa_amd.text.tokenizer import WordPieceTokenizer
+
+    st = Settings()
+    st.index_dir = str(tmp_path)
+    st.default_data_dir = str(tmp_path / "nodata")
+    st.snapshot_every = 2
+    enc = BertEncoder(BertConfig.preset("tiny-bert"), device="cpu")
+    w = SemanticIndexer(enc, WordPieceTokenizer(), st, device="cpu").startup(build_if_missing=True)
+    f = IndexFollower(str(tmp_path), d=enc.cfg.hidden, device="cpu")
+    f.poll()
+    assert f.index.ntotal == w.index.ntotal == len(f.metadata)
+    for d in range(5):                      # snapshots rotate the log every 2 batches
+        w.index_document(200 + d, f"Note {d}: Vide de Qi, Rate. " * 25)
+        w.commit()
+        f.poll()
+        assert f.index.ntotal == w.index.ntotal and len(f.metadata) == f.index.ntotal
+    assert [m["doc_id"] for m in f.metadata] == [m["doc_id"] for m in w.metadata]
+    assert torch.allclose(f.index.xb.float(), w.index.xb.float())
+    g = IndexFollower(str(tmp_path), d=enc.cfg.hidden, device="cpu")   # late joiner
+    w.index_document(300, "Late note. " * 40)
+    w.commit()
+    w.index_document(301, "Later note. " * 40)
+    w.commit()                               # rotation happened before g ever polled
+    g.poll()
+    assert g.index.ntotal == w.index.ntotal
