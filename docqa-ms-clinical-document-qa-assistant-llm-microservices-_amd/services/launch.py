@@ -33,6 +33,51 @@ def serve(app, port: int, host: str) -> threading.Thread:
     return t
 
 
+def supervise(groups: list[str], argv: list[str], max_restarts: int = 10, backoff_s: float = 1.0) -> None:
+    """Run each service group as a child process and restart it when it dies (SURVEY.md
+    §5.3: the reference only retries its AMQP connection every 5 s; a process whose GPU
+    context is poisoned -- a sticky HIP error -- can only be recovered by a restart).
+    Children get DOCQA_EXIT_ON_DEVICE_ERROR=1 so a device fault ends them promptly."""
+    import os
+    import subprocess
+    import sys
+    import time
+
+    env = dict(os.environ, DOCQA_EXIT_ON_DEVICE_ERROR="1")
+    procs: dict[str, subprocess.Popen] = {}
+    restarts = {g: 0 for g in groups}
+    next_start = {g: 0.0 for g in groups}
+
+    def spawn(g: str) -> subprocess.Popen:
+        print(f"[supervisor] starting {g}", flush=True)
+        return subprocess.Popen([sys.executable, "-m", "docqa_amd.services.launch", *argv, "--services", g], env=env)
+
+    for g in groups:
+        procs[g] = spawn(g)
+    try:
+        while procs:
+            time.sleep(0.5)
+            for g, p in list(procs.items()):
+                rc = p.poll()
+                if rc is None:
+                    continue
+                if restarts[g] >= max_restarts:
+                    print(f"[supervisor] {g} exited {rc}; restart budget spent", flush=True)
+                    del procs[g]
+                    continue
+                now = time.monotonic()
+                if next_start[g] == 0.0:
+                    next_start[g] = now + backoff_s * (2 ** restarts[g])
+                    print(f"[supervisor] {g} exited {rc}; restarting", flush=True)
+                if now >= next_start[g]:
+                    restarts[g] += 1
+                    next_start[g] = 0.0
+                    procs[g] = spawn(g)
+    except KeyboardInterrupt:
+        for p in procs.values():
+            p.terminate()
+
+
 def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("--device", default="cuda")
@@ -43,7 +88,17 @@ def main() -> None:
     ap.add_argument("--real-synthese", action="store_true")
     ap.add_argument("--services", default="", help="comma list of ingest,deid,indexer,qa,synthese,ui (default all)")
     ap.add_argument("--port-offset", type=int, default=0, help="added to every reference port (tests)")
+    ap.add_argument("--supervise", default="", help='service groups, one child process each, restarted '
+                    'when they die: e.g. "ingest,ui;deid;indexer;qa"')
     a = ap.parse_args()
+    if a.supervise:
+        import sys
+
+        argv = [x for x in sys.argv[1:]]
+        i = argv.index("--supervise")
+        del argv[i:i + 2]
+        supervise([g for g in a.supervise.split(";") if g], argv)
+        return
     logging.basicConfig(level=logging.INFO)
     opts = StackOptions(llm="tiny" if a.tiny else a.llm, embed="tiny-bert" if a.tiny else a.embed,
                         ner="tiny-bert" if a.tiny else "clinical-bert", device=a.device,

@@ -103,6 +103,20 @@ class DynamicBatcher:
         self._t.join(timeout=60)
 
 
+def _maybe_exit_on_device_error(e: Exception) -> None:
+    """A HIP error is sticky: the process's GPU context cannot serve again.  Under the
+    supervisor (DOCQA_EXIT_ON_DEVICE_ERROR=1) exit so it restarts this service; otherwise
+    keep serving the error to clients (every later request fails fast)."""
+    import os
+
+    msg = f"{type(e).__name__}: {e}"
+    if os.environ.get("DOCQA_EXIT_ON_DEVICE_ERROR") == "1" and ("HIP error" in msg or "AcceleratorError" in msg):
+        import logging
+
+        logging.getLogger("llm-qa").critical("device error, exiting for a supervised restart: %s", msg)
+        os._exit(70)
+
+
 class ContinuousBatcher:
     """Scheduler thread: admit arrivals (batched embed + kNN + prompt assembly), then one
     continuous-batching engine step; repeat."""
@@ -158,6 +172,7 @@ class ContinuousBatcher:
                     self.engine.step()
                 except Exception as e:  # noqa: BLE001
                     self.engine._fail_all(e)
+                    _maybe_exit_on_device_error(e)
 
     def _admit(self, items) -> None:
         pipe, params = self.pipe, self._params()

@@ -107,3 +107,34 @@ def test_services_in_separate_processes(tmp_path):
                 os.killpg(p.pid, signal.SIGKILL)
         for lf in logs:
             lf.close()
+
+
+def test_supervisor_restarts_a_dead_service(tmp_path):
+    """--supervise runs each group as a child and restarts it after it dies."""
+    off = _free_offset()
+    env = dict(os.environ, DOCQA_BUS="spool", DOCQA_SPOOL_DIR=str(tmp_path / "spool"),
+               INDEX_DIR=str(tmp_path / "index"), DATABASE_URL=f"sqlite:///{tmp_path}/docs.db",
+               DEFAULT_DATA_DIR=str(tmp_path / "nodata"), PYTHONUNBUFFERED="1")
+    lf = open(tmp_path / "sup.log", "w")
+    sup = subprocess.Popen([sys.executable, "-m", "docqa_amd.services.launch", "--tiny", "--device", "cpu",
+                            "--port-offset", str(off), "--supervise", "ingest"], cwd=ROOT, env=env,
+                           stdout=lf, stderr=subprocess.STDOUT, start_new_session=True)
+    try:
+        url = f"http://127.0.0.1:{8000 + off}/health"
+        assert _wait(url, time.time() + 120)
+        # kill the child serving ingest (the supervisor's only child)
+        import psutil
+
+        kids = psutil.Process(sup.pid).children()
+        assert len(kids) == 1
+        kids[0].kill()
+        time.sleep(1.0)
+        assert _wait(url, time.time() + 120), (tmp_path / "sup.log").read_text()[-2000:]
+        assert "restarting" in (tmp_path / "sup.log").read_text()
+    finally:
+        os.killpg(sup.pid, signal.SIGTERM)
+        try:
+            sup.wait(timeout=20)
+        except subprocess.TimeoutExpired:
+            os.killpg(sup.pid, signal.SIGKILL)
+        lf.close()
