@@ -119,7 +119,10 @@ __global__ __launch_bounds__(256) void rmsnorm_row_kernel(const uint16_t* __rest
 // P[s][row][:] (the skinny GEMM's split-K combine fused here instead of a separate
 // reduce launch + bf16 round trip).  x is rounded to bf16 before the residual add so the
 // result matches projection -> bf16 -> add_rmsnorm bit for bit.
-template <int NV>
+// NS > 0: S == NS at compile time -- every slab, the residual and the weight chunk are
+// loaded before the first add, so the row costs one memory latency instead of S + 2
+// dependent ones (at 128 decode rows this kernel is latency-bound, not bandwidth-bound).
+template <int NV, int NS>
 __global__ __launch_bounds__(256) void add_rmsnorm_splitk_kernel(const float* __restrict__ P,
                                                                  int S, size_t slab,
                                                                  uint16_t* __restrict__ residual,
@@ -130,24 +133,51 @@ __global__ __launch_bounds__(256) void add_rmsnorm_splitk_kernel(const float* __
   const int tid = threadIdx.x;
   const int nchunk = H >> 3;
   uint4* rr = reinterpret_cast<uint4*>(residual + (size_t)row * H);
+  const uint4* wr = reinterpret_cast<const uint4*>(w);
   float v[NV][8];
+  uint4 rres[NV], wres[NV];
   float ss = 0.f;
 #pragma unroll
   for (int i = 0; i < NV; ++i) {
     const int c = tid + 256 * i;
     if (c < nchunk) {
+      rres[i] = rr[c];
+      wres[i] = wr[c];
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < NV; ++i) {
+    const int c = tid + 256 * i;
+    if (c < nchunk) {
       const float* pr = P + (size_t)row * H + c * 8;
-      float4 a = *reinterpret_cast<const float4*>(pr);
-      float4 b = *reinterpret_cast<const float4*>(pr + 4);
-      for (int sl = 1; sl < S; ++sl) {
-        const float4 a2 = *reinterpret_cast<const float4*>(pr + sl * slab);
-        const float4 b2 = *reinterpret_cast<const float4*>(pr + sl * slab + 4);
-        a.x += a2.x; a.y += a2.y; a.z += a2.z; a.w += a2.w;
-        b.x += b2.x; b.y += b2.y; b.z += b2.z; b.w += b2.w;
+      float4 a, b;
+      if constexpr (NS > 0) {
+        float4 pa[NS], pb[NS];
+#pragma unroll
+        for (int sl = 0; sl < NS; ++sl) {
+          pa[sl] = *reinterpret_cast<const float4*>(pr + sl * slab);
+          pb[sl] = *reinterpret_cast<const float4*>(pr + sl * slab + 4);
+        }
+        a = pa[0];
+        b = pb[0];
+#pragma unroll
+        for (int sl = 1; sl < NS; ++sl) {
+          a.x += pa[sl].x; a.y += pa[sl].y; a.z += pa[sl].z; a.w += pa[sl].w;
+          b.x += pb[sl].x; b.y += pb[sl].y; b.z += pb[sl].z; b.w += pb[sl].w;
+        }
+      } else {
+        a = *reinterpret_cast<const float4*>(pr);
+        b = *reinterpret_cast<const float4*>(pr + 4);
+        for (int sl = 1; sl < S; ++sl) {
+          const float4 a2 = *reinterpret_cast<const float4*>(pr + sl * slab);
+          const float4 b2 = *reinterpret_cast<const float4*>(pr + sl * slab + 4);
+          a.x += a2.x; a.y += a2.y; a.z += a2.z; a.w += a2.w;
+          b.x += b2.x; b.y += b2.y; b.z += b2.z; b.w += b2.w;
+        }
       }
       const float x8[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
       float r[8];
-      unpack8(rr[c], r);
+      unpack8(rres[i], r);
 #pragma unroll
       for (int j = 0; j < 8; ++j) v[i][j] = bf2f(f2bf(bf2f(f2bf(x8[j])) + r[j]));
       rr[c] = pack8(v[i]);
@@ -161,14 +191,13 @@ __global__ __launch_bounds__(256) void add_rmsnorm_splitk_kernel(const float* __
   __syncthreads();
   ss = red[0] + red[1] + red[2] + red[3];
   const float inv = rsqrtf(ss / (float)H + eps);
-  const uint4* wr = reinterpret_cast<const uint4*>(w);
   uint4* orow = reinterpret_cast<uint4*>(out + (size_t)row * H);
 #pragma unroll
   for (int i = 0; i < NV; ++i) {
     const int c = tid + 256 * i;
     if (c < nchunk) {
       float g[8], o[8];
-      unpack8(wr[c], g);
+      unpack8(wres[i], g);
 #pragma unroll
       for (int j = 0; j < 8; ++j) o[j] = v[i][j] * inv * g[j];
       orow[c] = pack8(o);
@@ -276,6 +305,24 @@ int docqa_add_rmsnorm(const void* x, void* residual, const void* w, void* out, i
   return launch_rms<true>(x, residual, w, out, rows, H, eps, s);
 }
 
+template <int NV>
+static void launch_arns(const float* P, int S, size_t slab, uint16_t* rp, const uint16_t* wp,
+                        uint16_t* op, int rows, int H, float eps, hipStream_t s) {
+#define DOCQA_ARNS(NS_) add_rmsnorm_splitk_kernel<NV, NS_><<<rows, 256, 0, s>>>(P, S, slab, rp, wp, op, H, eps)
+  switch (S) {
+    case 1: DOCQA_ARNS(1); break;
+    case 2: DOCQA_ARNS(2); break;
+    case 3: DOCQA_ARNS(3); break;
+    case 4: DOCQA_ARNS(4); break;
+    case 5: DOCQA_ARNS(5); break;
+    case 6: DOCQA_ARNS(6); break;
+    case 7: DOCQA_ARNS(7); break;
+    case 8: DOCQA_ARNS(8); break;
+    default: DOCQA_ARNS(0); break;
+  }
+#undef DOCQA_ARNS
+}
+
 int docqa_add_rmsnorm_splitk(const float* P, int S, void* residual, const void* w, void* out,
                              int rows, int H, float eps, hipStream_t s) {
   if (rows == 0) return 0;
@@ -284,10 +331,10 @@ int docqa_add_rmsnorm_splitk(const float* P, int S, void* residual, const void* 
   const int nvr = (H / 8 + 255) / 256;
   uint16_t *rp = (uint16_t*)residual, *op = (uint16_t*)out;
   const uint16_t* wp = (const uint16_t*)w;
-  if (nvr <= 1) add_rmsnorm_splitk_kernel<1><<<rows, 256, 0, s>>>(P, S, slab, rp, wp, op, H, eps);
-  else if (nvr <= 2) add_rmsnorm_splitk_kernel<2><<<rows, 256, 0, s>>>(P, S, slab, rp, wp, op, H, eps);
-  else if (nvr <= 4) add_rmsnorm_splitk_kernel<4><<<rows, 256, 0, s>>>(P, S, slab, rp, wp, op, H, eps);
-  else return -1;
+  if (nvr > 4) return -1;
+  if (nvr <= 1) launch_arns<1>(P, S, slab, rp, wp, op, rows, H, eps, s);
+  else if (nvr <= 2) launch_arns<2>(P, S, slab, rp, wp, op, rows, H, eps, s);
+  else launch_arns<4>(P, S, slab, rp, wp, op, rows, H, eps, s);
   DOCQA_CHECK_LAUNCH();
   return 0;
 }

@@ -20,24 +20,50 @@
 using namespace docqa;
 
 // sum of S fp32 split-K partial slabs at element offset `off`, rounded to bf16 (as the
-// unfused projection -> bf16 path would), n = 4 or 8 values
-template <int N>
+// unfused projection -> bf16 path would), n = 4 or 8 values.  NS > 0: S == NS known at
+// compile time, so every slab load is issued before the first add (one memory latency
+// instead of S dependent ones -- the decode consumers are latency-bound at 128 rows);
+// NS == 0: runtime S.  Summation order is slab 0, 1, 2, ... either way.
+template <int N, int NS>
 __device__ __forceinline__ void load_partials(const float* P, int S, size_t slab, size_t off, float* x) {
+  float4 a[N / 4];
+  if constexpr (NS > 0) {
+    float4 p[NS][N / 4];
 #pragma unroll
-  for (int j = 0; j < N; j += 4) {
-    float4 a = *reinterpret_cast<const float4*>(P + off + j);
-    for (int sl = 1; sl < S; ++sl) {
-      const float4 b = *reinterpret_cast<const float4*>(P + sl * slab + off + j);
-      a.x += b.x; a.y += b.y; a.z += b.z; a.w += b.w;
+    for (int sl = 0; sl < NS; ++sl)
+#pragma unroll
+      for (int j = 0; j < N / 4; ++j) p[sl][j] = *reinterpret_cast<const float4*>(P + sl * slab + off + 4 * j);
+#pragma unroll
+    for (int j = 0; j < N / 4; ++j) {
+      a[j] = p[0][j];
+#pragma unroll
+      for (int sl = 1; sl < NS; ++sl) {
+        a[j].x += p[sl][j].x; a[j].y += p[sl][j].y; a[j].z += p[sl][j].z; a[j].w += p[sl][j].w;
+      }
     }
-    x[j] = bf2f(f2bf(a.x)); x[j + 1] = bf2f(f2bf(a.y));
-    x[j + 2] = bf2f(f2bf(a.z)); x[j + 3] = bf2f(f2bf(a.w));
+  } else {
+#pragma unroll
+    for (int j = 0; j < N / 4; ++j) {
+      a[j] = *reinterpret_cast<const float4*>(P + off + 4 * j);
+      for (int sl = 1; sl < S; ++sl) {
+        const float4 b = *reinterpret_cast<const float4*>(P + sl * slab + off + 4 * j);
+        a[j].x += b.x; a[j].y += b.y; a[j].z += b.z; a[j].w += b.w;
+      }
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < N / 4; ++j) {
+    x[4 * j] = bf2f(f2bf(a[j].x)); x[4 * j + 1] = bf2f(f2bf(a[j].y));
+    x[4 * j + 2] = bf2f(f2bf(a[j].z)); x[4 * j + 3] = bf2f(f2bf(a[j].w));
   }
 }
 
 // SPLIT: the packed QKV row comes from a split-K decode projection as S fp32 partial slabs
 // P[s][t][:] and is written (rotated) into `qkv` -- the combine fused into this pass.
-template <bool SPLIT>
+// Grid (T, ceil(heads / heads-per-workgroup)): one head slice per thread and no loop, so
+// a 128-token decode batch is 384 workgroups (Llama-3-8B: 48 heads / 16 per workgroup)
+// instead of 128 workgroups each walking three passes.
+template <bool SPLIT, int NS>
 __global__ __launch_bounds__(256) void rope_cache_kernel(
     uint16_t* __restrict__ qkv, const int* __restrict__ positions,
     const float* __restrict__ cos_sin, const int* __restrict__ slot_mapping,
@@ -47,69 +73,73 @@ __global__ __launch_bounds__(256) void rope_cache_kernel(
   const int tph = D >> 3;                 // threads per head
   const int heads_per_pass = 256 / tph;
   const int sub = threadIdx.x % tph;
+  const int h = blockIdx.y * heads_per_pass + threadIdx.x / tph;
+  const int total = Hq + 2 * Hkv;
+  if (h >= total) return;
   const int pos = positions[t];
   const int slot = slot_mapping ? slot_mapping[t] : -1;
   const int half = D >> 1;
-  uint16_t* row = qkv + (size_t)t * row_stride;
-  const float* cs = cos_sin + (size_t)pos * D;
-  const int total = Hq + 2 * Hkv;
-  for (int h = threadIdx.x / tph; h < total; h += heads_per_pass) {
-    uint16_t* hp = row + h * D;
-    if (h < Hq + Hkv) {
-      const int i0 = sub * 4;
-      const float4 c = *reinterpret_cast<const float4*>(cs + i0);
-      const float4 s = *reinterpret_cast<const float4*>(cs + half + i0);
-      float x1[4], x2[4];
-      if constexpr (SPLIT) {
-        const size_t base = (size_t)t * row_stride + h * D;
-        load_partials<4>(P, S, slab, base + i0, x1);
-        load_partials<4>(P, S, slab, base + half + i0, x2);
-      } else {
-        const uint2 a = *reinterpret_cast<const uint2*>(hp + i0);
-        const uint2 b = *reinterpret_cast<const uint2*>(hp + half + i0);
-        x1[0] = __uint_as_float(a.x << 16); x1[1] = __uint_as_float(a.x & 0xffff0000u);
-        x1[2] = __uint_as_float(a.y << 16); x1[3] = __uint_as_float(a.y & 0xffff0000u);
-        x2[0] = __uint_as_float(b.x << 16); x2[1] = __uint_as_float(b.x & 0xffff0000u);
-        x2[2] = __uint_as_float(b.y << 16); x2[3] = __uint_as_float(b.y & 0xffff0000u);
-      }
-      const float cc[4] = {c.x, c.y, c.z, c.w}, ss[4] = {s.x, s.y, s.z, s.w};
-      float o1[4], o2[4];
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        o1[j] = x1[j] * cc[j] - x2[j] * ss[j];
-        o2[j] = x2[j] * cc[j] + x1[j] * ss[j];
-      }
-      uint2 oa, ob;
-      oa.x = pack2(o1[0], o1[1]); oa.y = pack2(o1[2], o1[3]);
-      ob.x = pack2(o2[0], o2[1]); ob.y = pack2(o2[2], o2[3]);
-      *reinterpret_cast<uint2*>(hp + i0) = oa;
-      *reinterpret_cast<uint2*>(hp + half + i0) = ob;
-      if (h >= Hq && slot >= 0) {
-        const int kh = h - Hq;
-        const int blk = slot / BS, off = slot - blk * BS;
-        uint16_t* dst = k_cache + (((size_t)blk * Hkv + kh) * BS + off) * D;
-        *reinterpret_cast<uint2*>(dst + i0) = oa;
-        *reinterpret_cast<uint2*>(dst + half + i0) = ob;
-      }
+  uint16_t* hp = qkv + (size_t)t * row_stride + h * D;
+  if (h < Hq + Hkv) {
+    const int i0 = sub * 4;
+    const float* cs = cos_sin + (size_t)pos * D;
+    const float4 c = *reinterpret_cast<const float4*>(cs + i0);
+    const float4 s = *reinterpret_cast<const float4*>(cs + half + i0);
+    float x1[4], x2[4];
+    if constexpr (SPLIT) {
+      const size_t base = (size_t)t * row_stride + h * D;
+      load_partials<4, NS>(P, S, slab, base + i0, x1);
+      load_partials<4, NS>(P, S, slab, base + half + i0, x2);
     } else {
-      uint4 vv;
-      if constexpr (SPLIT) {
-        float x8[8];
-        load_partials<8>(P, S, slab, (size_t)t * row_stride + h * D + sub * 8, x8);
-        vv = pack8(x8);
-        *reinterpret_cast<uint4*>(hp + sub * 8) = vv;
-      } else {
-        if (slot < 0) continue;
-        vv = *reinterpret_cast<const uint4*>(hp + sub * 8);
-      }
-      if (slot >= 0) {
-        const int vh = h - Hq - Hkv;
-        const int blk = slot / BS, off = slot - blk * BS;
-        uint16_t* dst = v_cache + (((size_t)blk * Hkv + vh) * BS + off) * D;
-        *reinterpret_cast<uint4*>(dst + sub * 8) = vv;
-      }
+      const uint2 a = *reinterpret_cast<const uint2*>(hp + i0);
+      const uint2 b = *reinterpret_cast<const uint2*>(hp + half + i0);
+      x1[0] = __uint_as_float(a.x << 16); x1[1] = __uint_as_float(a.x & 0xffff0000u);
+      x1[2] = __uint_as_float(a.y << 16); x1[3] = __uint_as_float(a.y & 0xffff0000u);
+      x2[0] = __uint_as_float(b.x << 16); x2[1] = __uint_as_float(b.x & 0xffff0000u);
+      x2[2] = __uint_as_float(b.y << 16); x2[3] = __uint_as_float(b.y & 0xffff0000u);
+    }
+    const float cc[4] = {c.x, c.y, c.z, c.w}, ss[4] = {s.x, s.y, s.z, s.w};
+    float o1[4], o2[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      o1[j] = x1[j] * cc[j] - x2[j] * ss[j];
+      o2[j] = x2[j] * cc[j] + x1[j] * ss[j];
+    }
+    uint2 oa, ob;
+    oa.x = pack2(o1[0], o1[1]); oa.y = pack2(o1[2], o1[3]);
+    ob.x = pack2(o2[0], o2[1]); ob.y = pack2(o2[2], o2[3]);
+    *reinterpret_cast<uint2*>(hp + i0) = oa;
+    *reinterpret_cast<uint2*>(hp + half + i0) = ob;
+    if (h >= Hq && slot >= 0) {
+      const int kh = h - Hq;
+      const int blk = slot / BS, off = slot - blk * BS;
+      uint16_t* dst = k_cache + (((size_t)blk * Hkv + kh) * BS + off) * D;
+      *reinterpret_cast<uint2*>(dst + i0) = oa;
+      *reinterpret_cast<uint2*>(dst + half + i0) = ob;
+    }
+  } else {
+    uint4 vv;
+    if constexpr (SPLIT) {
+      float x8[8];
+      load_partials<8, NS>(P, S, slab, (size_t)t * row_stride + h * D + sub * 8, x8);
+      vv = pack8(x8);
+      *reinterpret_cast<uint4*>(hp + sub * 8) = vv;
+    } else {
+      if (slot < 0) return;
+      vv = *reinterpret_cast<const uint4*>(hp + sub * 8);
+    }
+    if (slot >= 0) {
+      const int vh = h - Hq - Hkv;
+      const int blk = slot / BS, off = slot - blk * BS;
+      uint16_t* dst = v_cache + (((size_t)blk * Hkv + vh) * BS + off) * D;
+      *reinterpret_cast<uint4*>(dst + sub * 8) = vv;
     }
   }
+}
+
+static dim3 rope_grid(int T, int Hq, int Hkv, int D) {
+  const int hpp = 256 / (D / 8);
+  return dim3(T, (Hq + 2 * Hkv + hpp - 1) / hpp);
 }
 
 int docqa_rope_cache(void* qkv, const int* positions, const float* cos_sin,
@@ -117,9 +147,9 @@ int docqa_rope_cache(void* qkv, const int* positions, const float* cos_sin,
                      int Hkv, int D, int row_stride, int BS, hipStream_t s) {
   if (T == 0) return 0;
   if (D % 8 != 0 || (256 % (D / 8)) != 0) return -1;
-  rope_cache_kernel<false><<<T, 256, 0, s>>>((uint16_t*)qkv, positions, cos_sin, slot_mapping,
-                                             (uint16_t*)k_cache, (uint16_t*)v_cache, Hq, Hkv, D,
-                                             row_stride, BS, nullptr, 0, 0);
+  rope_cache_kernel<false, 0><<<rope_grid(T, Hq, Hkv, D), 256, 0, s>>>(
+      (uint16_t*)qkv, positions, cos_sin, slot_mapping, (uint16_t*)k_cache, (uint16_t*)v_cache,
+      Hq, Hkv, D, row_stride, BS, nullptr, 0, 0);
   DOCQA_CHECK_LAUNCH();
   return 0;
 }
@@ -131,9 +161,24 @@ int docqa_rope_cache_splitk(const float* P, int S, void* qkv_out, const int* pos
                             hipStream_t s) {
   if (T == 0) return 0;
   if (D % 8 != 0 || (256 % (D / 8)) != 0 || S < 1 || row_stride % 4 != 0) return -1;
-  rope_cache_kernel<true><<<T, 256, 0, s>>>((uint16_t*)qkv_out, positions, cos_sin, slot_mapping,
-                                            (uint16_t*)k_cache, (uint16_t*)v_cache, Hq, Hkv, D,
-                                            row_stride, BS, P, S, (size_t)T * row_stride);
+  const dim3 grid = rope_grid(T, Hq, Hkv, D);
+  const size_t slab = (size_t)T * row_stride;
+  uint16_t *q = (uint16_t*)qkv_out, *kc = (uint16_t*)k_cache, *vc = (uint16_t*)v_cache;
+#define DOCQA_ROPE_SPLIT(NS_)                                                                  \
+  rope_cache_kernel<true, NS_><<<grid, 256, 0, s>>>(q, positions, cos_sin, slot_mapping, kc, vc, \
+                                                    Hq, Hkv, D, row_stride, BS, P, S, slab)
+  switch (S) {
+    case 1: DOCQA_ROPE_SPLIT(1); break;
+    case 2: DOCQA_ROPE_SPLIT(2); break;
+    case 3: DOCQA_ROPE_SPLIT(3); break;
+    case 4: DOCQA_ROPE_SPLIT(4); break;
+    case 5: DOCQA_ROPE_SPLIT(5); break;
+    case 6: DOCQA_ROPE_SPLIT(6); break;
+    case 7: DOCQA_ROPE_SPLIT(7); break;
+    case 8: DOCQA_ROPE_SPLIT(8); break;
+    default: DOCQA_ROPE_SPLIT(0); break;
+  }
+#undef DOCQA_ROPE_SPLIT
   DOCQA_CHECK_LAUNCH();
   return 0;
 }

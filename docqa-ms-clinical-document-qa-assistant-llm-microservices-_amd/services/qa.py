@@ -157,9 +157,15 @@ class ContinuousBatcher:
     def _loop(self) -> None:
         import torch
 
+        from ..parallel.health import Watchdog
+
+        # DOCQA_WATCHDOG_S=<s>: exit (for a supervised restart) when a step hangs that long
+        wd = Watchdog.from_env()
         while not self._stop.is_set():
             items = self._drain()
             if items:
+                if wd:
+                    wd.busy()
                 try:
                     with torch.inference_mode():
                         self._admit(items)
@@ -168,11 +174,19 @@ class ContinuousBatcher:
                         if not it[2].done():
                             it[2].set_exception(e)
             if self.engine.has_work():
+                if wd:
+                    wd.busy()
                 try:
                     self.engine.step()
                 except Exception as e:  # noqa: BLE001
                     self.engine._fail_all(e)
                     _maybe_exit_on_device_error(e)
+                if wd:
+                    wd.beat()
+            elif wd:
+                wd.idle()
+        if wd:
+            wd.stop()
 
     def _admit(self, items) -> None:
         pipe, params = self.pipe, self._params()
