@@ -66,7 +66,7 @@ struct PagedKV {
 
 // PFX (cascade decode, docqa_cascade.h): the query rows are the B sequences of a decode
 // step (one new token each, rows of the packed QKV buffer), the keys are one chunk
-// (blockIdx.z) of the prompt prefix they all share, read through the shared block table
+// (blockIdx.y) of the prompt prefix they all share, read through the shared block table
 // (row 0 of pk.block_tables), no causal mask; the epilogue writes the un-normalised
 // accumulator and (max, sum) of the chunk instead of normalised bf16 rows.
 template <int D, bool CAUSAL, bool PAGED, int G, int WPH, bool PFX = false>
@@ -80,7 +80,13 @@ __global__ __launch_bounds__(64 * G * WPH) void flash_prefill_kernel(
   uint16_t* sK = smem;
   uint16_t* sV = smem + KB * D;
 
-  const int qt = blockIdx.x, hb = blockIdx.y, b = blockIdx.z;
+  // grid (heads, sequences, q-tiles): workgroups are dealt to the 8 XCDs round-robin by
+  // linear id, so with q-tiles fastest (the old (q-tile, head, seq) grid) XCD x received
+  // q-tile x of every sequence -- in a RAG prefill most sequences have 1-2 tiles of new
+  // tokens and one long prompt sets the grid to 8, so XCDs 2..7 got only empty tiles and
+  // the work ran on two XCDs (4x slower on the bench's real batches).  Heads fastest
+  // spreads every tile over all XCDs, and the empty high tiles are dispatched last.
+  const int hb = blockIdx.x, b = blockIdx.y, qt = blockIdx.z;
   int seq0, L, kv_beg = 0, pfx_end = 0;
   if constexpr (PFX) {
     seq0 = 0;
@@ -97,7 +103,7 @@ __global__ __launch_bounds__(64 * G * WPH) void flash_prefill_kernel(
   const int q_start = qt * QBW;
   if (q_start >= L) return;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  // G > 1: blockIdx.y is the KV head and wave / WPH picks the query head of its group
+  // G > 1: blockIdx.x is the KV head and wave / WPH picks the query head of its group
   const int h = G > 1 ? hb * G + wave / WPH : hb;
   const int kvh = G > 1 ? hb : h / (Hq / Hkv);
   const int P0 = (PAGED && !PFX) ? pk.ctx_start[b] : 0;   // absolute position of query row 0
@@ -325,10 +331,10 @@ static int prefill_dispatch(hipStream_t s, int B, int max_len, int head_dim, int
                             float scale, const PagedKV& pk) {
   const bool gqa4 = head_dim == 128 && Hq == 4 * Hkv;
   if (gqa4) {
-    dim3 grid((max_len + 63) / 64, Hkv, B);
+    dim3 grid(Hkv, B, (max_len + 63) / 64);
     launch_prefill<128, 4, 2>(grid, s, causal, qkv, row_stride, cu, out, o_stride, Hq, Hkv, scale, pk);
   } else {
-    dim3 grid((max_len + QB - 1) / QB, Hq, B);
+    dim3 grid(Hq, B, (max_len + QB - 1) / QB);
     switch (head_dim) {
       case 32: launch_prefill<32, 1, 4>(grid, s, causal, qkv, row_stride, cu, out, o_stride, Hq, Hkv, scale, pk); break;
       case 64: launch_prefill<64, 1, 4>(grid, s, causal, qkv, row_stride, cu, out, o_stride, Hq, Hkv, scale, pk); break;
@@ -376,7 +382,7 @@ int docqa_cascade_prefix(const void* qkv, int row_stride, int rows, int Hq, int 
   if (Hq != 4 * Hkv || BS != 64 || nchunk < 1) return -1;
   PagedKV pk{(const uint16_t*)k_cache, (const uint16_t*)v_cache, prefix_table, 0, nullptr, BS, 6};
   const CascadeOut co{acc, ml, plen, nchunk, rows};
-  dim3 grid((rows + 63) / 64, Hkv, nchunk);
+  dim3 grid(Hkv, nchunk, (rows + 63) / 64);
   flash_prefill_kernel<128, false, true, 4, 2, true><<<grid, 512, 0, s>>>(
       (const uint16_t*)qkv, row_stride, nullptr, nullptr, 0, Hq, Hkv, scale, pk, co);
   DOCQA_CHECK_LAUNCH();

@@ -17,6 +17,7 @@ request in the reference (llm-qa/main.py:117, one request at a time, greedy at T
 """
 from __future__ import annotations
 
+import json
 import math
 import os
 import time
@@ -28,6 +29,9 @@ from .. import ops
 from ..utils import tracing
 from ..models.llama import AttnMeta, LlamaModel
 from .kv_cache import KVCache
+
+_PREFILL_LOG = os.environ.get("DOCQA_PREFILL_LOG") == "1"   # one JSON line per prefill chunk
+_PREFILL_DUMP = os.environ.get("DOCQA_PREFILL_DUMP", "")       # dir: save paged-prefill shapes for replay
 
 
 @dataclass
@@ -169,6 +173,16 @@ class LLMEngine:
                 meta.block_tables = bt.to(dev, non_blocking=True)
                 meta.prefix_lens = torch.tensor(cached[i:j], dtype=torch.int32).to(dev, non_blocking=True)
             last = torch.tensor(cu[1:], dtype=torch.int64).to(dev, non_blocking=True) - 1
+            if _PREFILL_DUMP and meta.block_tables is not None:
+                os.makedirs(_PREFILL_DUMP, exist_ok=True)
+                torch.save({"cu": torch.tensor(cu, dtype=torch.int32), "ctx": torch.tensor(cached[i:j], dtype=torch.int32),
+                            "bt": meta.block_tables.cpu()},
+                           os.path.join(_PREFILL_DUMP, f"prefill_{time.time_ns()}.pt"))
+            if _PREFILL_LOG:
+                new = [len(p) - c for p, c in zip(prompts[i:j], cached[i:j])]
+                print(json.dumps({"prefill_chunk": j - i, "new_sum": sum(new), "new_max": max(new),
+                                  "cached_mean": sum(cached[i:j]) / (j - i), "cached_max": max(cached[i:j]),
+                                  "cached_min": min(cached[i:j])}), flush=True)
             logits = self.model.forward(t_ids, meta, self.kv.caches, logits_index=last)
             firsts.append(logits)
             i = j

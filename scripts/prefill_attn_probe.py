@@ -1,5 +1,6 @@
 """Prefill attention probe: paged (prefix-cached) causal prefill at RAG shapes vs the
 contiguous kernel, to locate the prefill-attention cost seen in the bench profile."""
+import json
 import math
 import sys
 from pathlib import Path
@@ -54,5 +55,83 @@ def main():
     print(f"bench-mix B={B} new mean={T / B:.0f} max={max(news)} prefix 320..768: {t:.1f} us  {flops / t / 1e6:.1f} TFLOP/s")
 
 
+def replay(dump_dir: str):
+    """Time the paged prefill kernel on the exact (cu_seqlens, cached lengths, block tables)
+    the engine saved with DOCQA_PREFILL_DUMP=<dir>, with the real (shared) block ids and
+    with the same lengths on private contiguous blocks."""
+    import glob
+
+    assert ops.load_native()
+    nat = torch.ops.docqa
+    Hq, Hkv, D, BS = 32, 8, 128, 64
+    scale = 1 / math.sqrt(D)
+    for f in sorted(glob.glob(f"{dump_dir}/prefill_*.pt")):
+        d = torch.load(f, weights_only=True)
+        cu, ctx, bt = d["cu"], d["ctx"], d["bt"]
+        B = len(ctx)
+        news = (cu[1:] - cu[:-1]).tolist()
+        T = int(cu[-1])
+        W = (Hq + 2 * Hkv) * D
+        qkv = (torch.randn(T, W, device="cuda") * 0.5).bfloat16()
+        nb = int(bt.max()) + 1
+        maxb = bt.shape[1]
+        kc = torch.randn(max(nb, B * maxb) + 1, Hkv, BS, D, device="cuda").bfloat16()
+        vc = torch.randn_like(kc)
+        flops = sum(4 * Hq * D * (n * p + n * n / 2) for n, p in zip(news, ctx.tolist()))
+        cud, csd = cu.cuda(), ctx.cuda()
+        uniq = len(set(bt[r, k].item() for r in range(B) for k in range((int(ctx[r]) + news[r] + BS - 1) // BS)))
+        for name, table in (("real", bt.cuda()), ("private", torch.arange(B * maxb, dtype=torch.int32, device="cuda").view(B, maxb))):
+            t = timeit(lambda: nat.flash_prefill_paged(qkv, cud, max(news), Hq, Hkv, D, scale, kc, vc, table, csd), iters=10)
+            print(json.dumps({"file": f.split("/")[-1], "tables": name, "B": B, "new_sum": T, "new_max": max(news),
+                              "ctx_mean": round(float(ctx.float().mean()), 1), "ctx_max": int(ctx.max()),
+                              "unique_blocks": uniq, "us": round(t, 1), "tflops": round(flops / t / 1e6, 1)}), flush=True)
+
+
+def replay_variants(dump_dir: str):
+    """Which property of the real batch makes the paged prefill slow: subsets of the
+    sequences, uniform new lengths, no cached prefix."""
+    import glob
+
+    assert ops.load_native()
+    nat = torch.ops.docqa
+    Hq, Hkv, D, BS = 32, 8, 128, 64
+    scale = 1 / math.sqrt(D)
+    f = sorted(glob.glob(f"{dump_dir}/prefill_*.pt"))[-1]
+    d = torch.load(f, weights_only=True)
+    news0, ctx0 = (d["cu"][1:] - d["cu"][:-1]).tolist(), d["ctx"].tolist()
+    W = (Hq + 2 * Hkv) * D
+    maxb = 40
+    kc = torch.randn(128 * maxb + 1, Hkv, BS, D, device="cuda").bfloat16()
+    vc = torch.randn_like(kc)
+
+    def run(name, news, ctx):
+        B = len(news)
+        cu = torch.tensor([0] + list(__import__("itertools").accumulate(news)), dtype=torch.int32, device="cuda")
+        T = int(cu[-1])
+        qkv = (torch.randn(T, W, device="cuda") * 0.5).bfloat16()
+        bt = torch.arange(B * maxb, dtype=torch.int32, device="cuda").view(B, maxb)
+        cs = torch.tensor(ctx, dtype=torch.int32, device="cuda")
+        flops = sum(4 * Hq * D * (n * p + n * n / 2) for n, p in zip(news, ctx))
+        t = timeit(lambda: nat.flash_prefill_paged(qkv, cu, max(news), Hq, Hkv, D, scale, kc, vc, bt, cs), iters=10)
+        print(json.dumps({"variant": name, "B": B, "new_sum": T, "new_max": max(news), "us": round(t, 1),
+                          "tflops": round(flops / t / 1e6, 1)}), flush=True)
+
+    run("real", news0, ctx0)
+    for k in (16, 32, 64):
+        run(f"first{k}", news0[:k], ctx0[:k])
+    order = sorted(range(128), key=lambda i: -news0[i])
+    run("longest16", [news0[i] for i in order[:16]], [ctx0[i] for i in order[:16]])
+    run("shortest112", [news0[i] for i in order[16:]], [ctx0[i] for i in order[16:]])
+    run("new_capped64", [min(n, 64) for n in news0], ctx0)
+    run("ctx0", news0, [0] * 128)
+    run("uniform", [sum(news0) // 128] * 128, [sum(ctx0) // 128 // 64 * 64] * 128)
+
+
 if __name__ == "__main__":
-    main()
+    if len(sys.argv) > 2 and sys.argv[1] == "--variants":
+        replay_variants(sys.argv[2])
+        sys.exit(0)
+    if len(sys.argv) > 2 and sys.argv[1] == "--replay":
+        replay(sys.argv[2])
+    else:
+        main()

@@ -293,6 +293,37 @@ def test_splitk_fused_consumers(native, S, M, tile):
     _close(vc1, vc2, 1e-2)
 
 
+@pytest.mark.parametrize("S", [1, 3, 5, 8, 9, 12])
+def test_splitk_consumers_slab_counts(native, S):
+    """The consumers' compile-time slab counts (1..8) and the runtime-S fallback (>8)."""
+    from docqa_amd.ops import reference as R
+
+    M, H = 70, 4096
+    P = torch.randn(S, M, H, device="cuda") / S
+    r1 = torch.randn(M, H, device="cuda", dtype=torch.bfloat16)
+    r2 = r1.clone()
+    g = (torch.rand(H, device="cuda") + 0.5).bfloat16()
+    o1 = torch.ops.docqa.add_rmsnorm_splitk(P, r1, g, 1e-5)
+    o2 = R.add_rmsnorm(P.sum(0).bfloat16(), r2, g, 1e-5)
+    _close(r1, r2, 1e-2, 1e-2)
+    _close(o1, o2, 3e-2, 1e-2)
+    Hq, Hkv, D, BS, T = 32, 8, 128, 16, M
+    Pq = torch.randn(S, T, (Hq + 2 * Hkv) * D, device="cuda")
+    cs = R.rope_cos_sin(1024, D, 500000.0, "cuda")
+    pos = torch.randint(0, 1000, (T,), device="cuda", dtype=torch.int32)
+    slots = torch.randperm(8 * BS, device="cuda")[:T].int()
+    slots[5] = -1
+    kc1 = torch.zeros(8, Hkv, BS, D, device="cuda", dtype=torch.bfloat16)
+    vc1 = torch.zeros_like(kc1)
+    kc2, vc2 = kc1.clone(), vc1.clone()
+    q1 = torch.ops.docqa.rope_cache_splitk(Pq, pos, cs, slots, kc1, vc1, Hq, Hkv, D)
+    q2 = Pq.sum(0).bfloat16()
+    R.rope_cache(q2, pos, cs, slots, kc2, vc2, Hq, Hkv, D)
+    _close(q1, q2, 2e-2, 1e-2)
+    _close(kc1, kc2, 2e-2, 1e-2)
+    _close(vc1, vc2, 2e-2, 1e-2)   # fp32 sum order differs from torch's -> 1 bf16 ulp
+
+
 @pytest.mark.parametrize("M", [1, 16, 33, 64, 97, 128])
 @pytest.mark.parametrize("N,K", [(28672, 4096), (1024, 512)])
 def test_dgemm_glu(native, M, N, K):
