@@ -34,6 +34,11 @@
 using namespace docqa;
 
 constexpr int kMinChunk = 64;   // smallest context slice worth a workgroup
+// kDecodeGridNote: grids are (KV head, sequence, partition).  Workgroups go to the 8 XCDs
+// round-robin by linear id; with partitions fastest, XCD x would receive partition x of
+// every sequence and the high partitions are empty for the short contexts of a mixed
+// batch (the prefill kernel measured 3.7x from the same reordering).  KV heads fastest
+// spreads every sequence over the XCDs, empty partitions are dispatched last.
 typedef __attribute__((address_space(3))) i16x4 lds_i16x4;
 
 // KV heads per workgroup of the MFMA decode kernel in the one-partition regime (knob)
@@ -184,7 +189,7 @@ __device__ __forceinline__ void finish_partition(
       if (np > 0) {   // cascade: fold in the shared-prefix chunk partials
         // every chunk's (max, sum, acc) load is issued before the first is used (indices
         // clamped, extra chunks weighted 0): one memory latency, not 2 x np dependent ones
-        const size_t B = gridDim.z, Hq = (size_t)Hkv * G;
+        const size_t B = gridDim.y, Hq = (size_t)Hkv * G;
         float pm[kCascadeMaxChunks], pl[kCascadeMaxChunks], pa[kCascadeMaxChunks];
 #pragma unroll
         for (int c = 0; c < kCascadeMaxChunks; ++c) {
@@ -230,7 +235,7 @@ __global__ __launch_bounds__(256, OCC) void paged_decode_kernel(
     float* __restrict__ tmp_ml, int Hkv, int BS, int log2BS, int max_parts, float scale,
     uint16_t* __restrict__ out, int out_stride) {
   static_assert(D == 128, "decode kernel is specialised for head_dim 128");
-  const int part = blockIdx.x, kvh = blockIdx.y, b = blockIdx.z;
+  const int part = blockIdx.z, kvh = blockIdx.x, b = blockIdx.y;
   const int L = context_lens[b];
   const int slice = split_chunk(L, max_parts);
   const int start = part * slice;
@@ -380,7 +385,7 @@ __global__ __launch_bounds__(256) void paged_decode_ring_kernel(
   __shared__ float s_m[4][G], s_l[4][G];
   __shared__ int s_bt[256];                      // block ids of the slice (<= 16k tokens)
 
-  const int part = blockIdx.x, kvh = blockIdx.y, b = blockIdx.z;
+  const int part = blockIdx.z, kvh = blockIdx.x, b = blockIdx.y;
   const int L = context_lens[b];
   // cascade: keys [0, P) are the shared prefix (attended by the prefix kernel), this
   // kernel covers the sequence's own suffix [P, L); P is a multiple of 64
@@ -464,7 +469,7 @@ __global__ __launch_bounds__(256) void paged_decode_ring_kernel(
     // q for the G heads of the group and (slice owner) the new K/V: sum of the split-K
     // partial slabs, rounded to bf16, RoPE; the new K/V row also goes to the paged cache
     const int W = (fz.Hq + 2 * Hkv) * D;
-    const size_t slab = (size_t)gridDim.z * W;
+    const size_t slab = (size_t)gridDim.y * W;
     const float* row = fz.P + (size_t)b * W;
     const float* cs = fz.cos_sin + (size_t)fz.positions[b] * D;
 #pragma unroll
@@ -557,7 +562,7 @@ __global__ __launch_bounds__(256) void paged_decode_mfma_kernel(
   // HPW KV heads per workgroup, one after the other through the same ring (the K/V tile
   // stream runs on across the head boundary): 1/HPW of the workgroups -- one launch round
   // at batch 128 -- and the next head's ring fill overlaps the current head's tail.
-  const int part = blockIdx.x, kvh0 = blockIdx.y * HPW, b = blockIdx.z;
+  const int part = blockIdx.z, kvh0 = blockIdx.x * HPW, b = blockIdx.y;
   const int L = context_lens[b];
   const int P = ci.plen ? *ci.plen : 0;
   const int slice = split_chunk(L - P, max_parts);
@@ -625,7 +630,7 @@ __global__ __launch_bounds__(256) void paged_decode_mfma_kernel(
       if (np > 0) {   // cascade: fold in the shared-prefix chunk partials
         // (max, sum) of every chunk first (loads issued together), then the accumulators
         // in groups of 4 chunks: bounded registers, 8 loads in flight per group
-        const size_t B = gridDim.z, Hq = (size_t)Hkv * G;
+        const size_t B = gridDim.y, Hq = (size_t)Hkv * G;
         float pm[kCascadeMaxChunks], pl[kCascadeMaxChunks];
 #pragma unroll
         for (int c = 0; c < kCascadeMaxChunks; ++c) {
@@ -817,7 +822,7 @@ int docqa_paged_decode(const void* q, int q_stride, const void* k_cache, const v
   int log2BS = 0;
   while ((1 << log2BS) < BS) ++log2BS;
   const int G = Hq / Hkv;
-  dim3 grid(max_parts, Hkv, B);
+  dim3 grid(Hkv, B, max_parts);   // partitions slowest: see kDecodeGridNote
   const bool direct = max_parts == 1;
   // U (tokens in flight per lane group per buffer) and occupancy: measured on HBM-resident
   // caches (benchmarks/bench_decode_attn.py, profiles/r1_decode_attention_sweep_hbm.log):
@@ -841,7 +846,7 @@ int docqa_paged_decode(const void* q, int q_stride, const void* k_cache, const v
 #define DMFMA(GG)                                                                             \
     do {                                                                                      \
       if (direct && Hkv % 2 == 0 && hpw_knob() == 2)                                          \
-        paged_decode_mfma_kernel<GG, true, 2><<<dim3(1, Hkv / 2, B), 256, 0, s>>>(            \
+        paged_decode_mfma_kernel<GG, true, 2><<<dim3(Hkv / 2, B, 1), 256, 0, s>>>(            \
             (const uint16_t*)q, q_stride, (const uint16_t*)k_cache, (const uint16_t*)v_cache, \
             block_tables, maxb, context_lens, tmp_out, tmp_ml, Hkv, max_parts, scale,         \
             (uint16_t*)out, out_stride, CascadeIn{});                                         \
@@ -945,7 +950,7 @@ int docqa_paged_decode_fused(const float* P, int S, const int* positions, const 
   if (B == 0) return 0;
   if (BS != 64 || maxb > 256 || Hq % Hkv != 0 || S < 1) return -1;
   const int G = Hq / Hkv;
-  dim3 grid(max_parts, Hkv, B);
+  dim3 grid(Hkv, B, max_parts);   // partitions slowest: see kDecodeGridNote
   const bool direct = max_parts == 1;
   FusedQKV fz{P, S, positions, cos_sin, slot_mapping, Hq};
 #define DFUSED(GG)                                                                            \
@@ -993,10 +998,10 @@ int docqa_paged_decode_cascade(const void* q, int q_stride, void* k_cache, void*
                                 BS, nchunk, pacc, pml, s);
   if (rc) return rc;
   const CascadeIn ci{pacc, pml, plen, nchunk};
-  dim3 grid(max_parts, Hkv, B);
+  dim3 grid(Hkv, B, max_parts);   // partitions slowest: see kDecodeGridNote
   if (mfma_decode_on(Hq / Hkv)) {
     if (max_parts == 1 && Hkv % 2 == 0 && hpw_knob() == 2)
-      paged_decode_mfma_kernel<4, true, 2><<<dim3(1, Hkv / 2, B), 256, 0, s>>>(
+      paged_decode_mfma_kernel<4, true, 2><<<dim3(Hkv / 2, B, 1), 256, 0, s>>>(
           (const uint16_t*)q, q_stride, (const uint16_t*)k_cache, (const uint16_t*)v_cache, block_tables, maxb,
           context_lens, tmp_out, tmp_ml, Hkv, max_parts, scale, (uint16_t*)out, out_stride, ci);
     else if (max_parts == 1 && mfma_nsr() == 3)
