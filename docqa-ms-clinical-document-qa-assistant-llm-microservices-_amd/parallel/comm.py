@@ -47,10 +47,12 @@ def state() -> ParallelState:
     return _STATE
 
 
-def init_distributed(tp_size: int = 1, backend: str | None = None, timeout_s: int = 600) -> ParallelState:
+def init_distributed(tp_size: int = 1, backend: str | None = None, timeout_s: int = 600,
+                     store=None) -> ParallelState:
     """Initialise torch.distributed from torchrun env vars (RANK/WORLD_SIZE/MASTER_*).
 
-    Safe to call without a launcher: falls back to a single-process state.
+    Safe to call without a launcher: falls back to a single-process state.  ``store``: an
+    existing rendezvous store (parallel/health.py:reinit re-forms the groups on it).
     """
     global _STATE
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -67,6 +69,8 @@ def init_distributed(tp_size: int = 1, backend: str | None = None, timeout_s: in
         torch.cuda.set_device(local_rank)
     if not dist.is_initialized():
         kw = {}
+        if store is not None:
+            kw["store"] = store
         if backend == "nccl":
             kw["device_id"] = torch.device("cuda", local_rank)
         dist.init_process_group(backend=backend, rank=rank, world_size=world,

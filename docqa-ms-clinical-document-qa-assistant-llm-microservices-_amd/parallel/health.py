@@ -140,8 +140,22 @@ class Watchdog:
 def reinit(tp_size: int | None = None, backend: str | None = None, timeout_s: int = 600) -> comm.ParallelState:
     """Tear down every process group and re-form them from the same rendezvous env.  All
     ranks must call it (planned TP resize; the gloo path)."""
+    global _GEN
     old = comm.state()
     tp = tp_size or old.tp_size
     be = backend or (old.backend if old.backend != "none" else None)
+    store = None
+    if dist.is_initialized():
+        # keep the rendezvous store alive across the teardown and re-form the groups under
+        # a fresh key prefix: re-creating the TCP store on MASTER_PORT races with peers
+        # still reading the old one
+        base = dist.distributed_c10d._get_default_store()
+        _GEN += 1
+        store = dist.PrefixStore(f"docqa_reinit_{_GEN}", base)
+        _STORES.append(base)
     comm.destroy()
-    return comm.init_distributed(tp_size=tp, backend=be, timeout_s=timeout_s)
+    return comm.init_distributed(tp_size=tp, backend=be, timeout_s=timeout_s, store=store)
+
+
+_GEN = 0
+_STORES: list = []       # stores of torn-down groups, kept alive for the re-formed ones

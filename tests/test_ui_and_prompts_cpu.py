@@ -1,0 +1,102 @@
+"""clinical-ui proxy app (services/ui.py, reference clinical-ui/app.py:1-118) and the prompt
+templates (services/synthese.py, pipeline/rag.py; reference synthese-comparative/api/
+routes.py:45-101 and llm-qa/main.py:72-95).  The UI's upstream calls go to an
+httpx.MockTransport, so no server is started."""
+import json
+
+import httpx
+import pytest
+from fastapi.testclient import TestClient
+
+import docqa_amd.services.ui as ui
+
+
+@pytest.fixture
+def upstream(monkeypatch):
+    """Fake doc-ingestor (port 8000) + llm-qa (port 8001); records the requests."""
+    seen = []
+
+    def handler(req: httpx.Request) -> httpx.Response:
+        seen.append(req)
+        host, path = req.url.port, req.url.path
+        if path == "/health":
+            return httpx.Response(200, json={"status": "ok"}) if host == 8000 else httpx.Response(500)
+        if host == 8000 and path == "/ingest/":
+            return httpx.Response(200, json={"doc_id": 7, "status": "PENDING"})
+        if host == 8000 and path == "/documents/7":
+            return httpx.Response(200, json={"id": 7, "status": "INDEXED"})
+        if host == 8001 and path == "/ask/":
+            q = json.loads(req.content)["question"]
+            if q == "no-index":
+                return httpx.Response(503, json={"detail": "Index non chargé."})
+            return httpx.Response(200, json={"answer": f"re: {q}", "sources": ["Dossier Patient 1"]})
+        return httpx.Response(404, json={"detail": "not found"})
+
+    real = httpx.AsyncClient
+
+    class Mocked(real):
+        def __init__(self, *a, **kw):
+            kw["transport"] = httpx.MockTransport(handler)
+            super().__init__(*a, **kw)
+
+    monkeypatch.setattr(ui.httpx, "AsyncClient", Mocked)
+    return seen
+
+
+def test_ui_page_wires_the_reference_flows():
+    c = TestClient(ui.create_app())
+    html = c.get("/").text
+    for needle in ("/ui/health", "/ui/ingest", "/ui/ask", "/ui/documents/", "compte-rendu", "Sources"):
+        assert needle in html
+
+
+def test_ui_health_probes_each_service(upstream):
+    c = TestClient(ui.create_app())
+    assert c.get("/ui/health").json() == {"doc-ingestor": True, "llm-qa": False}
+
+
+def test_ui_upload_and_readiness_poll(upstream):
+    c = TestClient(ui.create_app())
+    r = c.post("/ui/ingest", files={"file": ("note.txt", b"Patient: Jean", "text/plain")},
+               data={"doc_type": "compte-rendu"})
+    assert r.status_code == 200 and r.json()["doc_id"] == 7
+    fwd = [q for q in upstream if q.url.path == "/ingest/"][0]
+    assert fwd.headers["content-type"].startswith("multipart/form-data")
+    assert b"compte-rendu" in fwd.content and b"Patient: Jean" in fwd.content
+    assert c.get("/ui/documents/7").json()["status"] == "INDEXED"
+
+
+def test_ui_ask_proxies_answer_and_errors(upstream):
+    c = TestClient(ui.create_app())
+    r = c.post("/ui/ask", json={"question": "dose ?"})
+    assert r.json() == {"answer": "re: dose ?", "sources": ["Dossier Patient 1"]}
+    r = c.post("/ui/ask", json={"question": "no-index"})
+    assert r.status_code == 503 and r.json()["detail"] == "Index non chargé."
+
+
+def test_synthese_templates_have_the_reference_slots():
+    from docqa_amd.services.synthese import MULTI_PATIENT_TEMPLATE, SINGLE_PATIENT_TEMPLATE
+
+    s = SINGLE_PATIENT_TEMPLATE.format(patient_alias="PATIENT_1", from_date="N/A", to_date="N/A",
+                                       focus="diabète", documents="[d1]\nnote")
+    assert "PATIENT_1" in s and "diabète" in s and "[d1]\nnote" in s
+    for sec in ("Contexte général", "Focus clinique (diabète)", "Événements clés", "Points de vigilance"):
+        assert sec in s
+    m = MULTI_PATIENT_TEMPLATE.format(patients="PATIENT_1, PATIENT_2", from_date="N/A", to_date="N/A",
+                                      focus="général", documents_by_patient="=== PATIENT_1 ===\n...")
+    assert "PATIENT_1, PATIENT_2" in m and "=== PATIENT_1 ===" in m
+
+
+def test_rag_template_puts_fixed_text_first_for_the_prefix_cache():
+    """Two questions with different contexts share every token up to the context slot."""
+    from docqa_amd.pipeline.rag import DEFAULT_TEMPLATE
+    from docqa_amd.text.tokenizer import ChatTokenizer
+
+    assert DEFAULT_TEMPLATE.index("{context}") < DEFAULT_TEMPLATE.index("{question}")
+    head = DEFAULT_TEMPLATE.split("{context}")[0]
+    assert len(head) > 400                       # the shared instruction block
+    tok = ChatTokenizer(model_vocab=128256)
+    a = tok.chat_prompt(DEFAULT_TEMPLATE.format(context="Ginseng score 10", question="Quelle plante ?"))
+    b = tok.chat_prompt(DEFAULT_TEMPLATE.format(context="Réglisse score 7", question="Posologie ?"))
+    common = next(i for i, (x, y) in enumerate(zip(a, b)) if x != y)
+    assert common >= len(tok.chat_prompt(head)) - 8
