@@ -175,6 +175,44 @@ at::Tensor bert_embed_ln(const at::Tensor& ids, const at::Tensor& pos,
   return out;
 }
 
+// decode-step state: paged-cache slot of every row's next token (-1: padded row)
+at::Tensor decode_slots(const at::Tensor& block_tables, const at::Tensor& positions,
+                        const at::Tensor& valid, int64_t BS) {
+  CHECK_GPU(block_tables);
+  TORCH_CHECK(block_tables.scalar_type() == at::kInt && positions.scalar_type() == at::kInt &&
+                  valid.scalar_type() == at::kInt, "decode_slots: int32 tensors");
+  TORCH_CHECK(block_tables.dim() == 2 && block_tables.is_contiguous() && positions.is_contiguous() &&
+                  valid.is_contiguous(), "decode_slots: contiguous [B, maxb], [B], [B]");
+  const int B = block_tables.size(0);
+  TORCH_CHECK(positions.numel() == B && valid.numel() == B, "decode_slots: B mismatch");
+  c10::DeviceGuard g(block_tables.device());
+  auto slots = at::empty({B}, positions.options());
+  CHECK_RC(docqa_decode_slots(block_tables.data_ptr<int>(), block_tables.size(1), positions.data_ptr<int>(),
+                              valid.data_ptr<int>(), slots.data_ptr<int>(), B, (int)BS, stream()),
+           "decode_slots");
+  return slots;
+}
+
+// out <- nxt, tokens <- nxt, positions += valid, context_lens += valid (in place)
+void decode_advance(const at::Tensor& nxt, at::Tensor out, at::Tensor tokens, at::Tensor positions,
+                    at::Tensor context_lens, const at::Tensor& valid) {
+  CHECK_GPU(nxt);
+  const int B = nxt.numel();
+  TORCH_CHECK(nxt.scalar_type() == at::kLong && out.scalar_type() == at::kLong &&
+                  tokens.scalar_type() == at::kInt && positions.scalar_type() == at::kInt &&
+                  context_lens.scalar_type() == at::kInt && valid.scalar_type() == at::kInt,
+              "decode_advance: int64 nxt/out, int32 state");
+  TORCH_CHECK(out.numel() == B && tokens.numel() == B && positions.numel() == B &&
+                  context_lens.numel() == B && valid.numel() == B, "decode_advance: B mismatch");
+  TORCH_CHECK(nxt.is_contiguous() && out.is_contiguous() && tokens.is_contiguous() &&
+                  positions.is_contiguous() && context_lens.is_contiguous() && valid.is_contiguous(),
+              "decode_advance: contiguous tensors");
+  c10::DeviceGuard g(nxt.device());
+  CHECK_RC(docqa_decode_advance(nxt.data_ptr<int64_t>(), out.data_ptr<int64_t>(), tokens.data_ptr<int>(),
+                                positions.data_ptr<int>(), context_lens.data_ptr<int>(), valid.data_ptr<int>(),
+                                B, stream()), "decode_advance");
+}
+
 at::Tensor argmax(const at::Tensor& logits) {
   CHECK_GPU(logits);
   TORCH_CHECK(logits.dim() == 2 && logits.stride(1) == 1, "argmax wants [rows, V] with unit stride");
@@ -532,6 +570,8 @@ TORCH_LIBRARY(docqa, m) {
   m.def("bert_embed_ln(Tensor ids, Tensor pos, Tensor? token_type, Tensor wte, Tensor wpe, "
         "Tensor wtt, Tensor gamma, Tensor beta, float eps) -> Tensor");
   m.def("argmax(Tensor logits) -> Tensor");
+  m.def("decode_slots(Tensor block_tables, Tensor positions, Tensor valid, int BS) -> Tensor");
+  m.def("decode_advance(Tensor nxt, Tensor(a!) out, Tensor(b!) tokens, Tensor(c!) positions, Tensor(d!) context_lens, Tensor valid) -> ()");
   m.def("sample(Tensor logits, Tensor inv_temp, Tensor top_k, Tensor top_p, Tensor u) -> Tensor");
   m.def("paged_decode(Tensor q, Tensor k_cache, Tensor v_cache, Tensor block_tables, "
         "Tensor context_lens, int Hq, int max_context, float scale) -> Tensor");
@@ -577,6 +617,8 @@ TORCH_LIBRARY_IMPL(docqa, CUDA, m) {
   m.impl("embedding", &embedding);
   m.impl("bert_embed_ln", &bert_embed_ln);
   m.impl("argmax", &argmax);
+  m.impl("decode_slots", &decode_slots);
+  m.impl("decode_advance", &decode_advance);
   m.impl("sample", &sample);
   m.impl("paged_decode", &paged_decode);
   m.impl("flash_prefill", &flash_prefill);

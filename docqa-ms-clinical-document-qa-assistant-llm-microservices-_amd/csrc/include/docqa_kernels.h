@@ -22,6 +22,10 @@ int docqa_bias_act(const void* x, const void* bias, const void* res, void* out, 
                    int gelu, hipStream_t s);
 
 int docqa_embedding(const int* ids, const void* table, void* out, int T, int H, int V, hipStream_t s);
+int docqa_decode_slots(const int* block_tables, int maxb, const int* positions, const int* valid,
+                       int* slots, int B, int BS, hipStream_t s);
+int docqa_decode_advance(const int64_t* nxt, int64_t* out, int* tokens, int* positions,
+                         int* context_lens, const int* valid, int B, hipStream_t s);
 int docqa_bert_embed_ln(const int* ids, const int* pos, const int* tt, const void* wte,
                         const void* wpe, const void* wtt, const void* g, const void* b, void* out,
                         int T, int H, float eps, hipStream_t s);

@@ -299,3 +299,52 @@ int docqa_sample(const float* logits, int rows, int V, int ld, const float* inv_
   DOCQA_CHECK_LAUNCH();
   return 0;
 }
+
+// ---- decode-step state (engine/llm_engine.py:_step_body): one launch each instead of the
+// ~15 tiny tensor ops (gather, where, div/mod, casts, copies, adds) a step otherwise
+// spends ~60 us of graph time on.
+//   slots[i] = valid[i] ? block_tables[i][pos[i] / BS] * BS + pos[i] % BS : -1
+__global__ __launch_bounds__(256) void decode_slots_kernel(const int* __restrict__ bt, int maxb,
+                                                           const int* __restrict__ pos,
+                                                           const int* __restrict__ valid,
+                                                           int* __restrict__ slots, int B, int BS) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= B) return;
+  const int p = pos[i];
+  const int blk = p / BS;
+  slots[i] = (valid[i] && blk < maxb) ? bt[(size_t)i * maxb + blk] * BS + (p - blk * BS) : -1;
+}
+
+//   out[i] = nxt[i]; tokens[i] = nxt[i]; pos[i] += valid[i]; ctx[i] += valid[i]
+__global__ __launch_bounds__(256) void decode_advance_kernel(const int64_t* __restrict__ nxt,
+                                                             int64_t* __restrict__ out,
+                                                             int* __restrict__ tokens,
+                                                             int* __restrict__ pos,
+                                                             int* __restrict__ ctx,
+                                                             const int* __restrict__ valid, int B) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= B) return;
+  const int64_t t = nxt[i];
+  const int v = valid[i];
+  out[i] = t;
+  tokens[i] = (int)t;
+  pos[i] += v;
+  ctx[i] += v;
+}
+
+int docqa_decode_slots(const int* block_tables, int maxb, const int* positions, const int* valid,
+                       int* slots, int B, int BS, hipStream_t s) {
+  if (B == 0) return 0;
+  if (BS <= 0 || maxb <= 0) return -1;
+  decode_slots_kernel<<<(B + 255) / 256, 256, 0, s>>>(block_tables, maxb, positions, valid, slots, B, BS);
+  DOCQA_CHECK_LAUNCH();
+  return 0;
+}
+
+int docqa_decode_advance(const int64_t* nxt, int64_t* out, int* tokens, int* positions,
+                         int* context_lens, const int* valid, int B, hipStream_t s) {
+  if (B == 0) return 0;
+  decode_advance_kernel<<<(B + 255) / 256, 256, 0, s>>>(nxt, out, tokens, positions, context_lens, valid, B);
+  DOCQA_CHECK_LAUNCH();
+  return 0;
+}

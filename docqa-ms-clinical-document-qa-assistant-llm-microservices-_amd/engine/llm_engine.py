@@ -190,11 +190,8 @@ class LLMEngine:
 
     # ------------------------------------------------------------------ decode step
     def _step_body(self, g: _DecodeGraph) -> None:
-        BS = self.block_size
-        valid = g.valid.bool()
-        blk = torch.gather(g.block_tables, 1, (g.positions // BS).long()[:, None])[:, 0]
-        slots = torch.where(valid, blk * BS + g.positions % BS, torch.full_like(blk, -1))
-        meta = AttnMeta(prefill=False, positions=g.positions, slot_mapping=slots.int(),
+        slots = ops.decode_slots(g.block_tables, g.positions, g.valid, self.block_size)
+        meta = AttnMeta(prefill=False, positions=g.positions, slot_mapping=slots,
                         block_tables=g.block_tables, context_lens=g.context_lens,
                         max_context=self.max_context)
         if g.cascade:
@@ -202,10 +199,7 @@ class LLMEngine:
             meta.cascade_chunks = self._cascade_chunks(g.bp)
         logits = self.model.forward(g.tokens, meta, self.kv.caches)
         nxt = self._select(logits, g)
-        g.out.copy_(nxt)
-        g.tokens.copy_(nxt.int())
-        g.positions.add_(g.valid)
-        g.context_lens.add_(g.valid)
+        ops.decode_advance(nxt.long().contiguous(), g.out, g.tokens, g.positions, g.context_lens, g.valid)
 
     def _select(self, logits, g: _DecodeGraph):
         from .. import ops

@@ -271,6 +271,21 @@ def bert_embed_ln(ids, pos, token_type, wte, wpe, wtt, gamma, beta, eps):
 
 
 # ----------------------------------------------------------------------------- sampling
+def decode_slots(block_tables, positions, valid, BS: int):
+    """Paged-cache slot of each decode row's next token, -1 for padded rows."""
+    if _gpu(block_tables):
+        return _native().decode_slots(block_tables, positions, valid, BS)
+    return ref.decode_slots(block_tables, positions, valid, BS)
+
+
+def decode_advance(nxt, out, tokens, positions, context_lens, valid) -> None:
+    """In place: out <- nxt, tokens <- nxt, positions / context_lens += valid."""
+    if _gpu(nxt):
+        _native().decode_advance(nxt, out, tokens, positions, context_lens, valid)
+        return
+    ref.decode_advance(nxt, out, tokens, positions, context_lens, valid)
+
+
 def argmax(logits):
     if _gpu(logits):
         return _native().argmax(logits)

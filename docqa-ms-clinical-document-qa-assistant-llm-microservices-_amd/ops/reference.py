@@ -282,3 +282,15 @@ def pool_l2(h, cu_seqlens, mean, normalize):
     if normalize:
         out = F.normalize(out, dim=-1, eps=1e-12)
     return out
+
+
+def decode_slots(block_tables, positions, valid, BS: int):
+    blk = torch.gather(block_tables, 1, (positions // BS).long().clamp(max=block_tables.shape[1] - 1)[:, None])[:, 0]
+    return torch.where(valid.bool(), blk * BS + positions % BS, torch.full_like(blk, -1)).int()
+
+
+def decode_advance(nxt, out, tokens, positions, context_lens, valid) -> None:
+    out.copy_(nxt)
+    tokens.copy_(nxt.int())
+    positions.add_(valid)
+    context_lens.add_(valid)

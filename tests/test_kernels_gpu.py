@@ -504,3 +504,22 @@ def test_padded_slots_get_defined_outputs(native, B):
     tab = torch.randn(50, 64, device="cuda").bfloat16()
     e = native.embedding(torch.tensor([3, 2 ** 31 - 1, -5], device="cuda", dtype=torch.int32), tab)
     assert torch.equal(e[1], tab[0]) and torch.equal(e[2], tab[0]) and torch.equal(e[0], tab[3])
+
+
+def test_decode_state_kernels(native):
+    """decode_slots / decode_advance (one launch each per decode step) vs the reference."""
+    from docqa_amd.ops import reference as R
+
+    B, maxb, BS = 77, 32, 64
+    bt = torch.randperm(B * maxb, device="cuda").int().view(B, maxb)
+    pos = torch.randint(0, maxb * BS, (B,), device="cuda", dtype=torch.int32)
+    valid = (torch.rand(B, device="cuda") > 0.3).int()
+    assert torch.equal(torch.ops.docqa.decode_slots(bt, pos, valid, BS), R.decode_slots(bt, pos, valid, BS))
+    nxt = torch.randint(0, 128256, (B,), device="cuda", dtype=torch.long)
+    st1 = [torch.zeros(B, device="cuda", dtype=torch.long), torch.zeros(B, device="cuda", dtype=torch.int32),
+           pos.clone(), pos.clone() + 1]
+    st2 = [t.clone() for t in st1]
+    torch.ops.docqa.decode_advance(nxt, *st1, valid)
+    R.decode_advance(nxt, *st2, valid)
+    for a, b in zip(st1, st2):
+        assert torch.equal(a, b)
