@@ -16,6 +16,9 @@ import torch
 from benchmarks.bench_kernels import timeit
 
 
+MIX = os.environ.get("MIX", "uniform")      # uniform | random | sorted | lpt context lengths
+
+
 def main():
     from docqa_amd import ops
 
@@ -27,21 +30,32 @@ def main():
     if os.environ.get("SHAPES"):
         shapes = [tuple(int(v) for v in x.split("x")) for x in os.environ["SHAPES"].split(",")]
     for (B, ctx) in shapes:
-        maxb = (ctx + BS - 1) // BS
+        maxb = (ctx * (2 if MIX != "uniform" else 1) + BS - 1) // BS
         nbytes = 2 * B * maxb * Hkv * BS * D * 2
         copies = max(2, (1 << 30) // nbytes + 1)
         caches = [(torch.randn(B * maxb, Hkv, BS, D, device="cuda", dtype=torch.bfloat16),
                    torch.randn(B * maxb, Hkv, BS, D, device="cuda", dtype=torch.bfloat16)) for _ in range(copies)]
         bt = torch.arange(B * maxb, device="cuda", dtype=torch.int32).view(B, maxb)
         cl = torch.full((B,), ctx, device="cuda", dtype=torch.int32)
+        if MIX != "uniform":
+            # same mean context, lengths spread over [0.4, 1.6] x ctx (a RAG batch), in
+            # random order or longest first (LPT dispatch order)
+            g = torch.Generator().manual_seed(0)
+            lens = (ctx * (0.4 + 1.2 * torch.rand(B, generator=g))).int().clamp(1, maxb * BS)
+            if MIX == "sorted":   # the rows themselves sorted (no order input)
+                lens = lens.sort(descending=True).values
+            cl = lens.to(torch.int32).cuda()
         q = torch.randn(B, (Hq + 2 * Hkv) * D, device="cuda", dtype=torch.bfloat16)
+        # MIX=lpt: random lengths, dispatched longest first through the kernel's order input
+        order = torch.argsort(cl.cpu(), descending=True).int().cuda() if MIX == "lpt" else None
         it = iter(range(1 << 30))
 
         def run():
             kc, vc = caches[next(it) % copies]
-            return nat.paged_decode(q, kc, vc, bt, cl, Hq, 2048 if ctx < 2048 else 4096, 1 / math.sqrt(D))
+            return nat.paged_decode(q, kc, vc, bt, cl, Hq, 2048 if ctx < 2048 else 4096, 1 / math.sqrt(D), order)
         t = timeit(run, iters=4 * copies)
-        res.append({"B": B, "ctx": ctx, "us": round(t, 1), "kv_TBps": round(2 * B * ctx * Hkv * D * 2 / t / 1e6, 2)})
+        kv = 2 * int(cl.sum()) * Hkv * D * 2
+        res.append({"B": B, "ctx": ctx, "mix": MIX, "us": round(t, 1), "kv_TBps": round(kv / t / 1e6, 2)})
         del caches
         torch.cuda.empty_cache()
     print(json.dumps({"mfma": os.environ.get("DOCQA_DECODE_MFMA", "1"), "nsr": os.environ.get("DOCQA_DECODE_NSR", "4"),

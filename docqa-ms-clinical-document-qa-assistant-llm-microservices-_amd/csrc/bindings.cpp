@@ -246,9 +246,18 @@ at::Tensor sample(const at::Tensor& logits, const at::Tensor& inv_temp, const at
   return out;
 }
 
+// optional LPT dispatch order of the decode workgroups (int32 permutation of [0, B))
+static const int* order_ptr(const c10::optional<at::Tensor>& order, int B) {
+  if (!order.has_value() || !order->defined()) return nullptr;
+  TORCH_CHECK(order->scalar_type() == at::kInt && order->is_contiguous() && order->numel() == B,
+              "order: contiguous int32 [B]");
+  return order->data_ptr<int>();
+}
+
 at::Tensor paged_decode(const at::Tensor& q, const at::Tensor& k_cache, const at::Tensor& v_cache,
                         const at::Tensor& block_tables, const at::Tensor& context_lens,
-                        int64_t Hq, int64_t max_context, double scale) {
+                        int64_t Hq, int64_t max_context, double scale,
+                        const c10::optional<at::Tensor>& order) {
   // q: [B, >= Hq*D] rows (e.g. the packed QKV buffer), caches [NB, Hkv, BS, D]
   CHECK_GPU(q); CHECK_BF16(q); CHECK_BF16(k_cache); CHECK_BF16(v_cache);
   CHECK_I32(block_tables); CHECK_I32(context_lens); CHECK_CONTIG(block_tables);
@@ -264,7 +273,7 @@ at::Tensor paged_decode(const at::Tensor& q, const at::Tensor& k_cache, const at
                               block_tables.data_ptr<int>(), block_tables.size(1),
                               context_lens.data_ptr<int>(), out.data_ptr(), Hq * D,
                               tmp_out.data_ptr<float>(), tmp_ml.data_ptr<float>(), B, Hq, Hkv, D,
-                              BS, max_parts, (float)scale, stream()), "paged_decode");
+                              BS, max_parts, (float)scale, order_ptr(order, B), stream()), "paged_decode");
   return out;
 }
 
@@ -275,7 +284,7 @@ at::Tensor paged_decode_cascade(const at::Tensor& q, at::Tensor k_cache, at::Ten
                                 const at::Tensor& block_tables, const at::Tensor& context_lens,
                                 int64_t Hq, int64_t max_context, double scale,
                                 const at::Tensor& prefix_table, const at::Tensor& prefix_len,
-                                int64_t nchunk) {
+                                int64_t nchunk, const c10::optional<at::Tensor>& order) {
   CHECK_GPU(q); CHECK_BF16(q); CHECK_BF16(k_cache); CHECK_BF16(v_cache);
   CHECK_I32(block_tables); CHECK_I32(context_lens); CHECK_CONTIG(block_tables);
   CHECK_I32(prefix_table); CHECK_I32(prefix_len); CHECK_CONTIG(prefix_table);
@@ -299,7 +308,8 @@ at::Tensor paged_decode_cascade(const at::Tensor& q, at::Tensor k_cache, at::Ten
                                       tmp_out.data_ptr<float>(), tmp_ml.data_ptr<float>(), B, Hq, Hkv, BS,
                                       max_parts, (float)scale, prefix_table.data_ptr<int>(),
                                       prefix_len.data_ptr<int>(), (int)nchunk, pacc.data_ptr<float>(),
-                                      pml.data_ptr<float>(), stream()), "paged_decode_cascade");
+                                      pml.data_ptr<float>(), order_ptr(order, B), stream()),
+           "paged_decode_cascade");
   return out;
 }
 
@@ -308,7 +318,8 @@ at::Tensor paged_decode_cascade(const at::Tensor& q, at::Tensor k_cache, at::Ten
 at::Tensor paged_decode_fused(const at::Tensor& P, const at::Tensor& positions, const at::Tensor& cos_sin,
                               const at::Tensor& slot_mapping, at::Tensor k_cache, at::Tensor v_cache,
                               const at::Tensor& block_tables, const at::Tensor& context_lens,
-                              int64_t Hq, int64_t max_context, double scale) {
+                              int64_t Hq, int64_t max_context, double scale,
+                              const c10::optional<at::Tensor>& order) {
   CHECK_GPU(P); CHECK_CONTIG(P); CHECK_BF16(k_cache); CHECK_BF16(v_cache);
   CHECK_I32(positions); CHECK_I32(slot_mapping); CHECK_I32(block_tables); CHECK_I32(context_lens);
   CHECK_CONTIG(block_tables);
@@ -327,7 +338,8 @@ at::Tensor paged_decode_fused(const at::Tensor& P, const at::Tensor& positions, 
                                     k_cache.data_ptr(), v_cache.data_ptr(), block_tables.data_ptr<int>(),
                                     block_tables.size(1), context_lens.data_ptr<int>(), out.data_ptr(),
                                     Hq * D, tmp_out.data_ptr<float>(), tmp_ml.data_ptr<float>(), B, Hq,
-                                    Hkv, BS, max_parts, (float)scale, stream()), "paged_decode_fused");
+                                    Hkv, BS, max_parts, (float)scale, order_ptr(order, B), stream()),
+           "paged_decode_fused");
   return out;
 }
 
@@ -574,7 +586,7 @@ TORCH_LIBRARY(docqa, m) {
   m.def("decode_advance(Tensor nxt, Tensor(a!) out, Tensor(b!) tokens, Tensor(c!) positions, Tensor(d!) context_lens, Tensor valid) -> ()");
   m.def("sample(Tensor logits, Tensor inv_temp, Tensor top_k, Tensor top_p, Tensor u) -> Tensor");
   m.def("paged_decode(Tensor q, Tensor k_cache, Tensor v_cache, Tensor block_tables, "
-        "Tensor context_lens, int Hq, int max_context, float scale) -> Tensor");
+        "Tensor context_lens, int Hq, int max_context, float scale, Tensor? order=None) -> Tensor");
   m.def("flash_prefill(Tensor qkv, Tensor cu_seqlens, int max_len, int Hq, int Hkv, int D, "
         "float scale, bool causal) -> Tensor");
   m.def("knn(Tensor xb, Tensor xb_norms, Tensor xq, int k, bool inner_product, int id_offset) "
@@ -591,10 +603,10 @@ TORCH_LIBRARY(docqa, m) {
   m.def("dgemm_glu(Tensor x, Tensor w) -> Tensor");
   m.def("paged_decode_cascade(Tensor q, Tensor k_cache, Tensor v_cache, Tensor block_tables, "
         "Tensor context_lens, int Hq, int max_context, float scale, Tensor prefix_table, Tensor prefix_len, "
-        "int nchunk) -> Tensor");
+        "int nchunk, Tensor? order=None) -> Tensor");
   m.def("paged_decode_fused(Tensor P, Tensor positions, Tensor cos_sin, Tensor slot_mapping, "
         "Tensor(a!) k_cache, Tensor(b!) v_cache, Tensor block_tables, Tensor context_lens, int Hq, "
-        "int max_context, float scale) -> Tensor");
+        "int max_context, float scale, Tensor? order=None) -> Tensor");
   m.def("ar_oneshot(Tensor x, int rank, int[] regions, int max_elems, Tensor(a!) epochs, Tensor(b!) err) -> Tensor");
   m.def("ar_region_bytes(int max_elems) -> int", &ar_region_bytes);
   m.def("ar_alloc(int bytes) -> int", &ar_alloc);

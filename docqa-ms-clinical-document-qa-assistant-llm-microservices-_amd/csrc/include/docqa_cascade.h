@@ -19,6 +19,11 @@ struct CascadeIn {        // prefix partials consumed by the decode kernel / mer
   const float* ml;        // [nchunk, B, Hq, 2] (running max in log2 units, sum p)
   const int* plen;        // device scalar: shared prefix length (multiple of 64); null: none
   int nchunk;
+  // dispatch order of the decode workgroups: grid row y serves sequence order[y] (a
+  // permutation, longest context first -- LPT -- so the short sequences fill the tail of
+  // the last launch round); null: identity.  Not a cascade input, but every decode kernel
+  // launch carries this struct.
+  const int* order = nullptr;
 };
 
 struct CascadeOut {       // prefix partials produced by the MFMA prefix kernel

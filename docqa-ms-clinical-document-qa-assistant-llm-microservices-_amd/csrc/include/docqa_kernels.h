@@ -38,13 +38,14 @@ int docqa_sample(const float* logits, int rows, int V, int ld, const float* inv_
 int docqa_paged_decode(const void* q, int q_stride, const void* k_cache, const void* v_cache,
                        const int* block_tables, int maxb, const int* context_lens, void* out,
                        int out_stride, float* tmp_out, float* tmp_ml, int B, int Hq, int Hkv,
-                       int D, int BS, int max_parts, float scale, hipStream_t s);
+                       int D, int BS, int max_parts, float scale, const int* order, hipStream_t s);
 int docqa_decode_splits(int B, int Hkv, int max_context);
 int docqa_paged_decode_cascade(const void* q, int q_stride, void* k_cache, void* v_cache,
                                const int* block_tables, int maxb, const int* context_lens, void* out,
                                int out_stride, float* tmp_out, float* tmp_ml, int B, int Hq, int Hkv,
                                int BS, int max_parts, float scale, const int* prefix_table,
-                               const int* plen, int nchunk, float* pacc, float* pml, hipStream_t s);
+                               const int* plen, int nchunk, float* pacc, float* pml, const int* order,
+                               hipStream_t s);
 
 int docqa_flash_prefill(const void* qkv, int row_stride, const int* cu_seqlens, void* out,
                         int o_stride, int B, int max_len, int Hq, int Hkv, int head_dim,
@@ -76,7 +77,7 @@ int docqa_paged_decode_fused(const float* P, int S, const int* positions, const 
                              const int* slot_mapping, void* k_cache, void* v_cache,
                              const int* block_tables, int maxb, const int* context_lens, void* out,
                              int out_stride, float* tmp_out, float* tmp_ml, int B, int Hq, int Hkv,
-                             int BS, int max_parts, float scale, hipStream_t s);
+                             int BS, int max_parts, float scale, const int* order, hipStream_t s);
 int docqa_dgemm_splits(int N, int K);
 int docqa_dgemm_glu(const void* X, const void* W, void* Y, int M, int N, int K, hipStream_t s);
 int docqa_dgemm(const void* X, const void* W, void* Y, float* partial, int M, int N, int K, int S,

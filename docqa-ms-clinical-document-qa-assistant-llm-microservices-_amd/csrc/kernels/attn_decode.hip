@@ -385,7 +385,7 @@ __global__ __launch_bounds__(256) void paged_decode_ring_kernel(
   __shared__ float s_m[4][G], s_l[4][G];
   __shared__ int s_bt[256];                      // block ids of the slice (<= 16k tokens)
 
-  const int part = blockIdx.z, kvh = blockIdx.x, b = blockIdx.y;
+  const int part = blockIdx.z, kvh = blockIdx.x, b = ci.order ? ci.order[blockIdx.y] : blockIdx.y;
   const int L = context_lens[b];
   // cascade: keys [0, P) are the shared prefix (attended by the prefix kernel), this
   // kernel covers the sequence's own suffix [P, L); P is a multiple of 64
@@ -562,7 +562,7 @@ __global__ __launch_bounds__(256) void paged_decode_mfma_kernel(
   // HPW KV heads per workgroup, one after the other through the same ring (the K/V tile
   // stream runs on across the head boundary): 1/HPW of the workgroups -- one launch round
   // at batch 128 -- and the next head's ring fill overlaps the current head's tail.
-  const int part = blockIdx.z, kvh0 = blockIdx.x * HPW, b = blockIdx.y;
+  const int part = blockIdx.z, kvh0 = blockIdx.x * HPW, b = ci.order ? ci.order[blockIdx.y] : blockIdx.y;
   const int L = context_lens[b];
   const int P = ci.plen ? *ci.plen : 0;
   const int slice = split_chunk(L - P, max_parts);
@@ -816,9 +816,11 @@ __global__ __launch_bounds__(D) void paged_decode_reduce(const float* __restrict
 int docqa_paged_decode(const void* q, int q_stride, const void* k_cache, const void* v_cache,
                        const int* block_tables, int maxb, const int* context_lens, void* out,
                        int out_stride, float* tmp_out, float* tmp_ml, int B, int Hq, int Hkv,
-                       int D, int BS, int max_parts, float scale, hipStream_t s) {
+                       int D, int BS, int max_parts, float scale, const int* order, hipStream_t s) {
   if (B == 0) return 0;
   if (D != 128 || (BS & (BS - 1)) != 0 || Hq % Hkv != 0) return -1;
+  CascadeIn oi{};
+  oi.order = order;
   int log2BS = 0;
   while ((1 << log2BS) < BS) ++log2BS;
   const int G = Hq / Hkv;
@@ -849,17 +851,17 @@ int docqa_paged_decode(const void* q, int q_stride, const void* k_cache, const v
         paged_decode_mfma_kernel<GG, true, 2><<<dim3(Hkv / 2, B, 1), 256, 0, s>>>(            \
             (const uint16_t*)q, q_stride, (const uint16_t*)k_cache, (const uint16_t*)v_cache, \
             block_tables, maxb, context_lens, tmp_out, tmp_ml, Hkv, max_parts, scale,         \
-            (uint16_t*)out, out_stride, CascadeIn{});                                         \
+            (uint16_t*)out, out_stride, oi);                                         \
       else if (direct)                                                                        \
         paged_decode_mfma_kernel<GG, true><<<grid, 256, 0, s>>>(                              \
             (const uint16_t*)q, q_stride, (const uint16_t*)k_cache, (const uint16_t*)v_cache, \
             block_tables, maxb, context_lens, tmp_out, tmp_ml, Hkv, max_parts, scale,         \
-            (uint16_t*)out, out_stride, CascadeIn{});                                         \
+            (uint16_t*)out, out_stride, oi);                                         \
       else                                                                                    \
         paged_decode_mfma_kernel<GG, false><<<grid, 256, 0, s>>>(                             \
             (const uint16_t*)q, q_stride, (const uint16_t*)k_cache, (const uint16_t*)v_cache, \
             block_tables, maxb, context_lens, tmp_out, tmp_ml, Hkv, max_parts, scale,         \
-            (uint16_t*)out, out_stride, CascadeIn{});                                         \
+            (uint16_t*)out, out_stride, oi);                                         \
     } while (0)
     if (G == 4) DMFMA(4);
     else DMFMA(8);
@@ -882,12 +884,12 @@ int docqa_paged_decode(const void* q, int q_stride, const void* k_cache, const v
         paged_decode_ring_kernel<GG, true><<<grid, 256, 0, s>>>(                              \
             (const uint16_t*)q, q_stride, (uint16_t*)k_cache, (uint16_t*)v_cache,             \
             block_tables, maxb, context_lens, tmp_out, tmp_ml, Hkv, max_parts, scale,         \
-            (uint16_t*)out, out_stride, FusedQKV{}, CascadeIn{});                                          \
+            (uint16_t*)out, out_stride, FusedQKV{}, oi);                                          \
       else                                                                                    \
         paged_decode_ring_kernel<GG, false><<<grid, 256, 0, s>>>(                             \
             (const uint16_t*)q, q_stride, (uint16_t*)k_cache, (uint16_t*)v_cache,             \
             block_tables, maxb, context_lens, tmp_out, tmp_ml, Hkv, max_parts, scale,         \
-            (uint16_t*)out, out_stride, FusedQKV{}, CascadeIn{});                                          \
+            (uint16_t*)out, out_stride, FusedQKV{}, oi);                                          \
     } while (0)
     switch (G) {
       case 1: DRING(1); break;
@@ -946,9 +948,11 @@ int docqa_paged_decode_fused(const float* P, int S, const int* positions, const 
                              const int* slot_mapping, void* k_cache, void* v_cache,
                              const int* block_tables, int maxb, const int* context_lens, void* out,
                              int out_stride, float* tmp_out, float* tmp_ml, int B, int Hq, int Hkv,
-                             int BS, int max_parts, float scale, hipStream_t s) {
+                             int BS, int max_parts, float scale, const int* order, hipStream_t s) {
   if (B == 0) return 0;
   if (BS != 64 || maxb > 256 || Hq % Hkv != 0 || S < 1) return -1;
+  CascadeIn oi{};
+  oi.order = order;
   const int G = Hq / Hkv;
   dim3 grid(Hkv, B, max_parts);   // partitions slowest: see kDecodeGridNote
   const bool direct = max_parts == 1;
@@ -958,11 +962,11 @@ int docqa_paged_decode_fused(const float* P, int S, const int* positions, const 
     if (direct)                                                                               \
       paged_decode_ring_kernel<GG, true, true><<<grid, 256, 0, s>>>(                          \
           nullptr, 0, (uint16_t*)k_cache, (uint16_t*)v_cache, block_tables, maxb,             \
-          context_lens, tmp_out, tmp_ml, Hkv, max_parts, scale, (uint16_t*)out, out_stride, fz, CascadeIn{}); \
+          context_lens, tmp_out, tmp_ml, Hkv, max_parts, scale, (uint16_t*)out, out_stride, fz, oi); \
     else                                                                                      \
       paged_decode_ring_kernel<GG, false, true><<<grid, 256, 0, s>>>(                         \
           nullptr, 0, (uint16_t*)k_cache, (uint16_t*)v_cache, block_tables, maxb,             \
-          context_lens, tmp_out, tmp_ml, Hkv, max_parts, scale, (uint16_t*)out, out_stride, fz, CascadeIn{}); \
+          context_lens, tmp_out, tmp_ml, Hkv, max_parts, scale, (uint16_t*)out, out_stride, fz, oi); \
   } while (0)
   switch (G) {
     case 1: DFUSED(1); break;
@@ -991,13 +995,14 @@ int docqa_paged_decode_cascade(const void* q, int q_stride, void* k_cache, void*
                                const int* block_tables, int maxb, const int* context_lens, void* out,
                                int out_stride, float* tmp_out, float* tmp_ml, int B, int Hq, int Hkv,
                                int BS, int max_parts, float scale, const int* prefix_table,
-                               const int* plen, int nchunk, float* pacc, float* pml, hipStream_t s) {
+                               const int* plen, int nchunk, float* pacc, float* pml, const int* order,
+                               hipStream_t s) {
   if (B == 0) return 0;
   if (BS != 64 || maxb > 256 || Hq != 4 * Hkv || nchunk < 1 || nchunk > kCascadeMaxChunks) return -1;
   int rc = docqa_cascade_prefix(q, q_stride, B, Hq, Hkv, scale, k_cache, v_cache, prefix_table, plen,
                                 BS, nchunk, pacc, pml, s);
   if (rc) return rc;
-  const CascadeIn ci{pacc, pml, plen, nchunk};
+  const CascadeIn ci{pacc, pml, plen, nchunk, order};
   dim3 grid(Hkv, B, max_parts);   // partitions slowest: see kDecodeGridNote
   if (mfma_decode_on(Hq / Hkv)) {
     if (max_parts == 1 && Hkv % 2 == 0 && hpw_knob() == 2)

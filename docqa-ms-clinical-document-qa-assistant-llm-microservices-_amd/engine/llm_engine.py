@@ -78,6 +78,10 @@ class _DecodeGraph:
         # cascade decode: block ids / length of the prompt prefix every row shares
         self.shared_table = torch.zeros(eng.max_blocks_per_seq, dtype=torch.int32, device=dev)
         self.shared_len = torch.zeros(1, dtype=torch.int32, device=dev)
+        # decode-attention dispatch order (LPT: longest context first), a permutation of
+        # [0, bp) per bucket -- never a view of another bucket's buffer
+        self.order = torch.arange(bp, dtype=torch.int32, device=dev)
+        self.order_key = None
         self.cascade = False
         self.greedy = True
         self.graph = None
@@ -93,6 +97,8 @@ class _DecodeGraph:
                      "top_k", "top_p", "out"):
             setattr(g, name, getattr(master, name)[:bp])
         g.shared_table, g.shared_len = master.shared_table, master.shared_len
+        g.order = torch.arange(bp, dtype=torch.int32, device=master.tokens.device)
+        g.order_key = None
         g.cascade, g.greedy, g.graph = False, True, None
         return g
 
@@ -123,6 +129,9 @@ class LLMEngine:
         self.cascade = os.environ.get("DOCQA_CASCADE", "1") == "1"
         self.cascade_min_tokens = int(os.environ.get("DOCQA_CASCADE_MIN_TOKENS", "128"))
         self.cascade_min_batch = int(os.environ.get("DOCQA_CASCADE_MIN_BATCH", "4"))
+        # LPT dispatch of the decode-attention workgroups (mixed context lengths cost ~15 %
+        # in random order, benchmarks/bench_decode_attn.py MIX=random vs sorted)
+        self.lpt = os.environ.get("DOCQA_DECODE_LPT", "1") == "1"
         self._graphs: dict[tuple, _DecodeGraph] = {}
         self._pool = None
         self.stats = GenStats()
@@ -193,7 +202,7 @@ class LLMEngine:
         slots = ops.decode_slots(g.block_tables, g.positions, g.valid, self.block_size)
         meta = AttnMeta(prefill=False, positions=g.positions, slot_mapping=slots,
                         block_tables=g.block_tables, context_lens=g.context_lens,
-                        max_context=self.max_context)
+                        max_context=self.max_context, seq_order=g.order if self.lpt else None)
         if g.cascade:
             meta.shared_table, meta.shared_len = g.shared_table, g.shared_len
             meta.cascade_chunks = self._cascade_chunks(g.bp)
@@ -219,6 +228,17 @@ class LLMEngine:
             g.cascade = cascade
             self._graphs[key] = g
         return g
+
+    def set_order(self, g: _DecodeGraph, lens: list[int], key=None) -> None:
+        """Dispatch order of bucket ``g``'s decode rows: active rows [0, len(lens)) by
+        descending context length, then the padded rows.  Contexts all grow by one token a
+        step, so the order stays valid until the batch composition changes (``key``: skip
+        the upload when it is unchanged)."""
+        if key is not None and g.order_key == key:
+            return
+        order = sorted(range(len(lens)), key=lambda i: -lens[i]) + list(range(len(lens), g.bp))
+        g.order.copy_(torch.tensor(order, dtype=torch.int32).to(g.order.device, non_blocking=True))
+        g.order_key = key
 
     def _cascade_chunks(self, bp: int) -> int:
         """Key chunks of the shared-prefix kernel: about 256 workgroups of (64 rows, KV
@@ -346,6 +366,7 @@ class LLMEngine:
             pos[:B] = torch.tensor(lens, dtype=torch.int32)
             g.positions.copy_(pos.to(dev))
             g.context_lens.copy_((pos + vl).to(dev))
+            self.set_order(g, lens)
             if not greedy:
                 g.inv_temp.fill_(1.0 / params.temperature)
                 g.top_k.fill_(params.top_k)

@@ -83,6 +83,7 @@ class ContinuousEngine:
         self._pending = None               # (event, pinned host tokens, slot -> request) of the last step
         self._host = None
         self._flip = 0
+        self._version = 0                  # bumped whenever the running set changes
 
     # ------------------------------------------------------------------ client side
     def submit(self, prompt: list[int], params: SamplingParams | None = None, on_token=None) -> cf.Future:
@@ -164,6 +165,7 @@ class ContinuousEngine:
             if not r.future.done():
                 r.future.set_exception(e)
         self.running = []
+        self._version += 1
         self._master.valid.zero_()
         self._master.context_lens.zero_()
 
@@ -274,6 +276,7 @@ class ContinuousEngine:
         m.top_k[sl].copy_(tk.to(dev, non_blocking=True))
         m.top_p[sl].copy_(tp.to(dev, non_blocking=True))
         self.running.extend(reqs)
+        self._version += 1
 
     def _sample_rows(self, logits: torch.Tensor, params: list[SamplingParams]) -> list[int]:
         model = self.eng.model
@@ -302,6 +305,9 @@ class ContinuousEngine:
         bp = _bucket(n, eng.max_batch) if self.pad_buckets else n
         greedy = all(r.params.temperature <= 0 for r in self.running)
         g = self._graph(bp, greedy, self._nshared > 0)
+        if eng.lpt:
+            # re-rank only when the running set changed (admission / retirement)
+            eng.set_order(g, [len(r.prompt) + len(r.out) for r in self.running], key=self._version)
         t0 = time.perf_counter()
         with tracing.span("sched.decode", running=n, bucket=bp, cascade=self._nshared > 0):
             if eng.use_graphs:
@@ -383,6 +389,7 @@ class ContinuousEngine:
         m.positions[k:n].zero_()
         m.tokens[k:n].zero_()
         self.running = [self.running[i] for i in keep]
+        self._version += 1
 
     def _update_shared(self) -> None:
         """Cascade decode applies when all running slots share leading cached blocks."""

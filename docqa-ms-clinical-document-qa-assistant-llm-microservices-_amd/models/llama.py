@@ -88,6 +88,9 @@ class AttnMeta:
     shared_table: torch.Tensor | None = None
     shared_len: torch.Tensor | None = None
     cascade_chunks: int = 8
+    # (decode) workgroup dispatch order: int32 permutation of the rows, longest context
+    # first (LPT), so short sequences fill the last launch round; None: row order
+    seq_order: torch.Tensor | None = None
 
 
 class LlamaModel:
@@ -239,13 +242,13 @@ class LlamaModel:
                     ops.rope_cache(qkv, meta.positions, self.cos_sin, meta.slot_mapping, kc, vc, hq, hkv, D)
                 a = ops.paged_decode_cascade(qkv, kc, vc, meta.block_tables, meta.context_lens, hq,
                                              meta.max_context, self.scale, meta.shared_table,
-                                             meta.shared_len, meta.cascade_chunks)
+                                             meta.shared_len, meta.cascade_chunks, meta.seq_order)
                 qkv = None
             elif sq and ops.fused_decode_ok(kc, meta.block_tables):
                 # QKV partials -> RoPE + new-token cache write + attention, one launch
                 a = ops.paged_decode_fused(ops.dgemm_partial(x, L["qkv"], sq, tq), meta.positions, self.cos_sin,
                                            meta.slot_mapping, kc, vc, meta.block_tables, meta.context_lens,
-                                           hq, meta.max_context, self.scale)
+                                           hq, meta.max_context, self.scale, meta.seq_order)
                 qkv = None
             elif sq:
                 qkv = ops.rope_cache_splitk(ops.dgemm_partial(x, L["qkv"], sq, tq), meta.positions, self.cos_sin,
@@ -263,7 +266,7 @@ class LlamaModel:
                 a = ops.flash_prefill(qkv, meta.cu_seqlens, meta.max_len, hq, hkv, D, self.scale, True)
             else:
                 a = ops.paged_decode(qkv, kc, vc, meta.block_tables, meta.context_lens, hq,
-                                     meta.max_context, self.scale)
+                                     meta.max_context, self.scale, meta.seq_order)
             if so:
                 x = ops.add_rmsnorm_splitk(ops.dgemm_partial(a, L["o"], so, to), residual, L["post_norm"], eps)
             else:

@@ -228,13 +228,13 @@ def add_rmsnorm_splitk(P, residual, w, eps: float):
 
 
 def paged_decode_fused(P, positions, cos_sin, slot_mapping, k_cache, v_cache, block_tables,
-                       context_lens, Hq, max_context, scale):
+                       context_lens, Hq, max_context, scale, order=None):
     """Decode attention straight from the QKV projection's split-K partial slabs: RoPE,
     paged-cache write of the new token and attention in one launch (attn_decode.hip ring
     kernel, FUSED mode).  Same result as rope_cache_splitk + paged_decode."""
     if _gpu(P):
         return _native().paged_decode_fused(P, positions, cos_sin, slot_mapping, k_cache, v_cache,
-                                            block_tables, context_lens, Hq, max_context, scale)
+                                            block_tables, context_lens, Hq, max_context, scale, order)
     Hkv, D = k_cache.shape[1], k_cache.shape[3]
     qkv = rope_cache_splitk(P, positions, cos_sin, slot_mapping, k_cache, v_cache, Hq, Hkv, D)
     return ref.paged_decode(qkv, k_cache, v_cache, block_tables, context_lens, Hq, max_context, scale)
@@ -299,10 +299,12 @@ def sample(logits, inv_temp, top_k, top_p, u):
 
 
 # ----------------------------------------------------------------------------- attention
-def paged_decode(q, k_cache, v_cache, block_tables, context_lens, Hq, max_context, scale):
+def paged_decode(q, k_cache, v_cache, block_tables, context_lens, Hq, max_context, scale, order=None):
+    """``order``: optional int32 permutation of the rows -- the workgroup dispatch order
+    (longest context first); results do not depend on it."""
     if _gpu(q):
         return _native().paged_decode(q, k_cache, v_cache, block_tables, context_lens, Hq,
-                                      max_context, scale)
+                                      max_context, scale, order)
     return ref.paged_decode(q, k_cache, v_cache, block_tables, context_lens, Hq, max_context, scale)
 
 
@@ -317,14 +319,14 @@ def cascade_ok(k_cache, block_tables, Hq: int) -> bool:
 
 
 def paged_decode_cascade(q, k_cache, v_cache, block_tables, context_lens, Hq, max_context, scale,
-                         prefix_table, prefix_len, nchunk: int = 8):
+                         prefix_table, prefix_len, nchunk: int = 8, order=None):
     """Decode attention with the batch's shared prompt prefix attended once for all rows
     (csrc/include/docqa_cascade.h): keys [0, prefix_len) from ``prefix_table``, keys
     [prefix_len, L) from each row's block table.  Same result as :func:`paged_decode`
     when the prefix blocks are the ones every row's table starts with."""
     if _gpu(q):
         return _native().paged_decode_cascade(q, k_cache, v_cache, block_tables, context_lens, Hq,
-                                              max_context, scale, prefix_table, prefix_len, nchunk)
+                                              max_context, scale, prefix_table, prefix_len, nchunk, order)
     return ref.paged_decode_cascade(q, k_cache, v_cache, block_tables, context_lens, Hq, max_context,
                                     scale, prefix_table, prefix_len, nchunk)
 

@@ -523,3 +523,31 @@ def test_decode_state_kernels(native):
     R.decode_advance(nxt, *st2, valid)
     for a, b in zip(st1, st2):
         assert torch.equal(a, b)
+
+
+@pytest.mark.parametrize("G", [4, 8])
+def test_decode_dispatch_order_is_result_invariant(native, G):
+    """An LPT dispatch order (grid row y -> sequence order[y]) changes only scheduling:
+    plain (G=4: VALU ring kernel, G=8: MFMA kernel) and cascade decode give the same rows
+    with and without it."""
+    B, Hkv, D, BS, maxb = 37, 8, 128, 64, 16
+    Hq = Hkv * G
+    lens = torch.randint(200, maxb * BS, (B,)).int()
+    kc = torch.randn(B * maxb + 8, Hkv, BS, D, device="cuda", dtype=torch.bfloat16)
+    vc = torch.randn_like(kc)
+    bt = (torch.randperm(B * maxb, device="cuda").int() + 8).view(B, maxb)
+    bt[:, :3] = torch.arange(3, device="cuda", dtype=torch.int32)     # shared 192-token prefix
+    cl = lens.cuda()
+    q = torch.randn(B, (Hq + 2 * Hkv) * D, device="cuda", dtype=torch.bfloat16)
+    order = torch.argsort(lens, descending=True).int().cuda()
+    s = 1 / math.sqrt(D)
+    a = torch.ops.docqa.paged_decode(q, kc, vc, bt, cl, Hq, maxb * BS, s)
+    b = torch.ops.docqa.paged_decode(q, kc, vc, bt, cl, Hq, maxb * BS, s, order)
+    assert torch.equal(a, b)
+    if G != 4:
+        return
+    st = torch.arange(maxb, device="cuda", dtype=torch.int32)
+    pl = torch.tensor([192], device="cuda", dtype=torch.int32)
+    a = torch.ops.docqa.paged_decode_cascade(q, kc, vc, bt, cl, Hq, maxb * BS, s, st, pl, 3)
+    b = torch.ops.docqa.paged_decode_cascade(q, kc, vc, bt, cl, Hq, maxb * BS, s, st, pl, 3, order)
+    assert torch.equal(a, b)
