@@ -86,7 +86,10 @@ __global__ __launch_bounds__(64 * G * WPH) void flash_prefill_kernel(
   // tokens and one long prompt sets the grid to 8, so XCDs 2..7 got only empty tiles and
   // the work ran on two XCDs (4x slower on the bench's real batches).  Heads fastest
   // spreads every tile over all XCDs, and the empty high tiles are dispatched last.
-  const int hb = blockIdx.x, b = blockIdx.y, qt = blockIdx.z;
+  // q-tiles in reverse: under the causal mask the last tile of a long prompt attends to
+  // the most keys, so the heaviest workgroups are dispatched first (LPT) and the empty
+  // tiles past short prompts exit at once
+  const int hb = blockIdx.x, b = blockIdx.y, qt = gridDim.z - 1 - blockIdx.z;
   int seq0, L, kv_beg = 0, pfx_end = 0;
   if constexpr (PFX) {
     seq0 = 0;
