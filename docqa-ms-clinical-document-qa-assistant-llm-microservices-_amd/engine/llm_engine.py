@@ -276,6 +276,12 @@ class LLMEngine:
         if tune and tunable is not None:
             tunable.enable(True)
             tunable.tuning_enable(True)
+            # time candidates on cold weights: a decode step streams every layer's weights
+            # from HBM once (16 GB >> the 256 MB MALL), so solutions must be ranked with
+            # the operands rotated past the caches, not re-read hot
+            rot = int(os.environ.get("DOCQA_TUNE_ROTATE_MB", "512"))
+            if rot > 0 and hasattr(tunable, "set_rotating_buffer_size"):
+                tunable.set_rotating_buffer_size(rot)
         saved = [t.clone() for t in (g.tokens, g.positions, g.context_lens)]
         try:
             s = torch.cuda.Stream()
