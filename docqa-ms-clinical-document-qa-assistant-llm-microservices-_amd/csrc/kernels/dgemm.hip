@@ -26,7 +26,8 @@
 //   * 65..128 rows: each wave owns two 16-row m-tiles over the whole k-block, so every
 //     B fragment read from the LDS ring feeds two MFMAs and the weights still stream from
 //     HBM exactly once (a second pass over 64-row halves would read them twice).
-// Shapes: N % (16 NT) == 0, (K / S) % 512 == 0 (whole 4-stage ring turns), M <= 128.
+// Shapes: N % (16 NT) == 0, (K / S) % 512 == 0 (whole 4-stage ring turns), M <= 128
+// (M <= 192 with 64-row weight tiles: three m-tiles per wave, no fused SwiGLU).
 #include "docqa_common.h"
 #include "docqa_asm.h"
 #include <stdlib.h>
@@ -34,7 +35,7 @@
 using namespace docqa;
 
 namespace {
-constexpr int BN = 64, BKD = 128, NS = 4, MR = 128;   // NS: default ring slots, K granule 4 stages
+constexpr int BN = 64, BKD = 128, NS = 4, MR = 192;   // NS: default ring slots, K granule 4 stages
 constexpr int KSTEPS = BKD / 32;               // 16x16x32 k-steps per stage
 enum { EPI_BF16 = 0, EPI_PARTIAL = 1, EPI_GLU = 2 };
 typedef __attribute__((address_space(3))) void lds_void;
@@ -57,9 +58,14 @@ __device__ __forceinline__ void wait_vm_n(bf16x8 (&x)[SPW]) {
     asm volatile("s_waitcnt vmcnt(%2)" : "+v"(x[0]), "+v"(x[1]) : "i"(N) : "memory");
   else if constexpr (SPW == 4)
     asm volatile("s_waitcnt vmcnt(%4)" : "+v"(x[0]), "+v"(x[1]), "+v"(x[2]), "+v"(x[3]) : "i"(N) : "memory");
-  else
+  else if constexpr (SPW == 8)
     asm volatile("s_waitcnt vmcnt(%8)" : "+v"(x[0]), "+v"(x[1]), "+v"(x[2]), "+v"(x[3]), "+v"(x[4]), "+v"(x[5]),
                  "+v"(x[6]), "+v"(x[7]) : "i"(N) : "memory");
+  else {
+    static_assert(SPW == 12, "X fragment sets of 1, 2, 4, 8 or 12");
+    asm volatile("s_waitcnt vmcnt(%12)" : "+v"(x[0]), "+v"(x[1]), "+v"(x[2]), "+v"(x[3]), "+v"(x[4]), "+v"(x[5]),
+                 "+v"(x[6]), "+v"(x[7]), "+v"(x[8]), "+v"(x[9]), "+v"(x[10]), "+v"(x[11]) : "i"(N) : "memory");
+  }
 }
 
 // keep x's registers allocated up to this point (for loads that are drained, never read)
@@ -97,7 +103,7 @@ __global__ __launch_bounds__(256) void dgemm_kernel(const uint16_t* __restrict__
   constexpr int XR = MPW * SPW;                  // X fragments per wave per stage
   constexpr int STAGE = NT * 16 * BKD;           // elements of one W stage (NT x 4 KB)
   static_assert(NSR >= 4, "ring needs >= 4 slots");
-  static_assert(MT <= 4 || MT == 8, "MT in {1, 2, 4, 8}");
+  static_assert(MT <= 4 || MT == 8 || MT == 12, "MT in {1, 2, 4, 8, 12}");
   __shared__ __attribute__((aligned(16))) uint16_t sw[NSR * STAGE];   // W ring
   // XCD-aware split-K placement: workgroups are dealt to the 8 XCDs round-robin by linear
   // id, so with the plain (tile, slice) grid every XCD sees every K slice and its 4 MB L2
@@ -331,11 +337,17 @@ static void launch_mt(int mt, dim3 grid, hipStream_t s, const uint16_t* x, const
   if (mt == 1) dgemm_kernel<EPI, 1, NT, NSR><<<grid, 256, 0, s>>>(x, w, y, p, M, N, K, Ks, xr);
   else if (mt == 2) dgemm_kernel<EPI, 2, NT, NSR><<<grid, 256, 0, s>>>(x, w, y, p, M, N, K, Ks, xr);
   else if (mt <= 4) dgemm_kernel<EPI, 4, NT, NSR><<<grid, 256, 0, s>>>(x, w, y, p, M, N, K, Ks, xr);
-  else if constexpr (NSR == 4) {
-    if (xa_knob() == 3) dgemm_kernel<EPI, 8, NT, NSR, 3><<<grid, 256, 0, s>>>(x, w, y, p, M, N, K, Ks, xr);
-    else dgemm_kernel<EPI, 8, NT, NSR><<<grid, 256, 0, s>>>(x, w, y, p, M, N, K, Ks, xr);
-  } else {
-    dgemm_kernel<EPI, 8, NT, NSR><<<grid, 256, 0, s>>>(x, w, y, p, M, N, K, Ks, xr);
+  else if (mt <= 8) {
+    if constexpr (NSR == 4) {
+      if (xa_knob() == 3) dgemm_kernel<EPI, 8, NT, NSR, 3><<<grid, 256, 0, s>>>(x, w, y, p, M, N, K, Ks, xr);
+      else dgemm_kernel<EPI, 8, NT, NSR><<<grid, 256, 0, s>>>(x, w, y, p, M, N, K, Ks, xr);
+    } else {
+      dgemm_kernel<EPI, 8, NT, NSR><<<grid, 256, 0, s>>>(x, w, y, p, M, N, K, Ks, xr);
+    }
+  } else if constexpr (NT <= 4 && EPI != EPI_GLU) {
+    // 129-192 rows: three m-tiles per wave (the 128-row 128-wide tile would not fit the
+    // register file at three m-tiles)
+    dgemm_kernel<EPI, 12, NT, NSR><<<grid, 256, 0, s>>>(x, w, y, p, M, N, K, Ks, xr);
   }
 }
 
@@ -368,6 +380,7 @@ int docqa_dgemm_partial(const void* X, const void* W, float* P, int M, int N, in
                         int tile_rows, hipStream_t s) {
   if (M == 0) return 0;
   if (!P || (tile_rows != 64 && tile_rows != 128) || !shape_ok(M, N, K, S, tile_rows)) return -1;
+  if (tile_rows == 128 && M > 128) return -1;   // 12 m-tiles: 64-row weight tiles only
   const int mt = (M + 15) / 16;
   const uint16_t* x = (const uint16_t*)X;
   const uint16_t* w = (const uint16_t*)W;
@@ -390,6 +403,7 @@ int docqa_dgemm_partial(const void* X, const void* W, float* P, int M, int N, in
 // Y[M, N/2] = silu(gate) * up for the 8-interleaved gate|up weight W [N, K] (N = 2 I)
 int docqa_dgemm_glu(const void* X, const void* W, void* Y, int M, int N, int K, hipStream_t s) {
   if (M == 0) return 0;
+  if (M > 128) return -1;
   const int mt = (M + 15) / 16;
   const uint16_t* x = (const uint16_t*)X;
   const uint16_t* w = (const uint16_t*)W;

@@ -178,8 +178,15 @@ def decode_plan(M: int, N: int, K: int) -> tuple[int, int]:
     64-row tiles with the smallest split giving >= 192 workgroups; at 65-128 rows 128-row
     tiles (X re-read from L2 half as often) where such a split exists (QKV S=4: 21.9 us vs
     hipBLASLt 25.2 at M=128; O S=8: 17.2 vs 24.4), else 64-row tiles (down S=4: 40.7 vs 75.1)."""
-    if M > 128 or N % 64 or N >= 65536 or (N >= 16384 and M > 32):
+    if M > 192 or N % 64 or N >= 65536 or (N >= 16384 and M > 32):
         return 0, 64
+    if M > 128:
+        # 129-192 rows (three m-tiles per wave, 64-row tiles only): only where a split gives
+        # a full round of 256 workgroups -- O 21.8 us vs tuned hipBLASLt 23.9, down 54.2 vs
+        # 65.3 at M=192; QKV (192 workgroups at S=2: 33.7 vs 27.3) stays on hipBLASLt
+        # (profiles/r1_dgemm_m192_sweep.log)
+        S = _splits_for(N, K, 64)
+        return (S, 64) if S and (N // 64) * S >= 256 else (0, 64)
     if M <= 64:
         return _splits_for(N, K, 64), 64
     S64 = _splits_for(N, K, 64)

@@ -27,7 +27,9 @@ def main():
             it = iter(range(1 << 30))
             row = {"proj": name, "M": M}
             row["hipblaslt_us"] = round(timeit(lambda: F.linear(x, ws[next(it) % copies]), iters=4 * copies), 1)
-            if name == "gate_up":
+            if name == "gate_up" and M > 128:
+                pass
+            elif name == "gate_up":
                 y = nat.dgemm_glu(x, ws[0])
                 gu = ref.bfloat16()
                 from docqa_amd.ops import reference as R
@@ -39,7 +41,7 @@ def main():
             else:
                 for tr in (64, 128):
                     for S in (1, 2, 4, 8):
-                        if K % S or (K // S) % 512 or N % tr:
+                        if K % S or (K // S) % 512 or N % tr or (M > 128 and tr == 128):
                             continue
                         P = nat.dgemm_partial(x, ws[0], S, tr)
                         err = (P.sum(0) - ref).abs().max().item()

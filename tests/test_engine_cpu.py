@@ -113,6 +113,9 @@ def test_splitk_reference_ops_cpu():
     assert ops.decode_plan(128, 6144, 4096) == (4, 128) and ops.decode_plan(128, 4096, 4096) == (4, 64)
     assert ops.decode_plan(128, 4096, 14336) == (4, 64) and ops.decode_plan(100, 28672, 4096)[0] == 0
     assert ops.decode_plan(129, 6144, 4096)[0] == 0
+    # 129-192 rows: O / down on 64-row tiles x 4 slabs, QKV / gate|up / LM head on hipBLASLt
+    assert ops.decode_plan(192, 4096, 4096) == (4, 64) and ops.decode_plan(160, 4096, 14336) == (4, 64)
+    assert ops.decode_plan(192, 28672, 4096)[0] == 0 and ops.decode_plan(193, 4096, 4096)[0] == 0
     r1 = torch.randn(5, 256).bfloat16()
     r2 = r1.clone()
     g = torch.ones(256).bfloat16()

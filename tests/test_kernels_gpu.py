@@ -244,7 +244,7 @@ def test_gemm_asymmetric_identity(native):
     assert torch.equal(o[:64, :], w.float()[:, :64].T[:64, :])
 
 
-@pytest.mark.parametrize("M", [1, 5, 16, 31, 64, 65, 100, 128])
+@pytest.mark.parametrize("M", [1, 5, 16, 31, 64, 65, 100, 128, 129, 192])
 @pytest.mark.parametrize("N,K,S", [(6144, 4096, 0), (4096, 4096, 0), (4096, 14336, 0), (28672, 4096, 0),
                                    (512, 1024, 1), (512, 1024, 2), (640, 3584, 7)])
 def test_dgemm(native, M, N, K, S):
@@ -257,7 +257,8 @@ def test_dgemm(native, M, N, K, S):
         _close(o1, o2, 2e-2, 1e-2)
 
 
-@pytest.mark.parametrize("S,M,tile", [(1, 37, 64), (4, 37, 64), (4, 100, 128), (8, 128, 128), (2, 128, 64)])
+@pytest.mark.parametrize("S,M,tile", [(1, 37, 64), (4, 37, 64), (4, 100, 128), (8, 128, 128), (2, 128, 64),
+                                     (4, 160, 64), (4, 192, 64)])
 def test_splitk_fused_consumers(native, S, M, tile):
     """dgemm_partial + add_rmsnorm_splitk / rope_cache_splitk == reference on bf16(sum P)."""
     from docqa_amd.ops import reference as R
@@ -280,9 +281,10 @@ def test_splitk_fused_consumers(native, S, M, tile):
     Pq = torch.randn(S, T, (Hq + 2 * Hkv) * D, device="cuda")
     cs = R.rope_cos_sin(1024, D, 500000.0, "cuda")
     pos = torch.randint(0, 1000, (T,), device="cuda", dtype=torch.int32)
-    slots = torch.randperm(8 * BS, device="cuda")[:T].int()
+    nblk = max(8, (T + BS - 1) // BS + 1)
+    slots = torch.randperm(nblk * BS, device="cuda")[:T].int()
     slots[3] = -1
-    kc1 = torch.zeros(8, Hkv, BS, D, device="cuda", dtype=torch.bfloat16)
+    kc1 = torch.zeros(nblk, Hkv, BS, D, device="cuda", dtype=torch.bfloat16)
     vc1 = torch.zeros_like(kc1)
     kc2, vc2 = kc1.clone(), vc1.clone()
     q1 = torch.ops.docqa.rope_cache_splitk(Pq, pos, cs, slots, kc1, vc1, Hq, Hkv, D)
