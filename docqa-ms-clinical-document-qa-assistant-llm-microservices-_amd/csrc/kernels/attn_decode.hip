@@ -65,6 +65,17 @@ static int mfma_nsr() {
 // ahead; the MFMA kernel wins on long contexts (5.2 vs 4.6 TB/s at 2k tokens) and its
 // per-token cost does not grow with G, so it is the default for G >= 8 (Llama-3-70B).
 // DOCQA_DECODE_MFMA=1 / 0 forces it on / off.
+// VALU ring depth: 3 (3 workgroups/CU, default) or 4 (2 workgroups/CU).  LPT-ordered
+// mixed batches, bench_decode_attn.py: B=192 ctx 352 55.4 vs 63.3 us, B=192 ctx 640
+// 92.4 vs 102.6, B=128 ctx 352 43.3 vs 45.4 (profiles/r1_decode_ring_nsr.log)
+static int ring_nsr() {
+  static const int v = [] {
+    const char* e = getenv("DOCQA_RING_NSR");
+    return e ? atoi(e) : 3;
+  }();
+  return v == 4 ? 4 : 3;
+}
+
 static bool mfma_decode_on(int G) {
   static const int v = [] {
     const char* e = getenv("DOCQA_DECODE_MFMA");
@@ -371,17 +382,26 @@ __device__ __forceinline__ void rope8(float (&x)[8], int c, const float* cs) {
   }
 }
 
-template <int G, bool DIRECT, bool FUSED = false>
+// NSR: ring slots.  4 (64 KB + 8 KB merge scratch: 2 workgroups/CU) or 3 (48 KB with the
+// merge scratch aliased onto the drained ring: 3 workgroups/CU -- the same bytes in flight
+// per CU spread over more workgroups, so one workgroup's prologue / epilogue overlaps
+// the others' streaming and a batch-192 step needs two launch rounds instead of three).
+template <int G, bool DIRECT, bool FUSED = false, int NSR = 4>
 __global__ __launch_bounds__(256) void paged_decode_ring_kernel(
     const uint16_t* __restrict__ q, int q_stride, uint16_t* __restrict__ k_cache,
     uint16_t* __restrict__ v_cache, const int* __restrict__ block_tables, int maxb,
     const int* __restrict__ context_lens, float* __restrict__ tmp_out,
     float* __restrict__ tmp_ml, int Hkv, int max_parts, float scale,
     uint16_t* __restrict__ out, int out_stride, FusedQKV fz, CascadeIn ci) {
-  constexpr int D = 128, TT = 32, NSR = 4, U = 2;
+  constexpr int D = 128, TT = 32, U = 2;
+  static_assert(NSR == 3 || NSR == 4, "ring of 3 or 4 slots");
   constexpr int TILE = TT * D;                   // elements of one K (or V) tile: 8 KB
-  __shared__ __attribute__((aligned(16))) uint16_t ring[NSR * 2 * TILE];   // 64 KB
-  __shared__ float s_acc[4][G][D];
+  constexpr bool ALIAS = NSR == 3;               // merge scratch on the drained ring
+  static_assert(!ALIAS || 4 * G * D * 4 <= NSR * 2 * TILE * 2, "scratch fits the ring");
+  __shared__ __attribute__((aligned(16))) uint16_t ring[NSR * 2 * TILE];   // 48 / 64 KB
+  __shared__ float s_acc_own[ALIAS ? 1 : 4][ALIAS ? 1 : G][ALIAS ? 1 : D];
+  float (*s_acc)[G][D] = ALIAS ? reinterpret_cast<float (*)[G][D]>(ring)
+                               : reinterpret_cast<float (*)[G][D]>(&s_acc_own[0][0][0]);
   __shared__ float s_m[4][G], s_l[4][G];
   __shared__ int s_bt[256];                      // block ids of the slice (<= 16k tokens)
 
@@ -461,7 +481,7 @@ __global__ __launch_bounds__(256) void paged_decode_ring_kernel(
   if (ntile > 0) {
     stage(0);
     stage(1);
-    stage(2);
+    if constexpr (NSR == 4) stage(2);
   }
 
   uint4 knew = make_uint4(0, 0, 0, 0), vnew = make_uint4(0, 0, 0, 0);
@@ -499,9 +519,9 @@ __global__ __launch_bounds__(256) void paged_decode_ring_kernel(
   }
 
   for (int i = 0; i < ntile; ++i) {
-    wait_vmcnt<8>();                             // tiles i+1, i+2 (4 DMAs each) may fly
+    wait_vmcnt<4 * (NSR - 2)>();                 // the next NSR-2 tiles (4 DMAs each) may fly
     ring_barrier();                              // tile i visible; slot (i-1) % NSR free
-    stage(i + 3);
+    stage(i + NSR - 1);
     const uint16_t* kt = ring + (i % NSR) * 2 * TILE;
     const uint16_t* vt = kt + TILE;
     uint4 kr[U], vr[U];
@@ -521,6 +541,7 @@ __global__ __launch_bounds__(256) void paged_decode_ring_kernel(
     attend_rows<G, 1>(kr1, vr1, ok1, qv, qs, m, l, acc);
   }
   wait_vmcnt<0>();                               // drain the clamped tail DMAs
+  if constexpr (ALIAS) __syncthreads();          // every wave done with the ring
 
   finish_partition<G, D, DIRECT>(m, l, acc, s_acc, s_m, s_l, tid, wave, tg, chunk, b, kvh, part,
                                  Hkv, max_parts, tmp_out, tmp_ml, out, out_stride, ci);
@@ -880,7 +901,12 @@ int docqa_paged_decode(const void* q, int q_stride, const void* k_cache, const v
   if (ring_env && BS == 64 && maxb <= 256) {
 #define DRING(GG)                                                                             \
     do {                                                                                      \
-      if (direct)                                                                             \
+      if (direct && ring_nsr() == 3)                                                          \
+        paged_decode_ring_kernel<GG, true, false, 3><<<grid, 256, 0, s>>>(                    \
+            (const uint16_t*)q, q_stride, (uint16_t*)k_cache, (uint16_t*)v_cache,             \
+            block_tables, maxb, context_lens, tmp_out, tmp_ml, Hkv, max_parts, scale,         \
+            (uint16_t*)out, out_stride, FusedQKV{}, oi);                                      \
+      else if (direct)                                                                        \
         paged_decode_ring_kernel<GG, true><<<grid, 256, 0, s>>>(                              \
             (const uint16_t*)q, q_stride, (uint16_t*)k_cache, (uint16_t*)v_cache,             \
             block_tables, maxb, context_lens, tmp_out, tmp_ml, Hkv, max_parts, scale,         \
@@ -1024,7 +1050,11 @@ int docqa_paged_decode_cascade(const void* q, int q_stride, void* k_cache, void*
       paged_decode_reduce<128><<<dim3(Hq, B), 128, 0, s>>>(tmp_out, tmp_ml, context_lens, (uint16_t*)out,
                                                            out_stride, Hq, max_parts, ci);
     }
-  } else if (max_parts == 1)
+  } else if (max_parts == 1 && ring_nsr() == 3)
+    paged_decode_ring_kernel<4, true, false, 3><<<grid, 256, 0, s>>>(
+        (const uint16_t*)q, q_stride, (uint16_t*)k_cache, (uint16_t*)v_cache, block_tables, maxb,
+        context_lens, tmp_out, tmp_ml, Hkv, max_parts, scale, (uint16_t*)out, out_stride, FusedQKV{}, ci);
+  else if (max_parts == 1)
     paged_decode_ring_kernel<4, true><<<grid, 256, 0, s>>>(
         (const uint16_t*)q, q_stride, (uint16_t*)k_cache, (uint16_t*)v_cache, block_tables, maxb,
         context_lens, tmp_out, tmp_ml, Hkv, max_parts, scale, (uint16_t*)out, out_stride, FusedQKV{}, ci);
