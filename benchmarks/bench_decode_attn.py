@@ -25,7 +25,7 @@ def main():
     assert ops.load_native()
     nat = torch.ops.docqa
     res = []
-    Hq, Hkv, D, BS = 32, 8, 128, 64
+    Hq, Hkv, D, BS = int(os.environ.get("HQ", "32")), 8, 128, 64   # HQ=64: Llama-3-70B (G=8)
     shapes = [(64, 640), (64, 1024), (32, 640), (8, 1024), (1, 4096)]
     if os.environ.get("SHAPES"):
         shapes = [tuple(int(v) for v in x.split("x")) for x in os.environ["SHAPES"].split(",")]
