@@ -73,7 +73,7 @@ static int ring_nsr() {
     const char* e = getenv("DOCQA_RING_NSR");
     return e ? atoi(e) : 3;
   }();
-  return v == 4 ? 4 : 3;
+  return v == 4 ? 4 : v == 2 ? 2 : 3;
 }
 
 static bool mfma_decode_on(int G) {
@@ -394,9 +394,9 @@ __global__ __launch_bounds__(256) void paged_decode_ring_kernel(
     float* __restrict__ tmp_ml, int Hkv, int max_parts, float scale,
     uint16_t* __restrict__ out, int out_stride, FusedQKV fz, CascadeIn ci) {
   constexpr int D = 128, TT = 32, U = 2;
-  static_assert(NSR == 3 || NSR == 4, "ring of 3 or 4 slots");
+  static_assert(NSR >= 2 && NSR <= 4, "ring of 2..4 slots");
   constexpr int TILE = TT * D;                   // elements of one K (or V) tile: 8 KB
-  constexpr bool ALIAS = NSR == 3;               // merge scratch on the drained ring
+  constexpr bool ALIAS = NSR <= 3;               // merge scratch on the drained ring
   static_assert(!ALIAS || 4 * G * D * 4 <= NSR * 2 * TILE * 2, "scratch fits the ring");
   __shared__ __attribute__((aligned(16))) uint16_t ring[NSR * 2 * TILE];   // 48 / 64 KB
   __shared__ float s_acc_own[ALIAS ? 1 : 4][ALIAS ? 1 : G][ALIAS ? 1 : D];
@@ -480,7 +480,7 @@ __global__ __launch_bounds__(256) void paged_decode_ring_kernel(
   };
   if (ntile > 0) {
     stage(0);
-    stage(1);
+    if constexpr (NSR >= 3) stage(1);
     if constexpr (NSR == 4) stage(2);
   }
 
@@ -901,7 +901,12 @@ int docqa_paged_decode(const void* q, int q_stride, const void* k_cache, const v
   if (ring_env && BS == 64 && maxb <= 256) {
 #define DRING(GG)                                                                             \
     do {                                                                                      \
-      if (direct && ring_nsr() == 3)                                                          \
+      if (direct && ring_nsr() == 2)                                                          \
+        paged_decode_ring_kernel<GG, true, false, 2><<<grid, 256, 0, s>>>(                    \
+            (const uint16_t*)q, q_stride, (uint16_t*)k_cache, (uint16_t*)v_cache,             \
+            block_tables, maxb, context_lens, tmp_out, tmp_ml, Hkv, max_parts, scale,         \
+            (uint16_t*)out, out_stride, FusedQKV{}, oi);                                      \
+      else if (direct && ring_nsr() == 3)                                                     \
         paged_decode_ring_kernel<GG, true, false, 3><<<grid, 256, 0, s>>>(                    \
             (const uint16_t*)q, q_stride, (uint16_t*)k_cache, (uint16_t*)v_cache,             \
             block_tables, maxb, context_lens, tmp_out, tmp_ml, Hkv, max_parts, scale,         \
@@ -1050,7 +1055,11 @@ int docqa_paged_decode_cascade(const void* q, int q_stride, void* k_cache, void*
       paged_decode_reduce<128><<<dim3(Hq, B), 128, 0, s>>>(tmp_out, tmp_ml, context_lens, (uint16_t*)out,
                                                            out_stride, Hq, max_parts, ci);
     }
-  } else if (max_parts == 1 && ring_nsr() == 3)
+  } else if (max_parts == 1 && ring_nsr() == 2)
+    paged_decode_ring_kernel<4, true, false, 2><<<grid, 256, 0, s>>>(
+        (const uint16_t*)q, q_stride, (uint16_t*)k_cache, (uint16_t*)v_cache, block_tables, maxb,
+        context_lens, tmp_out, tmp_ml, Hkv, max_parts, scale, (uint16_t*)out, out_stride, FusedQKV{}, ci);
+  else if (max_parts == 1 && ring_nsr() == 3)
     paged_decode_ring_kernel<4, true, false, 3><<<grid, 256, 0, s>>>(
         (const uint16_t*)q, q_stride, (uint16_t*)k_cache, (uint16_t*)v_cache, block_tables, maxb,
         context_lens, tmp_out, tmp_ml, Hkv, max_parts, scale, (uint16_t*)out, out_stride, FusedQKV{}, ci);
