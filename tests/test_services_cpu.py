@@ -270,6 +270,30 @@ def test_stack_persistence_resume(stack, tmp_path):
     assert idx.ntotal == len(meta) == stack.indexer.index.ntotal
 
 
+def test_indexer_add_to_index_and_empty(tmp_path):
+    """semantic-indexer/tests/test_indexer.py:34-59: one add creates the index, embeds the
+    text once and records {text_content, source}; blank text adds nothing."""
+    from docqa_amd.config import Settings
+    from docqa_amd.models.bert import BertConfig, BertEncoder
+    from docqa_amd.services.indexer import SemanticIndexer
+    from docqa_amd.text.tokenizer import WordPieceTokenizer
+
+    st = Settings()
+    st.index_dir = str(tmp_path)
+    enc = BertEncoder(BertConfig.preset("tiny-bert"), device="cpu")
+    idx = SemanticIndexer(enc, WordPieceTokenizer(), st, device="cpu")
+    assert idx.index is None
+    assert idx.add_to_index("   ", "source") is False
+    assert idx.metadata == [] and idx.index is None
+    assert idx.add_to_index("Test sentence", "test_source.txt") is True
+    assert idx.index is not None and idx.index.ntotal == 1
+    assert len(idx.metadata) == 1
+    assert idx.metadata[0]["text_content"] == "Test sentence"
+    assert idx.metadata[0]["source"] == "test_source.txt"
+    hits = idx.search("Test sentence", k=1)
+    assert hits and hits[0]["source"] == "test_source.txt"
+
+
 def test_indexer_group_commit_burst(tmp_path, monkeypatch):
     """A burst of clean documents is embedded, snapshotted and acked in groups (fewer
     index snapshots than documents); every document still ends INDEXED, chunked at 500
