@@ -419,7 +419,7 @@ at::Tensor dgemm_partial(const at::Tensor& x, const at::Tensor& w, int64_t split
   const int K = x.size(-1), N = w.size(0);
   TORCH_CHECK(w.size(1) == K, "dgemm_partial: K mismatch");
   const int M = x.numel() / K;
-  TORCH_CHECK(M <= 192 && splits >= 1 && (M <= 128 || tile_rows == 64), "dgemm_partial: at most 128 rows (192 with 64-row tiles), splits >= 1");
+  TORCH_CHECK(M <= 192 && splits >= 1, "dgemm_partial: at most 192 rows, splits >= 1");
   c10::DeviceGuard g(x.device());
   auto part = at::empty({splits, M, N}, x.options().dtype(at::kFloat));
   CHECK_RC(docqa_dgemm_partial(x.data_ptr(), w.data_ptr(), part.data_ptr<float>(), M, N, K, (int)splits,

@@ -344,9 +344,8 @@ static void launch_mt(int mt, dim3 grid, hipStream_t s, const uint16_t* x, const
     } else {
       dgemm_kernel<EPI, 8, NT, NSR><<<grid, 256, 0, s>>>(x, w, y, p, M, N, K, Ks, xr);
     }
-  } else if constexpr (NT <= 4 && EPI != EPI_GLU) {
-    // 129-192 rows: three m-tiles per wave (the 128-row 128-wide tile would not fit the
-    // register file at three m-tiles)
+  } else if constexpr (NT <= 8 && EPI != EPI_GLU) {
+    // 129-192 rows: three m-tiles per wave
     dgemm_kernel<EPI, 12, NT, NSR><<<grid, 256, 0, s>>>(x, w, y, p, M, N, K, Ks, xr);
   }
 }
@@ -380,7 +379,6 @@ int docqa_dgemm_partial(const void* X, const void* W, float* P, int M, int N, in
                         int tile_rows, hipStream_t s) {
   if (M == 0) return 0;
   if (!P || (tile_rows != 64 && tile_rows != 128) || !shape_ok(M, N, K, S, tile_rows)) return -1;
-  if (tile_rows == 128 && M > 128) return -1;   // 12 m-tiles: 64-row weight tiles only
   const int mt = (M + 15) / 16;
   const uint16_t* x = (const uint16_t*)X;
   const uint16_t* w = (const uint16_t*)W;
