@@ -18,7 +18,32 @@ hipStream_t stream() { return c10::hip::getCurrentHIPStream().stream(); }
 #define CHECK_BF16(t) TORCH_CHECK((t).scalar_type() == at::kBFloat16, #t " must be bfloat16")
 #define CHECK_I32(t) TORCH_CHECK((t).scalar_type() == at::kInt, #t " must be int32")
 #define CHECK_CONTIG(t) TORCH_CHECK((t).is_contiguous(), #t " must be contiguous")
-#define CHECK_RC(rc, name) TORCH_CHECK((rc) == 0, "docqa kernel " name " failed with code ", (rc))
+// DOCQA_KERNEL_DEBUG=1: synchronous kernel checking (the HIP_LAUNCH_BLOCKING of this
+// extension): after every op that is not being graph-captured, the stream
+// is synchronised and any asynchronous fault is reported with the op's name -- a
+// faulting kernel is named by the op that launched it, not by a later unrelated sync.
+static bool kernel_debug() {
+  static const bool on = [] {
+    const char* e = getenv("DOCQA_KERNEL_DEBUG");
+    return e && atoi(e) != 0;
+  }();
+  return on;
+}
+
+static void debug_sync(const char* name) {
+  hipStream_t s = stream();
+  hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+  if (hipStreamIsCapturing(s, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone) return;
+  const hipError_t e = hipStreamSynchronize(s);
+  TORCH_CHECK(e == hipSuccess, "docqa kernel ", name, " faulted (DOCQA_KERNEL_DEBUG): ", hipGetErrorString(e));
+}
+
+#define CHECK_RC(rc, name)                                                                 \
+  do {                                                                                     \
+    const int rc__ = (rc);                                                                 \
+    TORCH_CHECK(rc__ == 0, "docqa kernel " name " failed with code ", rc__);               \
+    if (kernel_debug()) debug_sync(name);                                                  \
+  } while (0)
 
 at::Tensor rmsnorm(const at::Tensor& x, const at::Tensor& w, double eps) {
   CHECK_GPU(x); CHECK_BF16(x); CHECK_BF16(w); CHECK_CONTIG(x); CHECK_CONTIG(w);

@@ -553,3 +553,35 @@ def test_decode_dispatch_order_is_result_invariant(native, G):
     a = torch.ops.docqa.paged_decode_cascade(q, kc, vc, bt, cl, Hq, maxb * BS, s, st, pl, 3)
     b = torch.ops.docqa.paged_decode_cascade(q, kc, vc, bt, cl, Hq, maxb * BS, s, st, pl, 3, order)
     assert torch.equal(a, b)
+
+
+def test_kernel_debug_mode_syncs_outside_capture_only(tmp_path):
+    """DOCQA_KERNEL_DEBUG=1 (synchronous fault checking per op) runs eager ops and leaves
+    HIP-graph capture alone (a sync inside a capture would invalidate it)."""
+    import os
+    import subprocess
+    import sys
+
+    code = """
+import torch
+from docqa_amd import ops
+assert ops.load_native()
+x = torch.randn(64, 4096, device='cuda', dtype=torch.bfloat16)
+w = (torch.rand(4096, device='cuda') + 0.5).bfloat16()
+y = ops.rmsnorm(x, w, 1e-5)
+torch.cuda.synchronize()
+g = torch.cuda.CUDAGraph()
+s = torch.cuda.Stream()
+with torch.cuda.stream(s):
+    ops.rmsnorm(x, w, 1e-5)
+torch.cuda.synchronize()
+with torch.cuda.graph(g):
+    z = ops.rmsnorm(x, w, 1e-5)
+g.replay()
+torch.cuda.synchronize()
+assert torch.equal(y, z)
+print('debug-ok')
+"""
+    env = dict(os.environ, DOCQA_KERNEL_DEBUG="1")
+    r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0 and "debug-ok" in r.stdout, r.stderr[-2000:]
