@@ -124,15 +124,11 @@ __device__ __forceinline__ void attend_rows(const uint4 (&kr)[U], const uint4 (&
       float mx = m[g];
 #pragma unroll
       for (int u = 0; u < U; ++u) mx = fmaxf(mx, s[u][g]);
-      // rescale only where the running max grew (corr would be exactly 1 elsewhere): once
-      // the max settles, whole waves skip the 10 VALU ops per head (bit-identical result)
-      if (mx > m[g]) {
-        const float corr = exp2f(m[g] - mx);
-        m[g] = mx;
-        l[g] *= corr;
+      const float corr = exp2f(m[g] - mx);
+      m[g] = mx;
+      l[g] *= corr;
 #pragma unroll
-        for (int j = 0; j < 8; ++j) acc[g][j] *= corr;
-      }
+      for (int j = 0; j < 8; ++j) acc[g][j] *= corr;
     }
 #pragma unroll
     for (int u = 0; u < U; ++u) {
