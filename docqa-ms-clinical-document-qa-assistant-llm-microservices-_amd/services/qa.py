@@ -9,11 +9,12 @@ Contract (llm-qa/main.py:108-126 and synthese-comparative/core/llm_client.py:42-
   GET  /metrics             Prometheus text (requests, batch sizes, stage latencies)
 
 Serving model: the reference answers one blocking request at a time per process
-(llm-qa/main.py:111-117).  Here (``DOCQA_SERVING=continuous``, default) a scheduler thread
-owns the GPU: between two decode steps it takes every request that arrived, embeds and
-searches them as one batch, and hands their prompts to the continuous-batching engine
-(engine/scheduler.py), where they join the running decode batch at the next step and
-leave it when they finish -- no request waits for another batch to drain.
+(llm-qa/main.py:111-117).  Here (``DOCQA_SERVING=continuous``, default) a prep thread
+takes every request that arrived, embeds and searches them as one batch on a side HIP
+stream and hands their prompts to the continuous-batching engine (engine/scheduler.py),
+whose scheduler thread admits them into the running decode batch at the next step; they
+leave it when they finish -- no request waits for another batch to drain, and question
+embedding overlaps the decode steps instead of pausing them.
 ``DOCQA_SERVING=batch`` keeps the static dynamic batcher: drain the queue every
 ``BATCH_WINDOW_MS`` (or at ``MAX_BATCH``) and run the batch from prefill to last token.
 """
@@ -118,8 +119,11 @@ def _maybe_exit_on_device_error(e: Exception) -> None:
 
 
 class ContinuousBatcher:
-    """Scheduler thread: admit arrivals (batched embed + kNN + prompt assembly), then one
-    continuous-batching engine step; repeat."""
+    """Two threads: the prep thread takes every request that arrived, embeds and searches
+    them as one batch on a side HIP stream and submits their prompts to the
+    continuous-batching engine; the scheduler thread only runs engine steps (admission
+    prefills + decode).  Question embedding therefore never stalls the decode loop -- with
+    the embed inline, every arrival burst under load cost the running batch a step."""
 
     def __init__(self, pipeline, settings: Settings, metrics: Metrics):
         from ..engine.scheduler import ContinuousEngine
@@ -130,7 +134,9 @@ class ContinuousBatcher:
         self.engine = ContinuousEngine(pipeline.engine, max_running=settings.max_batch)
         self.q: queue.Queue = queue.Queue()
         self._stop = threading.Event()
+        self._prep = threading.Thread(target=self._prep_loop, name="qa-prep", daemon=True)
         self._t = threading.Thread(target=self._loop, name="qa-scheduler", daemon=True)
+        self._prep.start()
         self._t.start()
 
     def submit(self, kind: str, payload: str) -> cf.Future:
@@ -145,7 +151,7 @@ class ContinuousBatcher:
     def _drain(self) -> list:
         items = []
         try:
-            items.append(self.q.get(timeout=0 if self.engine.has_work() else 0.1))
+            items.append(self.q.get(timeout=0.1))
         except queue.Empty:
             return items
         while True:
@@ -154,37 +160,46 @@ class ContinuousBatcher:
             except queue.Empty:
                 return items
 
-    def _loop(self) -> None:
+    def _prep_loop(self) -> None:
         import torch
 
+        cuda = self.pipe.engine.device.type == "cuda"
+        side = torch.cuda.Stream() if cuda else None
+        while not self._stop.is_set():
+            items = self._drain()
+            if not items:
+                continue
+            try:
+                with torch.inference_mode(), (torch.cuda.stream(side) if cuda else _nullctx()):
+                    self._admit(items)
+            except Exception as e:  # noqa: BLE001
+                for it in items:
+                    if not it[2].done():
+                        it[2].set_exception(e)
+
+    def _loop(self) -> None:
         from ..parallel.health import Watchdog
 
         # DOCQA_WATCHDOG_S=<s>: exit (for a supervised restart) when a step hangs that long
         wd = Watchdog.from_env()
+        eng = self.engine
         while not self._stop.is_set():
-            items = self._drain()
-            if items:
+            if not eng.has_work():
                 if wd:
-                    wd.busy()
-                try:
-                    with torch.inference_mode():
-                        self._admit(items)
-                except Exception as e:  # noqa: BLE001
-                    for it in items:
-                        if not it[2].done():
-                            it[2].set_exception(e)
-            if self.engine.has_work():
-                if wd:
-                    wd.busy()
-                try:
-                    self.engine.step()
-                except Exception as e:  # noqa: BLE001
-                    self.engine._fail_all(e)
-                    _maybe_exit_on_device_error(e)
-                if wd:
-                    wd.beat()
-            elif wd:
-                wd.idle()
+                    wd.idle()
+                with eng._cv:
+                    if not eng.has_work():
+                        eng._cv.wait(timeout=0.05)
+                continue
+            if wd:
+                wd.busy()
+            try:
+                eng.step()
+            except Exception as e:  # noqa: BLE001
+                eng._fail_all(e)
+                _maybe_exit_on_device_error(e)
+            if wd:
+                wd.beat()
         if wd:
             wd.stop()
 
@@ -227,7 +242,16 @@ class ContinuousBatcher:
 
     def stop(self) -> None:
         self._stop.set()
+        self._prep.join(timeout=60)
         self._t.join(timeout=60)
+
+
+class _nullctx:
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        return False
 
 
 def create_app(pipeline=None, settings: Settings | None = None) -> FastAPI:
