@@ -16,8 +16,11 @@ from docqa_amd import ops
 def main():
     assert ops.load_native()
     nat = torch.ops.docqa
-    Ms = [int(m) for m in (sys.argv[1].split(",") if len(sys.argv) > 1 else ["64", "96", "128"])]
-    for (name, N, K) in [("qkv", 6144, 4096), ("o", 4096, 4096), ("down", 4096, 14336), ("gate_up", 28672, 4096)]:
+    Ms = [int(m) for m in (sys.argv[1].split(",") if len(sys.argv) > 1 and sys.argv[1][0].isdigit() else ["64", "96", "128"])]
+    projs = [("qkv", 6144, 4096), ("o", 4096, 4096), ("down", 4096, 14336), ("gate_up", 28672, 4096)]
+    if "--lm-head" in sys.argv:
+        projs = [("lm_head", 128256, 4096)]
+    for (name, N, K) in projs:
         nb = N * K * 2
         copies = max(2, (1 << 30) // nb + 1)
         ws = [(torch.randn(N, K, device="cuda") / K ** 0.5).bfloat16() for _ in range(copies)]
@@ -40,7 +43,7 @@ def main():
                                                         iters=4 * copies), 1)
             else:
                 for tr in (64, 128):
-                    for S in (1, 2, 4, 7, 8):
+                    for S in ((1,) if name == "lm_head" else (1, 2, 4, 7, 8)):
                         if K % S or (K // S) % 512 or N % tr :
                             continue
                         P = nat.dgemm_partial(x, ws[0], S, tr)
