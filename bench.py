@@ -97,6 +97,9 @@ def main() -> None:
     # while batch i generates) and no collective is pending at the barriers.
     for _ in pipe.answer_pipelined([batch_for(w) for w in range(a.warmup)], params):
         pass
+    # the cascade decode graph is first needed once prompt prefixes are cached (after the
+    # first warm-up batch): capture it here, not inside the timed steps
+    pipe.engine.warm_graphs(a.batch)
     sync()
     comm.barrier()
     sync()

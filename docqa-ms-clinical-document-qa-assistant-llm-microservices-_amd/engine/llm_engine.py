@@ -307,6 +307,22 @@ class LLMEngine:
             t.copy_(v)
         g.graph = graph
 
+    @torch.inference_mode()
+    def warm_graphs(self, batch: int, greedy: bool = True) -> None:
+        """Capture the decode graphs (plain and cascade) of the bucket serving ``batch``
+        sequences now, with empty slots (valid 0: nothing is written to the KV cache), so
+        the first batch that hits the cascade path does not pay a capture / GEMM tuning."""
+        if not self.use_graphs:
+            return
+        bp = _bucket(batch, self.max_batch)
+        for cascade in ([False, True] if self.cascade else [False]):
+            g = self._get_graph(bp, greedy, cascade)
+            if g.graph is None:
+                for t in (g.valid, g.positions, g.context_lens, g.tokens):
+                    t.zero_()
+                g.shared_len.zero_()
+                self._capture(g)
+
     # ------------------------------------------------------------------ generate
     @torch.inference_mode()
     def generate(self, prompts: list[list[int]], params: SamplingParams | None = None,
