@@ -13,6 +13,7 @@ The reference serves one request at a time; here every stage is batched.
 """
 from __future__ import annotations
 
+import os
 import time
 from dataclasses import dataclass, field
 
@@ -162,7 +163,7 @@ class RAGPipeline:
 
     @torch.inference_mode()
     def answer_pipelined(self, batches: list[list[str]], params: SamplingParams | None = None,
-                         lead_steps: int = 12):
+                         lead_steps: int | None = None):
         """Yield (answers, StageTimes, latency_s) per batch.  Batch i+1's embedding and
         kNN search run on a side HIP stream and its prompt assembly on a helper thread,
         released when batch i's decode is ``lead_steps`` steps from its end, so they
@@ -172,6 +173,8 @@ class RAGPipeline:
         import concurrent.futures as cf
 
         params = params or SamplingParams(stop_on_eos=True)
+        if lead_steps is None:
+            lead_steps = int(os.environ.get("DOCQA_PIPELINE_LEAD", "12"))
         cuda = self.engine.device.type == "cuda"
         stream = torch.cuda.Stream() if cuda else None
         with cf.ThreadPoolExecutor(1, thread_name_prefix="rag-prep") as ex:
