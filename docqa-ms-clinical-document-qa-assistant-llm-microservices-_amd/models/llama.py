@@ -15,7 +15,8 @@ MI355X-first layout:
     request-level data parallel) and 70B (140 GB) runs TP=8 (17.6 GB/GPU).
 
 Weights are random-initialised on the device (no checkpoints are reachable offline);
-``load_safetensors`` maps Hugging Face Llama checkpoints when one is available.
+``models/checkpoint.py`` loads Hugging Face Llama checkpoints (safetensors) when one is
+available: pass the checkpoint directory wherever a preset name is accepted.
 
 Reference parity: replaces the Ollama/llama.cpp Mistral-7B generator behind
 ``ChatOllama(model="mistral", temperature=0)`` (llm-qa/main.py:66-69).

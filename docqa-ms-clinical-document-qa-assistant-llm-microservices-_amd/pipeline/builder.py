@@ -9,8 +9,7 @@ import torch
 from ..engine.llm_engine import LLMEngine
 from ..index.flat import FlatIndex
 from ..index.sharded import ShardedFlatIndex
-from ..models.bert import BertConfig, BertEncoder
-from ..models.llama import LlamaConfig, LlamaModel
+from ..models import checkpoint as ck
 from ..parallel import comm
 from ..text.tokenizer import ChatTokenizer, WordPieceTokenizer
 from .corpus import build_corpus, embed_records
@@ -35,10 +34,12 @@ def build_stack(sc: StackConfig, device="cuda", log=print) -> tuple[RAGPipeline,
     info = {}
     t0 = time.perf_counter()
     s = comm.state()
-    llm_cfg = LlamaConfig.preset(sc.llm)
+    # names are presets (random-init weights) or Hugging Face checkpoint directories
+    ck.use_checkpoint_tokenizers(sc.llm, sc.embed)
+    llm_cfg = ck.resolve_llama_config(sc.llm)
     enc_tok = WordPieceTokenizer()
     chat_tok = ChatTokenizer(model_vocab=llm_cfg.vocab_size)
-    encoder = BertEncoder(BertConfig.preset(sc.embed), device=device, seed=sc.seed)
+    encoder = ck.resolve_bert(sc.embed, device=device, seed=sc.seed)
     records = build_corpus(sc.n_notes, sc.kb_dir, sc.seed)
     # contiguous shard per data-parallel rank: global ids = shard offset + local row
     n = len(records)
@@ -52,7 +53,7 @@ def build_stack(sc: StackConfig, device="cuda", log=print) -> tuple[RAGPipeline,
         torch.cuda.synchronize()
     info["index_build_s"] = time.perf_counter() - t0
     info["index_vectors"] = n
-    model = LlamaModel(llm_cfg, device=device, seed=sc.seed)
+    model = ck.resolve_llama(sc.llm, device=device, seed=sc.seed)
     engine = LLMEngine(model, max_batch=sc.max_batch, max_context=sc.max_context,
                        use_graphs=sc.use_graphs)
     pipe = RAGPipeline(encoder, enc_tok, index, records, engine, chat_tok, k=sc.k,

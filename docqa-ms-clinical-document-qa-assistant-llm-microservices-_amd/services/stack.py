@@ -19,8 +19,8 @@ from ..index.follower import IndexFollower
 from ..config import Settings
 from ..deid.engine import NER_LABELS, DeidEngine
 from ..engine.llm_engine import LLMEngine
-from ..models.bert import BertConfig, BertEncoder, BertTokenClassifier
-from ..models.llama import LlamaConfig, LlamaModel
+from ..models import checkpoint as ck
+from ..models.bert import BertConfig, BertTokenClassifier
 from ..pipeline.rag import RAGPipeline
 from ..store import docs_db
 from ..text.tokenizer import ChatTokenizer, WordPieceTokenizer
@@ -92,15 +92,19 @@ class DocQAStack:
         self.broker = (get_broker(self.st) if self.st.bus_backend != "inproc"
                        else InProcBroker(self.st.bus_journal_dir or None))
         self.db = docs_db.DocsDB(self.st.database_url) if svc & {"ingest", "indexer"} else None
+        ck.use_checkpoint_tokenizers(opts.llm, opts.embed)
         self.enc_tok = WordPieceTokenizer()
-        llm_cfg = LlamaConfig.preset(opts.llm)
+        llm_cfg = ck.resolve_llama_config(opts.llm)
         self.chat_tok = ChatTokenizer(model_vocab=llm_cfg.vocab_size)
-        self.encoder = BertEncoder(BertConfig.preset(opts.embed), device=dev) if svc & {"indexer", "qa"} else None
+        self.encoder = ck.resolve_bert(opts.embed, device=dev) if svc & {"indexer", "qa"} else None
         self.deid = self.indexer = self.follower = self.engine = self.pipeline = None
         self.ingest_app = self.qa_app = self.indexer_app = self.synthese_app = self.ui_app = None
         if "deid" in svc:
-            ner_model = (BertTokenClassifier(BertConfig.preset(opts.ner), NER_LABELS, device=dev)
-                         if opts.ner_in_loop else None)
+            ner_model = None
+            if opts.ner_in_loop:
+                ner_model = (ck.load_bert_token_classifier(opts.ner, NER_LABELS, device=dev)
+                             if ck.is_checkpoint(opts.ner)
+                             else BertTokenClassifier(BertConfig.preset(opts.ner), NER_LABELS, device=dev))
             self.deid_engine = DeidEngine(ner_model, self.enc_tok, use_model=opts.ner_in_loop)
             self.deid = deid_worker.DeidWorker(self.deid_engine, self.st, self.broker).start()
         if "indexer" in svc:
@@ -117,7 +121,7 @@ class DocQAStack:
                 self.follower = IndexFollower(self.st.index_dir, self.st.index_file, self.st.metadata_file,
                                               d=self.encoder.cfg.hidden, device=dev).start()
                 index, metadata = self.follower.index, self.follower.metadata
-            self.model = LlamaModel(llm_cfg, device=dev)
+            self.model = ck.resolve_llama(opts.llm, device=dev)
             self.engine = LLMEngine(self.model, max_batch=opts.max_batch, max_context=opts.max_context,
                                     use_graphs=opts.use_graphs)
             self.pipeline = RAGPipeline(self.encoder, self.enc_tok, index, metadata,

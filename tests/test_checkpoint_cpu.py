@@ -1,0 +1,151 @@
+"""Hugging Face checkpoint IO (models/checkpoint.py): a Llama model written as
+config.json + safetensors (single file and sharded with an index) loads back to the same
+logits; a BERT / sentence-transformers layout and a token-classification head map onto
+the encoder kernels' layout.  Random tiny models on CPU (no hub is reachable)."""
+import json
+
+import torch
+
+
+def _llama_logits(model, ids):
+    from docqa_amd.models.llama import AttnMeta
+
+    T = len(ids)
+    meta = AttnMeta(prefill=True, positions=torch.arange(T, dtype=torch.int32),
+                    slot_mapping=torch.arange(T, dtype=torch.int32),
+                    cu_seqlens=torch.tensor([0, T], dtype=torch.int32), max_len=T)
+    shape = (1, model.hkv, 64, model.cfg.head_dim)
+    caches = [(torch.zeros(shape, dtype=model.dtype), torch.zeros(shape, dtype=model.dtype))
+              for _ in model.layers]
+    return model.forward(torch.tensor(ids, dtype=torch.int32), meta, caches)
+
+
+def test_llama_roundtrip_single_and_sharded(tmp_path):
+    from safetensors.torch import save_file
+
+    from docqa_amd.models import checkpoint as ck
+    from docqa_amd.models.llama import LlamaConfig, LlamaModel
+
+    m = LlamaModel(LlamaConfig.preset("tiny"), device="cpu", seed=3)
+    ids = [1, 17, 230, 4000, 9, 77]
+    ref = _llama_logits(m, ids)
+    ck.save_llama(m, tmp_path / "one")
+    assert ck.is_checkpoint(tmp_path / "one")
+    m1 = ck.resolve_llama(tmp_path / "one", device="cpu")
+    assert m1.cfg.layers == m.cfg.layers and m1.cfg.kv_heads == m.cfg.kv_heads
+    assert torch.equal(_llama_logits(m1, ids), ref)
+    # sharded layout: two files + model.safetensors.index.json
+    sd = m.export_state_dict_hf()
+    keys = sorted(sd)
+    half = len(keys) // 2
+    d = tmp_path / "sharded"
+    d.mkdir()
+    (d / "config.json").write_text((tmp_path / "one" / "config.json").read_text())
+    parts = {"model-00001-of-00002.safetensors": keys[:half], "model-00002-of-00002.safetensors": keys[half:]}
+    for f, ks in parts.items():
+        save_file({k: sd[k].contiguous() for k in ks}, str(d / f))
+    (d / "model.safetensors.index.json").write_text(json.dumps(
+        {"weight_map": {k: f for f, ks in parts.items() for k in ks}}))
+    lazy = ck.LazySafetensors(d)
+    assert len(lazy) == len(sd) and "model.norm.weight" in lazy
+    m2 = ck.load_llama(d, device="cpu")
+    assert torch.equal(_llama_logits(m2, ids), ref)
+    # preset names still give random-init architectures
+    assert ck.resolve_llama_config("tiny").hidden == 256
+
+
+def _bert_hf_state(enc, prefix=""):
+    sd = {prefix + "embeddings.word_embeddings.weight": enc.wte,
+          prefix + "embeddings.position_embeddings.weight": enc.wpe,
+          prefix + "embeddings.token_type_embeddings.weight": enc.wtt,
+          prefix + "embeddings.LayerNorm.weight": enc.emb_g, prefix + "embeddings.LayerNorm.bias": enc.emb_b}
+    H = enc.cfg.hidden
+    for i, L in enumerate(enc.layers):
+        p = f"{prefix}encoder.layer.{i}."
+        for j, n in enumerate(("query", "key", "value")):
+            sd[p + f"attention.self.{n}.weight"] = L["qkv_w"][j * H:(j + 1) * H]
+            sd[p + f"attention.self.{n}.bias"] = L["qkv_b"][j * H:(j + 1) * H]
+        sd.update({p + "attention.output.dense.weight": L["o_w"], p + "attention.output.dense.bias": L["o_b"],
+                   p + "attention.output.LayerNorm.weight": L["ln1_g"], p + "attention.output.LayerNorm.bias": L["ln1_b"],
+                   p + "intermediate.dense.weight": L["up_w"], p + "intermediate.dense.bias": L["up_b"],
+                   p + "output.dense.weight": L["down_w"], p + "output.dense.bias": L["down_b"],
+                   p + "output.LayerNorm.weight": L["ln2_g"], p + "output.LayerNorm.bias": L["ln2_b"]})
+    return {k: v.contiguous().clone() for k, v in sd.items()}
+
+
+def _bert_hf_config(cfg):
+    return {"vocab_size": cfg.vocab_size, "hidden_size": cfg.hidden, "num_hidden_layers": cfg.layers,
+            "num_attention_heads": cfg.heads, "intermediate_size": cfg.intermediate,
+            "max_position_embeddings": cfg.max_position, "type_vocab_size": cfg.type_vocab,
+            "layer_norm_eps": cfg.eps}
+
+
+def test_sentence_transformers_encoder_layout(tmp_path):
+    from safetensors.torch import save_file
+
+    from docqa_amd.models import checkpoint as ck
+    from docqa_amd.models.bert import BertConfig, BertEncoder
+
+    cfg = BertConfig.preset("tiny-bert")
+    enc = BertEncoder(cfg, device="cpu", seed=5)
+    d = tmp_path / "minilm"
+    d.mkdir()
+    (d / "config.json").write_text(json.dumps(_bert_hf_config(cfg)))
+    (d / "modules.json").write_text(json.dumps([{"type": "sentence_transformers.models.Transformer"},
+                                                {"type": "sentence_transformers.models.Pooling"},
+                                                {"type": "sentence_transformers.models.Normalize"}]))
+    (d / "1_Pooling").mkdir()
+    (d / "1_Pooling" / "config.json").write_text(json.dumps({"pooling_mode_mean_tokens": True}))
+    save_file(_bert_hf_state(enc), str(d / "model.safetensors"))
+    got = ck.resolve_bert(d, device="cpu")
+    assert got.cfg.pooling == "mean" and got.cfg.normalize
+    toks = [[2, 100, 200, 3], [2, 55, 3]]
+    assert torch.allclose(got.encode(toks), enc.encode(toks))
+
+
+def test_token_classifier_head_and_labels(tmp_path):
+    from safetensors.torch import save_file
+
+    from docqa_amd.models import checkpoint as ck
+    from docqa_amd.models.bert import BertConfig, BertTokenClassifier
+
+    cfg = BertConfig.preset("tiny-bert")
+    labels = ["O", "B-PERSON", "I-PERSON", "B-DATE_TIME"]
+    clf = BertTokenClassifier(cfg, labels, device="cpu", seed=7)
+    d = tmp_path / "ner"
+    d.mkdir()
+    hf = _bert_hf_config(cfg)
+    hf["id2label"] = {str(i): lab for i, lab in enumerate(labels)}
+    (d / "config.json").write_text(json.dumps(hf))
+    sd = _bert_hf_state(clf, prefix="bert.")
+    sd["classifier.weight"] = clf.cls_w[:len(labels)].clone()
+    sd["classifier.bias"] = clf.cls_b[:len(labels)].clone()
+    save_file(sd, str(d / "model.safetensors"))
+    got = ck.load_bert_token_classifier(d, ["unused"], device="cpu")
+    assert got.labels == labels
+    toks = [[2, 100, 200, 300, 3]]
+    assert got.predict(toks) == clf.predict(toks)
+
+
+def test_stack_runs_from_checkpoint_directories(tmp_path):
+    """build_stack with LLM / embedder given as checkpoint directories (what a user with real
+    weights passes via LLM_MODEL / EMBED_MODEL) answers a question end to end."""
+    from safetensors.torch import save_file
+
+    from docqa_amd.engine.llm_engine import SamplingParams
+    from docqa_amd.models import checkpoint as ck
+    from docqa_amd.models.bert import BertConfig, BertEncoder
+    from docqa_amd.models.llama import LlamaConfig, LlamaModel
+    from docqa_amd.pipeline.builder import StackConfig, build_stack
+
+    ck.save_llama(LlamaModel(LlamaConfig.preset("tiny"), device="cpu", seed=1), tmp_path / "llm")
+    cfg = BertConfig.preset("tiny-bert")
+    d = tmp_path / "emb"
+    d.mkdir()
+    (d / "config.json").write_text(json.dumps(_bert_hf_config(cfg)))
+    save_file(_bert_hf_state(BertEncoder(cfg, device="cpu", seed=2)), str(d / "model.safetensors"))
+    pipe, info = build_stack(StackConfig(llm=str(tmp_path / "llm"), embed=str(d), n_notes=8, max_batch=4,
+                                         max_context=2048, use_graphs=False), device="cpu", log=lambda *a: None)
+    assert pipe.engine.model.cfg.name == "llm" and pipe.encoder.cfg.hidden == cfg.hidden
+    ans = pipe.answer_batch(["Quelle plante pour le syndrome ?"], SamplingParams(max_new_tokens=4, stop_on_eos=False))
+    assert len(ans) == 1 and len(ans[0].token_ids) == 4 and len(ans[0].sources) == 3
