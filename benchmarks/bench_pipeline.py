@@ -59,8 +59,8 @@ def main():
     from docqa_amd.engine.llm_engine import LLMEngine, SamplingParams
     from docqa_amd.index.flat import FlatIndex
     from docqa_amd.index.sharded import ShardedFlatIndex
-    from docqa_amd.models.bert import BertConfig, BertEncoder, BertTokenClassifier
-    from docqa_amd.models.llama import LlamaConfig, LlamaModel
+    from docqa_amd.models.bert import BertConfig, BertTokenClassifier
+    from docqa_amd.models import checkpoint as ck
     from docqa_amd.parallel import comm
     from docqa_amd.pipeline.corpus import embed_records
     from docqa_amd.pipeline.rag import RAGPipeline
@@ -96,8 +96,9 @@ def main():
     t_setup = time.perf_counter()
     enc_tok = WordPieceTokenizer()
     ner_tok = WordPieceTokenizer(max_len=256)
-    encoder = BertEncoder(BertConfig.preset(a.embed), device=dev, seed=0)
-    ner = BertTokenClassifier(BertConfig.preset(a.ner), NER_LABELS, device=dev)
+    encoder = ck.resolve_bert(a.embed, device=dev, seed=0)        # preset or checkpoint dir
+    ner = (ck.load_bert_token_classifier(a.ner, NER_LABELS, device=dev) if ck.is_checkpoint(a.ner)
+           else BertTokenClassifier(BertConfig.preset(a.ner), NER_LABELS, device=dev))
     deid = DeidEngine(ner, ner_tok, use_model=True)
     local = FlatIndex(encoder.cfg.hidden, "l2", dev, capacity=1 << 16)
     # knowledge-base bootstrap (semantic-indexer startup), sharded across the ranks
@@ -146,8 +147,8 @@ def main():
         all_records, index = records, local
 
     # ---------------------------------------------------------------- stage 2: QA
-    llm_cfg = LlamaConfig.preset(a.llm)
-    model = LlamaModel(llm_cfg, device=dev, seed=0)
+    model = ck.resolve_llama(a.llm, device=dev, seed=0)
+    llm_cfg = model.cfg
     engine = LLMEngine(model, max_batch=a.batch, max_context=a.max_context, use_graphs=cuda)
     chat_tok = ChatTokenizer(model_vocab=llm_cfg.vocab_size)
     pipe = RAGPipeline(encoder, enc_tok, index, all_records, engine, chat_tok, k=a.k,
