@@ -152,3 +152,32 @@ def test_chunked_prefill_matches_single_pass():
                         max_prefill_tokens=32, prefix_cache=False).generate(prompts, sp)
     assert one == chunked
     assert one[0] == _naive_greedy(m, prompts[0], 6)
+
+
+def test_lpt_dispatch_order_and_decode_state_ops():
+    """set_order: active rows longest-context first, then the padded rows (a permutation of
+    the bucket); re-uploaded only when the batch key changes.  decode_slots /
+    decode_advance references: slot = block * BS + offset (-1 for padded rows)."""
+    from docqa_amd import ops
+    from docqa_amd.engine.llm_engine import _DecodeGraph
+
+    m = LlamaModel(LlamaConfig.preset("tiny"), device="cpu")
+    eng = LLMEngine(m, max_batch=8, max_context=128, block_size=16, use_graphs=False)
+    g = _DecodeGraph(eng, 8)
+    eng.set_order(g, [30, 90, 10, 50, 70], key=1)
+    assert g.order.tolist() == [1, 4, 3, 0, 2, 5, 6, 7]
+    g.order.fill_(0)
+    eng.set_order(g, [1, 2, 3], key=1)          # same key: untouched
+    assert g.order.tolist() == [0] * 8
+    eng.set_order(g, [1, 2, 3], key=2)
+    assert g.order.tolist() == [2, 1, 0, 3, 4, 5, 6, 7]
+
+    bt = torch.tensor([[5, 6, 7], [8, 9, 10]], dtype=torch.int32)
+    pos = torch.tensor([17, 3], dtype=torch.int32)
+    valid = torch.tensor([1, 0], dtype=torch.int32)
+    assert ops.decode_slots(bt, pos, valid, 16).tolist() == [6 * 16 + 1, -1]
+    out, tok = torch.zeros(2, dtype=torch.long), torch.zeros(2, dtype=torch.int32)
+    ctx = pos + 1
+    ops.decode_advance(torch.tensor([11, 12]), out, tok, pos, ctx, valid)
+    assert out.tolist() == [11, 12] and tok.tolist() == [11, 12]
+    assert pos.tolist() == [18, 3] and ctx.tolist() == [19, 4]
