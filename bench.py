@@ -36,10 +36,10 @@ def main() -> None:
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
-    # 192: the largest batch whose p50 answer latency (~1.5 s) stays below the measured
-    # reference-equivalent p50 (1.62 s) -- 128 gives ~111 q/s at ~1.25 s p50,
-    # 256 ~157 q/s at ~1.73 s (profiles/r1_bench_batch_sweep.log)
-    ap.add_argument("--batch", type=int, default=192, help="questions per data-parallel rank per step")
+    # 256: the largest power-of-two batch whose p50 answer latency (~1.52 s) stays below the
+    # measured reference-equivalent p50 (1.62 s); 128 gives ~117 q/s at
+    # ~1.16 s p50, 192 ~146 q/s at ~1.35 s (profiles/r1_bench_batch_sweep.log)
+    ap.add_argument("--batch", type=int, default=256, help="questions per data-parallel rank per step")
     ap.add_argument("--max-new-tokens", type=int, default=128)
     ap.add_argument("--llm", default="llama3-8b")
     ap.add_argument("--embed", default="minilm-l6")

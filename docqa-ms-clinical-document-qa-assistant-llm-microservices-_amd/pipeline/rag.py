@@ -81,6 +81,16 @@ class RAGPipeline:
         self.template = template
         self.max_prompt_tokens = max_prompt_tokens
         self.last_times = StageTimes()
+        # token ids of every retrieved chunk, tokenised once: a prompt is then assembled
+        # from cached pieces split at paragraph boundaries (the byte-level BPE never merges
+        # across a newline pre-token), so only the question is tokenised per request
+        self._chunk_ids: dict[int, list[int]] = {}
+        self._pieces = None
+        if hasattr(chat_tokenizer, "special") and template.count("{context}") == 1 \
+                and template.count("{question}") == 1 and template.index("{context}") < template.index("{question}"):
+            head, _, rest = template.partition("{context}")
+            mid, _, tail = rest.partition("{question}")
+            self._pieces = (head, mid, tail)
 
     def _sync(self):
         if self.engine.device.type == "cuda":
@@ -94,14 +104,47 @@ class RAGPipeline:
         D, I = self.index.search(q, self.k)
         return D, I
 
+    def _piece_prompt(self, qtext: str, ids: list[int]) -> list[int]:
+        ct = self.chat_tok
+        if not hasattr(self, "_frame"):
+            s = ct.special
+            head, mid, tail = self._pieces
+            self._frame = ([s("<|begin_of_text|>"), s("<|start_header_id|>")] + ct.encode("user")
+                           + [s("<|end_header_id|>")] + ct.encode("\n\n" + head),
+                           ct.encode("\n\n"), ct.encode(mid),
+                           ct.encode(tail) + [s("<|eot_id|>"), s("<|start_header_id|>")] + ct.encode("assistant")
+                           + [s("<|end_header_id|>")] + ct.encode("\n\n"))
+        pre, sep, mid_ids, post = self._frame
+        out = list(pre)
+        first = True
+        for i in ids:
+            if not 0 <= i < len(self.metadata):
+                continue
+            c = self._chunk_ids.get(i)
+            if c is None:
+                c = self._chunk_ids[i] = ct.encode(self.metadata[i]["text_content"])
+            if not first:
+                out += sep
+            out += c
+            first = False
+        return out + mid_ids + ct.encode(qtext) + post
+
     def build_prompts(self, questions: list[str], I: list[list[int]]) -> list[list[int]]:
-        prompts = []
+        if self._pieces is not None and os.environ.get("DOCQA_PROMPT_PIECES", "1") == "1":
+            prompts = [self._piece_prompt(q, ids) for q, ids in zip(questions, I)]
+            lim = self.max_prompt_tokens
+            if lim:
+                prompts = [p if len(p) <= lim else p[: lim // 2] + p[-lim // 2:] for p in prompts]
+            return prompts
+        texts = []
         for qtext, ids in zip(questions, I):
             ctx = "\n\n".join(self.metadata[i]["text_content"] for i in ids if 0 <= i < len(self.metadata))
-            p = self.chat_tok.chat_prompt(self.template.format(context=ctx, question=qtext))
-            if self.max_prompt_tokens and len(p) > self.max_prompt_tokens:
-                p = p[: self.max_prompt_tokens // 2] + p[-self.max_prompt_tokens // 2:]
-            prompts.append(p)
+            texts.append(self.template.format(context=ctx, question=qtext))
+        enc = getattr(self.chat_tok, "encode_batch_chat", None)
+        prompts = enc(texts) if enc else [self.chat_tok.chat_prompt(t) for t in texts]
+        lim = self.max_prompt_tokens
+        if lim:
+            prompts = [p if len(p) <= lim else p[: lim // 2] + p[-lim // 2:] for p in prompts]
         return prompts
 
     @torch.inference_mode()
@@ -174,7 +217,9 @@ class RAGPipeline:
 
         params = params or SamplingParams(stop_on_eos=True)
         if lead_steps is None:
-            lead_steps = int(os.environ.get("DOCQA_PIPELINE_LEAD", "12"))
+            # prompts are assembled from cached chunk token ids (~6 ms for 256 questions),
+            # so batch i+1's preparation fits in the last 4 decode steps of batch i
+            lead_steps = int(os.environ.get("DOCQA_PIPELINE_LEAD", "4"))
         cuda = self.engine.device.type == "cuda"
         stream = torch.cuda.Stream() if cuda else None
         with cf.ThreadPoolExecutor(1, thread_name_prefix="rag-prep") as ex:

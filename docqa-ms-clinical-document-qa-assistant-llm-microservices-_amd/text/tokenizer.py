@@ -158,4 +158,15 @@ class ChatTokenizer:
         return self.tok.decode(keep)
 
     def encode_batch_chat(self, users: list[str]) -> list[list[int]]:
-        return [self.chat_prompt(u) for u in users]
+        """chat_prompt for many user turns: the user texts are tokenised in one
+        ``encode_batch`` call (parallel in the Rust tokenizer) and the constant framing
+        tokens once -- identical ids to per-prompt :meth:`chat_prompt`."""
+        if not users:
+            return []
+        s = self.special
+        head = [s("<|begin_of_text|>"), s("<|start_header_id|>")] + self.encode("user") + [s("<|end_header_id|>")]
+        tail = ([s("<|eot_id|>"), s("<|start_header_id|>")] + self.encode("assistant")
+                + [s("<|end_header_id|>")] + self.encode("\n\n"))
+        m = self._to_model
+        bodies = [[m.get(i, i) for i in e.ids] for e in self.tok.encode_batch(["\n\n" + u for u in users])]
+        return [head + b + tail for b in bodies]

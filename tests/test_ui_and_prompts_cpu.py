@@ -100,3 +100,30 @@ def test_rag_template_puts_fixed_text_first_for_the_prefix_cache():
     b = tok.chat_prompt(DEFAULT_TEMPLATE.format(context="Réglisse score 7", question="Posologie ?"))
     common = next(i for i, (x, y) in enumerate(zip(a, b)) if x != y)
     assert common >= len(tok.chat_prompt(head)) - 8
+
+
+def test_prompt_pieces_identical_to_full_tokenisation(monkeypatch):
+    """RAG prompts assembled from cached per-chunk token ids equal the token ids of the
+    formatted prompt (the byte-level BPE does not merge across the paragraph breaks the
+    pieces are split at)."""
+    import torch
+
+    from docqa_amd.pipeline.rag import RAGPipeline
+    from docqa_amd.text.synthetic import synthetic_questions
+    from docqa_amd.text.tokenizer import ChatTokenizer
+
+    tok = ChatTokenizer(model_vocab=128256)
+    meta = [{"text_content": f"Patient {i} : toux chronique, fatigue ; Ren Shen (score {i % 10}).",
+             "source": f"s{i}"} for i in range(20)]
+
+    class _Eng:
+        device = torch.device("cpu")
+
+    pipe = RAGPipeline(None, None, None, meta, _Eng(), tok)
+    qs = synthetic_questions(24, seed=3)
+    I = [[(7 * j + r) % 20 for r in range(3)] for j in range(len(qs))]
+    monkeypatch.setenv("DOCQA_PROMPT_PIECES", "0")
+    full = pipe.build_prompts(qs, I)
+    monkeypatch.setenv("DOCQA_PROMPT_PIECES", "1")
+    assert pipe.build_prompts(qs, I) == full
+    assert tok.encode_batch_chat([qs[0]]) == [tok.chat_prompt(qs[0])]
