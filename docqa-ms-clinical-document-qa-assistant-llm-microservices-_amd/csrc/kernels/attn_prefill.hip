@@ -27,6 +27,7 @@
 // and the MiniLM encoder attention inside sentence-transformers
 // (semantic-indexer/indexer.py:37).
 #include "docqa_common.h"
+#include <stdlib.h>
 #include "docqa_cascade.h"
 #include <float.h>
 
@@ -385,9 +386,19 @@ int docqa_cascade_prefix(const void* qkv, int row_stride, int rows, int Hq, int 
   if (Hq != 4 * Hkv || BS != 64 || nchunk < 1) return -1;
   PagedKV pk{(const uint16_t*)k_cache, (const uint16_t*)v_cache, prefix_table, 0, nullptr, BS, 6};
   const CascadeOut co{acc, ml, plen, nchunk, rows};
-  dim3 grid(Hkv, nchunk, (rows + 63) / 64);
-  flash_prefill_kernel<128, false, true, 4, 2, true><<<grid, 512, 0, s>>>(
-      (const uint16_t*)qkv, row_stride, nullptr, nullptr, 0, Hq, Hkv, scale, pk, co);
+  static const int wph = [] {   // waves per head: 2 (64-row tiles) or 1 (32-row tiles, 2x workgroups)
+    const char* e = getenv("DOCQA_CASCADE_WPH");
+    return e && atoi(e) == 1 ? 1 : 2;
+  }();
+  if (wph == 1) {
+    dim3 grid(Hkv, nchunk, (rows + 31) / 32);
+    flash_prefill_kernel<128, false, true, 4, 1, true><<<grid, 256, 0, s>>>(
+        (const uint16_t*)qkv, row_stride, nullptr, nullptr, 0, Hq, Hkv, scale, pk, co);
+  } else {
+    dim3 grid(Hkv, nchunk, (rows + 63) / 64);
+    flash_prefill_kernel<128, false, true, 4, 2, true><<<grid, 512, 0, s>>>(
+        (const uint16_t*)qkv, row_stride, nullptr, nullptr, 0, Hq, Hkv, scale, pk, co);
+  }
   DOCQA_CHECK_LAUNCH();
   return 0;
 }
