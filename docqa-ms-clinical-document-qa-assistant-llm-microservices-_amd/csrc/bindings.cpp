@@ -338,6 +338,47 @@ at::Tensor paged_decode_cascade(const at::Tensor& q, at::Tensor k_cache, at::Ten
   return out;
 }
 
+// cascade decode over the UNROTATED packed QKV of a library GEMM: RoPE, the new token's
+// cache write and the attention in the cascade kernels (fallback: rope_cache in place)
+at::Tensor paged_decode_cascade_rope(at::Tensor qkv, const at::Tensor& positions, const at::Tensor& cos_sin,
+                                     const at::Tensor& slot_mapping, at::Tensor k_cache, at::Tensor v_cache,
+                                     const at::Tensor& block_tables, const at::Tensor& context_lens,
+                                     int64_t Hq, int64_t max_context, double scale,
+                                     const at::Tensor& prefix_table, const at::Tensor& prefix_len,
+                                     int64_t nchunk, const c10::optional<at::Tensor>& order) {
+  CHECK_GPU(qkv); CHECK_BF16(qkv); CHECK_BF16(k_cache); CHECK_BF16(v_cache);
+  CHECK_I32(positions); CHECK_I32(slot_mapping); CHECK_I32(block_tables); CHECK_I32(context_lens);
+  CHECK_CONTIG(block_tables); CHECK_I32(prefix_table); CHECK_I32(prefix_len); CHECK_CONTIG(prefix_table);
+  TORCH_CHECK(qkv.dim() == 2 && qkv.stride(1) == 1, "qkv must be [B, width] with unit stride");
+  TORCH_CHECK(cos_sin.scalar_type() == at::kFloat, "cos_sin must be fp32");
+  const int B = qkv.size(0);
+  const int Hkv = k_cache.size(1), BS = k_cache.size(2), D = k_cache.size(3);
+  TORCH_CHECK(D == 128 && BS == 64 && Hq == 4 * Hkv, "cascade decode: head_dim 128, 64-token blocks, GQA 4");
+  TORCH_CHECK(qkv.size(1) >= (Hq + 2 * Hkv) * D, "qkv rows narrower than the packed QKV width");
+  TORCH_CHECK(positions.numel() == B && slot_mapping.numel() == B && context_lens.numel() == B,
+              "positions / slot_mapping / context_lens must have B entries");
+  TORCH_CHECK(block_tables.size(1) <= 256, "cascade decode: <= 256 blocks per sequence");
+  TORCH_CHECK(prefix_table.numel() >= 1 && prefix_len.numel() == 1, "cascade decode: prefix table / length");
+  const int max_parts = docqa_decode_splits(B, Hkv, max_context);
+  c10::DeviceGuard g(qkv.device());
+  auto out = at::empty({B, Hq * D}, qkv.options());
+  auto f32 = qkv.options().dtype(at::kFloat);
+  auto tmp_out = at::empty({B, Hq, max_parts, D}, f32);
+  auto tmp_ml = at::empty({B, Hq, max_parts, 2}, f32);
+  auto pacc = at::empty({nchunk, B, Hq, D}, f32);
+  auto pml = at::empty({nchunk, B, Hq, 2}, f32);
+  CHECK_RC(docqa_paged_decode_cascade_rope(qkv.data_ptr(), qkv.stride(0), positions.data_ptr<int>(),
+                                           cos_sin.data_ptr<float>(), slot_mapping.data_ptr<int>(),
+                                           k_cache.data_ptr(), v_cache.data_ptr(), block_tables.data_ptr<int>(),
+                                           block_tables.size(1), context_lens.data_ptr<int>(), out.data_ptr(),
+                                           Hq * D, tmp_out.data_ptr<float>(), tmp_ml.data_ptr<float>(), B, Hq,
+                                           Hkv, BS, max_parts, (float)scale, prefix_table.data_ptr<int>(),
+                                           prefix_len.data_ptr<int>(), (int)nchunk, pacc.data_ptr<float>(),
+                                           pml.data_ptr<float>(), order_ptr(order, B), stream()),
+           "paged_decode_cascade_rope");
+  return out;
+}
+
 // decode step attention fed by the QKV projection's split-K partial slabs: RoPE + cache
 // write of the new token + paged attention in one launch (ring kernel)
 at::Tensor paged_decode_fused(const at::Tensor& P, const at::Tensor& positions, const at::Tensor& cos_sin,
@@ -629,6 +670,10 @@ TORCH_LIBRARY(docqa, m) {
   m.def("paged_decode_cascade(Tensor q, Tensor k_cache, Tensor v_cache, Tensor block_tables, "
         "Tensor context_lens, int Hq, int max_context, float scale, Tensor prefix_table, Tensor prefix_len, "
         "int nchunk, Tensor? order=None) -> Tensor");
+  m.def("paged_decode_cascade_rope(Tensor(a!) qkv, Tensor positions, Tensor cos_sin, Tensor slot_mapping, "
+        "Tensor(b!) k_cache, Tensor(c!) v_cache, Tensor block_tables, Tensor context_lens, int Hq, "
+        "int max_context, float scale, Tensor prefix_table, Tensor prefix_len, int nchunk, "
+        "Tensor? order=None) -> Tensor");
   m.def("paged_decode_fused(Tensor P, Tensor positions, Tensor cos_sin, Tensor slot_mapping, "
         "Tensor(a!) k_cache, Tensor(b!) v_cache, Tensor block_tables, Tensor context_lens, int Hq, "
         "int max_context, float scale, Tensor? order=None) -> Tensor");
@@ -670,6 +715,7 @@ TORCH_LIBRARY_IMPL(docqa, CUDA, m) {
   m.impl("dgemm_glu", &dgemm_glu);
   m.impl("paged_decode_fused", &paged_decode_fused);
   m.impl("paged_decode_cascade", &paged_decode_cascade);
+  m.impl("paged_decode_cascade_rope", &paged_decode_cascade_rope);
   m.impl("ar_oneshot", &ar_oneshot);
   m.impl("add_rmsnorm_splitk", &add_rmsnorm_splitk);
   m.impl("rope_cache_splitk", &rope_cache_splitk);

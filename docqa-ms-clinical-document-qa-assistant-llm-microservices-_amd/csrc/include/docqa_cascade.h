@@ -32,6 +32,10 @@ struct CascadeOut {       // prefix partials produced by the MFMA prefix kernel
   const int* plen;
   int nchunk;
   int rows;               // B: query rows = decode sequences
+  // fused RoPE: the query rows are the library GEMM's unrotated QKV; rotate them on load
+  // (null: already rotated)
+  const int* positions = nullptr;
+  const float* cos_sin = nullptr;
 };
 
 // keys per chunk (a multiple of the 64-key tile) and chunks holding >= 1 key

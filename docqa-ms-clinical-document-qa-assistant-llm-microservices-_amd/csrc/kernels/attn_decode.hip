@@ -352,7 +352,16 @@ struct FusedQKV {
   const float* cos_sin;      // [max_pos, D] = [cos(D/2) | sin(D/2)]
   const int* slot_mapping;   // [B], -1: no cache write
   int Hq;
+  // bf16 source instead of the slabs: the packed, not yet rotated QKV rows of a library
+  // GEMM ([B, q_stride]); P is then null
+  const uint16_t* qkv = nullptr;
+  int q_stride = 0;
 };
+
+// 8 consecutive values of a fused-QKV row at element offset `off`: slab sum (split-K
+// projection) or bf16 load (library GEMM output)
+__device__ __forceinline__ void fused_row8(const FusedQKV& fz, int b, int W, size_t slab, int off,
+                                           float (&x)[8]);
 
 // sum of the S slabs of 8 consecutive values, rounded to bf16 like the unfused path
 __device__ __forceinline__ void sum_slabs8(const float* p, int S, size_t slab, float (&x)[8]) {
@@ -366,6 +375,15 @@ __device__ __forceinline__ void sum_slabs8(const float* p, int S, size_t slab, f
   const float v[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
 #pragma unroll
   for (int j = 0; j < 8; ++j) x[j] = bf2f(f2bf(v[j]));
+}
+
+__device__ __forceinline__ void fused_row8(const FusedQKV& fz, int b, int W, size_t slab, int off,
+                                           float (&x)[8]) {
+  if (fz.P) {
+    sum_slabs8(fz.P + (size_t)b * W + off, fz.S, slab, x);
+  } else {
+    unpack8(*reinterpret_cast<const uint4*>(fz.qkv + (size_t)b * fz.q_stride + off), x);
+  }
 }
 
 // rotate-half RoPE of one 8-dim chunk (chunk index c of 16, D = 128): partner chunk c ^ 8
@@ -490,12 +508,11 @@ __global__ __launch_bounds__(256) void paged_decode_ring_kernel(
     // partial slabs, rounded to bf16, RoPE; the new K/V row also goes to the paged cache
     const int W = (fz.Hq + 2 * Hkv) * D;
     const size_t slab = (size_t)gridDim.y * W;
-    const float* row = fz.P + (size_t)b * W;
     const float* cs = fz.cos_sin + (size_t)fz.positions[b] * D;
 #pragma unroll
     for (int g = 0; g < G; ++g) {
       float x[8];
-      sum_slabs8(row + (size_t)(kvh * G + g) * D + chunk * 8, fz.S, slab, x);
+      fused_row8(fz, b, W, slab, (kvh * G + g) * D + chunk * 8, x);
       rope8(x, chunk, cs);
       qv[g][0] = __builtin_bit_cast(bf16x2, pack2(x[0], x[1]));
       qv[g][1] = __builtin_bit_cast(bf16x2, pack2(x[2], x[3]));
@@ -504,9 +521,9 @@ __global__ __launch_bounds__(256) void paged_decode_ring_kernel(
     }
     if (owns_last && wave == 0 && tg == 0) {
       float kx[8], vx[8];
-      sum_slabs8(row + (size_t)(fz.Hq + kvh) * D + chunk * 8, fz.S, slab, kx);
+      fused_row8(fz, b, W, slab, (fz.Hq + kvh) * D + chunk * 8, kx);
       rope8(kx, chunk, cs);
-      sum_slabs8(row + (size_t)(fz.Hq + Hkv + kvh) * D + chunk * 8, fz.S, slab, vx);
+      fused_row8(fz, b, W, slab, (fz.Hq + Hkv + kvh) * D + chunk * 8, vx);
       knew = pack8(kx);
       vnew = pack8(vx);
       const int slot = fz.slot_mapping[b];
@@ -1016,7 +1033,62 @@ int docqa_paged_decode_fused(const float* P, int S, const int* positions, const 
 
 int docqa_cascade_prefix(const void* qkv, int row_stride, int rows, int Hq, int Hkv, float scale,
                          const void* k_cache, const void* v_cache, const int* prefix_table,
-                         const int* plen, int BS, int nchunk, float* acc, float* ml, hipStream_t s);
+                         const int* plen, int BS, int nchunk, float* acc, float* ml,
+                         const int* positions, const float* cos_sin, hipStream_t s);
+int docqa_rope_cache(void* qkv, const int* positions, const float* cos_sin,
+                     const int* slot_mapping, void* k_cache, void* v_cache, int T, int Hq,
+                     int Hkv, int D, int row_stride, int BS, hipStream_t s);
+
+// Cascade decode with the step's RoPE + paged-cache write fused in (the batch sizes whose
+// QKV projection runs on the library GEMM, > 192 rows): the prefix kernel rotates the
+// query rows as it loads them, the ring kernel (FUSED mode, bf16 source) rotates its
+// queries, writes the new token's rotated K and V to the cache and attends to it from
+// registers -- one launch and one QKV round trip fewer per layer.  Shapes the fused ring
+// does not cover (split partitions, MFMA decode) fall back to rope_cache + cascade.
+int docqa_paged_decode_cascade(const void* q, int q_stride, void* k_cache, void* v_cache,
+                               const int* block_tables, int maxb, const int* context_lens, void* out,
+                               int out_stride, float* tmp_out, float* tmp_ml, int B, int Hq, int Hkv,
+                               int BS, int max_parts, float scale, const int* prefix_table,
+                               const int* plen, int nchunk, float* pacc, float* pml, const int* order,
+                               hipStream_t s);
+
+int docqa_paged_decode_cascade_rope(void* qkv, int q_stride, const int* positions,
+                                    const float* cos_sin, const int* slot_mapping, void* k_cache,
+                                    void* v_cache, const int* block_tables, int maxb,
+                                    const int* context_lens, void* out, int out_stride,
+                                    float* tmp_out, float* tmp_ml, int B, int Hq, int Hkv, int BS,
+                                    int max_parts, float scale, const int* prefix_table,
+                                    const int* plen, int nchunk, float* pacc, float* pml,
+                                    const int* order, hipStream_t s) {
+  if (B == 0) return 0;
+  if (BS != 64 || maxb > 256 || Hq != 4 * Hkv || nchunk < 1 || nchunk > kCascadeMaxChunks) return -1;
+  if (max_parts != 1 || mfma_decode_on(Hq / Hkv)) {
+    const int rc = docqa_rope_cache(qkv, positions, cos_sin, slot_mapping, k_cache, v_cache, B, Hq, Hkv,
+                                    128, q_stride, BS, s);
+    if (rc) return rc;
+    return docqa_paged_decode_cascade(qkv, q_stride, k_cache, v_cache, block_tables, maxb, context_lens, out,
+                                      out_stride, tmp_out, tmp_ml, B, Hq, Hkv, BS, max_parts, scale,
+                                      prefix_table, plen, nchunk, pacc, pml, order, s);
+  }
+  int rc = docqa_cascade_prefix(qkv, q_stride, B, Hq, Hkv, scale, k_cache, v_cache, prefix_table, plen,
+                                BS, nchunk, pacc, pml, positions, cos_sin, s);
+  if (rc) return rc;
+  const CascadeIn ci{pacc, pml, plen, nchunk, order};
+  FusedQKV fz{nullptr, 0, positions, cos_sin, slot_mapping, Hq};
+  fz.qkv = (const uint16_t*)qkv;
+  fz.q_stride = q_stride;
+  dim3 grid(Hkv, B, 1);
+  if (ring_nsr() == 4)
+    paged_decode_ring_kernel<4, true, true, 4><<<grid, 256, 0, s>>>(
+        nullptr, 0, (uint16_t*)k_cache, (uint16_t*)v_cache, block_tables, maxb, context_lens, tmp_out,
+        tmp_ml, Hkv, 1, scale, (uint16_t*)out, out_stride, fz, ci);
+  else
+    paged_decode_ring_kernel<4, true, true, 3><<<grid, 256, 0, s>>>(
+        nullptr, 0, (uint16_t*)k_cache, (uint16_t*)v_cache, block_tables, maxb, context_lens, tmp_out,
+        tmp_ml, Hkv, 1, scale, (uint16_t*)out, out_stride, fz, ci);
+  DOCQA_CHECK_LAUNCH();
+  return 0;
+}
 
 // Cascade decode attention (docqa_cascade.h): MFMA prefix partials over the shared prompt
 // prefix [0, *plen) for all B rows, then the ring kernel over each suffix [*plen, L) with
@@ -1031,7 +1103,7 @@ int docqa_paged_decode_cascade(const void* q, int q_stride, void* k_cache, void*
   if (B == 0) return 0;
   if (BS != 64 || maxb > 256 || Hq != 4 * Hkv || nchunk < 1 || nchunk > kCascadeMaxChunks) return -1;
   int rc = docqa_cascade_prefix(q, q_stride, B, Hq, Hkv, scale, k_cache, v_cache, prefix_table, plen,
-                                BS, nchunk, pacc, pml, s);
+                                BS, nchunk, pacc, pml, nullptr, nullptr, s);
   if (rc) return rc;
   const CascadeIn ci{pacc, pml, plen, nchunk, order};
   dim3 grid(Hkv, B, max_parts);   // partitions slowest: see kDecodeGridNote

@@ -131,6 +131,23 @@ __global__ __launch_bounds__(64 * G * WPH) void flash_prefill_kernel(
       uint4 v = ok ? *reinterpret_cast<const uint4*>(qp + ks * 16 + hh * 8) : make_uint4(0, 0, 0, 0);
       qf[ks] = *reinterpret_cast<bf16x8*>(&v);
     }
+    if constexpr (PFX && D == 128) {
+      // fused RoPE (rotate-half): dim d of fragment ks pairs with d + 64 of fragment ks + 4,
+      // both in this lane; fp32 rotate, bf16 round -- as rope_cache would have stored them
+      if (co.cos_sin && ok) {
+        const float* cs = co.cos_sin + (size_t)co.positions[my_q] * D;
+#pragma unroll
+        for (int ks = 0; ks < NKS / 2; ++ks)
+#pragma unroll
+          for (int j = 0; j < 8; ++j) {
+            const int d = ks * 16 + hh * 8 + j;
+            const float c = cs[d], sn = cs[64 + d];
+            const float x1 = (float)qf[ks][j], x2 = (float)qf[ks + 4][j];
+            qf[ks][j] = (__bf16)(x1 * c - x2 * sn);
+            qf[ks + 4][j] = (__bf16)(x2 * c + x1 * sn);
+          }
+      }
+    }
   }
 
   f32x16 o[NDT];
@@ -381,11 +398,14 @@ int docqa_flash_prefill_paged(const void* qkv, int row_stride, const int* cu_seq
 // KV head): one workgroup per (64 rows, KV head, key chunk), 8 waves.
 int docqa_cascade_prefix(const void* qkv, int row_stride, int rows, int Hq, int Hkv, float scale,
                          const void* k_cache, const void* v_cache, const int* prefix_table,
-                         const int* plen, int BS, int nchunk, float* acc, float* ml, hipStream_t s) {
+                         const int* plen, int BS, int nchunk, float* acc, float* ml,
+                         const int* positions, const float* cos_sin, hipStream_t s) {
   if (rows == 0) return 0;
   if (Hq != 4 * Hkv || BS != 64 || nchunk < 1) return -1;
   PagedKV pk{(const uint16_t*)k_cache, (const uint16_t*)v_cache, prefix_table, 0, nullptr, BS, 6};
-  const CascadeOut co{acc, ml, plen, nchunk, rows};
+  CascadeOut co{acc, ml, plen, nchunk, rows};
+  co.positions = positions;
+  co.cos_sin = cos_sin;
   static const int wph = [] {   // waves per head: 2 (64-row tiles) or 1 (32-row tiles, 2x workgroups)
     const char* e = getenv("DOCQA_CASCADE_WPH");
     return e && atoi(e) == 1 ? 1 : 2;

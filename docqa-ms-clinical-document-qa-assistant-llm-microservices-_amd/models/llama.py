@@ -24,6 +24,7 @@ Reference parity: replaces the Ollama/llama.cpp Mistral-7B generator behind
 from __future__ import annotations
 
 import math
+import os
 from dataclasses import dataclass, field
 
 import torch
@@ -31,6 +32,12 @@ import torch.nn.functional as F
 
 from .. import ops
 from ..parallel import comm
+
+# cascade decode over a library-GEMM QKV: DOCQA_CASCADE_ROPE=1 fuses RoPE + the new
+# token's cache write into the cascade kernels (ops.paged_decode_cascade_rope).  Off by
+# default: measured 2.5 % slower per decode step at batch 256 than the separate rope_cache
+# launch (the ring's fused preamble delays its K/V stream; profiles/r1_cascade_rope_ab.log)
+_CASCADE_ROPE = os.environ.get("DOCQA_CASCADE_ROPE", "0") == "1"
 
 
 @dataclass
@@ -238,12 +245,22 @@ class LlamaModel:
                 if sq:
                     qkv = ops.rope_cache_splitk(ops.dgemm_partial(x, L["qkv"], sq, tq), meta.positions,
                                                 self.cos_sin, meta.slot_mapping, kc, vc, hq, hkv, D)
-                else:
+                    a = ops.paged_decode_cascade(qkv, kc, vc, meta.block_tables, meta.context_lens, hq,
+                                                 meta.max_context, self.scale, meta.shared_table,
+                                                 meta.shared_len, meta.cascade_chunks, meta.seq_order)
+                elif not _CASCADE_ROPE:
                     qkv = lin(x, L["qkv"])
                     ops.rope_cache(qkv, meta.positions, self.cos_sin, meta.slot_mapping, kc, vc, hq, hkv, D)
-                a = ops.paged_decode_cascade(qkv, kc, vc, meta.block_tables, meta.context_lens, hq,
-                                             meta.max_context, self.scale, meta.shared_table,
-                                             meta.shared_len, meta.cascade_chunks, meta.seq_order)
+                    a = ops.paged_decode_cascade(qkv, kc, vc, meta.block_tables, meta.context_lens, hq,
+                                                 meta.max_context, self.scale, meta.shared_table,
+                                                 meta.shared_len, meta.cascade_chunks, meta.seq_order)
+                else:
+                    # library-GEMM QKV: RoPE + new-token cache write fused into the cascade kernels
+                    a = ops.paged_decode_cascade_rope(lin(x, L["qkv"]), meta.positions, self.cos_sin,
+                                                      meta.slot_mapping, kc, vc, meta.block_tables,
+                                                      meta.context_lens, hq, meta.max_context, self.scale,
+                                                      meta.shared_table, meta.shared_len,
+                                                      meta.cascade_chunks, meta.seq_order)
                 qkv = None
             elif sq and ops.fused_decode_ok(kc, meta.block_tables):
                 # QKV partials -> RoPE + new-token cache write + attention, one launch

@@ -325,6 +325,23 @@ def cascade_ok(k_cache, block_tables, Hq: int) -> bool:
             and block_tables.shape[1] <= 256)
 
 
+def paged_decode_cascade_rope(qkv, positions, cos_sin, slot_mapping, k_cache, v_cache, block_tables,
+                              context_lens, Hq, max_context, scale, prefix_table, prefix_len,
+                              nchunk: int = 8, order=None):
+    """Cascade decode over the unrotated packed QKV rows of a library GEMM: RoPE, the new
+    token's paged-cache write and the attention inside the cascade kernels (the prefix
+    kernel rotates queries on load, the ring kernel rotates its queries and writes / attends
+    the new K/V from registers).  ``qkv`` may be rotated in place (fallback path)."""
+    if _gpu(qkv):
+        return _native().paged_decode_cascade_rope(qkv, positions, cos_sin, slot_mapping, k_cache, v_cache,
+                                                   block_tables, context_lens, Hq, max_context, scale,
+                                                   prefix_table, prefix_len, nchunk, order)
+    Hkv, D = k_cache.shape[1], k_cache.shape[3]
+    ref.rope_cache(qkv, positions, cos_sin, slot_mapping, k_cache, v_cache, Hq, Hkv, D)
+    return ref.paged_decode_cascade(qkv, k_cache, v_cache, block_tables, context_lens, Hq, max_context,
+                                    scale, prefix_table, prefix_len, nchunk)
+
+
 def paged_decode_cascade(q, k_cache, v_cache, block_tables, context_lens, Hq, max_context, scale,
                          prefix_table, prefix_len, nchunk: int = 8, order=None):
     """Decode attention with the batch's shared prompt prefix attended once for all rows

@@ -444,6 +444,41 @@ def test_pool_l2(native, mean):
     _close(native.pool_l2(h, cu, mean, True), R.pool_l2(h, cu, mean, True), 1e-4)
 
 
+@pytest.mark.parametrize("B", [37, 256])
+def test_paged_decode_cascade_rope_matches_unfused(native, B):
+    """Fused RoPE + new-token cache write inside the cascade kernels == rope_cache followed
+    by the cascade decode (outputs and the written cache rows; a padded row stays zero)."""
+    Hkv, G, D, BS, maxb, Lp = 8, 4, 128, 64, 16, 192
+    Hq = G * Hkv
+    npb = Lp // BS
+    NB = npb + B * (maxb - npb) + 1
+    kc = torch.randn(NB, Hkv, BS, D, device="cuda", dtype=torch.bfloat16)
+    vc = torch.randn_like(kc)
+    bt = torch.zeros(B, maxb, dtype=torch.int32, device="cuda")
+    bt[:, :npb] = torch.arange(npb, dtype=torch.int32, device="cuda")
+    bt[:, npb:] = (npb + torch.arange(B * (maxb - npb), dtype=torch.int32, device="cuda")).view(B, -1)
+    cl = (Lp + 1 + torch.randint(0, maxb * BS - Lp - 1, (B,), device="cuda")).int()
+    pos = cl - 1
+    slots = (torch.gather(bt, 1, (pos // BS).long()[:, None])[:, 0] * BS + pos % BS).int()
+    cl[3], slots[3] = 0, -1                                   # padded row
+    qkv = (torch.randn(B, (Hq + 2 * Hkv) * D, device="cuda") * 0.5).bfloat16()
+    from docqa_amd.ops import reference as R
+    cs = R.rope_cos_sin(4096, D, 500000.0, "cuda")
+    st = torch.arange(maxb, dtype=torch.int32, device="cuda")
+    pl = torch.tensor([Lp], dtype=torch.int32, device="cuda")
+    scale = 1 / math.sqrt(D)
+    q1, kc1, vc1 = qkv.clone(), kc.clone(), vc.clone()
+    native.rope_cache(q1, pos, cs, slots, kc1, vc1, Hq, Hkv, D)
+    o1 = torch.ops.docqa.paged_decode_cascade(q1, kc1, vc1, bt, cl, Hq, maxb * BS, scale, st, pl, 3)
+    q2, kc2, vc2 = qkv.clone(), kc.clone(), vc.clone()
+    o2 = torch.ops.docqa.paged_decode_cascade_rope(q2, pos, cs, slots, kc2, vc2, bt, cl, Hq, maxb * BS,
+                                                   scale, st, pl, 3)
+    _close(o2, o1, 2e-2, 1e-2)
+    _close(kc2, kc1, 2e-2, 1e-2)
+    _close(vc2, vc1, 0.0)
+    assert o2[3].abs().max().item() == 0
+
+
 @pytest.mark.parametrize("B,Lp,nchunk", [(5, 448, 4), (64, 448, 16), (128, 448, 16), (128, 960, 8),
                                          (200, 192, 1), (64, 0, 8)])
 def test_paged_decode_cascade(native, B, Lp, nchunk):
