@@ -257,6 +257,25 @@ at::Tensor argmax(const at::Tensor& logits) {
   return out;
 }
 
+// fused NER head + argmax: h [T, H] bf16 (row stride may exceed H), w [NL, H] bf16 with
+// NL in {8, 16, 32} (zero-padded label rows), bias [NL] bf16; labels >= n_valid never win
+at::Tensor token_cls_argmax(const at::Tensor& h, const at::Tensor& w, const at::Tensor& bias,
+                            int64_t n_valid) {
+  CHECK_GPU(h); CHECK_GPU(w); CHECK_GPU(bias);
+  CHECK_BF16(h); CHECK_BF16(w); CHECK_BF16(bias);
+  CHECK_CONTIG(w); CHECK_CONTIG(bias);
+  TORCH_CHECK(h.dim() == 2 && h.stride(1) == 1, "token_cls_argmax wants h [T, H] with unit stride");
+  TORCH_CHECK(w.dim() == 2 && w.size(1) == h.size(1), "token_cls_argmax: w [NL, H] must match h");
+  TORCH_CHECK(bias.numel() == w.size(0), "token_cls_argmax: bias [NL]");
+  const int T = h.size(0), H = h.size(1), NL = w.size(0);
+  c10::DeviceGuard g(h.device());
+  auto out = at::empty({T}, h.options().dtype(at::kLong));
+  CHECK_RC(docqa_token_cls_argmax(h.data_ptr(), h.stride(0), w.data_ptr(), bias.data_ptr(), NL,
+                                  (int)n_valid, T, H, out.data_ptr<int64_t>(), stream()),
+           "token_cls_argmax");
+  return out;
+}
+
 at::Tensor sample(const at::Tensor& logits, const at::Tensor& inv_temp, const at::Tensor& top_k,
                   const at::Tensor& top_p, const at::Tensor& u) {
   CHECK_GPU(logits);
@@ -648,6 +667,7 @@ TORCH_LIBRARY(docqa, m) {
   m.def("bert_embed_ln(Tensor ids, Tensor pos, Tensor? token_type, Tensor wte, Tensor wpe, "
         "Tensor wtt, Tensor gamma, Tensor beta, float eps) -> Tensor");
   m.def("argmax(Tensor logits) -> Tensor");
+  m.def("token_cls_argmax(Tensor h, Tensor w, Tensor bias, int n_valid) -> Tensor");
   m.def("decode_slots(Tensor block_tables, Tensor positions, Tensor valid, int BS) -> Tensor");
   m.def("decode_advance(Tensor nxt, Tensor(a!) out, Tensor(b!) tokens, Tensor(c!) positions, Tensor(d!) context_lens, Tensor valid) -> ()");
   m.def("sample(Tensor logits, Tensor inv_temp, Tensor top_k, Tensor top_p, Tensor u) -> Tensor");
@@ -699,6 +719,7 @@ TORCH_LIBRARY_IMPL(docqa, CUDA, m) {
   m.impl("embedding", &embedding);
   m.impl("bert_embed_ln", &bert_embed_ln);
   m.impl("argmax", &argmax);
+  m.impl("token_cls_argmax", &token_cls_argmax);
   m.impl("decode_slots", &decode_slots);
   m.impl("decode_advance", &decode_advance);
   m.impl("sample", &sample);

@@ -31,6 +31,8 @@ int docqa_bert_embed_ln(const int* ids, const int* pos, const int* tt, const voi
                         int T, int H, float eps, hipStream_t s);
 int docqa_argmax(const void* logits, int rows, int V, int ld, int is_bf16, float* ws_v, int* ws_i,
                  int splits, int64_t* out, hipStream_t s);
+int docqa_token_cls_argmax(const void* h, int ldh, const void* w, const void* bias, int n_rows,
+                           int n_valid, int T, int H, int64_t* out, hipStream_t s);
 int docqa_sample(const float* logits, int rows, int V, int ld, const float* inv_temp,
                  const int* top_k, const float* top_p, const float* u, int64_t* out,
                  hipStream_t s);

@@ -348,3 +348,93 @@ int docqa_decode_advance(const int64_t* nxt, int64_t* out, int* tokens, int* pos
   DOCQA_CHECK_LAUNCH();
   return 0;
 }
+
+// token_cls_argmax: the NER token-classification head fused with its argmax
+// (SURVEY.md §2.3 "Token-classification head + argmax"; the deid-service's spaCy NER at
+// deid-service/anonymizer.py:41-45 is replaced by a BERT token classifier).  logits never
+// reach HBM: the [NL, H] head (NL <= 32 label rows, padded) sits in LDS, one 64-wide wave
+// owns a token, each lane dots 8 bf16 of the hidden row per step against every label row
+// (fp32 accumulate), a reduce-scatter butterfly over the labels, and a wave argmax keeps
+// the first maximum (torch.argmax tie rule).  Waves stride over tokens so the head is staged once per block.
+template <int NL>
+__global__ __launch_bounds__(256) void token_cls_argmax_kernel(
+    const uint16_t* __restrict__ h, int ldh, const uint16_t* __restrict__ w,
+    const uint16_t* __restrict__ bias, int n_valid, int T, int H, int64_t* __restrict__ out) {
+  extern __shared__ uint4 w_lds[];  // [NL][H/8]
+  const int H8 = H >> 3;
+  const uint4* wg = reinterpret_cast<const uint4*>(w);
+  for (int i = threadIdx.x; i < NL * H8; i += blockDim.x) w_lds[i] = wg[i];
+  __syncthreads();
+  const int lane = threadIdx.x & 63;
+  const int wave = threadIdx.x >> 6;
+  const int nwaves = gridDim.x * (blockDim.x >> 6);
+  for (int t = blockIdx.x * (blockDim.x >> 6) + wave; t < T; t += nwaves) {
+    const uint4* hr = reinterpret_cast<const uint4*>(h + (size_t)t * ldh);
+    float acc[NL];
+#pragma unroll
+    for (int n = 0; n < NL; ++n) acc[n] = 0.f;
+    for (int c = lane; c < H8; c += 64) {
+      float hf[8];
+      unpack8(hr[c], hf);
+#pragma unroll
+      for (int n = 0; n < NL; ++n) {
+        float wf[8];
+        unpack8(w_lds[n * H8 + c], wf);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) acc[n] = fmaf(hf[j], wf[j], acc[n]);
+      }
+    }
+    // reduce-scatter butterfly: each xor step halves the label array a lane carries
+    // (NL-1 shuffles in total instead of NL full wave_sums), leaving lane `lab`'s label
+    // summed over its lane group; the remaining xor steps finish the sum.
+    int lab = 0;
+#pragma unroll
+    for (int st = 0; (NL >> st) > 1; ++st) {
+      const int half = NL >> (st + 1);
+      const int o = 32 >> st;
+      const bool up = (lane & o) != 0;
+#pragma unroll
+      for (int i = 0; i < half; ++i) {
+        const float send = up ? acc[i] : acc[i + half];
+        const float keep = up ? acc[i + half] : acc[i];
+        acc[i] = keep + __shfl_xor(send, o, 64);
+      }
+      lab = lab * 2 + (up ? 1 : 0);
+    }
+#pragma unroll
+    for (int o = 32 / NL; o >= 1; o >>= 1) acc[0] += __shfl_xor(acc[0], o, 64);
+    float best = lab < n_valid ? acc[0] + bf2f(bias[lab]) : -FLT_MAX;
+    int best_i = lab;
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) {  // wave argmax, lowest label wins ties
+      const float ov = __shfl_xor(best, o, 64);
+      const int oi = __shfl_xor(best_i, o, 64);
+      if (ov > best || (ov == best && oi < best_i)) { best = ov; best_i = oi; }
+    }
+    if (lane == 0) out[t] = best_i;
+  }
+}
+
+int docqa_token_cls_argmax(const void* h, int ldh, const void* w, const void* bias, int n_rows,
+                           int n_valid, int T, int H, int64_t* out, hipStream_t s) {
+  if (T == 0) return 0;
+  if (H % 8 != 0 || ldh % 8 != 0 || n_valid < 1 || n_valid > n_rows) return -1;
+  int nb = (T + 3) / 4;
+  if (nb > 1024) nb = 1024;
+  const auto* hp = static_cast<const uint16_t*>(h);
+  const auto* wp = static_cast<const uint16_t*>(w);
+  const auto* bp = static_cast<const uint16_t*>(bias);
+#define TCA(NL)                                                                             \
+  do {                                                                                      \
+    const size_t lds = (size_t)NL * H * 2;                                                  \
+    if (lds > 64 * 1024) return -1;                                                         \
+    token_cls_argmax_kernel<NL><<<nb, 256, lds, s>>>(hp, ldh, wp, bp, n_valid, T, H, out); \
+  } while (0)
+  if (n_rows == 8) TCA(8);
+  else if (n_rows == 16) TCA(16);
+  else if (n_rows == 32) TCA(32);
+  else return -1;
+#undef TCA
+  DOCQA_CHECK_LAUNCH();
+  return 0;
+}

@@ -23,6 +23,7 @@ Reference parity:
 from __future__ import annotations
 
 import math
+import os
 from dataclasses import dataclass
 
 import torch
@@ -194,7 +195,8 @@ class BertTokenClassifier(BertEncoder):
         g = torch.Generator(device=self.device)
         g.manual_seed(seed + 99)
         n = len(self.labels)
-        npad = (n + 7) // 8 * 8
+        # 8/16/32 label rows: the shapes the fused head+argmax kernel is compiled for
+        npad = next((c for c in (8, 16, 32) if n <= c), (n + 7) // 8 * 8)
         self.cls_w = torch.zeros(npad, cfg.hidden, device=self.device, dtype=dtype)
         self.cls_w[:n].normal_(0.0, 0.02, generator=g)
         self.cls_b = torch.zeros(npad, device=self.device, dtype=dtype)
@@ -203,6 +205,12 @@ class BertTokenClassifier(BertEncoder):
     @torch.inference_mode()
     def predict_packed(self, ids, cu_seqlens, max_len) -> torch.Tensor:
         h = self.hidden_states(ids, cu_seqlens, max_len)
+        if (self.cls_w.shape[0] <= 32 and h.dtype == torch.bfloat16
+                and os.environ.get("DOCQA_NER_FUSED", "0") == "1"):
+            # fused head + argmax (embed_sample.hip): the [T, labels] logits never hit HBM.
+            # Opt-in: measured at parity with hipBLASLt + argmax on clinical-bert (batch 256:
+            # 14.60 vs 14.46-14.51 ms, profiles/r1_bench_deid_fused_ab.json)
+            return ops.token_cls_argmax(h, self.cls_w, self.cls_b, len(self.labels))
         logits = F.linear(h, self.cls_w, self.cls_b)
         return ops.argmax(logits)  # [T] label ids
 

@@ -299,6 +299,13 @@ def argmax(logits):
     return ref.argmax(logits)
 
 
+def token_cls_argmax(h, w, bias, n_valid: int):
+    """Fused token-classification head + argmax: argmax_n(h @ w[:n_valid].T + bias)."""
+    if _gpu(h):
+        return _native().token_cls_argmax(h, w, bias, int(n_valid))
+    return ref.token_cls_argmax(h, w, bias, n_valid)
+
+
 def sample(logits, inv_temp, top_k, top_p, u):
     if _gpu(logits):
         return _native().sample(logits.float().contiguous(), inv_temp, top_k, top_p, u)

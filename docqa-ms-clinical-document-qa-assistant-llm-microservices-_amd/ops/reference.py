@@ -124,6 +124,11 @@ def argmax(logits):
     return logits.float().argmax(dim=-1)
 
 
+def token_cls_argmax(h, w, bias, n_valid):
+    logits = h.float() @ w[:n_valid].float().t() + bias[:n_valid].float()
+    return logits.argmax(dim=-1)
+
+
 def sample(logits, inv_temp, top_k, top_p, u):
     out = torch.empty(logits.shape[0], dtype=torch.long, device=logits.device)
     for r in range(logits.shape[0]):

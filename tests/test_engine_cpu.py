@@ -181,3 +181,18 @@ def test_lpt_dispatch_order_and_decode_state_ops():
     ops.decode_advance(torch.tensor([11, 12]), out, tok, pos, ctx, valid)
     assert out.tolist() == [11, 12] and tok.tolist() == [11, 12]
     assert pos.tolist() == [18, 3] and ctx.tolist() == [19, 4]
+
+
+def test_token_cls_argmax_reference_cpu():
+    """CPU path of the fused NER head + argmax: padded label rows never win."""
+    import torch
+
+    from docqa_amd import ops
+
+    h = torch.randn(33, 64)
+    w = torch.zeros(16, 64)
+    w[:9] = torch.randn(9, 64)
+    b = torch.zeros(16)
+    b[9:] = 1e9  # would win if the padded rows were not excluded
+    got = ops.token_cls_argmax(h, w, b, 9)
+    assert torch.equal(got, (h @ w[:9].t() + b[:9]).argmax(-1))

@@ -115,6 +115,28 @@ def test_argmax(native, V, dtype):
     assert torch.equal(native.argmax(x).cpu(), x.float().argmax(-1).cpu())
 
 
+@pytest.mark.parametrize("T,H,NL,nv", [(1, 384, 8, 5), (257, 768, 16, 9), (5000, 768, 16, 9),
+                                        (64, 1024, 32, 31)])
+def test_token_cls_argmax(native, T, H, NL, nv):
+    # fused NER head + argmax vs the fp32 reference of the same op; h has a padded row
+    # stride like a slice of a wider activation buffer
+    g = torch.Generator(device="cuda").manual_seed(T + NL)
+    hbuf = torch.randn(T, H + 64, device="cuda", generator=g).bfloat16()
+    h = hbuf[:, :H]
+    w = torch.zeros(NL, H, device="cuda", dtype=torch.bfloat16)
+    w[:nv] = (torch.randn(nv, H, device="cuda", generator=g) * 0.05).bfloat16()
+    b = torch.full((NL,), -1e4, device="cuda").bfloat16()
+    b[:nv] = (torch.randn(nv, device="cuda", generator=g) * 0.1).bfloat16()
+    got = native.token_cls_argmax(h, w, b, nv).cpu()
+    logits = (h.float() @ w[:nv].float().t() + b[:nv].float()).cpu()
+    want = logits.argmax(-1)
+    top2 = logits.topk(2, dim=-1).values
+    ambiguous = (top2[:, 0] - top2[:, 1]) < 1e-4
+    assert got.shape == (T,) and got.dtype == torch.int64
+    assert int(got.max()) < nv
+    assert torch.equal(got[~ambiguous], want[~ambiguous])
+
+
 def test_sample_greedy_limit(native):
     # top_k=1 must reproduce argmax whatever u is
     x = torch.randn(8, 5000, device="cuda")

@@ -195,3 +195,26 @@ def test_checkpoint_roundtrip_generates_identically(native, tmp_path):
     a = LLMEngine(m, max_batch=4, max_context=256).generate(prompts, sp)
     b = LLMEngine(m2, max_batch=4, max_context=256).generate(prompts, sp)
     assert a == b
+
+
+def test_token_classifier_fused_head_matches_unfused(native, monkeypatch):
+    """NER predict (fused head+argmax kernel) == F.linear + argmax on the same hidden states."""
+    monkeypatch.setenv("DOCQA_NER_FUSED", "1")
+    from docqa_amd.deid.engine import NER_LABELS
+    from docqa_amd.models.bert import BertConfig, BertTokenClassifier, pack
+
+    clf = BertTokenClassifier(BertConfig.preset("clinical-bert"), NER_LABELS, device="cuda", seed=3)
+    assert clf.cls_w.shape[0] == 16
+    g = torch.Generator().manual_seed(0)
+    toks = [torch.randint(1000, 20000, (n,), generator=g).tolist() for n in (7, 130, 256, 33)]
+    ids, cu, max_len = pack(toks, clf.cfg.max_seq_len, clf.device)
+    got = clf.predict_packed(ids, cu, max_len)
+    with torch.inference_mode():
+        h = clf.hidden_states(ids, cu, max_len)
+        logits = (h.float() @ clf.cls_w[:len(NER_LABELS)].float().t()
+                  + clf.cls_b[:len(NER_LABELS)].float())
+    top2 = logits.topk(2, dim=-1).values
+    clear = (top2[:, 0] - top2[:, 1]) > 1e-3
+    assert got.shape == (ids.numel(),)
+    assert torch.equal(got[clear].cpu(), logits.argmax(-1)[clear].cpu())
+    assert clear.float().mean().item() > 0.95
