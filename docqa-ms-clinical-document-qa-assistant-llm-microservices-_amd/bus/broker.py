@@ -214,6 +214,11 @@ class InProcBroker:
         with q.cv:
             return len(q.ready)
 
+    @staticmethod
+    def persistent_properties() -> Properties:
+        """Message properties for a persistent publish (every in-proc message is)."""
+        return Properties(delivery_mode=2)
+
     def channel(self) -> InProcChannel:
         return InProcChannel(self)
 
@@ -347,6 +352,8 @@ class SpoolBroker:
         self.declare(queue)
         return len(os.listdir(self._dirs(queue)[0]))
 
+    persistent_properties = staticmethod(InProcBroker.persistent_properties)
+
     def channel(self) -> SpoolChannel:
         return SpoolChannel(self)
 
@@ -358,9 +365,36 @@ class SpoolBroker:
         return got[1]
 
 
+class _AmqpChannel:
+    """A pika channel that owns its BlockingConnection: ``close()`` closes both, so a
+    consumer loop (or a failed one, before the reconnect) never leaks a connection."""
+
+    def __init__(self, conn):
+        self._conn = conn
+        self._ch = conn.channel()
+
+    def __getattr__(self, name):
+        return getattr(self._ch, name)
+
+    def close(self):  # pragma: no cover - needs a broker
+        try:
+            if self._ch.is_open:
+                self._ch.close()
+        finally:
+            if self._conn.is_open:
+                self._conn.close()
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+
 class AmqpBroker:
-    """RabbitMQ via pika (only when pika is importable).  Opens one connection per
-    publisher call like the reference (doc-ingestor/processing.py:21-44)."""
+    """RabbitMQ via pika (only when pika is importable).  ``publish`` opens one connection
+    per message, publishes persistently and closes it, like the reference
+    (doc-ingestor/processing.py:21-44); ``channel()`` is for long-lived consumers."""
 
     def __init__(self, host: str = "localhost"):
         try:
@@ -368,6 +402,12 @@ class AmqpBroker:
         except ImportError as e:  # pragma: no cover - pika is absent in CI
             raise RuntimeError("AMQP backend requested but pika is not installed") from e
         self.host = host
+
+    @staticmethod
+    def persistent_properties():  # pragma: no cover
+        import pika
+
+        return pika.BasicProperties(delivery_mode=2)
 
     def publish(self, queue: str, body: bytes) -> None:  # pragma: no cover
         import pika
@@ -384,8 +424,7 @@ class AmqpBroker:
     def channel(self):  # pragma: no cover
         import pika
 
-        conn = pika.BlockingConnection(pika.ConnectionParameters(host=self.host))
-        return conn.channel()
+        return _AmqpChannel(pika.BlockingConnection(pika.ConnectionParameters(host=self.host)))
 
 
 _default: InProcBroker | None = None

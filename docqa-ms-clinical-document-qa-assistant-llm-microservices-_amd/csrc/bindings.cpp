@@ -18,6 +18,9 @@ hipStream_t stream() { return c10::hip::getCurrentHIPStream().stream(); }
 #define CHECK_BF16(t) TORCH_CHECK((t).scalar_type() == at::kBFloat16, #t " must be bfloat16")
 #define CHECK_I32(t) TORCH_CHECK((t).scalar_type() == at::kInt, #t " must be int32")
 #define CHECK_CONTIG(t) TORCH_CHECK((t).is_contiguous(), #t " must be contiguous")
+#define CHECK_ALIGN16(t) \
+  TORCH_CHECK((reinterpret_cast<uintptr_t>((t).data_ptr()) & 15u) == 0, \
+              #t " must be 16-byte aligned (storage offset a multiple of 16 bytes)")
 // DOCQA_KERNEL_DEBUG=1: synchronous kernel checking (the HIP_LAUNCH_BLOCKING of this
 // extension): after every op that is not being graph-captured, the stream
 // is synchronised and any asynchronous fault is reported with the op's name -- a
@@ -267,6 +270,7 @@ at::Tensor token_cls_argmax(const at::Tensor& h, const at::Tensor& w, const at::
   TORCH_CHECK(h.dim() == 2 && h.stride(1) == 1, "token_cls_argmax wants h [T, H] with unit stride");
   TORCH_CHECK(w.dim() == 2 && w.size(1) == h.size(1), "token_cls_argmax: w [NL, H] must match h");
   TORCH_CHECK(bias.numel() == w.size(0), "token_cls_argmax: bias [NL]");
+  CHECK_ALIGN16(h); CHECK_ALIGN16(w); CHECK_ALIGN16(bias);
   const int T = h.size(0), H = h.size(1), NL = w.size(0);
   c10::DeviceGuard g(h.device());
   auto out = at::empty({T}, h.options().dtype(at::kLong));
@@ -489,7 +493,7 @@ at::Tensor dgemm_glu(const at::Tensor& x, const at::Tensor& w) {
   const int K = x.size(-1), N = w.size(0);
   TORCH_CHECK(w.size(1) == K && N % 16 == 0, "dgemm_glu: shape mismatch");
   const int M = x.numel() / K;
-  TORCH_CHECK(M <= 128, "dgemm_glu: at most 128 rows");
+  TORCH_CHECK(M <= 256, "dgemm_glu: at most 256 rows");
   auto sizes = x.sizes().vec();
   sizes.back() = N / 2;
   c10::DeviceGuard g(x.device());
@@ -504,7 +508,7 @@ at::Tensor dgemm_partial(const at::Tensor& x, const at::Tensor& w, int64_t split
   const int K = x.size(-1), N = w.size(0);
   TORCH_CHECK(w.size(1) == K, "dgemm_partial: K mismatch");
   const int M = x.numel() / K;
-  TORCH_CHECK(M <= 192 && splits >= 1, "dgemm_partial: at most 192 rows, splits >= 1");
+  TORCH_CHECK(M <= 256 && splits >= 1, "dgemm_partial: at most 256 rows, splits >= 1");
   c10::DeviceGuard g(x.device());
   auto part = at::empty({splits, M, N}, x.options().dtype(at::kFloat));
   CHECK_RC(docqa_dgemm_partial(x.data_ptr(), w.data_ptr(), part.data_ptr<float>(), M, N, K, (int)splits,
@@ -517,7 +521,7 @@ at::Tensor dgemm(const at::Tensor& x, const at::Tensor& w, int64_t splits) {
   const int K = x.size(-1), N = w.size(0);
   TORCH_CHECK(w.size(1) == K, "dgemm: K mismatch");
   const int M = x.numel() / K;
-  TORCH_CHECK(M <= 192, "dgemm: at most 192 rows");
+  TORCH_CHECK(M <= 256, "dgemm: at most 256 rows");
   const int S = splits > 0 ? (int)splits : docqa_dgemm_splits(N, K);
   auto sizes = x.sizes().vec();
   sizes.back() = N;

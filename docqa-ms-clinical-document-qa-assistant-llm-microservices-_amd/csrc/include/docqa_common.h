@@ -97,5 +97,12 @@ __device__ __forceinline__ int xcd_remap(int orig, int nwg) {
 
 }  // namespace docqa
 
+// 16-byte alignment of an operand a kernel reads or writes with uint4 / float4 accesses:
+// host launchers refuse misaligned views (a storage offset that is not a multiple of
+// 8 bf16 / 4 fp32 elements) instead of faulting on the GPU
+static inline bool docqa_aligned16(const void* p) {
+  return (reinterpret_cast<uintptr_t>(p) & 15u) == 0;
+}
+
 #define DOCQA_CHECK_LAUNCH() \
   do { hipError_t e__ = hipGetLastError(); if (e__ != hipSuccess) return (int)e__; } while (0)

@@ -258,7 +258,7 @@ __global__ __launch_bounds__(256) void sample_kernel(const float* __restrict__ l
 
 int docqa_embedding(const int* ids, const void* table, void* out, int T, int H, int V, hipStream_t s) {
   if (T == 0) return 0;
-  if (H % 8 != 0) return -1;
+  if (H % 8 != 0 || !docqa_aligned16(table) || !docqa_aligned16(out)) return -1;
   embedding_gather_kernel<<<T, 256, 0, s>>>(ids, (const uint16_t*)table, (uint16_t*)out, H, V);
   DOCQA_CHECK_LAUNCH();
   return 0;
@@ -268,7 +268,8 @@ int docqa_bert_embed_ln(const int* ids, const int* pos, const int* tt, const voi
                         const void* wpe, const void* wtt, const void* g, const void* b, void* out,
                         int T, int H, float eps, hipStream_t s) {
   if (T == 0) return 0;
-  if (H % 8 != 0) return -1;
+  if (H % 8 != 0 || !docqa_aligned16(wte) || !docqa_aligned16(wpe) || !docqa_aligned16(wtt) ||
+      !docqa_aligned16(g) || !docqa_aligned16(b) || !docqa_aligned16(out)) return -1;
   const int nv = (H / 8 + 63) / 64;
   dim3 grid((T + 3) / 4);
 #define BE(N) bert_embed_ln_kernel<N><<<grid, 256, 0, s>>>(ids, pos, tt, (const uint16_t*)wte, (const uint16_t*)wpe, (const uint16_t*)wtt, (const uint16_t*)g, (const uint16_t*)b, (uint16_t*)out, T, H, eps)
@@ -283,6 +284,7 @@ int docqa_argmax(const void* logits, int rows, int V, int ld, int is_bf16, float
   if (rows == 0) return 0;
   if (is_bf16 && (V % 8 != 0 || ld % 8 != 0)) return -1;
   if (!is_bf16 && (ld % 4 != 0)) return -1;
+  if (!docqa_aligned16(logits)) return -1;
   dim3 g1(splits, rows);
   if (is_bf16) argmax_pass1<true><<<g1, 256, 0, s>>>(logits, V, ld, splits, ws_v, ws_i);
   else argmax_pass1<false><<<g1, 256, 0, s>>>(logits, V, ld, splits, ws_v, ws_i);
@@ -419,6 +421,7 @@ int docqa_token_cls_argmax(const void* h, int ldh, const void* w, const void* bi
                            int n_valid, int T, int H, int64_t* out, hipStream_t s) {
   if (T == 0) return 0;
   if (H % 8 != 0 || ldh % 8 != 0 || n_valid < 1 || n_valid > n_rows) return -1;
+  if (!docqa_aligned16(h) || !docqa_aligned16(w) || !docqa_aligned16(bias)) return -1;
   int nb = (T + 3) / 4;
   if (nb > 1024) nb = 1024;
   const auto* hp = static_cast<const uint16_t*>(h);

@@ -12,36 +12,87 @@ the CPU.  Documents longer than the encoder window are split into overlapping wi
 """
 from __future__ import annotations
 
+import json
+import os
 from dataclasses import dataclass
 
 from ..utils import tracing
 from .recognizers import ENTITIES, Span, context_spans, pattern_spans, resolve_overlaps
 
 NER_LABELS = ["O", "B-PER", "I-PER", "B-LOC", "I-LOC", "B-NRP", "I-NRP", "B-DATE", "I-DATE"]
-_LABEL_ENTITY = {"PER": "PERSON", "LOC": "LOCATION", "NRP": "NRP", "DATE": "DATE_TIME"}
+
+# Checkpoint label type -> Presidio entity (the six entities of
+# deid-service/anonymizer.py:43 plus the usual extra NER types).  Real token-classifier
+# checkpoints bring their own id2label (models/checkpoint.py:load_bert_token_classifier),
+# so both the CoNLL short forms (PER/LOC) and the Presidio / OntoNotes / i2b2 long forms
+# are accepted.  Types mapped to None, and types missing from the table, are treated as
+# "O" (skipped) rather than raising.  Extend or override with DOCQA_NER_LABEL_MAP='{"TYPE":
+# "ENTITY", ...}' or the ``label_map`` argument of :class:`DeidEngine`.
+DEFAULT_LABEL_ENTITY: dict[str, str | None] = {
+    "PER": "PERSON", "PERSON": "PERSON", "NAME": "PERSON", "PATIENT": "PERSON",
+    "DOCTOR": "PERSON", "STAFF": "PERSON", "USERNAME": "PERSON",
+    "LOC": "LOCATION", "LOCATION": "LOCATION", "GPE": "LOCATION", "CITY": "LOCATION",
+    "STATE": "LOCATION", "COUNTRY": "LOCATION", "STREET": "LOCATION", "ZIP": "LOCATION",
+    "FAC": "LOCATION", "HOSPITAL": "LOCATION", "ADDRESS": "LOCATION",
+    "NRP": "NRP", "NORP": "NRP",
+    "DATE": "DATE_TIME", "DATE_TIME": "DATE_TIME", "TIME": "DATE_TIME", "AGE": None,
+    "PHONE": "PHONE_NUMBER", "PHONE_NUMBER": "PHONE_NUMBER", "FAX": "PHONE_NUMBER",
+    "EMAIL": "EMAIL_ADDRESS", "EMAIL_ADDRESS": "EMAIL_ADDRESS",
+    "ORG": "ORGANIZATION", "ORGANIZATION": "ORGANIZATION",
+    "MISC": None,
+}
 
 
-def bio_to_spans(labels: list[str], offsets: list[tuple[int, int]], score: float = 0.85) -> list[Span]:
-    """BIO tag sequence + token char offsets -> entity spans (I- without B- opens a span)."""
+def label_entity_map(overrides: dict | None = None) -> dict[str, str | None]:
+    """The default table, updated from ``DOCQA_NER_LABEL_MAP`` (JSON) and ``overrides``."""
+    table = dict(DEFAULT_LABEL_ENTITY)
+    env = os.environ.get("DOCQA_NER_LABEL_MAP")
+    if env:
+        table.update({str(k).upper(): v for k, v in json.loads(env).items()})
+    if overrides:
+        table.update({str(k).upper(): v for k, v in overrides.items()})
+    return table
+
+
+def _split_label(lab: str) -> tuple[str, str]:
+    """'B-PER' -> ('B', 'PER'); BIOES 'S-'/'E-'/'L-'/'U-' prefixes map onto B/I;
+    an un-prefixed type (IO scheme) continues the open span."""
+    if len(lab) > 2 and lab[1] in "-_" and lab[0] in "BIESLU":
+        tag, typ = lab[0], lab[2:]
+        return ("B" if tag in "BSU" else "I"), typ
+    return "I", lab
+
+
+def bio_to_spans(labels: list[str], offsets: list[tuple[int, int]], score: float = 0.85,
+                 label_map: dict[str, str | None] | None = None) -> list[Span]:
+    """BIO tag sequence + token char offsets -> entity spans (I- without B- opens a span).
+    Types the label map does not name (or maps to None) close any open span and are
+    skipped, like "O"."""
+    table = DEFAULT_LABEL_ENTITY if label_map is None else label_map
     spans: list[Span] = []
-    cur_type, cur_start, cur_end = None, 0, 0
+    cur_ent, cur_type, cur_start, cur_end = None, None, 0, 0
+
+    def close():
+        if cur_ent:
+            spans.append(Span(cur_start, cur_end, cur_ent, score))
+
     for lab, (s, e) in zip(labels, offsets):
         if s == e:  # special token
             continue
-        if lab == "O":
-            if cur_type:
-                spans.append(Span(cur_start, cur_end, _LABEL_ENTITY[cur_type], score))
-                cur_type = None
+        ent = None
+        if lab != "O":
+            tag, typ = _split_label(lab)
+            ent = table.get(typ.upper())
+        if ent is None:
+            close()
+            cur_ent = cur_type = None
             continue
-        tag, typ = lab.split("-", 1)
         if tag == "B" or typ != cur_type:
-            if cur_type:
-                spans.append(Span(cur_start, cur_end, _LABEL_ENTITY[cur_type], score))
-            cur_type, cur_start, cur_end = typ, s, e
+            close()
+            cur_ent, cur_type, cur_start, cur_end = ent, typ, s, e
         else:
             cur_end = e
-    if cur_type:
-        spans.append(Span(cur_start, cur_end, _LABEL_ENTITY[cur_type], score))
+    close()
     return spans
 
 
@@ -55,8 +106,9 @@ class AnalyzerResult:
 
 class DeidEngine:
     def __init__(self, ner_model=None, tokenizer=None, use_model: bool = False,
-                 window: int = 256, stride: int = 192):
+                 window: int = 256, stride: int = 192, label_map: dict | None = None):
         self.ner = ner_model
+        self.label_map = label_entity_map(label_map)
         self.tok = tokenizer
         self.use_model = use_model and ner_model is not None and tokenizer is not None
         self.window = window
@@ -83,7 +135,7 @@ class DeidEngine:
         out: list[list[Span]] = [[] for _ in texts]
         for (ids, offs), owner, p in zip(windows, owners, preds):
             labels = [self.ner.labels[i] if i < len(self.ner.labels) else "O" for i in p[1:-1]]
-            out[owner] += bio_to_spans(labels, list(offs))
+            out[owner] += bio_to_spans(labels, list(offs), label_map=self.label_map)
         return out
 
     def analyze_batch(self, texts: list[str], entities=None) -> list[list[AnalyzerResult]]:

@@ -114,6 +114,10 @@ class LLMEngine:
         self.block_size = block_size
         self.max_blocks_per_seq = (max_context + block_size - 1) // block_size
         self.max_context = self.max_blocks_per_seq * block_size
+        sw = getattr(model.cfg, "sliding_window", None)
+        if sw is not None and self.max_context > sw:
+            raise ValueError(f"max_context {self.max_context} exceeds the model's sliding window {sw}: "
+                             "the attention kernels attend to the whole context")
         self.max_prefill_tokens = max_prefill_tokens
         if num_blocks is None:
             num_blocks = max_batch * self.max_blocks_per_seq + 1

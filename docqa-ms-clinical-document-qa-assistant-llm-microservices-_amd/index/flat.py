@@ -68,6 +68,31 @@ class FlatIndex:
         with self._lock:
             self.ntotal = 0
 
+    def replace(self, x, before_swap=None) -> None:
+        """Replace the whole content with ``x`` [n, d] without an empty or partial
+        intermediate state: the new storage is built off to the side, then swapped in
+        under the lock (``before_swap()``, e.g. a metadata swap, runs under the same
+        lock), so a concurrent search sees either the old or the new index."""
+        x = torch.as_tensor(x)
+        if x.dim() == 1:
+            x = x[None]
+        if x.numel() and x.shape[1] != self.d:
+            raise ValueError(f"dimension mismatch: {x.shape[1]} != {self.d}")
+        n = x.shape[0] if x.numel() else 0
+        cap = max(1024, n)
+        xb = torch.empty(cap, self.d, device=self.device, dtype=self.storage_dtype)
+        nm = torch.empty(cap, device=self.device, dtype=torch.float32)
+        if n:
+            stored = x.to(self.device, dtype=torch.float32).to(self.storage_dtype)
+            xb[:n] = stored
+            nm[:n] = (stored.float() ** 2).sum(1)
+        if self.device.type == "cuda":
+            torch.cuda.current_stream(self.device).synchronize()
+        with self._lock:
+            if before_swap is not None:
+                before_swap()
+            self._xb, self._norms, self.ntotal = xb, nm, n
+
     # ------------------------------------------------------------------ query
     @property
     def xb(self) -> torch.Tensor:

@@ -62,10 +62,15 @@ class IndexFollower:
             threading.Event().wait(0.05)
         else:
             raise RuntimeError("index snapshot kept changing under the reader")
-        self.index.reset()
-        self.metadata[:] = meta
-        if n:
-            self.index.add(torch.from_numpy(data.xb))
+        # the llm-qa prep thread searches this index concurrently: build the new vectors
+        # off to the side and swap vectors + metadata together under the index lock, so a
+        # search never sees an empty or half-loaded index (nor ids without records)
+        xb = torch.from_numpy(data.xb) if n else torch.empty(0, self.index.d)
+
+        def swap_meta():
+            self.metadata[:] = meta
+
+        self.index.replace(xb, before_swap=swap_meta)
         self._marker = mk
         self.last_seq = mk["wal_seq"]
         self._offset = 0

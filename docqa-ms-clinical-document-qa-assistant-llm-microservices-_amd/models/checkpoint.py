@@ -19,6 +19,7 @@ from pathlib import Path
 
 import torch
 
+from ..ops import reference as ref
 from .bert import BertConfig, BertEncoder, BertTokenClassifier
 from .llama import LlamaConfig, LlamaModel
 
@@ -66,7 +67,26 @@ def is_checkpoint(name_or_path) -> bool:
 
 
 # --------------------------------------------------------------------------- Llama
+# decoder families whose weights map 1:1 onto models/llama.py (Mistral-7B is the
+# reference's generator, llm-qa/main.py:69; Llama-3 the BASELINE.json one)
+SUPPORTED_DECODERS = ("llama", "mistral")
+
+
 def llama_config_from_hf(hf: dict, name: str = "hf") -> LlamaConfig:
+    """Hugging Face config.json -> :class:`LlamaConfig`.  Refuses what the decoder would
+    otherwise load silently wrong: other model types (e.g. Qwen2 with q/k/v biases),
+    ``attention_bias`` / ``mlp_bias``, and unsupported ``rope_scaling`` types."""
+    mt = hf.get("model_type", "llama")
+    if mt not in SUPPORTED_DECODERS:
+        raise NotImplementedError(f"model_type {mt!r} is not supported (supported: {SUPPORTED_DECODERS})")
+    for flag in ("attention_bias", "mlp_bias"):
+        if hf.get(flag):
+            raise NotImplementedError(f"{flag}=true checkpoints are not supported (no bias terms in the decoder)")
+    if hf.get("hidden_act", "silu") not in ("silu", "swish"):
+        raise NotImplementedError(f"hidden_act {hf['hidden_act']!r} is not supported (SwiGLU only)")
+    scaling = hf.get("rope_scaling") or None
+    if scaling is not None:
+        ref.rope_inv_freq(8, 10000.0, scaling)   # raises on an unsupported type / missing keys
     heads = hf["num_attention_heads"]
     eos = hf.get("eos_token_id", 128009)
     if isinstance(eos, list):
@@ -78,7 +98,8 @@ def llama_config_from_hf(hf: dict, name: str = "hf") -> LlamaConfig:
                        rope_theta=float(hf.get("rope_theta", 10000.0)),
                        rms_eps=float(hf.get("rms_norm_eps", 1e-5)),
                        max_position=hf.get("max_position_embeddings", 8192),
-                       bos_token_id=hf.get("bos_token_id", 128000), eos_token_id=eos)
+                       bos_token_id=hf.get("bos_token_id", 128000), eos_token_id=eos,
+                       rope_scaling=scaling, sliding_window=hf.get("sliding_window"))
 
 
 def llama_config_to_hf(cfg: LlamaConfig) -> dict:
@@ -88,7 +109,9 @@ def llama_config_to_hf(cfg: LlamaConfig) -> dict:
             "num_attention_heads": cfg.heads, "num_key_value_heads": cfg.kv_heads,
             "head_dim": cfg.head_dim, "rope_theta": cfg.rope_theta, "rms_norm_eps": cfg.rms_eps,
             "max_position_embeddings": cfg.max_position, "bos_token_id": cfg.bos_token_id,
-            "eos_token_id": cfg.eos_token_id, "torch_dtype": "bfloat16", "tie_word_embeddings": False}
+            "eos_token_id": cfg.eos_token_id, "torch_dtype": "bfloat16", "tie_word_embeddings": False,
+            "rope_scaling": cfg.rope_scaling, "attention_bias": False, "mlp_bias": False,
+            "hidden_act": "silu"}
 
 
 def load_llama(path, device="cuda", dtype=torch.bfloat16) -> LlamaModel:

@@ -55,6 +55,11 @@ class LlamaConfig:
     max_position: int = 8192
     bos_token_id: int = 128000
     eos_token_id: int = 128009
+    # Hugging Face rope_scaling dict (None, "linear" or "llama3"; ops.reference.rope_inv_freq)
+    rope_scaling: dict | None = None
+    # Mistral-style sliding-window attention span (None = full causal attention); the
+    # engine refuses a context longer than the window since its kernels attend to all of it
+    sliding_window: int | None = None
 
     @staticmethod
     def preset(name: str) -> "LlamaConfig":
@@ -118,7 +123,8 @@ class LlamaModel:
         self.vocab_shard = (cfg.vocab_size + self.tp - 1) // self.tp
         self.vocab_start = self.tp_rank * self.vocab_shard
         self.scale = 1.0 / math.sqrt(cfg.head_dim)
-        self.cos_sin = ops.rope_cos_sin(cfg.max_position, cfg.head_dim, cfg.rope_theta, self.device)
+        self.cos_sin = ops.rope_cos_sin(cfg.max_position, cfg.head_dim, cfg.rope_theta, self.device,
+                                        scaling=cfg.rope_scaling)
         self.layers: list[dict] = []
         if init:
             self._random_init(seed)

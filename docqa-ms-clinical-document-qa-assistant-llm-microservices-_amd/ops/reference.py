@@ -36,9 +36,41 @@ def layernorm(x, residual, gamma, beta, eps):
     return F.layer_norm(xf, (x.shape[-1],), gamma.float(), beta.float(), eps).to(x.dtype)
 
 
-def rope_cos_sin(max_pos: int, head_dim: int, theta: float, device=None) -> torch.Tensor:
+def rope_inv_freq(head_dim: int, theta: float, scaling: dict | None = None) -> torch.Tensor:
+    """fp64 RoPE inverse frequencies, with Hugging Face ``rope_scaling`` applied.
+
+    * ``None`` / ``"default"``: theta^(-2i/d).
+    * ``"linear"``: every frequency divided by ``factor`` (position interpolation).
+    * ``"llama3"`` (Llama-3.1 / 3.2): wavelengths longer than
+      ``original_max_position_embeddings / low_freq_factor`` are divided by ``factor``,
+      shorter than ``.../high_freq_factor`` kept, and the band between is blended with
+      ``s = (L_orig / wavelen - low) / (high - low)``: ``(1 - s) * f / factor + s * f``.
+    Anything else raises: a checkpoint must not load with silently wrong positions."""
+    inv = 1.0 / (theta ** (torch.arange(0, head_dim, 2, dtype=torch.float64) / head_dim))
+    if not scaling:
+        return inv
+    kind = scaling.get("rope_type", scaling.get("type", "default"))
+    if kind == "default":
+        return inv
+    factor = float(scaling["factor"])
+    if kind == "linear":
+        return inv / factor
+    if kind == "llama3":
+        low, high = float(scaling["low_freq_factor"]), float(scaling["high_freq_factor"])
+        orig = float(scaling["original_max_position_embeddings"])
+        wavelen = 2 * math.pi / inv
+        scaled = torch.where(wavelen > orig / low, inv / factor, inv)
+        smooth = (orig / wavelen - low) / (high - low)
+        blended = (1 - smooth) * scaled / factor + smooth * scaled
+        medium = (wavelen >= orig / high) & (wavelen <= orig / low)
+        return torch.where(medium, blended, scaled)
+    raise NotImplementedError(f"rope_scaling type {kind!r} is not supported")
+
+
+def rope_cos_sin(max_pos: int, head_dim: int, theta: float, device=None,
+                 scaling: dict | None = None) -> torch.Tensor:
     """fp32 table [max_pos, head_dim]: first half cos, second half sin (rotate-half RoPE)."""
-    inv_freq = 1.0 / (theta ** (torch.arange(0, head_dim, 2, dtype=torch.float64) / head_dim))
+    inv_freq = rope_inv_freq(head_dim, theta, scaling)
     t = torch.arange(max_pos, dtype=torch.float64)
     freqs = torch.outer(t, inv_freq)
     return torch.cat([freqs.cos(), freqs.sin()], dim=-1).float().to(device)

@@ -53,7 +53,8 @@ class DeidWorker:
             logger.info("[->] doc %s (%d chars)", doc_id, len(raw))
             out = self.clean_message(message, self.engine.process_text_anonymization(raw))
             ch.queue_declare(queue=self.out_q, durable=True)
-            ch.basic_publish(exchange="", routing_key=self.out_q, body=json.dumps(out))
+            ch.basic_publish(exchange="", routing_key=self.out_q, body=json.dumps(out),
+                             properties=self.broker.persistent_properties())
             ch.basic_ack(delivery_tag=method.delivery_tag)
             self.processed += 1
             logger.info("[<-] doc %s anonymised -> %s", doc_id, self.out_q)
@@ -66,6 +67,7 @@ class DeidWorker:
 
     def run_forever(self, retry_s: float = 5.0) -> None:
         while True:
+            ch = None
             try:
                 ch = self.broker.channel()
                 self._ch = ch
@@ -79,7 +81,21 @@ class DeidWorker:
                 return
             except Exception as e:  # noqa: BLE001 - broker unavailable: retry
                 logger.warning("broker unavailable (%s); retrying in %.0fs", e, retry_s)
+                self._close_channel(ch)
+                ch = None
                 time.sleep(retry_s)
+            finally:
+                self._close_channel(ch)
+
+    @staticmethod
+    def _close_channel(ch) -> None:
+        """Close a consumer channel (and, under AMQP, its connection) before reconnecting."""
+        if ch is None:
+            return
+        try:
+            ch.close()
+        except Exception:  # noqa: BLE001 - already broken
+            pass
 
     def start(self) -> "DeidWorker":
         self._thread = threading.Thread(target=self.run_forever, name="deid-worker", daemon=True)

@@ -31,10 +31,12 @@ from .multipart import FilePart, parse_multipart
 
 
 def publish_to_queue(broker, queue: str, doc_id: int, text: str, metadata: dict) -> None:
+    """One persistent message on the durable ``queue`` (doc-ingestor/processing.py:21-44).
+
+    ``broker.publish`` declares the queue, sets ``delivery_mode=2`` and, for AMQP, closes
+    the connection it opened, like the reference; no channel is left open per upload."""
     body = json.dumps({"doc_id": doc_id, "text": text, "metadata": metadata})
-    ch = broker.channel()
-    ch.queue_declare(queue=queue, durable=True)
-    ch.basic_publish(exchange="", routing_key=queue, body=body)
+    broker.publish(queue, body.encode())
 
 
 def create_app(settings: Settings | None = None, db: docs_db.DocsDB | None = None, broker=None) -> FastAPI:

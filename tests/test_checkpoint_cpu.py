@@ -149,3 +149,82 @@ def test_stack_runs_from_checkpoint_directories(tmp_path):
     assert pipe.engine.model.cfg.name == "llm" and pipe.encoder.cfg.hidden == cfg.hidden
     ans = pipe.answer_batch(["Quelle plante pour le syndrome ?"], SamplingParams(max_new_tokens=4, stop_on_eos=False))
     assert len(ans) == 1 and len(ans[0].token_ids) == 4 and len(ans[0].sources) == 3
+
+
+def test_llama3_rope_scaling_inv_freq_closed_form():
+    """Llama-3.1 rope_scaling (type llama3) against the closed-form per-frequency rule."""
+    import math
+
+    from docqa_amd.ops import reference as ref
+
+    sc = {"rope_type": "llama3", "factor": 8.0, "low_freq_factor": 1.0, "high_freq_factor": 4.0,
+          "original_max_position_embeddings": 8192}
+    got = ref.rope_inv_freq(128, 500000.0, sc)
+    for i, g in enumerate(got.tolist()):
+        f = 500000.0 ** (-(2 * i) / 128)
+        wl = 2 * math.pi / f
+        if wl < 8192 / 4.0:
+            want = f                       # high frequency: kept
+        elif wl > 8192 / 1.0:
+            want = f / 8.0                 # low frequency: divided by factor
+        else:
+            s = (8192 / wl - 1.0) / (4.0 - 1.0)
+            want = (1 - s) * f / 8.0 + s * f
+        assert abs(g - want) <= 1e-12 * max(1.0, abs(want)), (i, g, want)
+    # the scaled table differs from the plain one only in the low/medium bands
+    plain = ref.rope_inv_freq(128, 500000.0)
+    assert torch.equal(got[:20], plain[:20]) and not torch.equal(got, plain)
+    assert torch.allclose(ref.rope_inv_freq(64, 1e4, {"type": "linear", "factor": 2.0}),
+                          ref.rope_inv_freq(64, 1e4) / 2)
+    cs = ref.rope_cos_sin(16, 128, 500000.0, scaling=sc)
+    assert torch.allclose(cs[5, 64:], torch.sin(5 * got).float())
+
+
+def test_llama_config_from_hf_refuses_unsupported():
+    import pytest
+
+    from docqa_amd.models import checkpoint as ck
+    from docqa_amd.models.llama import LlamaConfig
+
+    base = ck.llama_config_to_hf(LlamaConfig.preset("tiny"))
+    cfg = ck.llama_config_from_hf(dict(base, rope_scaling={"rope_type": "llama3", "factor": 32.0,
+                                                            "low_freq_factor": 1.0, "high_freq_factor": 4.0,
+                                                            "original_max_position_embeddings": 8192}))
+    assert cfg.rope_scaling["factor"] == 32.0
+    # Mistral (the reference's generator) loads; its sliding window is recorded
+    m = ck.llama_config_from_hf(dict(base, model_type="mistral", sliding_window=4096))
+    assert m.sliding_window == 4096
+    for bad in (dict(base, model_type="qwen2"), dict(base, attention_bias=True), dict(base, mlp_bias=True),
+                dict(base, rope_scaling={"rope_type": "yarn", "factor": 4.0}), dict(base, hidden_act="gelu")):
+        with pytest.raises(NotImplementedError):
+            ck.llama_config_from_hf(bad)
+
+
+def test_engine_refuses_context_beyond_sliding_window():
+    import pytest
+
+    from docqa_amd.engine.llm_engine import LLMEngine
+    from docqa_amd.models.llama import LlamaConfig, LlamaModel
+
+    cfg = LlamaConfig.preset("tiny")
+    cfg.sliding_window = 256
+    model = LlamaModel(cfg, device="cpu", seed=0)
+    with pytest.raises(ValueError):
+        LLMEngine(model, max_batch=2, max_context=512, use_graphs=False)
+    LLMEngine(model, max_batch=2, max_context=256, use_graphs=False)
+
+
+def test_rope_scaled_checkpoint_round_trip(tmp_path):
+    """A llama3-scaled checkpoint round-trips and the model uses the scaled table."""
+    from docqa_amd.models import checkpoint as ck
+    from docqa_amd.models.llama import LlamaConfig, LlamaModel
+    from docqa_amd.ops import reference as ref
+
+    cfg = LlamaConfig.preset("tiny")
+    cfg.rope_scaling = {"rope_type": "llama3", "factor": 8.0, "low_freq_factor": 1.0,
+                        "high_freq_factor": 4.0, "original_max_position_embeddings": 64}
+    ck.save_llama(LlamaModel(cfg, device="cpu", seed=1), tmp_path / "m")
+    got = ck.load_llama(tmp_path / "m", device="cpu")
+    assert got.cfg.rope_scaling == cfg.rope_scaling
+    want = ref.rope_cos_sin(cfg.max_position, cfg.head_dim, cfg.rope_theta, scaling=cfg.rope_scaling)
+    assert torch.equal(got.cos_sin, want)

@@ -137,6 +137,24 @@ def test_token_cls_argmax(native, T, H, NL, nv):
     assert torch.equal(got[~ambiguous], want[~ambiguous])
 
 
+def test_vector_load_kernels_refuse_misaligned_views(native):
+    """uint4-loading launchers reject views whose storage offset breaks 16-byte alignment
+     instead of faulting on the GPU."""
+    H, NL = 256, 16
+    hbuf = torch.randn(8 * (H + 8) + 1, device="cuda").bfloat16()
+    h = hbuf[1:1 + 8 * (H + 8)].view(8, H + 8)[:, :H]          # offset of one element
+    w = torch.zeros(NL, H, device="cuda", dtype=torch.bfloat16)
+    b = torch.zeros(NL, device="cuda", dtype=torch.bfloat16)
+    with pytest.raises(RuntimeError):
+        native.token_cls_argmax(h, w, b, 4)
+    wbuf = torch.zeros(NL * H + 1, device="cuda", dtype=torch.bfloat16)
+    with pytest.raises(RuntimeError):
+        native.token_cls_argmax(hbuf[:8 * H].view(8, H), wbuf[1:].view(NL, H), b, 4)
+    logits = torch.randn(4 * 1024 + 1, device="cuda").bfloat16()[1:].view(4, 1024)
+    with pytest.raises(RuntimeError):
+        native.argmax(logits)
+
+
 def test_sample_greedy_limit(native):
     # top_k=1 must reproduce argmax whatever u is
     x = torch.randn(8, 5000, device="cuda")
@@ -266,7 +284,7 @@ def test_gemm_asymmetric_identity(native):
     assert torch.equal(o[:64, :], w.float()[:, :64].T[:64, :])
 
 
-@pytest.mark.parametrize("M", [1, 5, 16, 31, 64, 65, 100, 128, 129, 192])
+@pytest.mark.parametrize("M", [1, 5, 16, 31, 64, 65, 100, 128, 129, 192, 193, 230, 256])
 @pytest.mark.parametrize("N,K,S", [(6144, 4096, 0), (4096, 4096, 0), (4096, 14336, 0), (28672, 4096, 0),
                                    (512, 1024, 1), (512, 1024, 2), (640, 3584, 7)])
 def test_dgemm(native, M, N, K, S):
@@ -280,7 +298,8 @@ def test_dgemm(native, M, N, K, S):
 
 
 @pytest.mark.parametrize("S,M,tile", [(1, 37, 64), (4, 37, 64), (4, 100, 128), (8, 128, 128), (2, 128, 64),
-                                     (4, 160, 64), (4, 192, 64)])
+                                     (4, 160, 64), (4, 192, 64), (4, 256, 64), (2, 200, 64), (8, 256, 128),
+                                     (4, 241, 128)])
 def test_splitk_fused_consumers(native, S, M, tile):
     """dgemm_partial + add_rmsnorm_splitk / rope_cache_splitk == reference on bf16(sum P)."""
     from docqa_amd.ops import reference as R
@@ -348,7 +367,7 @@ def test_splitk_consumers_slab_counts(native, S):
     _close(vc1, vc2, 2e-2, 1e-2)   # fp32 sum order differs from torch's -> 1 bf16 ulp
 
 
-@pytest.mark.parametrize("M", [1, 16, 33, 64, 97, 128])
+@pytest.mark.parametrize("M", [1, 16, 33, 64, 97, 128, 129, 200, 256])
 @pytest.mark.parametrize("N,K", [(28672, 4096), (1024, 512)])
 def test_dgemm_glu(native, M, N, K):
     """Fused SwiGLU decode GEMM (8-interleaved gate|up) vs fp32 GEMM + reference SwiGLU."""
@@ -395,9 +414,11 @@ def test_paged_decode_fused(native, B, Hkv, S):
     _close(o1[valid], o2[valid], 2e-2, 1e-2)
 
 
-def test_dgemm_asymmetric_identity(native):
-    """X = I rows against an asymmetric W: Y must be W's columns, catches transposed writes."""
-    M, N, K = 48, 128, 512
+@pytest.mark.parametrize("M", [48, 256])
+def test_dgemm_asymmetric_identity(native, M):
+    """X = I rows against an asymmetric W: Y must be W's columns, catches transposed writes
+    (M=256: the 8-wave layout, every wave's rows distinct)."""
+    N, K = 128, 1024
     x = torch.zeros(M, K, device="cuda", dtype=torch.bfloat16)
     x[torch.arange(M), torch.arange(M) * 3] = 1
     w = (torch.arange(N * K, device="cuda").view(N, K) % 97).bfloat16()

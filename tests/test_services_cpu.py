@@ -126,6 +126,60 @@ def test_bio_decoding():
     assert [(s.entity_type, s.start, s.end) for s in sp] == [("PERSON", 0, 10), ("LOCATION", 14, 18), ("NRP", 19, 25)]
 
 
+def test_bio_decoding_checkpoint_label_forms():
+    """Real checkpoints name their own types (id2label): long Presidio/OntoNotes forms,
+    BIOES prefixes, and types outside the six entities must not raise."""
+    from docqa_amd.deid.engine import bio_to_spans, label_entity_map
+
+    labels = ["B-PERSON", "I-PERSON", "B-ORG", "I-ORG", "B-MISC", "B-DATE_TIME", "S-LOC", "B-WEIRD"]
+    offs = [(0, 4), (5, 9), (10, 13), (14, 17), (18, 22), (23, 33), (34, 40), (41, 45)]
+    sp = bio_to_spans(labels, offs)
+    assert [(s.entity_type, s.start, s.end) for s in sp] == [
+        ("PERSON", 0, 9), ("ORGANIZATION", 10, 17), ("DATE_TIME", 23, 33), ("LOCATION", 34, 40)]
+    # a configurable table: map MISC onto NRP, drop ORG
+    table = label_entity_map({"MISC": "NRP", "ORG": None})
+    sp = bio_to_spans(labels, offs, label_map=table)
+    assert [s.entity_type for s in sp] == ["PERSON", "NRP", "DATE_TIME", "LOCATION"]
+
+
+def test_deid_engine_with_checkpoint_labels(tmp_path, monkeypatch):
+    """DeidEngine over a token classifier loaded from a checkpoint whose id2label uses
+    PERSON / DATE_TIME / ORG / MISC: every prediction decodes without KeyError, and only
+    the six reference entities reach the anonymized text."""
+    import json as _json
+
+    from safetensors.torch import save_file
+
+    from docqa_amd.deid.engine import DeidEngine
+    from docqa_amd.models import checkpoint as ck
+    from docqa_amd.models.bert import BertConfig, BertTokenClassifier
+    from docqa_amd.text.tokenizer import WordPieceTokenizer
+    from tests.test_checkpoint_cpu import _bert_hf_config, _bert_hf_state
+
+    cfg = BertConfig.preset("tiny-bert")
+    labels = ["O", "B-PERSON", "I-PERSON", "B-DATE_TIME", "B-ORG", "I-ORG", "B-MISC"]
+    clf = BertTokenClassifier(cfg, labels, device="cpu", seed=3)
+    d = tmp_path / "ner"
+    d.mkdir()
+    hf = _bert_hf_config(cfg)
+    hf["id2label"] = {str(i): lab for i, lab in enumerate(labels)}
+    (d / "config.json").write_text(_json.dumps(hf))
+    sd = _bert_hf_state(clf, prefix="bert.")
+    sd["classifier.weight"] = clf.cls_w[:len(labels)].clone()
+    sd["classifier.bias"] = clf.cls_b[:len(labels)].clone()
+    save_file(sd, str(d / "model.safetensors"))
+    ner = ck.load_bert_token_classifier(d, ["unused"], device="cpu")
+    tok = WordPieceTokenizer(vocab_size=cfg.vocab_size)
+    eng = DeidEngine(ner, tok, use_model=True)
+    text = "Patient John Smith seen at Mercy Hospital on 2024-03-02 by the ORG team."
+    # force every label type to appear: cycle predictions through all label ids
+    monkeypatch.setattr(ner, "predict", lambda toks: [[i % len(labels) for i in range(len(t))] for t in toks])
+    out = eng.process_text_anonymization(text)
+    assert isinstance(out, str) and out
+    for r in eng.analyze(text):
+        assert r.entity_type in {"PERSON", "PHONE_NUMBER", "EMAIL_ADDRESS", "DATE_TIME", "NRP", "LOCATION"}
+
+
 def test_deid_worker_callback_ack_nack():
     from docqa_amd.services.deid_worker import DeidWorker
 

@@ -76,3 +76,11 @@ def test_nack_requeue_dlq_and_dead_consumer_recovery(tmp_path):
     assert b.depth("q") == 0
     b2 = SpoolBroker(root)
     assert b2.depth("q") == 1 and b2.get_nowait("q") == b"c"
+
+
+def test_every_broker_exposes_persistent_properties(tmp_path):
+    """deid_worker publishes with ``broker.persistent_properties()`` on every backend."""
+    from docqa_amd.bus.broker import InProcBroker, SpoolBroker
+
+    for b in (InProcBroker(), SpoolBroker(str(tmp_path / "spool"))):
+        assert b.persistent_properties().delivery_mode == 2

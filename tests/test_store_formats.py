@@ -162,3 +162,47 @@ def test_index_follower_tails_writer_across_snapshots(tmp_path):
     w.commit()                               # rotation happened before g ever polled
     g.poll()
     assert g.index.ntotal == w.index.ntotal
+
+
+def test_index_follower_reload_is_atomic_for_concurrent_search(tmp_path):
+    """Snapshot reloads swap vectors + metadata together: a search racing the reload never
+    sees an empty / partial index or an id without its record."""
+    import threading
+
+    import torch
+
+    from docqa_amd.config import Settings
+    from docqa_amd.index.follower import IndexFollower
+    from docqa_amd.models.bert import BertConfig, BertEncoder
+    from docqa_amd.services.indexer import SemanticIndexer
+    from docqa_amd.text.tokenizer import WordPieceTokenizer
+
+    st = Settings()
+    st.index_dir = str(tmp_path)
+    st.default_data_dir = str(tmp_path / "nodata")
+    enc = BertEncoder(BertConfig.preset("tiny-bert"), device="cpu")
+    w = SemanticIndexer(enc, WordPieceTokenizer(), st, device="cpu").startup(build_if_missing=True)
+    f = IndexFollower(str(tmp_path), d=enc.cfg.hidden, device="cpu")
+    f.poll()
+    n0 = f.index.ntotal
+    assert n0 > 0
+    q = torch.randn(4, enc.cfg.hidden)
+    bad, stop = [], threading.Event()
+
+    def searcher():
+        while not stop.is_set():
+            n = f.index.ntotal
+            D, I = f.index.search(q, 3)
+            if n < n0 or (I < 0).any() or int(I.max()) >= len(f.metadata):
+                bad.append((n, I.tolist(), len(f.metadata)))
+
+    t = threading.Thread(target=searcher)
+    t.start()
+    try:
+        for _ in range(30):
+            f._load_snapshot()
+    finally:
+        stop.set()
+        t.join()
+    assert not bad, bad[:3]
+    assert f.index.ntotal == n0 == len(f.metadata)
