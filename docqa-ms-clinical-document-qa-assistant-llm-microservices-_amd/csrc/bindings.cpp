@@ -534,6 +534,62 @@ at::Tensor dgemm(const at::Tensor& x, const at::Tensor& w, int64_t splits) {
   return out;
 }
 
+// mid-M decode GEMM (193..512 rows): splits == 1 -> bf16 [.., N]; splits > 1 -> fp32
+// split-K slabs [S, M, N] for the fused consumers (add_rmsnorm_splitk / rope_cache_splitk)
+at::Tensor mgemm(const at::Tensor& x, const at::Tensor& w, int64_t splits, int64_t cfg) {
+  CHECK_GPU(x); CHECK_BF16(x); CHECK_BF16(w); CHECK_CONTIG(x); CHECK_CONTIG(w);
+  CHECK_ALIGN16(x); CHECK_ALIGN16(w);
+  const int K = x.size(-1), N = w.size(0);
+  TORCH_CHECK(w.size(1) == K, "mgemm: K mismatch");
+  const int M = x.numel() / K;
+  TORCH_CHECK(splits >= 1, "mgemm: splits >= 1");
+  c10::DeviceGuard g(x.device());
+  at::Tensor out;
+  if (splits == 1) {
+    auto sizes = x.sizes().vec();
+    sizes.back() = N;
+    out = at::empty(sizes, x.options());
+    CHECK_RC(docqa_mgemm(x.data_ptr(), w.data_ptr(), out.data_ptr(), nullptr, M, N, K, 1, (int)cfg, stream()),
+             "mgemm");
+  } else {
+    out = at::empty({splits, M, N}, x.options().dtype(at::kFloat));
+    CHECK_RC(docqa_mgemm(x.data_ptr(), w.data_ptr(), nullptr, out.data_ptr<float>(), M, N, K, (int)splits,
+                         (int)cfg, stream()), "mgemm");
+  }
+  return out;
+}
+
+// mid-M gate|up projection with fused SwiGLU: x [M, K], w [2I, K] (8-interleaved) -> [M, I]
+at::Tensor mgemm_glu(const at::Tensor& x, const at::Tensor& w, int64_t cfg) {
+  CHECK_GPU(x); CHECK_BF16(x); CHECK_BF16(w); CHECK_CONTIG(x); CHECK_CONTIG(w);
+  CHECK_ALIGN16(x); CHECK_ALIGN16(w);
+  const int K = x.size(-1), N = w.size(0);
+  TORCH_CHECK(w.size(1) == K && N % 16 == 0, "mgemm_glu: shape mismatch");
+  const int M = x.numel() / K;
+  auto sizes = x.sizes().vec();
+  sizes.back() = N / 2;
+  c10::DeviceGuard g(x.device());
+  auto out = at::empty(sizes, x.options());
+  CHECK_RC(docqa_mgemm_glu(x.data_ptr(), w.data_ptr(), out.data_ptr(), M, N, K, (int)cfg, stream()), "mgemm_glu");
+  return out;
+}
+
+// LM head + greedy pick: argmax over the first n_valid columns of bf16(x . w^T) -> int64 [M]
+at::Tensor mgemm_argmax(const at::Tensor& x, const at::Tensor& w, int64_t n_valid, int64_t cfg) {
+  CHECK_GPU(x); CHECK_BF16(x); CHECK_BF16(w); CHECK_CONTIG(x); CHECK_CONTIG(w);
+  CHECK_ALIGN16(x); CHECK_ALIGN16(w);
+  const int K = x.size(-1), N = w.size(0), bn = docqa_mgemm_tile_n((int)cfg);   // weight-tile rows
+  TORCH_CHECK(w.size(1) == K && bn > 0 && N % bn == 0, "mgemm_argmax: shape mismatch");
+  const int M = x.numel() / K;
+  c10::DeviceGuard g(x.device());
+  auto out = at::empty({M}, x.options().dtype(at::kLong));
+  auto ws_v = at::empty({M, N / bn}, x.options().dtype(at::kFloat));
+  auto ws_i = at::empty({M, N / bn}, x.options().dtype(at::kInt));
+  CHECK_RC(docqa_mgemm_argmax(x.data_ptr(), w.data_ptr(), out.data_ptr<int64_t>(), ws_v.data_ptr<float>(),
+                              ws_i.data_ptr<int>(), M, N, K, (int)n_valid, (int)cfg, stream()), "mgemm_argmax");
+  return out;
+}
+
 std::tuple<at::Tensor, at::Tensor> knn(const at::Tensor& xb, const at::Tensor& xb_norms,
                                        const at::Tensor& xq, int64_t k, bool inner_product,
                                        int64_t id_offset) {
@@ -691,6 +747,9 @@ TORCH_LIBRARY(docqa, m) {
   m.def("dgemm(Tensor x, Tensor w, int splits) -> Tensor");
   m.def("dgemm_partial(Tensor x, Tensor w, int splits, int tile_rows=64) -> Tensor");
   m.def("dgemm_glu(Tensor x, Tensor w) -> Tensor");
+  m.def("mgemm(Tensor x, Tensor w, int splits, int cfg=0) -> Tensor");
+  m.def("mgemm_glu(Tensor x, Tensor w, int cfg=0) -> Tensor");
+  m.def("mgemm_argmax(Tensor x, Tensor w, int n_valid, int cfg=0) -> Tensor");
   m.def("paged_decode_cascade(Tensor q, Tensor k_cache, Tensor v_cache, Tensor block_tables, "
         "Tensor context_lens, int Hq, int max_context, float scale, Tensor prefix_table, Tensor prefix_len, "
         "int nchunk, Tensor? order=None) -> Tensor");
@@ -738,6 +797,9 @@ TORCH_LIBRARY_IMPL(docqa, CUDA, m) {
   m.impl("dgemm", &dgemm);
   m.impl("dgemm_partial", &dgemm_partial);
   m.impl("dgemm_glu", &dgemm_glu);
+  m.impl("mgemm", &mgemm);
+  m.impl("mgemm_glu", &mgemm_glu);
+  m.impl("mgemm_argmax", &mgemm_argmax);
   m.impl("paged_decode_fused", &paged_decode_fused);
   m.impl("paged_decode_cascade", &paged_decode_cascade);
   m.impl("paged_decode_cascade_rope", &paged_decode_cascade_rope);

@@ -94,6 +94,12 @@ int docqa_dgemm(const void* X, const void* W, void* Y, float* partial, int M, in
                 hipStream_t s);
 int docqa_gemm(const void* A, const void* W, const void* bias, const void* res, void* C, int M,
                int N, int K, int epi, hipStream_t s);
+int docqa_mgemm(const void* X, const void* W, void* Y, float* P, int M, int N, int K, int S, int cfg,
+                hipStream_t s);
+int docqa_mgemm_glu(const void* X, const void* W, void* Y, int M, int N, int K, int cfg, hipStream_t s);
+int docqa_mgemm_argmax(const void* X, const void* W, int64_t* out, float* ws_v, int* ws_i, int M, int N,
+                       int K, int n_valid, int cfg, hipStream_t s);
+int docqa_mgemm_tile_n(int cfg);
 
 int docqa_knn_workspace_blocks(int N);
 int docqa_knn_kpad(int k);

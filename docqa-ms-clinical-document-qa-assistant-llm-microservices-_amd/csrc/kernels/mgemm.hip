@@ -1,0 +1,397 @@
+// mgemm.hip -- "mid-M" decode GEMM for the Llama generator at batch buckets of 193..512
+// rows (the bench's 256-question decode step):  Y[M, N] = X[M, K] . W[N, K]^T.
+//
+// Between the skinny weight-streaming regime (dgemm.hip, <= 192 rows: X in VGPRs, W through
+// an LDS-DMA ring) and a plain large GEMM, a 256-row decode projection is limited by the
+// chip's L2 -> LDS traffic, not by HBM: every workgroup re-reads its K slice of X (2 MB at
+// K = 4096) from L2, so the X bytes moved are (N / BN) x 2 MB -- for the Llama-3-8B QKV at
+// BN = 128 twice the 48 MB of weights (measured: time tracks total L2->LDS bytes, hot or
+// cold weights alike; cdna_hip_programming.md §5 "Projection GEMM at M = 256").  The design
+// therefore maximises the tile width per workgroup:
+//   * one workgroup owns ALL 256 rows x BN weight rows (BN = 128 or 256) x one K slice:
+//     the weight tile is streamed from HBM exactly once and X is re-read only N / BN times;
+//   * both operands go HBM/L2 -> LDS by LDS-DMA (global_load_lds 16 B, source-address XOR
+//     swizzle so the 16-row MFMA fragment reads are bank-conflict-free) into a ring of
+//     BKS-deep k-stages (64 at BN = 128: 3 x 48 KB; 32 at BN = 256: 4 x 32 KB) with counted
+//     vmcnt waits and raw s_barrier (no __syncthreads: its release fence would drain the
+//     ring, §5 "Pipelining across barriers");
+//   * the fragments of stage k+1 are read from LDS while the MFMAs of stage k run (two
+//     register sets, loop unrolled by two), NSR-2 DMA stages stream behind them;
+//   * waves WM (M) x WN (N), each a (256/WM) x (BN/WN) sub-tile of mfma_f32_16x16x32_bf16
+//     accumulators;
+//   * split-K over the grid with XCD-aware slice placement (one K slice per XCD, so its
+//     4 MB L2 holds only that slice of X); the fp32 slabs [S, M, N] are combined by the
+//     consumer kernel that exists anyway (add_rmsnorm_splitk / rope_cache_splitk);
+//   * epilogues through a per-wave LDS scratch (16 rows at a time) so global stores are
+//     full 64-B lane runs: bf16, fp32 split-K slab, fused SwiGLU over the 8-interleaved
+//     gate|up rows (the decode GEMM's layout), or the LM head's greedy argmax (per-row max
+//     over the tile, ties to the lowest id as torch.argmax, compared in bf16 so it picks
+//     the token the unfused bf16 logits would) -- the [M, 128256] logits never reach HBM.
+// Shapes: N % BN == 0, K % (S * 2 * BKS) == 0, any M (rows tiled by 256, tail rows clamped
+// on load and never stored).
+#include "docqa_common.h"
+#include "docqa_asm.h"
+#include <float.h>
+#include <stdlib.h>
+
+using namespace docqa;
+
+namespace {
+constexpr int BM = 256;
+enum { EPI_BF16 = 0, EPI_PARTIAL = 1, EPI_GLU = 2, EPI_ARGMAX = 3 };
+
+// element offset of 16-B chunk `ch` of `row` in a [rows][BKS] bf16 tile: the XOR spreads
+// the 16 rows of a fragment read over all 64 banks (128-B rows: pairs of rows share a
+// 256-B bank row; 64-B rows: quads do)
+template <int BKS>
+__device__ __forceinline__ int swz(int row, int ch) {
+  if constexpr (BKS == 64) return row * 64 + ((ch ^ ((row >> 1) & 7)) << 3);
+  else return row * 32 + ((ch ^ ((row >> 2) & 3)) << 3);
+}
+
+__device__ __forceinline__ float silu_f(float x) { return x / (1.f + __expf(-x)); }
+
+__device__ __forceinline__ void better(float& bv, int& bi, float v, int i) {
+  if (v > bv || (v == bv && i < bi)) { bv = v; bi = i; }
+}
+
+template <int EPI, int BN, int BKS, int NSR, int WM, int WN>
+__global__ __launch_bounds__(WM * WN * 64) void mgemm_kernel(const uint16_t* __restrict__ X,
+                                                             const uint16_t* __restrict__ W,
+                                                             uint16_t* __restrict__ Y,
+                                                             float* __restrict__ P,
+                                                             float* __restrict__ pv, int* __restrict__ pi,
+                                                             int M, int N, int K, int Ks, int S,
+                                                             int ntiles, int remap, int n_valid) {
+  constexpr int WAVES = WM * WN;
+  constexpr int MI = BM / WM / 16;                      // 16-row m-tiles per wave
+  constexpr int CW = BN / WN;                           // output columns per wave
+  constexpr int NJ = CW / 16;                           // 16-col n-tiles per wave
+  constexpr int KS = BKS / 32;                          // MFMA k-steps per stage
+  constexpr int CPR = BKS / 8;                          // 16-B chunks per tile row
+  constexpr int RPI = 64 / CPR;                         // tile rows per DMA instruction
+  constexpr int A_PER_WAVE = BM / RPI / WAVES;          // 1-KiB DMA instructions per stage
+  constexpr int B_PER_WAVE = BN / RPI / WAVES;
+  constexpr int PER_STAGE = A_PER_WAVE + B_PER_WAVE;
+  constexpr int SLOT = (BM + BN) * BKS;                 // elements per ring slot
+  constexpr int SCR = CW + 4;                           // scratch row pitch (floats)
+  static_assert(NSR >= 3, "fragment-prefetch ring needs >= 3 slots");
+  static_assert(A_PER_WAVE * RPI * WAVES == BM && B_PER_WAVE * RPI * WAVES == BN, "DMA split");
+  static_assert(NSR * SLOT * 2 <= 160 * 1024, "LDS");
+  __shared__ __attribute__((aligned(16))) uint16_t smem[NSR * SLOT];
+
+  const int L = blockIdx.x;
+  int tile, slice;
+  if (remap == 1) {            // 8 % S == 0: XCD x runs slice x % S
+    const int xcd = L & 7, j = L >> 3;
+    slice = xcd % S;
+    tile = j * (8 / S) + xcd / S;
+  } else if (remap == 2) {     // S % 8 == 0: XCD x runs slices x, x + 8, ...
+    const int xcd = L & 7, j = L >> 3, q = S / 8;
+    slice = xcd + 8 * (j % q);
+    tile = j / q;
+  } else {
+    tile = L % ntiles;
+    slice = L / ntiles;
+  }
+  const int n0 = tile * BN, m0 = blockIdx.y * BM, kbeg = slice * Ks;
+  const int nk = Ks / BKS;     // even, >= 2
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int fr = lane & 15, fq = lane >> 4;
+  const int wm = wave % WM, wn = wave / WM;
+
+  // per-lane DMA sources (k offset added per stage): instruction q covers tile rows
+  // RPI q .. RPI q + RPI-1; lane -> physical 16-B chunk, source = the logical chunk the
+  // swizzle puts there
+  const uint16_t* asrc[A_PER_WAVE];
+  const uint16_t* bsrc[B_PER_WAVE];
+  auto lchunk = [&](int r, int pc) {
+    if constexpr (BKS == 64) return pc ^ ((r >> 1) & 7);
+    else return pc ^ ((r >> 2) & 3);
+  };
+#pragma unroll
+  for (int i = 0; i < A_PER_WAVE; ++i) {
+    const int p = (i * WAVES + wave) * 64 + lane, r = p / CPR;
+    asrc[i] = X + (size_t)min(m0 + r, M - 1) * K + kbeg + lchunk(r, p % CPR) * 8;
+  }
+#pragma unroll
+  for (int i = 0; i < B_PER_WAVE; ++i) {
+    const int p = (i * WAVES + wave) * 64 + lane, r = p / CPR;
+    bsrc[i] = W + (size_t)(n0 + r) * K + kbeg + lchunk(r, p % CPR) * 8;
+  }
+  const uint32_t base = lds_u32(smem);
+  auto stage = [&](int kt) {
+    const uint32_t slot = base + (uint32_t)((kt % NSR) * SLOT * 2);
+    const int ko = kt * BKS;
+#pragma unroll
+    for (int i = 0; i < A_PER_WAVE; ++i)
+      glds16<false>(asrc[i] + ko, slot + (uint32_t)((i * WAVES + wave) * 1024));
+#pragma unroll
+    for (int i = 0; i < B_PER_WAVE; ++i)
+      glds16<true>(bsrc[i] + ko, slot + (uint32_t)(BM * BKS * 2 + (i * WAVES + wave) * 1024));
+  };
+
+  f32x4 acc[MI][NJ];
+#pragma unroll
+  for (int i = 0; i < MI; ++i)
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  // fragments of one stage: [k-step][m-tile] A, [k-step][n-tile] B
+  struct Frag { bf16x8 a[KS][MI]; bf16x8 b[KS][NJ]; };
+  auto load_frags = [&](Frag& f, int kt) {
+    const uint16_t* sa = smem + (kt % NSR) * SLOT;
+    const uint16_t* sb = sa + BM * BKS;
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) {
+      const int ch = ks * 4 + fq;
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) f.b[ks][j] = *reinterpret_cast<const bf16x8*>(sb + swz<BKS>(wn * CW + j * 16 + fr, ch));
+#pragma unroll
+      for (int i = 0; i < MI; ++i)
+        f.a[ks][i] = *reinterpret_cast<const bf16x8*>(sa + swz<BKS>(wm * (BM / WM) + i * 16 + fr, ch));
+    }
+  };
+  auto mma = [&](const Frag& f) {
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks)
+#pragma unroll
+      for (int i = 0; i < MI; ++i)
+#pragma unroll
+        for (int j = 0; j < NJ; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(f.a[ks][i], f.b[ks][j], acc[i][j], 0, 0, 0);
+  };
+  // Schedule (NSR slots): the fragments of stage kt+1 are read from LDS while the MFMAs of
+  // stage kt run, and NSR-2 DMA stages stream behind them.  Step kt: [frags(kt) landed:
+  // lgkmcnt(0)] [DMA(kt+1) landed: vmcnt] barrier [DMA(kt+NSR) into slot kt % NSR, which
+  // frags(kt) -- now in registers in every wave -- vacated] [ds_read frags(kt+1)] [MFMA(kt)]
+  auto step = [&](Frag& cur, Frag& nxt, int kt) {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    if (kt + 1 < nk) {
+      // DMA stages issued so far: 0 .. min(nk - 1, kt + NSR - 1); kt+1 must have landed
+      const int ahead = min(nk - 1, kt + NSR - 1) - (kt + 1);
+      if (ahead >= NSR - 2) wait_vmcnt<(NSR - 2) * PER_STAGE>();
+      else if (NSR >= 4 && ahead == NSR - 3) wait_vmcnt<(NSR >= 4 ? NSR - 3 : 0) * PER_STAGE>();
+      else if (NSR >= 5 && ahead == NSR - 4) wait_vmcnt<(NSR >= 5 ? NSR - 4 : 0) * PER_STAGE>();
+      else wait_vmcnt<0>();
+      ring_barrier();
+      if (kt + NSR < nk) stage(kt + NSR);
+      load_frags(nxt, kt + 1);
+    }
+    mma(cur);
+  };
+  Frag f0, f1;
+#pragma unroll
+  for (int j = 0; j < NSR; ++j)
+    if (j < nk) stage(j);
+  if (nk >= NSR) wait_vmcnt<(NSR - 1) * PER_STAGE>();
+  else wait_vmcnt<0>();
+  ring_barrier();
+  load_frags(f0, 0);
+  for (int kt = 0; kt < nk; kt += 2) {
+    step(f0, f1, kt);
+    step(f1, f0, kt + 1);
+  }
+  wait_vmcnt<0>();
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  ring_barrier();   // every wave is done reading the ring: reuse it as epilogue scratch
+
+  // epilogue, 16 rows at a time: accumulators -> per-wave scratch [16][CW] -> re-read so
+  // that consecutive lanes own consecutive 16-B pieces of a row (coalesced row stores)
+  float* scr = reinterpret_cast<float*>(smem) + wave * 16 * SCR;
+  const int rbase = m0 + wm * (BM / WM), cbase = n0 + wn * CW;
+  float bestv[MI];
+  int besti[MI];
+#pragma unroll
+  for (int i = 0; i < MI; ++i) {
+#pragma unroll
+    for (int j = 0; j < NJ; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) scr[(fq * 4 + r) * SCR + j * 16 + fr] = acc[i][j][r];
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    // EPC: output columns per lane (fp32 slab 4, bf16 8, SwiGLU 16 inputs -> 8 outputs)
+    constexpr int EPC = EPI == EPI_PARTIAL ? 4 : EPI == EPI_BF16 ? 8 : 16;
+    constexpr int LPR = CW / EPC, RPS = 64 / LPR;          // lanes per row, rows per sweep
+    if constexpr (EPI != EPI_ARGMAX) {
+#pragma unroll
+      for (int it = 0; it < 16 / RPS; ++it) {
+        const int r = it * RPS + lane / LPR, c = (lane % LPR) * EPC;
+        float v[EPC];
+#pragma unroll
+        for (int e = 0; e < EPC / 4; ++e) {
+          const float4 t = *reinterpret_cast<const float4*>(scr + r * SCR + c + e * 4);
+          v[e * 4] = t.x; v[e * 4 + 1] = t.y; v[e * 4 + 2] = t.z; v[e * 4 + 3] = t.w;
+        }
+        const int row = rbase + i * 16 + r, col = cbase + c;
+        if (row < M) {
+          if constexpr (EPI == EPI_PARTIAL) {
+            *reinterpret_cast<float4*>(P + ((size_t)slice * M + row) * N + col) = float4{v[0], v[1], v[2], v[3]};
+          } else if constexpr (EPI == EPI_BF16) {
+            *reinterpret_cast<uint4*>(Y + (size_t)row * N + col) = pack8(v);
+          } else {
+            // 16 consecutive columns = one (gate 8, up 8) interleave group
+            float o[8];
+#pragma unroll
+            for (int e = 0; e < 8; ++e) {
+              const float gv = bf2f(f2bf(v[e])), uv = bf2f(f2bf(v[8 + e]));   // as the bf16 GEMM output
+              o[e] = silu_f(gv) * uv;
+            }
+            *reinterpret_cast<uint4*>(Y + (size_t)row * (N >> 1) + (col >> 1)) = pack8(o);
+          }
+        }
+      }
+    } else {
+      // 4 lanes per row, CW/4 columns each; the row's best (value, id) after 2 shuffles
+      constexpr int CPL = CW / 4;
+      const int rr = lane >> 2, cc = (lane & 3) * CPL;
+      float bv = -FLT_MAX;
+      int bi = 0x7fffffff;
+#pragma unroll
+      for (int e = 0; e < CPL / 4; ++e) {
+        const float4 t = *reinterpret_cast<const float4*>(scr + rr * SCR + cc + e * 4);
+        const float tv[4] = {t.x, t.y, t.z, t.w};
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int col = cbase + cc + e * 4 + q;
+          if (col < n_valid) better(bv, bi, bf2f(f2bf(tv[q])), col);
+        }
+      }
+#pragma unroll
+      for (int o = 1; o <= 2; o <<= 1) {
+        const float ov = __shfl_xor(bv, o, 64);
+        const int oi = __shfl_xor(bi, o, 64);
+        better(bv, bi, ov, oi);
+      }
+      bestv[i] = bv;
+      besti[i] = bi;
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  }
+  if constexpr (EPI == EPI_ARGMAX) {
+    // merge the WN column waves of each row through LDS, one partial per (row, tile)
+    __syncthreads();
+    float* rv = reinterpret_cast<float*>(smem);
+    int* ri = reinterpret_cast<int*>(smem) + BM * WN;
+    if ((lane & 3) == 0) {
+#pragma unroll
+      for (int i = 0; i < MI; ++i) {
+        const int lr = wm * (BM / WM) + i * 16 + (lane >> 2);
+        rv[lr * WN + wn] = bestv[i];
+        ri[lr * WN + wn] = besti[i];
+      }
+    }
+    __syncthreads();
+    for (int lr = tid; lr < BM; lr += WAVES * 64) {
+      const int row = m0 + lr;
+      if (row >= M) continue;
+      float bv = rv[lr * WN];
+      int bi = ri[lr * WN];
+#pragma unroll
+      for (int w = 1; w < WN; ++w) better(bv, bi, rv[lr * WN + w], ri[lr * WN + w]);
+      pv[(size_t)row * ntiles + tile] = bv;
+      pi[(size_t)row * ntiles + tile] = bi;
+    }
+  }
+}
+
+__global__ __launch_bounds__(64) void mgemm_argmax_merge(const float* __restrict__ pv,
+                                                         const int* __restrict__ pi, int parts,
+                                                         int64_t* __restrict__ out) {
+  const int row = blockIdx.x;
+  float bv = -FLT_MAX;
+  int bi = 0x7fffffff;
+  for (int s = threadIdx.x; s < parts; s += 64)
+    better(bv, bi, pv[(size_t)row * parts + s], pi[(size_t)row * parts + s]);
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const float ov = __shfl_xor(bv, o, 64);
+    const int oi = __shfl_xor(bi, o, 64);
+    better(bv, bi, ov, oi);
+  }
+  if (threadIdx.x == 0) out[row] = bi == 0x7fffffff ? 0 : bi;   // all-NaN row: a valid id
+}
+
+// Variants (``cfg``): the tile width and wave layout
+//   1: BN 128, 64-deep stages x 3, waves 2 x 2 (128 x 64 each, 1 wave / SIMD)
+//   2: BN 128, 64-deep stages x 3, waves 4 x 2 ( 64 x 64 each, 2 waves / SIMD)
+//   3: BN 256, 32-deep stages x 4, waves 2 x 4 (128 x 64 each, 2 waves / SIMD)
+//   4: BN 256, 32-deep stages x 4, waves 2 x 2 (128 x 128 each, 1 wave / SIMD)
+struct Cfg { int bn, bks; };
+constexpr Cfg kCfg[5] = {{0, 0}, {128, 64}, {128, 64}, {256, 32}, {256, 32}};
+
+template <int EPI, int BN, int BKS, int NSR, int WM, int WN>
+int launch(const uint16_t* x, const uint16_t* w, uint16_t* y, float* p, float* pv, int* pi, int M,
+           int N, int K, int S, int n_valid, hipStream_t s) {
+  const int ntiles = N / BN, Ks = K / S;
+  int remap = 0;
+  if (S > 1 && 8 % S == 0 && (ntiles * S) % 8 == 0) remap = 1;
+  else if (S > 8 && S % 8 == 0) remap = 2;
+  dim3 grid(ntiles * S, (M + BM - 1) / BM);
+  mgemm_kernel<EPI, BN, BKS, NSR, WM, WN><<<grid, WM * WN * 64, 0, s>>>(x, w, y, p, pv, pi, M, N, K, Ks, S,
+                                                                      ntiles, remap, n_valid);
+  DOCQA_CHECK_LAUNCH();
+  return 0;
+}
+
+template <int EPI>
+int launch_cfg(int cfg, const uint16_t* x, const uint16_t* w, uint16_t* y, float* p, float* pv, int* pi,
+               int M, int N, int K, int S, int n_valid, hipStream_t s) {
+  switch (cfg) {
+    case 1: return launch<EPI, 128, 64, 3, 2, 2>(x, w, y, p, pv, pi, M, N, K, S, n_valid, s);
+    case 2: return launch<EPI, 128, 64, 3, 4, 2>(x, w, y, p, pv, pi, M, N, K, S, n_valid, s);
+    case 3: return launch<EPI, 256, 32, 4, 2, 4>(x, w, y, p, pv, pi, M, N, K, S, n_valid, s);
+    case 4: return launch<EPI, 256, 32, 4, 2, 2>(x, w, y, p, pv, pi, M, N, K, S, n_valid, s);
+    default: return -1;
+  }
+}
+
+bool shape_ok(int M, int N, int K, int S, int cfg) {
+  if (cfg < 1 || cfg > 4 || M <= 0 || S < 1) return false;
+  // whole pairs of stages per K slice (the main loop is unrolled by two)
+  return N % kCfg[cfg].bn == 0 && K % (S * 2 * kCfg[cfg].bks) == 0;
+}
+}  // namespace
+
+constexpr int kDefaultCfg = 2;
+int docqa_mgemm_tile_n(int cfg) {
+  if (cfg == 0) cfg = kDefaultCfg;
+  return cfg >= 1 && cfg <= 4 ? kCfg[cfg].bn : 0;
+}
+
+// S == 1: Y bf16 [M, N];  S > 1: P fp32 split-K slabs [S, M, N] (combined by the consumer)
+int docqa_mgemm(const void* X, const void* W, void* Y, float* P, int M, int N, int K, int S, int cfg,
+                hipStream_t s) {
+  if (cfg == 0) cfg = kDefaultCfg;
+  if (M == 0) return 0;
+  if (!shape_ok(M, N, K, S, cfg) || (S == 1 ? Y == nullptr : P == nullptr)) return -1;
+  if (!docqa_aligned16(X) || !docqa_aligned16(W) || !docqa_aligned16(S == 1 ? Y : (void*)P)) return -1;
+  const uint16_t *x = (const uint16_t*)X, *w = (const uint16_t*)W;
+  if (S == 1) return launch_cfg<EPI_BF16>(cfg, x, w, (uint16_t*)Y, nullptr, nullptr, nullptr, M, N, K, 1, N, s);
+  return launch_cfg<EPI_PARTIAL>(cfg, x, w, nullptr, P, nullptr, nullptr, M, N, K, S, N, s);
+}
+
+// Y[M, N/2] = silu(gate) * up for the 8-interleaved gate|up weight W [N, K] (N = 2 I)
+int docqa_mgemm_glu(const void* X, const void* W, void* Y, int M, int N, int K, int cfg, hipStream_t s) {
+  if (cfg == 0) cfg = kDefaultCfg;
+  if (M == 0) return 0;
+  if (!shape_ok(M, N, K, 1, cfg) || !docqa_aligned16(X) || !docqa_aligned16(W) || !docqa_aligned16(Y)) return -1;
+  return launch_cfg<EPI_GLU>(cfg, (const uint16_t*)X, (const uint16_t*)W, (uint16_t*)Y, nullptr, nullptr, nullptr,
+                             M, N, K, 1, N, s);
+}
+
+// out[M] = argmax over the first n_valid columns of bf16(X . W^T) (LM head + greedy pick);
+// ws_v / ws_i: [M, N / tile_n] partials
+int docqa_mgemm_argmax(const void* X, const void* W, int64_t* out, float* ws_v, int* ws_i, int M, int N,
+                       int K, int n_valid, int cfg, hipStream_t s) {
+  if (cfg == 0) cfg = kDefaultCfg;
+  if (M == 0) return 0;
+  if (!shape_ok(M, N, K, 1, cfg) || n_valid <= 0 || n_valid > N) return -1;
+  if (!docqa_aligned16(X) || !docqa_aligned16(W)) return -1;
+  const int rc = launch_cfg<EPI_ARGMAX>(cfg, (const uint16_t*)X, (const uint16_t*)W, nullptr, nullptr, ws_v, ws_i,
+                                        M, N, K, 1, n_valid, s);
+  if (rc) return rc;
+  mgemm_argmax_merge<<<M, 64, 0, s>>>(ws_v, ws_i, N / kCfg[cfg].bn, out);
+  DOCQA_CHECK_LAUNCH();
+  return 0;
+}

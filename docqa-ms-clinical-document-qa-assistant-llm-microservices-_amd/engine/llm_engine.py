@@ -210,8 +210,11 @@ class LLMEngine:
         if g.cascade:
             meta.shared_table, meta.shared_len = g.shared_table, g.shared_len
             meta.cascade_chunks = self._cascade_chunks(g.bp)
-        logits = self.model.forward(g.tokens, meta, self.kv.caches)
-        nxt = self._select(logits, g)
+        if g.greedy:
+            # greedy: the LM head's argmax is fused into its GEMM (no [B, vocab] logits)
+            nxt = self.model.forward(g.tokens, meta, self.kv.caches, greedy_ids=True)
+        else:
+            nxt = self._select(self.model.forward(g.tokens, meta, self.kv.caches), g)
         ops.decode_advance(nxt.long().contiguous(), g.out, g.tokens, g.positions, g.context_lens, g.valid)
 
     def _select(self, logits, g: _DecodeGraph):

@@ -221,9 +221,11 @@ class LlamaModel:
 
     # ------------------------------------------------------------------ forward
     def forward(self, input_ids: torch.Tensor, meta: AttnMeta, kv_caches: list,
-                logits_index: torch.Tensor | None = None) -> torch.Tensor:
-        """input_ids [T] int32 -> logits fp32 [R, vocab_shard] for the rows selected by
-        ``logits_index`` (all rows if None).  kv_caches: list of (k_cache, v_cache)."""
+                logits_index: torch.Tensor | None = None, greedy_ids: bool = False) -> torch.Tensor:
+        """input_ids [T] int32 -> logits [R, vocab_shard] for the rows selected by
+        ``logits_index`` (all rows if None).  kv_caches: list of (k_cache, v_cache).
+        ``greedy_ids``: return the greedy token ids int64 [R] instead (the LM head's argmax
+        is fused into its GEMM where :func:`ops.lm_head_argmax_ok`)."""
         cfg = self.cfg
         D, hq, hkv, eps = cfg.head_dim, self.hq, self.hkv, cfg.rms_eps
         h = ops.embedding(input_ids, self.embed)
@@ -238,18 +240,38 @@ class LlamaModel:
         M = x.shape[0]
         sq = so = sd = 0
         tq = to = td = 64
-        if decode and self.tp == 1 and self.layers:
+        # 193..512 rows (batch-256 decode buckets): the mid-M MFMA GEMM (mgemm.hip) -- split-K
+        # slabs for QKV / O / down into the same fused consumers, fused SwiGLU for gate|up
+        mid = decode and self.tp == 1 and bool(self.layers) and ops.mid_plan(M, *self.layers[0]["qkv"].shape)[0] > 0
+        if mid:
+            L0 = self.layers[0]
+            (sq, cq), (so, co), (sd, cd) = (ops.mid_plan(M, *L0[k].shape) for k in ("qkv", "o", "down"))
+            cg = ops.mid_plan(M, *L0["gate_up"].shape)[1]
+
+            def part(a, w, S, c):
+                return ops.mgemm_partial(a, w, S, c) if S > 1 else ops.mgemm_partial(a, w, 1, c).float()[None]
+
+            qkv_part = lambda a, w: part(a, w, sq, cq)   # noqa: E731
+            o_part = lambda a, w: part(a, w, so, co)     # noqa: E731
+            down_part = lambda a, w: part(a, w, sd, cd)  # noqa: E731
+            glu = lambda a, w: ops.mgemm_glu(a, w, cg)   # noqa: E731
+        elif decode and self.tp == 1 and self.layers:
             L0 = self.layers[0]
             sq, tq = ops.decode_plan(M, *L0["qkv"].shape)
             so, to = ops.decode_plan(M, *L0["o"].shape)
             sd, td = ops.decode_plan(M, *L0["down"].shape)
+        if not mid:
+            qkv_part = lambda a, w: ops.dgemm_partial(a, w, sq, tq)   # noqa: E731
+            o_part = lambda a, w: ops.dgemm_partial(a, w, so, to)     # noqa: E731
+            down_part = lambda a, w: ops.dgemm_partial(a, w, sd, td)  # noqa: E731
+            glu = ops.glu_linear
         cascade = decode and meta.shared_len is not None
         for i, L in enumerate(self.layers):
             kc, vc = kv_caches[i]
             if cascade:
                 # shared-prefix decode: RoPE + cache write, then prefix-once + suffix attention
                 if sq:
-                    qkv = ops.rope_cache_splitk(ops.dgemm_partial(x, L["qkv"], sq, tq), meta.positions,
+                    qkv = ops.rope_cache_splitk(qkv_part(x, L["qkv"]), meta.positions,
                                                 self.cos_sin, meta.slot_mapping, kc, vc, hq, hkv, D)
                     a = ops.paged_decode_cascade(qkv, kc, vc, meta.block_tables, meta.context_lens, hq,
                                                  meta.max_context, self.scale, meta.shared_table,
@@ -270,12 +292,12 @@ class LlamaModel:
                 qkv = None
             elif sq and ops.fused_decode_ok(kc, meta.block_tables):
                 # QKV partials -> RoPE + new-token cache write + attention, one launch
-                a = ops.paged_decode_fused(ops.dgemm_partial(x, L["qkv"], sq, tq), meta.positions, self.cos_sin,
+                a = ops.paged_decode_fused(qkv_part(x, L["qkv"]), meta.positions, self.cos_sin,
                                            meta.slot_mapping, kc, vc, meta.block_tables, meta.context_lens,
                                            hq, meta.max_context, self.scale, meta.seq_order)
                 qkv = None
             elif sq:
-                qkv = ops.rope_cache_splitk(ops.dgemm_partial(x, L["qkv"], sq, tq), meta.positions, self.cos_sin,
+                qkv = ops.rope_cache_splitk(qkv_part(x, L["qkv"]), meta.positions, self.cos_sin,
                                             meta.slot_mapping, kc, vc, hq, hkv, D)
             else:
                 qkv = lin(x, L["qkv"])
@@ -292,22 +314,26 @@ class LlamaModel:
                 a = ops.paged_decode(qkv, kc, vc, meta.block_tables, meta.context_lens, hq,
                                      meta.max_context, self.scale, meta.seq_order)
             if so:
-                x = ops.add_rmsnorm_splitk(ops.dgemm_partial(a, L["o"], so, to), residual, L["post_norm"], eps)
+                x = ops.add_rmsnorm_splitk(o_part(a, L["o"]), residual, L["post_norm"], eps)
             else:
                 o = comm.tp_all_reduce(lin(a, L["o"]))
                 x = ops.add_rmsnorm(o, residual, L["post_norm"], eps)
             if decode:
-                g = ops.glu_linear(x, L["gate_up"])
+                g = glu(x, L["gate_up"])
             else:
                 g = ops.silu_mul(F.linear(x, L["gate_up"]), interleaved=True)
             nxt = self.layers[i + 1]["in_norm"] if i + 1 < nl else self.final_norm
             if sd:
-                x = ops.add_rmsnorm_splitk(ops.dgemm_partial(g, L["down"], sd, td), residual, nxt, eps)
+                x = ops.add_rmsnorm_splitk(down_part(g, L["down"]), residual, nxt, eps)
             else:
                 m = comm.tp_all_reduce(lin(g, L["down"]))
                 x = ops.add_rmsnorm(m, residual, nxt, eps)
         if logits_index is not None:
             x = x.index_select(0, logits_index)
+        if greedy_ids:
+            if self.tp == 1 and ops.lm_head_argmax_ok(x.shape[0], *self.lm_head.shape):
+                return ops.lm_head_argmax(x, self.lm_head, self.cfg.vocab_size)
+            return self.greedy(F.linear(x, self.lm_head))
         return F.linear(x, self.lm_head)
 
     def greedy(self, logits: torch.Tensor) -> torch.Tensor:

@@ -227,6 +227,61 @@ def dgemm_partial(x, w, splits: int, tile_rows: int = 64):
     return torch.einsum("msk,nsk->smn", xs, ws).contiguous()
 
 
+MID_M_MIN, MID_M_MAX = 193, 512
+_MID_OFF = os.environ.get("DOCQA_MID_GEMM", "1") == "0"
+_MID_CFG = int(os.environ.get("DOCQA_MID_CFG", "2"))
+
+
+def mid_plan(M: int, N: int, K: int) -> tuple[int, int]:
+    """(split-K count, kernel variant) of the mid-M decode GEMM (csrc/kernels/mgemm.hip) for
+    an [M, K] x [N, K]^T projection at 193..512 rows; (0, 0) where it does not apply.
+
+    Every workgroup owns all 256 rows of an m-tile x 128 weight rows; S is the largest power
+    of two keeping (N / 128) x m-tiles x S <= 256 workgroups (one round on the 256 CUs).
+    Measured at M = 256 against hipBLASLt (scripts/mgemm_probe.py, weights rotated past the
+    MALL; profiles/r2_mgemm_probe_m256.log): QKV S=4 22.3 us vs 42.3, O S=8 17.5 vs 23.0,
+    down S=8 40.2 vs 63.1, fused SwiGLU gate|up S=1 75.4 vs 74.7 + a 5.9 us silu_mul."""
+    if _MID_OFF or not (MID_M_MIN <= M <= MID_M_MAX) or N % 128 or K % 128:
+        return 0, 0
+    tiles = (N // 128) * ((M + 255) // 256)
+    S = 1
+    while tiles * S * 2 <= 256 and K % (S * 2 * 128) == 0:
+        S *= 2
+    return S, _MID_CFG
+
+
+def mgemm_partial(x, w, splits: int, cfg: int = 0):
+    """Split-K partial slabs [S, M, N] fp32 of x @ w^T on the mid-M decode GEMM (S = 1:
+    the bf16 product [M, N])."""
+    if _gpu(x):
+        return _native().mgemm(x.contiguous(), w, splits, cfg)
+    if splits == 1:
+        return torch.nn.functional.linear(x, w)
+    K = w.shape[1]
+    xs = x.float().reshape(-1, splits, K // splits)
+    ws = w.float().reshape(-1, splits, K // splits)
+    return torch.einsum("msk,nsk->smn", xs, ws).contiguous()
+
+
+def mgemm_glu(x, w_il, cfg: int = 0):
+    """silu(x Wg^T) * (x Wu^T) for 8-interleaved gate|up weights on the mid-M decode GEMM."""
+    if _gpu(x):
+        return _native().mgemm_glu(x.contiguous(), w_il, cfg)
+    return silu_mul(torch.nn.functional.linear(x, w_il), interleaved=True)
+
+
+def lm_head_argmax(x, w, n_valid: int, cfg: int = 0):
+    """Greedy token ids argmax(bf16(x @ w[:n_valid]^T)) with the LM-head GEMM and the argmax
+    fused (mgemm.hip EPI_ARGMAX): the [M, vocab] logits never reach HBM."""
+    if _gpu(x):
+        return _native().mgemm_argmax(x.contiguous(), w, int(n_valid), cfg)
+    return ref.argmax(torch.nn.functional.linear(x, w[:n_valid]))
+
+
+def lm_head_argmax_ok(M: int, N: int, K: int) -> bool:
+    return not _MID_OFF and MID_M_MIN <= M <= MID_M_MAX and N % 128 == 0 and K % 128 == 0
+
+
 def add_rmsnorm_splitk(P, residual, w, eps: float):
     """residual <- residual + bf16(sum_s P[s]); returns rmsnorm(residual) * w."""
     if _gpu(P):

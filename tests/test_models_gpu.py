@@ -99,6 +99,55 @@ def test_llama_prefill_decode_logits_native_vs_reference(native):
     assert _rel(d1, d2) < 0.03
 
 
+def test_llama_mid_batch_decode_native_vs_reference(native):
+    """A 256-row decode step (the mid-M GEMM path: split-K QKV / O / down slabs, fused
+    SwiGLU, fused LM-head argmax) against the same step on the fp32 reference ops."""
+    from docqa_amd.engine.kv_cache import KVCache
+    from docqa_amd.models.llama import LlamaConfig, LlamaModel
+
+    m = LlamaModel(LlamaConfig.preset("llama3-1b-test"), device="cuda", seed=5)
+    assert native.mid_plan(256, *m.layers[0]["qkv"].shape)[0] > 0
+    g = torch.Generator().manual_seed(3)
+    prompts = [torch.randint(0, 32000, (int(n),), generator=g).tolist()
+               for n in torch.randint(3, 90, (256,), generator=g)]
+    BS = 64
+    nxt = torch.randint(0, 32000, (256,), generator=g).tolist()
+    kv1 = KVCache(m.cfg.layers, 800, m.hkv, m.cfg.head_dim, BS).caches
+    kv2 = KVCache(m.cfg.layers, 800, m.hkv, m.cfg.head_dim, BS).caches
+    _, tables = _prefill_logits(m, kv1, prompts, BS)
+    d1 = _decode_logits(m, kv1, prompts, tables, nxt, BS)
+    with native.use_reference():
+        _prefill_logits(m, kv2, prompts, BS)
+        d2 = _decode_logits(m, kv2, prompts, tables, nxt, BS)
+    assert _rel(d1, d2) < 0.03
+    # fused LM head + argmax on the same step == argmax of the bf16 logits (up to near-ties)
+    _prefill_logits(m, kv1, prompts, BS)
+    ids = _decode_ids(m, kv1, prompts, tables, nxt, BS)
+    ref = d1.float().argmax(1)
+    top = d1.float().max(1).values
+    pick = d1.float().gather(1, ids[:, None])[:, 0]
+    assert ((top - pick) <= 2e-2 * top.abs().clamp_min(1)).all()
+    assert (ids == ref).float().mean().item() > 0.95
+
+
+def _decode_ids(m, kv, prompts, tables, next_tok, BS):
+    from docqa_amd.models.llama import AttnMeta
+
+    B = len(prompts)
+    maxb = max(len(t) for t in tables)
+    bt = torch.zeros(B, maxb, dtype=torch.int32)
+    for i, t in enumerate(tables):
+        bt[i, :len(t)] = torch.tensor(t)
+    lens = [len(p) for p in prompts]
+    slots = [tables[i][lens[i] // BS] * BS + lens[i] % BS for i in range(B)]
+    meta = AttnMeta(prefill=False, positions=torch.tensor(lens, dtype=torch.int32, device="cuda"),
+                    slot_mapping=torch.tensor(slots, dtype=torch.int32, device="cuda"),
+                    block_tables=bt.cuda(),
+                    context_lens=torch.tensor([n + 1 for n in lens], dtype=torch.int32, device="cuda"),
+                    max_context=maxb * BS)
+    return m.forward(torch.tensor(next_tok, dtype=torch.int32, device="cuda"), meta, kv, greedy_ids=True)
+
+
 def test_llama_graph_vs_eager(native, monkeypatch):
     monkeypatch.setenv("DOCQA_TUNE_DECODE", "0")  # same GEMM kernels on both paths
     from docqa_amd.engine.llm_engine import LLMEngine, SamplingParams
