@@ -138,19 +138,38 @@ __global__ __launch_bounds__(WM * WN * 64) void mgemm_kernel(const uint16_t* __r
 #pragma unroll
     for (int j = 0; j < NJ; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  // fragments of one stage: [k-step][m-tile] A, [k-step][n-tile] B
+  // fragments of one stage: [k-step][m-tile] A, [k-step][n-tile] B.  They are read by
+  // inline-asm ds_read_b128 (invisible to hipcc's waitcnt pass, which otherwise drains
+  // every outstanding LDS read -- the next stage's prefetch included -- before the first
+  // MFMA of the current stage) and published by an explicit lgkmcnt(0) that names them
+  // (`publish`), so no MFMA reading them can be scheduled above the wait.
   struct Frag { bf16x8 a[KS][MI]; bf16x8 b[KS][NJ]; };
+  const uint32_t a_off = (uint32_t)(wm * (BM / WM) + fr), b_off = (uint32_t)(BM + wn * CW + fr);
   auto load_frags = [&](Frag& f, int kt) {
-    const uint16_t* sa = smem + (kt % NSR) * SLOT;
-    const uint16_t* sb = sa + BM * BKS;
+    const uint32_t slot = base + (uint32_t)((kt % NSR) * SLOT * 2);
 #pragma unroll
     for (int ks = 0; ks < KS; ++ks) {
       const int ch = ks * 4 + fq;
 #pragma unroll
-      for (int j = 0; j < NJ; ++j) f.b[ks][j] = *reinterpret_cast<const bf16x8*>(sb + swz<BKS>(wn * CW + j * 16 + fr, ch));
+      for (int j = 0; j < NJ; ++j) {
+        const uint32_t ad = slot + (uint32_t)swz<BKS>(b_off + j * 16, ch) * 2;
+        asm volatile("ds_read_b128 %0, %1" : "=v"(f.b[ks][j]) : "v"(ad) : "memory");
+      }
 #pragma unroll
-      for (int i = 0; i < MI; ++i)
-        f.a[ks][i] = *reinterpret_cast<const bf16x8*>(sa + swz<BKS>(wm * (BM / WM) + i * 16 + fr, ch));
+      for (int i = 0; i < MI; ++i) {
+        const uint32_t ad = slot + (uint32_t)swz<BKS>(a_off + i * 16, ch) * 2;
+        asm volatile("ds_read_b128 %0, %1" : "=v"(f.a[ks][i]) : "v"(ad) : "memory");
+      }
+    }
+  };
+  auto publish = [&](Frag& f) {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) {
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) asm volatile("" : "+v"(f.b[ks][j]));
+#pragma unroll
+      for (int i = 0; i < MI; ++i) asm volatile("" : "+v"(f.a[ks][i]));
     }
   };
   auto mma = [&](const Frag& f) {
@@ -164,22 +183,25 @@ __global__ __launch_bounds__(WM * WN * 64) void mgemm_kernel(const uint16_t* __r
   };
   // Schedule (NSR slots): the fragments of stage kt+1 are read from LDS while the MFMAs of
   // stage kt run, and NSR-2 DMA stages stream behind them.  Step kt: [frags(kt) landed:
-  // lgkmcnt(0)] [DMA(kt+1) landed: vmcnt] barrier [DMA(kt+NSR) into slot kt % NSR, which
-  // frags(kt) -- now in registers in every wave -- vacated] [ds_read frags(kt+1)] [MFMA(kt)]
+  // publish] [DMA(kt+1) landed: vmcnt] barrier [DMA(kt+NSR) into slot kt % NSR, which
+  // frags(kt) -- now in registers in every wave -- vacated] [ds_read frags(kt+1)] [MFMA(kt)].
+  // The fragment reads are issued on every step (the last one reads a dead slot) so the
+  // only control flow in the loop is scalar branches around asm (DMA issue, vmcnt).
   auto step = [&](Frag& cur, Frag& nxt, int kt) {
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    if (kt + 1 < nk) {
-      // DMA stages issued so far: 0 .. min(nk - 1, kt + NSR - 1); kt+1 must have landed
-      const int ahead = min(nk - 1, kt + NSR - 1) - (kt + 1);
-      if (ahead >= NSR - 2) wait_vmcnt<(NSR - 2) * PER_STAGE>();
-      else if (NSR >= 4 && ahead == NSR - 3) wait_vmcnt<(NSR >= 4 ? NSR - 3 : 0) * PER_STAGE>();
-      else if (NSR >= 5 && ahead == NSR - 4) wait_vmcnt<(NSR >= 5 ? NSR - 4 : 0) * PER_STAGE>();
-      else wait_vmcnt<0>();
-      ring_barrier();
-      if (kt + NSR < nk) stage(kt + NSR);
-      load_frags(nxt, kt + 1);
-    }
+    publish(cur);
+    // DMA stages issued so far: 0 .. min(nk - 1, kt + NSR - 1); kt+1 must have landed
+    const int ahead = min(nk - 1, kt + NSR - 1) - (kt + 1);
+    if (ahead >= NSR - 2) wait_vmcnt<(NSR - 2) * PER_STAGE>();
+    else if (NSR >= 4 && ahead == NSR - 3) wait_vmcnt<(NSR >= 4 ? NSR - 3 : 0) * PER_STAGE>();
+    else if (NSR >= 5 && ahead == NSR - 4) wait_vmcnt<(NSR >= 5 ? NSR - 4 : 0) * PER_STAGE>();
+    else wait_vmcnt<0>();
+    ring_barrier();
+    if (kt + NSR < nk) stage(kt + NSR);
+    load_frags(nxt, kt + 1);
     mma(cur);
+    // keep this stage's MFMAs above the next stage's publish wait (hipcc otherwise sinks
+    // some of them below it, where they wait for the whole prefetch)
+    __builtin_amdgcn_sched_barrier(0);
   };
   Frag f0, f1;
 #pragma unroll

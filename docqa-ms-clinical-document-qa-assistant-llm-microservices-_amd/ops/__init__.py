@@ -236,17 +236,18 @@ def mid_plan(M: int, N: int, K: int) -> tuple[int, int]:
     """(split-K count, kernel variant) of the mid-M decode GEMM (csrc/kernels/mgemm.hip) for
     an [M, K] x [N, K]^T projection at 193..512 rows; (0, 0) where it does not apply.
 
-    Every workgroup owns all 256 rows of an m-tile x 128 weight rows; S is the largest power
-    of two keeping (N / 128) x m-tiles x S <= 256 workgroups (one round on the 256 CUs).
+    Every workgroup owns all 256 rows of an m-tile x 128 weight rows; S is the largest
+    divisor of K / 128 keeping (N / 128) x m-tiles x S <= 224 workgroups (one round on the
+    256 CUs; fewer, larger slabs for the consumer where a round is already full).
     Measured at M = 256 against hipBLASLt (scripts/mgemm_probe.py, weights rotated past the
-    MALL; profiles/r2_mgemm_probe_m256.log): QKV S=4 22.3 us vs 42.3, O S=8 17.5 vs 23.0,
-    down S=8 40.2 vs 63.1, fused SwiGLU gate|up S=1 75.4 vs 74.7 + a 5.9 us silu_mul."""
+    MALL; profiles/r2_mgemm_probe_m256_v5.log): QKV S=4 21.9 us vs 43.1, O S=4 20.3 vs
+    26.8 (S=8: 20.8 with twice the slab bytes), down S=7 40.1 vs 63.3, fused SwiGLU gate|up
+    S=1 75.4 vs 67.8 + a 5.9 us silu_mul + a [M, 2I] round trip."""
     if _MID_OFF or not (MID_M_MIN <= M <= MID_M_MAX) or N % 128 or K % 128:
         return 0, 0
     tiles = (N // 128) * ((M + 255) // 256)
-    S = 1
-    while tiles * S * 2 <= 256 and K % (S * 2 * 128) == 0:
-        S *= 2
+    kb = K // 128
+    S = max(s for s in range(1, kb + 1) if kb % s == 0 and (s == 1 or tiles * s <= 224))
     return S, _MID_CFG
 
 
