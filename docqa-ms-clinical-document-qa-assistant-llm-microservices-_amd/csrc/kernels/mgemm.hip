@@ -55,7 +55,10 @@ __device__ __forceinline__ void better(float& bv, int& bi, float v, int i) {
   if (v > bv || (v == bv && i < bi)) { bv = v; bi = i; }
 }
 
-template <int EPI, int BN, int BKS, int NSR, int WM, int WN>
+// PF: fragment prefetch (stage k+1's LDS reads under stage k's MFMAs, two register sets);
+// PF = 0 reads each stage's fragments after its barrier (one register set, for the
+// 128 x 128-per-wave layout whose two sets would not fit)
+template <int EPI, int BN, int BKS, int NSR, int WM, int WN, int PF = 1>
 __global__ __launch_bounds__(WM * WN * 64) void mgemm_kernel(const uint16_t* __restrict__ X,
                                                              const uint16_t* __restrict__ W,
                                                              uint16_t* __restrict__ Y,
@@ -75,7 +78,7 @@ __global__ __launch_bounds__(WM * WN * 64) void mgemm_kernel(const uint16_t* __r
   constexpr int PER_STAGE = A_PER_WAVE + B_PER_WAVE;
   constexpr int SLOT = (BM + BN) * BKS;                 // elements per ring slot
   constexpr int SCR = CW + 4;                           // scratch row pitch (floats)
-  static_assert(NSR >= 3, "fragment-prefetch ring needs >= 3 slots");
+  static_assert(NSR >= 2, "ring needs >= 2 slots");
   static_assert(A_PER_WAVE * RPI * WAVES == BM && B_PER_WAVE * RPI * WAVES == BN, "DMA split");
   static_assert(NSR * SLOT * 2 <= 160 * 1024, "LDS");
   __shared__ __attribute__((aligned(16))) uint16_t smem[NSR * SLOT];
@@ -203,17 +206,49 @@ __global__ __launch_bounds__(WM * WN * 64) void mgemm_kernel(const uint16_t* __r
     // some of them below it, where they wait for the whole prefetch)
     __builtin_amdgcn_sched_barrier(0);
   };
-  Frag f0, f1;
 #pragma unroll
   for (int j = 0; j < NSR; ++j)
     if (j < nk) stage(j);
-  if (nk >= NSR) wait_vmcnt<(NSR - 1) * PER_STAGE>();
-  else wait_vmcnt<0>();
-  ring_barrier();
-  load_frags(f0, 0);
-  for (int kt = 0; kt < nk; kt += 2) {
-    step(f0, f1, kt);
-    step(f1, f0, kt + 1);
+  if constexpr (PF) {
+    Frag f0, f1;
+    if (nk >= NSR) wait_vmcnt<(NSR - 1) * PER_STAGE>();
+    else wait_vmcnt<0>();
+    ring_barrier();
+    load_frags(f0, 0);
+    for (int kt = 0; kt < nk; kt += 2) {
+      step(f0, f1, kt);
+      step(f1, f0, kt + 1);
+    }
+  } else {
+    // plain ring: [DMA(kt) landed] barrier [DMA(kt+NSR-1) into the slot read in step kt-1]
+    // [fragments of kt -> MFMAs, k-step by k-step so the compiler overlaps the reads]
+    const uint16_t* sbase = smem;
+    for (int kt = 0; kt < nk; ++kt) {
+      // stages issued so far: 0 .. NSR-1 by the prologue, then one per step from step 1
+      const int ahead = min(nk - 1, kt == 0 ? NSR - 1 : kt + NSR - 2) - kt;
+      if (ahead >= NSR - 1) wait_vmcnt<(NSR - 1) * PER_STAGE>();
+      else if (NSR >= 3 && ahead == NSR - 2) wait_vmcnt<(NSR >= 3 ? NSR - 2 : 0) * PER_STAGE>();
+      else wait_vmcnt<0>();
+      ring_barrier();
+      if (kt + NSR - 1 < nk && kt > 0) stage(kt + NSR - 1);
+      const uint16_t* sa = sbase + (kt % NSR) * SLOT;
+      const uint16_t* sb = sa + BM * BKS;
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks) {
+        const int ch = ks * 4 + fq;
+        bf16x8 b[NJ];
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) b[j] = *reinterpret_cast<const bf16x8*>(sb + swz<BKS>(wn * CW + j * 16 + fr, ch));
+#pragma unroll
+        for (int i = 0; i < MI; ++i) {
+          const bf16x8 a = *reinterpret_cast<const bf16x8*>(sa + swz<BKS>(wm * (BM / WM) + i * 16 + fr, ch));
+#pragma unroll
+          for (int j = 0; j < NJ; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b[j], acc[i][j], 0, 0, 0);
+        }
+      }
+      // every wave's reads of this slot retire before the next barrier frees it
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    }
   }
   wait_vmcnt<0>();
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -339,10 +374,13 @@ __global__ __launch_bounds__(64) void mgemm_argmax_merge(const float* __restrict
 //   2: BN 128, 64-deep stages x 3, waves 4 x 2 ( 64 x 64 each, 2 waves / SIMD)
 //   3: BN 256, 32-deep stages x 4, waves 2 x 4 (128 x 64 each, 2 waves / SIMD)
 //   4: BN 256, 32-deep stages x 4, waves 2 x 2 (128 x 128 each, 1 wave / SIMD)
+//   5: BN 256, 64-deep stages x 2, waves 2 x 2 (128 x 128 each, 1 wave / SIMD), no prefetch
+//   6: BN 256, 64-deep stages x 2, waves 2 x 4 (128 x 64 each, 2 waves / SIMD), no prefetch
 struct Cfg { int bn, bks; };
-constexpr Cfg kCfg[5] = {{0, 0}, {128, 64}, {128, 64}, {256, 32}, {256, 32}};
+constexpr int kNumCfg = 6;
+constexpr Cfg kCfg[kNumCfg + 1] = {{0, 0}, {128, 64}, {128, 64}, {256, 32}, {256, 32}, {256, 64}, {256, 64}};
 
-template <int EPI, int BN, int BKS, int NSR, int WM, int WN>
+template <int EPI, int BN, int BKS, int NSR, int WM, int WN, int PF = 1>
 int launch(const uint16_t* x, const uint16_t* w, uint16_t* y, float* p, float* pv, int* pi, int M,
            int N, int K, int S, int n_valid, hipStream_t s) {
   const int ntiles = N / BN, Ks = K / S;
@@ -350,7 +388,7 @@ int launch(const uint16_t* x, const uint16_t* w, uint16_t* y, float* p, float* p
   if (S > 1 && 8 % S == 0 && (ntiles * S) % 8 == 0) remap = 1;
   else if (S > 8 && S % 8 == 0) remap = 2;
   dim3 grid(ntiles * S, (M + BM - 1) / BM);
-  mgemm_kernel<EPI, BN, BKS, NSR, WM, WN><<<grid, WM * WN * 64, 0, s>>>(x, w, y, p, pv, pi, M, N, K, Ks, S,
+  mgemm_kernel<EPI, BN, BKS, NSR, WM, WN, PF><<<grid, WM * WN * 64, 0, s>>>(x, w, y, p, pv, pi, M, N, K, Ks, S,
                                                                       ntiles, remap, n_valid);
   DOCQA_CHECK_LAUNCH();
   return 0;
@@ -364,12 +402,14 @@ int launch_cfg(int cfg, const uint16_t* x, const uint16_t* w, uint16_t* y, float
     case 2: return launch<EPI, 128, 64, 3, 4, 2>(x, w, y, p, pv, pi, M, N, K, S, n_valid, s);
     case 3: return launch<EPI, 256, 32, 4, 2, 4>(x, w, y, p, pv, pi, M, N, K, S, n_valid, s);
     case 4: return launch<EPI, 256, 32, 4, 2, 2>(x, w, y, p, pv, pi, M, N, K, S, n_valid, s);
+    case 5: return launch<EPI, 256, 64, 2, 2, 2, 0>(x, w, y, p, pv, pi, M, N, K, S, n_valid, s);
+    case 6: return launch<EPI, 256, 64, 2, 2, 4, 0>(x, w, y, p, pv, pi, M, N, K, S, n_valid, s);
     default: return -1;
   }
 }
 
 bool shape_ok(int M, int N, int K, int S, int cfg) {
-  if (cfg < 1 || cfg > 4 || M <= 0 || S < 1) return false;
+  if (cfg < 1 || cfg > kNumCfg || M <= 0 || S < 1) return false;
   // whole pairs of stages per K slice (the main loop is unrolled by two)
   return N % kCfg[cfg].bn == 0 && K % (S * 2 * kCfg[cfg].bks) == 0;
 }
@@ -378,7 +418,7 @@ bool shape_ok(int M, int N, int K, int S, int cfg) {
 constexpr int kDefaultCfg = 2;
 int docqa_mgemm_tile_n(int cfg) {
   if (cfg == 0) cfg = kDefaultCfg;
-  return cfg >= 1 && cfg <= 4 ? kCfg[cfg].bn : 0;
+  return cfg >= 1 && cfg <= kNumCfg ? kCfg[cfg].bn : 0;
 }
 
 // S == 1: Y bf16 [M, N];  S > 1: P fp32 split-K slabs [S, M, N] (combined by the consumer)

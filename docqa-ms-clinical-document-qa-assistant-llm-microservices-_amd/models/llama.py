@@ -238,33 +238,28 @@ class LlamaModel:
         decode = not meta.prefill
         lin = ops.decode_linear if decode else F.linear
         M = x.shape[0]
-        sq = so = sd = 0
-        tq = to = td = 64
-        # 193..512 rows (batch-256 decode buckets): the mid-M MFMA GEMM (mgemm.hip) -- split-K
-        # slabs for QKV / O / down into the same fused consumers, fused SwiGLU for gate|up
-        mid = decode and self.tp == 1 and bool(self.layers) and ops.mid_plan(M, *self.layers[0]["qkv"].shape)[0] > 0
-        if mid:
+        # decode projections, per projection: the mid-M MFMA GEMM (mgemm.hip, 129..512 rows
+        # where it wins -- ops.mid_plan) or the skinny weight-streaming kernel (dgemm.hip,
+        # <= 192 rows -- ops.decode_plan) emit split-K slabs into the fused consumers
+        # (rope_cache_splitk / add_rmsnorm_splitk); split 0 = library GEMM + plain consumer
+        plans = {}
+        if decode and self.tp == 1 and self.layers:
             L0 = self.layers[0]
-            (sq, cq), (so, co), (sd, cd) = (ops.mid_plan(M, *L0[k].shape) for k in ("qkv", "o", "down"))
-            cg = ops.mid_plan(M, *L0["gate_up"].shape)[1]
-
-            def part(a, w, S, c):
-                return ops.mgemm_partial(a, w, S, c) if S > 1 else ops.mgemm_partial(a, w, 1, c).float()[None]
-
-            qkv_part = lambda a, w: part(a, w, sq, cq)   # noqa: E731
-            o_part = lambda a, w: part(a, w, so, co)     # noqa: E731
-            down_part = lambda a, w: part(a, w, sd, cd)  # noqa: E731
-            glu = lambda a, w: ops.mgemm_glu(a, w, cg)   # noqa: E731
-        elif decode and self.tp == 1 and self.layers:
-            L0 = self.layers[0]
-            sq, tq = ops.decode_plan(M, *L0["qkv"].shape)
-            so, to = ops.decode_plan(M, *L0["o"].shape)
-            sd, td = ops.decode_plan(M, *L0["down"].shape)
-        if not mid:
-            qkv_part = lambda a, w: ops.dgemm_partial(a, w, sq, tq)   # noqa: E731
-            o_part = lambda a, w: ops.dgemm_partial(a, w, so, to)     # noqa: E731
-            down_part = lambda a, w: ops.dgemm_partial(a, w, sd, td)  # noqa: E731
+            for k in ("qkv", "o", "down"):
+                S, c = ops.mid_plan(M, *L0[k].shape)
+                if S:
+                    plans[k] = (S, lambda a, w, S=S, c=c: (ops.mgemm_partial(a, w, S, c) if S > 1
+                                                          else ops.mgemm_partial(a, w, 1, c).float()[None]))
+                else:
+                    S, t = ops.decode_plan(M, *L0[k].shape)
+                    plans[k] = (S, lambda a, w, S=S, t=t: ops.dgemm_partial(a, w, S, t))
+            Sg, cg = ops.mid_plan(M, *L0["gate_up"].shape)
+            glu = (lambda a, w: ops.mgemm_glu(a, w, cg)) if Sg else ops.glu_linear
+        else:
             glu = ops.glu_linear
+        sq, qkv_part = plans.get("qkv", (0, None))
+        so, o_part = plans.get("o", (0, None))
+        sd, down_part = plans.get("down", (0, None))
         cascade = decode and meta.shared_len is not None
         for i, L in enumerate(self.layers):
             kc, vc = kv_caches[i]

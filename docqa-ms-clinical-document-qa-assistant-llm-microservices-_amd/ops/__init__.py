@@ -227,14 +227,14 @@ def dgemm_partial(x, w, splits: int, tile_rows: int = 64):
     return torch.einsum("msk,nsk->smn", xs, ws).contiguous()
 
 
-MID_M_MIN, MID_M_MAX = 193, 512
+MID_M_MIN, MID_M_MAX = 129, 512
 _MID_OFF = os.environ.get("DOCQA_MID_GEMM", "1") == "0"
 _MID_CFG = int(os.environ.get("DOCQA_MID_CFG", "2"))
 
 
 def mid_plan(M: int, N: int, K: int) -> tuple[int, int]:
     """(split-K count, kernel variant) of the mid-M decode GEMM (csrc/kernels/mgemm.hip) for
-    an [M, K] x [N, K]^T projection at 193..512 rows; (0, 0) where it does not apply.
+    an [M, K] x [N, K]^T projection at 129..512 rows; (0, 0) where it does not apply.
 
     Every workgroup owns all 256 rows of an m-tile x 128 weight rows; S is the largest
     divisor of K / 128 keeping (N / 128) x m-tiles x S <= 224 workgroups (one round on the
@@ -244,6 +244,11 @@ def mid_plan(M: int, N: int, K: int) -> tuple[int, int]:
     26.8 (S=8: 20.8 with twice the slab bytes), down S=7 40.1 vs 63.3, fused SwiGLU gate|up
     S=1 75.4 vs 67.8 + a 5.9 us silu_mul + a [M, 2I] round trip."""
     if _MID_OFF or not (MID_M_MIN <= M <= MID_M_MAX) or N % 128 or K % 128:
+        return 0, 0
+    if M <= 192 and N >= 16384:
+        # 129..192 rows: the wide gate|up stays on hipBLASLt + silu_mul (56-62 us vs the
+        # fused 66-70 at M = 128-192); QKV / O / down gain (QKV 21.4 vs 33.7 at M = 192,
+        # down 38.5 vs dgemm 54.2; profiles/r2_mgemm_probe_m128_192.log)
         return 0, 0
     tiles = (N // 128) * ((M + 255) // 256)
     kb = K // 128
@@ -271,16 +276,24 @@ def mgemm_glu(x, w_il, cfg: int = 0):
     return silu_mul(torch.nn.functional.linear(x, w_il), interleaved=True)
 
 
-def lm_head_argmax(x, w, n_valid: int, cfg: int = 0):
+# LM head: 256-wide tiles (mgemm.hip cfg 6) halve the X re-reads of the 1002-tile vocab
+# sweep -- 281 vs 326 us with the argmax fused at M = 256 (profiles/r2_mgemm_probe_m256_v6.log)
+_LM_CFG = int(os.environ.get("DOCQA_LM_HEAD_CFG", "6"))
+
+
+def lm_head_argmax(x, w, n_valid: int, cfg: int = -1):
     """Greedy token ids argmax(bf16(x @ w[:n_valid]^T)) with the LM-head GEMM and the argmax
     fused (mgemm.hip EPI_ARGMAX): the [M, vocab] logits never reach HBM."""
     if _gpu(x):
+        if cfg < 0:
+            cfg = _LM_CFG if w.shape[0] % 256 == 0 else _MID_CFG
         return _native().mgemm_argmax(x.contiguous(), w, int(n_valid), cfg)
     return ref.argmax(torch.nn.functional.linear(x, w[:n_valid]))
 
 
 def lm_head_argmax_ok(M: int, N: int, K: int) -> bool:
-    return not _MID_OFF and MID_M_MIN <= M <= MID_M_MAX and N % 128 == 0 and K % 128 == 0
+    # from 193 rows (below, hipBLASLt + the argmax kernel is faster: 250 vs 274 us at M=128)
+    return not _MID_OFF and 193 <= M <= MID_M_MAX and N % 128 == 0 and K % 128 == 0
 
 
 def add_rmsnorm_splitk(P, residual, w, eps: float):

@@ -36,9 +36,11 @@ for (name, N, K) in [("qkv", 6144, 4096), ("o", 4096, 4096), ("gate_up", 28672, 
         got = nat.gemm(x, ws[0], None, None, 0).float()
         row["gemm128_err"] = float((got - ref).abs().max() / ref.abs().max())
         if hasattr(nat, "mgemm"):
-            for bn in (1, 2, 3, 4):
+            for bn in [int(c) for c in os.environ.get("PROBE_CFGS", "2,5,6").split(",")]:
                 for S in (1, 2, 4, 7, 8, 14, 16):
                     if K % (S * 128) or N % (128 if bn < 3 else 256) or (S > 1 and name in ("gate_up", "lm_head")):
+                        continue
+                    if S > 1 and (N // (128 if bn < 3 else 256)) * S > 512:
                         continue
                     it = iter(range(1 << 30))
                     try:

@@ -27,7 +27,8 @@ def _close(a, b, atol, rtol=0.0):
 @pytest.mark.parametrize("N,K,S,bn", [(6144, 4096, 4, 2), (4096, 4096, 8, 4), (4096, 14336, 7, 1),
                                       (4096, 14336, 8, 3), (1024, 1024, 1, 2), (1024, 1024, 2, 4),
                                       (512, 128, 1, 4), (768, 2048, 16, 1), (768, 3072, 4, 3),
-                                      (6144, 4096, 8, 3), (512, 64, 1, 3)])
+                                      (6144, 4096, 8, 3), (512, 64, 1, 3), (6144, 4096, 8, 5), (4096, 14336, 14, 6),
+                                      (1024, 1024, 1, 5), (512, 128, 1, 6), (768, 1024, 2, 6)])
 def test_mgemm(native, M, N, K, S, bn):
     x = torch.randn(M, K, device="cuda", dtype=torch.bfloat16)
     w = (torch.randn(N, K, device="cuda") / K ** 0.5).bfloat16()
@@ -42,7 +43,7 @@ def test_mgemm(native, M, N, K, S, bn):
             _close(out.sum(0), ref, 2e-3, 1e-3)
 
 
-@pytest.mark.parametrize("bn", [1, 2, 3, 4])
+@pytest.mark.parametrize("bn", [1, 2, 3, 4, 5, 6])
 def test_mgemm_asymmetric_identity(native, bn):
     """X = I rows against an asymmetric W: catches transposed / mis-placed tile writes."""
     M, N, K = 256, 512, 1024
@@ -56,7 +57,7 @@ def test_mgemm_asymmetric_identity(native, bn):
 
 
 @pytest.mark.parametrize("M", [200, 256, 333])
-@pytest.mark.parametrize("bn", [1, 2, 3, 4])
+@pytest.mark.parametrize("bn", [1, 2, 3, 4, 5, 6])
 def test_mgemm_glu(native, M, bn):
     from docqa_amd.ops import reference as R
 
@@ -69,7 +70,7 @@ def test_mgemm_glu(native, M, bn):
 
 
 @pytest.mark.parametrize("M", [1, 256, 300])
-@pytest.mark.parametrize("bn", [1, 2, 3, 4])
+@pytest.mark.parametrize("bn", [1, 2, 3, 4, 5, 6])
 def test_mgemm_argmax(native, M, bn):
     """LM head + greedy pick == argmax of the bf16 logits (ties: lowest id)."""
     N, K = 128256, 4096
