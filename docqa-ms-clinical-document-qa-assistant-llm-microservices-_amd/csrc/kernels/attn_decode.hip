@@ -811,6 +811,293 @@ __global__ __launch_bounds__(256) void paged_decode_mfma_kernel(
   wait_vmcnt<0>();                               // drain the clamped tail DMAs
 }
 
+// ---------------------------------------------------------------------------------------
+// Grouped decode attention over prefix-cache-shared KV blocks (Llama-3 GQA, G = 4).
+// In a RAG batch many rows retrieved the same chunks, and the prefix cache maps identical
+// prompt prefixes to the SAME physical KV blocks (a trie of blocks beyond the template
+// prefix that cascade attends once).  The per-row kernels re-read such a block once per
+// row.  Here a workgroup serves a GROUP of up to 4 rows (groups[4 g .. 4 g + 3], -1 = none:
+// the host packs rows with common block prefixes together) for one KV head: the 16 MFMA columns
+// are the 4 rows x 4 query heads, so a block shared by k rows of the group is streamed
+// once and scored against all their queries in the same MFMAs (the per-row MFMA kernel
+// leaves 12 of the 16 columns empty).  Blocks of only some rows are processed with the
+// other rows' columns masked; every column keeps its own online softmax, so the result
+// is exactly the per-row attention.  The tile list (block, half, row mask) is built in
+// LDS by wave 0 -- one lane per block position, a wave prefix sum for the offsets -- and
+// then streamed through the same LDS-DMA ring as the MFMA kernel.  Keys [P, L) per row
+// (P: the cascade prefix, attended by the prefix kernel and merged here).
+constexpr int kGroupMaxPos = 64;     // block positions beyond the cascade prefix (4096 tokens)
+
+template <int NSR = 3>
+__global__ __launch_bounds__(256) void paged_decode_group_kernel(
+    const uint16_t* __restrict__ q, int q_stride, const uint16_t* __restrict__ k_cache,
+    const uint16_t* __restrict__ v_cache, const int* __restrict__ block_tables, int maxb,
+    const int* __restrict__ context_lens, int B, int Hkv, float scale,
+    uint16_t* __restrict__ out, int out_stride, const int* __restrict__ groups, CascadeIn ci) {
+  constexpr int G = 4, R = 4, D = 128, TT = 32, MAXT = kGroupMaxPos * 8;
+  constexpr int TILE = TT * D;                   // elements of one K (or V) tile: 8 KB
+  __shared__ __attribute__((aligned(16))) uint16_t ring[NSR * 2 * TILE];
+  __shared__ int2 s_tl[MAXT];                    // (block id, pos << 8 | half << 4 | row mask)
+  __shared__ int s_nt;
+
+  const int kvh = blockIdx.x, grp = blockIdx.y;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int hl = lane & 15, lg = lane >> 4;      // MFMA column (row slot x head) / lane group
+  const int P = ci.plen ? *ci.plen : 0;          // multiple of 64
+  int rows[R], Ls[R];
+#pragma unroll
+  for (int r = 0; r < R; ++r) {
+    const int row = groups[R * grp + r];
+    rows[r] = row >= 0 && row < B ? row : -1;
+    Ls[r] = rows[r] >= 0 ? context_lens[rows[r]] : 0;
+  }
+
+  // ---- tile list: lane j of wave 0 owns block position P/64 + j
+  if (wave == 0) {
+    const int pos = (P >> 6) + lane;
+    int ids[R];
+    bool alive[R];
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      alive[r] = pos < maxb && 64 * pos < Ls[r];
+      ids[r] = alive[r] ? block_tables[(size_t)rows[r] * maxb + pos] : -1;
+    }
+    int2 ent[2 * R];
+    int cnt = 0;
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      bool first = alive[r];
+#pragma unroll
+      for (int r2 = 0; r2 < r; ++r2) first = first && !(alive[r2] && ids[r2] == ids[r]);
+      if (first) {
+        int mask = 0, two = 0;
+#pragma unroll
+        for (int r2 = 0; r2 < R; ++r2)
+          if (alive[r2] && ids[r2] == ids[r]) { mask |= 1 << r2; two |= Ls[r2] > 64 * pos + 32; }
+#pragma unroll
+        for (int h = 0; h < 2; ++h)
+          if (h == 0 || two) ent[cnt++] = make_int2(ids[r], (pos << 8) | (h << 4) | mask);
+      }
+    }
+    // exclusive prefix sum of the per-lane counts (tiles stay in position order)
+    int off = cnt;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const int v = __shfl_up(off, o, 64);
+      if (lane >= o) off += v;
+    }
+    const int total = __shfl(off, 63, 64);
+    off -= cnt;
+    for (int e = 0; e < cnt; ++e) s_tl[off + e] = ent[e];
+    if (lane == 0) s_nt = total;
+  }
+  // Q^T fragments: column hl = row slot hl / 4, head hl % 4
+  const int crow = rows[hl >> 2], cL = Ls[hl >> 2], cbit = 1 << (hl >> 2);
+  bf16x8 qf[4];
+  {
+    const uint16_t* qp = q + (size_t)max(crow, 0) * q_stride + (size_t)(kvh * G + (hl & 3)) * D + lg * 8;
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) {
+      const uint4 v = crow >= 0 ? *reinterpret_cast<const uint4*>(qp + ks * 32) : make_uint4(0, 0, 0, 0);
+      qf[ks] = __builtin_bit_cast(bf16x8, v);
+    }
+  }
+  __syncthreads();
+  const int nt = s_nt;
+
+  const float qs = scale * kLog2e;
+  const uint32_t ring_base = lds_u32(ring);
+  const int prow = lane >> 4, pslot = lane & 15;  // DMA piece geometry: 4 rows x 16 slots
+  auto stage = [&](int j) {
+    const int2 e = s_tl[min(j, nt - 1)];
+    const int tok0 = ((e.y >> 4) & 1) * TT;
+    const size_t row0 = ((size_t)e.x * Hkv + kvh) * 64 + tok0;
+    const uint16_t* kp = k_cache + row0 * D;
+    const uint16_t* vp = v_cache + row0 * D;
+    const uint32_t dst = ring_base + (uint32_t)((j % NSR) * 2 * TILE * 2);
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int c = i * 4 + wave;                // 1 KB piece = tile rows 4c .. 4c+3
+      const int t = 4 * c + prow;
+      glds16<true>(kp + t * D + ((pslot ^ (t & 15)) << 3), dst + c * 1024);
+      glds16<true>(vp + t * D + ((pslot ^ vswz(t)) << 3), dst + TILE * 2 + c * 1024);
+    }
+  };
+  if (nt > 0) {
+    stage(0);
+    stage(1);
+    if constexpr (NSR == 4) stage(2);
+  }
+  float m = -FLT_MAX, l = 0.f;
+  f32x4 acc[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
+  for (int jt = 0; jt < nt; ++jt) {
+    wait_vmcnt<4 * (NSR - 2)>();                 // the next NSR-2 tiles (4 DMAs each) may fly
+    ring_barrier();                              // tile jt visible; slot (jt-1) % NSR free
+    stage(jt + NSR - 1);
+    const int2 e = s_tl[jt];
+    const bool mine = (e.y & cbit) != 0;         // this column's row reads this block
+    const int base = (e.y >> 8) * 64 + ((e.y >> 4) & 1) * TT;   // absolute position of token 0
+    const uint16_t* kt = ring + (jt % NSR) * 2 * TILE;
+    const uint16_t* vt = kt + TILE;
+    f32x4 x[2];
+#pragma unroll
+    for (int c = 0; c < 2; ++c) {
+      x[c] = f32x4{0.f, 0.f, 0.f, 0.f};
+      const int t = 16 * c + hl;
+#pragma unroll
+      for (int ks = 0; ks < 4; ++ks) {
+        const bf16x8 a = *reinterpret_cast<const bf16x8*>(kt + t * D + (((4 * ks + lg) ^ (t & 15)) << 3));
+        x[c] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, qf[ks], x[c], 0, 0, 0);
+      }
+    }
+    // ---- per-column online softmax: lane = 4 tokens (16c + 4 lg + r) of column hl
+    float mx = -FLT_MAX;
+#pragma unroll
+    for (int c = 0; c < 2; ++c)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int tok = base + 16 * c + 4 * lg + r;
+        const float v = (mine && tok < cL) ? x[c][r] * qs : -FLT_MAX;
+        x[c][r] = v;
+        mx = fmaxf(mx, v);
+      }
+    mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
+    mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+    const float m_new = fmaxf(m, mx);
+    const float alpha = m_new == -FLT_MAX ? 1.f : exp2f(m - m_new);
+    float ps = 0.f;
+#pragma unroll
+    for (int c = 0; c < 2; ++c)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float p = x[c][r] == -FLT_MAX ? 0.f : exp2f(x[c][r] - m_new);
+        x[c][r] = p;
+        ps += p;
+      }
+    ps += __shfl_xor(ps, 16, 64);
+    ps += __shfl_xor(ps, 32, 64);
+    l = l * alpha + ps;
+    m = m_new;
+#pragma unroll
+    for (int dd = 0; dd < 2; ++dd) acc[dd] *= alpha;
+    // ---- O^T += V^T P^T (this wave's 32 dims)
+#pragma unroll
+    for (int c = 0; c < 2; ++c) {
+      i16x4 pb;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) pb[r] = (short)f2bf(x[c][r]);
+      const int row = 16 * c + 4 * lg + (hl >> 2), pp = hl & 3;
+#pragma unroll
+      for (int dd = 0; dd < 2; ++dd) {
+        const int ch = 2 * (2 * wave + dd) + (pp >> 1);
+        const uint16_t* va = vt + row * D + ((ch ^ vswz(row)) << 3) + 4 * (pp & 1);
+        const i16x4 a = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_i16x4*)va);
+        acc[dd] = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(a, pb, acc[dd], 0, 0, 0);
+      }
+    }
+  }
+  wait_vmcnt<0>();                               // drain the clamped tail DMAs
+
+  // ---- epilogue: lane holds O^T[dim 16 dt + 4 lg + r][column hl], dt = 2 wave + dd
+  if (crow < 0) return;
+  const int h = kvh * G + (hl & 3);
+  uint16_t* op = out + (size_t)crow * out_stride + (size_t)h * D;
+  if (cL <= P) {                                 // a padded decode slot: defined zeros
+#pragma unroll
+    for (int dd = 0; dd < 2; ++dd) *reinterpret_cast<uint2*>(op + 16 * (2 * wave + dd) + 4 * lg) = make_uint2(0, 0);
+    return;
+  }
+  float den = l;
+  float o[2][4];
+#pragma unroll
+  for (int dd = 0; dd < 2; ++dd)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) o[dd][r] = acc[dd][r];
+  const int np = ci.plen ? cascade_parts(P, ci.nchunk) : 0;
+  if (np > 0) {   // cascade: fold in the shared-prefix chunk partials of this column's row
+    const size_t Hq = (size_t)Hkv * G;
+    float pm[kCascadeMaxChunks], pl[kCascadeMaxChunks];
+#pragma unroll
+    for (int c = 0; c < kCascadeMaxChunks; ++c) {
+      const size_t r = ((size_t)min(c, np - 1) * B + crow) * Hq + h;
+      const float2 mlv = *reinterpret_cast<const float2*>(ci.ml + r * 2);
+      pm[c] = c < np ? mlv.x : -FLT_MAX;
+      pl[c] = mlv.y;
+    }
+    float M2 = m;
+#pragma unroll
+    for (int c = 0; c < kCascadeMaxChunks; ++c) M2 = fmaxf(M2, pm[c]);
+    const float f0 = m == -FLT_MAX ? 0.f : exp2f(m - M2);
+    den = l * f0;
+#pragma unroll
+    for (int dd = 0; dd < 2; ++dd)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) o[dd][r] *= f0;
+    for (int c0 = 0; c0 < np; c0 += 4) {
+      f32x4 pa[4][2];
+#pragma unroll
+      for (int cc = 0; cc < 4; ++cc) {
+        const size_t r = ((size_t)min(c0 + cc, np - 1) * B + crow) * Hq + h;
+#pragma unroll
+        for (int dd = 0; dd < 2; ++dd)
+          pa[cc][dd] = *reinterpret_cast<const f32x4*>(ci.acc + r * D + 16 * (2 * wave + dd) + 4 * lg);
+      }
+#pragma unroll
+      for (int cc = 0; cc < 4; ++cc) {
+        float pmc = -FLT_MAX, plc = 0.f;
+#pragma unroll
+        for (int c = 0; c < kCascadeMaxChunks; ++c)
+          if (c == c0 + cc) { pmc = pm[c]; plc = pl[c]; }
+        const float f = pmc == -FLT_MAX ? 0.f : exp2f(pmc - M2);
+        den += f * plc;
+#pragma unroll
+        for (int dd = 0; dd < 2; ++dd)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) o[dd][r] += f * pa[cc][dd][r];
+      }
+    }
+  }
+  const float inv = den > 0.f ? 1.f / den : 0.f;
+#pragma unroll
+  for (int dd = 0; dd < 2; ++dd) {
+    uint2 v;
+    v.x = pack2(o[dd][0] * inv, o[dd][1] * inv);
+    v.y = pack2(o[dd][2] * inv, o[dd][3] * inv);
+    *reinterpret_cast<uint2*>(op + 16 * (2 * wave + dd) + 4 * lg) = v;
+  }
+}
+
+// forward declaration (defined below with the other cascade launchers)
+int docqa_cascade_prefix(const void* qkv, int row_stride, int rows, int Hq, int Hkv, float scale,
+                         const void* k_cache, const void* v_cache, const int* prefix_table,
+                         const int* plen, int BS, int nchunk, float* acc, float* ml,
+                         const int* positions, const float* cos_sin, hipStream_t s);
+
+// Grouped cascade decode: MFMA prefix partials over the shared prompt prefix, then the
+// group kernel over each row's keys [*plen, L) with the rows packed by shared blocks
+// (groups: [ngroups, 4] row ids, -1 = none; every batch row in exactly one group).
+int docqa_paged_decode_cascade_grouped(const void* q, int q_stride, void* k_cache, void* v_cache,
+                                       const int* block_tables, int maxb, const int* context_lens,
+                                       void* out, int out_stride, int B, int Hq, int Hkv, int BS,
+                                       float scale, const int* prefix_table, const int* plen, int nchunk,
+                                       float* pacc, float* pml, const int* groups, int ngroups,
+                                       hipStream_t s) {
+  if (B == 0) return 0;
+  if (BS != 64 || maxb > kGroupMaxPos || Hq != 4 * Hkv || nchunk < 1 || nchunk > kCascadeMaxChunks ||
+      ngroups < 1)
+    return -1;
+  int rc = docqa_cascade_prefix(q, q_stride, B, Hq, Hkv, scale, k_cache, v_cache, prefix_table, plen, BS,
+                                nchunk, pacc, pml, nullptr, nullptr, s);
+  if (rc) return rc;
+  const CascadeIn ci{pacc, pml, plen, nchunk, nullptr};
+  paged_decode_group_kernel<3><<<dim3(Hkv, ngroups), 256, 0, s>>>(
+      (const uint16_t*)q, q_stride, (const uint16_t*)k_cache, (const uint16_t*)v_cache, block_tables, maxb,
+      context_lens, B, Hkv, scale, (uint16_t*)out, out_stride, groups, ci);
+  DOCQA_CHECK_LAUNCH();
+  return 0;
+}
+
 // log-sum-exp merge of a sequence's context partitions (and, cascade, of the shared-prefix
 // chunk partials) -> normalised bf16 output
 template <int D>

@@ -60,6 +60,13 @@ def _bucket(n: int, cap: int) -> int:
     return min(b, cap)
 
 
+def _identity_groups(bp: int, dev) -> torch.Tensor:
+    cap = (bp + 1) // 2
+    g = torch.full((cap * 4,), -1, dtype=torch.int32)
+    g[:bp] = torch.arange(bp, dtype=torch.int32)   # consecutive quads until set_groups runs
+    return g.to(dev)
+
+
 class _DecodeGraph:
     """Static buffers + captured graph for one batch bucket."""
 
@@ -82,6 +89,10 @@ class _DecodeGraph:
         # [0, bp) per bucket -- never a view of another bucket's buffer
         self.order = torch.arange(bp, dtype=torch.int32, device=dev)
         self.order_key = None
+        # grouped cascade decode: rows packed into groups of <= 4 by shared prefix-cache
+        # blocks (room for bp / 2 groups; unused groups are all -1 and exit at once)
+        self.groups = _identity_groups(bp, dev)
+        self.groups_key = None
         self.cascade = False
         self.greedy = True
         self.graph = None
@@ -99,6 +110,8 @@ class _DecodeGraph:
         g.shared_table, g.shared_len = master.shared_table, master.shared_len
         g.order = torch.arange(bp, dtype=torch.int32, device=master.tokens.device)
         g.order_key = None
+        g.groups = _identity_groups(bp, master.tokens.device)
+        g.groups_key = None
         g.cascade, g.greedy, g.graph = False, True, None
         return g
 
@@ -136,6 +149,8 @@ class LLMEngine:
         # LPT dispatch of the decode-attention workgroups (mixed context lengths cost ~15 %
         # in random order, benchmarks/bench_decode_attn.py MIX=random vs sorted)
         self.lpt = os.environ.get("DOCQA_DECODE_LPT", "1") == "1"
+        # grouped cascade decode: rows sharing prefix-cache blocks attended together
+        self.group_decode = os.environ.get("DOCQA_DECODE_GROUP", "1") == "1"
         self._graphs: dict[tuple, _DecodeGraph] = {}
         self._pool = None
         self.stats = GenStats()
@@ -210,6 +225,8 @@ class LLMEngine:
         if g.cascade:
             meta.shared_table, meta.shared_len = g.shared_table, g.shared_len
             meta.cascade_chunks = self._cascade_chunks(g.bp)
+            if self.group_decode and ops.grouped_decode_ok(self.kv.caches[0][0], g.block_tables, self.model.hq):
+                meta.decode_groups = g.groups
         if g.greedy:
             # greedy: the LM head's argmax is fused into its GEMM (no [B, vocab] logits)
             nxt = self.model.forward(g.tokens, meta, self.kv.caches, greedy_ids=True)
@@ -246,6 +263,21 @@ class LLMEngine:
         order = sorted(range(len(lens)), key=lambda i: -lens[i]) + list(range(len(lens), g.bp))
         g.order.copy_(torch.tensor(order, dtype=torch.int32).to(g.order.device, non_blocking=True))
         g.order_key = key
+
+    def set_groups(self, g: _DecodeGraph, tables: list[list[int]], lens: list[int], skip: int,
+                   key=None) -> None:
+        """Pack the active rows of bucket ``g`` into groups of <= 4 that share prefix-cache
+        blocks beyond the ``skip`` cascade-prefix blocks (ops.pack_decode_groups); padded
+        rows take no group.  Static while the batch composition is unchanged (``key``)."""
+        if not self.group_decode or (key is not None and g.groups_key == key):
+            return
+        cap = g.groups.numel() // 4
+        quads = ops.pack_decode_groups(tables, lens, skip, self.block_size, cap)
+        flat = torch.full((cap * 4,), -1, dtype=torch.int32)
+        for i, qd in enumerate(quads):
+            flat[4 * i:4 * i + len(qd)] = torch.tensor(qd, dtype=torch.int32)
+        g.groups.copy_(flat.to(g.groups.device, non_blocking=True))
+        g.groups_key = key
 
     def _cascade_chunks(self, bp: int) -> int:
         """Key chunks of the shared-prefix kernel: about 256 workgroups of (64 rows, KV
@@ -396,6 +428,8 @@ class LLMEngine:
             g.positions.copy_(pos.to(dev))
             g.context_lens.copy_((pos + vl).to(dev))
             self.set_order(g, lens)
+            if nshared:
+                self.set_groups(g, tables, [n + params.max_new_tokens for n in lens], nshared)
             if not greedy:
                 g.inv_temp.fill_(1.0 / params.temperature)
                 g.top_k.fill_(params.top_k)

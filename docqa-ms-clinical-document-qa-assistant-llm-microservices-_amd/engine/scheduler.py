@@ -308,6 +308,10 @@ class ContinuousEngine:
         if eng.lpt:
             # re-rank only when the running set changed (admission / retirement)
             eng.set_order(g, [len(r.prompt) + len(r.out) for r in self.running], key=self._version)
+        if self._nshared > 0:
+            eng.set_groups(g, [r.blocks for r in self.running],
+                           [len(r.prompt) + r.params.max_new_tokens for r in self.running], self._nshared,
+                           key=(self._version, self._nshared))
         t0 = time.perf_counter()
         with tracing.span("sched.decode", running=n, bucket=bp, cascade=self._nshared > 0):
             if eng.use_graphs:

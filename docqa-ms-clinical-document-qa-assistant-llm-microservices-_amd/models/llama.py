@@ -104,6 +104,9 @@ class AttnMeta:
     # (decode) workgroup dispatch order: int32 permutation of the rows, longest context
     # first (LPT), so short sequences fill the last launch round; None: row order
     seq_order: torch.Tensor | None = None
+    # (decode, cascade) rows packed in groups of <= 4 sharing prefix-cache blocks
+    # (ops.paged_decode_cascade_grouped); None: per-row suffix attention
+    decode_groups: torch.Tensor | None = None
 
 
 class LlamaModel:
@@ -268,15 +271,25 @@ class LlamaModel:
                 if sq:
                     qkv = ops.rope_cache_splitk(qkv_part(x, L["qkv"]), meta.positions,
                                                 self.cos_sin, meta.slot_mapping, kc, vc, hq, hkv, D)
-                    a = ops.paged_decode_cascade(qkv, kc, vc, meta.block_tables, meta.context_lens, hq,
-                                                 meta.max_context, self.scale, meta.shared_table,
-                                                 meta.shared_len, meta.cascade_chunks, meta.seq_order)
+                    if meta.decode_groups is not None:
+                        a = ops.paged_decode_cascade_grouped(qkv, kc, vc, meta.block_tables, meta.context_lens,
+                                                             hq, self.scale, meta.shared_table, meta.shared_len,
+                                                             meta.cascade_chunks, meta.decode_groups)
+                    else:
+                        a = ops.paged_decode_cascade(qkv, kc, vc, meta.block_tables, meta.context_lens, hq,
+                                                     meta.max_context, self.scale, meta.shared_table,
+                                                     meta.shared_len, meta.cascade_chunks, meta.seq_order)
                 elif not _CASCADE_ROPE:
                     qkv = lin(x, L["qkv"])
                     ops.rope_cache(qkv, meta.positions, self.cos_sin, meta.slot_mapping, kc, vc, hq, hkv, D)
-                    a = ops.paged_decode_cascade(qkv, kc, vc, meta.block_tables, meta.context_lens, hq,
-                                                 meta.max_context, self.scale, meta.shared_table,
-                                                 meta.shared_len, meta.cascade_chunks, meta.seq_order)
+                    if meta.decode_groups is not None:
+                        a = ops.paged_decode_cascade_grouped(qkv, kc, vc, meta.block_tables, meta.context_lens,
+                                                             hq, self.scale, meta.shared_table, meta.shared_len,
+                                                             meta.cascade_chunks, meta.decode_groups)
+                    else:
+                        a = ops.paged_decode_cascade(qkv, kc, vc, meta.block_tables, meta.context_lens, hq,
+                                                     meta.max_context, self.scale, meta.shared_table,
+                                                     meta.shared_len, meta.cascade_chunks, meta.seq_order)
                 else:
                     # library-GEMM QKV: RoPE + new-token cache write fused into the cascade kernels
                     a = ops.paged_decode_cascade_rope(lin(x, L["qkv"]), meta.positions, self.cos_sin,

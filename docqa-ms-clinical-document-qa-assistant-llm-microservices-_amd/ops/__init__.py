@@ -431,6 +431,75 @@ def paged_decode_cascade(q, k_cache, v_cache, block_tables, context_lens, Hq, ma
                                     scale, prefix_table, prefix_len, nchunk)
 
 
+def paged_decode_cascade_grouped(q, k_cache, v_cache, block_tables, context_lens, Hq, scale,
+                                 prefix_table, prefix_len, nchunk: int, groups):
+    """Cascade decode with the suffix attention of rows that share prefix-cache KV blocks
+    done together (csrc/kernels/attn_decode.hip paged_decode_group_kernel): ``groups``
+    int32 [ngroups * 4] packs every row into one group of <= 4 (-1 = empty slot), and a
+    block shared by k rows of a group is read once instead of k times.  Same result as
+    :func:`paged_decode_cascade` for any packing."""
+    if _gpu(q):
+        return _native().paged_decode_cascade_grouped(q, k_cache, v_cache, block_tables, context_lens, Hq,
+                                                      scale, prefix_table, prefix_len, nchunk, groups)
+    max_context = block_tables.shape[1] * k_cache.shape[2]
+    return ref.paged_decode_cascade(q, k_cache, v_cache, block_tables, context_lens, Hq, max_context,
+                                    scale, prefix_table, prefix_len, nchunk)
+
+
+def grouped_decode_ok(k_cache, block_tables, Hq: int) -> bool:
+    """Shapes the grouped cascade kernel supports (cascade shapes, <= 64 blocks per row)."""
+    return cascade_ok(k_cache, block_tables, Hq) and block_tables.shape[1] <= 64
+
+
+def pack_decode_groups(tables: list[list[int]], lens: list[int], skip: int, block_size: int,
+                       cap: int) -> list[list[int]]:
+    """Pack the rows of a decode batch into groups of <= 4 for the grouped decode kernel:
+    rows are sorted by their block ids beyond the ``skip`` cascade-prefix blocks (rows whose
+    prompts share prefix-cache blocks become neighbours), clusters of rows sharing their
+    first such block stay together where they fit, and the groups are ordered by distinct
+    blocks, largest first (LPT).  Falls back to plain consecutive quads when the packing
+    would exceed ``cap`` groups."""
+    n = len(tables)
+    if n == 0:
+        return []
+    idx = sorted(range(n), key=lambda i: tables[i][skip:])
+
+    def first(i):
+        return tables[i][skip] if len(tables[i]) > skip else -1 - i
+
+    clusters, cur = [], [idx[0]]
+    for a, b in zip(idx, idx[1:]):
+        if first(a) == first(b) and first(a) >= 0:
+            cur.append(b)
+        else:
+            clusters.append(cur)
+            cur = [b]
+    clusters.append(cur)
+    quads, cur = [], []
+    for cl in clusters:
+        while len(cl) > 4:
+            quads.append(cl[:4])
+            cl = cl[4:]
+        if len(cur) + len(cl) > 4:
+            quads.append(cur)
+            cur = []
+        cur = cur + cl
+    if cur:
+        quads.append(cur)
+    if len(quads) > cap:
+        quads = [idx[i:i + 4] for i in range(0, n, 4)]
+
+    def work(qd):
+        blocks = set()
+        for r in qd:
+            nb = (lens[r] + block_size - 1) // block_size
+            blocks.update(tables[r][skip:nb])
+        return len(blocks)
+
+    quads.sort(key=work, reverse=True)
+    return quads
+
+
 def flash_prefill(qkv, cu_seqlens, max_len, Hq, Hkv, D, scale, causal=True):
     if _gpu(qkv):
         return _native().flash_prefill(qkv, cu_seqlens, max_len, Hq, Hkv, D, scale, causal)

@@ -196,3 +196,25 @@ def test_token_cls_argmax_reference_cpu():
     b[9:] = 1e9  # would win if the padded rows were not excluded
     got = ops.token_cls_argmax(h, w, b, 9)
     assert torch.equal(got, (h @ w[:9].t() + b[:9]).argmax(-1))
+
+
+def test_pack_decode_groups_covers_rows_and_keeps_clusters():
+    """Every row in exactly one group of <= 4; rows sharing their first block past the
+    cascade prefix share a group when the cluster fits; LPT order (most blocks first)."""
+    from docqa_amd import ops
+
+    skip = 2
+    tables = [[0, 1, 10, 11, 50], [0, 1, 10, 11, 51], [0, 1, 20, 52, 53], [0, 1, 10, 12, 54],
+              [0, 1, 30, 55, 56], [0, 1, 20, 57, 58], [0, 1, 60, 61, 62]]
+    lens = [300] * len(tables)
+    quads = ops.pack_decode_groups(tables, lens, skip, 64, cap=4)
+    assert sorted(r for q in quads for r in q) == list(range(len(tables)))
+    assert all(1 <= len(q) <= 4 for q in quads)
+    where = {r: i for i, q in enumerate(quads) for r in q}
+    assert where[0] == where[1] == where[3]          # cluster of first block 10
+    assert where[2] == where[5]                      # cluster of first block 20
+    work = [len({b for r in q for b in tables[r][skip:5]}) for q in quads]
+    assert work == sorted(work, reverse=True)
+    # too many groups for the cap: consecutive quads of the sorted rows
+    quads = ops.pack_decode_groups(tables, lens, skip, 64, cap=1)
+    assert sorted(r for q in quads for r in q) == list(range(len(tables)))

@@ -1,0 +1,97 @@
+"""Grouped cascade decode (attn_decode.hip paged_decode_group_kernel): rows that share
+prefix-cache KV blocks are attended together in groups of <= 4; the result must equal the
+per-row cascade decode and the fp32 reference for any packing of the rows."""
+import math
+import random
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module", autouse=True)
+def native():
+    from docqa_amd import ops
+
+    assert ops.load_native(build_if_missing=True)
+    torch.manual_seed(0)
+    return ops
+
+
+def _trie_batch(B, P_blocks, maxb, seed):
+    """Block tables with a common prefix of P_blocks and clusters of rows sharing 1-4 more
+    blocks (a prefix-cache trie), then unique blocks; context lengths past the prefix."""
+    rnd = random.Random(seed)
+    nxt = P_blocks
+    prefix = list(range(P_blocks))
+    tables, lens = [], []
+    while len(tables) < B:
+        csize = rnd.choice([1, 1, 2, 3, 5])
+        depth = rnd.randint(0, 4)
+        shared = list(range(nxt, nxt + depth))
+        nxt += depth
+        for _ in range(min(csize, B - len(tables))):
+            own = list(range(nxt, nxt + maxb - P_blocks - depth))
+            nxt += len(own)
+            tables.append(prefix + shared + own)
+            lens.append(64 * (P_blocks + depth) + rnd.randint(1, 64 * 3))
+    return tables, lens, nxt
+
+
+@pytest.mark.parametrize("B,Hkv,seed", [(37, 8, 0), (64, 2, 1), (5, 8, 2), (256, 8, 3)])
+def test_grouped_cascade_matches_per_row(native, B, Hkv, seed):
+    from docqa_amd.ops import reference as R
+
+    Hq, D, BS, Pb, maxb = 4 * Hkv, 128, 64, 3, 12
+    tables, lens, nblk = _trie_batch(B, Pb, maxb, seed)
+    kc = torch.randn(nblk, Hkv, BS, D, device="cuda", dtype=torch.bfloat16)
+    vc = torch.randn_like(kc)
+    bt = torch.tensor(tables, dtype=torch.int32, device="cuda")
+    cl = torch.tensor(lens, dtype=torch.int32, device="cuda")
+    q = torch.randn(B, (Hq + 2 * Hkv) * D, device="cuda", dtype=torch.bfloat16)
+    pt = torch.zeros(maxb, dtype=torch.int32, device="cuda")
+    pt[:Pb] = bt[0, :Pb]
+    plen = torch.tensor([Pb * BS], dtype=torch.int32, device="cuda")
+    scale = 1 / math.sqrt(D)
+    ref = native.paged_decode_cascade(q, kc, vc, bt, cl, Hq, maxb * BS, scale, pt, plen, 4)
+    with native.use_reference():
+        ref32 = native.paged_decode_cascade(q, kc, vc, bt, cl, Hq, maxb * BS, scale, pt, plen, 4)
+    cap = (B + 1) // 2
+    for packing in ("trie", "consecutive", "reversed"):
+        if packing == "trie":
+            quads = native.pack_decode_groups(tables, lens, Pb, BS, cap)
+        elif packing == "consecutive":
+            quads = [list(range(i, min(B, i + 4))) for i in range(0, B, 4)]
+        else:
+            rows = list(range(B))[::-1]
+            quads = [rows[i:i + 3] for i in range(0, B, 3)]
+        assert sorted(r for qd in quads for r in qd) == list(range(B))
+        flat = torch.full((max(cap, len(quads)) * 4,), -1, dtype=torch.int32)
+        for i, qd in enumerate(quads):
+            flat[4 * i:4 * i + len(qd)] = torch.tensor(qd, dtype=torch.int32)
+        out = native.paged_decode_cascade_grouped(q, kc, vc, bt, cl, Hq, scale, pt, plen, 4, flat.cuda())
+        err = (out.float() - ref.float()).abs().max().item()
+        assert err < 2e-2, (packing, err)
+        err32 = (out.float() - ref32.float()).abs().max().item()
+        assert err32 < 3e-2, (packing, err32)
+
+
+def test_grouped_cascade_padded_rows_zero(native):
+    """Rows with no keys past the prefix (padded decode slots) get zeros."""
+    Hkv, D, BS, Pb, maxb = 2, 128, 64, 2, 6
+    Hq, B = 4 * Hkv, 6
+    tables, lens, nblk = _trie_batch(B, Pb, maxb, 7)
+    lens[2] = 0
+    lens[5] = Pb * BS
+    kc = torch.randn(nblk, Hkv, BS, D, device="cuda", dtype=torch.bfloat16)
+    vc = torch.randn_like(kc)
+    bt = torch.tensor(tables, dtype=torch.int32, device="cuda")
+    cl = torch.tensor(lens, dtype=torch.int32, device="cuda")
+    q = torch.randn(B, (Hq + 2 * Hkv) * D, device="cuda", dtype=torch.bfloat16)
+    pt = bt[0].clone()
+    plen = torch.tensor([Pb * BS], dtype=torch.int32, device="cuda")
+    groups = torch.tensor([0, 1, 2, 3, 4, 5, -1, -1], dtype=torch.int32, device="cuda")
+    out = native.paged_decode_cascade_grouped(q, kc, vc, bt, cl, Hq, 1 / math.sqrt(D), pt, plen, 2, groups)
+    assert torch.isfinite(out.float()).all()
+    assert (out[2] == 0).all() and (out[5] == 0).all()
