@@ -1091,9 +1091,18 @@ int docqa_paged_decode_cascade_grouped(const void* q, int q_stride, void* k_cach
                                 nchunk, pacc, pml, nullptr, nullptr, s);
   if (rc) return rc;
   const CascadeIn ci{pacc, pml, plen, nchunk, nullptr};
-  paged_decode_group_kernel<3><<<dim3(Hkv, ngroups), 256, 0, s>>>(
-      (const uint16_t*)q, q_stride, (const uint16_t*)k_cache, (const uint16_t*)v_cache, block_tables, maxb,
-      context_lens, B, Hkv, scale, (uint16_t*)out, out_stride, groups, ci);
+  static const int nsr = [] {   // ring slots (A/B knob): 3 (3 workgroups / CU) or 4 (2)
+    const char* e = getenv("DOCQA_GROUP_NSR");
+    return e && atoi(e) == 4 ? 4 : 3;
+  }();
+  if (nsr == 4)
+    paged_decode_group_kernel<4><<<dim3(Hkv, ngroups), 256, 0, s>>>(
+        (const uint16_t*)q, q_stride, (const uint16_t*)k_cache, (const uint16_t*)v_cache, block_tables, maxb,
+        context_lens, B, Hkv, scale, (uint16_t*)out, out_stride, groups, ci);
+  else
+    paged_decode_group_kernel<3><<<dim3(Hkv, ngroups), 256, 0, s>>>(
+        (const uint16_t*)q, q_stride, (const uint16_t*)k_cache, (const uint16_t*)v_cache, block_tables, maxb,
+        context_lens, B, Hkv, scale, (uint16_t*)out, out_stride, groups, ci);
   DOCQA_CHECK_LAUNCH();
   return 0;
 }
