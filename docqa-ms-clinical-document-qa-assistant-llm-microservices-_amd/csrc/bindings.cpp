@@ -532,6 +532,10 @@ at::Tensor dgemm_glu(const at::Tensor& x, const at::Tensor& w) {
   sizes.back() = N / 2;
   c10::DeviceGuard g(x.device());
   auto out = at::empty(sizes, x.options());
+  if (M > 128) {   // past the skinny kernel's rows: the mid-M kernel's fused SwiGLU
+    CHECK_RC(docqa_mgemm_glu(x.data_ptr(), w.data_ptr(), out.data_ptr(), M, N, K, 0, stream()), "dgemm_glu");
+    return out;
+  }
   CHECK_RC(docqa_dgemm_glu(x.data_ptr(), w.data_ptr(), out.data_ptr(), M, N, K, stream()), "dgemm_glu");
   return out;
 }
@@ -545,6 +549,11 @@ at::Tensor dgemm_partial(const at::Tensor& x, const at::Tensor& w, int64_t split
   TORCH_CHECK(M <= 256 && splits >= 1, "dgemm_partial: at most 256 rows, splits >= 1");
   c10::DeviceGuard g(x.device());
   auto part = at::empty({splits, M, N}, x.options().dtype(at::kFloat));
+  if (M > 192) {   // past the skinny kernel's rows: the mid-M kernel's split-K slabs
+    CHECK_RC(docqa_mgemm(x.data_ptr(), w.data_ptr(), nullptr, part.data_ptr<float>(), M, N, K, (int)splits, 0,
+                         stream()), "dgemm_partial");
+    return part;
+  }
   CHECK_RC(docqa_dgemm_partial(x.data_ptr(), w.data_ptr(), part.data_ptr<float>(), M, N, K, (int)splits,
                                (int)tile_rows, stream()), "dgemm_partial");
   return part;
@@ -561,6 +570,10 @@ at::Tensor dgemm(const at::Tensor& x, const at::Tensor& w, int64_t splits) {
   sizes.back() = N;
   c10::DeviceGuard g(x.device());
   auto out = at::empty(sizes, x.options());
+  if (M > 192) {   // past the skinny kernel's rows: the mid-M kernel, bf16 out
+    CHECK_RC(docqa_mgemm(x.data_ptr(), w.data_ptr(), out.data_ptr(), nullptr, M, N, K, 1, 0, stream()), "dgemm");
+    return out;
+  }
   at::Tensor part;
   if (S > 1) part = at::empty({S, M, N}, x.options().dtype(at::kFloat));
   CHECK_RC(docqa_dgemm(x.data_ptr(), w.data_ptr(), out.data_ptr(), S > 1 ? part.data_ptr<float>() : nullptr,

@@ -421,16 +421,17 @@ int docqa_mgemm_tile_n(int cfg) {
   return cfg >= 1 && cfg <= kNumCfg ? kCfg[cfg].bn : 0;
 }
 
-// S == 1: Y bf16 [M, N];  S > 1: P fp32 split-K slabs [S, M, N] (combined by the consumer)
+// P given: fp32 split-K slabs [S, M, N] (S >= 1, combined by the consumer); else S == 1 and
+// Y bf16 [M, N]
 int docqa_mgemm(const void* X, const void* W, void* Y, float* P, int M, int N, int K, int S, int cfg,
                 hipStream_t s) {
   if (cfg == 0) cfg = kDefaultCfg;
   if (M == 0) return 0;
-  if (!shape_ok(M, N, K, S, cfg) || (S == 1 ? Y == nullptr : P == nullptr)) return -1;
-  if (!docqa_aligned16(X) || !docqa_aligned16(W) || !docqa_aligned16(S == 1 ? Y : (void*)P)) return -1;
+  if (!shape_ok(M, N, K, S, cfg) || (P == nullptr && (S != 1 || Y == nullptr))) return -1;
+  if (!docqa_aligned16(X) || !docqa_aligned16(W) || !docqa_aligned16(P ? (void*)P : Y)) return -1;
   const uint16_t *x = (const uint16_t*)X, *w = (const uint16_t*)W;
-  if (S == 1) return launch_cfg<EPI_BF16>(cfg, x, w, (uint16_t*)Y, nullptr, nullptr, nullptr, M, N, K, 1, N, s);
-  return launch_cfg<EPI_PARTIAL>(cfg, x, w, nullptr, P, nullptr, nullptr, M, N, K, S, N, s);
+  if (P) return launch_cfg<EPI_PARTIAL>(cfg, x, w, nullptr, P, nullptr, nullptr, M, N, K, S, N, s);
+  return launch_cfg<EPI_BF16>(cfg, x, w, (uint16_t*)Y, nullptr, nullptr, nullptr, M, N, K, 1, N, s);
 }
 
 // Y[M, N/2] = silu(gate) * up for the 8-interleaved gate|up weight W [N, K] (N = 2 I)
