@@ -395,6 +395,45 @@ at::Tensor paged_decode_cascade_grouped(const at::Tensor& q, at::Tensor k_cache,
   return out;
 }
 
+// grouped cascade decode with long groups split over several workgroups: plan [2, cap, 8]
+// int32 = work items (4 row ids, first / end block position, partial slot or -1, 0) and
+// merges (4 row ids, first slot, slots, 0, 0) -- ops.split_decode_groups
+at::Tensor paged_decode_cascade_split(const at::Tensor& q, at::Tensor k_cache, at::Tensor v_cache,
+                                      const at::Tensor& block_tables, const at::Tensor& context_lens,
+                                      int64_t Hq, double scale, const at::Tensor& prefix_table,
+                                      const at::Tensor& prefix_len, int64_t nchunk, const at::Tensor& plan) {
+  CHECK_GPU(q); CHECK_BF16(q); CHECK_BF16(k_cache); CHECK_BF16(v_cache);
+  CHECK_I32(block_tables); CHECK_I32(context_lens); CHECK_CONTIG(block_tables);
+  CHECK_I32(prefix_table); CHECK_I32(prefix_len); CHECK_CONTIG(prefix_table);
+  CHECK_I32(plan); CHECK_CONTIG(plan);
+  TORCH_CHECK(q.stride(-1) == 1, "q rows must be contiguous");
+  const int B = q.size(0);
+  const int Hkv = k_cache.size(1), BS = k_cache.size(2), D = k_cache.size(3);
+  TORCH_CHECK(D == 128 && BS == 64 && Hq == 4 * Hkv, "split decode: head_dim 128, 64-token blocks, GQA 4");
+  TORCH_CHECK(block_tables.size(1) <= 64, "split decode: <= 64 blocks per sequence");
+  TORCH_CHECK(context_lens.numel() == B && block_tables.size(0) >= B, "split decode: B rows");
+  TORCH_CHECK(plan.dim() == 3 && plan.size(0) == 2 && plan.size(2) == 8 && plan.size(1) >= 1, "plan: [2, cap, 8]");
+  TORCH_CHECK(prefix_table.numel() >= 1 && prefix_len.numel() == 1, "cascade decode: prefix table / length");
+  const int cap = plan.size(1);
+  c10::DeviceGuard g(q.device());
+  auto out = at::empty({B, Hq * D}, q.options());
+  auto f32 = q.options().dtype(at::kFloat);
+  auto pacc = at::empty({nchunk, B, Hq, D}, f32);
+  auto pml = at::empty({nchunk, B, Hq, 2}, f32);
+  auto ws_acc = at::empty({cap, Hkv, 16, D}, f32);
+  auto ws_ml = at::empty({cap, Hkv, 16, 2}, f32);
+  const int* pp = plan.data_ptr<int>();
+  CHECK_RC(docqa_paged_decode_cascade_split(q.data_ptr(), q.stride(0), k_cache.data_ptr(), v_cache.data_ptr(),
+                                            block_tables.data_ptr<int>(), block_tables.size(1),
+                                            context_lens.data_ptr<int>(), out.data_ptr(), Hq * D, B, Hq, Hkv,
+                                            BS, (float)scale, prefix_table.data_ptr<int>(),
+                                            prefix_len.data_ptr<int>(), (int)nchunk, pacc.data_ptr<float>(),
+                                            pml.data_ptr<float>(), pp, pp + 8 * cap, cap, ws_acc.data_ptr<float>(),
+                                            ws_ml.data_ptr<float>(), stream()),
+           "paged_decode_cascade_split");
+  return out;
+}
+
 // cascade decode over the UNROTATED packed QKV of a library GEMM: RoPE, the new token's
 // cache write and the attention in the cascade kernels (fallback: rope_cache in place)
 at::Tensor paged_decode_cascade_rope(at::Tensor qkv, const at::Tensor& positions, const at::Tensor& cos_sin,
@@ -803,6 +842,9 @@ TORCH_LIBRARY(docqa, m) {
   m.def("paged_decode_cascade_grouped(Tensor q, Tensor k_cache, Tensor v_cache, Tensor block_tables, "
         "Tensor context_lens, int Hq, float scale, Tensor prefix_table, Tensor prefix_len, int nchunk, "
         "Tensor groups) -> Tensor");
+  m.def("paged_decode_cascade_split(Tensor q, Tensor k_cache, Tensor v_cache, Tensor block_tables, "
+        "Tensor context_lens, int Hq, float scale, Tensor prefix_table, Tensor prefix_len, int nchunk, "
+        "Tensor plan) -> Tensor");
   m.def("paged_decode_cascade_rope(Tensor(a!) qkv, Tensor positions, Tensor cos_sin, Tensor slot_mapping, "
         "Tensor(b!) k_cache, Tensor(c!) v_cache, Tensor block_tables, Tensor context_lens, int Hq, "
         "int max_context, float scale, Tensor prefix_table, Tensor prefix_len, int nchunk, "
@@ -854,6 +896,7 @@ TORCH_LIBRARY_IMPL(docqa, CUDA, m) {
   m.impl("paged_decode_cascade", &paged_decode_cascade);
   m.impl("paged_decode_cascade_rope", &paged_decode_cascade_rope);
   m.impl("paged_decode_cascade_grouped", &paged_decode_cascade_grouped);
+  m.impl("paged_decode_cascade_split", &paged_decode_cascade_split);
   m.impl("ar_oneshot", &ar_oneshot);
   m.impl("add_rmsnorm_splitk", &add_rmsnorm_splitk);
   m.impl("rope_cache_splitk", &rope_cache_splitk);

@@ -828,12 +828,18 @@ __global__ __launch_bounds__(256) void paged_decode_mfma_kernel(
 // (P: the cascade prefix, attended by the prefix kernel and merged here).
 constexpr int kGroupMaxPos = 64;     // block positions beyond the cascade prefix (4096 tokens)
 
-template <int NSR = 3>
+// SPLIT: `groups` is a work-item list [cap, 8] = (4 row ids, first block position, end
+// block position, partial slot or -1, 0): a long group's block positions are split over
+// several items (workgroups), each writing an un-normalised partial (m, l, O) for its 16
+// columns to ws_ml / ws_acc[slot] that group_split_merge_kernel combines; an item of an
+// unsplit group (slot -1) finishes as the plain kernel does.
+template <int NSR = 3, bool SPLIT = false>
 __global__ __launch_bounds__(256) void paged_decode_group_kernel(
     const uint16_t* __restrict__ q, int q_stride, const uint16_t* __restrict__ k_cache,
     const uint16_t* __restrict__ v_cache, const int* __restrict__ block_tables, int maxb,
     const int* __restrict__ context_lens, int B, int Hkv, float scale,
-    uint16_t* __restrict__ out, int out_stride, const int* __restrict__ groups, CascadeIn ci) {
+    uint16_t* __restrict__ out, int out_stride, const int* __restrict__ groups, CascadeIn ci,
+    float* __restrict__ ws_acc = nullptr, float* __restrict__ ws_ml = nullptr) {
   constexpr int G = 4, R = 4, D = 128, TT = 32, MAXT = kGroupMaxPos * 8;
   constexpr int TILE = TT * D;                   // elements of one K (or V) tile: 8 KB
   __shared__ __attribute__((aligned(16))) uint16_t ring[NSR * 2 * TILE];
@@ -845,22 +851,30 @@ __global__ __launch_bounds__(256) void paged_decode_group_kernel(
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int hl = lane & 15, lg = lane >> 4;      // MFMA column (row slot x head) / lane group
   const int P = ci.plen ? *ci.plen : 0;          // multiple of 64
+  const int* gp = groups + (SPLIT ? 8 : R) * grp;
   int rows[R], Ls[R];
 #pragma unroll
   for (int r = 0; r < R; ++r) {
-    const int row = groups[R * grp + r];
+    const int row = gp[r];
     rows[r] = row >= 0 && row < B ? row : -1;
     Ls[r] = rows[r] >= 0 ? context_lens[rows[r]] : 0;
   }
+  int lo = 0, hi = maxb, part = -1;
+  if constexpr (SPLIT) {
+    if (rows[0] < 0 && rows[1] < 0 && rows[2] < 0 && rows[3] < 0) return;   // unused item
+    lo = gp[4];
+    hi = min(gp[5], maxb);
+    part = gp[6];
+  }
 
-  // ---- tile list: lane j of wave 0 owns block position P/64 + j
+  // ---- tile list: lane j of wave 0 owns block position max(P/64, lo) + j
   if (wave == 0) {
-    const int pos = (P >> 6) + lane;
+    const int pos = max(P >> 6, lo) + lane;
     int ids[R];
     bool alive[R];
 #pragma unroll
     for (int r = 0; r < R; ++r) {
-      alive[r] = pos < maxb && 64 * pos < Ls[r];
+      alive[r] = pos < hi && 64 * pos < Ls[r];
       ids[r] = alive[r] ? block_tables[(size_t)rows[r] * maxb + pos] : -1;
     }
     int2 ent[2 * R];
@@ -1001,6 +1015,16 @@ __global__ __launch_bounds__(256) void paged_decode_group_kernel(
 
   // ---- epilogue: lane holds O^T[dim 16 dt + 4 lg + r][column hl], dt = 2 wave + dd
   if (crow < 0) return;
+  if constexpr (SPLIT) {
+    if (part >= 0) {   // one partial of a split group: (m, l) + un-normalised O^T
+      const size_t cidx = ((size_t)part * Hkv + kvh) * 16 + hl;
+#pragma unroll
+      for (int dd = 0; dd < 2; ++dd)
+        *reinterpret_cast<f32x4*>(ws_acc + cidx * D + 16 * (2 * wave + dd) + 4 * lg) = acc[dd];
+      if (wave == 0 && lg == 0) *reinterpret_cast<float2*>(ws_ml + cidx * 2) = make_float2(m, l);
+      return;
+    }
+  }
   const int h = kvh * G + (hl & 3);
   uint16_t* op = out + (size_t)crow * out_stride + (size_t)h * D;
   if (cL <= P) {                                 // a padded decode slot: defined zeros
@@ -1068,6 +1092,58 @@ __global__ __launch_bounds__(256) void paged_decode_group_kernel(
   }
 }
 
+// Combines the partials of every split group (merges [cap, 8] = (4 row ids, first slot,
+// slots, 0, 0); slots 0: nothing to merge) with the cascade prefix partials of each column's
+// row, then normalises: thread = (column, 8 dims).
+__global__ __launch_bounds__(256) void group_split_merge_kernel(const int* __restrict__ merges,
+                                                                const float* __restrict__ ws_acc,
+                                                                const float* __restrict__ ws_ml,
+                                                                const int* __restrict__ context_lens, int B,
+                                                                int Hkv, uint16_t* __restrict__ out,
+                                                                int out_stride, CascadeIn ci) {
+  constexpr int D = 128;
+  const int kvh = blockIdx.x;
+  const int* mg = merges + 8 * blockIdx.y;
+  const int first = mg[4], np = mg[5];
+  if (np <= 0) return;
+  const int t = threadIdx.x, col = t >> 4, d0 = (t & 15) * 8;
+  const int row = mg[col >> 2];
+  if (row < 0 || row >= B) return;
+  const int Hq = Hkv * 4, h = kvh * 4 + (col & 3);
+  uint16_t* op = out + (size_t)row * out_stride + (size_t)h * D + d0;
+  const int P = ci.plen ? *ci.plen : 0;
+  if (context_lens[row] <= P) {                  // a padded decode slot: defined zeros
+    *reinterpret_cast<uint4*>(op) = make_uint4(0, 0, 0, 0);
+    return;
+  }
+  const int nc = ci.plen ? cascade_parts(P, ci.nchunk) : 0;
+  float M = -FLT_MAX;
+  for (int p = 0; p < np; ++p) M = fmaxf(M, ws_ml[(((size_t)(first + p) * Hkv + kvh) * 16 + col) * 2]);
+  for (int c = 0; c < nc; ++c) M = fmaxf(M, ci.ml[(((size_t)c * B + row) * Hq + h) * 2]);
+  float num[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f}, den = 0.f;
+  auto fold = [&](float pm, float pl, const float* pa) {
+    const float w = pm == -FLT_MAX ? 0.f : exp2f(pm - M);
+    den += w * pl;
+    const float4 a0 = *reinterpret_cast<const float4*>(pa);
+    const float4 a1 = *reinterpret_cast<const float4*>(pa + 4);
+    num[0] += w * a0.x; num[1] += w * a0.y; num[2] += w * a0.z; num[3] += w * a0.w;
+    num[4] += w * a1.x; num[5] += w * a1.y; num[6] += w * a1.z; num[7] += w * a1.w;
+  };
+  for (int p = 0; p < np; ++p) {
+    const size_t ci2 = ((size_t)(first + p) * Hkv + kvh) * 16 + col;
+    const float2 ml = *reinterpret_cast<const float2*>(ws_ml + ci2 * 2);
+    fold(ml.x, ml.y, ws_acc + ci2 * D + d0);
+  }
+  for (int c = 0; c < nc; ++c) {
+    const size_t r = ((size_t)c * B + row) * Hq + h;
+    fold(ci.ml[r * 2], ci.ml[r * 2 + 1], ci.acc + r * D + d0);
+  }
+  const float inv = den > 0.f ? 1.f / den : 0.f;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) num[e] *= inv;
+  *reinterpret_cast<uint4*>(op) = pack8(num);
+}
+
 // forward declaration (defined below with the other cascade launchers)
 int docqa_cascade_prefix(const void* qkv, int row_stride, int rows, int Hq, int Hkv, float scale,
                          const void* k_cache, const void* v_cache, const int* prefix_table,
@@ -1103,6 +1179,32 @@ int docqa_paged_decode_cascade_grouped(const void* q, int q_stride, void* k_cach
     paged_decode_group_kernel<3><<<dim3(Hkv, ngroups), 256, 0, s>>>(
         (const uint16_t*)q, q_stride, (const uint16_t*)k_cache, (const uint16_t*)v_cache, block_tables, maxb,
         context_lens, B, Hkv, scale, (uint16_t*)out, out_stride, groups, ci);
+  DOCQA_CHECK_LAUNCH();
+  return 0;
+}
+
+// Grouped cascade decode with long groups split over several workgroups: items [cap, 8]
+// (see paged_decode_group_kernel SPLIT), merges [cap, 8] (group_split_merge_kernel),
+// ws_acc [slots, Hkv, 16, 128] / ws_ml [slots, Hkv, 16, 2] fp32 partials.
+int docqa_paged_decode_cascade_split(const void* q, int q_stride, void* k_cache, void* v_cache,
+                                     const int* block_tables, int maxb, const int* context_lens,
+                                     void* out, int out_stride, int B, int Hq, int Hkv, int BS,
+                                     float scale, const int* prefix_table, const int* plen, int nchunk,
+                                     float* pacc, float* pml, const int* items, const int* merges, int cap,
+                                     float* ws_acc, float* ws_ml, hipStream_t s) {
+  if (B == 0) return 0;
+  if (BS != 64 || maxb > kGroupMaxPos || Hq != 4 * Hkv || nchunk < 1 || nchunk > kCascadeMaxChunks || cap < 1)
+    return -1;
+  int rc = docqa_cascade_prefix(q, q_stride, B, Hq, Hkv, scale, k_cache, v_cache, prefix_table, plen, BS,
+                                nchunk, pacc, pml, nullptr, nullptr, s);
+  if (rc) return rc;
+  const CascadeIn ci{pacc, pml, plen, nchunk, nullptr};
+  paged_decode_group_kernel<3, true><<<dim3(Hkv, cap), 256, 0, s>>>(
+      (const uint16_t*)q, q_stride, (const uint16_t*)k_cache, (const uint16_t*)v_cache, block_tables, maxb,
+      context_lens, B, Hkv, scale, (uint16_t*)out, out_stride, items, ci, ws_acc, ws_ml);
+  DOCQA_CHECK_LAUNCH();
+  group_split_merge_kernel<<<dim3(Hkv, cap), 256, 0, s>>>(merges, ws_acc, ws_ml, context_lens, B, Hkv,
+                                                          (uint16_t*)out, out_stride, ci);
   DOCQA_CHECK_LAUNCH();
   return 0;
 }

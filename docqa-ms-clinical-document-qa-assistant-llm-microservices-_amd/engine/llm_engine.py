@@ -60,8 +60,22 @@ def _bucket(n: int, cap: int) -> int:
     return min(b, cap)
 
 
+def _split_groups_on() -> bool:
+    return os.environ.get("DOCQA_GROUP_SPLIT", "1") == "1"
+
+
 def _identity_groups(bp: int, dev) -> torch.Tensor:
     cap = (bp + 1) // 2
+    if _split_groups_on():
+        # split plan [2, bp, 8]: consecutive unsplit quads until set_groups runs
+        g = torch.full((2, max(bp, 1), 8), -1, dtype=torch.int32)
+        g[:, :, 4:] = 0
+        for i in range(cap):
+            q = list(range(4 * i, min(4 * i + 4, bp)))
+            g[0, i, :len(q)] = torch.tensor(q, dtype=torch.int32)
+            g[0, i, 5] = 1 << 20
+            g[0, i, 6] = -1
+        return g.to(dev)
     g = torch.full((cap * 4,), -1, dtype=torch.int32)
     g[:bp] = torch.arange(bp, dtype=torch.int32)   # consecutive quads until set_groups runs
     return g.to(dev)
@@ -270,6 +284,14 @@ class LLMEngine:
         blocks beyond the ``skip`` cascade-prefix blocks (ops.pack_decode_groups); padded
         rows take no group.  Static while the batch composition is unchanged (``key``)."""
         if not self.group_decode or (key is not None and g.groups_key == key):
+            return
+        if g.groups.dim() == 3:   # split plan: long groups over several workgroups
+            cap = g.groups.shape[1]
+            quads = ops.pack_decode_groups(tables, lens, skip, self.block_size, (g.bp + 1) // 2)
+            plan = ops.split_decode_groups(quads, tables, lens, skip, self.block_size, cap,
+                                           int(os.environ.get("DOCQA_GROUP_TILES", "12")))
+            g.groups.copy_(plan.to(g.groups.device, non_blocking=True))
+            g.groups_key = key
             return
         cap = g.groups.numel() // 4
         quads = ops.pack_decode_groups(tables, lens, skip, self.block_size, cap)

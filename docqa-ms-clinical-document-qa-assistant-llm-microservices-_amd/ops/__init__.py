@@ -437,8 +437,13 @@ def paged_decode_cascade_grouped(q, k_cache, v_cache, block_tables, context_lens
     done together (csrc/kernels/attn_decode.hip paged_decode_group_kernel): ``groups``
     int32 [ngroups * 4] packs every row into one group of <= 4 (-1 = empty slot), and a
     block shared by k rows of a group is read once instead of k times.  Same result as
-    :func:`paged_decode_cascade` for any packing."""
+    :func:`paged_decode_cascade` for any packing.  ``groups`` may also be a split plan
+    int32 [2, cap, 8] from :func:`split_decode_groups` (long groups over several
+    workgroups, partials merged by log-sum-exp)."""
     if _gpu(q):
+        if groups.dim() == 3:
+            return _native().paged_decode_cascade_split(q, k_cache, v_cache, block_tables, context_lens, Hq,
+                                                        scale, prefix_table, prefix_len, nchunk, groups)
         return _native().paged_decode_cascade_grouped(q, k_cache, v_cache, block_tables, context_lens, Hq,
                                                       scale, prefix_table, prefix_len, nchunk, groups)
     max_context = block_tables.shape[1] * k_cache.shape[2]
@@ -498,6 +503,70 @@ def pack_decode_groups(tables: list[list[int]], lens: list[int], skip: int, bloc
 
     quads.sort(key=work, reverse=True)
     return quads
+
+
+def group_tiles_by_position(tables: list[list[int]], lens: list[int], rows: list[int], skip: int,
+                            block_size: int) -> list[tuple[int, int]]:
+    """(block position, 32-token K/V tiles) the grouped decode kernel streams for ``rows``
+    at each position beyond the ``skip`` cascade-prefix blocks: one or two tiles (by the
+    longest length among the rows reading it) per DISTINCT block id at that position."""
+    half = block_size // 2
+    nb = max((lens[r] + block_size - 1) // block_size for r in rows)
+    out = []
+    for pos in range(skip, nb):
+        live: dict[int, int] = {}
+        for r in rows:
+            if pos * block_size < lens[r] and pos < len(tables[r]):
+                b = tables[r][pos]
+                live[b] = max(live.get(b, 0), lens[r])
+        if live:
+            out.append((pos, sum(1 + (L > pos * block_size + half) for L in live.values())))
+    return out
+
+
+def split_decode_groups(quads: list[list[int]], tables: list[list[int]], lens: list[int], skip: int,
+                        block_size: int, cap: int, tiles_per_item: int = 12) -> torch.Tensor:
+    """Split plan for the grouped cascade decode (``paged_decode_cascade_grouped`` with a
+    [2, cap, 8] int32 ``groups``): every group of :func:`pack_decode_groups` is cut at block
+    positions into work items of about ``tiles_per_item`` K/V tiles (``lens``: the lengths
+    at the END of decode, so an item's range stays valid for every step), one workgroup per
+    item and KV head.  A group that needs one item finishes in its workgroup; the items of
+    a longer group write partials that a merge kernel combines.  Items are ordered largest
+    first (LPT).  plan[0]: items (4 rows, first position, end position, slot or -1, 0);
+    plan[1]: merges (4 rows, first slot, slots, 0, 0)."""
+    items, merges, nslot = [], [], 0
+    budget = max(1, tiles_per_item)
+    while True:
+        items, merges, nslot = [], [], 0
+        for qd in quads:
+            rows4 = (list(qd) + [-1] * 4)[:4]
+            per = group_tiles_by_position(tables, lens, list(qd), skip, block_size)
+            cuts, acc, start = [], 0, skip
+            for pos, t in per:
+                if acc and acc + t > budget:
+                    cuts.append((start, pos, acc))
+                    start, acc = pos, 0
+                acc += t
+            end = max((lens[r] + block_size - 1) // block_size for r in qd)
+            cuts.append((start, max(end, start + 1), acc))
+            if len(cuts) == 1:
+                items.append((cuts[0][2], rows4 + [skip, 1 << 20, -1, 0]))
+            else:
+                merges.append(rows4 + [nslot, len(cuts), 0, 0])
+                for lo, hi, t in cuts:
+                    items.append((t, rows4 + [lo, hi, nslot, 0]))
+                    nslot += 1
+        if len(items) <= cap and len(merges) <= cap:
+            break
+        budget *= 2
+    items.sort(key=lambda it: -it[0])
+    plan = torch.full((2, cap, 8), -1, dtype=torch.int32)
+    plan[:, :, 4:] = 0
+    if items:
+        plan[0, :len(items)] = torch.tensor([it[1] for it in items], dtype=torch.int32)
+    if merges:
+        plan[1, :len(merges)] = torch.tensor(merges, dtype=torch.int32)
+    return plan
 
 
 def flash_prefill(qkv, cu_seqlens, max_len, Hq, Hkv, D, scale, causal=True):

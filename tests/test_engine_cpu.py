@@ -1,6 +1,7 @@
 """Generation engine on CPU (reference ops, fp32 tiny Llama): paged KV cache + varlen
 prefill + decode loop must reproduce a naive full-recompute greedy decode, and be
 invariant to batching."""
+import pytest
 import torch
 
 from docqa_amd.engine.kv_cache import KVCache, PyBlockAllocator
@@ -218,3 +219,47 @@ def test_pack_decode_groups_covers_rows_and_keeps_clusters():
     # too many groups for the cap: consecutive quads of the sorted rows
     quads = ops.pack_decode_groups(tables, lens, skip, 64, cap=1)
     assert sorted(r for q in quads for r in q) == list(range(len(tables)))
+
+
+@pytest.mark.parametrize("tiles", [1, 2, 5, 100])
+def test_split_decode_groups_plan(tiles):
+    """Split plan: each group's block positions past the prefix are covered by its items
+    exactly once (contiguous ranges), split groups own consecutive partial slots listed in
+    a merge row, unsplit groups finish in place (slot -1), items are largest first, and
+    the tile budget is respected wherever a cut was possible."""
+    from docqa_amd import ops
+
+    skip = 2
+    tables = [[0, 1, 10, 11, 50, 70], [0, 1, 10, 11, 51, 71], [0, 1, 20, 52, 53, 72], [0, 1, 10, 12, 54, 73],
+              [0, 1, 30, 55, 56, 74], [0, 1, 20, 57, 58, 75], [0, 1, 60, 61, 62, 76]]
+    lens = [330, 300, 370, 250, 384, 200, 310]
+    quads = ops.pack_decode_groups(tables, lens, skip, 64, cap=4)
+    plan = ops.split_decode_groups(quads, tables, lens, skip, 64, cap=16, tiles_per_item=tiles)
+    assert plan.shape == (2, 16, 8) and plan.dtype == torch.int32
+    items = [r.tolist() for r in plan[0] if (r[:4] >= 0).any()]
+    merges = [r.tolist() for r in plan[1] if r[5] > 0]
+    slots = sorted(it[6] for it in items if it[6] >= 0)
+    assert slots == list(range(len(slots)))
+    for qd in quads:
+        key = sorted(qd)
+        mine = [it for it in items if sorted(r for r in it[:4] if r >= 0) == key]
+        nb = max((lens[r] + 63) // 64 for r in qd)
+        cover = []
+        for it in sorted(mine, key=lambda it: it[4]):
+            cover += list(range(max(it[4], skip), min(it[5], nb)))
+        assert cover == list(range(skip, nb))
+        if len(mine) == 1:
+            assert mine[0][6] == -1
+        else:
+            mg = [m for m in merges if sorted(r for r in m[:4] if r >= 0) == key]
+            assert len(mg) == 1 and mg[0][5] == len(mine)
+            assert sorted(it[6] for it in mine) == list(range(mg[0][4], mg[0][4] + len(mine)))
+            per = dict(ops.group_tiles_by_position(tables, lens, qd, skip, 64))
+            for it in mine:
+                t = sum(per.get(p, 0) for p in range(it[4], min(it[5], nb)))
+                single = it[5] - it[4] == 1
+                assert t <= tiles or single
+    if tiles == 1:
+        assert merges
+    if tiles == 100:
+        assert not merges

@@ -95,3 +95,55 @@ def test_grouped_cascade_padded_rows_zero(native):
     out = native.paged_decode_cascade_grouped(q, kc, vc, bt, cl, Hq, 1 / math.sqrt(D), pt, plen, 2, groups)
     assert torch.isfinite(out.float()).all()
     assert (out[2] == 0).all() and (out[5] == 0).all()
+
+
+@pytest.mark.parametrize("B,Hkv,seed", [(37, 8, 0), (256, 8, 3), (9, 2, 5)])
+@pytest.mark.parametrize("tiles", [1, 3, 12, 1000])
+def test_split_grouped_cascade_matches_per_row(native, B, Hkv, seed, tiles):
+    """Split plan (long groups over several workgroups + LSE merge) == per-row cascade and
+    the fp32 reference; planned with END-of-decode lengths longer than the current ones,
+    so some items have no keys yet."""
+    Hq, D, BS, Pb, maxb = 4 * Hkv, 128, 64, 3, 12
+    tables, lens, nblk = _trie_batch(B, Pb, maxb, seed)
+    kc = torch.randn(nblk, Hkv, BS, D, device="cuda", dtype=torch.bfloat16)
+    vc = torch.randn_like(kc)
+    bt = torch.tensor(tables, dtype=torch.int32, device="cuda")
+    cl = torch.tensor(lens, dtype=torch.int32, device="cuda")
+    q = torch.randn(B, (Hq + 2 * Hkv) * D, device="cuda", dtype=torch.bfloat16)
+    pt = torch.zeros(maxb, dtype=torch.int32, device="cuda")
+    pt[:Pb] = bt[0, :Pb]
+    plen = torch.tensor([Pb * BS], dtype=torch.int32, device="cuda")
+    scale = 1 / math.sqrt(D)
+    ref = native.paged_decode_cascade(q, kc, vc, bt, cl, Hq, maxb * BS, scale, pt, plen, 4)
+    with native.use_reference():
+        ref32 = native.paged_decode_cascade(q, kc, vc, bt, cl, Hq, maxb * BS, scale, pt, plen, 4)
+    end_lens = [min(L + 128, maxb * BS) for L in lens]
+    quads = native.pack_decode_groups(tables, end_lens, Pb, BS, (B + 1) // 2)
+    plan = native.split_decode_groups(quads, tables, end_lens, Pb, BS, max(B, 4), tiles)
+    if tiles == 1:
+        assert (plan[1, :, 5] > 1).any()   # some group really is split
+    out = native.paged_decode_cascade_grouped(q, kc, vc, bt, cl, Hq, scale, pt, plen, 4, plan.cuda())
+    err = (out.float() - ref.float()).abs().max().item()
+    assert err < 2e-2, err
+    err32 = (out.float() - ref32.float()).abs().max().item()
+    assert err32 < 3e-2, err32
+
+
+def test_split_grouped_cascade_padded_rows_zero(native):
+    Hkv, D, BS, Pb, maxb = 2, 128, 64, 2, 6
+    Hq, B = 4 * Hkv, 6
+    tables, lens, nblk = _trie_batch(B, Pb, maxb, 7)
+    plan = native.split_decode_groups([[0, 1, 2], [3, 4, 5]], tables, [maxb * BS] * B, Pb, BS, 8, 1)
+    lens[2] = 0
+    lens[5] = Pb * BS
+    kc = torch.randn(nblk, Hkv, BS, D, device="cuda", dtype=torch.bfloat16)
+    vc = torch.randn_like(kc)
+    bt = torch.tensor(tables, dtype=torch.int32, device="cuda")
+    cl = torch.tensor(lens, dtype=torch.int32, device="cuda")
+    q = torch.randn(B, (Hq + 2 * Hkv) * D, device="cuda", dtype=torch.bfloat16)
+    pt = bt[0].clone()
+    plen = torch.tensor([Pb * BS], dtype=torch.int32, device="cuda")
+    out = native.paged_decode_cascade_grouped(q, kc, vc, bt, cl, Hq, 1 / math.sqrt(D), pt, plen, 2, plan.cuda())
+    assert torch.isfinite(out.float()).all()
+    assert (out[2] == 0).all() and (out[5] == 0).all()
+    assert (out[0].float().abs().sum() > 0) and (out[4].float().abs().sum() > 0)
