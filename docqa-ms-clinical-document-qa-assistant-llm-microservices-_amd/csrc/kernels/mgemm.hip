@@ -55,6 +55,121 @@ __device__ __forceinline__ void better(float& bv, int& bi, float v, int i) {
   if (v > bv || (v == bv && i < bi)) { bv = v; bi = i; }
 }
 
+// Epilogue shared by the kernels: accumulators -> per-wave LDS scratch (the drained ring)
+// -> bf16 / fp32 split-K slab / fused SwiGLU / LM-head argmax partials.
+template <int EPI, int BN, int WM, int WN>
+__device__ __forceinline__ void mgemm_epilogue(f32x4 (&acc)[BM / WM / 16][BN / WN / 16], uint16_t* smem,
+                                               uint16_t* __restrict__ Y, float* __restrict__ P,
+                                               float* __restrict__ pv, int* __restrict__ pi, int M, int N,
+                                               int m0, int n0, int slice, int tile, int ntiles, int n_valid) {
+  constexpr int WAVES = WM * WN;
+  constexpr int MI = BM / WM / 16;
+  constexpr int CW = BN / WN;
+  constexpr int NJ = CW / 16;
+  constexpr int SCR = CW + 4;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int fr = lane & 15, fq = lane >> 4;
+  const int wm = wave % WM, wn = wave / WM;
+
+  // epilogue, 16 rows at a time: accumulators -> per-wave scratch [16][CW] -> re-read so
+  // that consecutive lanes own consecutive 16-B pieces of a row (coalesced row stores)
+  float* scr = reinterpret_cast<float*>(smem) + wave * 16 * SCR;
+  const int rbase = m0 + wm * (BM / WM), cbase = n0 + wn * CW;
+  float bestv[MI];
+  int besti[MI];
+#pragma unroll
+  for (int i = 0; i < MI; ++i) {
+#pragma unroll
+    for (int j = 0; j < NJ; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) scr[(fq * 4 + r) * SCR + j * 16 + fr] = acc[i][j][r];
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    // EPC: output columns per lane (fp32 slab 4, bf16 8, SwiGLU 16 inputs -> 8 outputs)
+    constexpr int EPC = EPI == EPI_PARTIAL ? 4 : EPI == EPI_BF16 ? 8 : 16;
+    constexpr int LPR = CW / EPC, RPS = 64 / LPR;          // lanes per row, rows per sweep
+    if constexpr (EPI != EPI_ARGMAX) {
+#pragma unroll
+      for (int it = 0; it < 16 / RPS; ++it) {
+        const int r = it * RPS + lane / LPR, c = (lane % LPR) * EPC;
+        float v[EPC];
+#pragma unroll
+        for (int e = 0; e < EPC / 4; ++e) {
+          const float4 t = *reinterpret_cast<const float4*>(scr + r * SCR + c + e * 4);
+          v[e * 4] = t.x; v[e * 4 + 1] = t.y; v[e * 4 + 2] = t.z; v[e * 4 + 3] = t.w;
+        }
+        const int row = rbase + i * 16 + r, col = cbase + c;
+        if (row < M) {
+          if constexpr (EPI == EPI_PARTIAL) {
+            *reinterpret_cast<float4*>(P + ((size_t)slice * M + row) * N + col) = float4{v[0], v[1], v[2], v[3]};
+          } else if constexpr (EPI == EPI_BF16) {
+            *reinterpret_cast<uint4*>(Y + (size_t)row * N + col) = pack8(v);
+          } else {
+            // 16 consecutive columns = one (gate 8, up 8) interleave group
+            float o[8];
+#pragma unroll
+            for (int e = 0; e < 8; ++e) {
+              const float gv = bf2f(f2bf(v[e])), uv = bf2f(f2bf(v[8 + e]));   // as the bf16 GEMM output
+              o[e] = silu_f(gv) * uv;
+            }
+            *reinterpret_cast<uint4*>(Y + (size_t)row * (N >> 1) + (col >> 1)) = pack8(o);
+          }
+        }
+      }
+    } else {
+      // 4 lanes per row, CW/4 columns each; the row's best (value, id) after 2 shuffles
+      constexpr int CPL = CW / 4;
+      const int rr = lane >> 2, cc = (lane & 3) * CPL;
+      float bv = -FLT_MAX;
+      int bi = 0x7fffffff;
+#pragma unroll
+      for (int e = 0; e < CPL / 4; ++e) {
+        const float4 t = *reinterpret_cast<const float4*>(scr + rr * SCR + cc + e * 4);
+        const float tv[4] = {t.x, t.y, t.z, t.w};
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int col = cbase + cc + e * 4 + q;
+          if (col < n_valid) better(bv, bi, bf2f(f2bf(tv[q])), col);
+        }
+      }
+#pragma unroll
+      for (int o = 1; o <= 2; o <<= 1) {
+        const float ov = __shfl_xor(bv, o, 64);
+        const int oi = __shfl_xor(bi, o, 64);
+        better(bv, bi, ov, oi);
+      }
+      bestv[i] = bv;
+      besti[i] = bi;
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  }
+  if constexpr (EPI == EPI_ARGMAX) {
+    // merge the WN column waves of each row through LDS, one partial per (row, tile)
+    __syncthreads();
+    float* rv = reinterpret_cast<float*>(smem);
+    int* ri = reinterpret_cast<int*>(smem) + BM * WN;
+    if ((lane & 3) == 0) {
+#pragma unroll
+      for (int i = 0; i < MI; ++i) {
+        const int lr = wm * (BM / WM) + i * 16 + (lane >> 2);
+        rv[lr * WN + wn] = bestv[i];
+        ri[lr * WN + wn] = besti[i];
+      }
+    }
+    __syncthreads();
+    for (int lr = tid; lr < BM; lr += WAVES * 64) {
+      const int row = m0 + lr;
+      if (row >= M) continue;
+      float bv = rv[lr * WN];
+      int bi = ri[lr * WN];
+#pragma unroll
+      for (int w = 1; w < WN; ++w) better(bv, bi, rv[lr * WN + w], ri[lr * WN + w]);
+      pv[(size_t)row * ntiles + tile] = bv;
+      pi[(size_t)row * ntiles + tile] = bi;
+    }
+  }
+}
+
 // PF: fragment prefetch (stage k+1's LDS reads under stage k's MFMAs, two register sets);
 // PF = 0 reads each stage's fragments after its barrier (one register set, for the
 // 128 x 128-per-wave layout whose two sets would not fit)
@@ -253,103 +368,7 @@ __global__ __launch_bounds__(WM * WN * 64) void mgemm_kernel(const uint16_t* __r
   wait_vmcnt<0>();
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   ring_barrier();   // every wave is done reading the ring: reuse it as epilogue scratch
-
-  // epilogue, 16 rows at a time: accumulators -> per-wave scratch [16][CW] -> re-read so
-  // that consecutive lanes own consecutive 16-B pieces of a row (coalesced row stores)
-  float* scr = reinterpret_cast<float*>(smem) + wave * 16 * SCR;
-  const int rbase = m0 + wm * (BM / WM), cbase = n0 + wn * CW;
-  float bestv[MI];
-  int besti[MI];
-#pragma unroll
-  for (int i = 0; i < MI; ++i) {
-#pragma unroll
-    for (int j = 0; j < NJ; ++j)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) scr[(fq * 4 + r) * SCR + j * 16 + fr] = acc[i][j][r];
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    // EPC: output columns per lane (fp32 slab 4, bf16 8, SwiGLU 16 inputs -> 8 outputs)
-    constexpr int EPC = EPI == EPI_PARTIAL ? 4 : EPI == EPI_BF16 ? 8 : 16;
-    constexpr int LPR = CW / EPC, RPS = 64 / LPR;          // lanes per row, rows per sweep
-    if constexpr (EPI != EPI_ARGMAX) {
-#pragma unroll
-      for (int it = 0; it < 16 / RPS; ++it) {
-        const int r = it * RPS + lane / LPR, c = (lane % LPR) * EPC;
-        float v[EPC];
-#pragma unroll
-        for (int e = 0; e < EPC / 4; ++e) {
-          const float4 t = *reinterpret_cast<const float4*>(scr + r * SCR + c + e * 4);
-          v[e * 4] = t.x; v[e * 4 + 1] = t.y; v[e * 4 + 2] = t.z; v[e * 4 + 3] = t.w;
-        }
-        const int row = rbase + i * 16 + r, col = cbase + c;
-        if (row < M) {
-          if constexpr (EPI == EPI_PARTIAL) {
-            *reinterpret_cast<float4*>(P + ((size_t)slice * M + row) * N + col) = float4{v[0], v[1], v[2], v[3]};
-          } else if constexpr (EPI == EPI_BF16) {
-            *reinterpret_cast<uint4*>(Y + (size_t)row * N + col) = pack8(v);
-          } else {
-            // 16 consecutive columns = one (gate 8, up 8) interleave group
-            float o[8];
-#pragma unroll
-            for (int e = 0; e < 8; ++e) {
-              const float gv = bf2f(f2bf(v[e])), uv = bf2f(f2bf(v[8 + e]));   // as the bf16 GEMM output
-              o[e] = silu_f(gv) * uv;
-            }
-            *reinterpret_cast<uint4*>(Y + (size_t)row * (N >> 1) + (col >> 1)) = pack8(o);
-          }
-        }
-      }
-    } else {
-      // 4 lanes per row, CW/4 columns each; the row's best (value, id) after 2 shuffles
-      constexpr int CPL = CW / 4;
-      const int rr = lane >> 2, cc = (lane & 3) * CPL;
-      float bv = -FLT_MAX;
-      int bi = 0x7fffffff;
-#pragma unroll
-      for (int e = 0; e < CPL / 4; ++e) {
-        const float4 t = *reinterpret_cast<const float4*>(scr + rr * SCR + cc + e * 4);
-        const float tv[4] = {t.x, t.y, t.z, t.w};
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          const int col = cbase + cc + e * 4 + q;
-          if (col < n_valid) better(bv, bi, bf2f(f2bf(tv[q])), col);
-        }
-      }
-#pragma unroll
-      for (int o = 1; o <= 2; o <<= 1) {
-        const float ov = __shfl_xor(bv, o, 64);
-        const int oi = __shfl_xor(bi, o, 64);
-        better(bv, bi, ov, oi);
-      }
-      bestv[i] = bv;
-      besti[i] = bi;
-    }
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-  }
-  if constexpr (EPI == EPI_ARGMAX) {
-    // merge the WN column waves of each row through LDS, one partial per (row, tile)
-    __syncthreads();
-    float* rv = reinterpret_cast<float*>(smem);
-    int* ri = reinterpret_cast<int*>(smem) + BM * WN;
-    if ((lane & 3) == 0) {
-#pragma unroll
-      for (int i = 0; i < MI; ++i) {
-        const int lr = wm * (BM / WM) + i * 16 + (lane >> 2);
-        rv[lr * WN + wn] = bestv[i];
-        ri[lr * WN + wn] = besti[i];
-      }
-    }
-    __syncthreads();
-    for (int lr = tid; lr < BM; lr += WAVES * 64) {
-      const int row = m0 + lr;
-      if (row >= M) continue;
-      float bv = rv[lr * WN];
-      int bi = ri[lr * WN];
-#pragma unroll
-      for (int w = 1; w < WN; ++w) better(bv, bi, rv[lr * WN + w], ri[lr * WN + w]);
-      pv[(size_t)row * ntiles + tile] = bv;
-      pi[(size_t)row * ntiles + tile] = bi;
-    }
-  }
+  mgemm_epilogue<EPI, BN, WM, WN>(acc, smem, Y, P, pv, pi, M, N, m0, n0, slice, tile, ntiles, n_valid);
 }
 
 __global__ __launch_bounds__(64) void mgemm_argmax_merge(const float* __restrict__ pv,
@@ -377,6 +396,11 @@ __global__ __launch_bounds__(64) void mgemm_argmax_merge(const float* __restrict
 //   5: BN 256, 64-deep stages x 2, waves 2 x 2 (128 x 128 each, 1 wave / SIMD), no prefetch
 //   6: BN 256, 64-deep stages x 2, waves 2 x 4 (128 x 64 each, 2 waves / SIMD), no prefetch
 struct Cfg { int bn, bks; };
+// (Decoupled X / W rings -- weights DMA'd by half the waves into a deeper ring of their
+// own, so the HBM stream can run further ahead than the L2-resident activations -- measured
+// no faster: 64-deep stages at (3 X, 4 W) / (2, 6) slots equal or 5-10 % slower than cfg 2,
+// 32-deep stages 40-50 % slower: the per-stage barrier + LDS traffic, not the weight
+// latency, sets the stage time; profiles/r2_mgemm_probe_dq_rings.log.)
 constexpr int kNumCfg = 6;
 constexpr Cfg kCfg[kNumCfg + 1] = {{0, 0}, {128, 64}, {128, 64}, {256, 32}, {256, 32}, {256, 64}, {256, 64}};
 

@@ -38,9 +38,10 @@ for (name, N, K) in [("qkv", 6144, 4096), ("o", 4096, 4096), ("gate_up", 28672, 
         if hasattr(nat, "mgemm"):
             for bn in [int(c) for c in os.environ.get("PROBE_CFGS", "2,5,6").split(",")]:
                 for S in (1, 2, 4, 7, 8, 14, 16):
-                    if K % (S * 128) or N % (128 if bn < 3 else 256) or (S > 1 and name in ("gate_up", "lm_head")):
+                    BNc = 256 if 3 <= bn <= 6 else 128
+                    if K % (S * 128) or N % BNc or (S > 1 and name in ("gate_up", "lm_head")):
                         continue
-                    if S > 1 and (N // (128 if bn < 3 else 256)) * S > 512:
+                    if S > 1 and (N // BNc) * S > 512:
                         continue
                     it = iter(range(1 << 30))
                     try:
