@@ -1195,10 +1195,18 @@ int docqa_paged_decode_cascade_split(const void* q, int q_stride, void* k_cache,
   if (B == 0) return 0;
   if (BS != 64 || maxb > kGroupMaxPos || Hq != 4 * Hkv || nchunk < 1 || nchunk > kCascadeMaxChunks || cap < 1)
     return -1;
-  int rc = docqa_cascade_prefix(q, q_stride, B, Hq, Hkv, scale, k_cache, v_cache, prefix_table, plen, BS,
-                                nchunk, pacc, pml, nullptr, nullptr, s);
-  if (rc) return rc;
-  const CascadeIn ci{pacc, pml, plen, nchunk, nullptr};
+  // DOCQA_GROUP_INLINE_PREFIX=1: no prefix kernel -- the plan's items start at block 0, so
+  // every group streams the shared template blocks itself (L2 hits after the first group)
+  static const bool inline_prefix = [] {
+    const char* e = getenv("DOCQA_GROUP_INLINE_PREFIX");
+    return e && atoi(e) == 1;
+  }();
+  if (!inline_prefix) {
+    const int rc = docqa_cascade_prefix(q, q_stride, B, Hq, Hkv, scale, k_cache, v_cache, prefix_table, plen,
+                                        BS, nchunk, pacc, pml, nullptr, nullptr, s);
+    if (rc) return rc;
+  }
+  const CascadeIn ci{pacc, pml, inline_prefix ? nullptr : plen, nchunk, nullptr};
   paged_decode_group_kernel<3, true><<<dim3(Hkv, cap), 256, 0, s>>>(
       (const uint16_t*)q, q_stride, (const uint16_t*)k_cache, (const uint16_t*)v_cache, block_tables, maxb,
       context_lens, B, Hkv, scale, (uint16_t*)out, out_stride, items, ci, ws_acc, ws_ml);

@@ -511,16 +511,20 @@ def group_tiles_by_position(tables: list[list[int]], lens: list[int], rows: list
     at each position beyond the ``skip`` cascade-prefix blocks: one or two tiles (by the
     longest length among the rows reading it) per DISTINCT block id at that position."""
     half = block_size // 2
-    nb = max((lens[r] + block_size - 1) // block_size for r in rows)
+    rl = [(tables[r], lens[r]) for r in rows]
+    nb = max((L + block_size - 1) // block_size for _, L in rl)
     out = []
     for pos in range(skip, nb):
+        lo = pos * block_size
         live: dict[int, int] = {}
-        for r in rows:
-            if pos * block_size < lens[r] and pos < len(tables[r]):
-                b = tables[r][pos]
-                live[b] = max(live.get(b, 0), lens[r])
+        for t, L in rl:
+            if lo < L and pos < len(t):
+                b = t[pos]
+                if live.get(b, 0) < L:
+                    live[b] = L
         if live:
-            out.append((pos, sum(1 + (L > pos * block_size + half) for L in live.values())))
+            thr = lo + half
+            out.append((pos, len(live) + sum(1 for L in live.values() if L > thr)))
     return out
 
 

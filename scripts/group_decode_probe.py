@@ -3,6 +3,7 @@ clusters of rows sharing prefix-cache blocks, unique tails), caches rotated past
 Usage: python scripts/group_decode_probe.py [B]"""
 import json
 import math
+import os
 import random
 import sys
 from pathlib import Path
@@ -63,8 +64,15 @@ def main():
     it = iter(range(1 << 30))
     t_grp = timeit(lambda: ops.paged_decode_cascade_grouped(q, *caches[next(it) % copies], bt, cl, Hq, scale, pt,
                                                             plen, nchunk, groups), iters=4 * copies)
+    plan = ops.split_decode_groups(quads, tables, lens, Pb, BS, B, int(os.environ.get("DOCQA_GROUP_TILES", "12"))).cuda()
+    it = iter(range(1 << 30))
+    t_split = timeit(lambda: ops.paged_decode_cascade_grouped(q, *caches[next(it) % copies], bt, cl, Hq, scale, pt,
+                                                              plen, nchunk, plan), iters=4 * copies)
+    tiles = sum(t for qd in quads for _, t in ops.group_tiles_by_position(tables, lens, qd, Pb, BS))
     kv_row = 2 * sum(l - Pb * BS for l in lens) * Hkv * D * 2
     print(json.dumps({"B": B, "groups": len(quads), "per_row_blocks": per_row, "grouped_blocks": grouped,
+                      "split_us": round(t_split, 1), "split_tiles_MB": round(tiles * Hkv * 16 / 1024, 1),
+                      "split_TBps": round(tiles * Hkv * 16384 / t_split / 1e6, 2),
                       "ring_us": round(t_ring, 1), "grouped_us": round(t_grp, 1),
                       "ring_suffix_TBps": round(kv_row / t_ring / 1e6, 2)}), flush=True)
 
