@@ -47,6 +47,36 @@ class SamplingParams:
 
 
 @dataclass
+class Reservation:
+    """KV blocks reserved for a batch (LLMEngine.reserve): per prompt its block table and
+    the number of leading tokens already in the prefix cache."""
+    tables: list
+    cached: list
+    max_new_tokens: int
+    n: int
+
+
+@dataclass
+class Launched:
+    """A batch enqueued by LLMEngine.launch: its reservation, the pinned host buffer its
+    tokens are copied to and the (prefill start, prefill end, decode end) events."""
+    reservation: Reservation
+    host: torch.Tensor
+    events: list | None
+    params: "SamplingParams"
+    t0: float
+    t1: float
+
+    @property
+    def done_event(self):
+        return self.events[2] if self.events else None
+
+    @property
+    def start_event(self):
+        return self.events[0] if self.events else None
+
+
+@dataclass
 class GenStats:
     prefill_s: float = 0.0
     decode_s: float = 0.0
@@ -426,8 +456,14 @@ class LLMEngine:
 
     def _generate_batch(self, prompts: list[list[int]], params: SamplingParams,
                         on_step=None) -> list[list[int]]:
-        B = len(prompts)
-        dev = self.device
+        return self.collect(self.launch(prompts, params, on_step))
+
+    def reserve(self, prompts: list[list[int]], params: SamplingParams) -> "Reservation":
+        """KV blocks of a batch: the longest cached prompt prefix of each prompt (prefix
+        cache, refcounted) + fresh blocks for the rest of the prompt and the generation.
+        Host-only work (~12 ms for 256 RAG prompts), so a pipelined caller runs it on its
+        preparation thread while the previous batch decodes; pass the result to
+        :meth:`launch` (or :meth:`release` it)."""
         lens = [len(p) for p in prompts]
         need = max(lens) + params.max_new_tokens
         if need > self.max_context:
@@ -448,9 +484,42 @@ class LLMEngine:
             for tb in tables:
                 alloc.free(tb)
             raise
+        return Reservation(tables, cached, params.max_new_tokens, len(prompts))
+
+    def release(self, r: "Reservation") -> None:
+        for tb in r.tables:
+            self.kv.allocator.free(tb)
+        r.tables = []
+
+    def launch(self, prompts: list[list[int]], params: SamplingParams | None = None, on_step=None,
+               reserved: "Reservation | None" = None) -> "Launched":
+        """Enqueue one batch (<= max_batch prompts): prefill, first-token selection and every
+        decode step (HIP-graph replays), then an async copy of the generated ids to pinned
+        host memory -- WITHOUT waiting for any of it.  :meth:`collect` waits and returns the
+        tokens.  Launching batch i+1 before collecting batch i queues its prefill right
+        behind batch i's last decode step, so the host work between batches (collecting,
+        detokenising, the next batch's set-up) never leaves the GPU idle.  Batches on one
+        stream share the bucket's graph buffers; every write to them is stream-ordered."""
+        params = params or SamplingParams()
+        B = len(prompts)
+        if B > self.max_batch:
+            raise ValueError(f"launch: {B} prompts > max_batch {self.max_batch}")
+        dev = self.device
+        cuda = dev.type == "cuda"
+        lens = [len(p) for p in prompts]
+        if reserved is not None and (reserved.n != B or reserved.max_new_tokens != params.max_new_tokens):
+            self.release(reserved)
+            reserved = None
+        r = reserved if reserved is not None else self.reserve(prompts, params)
+        tables, cached = r.tables, r.cached
+        alloc = self.kv.allocator
+        use_pc = self.prefix_cache and hasattr(alloc, "match_prefix")
         try:
             greedy = params.temperature <= 0.0
             t0 = time.perf_counter()
+            ev = [torch.cuda.Event(enable_timing=True) for _ in range(3)] if cuda else None
+            if cuda:
+                ev[0].record()
             with tracing.span("engine.prefill", seqs=B, tokens=sum(lens) - sum(cached)):
                 logits = self._prefill(prompts, tables, cached)
             if use_pc:
@@ -466,8 +535,8 @@ class LLMEngine:
                 g.shared_len.fill_(nshared * self.block_size)
             # state for the first decode step
             bt = torch.zeros(g.bp, self.max_blocks_per_seq, dtype=torch.int32)
-            for r, tb in enumerate(tables):
-                bt[r, :len(tb)] = torch.tensor(tb, dtype=torch.int32)
+            for i, tb in enumerate(tables):
+                bt[i, :len(tb)] = torch.tensor(tb, dtype=torch.int32)
             _upload(g.block_tables, bt)
             vl = torch.zeros(g.bp, dtype=torch.int32)
             vl[:B] = 1
@@ -485,16 +554,18 @@ class LLMEngine:
                 g.top_p.fill_(params.top_p)
                 if params.seed:
                     torch.manual_seed(params.seed)
-            first = self._select(logits, g) if greedy else self._select(logits, g)
+            first = self._select(logits, g)
             gen = torch.empty(B, params.max_new_tokens, dtype=torch.long, device=dev)
             gen[:, 0] = first
             tok = torch.zeros(g.bp, dtype=torch.int32, device=dev)
             tok[:B] = first.int()
             g.tokens.copy_(tok)
-            if dev.type == "cuda":  # this stream only: a pipelined prep stream keeps running
-                torch.cuda.current_stream().synchronize()
+            if cuda:
+                ev[1].record()
             t1 = time.perf_counter()
             if self.use_graphs and g.graph is None and params.max_new_tokens > 1:
+                if cuda:  # this stream only: a pipelined prep stream keeps running
+                    torch.cuda.current_stream().synchronize()
                 self._capture(g)
             for step in range(1, params.max_new_tokens):
                 if on_step is not None:
@@ -504,16 +575,34 @@ class LLMEngine:
                 else:
                     self._step_body(g)
                 gen[:, step] = g.out[:B]
-            result = gen.tolist()  # the one host sync of the decode loop
-            t2 = time.perf_counter()
-            self.stats.prefill_s += t1 - t0
-            self.stats.decode_s += t2 - t1
-            self.stats.prompt_tokens += sum(lens)
-            self.stats.generated_tokens += B * params.max_new_tokens
+            if cuda:
+                host = torch.empty(gen.shape, dtype=gen.dtype, pin_memory=True)
+                host.copy_(gen, non_blocking=True)
+                ev[2].record()
+            else:
+                host = gen
+        except BaseException:
+            self.release(r)
+            raise
+        self.stats.prompt_tokens += sum(lens)
+        self.stats.generated_tokens += B * params.max_new_tokens
+        return Launched(r, host, ev, params, t0, t1)
+
+    def collect(self, h: "Launched") -> list[list[int]]:
+        """Wait for a :meth:`launch`ed batch, free its KV blocks and return its tokens."""
+        try:
+            if h.events is not None:
+                h.events[2].synchronize()
+                self.stats.prefill_s += h.events[0].elapsed_time(h.events[1]) / 1e3
+                self.stats.decode_s += h.events[1].elapsed_time(h.events[2]) / 1e3
+            else:
+                t2 = time.perf_counter()
+                self.stats.prefill_s += h.t1 - h.t0
+                self.stats.decode_s += t2 - h.t1
+            result = h.host.tolist()
         finally:
-            for tb in tables:
-                alloc.free(tb)
-        if params.stop_on_eos:
+            self.release(h.reservation)
+        if h.params.stop_on_eos:
             eos = self.cfg.eos_token_id
             result = [r[: r.index(eos) + 1] if eos in r else r for r in result]
         return result

@@ -179,9 +179,10 @@ class RAGPipeline:
 
     # ------------------------------------------------------------------ pipelined
     @torch.inference_mode()
-    def _prepare(self, questions: list[str], stream, gate):
+    def _prepare(self, questions: list[str], stream, gate, params=None):
         """embed + kNN on a side HIP stream (held back by ``gate`` until the running
-        generation is ``lead_steps`` from its end), then host-side prompt assembly."""
+        generation is ``lead_steps`` from its end), then host-side prompt assembly and
+        (``params`` given) the batch's KV-block reservation."""
         t0 = time.perf_counter()
         ev_start = None
         sp = tracing.span("rag.prepare", n=len(questions))
@@ -201,8 +202,11 @@ class RAGPipeline:
             I = I.tolist()
         t1 = time.perf_counter()
         prompts = self.build_prompts(questions, I)
+        reserved = None
+        if params is not None and len(prompts) <= self.engine.max_batch:
+            reserved = self.engine.reserve(prompts, params)
         sp.__exit__(None, None, None)
-        return questions, I, prompts, ev_start, t0, t1, time.perf_counter()
+        return questions, I, prompts, reserved, ev_start, t0, t1, time.perf_counter()
 
     @torch.inference_mode()
     def answer_pipelined(self, batches: list[list[str]], params: SamplingParams | None = None,
@@ -217,45 +221,85 @@ class RAGPipeline:
 
         params = params or SamplingParams(stop_on_eos=True)
         if lead_steps is None:
-            # prompts are assembled from cached chunk token ids (~6 ms for 256 questions),
-            # so batch i+1's preparation fits in the last 4 decode steps of batch i
+            # embed + kNN (side stream) + prompt assembly + KV reservation of batch i+1 should
+            # finish before batch i's last decode step, so batch i+1's prefill is queued right
+            # behind it (launch-before-collect below); an earlier start only adds latency
+            # (measured: lead 4 / 8 / 16 steps -> 205.1 / 204.8 / 204.4 q/s, p50 1264 / 1301 /
+            # 1370 ms; profiles/r2_ab_pipeline_lead.log)
             lead_steps = int(os.environ.get("DOCQA_PIPELINE_LEAD", "4"))
-        cuda = self.engine.device.type == "cuda"
+        eng = self.engine
+        cuda = eng.device.type == "cuda"
         stream = torch.cuda.Stream() if cuda else None
+        pending = None   # (Launched, questions, I, ev_start, t0, t1, t2, t3) of the batch in flight
+
+        def finish(p):
+            h, questions, I, ev_start, t0, t1, t2, t3 = p
+            outs = eng.collect(h)
+            t4 = time.perf_counter()
+            if cuda:
+                latency = ev_start.elapsed_time(h.done_event) / 1e3
+                gen_s = h.start_event.elapsed_time(h.done_event) / 1e3
+            else:
+                latency, gen_s = t4 - t0, t4 - t3
+            st = StageTimes(embed_s=t1 - t0, search_s=0.0, prompt_s=t2 - t1, generate_s=gen_s)
+            self.last_times = st
+            res = [Answer(answer=self.chat_tok.decode(toks),
+                          sources=[self.metadata[j].get("source") for j in ids if 0 <= j < len(self.metadata)],
+                          token_ids=toks) for ids, toks in zip(I, outs)]
+            return res, st, latency
+
         with cf.ThreadPoolExecutor(1, thread_name_prefix="rag-prep") as ex:
-            fut = ex.submit(self._prepare, batches[0], stream, None) if batches else None
-            for i in range(len(batches)):
-                questions, I, prompts, ev_start, t0, t1, t2 = fut.result()
-                fut = None
-                nxt = batches[i + 1] if i + 1 < len(batches) else None
+            fut = ex.submit(self._prepare, batches[0], stream, None, params) if batches else None
+            try:
+                for i in range(len(batches)):
+                    questions, I, prompts, reserved, ev_start, t0, t1, t2 = fut.result()
+                    fut = None
+                    nxt = batches[i + 1] if i + 1 < len(batches) else None
 
-                def on_step(step, total, nxt=nxt):
-                    nonlocal fut
-                    if nxt is not None and fut is None and step >= max(1, total - lead_steps):
-                        gate = None
-                        if cuda:
-                            gate = torch.cuda.Event()
-                            gate.record()
-                        fut = ex.submit(self._prepare, nxt, stream, gate)
+                    def on_step(step, total, nxt=nxt):
+                        nonlocal fut
+                        if nxt is not None and fut is None and step >= max(1, total - lead_steps):
+                            gate = None
+                            if cuda:
+                                gate = torch.cuda.Event()
+                                gate.record()
+                            fut = ex.submit(self._prepare, nxt, stream, gate, params)
 
-                t3 = time.perf_counter()
-                outs = self.engine.generate(prompts, params, on_step=on_step)
-                t4 = time.perf_counter()
-                if nxt is not None and fut is None:   # single-step generations
-                    fut = ex.submit(self._prepare, nxt, stream, None)
-                if cuda:
-                    ev_done = torch.cuda.Event(enable_timing=True)
-                    ev_done.record()
-                    ev_done.synchronize()
-                    latency = ev_start.elapsed_time(ev_done) / 1e3
-                else:
-                    latency = t4 - t0
-                st = StageTimes(embed_s=t1 - t0, search_s=0.0, prompt_s=t2 - t1, generate_s=t4 - t3)
-                self.last_times = st
-                res = [Answer(answer=self.chat_tok.decode(toks),
-                              sources=[self.metadata[j].get("source") for j in ids if 0 <= j < len(self.metadata)],
-                              token_ids=toks) for ids, toks in zip(I, outs)]
-                yield res, st, latency
+                    t3 = time.perf_counter()
+                    if len(prompts) <= eng.max_batch:
+                        h = eng.launch(prompts, params, on_step=on_step, reserved=reserved)
+                    else:   # larger than one engine batch: plain blocking generation
+                        h = None
+                        outs = eng.generate(prompts, params, on_step=on_step)
+                    if nxt is not None and fut is None:   # single-step generations
+                        fut = ex.submit(self._prepare, nxt, stream, None, params)
+                    # batch i is queued behind batch i-1: collect and answer batch i-1 now
+                    if pending is not None:
+                        p, pending = pending, None
+                        yield finish(p)
+                    if h is not None:
+                        pending = (h, questions, I, ev_start, t0, t1, t2, t3)
+                    else:
+                        t4 = time.perf_counter()
+                        st = StageTimes(embed_s=t1 - t0, search_s=0.0, prompt_s=t2 - t1, generate_s=t4 - t3)
+                        self.last_times = st
+                        yield ([Answer(answer=self.chat_tok.decode(toks),
+                                       sources=[self.metadata[j].get("source") for j in ids
+                                                if 0 <= j < len(self.metadata)], token_ids=toks)
+                                for ids, toks in zip(I, outs)], st, t4 - t0)
+                if pending is not None:
+                    p, pending = pending, None
+                    yield finish(p)
+            finally:
+                if pending is not None:   # abandoned generator: wait, free the blocks
+                    eng.collect(pending[0])
+                if fut is not None:
+                    try:
+                        r = fut.result()[3]
+                        if r is not None:
+                            eng.release(r)
+                    except Exception:
+                        pass
 
 
 class _nullctx:
