@@ -22,7 +22,7 @@ import math
 import itertools
 import os
 import time
-from dataclasses import dataclass
+from dataclasses import dataclass, field
 
 import numpy as np
 import torch
@@ -30,7 +30,7 @@ import torch
 from .. import ops
 from ..utils import tracing
 from ..models.llama import AttnMeta, LlamaModel
-from .kv_cache import KVCache
+from .kv_cache import KVCache, TailCache
 
 _PREFILL_LOG = os.environ.get("DOCQA_PREFILL_LOG") == "1"   # one JSON line per prefill chunk
 _PREFILL_DUMP = os.environ.get("DOCQA_PREFILL_DUMP", "")       # dir: save paged-prefill shapes for replay
@@ -49,11 +49,14 @@ class SamplingParams:
 @dataclass
 class Reservation:
     """KV blocks reserved for a batch (LLMEngine.reserve): per prompt its block table and
-    the number of leading tokens already in the prefix cache."""
+    the number of leading tokens already in the prefix cache; ``copies``: token-granular
+    prefix hits (source block, destination block, rows) to copy before the prefill, their
+    source blocks pinned until then."""
     tables: list
     cached: list
     max_new_tokens: int
     n: int
+    copies: list = field(default_factory=list)
 
 
 @dataclass
@@ -226,6 +229,10 @@ class LLMEngine:
         self.lpt = os.environ.get("DOCQA_DECODE_LPT", "1") == "1"
         # grouped cascade decode: rows sharing prefix-cache blocks attended together
         self.group_decode = os.environ.get("DOCQA_DECODE_GROUP", "1") == "1"
+        # token-granular prefix reuse below the block size (engine/kv_cache.py TailCache)
+        cap = int(os.environ.get("DOCQA_TAIL_CACHE", "1024"))
+        self.tail = (TailCache(self.kv.allocator, block_size, cap)
+                     if self.prefix_cache and cap > 0 and hasattr(self.kv.allocator, "match_prefix") else None)
         self._graphs: dict[tuple, _DecodeGraph] = {}
         self._pool = None
         self.stats = GenStats()
@@ -470,26 +477,57 @@ class LLMEngine:
             raise ValueError(f"prompt+generation {need} exceeds max_context {self.max_context}")
         alloc = self.kv.allocator
         use_pc = self.prefix_cache and hasattr(alloc, "match_prefix")
-        tables, cached = [], []
+        BS = self.block_size
+        r = Reservation([], [], params.max_new_tokens, len(prompts))
         try:
             for p in prompts:
                 hit = alloc.match_prefix(p) if use_pc else []
-                if hit and len(hit) * self.block_size >= len(p):
+                if hit and len(hit) * BS >= len(p):
                     alloc.free([hit[-1]])  # always recompute >= 1 token (its logits seed decode)
                     hit = hit[:-1]
-                tables.append(hit)
-                cached.append(len(hit) * self.block_size)
-                tables[-1] = hit + alloc.alloc(self.kv.blocks_for(len(p) + params.max_new_tokens) - len(hit))
+                r.tables.append(hit)
+                fresh = self._alloc_blocks(self.kv.blocks_for(len(p) + params.max_new_tokens) - len(hit))
+                r.tables[-1] = hit + fresh
+                k, c = len(hit), len(hit) * BS
+                if self.tail is not None and fresh:
+                    t = self.tail.lookup(p, k, len(p) - 1 - c)
+                    if t is not None:
+                        r.copies.append((t[0], fresh[0], t[1]))
+                        c += t[1]
+                r.cached.append(c)
         except MemoryError:
-            for tb in tables:
-                alloc.free(tb)
+            self.release(r)
             raise
-        return Reservation(tables, cached, params.max_new_tokens, len(prompts))
+        return r
+
+    def _alloc_blocks(self, n: int) -> list[int]:
+        try:
+            return self.kv.allocator.alloc(n)
+        except MemoryError:
+            # blocks pinned by the token-granular prefix cache are the first to give way
+            if self.tail is None or not self.tail.shrink(max(n, len(self.tail) // 2)):
+                raise
+            return self.kv.allocator.alloc(n)
 
     def release(self, r: "Reservation") -> None:
         for tb in r.tables:
             self.kv.allocator.free(tb)
         r.tables = []
+        if r.copies:
+            self.tail.unpin([src for src, _, _ in r.copies])
+            r.copies = []
+
+    def _copy_prefix_rows(self, copies: list) -> None:
+        """K/V rows [0, m) of each source block -> the same rows of its destination block,
+        every layer (token-granular prefix hits, queued before the prefill reads them)."""
+        src = torch.tensor([s for s, _, m in copies for _ in range(m)], dtype=torch.long)
+        dst = torch.tensor([d for _, d, m in copies for _ in range(m)], dtype=torch.long)
+        rows = torch.tensor([i for _, _, m in copies for i in range(m)], dtype=torch.long)
+        if self.device.type == "cuda":
+            src, dst, rows = (t.pin_memory().to(self.device, non_blocking=True) for t in (src, dst, rows))
+        for kc, vc in self.kv.caches:
+            kc[dst, :, rows] = kc[src, :, rows]
+            vc[dst, :, rows] = vc[src, :, rows]
 
     def launch(self, prompts: list[list[int]], params: SamplingParams | None = None, on_step=None,
                reserved: "Reservation | None" = None) -> "Launched":
@@ -520,11 +558,17 @@ class LLMEngine:
             ev = [torch.cuda.Event(enable_timing=True) for _ in range(3)] if cuda else None
             if cuda:
                 ev[0].record()
+            if r.copies:
+                self._copy_prefix_rows(r.copies)
+                self.tail.unpin([src for src, _, _ in r.copies])   # the copy is queued
+                r.copies = []
             with tracing.span("engine.prefill", seqs=B, tokens=sum(lens) - sum(cached)):
                 logits = self._prefill(prompts, tables, cached)
             if use_pc:
                 for p, tb in zip(prompts, tables):
                     alloc.register_prefix(p, tb)
+                    if self.tail is not None:
+                        self.tail.register(p, tb)
             self.stats.cached_tokens += sum(cached)
             nshared = self._shared_prefix_blocks(tables, cached)
             g = self._get_graph(_bucket(B, self.max_batch) if self.use_graphs else B, greedy, nshared > 0)

@@ -48,7 +48,41 @@ def test_engine_batch_invariance_and_block_reuse():
     batch = eng.generate(prompts, sp)
     single = [eng.generate([p], sp)[0] for p in prompts]
     assert batch == single
+    if eng.tail is not None:
+        eng.tail.clear()   # blocks pinned by the token-granular prefix cache
     assert eng.kv.allocator.num_free() == free0  # every block returned
+
+
+def test_token_granular_prefix_reuse_identical_tokens():
+    """Prompts diverging INSIDE a KV block (RAG chunk / question boundaries): the
+    token-granular prefix cache copies the common rows of the block instead of
+    recomputing them; greedy tokens equal the no-cache engine's, blocks are accounted."""
+    import os
+
+    m = _model()
+    base = list(range(10, 47))                       # 2 full 16-token blocks + 5 tokens
+    prompts1 = [base + [5, 6, 7, 8], base + [9, 9]]
+    prompts2 = [base + [5, 6, 7, 1, 2, 3], base + [9, 4], base[:20] + [3, 3, 3]]
+    sp = SamplingParams(max_new_tokens=6, stop_on_eos=False)
+    eng = LLMEngine(m, max_batch=8, max_context=128, block_size=16, use_graphs=False)
+    if eng.tail is None:
+        pytest.skip("prefix cache needs the native block manager")
+    free0 = eng.kv.allocator.num_free()
+    eng.generate(prompts1, sp)
+    c0 = eng.stats.cached_tokens
+    got = eng.generate(prompts2, sp)
+    # base[32:37] + [5, 6, 7] of prompt 0, base[32:37] + [9] of prompt 1, base[16:20] of prompt 2
+    assert eng.stats.cached_tokens - c0 == (32 + 8) + (32 + 6) + (16 + 4)
+    assert eng.tail.hit_tokens == 8 + 6 + 4
+    os.environ["DOCQA_PREFIX_CACHE"] = "0"
+    try:
+        ref = LLMEngine(m, max_batch=8, max_context=128, block_size=16, use_graphs=False)
+    finally:
+        del os.environ["DOCQA_PREFIX_CACHE"]
+    assert ref.tail is None
+    assert got == ref.generate(prompts2, sp)
+    eng.tail.clear()
+    assert eng.kv.allocator.num_free() == free0
 
 
 def test_engine_max_batch_chunking_and_eos_stop():
