@@ -25,6 +25,14 @@ struct BlockManager : torch::CustomClassHolder {
   void free(std::vector<int64_t> b) { core.free(b); }
   std::vector<int64_t> match_prefix(std::vector<int64_t> t) { return core.match_prefix(t); }
   void register_prefix(std::vector<int64_t> t, std::vector<int64_t> b) { core.register_prefix(t, b); }
+  std::vector<int64_t> match_alloc_batch(std::vector<int64_t> keys, std::vector<int64_t> nb,
+                                         std::vector<int64_t> lens, std::vector<int64_t> need) {
+    return core.match_alloc_batch(keys, nb, lens, need);
+  }
+  void register_batch(std::vector<int64_t> keys, std::vector<int64_t> nb, std::vector<int64_t> tables,
+                      std::vector<int64_t> ntab) {
+    core.register_batch(keys, nb, tables, ntab);
+  }
   std::vector<int64_t> stats() { return core.stats(); }
   docqa_rt::BlockManagerCore core;
 };
@@ -42,5 +50,7 @@ TORCH_LIBRARY(docqa_rt, m) {
       .def("free", &BlockManager::free)
       .def("match_prefix", &BlockManager::match_prefix)
       .def("register_prefix", &BlockManager::register_prefix)
+      .def("match_alloc_batch", &BlockManager::match_alloc_batch)
+      .def("register_batch", &BlockManager::register_batch)
       .def("stats", &BlockManager::stats);
 }

@@ -118,6 +118,81 @@ class BlockManagerCore {
     }
   }
 
+  // Batched reservation with caller-computed block keys (one call for a whole batch:
+  // the per-call cost of the bound methods, not the hashing, dominated 256 single calls).
+  // Prompt i has nb[i] full-block keys in `keys` (chained: key j covers tokens
+  // [0, (j+1) bs)), lens[i] tokens and needs need[i] blocks: its longest cached key prefix
+  // is shared (the last hit is dropped when it would cover the whole prompt -- >= 1 token
+  // is always recomputed), then fresh blocks complete the table.  Returns
+  // [hits_0 .. hits_{B-1}, table_0 (need_0 ids), ..., table_{B-1}].  All or nothing: on
+  // exhaustion every block taken or shared for the batch is released and it throws.
+  std::vector<int64_t> match_alloc_batch(const std::vector<int64_t>& keys, const std::vector<int64_t>& nb,
+                                         const std::vector<int64_t>& lens, const std::vector<int64_t>& need) {
+    std::lock_guard<std::mutex> g(mu_);
+    const size_t B = nb.size();
+    if (lens.size() != B || need.size() != B) throw std::runtime_error("match_alloc_batch: sizes");
+    std::vector<int64_t> out(B);
+    size_t total = 0;
+    for (size_t i = 0; i < B; ++i) total += (size_t)need[i];
+    out.reserve(B + total);
+    size_t off = 0;
+    try {
+      for (size_t i = 0; i < B; ++i) {
+        if (off + (size_t)nb[i] > keys.size()) throw std::runtime_error("match_alloc_batch: keys");
+        int64_t hits = 0;
+        for (int64_t j = 0; j < nb[i] && hits < need[i]; ++j) {
+          auto it = table_.find((uint64_t)keys[off + j]);
+          if (it == table_.end()) break;
+          const int64_t b = it->second;
+          if (ref_[b] == 0) lru_erase(b);
+          ++ref_[b];
+          out.push_back(b);
+          ++hits;
+        }
+        if (hits > 0 && hits * bs_ >= lens[i]) {
+          release_one(out.back());
+          out.pop_back();
+          --hits;
+        }
+        ++lookups_;
+        hit_blocks_ += hits;
+        out[i] = hits;
+        const int64_t fresh = need[i] - hits;
+        if (fresh > (int64_t)free_.size() + (int64_t)lru_.size()) throw std::runtime_error("KV cache exhausted");
+        for (int64_t j = 0; j < fresh; ++j) out.push_back(take_one());
+        off += (size_t)nb[i];
+      }
+    } catch (...) {
+      for (size_t k = B; k < out.size(); ++k) release_one(out[k]);
+      throw;
+    }
+    return out;
+  }
+
+  // Publish the first nb[i] blocks of table i under its caller-computed keys (the keys
+  // match_alloc_batch looks up); tables flat with ntab[i] ids each.
+  void register_batch(const std::vector<int64_t>& keys, const std::vector<int64_t>& nb,
+                      const std::vector<int64_t>& tables, const std::vector<int64_t>& ntab) {
+    std::lock_guard<std::mutex> g(mu_);
+    size_t ko = 0, to = 0;
+    for (size_t i = 0; i < nb.size(); ++i) {
+      const int64_t full = std::min(nb[i], ntab[i]);
+      if (ko + (size_t)nb[i] > keys.size() || to + (size_t)ntab[i] > tables.size())
+        throw std::runtime_error("register_batch: sizes");
+      for (int64_t j = 0; j < full; ++j) {
+        const uint64_t h = (uint64_t)keys[ko + j];
+        const int64_t b = tables[to + j];
+        check(b);
+        if (table_.count(h) || cached_[b]) continue;
+        table_[h] = b;
+        hash_of_[b] = h;
+        cached_[b] = true;
+      }
+      ko += (size_t)nb[i];
+      to += (size_t)ntab[i];
+    }
+  }
+
   std::vector<int64_t> stats() {
     std::lock_guard<std::mutex> g(mu_);
     return {(int64_t)free_.size(), (int64_t)lru_.size(), (int64_t)table_.size(), lookups_, hit_blocks_};
@@ -128,6 +203,17 @@ class BlockManagerCore {
     uint64_t h = parent;
     for (int64_t j = i * bs_; j < (i + 1) * bs_; ++j) h = mix(h, (uint64_t)t[j]);
     return h;
+  }
+  void release_one(int64_t b) {   // free() of one block, lock held
+    if (ref_[b] <= 0) throw std::runtime_error("double free of KV block");
+    if (--ref_[b] == 0) {
+      if (cached_[b]) {
+        lru_.push_back(b);
+        lru_pos_[b] = std::prev(lru_.end());
+      } else {
+        free_.push_back(b);
+      }
+    }
   }
   void check(int64_t b) const {
     if (b < 0 || b >= n_) throw std::runtime_error("KV block id out of range");

@@ -37,17 +37,41 @@ int main(int argc, char** argv) {
         std::vector<int64_t> prompt = tpl;
         const int extra = 1 + rng() % 40;
         for (int i = 0; i < extra; ++i) prompt.push_back(rng() % 50000);
-        std::vector<int64_t> blocks = bm.match_prefix(prompt);
-        const int64_t need = ((int64_t)prompt.size() + 8 + BS - 1) / BS - (int64_t)blocks.size();
-        try {
-          auto nb = bm.alloc(need);
-          blocks.insert(blocks.end(), nb.begin(), nb.end());
-        } catch (const std::runtime_error&) {
-          ++oom;
-          bm.free(blocks);
-          continue;
+        std::vector<int64_t> blocks;
+        if (it % 2) {   // the engine's batched, caller-keyed path (match_alloc_batch / register_batch)
+          std::vector<int64_t> keys;
+          uint64_t h = 7;
+          for (size_t j = 0; j + BS <= prompt.size(); j += BS) {
+            for (size_t q = j; q < j + BS; ++q) h = docqa_rt::mix(h, (uint64_t)prompt[q]);
+            keys.push_back((int64_t)h);
+          }
+          const int64_t total = ((int64_t)prompt.size() + 8 + BS - 1) / BS;
+          std::vector<int64_t> out;
+          try {
+            out = bm.match_alloc_batch(keys, {(int64_t)keys.size()}, {(int64_t)prompt.size()}, {total});
+          } catch (const std::runtime_error&) {
+            ++oom;
+            continue;
+          }
+          blocks.assign(out.begin() + 1, out.end());
+          if ((int64_t)blocks.size() != total || out[0] * BS >= (int64_t)prompt.size()) {
+            fprintf(stderr, "match_alloc_batch: bad table\n");
+            std::abort();
+          }
+          bm.register_batch(keys, {(int64_t)keys.size()}, blocks, {total});
+        } else {
+          blocks = bm.match_prefix(prompt);
+          const int64_t need = ((int64_t)prompt.size() + 8 + BS - 1) / BS - (int64_t)blocks.size();
+          try {
+            auto nb = bm.alloc(need);
+            blocks.insert(blocks.end(), nb.begin(), nb.end());
+          } catch (const std::runtime_error&) {
+            ++oom;
+            bm.free(blocks);
+            continue;
+          }
+          bm.register_prefix(prompt, blocks);
         }
-        bm.register_prefix(prompt, blocks);
         if (rng() % 4 == 0) {         // a second holder of the prompt's leading blocks
           std::vector<int64_t> head(blocks.begin(), blocks.begin() + std::min<size_t>(2, blocks.size()));
           bm.share(head);

@@ -84,6 +84,18 @@ class KVCache:
         return (tokens + self.block_size - 1) // self.block_size
 
 
+def chain_keys(tokens, block_size: int, nblocks: int) -> list[int]:
+    """keys[j] (j = 0 .. nblocks): chain hash of tokens [0, j * block_size) -- the key of
+    block position j for the token-granular cache, and (j >= 1) of full block j - 1 for
+    the block prefix cache (LLMEngine.reserve)."""
+    h = TailCache.SEED
+    out = [h]
+    for j in range(nblocks):
+        h = hash((h, tuple(tokens[j * block_size:(j + 1) * block_size])))
+        out.append(h)
+    return out
+
+
 class TailCache:
     """Token-granular extension of the block prefix cache (RadixAttention-style reuse below
     the 64-token block granularity).
@@ -92,12 +104,12 @@ class TailCache:
     Where two RAG prompts diverge inside a block -- at a retrieved-chunk boundary or in the
     question -- the tokens of that block before the divergence point are identical too,
     and so are their K/V (causal attention: position t depends only on tokens <= t).  This
-    cache remembers, for every block position of every prefilled prompt, (block id, the
-    prompt's tokens in that block), indexed by a chain hash of all tokens before the block
-    and the block's first token.  A new prompt whose full-block match stops at block k
-    looks block k up here; the longest common token run m over the stored variants is
-    copied into the prompt's own fresh block (a K/V row copy instead of m tokens of
-    prefill) and prefill starts at 64 k + m.
+    cache remembers, for every block position of every prefilled prompt, (the prompt's
+    tokens in that block, block id), keyed by a chain hash of all tokens before the block;
+    the variants of one key are kept sorted, so the variant sharing the longest token run
+    with a new prompt is a neighbour of its bisection point.  A prompt whose full-block
+    match stops at block k copies the common K/V rows of that variant into its own fresh
+    block (one gather/scatter per layer) and prefill starts at 64 k + m.
 
     Each entry pins its block (one allocator reference), so the rows it promises are never
     reallocated; entries are evicted least-recently-used beyond ``capacity``.  Thread-safe
@@ -112,10 +124,9 @@ class TailCache:
         self.alloc = allocator
         self.bs = block_size
         self.capacity = capacity
-        # LRU over entries: (prefix key, block) -> tokens; index (prefix key, first token)
-        # -> {block: tokens}
+        # LRU over entries (prefix key, block) -> tokens; per key a sorted [(tokens, block)]
         self._lru: "collections.OrderedDict[tuple[int, int], tuple]" = collections.OrderedDict()
-        self._idx: dict[tuple[int, int], dict[int, tuple]] = {}
+        self._var: dict[int, list[tuple[tuple, int]]] = {}
         self._lock = threading.Lock()
         self.lookups = 0
         self.hit_tokens = 0
@@ -123,43 +134,54 @@ class TailCache:
     def __len__(self) -> int:
         return len(self._lru)
 
-    def _chain(self, tokens, nblocks: int) -> list[int]:
+    def chain(self, tokens, nblocks: int) -> list[int]:
         """keys[j]: key of block position j = chain hash of every token before it."""
-        bs, h = self.bs, self.SEED
-        out = [h]
-        for j in range(nblocks):
-            h = hash((h, tuple(tokens[j * bs:(j + 1) * bs])))
-            out.append(h)
-        return out
+        return chain_keys(tokens, self.bs, nblocks)
 
     def _drop(self, key: int, blk: int) -> None:
-        toks = self._lru.pop((key, blk))
-        variants = self._idx.get((key, toks[0]))
-        if variants is not None:
-            variants.pop(blk, None)
-            if not variants:
-                del self._idx[(key, toks[0])]
+        import bisect
 
-    def lookup(self, tokens, k: int, limit: int) -> tuple[int, int] | None:
+        toks = self._lru.pop((key, blk))
+        lst = self._var.get(key)
+        if lst is not None:
+            i = bisect.bisect_left(lst, (toks, blk))
+            if i < len(lst) and lst[i] == (toks, blk):
+                del lst[i]
+            if not lst:
+                del self._var[key]
+
+    @staticmethod
+    def _lcp(a: tuple, b) -> int:
+        n, m = min(len(a), len(b)), 0
+        while m < n and a[m] == b[m]:
+            m += 1
+        return m
+
+    def lookup(self, tokens, k: int, limit: int, keys: list[int] | None = None) -> tuple[int, int] | None:
         """(source block, m): the longest cached token run at block position ``k`` that
         ``tokens`` continue, m <= ``limit``; pins the source block (release it with
-        :meth:`unpin` once the copy is queued).  None when nothing matches."""
+        :meth:`unpin` once the copy is queued).  None when nothing matches.  ``keys``:
+        precomputed :meth:`chain` of at least k blocks."""
+        import bisect
+
         if limit <= 0:
             return None
-        key = self._chain(tokens, k)[k]
-        seg = tokens[k * self.bs:k * self.bs + min(self.bs, limit)]
+        key = (keys if keys is not None else self.chain(tokens, k))[k]
+        seg = tuple(tokens[k * self.bs:k * self.bs + min(self.bs, limit)])
         with self._lock:
             self.lookups += 1
-            variants = self._idx.get((key, seg[0]))
-            if not variants:
+            lst = self._var.get(key)
+            if not lst:
                 return None
+            i = bisect.bisect_left(lst, (seg,))
             best, bm = -1, 0
-            for blk, toks in variants.items():
-                m, n = 1, min(len(toks), len(seg))
-                while m < n and toks[m] == seg[m]:
-                    m += 1
-                if m > bm:
-                    best, bm = blk, m
+            for j in (i - 1, i):
+                if 0 <= j < len(lst):
+                    m = self._lcp(lst[j][0], seg)
+                    if m > bm:
+                        best, bm = lst[j][1], m
+            if bm == 0:
+                return None
             self._lru.move_to_end((key, best))
             self.alloc.share([best])
             self.hit_tokens += bm
@@ -169,12 +191,15 @@ class TailCache:
         if blocks:
             self.alloc.free(blocks)
 
-    def register(self, tokens, table: list[int]) -> None:
+    def register(self, tokens, table: list[int], keys: list[int] | None = None) -> None:
         """Publish every block position of a prefilled prompt (its prompt tokens only: the
         rows past the prompt belong to generation)."""
+        import bisect
+
         bs = self.bs
         nb = min((len(tokens) + bs - 1) // bs, len(table))
-        keys = self._chain(tokens, nb)
+        if keys is None or len(keys) < nb + 1:
+            keys = self.chain(tokens, nb)
         freed = []
         with self._lock:
             for j in range(nb):
@@ -183,17 +208,13 @@ class TailCache:
                 if (key, blk) in self._lru:
                     self._lru.move_to_end((key, blk))
                     continue
-                variants = self._idx.setdefault((key, toks[0]), {})
-                covered = None
-                for b2, t2 in variants.items():
-                    if t2[:len(toks)] == toks:   # an entry already promises these tokens
-                        covered = b2
-                        break
-                if covered is not None:
-                    self._lru.move_to_end((key, covered))
+                lst = self._var.setdefault(key, [])
+                i = bisect.bisect_left(lst, (toks,))
+                if i < len(lst) and lst[i][0][:len(toks)] == toks:   # already promised
+                    self._lru.move_to_end((key, lst[i][1]))
                     continue
                 self.alloc.share([blk])
-                variants[blk] = toks
+                lst.insert(i, (toks, blk))
                 self._lru[(key, blk)] = toks
             while len(self._lru) > self.capacity:
                 (key, blk), _ = next(iter(self._lru.items()))

@@ -30,7 +30,7 @@ import torch
 from .. import ops
 from ..utils import tracing
 from ..models.llama import AttnMeta, LlamaModel
-from .kv_cache import KVCache, TailCache
+from .kv_cache import KVCache, TailCache, chain_keys
 
 _PREFILL_LOG = os.environ.get("DOCQA_PREFILL_LOG") == "1"   # one JSON line per prefill chunk
 _PREFILL_DUMP = os.environ.get("DOCQA_PREFILL_DUMP", "")       # dir: save paged-prefill shapes for replay
@@ -57,6 +57,7 @@ class Reservation:
     max_new_tokens: int
     n: int
     copies: list = field(default_factory=list)
+    keys: list | None = None   # per prompt: chained block keys (kv_cache.chain_keys)
 
 
 @dataclass
@@ -229,10 +230,11 @@ class LLMEngine:
         self.lpt = os.environ.get("DOCQA_DECODE_LPT", "1") == "1"
         # grouped cascade decode: rows sharing prefix-cache blocks attended together
         self.group_decode = os.environ.get("DOCQA_DECODE_GROUP", "1") == "1"
+        # the prefix cache needs the native block manager (batched hash-keyed lookups)
+        self._use_pc = self.prefix_cache and hasattr(self.kv.allocator, "match_alloc_batch")
         # token-granular prefix reuse below the block size (engine/kv_cache.py TailCache)
         cap = int(os.environ.get("DOCQA_TAIL_CACHE", "1024"))
-        self.tail = (TailCache(self.kv.allocator, block_size, cap)
-                     if self.prefix_cache and cap > 0 and hasattr(self.kv.allocator, "match_prefix") else None)
+        self.tail = TailCache(self.kv.allocator, block_size, cap) if self._use_pc and cap > 0 else None
         self._graphs: dict[tuple, _DecodeGraph] = {}
         self._pool = None
         self.stats = GenStats()
@@ -475,39 +477,47 @@ class LLMEngine:
         need = max(lens) + params.max_new_tokens
         if need > self.max_context:
             raise ValueError(f"prompt+generation {need} exceeds max_context {self.max_context}")
+        with tracing.span("engine.reserve", seqs=len(prompts)):
+            return self._reserve(prompts, params, lens)
+
+    def _reserve(self, prompts, params, lens) -> "Reservation":
         alloc = self.kv.allocator
-        use_pc = self.prefix_cache and hasattr(alloc, "match_prefix")
         BS = self.block_size
+        need = [self.kv.blocks_for(n + params.max_new_tokens) for n in lens]
         r = Reservation([], [], params.max_new_tokens, len(prompts))
+        if not self._use_pc:
+            for n in need:
+                r.tables.append(self._retry(lambda n=n: alloc.alloc(n)))
+            r.cached = [0] * len(prompts)
+            return r
+        # one native call for the batch: longest cached full-block prefix of every prompt
+        # (chained keys computed here, reused by the token-granular cache and registration)
+        r.keys = [chain_keys(p, BS, (len(p) + BS - 1) // BS) for p in prompts]
+        hits, r.tables = self._retry(lambda: alloc.match_alloc_batch(
+            [k[1:len(p) // BS + 1] for k, p in zip(r.keys, prompts)], lens, need))
         try:
-            for p in prompts:
-                hit = alloc.match_prefix(p) if use_pc else []
-                if hit and len(hit) * BS >= len(p):
-                    alloc.free([hit[-1]])  # always recompute >= 1 token (its logits seed decode)
-                    hit = hit[:-1]
-                r.tables.append(hit)
-                fresh = self._alloc_blocks(self.kv.blocks_for(len(p) + params.max_new_tokens) - len(hit))
-                r.tables[-1] = hit + fresh
-                k, c = len(hit), len(hit) * BS
-                if self.tail is not None and fresh:
-                    t = self.tail.lookup(p, k, len(p) - 1 - c)
+            for i, p in enumerate(prompts):
+                k, c = hits[i], hits[i] * BS
+                if self.tail is not None and k < len(r.tables[i]):
+                    t = self.tail.lookup(p, k, len(p) - 1 - c, keys=r.keys[i])
                     if t is not None:
-                        r.copies.append((t[0], fresh[0], t[1]))
+                        r.copies.append((t[0], r.tables[i][k], t[1]))
                         c += t[1]
                 r.cached.append(c)
-        except MemoryError:
+        except BaseException:
             self.release(r)
             raise
         return r
 
-    def _alloc_blocks(self, n: int) -> list[int]:
+    def _retry(self, fn):
+        """``fn()``; on KV-pool exhaustion, once more after the blocks pinned by the
+        token-granular prefix cache give way."""
         try:
-            return self.kv.allocator.alloc(n)
+            return fn()
         except MemoryError:
-            # blocks pinned by the token-granular prefix cache are the first to give way
-            if self.tail is None or not self.tail.shrink(max(n, len(self.tail) // 2)):
+            if self.tail is None or not self.tail.shrink(max(1, len(self.tail))):
                 raise
-            return self.kv.allocator.alloc(n)
+            return fn()
 
     def release(self, r: "Reservation") -> None:
         for tb in r.tables:
@@ -517,14 +527,41 @@ class LLMEngine:
             self.tail.unpin([src for src, _, _ in r.copies])
             r.copies = []
 
+    def queue_prefix_copies(self, r: "Reservation") -> None:
+        """Queue the token-granular prefix hits' K/V row copies of a reservation (before its
+        prefill reads them) and drop the pins on their sources (stream order keeps them
+        valid until copied)."""
+        if r.copies:
+            self._copy_prefix_rows(r.copies)
+            self.tail.unpin([src for src, _, _ in r.copies])
+            r.copies = []
+
+    def register_prefixes(self, prompts: list[list[int]], tables: list[list[int]], keys=None) -> None:
+        """Publish prefilled prompts to the block prefix cache (full blocks, one native
+        call) and to the token-granular cache (every block position)."""
+        if not self._use_pc:
+            return
+        BS = self.block_size
+        keys = [k if k is not None else chain_keys(p, BS, (len(p) + BS - 1) // BS)
+                for p, k in zip(prompts, keys or [None] * len(prompts))]
+        self.kv.allocator.register_batch([k[1:len(p) // BS + 1] for k, p in zip(keys, prompts)], tables)
+        if self.tail is not None:
+            for p, tb, k in zip(prompts, tables, keys):
+                self.tail.register(p, tb, keys=k)
+
     def _copy_prefix_rows(self, copies: list) -> None:
         """K/V rows [0, m) of each source block -> the same rows of its destination block,
         every layer (token-granular prefix hits, queued before the prefill reads them)."""
-        src = torch.tensor([s for s, _, m in copies for _ in range(m)], dtype=torch.long)
-        dst = torch.tensor([d for _, d, m in copies for _ in range(m)], dtype=torch.long)
-        rows = torch.tensor([i for _, _, m in copies for i in range(m)], dtype=torch.long)
-        if self.device.type == "cuda":
-            src, dst, rows = (t.pin_memory().to(self.device, non_blocking=True) for t in (src, dst, rows))
+        # one [n, 3] (src, dst, rows) upload, expanded on the device (no host sync:
+        # output_size is known here)
+        tab = torch.tensor(copies, dtype=torch.long)
+        R = int(tab[:, 2].sum())
+        tab = tab.to(self.device, non_blocking=True)
+        m = tab[:, 2]
+        src = torch.repeat_interleave(tab[:, 0], m, output_size=R)
+        dst = torch.repeat_interleave(tab[:, 1], m, output_size=R)
+        start = torch.cumsum(m, 0) - m
+        rows = torch.arange(R, device=self.device) - torch.repeat_interleave(start, m, output_size=R)
         for kc, vc in self.kv.caches:
             kc[dst, :, rows] = kc[src, :, rows]
             vc[dst, :, rows] = vc[src, :, rows]
@@ -538,6 +575,10 @@ class LLMEngine:
         behind batch i's last decode step, so the host work between batches (collecting,
         detokenising, the next batch's set-up) never leaves the GPU idle.  Batches on one
         stream share the bucket's graph buffers; every write to them is stream-ordered."""
+        with tracing.span("engine.launch", seqs=len(prompts)):
+            return self._launch(prompts, params, on_step, reserved)
+
+    def _launch(self, prompts, params, on_step, reserved) -> "Launched":
         params = params or SamplingParams()
         B = len(prompts)
         if B > self.max_batch:
@@ -551,24 +592,19 @@ class LLMEngine:
         r = reserved if reserved is not None else self.reserve(prompts, params)
         tables, cached = r.tables, r.cached
         alloc = self.kv.allocator
-        use_pc = self.prefix_cache and hasattr(alloc, "match_prefix")
+        use_pc = self._use_pc
         try:
             greedy = params.temperature <= 0.0
             t0 = time.perf_counter()
             ev = [torch.cuda.Event(enable_timing=True) for _ in range(3)] if cuda else None
             if cuda:
                 ev[0].record()
-            if r.copies:
-                self._copy_prefix_rows(r.copies)
-                self.tail.unpin([src for src, _, _ in r.copies])   # the copy is queued
-                r.copies = []
+            self.queue_prefix_copies(r)
             with tracing.span("engine.prefill", seqs=B, tokens=sum(lens) - sum(cached)):
                 logits = self._prefill(prompts, tables, cached)
             if use_pc:
-                for p, tb in zip(prompts, tables):
-                    alloc.register_prefix(p, tb)
-                    if self.tail is not None:
-                        self.tail.register(p, tb)
+                with tracing.span("engine.register", seqs=B):
+                    self.register_prefixes(prompts, tables, r.keys)
             self.stats.cached_tokens += sum(cached)
             nshared = self._shared_prefix_blocks(tables, cached)
             g = self._get_graph(_bucket(B, self.max_batch) if self.use_graphs else B, greedy, nshared > 0)
@@ -611,6 +647,8 @@ class LLMEngine:
                 if cuda:  # this stream only: a pipelined prep stream keeps running
                     torch.cuda.current_stream().synchronize()
                 self._capture(g)
+            sp_dec = tracing.span("engine.decode_enqueue", steps=params.max_new_tokens - 1)
+            sp_dec.__enter__()
             for step in range(1, params.max_new_tokens):
                 if on_step is not None:
                     on_step(step, params.max_new_tokens)
@@ -619,6 +657,7 @@ class LLMEngine:
                 else:
                     self._step_body(g)
                 gen[:, step] = g.out[:B]
+            sp_dec.__exit__(None, None, None)
             if cuda:
                 host = torch.empty(gen.shape, dtype=gen.dtype, pin_memory=True)
                 host.copy_(gen, non_blocking=True)
@@ -634,6 +673,10 @@ class LLMEngine:
 
     def collect(self, h: "Launched") -> list[list[int]]:
         """Wait for a :meth:`launch`ed batch, free its KV blocks and return its tokens."""
+        with tracing.span("engine.collect", seqs=h.reservation.n):
+            return self._collect(h)
+
+    def _collect(self, h: "Launched") -> list[list[int]]:
         try:
             if h.events is not None:
                 h.events[2].synchronize()

@@ -54,6 +54,7 @@ class Request:
     out: list[int] = field(default_factory=list)
     blocks: list[int] = field(default_factory=list)
     cached: int = 0
+    res: object = None   # the engine Reservation (prefix-copy pins, block keys)
     t_arrival: float = 0.0
     t_first: float = 0.0
     done: bool = False
@@ -181,26 +182,22 @@ class ContinuousEngine:
 
     def _take_waiting(self) -> list[Request]:
         eng, alloc = self.eng, self.eng.kv.allocator
-        use_pc = eng.prefix_cache and hasattr(alloc, "match_prefix")
         admitted, budget = [], 0
         with self._cv:
             while self.waiting and len(self.running) + len(admitted) < self.max_running:
                 r = self.waiting[0]
-                hit = alloc.match_prefix(r.prompt) if use_pc else []
-                if hit and len(hit) * eng.block_size >= len(r.prompt):
-                    alloc.free([hit[-1]])        # recompute >= 1 token: its logits seed decode
-                    hit = hit[:-1]
-                need = eng.kv.blocks_for(len(r.prompt) + r.params.max_new_tokens) - len(hit)
                 try:
-                    new = alloc.alloc(need)
+                    # prefix-cache hits (whole blocks + token-granular rows), fresh blocks
+                    res = eng.reserve([r.prompt], r.params)
                 except MemoryError:
-                    alloc.free(hit)
                     if not self.running and not admitted:   # can never fit: fail, don't stall
+                        need = eng.kv.blocks_for(len(r.prompt) + r.params.max_new_tokens)
                         self.waiting.popleft().future.set_exception(MemoryError(
                             f"request needs {need} KV blocks, the cache has {alloc.num_free()} free"))
                         continue
                     break                        # retry after running requests retire
-                r.blocks, r.cached = hit + new, len(hit) * eng.block_size
+                r.blocks, r.cached, r.res = res.tables[0], res.cached[0], res
+                res.tables = []                  # owned by the request from here on
                 admitted.append(self.waiting.popleft())
                 budget += len(r.prompt) - r.cached
                 if budget >= eng.max_prefill_tokens:
@@ -220,16 +217,18 @@ class ContinuousEngine:
         t0 = time.perf_counter()
         try:
             with tracing.span("sched.admit", seqs=len(adm), tokens=sum(len(r.prompt) - r.cached for r in adm)):
+                for r in adm:
+                    eng.queue_prefix_copies(r.res)
                 logits = eng._prefill([r.prompt for r in adm], [r.blocks for r in adm], [r.cached for r in adm])
                 first = self._sample_rows(logits, [r.params for r in adm])
         except Exception as e:  # noqa: BLE001
             for r in adm:
+                eng.release(r.res)
                 alloc.free(r.blocks)
                 r.future.set_exception(e)
             return
-        if eng.prefix_cache and hasattr(alloc, "register_prefix"):
-            for r in adm:
-                alloc.register_prefix(r.prompt, r.blocks)
+        eng.register_prefixes([r.prompt for r in adm], [r.blocks for r in adm], [r.res.keys[0] if r.res.keys else None
+                                                                                  for r in adm])
         now = time.perf_counter()
         eng.stats.prefill_s += now - t0
         eng.stats.prompt_tokens += sum(len(r.prompt) for r in adm)

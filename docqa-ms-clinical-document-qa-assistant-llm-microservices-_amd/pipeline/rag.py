@@ -104,7 +104,7 @@ class RAGPipeline:
         D, I = self.index.search(q, self.k)
         return D, I
 
-    def _piece_prompt(self, qtext: str, ids: list[int]) -> list[int]:
+    def _piece_prompt(self, qtext: str, ids: list[int], qids: list[int] | None = None) -> list[int]:
         ct = self.chat_tok
         if not hasattr(self, "_frame"):
             s = ct.special
@@ -127,11 +127,13 @@ class RAGPipeline:
                 out += sep
             out += c
             first = False
-        return out + mid_ids + ct.encode(qtext) + post
+        return out + mid_ids + (qids if qids is not None else ct.encode(qtext)) + post
 
     def build_prompts(self, questions: list[str], I: list[list[int]]) -> list[list[int]]:
         if self._pieces is not None and os.environ.get("DOCQA_PROMPT_PIECES", "1") == "1":
-            prompts = [self._piece_prompt(q, ids) for q, ids in zip(questions, I)]
+            many = getattr(self.chat_tok, "encode_many", None)
+            qids = many(questions) if many else [None] * len(questions)
+            prompts = [self._piece_prompt(q, ids, qi) for q, ids, qi in zip(questions, I, qids)]
             lim = self.max_prompt_tokens
             if lim:
                 prompts = [p if len(p) <= lim else p[: lim // 2] + p[-lim // 2:] for p in prompts]
@@ -201,7 +203,8 @@ class RAGPipeline:
             _, I = self.index.search(qemb, self.k)
             I = I.tolist()
         t1 = time.perf_counter()
-        prompts = self.build_prompts(questions, I)
+        with tracing.span("rag.prompts", n=len(questions)):
+            prompts = self.build_prompts(questions, I)
         reserved = None
         if params is not None and len(prompts) <= self.engine.max_batch:
             reserved = self.engine.reserve(prompts, params)
@@ -243,13 +246,20 @@ class RAGPipeline:
                 latency, gen_s = t4 - t0, t4 - t3
             st = StageTimes(embed_s=t1 - t0, search_s=0.0, prompt_s=t2 - t1, generate_s=gen_s)
             self.last_times = st
-            res = [Answer(answer=self.chat_tok.decode(toks),
+            with tracing.span("rag.detokenise", n=len(outs)):
+                res = [Answer(answer=self.chat_tok.decode(toks),
                           sources=[self.metadata[j].get("source") for j in ids if 0 <= j < len(self.metadata)],
-                          token_ids=toks) for ids, toks in zip(I, outs)]
+                              token_ids=toks) for ids, toks in zip(I, outs)]
             return res, st, latency
 
-        with cf.ThreadPoolExecutor(1, thread_name_prefix="rag-prep") as ex:
+        # batch i-1 is collected and detokenised on a helper thread as soon as batch i's
+        # decode starts being enqueued (its prefill is queued by then): enqueueing the
+        # decode graphs blocks the host on the stream's queue depth until about the end of
+        # the batch, so collecting after launch() returned left the GPU idle meanwhile
+        with cf.ThreadPoolExecutor(1, thread_name_prefix="rag-prep") as ex, \
+                cf.ThreadPoolExecutor(1, thread_name_prefix="rag-collect") as col:
             fut = ex.submit(self._prepare, batches[0], stream, None, params) if batches else None
+            fin = None
             try:
                 for i in range(len(batches)):
                     questions, I, prompts, reserved, ev_start, t0, t1, t2 = fut.result()
@@ -257,7 +267,10 @@ class RAGPipeline:
                     nxt = batches[i + 1] if i + 1 < len(batches) else None
 
                     def on_step(step, total, nxt=nxt):
-                        nonlocal fut
+                        nonlocal fut, fin, pending
+                        if pending is not None and fin is None:
+                            p, pending = pending, None
+                            fin = col.submit(finish, p)
                         if nxt is not None and fut is None and step >= max(1, total - lead_steps):
                             gate = None
                             if cuda:
@@ -273,10 +286,12 @@ class RAGPipeline:
                         outs = eng.generate(prompts, params, on_step=on_step)
                     if nxt is not None and fut is None:   # single-step generations
                         fut = ex.submit(self._prepare, nxt, stream, None, params)
-                    # batch i is queued behind batch i-1: collect and answer batch i-1 now
-                    if pending is not None:
+                    if pending is not None:   # no decode step enqueued: collect batch i-1 now
                         p, pending = pending, None
-                        yield finish(p)
+                        fin = col.submit(finish, p)
+                    if fin is not None:
+                        f, fin = fin, None
+                        yield f.result()
                     if h is not None:
                         pending = (h, questions, I, ev_start, t0, t1, t2, t3)
                     else:
@@ -291,6 +306,11 @@ class RAGPipeline:
                     p, pending = pending, None
                     yield finish(p)
             finally:
+                if fin is not None:
+                    try:
+                        fin.result()
+                    except Exception:
+                        pass
                 if pending is not None:   # abandoned generator: wait, free the blocks
                     eng.collect(pending[0])
                 if fut is not None:

@@ -39,6 +39,25 @@ class NativeBlockAllocator:
     def register_prefix(self, tokens: list[int], blocks: list[int]) -> None:
         self._m.register_prefix(list(tokens), list(blocks))
 
+    def match_alloc_batch(self, keys: list[list[int]], lens: list[int], need: list[int]):
+        """One native call for a whole batch (block_manager_core.h match_alloc_batch):
+        ``keys[i]``: chained keys of prompt i's full blocks.  Returns (hits, tables)."""
+        flat = [k for ks in keys for k in ks]
+        try:
+            out = self._m.match_alloc_batch(flat, [len(ks) for ks in keys], list(lens), list(need))
+        except RuntimeError as e:
+            raise MemoryError(str(e)) from e
+        B = len(keys)
+        hits, tables, o = list(out[:B]), [], B
+        for n in need:
+            tables.append(list(out[o:o + n]))
+            o += n
+        return hits, tables
+
+    def register_batch(self, keys: list[list[int]], tables: list[list[int]]) -> None:
+        self._m.register_batch([k for ks in keys for k in ks], [len(ks) for ks in keys],
+                               [b for tb in tables for b in tb], [len(tb) for tb in tables])
+
     def stats(self) -> dict:
         f, lru, cached, lookups, hits = self._m.stats()
         return {"free": f, "evictable": lru, "cached_blocks": cached, "lookups": lookups,

@@ -136,6 +136,12 @@ class ChatTokenizer:
     def encode(self, text: str) -> list[int]:
         return [self._to_model.get(i, i) for i in self.tok.encode(text).ids]
 
+    def encode_many(self, texts: list[str]) -> list[list[int]]:
+        """:meth:`encode` of many texts in one ``encode_batch`` call (parallel in the Rust
+        tokenizer); identical ids."""
+        tm = self._to_model
+        return [[tm.get(i, i) for i in e.ids] for e in self.tok.encode_batch(list(texts))]
+
     def chat_prompt(self, user: str, system: str | None = None) -> list[int]:
         s = self.special
         ids = [s("<|begin_of_text|>")]

@@ -10,17 +10,21 @@ from docqa_amd.models.llama import LlamaConfig, LlamaModel
 def test_prefix_cache_reuse_is_exact():
     m = LlamaModel(LlamaConfig.preset("tiny"), device="cpu", dtype=torch.float32, seed=3)
     eng = LLMEngine(m, max_batch=4, max_context=512, block_size=16, use_graphs=False)
-    assert hasattr(eng.kv.allocator, "match_prefix"), "native block manager not loaded"
+    assert hasattr(eng.kv.allocator, "match_alloc_batch"), "native block manager not loaded"
     pre = list(range(100, 180))                    # 5 full shared blocks
     ps = [pre + [1, 2, 3], pre + [9, 8, 7, 6, 5], pre[:32]]  # last: prompt == 2 full blocks
     sp = SamplingParams(max_new_tokens=5, stop_on_eos=False)
     first = eng.generate(ps, sp)
     assert eng.stats.cached_tokens == 0
     second = eng.generate(ps, sp)
-    assert eng.stats.cached_tokens == 80 + 80 + 16   # full hit, full hit, all-but-last-block
+    # whole blocks (80, 80, 16: the last prompt's second block is recomputed) + the
+    # token-granular rows of the partial block: every token but the last one is cached
+    assert eng.stats.cached_tokens == sum(len(p) - 1 for p in ps)
+    assert eng.tail.hit_tokens == 2 + 4 + 15
     ref = LLMEngine(m, max_batch=4, max_context=512, block_size=16, use_graphs=False,
                     prefix_cache=False).generate(ps, sp)
     assert first == second == ref
+    eng.tail.clear()   # blocks pinned by the token-granular prefix cache
     st = eng.kv.allocator.stats()
     assert st["free"] + st["evictable"] == eng.kv.num_blocks
 
