@@ -76,3 +76,62 @@ def test_cascade_reference_op_equals_paged_decode():
     c = R.paged_decode_cascade(q, kc, vc, bt, cl, Hq, 128, 0.1, torch.tensor(shared + [0] * 5, dtype=torch.int32),
                                torch.tensor([48], dtype=torch.int32))
     assert torch.allclose(a, c, atol=1e-5)
+
+
+def test_tail_cache_lookup_register_evict_accounting():
+    """TailCache (token-granular prefix reuse): the best variant is found by bisection,
+    entries pin their blocks, LRU eviction and shrink return them, and concurrent
+    register/lookup from two threads keeps the allocator's accounting exact."""
+    import random
+    import threading
+
+    from docqa_amd import ops
+    from docqa_amd.engine.kv_cache import TailCache, make_allocator
+
+    assert ops.load_native()
+    a = make_allocator(256, 16)
+    tc = TailCache(a, 16, capacity=40)
+    base = list(range(100, 116))                              # one full block
+    p1 = base + [1, 2, 3, 4, 5]
+    p2 = base + [1, 2, 9, 9]
+    t1, t2 = a.alloc(2), a.alloc(2)
+    tc.register(p1, t1)
+    tc.register(p2, t2)
+    # block 1 variants: (1,2,3,4,5) and (1,2,9,9); a prompt continuing 1,2,3,4 matches p1's
+    hit = tc.lookup(base + [1, 2, 3, 4, 7, 7], 1, limit=10)
+    assert hit == (t1[1], 4)
+    tc.unpin([hit[0]])
+    assert tc.lookup(base + [5, 5], 1, limit=10) is None       # no variant starts with 5
+    hit = tc.lookup(base + [1, 2, 3], 1, limit=2)             # capped by the limit
+    assert hit is not None and hit[1] == 2
+    tc.unpin([hit[0]])
+    a.free(t1)
+    a.free(t2)
+    tc.clear()
+    assert a.num_free() == 256
+
+    errors = []
+
+    def worker(seed):
+        r = random.Random(seed)
+        try:
+            for _ in range(300):
+                p = base + [r.randrange(4) for _ in range(r.randrange(1, 30))]
+                tb = a.alloc((len(p) + 15) // 16)
+                h = tc.lookup(p, 1, len(p) - 17) if len(p) > 17 else None
+                if h is not None:
+                    tc.unpin([h[0]])
+                tc.register(p, tb)
+                a.free(tb)
+        except Exception as e:  # noqa: BLE001
+            errors.append(e)
+
+    th = [threading.Thread(target=worker, args=(s,)) for s in (1, 2)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    assert not errors
+    assert len(tc) <= 40
+    tc.clear()
+    assert a.num_free() == 256
