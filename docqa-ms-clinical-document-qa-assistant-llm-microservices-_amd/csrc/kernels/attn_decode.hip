@@ -1211,7 +1211,9 @@ int docqa_paged_decode_cascade_split(const void* q, int q_stride, void* k_cache,
       (const uint16_t*)q, q_stride, (const uint16_t*)k_cache, (const uint16_t*)v_cache, block_tables, maxb,
       context_lens, B, Hkv, scale, (uint16_t*)out, out_stride, items, ci, ws_acc, ws_ml);
   DOCQA_CHECK_LAUNCH();
-  group_split_merge_kernel<<<dim3(Hkv, cap), 256, 0, s>>>(merges, ws_acc, ws_ml, context_lens, B, Hkv,
+  // merge rows: at most (cap + 1) / 2 (ops.split_decode_groups guarantees it), so half the
+  // grid -- the empty workgroups of the unused merge rows are not free
+  group_split_merge_kernel<<<dim3(Hkv, (cap + 1) / 2), 256, 0, s>>>(merges, ws_acc, ws_ml, context_lens, B, Hkv,
                                                           (uint16_t*)out, out_stride, ci);
   DOCQA_CHECK_LAUNCH();
   return 0;

@@ -537,7 +537,8 @@ def split_decode_groups(quads: list[list[int]], tables: list[list[int]], lens: l
     item and KV head.  A group that needs one item finishes in its workgroup; the items of
     a longer group write partials that a merge kernel combines.  Items are ordered largest
     first (LPT).  plan[0]: items (4 rows, first position, end position, slot or -1, 0);
-    plan[1]: merges (4 rows, first slot, slots, 0, 0)."""
+    plan[1]: merges (4 rows, first slot, slots, 0, 0) -- at most (cap + 1) // 2 of them
+    (the merge kernel's grid)."""
     items, merges, nslot = [], [], 0
     budget = max(1, tiles_per_item)
     while True:
@@ -560,8 +561,10 @@ def split_decode_groups(quads: list[list[int]], tables: list[list[int]], lens: l
                 for lo, hi, t in cuts:
                     items.append((t, rows4 + [lo, hi, nslot, 0]))
                     nslot += 1
-        if len(items) <= cap and len(merges) <= cap:
+        if len(items) <= cap and len(merges) <= (cap + 1) // 2:
             break
+        if budget > 1 << 20:
+            raise ValueError(f"split_decode_groups: {len(quads)} groups exceed the plan capacity {cap}")
         budget *= 2
     items.sort(key=lambda it: -it[0])
     plan = torch.full((2, cap, 8), -1, dtype=torch.int32)
