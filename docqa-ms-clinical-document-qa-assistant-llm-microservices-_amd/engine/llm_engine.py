@@ -233,7 +233,8 @@ class LLMEngine:
         # the prefix cache needs the native block manager (batched hash-keyed lookups)
         self._use_pc = self.prefix_cache and hasattr(self.kv.allocator, "match_alloc_batch")
         # token-granular prefix reuse below the block size (engine/kv_cache.py TailCache)
-        cap = int(os.environ.get("DOCQA_TAIL_CACHE", "1024"))
+        # (each entry pins one block: at most an eighth of the pool)
+        cap = min(int(os.environ.get("DOCQA_TAIL_CACHE", "1024")), num_blocks // 8)
         self.tail = TailCache(self.kv.allocator, block_size, cap) if self._use_pc and cap > 0 else None
         self._graphs: dict[tuple, _DecodeGraph] = {}
         self._pool = None
