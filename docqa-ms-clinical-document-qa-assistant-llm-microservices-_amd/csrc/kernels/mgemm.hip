@@ -401,12 +401,20 @@ struct Cfg { int bn, bks; };
 // no faster: 64-deep stages at (3 X, 4 W) / (2, 6) slots equal or 5-10 % slower than cfg 2,
 // 32-deep stages 40-50 % slower: the per-stage barrier + LDS traffic, not the weight
 // latency, sets the stage time; profiles/r2_mgemm_probe_dq_rings.log.)
-constexpr int kNumCfg = 6;
-constexpr Cfg kCfg[kNumCfg + 1] = {{0, 0}, {128, 64}, {128, 64}, {256, 32}, {256, 32}, {256, 64}, {256, 64}};
+//   7: BN  64, 64-deep stages x 3, waves 4 x 2 ( 64 x 32 each, 2 waves / SIMD): twice the
+//      workgroups of cfg 2 for the narrow projections that otherwise fill half the chip
+constexpr int kNumCfg = 7;
+constexpr Cfg kCfg[kNumCfg + 1] = {{0, 0}, {128, 64}, {128, 64}, {256, 32}, {256, 32}, {256, 64}, {256, 64},
+                                   {64, 64}};
 
 template <int EPI, int BN, int BKS, int NSR, int WM, int WN, int PF = 1>
 int launch(const uint16_t* x, const uint16_t* w, uint16_t* y, float* p, float* pv, int* pi, int M,
            int N, int K, int S, int n_valid, hipStream_t s) {
+  // the epilogue sweeps 16-row slices with (columns per wave) / (columns per lane) lanes per
+  // row: the SwiGLU epilogue (16 columns per lane) needs >= 64 columns per wave
+  if constexpr (EPI == EPI_GLU && BN / WN < 64) {
+    return -1;
+  } else {
   const int ntiles = N / BN, Ks = K / S;
   int remap = 0;
   if (S > 1 && 8 % S == 0 && (ntiles * S) % 8 == 0) remap = 1;
@@ -416,6 +424,7 @@ int launch(const uint16_t* x, const uint16_t* w, uint16_t* y, float* p, float* p
                                                                       ntiles, remap, n_valid);
   DOCQA_CHECK_LAUNCH();
   return 0;
+  }
 }
 
 template <int EPI>
@@ -428,6 +437,7 @@ int launch_cfg(int cfg, const uint16_t* x, const uint16_t* w, uint16_t* y, float
     case 4: return launch<EPI, 256, 32, 4, 2, 2>(x, w, y, p, pv, pi, M, N, K, S, n_valid, s);
     case 5: return launch<EPI, 256, 64, 2, 2, 2, 0>(x, w, y, p, pv, pi, M, N, K, S, n_valid, s);
     case 6: return launch<EPI, 256, 64, 2, 2, 4, 0>(x, w, y, p, pv, pi, M, N, K, S, n_valid, s);
+    case 7: return launch<EPI, 64, 64, 3, 4, 2>(x, w, y, p, pv, pi, M, N, K, S, n_valid, s);
     default: return -1;
   }
 }

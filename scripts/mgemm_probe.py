@@ -38,7 +38,7 @@ for (name, N, K) in [("qkv", 6144, 4096), ("o", 4096, 4096), ("gate_up", 28672, 
         if hasattr(nat, "mgemm"):
             for bn in [int(c) for c in os.environ.get("PROBE_CFGS", "2,5,6").split(",")]:
                 for S in (1, 2, 4, 7, 8, 14, 16):
-                    BNc = 256 if 3 <= bn <= 6 else 128
+                    BNc = 256 if 3 <= bn <= 6 else 64 if bn == 7 else 128
                     if K % (S * 128) or N % BNc or (S > 1 and name in ("gate_up", "lm_head")):
                         continue
                     if S > 1 and (N // BNc) * S > 512:
@@ -49,14 +49,17 @@ for (name, N, K) in [("qkv", 6144, 4096), ("o", 4096, 4096), ("gate_up", 28672, 
                                                            iters=4 * copies), 1)
                     except RuntimeError as e:
                         row[f"c{bn}_S{S}"] = str(e)[:60]
-                if name == "gate_up":
-                    it = iter(range(1 << 30))
-                    row[f"glu{bn}"] = round(timeit(lambda: nat.mgemm_glu(x, ws[next(it) % copies], bn),
-                                                   iters=4 * copies), 1)
-                if name == "lm_head":
-                    it = iter(range(1 << 30))
-                    row[f"argmax{bn}"] = round(timeit(lambda: nat.mgemm_argmax(x, ws[next(it) % copies], N, bn),
-                                                      iters=4 * copies), 1)
+                try:
+                    if name == "gate_up":
+                        it = iter(range(1 << 30))
+                        row[f"glu{bn}"] = round(timeit(lambda: nat.mgemm_glu(x, ws[next(it) % copies], bn),
+                                                       iters=4 * copies), 1)
+                    if name == "lm_head":
+                        it = iter(range(1 << 30))
+                        row[f"argmax{bn}"] = round(timeit(lambda: nat.mgemm_argmax(x, ws[next(it) % copies], N, bn),
+                                                          iters=4 * copies), 1)
+                except RuntimeError as e:
+                    row[f"fused{bn}"] = str(e)[:60]
         row["hbm_TBs_at_hipblaslt"] = round(nb / row["hipblaslt_us"] / 1e6, 2)
         print(json.dumps(row), flush=True)
         res.append(row)

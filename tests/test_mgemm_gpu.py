@@ -28,7 +28,8 @@ def _close(a, b, atol, rtol=0.0):
                                       (4096, 14336, 8, 3), (1024, 1024, 1, 2), (1024, 1024, 2, 4),
                                       (512, 128, 1, 4), (768, 2048, 16, 1), (768, 3072, 4, 3),
                                       (6144, 4096, 8, 3), (512, 64, 1, 3), (6144, 4096, 8, 5), (4096, 14336, 14, 6),
-                                      (1024, 1024, 1, 5), (512, 128, 1, 6), (768, 1024, 2, 6)])
+                                      (1024, 1024, 1, 5), (512, 128, 1, 6), (768, 1024, 2, 6),
+                                      (4096, 4096, 4, 7), (4096, 14336, 7, 7), (6144, 4096, 2, 7), (64, 128, 1, 7)])
 def test_mgemm(native, M, N, K, S, bn):
     x = torch.randn(M, K, device="cuda", dtype=torch.bfloat16)
     w = (torch.randn(N, K, device="cuda") / K ** 0.5).bfloat16()
@@ -43,7 +44,7 @@ def test_mgemm(native, M, N, K, S, bn):
             _close(out.sum(0), ref, 2e-3, 1e-3)
 
 
-@pytest.mark.parametrize("bn", [1, 2, 3, 4, 5, 6])
+@pytest.mark.parametrize("bn", [1, 2, 3, 4, 5, 6, 7])
 def test_mgemm_asymmetric_identity(native, bn):
     """X = I rows against an asymmetric W: catches transposed / mis-placed tile writes."""
     M, N, K = 256, 512, 1024
@@ -92,6 +93,14 @@ def test_mgemm_argmax(native, M, bn):
     x2 = x.abs()
     got2 = torch.ops.docqa.mgemm_argmax(x2, w2, N - 128, bn)
     assert (got2 < N - 128).all()
+
+
+def test_mgemm_glu_rejects_narrow_tiles(native):
+    """cfg 7 (64-wide tiles) has no SwiGLU epilogue: refused, not silently wrong."""
+    x = torch.randn(256, 4096, device="cuda", dtype=torch.bfloat16)
+    w = torch.randn(1024, 4096, device="cuda", dtype=torch.bfloat16)
+    with pytest.raises(RuntimeError):
+        torch.ops.docqa.mgemm_glu(x, w, 7)
 
 
 def test_mgemm_argmax_ties(native):
