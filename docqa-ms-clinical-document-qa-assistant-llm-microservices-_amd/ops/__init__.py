@@ -231,6 +231,7 @@ MID_M_MIN, MID_M_MAX = 129, 512
 _MID_OFF = os.environ.get("DOCQA_MID_GEMM", "1") == "0"
 _MID_CFG = int(os.environ.get("DOCQA_MID_CFG", "2"))
 _MID_NARROW = os.environ.get("DOCQA_MID_NARROW", "1") == "1"
+_MID_WG_CAP = int(os.environ.get("DOCQA_MID_WG_CAP", "224"))
 
 
 def mid_plan(M: int, N: int, K: int) -> tuple[int, int]:
@@ -253,7 +254,7 @@ def mid_plan(M: int, N: int, K: int) -> tuple[int, int]:
         return 0, 0
     tiles = (N // 128) * ((M + 255) // 256)
     kb = K // 128
-    S = max(s for s in range(1, kb + 1) if kb % s == 0 and (s == 1 or tiles * s <= 224))
+    S = max(s for s in range(1, kb + 1) if kb % s == 0 and (s == 1 or tiles * s <= _MID_WG_CAP))
     if _MID_CFG == 2 and _MID_NARROW and S > 1 and tiles * S <= 128 and N % 64 == 0:
         # the split left half the chip idle (O: 32 tiles x S=4): 64-wide tiles (cfg 7) at
         # the same split fill it with the same slab bytes -- O 17.5 vs 20.7 us
