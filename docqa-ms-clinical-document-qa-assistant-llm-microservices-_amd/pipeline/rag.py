@@ -215,11 +215,13 @@ class RAGPipeline:
     def answer_pipelined(self, batches: list[list[str]], params: SamplingParams | None = None,
                          lead_steps: int | None = None):
         """Yield (answers, StageTimes, latency_s) per batch.  Batch i+1's embedding and
-        kNN search run on a side HIP stream and its prompt assembly on a helper thread,
-        released when batch i's decode is ``lead_steps`` steps from its end, so they
-        overlap the tail of batch i's generation (embed/search/generate overlap).
-        Latency is measured on the GPU clock from the moment batch i+1's embedding may
-        start to its answers being ready."""
+        kNN search run on a side HIP stream and its prompt assembly + KV reservation on a
+        helper thread, released when batch i's decode is ``lead_steps`` steps from its
+        end, so they overlap the tail of batch i's generation; batch i+1 is then launched
+        (prefill + decode graphs queued behind batch i) before batch i is collected and
+        detokenised on a second helper thread, so the GPU never waits on host work between
+        batches.  Latency is measured on the GPU clock from the moment batch i+1's
+        embedding may start to its answers being ready."""
         import concurrent.futures as cf
 
         params = params or SamplingParams(stop_on_eos=True)
@@ -248,7 +250,7 @@ class RAGPipeline:
             self.last_times = st
             with tracing.span("rag.detokenise", n=len(outs)):
                 res = [Answer(answer=self.chat_tok.decode(toks),
-                          sources=[self.metadata[j].get("source") for j in ids if 0 <= j < len(self.metadata)],
+                              sources=[self.metadata[j].get("source") for j in ids if 0 <= j < len(self.metadata)],
                               token_ids=toks) for ids, toks in zip(I, outs)]
             return res, st, latency
 
