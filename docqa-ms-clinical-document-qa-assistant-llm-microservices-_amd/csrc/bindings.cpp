@@ -110,6 +110,21 @@ void rope_cache(at::Tensor qkv, const at::Tensor& positions, const at::Tensor& c
                             T, Hq, Hkv, D, qkv.size(-1), BS, stream()), "rope_cache");
 }
 
+// token-granular prefix copies: K/V rows [0, m) of block src -> block dst in every pool
+// (caches: int64 [2 L] device addresses of the [num_blocks, Hkv, BS, D] bf16 pools,
+// tab: int32 [n, 3] (src, dst, m))
+void kv_copy_rows(const at::Tensor& caches, const at::Tensor& tab, int64_t num_blocks, int64_t Hkv, int64_t BS,
+                  int64_t D) {
+  CHECK_GPU(caches); CHECK_GPU(tab); CHECK_I32(tab); CHECK_CONTIG(tab); CHECK_CONTIG(caches);
+  TORCH_CHECK(caches.scalar_type() == at::kLong && caches.dim() == 1, "caches: int64 [2 L] addresses");
+  TORCH_CHECK(tab.dim() == 2 && tab.size(1) == 3, "tab: [n, 3] (src, dst, rows)");
+  c10::DeviceGuard g(tab.device());
+  CHECK_RC(docqa_kv_copy_rows(reinterpret_cast<const uint64_t*>(caches.data_ptr<int64_t>()), (int)caches.numel(),
+                              tab.data_ptr<int>(), (int)tab.size(0), (int)num_blocks, (int)Hkv, (int)BS, (int)D,
+                              stream()),
+           "kv_copy_rows");
+}
+
 // split-K partial slabs P [S, rows, H] fp32 -> residual += bf16(sum P); rmsnorm(residual) * w
 at::Tensor add_rmsnorm_splitk(const at::Tensor& P, at::Tensor residual, const at::Tensor& w, double eps) {
   CHECK_GPU(P); CHECK_CONTIG(P); CHECK_BF16(residual); CHECK_CONTIG(residual); CHECK_BF16(w);
@@ -842,6 +857,7 @@ TORCH_LIBRARY(docqa, m) {
   m.def("paged_decode_cascade_grouped(Tensor q, Tensor k_cache, Tensor v_cache, Tensor block_tables, "
         "Tensor context_lens, int Hq, float scale, Tensor prefix_table, Tensor prefix_len, int nchunk, "
         "Tensor groups) -> Tensor");
+  m.def("kv_copy_rows(Tensor caches, Tensor tab, int num_blocks, int Hkv, int BS, int D) -> ()");
   m.def("paged_decode_cascade_split(Tensor q, Tensor k_cache, Tensor v_cache, Tensor block_tables, "
         "Tensor context_lens, int Hq, float scale, Tensor prefix_table, Tensor prefix_len, int nchunk, "
         "Tensor plan) -> Tensor");
@@ -897,6 +913,7 @@ TORCH_LIBRARY_IMPL(docqa, CUDA, m) {
   m.impl("paged_decode_cascade_rope", &paged_decode_cascade_rope);
   m.impl("paged_decode_cascade_grouped", &paged_decode_cascade_grouped);
   m.impl("paged_decode_cascade_split", &paged_decode_cascade_split);
+  m.impl("kv_copy_rows", &kv_copy_rows);
   m.impl("ar_oneshot", &ar_oneshot);
   m.impl("add_rmsnorm_splitk", &add_rmsnorm_splitk);
   m.impl("rope_cache_splitk", &rope_cache_splitk);

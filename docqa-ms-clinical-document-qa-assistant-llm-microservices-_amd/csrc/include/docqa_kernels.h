@@ -13,6 +13,8 @@ int docqa_add_rmsnorm(const void* x, void* residual, const void* w, void* out, i
 int docqa_layernorm(const void* x, const void* residual, const void* g, const void* b, void* out,
                     int rows, int H, float eps, hipStream_t s);
 
+int docqa_kv_copy_rows(const uint64_t* caches, int ntensors, const int* tab, int n, int nblocks, int Hkv, int BS,
+                       int D, hipStream_t s);
 int docqa_rope_cache(void* qkv, const int* positions, const float* cos_sin,
                      const int* slot_mapping, void* k_cache, void* v_cache, int T, int Hq,
                      int Hkv, int D, int row_stride, int BS, hipStream_t s);

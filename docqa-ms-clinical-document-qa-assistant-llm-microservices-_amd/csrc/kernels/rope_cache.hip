@@ -182,3 +182,35 @@ int docqa_rope_cache_splitk(const float* P, int S, void* qkv_out, const int* pos
   DOCQA_CHECK_LAUNCH();
   return 0;
 }
+
+// Token-granular prefix reuse (engine/kv_cache.py TailCache): copy K/V rows [0, m) of a
+// source block into the same rows of a destination block, for every layer and both K and
+// V, in ONE launch (the per-layer tensor-indexing copies were 64 launches of ~40 us).
+// caches: [2 L] device pointers (k_0, v_0, k_1, v_1, ...) to [num_blocks, Hkv, BS, D]
+// pools; tab: [n, 3] int32 (src block, dst block, rows m).  Grid (n, 2 L): one workgroup
+// per (copy, tensor) moves m rows x Hkv heads, each row D bf16 contiguous, 16 B per lane.
+__global__ __launch_bounds__(256) void kv_copy_rows_kernel(const uint64_t* __restrict__ caches,
+                                                           const int* __restrict__ tab, int nblocks, int Hkv,
+                                                           int BS, int D) {
+  const int c = blockIdx.x;
+  uint16_t* base = reinterpret_cast<uint16_t*>(caches[blockIdx.y]);
+  const int src = tab[3 * c], dst = tab[3 * c + 1], m = tab[3 * c + 2];
+  if (src < 0 || src >= nblocks || dst < 0 || dst >= nblocks || m <= 0 || m > BS) return;
+  const int cpr = D / 8;                        // 16-B chunks per row
+  const int total = Hkv * m * cpr;
+  for (int i = threadIdx.x; i < total; i += blockDim.x) {
+    const int ch = i % cpr, r = (i / cpr) % m, h = i / (cpr * m);
+    const size_t so = (((size_t)src * Hkv + h) * BS + r) * D + ch * 8;
+    const size_t dso = (((size_t)dst * Hkv + h) * BS + r) * D + ch * 8;
+    *reinterpret_cast<uint4*>(base + dso) = *reinterpret_cast<const uint4*>(base + so);
+  }
+}
+
+int docqa_kv_copy_rows(const uint64_t* caches, int ntensors, const int* tab, int n, int nblocks, int Hkv, int BS,
+                       int D, hipStream_t s) {
+  if (n == 0 || ntensors == 0) return 0;
+  if (D % 8 != 0 || BS <= 0 || Hkv <= 0 || ntensors > 65535) return -1;
+  kv_copy_rows_kernel<<<dim3(n, ntensors), 256, 0, s>>>(caches, tab, nblocks, Hkv, BS, D);
+  DOCQA_CHECK_LAUNCH();
+  return 0;
+}

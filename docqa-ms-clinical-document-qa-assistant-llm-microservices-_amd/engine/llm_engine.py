@@ -553,19 +553,10 @@ class LLMEngine:
     def _copy_prefix_rows(self, copies: list) -> None:
         """K/V rows [0, m) of each source block -> the same rows of its destination block,
         every layer (token-granular prefix hits, queued before the prefill reads them)."""
-        # one [n, 3] (src, dst, rows) upload, expanded on the device (no host sync:
-        # output_size is known here)
-        tab = torch.tensor(copies, dtype=torch.long)
-        R = int(tab[:, 2].sum())
-        tab = tab.to(self.device, non_blocking=True)
-        m = tab[:, 2]
-        src = torch.repeat_interleave(tab[:, 0], m, output_size=R)
-        dst = torch.repeat_interleave(tab[:, 1], m, output_size=R)
-        start = torch.cumsum(m, 0) - m
-        rows = torch.arange(R, device=self.device) - torch.repeat_interleave(start, m, output_size=R)
-        for kc, vc in self.kv.caches:
-            kc[dst, :, rows] = kc[src, :, rows]
-            vc[dst, :, rows] = vc[src, :, rows]
+        if self.device.type == "cuda" and getattr(self, "_cache_ptrs", None) is None:
+            self._cache_ptrs = torch.tensor([t.data_ptr() for kv in self.kv.caches for t in kv],
+                                            dtype=torch.int64, device=self.device)
+        ops.kv_copy_rows(self.kv.caches, copies, getattr(self, "_cache_ptrs", None))
 
     def launch(self, prompts: list[list[int]], params: SamplingParams | None = None, on_step=None,
                reserved: "Reservation | None" = None) -> "Launched":

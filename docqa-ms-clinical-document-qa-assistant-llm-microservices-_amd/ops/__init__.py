@@ -512,6 +512,29 @@ def pack_decode_groups(tables: list[list[int]], lens: list[int], skip: int, bloc
     return quads
 
 
+def kv_copy_rows(pools: list, copies: list, ptrs: torch.Tensor | None = None) -> None:
+    """K/V rows [0, m) of block src -> the same rows of block dst in every paged pool
+    (``pools``: [(k, v)] per layer, [num_blocks, Hkv, BS, D]; ``copies``: [(src, dst, m)]).
+    GPU: one launch of csrc/kernels/rope_cache.hip kv_copy_rows over all pools (``ptrs``:
+    int64 device addresses of the pools in (k_0, v_0, k_1, ...) order, built by the
+    caller once); CPU: tensor indexing."""
+    if not copies:
+        return
+    k0 = pools[0][0]
+    if _gpu(k0):
+        if ptrs is None:
+            ptrs = torch.tensor([t.data_ptr() for kv in pools for t in kv], dtype=torch.int64, device=k0.device)
+        tab = torch.tensor(copies, dtype=torch.int32).pin_memory().to(k0.device, non_blocking=True)
+        _native().kv_copy_rows(ptrs, tab, k0.shape[0], k0.shape[1], k0.shape[2], k0.shape[3])
+        return
+    src = torch.tensor([s for s, _, m in copies for _ in range(m)], dtype=torch.long, device=k0.device)
+    dst = torch.tensor([d for _, d, m in copies for _ in range(m)], dtype=torch.long, device=k0.device)
+    rows = torch.tensor([i for _, _, m in copies for i in range(m)], dtype=torch.long, device=k0.device)
+    for kc, vc in pools:
+        kc[dst, :, rows] = kc[src, :, rows]
+        vc[dst, :, rows] = vc[src, :, rows]
+
+
 def group_tiles_by_position(tables: list[list[int]], lens: list[int], rows: list[int], skip: int,
                             block_size: int) -> list[tuple[int, int]]:
     """(block position, 32-token K/V tiles) the grouped decode kernel streams for ``rows``
