@@ -1207,9 +1207,18 @@ int docqa_paged_decode_cascade_split(const void* q, int q_stride, void* k_cache,
     if (rc) return rc;
   }
   const CascadeIn ci{pacc, pml, inline_prefix ? nullptr : plen, nchunk, nullptr};
-  paged_decode_group_kernel<3, true><<<dim3(Hkv, cap), 256, 0, s>>>(
-      (const uint16_t*)q, q_stride, (const uint16_t*)k_cache, (const uint16_t*)v_cache, block_tables, maxb,
-      context_lens, B, Hkv, scale, (uint16_t*)out, out_stride, items, ci, ws_acc, ws_ml);
+  static const int nsr = [] {   // ring slots (A/B knob): 3 (3 workgroups / CU) or 4 (2)
+    const char* e = getenv("DOCQA_GROUP_NSR");
+    return e && atoi(e) == 4 ? 4 : 3;
+  }();
+  if (nsr == 4)
+    paged_decode_group_kernel<4, true><<<dim3(Hkv, cap), 256, 0, s>>>(
+        (const uint16_t*)q, q_stride, (const uint16_t*)k_cache, (const uint16_t*)v_cache, block_tables, maxb,
+        context_lens, B, Hkv, scale, (uint16_t*)out, out_stride, items, ci, ws_acc, ws_ml);
+  else
+    paged_decode_group_kernel<3, true><<<dim3(Hkv, cap), 256, 0, s>>>(
+        (const uint16_t*)q, q_stride, (const uint16_t*)k_cache, (const uint16_t*)v_cache, block_tables, maxb,
+        context_lens, B, Hkv, scale, (uint16_t*)out, out_stride, items, ci, ws_acc, ws_ml);
   DOCQA_CHECK_LAUNCH();
   // merge rows: at most (cap + 1) / 2 (ops.split_decode_groups guarantees it), so half the
   // grid -- the empty workgroups of the unused merge rows are not free
