@@ -18,7 +18,6 @@ request in the reference (llm-qa/main.py:117, one request at a time, greedy at T
 from __future__ import annotations
 
 import json
-import math
 import itertools
 import os
 import time
