@@ -1117,26 +1117,49 @@ __global__ __launch_bounds__(256) void group_split_merge_kernel(const int* __res
     return;
   }
   const int nc = ci.plen ? cascade_parts(P, ci.nchunk) : 0;
-  float M = -FLT_MAX;
-  for (int p = 0; p < np; ++p) M = fmaxf(M, ws_ml[(((size_t)(first + p) * Hkv + kvh) * 16 + col) * 2]);
-  for (int c = 0; c < nc; ++c) M = fmaxf(M, ci.ml[(((size_t)c * B + row) * Hq + h) * 2]);
-  float num[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f}, den = 0.f;
-  auto fold = [&](float pm, float pl, const float* pa) {
-    const float w = pm == -FLT_MAX ? 0.f : exp2f(pm - M);
-    den += w * pl;
-    const float4 a0 = *reinterpret_cast<const float4*>(pa);
-    const float4 a1 = *reinterpret_cast<const float4*>(pa + 4);
-    num[0] += w * a0.x; num[1] += w * a0.y; num[2] += w * a0.z; num[3] += w * a0.w;
-    num[4] += w * a1.x; num[5] += w * a1.y; num[6] += w * a1.z; num[7] += w * a1.w;
-  };
-  for (int p = 0; p < np; ++p) {
-    const size_t ci2 = ((size_t)(first + p) * Hkv + kvh) * 16 + col;
-    const float2 ml = *reinterpret_cast<const float2*>(ws_ml + ci2 * 2);
-    fold(ml.x, ml.y, ws_acc + ci2 * D + d0);
-  }
-  for (int c = 0; c < nc; ++c) {
-    const size_t r = ((size_t)c * B + row) * Hq + h;
-    fold(ci.ml[r * 2], ci.ml[r * 2 + 1], ci.acc + r * D + d0);
+  // sources 0..np-1: this group's split items, np..np+nc-1: the prefix chunks.  Folded
+  // online in batches of 4 whose (m, l) and accumulator loads are all issued before the
+  // first use: one memory latency per 4 partials (a max pass followed by a fold pass with
+  // one source per iteration left every load exposed: ~2 latencies per partial)
+  const int ns = np + nc;
+  float M = -FLT_MAX, den = 0.f;
+  float num[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  for (int s0 = 0; s0 < ns; s0 += 4) {
+    float2 ml[4];
+    float4 a0[4], a1[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int s = min(s0 + j, ns - 1);
+      const float *pml, *pa;
+      if (s < np) {
+        const size_t c2 = ((size_t)(first + s) * Hkv + kvh) * 16 + col;
+        pml = ws_ml + c2 * 2;
+        pa = ws_acc + c2 * D + d0;
+      } else {
+        const size_t r = ((size_t)(s - np) * B + row) * Hq + h;
+        pml = ci.ml + r * 2;
+        pa = ci.acc + r * D + d0;
+      }
+      ml[j] = *reinterpret_cast<const float2*>(pml);
+      a0[j] = *reinterpret_cast<const float4*>(pa);
+      a1[j] = *reinterpret_cast<const float4*>(pa + 4);
+    }
+    float bm = M;
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+      if (s0 + j < ns) bm = fmaxf(bm, ml[j].x);
+    const float f = M == -FLT_MAX ? 0.f : exp2f(M - bm);   // rescale what is folded so far
+    den *= f;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) num[e] *= f;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const float w = (s0 + j >= ns || ml[j].x == -FLT_MAX) ? 0.f : exp2f(ml[j].x - bm);
+      den += w * ml[j].y;
+      num[0] += w * a0[j].x; num[1] += w * a0[j].y; num[2] += w * a0[j].z; num[3] += w * a0[j].w;
+      num[4] += w * a1[j].x; num[5] += w * a1[j].y; num[6] += w * a1[j].z; num[7] += w * a1[j].w;
+    }
+    M = bm;
   }
   const float inv = den > 0.f ? 1.f / den : 0.f;
 #pragma unroll

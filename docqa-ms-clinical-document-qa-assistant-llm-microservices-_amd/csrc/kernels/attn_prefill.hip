@@ -295,19 +295,31 @@ __global__ __launch_bounds__(64 * G * WPH) void flash_prefill_kernel(
   }
 
   if constexpr (PFX) {   // chunk partial: un-normalised O and (max, sum) per (row, head)
-    if (my_q < L) {
-      const size_t r = ((size_t)b * L + my_q) * Hq + h;
-      float* ap = co.acc + r * D;
+    // O^T is lane = query row, registers = dims: stored straight, every 16-B store lands in
+    // a different row (32 partial 128-B lines per instruction).  Transpose each 32-dim
+    // slice through a per-wave LDS scratch instead (the K/V tiles are dead after the
+    // loop's last barrier: 8 waves x 32 rows x 128 B fill the 32 KB; 16-B chunk c of row r
+    // sits at chunk c ^ (r & 7), so the 8 rows of a store group hit distinct banks) and 8
+    // lanes write one row's whole 128-B line.
+    static_assert(G * WPH * 32 * 32 * 4 <= 2 * KB * D * 2, "PFX scratch");
+    float* scr = reinterpret_cast<float*>(smem) + wave * 32 * 32;
+    const int rr = lane >> 3, ch = lane & 7;
+    float* ap = co.acc + ((size_t)b * L * Hq + h) * D;
 #pragma unroll
-      for (int dt = 0; dt < NDT; ++dt)
+    for (int dt = 0; dt < NDT; ++dt) {
 #pragma unroll
-        for (int g4 = 0; g4 < 4; ++g4) {
-          const int d0 = dt * 32 + 8 * g4 + 4 * hh;
-          *reinterpret_cast<float4*>(ap + d0) =
-              make_float4(o[dt][4 * g4 + 0], o[dt][4 * g4 + 1], o[dt][4 * g4 + 2], o[dt][4 * g4 + 3]);
-        }
-      if (hh == 0) *reinterpret_cast<float2*>(co.ml + r * 2) = make_float2(m_run, l_run);
+      for (int g4 = 0; g4 < 4; ++g4)
+        *reinterpret_cast<float4*>(scr + l32 * 32 + (((2 * g4 + hh) ^ (l32 & 7)) << 2)) =
+            make_float4(o[dt][4 * g4 + 0], o[dt][4 * g4 + 1], o[dt][4 * g4 + 2], o[dt][4 * g4 + 3]);
+#pragma unroll
+      for (int it = 0; it < 4; ++it) {
+        const int q = q_wave + it * 8 + rr;
+        const float4 v = *reinterpret_cast<const float4*>(scr + (it * 8 + rr) * 32 + ((ch ^ rr) << 2));
+        if (q < L) *reinterpret_cast<float4*>(ap + (size_t)q * Hq * D + dt * 32 + ch * 4) = v;
+      }
     }
+    if (my_q < L && hh == 0)
+      *reinterpret_cast<float2*>(co.ml + (((size_t)b * L + my_q) * Hq + h) * 2) = make_float2(m_run, l_run);
     return;
   }
   // ---- epilogue: O[q][dim] = O^T[dim][q] / l
