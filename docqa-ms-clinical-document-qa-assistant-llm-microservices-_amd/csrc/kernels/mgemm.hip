@@ -403,6 +403,11 @@ struct Cfg { int bn, bks; };
 // latency, sets the stage time; profiles/r2_mgemm_probe_dq_rings.log.)
 //   7: BN  64, 64-deep stages x 3, waves 4 x 2 ( 64 x 32 each, 2 waves / SIMD): twice the
 //      workgroups of cfg 2 for the narrow projections that otherwise fill half the chip
+// (Half-depth stages -- BN 128, 32-deep x 6 slots, the same 144 KB ring with 5 stages in
+// flight instead of 2 -- measured 1.3-1.6x SLOWER on every projection (QKV S=4 30.2 vs
+// 22.6 us, gate|up+SwiGLU 114.5 vs 81.1) and 23 % slower end to end: the stage time is a
+// fixed ~1000-cycle cost plus the LDS-DMA bytes, not the bytes in flight over the HBM
+// latency; profiles/r2_mgemm_probe_bks32_ring6.log, profiles/r2_ab_mid_cfg8_bks32.log.)
 constexpr int kNumCfg = 7;
 constexpr Cfg kCfg[kNumCfg + 1] = {{0, 0}, {128, 64}, {128, 64}, {256, 32}, {256, 32}, {256, 64}, {256, 64},
                                    {64, 64}};
