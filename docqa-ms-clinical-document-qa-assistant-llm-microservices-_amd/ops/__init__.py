@@ -474,7 +474,16 @@ def pack_decode_groups(tables: list[list[int]], lens: list[int], skip: int, bloc
     n = len(tables)
     if n == 0:
         return []
-    idx = sorted(range(n), key=lambda i: tables[i][skip:])
+    # sort key: block ids relabelled by first occurrence (row-major), so the packing -- and
+    # with it each row's split points and partial-merge order -- depends only on which rows
+    # share blocks, never on the physical ids the allocator handed out (a pipelined run
+    # frees batch i-1 and reserves batch i+1 on two threads in a timing-dependent order)
+    label: dict[int, int] = {}
+    for t in tables:
+        for b in t[skip:]:
+            label.setdefault(b, len(label))
+    keyed = [[label[b] for b in t[skip:]] for t in tables]
+    idx = sorted(range(n), key=lambda i: keyed[i])
 
     def first(i):
         return tables[i][skip] if len(tables[i]) > skip else -1 - i

@@ -255,6 +255,31 @@ def test_pack_decode_groups_covers_rows_and_keeps_clusters():
     assert sorted(r for q in quads for r in q) == list(range(len(tables)))
 
 
+@pytest.mark.parametrize("seed", [0, 1, 2])
+def test_pack_decode_groups_ignores_physical_block_ids(seed):
+    """The packing (and so the split plan and every row's partial-merge order) depends only
+    on which rows share blocks: renaming the physical blocks -- as a pipelined run's
+    timing-dependent free / reserve order does -- yields the same groups and plan."""
+    import random
+
+    from docqa_amd import ops
+
+    skip = 2
+    tables = [[0, 1, 10, 11, 50, 70], [0, 1, 10, 11, 51, 71], [0, 1, 20, 52, 53, 72], [0, 1, 10, 12, 54, 73],
+              [0, 1, 30, 55, 56, 74], [0, 1, 20, 57, 58, 75], [0, 1, 60, 61, 62, 76], [0, 1, 30, 77, 78, 79]]
+    lens = [330, 300, 370, 250, 384, 200, 310, 290]
+    ids = sorted({b for t in tables for b in t})
+    perm = dict(zip(ids, random.Random(seed).sample(range(1000, 2000), len(ids))))
+    renamed = [[perm[b] for b in t] for t in tables]
+    for cap in (2, 4):
+        q1 = ops.pack_decode_groups(tables, lens, skip, 64, cap)
+        q2 = ops.pack_decode_groups(renamed, lens, skip, 64, cap)
+        assert q1 == q2
+        p1 = ops.split_decode_groups(q1, tables, lens, skip, 64, cap=16, tiles_per_item=3)
+        p2 = ops.split_decode_groups(q2, renamed, lens, skip, 64, cap=16, tiles_per_item=3)
+        assert torch.equal(p1, p2)
+
+
 @pytest.mark.parametrize("tiles", [1, 2, 5, 100])
 def test_split_decode_groups_plan(tiles):
     """Split plan: each group's block positions past the prefix are covered by its items
