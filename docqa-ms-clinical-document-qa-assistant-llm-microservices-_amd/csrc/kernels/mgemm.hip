@@ -408,6 +408,9 @@ struct Cfg { int bn, bks; };
 // 22.6 us, gate|up+SwiGLU 114.5 vs 81.1) and 23 % slower end to end: the stage time is a
 // fixed ~1000-cycle cost plus the LDS-DMA bytes, not the bytes in flight over the HBM
 // latency; profiles/r2_mgemm_probe_bks32_ring6.log, profiles/r2_ab_mid_cfg8_bks32.log.)
+// (Raising the wave priority over each stage's MFMA burst (s_setprio 1 / 0 around mma):
+// 3-7 % slower per projection, 1.3 % slower end to end; profiles/r2_mgemm_probe_setprio.log,
+// profiles/r2_ab_mid_setprio.log.)
 constexpr int kNumCfg = 7;
 constexpr Cfg kCfg[kNumCfg + 1] = {{0, 0}, {128, 64}, {128, 64}, {256, 32}, {256, 32}, {256, 64}, {256, 64},
                                    {64, 64}};
