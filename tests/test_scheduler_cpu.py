@@ -96,3 +96,50 @@ def test_serving_thread_resolves_concurrent_futures():
         assert sorted(res) == list(range(6)) and all(len(res[i]) == 4 + i for i in range(6))
     finally:
         ce.stop()
+
+
+def test_admission_waits_for_a_group_when_slots_trickle_free(monkeypatch):
+    """Under overload the queue is long but slots free up one at a time: admission waits
+    until admit_min requests can join (waiting AND free) or admit_wait_s has passed since
+    the first one could, instead of a near-empty prefill pass per freed slot."""
+    import collections
+    import types
+
+    from docqa_amd.engine import scheduler as sch
+
+    eng = LLMEngine(_model(), max_batch=16, max_context=512, block_size=16, use_graphs=False)
+    ce = ContinuousEngine(eng)
+    assert ce.admit_min == 2
+    calls = []
+    monkeypatch.setattr(ce, "_take_waiting", lambda: calls.append(len(ce.waiting)) or [])
+    clock = [100.0]
+    monkeypatch.setattr(sch.time, "perf_counter", lambda: clock[0])
+    ce.waiting = collections.deque(types.SimpleNamespace(t_arrival=50.0) for _ in range(40))
+    ce.running = [object()] * 16                      # full: nothing can join
+    ce._admit()
+    assert calls == []
+    ce.running = [object()] * 15                      # one slot frees: 1 < admit_min, wait
+    ce._admit()
+    clock[0] += 0.01
+    ce._admit()
+    assert calls == []
+    ce.running = [object()] * 14                      # a second slot: a group of 2 can join
+    ce._admit()
+    assert calls == [40]
+    ce.running = [object()] * 16
+    ce._admit()                                       # full again: the timer resets
+    ce.running = [object()] * 15
+    clock[0] += 0.01
+    ce._admit()
+    assert calls == [40]
+    clock[0] += ce.admit_wait_s                       # the lone slot has waited long enough
+    ce._admit()
+    assert calls == [40, 40]
+    # light load: a single new arrival with free slots waits admit_wait_s from its arrival
+    ce.running = [object()] * 4
+    ce.waiting = collections.deque([types.SimpleNamespace(t_arrival=clock[0])])
+    ce._admit()
+    assert calls == [40, 40]
+    clock[0] += ce.admit_wait_s
+    ce._admit()
+    assert calls == [40, 40, 1]
