@@ -34,6 +34,7 @@ from __future__ import annotations
 import collections
 import concurrent.futures as cf
 import itertools
+import os
 import threading
 import time
 from dataclasses import dataclass, field
@@ -79,8 +80,8 @@ class ContinuousEngine:
         # decode over power-of-two slot buckets (padded slots: valid 0); on by default with
         # graphs, settable on CPU to exercise the padded-slot paths of the reference ops
         self.pad_buckets = engine.use_graphs
-        self.admit_min = max(1, self.max_running // 8)
-        self.admit_wait_s = 0.04
+        self.admit_min = max(1, self.max_running // int(os.environ.get("DOCQA_ADMIT_DIV", "8")))
+        self.admit_wait_s = float(os.environ.get("DOCQA_ADMIT_WAIT_MS", "40")) / 1e3
         self._free_t = None                # when a slot last became free with the batch full before
         self._pool = None
         self._pending = None               # (event, pinned host tokens, slot -> request) of the last step
