@@ -80,8 +80,8 @@ class ContinuousEngine:
         # decode over power-of-two slot buckets (padded slots: valid 0); on by default with
         # graphs, settable on CPU to exercise the padded-slot paths of the reference ops
         self.pad_buckets = engine.use_graphs
-        self.admit_min = max(1, self.max_running // int(os.environ.get("DOCQA_ADMIT_DIV", "8")))
-        self.admit_wait_s = float(os.environ.get("DOCQA_ADMIT_WAIT_MS", "40")) / 1e3
+        self.admit_min = max(1, self.max_running // int(os.environ.get("DOCQA_ADMIT_DIV", "4")))
+        self.admit_wait_s = float(os.environ.get("DOCQA_ADMIT_WAIT_MS", "160")) / 1e3
         self._free_t = None                # when a slot last became free with the batch full before
         self._pool = None
         self._pending = None               # (event, pinned host tokens, slot -> request) of the last step

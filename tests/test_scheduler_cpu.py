@@ -109,7 +109,7 @@ def test_admission_waits_for_a_group_when_slots_trickle_free(monkeypatch):
 
     eng = LLMEngine(_model(), max_batch=16, max_context=512, block_size=16, use_graphs=False)
     ce = ContinuousEngine(eng)
-    assert ce.admit_min == 2
+    ce.admit_min, ce.admit_wait_s = 2, 0.04
     calls = []
     monkeypatch.setattr(ce, "_take_waiting", lambda: calls.append(len(ce.waiting)) or [])
     clock = [100.0]
