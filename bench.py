@@ -29,6 +29,9 @@ ROOT = Path(__file__).resolve().parent
 REF_EQUIV_QPS = 0.6149
 sys.path.insert(0, str(ROOT))
 os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+# kernel arguments in device memory: +0.3-0.5 % on the decode loop's ~330 launches per step
+# (profiles/r2_ab_dev_kernarg.log); read by the HIP runtime at init, so set before torch
+os.environ.setdefault("HIP_FORCE_DEV_KERNARG", "1")
 
 
 def main() -> None:
