@@ -52,7 +52,14 @@ def main() -> None:
     ap.add_argument("--max-context", type=int, default=2048)
     ap.add_argument("--no-graphs", action="store_true")
     ap.add_argument("--device", default="cuda", help="cuda (MI355X) | cpu (CI rehearsal of the DP path with gloo)")
+    ap.add_argument("--questions", choices=("unique", "repeat"), default="unique",
+                    help="unique: every request a distinct question (default); repeat: the ~470-string "
+                         "template grid of rounds 1-2 (cache-hot ceiling)")
+    ap.add_argument("--template", choices=("cache_friendly", "reference"), default=None,
+                    help="QA prompt template (docqa_amd/prompts.py; default: env QA_TEMPLATE or cache_friendly)")
     a = ap.parse_args()
+    if a.template:
+        os.environ["QA_TEMPLATE"] = a.template
 
     import torch
     import torch.distributed as dist
@@ -61,7 +68,7 @@ def main() -> None:
     from docqa_amd.engine.llm_engine import SamplingParams
     from docqa_amd.parallel import comm
     from docqa_amd.pipeline.builder import StackConfig, build_stack
-    from docqa_amd.text.synthetic import synthetic_questions
+    from docqa_amd.text.synthetic import synthetic_questions, synthetic_unique_questions
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     if world != a.gpus:
@@ -88,7 +95,8 @@ def main() -> None:
 
     # distinct questions per (step, dp rank); identical within a TP group
     total_steps = a.warmup + a.steps
-    qs = synthetic_questions(total_steps * ps.dp_size * a.batch, seed=123)
+    gen_q = synthetic_unique_questions if a.questions == "unique" else synthetic_questions
+    qs = gen_q(total_steps * ps.dp_size * a.batch, seed=123)
 
     def batch_for(step: int) -> list[str]:
         base = (step * ps.dp_size + ps.dp_rank) * a.batch
@@ -109,10 +117,12 @@ def main() -> None:
     eng = pipe.engine
     s0 = (eng.stats.prefill_s, eng.stats.decode_s, eng.stats.prompt_tokens, eng.stats.cached_tokens)
     t0 = time.perf_counter()
-    step_times, stages = [], []
+    step_times, stages, chunks = [], [], set()
     for ans, st, lat in pipe.answer_pipelined([batch_for(a.warmup + s) for s in range(a.steps)], params):
         step_times.append(lat)   # per-batch answer latency: prepare start -> answers ready
         stages.append(st)
+        for x in ans:
+            chunks.update(x.chunk_ids)
     sync()
     comm.barrier()
     sync()
@@ -126,6 +136,14 @@ def main() -> None:
     queries = ps.dp_size * a.batch * a.steps
     qps = queries / elapsed_max
     s1 = (eng.stats.prefill_s, eng.stats.decode_s, eng.stats.prompt_tokens, eng.stats.cached_tokens)
+    # workload descriptors over the whole job's timed questions (every DP rank's batches)
+    timed_q = [q for s_ in range(a.steps) for d in range(ps.dp_size)
+               for q in qs[((a.warmup + s_) * ps.dp_size + d) * a.batch:((a.warmup + s_) * ps.dp_size + d + 1) * a.batch]]
+    seen_before = set(qs[:a.warmup * ps.dp_size * a.batch])
+    repeats = 0
+    for q in timed_q:
+        repeats += q in seen_before
+        seen_before.add(q)
     if ps.rank == 0:
         st = {k: round(1e3 * statistics.mean(getattr(x, k) for x in stages), 2)
               for k in ("embed_s", "search_s", "prompt_s", "generate_s")}
@@ -157,6 +175,13 @@ def main() -> None:
             "engine_ms_per_batch": {"prefill": round(1e3 * (s1[0] - s0[0]) / a.steps, 2),
                                     "decode": round(1e3 * (s1[1] - s0[1]) / a.steps, 2)},
             "prefix_cached_frac": round((s1[3] - s0[3]) / max(1, s1[2] - s0[2]), 3),
+            "workload": {
+                "questions": a.questions,
+                "template": os.environ.get("QA_TEMPLATE", "cache_friendly"),
+                "unique_question_frac": round(len(set(timed_q)) / max(1, len(timed_q)), 4),
+                "repeat_of_earlier_frac": round(repeats / max(1, len(timed_q)), 4),
+                "distinct_chunks_rank0": len(chunks),
+            },
         }
         print(json.dumps(out), flush=True)
     comm.destroy()

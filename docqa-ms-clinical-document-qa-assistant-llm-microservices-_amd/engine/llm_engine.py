@@ -486,8 +486,12 @@ class LLMEngine:
         need = [self.kv.blocks_for(n + params.max_new_tokens) for n in lens]
         r = Reservation([], [], params.max_new_tokens, len(prompts))
         if not self._use_pc:
-            for n in need:
-                r.tables.append(self._retry(lambda n=n: alloc.alloc(n)))
+            try:
+                for n in need:
+                    r.tables.append(self._retry(lambda n=n: alloc.alloc(n)))
+            except BaseException:
+                self.release(r)   # no partial reservation may outlive a failed one
+                raise
             r.cached = [0] * len(prompts)
             return r
         # one native call for the batch: longest cached full-block prefix of every prompt

@@ -109,7 +109,15 @@ class FlatIndex:
             xq = xq[None]
         xq = xq.to(self.device, dtype=torch.float32)
         with self._lock:
-            return ops.knn(self.xb, self.norms, xq, k, self.metric == "ip", id_offset)
+            xb, nm = self._xb, self._norms
+            if xb.is_cuda:
+                # the kernel may run on a side stream (the RAG prep stream) while a
+                # concurrent replace()/_grow() drops these buffers: keep the caching
+                # allocator from handing them out until this stream's work is done
+                s = torch.cuda.current_stream(self.device)
+                xb.record_stream(s)
+                nm.record_stream(s)
+            return ops.knn(xb[: self.ntotal], nm[: self.ntotal], xq, k, self.metric == "ip", id_offset)
 
     def reconstruct(self, i: int) -> np.ndarray:
         return self._xb[i].float().cpu().numpy()

@@ -256,7 +256,7 @@ class LlamaModel:
                 else:
                     S, t = ops.decode_plan(M, *L0[k].shape)
                     plans[k] = (S, lambda a, w, S=S, t=t: ops.dgemm_partial(a, w, S, t))
-            Sg, cg = ops.mid_plan(M, *L0["gate_up"].shape)
+            Sg, cg = ops.mid_plan(M, *L0["gate_up"].shape, glu=True)
             glu = (lambda a, w: ops.mgemm_glu(a, w, cg)) if Sg else ops.glu_linear
         else:
             glu = ops.glu_linear

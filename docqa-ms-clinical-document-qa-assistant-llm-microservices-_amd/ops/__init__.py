@@ -234,9 +234,11 @@ _MID_NARROW = os.environ.get("DOCQA_MID_NARROW", "1") == "1"
 _MID_WG_CAP = int(os.environ.get("DOCQA_MID_WG_CAP", "224"))
 
 
-def mid_plan(M: int, N: int, K: int) -> tuple[int, int]:
+def mid_plan(M: int, N: int, K: int, glu: bool = False) -> tuple[int, int]:
     """(split-K count, kernel variant) of the mid-M decode GEMM (csrc/kernels/mgemm.hip) for
     an [M, K] x [N, K]^T projection at 129..512 rows; (0, 0) where it does not apply.
+    ``glu``: the plan is for the fused-SwiGLU gate|up launch (mgemm_glu), which never
+    splits K and has no 64-wide (cfg 7) variant -- only a non-zero S means "use it".
 
     Every workgroup owns all 256 rows of an m-tile x 128 weight rows; S is the largest
     divisor of K / 128 keeping (N / 128) x m-tiles x S <= 224 workgroups (one round on the
@@ -255,6 +257,8 @@ def mid_plan(M: int, N: int, K: int) -> tuple[int, int]:
     tiles = (N // 128) * ((M + 255) // 256)
     kb = K // 128
     S = max(s for s in range(1, kb + 1) if kb % s == 0 and (s == 1 or tiles * s <= _MID_WG_CAP))
+    if glu:
+        return S, _MID_CFG
     if _MID_CFG == 2 and _MID_NARROW and S > 1 and tiles * S <= 128 and N % 64 == 0:
         # the split left half the chip idle (O: 32 tiles x S=4): 64-wide tiles (cfg 7) at
         # the same split fill it with the same slab bytes -- O 17.5 vs 20.7 us

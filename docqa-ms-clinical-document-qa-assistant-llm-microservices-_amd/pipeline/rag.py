@@ -21,32 +21,11 @@ import torch
 
 from ..utils import tracing
 from ..engine.llm_engine import LLMEngine, SamplingParams
+from ..prompts import CACHE_FRIENDLY_QA_TEMPLATE, qa_template
 
-# Expert-assistant prompt with the same slots as the reference's QA_CHAIN_PROMPT
-# (instructions, context block, practitioner question).  All fixed text comes FIRST so
-# every request shares a long token prefix: the engine's prefix cache then serves those
-# KV blocks from HBM instead of recomputing them (the reference puts the context in the
-# middle, which would make every prompt unique after ~30 tokens).
-DEFAULT_TEMPLATE = """Vous êtes un expert en pharmacopée chinoise (MTC) assistant un praticien.
-Vous recevez des extraits de la base de connaissances et des dossiers patients ; chaque
-plante y est accompagnée d'un score de pertinence.
-
-CONSIGNES :
-1. Repérez le syndrome du patient dans les extraits.
-2. Relevez les plantes associées à ce syndrome.
-3. Ordonnez-les par score de pertinence décroissant (10 = plante Empereur, 7 = plante Ministre).
-4. Répondez par une liste numérotée en justifiant chaque plante par son score et son rôle,
-   par exemple : "1. [Plante] (score 10, Empereur) : recommandée parce que ...".
-5. N'utilisez que les informations des extraits ; si elles sont insuffisantes, dites-le.
-
-EXTRAITS (base MTC et dossier patient) :
-{context}
-
-QUESTION DU PRATICIEN :
-{question}
-
-RÉPONSE DE L'EXPERT :
-"""
+# QA prompt: the cache-friendly reordering of the reference's QA_CHAIN_PROMPT by default,
+# the verbatim reference text with QA_TEMPLATE=reference (docqa_amd/prompts.py)
+DEFAULT_TEMPLATE = CACHE_FRIENDLY_QA_TEMPLATE
 
 
 @dataclass
@@ -65,12 +44,14 @@ class Answer:
     answer: str
     sources: list
     token_ids: list = field(default_factory=list)
+    chunk_ids: list = field(default_factory=list)   # index rows retrieved for the prompt
 
 
 class RAGPipeline:
     def __init__(self, encoder, enc_tokenizer, index, metadata: list[dict], engine: LLMEngine,
-                 chat_tokenizer, k: int = 3, template: str = DEFAULT_TEMPLATE,
+                 chat_tokenizer, k: int = 3, template: str | None = None,
                  max_prompt_tokens: int | None = None):
+        template = template if template is not None else qa_template()
         self.encoder = encoder
         self.enc_tok = enc_tokenizer
         self.index = index
@@ -173,7 +154,8 @@ class RAGPipeline:
         res = []
         for ids, toks in zip(I, outs):
             srcs = [self.metadata[i].get("source") for i in ids if 0 <= i < len(self.metadata)]
-            res.append(Answer(answer=self.chat_tok.decode(toks), sources=srcs, token_ids=toks))
+            res.append(Answer(answer=self.chat_tok.decode(toks), sources=srcs, token_ids=toks,
+                              chunk_ids=list(ids)))
         return res
 
     def answer(self, question: str, params: SamplingParams | None = None) -> Answer:
@@ -186,30 +168,41 @@ class RAGPipeline:
         generation is ``lead_steps`` from its end), then host-side prompt assembly and
         (``params`` given) the batch's KV-block reservation."""
         t0 = time.perf_counter()
-        ev_start = None
+        evs = None
         sp = tracing.span("rag.prepare", n=len(questions))
         sp.__enter__()
         if stream is not None:
             with torch.cuda.stream(stream):
                 if gate is not None:
                     stream.wait_event(gate)
-                ev_start = torch.cuda.Event(enable_timing=True)
-                ev_start.record(stream)
+                # GPU-clock stage times: embed = [e0, e1), kNN search = [e1, e2)
+                evs = tuple(torch.cuda.Event(enable_timing=True) for _ in range(3))
+                evs[0].record(stream)
                 qemb = self.embed(questions)
+                evs[1].record(stream)
                 _, I = self.index.search(qemb, self.k)
+                evs[2].record(stream)
                 I = I.tolist()       # waits for this side stream only
+            host = None
         else:
             qemb = self.embed(questions)
+            tm = time.perf_counter()
             _, I = self.index.search(qemb, self.k)
             I = I.tolist()
+            host = (tm - t0, time.perf_counter() - tm)
         t1 = time.perf_counter()
         with tracing.span("rag.prompts", n=len(questions)):
             prompts = self.build_prompts(questions, I)
         reserved = None
         if params is not None and len(prompts) <= self.engine.max_batch:
-            reserved = self.engine.reserve(prompts, params)
+            try:
+                reserved = self.engine.reserve(prompts, params)
+            except MemoryError:
+                # the batches still in flight hold the pool: the main loop collects them
+                # first and reserves this batch itself (reserved=None)
+                reserved = None
         sp.__exit__(None, None, None)
-        return questions, I, prompts, reserved, ev_start, t0, t1, time.perf_counter()
+        return questions, I, prompts, reserved, (evs, host), t0, t1, time.perf_counter()
 
     @torch.inference_mode()
     def answer_pipelined(self, batches: list[list[str]], params: SamplingParams | None = None,
@@ -235,23 +228,31 @@ class RAGPipeline:
         eng = self.engine
         cuda = eng.device.type == "cuda"
         stream = torch.cuda.Stream() if cuda else None
-        pending = None   # (Launched, questions, I, ev_start, t0, t1, t2, t3) of the batch in flight
+        pending = None   # (Launched, questions, I, stage timers, t0, t1, t2, t3) of the batch in flight
+
+        def stage_times(tm, t0, t1, t2, gen_s):
+            evs, host = tm
+            if evs is not None:
+                emb, srch = evs[0].elapsed_time(evs[1]) / 1e3, evs[1].elapsed_time(evs[2]) / 1e3
+            else:
+                emb, srch = host if host is not None else (t1 - t0, 0.0)
+            return StageTimes(embed_s=emb, search_s=srch, prompt_s=t2 - t1, generate_s=gen_s)
 
         def finish(p):
-            h, questions, I, ev_start, t0, t1, t2, t3 = p
+            h, questions, I, tm, t0, t1, t2, t3 = p
             outs = eng.collect(h)
             t4 = time.perf_counter()
             if cuda:
-                latency = ev_start.elapsed_time(h.done_event) / 1e3
+                latency = tm[0][0].elapsed_time(h.done_event) / 1e3
                 gen_s = h.start_event.elapsed_time(h.done_event) / 1e3
             else:
                 latency, gen_s = t4 - t0, t4 - t3
-            st = StageTimes(embed_s=t1 - t0, search_s=0.0, prompt_s=t2 - t1, generate_s=gen_s)
+            st = stage_times(tm, t0, t1, t2, gen_s)
             self.last_times = st
             with tracing.span("rag.detokenise", n=len(outs)):
                 res = [Answer(answer=self.chat_tok.decode(toks),
                               sources=[self.metadata[j].get("source") for j in ids if 0 <= j < len(self.metadata)],
-                              token_ids=toks) for ids, toks in zip(I, outs)]
+                              token_ids=toks, chunk_ids=list(ids)) for ids, toks in zip(I, outs)]
             return res, st, latency
 
         # batch i-1 is collected and detokenised on a helper thread as soon as batch i's
@@ -264,7 +265,7 @@ class RAGPipeline:
             fin = None
             try:
                 for i in range(len(batches)):
-                    questions, I, prompts, reserved, ev_start, t0, t1, t2 = fut.result()
+                    questions, I, prompts, reserved, tm, t0, t1, t2 = fut.result()
                     fut = None
                     nxt = batches[i + 1] if i + 1 < len(batches) else None
 
@@ -280,6 +281,11 @@ class RAGPipeline:
                                 gate.record()
                             fut = ex.submit(self._prepare, nxt, stream, gate, params)
 
+                    if reserved is None and pending is not None and len(prompts) <= eng.max_batch:
+                        # no KV reservation (pool held by the batch in flight): collect that
+                        # batch first so launch() can reserve this one
+                        p, pending = pending, None
+                        yield finish(p)
                     t3 = time.perf_counter()
                     if len(prompts) <= eng.max_batch:
                         h = eng.launch(prompts, params, on_step=on_step, reserved=reserved)
@@ -295,14 +301,15 @@ class RAGPipeline:
                         f, fin = fin, None
                         yield f.result()
                     if h is not None:
-                        pending = (h, questions, I, ev_start, t0, t1, t2, t3)
+                        pending = (h, questions, I, tm, t0, t1, t2, t3)
                     else:
                         t4 = time.perf_counter()
-                        st = StageTimes(embed_s=t1 - t0, search_s=0.0, prompt_s=t2 - t1, generate_s=t4 - t3)
+                        st = stage_times(tm, t0, t1, t2, t4 - t3)
                         self.last_times = st
                         yield ([Answer(answer=self.chat_tok.decode(toks),
                                        sources=[self.metadata[j].get("source") for j in ids
-                                                if 0 <= j < len(self.metadata)], token_ids=toks)
+                                                if 0 <= j < len(self.metadata)], token_ids=toks,
+                                       chunk_ids=list(ids))
                                 for ids, toks in zip(I, outs)], st, t4 - t0)
                 if pending is not None:
                     p, pending = pending, None

@@ -9,6 +9,9 @@ import torch
 
 from . import ops
 
+# the block manager's pool-exhaustion message (csrc/runtime/block_manager_core.h)
+_EXHAUSTED = "KV cache exhausted"
+
 
 class NativeBlockAllocator:
     """Python-facing wrapper with the :class:`engine.kv_cache.PyBlockAllocator` API."""
@@ -25,7 +28,9 @@ class NativeBlockAllocator:
         try:
             return list(self._m.alloc(n))
         except RuntimeError as e:
-            raise MemoryError(str(e)) from e
+            if _EXHAUSTED in str(e):
+                raise MemoryError(str(e)) from e
+            raise
 
     def share(self, blocks: list[int]) -> None:
         self._m.share(list(blocks))
@@ -46,7 +51,11 @@ class NativeBlockAllocator:
         try:
             out = self._m.match_alloc_batch(flat, [len(ks) for ks in keys], list(lens), list(need))
         except RuntimeError as e:
-            raise MemoryError(str(e)) from e
+            # only pool exhaustion is transient; invariant violations (bad sizes, ids out of
+            # range, double free) must surface as the corruption they are
+            if _EXHAUSTED in str(e):
+                raise MemoryError(str(e)) from e
+            raise
         B = len(keys)
         hits, tables, o = list(out[:B]), [], B
         for n in need:

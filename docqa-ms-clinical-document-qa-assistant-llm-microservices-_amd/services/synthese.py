@@ -29,46 +29,8 @@ from ..config import Settings
 from ..schemas import (ComparisonRow, MultiPatientComparisonResponse, PatientComparisonRequest,
                        PatientSummaryRequest, Section, SinglePatientSummaryResponse, SourceSnippet)
 
-SINGLE_PATIENT_TEMPLATE = """
-You are a clinical assistant. Write a structured summary of the clinical history of ONE
-anonymised patient.
-
-Context:
-- Patient alias: {patient_alias}
-- Time window: {from_date} to {to_date}
-- Clinical focus: {focus}
-
-Clinical notes:
-{documents}
-
-Task: produce, in FRENCH, a structured summary with the sections
-1. Contexte général
-2. Focus clinique ({focus})
-3. Événements clés
-4. Points de vigilance
-
-Return only the summary text (no comments, no JSON).
-"""
-
-MULTI_PATIENT_TEMPLATE = """
-You are a clinical assistant. Compare the clinical histories of SEVERAL anonymised
-patients.
-
-Context:
-- Patient aliases: {patients}
-- Time window: {from_date} to {to_date}
-- Clinical focus: {focus}
-
-Clinical notes by patient:
-{documents_by_patient}
-
-Task, in FRENCH:
-1. A global comparative summary
-2. The main differences between the patients (treatment, events, risks, ...)
-3. The key risk points of each patient
-
-Return only the final text (no comments, no JSON).
-"""
+# the reference's templates, verbatim (synthese-comparative/core/prompts.py:3-45)
+from ..prompts import MULTI_PATIENT_TEMPLATE, SINGLE_PATIENT_TEMPLATE  # noqa: E402
 
 
 class LLMClient:

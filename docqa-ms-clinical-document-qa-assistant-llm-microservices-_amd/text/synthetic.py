@@ -7,7 +7,10 @@
   same CSV->sentence templating (semantic-indexer/indexer.py:50-94) applies.
 * :func:`synthetic_notes` -- French clinical notes with realistic PII (names, dates,
   phones, e-mails, cities, nationalities) for the ingest -> deid -> index pipeline.
-* :func:`synthetic_questions` -- practitioner questions for the QA benchmark.
+* :func:`synthetic_questions` -- practitioner questions drawn from a small template x
+  syndrome x symptom grid (~470 distinct strings: the cache-hot "repeat" workload).
+* :func:`synthetic_unique_questions` -- pairwise-distinct questions (the default QA
+  benchmark workload: every request is new).
 """
 from __future__ import annotations
 
@@ -139,6 +142,51 @@ def synthetic_questions(n: int, seed: int = 0) -> list[str]:
     r = _rng(seed + 4242)
     return [r.choice(QUESTION_TEMPLATES).format(s=r.choice(SYNDROMES), y=r.choice(SYMPTOMS))
             for _ in range(n)]
+
+
+UNIQUE_TEMPLATES = [
+    "Patient {pid}, {age} ans, {sex}, consulte pour {y1} et {y2} depuis {w} semaines "
+    "(tension {sys}/{dia} mmHg). Quelles plantes recommander pour un syndrome « {s} » ?",
+    "Dossier {pid} : {sex} de {age} ans sous {med}, {y1} depuis {w} semaines. "
+    "Quel syndrome évoquer et quelle formule prescrire ?",
+    "Pour le patient {pid} ({age} ans) présentant {y1}, {y2} et un pouls {pouls}, "
+    "quelle est la plante Empereur du syndrome « {s} » et son score ?",
+    "Chez {sex_art} de {age} ans (dossier {pid}) traitée par {med}, peut-on associer des plantes "
+    "contre {y1} sans interaction ? Syndrome suspecté : « {s} ».",
+    "Le patient {pid}, {age} ans, signale {y1} apparue il y a {w} semaines et une langue {langue}. "
+    "Classe les plantes utiles selon leur score.",
+    "Quel traitement a été prescrit au patient {pid} suivi depuis {w} semaines pour {y1} "
+    "et {y2} (contrôle du {date}) ?",
+    "Patient {pid} ({sex}, {age} ans, {poids} kg) : {y1} et {y2} malgré {med}. "
+    "Quelle posologie de plantes pour « {s} » ?",
+    "Résume les plantes Ministre utiles au dossier {pid} : {y1} depuis {w} semaines, "
+    "tension {sys}/{dia} mmHg, syndrome « {s} » ({organ}).",
+]
+
+
+def synthetic_unique_questions(n: int, seed: int = 0) -> list[str]:
+    """``n`` pairwise-distinct practitioner questions, one per request (the reference
+    serves each ``/ask/`` call with a fresh question, llm-qa/main.py:111-117): patient id,
+    age, sex, symptom pair, duration, medication and vitals vary per question, so no two
+    requests share their question text and retrieval spreads over the corpus.  Collisions
+    are redrawn, so every question is distinct."""
+    r = _rng(seed + 9091)
+    out, seen = [], set()
+    while len(out) < n:
+        y1, y2 = r.sample(SYMPTOMS, 2)
+        fem = r.random() < 0.5
+        q = r.choice(UNIQUE_TEMPLATES).format(
+            pid=f"P{r.randint(1, 99999):05d}", age=r.randint(18, 92),
+            sex="femme" if fem else "homme", sex_art="une femme" if fem else "un homme",
+            y1=y1, y2=y2, w=r.randint(1, 52), s=r.choice(SYNDROMES), med=r.choice(MEDS),
+            sys=r.randint(95, 175), dia=r.randint(55, 105), poids=r.randint(45, 120),
+            pouls=r.choice(["fin", "rapide", "tendu", "faible", "glissant", "profond"]),
+            langue=r.choice(["pâle", "rouge", "enduit blanc", "enduit jaune", "violacée"]),
+            organ=r.choice(ORGANS), date=_date(r))
+        if q not in seen:
+            seen.add(q)
+            out.append(q)
+    return out
 
 
 def corpus_text(seed: int = 0, n_notes: int = 600) -> list[str]:

@@ -3,6 +3,7 @@ templates (services/synthese.py, pipeline/rag.py; reference synthese-comparative
 routes.py:45-101 and llm-qa/main.py:72-95).  The UI's upstream calls go to an
 httpx.MockTransport, so no server is started."""
 import json
+from pathlib import Path
 
 import httpx
 import pytest
@@ -127,3 +128,64 @@ def test_prompt_pieces_identical_to_full_tokenisation(monkeypatch):
     monkeypatch.setenv("DOCQA_PROMPT_PIECES", "1")
     assert pipe.build_prompts(qs, I) == full
     assert tok.encode_batch_chat([qs[0]]) == [tok.chat_prompt(qs[0])]
+
+
+REF = Path("/root/reference")
+
+
+def _ref_template(path: Path, marker: str) -> str:
+    src = path.read_text(encoding="utf-8")
+    i = src.index(marker) + len(marker)
+    return src[i:src.index('"""', i)]
+
+
+@pytest.mark.skipif(not (REF / "llm-qa" / "main.py").exists(), reason="reference not mounted")
+def test_reference_prompts_verbatim():
+    """The QA template selectable with QA_TEMPLATE=reference and the synthese templates are
+    byte-identical to the reference's (llm-qa/main.py:71-93, core/prompts.py:3-45)."""
+    from docqa_amd import prompts
+
+    assert prompts.REFERENCE_QA_TEMPLATE == _ref_template(REF / "llm-qa" / "main.py", 'template = """')
+    pr = REF / "synthese-comparative" / "core" / "prompts.py"
+    assert prompts.SINGLE_PATIENT_TEMPLATE == _ref_template(pr, 'SINGLE_PATIENT_TEMPLATE = """')
+    assert prompts.MULTI_PATIENT_TEMPLATE == _ref_template(pr, 'MULTI_PATIENT_TEMPLATE = """')
+    from docqa_amd.services import synthese
+    assert synthese.SINGLE_PATIENT_TEMPLATE is prompts.SINGLE_PATIENT_TEMPLATE
+    assert synthese.MULTI_PATIENT_TEMPLATE is prompts.MULTI_PATIENT_TEMPLATE
+
+
+def test_qa_template_selection(monkeypatch):
+    import torch
+
+    from docqa_amd import prompts
+    from docqa_amd.pipeline.rag import RAGPipeline
+    from docqa_amd.text.tokenizer import ChatTokenizer
+
+    class _Eng:
+        device = torch.device("cpu")
+
+    tok = ChatTokenizer(model_vocab=128256)
+    meta = [{"text_content": f"Ren Shen score {i}", "source": f"s{i}"} for i in range(4)]
+    monkeypatch.setenv("QA_TEMPLATE", "reference")
+    p = RAGPipeline(None, None, None, meta, _Eng(), tok)
+    assert p.template is prompts.REFERENCE_QA_TEMPLATE
+    # the piece-wise prompt assembly is exact for the reference order too
+    I = [[0, 1, 2], [3, 2, 1]]
+    qs = ["Quelle plante ?", "Posologie pour P00042 ?"]
+    monkeypatch.setenv("DOCQA_PROMPT_PIECES", "0")
+    full = p.build_prompts(qs, I)
+    monkeypatch.setenv("DOCQA_PROMPT_PIECES", "1")
+    assert p.build_prompts(qs, I) == full
+    monkeypatch.setenv("QA_TEMPLATE", "cache_friendly")
+    assert RAGPipeline(None, None, None, meta, _Eng(), tok).template is prompts.CACHE_FRIENDLY_QA_TEMPLATE
+    with pytest.raises(ValueError):
+        prompts.qa_template("nope")
+
+
+def test_unique_questions_are_distinct():
+    from docqa_amd.text.synthetic import synthetic_questions, synthetic_unique_questions
+
+    qs = synthetic_unique_questions(6400, seed=123)
+    assert len(set(qs)) == 6400
+    assert synthetic_unique_questions(50, seed=123) == qs[:50]
+    assert len(set(synthetic_questions(6400, seed=123))) < 1000   # the cache-hot grid
