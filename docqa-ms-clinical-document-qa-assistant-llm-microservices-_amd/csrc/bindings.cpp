@@ -686,10 +686,50 @@ at::Tensor mgemm_argmax(const at::Tensor& x, const at::Tensor& w, int64_t n_vali
   auto out = at::empty({M}, x.options().dtype(at::kLong));
   auto ws_v = at::empty({M, N / bn}, x.options().dtype(at::kFloat));
   auto ws_i = at::empty({M, N / bn}, x.options().dtype(at::kInt));
-  CHECK_RC(docqa_mgemm_argmax(x.data_ptr(), w.data_ptr(), out.data_ptr<int64_t>(), ws_v.data_ptr<float>(),
+  CHECK_RC(docqa_mgemm_argmax(x.data_ptr(), w.data_ptr(), out.data_ptr<int64_t>(), nullptr, ws_v.data_ptr<float>(),
                               ws_i.data_ptr<int>(), M, N, K, (int)n_valid, (int)cfg, stream()), "mgemm_argmax");
   return out;
 }
+
+// the same with the picked logit per row (vocab-parallel LM head: the TP group compares them)
+std::tuple<at::Tensor, at::Tensor> mgemm_argmax_val(const at::Tensor& x, const at::Tensor& w, int64_t n_valid,
+                                                    int64_t cfg) {
+  CHECK_GPU(x); CHECK_BF16(x); CHECK_BF16(w); CHECK_CONTIG(x); CHECK_CONTIG(w);
+  CHECK_ALIGN16(x); CHECK_ALIGN16(w);
+  const int K = x.size(-1), N = w.size(0), bn = docqa_mgemm_tile_n((int)cfg);
+  TORCH_CHECK(w.size(1) == K && bn > 0 && N % bn == 0, "mgemm_argmax_val: shape mismatch");
+  const int M = x.numel() / K;
+  c10::DeviceGuard g(x.device());
+  auto out = at::empty({M}, x.options().dtype(at::kLong));
+  auto outv = at::empty({M}, x.options().dtype(at::kFloat));
+  auto ws_v = at::empty({M, N / bn}, x.options().dtype(at::kFloat));
+  auto ws_i = at::empty({M, N / bn}, x.options().dtype(at::kInt));
+  CHECK_RC(docqa_mgemm_argmax(x.data_ptr(), w.data_ptr(), out.data_ptr<int64_t>(), outv.data_ptr<float>(),
+                              ws_v.data_ptr<float>(), ws_i.data_ptr<int>(), M, N, K, (int)n_valid, (int)cfg,
+                              stream()), "mgemm_argmax_val");
+  return {out, outv};
+}
+
+// prefill GEMM (pgemm.hip, 256 x 256 tiles): epi 0 -> x . w^T bf16 [.., N]; epi 1 -> fused
+// SwiGLU over 8-interleaved gate|up rows -> [.., N / 2]
+at::Tensor pgemm(const at::Tensor& x, const at::Tensor& w, int64_t epi) {
+  CHECK_GPU(x); CHECK_BF16(x); CHECK_BF16(w); CHECK_CONTIG(x); CHECK_CONTIG(w);
+  CHECK_ALIGN16(x); CHECK_ALIGN16(w);
+  const int K = x.size(-1), N = w.size(0);
+  TORCH_CHECK(w.size(1) == K, "pgemm: K mismatch");
+  TORCH_CHECK(epi == 0 || epi == 1, "pgemm: epi must be 0 (bf16) or 1 (SwiGLU)");
+  const int M = x.numel() / K;
+  TORCH_CHECK(M == 0 || docqa_pgemm_ok(M, N, K), "pgemm: unsupported shape M=", M, " N=", N, " K=", K,
+              " (N % 256, K % 128, 32-bit row offsets)");
+  auto sizes = x.sizes().vec();
+  sizes.back() = epi == 1 ? N / 2 : N;
+  c10::DeviceGuard g(x.device());
+  auto out = at::empty(sizes, x.options());
+  CHECK_RC(docqa_pgemm(x.data_ptr(), w.data_ptr(), out.data_ptr(), M, N, K, (int)epi, stream()), "pgemm");
+  return out;
+}
+
+bool pgemm_ok(int64_t M, int64_t N, int64_t K) { return docqa_pgemm_ok((int)M, (int)N, (int)K); }
 
 std::tuple<at::Tensor, at::Tensor> knn(const at::Tensor& xb, const at::Tensor& xb_norms,
                                        const at::Tensor& xq, int64_t k, bool inner_product,
@@ -799,18 +839,48 @@ int64_t ar_ipc_open(const at::Tensor& handle) {
 
 void ar_ipc_close(int64_t ptr) { TORCH_CHECK(docqa_ar_ipc_close((void*)(uintptr_t)ptr) == 0, "ipc close failed"); }
 
-at::Tensor ar_oneshot(const at::Tensor& in, int64_t rank, std::vector<int64_t> regions, int64_t max_elems,
-                      at::Tensor epochs, at::Tensor err) {
-  CHECK_GPU(in); CHECK_BF16(in); CHECK_CONTIG(in);
-  TORCH_CHECK(epochs.scalar_type() == at::kInt && err.scalar_type() == at::kInt, "epochs/err must be int32");
+// x: bf16 [M, H] partial (slabs false) or fp32 split-K slabs [S, M, H] (slabs true); residual /
+// w given: residual <- residual + allreduce(x) in place and the RMSNorm of it is returned,
+// else the all-reduced sum.  mode 0 one-shot, 1 two-shot (kernels/allreduce.hip).
+at::Tensor ar_run(const at::Tensor& x, bool slabs, const c10::optional<at::Tensor>& residual,
+                  const c10::optional<at::Tensor>& w, double eps, int64_t rank, std::vector<int64_t> regions,
+                  int64_t max_elems, int64_t mode, at::Tensor ctr, at::Tensor err) {
+  CHECK_GPU(x); CHECK_CONTIG(x); CHECK_ALIGN16(x);
+  TORCH_CHECK(ctr.scalar_type() == at::kInt && ctr.numel() >= 2 && err.scalar_type() == at::kInt,
+              "ctr int32[2] / err int32[1]");
   TORCH_CHECK(regions.size() >= 1 && regions.size() <= 8, "1..8 ranks");
+  const int H = x.size(-1);
+  int S = 0, M;
+  if (slabs) {
+    TORCH_CHECK(x.scalar_type() == at::kFloat && x.dim() == 3, "slabs must be fp32 [S, M, H]");
+    S = x.size(0);
+    M = x.size(1);
+  } else {
+    CHECK_BF16(x);
+    M = x.numel() / H;
+  }
+  const bool fused = residual.has_value();
+  TORCH_CHECK(fused == w.has_value(), "residual and w go together");
+  if (fused) {
+    CHECK_BF16(*residual); CHECK_CONTIG(*residual); CHECK_BF16(*w); CHECK_CONTIG(*w);
+    TORCH_CHECK(residual->numel() == (int64_t)M * H && w->numel() == H, "ar_run: residual / w shape");
+  }
   std::vector<void*> ptrs;
   for (auto r : regions) ptrs.push_back((void*)(uintptr_t)r);
-  c10::DeviceGuard g(in.device());
-  auto out = at::empty_like(in);
-  CHECK_RC(docqa_ar_oneshot(in.data_ptr(), out.data_ptr(), in.numel(), (int)rank, (int)regions.size(),
-                            ptrs.data(), (size_t)max_elems, (unsigned*)epochs.data_ptr(),
-                            (unsigned*)err.data_ptr(), stream()), "ar_oneshot");
+  c10::DeviceGuard g(x.device());
+  at::Tensor out;
+  if (mode == 2) {   // all-gather: [nranks, ..x's shape]
+    TORCH_CHECK(!slabs && !fused, "ar_run gather takes a bf16 payload only");
+    auto sizes = x.sizes().vec();
+    sizes.insert(sizes.begin(), (int64_t)regions.size());
+    out = at::empty(sizes, x.options());
+  } else {
+    out = slabs ? at::empty({M, H}, x.options().dtype(at::kBFloat16)) : at::empty_like(x);
+  }
+  CHECK_RC(docqa_ar_run(x.data_ptr(), S, out.data_ptr(), fused ? residual->data_ptr() : nullptr,
+                        fused ? w->data_ptr() : nullptr, (float)eps, M, H, (int)rank, (int)regions.size(),
+                        ptrs.data(), (size_t)max_elems, (int)mode, (unsigned*)ctr.data_ptr(),
+                        (unsigned*)err.data_ptr(), stream()), "ar_run");
   return out;
 }
 
@@ -851,6 +921,9 @@ TORCH_LIBRARY(docqa, m) {
   m.def("mgemm(Tensor x, Tensor w, int splits, int cfg=0) -> Tensor");
   m.def("mgemm_glu(Tensor x, Tensor w, int cfg=0) -> Tensor");
   m.def("mgemm_argmax(Tensor x, Tensor w, int n_valid, int cfg=0) -> Tensor");
+  m.def("pgemm(Tensor x, Tensor w, int epi=0) -> Tensor");
+  m.def("mgemm_argmax_val(Tensor x, Tensor w, int n_valid, int cfg=0) -> (Tensor, Tensor)");
+  m.def("pgemm_ok(int M, int N, int K) -> bool", &pgemm_ok);
   m.def("paged_decode_cascade(Tensor q, Tensor k_cache, Tensor v_cache, Tensor block_tables, "
         "Tensor context_lens, int Hq, int max_context, float scale, Tensor prefix_table, Tensor prefix_len, "
         "int nchunk, Tensor? order=None) -> Tensor");
@@ -868,7 +941,8 @@ TORCH_LIBRARY(docqa, m) {
   m.def("paged_decode_fused(Tensor P, Tensor positions, Tensor cos_sin, Tensor slot_mapping, "
         "Tensor(a!) k_cache, Tensor(b!) v_cache, Tensor block_tables, Tensor context_lens, int Hq, "
         "int max_context, float scale, Tensor? order=None) -> Tensor");
-  m.def("ar_oneshot(Tensor x, int rank, int[] regions, int max_elems, Tensor(a!) epochs, Tensor(b!) err) -> Tensor");
+  m.def("ar_run(Tensor x, bool slabs, Tensor(r!)? residual, Tensor? w, float eps, int rank, int[] regions, "
+        "int max_elems, int mode, Tensor(a!) ctr, Tensor(b!) err) -> Tensor");
   m.def("ar_region_bytes(int max_elems) -> int", &ar_region_bytes);
   m.def("ar_alloc(int bytes) -> int", &ar_alloc);
   m.def("ar_free(int ptr) -> ()", &ar_free);
@@ -908,13 +982,15 @@ TORCH_LIBRARY_IMPL(docqa, CUDA, m) {
   m.impl("mgemm", &mgemm);
   m.impl("mgemm_glu", &mgemm_glu);
   m.impl("mgemm_argmax", &mgemm_argmax);
+  m.impl("pgemm", &pgemm);
+  m.impl("mgemm_argmax_val", &mgemm_argmax_val);
   m.impl("paged_decode_fused", &paged_decode_fused);
   m.impl("paged_decode_cascade", &paged_decode_cascade);
   m.impl("paged_decode_cascade_rope", &paged_decode_cascade_rope);
   m.impl("paged_decode_cascade_grouped", &paged_decode_cascade_grouped);
   m.impl("paged_decode_cascade_split", &paged_decode_cascade_split);
   m.impl("kv_copy_rows", &kv_copy_rows);
-  m.impl("ar_oneshot", &ar_oneshot);
+  m.impl("ar_run", &ar_run);
   m.impl("add_rmsnorm_splitk", &add_rmsnorm_splitk);
   m.impl("rope_cache_splitk", &rope_cache_splitk);
 }

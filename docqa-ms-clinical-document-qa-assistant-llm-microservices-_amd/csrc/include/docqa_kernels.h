@@ -95,8 +95,9 @@ int docqa_ar_free(void* ptr);
 int docqa_ar_ipc_handle(void* ptr, void* handle_out);
 int docqa_ar_ipc_open(const void* handle, void** ptr);
 int docqa_ar_ipc_close(void* ptr);
-int docqa_ar_oneshot(const void* in, void* out, int n, int rank, int nranks, void* const* regions,
-                     size_t max_elems, unsigned* epochs, unsigned* err, hipStream_t s);
+int docqa_ar_run(const void* in, int S, void* out, void* residual, const void* w, float eps, int M, int H,
+                 int rank, int nranks, void* const* regions, size_t max_elems, int mode, unsigned* ctr,
+                 unsigned* err, hipStream_t s);
 int docqa_paged_decode_fused(const float* P, int S, const int* positions, const float* cos_sin,
                              const int* slot_mapping, void* k_cache, void* v_cache,
                              const int* block_tables, int maxb, const int* context_lens, void* out,
@@ -111,9 +112,11 @@ int docqa_gemm(const void* A, const void* W, const void* bias, const void* res, 
 int docqa_mgemm(const void* X, const void* W, void* Y, float* P, int M, int N, int K, int S, int cfg,
                 hipStream_t s);
 int docqa_mgemm_glu(const void* X, const void* W, void* Y, int M, int N, int K, int cfg, hipStream_t s);
-int docqa_mgemm_argmax(const void* X, const void* W, int64_t* out, float* ws_v, int* ws_i, int M, int N,
-                       int K, int n_valid, int cfg, hipStream_t s);
+int docqa_mgemm_argmax(const void* X, const void* W, int64_t* out, float* outv, float* ws_v, int* ws_i, int M,
+                       int N, int K, int n_valid, int cfg, hipStream_t s);
 int docqa_mgemm_tile_n(int cfg);
+bool docqa_pgemm_ok(int M, int N, int K);
+int docqa_pgemm(const void* A, const void* W, void* C, int M, int N, int K, int epi, hipStream_t s);
 
 int docqa_knn_workspace_blocks(int N);
 int docqa_knn_kpad(int k);

@@ -1,26 +1,38 @@
-// allreduce.hip -- one-shot all-reduce over IPC-mapped peer memory for the generator's
-// tensor-parallel decode all-reduces.
+// allreduce.hip -- tensor-parallel all-reduce over IPC-mapped peer memory for the Llama
+// generator's row-parallel projections, with the residual add +
+// RMSNorm that follows every such all-reduce fused in.
 //
-// TP decode all-reduces are small ([B, hidden] bf16: 1 MB at B = 64, hidden = 8192) and
-// latency-bound.  On one MI355X node the 8 GPUs are fully connected by xGMI (7 links per
-// GPU), so instead of a ring (one link per step, 2(N-1) hops) every rank reads all peers'
-// buffers at once over all links and reduces locally:
+// On one MI355X node the 8 GPUs are fully connected by xGMI (7 point-to-point links per
+// GPU).  A ring all-reduce uses one link per direction per step; here every rank reads its
+// peers' staging buffers directly, so all 7 links carry data at once:
 //
-//   1. each workgroup copies its contiguous slice of the local input into this rank's
-//      staging buffer (half `epoch & 1` of a double buffer);
-//   2. it publishes `epoch` into slot [wg][rank] of every peer's flag array and waits
-//      until its own slots [wg][p] hold `epoch` for every peer p (bounded spin);
-//   3. it sums slice `wg` of all N staging buffers (fp32 accumulate) into the output.
+//   ONESHOT (small, latency-bound messages -- decode at small batch):
+//     1. each workgroup writes its rows of the local partial (bf16, or the fp32 split-K
+//        slabs of the projection summed in registers) into this rank's staging area;
+//     2. it publishes the call's epoch into slot [0][wg][rank] of every peer's flag array
+//        and waits until its own slots [0][wg][p] reach the epoch (bounded spin);
+//     3. it sums its rows over all N staging areas (fp32, the same order on every rank, so
+//        every rank gets bit-identical results) -> epilogue.
+//   TWOSHOT (larger messages -- prefill, decode at batch >= ~64):
+//     1. as above;
+//     2'. reduce-scatter: each rank sums only its column chunk [r H/N, (r+1) H/N) of the
+//        workgroup's rows over all peers and writes it (bf16) to its result area, publishes
+//        slot [1][wg][rank] and waits for slots [1][wg][p];
+//     3'. all-gather: it reads every column chunk of its rows from the chunk's owner ->
+//        epilogue.  Each rank moves 2 (N-1)/N of the message over xGMI instead of N-1.
+//   Epilogue: plain (out = sum) or fused (residual <- bf16(residual + sum) in place,
+//   out = rmsnorm(residual) * w: exactly ops.add_rmsnorm), one wave per row.
 //
-// Double buffering needs only this one barrier per call: a rank can reuse a staging half
-// two calls later only after its peers have signalled in the call in between, i.e. after
-// they finished reading it.  Epochs live in device memory (one counter per workgroup),
-// so a HIP-graph replay of the kernel advances them correctly.
-//
-// Memory: staging + flags are allocated uncached (hipDeviceMallocUncached), so remote
-// reads/writes over xGMI bypass every cache and need no invalidation; flag stores/loads
-// are system-scope atomics.  Spins give up after a bound and raise an error word instead
-// of hanging the GPU (the grid is <= one workgroup per CU, all resident).
+// Synchronisation: one epoch per CALL (a device-side counter read by every workgroup at
+// start and advanced by the last workgroup to finish, so a HIP-graph replay advances it),
+// staging halves double-buffered by epoch parity, flags compared with >= (a peer may
+// already have published the next call's epoch).  A rank reuses a staging half two calls
+// later only after every peer has published in the call in between, i.e. after each peer's
+// previous kernel -- all its reads of that half -- has completed.  Staging and flags are
+// allocated uncached (hipDeviceMallocUncached): remote reads and writes over xGMI bypass
+// the caches; flag stores / loads are system-scope release / acquire atomics.  Spins give
+// up after a bound and set an error word instead of hanging the GPU (every grid is
+// <= 256 workgroups of 256 threads: all resident).
 #include "docqa_common.h"
 #include <cstring>
 
@@ -28,40 +40,46 @@ using namespace docqa;
 
 namespace {
 constexpr int kMaxRanks = 8;
-constexpr int kMaxWG = 128;
+constexpr int kMaxWG = 256;
 constexpr unsigned kSpinLimit = 1u << 24;
+constexpr size_t kFlagBytes = (size_t)2 * kMaxWG * kMaxRanks * sizeof(unsigned);
+
+enum { ONESHOT = 0, TWOSHOT = 1, GATHER = 2 };
+enum { SRC_BF16 = 0, SRC_F32 = 1 };
 
 struct ArPeers {
-  uint16_t* data[kMaxRanks];      // staging buffers (2 halves of `half_elems`)
-  unsigned* flags[kMaxRanks];     // [kMaxWG][kMaxRanks] epoch slots
+  uint16_t* data[kMaxRanks];      // staging data of each rank (2 halves x [in | result])
+  unsigned* flags[kMaxRanks];     // [2 phases][kMaxWG][kMaxRanks] epoch slots of each rank
 };
 
-__global__ __launch_bounds__(256) void allreduce_oneshot_kernel(
-    const uint16_t* __restrict__ in, uint16_t* __restrict__ out, int n, int per_wg, int rank,
-    int nranks, size_t half_elems, ArPeers peers, unsigned* __restrict__ epochs,
-    unsigned* __restrict__ err) {
-  const int wg = blockIdx.x, tid = threadIdx.x;
-  const unsigned epoch = epochs[wg] + 1;
-  const size_t half = (size_t)(epoch & 1) * half_elems;
-  const int lo = wg * per_wg;
-  const int hi = min(n, lo + per_wg);
+struct ArArgs {
+  const void* in;                 // bf16 [M, H] or fp32 slabs [S, M, H]
+  int S;
+  uint16_t* out;                  // [M, H]
+  uint16_t* residual;             // fused: [M, H], updated in place
+  const uint16_t* w;              // fused: [H]
+  float eps;
+  int M, H, rank, nranks;
+  size_t half_elems;              // elements of one [in | result] area
+  unsigned* ctr;                  // [0] epoch of the last call, [1] finished workgroups
+  unsigned* err;
+};
 
-  // 1. local slice -> own staging (16-B vectors; n and per_wg are multiples of 8)
-  uint16_t* mine = peers.data[rank] + half;
-  for (int i = lo + tid * 8; i < hi; i += 256 * 8)
-    *reinterpret_cast<uint4*>(mine + i) = *reinterpret_cast<const uint4*>(in + i);
+__device__ __forceinline__ void publish(const ArPeers& peers, int phase, int wg, int rank, int nranks,
+                                        unsigned epoch) {
   __threadfence_system();
   __syncthreads();
+  if ((int)threadIdx.x < nranks)
+    __hip_atomic_store(peers.flags[threadIdx.x] + ((size_t)phase * kMaxWG + wg) * kMaxRanks + rank, epoch,
+                       __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
 
-  // 2. barrier with the same workgroup on every peer
-  if (tid < nranks) {
-    __hip_atomic_store(peers.flags[tid] + wg * kMaxRanks + rank, epoch, __ATOMIC_RELEASE,
-                       __HIP_MEMORY_SCOPE_SYSTEM);
-  }
-  if (tid < nranks) {
-    const unsigned* slot = peers.flags[rank] + wg * kMaxRanks + tid;
+__device__ __forceinline__ void wait_peers(const ArPeers& peers, int phase, int wg, int rank, int nranks,
+                                           unsigned epoch, unsigned* err) {
+  if ((int)threadIdx.x < nranks) {
+    const unsigned* slot = peers.flags[rank] + ((size_t)phase * kMaxWG + wg) * kMaxRanks + threadIdx.x;
     unsigned spins = 0;
-    while (__hip_atomic_load(slot, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) != epoch) {
+    while ((int)(__hip_atomic_load(slot, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) - epoch) < 0) {
       __builtin_amdgcn_s_sleep(2);
       if (++spins > kSpinLimit) {
         atomicOr(err, 1u);
@@ -71,26 +89,156 @@ __global__ __launch_bounds__(256) void allreduce_oneshot_kernel(
   }
   __syncthreads();
   __atomic_thread_fence(__ATOMIC_ACQUIRE);   // system scope: no stale peer lines below
+}
 
-  // 3. reduce slice `wg` over all ranks
-  for (int i = lo + tid * 8; i < hi; i += 256 * 8) {
-    float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-    for (int p = 0; p < nranks; ++p) {
-      float v[8];
-      unpack8(*reinterpret_cast<const uint4*>(peers.data[p] + half + i), v);
+// residual <- bf16(residual + v) for 8 columns; returns the partial sum of squares
+__device__ __forceinline__ float fused_add(const ArArgs& a, size_t off, float* v) {
+  float r[8];
+  unpack8(*reinterpret_cast<const uint4*>(a.residual + off), r);
+  float ss = 0.f;
 #pragma unroll
-      for (int j = 0; j < 8; ++j) acc[j] += v[j];
-    }
-    *reinterpret_cast<uint4*>(out + i) = pack8(acc);
+  for (int e = 0; e < 8; ++e) {
+    v[e] = bf2f(f2bf(v[e] + r[e]));
+    ss += v[e] * v[e];
   }
-  if (tid == 0) epochs[wg] = epoch;
+  *reinterpret_cast<uint4*>(a.residual + off) = pack8(v);
+  return ss;
+}
+
+// out = bf16(residual * inv * w) for one row (residual re-read: this lane wrote it)
+__device__ __forceinline__ void fused_norm_row(const ArArgs& a, int row, float inv, int lane) {
+  for (int c = lane * 8; c < a.H; c += 512) {
+    const size_t off = (size_t)row * a.H + c;
+    float r[8], w[8];
+    unpack8(*reinterpret_cast<const uint4*>(a.residual + off), r);
+    unpack8(*reinterpret_cast<const uint4*>(a.w + c), w);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) r[e] = r[e] * inv * w[e];
+    *reinterpret_cast<uint4*>(a.out + off) = pack8(r);
+  }
+}
+
+template <int MODE, int SRC, bool FUSED>
+__global__ __launch_bounds__(256) void allreduce_kernel(ArArgs a, ArPeers peers) {
+  const int wg = blockIdx.x, G = gridDim.x;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const unsigned epoch = a.ctr[0] + 1;
+  const size_t half = (size_t)(epoch & 1) * 2 * a.half_elems;   // [in | result] of this call
+  const int r0 = (int)((long)a.M * wg / G), r1 = (int)((long)a.M * (wg + 1) / G);
+  const int H = a.H;
+  uint16_t* mine = peers.data[a.rank] + half;
+
+  // 1. local partial rows -> own staging "in" area (fp32 slabs summed here)
+  for (int row = r0 + wave; row < r1; row += 4) {
+    for (int c = lane * 8; c < H; c += 512) {
+      const size_t off = (size_t)row * H + c;
+      if constexpr (SRC == SRC_BF16) {
+        *reinterpret_cast<uint4*>(mine + off) = *reinterpret_cast<const uint4*>((const uint16_t*)a.in + off);
+      } else {
+        const float* P = (const float*)a.in;
+        const size_t slab = (size_t)a.M * H;
+        float v[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+        for (int s = 0; s < a.S; ++s) {
+          const float4 x0 = *reinterpret_cast<const float4*>(P + s * slab + off);
+          const float4 x1 = *reinterpret_cast<const float4*>(P + s * slab + off + 4);
+          v[0] += x0.x; v[1] += x0.y; v[2] += x0.z; v[3] += x0.w;
+          v[4] += x1.x; v[5] += x1.y; v[6] += x1.z; v[7] += x1.w;
+        }
+        *reinterpret_cast<uint4*>(mine + off) = pack8(v);
+      }
+    }
+  }
+  publish(peers, 0, wg, a.rank, a.nranks, epoch);
+  wait_peers(peers, 0, wg, a.rank, a.nranks, epoch, a.err);
+
+  if constexpr (MODE == GATHER) {
+    // all-gather of raw 16-B words: out[p] <- rank p's rows (bit-exact copies)
+    const size_t n = (size_t)a.M * H;
+    for (int p = 0; p < a.nranks; ++p)
+      for (int row = r0 + wave; row < r1; row += 4)
+        for (int c = lane * 8; c < H; c += 512) {
+          const size_t off = (size_t)row * H + c;
+          *reinterpret_cast<uint4*>(a.out + p * n + off) = *reinterpret_cast<const uint4*>(peers.data[p] + half + off);
+        }
+  } else if constexpr (MODE == ONESHOT) {
+    // 3. every rank sums its rows over all peers itself (same order everywhere)
+    for (int row = r0 + wave; row < r1; row += 4) {
+      float ss = 0.f;
+      for (int c = lane * 8; c < H; c += 512) {
+        const size_t off = (size_t)row * H + c;
+        float v[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+        for (int p = 0; p < a.nranks; ++p) {
+          float x[8];
+          unpack8(*reinterpret_cast<const uint4*>(peers.data[p] + half + off), x);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) v[e] += x[e];
+        }
+        if constexpr (FUSED) ss += fused_add(a, off, v);
+        else *reinterpret_cast<uint4*>(a.out + off) = pack8(v);
+      }
+      if constexpr (FUSED) {
+        ss = wave_sum(ss);
+        fused_norm_row(a, row, rsqrtf(ss / H + a.eps), lane);
+      }
+    }
+  } else {
+    // 2'. reduce-scatter: this rank's column chunk of the workgroup's rows
+    const int CH = H / a.nranks, c0 = a.rank * CH;
+    uint16_t* res = mine + a.half_elems;
+    for (int row = r0 + wave; row < r1; row += 4) {
+      for (int c = c0 + lane * 8; c < c0 + CH; c += 512) {
+        const size_t off = (size_t)row * H + c;
+        float v[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+        for (int p = 0; p < a.nranks; ++p) {
+          float x[8];
+          unpack8(*reinterpret_cast<const uint4*>(peers.data[p] + half + off), x);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) v[e] += x[e];
+        }
+        *reinterpret_cast<uint4*>(res + off) = pack8(v);
+      }
+    }
+    publish(peers, 1, wg, a.rank, a.nranks, epoch);
+    wait_peers(peers, 1, wg, a.rank, a.nranks, epoch, a.err);
+    // 3'. all-gather of the reduced chunks -> epilogue
+    for (int row = r0 + wave; row < r1; row += 4) {
+      float ss = 0.f;
+      for (int c = lane * 8; c < H; c += 512) {
+        const size_t off = (size_t)row * H + c;
+        const int owner = c / CH;
+        float v[8];
+        unpack8(*reinterpret_cast<const uint4*>(peers.data[owner] + half + a.half_elems + off), v);
+        if constexpr (FUSED) ss += fused_add(a, off, v);
+        else *reinterpret_cast<uint4*>(a.out + off) = pack8(v);
+      }
+      if constexpr (FUSED) {
+        ss = wave_sum(ss);
+        fused_norm_row(a, row, rsqrtf(ss / H + a.eps), lane);
+      }
+    }
+  }
+  // the last workgroup to finish advances the call epoch (read by the next call's grid)
+  __syncthreads();
+  if (tid == 0) {
+    __threadfence();
+    if (atomicAdd(a.ctr + 1, 1u) == (unsigned)G - 1) {
+      a.ctr[1] = 0;
+      a.ctr[0] = epoch;
+      __threadfence();
+    }
+  }
+}
+
+template <int MODE, int SRC, bool FUSED>
+int launch(const ArArgs& a, const ArPeers& p, int G, hipStream_t s) {
+  allreduce_kernel<MODE, SRC, FUSED><<<G, 256, 0, s>>>(a, p);
+  DOCQA_CHECK_LAUNCH();
+  return 0;
 }
 }  // namespace
 
-// staging + flag region of one rank: [flags kMaxWG * kMaxRanks u32][2 halves of max_elems]
-size_t docqa_ar_region_bytes(size_t max_elems) {
-  return (size_t)kMaxWG * kMaxRanks * sizeof(unsigned) + 2 * max_elems * sizeof(uint16_t);
-}
+// staging + flag region of one rank: [flags][2 halves x (in max_elems | result max_elems)]
+size_t docqa_ar_region_bytes(size_t max_elems) { return kFlagBytes + 4 * max_elems * sizeof(uint16_t); }
 
 int docqa_ar_alloc(size_t bytes, void** ptr) {
   if (hipExtMallocWithFlags(ptr, bytes, hipDeviceMallocUncached) != hipSuccess) return -1;
@@ -115,26 +263,47 @@ int docqa_ar_ipc_open(const void* handle, void** ptr) {
 
 int docqa_ar_ipc_close(void* ptr) { return hipIpcCloseMemHandle(ptr) == hipSuccess ? 0 : -1; }
 
-// regions[r]: rank r's region as mapped in this process (own allocation for r == rank)
-int docqa_ar_oneshot(const void* in, void* out, int n, int rank, int nranks,
-                     void* const* regions, size_t max_elems, unsigned* epochs, unsigned* err,
-                     hipStream_t s) {
-  if (n == 0) return 0;
-  if (nranks < 1 || nranks > kMaxRanks || n % 8 != 0 || (size_t)n > max_elems) return -1;
+// All-reduce (mode 0 / 1) or all-gather (mode 2: out [nranks, M, H], raw 16-bit words) of a
+// [M, H] tensor over `nranks` IPC-mapped regions (regions[r]: rank r's region
+// as mapped in this process).  in: bf16 [M, H] (S == 0) or fp32 split-K slabs [S, M, H];
+// residual / w given: fused add + RMSNorm epilogue (residual updated in place, out = the
+// normed rows), else out = the sum.  mode 0 one-shot, 1 two-shot, 2 gather.  ctr: int32 [2]
+// zeroed once, err: int32 [1].
+int docqa_ar_run(const void* in, int S, void* out, void* residual, const void* w, float eps, int M, int H,
+                 int rank, int nranks, void* const* regions, size_t max_elems, int mode, unsigned* ctr,
+                 unsigned* err, hipStream_t s) {
+  if (M == 0) return 0;
+  if (nranks < 1 || nranks > kMaxRanks || rank < 0 || rank >= nranks || H % 8 != 0 || M < 0) return -1;
+  if ((size_t)M * H > max_elems) return -1;
+  if (mode == TWOSHOT && (H % (8 * nranks) != 0)) return -1;
+  if ((residual == nullptr) != (w == nullptr)) return -1;
+  if (mode == GATHER && (S != 0 || residual != nullptr)) return -1;
+  if (!docqa_aligned16(in) || !docqa_aligned16(out) || (residual && !docqa_aligned16(residual))) return -1;
   ArPeers peers{};
-  const size_t flag_bytes = (size_t)kMaxWG * kMaxRanks * sizeof(unsigned);
   for (int r = 0; r < nranks; ++r) {
     peers.flags[r] = (unsigned*)regions[r];
-    peers.data[r] = (uint16_t*)((char*)regions[r] + flag_bytes);
+    peers.data[r] = (uint16_t*)((char*)regions[r] + kFlagBytes);
   }
-  // workgroups: ~16 KB of payload each, at most kMaxWG (all resident); same on every rank
-  int wgs = (n * 2 + 16383) / 16384;
-  wgs = wgs < 1 ? 1 : (wgs > kMaxWG ? kMaxWG : wgs);
-  int per_wg = (n + wgs - 1) / wgs;
-  per_wg = (per_wg + 7) / 8 * 8;
-  wgs = (n + per_wg - 1) / per_wg;
-  allreduce_oneshot_kernel<<<wgs, 256, 0, s>>>((const uint16_t*)in, (uint16_t*)out, n, per_wg,
-                                               rank, nranks, max_elems, peers, epochs, err);
-  DOCQA_CHECK_LAUNCH();
-  return 0;
+  ArArgs a{in, S, (uint16_t*)out, (uint16_t*)residual, (const uint16_t*)w, eps, M, H, rank, nranks,
+           max_elems, ctr, err};
+  // workgroups: one per few rows (4 waves, one row each at a time), <= kMaxWG, all resident;
+  // the same count on every rank (a function of M only)
+  int G = (M + 3) / 4;
+  if (G > kMaxWG) G = kMaxWG;
+  if (G < 1) G = 1;
+  const bool fused = residual != nullptr;
+  const int src = S > 0 ? SRC_F32 : SRC_BF16;
+#define AR_CASE(MD, SR, FU) \
+  if (mode == MD && src == SR && fused == FU) return launch<MD, SR, FU>(a, peers, G, s);
+  AR_CASE(ONESHOT, SRC_BF16, false)
+  AR_CASE(ONESHOT, SRC_BF16, true)
+  AR_CASE(ONESHOT, SRC_F32, false)
+  AR_CASE(ONESHOT, SRC_F32, true)
+  AR_CASE(TWOSHOT, SRC_BF16, false)
+  AR_CASE(TWOSHOT, SRC_BF16, true)
+  AR_CASE(TWOSHOT, SRC_F32, false)
+  AR_CASE(TWOSHOT, SRC_F32, true)
+  AR_CASE(GATHER, SRC_BF16, false)
+#undef AR_CASE
+  return -1;
 }

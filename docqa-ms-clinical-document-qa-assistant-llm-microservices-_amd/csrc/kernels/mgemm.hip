@@ -373,7 +373,7 @@ __global__ __launch_bounds__(WM * WN * 64) void mgemm_kernel(const uint16_t* __r
 
 __global__ __launch_bounds__(64) void mgemm_argmax_merge(const float* __restrict__ pv,
                                                          const int* __restrict__ pi, int parts,
-                                                         int64_t* __restrict__ out) {
+                                                         int64_t* __restrict__ out, float* __restrict__ outv) {
   const int row = blockIdx.x;
   float bv = -FLT_MAX;
   int bi = 0x7fffffff;
@@ -385,7 +385,10 @@ __global__ __launch_bounds__(64) void mgemm_argmax_merge(const float* __restrict
     const int oi = __shfl_xor(bi, o, 64);
     better(bv, bi, ov, oi);
   }
-  if (threadIdx.x == 0) out[row] = bi == 0x7fffffff ? 0 : bi;   // all-NaN row: a valid id
+  if (threadIdx.x == 0) {
+    out[row] = bi == 0x7fffffff ? 0 : bi;   // all-NaN row: a valid id
+    if (outv) outv[row] = bv;               // the row's best (bf16-rounded) logit, for TP picks
+  }
 }
 
 // Variants (``cfg``): the tile width and wave layout
@@ -485,10 +488,10 @@ int docqa_mgemm_glu(const void* X, const void* W, void* Y, int M, int N, int K, 
                              M, N, K, 1, N, s);
 }
 
-// out[M] = argmax over the first n_valid columns of bf16(X . W^T) (LM head + greedy pick);
-// ws_v / ws_i: [M, N / tile_n] partials
-int docqa_mgemm_argmax(const void* X, const void* W, int64_t* out, float* ws_v, int* ws_i, int M, int N,
-                       int K, int n_valid, int cfg, hipStream_t s) {
+// out[M] = argmax over the first n_valid columns of bf16(X . W^T) (LM head + greedy pick),
+// outv[M] (optional) its value; ws_v / ws_i: [M, N / tile_n] partials
+int docqa_mgemm_argmax(const void* X, const void* W, int64_t* out, float* outv, float* ws_v, int* ws_i, int M,
+                       int N, int K, int n_valid, int cfg, hipStream_t s) {
   if (cfg == 0) cfg = kDefaultCfg;
   if (M == 0) return 0;
   if (!shape_ok(M, N, K, 1, cfg) || n_valid <= 0 || n_valid > N) return -1;
@@ -496,7 +499,7 @@ int docqa_mgemm_argmax(const void* X, const void* W, int64_t* out, float* ws_v, 
   const int rc = launch_cfg<EPI_ARGMAX>(cfg, (const uint16_t*)X, (const uint16_t*)W, nullptr, nullptr, ws_v, ws_i,
                                         M, N, K, 1, n_valid, s);
   if (rc) return rc;
-  mgemm_argmax_merge<<<M, 64, 0, s>>>(ws_v, ws_i, N / kCfg[cfg].bn, out);
+  mgemm_argmax_merge<<<M, 64, 0, s>>>(ws_v, ws_i, N / kCfg[cfg].bn, out, outv);
   DOCQA_CHECK_LAUNCH();
   return 0;
 }

@@ -241,9 +241,11 @@ class LLMEngine:
 
     # ------------------------------------------------------------------ prefill
     def _prefill(self, prompts: list[list[int]], tables: list[list[int]],
-                 cached: list[int] | None = None) -> torch.Tensor:
+                 cached: list[int] | None = None, greedy: bool = False) -> torch.Tensor:
         """Prefill prompt tokens [cached[i], len) of each prompt (the first cached[i]
-        tokens are prefix-cache hits already in the paged KV cache)."""
+        tokens are prefix-cache hits already in the paged KV cache).  Returns the last
+        position's logits per prompt, or (``greedy``) its greedy token id (the LM head's
+        argmax fused into its GEMM: no [B, vocab] logits)."""
         dev, BS = self.device, self.block_size
         cached = list(cached or [0] * len(prompts))
         # chunked prefill: a prompt longer than the token budget is fed in budget-sized
@@ -289,8 +291,7 @@ class LLMEngine:
                 print(json.dumps({"prefill_chunk": j - i, "new_sum": sum(new), "new_max": max(new),
                                   "cached_mean": sum(cached[i:j]) / (j - i), "cached_max": max(cached[i:j]),
                                   "cached_min": min(cached[i:j])}), flush=True)
-            logits = self.model.forward(t_ids, meta, self.kv.caches, logits_index=last)
-            firsts.append(logits)
+            firsts.append(self.model.forward(t_ids, meta, self.kv.caches, logits_index=last, greedy_ids=greedy))
             i = j
         return torch.cat(firsts, 0)
 
@@ -596,7 +597,7 @@ class LLMEngine:
                 ev[0].record()
             self.queue_prefix_copies(r)
             with tracing.span("engine.prefill", seqs=B, tokens=sum(lens) - sum(cached)):
-                logits = self._prefill(prompts, tables, cached)
+                logits = self._prefill(prompts, tables, cached, greedy=greedy)
             if use_pc:
                 with tracing.span("engine.register", seqs=B):
                     self.register_prefixes(prompts, tables, r.keys)
@@ -629,7 +630,7 @@ class LLMEngine:
                 g.top_p.fill_(params.top_p)
                 if params.seed:
                     torch.manual_seed(params.seed)
-            first = self._select(logits, g)
+            first = logits if greedy else self._select(logits, g)
             gen = torch.empty(B, params.max_new_tokens, dtype=torch.long, device=dev)
             gen[:, 0] = first
             tok = torch.zeros(g.bp, dtype=torch.int32, device=dev)

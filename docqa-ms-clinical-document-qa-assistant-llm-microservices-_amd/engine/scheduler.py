@@ -234,8 +234,10 @@ class ContinuousEngine:
             with tracing.span("sched.admit", seqs=len(adm), tokens=sum(len(r.prompt) - r.cached for r in adm)):
                 for r in adm:
                     eng.queue_prefix_copies(r.res)
-                logits = eng._prefill([r.prompt for r in adm], [r.blocks for r in adm], [r.cached for r in adm])
-                first = self._sample_rows(logits, [r.params for r in adm])
+                greedy = all(r.params.temperature <= 0 for r in adm)
+                out = eng._prefill([r.prompt for r in adm], [r.blocks for r in adm], [r.cached for r in adm],
+                                   greedy=greedy)
+                first = out.tolist() if greedy else self._sample_rows(out, [r.params for r in adm])
         except Exception as e:  # noqa: BLE001
             for r in adm:
                 eng.release(r.res)

@@ -72,6 +72,13 @@ class LlamaConfig:
             return LlamaConfig(name=name, vocab_size=32000, hidden=2048, intermediate=8192,
                                layers=4, heads=16, kv_heads=4, max_position=4096,
                                bos_token_id=1, eos_token_id=2)
+        if name == "test-tp8":
+            # Llama-3-70B's GQA shape (8 KV heads, 128-d heads) at toy width: every TP degree
+            # 1 / 2 / 4 / 8 shards it, so the TP=8 paths run in CPU and one-GPU tests; a vocab
+            # that is not a multiple of 8 x 256 exercises the padded last LM-head shard
+            return LlamaConfig(name=name, vocab_size=4000, hidden=1024, intermediate=2048,
+                               layers=2, heads=32, kv_heads=8, head_dim=128, max_position=2048,
+                               bos_token_id=1, eos_token_id=2)
         if name == "tiny":
             return LlamaConfig(name="tiny", vocab_size=4096, hidden=256, intermediate=512,
                                layers=2, heads=4, kv_heads=2, head_dim=128, max_position=2048,
@@ -124,7 +131,13 @@ class LlamaModel:
         self.hkv = cfg.kv_heads // self.tp
         self.inter = cfg.intermediate // self.tp
         self.vocab_shard = (cfg.vocab_size + self.tp - 1) // self.tp
+        if self.tp > 1:
+            # whole 256-row tiles for the fused LM-head argmax kernel (mgemm.hip); the padded
+            # rows (ids >= vocab_size, on the last rank only) are zero and never picked
+            self.vocab_shard = (self.vocab_shard + 255) // 256 * 256
         self.vocab_start = self.tp_rank * self.vocab_shard
+        # ids this rank's LM-head shard holds
+        self.vocab_valid = max(0, min(cfg.vocab_size - self.vocab_start, self.vocab_shard))
         self.scale = 1.0 / math.sqrt(cfg.head_dim)
         self.cos_sin = ops.rope_cos_sin(cfg.max_position, cfg.head_dim, cfg.rope_theta, self.device,
                                         scaling=cfg.rope_scaling)
@@ -148,6 +161,8 @@ class LlamaModel:
         self.embed = w(cfg.vocab_size, H)
         self.final_norm = torch.ones(H, device=dev, dtype=dt)
         self.lm_head = w(self.vocab_shard, H)
+        if self.vocab_valid < self.vocab_shard:
+            self.lm_head[self.vocab_valid:] = 0
         out_std = std / math.sqrt(2 * cfg.layers)
         for _ in range(cfg.layers):
             self.layers.append({
@@ -235,18 +250,18 @@ class LlamaModel:
         residual = h
         x = ops.rmsnorm(h, self.layers[0]["in_norm"], eps)
         nl = len(self.layers)
-        # decode steps stream every weight once for <= 128 rows: skinny ring GEMM; at TP=1
-        # its split-K combine is fused into the consumer (rope / add_rmsnorm), so QKV, O
-        # and down leave fp32 partial slabs instead of a bf16 tensor + a reduce launch
+        # decode steps stream every weight once: per projection the mid-M MFMA GEMM
+        # (mgemm.hip, 129..512 rows where it wins -- ops.mid_plan) or the skinny
+        # weight-streaming kernel (dgemm.hip, <= 192 rows -- ops.decode_plan) emits fp32
+        # split-K slabs straight into the fused consumers: RoPE + KV write for QKV, and for the
+        # row-parallel O / down the (TP all-reduce +) residual add + RMSNorm
+        # (comm.tp_add_rmsnorm); split 0 = library GEMM + plain consumer.  Prefill (large M):
+        # the 256 x 256 MFMA GEMM (pgemm.hip) with SwiGLU fused into the gate|up epilogue.
         decode = not meta.prefill
-        lin = ops.decode_linear if decode else F.linear
+        lin = ops.decode_linear if decode else ops.prefill_linear
         M = x.shape[0]
-        # decode projections, per projection: the mid-M MFMA GEMM (mgemm.hip, 129..512 rows
-        # where it wins -- ops.mid_plan) or the skinny weight-streaming kernel (dgemm.hip,
-        # <= 192 rows -- ops.decode_plan) emit split-K slabs into the fused consumers
-        # (rope_cache_splitk / add_rmsnorm_splitk); split 0 = library GEMM + plain consumer
         plans = {}
-        if decode and self.tp == 1 and self.layers:
+        if decode and self.layers:
             L0 = self.layers[0]
             for k in ("qkv", "o", "down"):
                 S, c = ops.mid_plan(M, *L0[k].shape)
@@ -259,7 +274,7 @@ class LlamaModel:
             Sg, cg = ops.mid_plan(M, *L0["gate_up"].shape, glu=True)
             glu = (lambda a, w: ops.mgemm_glu(a, w, cg)) if Sg else ops.glu_linear
         else:
-            glu = ops.glu_linear
+            glu = ops.prefill_glu
         sq, qkv_part = plans.get("qkv", (0, None))
         so, o_part = plans.get("o", (0, None))
         sd, down_part = plans.get("down", (0, None))
@@ -321,39 +336,49 @@ class LlamaModel:
             else:
                 a = ops.paged_decode(qkv, kc, vc, meta.block_tables, meta.context_lens, hq,
                                      meta.max_context, self.scale, meta.seq_order)
-            if so:
-                x = ops.add_rmsnorm_splitk(o_part(a, L["o"]), residual, L["post_norm"], eps)
-            else:
-                o = comm.tp_all_reduce(lin(a, L["o"]))
-                x = ops.add_rmsnorm(o, residual, L["post_norm"], eps)
-            if decode:
-                g = glu(x, L["gate_up"])
-            else:
-                g = ops.silu_mul(F.linear(x, L["gate_up"]), interleaved=True)
+            # row-parallel O: (TP all-reduce +) residual add + RMSNorm in one consumer
+            x = comm.tp_add_rmsnorm(o_part(a, L["o"]) if so else lin(a, L["o"]), residual, L["post_norm"], eps)
+            g = glu(x, L["gate_up"])
             nxt = self.layers[i + 1]["in_norm"] if i + 1 < nl else self.final_norm
-            if sd:
-                x = ops.add_rmsnorm_splitk(down_part(g, L["down"]), residual, nxt, eps)
-            else:
-                m = comm.tp_all_reduce(lin(g, L["down"]))
-                x = ops.add_rmsnorm(m, residual, nxt, eps)
+            x = comm.tp_add_rmsnorm(down_part(g, L["down"]) if sd else lin(g, L["down"]), residual, nxt, eps)
         if logits_index is not None:
             x = x.index_select(0, logits_index)
         if greedy_ids:
-            if self.tp == 1 and ops.lm_head_argmax_ok(x.shape[0], *self.lm_head.shape):
+            return self.greedy_ids(x)
+        return ops.prefill_linear(x, self.lm_head) if x.shape[0] > 512 else F.linear(x, self.lm_head)
+
+    def greedy_ids(self, x: torch.Tensor) -> torch.Tensor:
+        """Greedy token ids int64 [R] of the final normed hidden rows ``x``: the LM-head GEMM
+        with its argmax fused (mgemm.hip EPI_ARGMAX, no [R, vocab] logits) where the shape
+        allows, the vocab-parallel pick resolved by one packed-key MAX all-reduce at TP > 1."""
+        R = x.shape[0]
+        N, K = self.lm_head.shape
+        fused = ops.lm_head_argmax_ok(R, N, K) or (self.tp > 1 and 0 < R <= ops.MID_M_MAX
+                                                   and ops.lm_head_argmax_shape_ok(N, K))
+        if self.tp == 1:
+            if fused:
                 return ops.lm_head_argmax(x, self.lm_head, self.cfg.vocab_size)
             return self.greedy(F.linear(x, self.lm_head))
-        return F.linear(x, self.lm_head)
+        if fused and self.vocab_valid > 0:
+            ids, vals = ops.lm_head_argmax(x, self.lm_head, self.vocab_valid, with_values=True)
+        else:
+            logits = F.linear(x, self.lm_head)[:, : max(1, self.vocab_valid)]
+            ids = ops.argmax(logits)
+            vals = logits.gather(1, ids[:, None])[:, 0].float()
+        if self.vocab_valid == 0:
+            vals = torch.full_like(vals, float("-inf"))
+        return comm.tp_argmax(vals, ids + self.vocab_start)
 
     def greedy(self, logits: torch.Tensor) -> torch.Tensor:
         """argmax over the (possibly vocab-parallel) logits -> int64 [R]."""
         if self.tp == 1:
             return ops.argmax(logits)
-        idx = ops.argmax(logits)
-        val = logits.gather(1, idx[:, None]).float()
-        pair = torch.cat([val, (idx + self.vocab_start).float()[:, None]], dim=1)  # [R, 2]
-        allp = comm.tp_all_gather_last(pair).view(pair.shape[0], self.tp, 2)
-        best = allp[..., 0].argmax(dim=1)
-        return allp[torch.arange(pair.shape[0], device=pair.device), best, 1].long()
+        valid = logits[:, : max(1, self.vocab_valid)]
+        idx = ops.argmax(valid)
+        val = valid.gather(1, idx[:, None])[:, 0].float()
+        if self.vocab_valid == 0:
+            val = torch.full_like(val, float("-inf"))
+        return comm.tp_argmax(val, idx + self.vocab_start)
 
     def full_logits(self, logits: torch.Tensor) -> torch.Tensor:
         full = comm.tp_all_gather_last(logits)

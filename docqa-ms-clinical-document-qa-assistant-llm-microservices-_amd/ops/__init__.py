@@ -287,19 +287,71 @@ def mgemm_glu(x, w_il, cfg: int = 0):
     return silu_mul(torch.nn.functional.linear(x, w_il), interleaved=True)
 
 
+# ----------------------------------------------------------------------------- prefill GEMM
+_PGEMM_OFF = os.environ.get("DOCQA_PGEMM", "1") == "0"
+# below this many 256 x 256 tiles the 128 x 128 encoder GEMM (gemm.hip, 4x the workgroups)
+# fills the chip better (scripts/pgemm_probe.py)
+_PGEMM_MIN_TILES = int(os.environ.get("DOCQA_PGEMM_MIN_TILES", "128"))
+
+
+def pgemm_ok(M: int, N: int, K: int) -> bool:
+    """Shapes the prefill GEMM (csrc/kernels/pgemm.hip) takes: N % 256, K % 128, 32-bit
+    row offsets, and enough 256 x 256 tiles to fill the chip."""
+    return (not _PGEMM_OFF and M > 0 and N % 256 == 0 and K % 128 == 0
+            and max(M, N) * K * 2 < (1 << 32) and ((M + 255) // 256) * (N // 256) >= _PGEMM_MIN_TILES)
+
+
+def prefill_linear(x, w):
+    """x @ w^T for the prefill projections (M = packed prompt tokens) on the hand-written
+    MFMA GEMMs: the 256 x 256 8-phase kernel (pgemm.hip) where it has enough tiles, else
+    the 128 x 128 kernel (gemm.hip); hipBLASLt only for shapes neither takes."""
+    if _gpu(x):
+        N, K = w.shape
+        M = x.numel() // K
+        if pgemm_ok(M, N, K):
+            return _native().pgemm(x.contiguous(), w, 0)
+        if N % 128 == 0 and K % 64 == 0:
+            return _native().gemm(x.contiguous(), w, None, None, EPI_NONE)
+    return torch.nn.functional.linear(x, w)
+
+
+def prefill_glu(x, w_il):
+    """silu(x Wg^T) * (x Wu^T) for 8-interleaved gate|up weights at prefill sizes: SwiGLU
+    fused into the 256 x 256 GEMM's epilogue (no [M, 2I] round trip through HBM)."""
+    if _gpu(x):
+        N, K = w_il.shape
+        M = x.numel() // K
+        if pgemm_ok(M, N, K):
+            return _native().pgemm(x.contiguous(), w_il, 1)
+        if N % 128 == 0 and K % 128 == 0:
+            return _native().mgemm_glu(x.contiguous(), w_il, 2)
+    return silu_mul(prefill_linear(x, w_il), interleaved=True)
+
+
 # LM head: 256-wide tiles (mgemm.hip cfg 6) halve the X re-reads of the 1002-tile vocab
 # sweep -- 281 vs 326 us with the argmax fused at M = 256 (profiles/r2_mgemm_probe_m256_v6.log)
 _LM_CFG = int(os.environ.get("DOCQA_LM_HEAD_CFG", "6"))
 
 
-def lm_head_argmax(x, w, n_valid: int, cfg: int = -1):
+def lm_head_argmax(x, w, n_valid: int, cfg: int = -1, with_values: bool = False):
     """Greedy token ids argmax(bf16(x @ w[:n_valid]^T)) with the LM-head GEMM and the argmax
-    fused (mgemm.hip EPI_ARGMAX): the [M, vocab] logits never reach HBM."""
+    fused (mgemm.hip EPI_ARGMAX): the [M, vocab] logits never reach HBM.  ``with_values``:
+    (ids, picked logit fp32) -- a vocab-parallel shard's candidates for comm.tp_argmax."""
     if _gpu(x):
         if cfg < 0:
             cfg = _LM_CFG if w.shape[0] % 256 == 0 else _MID_CFG
+        if with_values:
+            return _native().mgemm_argmax_val(x.contiguous(), w, int(n_valid), cfg)
         return _native().mgemm_argmax(x.contiguous(), w, int(n_valid), cfg)
-    return ref.argmax(torch.nn.functional.linear(x, w[:n_valid]))
+    logits = torch.nn.functional.linear(x, w[:n_valid])
+    ids = ref.argmax(logits)
+    if with_values:
+        return ids, logits.gather(1, ids[:, None])[:, 0].float()
+    return ids
+
+
+def lm_head_argmax_shape_ok(N: int, K: int) -> bool:
+    return not _MID_OFF and N % 128 == 0 and K % 128 == 0
 
 
 def lm_head_argmax_ok(M: int, N: int, K: int) -> bool:
@@ -339,7 +391,8 @@ def rope_cache_splitk(P, positions, cos_sin, slot_mapping, k_cache, v_cache, Hq,
         if slot_mapping is None:
             k_cache = v_cache = P
         return _native().rope_cache_splitk(P, positions, cos_sin, slot_mapping, k_cache, v_cache, Hq, Hkv, D)
-    qkv = P.sum(0).to(torch.bfloat16)
+    # the model dtype: bf16 on the GPU path, fp32 for CPU reference models
+    qkv = P.sum(0).to(k_cache.dtype if slot_mapping is not None else torch.bfloat16)
     ref.rope_cache(qkv, positions, cos_sin, slot_mapping, k_cache, v_cache, Hq, Hkv, D)
     return qkv
 

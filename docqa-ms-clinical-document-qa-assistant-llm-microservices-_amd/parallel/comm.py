@@ -93,6 +93,9 @@ def init_distributed(tp_size: int = 1, backend: str | None = None, timeout_s: in
     _STATE = ParallelState(rank=rank, world_size=world, local_rank=local_rank, tp_size=tp_size,
                            tp_rank=rank % tp_size, dp_size=dp_size, dp_rank=rank // tp_size,
                            tp_group=tp_group, dp_group=dp_group, backend=backend)
+    if tp_size > 1 and backend == "nccl" and os.environ.get("DOCQA_CUSTOM_AR", "1") == "1":
+        # every TP group sets up its IPC all-reduce at once (collective within the group)
+        enable_custom_all_reduce()
     return _STATE
 
 
@@ -104,16 +107,33 @@ def set_state(s: ParallelState) -> None:
 _CUSTOM_AR = None
 
 
-def enable_custom_all_reduce(max_bytes: int = 8 << 20, force: bool = False):
-    """Use the one-shot IPC all-reduce (parallel/custom_ar.py) for TP all-reduces that fit
-    ``max_bytes`` (bf16, contiguous); RCCL keeps everything else.  Opt-in
-    (DOCQA_CUSTOM_AR=1 in bench.py): validated 2-rank on one GPU, not yet on a multi-GPU
-    node."""
+def enable_custom_all_reduce(max_bytes: int | None = None, force: bool = False):
+    """Route the TP all-reduces through the IPC all-reduce (parallel/custom_ar.py: one-shot /
+    two-shot over all xGMI links, residual + RMSNorm fused) for every message that fits
+    ``max_bytes`` (default 64 MB, env DOCQA_AR_MAX_MB); RCCL keeps everything else.  Called
+    by ``init_distributed`` at TP > 1 on RCCL unless DOCQA_CUSTOM_AR=0; a failed IPC mapping
+    or self-test leaves RCCL in charge (returns None)."""
     global _CUSTOM_AR
     s = _STATE
     if s.tp_size > 1 and (s.backend == "nccl" or force) and _CUSTOM_AR is None:
         from .custom_ar import CustomAllReduce
-        _CUSTOM_AR = CustomAllReduce(group=s.tp_group, max_bytes=max_bytes)
+        if max_bytes is None:
+            max_bytes = int(os.environ.get("DOCQA_AR_MAX_MB", "64")) << 20
+        car = None
+        try:
+            car = CustomAllReduce(group=s.tp_group, max_bytes=max_bytes)
+            ok = car.self_test()
+        except Exception as e:  # pragma: no cover - depends on the node's IPC support
+            print(f"[comm] custom all-reduce unavailable ({e}); using RCCL", flush=True)
+            ok = False
+        if ok:
+            _CUSTOM_AR = car
+        elif car is not None:
+            car.close()
+    return _CUSTOM_AR
+
+
+def custom_all_reduce():
     return _CUSTOM_AR
 
 
@@ -124,6 +144,46 @@ def tp_all_reduce(t: torch.Tensor) -> torch.Tensor:
             return _CUSTOM_AR.all_reduce(t)
         dist.all_reduce(t, group=s.tp_group)
     return t
+
+
+def tp_add_rmsnorm(x: torch.Tensor, residual: torch.Tensor, w: torch.Tensor, eps: float) -> torch.Tensor:
+    """The end of a row-parallel projection: residual <- residual + sum over the TP group of
+    ``x`` (a bf16 partial [M, H] or the GEMM's fp32 split-K slabs [S, M, H]), returns
+    rmsnorm(residual) * w.  TP = 1: the fused split-K consumer / add_rmsnorm kernel; TP > 1:
+    one launch of the IPC all-reduce with the add + norm in its epilogue, else RCCL
+    all-reduce + add_rmsnorm."""
+    from .. import ops
+
+    slabs = x.dim() == residual.dim() + 1     # split-K slabs [S, M, H] vs a partial [M, H]
+    s = _STATE
+    if s.tp_size == 1:
+        return ops.add_rmsnorm_splitk(x, residual, w, eps) if slabs else ops.add_rmsnorm(x, residual, w, eps)
+    if _CUSTOM_AR is not None and _CUSTOM_AR.supports(x):
+        return _CUSTOM_AR.reduce_add_rmsnorm(x, residual, w, eps)
+    y = x.sum(0).to(residual.dtype) if slabs else x.contiguous()
+    dist.all_reduce(y, group=s.tp_group)
+    return ops.add_rmsnorm(y, residual, w, eps)
+
+
+def tp_argmax(vals: torch.Tensor, ids: torch.Tensor) -> torch.Tensor:
+    """Greedy pick over a vocab-parallel LM head: each rank's row-best (value, global id) ->
+    the group's best id, ties to the lowest id (torch.argmax order) -- one int64 MAX
+    all-reduce of packed keys [order-preserving value bits | ~id] instead of gathering
+    [B, vocab] logits or (value, id) pairs."""
+    s = _STATE
+    v = vals.float().contiguous().view(torch.int32).to(torch.int64)
+    ordered = torch.where(v >= 0, v, v ^ 0x7FFFFFFF)          # int32 range, monotonic in the float
+    key = ordered * (1 << 32) + ((1 << 32) - 1 - ids.to(torch.int64))   # exact in int64
+    if s.tp_size > 1:
+        if _CUSTOM_AR is not None and key.is_cuda and key.numel() % 2 == 0:
+            # IPC all-gather of the [R] keys + a local max: graph-capturable on any backend
+            key = _CUSTOM_AR.all_gather_raw(key).max(dim=0).values
+        elif _CUSTOM_AR is not None and key.is_cuda:
+            pad = torch.cat([key, key[:1]])
+            key = _CUSTOM_AR.all_gather_raw(pad).max(dim=0).values[: key.numel()]
+        else:
+            dist.all_reduce(key, op=dist.ReduceOp.MAX, group=s.tp_group)
+    return (1 << 32) - 1 - torch.remainder(key, 1 << 32)
 
 
 def tp_all_gather_last(t: torch.Tensor) -> torch.Tensor:

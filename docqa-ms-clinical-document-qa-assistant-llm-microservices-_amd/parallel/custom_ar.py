@@ -1,26 +1,38 @@
-"""One-shot all-reduce over IPC-mapped peer memory (csrc/kernels/allreduce.hip) for the
-tensor-parallel decode all-reduces: every rank reads all peers' staging buffers at once
-over xGMI's point-to-point links instead of a ring's 2(N-1) dependent hops.
+"""Tensor-parallel all-reduce over IPC-mapped peer memory (csrc/kernels/allreduce.hip) with
+the residual add + RMSNorm that follows every row-parallel projection fused in.
 
-Setup (once per TP group): each rank allocates an uncached staging+flag region, exports
+Every rank reads its peers' staging buffers directly, so all 7 xGMI links of an MI355X
+carry data at once instead of a ring's one link per step:
+  * one-shot (messages <= ``oneshot_max_bytes``, latency-bound decode all-reduces): each
+    rank sums all N staging buffers itself -- one cross-rank barrier;
+  * two-shot (larger messages: decode at big batch, prefill): reduce-scatter of column
+    chunks + all-gather -- 2 (N-1)/N of the message over xGMI instead of N-1.
+The split-K fp32 slabs of the decode GEMMs go in directly (summed in registers on the
+way into the staging buffer), so a row-parallel projection costs one GEMM launch and one
+all-reduce launch that already writes the next layer's normed input.
+
+Setup (once per TP group): each rank allocates an uncached staging + flag region, exports
 its HIP IPC handle, the handles are exchanged with ``all_gather_object`` over the group,
-and every rank maps its peers' regions.  ``all_reduce(x)`` is then one kernel launch
-(HIP-graph capturable: the barrier epochs live in device memory).  Payloads above
-``max_bytes``, non-bf16 tensors and CPU tensors go to RCCL (torch.distributed).
+and every rank maps its peers' regions; a self-test all-reduce then checks the mapping
+before the caller relies on it (parallel/comm.py falls back to RCCL otherwise).  Calls are
+HIP-graph capturable: the call epoch lives in device memory.
 
 Reference parity: none (the reference has no collectives); this is the
 custom all-reduce of SURVEY.md §2.3 / §5.8.
 """
 from __future__ import annotations
 
+import os
+
 import torch
 import torch.distributed as dist
 
-_MAX_WG = 128
+ONESHOT, TWOSHOT, GATHER = 0, 1, 2
 
 
 class CustomAllReduce:
-    def __init__(self, group=None, max_bytes: int = 8 << 20, device=None):
+    def __init__(self, group=None, max_bytes: int = 64 << 20, device=None,
+                 oneshot_max_bytes: int | None = None):
         from .. import ops
 
         ops.load_native()
@@ -29,16 +41,17 @@ class CustomAllReduce:
         self.rank = dist.get_rank(group)
         self.world = dist.get_world_size(group)
         if self.world > 8:
-            raise ValueError("one-shot all-reduce supports up to 8 ranks (one xGMI hive)")
+            raise ValueError("the IPC all-reduce supports up to 8 ranks (one xGMI hive)")
         self.device = torch.device(device or f"cuda:{torch.cuda.current_device()}")
         self.max_elems = max_bytes // 2 // 8 * 8
-        nbytes = self.nat.ar_region_bytes(self.max_elems)
-        self.own = self.nat.ar_alloc(nbytes)
+        if oneshot_max_bytes is None:
+            oneshot_max_bytes = int(os.environ.get("DOCQA_AR_ONESHOT_MAX", str(256 << 10)))
+        self.oneshot_max_bytes = oneshot_max_bytes
+        self.own = self.nat.ar_alloc(self.nat.ar_region_bytes(self.max_elems))
         handle = self.nat.ar_ipc_handle(self.own)
         handles = [None] * self.world
         dist.all_gather_object(handles, handle.tolist(), group=group)
-        self.regions = []
-        self._opened = []
+        self.regions, self._opened = [], []
         for r, h in enumerate(handles):
             if r == self.rank:
                 self.regions.append(self.own)
@@ -46,17 +59,82 @@ class CustomAllReduce:
                 p = self.nat.ar_ipc_open(torch.tensor(h, dtype=torch.uint8))
                 self._opened.append(p)
                 self.regions.append(p)
-        self.epochs = torch.zeros(_MAX_WG, dtype=torch.int32, device=self.device)
+        self.ctr = torch.zeros(2, dtype=torch.int32, device=self.device)
         self.err = torch.zeros(1, dtype=torch.int32, device=self.device)
         dist.barrier(group=group)
 
-    def supports(self, t: torch.Tensor) -> bool:
-        return (t.is_cuda and t.dtype == torch.bfloat16 and t.is_contiguous()
-                and t.numel() % 8 == 0 and t.numel() <= self.max_elems)
+    # ------------------------------------------------------------------ capability
+    def _fits(self, M: int, H: int, mode: int) -> bool:
+        return M * H <= self.max_elems and H % 8 == 0 and (mode == ONESHOT or H % (8 * self.world) == 0)
 
-    def all_reduce(self, t: torch.Tensor) -> torch.Tensor:
-        """Sum of ``t`` over the group (a new tensor; ``t`` is not modified)."""
-        return self.nat.ar_oneshot(t, self.rank, self.regions, self.max_elems, self.epochs, self.err)
+    def mode_for(self, M: int, H: int) -> int:
+        return ONESHOT if M * H * 2 <= self.oneshot_max_bytes or H % (8 * self.world) else TWOSHOT
+
+    def supports(self, t: torch.Tensor) -> bool:
+        if not (t.is_cuda and t.is_contiguous() and t.dim() >= 1):
+            return False
+        H = t.shape[-1]
+        if t.dtype == torch.bfloat16:
+            M = t.numel() // H
+        elif t.dtype == torch.float32 and t.dim() == 3:   # split-K slabs [S, M, H]
+            M = t.shape[1]
+        else:
+            return False
+        return self._fits(M, H, self.mode_for(M, H))
+
+    # ------------------------------------------------------------------ collectives
+    def all_reduce(self, t: torch.Tensor, mode: int | None = None) -> torch.Tensor:
+        """Sum of ``t`` (bf16 [.., H] or fp32 slabs [S, M, H]) over the group: a new bf16
+        tensor; ``t`` is not modified."""
+        slabs = t.dtype == torch.float32
+        H = t.shape[-1]
+        M = t.shape[1] if slabs else t.numel() // H
+        mode = self.mode_for(M, H) if mode is None else mode
+        return self.nat.ar_run(t, slabs, None, None, 0.0, self.rank, self.regions, self.max_elems, mode,
+                               self.ctr, self.err)
+
+    def reduce_add_rmsnorm(self, t: torch.Tensor, residual: torch.Tensor, w: torch.Tensor, eps: float,
+                           mode: int | None = None) -> torch.Tensor:
+        """residual <- residual + allreduce(t) (in place, bf16); returns rmsnorm(residual) * w
+        -- ops.add_rmsnorm over the group's summed partials in one launch."""
+        slabs = t.dtype == torch.float32
+        H = t.shape[-1]
+        M = t.shape[1] if slabs else t.numel() // H
+        mode = self.mode_for(M, H) if mode is None else mode
+        return self.nat.ar_run(t, slabs, residual, w, float(eps), self.rank, self.regions, self.max_elems,
+                               mode, self.ctr, self.err)
+
+    def all_gather_raw(self, t: torch.Tensor) -> torch.Tensor:
+        """All-gather of any contiguous GPU tensor whose byte size is a multiple of 16:
+        [world, *t.shape], bit-exact (the payload travels as raw 16-bit words) -- the
+        vocab-parallel LM head's (value, id) candidates inside a captured decode graph."""
+        nb = t.numel() * t.element_size()
+        if nb % 16 or nb // 2 > self.max_elems:
+            raise ValueError("all_gather_raw: payload must be a multiple of 16 bytes and fit the staging area")
+        words = t.contiguous().view(torch.bfloat16).view(1, nb // 2)
+        out = self.nat.ar_run(words, False, None, None, 0.0, self.rank, self.regions, self.max_elems, GATHER,
+                              self.ctr, self.err)
+        return out.view(t.dtype).view(self.world, *t.shape)
+
+    def self_test(self) -> bool:
+        """Both modes on a small tensor against the exact sum; False on any mismatch or a
+        peer that never arrived (every rank runs it collectively)."""
+        ok = True
+        for mode in (ONESHOT, TWOSHOT):
+            H = 8 * self.world * 4
+            x = torch.full((3, H), float(self.rank + 1), device=self.device, dtype=torch.bfloat16)
+            y = self.all_reduce(x, mode)
+            torch.cuda.synchronize(self.device)
+            ok = ok and bool(torch.all(y.float() == self.world * (self.world + 1) / 2))
+        ids = torch.arange(4, device=self.device, dtype=torch.int64) + 1000 * self.rank
+        gat = self.all_gather_raw(ids)
+        ok = ok and bool(torch.equal(gat.cpu(), torch.arange(4).repeat(self.world, 1)
+                                     + 1000 * torch.arange(self.world)[:, None]))
+        ok = ok and int(self.err.item()) == 0
+        on_gpu = dist.get_backend(self.group) != "gloo"
+        flag = torch.tensor([1 if ok else 0], dtype=torch.int32, device=self.device if on_gpu else "cpu")
+        dist.all_reduce(flag, op=dist.ReduceOp.MIN, group=self.group)
+        return bool(flag.item())
 
     def check(self) -> None:
         if int(self.err.item()):

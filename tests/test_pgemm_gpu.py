@@ -1,0 +1,68 @@
+"""Prefill GEMM (csrc/kernels/pgemm.hip: 256 x 256 x 64 8-phase MFMA schedule, LDS-DMA
+half-tiles, staggered wave rows) against the fp32 PyTorch reference of the same op,
+bf16 out and the fused SwiGLU epilogue over 8-interleaved gate|up rows."""
+import pytest
+import torch
+
+from docqa_amd import ops
+from docqa_amd.ops import reference as ref
+
+pytestmark = pytest.mark.gpu
+
+SHAPES = [  # (M, N, K): tails in M, one K-tile pair, deep K, Llama-3-8B / 70B-TP8 shapes
+    (256, 256, 128), (1, 256, 256), (300, 512, 256), (1000, 1280, 1024), (2048, 6144, 4096),
+    (513, 4096, 14336), (4096, 1024, 3584),
+]
+
+
+def _data(M, N, K, seed=0):
+    g = torch.Generator(device="cuda").manual_seed(seed)
+    x = torch.randn(M, K, device="cuda", generator=g).to(torch.bfloat16)
+    w = (torch.randn(N, K, device="cuda", generator=g) / K ** 0.5).to(torch.bfloat16)
+    return x, w
+
+
+@pytest.mark.parametrize("M,N,K", SHAPES)
+def test_pgemm_bf16_matches_fp32_reference(M, N, K):
+    assert ops.load_native()
+    x, w = _data(M, N, K)
+    y = torch.ops.docqa.pgemm(x, w, 0)
+    r = x.float() @ w.float().t()
+    assert y.shape == (M, N) and y.dtype == torch.bfloat16
+    err = (y.float() - r).abs().max().item()
+    assert err <= 2e-2 * r.abs().max().item() + 1e-3, err
+
+
+@pytest.mark.parametrize("M,N,K", [(256, 256, 128), (777, 1024, 512), (2048, 28672 // 8, 4096)])
+def test_pgemm_swiglu_epilogue(M, N, K):
+    x, w = _data(M, N, K, seed=1)
+    y = torch.ops.docqa.pgemm(x, w, 1)
+    r = ref.silu_mul((x.float() @ w.float().t()), interleaved=True).float()
+    assert y.shape == (M, N // 2)
+    err = (y.float() - r).abs().max().item()
+    assert err <= 2e-2 * r.abs().max().item() + 1e-3, err
+
+
+def test_pgemm_asymmetric_exact_small_ints():
+    """Integer-valued operands (exact in bf16 and fp32): every output element must be exact,
+    which catches a transposed or mis-placed C write that random data might blur."""
+    M, N, K = 512, 768, 256
+    g = torch.Generator(device="cuda").manual_seed(3)
+    x = torch.randint(-3, 4, (M, K), device="cuda", generator=g).to(torch.bfloat16)
+    w = torch.randint(-2, 3, (N, K), device="cuda", generator=g).to(torch.bfloat16)
+    w[:, 0] = torch.arange(N, device="cuda").remainder(7).to(torch.bfloat16)   # asymmetric in N
+    y = torch.ops.docqa.pgemm(x, w, 0).float()
+    r = (x.float() @ w.float().t()).to(torch.bfloat16).float()   # exact sums, one rounding
+    assert torch.equal(y, r)
+
+
+def test_prefill_dispatch_routes_to_hand_written_kernels():
+    x, w = _data(4096, 4096, 1024, seed=4)
+    assert ops.pgemm_ok(4096, 4096, 1024)
+    y = ops.prefill_linear(x, w)
+    r = x.float() @ w.float().t()
+    assert (y.float() - r).abs().max().item() <= 2e-2 * r.abs().max().item()
+    xs, ws = _data(40, 384, 256, seed=5)   # few tiles: the 128 x 128 kernel
+    ys = ops.prefill_linear(xs, ws)
+    rs = xs.float() @ ws.float().t()
+    assert (ys.float() - rs).abs().max().item() <= 2e-2 * rs.abs().max().item()

@@ -1,6 +1,8 @@
-"""Tensor-parallel Llama on GPU kernels (TP=2, both ranks on the 1-GPU box's cuda:0):
-column/row-parallel projections on the decode GEMM kernels, the one-shot IPC all-reduce,
-vocab-parallel logits -- must match the TP=1 model's prefill and decode logits."""
+"""Tensor-parallel Llama on GPU kernels (TP=2 and TP=4, every rank on the 1-GPU box's
+cuda:0): column/row-parallel projections on the decode / prefill GEMM kernels, the IPC
+all-reduce with the residual + RMSNorm fused (one-shot at decode, two-shot at prefill),
+vocab-parallel logits and the packed-key greedy pick -- must match the TP=1 model's
+prefill and decode logits, and every rank must generate the same tokens."""
 import os
 import socket
 import subprocess
@@ -22,7 +24,8 @@ def _port():
     return p
 
 
-def test_tp2_matches_tp1(tmp_path):
+@pytest.mark.parametrize("preset,tp", [("llama3-1b-test", 2), ("test-tp8", 4)])
+def test_tp_matches_tp1(tmp_path, preset, tp):
     sys.path.insert(0, str(Path(__file__).resolve().parent))
     from test_models_gpu import _decode_logits, _prefill_logits, _rel
 
@@ -31,11 +34,12 @@ def test_tp2_matches_tp1(tmp_path):
     from docqa_amd.models.llama import LlamaConfig, LlamaModel
 
     assert ops.load_native()
-    m = LlamaModel(LlamaConfig.preset("llama3-1b-test"), device="cuda", seed=9)
+    cfg = LlamaConfig.preset(preset)
+    m = LlamaModel(cfg, device="cuda", seed=9)
     sd_path, out_path = tmp_path / "sd.pt", tmp_path / "out.pt"
     torch.save(m.export_state_dict_hf(), sd_path)
     g = torch.Generator().manual_seed(1)
-    prompts = [torch.randint(0, 32000, (n,), generator=g).tolist() for n in (9, 130, 300)]
+    prompts = [torch.randint(0, cfg.vocab_size, (n,), generator=g).tolist() for n in (9, 130, 300)]
     kv = KVCache(m.cfg.layers, 64, m.hkv, m.cfg.head_dim, 64).caches
     p1, tables = _prefill_logits(m, kv, prompts, 64)
     d1 = _decode_logits(m, kv, prompts, tables, [5, 6, 7], 64)
@@ -44,11 +48,14 @@ def test_tp2_matches_tp1(tmp_path):
     env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0")
     for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK"):
         env.pop(k, None)
-    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(tp),
            "--master-addr", "127.0.0.1", "--master-port", str(_port()), str(ROOT / "tests" / "tp_gpu_worker.py"),
-           str(sd_path), str(out_path)]
+           str(sd_path), str(out_path), preset, str(tp)]
     r = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=600, env=env)
     assert r.returncode == 0, (r.stdout[-2000:], r.stderr[-4000:])
     out = torch.load(out_path, weights_only=True)
     assert _rel(out["prefill"], p1.float().cpu()) < 0.03
     assert _rel(out["decode"], d1.float().cpu()) < 0.03
+    toks = [torch.load(f"{out_path}.tok{r}", weights_only=True) for r in range(tp)]
+    assert all(t == toks[0] for t in toks[1:])
+    assert all(0 <= x < cfg.vocab_size for row in toks[0] for x in row)
