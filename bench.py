@@ -6,7 +6,7 @@ One step = one batch of ``--batch`` clinical questions per data-parallel rank, p
 through the whole llm-qa path: WordPiece tokenise -> MiniLM-L6 embed (HIP encoder
 kernels) -> kNN top-3 over the sharded flat L2 index (HIP MFMA distance+top-k, RCCL
 all-gathers across ranks) -> stuff prompt -> Llama-3-8B bf16 prefill + greedy decode
-of ``--max-new-tokens`` tokens (HIP attention/norm/rope kernels, hipBLASLt GEMMs,
+of ``--max-new-tokens`` tokens (hand-written HIP GEMM / attention / norm / rope kernels,
 HIP-graph decode loop) -> detokenise.  Synthetic clinical notes + random-init weights
 of the named architectures (no checkpoints or datasets are reachable).
 
@@ -80,8 +80,8 @@ def main() -> None:
     ps = comm.init_distributed(tp_size=a.tp, backend=None if cuda else "gloo")
     if cuda:
         assert ops.load_native(), "native HIP kernels not built (python -m docqa_amd.ops.build)"
-        if a.tp > 1 and os.environ.get("DOCQA_CUSTOM_AR", "0") == "1":
-            comm.enable_custom_all_reduce()
+        # TP > 1: init_distributed already set up the IPC all-reduce (fused residual + RMSNorm,
+        # one-/two-shot over all xGMI links) unless DOCQA_CUSTOM_AR=0; RCCL otherwise
     dev = f"cuda:{local_rank}" if cuda else "cpu"
 
     def sync():

@@ -14,7 +14,8 @@ the HIP kernels) and adds the chunks to its local shard of the flat L2 index.
 Stage 2 (QA, timed): batches of questions -> query embed -> sharded kNN (each GPU scans
 its shard with the fused MFMA distance + top-k kernel; the per-shard top-k is merged with
 one all-gather on a dedicated process group) -> RAG prompt -> TP generation (column /
-row-parallel projections, RCCL all-reduce, HIP-graph decode).
+row-parallel projections, the IPC all-reduce with residual + RMSNorm fused (RCCL when IPC
+mapping is unavailable), HIP-graph decode).
 Synthetic notes + random-init weights of the named architectures.  Rank 0 prints one
 JSON line.
 """
@@ -49,6 +50,8 @@ def main():
     ap.add_argument("--pipelined", action="store_true",
                     help="overlap batch i+1's embed/search with batch i's decode tail")
     ap.add_argument("--device", default="cuda")
+    ap.add_argument("--questions", choices=("unique", "repeat"), default="unique",
+                    help="unique: every request a distinct question; repeat: the small template grid")
     a = ap.parse_args()
 
     import torch
@@ -66,7 +69,7 @@ def main():
     from docqa_amd.pipeline.rag import RAGPipeline
     from docqa_amd.text.chunking import chunk_chars
     from docqa_amd.text.kb import synthetic_kb_records
-    from docqa_amd.text.synthetic import synthetic_notes, synthetic_questions
+    from docqa_amd.text.synthetic import synthetic_notes, synthetic_questions, synthetic_unique_questions
     from docqa_amd.text.tokenizer import ChatTokenizer, WordPieceTokenizer
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -156,7 +159,8 @@ def main():
     sync()
     setup_s = tmax(time.perf_counter() - t_setup)
     params = SamplingParams(max_new_tokens=a.max_new_tokens, temperature=0.0, stop_on_eos=False)
-    qs = synthetic_questions((a.warmup + a.steps) * ps.dp_size * a.batch, seed=321)
+    gen_q = synthetic_unique_questions if a.questions == "unique" else synthetic_questions
+    qs = gen_q((a.warmup + a.steps) * ps.dp_size * a.batch, seed=321)
 
     def batch_for(step: int) -> list[str]:
         base = (step * ps.dp_size + ps.dp_rank) * a.batch
@@ -204,7 +208,9 @@ def main():
                        "parallelism": f"tp{tp}" + (f"xdp{ps.dp_size}" if ps.dp_size > 1 else ""),
                        "index": f"flat-L2 sharded x{ps.world_size}", "index_vectors": len(all_records),
                        "notes": len(notes), "batch": a.batch, "max_new_tokens": a.max_new_tokens,
-                       "k": a.k, "pipelined": a.pipelined},
+                       "k": a.k, "pipelined": a.pipelined, "questions": a.questions,
+                       "tp_all_reduce": "ipc-fused" if comm.custom_all_reduce() is not None else
+                                        ("rccl" if tp > 1 and cuda else ("gloo" if tp > 1 else "none"))},
             "setup_s": round(setup_s, 1),
             "prefix_cached_frac": round(engine.stats.cached_tokens / max(1, engine.stats.prompt_tokens), 3),
         }

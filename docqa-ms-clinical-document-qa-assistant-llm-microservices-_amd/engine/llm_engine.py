@@ -209,6 +209,14 @@ class LLMEngine:
         if sw is not None and self.max_context > sw:
             raise ValueError(f"max_context {self.max_context} exceeds the model's sliding window {sw}: "
                              "the attention kernels attend to the whole context")
+        if getattr(model, "tp", 1) > 1:
+            # TP prefill all-reduces ([tokens, hidden] bf16) stay inside the IPC all-reduce's
+            # staging area (two-shot over all xGMI links) instead of falling back to RCCL
+            from ..parallel import comm
+            car = comm.custom_all_reduce()
+            if car is not None:
+                cap = car.max_elems // model.cfg.hidden // block_size * block_size
+                max_prefill_tokens = max(block_size, min(max_prefill_tokens, cap))
         self.max_prefill_tokens = max_prefill_tokens
         if num_blocks is None:
             num_blocks = max_batch * self.max_blocks_per_seq + 1

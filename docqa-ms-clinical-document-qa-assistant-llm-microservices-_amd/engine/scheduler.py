@@ -62,9 +62,35 @@ class Request:
     done: bool = False
 
 
+class Lockstep:
+    """Keeps the continuous-batching engines of every rank of a tensor-parallel group in
+    step: the group leader (TP rank 0, which serves HTTP) owns the request queue and the
+    timing-dependent admission decision; before every engine step it broadcasts the
+    requests that arrived since the last step and that decision over a CPU (gloo) group.
+    Everything else a step does -- KV reservation, prefix-cache hits, prefill, decode,
+    retirement on EOS -- is a deterministic function of that input and of the greedy ids,
+    which the vocab-parallel argmax makes identical on every rank, so the followers' TP
+    forwards always match the leader's.  While idle the leader sends a heartbeat every
+    ``heartbeat_s`` so the followers' receive never times out."""
+
+    def __init__(self, group, src: int, leader: bool, heartbeat_s: float = 1.0):
+        self.group, self.src, self.leader, self.heartbeat_s = group, src, leader, heartbeat_s
+        self.last = time.monotonic()
+
+    def exchange(self, msg=None):
+        import torch.distributed as dist
+
+        box = [msg]
+        dist.broadcast_object_list(box, src=self.src, group=self.group)
+        self.last = time.monotonic()
+        return box[0]
+
+
 class ContinuousEngine:
-    def __init__(self, engine: LLMEngine, max_running: int | None = None):
+    def __init__(self, engine: LLMEngine, max_running: int | None = None, lockstep: Lockstep | None = None):
         self.eng = engine
+        self.lockstep = lockstep
+        self._unsynced: list = []           # lockstep leader: arrivals not yet broadcast
         self.max_running = min(max_running or engine.max_batch, engine.max_batch)
         self.waiting: collections.deque[Request] = collections.deque()
         self.running: list[Request] = []
@@ -99,12 +125,14 @@ class ContinuousEngine:
             return fut
         r = Request(next(self._ids), list(prompt), params, fut, on_token, t_arrival=time.perf_counter())
         with self._cv:
-            self.waiting.append(r)
+            # a lockstep leader queues arrivals for the next step's broadcast, so the
+            # followers see exactly the waiting queue its admission sees
+            (self._unsynced if self.lockstep is not None else self.waiting).append(r)
             self._cv.notify()
         return fut
 
     def has_work(self) -> bool:
-        return bool(self.waiting or self.running or self._pending)
+        return bool(self.waiting or self.running or self._pending or self._unsynced)
 
     def generate(self, prompts: list[list[int]], params: SamplingParams | None = None) -> list[list[int]]:
         """Submit all prompts and drive the scheduler in this thread until they finish."""
@@ -176,12 +204,51 @@ class ContinuousEngine:
     # ------------------------------------------------------------------ one iteration
     @torch.inference_mode()
     def step(self) -> None:
-        self._admit()
+        decision = None
+        if self.lockstep is not None:
+            if not self.lockstep.leader:
+                raise RuntimeError("a lockstep follower runs follow(), not step()")
+            with self._cv:
+                new, self._unsynced = self._unsynced, []
+                self.waiting.extend(new)
+            decision = self._admission_due()
+            self.lockstep.exchange(("step", [(r.prompt, r.params) for r in new], decision))
+        self._step(decision)
+
+    def _step(self, decision) -> None:
+        self._admit(decision)
         if self.running:
             self._decode()
         elif self._pending is not None:
             p, self._pending = self._pending, None
             self._process(p)
+
+    # ------------------------------------------------------------------ lockstep (TP)
+    def heartbeat(self) -> None:
+        """Lockstep leader, idle: keep the followers' receive alive."""
+        ls = self.lockstep
+        if ls is not None and ls.leader and time.monotonic() - ls.last >= ls.heartbeat_s:
+            ls.exchange(("noop",))
+
+    def stop_followers(self) -> None:
+        if self.lockstep is not None and self.lockstep.leader:
+            self.lockstep.exchange(("stop",))
+
+    @torch.inference_mode()
+    def follow(self) -> None:
+        """Lockstep follower loop: mirror every step the leader broadcasts until "stop"."""
+        ls = self.lockstep
+        while True:
+            msg = ls.exchange()
+            if msg[0] == "stop":
+                return
+            if msg[0] != "step":
+                continue
+            _, specs, decision = msg
+            for prompt, params in specs:
+                self.waiting.append(Request(next(self._ids), list(prompt), params, cf.Future(),
+                                            t_arrival=time.perf_counter()))
+            self._step(decision)
 
     def _take_waiting(self) -> list[Request]:
         eng, alloc = self.eng, self.eng.kv.allocator
@@ -207,7 +274,9 @@ class ContinuousEngine:
                     break
         return admitted
 
-    def _admit(self) -> None:
+    def _admission_due(self) -> bool:
+        """Whether the waiting requests are admitted at this step (the timing-dependent
+        half of admission; a lockstep leader broadcasts it)."""
         if self.running and self.waiting:
             # gather a group -- one prefill pass over the weights for several requests --
             # until admit_min requests can join or the first of them has waited
@@ -219,12 +288,19 @@ class ContinuousEngine:
             now = time.perf_counter()
             if free <= 0:
                 self._free_t = None
-                return
+                return False
             if self._free_t is None:
                 self._free_t = now             # a slot just became free
             start = max(self.waiting[0].t_arrival, self._free_t)   # first admissible moment
             if min(len(self.waiting), free) < self.admit_min and now - start < self.admit_wait_s:
-                return
+                return False
+        return True
+
+    def _admit(self, decision: bool | None = None) -> None:
+        if decision is None:
+            decision = self._admission_due()
+        if not decision:
+            return
         adm = self._take_waiting()
         if not adm:
             return

@@ -25,6 +25,7 @@ from __future__ import annotations
 
 import math
 import os
+import zlib
 from dataclasses import dataclass, field
 
 import torch
@@ -147,31 +148,51 @@ class LlamaModel:
 
     # ------------------------------------------------------------------ weights
     def _random_init(self, seed: int) -> None:
+        """Random weights (no checkpoints offline) that are TP-INVARIANT: every weight is
+        generated in fixed global blocks (per head for q / k / v / o, per 64 rows or columns
+        of the MLP, per 256 vocab rows of the LM head), each from its own seeded stream, so
+        a rank's shard holds exactly the bits the TP = 1 model has at those positions -- TP
+        runs and services are then token-exact against TP = 1 by construction."""
         cfg, dev, dt = self.cfg, self.device, self.dtype
         g = torch.Generator(device=dev)
-        g.manual_seed(seed * 7919 + self.tp_rank)
         std = 0.02
+        out_std = std / math.sqrt(2 * cfg.layers)
+        H, D, r = cfg.hidden, cfg.head_dim, self.tp_rank
 
-        def w(*shape, s=std):
+        def gen(key, shape, s=std):
+            g.manual_seed((seed * 1_000_003 + zlib.crc32(repr(key).encode())) & 0x7FFFFFFFFFFF)
             t = torch.empty(*shape, device=dev, dtype=dt)
             t.normal_(0.0, s, generator=g)
             return t
 
-        H, D = cfg.hidden, cfg.head_dim
-        self.embed = w(cfg.vocab_size, H)
+        def rows(key, lo, hi, width, blk, s=std):       # global rows [lo, hi) in blocks
+            return torch.cat([gen(key + (b,), (blk, width), s) for b in range(lo // blk, hi // blk)])
+
+        ib = 64 if self.inter % 64 == 0 else 8            # MLP block (divides every TP shard)
+        self.embed = gen(("embed",), (cfg.vocab_size, H))
         self.final_norm = torch.ones(H, device=dev, dtype=dt)
-        self.lm_head = w(self.vocab_shard, H)
+        # vocab block: the same for every TP degree (shards start at multiples of 256)
+        vb = next(b for b in (256, 8, 1) if cfg.vocab_size % b == 0)
+        self.lm_head = rows(("lm",), self.vocab_start, self.vocab_start + self.vocab_shard, H, vb)
         if self.vocab_valid < self.vocab_shard:
             self.lm_head[self.vocab_valid:] = 0
-        out_std = std / math.sqrt(2 * cfg.layers)
-        for _ in range(cfg.layers):
+        i0, i1 = r * self.inter, (r + 1) * self.inter
+        for li in range(cfg.layers):
+            q = rows((li, "q"), r * self.hq * D, (r + 1) * self.hq * D, H, D)
+            k = rows((li, "k"), r * self.hkv * D, (r + 1) * self.hkv * D, H, D)
+            v = rows((li, "v"), r * self.hkv * D, (r + 1) * self.hkv * D, H, D)
+            o = rows((li, "o"), r * self.hq * D, (r + 1) * self.hq * D, H, D, out_std).t()   # columns
+            gt = rows((li, "gate"), i0, i1, H, ib)
+            up = rows((li, "up"), i0, i1, H, ib)
+            dn = rows((li, "down"), i0, i1, H, ib, out_std).t()
             self.layers.append({
                 "in_norm": torch.ones(H, device=dev, dtype=dt),
-                "qkv": w((self.hq + 2 * self.hkv) * D, H),
-                "o": w(H, self.hq * D, s=out_std),
+                "qkv": torch.cat([q, k, v]).contiguous(),
+                "o": o.contiguous(),
                 "post_norm": torch.ones(H, device=dev, dtype=dt),
-                "gate_up": w(2 * self.inter, H),
-                "down": w(H, self.inter, s=out_std),
+                # rows interleaved in blocks of 8 (gate, up): the decode GEMMs' fused SwiGLU
+                "gate_up": ops.glu_interleave(gt, up).contiguous(),
+                "down": dn.contiguous(),
             })
 
     def load_state_dict_hf(self, sd: dict) -> None:

@@ -34,6 +34,9 @@ class ParallelState:
     tp_group: object = None
     dp_group: object = None
     backend: str = "none"
+    # CPU (gloo) group over the same ranks as tp_group: host-side control messages
+    # (the lockstep serving loop's broadcasts) that must not touch the GPU stream
+    tp_cpu_group: object = None
 
     @property
     def is_distributed(self) -> bool:
@@ -78,13 +81,14 @@ def init_distributed(tp_size: int = 1, backend: str | None = None, timeout_s: in
     if world % tp_size != 0:
         raise ValueError(f"world size {world} not divisible by tp {tp_size}")
     dp_size = world // tp_size
-    tp_group = dp_group = None
+    tp_group = dp_group = tp_cpu = None
     # every rank must create every group in the same order
     for d in range(dp_size):
         ranks = list(range(d * tp_size, (d + 1) * tp_size))
         g = dist.new_group(ranks) if tp_size > 1 else None
+        gc = (dist.new_group(ranks, backend="gloo") if backend != "gloo" else g) if tp_size > 1 else None
         if rank in ranks:
-            tp_group = g
+            tp_group, tp_cpu = g, gc
     for t in range(tp_size):
         ranks = list(range(t, world, tp_size))
         g = dist.new_group(ranks) if dp_size > 1 else None
@@ -92,7 +96,7 @@ def init_distributed(tp_size: int = 1, backend: str | None = None, timeout_s: in
             dp_group = g
     _STATE = ParallelState(rank=rank, world_size=world, local_rank=local_rank, tp_size=tp_size,
                            tp_rank=rank % tp_size, dp_size=dp_size, dp_rank=rank // tp_size,
-                           tp_group=tp_group, dp_group=dp_group, backend=backend)
+                           tp_group=tp_group, dp_group=dp_group, backend=backend, tp_cpu_group=tp_cpu)
     if tp_size > 1 and backend == "nccl" and os.environ.get("DOCQA_CUSTOM_AR", "1") == "1":
         # every TP group sets up its IPC all-reduce at once (collective within the group)
         enable_custom_all_reduce()
@@ -110,7 +114,8 @@ _CUSTOM_AR = None
 def enable_custom_all_reduce(max_bytes: int | None = None, force: bool = False):
     """Route the TP all-reduces through the IPC all-reduce (parallel/custom_ar.py: one-shot /
     two-shot over all xGMI links, residual + RMSNorm fused) for every message that fits
-    ``max_bytes`` (default 64 MB, env DOCQA_AR_MAX_MB); RCCL keeps everything else.  Called
+    ``max_bytes`` (default 128 MB = 8192 prefill tokens of a 8192-wide model; env
+    DOCQA_AR_MAX_MB); RCCL keeps everything else.  Called
     by ``init_distributed`` at TP > 1 on RCCL unless DOCQA_CUSTOM_AR=0; a failed IPC mapping
     or self-test leaves RCCL in charge (returns None)."""
     global _CUSTOM_AR
@@ -118,7 +123,7 @@ def enable_custom_all_reduce(max_bytes: int | None = None, force: bool = False):
     if s.tp_size > 1 and (s.backend == "nccl" or force) and _CUSTOM_AR is None:
         from .custom_ar import CustomAllReduce
         if max_bytes is None:
-            max_bytes = int(os.environ.get("DOCQA_AR_MAX_MB", "64")) << 20
+            max_bytes = int(os.environ.get("DOCQA_AR_MAX_MB", "128")) << 20
         car = None
         try:
             car = CustomAllReduce(group=s.tp_group, max_bytes=max_bytes)

@@ -10,6 +10,18 @@ one process per service like the reference's start_all.bat.
     python -m docqa_amd.services.launch --services deid --device cuda:1
     python -m docqa_amd.services.launch --services indexer --device cuda:2
     python -m docqa_amd.services.launch --services qa,ui --device cuda:3
+    # multi-GPU llm-qa (one process per GPU under torchrun, spawned by this launcher):
+    python -m docqa_amd.services.launch --gpus 8 --tp 8 --llm llama3-70b   # one TP=8 group
+    python -m docqa_amd.services.launch --gpus 8 --tp 2                     # 4 DP replicas x TP=2
+
+Multi-GPU layout (``--gpus N --tp T``): N / T data-parallel replicas of a T-way
+tensor-parallel generator.  Within a TP group, TP rank 0 serves HTTP and leads a lockstep
+continuous-batching loop (engine/scheduler.py Lockstep: arrivals + the admission decision
+broadcast before every step over a gloo group) that the other ranks mirror, each running
+its shard of every TP forward.  Replica 0's leader hosts every requested service on the
+reference ports and balances ``/ask/`` and ``/api/llm/summarize`` over the replicas;
+replica d's leader serves llm-qa on port 8001 + 100 d over the indexer's shared snapshot
+(index/follower.py).
 
 Ports (start_all.bat:18,31; synthese Dockerfile:27,36; clinical-ui Streamlit default):
 doc-ingestor 8000, llm-qa 8001, semantic-indexer 8003, synthese-comparative 8005, UI 8501.
@@ -78,6 +90,85 @@ def supervise(groups: list[str], argv: list[str], max_restarts: int = 10, backof
             p.terminate()
 
 
+def _free_port() -> int:
+    import socket
+
+    sk = socket.socket()
+    sk.bind(("127.0.0.1", 0))
+    port = sk.getsockname()[1]
+    sk.close()
+    return port
+
+
+def spawn_workers(gpus: int, argv: list[str]) -> int:
+    """Start this launcher once per GPU under torchrun (a child process: nothing here has
+    touched the GPU) and return its exit code."""
+    import subprocess
+    import sys
+
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={gpus}",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), "-m",
+           "docqa_amd.services.launch", *argv]
+    return subprocess.call(cmd)
+
+
+def run_parallel(a, opts: "StackOptions") -> None:
+    """One rank of ``--gpus N --tp T`` (under torchrun)."""
+    import os
+    import time
+
+    import torch
+
+    from ..engine.llm_engine import LLMEngine
+    from ..engine.scheduler import ContinuousEngine, Lockstep
+    from ..config import Settings
+    from ..models import checkpoint as ck
+    from ..parallel import comm
+
+    cuda = a.device != "cpu"
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if cuda:
+        torch.cuda.set_device(local)
+        opts.device = f"cuda:{local}"
+    ps = comm.init_distributed(tp_size=a.tp, backend=None if cuda else "gloo")
+    torch.manual_seed(1234)    # identical sampling streams on every rank of a TP group
+    ls = None
+    if ps.tp_size > 1:
+        ls = Lockstep(ps.tp_cpu_group, src=ps.dp_rank * ps.tp_size, leader=ps.tp_rank == 0)
+    st = Settings()
+    o = a.port_offset
+    if ps.tp_rank != 0:
+        # follower: only this rank's shard of the generator, mirroring the leader's steps
+        ck.use_checkpoint_tokenizers(opts.llm, opts.embed)
+        model = ck.resolve_llama(opts.llm, device=opts.device)
+        eng = LLMEngine(model, max_batch=opts.max_batch, max_context=opts.max_context, use_graphs=opts.use_graphs)
+        print(f"[rank {ps.rank}] TP follower of group {ps.dp_rank} ready", flush=True)
+        ContinuousEngine(eng, max_running=st.max_batch, lockstep=ls).follow()
+        comm.destroy()
+        return
+    opts.qa_lockstep = ls
+    apps_ports = []
+    if ps.dp_rank == 0:
+        opts.qa_replicas = tuple(f"http://{a.host}:{8001 + o + 100 * d}" for d in range(1, ps.dp_size))
+        stack = DocQAStack(opts)
+        apps_ports = [(stack.ingest_app, 8000), (stack.qa_app, 8001), (stack.indexer_app, 8003),
+                      (stack.synthese_app, 8005), (stack.ui_app, 8501)]
+    else:
+        opts.services = ("qa",)
+        stack = DocQAStack(opts)
+        apps_ports = [(stack.qa_app, 8001 + 100 * ps.dp_rank)]
+    threads = [serve(app, port + o, a.host) for app, port in apps_ports if app is not None]
+    print(f"DocQA rank {ps.rank} (replica {ps.dp_rank}, TP {ps.tp_size}) up: "
+          + ", ".join(f":{port + o}" for app, port in apps_ports if app is not None), flush=True)
+    try:
+        while any(t.is_alive() for t in threads):
+            time.sleep(1.0)
+    except KeyboardInterrupt:
+        pass
+    stack.close()
+    comm.destroy()
+
+
 def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("--device", default="cuda")
@@ -90,7 +181,17 @@ def main() -> None:
     ap.add_argument("--port-offset", type=int, default=0, help="added to every reference port (tests)")
     ap.add_argument("--supervise", default="", help='service groups, one child process each, restarted '
                     'when they die: e.g. "ingest,ui;deid;indexer;qa"')
+    ap.add_argument("--gpus", type=int, default=1, help="GPUs (one process each, torchrun)")
+    ap.add_argument("--tp", type=int, default=1, help="tensor-parallel size of the generator (divides --gpus)")
     a = ap.parse_args()
+    import os
+    import sys
+
+    under_torchrun = int(os.environ.get("WORLD_SIZE", "1")) > 1
+    if a.gpus > 1 and not under_torchrun:
+        if a.gpus % a.tp:
+            raise SystemExit("--tp must divide --gpus")
+        sys.exit(spawn_workers(a.gpus, sys.argv[1:]))
     if a.supervise:
         import sys
 
@@ -105,6 +206,9 @@ def main() -> None:
                         use_graphs=a.device != "cpu", max_context=2048 if a.tiny else 4096,
                         real_synthese=a.real_synthese,
                         services=tuple(x for x in a.services.split(",") if x))
+    if under_torchrun:
+        run_parallel(a, opts)
+        return
     stack = DocQAStack(opts)
     o = a.port_offset
     apps = [("ingest", stack.ingest_app, 8000), ("llm-qa", stack.qa_app, 8001),

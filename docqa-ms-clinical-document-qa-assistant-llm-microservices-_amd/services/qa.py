@@ -125,13 +125,15 @@ class ContinuousBatcher:
     prefills + decode).  Question embedding therefore never stalls the decode loop -- with
     the embed inline, every arrival burst under load cost the running batch a step."""
 
-    def __init__(self, pipeline, settings: Settings, metrics: Metrics):
+    def __init__(self, pipeline, settings: Settings, metrics: Metrics, lockstep=None):
         from ..engine.scheduler import ContinuousEngine
 
         self.pipe = pipeline
         self.st = settings
         self.metrics = metrics
-        self.engine = ContinuousEngine(pipeline.engine, max_running=settings.max_batch)
+        # lockstep: this process leads a tensor-parallel group whose other ranks mirror
+        # every engine step (engine/scheduler.py Lockstep; services/launch.py --tp)
+        self.engine = ContinuousEngine(pipeline.engine, max_running=settings.max_batch, lockstep=lockstep)
         self.q: queue.Queue = queue.Queue()
         self._stop = threading.Event()
         self._prep = threading.Thread(target=self._prep_loop, name="qa-prep", daemon=True)
@@ -190,6 +192,8 @@ class ContinuousBatcher:
                 with eng._cv:
                     if not eng.has_work():
                         eng._cv.wait(timeout=0.05)
+                if not eng.has_work():
+                    eng.heartbeat()          # TP followers: keep their receive alive
                 continue
             if wd:
                 wd.busy()
@@ -244,6 +248,7 @@ class ContinuousBatcher:
         self._stop.set()
         self._prep.join(timeout=60)
         self._t.join(timeout=60)
+        self.engine.stop_followers()
 
 
 class _nullctx:
@@ -254,13 +259,57 @@ class _nullctx:
         return False
 
 
-def create_app(pipeline=None, settings: Settings | None = None) -> FastAPI:
+class ReplicaRouter:
+    """Front-end over data-parallel llm-qa replicas (services/launch.py --gpus N): requests
+    go round-robin to this process's own batcher or to another replica's HTTP endpoint,
+    with the fewest requests in flight winning ties."""
+
+    def __init__(self, local, urls: list[str], timeout_s: float = 600.0):
+        import httpx
+
+        self.local = local
+        self.targets = [None] + list(urls)        # None: this process
+        self.inflight = [0] * len(self.targets)
+        self._rr = 0
+        self._lock = threading.Lock()
+        self.client = httpx.AsyncClient(timeout=timeout_s)
+
+    def _pick(self) -> int:
+        with self._lock:
+            n = len(self.targets)
+            order = [(self._rr + i) % n for i in range(n)]
+            i = min(order, key=lambda k: self.inflight[k])
+            self._rr = (i + 1) % n
+            self.inflight[i] += 1
+            return i
+
+    async def call(self, kind: str, path: str, payload: dict, key: str):
+        i = self._pick()
+        try:
+            if self.targets[i] is None:
+                return await asyncio.wrap_future(self.local.submit(kind, payload[key]))
+            r = await self.client.post(self.targets[i] + path, json=payload)
+            return JSONResponse(status_code=r.status_code, content=r.json())
+        finally:
+            with self._lock:
+                self.inflight[i] -= 1
+
+
+def create_app(pipeline=None, settings: Settings | None = None, lockstep=None,
+               replicas: list[str] | None = None) -> FastAPI:
+    """``lockstep``: this process leads a TP group (continuous serving only);
+    ``replicas``: base URLs of the other data-parallel llm-qa replicas to balance over."""
     st = settings or Settings()
     metrics = Metrics("llm_qa")
     app = FastAPI(title="Health LLM Assistant (MI355X)")
     app.state.pipeline = pipeline
     batcher_cls = ContinuousBatcher if st.serving_mode == "continuous" else DynamicBatcher
-    app.state.batcher = batcher_cls(pipeline, st, metrics) if pipeline is not None else None
+    if lockstep is not None and batcher_cls is not ContinuousBatcher:
+        raise ValueError("tensor-parallel serving needs DOCQA_SERVING=continuous")
+    kw = {"lockstep": lockstep} if lockstep is not None else {}
+    app.state.batcher = batcher_cls(pipeline, st, metrics, **kw) if pipeline is not None else None
+    router = ReplicaRouter(app.state.batcher, replicas) if replicas and app.state.batcher is not None else None
+    app.state.router = router
 
     def ready() -> bool:
         p = app.state.pipeline
@@ -271,6 +320,8 @@ def create_app(pipeline=None, settings: Settings | None = None) -> FastAPI:
         if not ready():
             return JSONResponse(status_code=503, content={"detail": "Index non chargé."})
         metrics.inc("ask_requests")
+        if router is not None:
+            return await router.call("ask", "/ask/", {"question": query.question}, "question")
         fut = app.state.batcher.submit("ask", query.question)
         return await asyncio.wrap_future(fut)
 
@@ -279,6 +330,8 @@ def create_app(pipeline=None, settings: Settings | None = None) -> FastAPI:
         if app.state.batcher is None:
             return JSONResponse(status_code=503, content={"detail": "LLM non chargé."})
         metrics.inc("summarize_requests")
+        if router is not None:
+            return await router.call("summarize", "/api/llm/summarize", {"prompt": req.prompt}, "prompt")
         fut = app.state.batcher.submit("summarize", req.prompt)
         return await asyncio.wrap_future(fut)
 

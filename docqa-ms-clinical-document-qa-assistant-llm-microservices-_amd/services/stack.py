@@ -41,6 +41,8 @@ class StackOptions:
     ner_in_loop: bool = False     # run the (random-init) NER model inside de-identification
     real_synthese: bool = False
     services: tuple = ()          # subset of ALL_SERVICES hosted by this process (empty: all)
+    qa_lockstep: object = None    # llm-qa leads a tensor-parallel group (services/launch.py --tp)
+    qa_replicas: tuple = ()       # llm-qa front-end over these data-parallel replica URLs
 
 
 class _LocalRetrieval(synthese.RetrievalClient):
@@ -127,7 +129,8 @@ class DocQAStack:
             self.pipeline = RAGPipeline(self.encoder, self.enc_tok, index, metadata,
                                         self.engine, self.chat_tok, k=self.st.top_k,
                                         max_prompt_tokens=opts.max_context - self.st.max_new_tokens - 8)
-            self.qa_app = qa.create_app(self.pipeline, self.st)
+            self.qa_app = qa.create_app(self.pipeline, self.st, lockstep=opts.qa_lockstep,
+                                        replicas=list(opts.qa_replicas) or None)
         if "ingest" in svc:
             self.ingest_app = ingest.create_app(self.st, self.db, self.broker)
         if "synthese" in svc:

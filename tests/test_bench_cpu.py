@@ -67,3 +67,22 @@ def test_pipeline_bench_tp2_gloo_sharded_index():
     d = _last_json(r.stdout)
     assert d["n_gpus"] == 2 and d["config"]["parallelism"] == "tp2" and d["value"] > 0
     assert d["ingest_docs_per_sec"] > 0 and d["config"]["index"] == "flat-L2 sharded x2"
+
+
+def test_pipeline_bench_tp8_gloo_replicated_index():
+    """Config 5 at its real parallel shape: 8 ranks, TP=8 over the 70B GQA layout at toy
+    width (test-tp8), index sharded over all 8 ranks with replicated queries."""
+    env = dict(os.environ)
+    for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
+        env.pop(k, None)
+    env["OMP_NUM_THREADS"] = "1"
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "8",
+           "--master-addr", "127.0.0.1", "--master-port", str(_port()),
+           str(ROOT / "benchmarks" / "bench_pipeline.py"), "--device", "cpu", "--llm", "test-tp8",
+           "--embed", "tiny-bert", "--ner", "tiny-bert", "--notes", "24", "--batch", "2",
+           "--steps", "1", "--warmup", "1", "--max-new-tokens", "2", "--max-context", "1024"]
+    r = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=1200, env=env)
+    assert r.returncode == 0, r.stderr[-3000:]
+    d = _last_json(r.stdout)
+    assert d["n_gpus"] == 8 and d["config"]["parallelism"] == "tp8" and d["value"] > 0
+    assert d["config"]["index"] == "flat-L2 sharded x8"
