@@ -41,6 +41,7 @@ from ..schemas import SearchRequest
 from ..store import metadata_io
 from ..store.segment_log import SegmentLog, read_snapshot_marker, write_snapshot_marker
 from ..text.chunking import chunk_chars
+from ..text.dates import in_window, parse_date
 from ..utils import tracing
 from ..text.kb import kb_records_from_dir, synthetic_kb_records
 
@@ -155,7 +156,7 @@ class SemanticIndexer:
         md = metadata or {}
         recs = [{"doc_id": str(doc_id), "text_content": c, "source": f"Dossier Patient {doc_id}",
                  "type": "patient_file", "patient_id": md.get("patient_id", str(doc_id)),
-                 "filename": md.get("filename")}
+                 "filename": md.get("filename"), "note_date": parse_date(md.get("note_date"))}
                 for c in chunk_chars(text or "", self.st.chunk_size)]
         return self.add_records(recs)
 
@@ -181,7 +182,7 @@ class SemanticIndexer:
                 md = msg.get("metadata") or {}
                 recs.extend({"doc_id": str(doc_id), "text_content": chunk, "source": f"Dossier Patient {doc_id}",
                              "type": "patient_file", "patient_id": md.get("patient_id", str(doc_id)),
-                             "filename": md.get("filename")}
+                             "filename": md.get("filename"), "note_date": parse_date(md.get("note_date"))}
                             for chunk in chunk_chars(msg.get("original_text_masked", "") or "", self.st.chunk_size))
                 done.append((c, m, doc_id))
             except Exception as e:  # noqa: BLE001 - malformed message: dead-letter it
@@ -234,10 +235,15 @@ class SemanticIndexer:
             return out
 
     def patient_snippets(self, patient_id: str, from_date=None, to_date=None, focus=None, limit: int = 20) -> list[dict]:
+        """The patient's chunks, optionally restricted to notes dated in [from_date, to_date]
+        (each chunk's ``note_date``, set at ingest: text/dates.py) and ranked by distance to
+        the ``focus`` text."""
         pid = str(patient_id)
+        lo, hi = parse_date(from_date), parse_date(to_date)
         with self.lock:
             rows = [(i, m) for i, m in enumerate(self.metadata)
-                    if m.get("type") == "patient_file" and (str(m.get("patient_id")) == pid or str(m.get("doc_id")) == pid)]
+                    if m.get("type") == "patient_file" and (str(m.get("patient_id")) == pid or str(m.get("doc_id")) == pid)
+                    and in_window(m.get("note_date"), lo, hi)]
         if focus and rows:
             q = self.encoder.encode(self.tok.encode_batch([focus]))
             ids = torch.tensor([i for i, _ in rows], device=self.index.xb.device)

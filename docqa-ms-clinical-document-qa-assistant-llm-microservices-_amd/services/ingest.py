@@ -16,6 +16,8 @@ loop as the reference's ``async def`` does.
 """
 from __future__ import annotations
 
+import datetime
+
 import json
 import os
 from pathlib import Path
@@ -27,6 +29,7 @@ from ..bus.broker import get_broker
 from ..config import Settings
 from ..store import docs_db
 from ..text.extraction import extract_text_from_file
+from ..text.dates import first_date
 from .multipart import FilePart, parse_multipart
 
 
@@ -75,7 +78,12 @@ def create_app(settings: Settings | None = None, db: docs_db.DocsDB | None = Non
             db.set_status(doc_id, docs_db.STATUS_ERROR_EXTRACTION)
             return {"error": "Impossible d'extraire le texte"}
         try:
-            publish_to_queue(broker, st.raw_queue, doc_id, text, {"filename": f.filename, "type": doc_type})
+            # the note's date (first clinical date in the raw text, else the upload day):
+            # de-identification masks the dates inside the text, and the indexer's
+            # patient-snippets window filter needs it (text/dates.py)
+            meta = {"filename": f.filename, "type": doc_type,
+                    "note_date": first_date(text) or datetime.date.today().isoformat()}
+            publish_to_queue(broker, st.raw_queue, doc_id, text, meta)
             db.set_status(doc_id, docs_db.STATUS_PROCESSED)
             return {"message": "Ingestion réussie", "doc_id": doc_id}
         except Exception as e:  # noqa: BLE001 - reference returns the error text

@@ -65,7 +65,10 @@ def test_ingest_success_error_and_listing(tmp_path):
     assert r.status_code == 200 and r.json() == {"message": "Ingestion réussie", "doc_id": 1}
     msg = json.loads(broker.get_nowait("raw_documents_queue"))
     assert list(msg) == ["doc_id", "text", "metadata"]
-    assert msg["metadata"] == {"filename": "note.txt", "type": "compte-rendu"}
+    # the reference's metadata keys, plus the note date for the patient-snippets window
+    # (a superset: consumers pass metadata through; text/dates.py)
+    md = dict(msg["metadata"])
+    assert md.pop("note_date") and md == {"filename": "note.txt", "type": "compte-rendu"}
     body, ct = encode_multipart({"file": FilePart("empty.txt", "text/plain", b"   "), "doc_type": "x"})
     r = c.post("/ingest/", content=body, headers={"content-type": ct})
     assert r.status_code == 200 and r.json() == {"error": "Impossible d'extraire le texte"}
