@@ -6,9 +6,12 @@ result ``content.strip()``, ``None`` on any exception (doc-ingestor/processing.p
 Native extractors (no JVM, no network):
   * plain text: UTF-8 (BOM/UTF-16 aware), latin-1 fallback;
   * DOCX: the ``word/document.xml`` part of the OOXML zip, paragraphs -> lines;
-  * PDF: content streams (raw or FlateDecode) scanned for the text-showing operators
-    ``Tj``, ``TJ``, ``'`` and ``"`` with PDF string escapes; text-positioning operators
-    (``Td``/``TD``/``T*``/``ET``) become line breaks;
+  * PDF: page tree -> content streams (raw or FlateDecode, objects inside /ObjStm object
+    streams too), text-showing operators ``Tj``/``TJ``/``'``/``"`` decoded per font
+    through its /ToUnicode CMap (1- or 2-byte codes: Type0 / Identity-H fonts) or WinAnsi,
+    literal and hex strings, TJ kerning gaps as spaces; text-positioning operators
+    (``Td``/``TD``/``T*``/``ET``/``Tm``) become line breaks.  Parity with Tika is
+    unpinned (no Tika offline): tests pin the decoding on generated fixtures;
   * HTML: tags stripped.
 If ``TIKA_URL`` is set the file is PUT to that Tika server instead, as in the reference.
 """
@@ -51,6 +54,16 @@ def extract_docx(data: bytes) -> str:
     return "\n".join(lines)
 
 
+# ---------------------------------------------------------------- PDF
+# Object-level reader: indirect objects (plain and inside /ObjStm object streams), page
+# tree with inherited /Resources, per-font decoding -- a /ToUnicode CMap (bfchar /
+# bfrange, 1- or 2-byte codes from its codespacerange: the Type0 / Identity-H fonts of
+# most generated PDFs), else WinAnsi (cp1252) for simple fonts -- literal and hex
+# strings, TJ arrays with kerning gaps as spaces.  Files it cannot parse that way fall
+# back to scanning every content stream with latin-1 decoding (the round-1 behaviour).
+_OBJ = re.compile(rb"(?<![0-9])(\d+)\s+(\d+)\s+obj\b(.*?)\bendobj", re.S)
+_STREAM = re.compile(rb"stream\r?\n(.*)\r?\nendstream\s*$", re.S)
+_REF = re.compile(rb"(\d+)\s+(\d+)\s+R")
 _PDF_STREAM = re.compile(rb"<<(.*?)>>\s*stream\r?\n(.*?)\r?\nendstream", re.S)
 _ESC = {b"n": b"\n", b"r": b"\r", b"t": b"\t", b"b": b"\b", b"f": b"\f", b"(": b"(", b")": b")", b"\\": b"\\"}
 
@@ -87,51 +100,268 @@ def _pdf_string(buf: bytes, i: int) -> tuple[bytes, int]:
     return bytes(out), i
 
 
-def _pdf_content_text(content: bytes) -> str:
+def _hex_string(buf: bytes, i: int) -> tuple[bytes, int]:
+    """<4a6f> -> bytes (odd digit count padded with 0), index after '>'."""
+    j = buf.find(b">", i)
+    j = len(buf) if j < 0 else j
+    h = re.sub(rb"\s", b"", buf[i + 1:j])
+    if len(h) % 2:
+        h += b"0"
+    try:
+        return bytes.fromhex(h.decode("ascii")), j + 1
+    except ValueError:
+        return b"", j + 1
+
+
+def _decompress(head: bytes, body: bytes) -> bytes | None:
+    if b"/FlateDecode" in head or b"/Fl " in head or head.rstrip().endswith(b"/Fl"):
+        try:
+            return zlib.decompress(body)
+        except zlib.error:
+            try:
+                return zlib.decompressobj().decompress(body)
+            except zlib.error:
+                return None
+    if b"/Filter" in head:
+        return None          # images / unsupported filters
+    return body
+
+
+class _Pdf:
+    def __init__(self, data: bytes):
+        self.objs: dict[int, tuple[bytes, bytes | None]] = {}
+        for m in _OBJ.finditer(data):
+            body = m.group(3)
+            sm = _STREAM.search(body)
+            if sm:
+                head = body[:sm.start()]
+                self.objs[int(m.group(1))] = (head, _decompress(head, sm.group(1)))
+            else:
+                self.objs[int(m.group(1))] = (body, None)
+        for num, (head, stream) in list(self.objs.items()):   # compressed object streams
+            if b"/ObjStm" in head and stream:
+                n = int(re.search(rb"/N\s+(\d+)", head).group(1))
+                first = int(re.search(rb"/First\s+(\d+)", head).group(1))
+                nums = [int(x) for x in stream[:first].split()]
+                offs = [(nums[2 * k], first + nums[2 * k + 1]) for k in range(min(n, len(nums) // 2))]
+                for k, (on, off) in enumerate(offs):
+                    end = offs[k + 1][1] if k + 1 < len(offs) else len(stream)
+                    self.objs.setdefault(on, (stream[off:end], None))
+
+    def get(self, ref: bytes | int | None):
+        if ref is None:
+            return None
+        if isinstance(ref, bytes):
+            m = _REF.match(ref.strip())
+            if not m:
+                return None
+            ref = int(m.group(1))
+        return self.objs.get(ref)
+
+    @staticmethod
+    def entry(head: bytes, key: bytes) -> bytes | None:
+        """Raw value of /key in a dictionary: a reference, a name, an array or a << dict >>."""
+        m = re.search(rb"/" + key + rb"(?![A-Za-z])\s*", head)
+        if not m:
+            return None
+        i = m.end()
+        if head[i:i + 2] == b"<<":
+            depth, j = 0, i
+            while j < len(head):
+                if head[j:j + 2] == b"<<":
+                    depth += 1
+                    j += 2
+                    continue
+                if head[j:j + 2] == b">>":
+                    depth -= 1
+                    j += 2
+                    if depth == 0:
+                        return head[i:j]
+                    continue
+                j += 1
+            return head[i:]
+        if head[i:i + 1] == b"[":
+            j = head.find(b"]", i)
+            return head[i:j + 1]
+        r = _REF.match(head, i)
+        if r:
+            return r.group(0)
+        t = re.match(rb"/?[^\s/<>\[\]()]+", head[i:])
+        return t.group(0) if t else None
+
+    def resolve_dict(self, v: bytes | None) -> bytes:
+        if v is None:
+            return b""
+        if v.startswith(b"<<"):
+            return v
+        o = self.get(v)
+        return o[0] if o else b""
+
+
+def _parse_cmap(data: bytes) -> tuple[dict, int]:
+    """ToUnicode CMap -> ({code: text}, code byte width)."""
+    width = 1
+    m = re.search(rb"begincodespacerange\s*<([0-9A-Fa-f]+)>", data)
+    if m:
+        width = max(1, len(m.group(1)) // 2)
+
+    def uni(h: bytes) -> str:
+        b = bytes.fromhex(h.decode("ascii"))
+        return b.decode("utf-16-be", errors="replace")
+
+    out: dict[int, str] = {}
+    for blk in re.finditer(rb"beginbfchar(.*?)endbfchar", data, re.S):
+        for a, b in re.findall(rb"<([0-9A-Fa-f]+)>\s*<([0-9A-Fa-f]*)>", blk.group(1)):
+            out[int(a, 16)] = uni(b)
+    for blk in re.finditer(rb"beginbfrange(.*?)endbfrange", data, re.S):
+        body = blk.group(1)
+        for m in re.finditer(rb"<([0-9A-Fa-f]+)>\s*<([0-9A-Fa-f]+)>\s*(<[0-9A-Fa-f]+>|\[[^\]]*\])", body):
+            lo, hi, dst = int(m.group(1), 16), int(m.group(2), 16), m.group(3)
+            if dst.startswith(b"["):
+                for k, h in enumerate(re.findall(rb"<([0-9A-Fa-f]+)>", dst)):
+                    out[lo + k] = uni(h)
+            else:
+                base = bytes.fromhex(dst[1:-1].decode("ascii"))
+                for c in range(lo, min(hi, lo + 65535) + 1):
+                    last = int.from_bytes(base[-2:], "big") + (c - lo)
+                    out[c] = (base[:-2] + last.to_bytes(2, "big")).decode("utf-16-be", errors="replace")
+    return out, width
+
+
+class _Font:
+    def __init__(self, pdf: _Pdf, head: bytes):
+        self.cmap, self.width = {}, 1
+        tu = _Pdf.entry(head, b"ToUnicode")
+        o = pdf.get(tu) if tu else None
+        if o and o[1]:
+            self.cmap, self.width = _parse_cmap(o[1])
+        elif b"/Type0" in head:
+            self.width = 2
+
+    def decode(self, s: bytes) -> str:
+        if self.cmap:
+            w = self.width
+            return "".join(self.cmap.get(int.from_bytes(s[k:k + w], "big"), "") for k in range(0, len(s) - w + 1, w))
+        if self.width == 2:
+            return ""          # CID font without a ToUnicode map: no recoverable text
+        return s.decode("cp1252", errors="replace")
+
+
+def _content_text(content: bytes, fonts: dict) -> str:
     parts: list[str] = []
-    i = 0
-    pending: list[bytes] = []
-    n = len(content)
+    font = None
+    i, n = 0, len(content)
+    operands: list = []
     while i < n:
         c = content[i:i + 1]
-        if c == b"(":
-            s, i = _pdf_string(content, i)
-            pending.append(s)
+        if c in b" \t\r\n\f\x00":
+            i += 1
             continue
-        if c == b"%":  # comment
+        if c == b"%":
             j = content.find(b"\n", i)
             i = n if j < 0 else j
             continue
-        m = re.match(rb"(Tj|TJ|'|\"|T\*|Td|TD|ET|Tm)\b", content[i:i + 3]) if c.isalpha() or c in b"'\"" else None
-        if m:
-            op = m.group(1)
-            if op in (b"Tj", b"TJ", b"'", b'"'):
-                if op in (b"'", b'"'):
-                    parts.append("\n")
-                parts.append(b"".join(pending).decode("latin-1"))
-                pending = []
-            elif op in (b"T*", b"Td", b"TD", b"ET", b"Tm"):
-                if parts and not parts[-1].endswith("\n"):
-                    parts.append("\n")
-            i += len(op)
+        if c == b"(":
+            s, i = _pdf_string(content, i)
+            operands.append(s)
             continue
-        i += 1
+        if c == b"<" and content[i:i + 2] != b"<<":
+            s, i = _hex_string(content, i)
+            operands.append(s)
+            continue
+        if c == b"[":
+            # TJ array: strings and kerning numbers
+            j, arr = i + 1, []
+            while j < n and content[j:j + 1] != b"]":
+                cj = content[j:j + 1]
+                if cj == b"(":
+                    s, j = _pdf_string(content, j)
+                    arr.append(s)
+                elif cj == b"<":
+                    s, j = _hex_string(content, j)
+                    arr.append(s)
+                else:
+                    m = re.match(rb"-?\d*\.?\d+", content[j:j + 32])
+                    if m:
+                        arr.append(float(m.group(0)))
+                        j += len(m.group(0))
+                    else:
+                        j += 1
+            operands.append(arr)
+            i = j + 1
+            continue
+        m = re.match(rb"/[^\s/<>\[\]()]+|-?\d*\.?\d+|[A-Za-z'\"*]+|<<|>>|\{|\}", content[i:i + 64])
+        if not m:
+            i += 1
+            continue
+        tok = m.group(0)
+        i += len(tok)
+        if tok[:1] == b"/" or re.match(rb"-?\d*\.?\d+$", tok) or tok in (b"<<", b">>", b"{", b"}"):
+            operands.append(tok)
+            continue
+        op = tok
+        dec = (font.decode if font is not None else (lambda b: b.decode("cp1252", errors="replace")))
+        if op == b"Tf" and len(operands) >= 2 and isinstance(operands[-2], bytes) and operands[-2][:1] == b"/":
+            font = fonts.get(operands[-2][1:])
+        elif op in (b"Tj", b"'", b'"') and operands and isinstance(operands[-1], bytes):
+            if op != b"Tj":
+                parts.append("\n")
+            parts.append(dec(operands[-1]))
+        elif op == b"TJ" and operands and isinstance(operands[-1], list):
+            for e in operands[-1]:
+                if isinstance(e, float):
+                    if e < -200:
+                        parts.append(" ")
+                else:
+                    parts.append(dec(e))
+        elif op in (b"T*", b"Td", b"TD", b"ET", b"Tm"):
+            if parts and not parts[-1].endswith("\n"):
+                parts.append("\n")
+        operands = []
     return "".join(parts)
 
 
+def _page_fonts(pdf: _Pdf, page_head: bytes, cache: dict) -> dict:
+    head, seen = page_head, 0
+    res = _Pdf.entry(head, b"Resources")
+    while res is None and seen < 32:           # inherited from the page tree
+        parent = pdf.get(_Pdf.entry(head, b"Parent"))
+        if parent is None:
+            break
+        head, seen = parent[0], seen + 1
+        res = _Pdf.entry(head, b"Resources")
+    fonts = {}
+    fd = pdf.resolve_dict(_Pdf.entry(pdf.resolve_dict(res), b"Font"))
+    for name, ref in re.findall(rb"/([^\s/<>\[\]()]+)\s+(\d+\s+\d+\s+R)", fd):
+        key = int(_REF.match(ref).group(1))
+        if key not in cache:
+            o = pdf.get(key)
+            cache[key] = _Font(pdf, o[0]) if o else None
+        if cache[key] is not None:
+            fonts[name] = cache[key]
+    return fonts
+
+
 def extract_pdf(data: bytes) -> str:
-    texts = []
+    pdf = _Pdf(data)
+    pages = [(num, o) for num, o in sorted(pdf.objs.items())
+             if re.search(rb"/Type\s*/Page(?![s\w])", o[0])]
+    texts, cache = [], {}
+    for _, (head, _) in pages:
+        fonts = _page_fonts(pdf, head, cache)
+        cont = _Pdf.entry(head, b"Contents")
+        refs = _REF.findall(cont) if cont else []
+        body = b"\n".join((pdf.get(int(r[0])) or (b"", None))[1] or b"" for r in refs)
+        if body:
+            texts.append(_content_text(body, fonts).strip("\n"))
+    out = "\n".join(t for t in texts if t.strip())
+    if out.strip():
+        return out
+    # no page tree recovered: every text-bearing stream, latin-1 strings
     for m in _PDF_STREAM.finditer(data):
-        head, body = m.group(1), m.group(2)
-        if b"/FlateDecode" in head:
-            try:
-                body = zlib.decompress(body)
-            except zlib.error:
-                continue
-        elif b"/Filter" in head:
-            continue  # image / unsupported filter
-        if b"BT" in body:
-            texts.append(_pdf_content_text(body))
+        body = _decompress(m.group(1), m.group(2))
+        if body and b"BT" in body:
+            texts.append(_content_text(body, {}))
     return "\n".join(t for t in texts if t.strip())
 
 
