@@ -55,6 +55,8 @@ def main() -> None:
     ap.add_argument("--questions", choices=("unique", "repeat"), default="unique",
                     help="unique: every request a distinct question (default); repeat: the ~470-string "
                          "template grid of rounds 1-2 (cache-hot ceiling)")
+    ap.add_argument("--kv-mem-fraction", type=float, default=0.85,
+                    help="KV pool = this fraction of the HBM free after the weights (0: max_batch full contexts)")
     ap.add_argument("--template", choices=("cache_friendly", "reference"), default=None,
                     help="QA prompt template (docqa_amd/prompts.py; default: env QA_TEMPLATE or cache_friendly)")
     a = ap.parse_args()
@@ -89,7 +91,8 @@ def main() -> None:
             torch.cuda.synchronize()
 
     sc = StackConfig(llm=a.llm, embed=a.embed, n_notes=a.notes, max_batch=a.batch,
-                     max_context=a.max_context, k=a.k, use_graphs=(not a.no_graphs) and cuda)
+                     max_context=a.max_context, k=a.k, use_graphs=(not a.no_graphs) and cuda,
+                     kv_mem_fraction=a.kv_mem_fraction or None)
     pipe, info = build_stack(sc, device=dev)
     params = SamplingParams(max_new_tokens=a.max_new_tokens, temperature=0.0, stop_on_eos=False)
 
@@ -168,6 +171,7 @@ def main() -> None:
                 "max_new_tokens": a.max_new_tokens,
                 "parallelism": f"dp{ps.dp_size}" + (f"xtp{a.tp}" if a.tp > 1 else ""),
                 "index_vectors": info.get("index_vectors"),
+                "kv_blocks": info.get("kv_blocks"),
             },
             "stage_ms_mean": st,
             "gen_tokens_per_sec": round(ps.dp_size * a.batch * a.max_new_tokens * a.steps / elapsed_max, 1),

@@ -197,7 +197,12 @@ class _DecodeGraph:
 class LLMEngine:
     def __init__(self, model: LlamaModel, max_batch: int = 64, max_context: int = 2048,
                  block_size: int = 64, num_blocks: int | None = None, use_graphs: bool = True,
-                 max_prefill_tokens: int = 65536, prefix_cache: bool = True):
+                 max_prefill_tokens: int = 65536, prefix_cache: bool = True,
+                 kv_mem_fraction: float | None = None):
+        """``num_blocks``: KV pool size; default ``max_batch`` full-context sequences, or --
+        with ``kv_mem_fraction`` (env DOCQA_KV_MEM_FRACTION) on a GPU -- that fraction of the
+        HBM still free after the weights, minus the prefill activation headroom (the block
+        prefix cache keeps every block the running batches do not need)."""
         self.model = model
         self.cfg = model.cfg
         self.device = model.device
@@ -220,6 +225,11 @@ class LLMEngine:
         self.max_prefill_tokens = max_prefill_tokens
         if num_blocks is None:
             num_blocks = max_batch * self.max_blocks_per_seq + 1
+            if kv_mem_fraction is None and os.environ.get("DOCQA_KV_MEM_FRACTION"):
+                kv_mem_fraction = float(os.environ["DOCQA_KV_MEM_FRACTION"])
+            if kv_mem_fraction and self.device.type == "cuda":
+                num_blocks = max(num_blocks, self._blocks_from_free_memory(model, block_size, kv_mem_fraction))
+        num_blocks = self._agree_across_tp(model, num_blocks)
         self.kv = KVCache(self.cfg.layers, num_blocks, model.hkv, self.cfg.head_dim, block_size,
                           self.device, model.dtype)
         self.use_graphs = use_graphs and self.device.type == "cuda"
@@ -246,6 +256,33 @@ class LLMEngine:
         self._graphs: dict[tuple, _DecodeGraph] = {}
         self._pool = None
         self.stats = GenStats()
+
+    @staticmethod
+    def _agree_across_tp(model, num_blocks: int) -> int:
+        """Every rank of a TP group must run the same block allocator (lockstep serving,
+        identical preemption / eviction decisions): the smallest pool of the group."""
+        import torch.distributed as dist
+
+        from ..parallel import comm
+
+        st = comm.state()
+        if getattr(model, "tp", 1) > 1 and st.tp_size > 1 and dist.is_initialized():
+            t = torch.tensor([num_blocks], dtype=torch.int64)
+            dist.all_reduce(t, op=dist.ReduceOp.MIN, group=st.tp_cpu_group or st.tp_group)
+            num_blocks = int(t.item())
+        return num_blocks
+
+    def _blocks_from_free_memory(self, model, block_size: int, fraction: float) -> int:
+        cfg = model.cfg
+        free, _ = torch.cuda.mem_get_info(self.device)
+        el = torch.finfo(model.dtype).bits // 8
+        block_bytes = cfg.layers * 2 * model.hkv * block_size * cfg.head_dim * el
+        # prefill activations at the token budget (hidden-sized buffers, QKV, the gate|up
+        # product / SwiGLU output) twice over, + 6 GB for graph pools, workspaces and the index
+        per_tok = (6 * cfg.hidden + (model.hq + 2 * model.hkv) * cfg.head_dim + 3 * model.inter) * el
+        headroom = 2 * self.max_prefill_tokens * per_tok + (6 << 30)
+        budget = int(free * fraction) - headroom
+        return max(0, budget // block_bytes)
 
     # ------------------------------------------------------------------ prefill
     def _prefill(self, prompts: list[list[int]], tables: list[list[int]],
@@ -476,23 +513,28 @@ class LLMEngine:
                         on_step=None) -> list[list[int]]:
         return self.collect(self.launch(prompts, params, on_step))
 
-    def reserve(self, prompts: list[list[int]], params: SamplingParams) -> "Reservation":
+    def reserve(self, prompts: list[list[int]], params: SamplingParams,
+                gen_tokens: int | None = None) -> "Reservation":
         """KV blocks of a batch: the longest cached prompt prefix of each prompt (prefix
         cache, refcounted) + fresh blocks for the rest of the prompt and the generation.
         Host-only work (~12 ms for 256 RAG prompts), so a pipelined caller runs it on its
         preparation thread while the previous batch decodes; pass the result to
         :meth:`launch` (or :meth:`release` it)."""
         lens = [len(p) for p in prompts]
-        need = max(lens) + params.max_new_tokens
+        gen = params.max_new_tokens if gen_tokens is None else gen_tokens
+        need = max(lens) + gen
         if need > self.max_context:
             raise ValueError(f"prompt+generation {need} exceeds max_context {self.max_context}")
         with tracing.span("engine.reserve", seqs=len(prompts)):
-            return self._reserve(prompts, params, lens)
+            return self._reserve(prompts, params, lens, gen)
 
-    def _reserve(self, prompts, params, lens) -> "Reservation":
+    def _reserve(self, prompts, params, lens, gen: int | None = None) -> "Reservation":
+        """``gen``: generated tokens to reserve blocks for (default: all max_new_tokens; the
+        continuous scheduler reserves a block ahead and grows tables as decode goes)."""
         alloc = self.kv.allocator
         BS = self.block_size
-        need = [self.kv.blocks_for(n + params.max_new_tokens) for n in lens]
+        gen = params.max_new_tokens if gen is None else gen
+        need = [self.kv.blocks_for(n + gen) for n in lens]
         r = Reservation([], [], params.max_new_tokens, len(prompts))
         if not self._use_pc:
             try:

@@ -60,6 +60,12 @@ class Request:
     t_arrival: float = 0.0
     t_first: float = 0.0
     done: bool = False
+    # preemption (recompute): generated tokens already folded into ``prompt`` when the
+    # request was re-queued, the original prompt length, and the next decode write position
+    gen_base: int = 0
+    orig_len: int = -1
+    pos: int = 0
+    preemptions: int = 0
 
 
 class Lockstep:
@@ -114,6 +120,15 @@ class ContinuousEngine:
         self._host = None
         self._flip = 0
         self._version = 0                  # bumped whenever the running set changes
+        # KV blocks on demand: admission reserves the prompt + ``reserve_ahead`` generated
+        # tokens (not all max_new_tokens), tables grow a block at a time as decode reaches
+        # them, and when the pool runs out the youngest running request is preempted and
+        # re-queued with its tokens so far appended to its prompt (recompute: its prompt
+        # blocks are still in the prefix cache).  DOCQA_PREEMPT=0: reserve everything up
+        # front, as before (no preemption ever needed).
+        self.preempt = os.environ.get("DOCQA_PREEMPT", "1") == "1"
+        self.reserve_ahead = int(os.environ.get("DOCQA_RESERVE_AHEAD", str(engine.block_size)))
+        self.preempted = 0
 
     # ------------------------------------------------------------------ client side
     def submit(self, prompt: list[int], params: SamplingParams | None = None, on_token=None) -> cf.Future:
@@ -256,12 +271,16 @@ class ContinuousEngine:
         with self._cv:
             while self.waiting and len(self.running) + len(admitted) < self.max_running:
                 r = self.waiting[0]
+                if r.orig_len < 0:
+                    r.orig_len = len(r.prompt)
+                remaining = r.params.max_new_tokens - r.gen_base
+                gen = min(remaining, self.reserve_ahead) if self.preempt else remaining
                 try:
                     # prefix-cache hits (whole blocks + token-granular rows), fresh blocks
-                    res = eng.reserve([r.prompt], r.params)
+                    res = eng.reserve([r.prompt], r.params, gen_tokens=gen)
                 except MemoryError:
                     if not self.running and not admitted:   # can never fit: fail, don't stall
-                        need = eng.kv.blocks_for(len(r.prompt) + r.params.max_new_tokens)
+                        need = eng.kv.blocks_for(len(r.prompt) + gen)
                         self.waiting.popleft().future.set_exception(MemoryError(
                             f"request needs {need} KV blocks, the cache has {alloc.num_free()} free"))
                         continue
@@ -352,7 +371,10 @@ class ContinuousEngine:
         for i, r in enumerate(reqs):
             bt[i, :len(r.blocks)] = torch.tensor(r.blocks, dtype=torch.int32)
             tok[i] = r.out[-1]
-            pos[i] = len(r.prompt) + len(r.out) - 1
+            # the input of the next step sits right after the prompt (+ tokens generated since
+            # (re-)admission; gen_base of them are already part of a resumed prompt)
+            r.pos = len(r.prompt) + len(r.out) - r.gen_base - 1
+            pos[i] = r.pos
             if r.params.temperature > 0:
                 it[i], tk[i], tp[i] = 1.0 / r.params.temperature, r.params.top_k, r.params.top_p
             else:
@@ -391,9 +413,72 @@ class ContinuousEngine:
             self._graphs[key] = g
         return g
 
+    # ------------------------------------------------------------------ KV on demand
+    def _grow_tables(self) -> None:
+        """Before a step: every running request gets the block its write position enters
+        (one block at a time); if the pool is out, preempt the youngest request and retry."""
+        if not self.preempt or not self.running:
+            return
+        eng, BS = self.eng, self.eng.block_size
+        while True:
+            short = [r for r in self.running if r.pos // BS >= len(r.blocks)]
+            if not short:
+                return
+            grown, failed = [], False
+            for r in short:
+                try:
+                    b = eng._retry(lambda: eng.kv.allocator.alloc(1))[0]
+                except MemoryError:
+                    failed = True
+                    break
+                r.blocks.append(b)
+                grown.append((self.running.index(r), len(r.blocks) - 1, b))
+            if grown:
+                idx = torch.tensor(grown, dtype=torch.long)
+                m = self._master
+                m.block_tables[idx[:, 0].to(m.block_tables.device), idx[:, 1].to(m.block_tables.device)] = \
+                    idx[:, 2].to(device=m.block_tables.device, dtype=torch.int32)
+            if not failed:
+                return
+            self._preempt_youngest()
+
+    def _preempt_youngest(self) -> None:
+        """Free the most recently admitted running request's blocks and re-queue it at the
+        front of the waiting queue with its generated tokens appended to its prompt."""
+        if self._pending is not None:       # every issued step's tokens reach the host first
+            p, self._pending = self._pending, None
+            self._process(p)
+        if not self.running:
+            return
+        v = max(self.running, key=lambda r: (r.t_arrival, r.rid))   # the latest arrival
+        if len(self.running) == 1 and v.pos // self.eng.block_size >= len(v.blocks):
+            # alone and still out of blocks: it can never finish in this pool
+            self.eng.kv.allocator.free(v.blocks)
+            v.blocks = []
+            v.done = True
+            if not v.future.done():
+                v.future.set_exception(MemoryError("KV cache exhausted by a single request"))
+            self._compact([])
+            self._update_shared()
+            return
+        self.eng.kv.allocator.free(v.blocks)
+        v.blocks, v.res, v.cached = [], None, 0
+        keep = [i for i, r in enumerate(self.running) if r is not v]
+        self._compact(keep)
+        v.prompt = v.prompt[:v.orig_len] + list(v.out)
+        v.gen_base = len(v.out)
+        v.preemptions += 1
+        self.preempted += 1
+        with self._cv:
+            self.waiting.appendleft(v)
+        self._update_shared()
+
     def _decode(self) -> None:
         eng = self.eng
+        self._grow_tables()
         n = len(self.running)
+        if n == 0:
+            return
         bp = _bucket(n, eng.max_batch) if self.pad_buckets else n
         greedy = all(r.params.temperature <= 0 for r in self.running)
         g = self._graph(bp, greedy, self._nshared > 0)
@@ -416,6 +501,8 @@ class ContinuousEngine:
                 eng._step_body(g)
         eng.stats.generated_tokens += n
         self.steps += 1
+        for r in self.running:
+            r.pos += 1
         snap = list(self.running)
         if g.out.device.type == "cuda":
             if self._host is None:

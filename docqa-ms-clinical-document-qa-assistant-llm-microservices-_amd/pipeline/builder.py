@@ -28,6 +28,7 @@ class StackConfig:
     storage_dtype: torch.dtype = torch.float32
     use_graphs: bool = True
     seed: int = 0
+    kv_mem_fraction: float | None = None   # size the KV pool from free HBM (LLMEngine)
 
 
 def build_stack(sc: StackConfig, device="cuda", log=print) -> tuple[RAGPipeline, dict]:
@@ -55,7 +56,8 @@ def build_stack(sc: StackConfig, device="cuda", log=print) -> tuple[RAGPipeline,
     info["index_vectors"] = n
     model = ck.resolve_llama(sc.llm, device=device, seed=sc.seed)
     engine = LLMEngine(model, max_batch=sc.max_batch, max_context=sc.max_context,
-                       use_graphs=sc.use_graphs)
+                       use_graphs=sc.use_graphs, kv_mem_fraction=sc.kv_mem_fraction)
+    info["kv_blocks"] = engine.kv.allocator.num_blocks if hasattr(engine.kv.allocator, "num_blocks") else None
     pipe = RAGPipeline(encoder, enc_tok, index, records, engine, chat_tok, k=sc.k,
                        max_prompt_tokens=sc.max_context - 256)
     info["setup_s"] = time.perf_counter() - t0

@@ -141,7 +141,8 @@ def run_parallel(a, opts: "StackOptions") -> None:
         # follower: only this rank's shard of the generator, mirroring the leader's steps
         ck.use_checkpoint_tokenizers(opts.llm, opts.embed)
         model = ck.resolve_llama(opts.llm, device=opts.device)
-        eng = LLMEngine(model, max_batch=opts.max_batch, max_context=opts.max_context, use_graphs=opts.use_graphs)
+        eng = LLMEngine(model, max_batch=opts.max_batch, max_context=opts.max_context, use_graphs=opts.use_graphs,
+                        kv_mem_fraction=opts.kv_mem_fraction)
         print(f"[rank {ps.rank}] TP follower of group {ps.dp_rank} ready", flush=True)
         ContinuousEngine(eng, max_running=st.max_batch, lockstep=ls).follow()
         comm.destroy()

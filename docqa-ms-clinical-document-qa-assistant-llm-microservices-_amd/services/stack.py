@@ -43,6 +43,7 @@ class StackOptions:
     services: tuple = ()          # subset of ALL_SERVICES hosted by this process (empty: all)
     qa_lockstep: object = None    # llm-qa leads a tensor-parallel group (services/launch.py --tp)
     qa_replicas: tuple = ()       # llm-qa front-end over these data-parallel replica URLs
+    kv_mem_fraction: float | None = 0.8   # KV pool from free HBM (GPU only; LLMEngine)
 
 
 class _LocalRetrieval(synthese.RetrievalClient):
@@ -125,7 +126,7 @@ class DocQAStack:
                 index, metadata = self.follower.index, self.follower.metadata
             self.model = ck.resolve_llama(opts.llm, device=dev)
             self.engine = LLMEngine(self.model, max_batch=opts.max_batch, max_context=opts.max_context,
-                                    use_graphs=opts.use_graphs)
+                                    use_graphs=opts.use_graphs, kv_mem_fraction=opts.kv_mem_fraction)
             self.pipeline = RAGPipeline(self.encoder, self.enc_tok, index, metadata,
                                         self.engine, self.chat_tok, k=self.st.top_k,
                                         max_prompt_tokens=opts.max_context - self.st.max_new_tokens - 8)

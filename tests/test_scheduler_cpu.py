@@ -143,3 +143,33 @@ def test_admission_waits_for_a_group_when_slots_trickle_free(monkeypatch):
     clock[0] += ce.admit_wait_s
     ce._admit()
     assert calls == [40, 40, 1]
+
+
+def test_undersized_pool_preempts_and_finishes_token_exact():
+    """KV blocks on demand + preemption by recompute: a pool that holds every prompt but not
+    every full generation at once admits optimistically, preempts the latest arrivals when
+    a table cannot grow, re-admits them with their tokens so far, and every request still
+    gets exactly the tokens it gets alone in a roomy pool."""
+    import torch
+
+    from docqa_amd.engine.llm_engine import LLMEngine, SamplingParams
+    from docqa_amd.engine.scheduler import ContinuousEngine
+    from docqa_amd.models.llama import LlamaConfig, LlamaModel
+
+    torch.manual_seed(0)
+    m = LlamaModel(LlamaConfig.preset("tiny"), device="cpu", dtype=torch.float32, seed=4)
+    g = torch.Generator().manual_seed(2)
+    prompts = [torch.randint(3, 4000, (int(n),), generator=g).tolist() for n in (20, 35, 9, 50, 28, 17)]
+    params = SamplingParams(max_new_tokens=40, stop_on_eos=False)
+    roomy = LLMEngine(m, max_batch=8, max_context=256, block_size=16, use_graphs=False, prefix_cache=False)
+    expect = [roomy.generate([p], params)[0] for p in prompts]
+    # full reservations would need sum(ceil((len + 40) / 16)) = 26 blocks; give it 14
+    small = LLMEngine(m, max_batch=8, max_context=256, block_size=16, num_blocks=14, use_graphs=False,
+                      prefix_cache=False)
+    ce = ContinuousEngine(small, max_running=8)
+    assert ce.preempt
+    free0 = small.kv.allocator.num_free()
+    got = ce.generate(prompts, params)
+    assert got == expect
+    assert ce.preempted > 0
+    assert small.kv.allocator.num_free() == free0          # every block came back
