@@ -58,6 +58,14 @@ class Settings:
     snapshot_every: int = field(default_factory=lambda: env_int("INDEX_SNAPSHOT_EVERY", 16))
     default_data_dir: str = field(default_factory=lambda: os.getenv("DEFAULT_DATA_DIR", "default_data"))
     chunk_size: int = field(default_factory=lambda: env_int("CHUNK_SIZE", 500))
+    # vector store: flat (IndexFlatL2, the reference's) | ivfpq (IndexRefineFlat over IVF-PQ,
+    # trained once IVF_TRAIN_MIN vectors are stored -- index/hybrid.py)
+    index_type: str = field(default_factory=lambda: os.getenv("INDEX_TYPE", "flat"))
+    ivf_nlist: int = field(default_factory=lambda: env_int("IVF_NLIST", 1024))
+    pq_m: int = field(default_factory=lambda: env_int("PQ_M", 0))                 # 0: d / 8
+    ivf_nprobe: int = field(default_factory=lambda: env_int("IVF_NPROBE", 32))
+    refine_k_factor: int = field(default_factory=lambda: env_int("REFINE_K_FACTOR", 4))
+    ivf_train_min: int = field(default_factory=lambda: env_int("IVF_TRAIN_MIN", 0))  # 0: 39 x nlist
     embed_model: str = field(default_factory=lambda: os.getenv("EMBED_MODEL", "minilm-l6"))
     # llm-qa
     llm_model: str = field(default_factory=lambda: os.getenv("LLM_MODEL", "llama3-8b"))

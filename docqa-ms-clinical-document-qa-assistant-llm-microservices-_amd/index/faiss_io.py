@@ -14,7 +14,11 @@ reference's shipped ``semantic-indexer/vector_store.faiss`` (996,909 B; SURVEY.m
     n_floats uint64              = ntotal * d
     data     float32[ntotal * d] little endian
 
-IVF-PQ (``IwPQ``) is written by :mod:`docqa_amd.index.ivfpq` with the same primitives.
+IVF-PQ (``IvPQ``) is written by :mod:`docqa_amd.index.ivfpq` with the same primitives, and
+``IndexRefineFlat`` (``IxRF``: header, base index, flat refine index, float k_factor, as
+faiss's index_write.cpp) wraps it for the semantic-indexer's INDEX_TYPE=ivfpq store.
+No IVF fixture ships with the reference: parity with faiss for these is unpinned
+(round-trip tested).
 Writes are atomic (temp file + rename), fixing the reference's non-atomic
 ``faiss.write_index`` + ``pickle.dump`` pair (semantic-indexer/indexer.py:26-30).
 """
@@ -105,9 +109,24 @@ def read_flat(r: Reader, fourcc: bytes) -> FlatIndexData:
     return FlatIndexData(d=d, metric=metric, xb=xb.reshape(ntotal, d))
 
 
-def read_index(path) -> object:
-    buf = Path(path).read_bytes()
-    r = Reader(buf)
+@dataclass
+class RefineIndexData:
+    """``IndexRefineFlat`` (fourcc ``IxRF``): an approximate base index re-ranked with the
+    exact vectors of a flat refine index."""
+    base: object
+    refine: FlatIndexData
+    k_factor: float
+
+    @property
+    def ntotal(self) -> int:
+        return self.refine.ntotal
+
+    @property
+    def d(self) -> int:
+        return self.refine.d
+
+
+def read_index_from(r: Reader) -> object:
     fourcc = r.read(4)
     if fourcc in (b"IxF2", b"IxFI", b"IxFl"):
         return read_flat(r, fourcc)
@@ -115,7 +134,31 @@ def read_index(path) -> object:
         from .ivfpq import read_ivfpq_body
 
         return read_ivfpq_body(r)
+    if fourcc == b"IxRF":
+        # faiss index_write.cpp IndexRefine: header, base index, refine index, k_factor
+        read_header(r)
+        base = read_index_from(r)
+        refine = read_index_from(r)
+        k_factor, = r.unpack("<f")
+        if not isinstance(refine, FlatIndexData):
+            raise ValueError("IxRF: only a flat refine index is supported")
+        return RefineIndexData(base, refine, float(k_factor))
     raise ValueError(f"unsupported FAISS index type {fourcc!r}")
+
+
+def read_index(path) -> object:
+    return read_index_from(Reader(Path(path).read_bytes()))
+
+
+def refine_bytes(base_bytes: bytes, xb: np.ndarray, k_factor: float, metric: int = METRIC_L2) -> bytes:
+    """IndexRefineFlat(base) with the exact vectors ``xb`` as its refine index."""
+    w = io.BytesIO()
+    w.write(b"IxRF")
+    write_header(w, int(xb.shape[1]) if xb.ndim == 2 else 0, int(xb.shape[0]), True, metric)
+    w.write(base_bytes)
+    w.write(flat_bytes(xb, metric))
+    w.write(struct.pack("<f", float(k_factor)))
+    return w.getvalue()
 
 
 def flat_bytes(xb: np.ndarray, metric: int = METRIC_L2) -> bytes:

@@ -32,12 +32,17 @@ log = logging.getLogger("docqa.index.follower")
 class IndexFollower:
     def __init__(self, index_dir: str, index_file: str = "vector_store.faiss",
                  metadata_file: str = "metadata_store.pkl", d: int = 384, device="cuda",
-                 poll_s: float = 0.2):
+                 poll_s: float = 0.2, settings=None):
         self.index_path = Path(index_dir) / index_file
         self.meta_path = Path(index_dir) / metadata_file
         self.wal_path = self.index_path.with_name(self.index_path.name + ".wal")
         self.marker_path = self.index_path.with_name(self.index_path.name + ".snapshot.json")
-        self.index = FlatIndex(d, "l2", device)
+        # the store type the writer uses (INDEX_TYPE): flat, or IVF-PQ + exact refine
+        if settings is not None:
+            from .hybrid import make_index
+            self.index = make_index(settings, d, device)
+        else:
+            self.index = FlatIndex(d, "l2", device)
         self.metadata: list[dict] = []
         self.poll_s = poll_s
         self.last_seq = 0          # highest WAL sequence applied
@@ -65,12 +70,18 @@ class IndexFollower:
         # the llm-qa prep thread searches this index concurrently: build the new vectors
         # off to the side and swap vectors + metadata together under the index lock, so a
         # search never sees an empty or half-loaded index (nor ids without records)
+        ivf = None
+        if isinstance(data, faiss_io.RefineIndexData):
+            ivf, data = data.base, data.refine
         xb = torch.from_numpy(data.xb) if n else torch.empty(0, self.index.d)
 
         def swap_meta():
             self.metadata[:] = meta
 
-        self.index.replace(xb, before_swap=swap_meta)
+        if ivf is not None and hasattr(self.index, "ivf"):
+            self.index.replace(xb, before_swap=swap_meta, ivf=ivf)
+        else:
+            self.index.replace(xb, before_swap=swap_meta)
         self._marker = mk
         self.last_seq = mk["wal_seq"]
         self._offset = 0

@@ -24,15 +24,20 @@ from ..parallel import comm
 from .flat import FlatIndex
 
 
-class ShardedFlatIndex:
-    """``replicated=True``: every rank of ``group`` searches with the SAME queries (a
+class ShardedIndex:
+    """``local``: this rank's shard -- a :class:`FlatIndex`, or any index whose
+    ``search(xq, k, id_offset=..., **kw)`` returns ids (IVF-PQ: :class:`ShardedIVFPQIndex`).
+    ``replicated=True``: every rank of ``group`` searches with the SAME queries (a
     tensor-parallel group serving one request stream, config 5): the query all-gather is
-    skipped and each shard answers the batch once."""
+    skipped and each shard answers the batch once.  ``max_queries``: every rank pads its
+    query batch to this static size, so no count exchange (and no host sync on the
+    device counts) is needed per search; larger batches take the count-exchange path."""
 
-    def __init__(self, local: FlatIndex, group=None, replicated: bool = False):
+    def __init__(self, local: FlatIndex, group=None, replicated: bool = False, max_queries: int | None = None):
         self.local = local
         self.group = group
         self.replicated = replicated
+        self.max_queries = max_queries
         s = comm.state()
         self.world = s.dp_size if group is None else dist.get_world_size(group)
         self.rank = s.dp_rank if group is None else dist.get_rank(group)
@@ -66,15 +71,24 @@ class ShardedFlatIndex:
     def id_offset(self) -> int:
         return self._offset
 
-    def search(self, xq: torch.Tensor, k: int):
+    def search(self, xq: torch.Tensor, k: int, **kw):
         xq = xq.to(self.local.device, dtype=torch.float32)
         if self.world == 1:
-            return self.local.search(xq, k)
+            return self.local.search(xq, k, **kw)
         nq = xq.shape[0]
         dev = xq.device
         if self.replicated:
-            D, I = self.local.search(xq, k, id_offset=self._offset)
+            D, I = self.local.search(xq, k, id_offset=self._offset, **kw)
             return self._merge(D, I, k, 0, nq)
+        if self.max_queries and nq <= self.max_queries:
+            # static padding: the padded (zero) rows are searched too and dropped
+            mx = self.max_queries
+            pad = torch.zeros(mx, self.d, device=dev, dtype=torch.float32)
+            pad[:nq] = xq
+            allq = [torch.empty_like(pad) for _ in range(self.world)]
+            dist.all_gather(allq, pad, group=self.group)
+            D, I = self.local.search(torch.cat(allq, 0), k, id_offset=self._offset, **kw)
+            return self._merge(D, I, k, self.rank * mx, nq)
         cnt = torch.tensor([nq], dtype=torch.long, device=dev)
         cnts = [torch.empty_like(cnt) for _ in range(self.world)]
         dist.all_gather(cnts, cnt, group=self.group)
@@ -85,7 +99,7 @@ class ShardedFlatIndex:
         allq = [torch.empty_like(pad) for _ in range(self.world)]
         dist.all_gather(allq, pad, group=self.group)
         Q = torch.cat([q[:c] for q, c in zip(allq, counts)], 0)
-        D, I = self.local.search(Q, k, id_offset=self._offset)
+        D, I = self.local.search(Q, k, id_offset=self._offset, **kw)
         return self._merge(D, I, k, sum(counts[: self.rank]), nq)
 
     def _merge(self, D, I, k: int, start: int, nq: int):
@@ -101,3 +115,77 @@ class ShardedFlatIndex:
         vals, pos = torch.topk(Dc, k, dim=1, largest=largest)
         ids = torch.gather(Ic, 1, pos)
         return vals[start:start + nq], ids[start:start + nq]
+
+
+ShardedFlatIndex = ShardedIndex
+
+
+class _IVFShard:
+    """One rank's inverted lists (global ids stored at add time) behind the shard API."""
+
+    metric = "l2"
+
+    def __init__(self, ivf):
+        self.ivf = ivf
+
+    @property
+    def d(self) -> int:
+        return self.ivf.d
+
+    @property
+    def device(self):
+        return self.ivf.device
+
+    @property
+    def ntotal(self) -> int:
+        return self.ivf.ntotal
+
+    def search(self, xq, k: int, id_offset: int = 0, nprobe: int | None = None):
+        return self.ivf.search(xq, k, nprobe=nprobe)       # ids are already global
+
+
+class ShardedIVFPQIndex(ShardedIndex):
+    """IVF-PQ sharded across ranks (config 5 at 10M+ vectors): ONE coarse quantizer and PQ
+    codebook, trained on rank 0 and broadcast, so every shard encodes into the same codes;
+    each rank holds the inverted lists of its own vectors under their global ids, scans its
+    lists for the probed centroids and the per-shard top-k merge is the same all-gather as
+    the flat shards -- equal to one IVF-PQ over every vector."""
+
+    @classmethod
+    def build(cls, local_x, d: int, nlist: int, M: int, train_sample=None, device="cuda", group=None,
+              replicated: bool = False, niter: int = 20, seed: int = 0, max_queries: int | None = None):
+        from .ivfpq import IVFPQIndex
+
+        s = comm.state()
+        group = group if group is not None else s.dp_group
+        rank = dist.get_rank(group) if group is not None else 0
+        ivf = IVFPQIndex(d, nlist, M, 8, device=device)
+        if rank == 0:
+            ivf.train(train_sample, niter=niter, seed=seed)
+            cent, pq = ivf.centroids.contiguous(), ivf.pq.contiguous()
+        else:
+            cent = torch.empty(nlist, d, device=device)
+            pq = torch.empty(M, 256, d // M, device=device)
+        if group is not None and dist.get_world_size(group) > 1:
+            src = dist.get_global_rank(group, 0)
+            dist.broadcast(cent, src=src, group=group)
+            dist.broadcast(pq, src=src, group=group)
+        ivf.centroids, ivf.pq = cent, pq
+        shard = _IVFShard(ivf)
+        obj = cls(shard, group=group, replicated=replicated, max_queries=max_queries)
+        # global ids: this shard's offset among the ranks' vector counts
+        n = int(local_x.shape[0])
+        counts = torch.tensor([n], dtype=torch.long, device=device)
+        if obj.world > 1:
+            parts = [torch.empty_like(counts) for _ in range(obj.world)]
+            dist.all_gather(parts, counts, group=obj.group)
+            offs = [int(p.item()) for p in parts]
+        else:
+            offs = [n]
+        start = sum(offs[: obj.rank])
+        ivf.add(local_x, ids=torch.arange(start, start + n, dtype=torch.long))
+        obj._offset, obj._ntotal = 0, sum(offs)
+        return obj
+
+    def refresh(self) -> None:   # ids are global from build time
+        pass

@@ -49,7 +49,8 @@ def build_stack(sc: StackConfig, device="cuda", log=print) -> tuple[RAGPipeline,
     emb = embed_records(encoder, enc_tok, records[lo:hi])
     local = FlatIndex(encoder.cfg.hidden, "l2", device, sc.storage_dtype, capacity=max(1024, hi - lo))
     local.add(emb)
-    index = ShardedFlatIndex(local) if s.dp_size > 1 else local
+    # queries padded to the static batch size: no per-search count exchange / host sync
+    index = ShardedFlatIndex(local, max_queries=sc.max_batch) if s.dp_size > 1 else local
     if device != "cpu" and torch.device(device).type == "cuda":
         torch.cuda.synchronize()
     info["index_build_s"] = time.perf_counter() - t0

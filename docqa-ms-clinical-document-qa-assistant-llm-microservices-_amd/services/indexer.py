@@ -35,7 +35,8 @@ from fastapi.responses import JSONResponse
 from ..bus.broker import get_broker
 from ..config import Settings
 from ..index import faiss_io
-from ..index.flat import FlatIndex
+from ..index.flat import FlatIndex  # noqa: F401  (the default store type)
+from ..index.hybrid import load_index, make_index
 from ..pipeline.corpus import embed_records
 from ..schemas import SearchRequest
 from ..store import metadata_io
@@ -85,14 +86,14 @@ class SemanticIndexer:
             dirty = False
             covered = 0
             if self.index_path.exists() and self.meta_path.exists():
-                self.index = FlatIndex.load(self.index_path, device=self.device)
+                self.index = load_index(self.st, self.index_path, self.device)
                 self.metadata = metadata_io.read_metadata(self.meta_path)
                 if len(self.metadata) != self.index.ntotal:
                     raise RuntimeError(f"index/metadata mismatch: {self.index.ntotal} vs {len(self.metadata)}")
                 covered = read_snapshot_marker(self.marker_path)["wal_seq"]
                 logger.info("resumed index (%d vectors)", self.index.ntotal)
             else:
-                self.index = FlatIndex(self.encoder.cfg.hidden, "l2", self.device)
+                self.index = make_index(self.st, self.encoder.cfg.hidden, self.device)
                 self.metadata = []
                 if build_if_missing:
                     recs = kb_records_from_dir(self.st.default_data_dir) or synthetic_kb_records()
@@ -139,7 +140,7 @@ class SemanticIndexer:
             emb = embed_records(self.encoder, self.tok, recs)
         with self.lock:
             if self.index is None:
-                self.index = FlatIndex(self.encoder.cfg.hidden, "l2", self.device)
+                self.index = make_index(self.st, self.encoder.cfg.hidden, self.device)
             if log and self.wal is not None:           # durable before it is visible
                 self.wal.append(recs, emb.float().cpu().numpy())
             self.index.add(emb)

@@ -122,7 +122,7 @@ class DocQAStack:
                 index, metadata = self.indexer.index, self.indexer.metadata
             else:
                 self.follower = IndexFollower(self.st.index_dir, self.st.index_file, self.st.metadata_file,
-                                              d=self.encoder.cfg.hidden, device=dev).start()
+                                              d=self.encoder.cfg.hidden, device=dev, settings=self.st).start()
                 index, metadata = self.follower.index, self.follower.metadata
             self.model = ck.resolve_llama(opts.llm, device=dev)
             self.engine = LLMEngine(self.model, max_batch=opts.max_batch, max_context=opts.max_context,
