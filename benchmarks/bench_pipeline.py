@@ -50,6 +50,9 @@ def main():
     ap.add_argument("--pipelined", action="store_true",
                     help="overlap batch i+1's embed/search with batch i's decode tail")
     ap.add_argument("--device", default="cuda")
+    ap.add_argument("--share-gpu", action="store_true",
+                    help="every rank on cuda:0: a one-GPU rehearsal of the TP=N path (gloo process group, "
+                         "IPC all-reduce between the ranks' processes); correctness, not speed")
     ap.add_argument("--questions", choices=("unique", "repeat"), default="unique",
                     help="unique: every request a distinct question; repeat: the small template grid")
     a = ap.parse_args()
@@ -75,10 +78,12 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     tp = a.tp or world
     cuda = a.device == "cuda"
-    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    local_rank = 0 if a.share_gpu else int(os.environ.get("LOCAL_RANK", "0"))
     if cuda:
         torch.cuda.set_device(local_rank)
-    ps = comm.init_distributed(tp_size=tp, backend=None if cuda else "gloo")
+    ps = comm.init_distributed(tp_size=tp, backend="gloo" if (a.share_gpu or not cuda) else None)
+    if cuda and a.share_gpu and tp > 1:
+        comm.enable_custom_all_reduce(force=True)
     if cuda:
         assert ops.load_native(), "native HIP kernels not built (python -m docqa_amd.ops.build)"
     dev = f"cuda:{local_rank}" if cuda else "cpu"
