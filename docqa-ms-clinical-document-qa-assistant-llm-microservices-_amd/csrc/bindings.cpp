@@ -725,7 +725,22 @@ at::Tensor pgemm(const at::Tensor& x, const at::Tensor& w, int64_t epi) {
   sizes.back() = epi == 1 ? N / 2 : N;
   c10::DeviceGuard g(x.device());
   auto out = at::empty(sizes, x.options());
-  CHECK_RC(docqa_pgemm(x.data_ptr(), w.data_ptr(), out.data_ptr(), M, N, K, (int)epi, stream()), "pgemm");
+  CHECK_RC(docqa_pgemm(x.data_ptr(), w.data_ptr(), out.data_ptr(), nullptr, M, N, K, 1, (int)epi, stream()), "pgemm");
+  return out;
+}
+
+// split-K fp32 slabs [S, M, N] of x . w^T on the 256 x 256 kernel (decode-sized M)
+at::Tensor pgemm_partial(const at::Tensor& x, const at::Tensor& w, int64_t splits) {
+  CHECK_GPU(x); CHECK_BF16(x); CHECK_BF16(w); CHECK_CONTIG(x); CHECK_CONTIG(w);
+  CHECK_ALIGN16(x); CHECK_ALIGN16(w);
+  const int K = x.size(-1), N = w.size(0);
+  TORCH_CHECK(w.size(1) == K && splits >= 1 && K % (splits * 128) == 0, "pgemm_partial: shape / splits");
+  const int M = x.numel() / K;
+  TORCH_CHECK(M == 0 || docqa_pgemm_ok(M, N, K), "pgemm_partial: unsupported shape");
+  c10::DeviceGuard g(x.device());
+  auto out = at::empty({splits, M, N}, x.options().dtype(at::kFloat));
+  CHECK_RC(docqa_pgemm(x.data_ptr(), w.data_ptr(), nullptr, out.data_ptr<float>(), M, N, K, (int)splits, 2,
+                       stream()), "pgemm_partial");
   return out;
 }
 
@@ -922,6 +937,7 @@ TORCH_LIBRARY(docqa, m) {
   m.def("mgemm_glu(Tensor x, Tensor w, int cfg=0) -> Tensor");
   m.def("mgemm_argmax(Tensor x, Tensor w, int n_valid, int cfg=0) -> Tensor");
   m.def("pgemm(Tensor x, Tensor w, int epi=0) -> Tensor");
+  m.def("pgemm_partial(Tensor x, Tensor w, int splits) -> Tensor");
   m.def("mgemm_argmax_val(Tensor x, Tensor w, int n_valid, int cfg=0) -> (Tensor, Tensor)");
   m.def("pgemm_ok(int M, int N, int K) -> bool", &pgemm_ok);
   m.def("paged_decode_cascade(Tensor q, Tensor k_cache, Tensor v_cache, Tensor block_tables, "
@@ -983,6 +999,7 @@ TORCH_LIBRARY_IMPL(docqa, CUDA, m) {
   m.impl("mgemm_glu", &mgemm_glu);
   m.impl("mgemm_argmax", &mgemm_argmax);
   m.impl("pgemm", &pgemm);
+  m.impl("pgemm_partial", &pgemm_partial);
   m.impl("mgemm_argmax_val", &mgemm_argmax_val);
   m.impl("paged_decode_fused", &paged_decode_fused);
   m.impl("paged_decode_cascade", &paged_decode_cascade);

@@ -116,7 +116,8 @@ int docqa_mgemm_argmax(const void* X, const void* W, int64_t* out, float* outv, 
                        int N, int K, int n_valid, int cfg, hipStream_t s);
 int docqa_mgemm_tile_n(int cfg);
 bool docqa_pgemm_ok(int M, int N, int K);
-int docqa_pgemm(const void* A, const void* W, void* C, int M, int N, int K, int epi, hipStream_t s);
+int docqa_pgemm(const void* A, const void* W, void* C, float* P, int M, int N, int K, int S, int epi,
+                hipStream_t s);
 
 int docqa_knn_workspace_blocks(int N);
 int docqa_knn_kpad(int k);

@@ -29,8 +29,10 @@
 //     SOURCE address (rule 21): the 16-row fragment reads are bank-conflict-free;
 //   * XCD-aware bijective block remap + groups of 4 m-tiles so an XCD's concurrent
 //     workgroups share A rows and W columns in its L2 (T1);
-//   * epilogue through the drained LDS: bf16 tile or fused SwiGLU, then 16-B row stores.
-// Shapes: N % 256 == 0, K % 128 == 0, any M (tail rows clamped on load, never stored);
+//   * epilogue through the drained LDS: bf16 tile, fused SwiGLU, or fp32 split-K slabs
+//     (decode-sized M: K split over workgroups, one slice per XCD, the slabs combined by
+//     the consumer -- RoPE + KV write, add + RMSNorm, or the TP all-reduce);
+// Shapes: N % 256 == 0, K % (128 S) == 0, any M (tail rows clamped on load, never stored);
 // byte offsets of A and W rows must fit 32 bits (saddr + voffset addressing).
 #include "docqa_common.h"
 #include "docqa_asm.h"
@@ -44,7 +46,7 @@ constexpr int BUF_B = 4 * HALF_B;        // bytes of one K-tile buffer (64 KiB)
 constexpr int SCR_PITCH = 72;            // epilogue scratch row pitch (bf16), 144 B
 constexpr int LDS_B = (2 * BUF_B > 8 * 128 * SCR_PITCH * 2) ? 2 * BUF_B : 8 * 128 * SCR_PITCH * 2;
 enum { HA0 = 0, HA1 = 1, HB0 = 2, HB1 = 3 };
-enum { EPI_BF16 = 0, EPI_GLU = 1 };
+enum { EPI_BF16 = 0, EPI_GLU = 1, EPI_PARTIAL = 2 };
 
 // byte offset of logical 16-B chunk `ch` of `row` inside a [128][64] bf16 half-tile
 __device__ __forceinline__ uint32_t swz(int row, int ch) {
@@ -86,11 +88,26 @@ __device__ __forceinline__ float silu_f(float x) { return x / (1.f + __expf(-x))
 template <int EPI>
 __global__ __launch_bounds__(512, 2) void pgemm_kernel(const uint16_t* __restrict__ A,
                                                       const uint16_t* __restrict__ W,
-                                                      uint16_t* __restrict__ C, int M, int N, int K,
-                                                      int ntm, int ntn) {
+                                                      uint16_t* __restrict__ C, float* __restrict__ P,
+                                                      int M, int N, int K, int ntm, int ntn, int S, int Ks) {
   __shared__ __attribute__((aligned(16))) char smem[LDS_B];
   const int nwg = ntm * ntn;
-  const int wg = xcd_remap(blockIdx.x, nwg);
+  // split-K (decode-sized M): workgroup -> (tile, K slice).  With S | 8 and whole rounds of
+  // 8, the workgroups of one XCD all take the same slice, so that XCD's L2 holds just that
+  // slice of A -- re-read by every tile (cf. mgemm.hip)
+  int tile_id, slice = 0;
+  if (S == 1) {
+    tile_id = xcd_remap(blockIdx.x, nwg);
+  } else if (8 % S == 0 && (nwg * S) % 8 == 0) {
+    const int xcd = blockIdx.x & 7, j = blockIdx.x >> 3;
+    slice = xcd % S;
+    tile_id = j * (8 / S) + xcd / S;
+  } else {
+    tile_id = blockIdx.x % nwg;
+    slice = blockIdx.x / nwg;
+  }
+  const int kbeg = slice * Ks;
+  const int wg = tile_id;
   // groups of GM m-tiles x all n-tiles: consecutive ids (one XCD's concurrent workgroups)
   // form a GM x (32 / GM) block of output tiles
   constexpr int GM = 4;
@@ -126,7 +143,7 @@ __global__ __launch_bounds__(512, 2) void pgemm_kernel(const uint16_t* __restric
     }
   // stage half-tile h of K-tile kt into buffer kt & 1
   auto stage = [&](int h, int kt) {
-    const uint16_t* base = (h == HA0 || h == HA1 ? A : W) + kt * BK;
+    const uint16_t* base = (h == HA0 || h == HA1 ? A : W) + kbeg + kt * BK;
     const uint32_t d = __builtin_amdgcn_readfirstlane(lds + (uint32_t)((kt & 1) * BUF_B + h * HALF_B + wave * 1024));
     glds_pair(base, soff[h][0], soff[h][1], d, d + 8 * 1024);
   };
@@ -200,7 +217,7 @@ __global__ __launch_bounds__(512, 2) void pgemm_kernel(const uint16_t* __restric
   // phase 1 of j+1; E.HB1 5 -> 1 -> 2; E.HA1 6 -> 2 -> 3; O.HA0 / HB0 7 / 8 -> 4 -> 5;
   // O.HB1 1 -> 5 -> 6; O.HA1 2 -> 6 -> 7).  The last iteration issues only phases 1-2 and
   // retires with the counts that keep the same guarantees (8, 8, 8, 4, 2, 0, 0, 0).
-  const int nk = K / BK;
+  const int nk = Ks / BK;
   const int nit = nk / 2;
   // prologue: everything the steady state assumes was issued in iteration -1
   stage(HA0, 0);
@@ -265,6 +282,32 @@ __global__ __launch_bounds__(512, 2) void pgemm_kernel(const uint16_t* __restric
       const uint4 v = *reinterpret_cast<const uint4*>(scr + r * SCR_PITCH + c);
       if (row < M) *reinterpret_cast<uint4*>(C + (size_t)row * N + n0 + wc * 64 + c) = v;
     }
+  } else if constexpr (EPI == EPI_PARTIAL) {
+    // fp32 split-K slab P[slice][row][col] (combined by the consumer kernel): each wave's
+    // 64-row halves through its own LDS scratch [64][68] so stores are whole 256-B row runs
+    float* fs = reinterpret_cast<float*>(smem) + wave * 64 * 68;
+    float* Ps = P + (size_t)slice * M * N;
+#pragma unroll
+    for (int mh = 0; mh < 2; ++mh) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int nh = 0; nh < 2; ++nh)
+#pragma unroll
+          for (int j = 0; j < 2; ++j)
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+              fs[(i * 16 + fk * 4 + r) * 68 + nh * 32 + j * 16 + fr] = acc[mh][i][nh][j][r];
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll 4
+      for (int it = 0; it < 16; ++it) {
+        const int r = it * 4 + (lane >> 4), c = (lane & 15) * 4;
+        const int row = m0 + wr * 128 + mh * 64 + r;
+        const float4 v = *reinterpret_cast<const float4*>(fs + r * 68 + c);
+        if (row < M) *reinterpret_cast<float4*>(Ps + (size_t)row * N + n0 + wc * 64 + c) = v;
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    }
   } else {
     // 16 consecutive GEMM columns = one (gate 8 | up 8) group: lane fr < 8 holds gate[fr],
     // lane fr + 8 the matching up (DPP row rotate by 8 pairs them); 32 outputs per wave row
@@ -305,18 +348,25 @@ bool docqa_pgemm_ok(int M, int N, int K) {
   return rows * (uint64_t)K * 2ull < (1ull << 32);
 }
 
-// epi 0: C [M, N] bf16; epi 1: C [M, N / 2] = silu(gate) * up (8-interleaved gate|up W)
-int docqa_pgemm(const void* A, const void* W, void* C, int M, int N, int K, int epi, hipStream_t s) {
+// epi 0: C [M, N] bf16; epi 1: C [M, N / 2] = silu(gate) * up (8-interleaved gate|up W);
+// epi 2: P [S, M, N] fp32 split-K slabs (S >= 1 slices of K / S)
+int docqa_pgemm(const void* A, const void* W, void* C, float* P, int M, int N, int K, int S, int epi,
+                hipStream_t s) {
   if (M == 0) return 0;
-  if (!docqa_pgemm_ok(M, N, K) || (epi != EPI_BF16 && epi != EPI_GLU)) return -1;
-  if (!docqa_aligned16(A) || !docqa_aligned16(W) || !docqa_aligned16(C)) return -1;
+  if (!docqa_pgemm_ok(M, N, K) || S < 1 || K % (S * 2 * BK) != 0) return -1;
+  if (epi == EPI_PARTIAL ? P == nullptr : (C == nullptr || S != 1)) return -1;
+  if (epi != EPI_BF16 && epi != EPI_GLU && epi != EPI_PARTIAL) return -1;
+  if (!docqa_aligned16(A) || !docqa_aligned16(W) || !docqa_aligned16(epi == EPI_PARTIAL ? (void*)P : C)) return -1;
   const int ntm = (M + BM - 1) / BM, ntn = N / BN;
   const uint16_t *a = (const uint16_t*)A, *w = (const uint16_t*)W;
   uint16_t* c = (uint16_t*)C;
+  const int grid = ntm * ntn * S, Ks = K / S;
   if (epi == EPI_BF16)
-    pgemm_kernel<EPI_BF16><<<ntm * ntn, 512, 0, s>>>(a, w, c, M, N, K, ntm, ntn);
+    pgemm_kernel<EPI_BF16><<<grid, 512, 0, s>>>(a, w, c, P, M, N, K, ntm, ntn, S, Ks);
+  else if (epi == EPI_GLU)
+    pgemm_kernel<EPI_GLU><<<grid, 512, 0, s>>>(a, w, c, P, M, N, K, ntm, ntn, S, Ks);
   else
-    pgemm_kernel<EPI_GLU><<<ntm * ntn, 512, 0, s>>>(a, w, c, M, N, K, ntm, ntn);
+    pgemm_kernel<EPI_PARTIAL><<<grid, 512, 0, s>>>(a, w, c, P, M, N, K, ntm, ntn, S, Ks);
   DOCQA_CHECK_LAUNCH();
   return 0;
 }

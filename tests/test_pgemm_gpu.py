@@ -66,3 +66,18 @@ def test_prefill_dispatch_routes_to_hand_written_kernels():
     ys = ops.prefill_linear(xs, ws)
     rs = xs.float() @ ws.float().t()
     assert (ys.float() - rs).abs().max().item() <= 2e-2 * rs.abs().max().item()
+
+
+@pytest.mark.parametrize("M,N,K,S", [(256, 6144, 4096, 8), (200, 4096, 14336, 4), (512, 1280, 8192, 16),
+                                     (37, 512, 1024, 2), (256, 256, 256, 1)])
+def test_pgemm_splitk_slabs(M, N, K, S):
+    x, w = _data(M, N, K, seed=6)
+    P = torch.ops.docqa.pgemm_partial(x, w, S)
+    assert P.shape == (S, M, N) and P.dtype == torch.float32
+    r = x.float() @ w.float().t()
+    err = (P.sum(0) - r).abs().max().item()
+    assert err <= 2e-3 * r.abs().max().item() + 1e-3, err
+    # each slab is its own K range
+    Ks = K // S
+    r0 = x[:, :Ks].float() @ w[:, :Ks].float().t()
+    assert (P[0] - r0).abs().max().item() <= 2e-3 * r0.abs().max().item() + 1e-3
