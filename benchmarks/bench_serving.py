@@ -1,19 +1,148 @@
-"""Online serving benchmark for llm-qa: open-loop Poisson arrivals of clinical questions
-into the service's scheduler (RAG embed + kNN + prompt + Llama-3-8B generation), the
-continuous-batching scheduler (engine/scheduler.py) against the static dynamic batcher.
-Reports completed queries/s and per-request latency percentiles (arrival -> answer).
-Synthetic questions, random-init weights.  One JSON line per mode."""
+"""Online serving benchmark for llm-qa: open-loop Poisson arrivals of clinical questions.
+
+Two entry points:
+
+* ``--entry launch`` (default) -- the deployed service: this script starts
+  ``python -m docqa_amd.services.launch --services indexer,qa`` (the same launcher an
+  operator runs; ``--gpus N --tp T`` for data/tensor-parallel replicas under torchrun) in
+  its own process group, waits until /ask/ answers, and fires the arrivals at
+  ``POST /ask/`` over HTTP (httpx).  Latency is arrival -> HTTP response, so it includes
+  the FastAPI/uvicorn front end, the batcher, RAG retrieval and generation.  This
+  process never touches the GPU.
+* ``--entry inproc`` -- the same pipeline in this process, scheduler A/B without HTTP:
+  the continuous-batching scheduler (engine/scheduler.py) against the static dynamic
+  batcher (``--modes continuous,batch``).
+
+Reports completed queries/s and latency percentiles.  Synthetic questions (unique by
+default, ``--questions repeat`` for the 14-template set), random-init weights.  One JSON
+line per mode.  Reference parity: the reference has no serving benchmark;
+its llm-qa /ask/ (llm-qa/main.py) is the endpoint under load.
+"""
 from __future__ import annotations
 
 import argparse
 import json
+import os
 import random
+import signal
 import statistics
+import subprocess
 import sys
 import time
 from pathlib import Path
 
-sys.path.insert(0, str(Path(__file__).resolve().parents[1]))
+ROOT = Path(__file__).resolve().parents[1]
+sys.path.insert(0, str(ROOT))
+
+
+def _arrivals(n: int, rate: float, seed: int = 0) -> list[float]:
+    rng = random.Random(seed)
+    t, out = 0.0, []
+    for _ in range(n):
+        t += rng.expovariate(rate)
+        out.append(t)
+    return out
+
+
+def _pcts(lat: list[float]) -> dict:
+    lat = sorted(lat)
+    return {"p50_latency_ms": round(1e3 * statistics.median(lat), 1),
+            "p90_latency_ms": round(1e3 * lat[int(0.9 * (len(lat) - 1))], 1),
+            "p99_latency_ms": round(1e3 * lat[int(0.99 * (len(lat) - 1))], 1)}
+
+
+def _questions(kind: str, n: int) -> list[str]:
+    from docqa_amd.text.synthetic import synthetic_questions, synthetic_unique_questions
+
+    return synthetic_unique_questions(n, seed=77) if kind == "unique" else synthetic_questions(n, seed=77)
+
+
+def run_launch(a, mode: str) -> dict:
+    """Start the service launcher, drive it over HTTP, stop it."""
+    import asyncio
+
+    import httpx
+
+    import tempfile
+
+    port = 8001 + a.port_offset
+    work = tempfile.mkdtemp(prefix="docqa_serving_bench_")   # fresh index / documents DB per run
+    env = dict(os.environ, INDEX_DIR=work, DATABASE_URL=f"sqlite:///{work}/documents.db", UPLOAD_DIR=work, MAX_NEW_TOKENS=str(a.max_new_tokens), MAX_BATCH=str(a.max_batch),
+               DOCQA_SERVING=mode, TEMPERATURE="0", HSA_ENABLE_IPC_MODE_LEGACY="0")
+    env.setdefault("PYTHONPATH", str(ROOT))
+    cmd = [sys.executable, "-m", "docqa_amd.services.launch", "--services", "indexer,qa",
+           "--llm", a.llm, "--device", a.device, "--port-offset", str(a.port_offset),
+           "--preload-notes", str(a.notes), "--gpus", str(a.gpus), "--tp", str(a.tp),
+           "--kv-mem-fraction", str(a.kv_mem_fraction)]
+    if a.tiny:
+        cmd.append("--tiny")
+    log = open(a.server_log, "w") if a.server_log else subprocess.DEVNULL
+    proc = subprocess.Popen(cmd, cwd=str(ROOT), env=env, stdout=log, stderr=subprocess.STDOUT,
+                            start_new_session=True)
+    qs = _questions(a.questions, a.requests + a.warmup)
+    url = f"http://127.0.0.1:{port}/ask/"
+
+    async def drive() -> dict:
+        limits = httpx.Limits(max_connections=4 * a.max_batch, max_keepalive_connections=4 * a.max_batch)
+        async with httpx.AsyncClient(timeout=900.0, limits=limits) as cl:
+            t_dead = time.perf_counter() + a.start_timeout
+            while True:                       # ready = the index answers a real question
+                if proc.poll() is not None:
+                    raise RuntimeError(f"launcher exited with {proc.returncode}")
+                try:
+                    r = await cl.post(url, json={"question": qs[0]})
+                    if r.status_code == 200:
+                        break
+                except httpx.HTTPError:
+                    pass
+                if time.perf_counter() > t_dead:
+                    raise TimeoutError("service did not become ready")
+                await asyncio.sleep(1.0)
+            # warm-up: graph capture / prefix cache of the fixed prompt text
+            rs = await asyncio.gather(*[cl.post(url, json={"question": q}) for q in qs[1:a.warmup]])
+            assert all(r.status_code == 200 for r in rs), [r.status_code for r in rs if r.status_code != 200][:4]
+            lat, errors = [], 0
+            t0 = time.perf_counter()
+
+            async def one(at: float, q: str):
+                nonlocal errors
+                delay = t0 + at - time.perf_counter()
+                if delay > 0:
+                    await asyncio.sleep(delay)
+                ts = time.perf_counter()
+                r = await cl.post(url, json={"question": q})
+                if r.status_code != 200 or not r.json().get("answer"):
+                    errors += 1
+                lat.append(time.perf_counter() - ts)
+
+            await asyncio.gather(*[one(at, q) for at, q in
+                                   zip(_arrivals(a.requests, a.rate), qs[a.warmup:])])
+            wall = time.perf_counter() - t0
+            return {"lat": lat, "wall": wall, "errors": errors}
+
+    try:
+        res = asyncio.run(drive())
+    finally:
+        try:
+            os.killpg(proc.pid, signal.SIGINT)
+            proc.wait(timeout=60)
+        except (subprocess.TimeoutExpired, ProcessLookupError):
+            try:
+                os.killpg(proc.pid, signal.SIGKILL)
+            except ProcessLookupError:
+                pass
+            proc.wait()
+        import shutil
+
+        shutil.rmtree(work, ignore_errors=True)
+    out = {"metric": "serving_qa_queries_per_sec", "entry": "services.launch (HTTP POST /ask/)",
+           "mode": mode, "offered_rate": a.rate, "value": round(a.requests / res["wall"], 2),
+           "unit": "queries/s", **_pcts(res["lat"]), "errors": res["errors"],
+           "requests": a.requests, "max_new_tokens": a.max_new_tokens, "max_batch": a.max_batch,
+           "gpus": a.gpus, "tp": a.tp, "llm": "tiny" if a.tiny else a.llm, "notes": a.notes, "questions": a.questions,
+           "dtype": "bf16" if a.device != "cpu" else "fp32",
+           "data": "synthetic questions and notes, random-init weights", "wall_s": round(res["wall"], 2)}
+    return out
 
 
 def main():
@@ -25,7 +154,22 @@ def main():
     ap.add_argument("--modes", default="continuous,batch")
     ap.add_argument("--llm", default="llama3-8b")
     ap.add_argument("--device", default="cuda")
+    ap.add_argument("--entry", choices=("launch", "inproc"), default="launch")
+    ap.add_argument("--questions", choices=("unique", "repeat"), default="unique")
+    ap.add_argument("--warmup", type=int, default=64)
+    ap.add_argument("--gpus", type=int, default=1, help="launch entry: GPUs of the service")
+    ap.add_argument("--tp", type=int, default=1, help="launch entry: tensor-parallel size")
+    ap.add_argument("--notes", type=int, default=1000, help="launch entry: synthetic notes indexed at start")
+    ap.add_argument("--port-offset", type=int, default=20000)
+    ap.add_argument("--kv-mem-fraction", type=float, default=0.8)
+    ap.add_argument("--start-timeout", type=float, default=900.0)
+    ap.add_argument("--tiny", action="store_true", help="tiny random models (CPU functional run)")
+    ap.add_argument("--server-log", default="", help="file for the launcher's output")
     a = ap.parse_args()
+    if a.entry == "launch":
+        for mode in a.modes.split(","):
+            print(json.dumps(run_launch(a, mode)), flush=True)
+        return
 
     import torch
 
@@ -33,7 +177,6 @@ def main():
     from docqa_amd.config import Settings
     from docqa_amd.pipeline.builder import StackConfig, build_stack
     from docqa_amd.services.qa import ContinuousBatcher, DynamicBatcher
-    from docqa_amd.text.synthetic import synthetic_questions
     from docqa_amd.utils.metrics import Metrics
 
     cuda = a.device == "cuda"
@@ -41,7 +184,7 @@ def main():
         assert ops.load_native()
     pipe, _ = build_stack(StackConfig(llm=a.llm, max_batch=a.max_batch, max_context=2048,
                                       use_graphs=cuda), device=a.device, log=lambda *x: None)
-    qs = synthetic_questions(a.requests + 64, seed=77)
+    qs = _questions(a.questions, a.requests + a.warmup)
     for mode in a.modes.split(","):
         st = Settings()
         st.max_new_tokens = a.max_new_tokens
@@ -52,17 +195,13 @@ def main():
         # warm-up: capture graphs / tune for the buckets this load will hit
         if mode == "continuous":
             b.engine.warmup()
-        for f in [b.submit("ask", q) for q in qs[:64]]:
+        for f in [b.submit("ask", q) for q in qs[:a.warmup]]:
             f.result(timeout=600)
         es = pipe.engine.stats
         s0 = (es.prefill_s, es.decode_s, es.generated_tokens, getattr(getattr(b, "engine", None), "steps", 0))
-        rng = random.Random(0)
-        t, arrivals = 0.0, []
-        for _ in range(a.requests):
-            t += rng.expovariate(a.rate)
-            arrivals.append(t)
+        arrivals = _arrivals(a.requests, a.rate)
         futs, t0 = [], time.perf_counter()
-        for at, q in zip(arrivals, qs[64:]):
+        for at, q in zip(arrivals, qs[a.warmup:]):
             now = time.perf_counter() - t0
             if at > now:
                 time.sleep(at - now)
@@ -75,11 +214,9 @@ def main():
         lat = sorted(v for v in b.metrics.values("ask_latency_s")[-a.requests:])
         b.stop()
         s1 = (es.prefill_s, es.decode_s, es.generated_tokens, getattr(getattr(b, "engine", None), "steps", 0))
-        out = {"metric": "serving_qa_queries_per_sec", "mode": mode, "offered_rate": a.rate,
-               "value": round(a.requests / (t_end - t0), 2), "unit": "queries/s",
-               "p50_latency_ms": round(1e3 * statistics.median(lat), 1),
-               "p90_latency_ms": round(1e3 * lat[int(0.9 * (len(lat) - 1))], 1),
-               "p99_latency_ms": round(1e3 * lat[int(0.99 * (len(lat) - 1))], 1),
+        out = {"metric": "serving_qa_queries_per_sec", "entry": "in-process batcher", "mode": mode,
+               "offered_rate": a.rate, "value": round(a.requests / (t_end - t0), 2), "unit": "queries/s",
+               **_pcts(lat), "questions": a.questions,
                "requests": a.requests, "max_new_tokens": a.max_new_tokens, "max_batch": a.max_batch,
                "llm": a.llm, "dtype": "bf16", "data": "synthetic questions, random-init weights",
                "engine_prefill_s": round(s1[0] - s0[0], 2), "engine_decode_s": round(s1[1] - s0[1], 2),

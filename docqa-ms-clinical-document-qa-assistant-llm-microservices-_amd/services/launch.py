@@ -34,6 +34,7 @@ import threading
 
 import uvicorn
 
+from ..config import Settings
 from .stack import DocQAStack, StackOptions
 
 
@@ -109,7 +110,15 @@ def spawn_workers(gpus: int, argv: list[str]) -> int:
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={gpus}",
            "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), "-m",
            "docqa_amd.services.launch", *argv]
-    return subprocess.call(cmd)
+    p = subprocess.Popen(cmd)
+    try:
+        return p.wait()
+    except KeyboardInterrupt:       # torchrun got the same SIGINT and shuts the ranks down
+        try:
+            return p.wait(timeout=120)
+        except subprocess.TimeoutExpired:
+            p.kill()
+            return p.wait()
 
 
 def run_parallel(a, opts: "StackOptions") -> None:
@@ -138,7 +147,12 @@ def run_parallel(a, opts: "StackOptions") -> None:
     st = Settings()
     o = a.port_offset
     if ps.tp_rank != 0:
-        # follower: only this rank's shard of the generator, mirroring the leader's steps
+        # follower: only this rank's shard of the generator, mirroring the leader's steps.
+        # Shutdown is the leader's "stop" message (a Ctrl-C reaches every rank at once;
+        # a follower that died first would leave the leader's last broadcast hanging).
+        import signal
+
+        signal.signal(signal.SIGINT, signal.SIG_IGN)
         ck.use_checkpoint_tokenizers(opts.llm, opts.embed)
         model = ck.resolve_llama(opts.llm, device=opts.device)
         eng = LLMEngine(model, max_batch=opts.max_batch, max_context=opts.max_context, use_graphs=opts.use_graphs,
@@ -184,6 +198,9 @@ def main() -> None:
                     'when they die: e.g. "ingest,ui;deid;indexer;qa"')
     ap.add_argument("--gpus", type=int, default=1, help="GPUs (one process each, torchrun)")
     ap.add_argument("--tp", type=int, default=1, help="tensor-parallel size of the generator (divides --gpus)")
+    ap.add_argument("--preload-notes", type=int, default=0,
+                    help="index this many synthetic clinical notes at start (serving benchmarks, demos)")
+    ap.add_argument("--kv-mem-fraction", type=float, default=0.8, help="KV pool share of free HBM")
     a = ap.parse_args()
     import os
     import sys
@@ -206,7 +223,9 @@ def main() -> None:
                         ner="tiny-bert" if a.tiny else "clinical-bert", device=a.device,
                         use_graphs=a.device != "cpu", max_context=2048 if a.tiny else 4096,
                         real_synthese=a.real_synthese,
-                        services=tuple(x for x in a.services.split(",") if x))
+                        services=tuple(x for x in a.services.split(",") if x),
+                        max_batch=Settings().max_batch, preload_notes=a.preload_notes,
+                        kv_mem_fraction=a.kv_mem_fraction)
     if under_torchrun:
         run_parallel(a, opts)
         return

@@ -44,6 +44,7 @@ class StackOptions:
     qa_lockstep: object = None    # llm-qa leads a tensor-parallel group (services/launch.py --tp)
     qa_replicas: tuple = ()       # llm-qa front-end over these data-parallel replica URLs
     kv_mem_fraction: float | None = 0.8   # KV pool from free HBM (GPU only; LLMEngine)
+    preload_notes: int = 0        # index this many synthetic clinical notes at start (benchmarks / demos)
 
 
 class _LocalRetrieval(synthese.RetrievalClient):
@@ -115,6 +116,11 @@ class DocQAStack:
             self.indexer = indexer_mod.SemanticIndexer(
                 self.encoder, self.enc_tok, self.st, device=dev,
                 on_indexed=lambda i: db.set_status(i, docs_db.STATUS_INDEXED)).startup()
+            if opts.preload_notes:
+                from ..pipeline.corpus import build_corpus
+
+                self.indexer.add_records(build_corpus(opts.preload_notes, None, 0))
+                self.indexer.commit()
             self.indexer.start_consumer(self.broker)
             self.indexer_app = indexer_mod.create_app(self.indexer)
         if "qa" in svc:

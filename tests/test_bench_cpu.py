@@ -86,3 +86,18 @@ def test_pipeline_bench_tp8_gloo_replicated_index():
     d = _last_json(r.stdout)
     assert d["n_gpus"] == 8 and d["config"]["parallelism"] == "tp8" and d["value"] > 0
     assert d["config"]["index"] == "flat-L2 sharded x8"
+
+
+def test_serving_bench_through_service_launcher():
+    """bench_serving's default entry: the services launcher in a child process group
+    (TP 2 under torchrun, gloo), Poisson arrivals over HTTP POST /ask/."""
+    env = dict(os.environ, PYTHONPATH=str(ROOT))
+    cmd = [sys.executable, str(ROOT / "benchmarks" / "bench_serving.py"), "--entry", "launch", "--tiny",
+           "--device", "cpu", "--requests", "16", "--warmup", "4", "--rate", "20", "--max-new-tokens", "6",
+           "--max-batch", "8", "--modes", "continuous", "--notes", "40", "--gpus", "2", "--tp", "2",
+           "--port-offset", str(21000 + os.getpid() % 5000)]
+    r = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=600, env=env)
+    assert r.returncode == 0, r.stderr[-3000:]
+    out = json.loads(r.stdout.strip().splitlines()[-1])
+    assert out["errors"] == 0 and out["requests"] == 16 and out["tp"] == 2
+    assert out["entry"].startswith("services.launch") and out["p50_latency_ms"] > 0
