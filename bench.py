@@ -119,6 +119,7 @@ def main() -> None:
     sync()
     eng = pipe.engine
     s0 = (eng.stats.prefill_s, eng.stats.decode_s, eng.stats.prompt_tokens, eng.stats.cached_tokens)
+    a0 = (eng.stats.attn_kv_blocks, eng.stats.attn_batches)
     t0 = time.perf_counter()
     step_times, stages, chunks = [], [], set()
     for ans, st, lat in pipe.answer_pipelined([batch_for(a.warmup + s) for s in range(a.steps)], params):
@@ -139,6 +140,9 @@ def main() -> None:
     queries = ps.dp_size * a.batch * a.steps
     qps = queries / elapsed_max
     s1 = (eng.stats.prefill_s, eng.stats.decode_s, eng.stats.prompt_tokens, eng.stats.cached_tokens)
+    a1 = (eng.stats.attn_kv_blocks, eng.stats.attn_batches)
+    kc = eng.kv.caches[0][0]
+    block_bytes = 2 * kc[0].numel() * kc.element_size()       # K + V of one block, one layer
     # workload descriptors over the whole job's timed questions (every DP rank's batches)
     timed_q = [q for s_ in range(a.steps) for d in range(ps.dp_size)
                for q in qs[((a.warmup + s_) * ps.dp_size + d) * a.batch:((a.warmup + s_) * ps.dp_size + d + 1) * a.batch]]
@@ -179,6 +183,11 @@ def main() -> None:
             "engine_ms_per_batch": {"prefill": round(1e3 * (s1[0] - s0[0]) / a.steps, 2),
                                     "decode": round(1e3 * (s1[1] - s0[1]) / a.steps, 2)},
             "prefix_cached_frac": round((s1[3] - s0[3]) / max(1, s1[2] - s0[2]), 3),
+            # distinct KV bytes one layer's decode attention must read at a batch's first
+            # decode step (cascade prefix once): the HBM floor of that kernel
+            "decode_attn_kv_mb_per_layer": round((a1[0] - a0[0]) * block_bytes / max(1, a1[1] - a0[1]) / 1e6, 1),
+            "decode_attn_kv_blocks": round((a1[0] - a0[0]) / max(1, a1[1] - a0[1]), 1),
+            "kv_block_tokens": eng.block_size,
             "workload": {
                 "questions": a.questions,
                 "template": os.environ.get("QA_TEMPLATE", "cache_friendly"),

@@ -57,6 +57,16 @@ def _questions(kind: str, n: int) -> list[str]:
     return synthetic_unique_questions(n, seed=77) if kind == "unique" else synthetic_questions(n, seed=77)
 
 
+def _engine_counters(text: str) -> dict:
+    """The continuous scheduler's counters from the llm-qa Prometheus text."""
+    out = {}
+    for line in text.splitlines():
+        if line.startswith("llm_qa_engine_"):
+            k, v = line.split()
+            out[k[len("llm_qa_engine_"):]] = float(v)
+    return out
+
+
 def run_launch(a, mode: str) -> dict:
     """Start the service launcher, drive it over HTTP, stop it."""
     import asyncio
@@ -102,6 +112,7 @@ def run_launch(a, mode: str) -> dict:
             rs = await asyncio.gather(*[cl.post(url, json={"question": q}) for q in qs[1:a.warmup]])
             assert all(r.status_code == 200 for r in rs), [r.status_code for r in rs if r.status_code != 200][:4]
             lat, errors = [], 0
+            c0 = _engine_counters((await cl.get(url.replace("/ask/", "/metrics"))).text)
             t0 = time.perf_counter()
 
             async def one(at: float, q: str):
@@ -118,7 +129,9 @@ def run_launch(a, mode: str) -> dict:
             await asyncio.gather(*[one(at, q) for at, q in
                                    zip(_arrivals(a.requests, a.rate), qs[a.warmup:])])
             wall = time.perf_counter() - t0
-            return {"lat": lat, "wall": wall, "errors": errors}
+            c1 = _engine_counters((await cl.get(url.replace("/ask/", "/metrics"))).text)
+            return {"lat": lat, "wall": wall, "errors": errors,
+                    "engine": {k: int(c1[k] - c0.get(k, 0)) for k in c1}}
 
     try:
         res = asyncio.run(drive())
@@ -141,7 +154,8 @@ def run_launch(a, mode: str) -> dict:
            "requests": a.requests, "max_new_tokens": a.max_new_tokens, "max_batch": a.max_batch,
            "gpus": a.gpus, "tp": a.tp, "llm": "tiny" if a.tiny else a.llm, "notes": a.notes, "questions": a.questions,
            "dtype": "bf16" if a.device != "cpu" else "fp32",
-           "data": "synthetic questions and notes, random-init weights", "wall_s": round(res["wall"], 2)}
+           "data": "synthetic questions and notes, random-init weights", "wall_s": round(res["wall"], 2),
+           "scheduler": res["engine"]}
     return out
 
 
@@ -198,7 +212,9 @@ def main():
         for f in [b.submit("ask", q) for q in qs[:a.warmup]]:
             f.result(timeout=600)
         es = pipe.engine.stats
-        s0 = (es.prefill_s, es.decode_s, es.generated_tokens, getattr(getattr(b, "engine", None), "steps", 0))
+        ce = getattr(b, "engine", None)
+        s0 = (es.prefill_s, es.decode_s, es.generated_tokens, getattr(ce, "steps", 0),
+              getattr(ce, "preempted", 0), getattr(ce, "kv_blocked", 0))
         arrivals = _arrivals(a.requests, a.rate)
         futs, t0 = [], time.perf_counter()
         for at, q in zip(arrivals, qs[a.warmup:]):
@@ -213,14 +229,16 @@ def main():
         # latency = resolve time - submit time (futures record completion via callbacks)
         lat = sorted(v for v in b.metrics.values("ask_latency_s")[-a.requests:])
         b.stop()
-        s1 = (es.prefill_s, es.decode_s, es.generated_tokens, getattr(getattr(b, "engine", None), "steps", 0))
+        s1 = (es.prefill_s, es.decode_s, es.generated_tokens, getattr(ce, "steps", 0),
+              getattr(ce, "preempted", 0), getattr(ce, "kv_blocked", 0))
         out = {"metric": "serving_qa_queries_per_sec", "entry": "in-process batcher", "mode": mode,
                "offered_rate": a.rate, "value": round(a.requests / (t_end - t0), 2), "unit": "queries/s",
                **_pcts(lat), "questions": a.questions,
                "requests": a.requests, "max_new_tokens": a.max_new_tokens, "max_batch": a.max_batch,
                "llm": a.llm, "dtype": "bf16", "data": "synthetic questions, random-init weights",
                "engine_prefill_s": round(s1[0] - s0[0], 2), "engine_decode_s": round(s1[1] - s0[1], 2),
-               "decode_steps": s1[3] - s0[3], "wall_s": round(t_end - t0, 2)}
+               "decode_steps": s1[3] - s0[3], "wall_s": round(t_end - t0, 2),
+               "scheduler": {"preemptions": s1[4] - s0[4], "kv_admission_blocked": s1[5] - s0[5]}}
         print(json.dumps(out), flush=True)
         if cuda:
             torch.cuda.synchronize()

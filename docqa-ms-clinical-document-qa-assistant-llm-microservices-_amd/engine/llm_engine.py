@@ -86,6 +86,10 @@ class GenStats:
     prompt_tokens: int = 0
     generated_tokens: int = 0
     cached_tokens: int = 0     # prompt tokens served from the prefix cache
+    # distinct KV blocks one decode step's attention reads at its first step (the cascade
+    # prefix counted once) -- the HBM floor of decode attention, summed over batches
+    attn_kv_blocks: int = 0
+    attn_batches: int = 0
 
 
 def _bucket(n: int, cap: int) -> int:
@@ -653,6 +657,8 @@ class LLMEngine:
                     self.register_prefixes(prompts, tables, r.keys)
             self.stats.cached_tokens += sum(cached)
             nshared = self._shared_prefix_blocks(tables, cached)
+            self.stats.attn_kv_blocks += nshared + len({b for t in tables for b in t[nshared:]})
+            self.stats.attn_batches += 1
             g = self._get_graph(_bucket(B, self.max_batch) if self.use_graphs else B, greedy, nshared > 0)
             if nshared:
                 st = torch.zeros(self.max_blocks_per_seq, dtype=torch.int32)

@@ -129,6 +129,7 @@ class ContinuousEngine:
         self.preempt = os.environ.get("DOCQA_PREEMPT", "1") == "1"
         self.reserve_ahead = int(os.environ.get("DOCQA_RESERVE_AHEAD", str(engine.block_size)))
         self.preempted = 0
+        self.kv_blocked = 0       # admissions deferred because the KV pool was out of blocks
 
     # ------------------------------------------------------------------ client side
     def submit(self, prompt: list[int], params: SamplingParams | None = None, on_token=None) -> cf.Future:
@@ -284,6 +285,7 @@ class ContinuousEngine:
                         self.waiting.popleft().future.set_exception(MemoryError(
                             f"request needs {need} KV blocks, the cache has {alloc.num_free()} free"))
                         continue
+                    self.kv_blocked += 1
                     break                        # retry after running requests retire
                 r.blocks, r.cached, r.res = res.tables[0], res.cached[0], res
                 res.tables = []                  # owned by the request from here on

@@ -202,6 +202,10 @@ class ContinuousBatcher:
             except Exception as e:  # noqa: BLE001
                 eng._fail_all(e)
                 _maybe_exit_on_device_error(e)
+            m = self.metrics
+            m.set("engine_steps", eng.steps)
+            m.set("engine_preemptions", eng.preempted)
+            m.set("engine_kv_admission_blocked", eng.kv_blocked)
             if wd:
                 wd.beat()
         if wd:

@@ -17,6 +17,11 @@ class Metrics:
         with self._lock:
             self._c[name] += v
 
+    def set(self, name: str, v: float) -> None:
+        """Set a counter to an absolute value (mirrors a counter kept elsewhere)."""
+        with self._lock:
+            self._c[name] = float(v)
+
     def observe(self, name: str, v: float) -> None:
         with self._lock:
             self._o[name].append(float(v))
