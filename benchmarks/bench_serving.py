@@ -67,18 +67,19 @@ def _engine_counters(text: str) -> dict:
     return out
 
 
-def run_launch(a, mode: str) -> dict:
-    """Start the service launcher, drive it over HTTP, stop it."""
+def run_launch(a, mode: str) -> list[dict]:
+    """Start the service launcher, drive it over HTTP at each offered rate, stop it."""
     import asyncio
+    import shutil
+    import tempfile
 
     import httpx
 
-    import tempfile
-
     port = 8001 + a.port_offset
     work = tempfile.mkdtemp(prefix="docqa_serving_bench_")   # fresh index / documents DB per run
-    env = dict(os.environ, INDEX_DIR=work, DATABASE_URL=f"sqlite:///{work}/documents.db", UPLOAD_DIR=work, MAX_NEW_TOKENS=str(a.max_new_tokens), MAX_BATCH=str(a.max_batch),
-               DOCQA_SERVING=mode, TEMPERATURE="0", HSA_ENABLE_IPC_MODE_LEGACY="0")
+    env = dict(os.environ, INDEX_DIR=work, DATABASE_URL=f"sqlite:///{work}/documents.db", UPLOAD_DIR=work,
+               MAX_NEW_TOKENS=str(a.max_new_tokens), MAX_BATCH=str(a.max_batch), DOCQA_SERVING=mode,
+               TEMPERATURE="0", HSA_ENABLE_IPC_MODE_LEGACY="0")
     env.setdefault("PYTHONPATH", str(ROOT))
     cmd = [sys.executable, "-m", "docqa_amd.services.launch", "--services", "indexer,qa",
            "--llm", a.llm, "--device", a.device, "--port-offset", str(a.port_offset),
@@ -89,10 +90,11 @@ def run_launch(a, mode: str) -> dict:
     log = open(a.server_log, "w") if a.server_log else subprocess.DEVNULL
     proc = subprocess.Popen(cmd, cwd=str(ROOT), env=env, stdout=log, stderr=subprocess.STDOUT,
                             start_new_session=True)
-    qs = _questions(a.questions, a.requests + a.warmup)
+    qs = _questions(a.questions, a.warmup + a.requests * len(a.rates))
     url = f"http://127.0.0.1:{port}/ask/"
+    murl = f"http://127.0.0.1:{port}/metrics"
 
-    async def drive() -> dict:
+    async def drive() -> list[dict]:
         limits = httpx.Limits(max_connections=4 * a.max_batch, max_keepalive_connections=4 * a.max_batch)
         async with httpx.AsyncClient(timeout=900.0, limits=limits) as cl:
             t_dead = time.perf_counter() + a.start_timeout
@@ -111,30 +113,33 @@ def run_launch(a, mode: str) -> dict:
             # warm-up: graph capture / prefix cache of the fixed prompt text
             rs = await asyncio.gather(*[cl.post(url, json={"question": q}) for q in qs[1:a.warmup]])
             assert all(r.status_code == 200 for r in rs), [r.status_code for r in rs if r.status_code != 200][:4]
-            lat, errors = [], 0
-            c0 = _engine_counters((await cl.get(url.replace("/ask/", "/metrics"))).text)
-            t0 = time.perf_counter()
+            results = []
+            for ri, rate in enumerate(a.rates):
+                batch_q = qs[a.warmup + ri * a.requests:a.warmup + (ri + 1) * a.requests]
+                lat, errors = [], 0
+                c0 = _engine_counters((await cl.get(murl)).text)
+                t0 = time.perf_counter()
 
-            async def one(at: float, q: str):
-                nonlocal errors
-                delay = t0 + at - time.perf_counter()
-                if delay > 0:
-                    await asyncio.sleep(delay)
-                ts = time.perf_counter()
-                r = await cl.post(url, json={"question": q})
-                if r.status_code != 200 or not r.json().get("answer"):
-                    errors += 1
-                lat.append(time.perf_counter() - ts)
+                async def one(at: float, q: str):
+                    nonlocal errors
+                    delay = t0 + at - time.perf_counter()
+                    if delay > 0:
+                        await asyncio.sleep(delay)
+                    ts = time.perf_counter()
+                    r = await cl.post(url, json={"question": q})
+                    if r.status_code != 200 or not r.json().get("answer"):
+                        errors += 1
+                    lat.append(time.perf_counter() - ts)
 
-            await asyncio.gather(*[one(at, q) for at, q in
-                                   zip(_arrivals(a.requests, a.rate), qs[a.warmup:])])
-            wall = time.perf_counter() - t0
-            c1 = _engine_counters((await cl.get(url.replace("/ask/", "/metrics"))).text)
-            return {"lat": lat, "wall": wall, "errors": errors,
-                    "engine": {k: int(c1[k] - c0.get(k, 0)) for k in c1}}
+                await asyncio.gather(*[one(at, q) for at, q in zip(_arrivals(a.requests, rate), batch_q)])
+                wall = time.perf_counter() - t0
+                c1 = _engine_counters((await cl.get(murl)).text)
+                results.append({"rate": rate, "lat": lat, "wall": wall, "errors": errors,
+                                "engine": {k: int(c1[k] - c0.get(k, 0)) for k in c1}})
+            return results
 
     try:
-        res = asyncio.run(drive())
+        runs = asyncio.run(drive())
     finally:
         try:
             os.killpg(proc.pid, signal.SIGINT)
@@ -145,23 +150,21 @@ def run_launch(a, mode: str) -> dict:
             except ProcessLookupError:
                 pass
             proc.wait()
-        import shutil
-
         shutil.rmtree(work, ignore_errors=True)
-    out = {"metric": "serving_qa_queries_per_sec", "entry": "services.launch (HTTP POST /ask/)",
-           "mode": mode, "offered_rate": a.rate, "value": round(a.requests / res["wall"], 2),
-           "unit": "queries/s", **_pcts(res["lat"]), "errors": res["errors"],
-           "requests": a.requests, "max_new_tokens": a.max_new_tokens, "max_batch": a.max_batch,
-           "gpus": a.gpus, "tp": a.tp, "llm": "tiny" if a.tiny else a.llm, "notes": a.notes, "questions": a.questions,
-           "dtype": "bf16" if a.device != "cpu" else "fp32",
-           "data": "synthetic questions and notes, random-init weights", "wall_s": round(res["wall"], 2),
-           "scheduler": res["engine"]}
-    return out
+    return [{"metric": "serving_qa_queries_per_sec", "entry": "services.launch (HTTP POST /ask/)",
+             "mode": mode, "offered_rate": res["rate"], "value": round(a.requests / res["wall"], 2),
+             "unit": "queries/s", **_pcts(res["lat"]), "errors": res["errors"],
+             "requests": a.requests, "max_new_tokens": a.max_new_tokens, "max_batch": a.max_batch,
+             "gpus": a.gpus, "tp": a.tp, "llm": "tiny" if a.tiny else a.llm, "notes": a.notes,
+             "questions": a.questions, "dtype": "bf16" if a.device != "cpu" else "fp32",
+             "data": "synthetic questions and notes, random-init weights", "wall_s": round(res["wall"], 2),
+             "scheduler": res["engine"]} for res in runs]
 
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--rate", type=float, default=80.0, help="mean arrivals per second")
+    ap.add_argument("--rate", default="80", help="mean arrivals per second (launch entry: a comma list, "
+                    "run one after another on the same service)")
     ap.add_argument("--requests", type=int, default=600)
     ap.add_argument("--max-new-tokens", type=int, default=128)
     ap.add_argument("--max-batch", type=int, default=128)
@@ -180,9 +183,12 @@ def main():
     ap.add_argument("--tiny", action="store_true", help="tiny random models (CPU functional run)")
     ap.add_argument("--server-log", default="", help="file for the launcher's output")
     a = ap.parse_args()
+    a.rates = [float(x) for x in a.rate.split(",")]
+    a.rate = a.rates[0]
     if a.entry == "launch":
         for mode in a.modes.split(","):
-            print(json.dumps(run_launch(a, mode)), flush=True)
+            for out in run_launch(a, mode):
+                print(json.dumps(out), flush=True)
         return
 
     import torch
