@@ -754,7 +754,7 @@ std::tuple<at::Tensor, at::Tensor> knn(const at::Tensor& xb, const at::Tensor& x
   const bool bf = xb.scalar_type() == at::kBFloat16;
   TORCH_CHECK(bf || xb.scalar_type() == at::kFloat, "database must be fp32 or bf16");
   TORCH_CHECK(xb.size(1) == xq.size(1), "dimension mismatch");
-  TORCH_CHECK(k >= 1 && docqa_knn_kpad(k) > 0, "k must be in [1, 32]");
+  TORCH_CHECK(k >= 1 && docqa_knn_kpad(k) > 0, "k must be in [1, 64]");
   const int N = xb.size(0), d = xb.size(1), nq = xq.size(0);
   c10::DeviceGuard g(xb.device());
   auto out_d = at::empty({nq, k}, xq.options());
@@ -800,8 +800,8 @@ std::tuple<at::Tensor, at::Tensor> ivfpq_search(const at::Tensor& xq, const at::
   const int nq = xq.size(0), d = xq.size(1), nprobe = probes.size(1), M = pq.size(0);
   TORCH_CHECK(pq.size(1) == 256 && pq.size(2) * M == d, "pq codebook must be [M, 256, d/M]");
   TORCH_CHECK(codes.size(1) == M, "codes must be [N, M]");
-  TORCH_CHECK(k >= 1 && k <= 32, "k must be in [1, 32]");
-  const int kp = k <= 4 ? 4 : k <= 8 ? 8 : k <= 16 ? 16 : 32;
+  TORCH_CHECK(k >= 1 && k <= 64, "k must be in [1, 64]");
+  const int kp = k <= 4 ? 4 : k <= 8 ? 8 : k <= 16 ? 16 : k <= 32 ? 32 : 64;
   c10::DeviceGuard g(xq.device());
   auto out_d = at::empty({nq, k}, xq.options());
   auto out_i = at::empty({nq, k}, xq.options().dtype(at::kLong));

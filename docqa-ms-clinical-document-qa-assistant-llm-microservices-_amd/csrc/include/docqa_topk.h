@@ -23,6 +23,7 @@ __device__ __forceinline__ void topk_insert(float (&td)[K], int (&ti)[K], float 
 }
 
 // Merge nblk partial lists per query: ws_d/ws_i [nq][nblk][K] -> out [nq][k_out].
+// Dynamic LDS: topk_merge_lds(K) bytes (128 KB at K = 64).
 //   qnorm_src != nullptr: add ||q||^2 (flat L2 produced ||x||^2 - 2 x.q)
 //   IP: scores were negated, flip back
 //   idmap != nullptr: translate candidate positions to stored 64-bit ids
@@ -31,8 +32,9 @@ __global__ __launch_bounds__(256) void topk_merge_kernel(
     const float* __restrict__ ws_d, const int* __restrict__ ws_i, int nblk,
     const float* __restrict__ qnorm_src, int d, int k_out, float* __restrict__ out_d,
     int64_t* __restrict__ out_i, int64_t id_offset, const int64_t* __restrict__ idmap) {
-  __shared__ float sd[256 * K];
-  __shared__ int si[256 * K];
+  extern __shared__ __attribute__((aligned(16))) unsigned char topk_smem[];
+  float* sd = reinterpret_cast<float*>(topk_smem);
+  int* si = reinterpret_cast<int*>(topk_smem + 256 * K * sizeof(float));
   __shared__ float qn;
   const int q = blockIdx.x, tid = threadIdx.x;
   float td[K];
@@ -75,5 +77,7 @@ __global__ __launch_bounds__(256) void topk_merge_kernel(
     }
   }
 }
+
+constexpr size_t topk_merge_lds(int K) { return (size_t)256 * K * 8; }
 
 }  // namespace docqa

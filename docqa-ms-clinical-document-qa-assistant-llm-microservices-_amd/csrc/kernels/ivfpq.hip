@@ -177,20 +177,23 @@ int docqa_ivfpq_search(const float* xq, const float* centroids, const float* pq,
                        float* ws_d, int* ws_i, float* out_d, int64_t* out_i, hipStream_t s) {
   if (nq == 0) return 0;
   if (d % M != 0 || M % 4 != 0) return -1;
-  const int kp = k <= 4 ? 4 : k <= 8 ? 8 : k <= 16 ? 16 : k <= 32 ? 32 : -1;
+  const int kp = k <= 4 ? 4 : k <= 8 ? 8 : k <= 16 ? 16 : k <= 32 ? 32 : k <= 64 ? 64 : -1;
   int rc;
   switch (kp) {
     case 4: rc = launch_scan<4>(xq, centroids, pq, codes, list_off, probes, nq, nprobe, d, M, ws_d, ws_i, s);
-      if (!rc) topk_merge_kernel<4, false><<<nq, 256, 0, s>>>(ws_d, ws_i, nprobe, nullptr, d, k, out_d, out_i, 0, ids);
+      if (!rc) topk_merge_kernel<4, false><<<nq, 256, topk_merge_lds(4), s>>>(ws_d, ws_i, nprobe, nullptr, d, k, out_d, out_i, 0, ids);
       break;
     case 8: rc = launch_scan<8>(xq, centroids, pq, codes, list_off, probes, nq, nprobe, d, M, ws_d, ws_i, s);
-      if (!rc) topk_merge_kernel<8, false><<<nq, 256, 0, s>>>(ws_d, ws_i, nprobe, nullptr, d, k, out_d, out_i, 0, ids);
+      if (!rc) topk_merge_kernel<8, false><<<nq, 256, topk_merge_lds(8), s>>>(ws_d, ws_i, nprobe, nullptr, d, k, out_d, out_i, 0, ids);
       break;
     case 16: rc = launch_scan<16>(xq, centroids, pq, codes, list_off, probes, nq, nprobe, d, M, ws_d, ws_i, s);
-      if (!rc) topk_merge_kernel<16, false><<<nq, 256, 0, s>>>(ws_d, ws_i, nprobe, nullptr, d, k, out_d, out_i, 0, ids);
+      if (!rc) topk_merge_kernel<16, false><<<nq, 256, topk_merge_lds(16), s>>>(ws_d, ws_i, nprobe, nullptr, d, k, out_d, out_i, 0, ids);
       break;
     case 32: rc = launch_scan<32>(xq, centroids, pq, codes, list_off, probes, nq, nprobe, d, M, ws_d, ws_i, s);
-      if (!rc) topk_merge_kernel<32, false><<<nq, 256, 0, s>>>(ws_d, ws_i, nprobe, nullptr, d, k, out_d, out_i, 0, ids);
+      if (!rc) topk_merge_kernel<32, false><<<nq, 256, topk_merge_lds(32), s>>>(ws_d, ws_i, nprobe, nullptr, d, k, out_d, out_i, 0, ids);
+      break;
+    case 64: rc = launch_scan<64>(xq, centroids, pq, codes, list_off, probes, nq, nprobe, d, M, ws_d, ws_i, s);
+      if (!rc) topk_merge_kernel<64, false><<<nq, 256, topk_merge_lds(64), s>>>(ws_d, ws_i, nprobe, nullptr, d, k, out_d, out_i, 0, ids);
       break;
     default: return -1;
   }

@@ -165,13 +165,13 @@ static int launch_knn(const void* xb, const float* norms, int N, int d, const fl
   if (lds > 160 * 1024) return -2;
   dim3 g1(nblk, (nq + 31) / 32);
   knn_tile_kernel<K, IP, BF16><<<g1, 256, lds, s>>>(xb, norms, N, d, xq, nq, rpb, ws_d, ws_i, nblk);
-  topk_merge_kernel<K, IP><<<nq, 256, 0, s>>>(ws_d, ws_i, nblk, xq, d, k, out_d, out_i, id_offset, nullptr);
+  topk_merge_kernel<K, IP><<<nq, 256, topk_merge_lds(K), s>>>(ws_d, ws_i, nblk, xq, d, k, out_d, out_i, id_offset, nullptr);
   DOCQA_CHECK_LAUNCH();
   return 0;
 }
 
 // ws_d/ws_i: [nq, nblk, Kpad] with Kpad = the template K the call selects (<= 64)
-int docqa_knn_kpad(int k) { return k <= 4 ? 4 : k <= 8 ? 8 : k <= 16 ? 16 : k <= 32 ? 32 : -1; }
+int docqa_knn_kpad(int k) { return k <= 4 ? 4 : k <= 8 ? 8 : k <= 16 ? 16 : k <= 32 ? 32 : k <= 64 ? 64 : -1; }
 
 int docqa_knn(const void* xb, const float* norms, int N, int d, int is_bf16, const float* xq,
               int nq, int k, int metric_ip, float* ws_d, int* ws_i, int nblk, float* out_d,
@@ -197,6 +197,7 @@ int docqa_knn(const void* xb, const float* norms, int N, int d, int is_bf16, con
     KNN_CASE(8)
     KNN_CASE(16)
     KNN_CASE(32)
+    KNN_CASE(64)
     default: return -1;
   }
 #undef KNN_CASE

@@ -102,7 +102,10 @@ class IVFPQIndex:
         nprobe = min(nprobe or self.nprobe, self.nlist)
         xq = torch.as_tensor(xq).to(self.device, torch.float32).contiguous()
         cn = (self.centroids ** 2).sum(1)
-        _, probes = ops.knn(self.centroids, cn, xq, nprobe, False, 0)
+        if nprobe <= 64:
+            _, probes = ops.knn(self.centroids, cn, xq, nprobe, False, 0)
+        else:   # wide probes (recall sweeps): the coarse distances are a small GEMM
+            probes = torch.topk(cn[None, :] - 2 * xq @ self.centroids.t(), nprobe, dim=1, largest=False).indices
         if self.device.type == "cuda":
             return ops._native().ivfpq_search(xq, self.centroids, self.pq, self.codes, self.ids,
                                               self.list_off, probes.contiguous(), k)

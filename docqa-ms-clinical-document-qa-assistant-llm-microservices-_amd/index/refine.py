@@ -30,7 +30,7 @@ class RefineFlat:
 
     def search(self, xq, k: int, k_factor: int | None = None, **base_kw):
         kf = k_factor or self.k_factor
-        kc = max(k, min(32, k * kf))
+        kc = max(k, min(64, k * kf))     # the GPU top-k kernels keep up to 64 per query
         xq = torch.as_tensor(xq).to(self.xb.device, torch.float32).contiguous()
         _, cand = self.base.search(xq, kc, **base_kw)
         cand = cand.to(self.xb.device)

@@ -19,7 +19,8 @@ if [ "$SKIP_PROF" != "1" ]; then
   TR=$(ls gpurun_out/prof_$TAG/*kernel_trace.csv | head -1)
   WIN=${WINDOW_MS:-1300}
   python scripts/trace_tail.py "$TR" --window-ms $WIN --steps ${TAIL_STEPS:-1} --top 40 --gaps ${GAPS:-0} > gpurun_out/prof_${TAG}_tail.txt
+  python scripts/phase_split.py "$TR" --last 3 > gpurun_out/prof_${TAG}_phases.txt
   rm -f gpurun_out/prof_$TAG/*kernel_trace.csv
-  head -45 gpurun_out/prof_${TAG}_tail.txt
+  head -45 gpurun_out/prof_${TAG}_tail.txt; cat gpurun_out/prof_${TAG}_phases.txt
 fi
 exit 0

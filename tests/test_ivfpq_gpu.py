@@ -6,8 +6,8 @@ import torch
 pytestmark = pytest.mark.gpu
 
 
-@pytest.mark.parametrize("d,M", [(64, 16), (768, 64), (96, 12)])
-def test_ivfpq_gpu_matches_reference(d, M):
+@pytest.mark.parametrize("d,M,k", [(64, 16, 10), (768, 64, 10), (96, 12, 10), (768, 64, 40), (64, 16, 64)])
+def test_ivfpq_gpu_matches_reference(d, M, k):
     from docqa_amd import ops
     from docqa_amd.index.ivfpq import IVFPQIndex
 
@@ -28,10 +28,10 @@ def test_ivfpq_gpu_matches_reference(d, M):
     codes_ref = ((r - idx.pq[None]) ** 2).sum(-1).argmin(-1).to(torch.uint8).cpu()
     assert (codes_gpu == codes_ref).float().mean() > 0.995  # fp near-ties only
     q = (x[:40] + 0.1 * torch.randn(40, d, generator=g)).cuda()
-    D, I = idx.search(q, 10, nprobe=8)
+    D, I = idx.search(q, k, nprobe=8)
     cn = (idx.centroids ** 2).sum(1)
     _, probes = ops.knn(idx.centroids, cn, q, 8, False, 0)
-    D2, I2 = idx._search_reference(q.cpu(), probes.cpu(), 10) if False else _ref(idx, q, probes, 10)
+    D2, I2 = _ref(idx, q, probes, k)
     torch.testing.assert_close(D.cpu(), D2, rtol=1e-3, atol=1e-3)
     assert (I.cpu() == I2).float().mean() > 0.97
     assert (I[:, 0].cpu() == torch.arange(40)).float().mean() > 0.9
@@ -43,3 +43,23 @@ def _ref(idx, q, probes, k):
         setattr(cpu, name, getattr(idx, name).cpu())
     cpu.ntotal = idx.ntotal
     return cpu._search_reference(q.cpu(), probes.cpu(), k)
+
+
+def test_ivfpq_wide_probe_matches_knn_probe_order():
+    """nprobe > 64 (recall sweeps) takes the GEMM + topk coarse step: same result set as
+    the kernel path would give with every list probed."""
+    from docqa_amd import ops
+    from docqa_amd.index.ivfpq import IVFPQIndex
+
+    assert ops.load_native()
+    g = torch.Generator().manual_seed(1)
+    x = torch.randn(30000, 64, generator=g)
+    idx = IVFPQIndex(64, 128, 16, device="cuda")
+    idx.train(x, niter=4)
+    idx.add(x)
+    q = x[:16].cuda()
+    D, I = idx.search(q, 10, nprobe=128)
+    cn = (idx.centroids ** 2).sum(1)
+    probes = torch.topk(cn[None] - 2 * q @ idx.centroids.t(), 128, dim=1, largest=False).indices
+    D2, I2 = _ref(idx, q, probes, 10)
+    torch.testing.assert_close(D.cpu(), D2, rtol=1e-3, atol=1e-3)

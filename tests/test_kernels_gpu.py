@@ -442,7 +442,8 @@ def test_flash_prefill_spike(native):
 
 
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
-@pytest.mark.parametrize("N,d,nq,k", [(649, 384, 1, 3), (5000, 384, 40, 10), (100000, 768, 7, 32), (10, 128, 3, 16)])
+@pytest.mark.parametrize("N,d,nq,k", [(649, 384, 1, 3), (5000, 384, 40, 10), (100000, 768, 7, 32), (10, 128, 3, 16),
+                                      (20000, 768, 33, 64), (1024, 768, 256, 40)])
 @pytest.mark.parametrize("ip", [False, True])
 def test_knn(native, dtype, N, d, nq, k, ip):
     from docqa_amd.ops import reference as R
