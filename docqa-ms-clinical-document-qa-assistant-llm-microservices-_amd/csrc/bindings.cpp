@@ -427,7 +427,8 @@ at::Tensor paged_decode_cascade_split(const at::Tensor& q, at::Tensor k_cache, a
   TORCH_CHECK(D == 128 && BS == 64 && Hq == 4 * Hkv, "split decode: head_dim 128, 64-token blocks, GQA 4");
   TORCH_CHECK(block_tables.size(1) <= 64, "split decode: <= 64 blocks per sequence");
   TORCH_CHECK(context_lens.numel() == B && block_tables.size(0) >= B, "split decode: B rows");
-  TORCH_CHECK(plan.dim() == 3 && plan.size(0) == 2 && plan.size(2) == 8 && plan.size(1) >= 1, "plan: [2, cap, 8]");
+  TORCH_CHECK(plan.dim() == 3 && (plan.size(0) == 2 || plan.size(0) == 3) && plan.size(2) == 8 &&
+              plan.size(1) >= 1, "plan: [2, cap, 8] (split) or [3, cap, 8] (persistent bins)");
   TORCH_CHECK(prefix_table.numel() >= 1 && prefix_len.numel() == 1, "cascade decode: prefix table / length");
   const int cap = plan.size(1);
   c10::DeviceGuard g(q.device());
@@ -438,6 +439,17 @@ at::Tensor paged_decode_cascade_split(const at::Tensor& q, at::Tensor k_cache, a
   auto ws_acc = at::empty({cap, Hkv, 16, D}, f32);
   auto ws_ml = at::empty({cap, Hkv, 16, 2}, f32);
   const int* pp = plan.data_ptr<int>();
+  if (plan.size(0) == 3) {
+    CHECK_RC(docqa_paged_decode_cascade_persist(q.data_ptr(), q.stride(0), k_cache.data_ptr(), v_cache.data_ptr(),
+                                                block_tables.data_ptr<int>(), block_tables.size(1),
+                                                context_lens.data_ptr<int>(), out.data_ptr(), Hq * D, B, Hq, Hkv,
+                                                BS, (float)scale, prefix_table.data_ptr<int>(),
+                                                prefix_len.data_ptr<int>(), (int)nchunk, pacc.data_ptr<float>(),
+                                                pml.data_ptr<float>(), pp, pp + 8 * cap, pp + 16 * cap, cap,
+                                                ws_acc.data_ptr<float>(), ws_ml.data_ptr<float>(), stream()),
+             "paged_decode_cascade_persist");
+    return out;
+  }
   CHECK_RC(docqa_paged_decode_cascade_split(q.data_ptr(), q.stride(0), k_cache.data_ptr(), v_cache.data_ptr(),
                                             block_tables.data_ptr<int>(), block_tables.size(1),
                                             context_lens.data_ptr<int>(), out.data_ptr(), Hq * D, B, Hq, Hkv,
@@ -744,6 +756,8 @@ at::Tensor pgemm_partial(const at::Tensor& x, const at::Tensor& w, int64_t split
   return out;
 }
 
+int64_t group_persist_bins(int64_t cap, int64_t Hkv) { return docqa_group_persist_bins((int)cap, (int)Hkv); }
+
 bool pgemm_ok(int64_t M, int64_t N, int64_t K) { return docqa_pgemm_ok((int)M, (int)N, (int)K); }
 
 std::tuple<at::Tensor, at::Tensor> knn(const at::Tensor& xb, const at::Tensor& xb_norms,
@@ -940,6 +954,7 @@ TORCH_LIBRARY(docqa, m) {
   m.def("pgemm_partial(Tensor x, Tensor w, int splits) -> Tensor");
   m.def("mgemm_argmax_val(Tensor x, Tensor w, int n_valid, int cfg=0) -> (Tensor, Tensor)");
   m.def("pgemm_ok(int M, int N, int K) -> bool", &pgemm_ok);
+  m.def("group_persist_bins(int cap, int Hkv) -> int", &group_persist_bins);
   m.def("paged_decode_cascade(Tensor q, Tensor k_cache, Tensor v_cache, Tensor block_tables, "
         "Tensor context_lens, int Hq, int max_context, float scale, Tensor prefix_table, Tensor prefix_len, "
         "int nchunk, Tensor? order=None) -> Tensor");

@@ -1167,6 +1167,306 @@ __global__ __launch_bounds__(256) void group_split_merge_kernel(const int* __res
   *reinterpret_cast<uint4*>(op) = pack8(num);
 }
 
+// ---------------------------------------------------------------------------------------
+// Persistent grouped decode (plan [3, cap, 8]): the split plan's work items are packed by
+// the host into bins of <= kBinItems (LPT by tile count, ops.split_decode_groups(bins=));
+// one workgroup per (KV head, bin) streams the tiles of ALL its items through ONE LDS-DMA
+// ring.  The split kernel above pays, per ~10-tile item, a block-table round trip (tile
+// list), the Q loads and the first DMA's latency before any math, and a ring drain at the
+// end (profiles/r2_pmc/group_split_decode.txt: 7.4 tiles per workgroup, waves parked 62 %
+// of their cycles).  Here the tile lists of every item of the bin are built up front by the
+// four waves together (one latency per workgroup), the ring runs across item boundaries,
+// and the next item's Q fragments load under the current item's tiles.  Every item writes
+// an un-normalised (m, l, O) partial to its slot; group_split_merge_kernel folds each
+// group's items and the cascade prefix chunks, and normalises.
+constexpr int kBinItems = 8;
+constexpr int kBinMaxTiles = 512;
+
+// workgroups per KV head of the persistent launch: ~3 per CU chip-wide, at least one per
+// identity quad (shared with ops.persist_bins)
+__host__ __device__ inline int group_persist_bins(int cap, int Hkv) {
+  const int a = 768 / (Hkv > 0 ? Hkv : 1), b = (cap + 3) / 4;
+  const int nb = a > b ? a : b;
+  return nb < cap ? nb : cap;
+}
+
+template <int NSR = 3>
+__global__ __launch_bounds__(256) void paged_decode_group_persist_kernel(
+    const uint16_t* __restrict__ q, int q_stride, const uint16_t* __restrict__ k_cache,
+    const uint16_t* __restrict__ v_cache, const int* __restrict__ block_tables, int maxb,
+    const int* __restrict__ context_lens, int B, int Hkv, float scale, const int* __restrict__ items,
+    const int* __restrict__ bins, CascadeIn ci, float* __restrict__ ws_acc, float* __restrict__ ws_ml) {
+  constexpr int G = 4, R = 4, D = 128, TT = 32;
+  constexpr int TILE = TT * D;
+  __shared__ __attribute__((aligned(16))) uint16_t ring[NSR * 2 * TILE];
+  __shared__ int2 s_tl[kBinMaxTiles];           // (block id, item << 16 | pos << 8 | half << 4 | mask)
+  __shared__ int s_it[kBinItems][8];            // rows[4], lo, hi, slot, - (all -1: no item)
+  __shared__ int s_L[kBinItems][4];             // context lengths of the item rows
+  __shared__ int s_cnt[kBinItems];
+
+  const int kvh = blockIdx.x, bin = blockIdx.y;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int hl = lane & 15, lg = lane >> 4;
+  const int P = ci.plen ? *ci.plen : 0;          // multiple of 64
+
+  if (tid < kBinItems * 8) {                     // the bin's items -> LDS
+    const int j = tid >> 3, f = tid & 7;
+    const int it = bins[bin * 8 + j];
+    int v = it >= 0 ? items[it * 8 + f] : -1;
+    if (f < 4) {
+      v = (v >= 0 && v < B) ? v : -1;
+      s_L[j][f] = v >= 0 ? context_lens[v] : 0;
+    }
+    s_it[j][f] = v;
+  }
+  __syncthreads();
+  int nit = 0;
+#pragma unroll
+  for (int j = 0; j < kBinItems; ++j) nit += s_it[j][6] >= 0 ? 1 : 0;
+  if (nit == 0) return;                          // unused bin (uniform)
+
+  // ---- tile lists of items wave and wave + 4: lane = one block position of the item
+  int2 ent[2][2 * R];
+  int cnt[2], off[2];
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {
+    const int j = wave + 4 * u;
+    cnt[u] = 0;
+    off[u] = 0;
+    if (j < nit) {
+      const int lo = s_it[j][4], hi = min(s_it[j][5], maxb);
+      const int pos = max(P >> 6, lo) + lane;
+      int ids[R];
+      bool alive[R];
+#pragma unroll
+      for (int r = 0; r < R; ++r) {
+        const int row = s_it[j][r];
+        alive[r] = row >= 0 && pos < hi && 64 * pos < s_L[j][r];
+        ids[r] = alive[r] ? block_tables[(size_t)row * maxb + pos] : -1;
+      }
+#pragma unroll
+      for (int r = 0; r < R; ++r) {
+        bool first = alive[r];
+#pragma unroll
+        for (int r2 = 0; r2 < r; ++r2) first = first && !(alive[r2] && ids[r2] == ids[r]);
+        if (first) {
+          int mask = 0, two = 0;
+#pragma unroll
+          for (int r2 = 0; r2 < R; ++r2)
+            if (alive[r2] && ids[r2] == ids[r]) { mask |= 1 << r2; two |= s_L[j][r2] > 64 * pos + 32; }
+#pragma unroll
+          for (int h = 0; h < 2; ++h)
+            if (h == 0 || two) {
+              const int y = (j << 16) | (pos << 8) | (h << 4) | mask;
+#pragma unroll
+              for (int e = 0; e < 2 * R; ++e)
+                if (e == cnt[u]) ent[u][e] = make_int2(ids[r], y);
+              cnt[u]++;
+            }
+        }
+      }
+      int o = cnt[u];                            // exclusive prefix sum over the lanes
+#pragma unroll
+      for (int d = 1; d < 64; d <<= 1) {
+        const int v = __shfl_up(o, d, 64);
+        if (lane >= d) o += v;
+      }
+      if (lane == 63) s_cnt[j] = o;
+      off[u] = o - cnt[u];
+    }
+  }
+  __syncthreads();
+  int base[kBinItems], NT = 0;
+#pragma unroll
+  for (int j = 0; j < kBinItems; ++j) {
+    base[j] = NT;
+    NT += j < nit ? s_cnt[j] : 0;
+  }
+  NT = min(NT, kBinMaxTiles);                    // the host plans <= kBinMaxTiles per bin
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {
+    const int j = wave + 4 * u;
+    if (j < nit) {
+      int b0 = 0;
+#pragma unroll
+      for (int jj = 0; jj < kBinItems; ++jj)
+        if (jj == j) b0 = base[jj];
+#pragma unroll
+      for (int e = 0; e < 2 * R; ++e)
+        if (e < cnt[u] && b0 + off[u] + e < kBinMaxTiles) s_tl[b0 + off[u] + e] = ent[u][e];
+    }
+  }
+  // items without any live tile: an empty partial (the merge reads every slot)
+  for (int j = wave; j < nit; j += 4) {
+    if (s_cnt[j] == 0) {
+      const size_t cidx = ((size_t)s_it[j][6] * Hkv + kvh) * 16 + hl;
+#pragma unroll
+      for (int dd = 0; dd < 2; ++dd)
+        *reinterpret_cast<f32x4*>(ws_acc + cidx * D + 16 * (2 * wave + dd) + 4 * lg) = f32x4{0.f, 0.f, 0.f, 0.f};
+      if (lg == 0) *reinterpret_cast<float2*>(ws_ml + cidx * 2) = make_float2(-FLT_MAX, 0.f);
+    }
+  }
+  // first item with tiles and the one after it: Q fragments of the current / next item,
+  // loaded before the barrier below (which drains them: nothing the compiler tracks is in
+  // flight when the ring loop starts)
+  auto next_live = [&](int j) {
+    int n = kBinItems;
+#pragma unroll
+    for (int jj = kBinItems - 1; jj >= 0; --jj)
+      if (jj > j && jj < nit && s_cnt[jj] > 0) n = jj;
+    return n;
+  };
+  auto qptr = [&](int j) {
+    const int row = j < nit ? s_it[j][hl >> 2] : -1;
+    return q + (size_t)max(row, 0) * q_stride + (size_t)(kvh * G + (hl & 3)) * D + lg * 8;
+  };
+  auto qrow = [&](int j) { return j < nit ? s_it[j][hl >> 2] : -1; };
+  int cur = next_live(-1);
+  int nxt = next_live(cur);
+  bf16x8 qf[4], qn[4];
+  {
+    const uint16_t* p0 = qptr(cur);
+    const uint16_t* p1 = qptr(nxt);
+    const bool v0 = qrow(cur) >= 0, v1 = qrow(nxt) >= 0;
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) {
+      const uint4 a = v0 ? *reinterpret_cast<const uint4*>(p0 + ks * 32) : make_uint4(0, 0, 0, 0);
+      const uint4 b = v1 ? *reinterpret_cast<const uint4*>(p1 + ks * 32) : make_uint4(0, 0, 0, 0);
+      qf[ks] = __builtin_bit_cast(bf16x8, a);
+      qn[ks] = __builtin_bit_cast(bf16x8, b);
+    }
+  }
+  __syncthreads();
+  if (NT == 0) return;                           // (uniform) nothing live in this bin
+  int cL = s_L[cur][hl >> 2];
+  const int cbit = 1 << (hl >> 2);
+  // the item after next: its Q goes straight into qn by inline-asm loads (invisible to the
+  // compiler's waitcnt pass, which would otherwise drain the ring before the copy); they are
+  // issued before a step's DMAs, so the next step's counted vmcnt wait covers them
+  auto prefetch_q = [&](int j) {
+    const uint16_t* p = qptr(j);
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks)
+      asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(qn[ks]) : "v"(p + ks * 32) : "memory");
+  };
+
+  const float qs = scale * kLog2e;
+  const uint32_t ring_base = lds_u32(ring);
+  const int prow = lane >> 4, pslot = lane & 15;  // DMA piece geometry: 4 rows x 16 slots
+  auto stage = [&](int j) {
+    const int2 e = s_tl[min(j, NT - 1)];
+    const int tok0 = ((e.y >> 4) & 1) * TT;
+    const size_t row0 = ((size_t)e.x * Hkv + kvh) * 64 + tok0;
+    const uint16_t* kp = k_cache + row0 * D;
+    const uint16_t* vp = v_cache + row0 * D;
+    const uint32_t dst = ring_base + (uint32_t)((j % NSR) * 2 * TILE * 2);
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int c = i * 4 + wave;                // 1 KB piece = tile rows 4c .. 4c+3
+      const int t = 4 * c + prow;
+      glds16<true>(kp + t * D + ((pslot ^ (t & 15)) << 3), dst + c * 1024);
+      glds16<true>(vp + t * D + ((pslot ^ vswz(t)) << 3), dst + TILE * 2 + c * 1024);
+    }
+  };
+  float m = -FLT_MAX, l = 0.f;
+  f32x4 acc[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
+  auto flush = [&](int j) {                      // partial of item j for this lane's column
+    const size_t cidx = ((size_t)s_it[j][6] * Hkv + kvh) * 16 + hl;
+#pragma unroll
+    for (int dd = 0; dd < 2; ++dd)
+      *reinterpret_cast<f32x4*>(ws_acc + cidx * D + 16 * (2 * wave + dd) + 4 * lg) = acc[dd];
+    if (wave == 0 && lg == 0) *reinterpret_cast<float2*>(ws_ml + cidx * 2) = make_float2(m, l);
+  };
+  stage(0);
+  stage(1);
+  if constexpr (NSR == 4) stage(2);
+  for (int jt = 0; jt < NT; ++jt) {
+    wait_vmcnt<4 * (NSR - 2)>();                 // the next NSR-2 tiles (4 DMAs each) may fly
+    ring_barrier();                              // tile jt visible; slot (jt-1) % NSR free
+    const int2 e = s_tl[jt];
+    const int it = __builtin_amdgcn_readfirstlane((e.y >> 16) & 7);
+    if (it != cur) {                             // item boundary (uniform): flush, switch
+      flush(cur);
+      cur = it;
+      const bool live = qrow(cur) >= 0;
+#pragma unroll
+      for (int ks = 0; ks < 4; ++ks) {
+        asm volatile("" : "+v"(qn[ks]));         // landed: the vmcnt wait above covered it
+        qf[ks] = live ? qn[ks] : bf16x8{};
+      }
+      nxt = next_live(cur);
+      prefetch_q(nxt);                           // issued before this step's DMAs
+      cL = s_L[cur][hl >> 2];
+      m = -FLT_MAX;
+      l = 0.f;
+      acc[0] = f32x4{0.f, 0.f, 0.f, 0.f};
+      acc[1] = f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+    stage(jt + NSR - 1);
+    const bool mine = (e.y & cbit) != 0;         // this column's row reads this block
+    const int tbase = ((e.y >> 8) & 0xff) * 64 + ((e.y >> 4) & 1) * TT;   // position of token 0
+    const uint16_t* kt = ring + (jt % NSR) * 2 * TILE;
+    const uint16_t* vt = kt + TILE;
+    f32x4 x[2];
+#pragma unroll
+    for (int c = 0; c < 2; ++c) {
+      x[c] = f32x4{0.f, 0.f, 0.f, 0.f};
+      const int t = 16 * c + hl;
+#pragma unroll
+      for (int ks = 0; ks < 4; ++ks) {
+        const bf16x8 a = *reinterpret_cast<const bf16x8*>(kt + t * D + (((4 * ks + lg) ^ (t & 15)) << 3));
+        x[c] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, qf[ks], x[c], 0, 0, 0);
+      }
+    }
+    float mx = -FLT_MAX;
+#pragma unroll
+    for (int c = 0; c < 2; ++c)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int tok = tbase + 16 * c + 4 * lg + r;
+        const float v = (mine && tok < cL) ? x[c][r] * qs : -FLT_MAX;
+        x[c][r] = v;
+        mx = fmaxf(mx, v);
+      }
+    mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
+    mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+    const float m_new = fmaxf(m, mx);
+    const float alpha = m_new == -FLT_MAX ? 1.f : exp2f(m - m_new);
+    float ps = 0.f;
+#pragma unroll
+    for (int c = 0; c < 2; ++c)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float p = x[c][r] == -FLT_MAX ? 0.f : exp2f(x[c][r] - m_new);
+        x[c][r] = p;
+        ps += p;
+      }
+    ps += __shfl_xor(ps, 16, 64);
+    ps += __shfl_xor(ps, 32, 64);
+    l = l * alpha + ps;
+    m = m_new;
+#pragma unroll
+    for (int dd = 0; dd < 2; ++dd) acc[dd] *= alpha;
+#pragma unroll
+    for (int c = 0; c < 2; ++c) {
+      i16x4 pb;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) pb[r] = (short)f2bf(x[c][r]);
+      const int row = 16 * c + 4 * lg + (hl >> 2), pp = hl & 3;
+#pragma unroll
+      for (int dd = 0; dd < 2; ++dd) {
+        const int ch = 2 * (2 * wave + dd) + (pp >> 1);
+        const uint16_t* va = vt + row * D + ((ch ^ vswz(row)) << 3) + 4 * (pp & 1);
+        const i16x4 a = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_i16x4*)va);
+        acc[dd] = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(a, pb, acc[dd], 0, 0, 0);
+      }
+    }
+  }
+  flush(cur);
+  wait_vmcnt<0>();                               // drain the clamped tail DMAs
+}
+
 // forward declaration (defined below with the other cascade launchers)
 int docqa_cascade_prefix(const void* qkv, int row_stride, int rows, int Hq, int Hkv, float scale,
                          const void* k_cache, const void* v_cache, const int* prefix_table,
@@ -1250,6 +1550,35 @@ int docqa_paged_decode_cascade_split(const void* q, int q_stride, void* k_cache,
   DOCQA_CHECK_LAUNCH();
   return 0;
 }
+
+// Persistent grouped cascade decode: plan [3, cap, 8] = items (4 rows, first position, end
+// position, slot, 0), merges (4 rows, first slot, slots, 0, 0) covering EVERY group, bins
+// (<= 8 item indices, -1 = none) -- group_persist_bins(cap, Hkv) of them.
+int docqa_paged_decode_cascade_persist(const void* q, int q_stride, void* k_cache, void* v_cache,
+                                       const int* block_tables, int maxb, const int* context_lens,
+                                       void* out, int out_stride, int B, int Hq, int Hkv, int BS,
+                                       float scale, const int* prefix_table, const int* plen, int nchunk,
+                                       float* pacc, float* pml, const int* items, const int* merges,
+                                       const int* bins, int cap, float* ws_acc, float* ws_ml, hipStream_t s) {
+  if (B == 0) return 0;
+  if (BS != 64 || maxb > kGroupMaxPos || Hq != 4 * Hkv || nchunk < 1 || nchunk > kCascadeMaxChunks || cap < 1)
+    return -1;
+  const int rc = docqa_cascade_prefix(q, q_stride, B, Hq, Hkv, scale, k_cache, v_cache, prefix_table, plen, BS,
+                                      nchunk, pacc, pml, nullptr, nullptr, s);
+  if (rc) return rc;
+  const CascadeIn ci{pacc, pml, plen, nchunk, nullptr};
+  const int nb = group_persist_bins(cap, Hkv);
+  paged_decode_group_persist_kernel<3><<<dim3(Hkv, nb), 256, 0, s>>>(
+      (const uint16_t*)q, q_stride, (const uint16_t*)k_cache, (const uint16_t*)v_cache, block_tables, maxb,
+      context_lens, B, Hkv, scale, items, bins, ci, ws_acc, ws_ml);
+  DOCQA_CHECK_LAUNCH();
+  group_split_merge_kernel<<<dim3(Hkv, cap), 256, 0, s>>>(merges, ws_acc, ws_ml, context_lens, B, Hkv,
+                                                          (uint16_t*)out, out_stride, ci);
+  DOCQA_CHECK_LAUNCH();
+  return 0;
+}
+
+int docqa_group_persist_bins(int cap, int Hkv) { return group_persist_bins(cap, Hkv); }
 
 // log-sum-exp merge of a sequence's context partitions (and, cascade, of the shared-prefix
 // chunk partials) -> normalised bf16 output

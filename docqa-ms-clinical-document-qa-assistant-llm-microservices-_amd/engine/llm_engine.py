@@ -132,17 +132,37 @@ def _split_groups_on() -> bool:
     return os.environ.get("DOCQA_GROUP_SPLIT", "1") == "1"
 
 
-def _identity_groups(bp: int, dev) -> torch.Tensor:
+def _persist_groups_on() -> bool:
+    """Persistent grouped decode (bins of work items per workgroup) on top of the split
+    plan; DOCQA_GROUP_PERSIST=0: one workgroup per item."""
+    return _split_groups_on() and os.environ.get("DOCQA_GROUP_PERSIST", "1") == "1"
+
+
+def _identity_groups(bp: int, dev, hkv: int = 8) -> torch.Tensor:
     cap = (bp + 1) // 2
     if _split_groups_on():
-        # split plan [2, bp, 8]: consecutive unsplit quads until set_groups runs
-        g = torch.full((2, max(bp, 1), 8), -1, dtype=torch.int32)
-        g[:, :, 4:] = 0
-        for i in range(cap):
+        # split plan [2, bp, 8] (persistent: [3, bp, 8]): consecutive unsplit quads until
+        # set_groups runs
+        persist = _persist_groups_on()
+        g = torch.full((3 if persist else 2, max(bp, 1), 8), -1, dtype=torch.int32)
+        g[:2, :, 4:] = 0
+        g[0, :, 6] = -1
+        nq = (bp + 3) // 4
+        for i in range(nq):
             q = list(range(4 * i, min(4 * i + 4, bp)))
             g[0, i, :len(q)] = torch.tensor(q, dtype=torch.int32)
             g[0, i, 5] = 1 << 20
-            g[0, i, 6] = -1
+            if persist:
+                g[0, i, 4] = 0
+                g[0, i, 6] = i
+                g[1, i, :len(q)] = torch.tensor(q, dtype=torch.int32)
+                g[1, i, 4], g[1, i, 5] = i, 1
+            else:
+                g[0, i, 6] = -1
+        if persist:   # one quad per bin (persist_bins >= bp / 4)
+            nb = ops.persist_bins(max(bp, 1), hkv)
+            for i in range(nq):
+                g[2, i % nb, i // nb] = i
         return g.to(dev)
     g = torch.full((cap * 4,), -1, dtype=torch.int32)
     g[:bp] = torch.arange(bp, dtype=torch.int32)   # consecutive quads until set_groups runs
@@ -173,11 +193,12 @@ class _DecodeGraph:
         self.order_key = None
         # grouped cascade decode: rows packed into groups of <= 4 by shared prefix-cache
         # blocks (room for bp / 2 groups; unused groups are all -1 and exit at once)
-        self.groups = _identity_groups(bp, dev)
+        self.groups = _identity_groups(bp, dev, eng.model.hkv)
         self.groups_key = None
         self.cascade = False
         self.greedy = True
         self.graph = None
+        self.hkv = eng.model.hkv
 
     @classmethod
     def view_of(cls, master: "_DecodeGraph", bp: int) -> "_DecodeGraph":
@@ -192,9 +213,10 @@ class _DecodeGraph:
         g.shared_table, g.shared_len = master.shared_table, master.shared_len
         g.order = torch.arange(bp, dtype=torch.int32, device=master.tokens.device)
         g.order_key = None
-        g.groups = _identity_groups(bp, master.tokens.device)
+        g.groups = _identity_groups(bp, master.tokens.device, master.hkv)
         g.groups_key = None
         g.cascade, g.greedy, g.graph = False, True, None
+        g.hkv = master.hkv
         return g
 
 
@@ -405,7 +427,8 @@ class LLMEngine:
             if os.environ.get("DOCQA_GROUP_INLINE_PREFIX", "0") == "1":
                 skip = 0   # the kernel attends the shared prefix inside each group
             plan = ops.split_decode_groups(quads, tables, lens, skip, self.block_size, cap,
-                                           int(os.environ.get("DOCQA_GROUP_TILES", "12")))
+                                           int(os.environ.get("DOCQA_GROUP_TILES", "12")),
+                                           bins=ops.persist_bins(cap, self.model.hkv) if g.groups.shape[0] == 3 else 0)
             _upload(g.groups, plan)
             g.groups_key = key
             return

@@ -624,8 +624,18 @@ def group_tiles_by_position(tables: list[list[int]], lens: list[int], rows: list
     return out
 
 
+def persist_bins(cap: int, Hkv: int) -> int:
+    """Workgroups per KV head of the persistent grouped decode (attn_decode.hip
+    group_persist_bins): ~3 per CU chip-wide, at least one per quad of ``cap`` rows."""
+    nb = max(768 // max(1, Hkv), (cap + 3) // 4)
+    return min(nb, cap)
+
+
+BIN_ITEMS, BIN_MAX_TILES = 8, 512    # attn_decode.hip kBinItems / kBinMaxTiles
+
+
 def split_decode_groups(quads: list[list[int]], tables: list[list[int]], lens: list[int], skip: int,
-                        block_size: int, cap: int, tiles_per_item: int = 12) -> torch.Tensor:
+                        block_size: int, cap: int, tiles_per_item: int = 12, bins: int = 0) -> torch.Tensor:
     """Split plan for the grouped cascade decode (``paged_decode_cascade_grouped`` with a
     [2, cap, 8] int32 ``groups``): every group of :func:`pack_decode_groups` is cut at block
     positions into work items of about ``tiles_per_item`` K/V tiles (``lens``: the lengths
@@ -634,8 +644,13 @@ def split_decode_groups(quads: list[list[int]], tables: list[list[int]], lens: l
     a longer group write partials that a merge kernel combines.  Items are ordered largest
     first (LPT).  plan[0]: items (4 rows, first position, end position, slot or -1, 0);
     plan[1]: merges (4 rows, first slot, slots, 0, 0) -- at most (cap + 1) // 2 of them
-    (the merge kernel's grid)."""
-    items, merges, nslot = [], [], 0
+    (the merge kernel's grid).
+
+    ``bins`` > 0: the PERSISTENT plan [3, cap, 8] instead -- every item writes a partial
+    (slot = its index), every group has a merge row, and plan[2] packs the items into
+    ``bins`` (:func:`persist_bins`) workgroups of <= 8 items and <= 512 tiles each, greedy
+    longest-first onto the least-loaded bin, so each workgroup streams ~total / bins tiles
+    through one ring."""
     budget = max(1, tiles_per_item)
     while True:
         items, merges, nslot = [], [], 0
@@ -650,25 +665,57 @@ def split_decode_groups(quads: list[list[int]], tables: list[list[int]], lens: l
                 acc += t
             end = max((lens[r] + block_size - 1) // block_size for r in qd)
             cuts.append((start, max(end, start + 1), acc))
-            if len(cuts) == 1:
+            if bins:
+                merges.append(rows4 + [nslot, len(cuts), 0, 0])
+                for lo, hi, t in cuts:
+                    items.append((t, rows4 + [lo, hi, nslot, 0]))
+                    nslot += 1
+            elif len(cuts) == 1:
                 items.append((cuts[0][2], rows4 + [skip, 1 << 20, -1, 0]))
             else:
                 merges.append(rows4 + [nslot, len(cuts), 0, 0])
                 for lo, hi, t in cuts:
                     items.append((t, rows4 + [lo, hi, nslot, 0]))
                     nslot += 1
-        if len(items) <= cap and len(merges) <= (cap + 1) // 2:
+        fits = len(items) <= cap and len(merges) <= (cap if bins else (cap + 1) // 2)
+        if fits and bins:
+            nb = min(bins, cap)
+            fits = len(items) <= nb * BIN_ITEMS and all(t <= BIN_MAX_TILES for t, _ in items)
+        if fits:
             break
         if budget > 1 << 20:
             raise ValueError(f"split_decode_groups: {len(quads)} groups exceed the plan capacity {cap}")
         budget *= 2
-    items.sort(key=lambda it: -it[0])
-    plan = torch.full((2, cap, 8), -1, dtype=torch.int32)
-    plan[:, :, 4:] = 0
+    if not bins:
+        items.sort(key=lambda it: -it[0])
+        plan = torch.full((2, cap, 8), -1, dtype=torch.int32)
+        plan[:, :, 4:] = 0
+        if items:
+            plan[0, :len(items)] = torch.tensor([it[1] for it in items], dtype=torch.int32)
+        if merges:
+            plan[1, :len(merges)] = torch.tensor(merges, dtype=torch.int32)
+        return plan
+    nb = min(bins, cap)
+    load, members = [0] * nb, [[] for _ in range(nb)]
+    for i in sorted(range(len(items)), key=lambda i: -items[i][0]):
+        t = items[i][0]
+        best = min((b for b in range(nb) if len(members[b]) < BIN_ITEMS and load[b] + t <= BIN_MAX_TILES),
+                   key=lambda b: load[b], default=None)
+        if best is None:    # every bin full: the plan cannot hold this batch
+            raise ValueError("split_decode_groups: items exceed the persistent bins")
+        members[best].append(i)
+        load[best] += t
+    plan = torch.full((3, cap, 8), -1, dtype=torch.int32)
+    plan[:2, :, 4:] = 0
+    plan[0, len(items):, 6] = -1           # unused item rows: no slot
     if items:
         plan[0, :len(items)] = torch.tensor([it[1] for it in items], dtype=torch.int32)
     if merges:
         plan[1, :len(merges)] = torch.tensor(merges, dtype=torch.int32)
+    for b, mem in enumerate(members):
+        # a bin streams its items in index order: keep them position-ordered per group
+        for j, i in enumerate(sorted(mem)):
+            plan[2, b, j] = i
     return plan
 
 

@@ -322,3 +322,53 @@ def test_split_decode_groups_plan(tiles):
         assert merges
     if tiles == 100:
         assert not merges
+
+
+@pytest.mark.parametrize("tiles,bins", [(1, 3), (2, 4), (5, 2), (100, 8)])
+def test_persistent_decode_plan(tiles, bins):
+    """Persistent plan [3, cap, 8]: every item owns slot = its index, every group has one
+    merge row over its consecutive slots, items tile each group's positions exactly once,
+    and the bins hold every item once with <= 8 items / <= 512 tiles, LPT-balanced."""
+    from docqa_amd import ops
+
+    skip = 2
+    tables = [[0, 1, 10, 11, 50, 70], [0, 1, 10, 11, 51, 71], [0, 1, 20, 52, 53, 72], [0, 1, 10, 12, 54, 73],
+              [0, 1, 30, 55, 56, 74], [0, 1, 20, 57, 58, 75], [0, 1, 60, 61, 62, 76]]
+    lens = [330, 300, 370, 250, 384, 200, 310]
+    quads = ops.pack_decode_groups(tables, lens, skip, 64, cap=4)
+    plan = ops.split_decode_groups(quads, tables, lens, skip, 64, cap=16, tiles_per_item=tiles, bins=bins)
+    assert plan.shape == (3, 16, 8)
+    items = [r.tolist() for r in plan[0] if r[6] >= 0]
+    assert [it[6] for it in items] == list(range(len(items)))
+    merges = [r.tolist() for r in plan[1] if r[5] > 0]
+    assert len(merges) == len(quads)
+    for qd in quads:
+        key = sorted(qd)
+        mg = [m for m in merges if sorted(r for r in m[:4] if r >= 0) == key]
+        assert len(mg) == 1
+        mine = items[mg[0][4]:mg[0][4] + mg[0][5]]
+        assert all(sorted(r for r in it[:4] if r >= 0) == key for it in mine)
+        nb = max((lens[r] + 63) // 64 for r in qd)
+        cover = []
+        for it in mine:
+            cover += list(range(max(it[4], skip), min(it[5], nb)))
+        assert cover == list(range(skip, nb))
+    binned = [int(i) for i in plan[2].flatten() if i >= 0]
+    assert sorted(binned) == list(range(len(items)))
+    assert all(int((plan[2, b] >= 0).sum()) <= ops.BIN_ITEMS for b in range(16))
+    assert int((plan[2, :, 0] >= 0).sum()) == min(bins, len(items))
+    assert ops.persist_bins(256, 8) == 96 and ops.persist_bins(512, 8) == 128 and ops.persist_bins(4, 2) == 4
+
+
+def test_persistent_identity_plan_cpu():
+    from docqa_amd import ops
+    from docqa_amd.engine.llm_engine import _identity_groups
+
+    g = _identity_groups(256, "cpu", 8)
+    assert g.shape == (3, 256, 8)
+    items = g[0][g[0, :, 6] >= 0]
+    assert items.shape[0] == 64 and items[:, :4].flatten().tolist() == list(range(256))
+    assert (g[1, :64, 5] == 1).all() and (g[1, :64, 4] == torch.arange(64)).all()
+    assert sorted(int(i) for i in g[2].flatten() if i >= 0) == list(range(64))
+    assert int((g[2, :, 1] >= 0).sum()) == 0          # one quad per bin
+    assert ops.persist_bins(256, 8) >= 64

@@ -147,3 +147,62 @@ def test_split_grouped_cascade_padded_rows_zero(native):
     assert torch.isfinite(out.float()).all()
     assert (out[2] == 0).all() and (out[5] == 0).all()
     assert (out[0].float().abs().sum() > 0) and (out[4].float().abs().sum() > 0)
+
+
+@pytest.mark.parametrize("B,Hkv,seed", [(37, 8, 0), (256, 8, 3), (9, 2, 5), (512, 8, 4)])
+@pytest.mark.parametrize("tiles", [1, 3, 12, 1000])
+def test_persistent_grouped_cascade_matches_per_row(native, B, Hkv, seed, tiles):
+    """Persistent plan (work items packed into bins, one ring per workgroup across item
+    boundaries, every group merged) == per-row cascade and the fp32 reference; END-of-decode
+    planning lengths, so some items have no live keys yet."""
+    Hq, D, BS, Pb, maxb = 4 * Hkv, 128, 64, 3, 12
+    tables, lens, nblk = _trie_batch(B, Pb, maxb, seed)
+    kc = torch.randn(nblk, Hkv, BS, D, device="cuda", dtype=torch.bfloat16)
+    vc = torch.randn_like(kc)
+    bt = torch.tensor(tables, dtype=torch.int32, device="cuda")
+    cl = torch.tensor(lens, dtype=torch.int32, device="cuda")
+    q = torch.randn(B, (Hq + 2 * Hkv) * D, device="cuda", dtype=torch.bfloat16)
+    pt = torch.zeros(maxb, dtype=torch.int32, device="cuda")
+    pt[:Pb] = bt[0, :Pb]
+    plen = torch.tensor([Pb * BS], dtype=torch.int32, device="cuda")
+    scale = 1 / math.sqrt(D)
+    ref = native.paged_decode_cascade(q, kc, vc, bt, cl, Hq, maxb * BS, scale, pt, plen, 4)
+    with native.use_reference():
+        ref32 = native.paged_decode_cascade(q, kc, vc, bt, cl, Hq, maxb * BS, scale, pt, plen, 4)
+    end_lens = [min(L + 128, maxb * BS) for L in lens]
+    cap = max(B, 4)
+    quads = native.pack_decode_groups(tables, end_lens, Pb, BS, (B + 1) // 2)
+    nb = native.persist_bins(cap, Hkv)
+    assert nb == torch.ops.docqa.group_persist_bins(cap, Hkv)
+    plan = native.split_decode_groups(quads, tables, end_lens, Pb, BS, cap, tiles, bins=nb)
+    assert plan.shape == (3, cap, 8)
+    used = plan[2][plan[2] >= 0]
+    assert used.numel() == int((plan[0, :, 6] >= 0).sum())          # every item in one bin
+    out = native.paged_decode_cascade_grouped(q, kc, vc, bt, cl, Hq, scale, pt, plen, 4, plan.cuda())
+    err = (out.float() - ref.float()).abs().max().item()
+    assert err < 2e-2, err
+    err32 = (out.float() - ref32.float()).abs().max().item()
+    assert err32 < 3e-2, err32
+
+
+def test_persistent_identity_plan_matches_per_row(native):
+    """The engine's identity plan (one quad per bin, before set_groups runs)."""
+    from docqa_amd.engine.llm_engine import _identity_groups
+
+    Hkv, D, BS, Pb, maxb, B = 8, 128, 64, 2, 10, 64
+    Hq = 4 * Hkv
+    tables, lens, nblk = _trie_batch(B, Pb, maxb, 11)
+    kc = torch.randn(nblk, Hkv, BS, D, device="cuda", dtype=torch.bfloat16)
+    vc = torch.randn_like(kc)
+    bt = torch.tensor(tables, dtype=torch.int32, device="cuda")
+    cl = torch.tensor(lens, dtype=torch.int32, device="cuda")
+    q = torch.randn(B, (Hq + 2 * Hkv) * D, device="cuda", dtype=torch.bfloat16)
+    pt = torch.zeros(maxb, dtype=torch.int32, device="cuda")
+    pt[:Pb] = bt[0, :Pb]
+    plen = torch.tensor([Pb * BS], dtype=torch.int32, device="cuda")
+    scale = 1 / math.sqrt(D)
+    plan = _identity_groups(B, "cuda", Hkv)
+    assert plan.shape[0] == 3
+    ref = native.paged_decode_cascade(q, kc, vc, bt, cl, Hq, maxb * BS, scale, pt, plen, 4)
+    out = native.paged_decode_cascade_grouped(q, kc, vc, bt, cl, Hq, scale, pt, plen, 4, plan)
+    assert (out.float() - ref.float()).abs().max().item() < 2e-2
