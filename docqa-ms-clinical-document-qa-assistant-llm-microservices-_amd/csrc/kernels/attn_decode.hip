@@ -1563,15 +1563,53 @@ int docqa_paged_decode_cascade_persist(const void* q, int q_stride, void* k_cach
   if (B == 0) return 0;
   if (BS != 64 || maxb > kGroupMaxPos || Hq != 4 * Hkv || nchunk < 1 || nchunk > kCascadeMaxChunks || cap < 1)
     return -1;
+  // The group kernel no longer reads the prefix partials (the merge does), so the shared-
+  // prefix kernel runs on a side stream beside it: its workgroups fill the CUs the group
+  // kernel's tail leaves idle.  Fork / join by events -- captured into the decode graph as
+  // parallel branches.  DOCQA_CASCADE_FORK=0: one stream.
+  static const bool fork = [] {
+    const char* e = getenv("DOCQA_CASCADE_FORK");
+    return !(e && atoi(e) == 0);
+  }();
+  hipStream_t side = s;
+  hipEvent_t ev_fork = nullptr, ev_join = nullptr;
+  if (fork) {
+    static hipStream_t streams[64] = {};
+    static hipEvent_t evs[64][2] = {};
+    int dev = 0;
+    if (hipGetDevice(&dev) == hipSuccess && dev >= 0 && dev < 64) {
+      // created on the first (eager) call: the engine runs every decode step body once
+      // before capturing it, and creation is not a stream operation a capture may contain
+      hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+      if (!streams[dev] && hipStreamIsCapturing(s, &cs) == hipSuccess && cs == hipStreamCaptureStatusNone) {
+        if (hipStreamCreateWithFlags(&streams[dev], hipStreamNonBlocking) != hipSuccess ||
+            hipEventCreateWithFlags(&evs[dev][0], hipEventDisableTiming) != hipSuccess ||
+            hipEventCreateWithFlags(&evs[dev][1], hipEventDisableTiming) != hipSuccess)
+          streams[dev] = nullptr;
+      }
+      if (streams[dev] && evs[dev][0] && evs[dev][1]) {
+        side = streams[dev];
+        ev_fork = evs[dev][0];
+        ev_join = evs[dev][1];
+      }
+    }
+  }
+  if (side != s) {
+    if (hipEventRecord(ev_fork, s) != hipSuccess || hipStreamWaitEvent(side, ev_fork, 0) != hipSuccess) return -3;
+  }
   const int rc = docqa_cascade_prefix(q, q_stride, B, Hq, Hkv, scale, k_cache, v_cache, prefix_table, plen, BS,
-                                      nchunk, pacc, pml, nullptr, nullptr, s);
+                                      nchunk, pacc, pml, nullptr, nullptr, side);
   if (rc) return rc;
+  if (side != s) {
+    if (hipEventRecord(ev_join, side) != hipSuccess) return -3;
+  }
   const CascadeIn ci{pacc, pml, plen, nchunk, nullptr};
   const int nb = group_persist_bins(cap, Hkv);
   paged_decode_group_persist_kernel<3><<<dim3(Hkv, nb), 256, 0, s>>>(
       (const uint16_t*)q, q_stride, (const uint16_t*)k_cache, (const uint16_t*)v_cache, block_tables, maxb,
       context_lens, B, Hkv, scale, items, bins, ci, ws_acc, ws_ml);
   DOCQA_CHECK_LAUNCH();
+  if (side != s && hipStreamWaitEvent(s, ev_join, 0) != hipSuccess) return -3;
   group_split_merge_kernel<<<dim3(Hkv, cap), 256, 0, s>>>(merges, ws_acc, ws_ml, context_lens, B, Hkv,
                                                           (uint16_t*)out, out_stride, ci);
   DOCQA_CHECK_LAUNCH();
