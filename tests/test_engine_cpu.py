@@ -372,3 +372,25 @@ def test_persistent_identity_plan_cpu():
     assert sorted(int(i) for i in g[2].flatten() if i >= 0) == list(range(64))
     assert int((g[2, :, 1] >= 0).sum()) == 0          # one quad per bin
     assert ops.persist_bins(256, 8) >= 64
+
+
+def test_mid_plan_glu_never_picks_narrow_tiles():
+    """the fused-SwiGLU gate|up launch has no 64-wide (cfg 7) variant."""
+    from docqa_amd import ops
+
+    for M, N, K in [(256, 1024, 256), (256, 28672, 4096), (512, 2048, 1024), (384, 4096, 512)]:
+        S, cfg = ops.mid_plan(M, N, K, glu=True)
+        assert cfg != 7
+        S2, cfg2 = ops.mid_plan(M, N, K)
+        assert S2 >= 1 or cfg2 == 0
+
+
+def test_reserve_rolls_back_without_prefix_cache():
+    """a batch that does not fit frees what it had reserved (prefix cache off)."""
+    m = _model()
+    eng = LLMEngine(m, max_batch=4, max_context=256, use_graphs=False, num_blocks=6, prefix_cache=False)
+    free0 = eng.kv.allocator.num_free()
+    prompts = [[5] * 100, [6] * 100, [7] * 100, [8] * 100]     # 2 blocks each with 16 new tokens
+    with pytest.raises(MemoryError):
+        eng.reserve(prompts, SamplingParams(max_new_tokens=16))
+    assert eng.kv.allocator.num_free() == free0

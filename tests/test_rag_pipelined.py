@@ -63,3 +63,35 @@ def test_pipelined_matches_sequential_gpu(monkeypatch):
     assert ops.load_native(build_if_missing=False)
     _check("llama3-1b-test", "cuda")
     assert ops.native_loaded()
+
+
+def test_pipelined_with_pool_for_one_batch_cpu(monkeypatch):
+    """KV pool that holds ONE batch (no prefix cache): the pipelined loop must not fail
+    when batch i+1 cannot be reserved while batch i runs -- it collects batch i first
+    (answer_pipelined MemoryError) -- and still answers like the sequential loop."""
+    monkeypatch.setenv("DOCQA_TUNE_DECODE", "0")
+    from docqa_amd.engine.llm_engine import LLMEngine, SamplingParams
+    from docqa_amd.text.synthetic import synthetic_questions
+
+    bs, new, nb = 4, 4, 3
+    qs = synthetic_questions(nb * bs, seed=5)
+    batches = [qs[i * bs:(i + 1) * bs] for i in range(nb)]
+    sp = SamplingParams(max_new_tokens=new, stop_on_eos=False)
+    outs = []
+    for mode in ("seq", "pipe"):
+        pipe = _stack("tiny", "cpu")
+        needs = []
+        for b in batches:
+            _, I = pipe.index.search(pipe.embed(b), pipe.k)
+            prompts = pipe.build_prompts(b, I.tolist())
+            needs.append(sum((len(p) + new + 63) // 64 for p in prompts))
+        blocks = max(needs)
+        assert 2 * min(needs) > blocks              # two batches never fit together
+        pipe.engine = LLMEngine(pipe.engine.model, max_batch=bs, max_context=2048, use_graphs=False,
+                                num_blocks=blocks, prefix_cache=False)
+        if mode == "seq":
+            outs.append([[a.token_ids for a in pipe.answer_batch(b, sp)] for b in batches])
+        else:
+            outs.append([[a.token_ids for a in ans] for ans, _, _ in pipe.answer_pipelined(batches, sp)])
+        assert pipe.engine.kv.allocator.num_free() == blocks
+    assert outs[0] == outs[1]
