@@ -1506,71 +1506,19 @@ int docqa_paged_decode_cascade_grouped(const void* q, int q_stride, void* k_cach
   return 0;
 }
 
-// Grouped cascade decode with long groups split over several workgroups: items [cap, 8]
-// (see paged_decode_group_kernel SPLIT), merges [cap, 8] (group_split_merge_kernel),
-// ws_acc [slots, Hkv, 16, 128] / ws_ml [slots, Hkv, 16, 2] fp32 partials.
-int docqa_paged_decode_cascade_split(const void* q, int q_stride, void* k_cache, void* v_cache,
-                                     const int* block_tables, int maxb, const int* context_lens,
-                                     void* out, int out_stride, int B, int Hq, int Hkv, int BS,
-                                     float scale, const int* prefix_table, const int* plen, int nchunk,
-                                     float* pacc, float* pml, const int* items, const int* merges, int cap,
-                                     float* ws_acc, float* ws_ml, hipStream_t s) {
-  if (B == 0) return 0;
-  if (BS != 64 || maxb > kGroupMaxPos || Hq != 4 * Hkv || nchunk < 1 || nchunk > kCascadeMaxChunks || cap < 1)
-    return -1;
-  // DOCQA_GROUP_INLINE_PREFIX=1: no prefix kernel -- the plan's items start at block 0, so
-  // every group streams the shared template blocks itself (L2 hits after the first group)
-  static const bool inline_prefix = [] {
-    const char* e = getenv("DOCQA_GROUP_INLINE_PREFIX");
-    return e && atoi(e) == 1;
-  }();
-  if (!inline_prefix) {
-    const int rc = docqa_cascade_prefix(q, q_stride, B, Hq, Hkv, scale, k_cache, v_cache, prefix_table, plen,
-                                        BS, nchunk, pacc, pml, nullptr, nullptr, s);
-    if (rc) return rc;
-  }
-  const CascadeIn ci{pacc, pml, inline_prefix ? nullptr : plen, nchunk, nullptr};
-  static const int nsr = [] {   // ring slots (A/B knob): 3 (3 workgroups / CU) or 4 (2)
-    const char* e = getenv("DOCQA_GROUP_NSR");
-    return e && atoi(e) == 4 ? 4 : 3;
-  }();
-  if (nsr == 4)
-    paged_decode_group_kernel<4, true><<<dim3(Hkv, cap), 256, 0, s>>>(
-        (const uint16_t*)q, q_stride, (const uint16_t*)k_cache, (const uint16_t*)v_cache, block_tables, maxb,
-        context_lens, B, Hkv, scale, (uint16_t*)out, out_stride, items, ci, ws_acc, ws_ml);
-  else
-    paged_decode_group_kernel<3, true><<<dim3(Hkv, cap), 256, 0, s>>>(
-        (const uint16_t*)q, q_stride, (const uint16_t*)k_cache, (const uint16_t*)v_cache, block_tables, maxb,
-        context_lens, B, Hkv, scale, (uint16_t*)out, out_stride, items, ci, ws_acc, ws_ml);
-  DOCQA_CHECK_LAUNCH();
-  // merge rows: at most (cap + 1) / 2 (ops.split_decode_groups guarantees it), so half the
-  // grid -- the empty workgroups of the unused merge rows are not free
-  group_split_merge_kernel<<<dim3(Hkv, (cap + 1) / 2), 256, 0, s>>>(merges, ws_acc, ws_ml, context_lens, B, Hkv,
-                                                          (uint16_t*)out, out_stride, ci);
-  DOCQA_CHECK_LAUNCH();
-  return 0;
-}
-
-// Persistent grouped cascade decode: plan [3, cap, 8] = items (4 rows, first position, end
-// position, slot, 0), merges (4 rows, first slot, slots, 0, 0) covering EVERY group, bins
-// (<= 8 item indices, -1 = none) -- group_persist_bins(cap, Hkv) of them.
-int docqa_paged_decode_cascade_persist(const void* q, int q_stride, void* k_cache, void* v_cache,
-                                       const int* block_tables, int maxb, const int* context_lens,
-                                       void* out, int out_stride, int B, int Hq, int Hkv, int BS,
-                                       float scale, const int* prefix_table, const int* plen, int nchunk,
-                                       float* pacc, float* pml, const int* items, const int* merges,
-                                       const int* bins, int cap, float* ws_acc, float* ws_ml, hipStream_t s) {
-  if (B == 0) return 0;
-  if (BS != 64 || maxb > kGroupMaxPos || Hq != 4 * Hkv || nchunk < 1 || nchunk > kCascadeMaxChunks || cap < 1)
-    return -1;
-  // The group kernel no longer reads the prefix partials (the merge does), so the shared-
-  // prefix kernel runs on a side stream beside it: its workgroups fill the CUs the group
-  // kernel's tail leaves idle.  Fork / join by events -- captured into the decode graph as
-  // parallel branches.  DOCQA_CASCADE_FORK=0: one stream.
+// Shared-prefix (cascade) kernel on a side stream, forked from / joined back to `s` by
+// events -- captured into the decode graph as parallel branches -- for launchers whose
+// suffix kernel does not read the prefix partials (only their merge does): its workgroups
+// fill the CUs the suffix kernel's tail leaves idle.  *join: the event `s` must wait for
+// before the merge (nullptr: ran on `s`, DOCQA_CASCADE_FORK=0 or no side stream).
+static int cascade_prefix_forked(const void* q, int q_stride, int B, int Hq, int Hkv, float scale, void* k_cache,
+                                 void* v_cache, const int* prefix_table, const int* plen, int BS, int nchunk,
+                                 float* pacc, float* pml, hipStream_t s, hipEvent_t* join) {
   static const bool fork = [] {
     const char* e = getenv("DOCQA_CASCADE_FORK");
     return !(e && atoi(e) == 0);
   }();
+  *join = nullptr;
   hipStream_t side = s;
   hipEvent_t ev_fork = nullptr, ev_join = nullptr;
   if (fork) {
@@ -1602,14 +1550,88 @@ int docqa_paged_decode_cascade_persist(const void* q, int q_stride, void* k_cach
   if (rc) return rc;
   if (side != s) {
     if (hipEventRecord(ev_join, side) != hipSuccess) return -3;
+    *join = ev_join;
   }
+  return 0;
+}
+
+// Grouped cascade decode with long groups split over several workgroups: items [cap, 8]
+// (see paged_decode_group_kernel SPLIT), merges [cap, 8] (group_split_merge_kernel),
+// ws_acc [slots, Hkv, 16, 128] / ws_ml [slots, Hkv, 16, 2] fp32 partials.
+int docqa_paged_decode_cascade_split(const void* q, int q_stride, void* k_cache, void* v_cache,
+                                     const int* block_tables, int maxb, const int* context_lens,
+                                     void* out, int out_stride, int B, int Hq, int Hkv, int BS,
+                                     float scale, const int* prefix_table, const int* plen, int nchunk,
+                                     float* pacc, float* pml, const int* items, const int* merges, int cap,
+                                     float* ws_acc, float* ws_ml, int defer, hipStream_t s) {
+  if (B == 0) return 0;
+  if (BS != 64 || maxb > kGroupMaxPos || Hq != 4 * Hkv || nchunk < 1 || nchunk > kCascadeMaxChunks || cap < 1)
+    return -1;
+  // DOCQA_GROUP_INLINE_PREFIX=1: no prefix kernel -- the plan's items start at block 0, so
+  // every group streams the shared template blocks itself (L2 hits after the first group)
+  static const bool inline_prefix = [] {
+    const char* e = getenv("DOCQA_GROUP_INLINE_PREFIX");
+    return e && atoi(e) == 1;
+  }();
+  // defer (a plan from ops.split_decode_groups(defer=True)): every item writes a partial
+  // and every group has a merge row, so no item reads the prefix partials and the prefix
+  // kernel is forked onto a side stream beside the group kernel
+  hipEvent_t ev_join = nullptr;
+  if (!inline_prefix) {
+    const int rc = defer ? cascade_prefix_forked(q, q_stride, B, Hq, Hkv, scale, k_cache, v_cache, prefix_table,
+                                                 plen, BS, nchunk, pacc, pml, s, &ev_join)
+                         : docqa_cascade_prefix(q, q_stride, B, Hq, Hkv, scale, k_cache, v_cache, prefix_table, plen,
+                                                BS, nchunk, pacc, pml, nullptr, nullptr, s);
+    if (rc) return rc;
+  }
+  const CascadeIn ci{pacc, pml, inline_prefix ? nullptr : plen, nchunk, nullptr};
+  static const int nsr = [] {   // ring slots (A/B knob): 3 (3 workgroups / CU) or 4 (2)
+    const char* e = getenv("DOCQA_GROUP_NSR");
+    return e && atoi(e) == 4 ? 4 : 3;
+  }();
+  if (nsr == 4)
+    paged_decode_group_kernel<4, true><<<dim3(Hkv, cap), 256, 0, s>>>(
+        (const uint16_t*)q, q_stride, (const uint16_t*)k_cache, (const uint16_t*)v_cache, block_tables, maxb,
+        context_lens, B, Hkv, scale, (uint16_t*)out, out_stride, items, ci, ws_acc, ws_ml);
+  else
+    paged_decode_group_kernel<3, true><<<dim3(Hkv, cap), 256, 0, s>>>(
+        (const uint16_t*)q, q_stride, (const uint16_t*)k_cache, (const uint16_t*)v_cache, block_tables, maxb,
+        context_lens, B, Hkv, scale, (uint16_t*)out, out_stride, items, ci, ws_acc, ws_ml);
+  DOCQA_CHECK_LAUNCH();
+  if (ev_join && hipStreamWaitEvent(s, ev_join, 0) != hipSuccess) return -3;
+  // merge rows: at most (cap + 1) / 2 (ops.split_decode_groups guarantees it), so half the
+  // grid -- the empty workgroups of the unused merge rows are not free; deferred: one per group
+  group_split_merge_kernel<<<dim3(Hkv, defer ? cap : (cap + 1) / 2), 256, 0, s>>>(merges, ws_acc, ws_ml, context_lens, B, Hkv,
+                                                          (uint16_t*)out, out_stride, ci);
+  DOCQA_CHECK_LAUNCH();
+  return 0;
+}
+
+// Persistent grouped cascade decode: plan [3, cap, 8] = items (4 rows, first position, end
+// position, slot, 0), merges (4 rows, first slot, slots, 0, 0) covering EVERY group, bins
+// (<= 8 item indices, -1 = none) -- group_persist_bins(cap, Hkv) of them.
+int docqa_paged_decode_cascade_persist(const void* q, int q_stride, void* k_cache, void* v_cache,
+                                       const int* block_tables, int maxb, const int* context_lens,
+                                       void* out, int out_stride, int B, int Hq, int Hkv, int BS,
+                                       float scale, const int* prefix_table, const int* plen, int nchunk,
+                                       float* pacc, float* pml, const int* items, const int* merges,
+                                       const int* bins, int cap, float* ws_acc, float* ws_ml, hipStream_t s) {
+  if (B == 0) return 0;
+  if (BS != 64 || maxb > kGroupMaxPos || Hq != 4 * Hkv || nchunk < 1 || nchunk > kCascadeMaxChunks || cap < 1)
+    return -1;
+  // The group kernel no longer reads the prefix partials (the merge does), so the shared-
+  // prefix kernel runs on a side stream beside it (cascade_prefix_forked).
+  hipEvent_t ev_join = nullptr;
+  const int rc = cascade_prefix_forked(q, q_stride, B, Hq, Hkv, scale, k_cache, v_cache, prefix_table, plen, BS,
+                                       nchunk, pacc, pml, s, &ev_join);
+  if (rc) return rc;
   const CascadeIn ci{pacc, pml, plen, nchunk, nullptr};
   const int nb = group_persist_bins(cap, Hkv);
   paged_decode_group_persist_kernel<3><<<dim3(Hkv, nb), 256, 0, s>>>(
       (const uint16_t*)q, q_stride, (const uint16_t*)k_cache, (const uint16_t*)v_cache, block_tables, maxb,
       context_lens, B, Hkv, scale, items, bins, ci, ws_acc, ws_ml);
   DOCQA_CHECK_LAUNCH();
-  if (side != s && hipStreamWaitEvent(s, ev_join, 0) != hipSuccess) return -3;
+  if (ev_join && hipStreamWaitEvent(s, ev_join, 0) != hipSuccess) return -3;
   group_split_merge_kernel<<<dim3(Hkv, cap), 256, 0, s>>>(merges, ws_acc, ws_ml, context_lens, B, Hkv,
                                                           (uint16_t*)out, out_stride, ci);
   DOCQA_CHECK_LAUNCH();

@@ -134,8 +134,17 @@ def _split_groups_on() -> bool:
 
 def _persist_groups_on() -> bool:
     """Persistent grouped decode (bins of work items per workgroup) on top of the split
-    plan; DOCQA_GROUP_PERSIST=0: one workgroup per item."""
-    return _split_groups_on() and os.environ.get("DOCQA_GROUP_PERSIST", "1") == "1"
+    plan, DOCQA_GROUP_PERSIST=1.  Off by default: one workgroup per item measured 5 %
+    faster end to end (153.4 vs 145.9 q/s, decode 1146 vs 1230 ms per batch, same box;
+    profiles/r3_ab_group_persist.log)."""
+    return _split_groups_on() and os.environ.get("DOCQA_GROUP_PERSIST", "0") == "1"
+
+
+def _defer_groups_on() -> bool:
+    """Split plan with every group merged by the merge kernel (ops.split_decode_groups
+    defer=True): the cascade-prefix kernel then runs on a side stream beside the group
+    kernel (AttnMeta.decode_defer)."""
+    return _split_groups_on() and os.environ.get("DOCQA_GROUP_DEFER", "0") == "1"
 
 
 def _identity_groups(bp: int, dev, hkv: int = 8) -> torch.Tensor:
@@ -144,6 +153,9 @@ def _identity_groups(bp: int, dev, hkv: int = 8) -> torch.Tensor:
         # split plan [2, bp, 8] (persistent: [3, bp, 8]): consecutive unsplit quads until
         # set_groups runs
         persist = _persist_groups_on()
+        # persistent / deferred plans: every quad writes a partial that the merge kernel
+        # folds with the prefix (nothing may read the forked prefix kernel's partials)
+        all_partial = persist or _defer_groups_on()
         g = torch.full((3 if persist else 2, max(bp, 1), 8), -1, dtype=torch.int32)
         g[:2, :, 4:] = 0
         g[0, :, 6] = -1
@@ -152,7 +164,7 @@ def _identity_groups(bp: int, dev, hkv: int = 8) -> torch.Tensor:
             q = list(range(4 * i, min(4 * i + 4, bp)))
             g[0, i, :len(q)] = torch.tensor(q, dtype=torch.int32)
             g[0, i, 5] = 1 << 20
-            if persist:
+            if all_partial:
                 g[0, i, 4] = 0
                 g[0, i, 6] = i
                 g[1, i, :len(q)] = torch.tensor(q, dtype=torch.int32)
@@ -377,6 +389,7 @@ class LLMEngine:
             meta.cascade_chunks = self._cascade_chunks(g.bp)
             if self.group_decode and ops.grouped_decode_ok(self.kv.caches[0][0], g.block_tables, self.model.hq):
                 meta.decode_groups = g.groups
+                meta.decode_defer = g.groups.dim() == 3 and _defer_groups_on()
         if g.greedy:
             # greedy: the LM head's argmax is fused into its GEMM (no [B, vocab] logits)
             nxt = self.model.forward(g.tokens, meta, self.kv.caches, greedy_ids=True)
@@ -428,7 +441,8 @@ class LLMEngine:
                 skip = 0   # the kernel attends the shared prefix inside each group
             plan = ops.split_decode_groups(quads, tables, lens, skip, self.block_size, cap,
                                            int(os.environ.get("DOCQA_GROUP_TILES", "12")),
-                                           bins=ops.persist_bins(cap, self.model.hkv) if g.groups.shape[0] == 3 else 0)
+                                           bins=ops.persist_bins(cap, self.model.hkv) if g.groups.shape[0] == 3 else 0,
+                                           defer=_defer_groups_on())
             _upload(g.groups, plan)
             g.groups_key = key
             return

@@ -115,6 +115,8 @@ class AttnMeta:
     # (decode, cascade) rows packed in groups of <= 4 sharing prefix-cache blocks
     # (ops.paged_decode_cascade_grouped); None: per-row suffix attention
     decode_groups: torch.Tensor | None = None
+    # decode_groups is a deferred split plan (ops.split_decode_groups(defer=True))
+    decode_defer: bool = False
 
 
 class LlamaModel:
@@ -310,7 +312,8 @@ class LlamaModel:
                     if meta.decode_groups is not None:
                         a = ops.paged_decode_cascade_grouped(qkv, kc, vc, meta.block_tables, meta.context_lens,
                                                              hq, self.scale, meta.shared_table, meta.shared_len,
-                                                             meta.cascade_chunks, meta.decode_groups)
+                                                             meta.cascade_chunks, meta.decode_groups,
+                                                             meta.decode_defer)
                     else:
                         a = ops.paged_decode_cascade(qkv, kc, vc, meta.block_tables, meta.context_lens, hq,
                                                      meta.max_context, self.scale, meta.shared_table,
@@ -321,7 +324,8 @@ class LlamaModel:
                     if meta.decode_groups is not None:
                         a = ops.paged_decode_cascade_grouped(qkv, kc, vc, meta.block_tables, meta.context_lens,
                                                              hq, self.scale, meta.shared_table, meta.shared_len,
-                                                             meta.cascade_chunks, meta.decode_groups)
+                                                             meta.cascade_chunks, meta.decode_groups,
+                                                             meta.decode_defer)
                     else:
                         a = ops.paged_decode_cascade(qkv, kc, vc, meta.block_tables, meta.context_lens, hq,
                                                      meta.max_context, self.scale, meta.shared_table,

@@ -496,18 +496,20 @@ def paged_decode_cascade(q, k_cache, v_cache, block_tables, context_lens, Hq, ma
 
 
 def paged_decode_cascade_grouped(q, k_cache, v_cache, block_tables, context_lens, Hq, scale,
-                                 prefix_table, prefix_len, nchunk: int, groups):
+                                 prefix_table, prefix_len, nchunk: int, groups, defer: bool = False):
     """Cascade decode with the suffix attention of rows that share prefix-cache KV blocks
     done together (csrc/kernels/attn_decode.hip paged_decode_group_kernel): ``groups``
     int32 [ngroups * 4] packs every row into one group of <= 4 (-1 = empty slot), and a
     block shared by k rows of a group is read once instead of k times.  Same result as
     :func:`paged_decode_cascade` for any packing.  ``groups`` may also be a split plan
     int32 [2, cap, 8] from :func:`split_decode_groups` (long groups over several
-    workgroups, partials merged by log-sum-exp)."""
+    workgroups, partials merged by log-sum-exp); ``defer``: that plan was built with
+    ``split_decode_groups(defer=True)`` (the prefix kernel then runs on a side stream)."""
     if _gpu(q):
         if groups.dim() == 3:
             return _native().paged_decode_cascade_split(q, k_cache, v_cache, block_tables, context_lens, Hq,
-                                                        scale, prefix_table, prefix_len, nchunk, groups)
+                                                        scale, prefix_table, prefix_len, nchunk, groups,
+                                                        defer and groups.shape[0] == 2)
         return _native().paged_decode_cascade_grouped(q, k_cache, v_cache, block_tables, context_lens, Hq,
                                                       scale, prefix_table, prefix_len, nchunk, groups)
     max_context = block_tables.shape[1] * k_cache.shape[2]
@@ -635,7 +637,8 @@ BIN_ITEMS, BIN_MAX_TILES = 8, 512    # attn_decode.hip kBinItems / kBinMaxTiles
 
 
 def split_decode_groups(quads: list[list[int]], tables: list[list[int]], lens: list[int], skip: int,
-                        block_size: int, cap: int, tiles_per_item: int = 12, bins: int = 0) -> torch.Tensor:
+                        block_size: int, cap: int, tiles_per_item: int = 12, bins: int = 0,
+                        defer: bool = False) -> torch.Tensor:
     """Split plan for the grouped cascade decode (``paged_decode_cascade_grouped`` with a
     [2, cap, 8] int32 ``groups``): every group of :func:`pack_decode_groups` is cut at block
     positions into work items of about ``tiles_per_item`` K/V tiles (``lens``: the lengths
@@ -650,8 +653,13 @@ def split_decode_groups(quads: list[list[int]], tables: list[list[int]], lens: l
     (slot = its index), every group has a merge row, and plan[2] packs the items into
     ``bins`` (:func:`persist_bins`) workgroups of <= 8 items and <= 512 tiles each, greedy
     longest-first onto the least-loaded bin, so each workgroup streams ~total / bins tiles
-    through one ring."""
+    through one ring.
+
+    ``defer``: every item writes a partial and every group has a merge row (at most ``cap``),
+    as in the persistent plan, so no item reads the cascade-prefix partials and the prefix
+    kernel runs on a side stream beside the group kernel (attn_decode.hip, DOCQA_GROUP_DEFER)."""
     budget = max(1, tiles_per_item)
+    all_partial = bool(bins) or defer
     while True:
         items, merges, nslot = [], [], 0
         for qd in quads:
@@ -665,7 +673,7 @@ def split_decode_groups(quads: list[list[int]], tables: list[list[int]], lens: l
                 acc += t
             end = max((lens[r] + block_size - 1) // block_size for r in qd)
             cuts.append((start, max(end, start + 1), acc))
-            if bins:
+            if all_partial:
                 merges.append(rows4 + [nslot, len(cuts), 0, 0])
                 for lo, hi, t in cuts:
                     items.append((t, rows4 + [lo, hi, nslot, 0]))
@@ -677,7 +685,7 @@ def split_decode_groups(quads: list[list[int]], tables: list[list[int]], lens: l
                 for lo, hi, t in cuts:
                     items.append((t, rows4 + [lo, hi, nslot, 0]))
                     nslot += 1
-        fits = len(items) <= cap and len(merges) <= (cap if bins else (cap + 1) // 2)
+        fits = len(items) <= cap and len(merges) <= (cap if all_partial else (cap + 1) // 2)
         if fits and bins:
             nb = min(bins, cap)
             fits = len(items) <= nb * BIN_ITEMS and all(t <= BIN_MAX_TILES for t, _ in items)

@@ -26,6 +26,7 @@ def main() -> None:
     ap.add_argument("--batches", type=int, default=3)
     ap.add_argument("--max-new-tokens", type=int, default=128)
     ap.add_argument("--notes", type=int, default=1000)
+    ap.add_argument("--questions", choices=("unique", "repeat"), default="unique")
     a = ap.parse_args()
 
     import torch
@@ -35,7 +36,7 @@ def main() -> None:
     from docqa_amd.models import checkpoint as ck
     from docqa_amd.pipeline.corpus import build_corpus, embed_records
     from docqa_amd.pipeline.rag import RAGPipeline
-    from docqa_amd.text.synthetic import synthetic_questions
+    from docqa_amd.text.synthetic import synthetic_questions, synthetic_unique_questions
     from docqa_amd.text.tokenizer import ChatTokenizer, WordPieceTokenizer
 
     torch.set_grad_enabled(False)
@@ -52,7 +53,8 @@ def main() -> None:
         device = torch.device("cpu")
 
     pipe = RAGPipeline(encoder, enc_tok, index, records, _Eng(), chat_tok, k=3, max_prompt_tokens=2048 - 256)
-    qs = synthetic_questions((a.batches + 2) * a.batch, seed=123)
+    gen = synthetic_unique_questions if a.questions == "unique" else synthetic_questions
+    qs = gen((a.batches + 2) * a.batch, seed=123)
     BS = 64
     for bi in range(2, 2 + a.batches):   # the bench's timed batches follow 2 warm-up batches
         qb = qs[bi * a.batch:(bi + 1) * a.batch]

@@ -324,6 +324,34 @@ def test_split_decode_groups_plan(tiles):
         assert not merges
 
 
+@pytest.mark.parametrize("tiles", [1, 2, 100])
+def test_deferred_split_plan(tiles):
+    """Deferred split plan (prefix kernel forked beside the group kernel): the same items
+    as the plain split plan, but every item writes a partial and every group -- split or
+    not -- has one merge row over its consecutive slots, so nothing reads the prefix
+    partials before the merge."""
+    from docqa_amd import ops
+
+    skip = 2
+    tables = [[0, 1, 10, 11, 50, 70], [0, 1, 10, 11, 51, 71], [0, 1, 20, 52, 53, 72], [0, 1, 10, 12, 54, 73],
+              [0, 1, 30, 55, 56, 74], [0, 1, 20, 57, 58, 75], [0, 1, 60, 61, 62, 76]]
+    lens = [330, 300, 370, 250, 384, 200, 310]
+    quads = ops.pack_decode_groups(tables, lens, skip, 64, cap=4)
+    plain = ops.split_decode_groups(quads, tables, lens, skip, 64, cap=16, tiles_per_item=tiles)
+    plan = ops.split_decode_groups(quads, tables, lens, skip, 64, cap=16, tiles_per_item=tiles, defer=True)
+    assert plan.shape == (2, 16, 8)
+    items = [r.tolist() for r in plan[0] if (r[:4] >= 0).any()]
+    # the same work items (rows; an unsplit group's range is explicit instead of open-ended)
+    assert sorted(it[:4] for it in items) == sorted(r[:4].tolist() for r in plain[0] if (r[:4] >= 0).any())
+    assert sorted(it[6] for it in items) == list(range(len(items)))
+    merges = [r.tolist() for r in plan[1] if r[5] > 0]
+    assert len(merges) == len(quads)
+    for m in merges:
+        key = sorted(r for r in m[:4] if r >= 0)
+        mine = [it for it in items if sorted(r for r in it[:4] if r >= 0) == key]
+        assert sorted(it[6] for it in mine) == list(range(m[4], m[4] + m[5]))
+
+
 @pytest.mark.parametrize("tiles,bins", [(1, 3), (2, 4), (5, 2), (100, 8)])
 def test_persistent_decode_plan(tiles, bins):
     """Persistent plan [3, cap, 8]: every item owns slot = its index, every group has one
@@ -360,10 +388,11 @@ def test_persistent_decode_plan(tiles, bins):
     assert ops.persist_bins(256, 8) == 96 and ops.persist_bins(512, 8) == 128 and ops.persist_bins(4, 2) == 4
 
 
-def test_persistent_identity_plan_cpu():
+def test_persistent_identity_plan_cpu(monkeypatch):
     from docqa_amd import ops
     from docqa_amd.engine.llm_engine import _identity_groups
 
+    monkeypatch.setenv("DOCQA_GROUP_PERSIST", "1")
     g = _identity_groups(256, "cpu", 8)
     assert g.shape == (3, 256, 8)
     items = g[0][g[0, :, 6] >= 0]
@@ -372,6 +401,24 @@ def test_persistent_identity_plan_cpu():
     assert sorted(int(i) for i in g[2].flatten() if i >= 0) == list(range(64))
     assert int((g[2, :, 1] >= 0).sum()) == 0          # one quad per bin
     assert ops.persist_bins(256, 8) >= 64
+
+
+@pytest.mark.parametrize("defer", [False, True])
+def test_split_identity_plan_cpu(monkeypatch, defer):
+    """Default (split) identity plan: consecutive quads; deferred: each quad writes slot i
+    and has merge row i (nothing reads the forked prefix kernel's partials)."""
+    from docqa_amd.engine.llm_engine import _identity_groups
+
+    monkeypatch.setenv("DOCQA_GROUP_PERSIST", "0")
+    monkeypatch.setenv("DOCQA_GROUP_DEFER", "1" if defer else "0")
+    g = _identity_groups(256, "cpu", 8)
+    assert g.shape == (2, 256, 8)
+    assert g[0, :64, :4].flatten().tolist() == list(range(256))
+    if defer:
+        assert (g[0, :64, 6] == torch.arange(64)).all()
+        assert (g[1, :64, 5] == 1).all() and (g[1, :64, 4] == torch.arange(64)).all()
+    else:
+        assert (g[0, :, 6] == -1).all() and (g[1, :, 5] == 0).all()
 
 
 def test_mid_plan_glu_never_picks_narrow_tiles():

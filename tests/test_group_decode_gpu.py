@@ -99,10 +99,12 @@ def test_grouped_cascade_padded_rows_zero(native):
 
 @pytest.mark.parametrize("B,Hkv,seed", [(37, 8, 0), (256, 8, 3), (9, 2, 5)])
 @pytest.mark.parametrize("tiles", [1, 3, 12, 1000])
-def test_split_grouped_cascade_matches_per_row(native, B, Hkv, seed, tiles):
+@pytest.mark.parametrize("defer", [False, True])
+def test_split_grouped_cascade_matches_per_row(native, B, Hkv, seed, tiles, defer):
     """Split plan (long groups over several workgroups + LSE merge) == per-row cascade and
     the fp32 reference; planned with END-of-decode lengths longer than the current ones,
-    so some items have no keys yet."""
+    so some items have no keys yet.  ``defer``: every group merged by the merge kernel and
+    the prefix kernel forked onto a side stream."""
     Hq, D, BS, Pb, maxb = 4 * Hkv, 128, 64, 3, 12
     tables, lens, nblk = _trie_batch(B, Pb, maxb, seed)
     kc = torch.randn(nblk, Hkv, BS, D, device="cuda", dtype=torch.bfloat16)
@@ -119,10 +121,12 @@ def test_split_grouped_cascade_matches_per_row(native, B, Hkv, seed, tiles):
         ref32 = native.paged_decode_cascade(q, kc, vc, bt, cl, Hq, maxb * BS, scale, pt, plen, 4)
     end_lens = [min(L + 128, maxb * BS) for L in lens]
     quads = native.pack_decode_groups(tables, end_lens, Pb, BS, (B + 1) // 2)
-    plan = native.split_decode_groups(quads, tables, end_lens, Pb, BS, max(B, 4), tiles)
+    plan = native.split_decode_groups(quads, tables, end_lens, Pb, BS, max(B, 4), tiles, defer=defer)
     if tiles == 1:
         assert (plan[1, :, 5] > 1).any()   # some group really is split
-    out = native.paged_decode_cascade_grouped(q, kc, vc, bt, cl, Hq, scale, pt, plen, 4, plan.cuda())
+    if defer:
+        assert (plan[0, :, 6][plan[0, :, 0] >= 0] >= 0).all()   # every item writes a partial
+    out = native.paged_decode_cascade_grouped(q, kc, vc, bt, cl, Hq, scale, pt, plen, 4, plan.cuda(), defer)
     err = (out.float() - ref.float()).abs().max().item()
     assert err < 2e-2, err
     err32 = (out.float() - ref32.float()).abs().max().item()
@@ -185,9 +189,15 @@ def test_persistent_grouped_cascade_matches_per_row(native, B, Hkv, seed, tiles)
     assert err32 < 3e-2, err32
 
 
-def test_persistent_identity_plan_matches_per_row(native):
-    """The engine's identity plan (one quad per bin, before set_groups runs)."""
-    from docqa_amd.engine.llm_engine import _identity_groups
+@pytest.mark.parametrize("mode", ["persist", "defer", "split"])
+def test_identity_plan_matches_per_row(native, monkeypatch, mode):
+    """The engine's identity plan (consecutive quads, before set_groups runs) in each plan
+    mode: persistent (one quad per bin), deferred (every quad merged, prefix forked) and
+    plain split (quads finish in their workgroup)."""
+    from docqa_amd.engine.llm_engine import _defer_groups_on, _identity_groups
+
+    monkeypatch.setenv("DOCQA_GROUP_PERSIST", "1" if mode == "persist" else "0")
+    monkeypatch.setenv("DOCQA_GROUP_DEFER", "1" if mode == "defer" else "0")
 
     Hkv, D, BS, Pb, maxb, B = 8, 128, 64, 2, 10, 64
     Hq = 4 * Hkv
@@ -202,7 +212,8 @@ def test_persistent_identity_plan_matches_per_row(native):
     plen = torch.tensor([Pb * BS], dtype=torch.int32, device="cuda")
     scale = 1 / math.sqrt(D)
     plan = _identity_groups(B, "cuda", Hkv)
-    assert plan.shape[0] == 3
+    assert plan.shape[0] == (3 if mode == "persist" else 2)
     ref = native.paged_decode_cascade(q, kc, vc, bt, cl, Hq, maxb * BS, scale, pt, plen, 4)
-    out = native.paged_decode_cascade_grouped(q, kc, vc, bt, cl, Hq, scale, pt, plen, 4, plan)
+    out = native.paged_decode_cascade_grouped(q, kc, vc, bt, cl, Hq, scale, pt, plen, 4, plan,
+                                              _defer_groups_on())
     assert (out.float() - ref.float()).abs().max().item() < 2e-2
