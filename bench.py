@@ -52,6 +52,9 @@ def main() -> None:
     ap.add_argument("--max-context", type=int, default=2048)
     ap.add_argument("--no-graphs", action="store_true")
     ap.add_argument("--device", default="cuda", help="cuda (MI355X) | cpu (CI rehearsal of the DP path with gloo)")
+    ap.add_argument("--share-gpu", action="store_true",
+                    help="every rank on cuda:0 (a one-GPU rehearsal of the N-rank DP path; process group "
+                         "backend from DOCQA_SHARE_GPU_BACKEND, default gloo); correctness, not speed")
     ap.add_argument("--questions", choices=("unique", "repeat"), default="unique",
                     help="unique: every request a distinct question (default); repeat: the ~470-string "
                          "template grid of rounds 1-2 (cache-hot ceiling)")
@@ -75,11 +78,16 @@ def main() -> None:
     world = int(os.environ.get("WORLD_SIZE", "1"))
     if world != a.gpus:
         print(f"[bench] warning: --gpus {a.gpus} but WORLD_SIZE {world}", file=sys.stderr)
-    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    local_rank = 0 if a.share_gpu else int(os.environ.get("LOCAL_RANK", "0"))
     cuda = a.device == "cuda"
     if cuda:
         torch.cuda.set_device(local_rank)
-    ps = comm.init_distributed(tp_size=a.tp, backend=None if cuda else "gloo")
+    backend = None if cuda else "gloo"
+    if a.share_gpu:
+        backend = os.environ.get("DOCQA_SHARE_GPU_BACKEND", "gloo")
+        if backend == "nccl":
+            os.environ["LOCAL_RANK"] = "0"    # init_distributed binds the rank to LOCAL_RANK's device
+    ps = comm.init_distributed(tp_size=a.tp, backend=backend)
     if cuda:
         assert ops.load_native(), "native HIP kernels not built (python -m docqa_amd.ops.build)"
         # TP > 1: init_distributed already set up the IPC all-reduce (fused residual + RMSNorm,

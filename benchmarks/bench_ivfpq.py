@@ -184,12 +184,27 @@ def bench_bge_indexer(a):
     qs = synthetic_unique_questions(a.nq, seed=5)
     xq = enc.encode(tok.encode_batch(qs)).float()
     De, Ie = store.flat.search(xq, a.k)
+    xb = store.flat.xb
+    kth = De[:, a.k - 1].to(xb.device).float()
+
+    def tie_aware(Ia):
+        # a returned id counts if its EXACT distance is within the k-th true neighbour's
+        # (+1e-4 relative): near-duplicate chunks (templated notes) sit at equal distances, and
+        # strict id recall then scores an equally near chunk as a miss
+        ids = Ia.to(xb.device)
+        rows = xb[ids.clamp_min(0)].float()
+        q = xq.to(xb.device)
+        d = ((rows - q[:, None, :]) ** 2).sum(-1)
+        ok = (ids >= 0) & (d <= kth[:, None] * (1 + 1e-4) + 1e-6)
+        return float(ok.float().mean())
+
     sweep = []
-    for nprobe in sorted({max(1, a.nprobe // 4), a.nprobe // 2, a.nprobe, 2 * a.nprobe}):
+    for nprobe in sorted({max(1, a.nprobe // 4), a.nprobe // 2, a.nprobe, 2 * a.nprobe, 4 * a.nprobe}):
         for kf in sorted({1, a.k_factor, 2 * a.k_factor}):
             store.k_factor = kf
             _, Ia = store.search(xq, a.k, nprobe=nprobe)
             rec = sum(len(set(Ia[j].tolist()) & set(Ie[j].tolist())) for j in range(a.nq)) / (a.nq * a.k)
+            rec_tie = tie_aware(Ia)
             torch.cuda.synchronize()
             t = time.perf_counter()
             for _ in range(a.iters):
@@ -197,14 +212,19 @@ def bench_bge_indexer(a):
             torch.cuda.synchronize()
             ms = (time.perf_counter() - t) / a.iters * 1e3
             sweep.append({"nprobe": nprobe, "k_factor": kf, "recall_at_k": round(rec, 4),
+                          "recall_at_k_tie_aware": round(rec_tie, 4),
                           "ms_per_batch": round(ms, 3), "qps": round(a.nq / ms * 1e3, 1)})
     store.k_factor = a.k_factor
     best = max((r for r in sweep if r["recall_at_k"] >= 0.8), key=lambda r: r["qps"], default=None)
+    best_tie = max((r for r in sweep if r["recall_at_k_tie_aware"] >= 0.8), key=lambda r: r["qps"], default=None)
+    # how tied the exact neighbours are: exact top-k distance spread relative to the 1st
+    spread = float(((De[:, a.k - 1] - De[:, 0]) / De[:, 0].clamp_min(1e-12)).median())
     out = {"metric": "ivfpq_indexer_recall_qps",
            "config": f"INDEX_TYPE=ivfpq IVF{a.nlist},PQ{a.M}+refine n={store.ntotal} d={store.d} k={a.k}",
            "data": "bge-base (random-init) embeddings of synthetic clinical-note chunks via SemanticIndexer",
            "build_s": round(build_s, 1), "chunks_per_sec": round(store.ntotal / build_s, 1),
-           "batch": a.nq, "sweep": sweep, "fastest_at_recall_0.8": best}
+           "batch": a.nq, "exact_top_k_rel_spread_median": round(spread, 6), "sweep": sweep,
+           "fastest_at_recall_0.8": best, "fastest_at_tie_aware_recall_0.8": best_tie}
     print(json.dumps(out), flush=True)
 
 

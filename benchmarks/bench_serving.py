@@ -79,7 +79,9 @@ def run_launch(a, mode: str) -> list[dict]:
     work = tempfile.mkdtemp(prefix="docqa_serving_bench_")   # fresh index / documents DB per run
     env = dict(os.environ, INDEX_DIR=work, DATABASE_URL=f"sqlite:///{work}/documents.db", UPLOAD_DIR=work,
                MAX_NEW_TOKENS=str(a.max_new_tokens), MAX_BATCH=str(a.max_batch), DOCQA_SERVING=mode,
-               TEMPERATURE="0", HSA_ENABLE_IPC_MODE_LEGACY="0")
+               TEMPERATURE="0", HSA_ENABLE_IPC_MODE_LEGACY="0",
+               # the server log must survive a crash of the service (no block-buffered stdout)
+               PYTHONUNBUFFERED="1", PYTHONFAULTHANDLER="1")
     env.setdefault("PYTHONPATH", str(ROOT))
     cmd = [sys.executable, "-m", "docqa_amd.services.launch", "--services", "indexer,qa",
            "--llm", a.llm, "--device", a.device, "--port-offset", str(a.port_offset),
@@ -116,25 +118,36 @@ def run_launch(a, mode: str) -> list[dict]:
             results = []
             for ri, rate in enumerate(a.rates):
                 batch_q = qs[a.warmup + ri * a.requests:a.warmup + (ri + 1) * a.requests]
-                lat, errors = [], 0
+                lat, errors, empty, retried = [], 0, 0, 0
                 c0 = _engine_counters((await cl.get(murl)).text)
                 t0 = time.perf_counter()
 
                 async def one(at: float, q: str):
-                    nonlocal errors
+                    nonlocal errors, empty, retried
                     delay = t0 + at - time.perf_counter()
                     if delay > 0:
                         await asyncio.sleep(delay)
                     ts = time.perf_counter()
-                    r = await cl.post(url, json={"question": q})
-                    if r.status_code != 200 or not r.json().get("answer"):
+                    for attempt in range(2):
+                        try:
+                            r = await cl.post(url, json={"question": q})
+                            break
+                        except (httpx.ReadError, httpx.RemoteProtocolError):
+                            # a pooled keep-alive connection the server closed as it was reused
+                            if attempt:
+                                raise
+                            retried += 1
+                    if r.status_code != 200:
                         errors += 1
+                    elif not r.json().get("answer"):
+                        empty += 1       # greedy random-init model: EOS as the first token
                     lat.append(time.perf_counter() - ts)
 
                 await asyncio.gather(*[one(at, q) for at, q in zip(_arrivals(a.requests, rate), batch_q)])
                 wall = time.perf_counter() - t0
                 c1 = _engine_counters((await cl.get(murl)).text)
                 results.append({"rate": rate, "lat": lat, "wall": wall, "errors": errors,
+                                "empty_answers": empty, "retried_connections": retried,
                                 "engine": {k: int(c1[k] - c0.get(k, 0)) for k in c1}})
             return results
 
@@ -154,6 +167,7 @@ def run_launch(a, mode: str) -> list[dict]:
     return [{"metric": "serving_qa_queries_per_sec", "entry": "services.launch (HTTP POST /ask/)",
              "mode": mode, "offered_rate": res["rate"], "value": round(a.requests / res["wall"], 2),
              "unit": "queries/s", **_pcts(res["lat"]), "errors": res["errors"],
+             "empty_answers": res["empty_answers"], "retried_connections": res["retried_connections"],
              "requests": a.requests, "max_new_tokens": a.max_new_tokens, "max_batch": a.max_batch,
              "gpus": a.gpus, "tp": a.tp, "llm": "tiny" if a.tiny else a.llm, "notes": a.notes,
              "questions": a.questions, "dtype": "bf16" if a.device != "cpu" else "fp32",

@@ -14,6 +14,7 @@ RAM.  Only safetensors are read -- no pickle-based formats.
 from __future__ import annotations
 
 import json
+import os
 from collections.abc import Mapping
 from pathlib import Path
 
@@ -143,10 +144,16 @@ def resolve_llama_config(name_or_path) -> LlamaConfig:
 
 
 def resolve_llama(name_or_path, device="cuda", seed: int = 0) -> LlamaModel:
-    """A checkpoint directory -> its weights; a preset name -> random-init weights."""
+    """A checkpoint directory -> its weights; a preset name -> random-init weights.
+    ``DOCQA_LLM_DTYPE`` (bfloat16 | float32; default bfloat16): the weight / KV dtype --
+    float32 for CPU rehearsals that compare TP = N against TP = 1 token for token (bf16
+    rounds each TP split's sums differently, which flips near-tied greedy picks of a
+    random-init model)."""
+    dtype = {"bfloat16": torch.bfloat16, "bf16": torch.bfloat16, "float32": torch.float32,
+             "fp32": torch.float32}[os.environ.get("DOCQA_LLM_DTYPE", "bfloat16")]
     if is_checkpoint(name_or_path):
-        return load_llama(name_or_path, device=device)
-    return LlamaModel(LlamaConfig.preset(str(name_or_path)), device=device, seed=seed)
+        return load_llama(name_or_path, device=device, dtype=dtype)
+    return LlamaModel(LlamaConfig.preset(str(name_or_path)), device=device, dtype=dtype, seed=seed)
 
 
 # --------------------------------------------------------------------------- BERT

@@ -298,6 +298,12 @@ class LlamaModel:
             glu = (lambda a, w: ops.mgemm_glu(a, w, cg)) if Sg else ops.glu_linear
         else:
             glu = ops.prefill_glu
+        if self.tp > 1 and not x.is_cuda:
+            # CPU TP rehearsal: row-parallel partials as fp32 slabs, all-reduced before the one
+            # bf16 rounding (comm.tp_add_rmsnorm), so TP = N tracks TP = 1's rounding
+            for k in ("o", "down"):
+                if not plans.get(k, (0, None))[0]:
+                    plans[k] = (1, lambda a, w: F.linear(a.float(), w.float())[None])
         sq, qkv_part = plans.get("qkv", (0, None))
         so, o_part = plans.get("o", (0, None))
         sd, down_part = plans.get("down", (0, None))

@@ -165,9 +165,11 @@ def tp_add_rmsnorm(x: torch.Tensor, residual: torch.Tensor, w: torch.Tensor, eps
         return ops.add_rmsnorm_splitk(x, residual, w, eps) if slabs else ops.add_rmsnorm(x, residual, w, eps)
     if _CUSTOM_AR is not None and _CUSTOM_AR.supports(x):
         return _CUSTOM_AR.reduce_add_rmsnorm(x, residual, w, eps)
-    y = x.sum(0).to(residual.dtype) if slabs else x.contiguous()
+    # fp32 slabs are summed across the group in fp32 and rounded once, as the TP = 1 GEMM
+    # rounds its fp32 accumulator once (rounding each rank's partial first flips bf16 ties)
+    y = x.sum(0) if slabs else x.contiguous()
     dist.all_reduce(y, group=s.tp_group)
-    return ops.add_rmsnorm(y, residual, w, eps)
+    return ops.add_rmsnorm(y.to(residual.dtype), residual, w, eps)
 
 
 def tp_argmax(vals: torch.Tensor, ids: torch.Tensor) -> torch.Tensor:

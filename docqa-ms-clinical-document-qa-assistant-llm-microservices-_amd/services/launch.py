@@ -39,7 +39,10 @@ from .stack import DocQAStack, StackOptions
 
 
 def serve(app, port: int, host: str) -> threading.Thread:
-    cfg = uvicorn.Config(app, host=host, port=port, log_level="warning")
+    # keep-alive longer than a client's idle gap between bursts: at uvicorn's 5 s default the
+    # server closes pooled connections just as a Poisson client reuses them (ReadError)
+    cfg = uvicorn.Config(app, host=host, port=port, log_level="warning", timeout_keep_alive=75,
+                         backlog=4096)
     server = uvicorn.Server(cfg)
     t = threading.Thread(target=server.run, name=f"uvicorn-{port}", daemon=True)
     t.start()

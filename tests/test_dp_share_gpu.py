@@ -1,0 +1,41 @@
+"""The data-parallel headline path on GPU kernels, rehearsed on the one-GPU box: bench.py
+under torchrun with two ranks that both bind cuda:0 (``--share-gpu``, gloo process group).
+Each rank holds a full generator replica and one shard of the flat index; the sharded kNN
+all-gathers every rank's top-k, the timing bracket is barrier + synchronize on both sides
+and the MAX over ranks -- the same code the driver's 8-GPU scaling run executes with one
+GPU per rank over RCCL."""
+import json
+import os
+import socket
+import subprocess
+import sys
+from pathlib import Path
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+ROOT = Path(__file__).resolve().parents[1]
+
+
+def _port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def test_bench_dp2_shared_gpu():
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0")
+    for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK"):
+        env.pop(k, None)
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", str(_port()), str(ROOT / "bench.py"),
+           "--gpus", "2", "--share-gpu", "--llm", "llama3-1b-test", "--batch", "16", "--max-new-tokens", "8",
+           "--steps", "2", "--warmup", "1", "--notes", "200", "--kv-mem-fraction", "0.02"]
+    r = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=300, env=env)
+    assert r.returncode == 0, (r.stdout[-2000:], r.stderr[-4000:])
+    out = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])
+    assert out["n_gpus"] == 2 and out["config"]["parallelism"] == "dp2"
+    assert out["config"]["global_batch"] == 32 and out["value"] > 0
+    assert out["workload"]["unique_question_frac"] == 1.0

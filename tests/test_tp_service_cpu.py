@@ -35,7 +35,10 @@ def _serve_and_ask(tmp: Path, extra: list[str]) -> list[dict]:
     tmp.mkdir(parents=True, exist_ok=True)
     off = _offset()
     env = dict(os.environ, INDEX_DIR=str(tmp), DATABASE_URL=f"sqlite:///{tmp / 'docs.db'}",
-               UPLOAD_DIR=str(tmp / "up"), MAX_NEW_TOKENS="12", MAX_BATCH="8", OMP_NUM_THREADS="2")
+               UPLOAD_DIR=str(tmp / "up"), MAX_NEW_TOKENS="12", MAX_BATCH="8", OMP_NUM_THREADS="2",
+               # fp32 weights: TP = 2 sums its row-parallel partials in another order than
+               # TP = 1, which in bf16 flips near-tied greedy picks of the random tiny model
+               DOCQA_LLM_DTYPE="float32")
     for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
         env.pop(k, None)
     log = open(tmp / "server.log", "w")
