@@ -41,6 +41,8 @@ def main():
     ap.add_argument("--iters", type=int, default=10)
     ap.add_argument("--data", default="lowrank", choices=["lowrank", "mixture", "bge"])
     ap.add_argument("--k-factor", type=int, default=4)
+    ap.add_argument("--rotation", choices=("pca", "none"), default="pca",
+                    help="PQ pre-rotation (index/ivfpq.py pca_rotation; FAISS IndexPreTransform)")
     a = ap.parse_args()
     if a.data == "bge":
         return bench_bge_indexer(a)
@@ -87,7 +89,7 @@ def main():
           if a.data == "lowrank" else anchor + scale * qe).contiguous()
 
     t = time.perf_counter()
-    idx = IVFPQIndex(a.d, a.nlist, a.M, device=dev)
+    idx = IVFPQIndex(a.d, a.nlist, a.M, device=dev, rotation=a.rotation)
     idx.train(xb, niter=10)
     torch.cuda.synchronize()
     train_s = time.perf_counter() - t
@@ -131,6 +133,7 @@ def main():
     torch.cuda.synchronize()
     refine_ms = (time.perf_counter() - t) / a.iters * 1e3
     out = {"metric": "ivfpq_search_qps", "config": f"IVF{a.nlist},PQ{a.M} n={a.n} d={a.d} nprobe={a.nprobe} k={a.k}",
+           "rotation": a.rotation,
            "data": a.data,
            "search": res, "recall_at_k": round(recall, 4), "recall_1_at_1": round(r1, 4),
            "refine_flat_k_factor3": {"recall_at_k": round(recall_r, 4), "ms_per_batch": round(refine_ms, 3),
@@ -160,7 +163,8 @@ def bench_bge_indexer(a):
 
     assert ops.load_native()
     os.environ.update({"INDEX_TYPE": "ivfpq", "IVF_NLIST": str(a.nlist), "PQ_M": str(a.M),
-                       "IVF_NPROBE": str(a.nprobe), "REFINE_K_FACTOR": str(a.k_factor), "INDEX_WAL": "false"})
+                       "IVF_NPROBE": str(a.nprobe), "REFINE_K_FACTOR": str(a.k_factor), "INDEX_WAL": "false",
+                       "PQ_ROTATION": a.rotation})
     st = Settings()
     st.index_dir = tempfile.mkdtemp(prefix="ivf_bge_")
     enc = BertEncoder(BertConfig.preset("bge-base"), device="cuda")
@@ -220,7 +224,8 @@ def bench_bge_indexer(a):
     # how tied the exact neighbours are: exact top-k distance spread relative to the 1st
     spread = float(((De[:, a.k - 1] - De[:, 0]) / De[:, 0].clamp_min(1e-12)).median())
     out = {"metric": "ivfpq_indexer_recall_qps",
-           "config": f"INDEX_TYPE=ivfpq IVF{a.nlist},PQ{a.M}+refine n={store.ntotal} d={store.d} k={a.k}",
+           "config": f"INDEX_TYPE=ivfpq {'PCAR,' if a.rotation == 'pca' else ''}IVF{a.nlist},PQ{a.M}+refine "
+                     f"n={store.ntotal} d={store.d} k={a.k}",
            "data": "bge-base (random-init) embeddings of synthetic clinical-note chunks via SemanticIndexer",
            "build_s": round(build_s, 1), "chunks_per_sec": round(store.ntotal / build_s, 1),
            "batch": a.nq, "exact_top_k_rel_spread_median": round(spread, 6), "sweep": sweep,

@@ -111,6 +111,9 @@ def run_launch(a, mode: str) -> list[dict]:
                     pass
                 if time.perf_counter() > t_dead:
                     raise TimeoutError("service did not become ready")
+                waited = a.start_timeout - (t_dead - time.perf_counter())
+                if int(waited) % 30 == 0:
+                    print(f"[bench_serving] waiting for the service ({waited:.0f} s)", file=sys.stderr, flush=True)
                 await asyncio.sleep(1.0)
             # warm-up: graph capture / prefix cache of the fixed prompt text
             rs = await asyncio.gather(*[cl.post(url, json={"question": q}) for q in qs[1:a.warmup]])
@@ -143,7 +146,20 @@ def run_launch(a, mode: str) -> list[dict]:
                         empty += 1       # greedy random-init model: EOS as the first token
                     lat.append(time.perf_counter() - ts)
 
-                await asyncio.gather(*[one(at, q) for at, q in zip(_arrivals(a.requests, rate), batch_q)])
+                async def progress():
+                    # a line every 15 s: a live run is visibly alive (and a wedged one visibly stuck)
+                    while True:
+                        await asyncio.sleep(15.0)
+                        print(f"[bench_serving] rate {rate}: {len(lat)}/{a.requests} done, errors {errors}, "
+                              f"{time.perf_counter() - t0:.0f} s", file=sys.stderr, flush=True)
+
+                pt = asyncio.create_task(progress())
+                try:
+                    await asyncio.wait_for(
+                        asyncio.gather(*[one(at, q) for at, q in zip(_arrivals(a.requests, rate), batch_q)]),
+                        timeout=a.run_timeout)
+                finally:
+                    pt.cancel()
                 wall = time.perf_counter() - t0
                 c1 = _engine_counters((await cl.get(murl)).text)
                 results.append({"rate": rate, "lat": lat, "wall": wall, "errors": errors,
@@ -194,6 +210,7 @@ def main():
     ap.add_argument("--port-offset", type=int, default=20000)
     ap.add_argument("--kv-mem-fraction", type=float, default=0.8)
     ap.add_argument("--start-timeout", type=float, default=900.0)
+    ap.add_argument("--run-timeout", type=float, default=600.0, help="launch entry: seconds per offered rate")
     ap.add_argument("--tiny", action="store_true", help="tiny random models (CPU functional run)")
     ap.add_argument("--server-log", default="", help="file for the launcher's output")
     a = ap.parse_args()

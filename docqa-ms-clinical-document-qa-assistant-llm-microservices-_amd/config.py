@@ -64,7 +64,12 @@ class Settings:
     ivf_nlist: int = field(default_factory=lambda: env_int("IVF_NLIST", 1024))
     pq_m: int = field(default_factory=lambda: env_int("PQ_M", 0))                 # 0: d / 8
     ivf_nprobe: int = field(default_factory=lambda: env_int("IVF_NPROBE", 32))
-    refine_k_factor: int = field(default_factory=lambda: env_int("REFINE_K_FACTOR", 4))
+    # exact re-rank of min(64, k x REFINE_K_FACTOR) IVF-PQ candidates (k = 3 for the QA
+    # retriever: 48 candidates)
+    refine_k_factor: int = field(default_factory=lambda: env_int("REFINE_K_FACTOR", 16))
+    # orthogonal PQ pre-rotation: pca (principal directions dealt round-robin to the
+    # sub-quantizers; FAISS IndexPreTransform) | none
+    pq_rotation: str = field(default_factory=lambda: os.environ.get("PQ_ROTATION", "pca"))
     ivf_train_min: int = field(default_factory=lambda: env_int("IVF_TRAIN_MIN", 0))  # 0: 39 x nlist
     embed_model: str = field(default_factory=lambda: os.getenv("EMBED_MODEL", "minilm-l6"))
     # llm-qa

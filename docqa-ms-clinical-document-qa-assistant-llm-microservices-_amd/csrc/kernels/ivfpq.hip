@@ -92,26 +92,11 @@ __global__ __launch_bounds__(256) void ivfpq_scan_kernel(
       if (dist < td[K - 1]) topk_insert<K>(td, ti, dist, (int)i);
     }
   }
-  // block merge through LDS (reuse the LUT region)
+  // block top-K of the 256 lane lists (threshold select; LUT region reused)
   __syncthreads();
   float* sd = smem;
-  int* si = reinterpret_cast<int*>(smem + 256 * K);
-#pragma unroll
-  for (int k = 0; k < K; ++k) { sd[tid * K + k] = td[k]; si[tid * K + k] = ti[k]; }
-  __syncthreads();
-  for (int stride = 128; stride > 0; stride >>= 1) {
-    if (tid < stride) {
-      const int o = tid + stride;
-#pragma unroll
-      for (int k = 0; k < K; ++k) {
-        const float v = sd[o * K + k];
-        if (v < td[K - 1]) topk_insert<K>(td, ti, v, si[o * K + k]);
-      }
-#pragma unroll
-      for (int k = 0; k < K; ++k) { sd[tid * K + k] = td[k]; si[tid * K + k] = ti[k]; }
-    }
-    __syncthreads();
-  }
+  int* si = reinterpret_cast<int*>(smem + K);
+  block_select_topk<K, 256>(td, ti, sd, si, reinterpret_cast<unsigned char*>(smem + 2 * K));
   if (tid < K) { ws_d[ob + tid] = sd[tid]; ws_i[ob + tid] = si[tid]; }
 }
 
@@ -160,7 +145,7 @@ static int launch_scan(const float* xq, const float* cent, const float* pq, cons
                        int M, float* ws_d, int* ws_i, hipStream_t s) {
   const int dsub = d / M;
   size_t lds = (size_t)(M * 256 + d) * 4;
-  const size_t merge = (size_t)256 * K * 8;
+  const size_t merge = (size_t)K * 8 + topk_select_lds(K);
   if (merge > lds) lds = merge;
   if (lds > 160 * 1024) return -2;
   const int items = nq * nprobe;

@@ -512,7 +512,11 @@ class LLMEngine:
                 if self._pool is None:
                     self._pool = torch.cuda.graph_pool_handle()
                 pool = self._pool
-            with torch.cuda.graph(graph, pool=pool):
+            # thread_local: the serving front end keeps embedding / searching / syncing on
+            # its prep thread while the scheduler thread captures a new bucket lazily; in the
+            # default global mode any sync on ANY thread invalidates the capture (and fails
+            # that thread's op: hipErrorStreamCaptureUnsupported)
+            with torch.cuda.graph(graph, pool=pool, capture_error_mode="thread_local"):
                 self._step_body(g)
         finally:
             if tune and tunable is not None:

@@ -134,6 +134,10 @@ def read_index_from(r: Reader) -> object:
         from .ivfpq import read_ivfpq_body
 
         return read_ivfpq_body(r)
+    if fourcc == b"IxPT":
+        from .ivfpq import read_pretransform_body
+
+        return read_pretransform_body(r)
     if fourcc == b"IxRF":
         # faiss index_write.cpp IndexRefine: header, base index, refine index, k_factor
         read_header(r)

@@ -29,7 +29,8 @@ from .refine import RefineFlat
 
 class IVFPQRefineIndex:
     def __init__(self, d: int, nlist: int = 1024, M: int = 0, nprobe: int = 32, k_factor: int = 4,
-                 train_min: int = 0, device="cuda", storage_dtype=torch.float32, seed: int = 0):
+                 train_min: int = 0, device="cuda", storage_dtype=torch.float32, seed: int = 0,
+                 rotation: str = "pca"):
         self.d = d
         self.metric = "l2"
         self.nlist = nlist
@@ -40,6 +41,7 @@ class IVFPQRefineIndex:
         self.k_factor = k_factor
         self.train_min = train_min or 39 * nlist
         self.seed = seed
+        self.rotation = rotation          # PQ pre-rotation (ivfpq.pca_rotation) or "none"
         self.device = torch.device(device)
         self.flat = FlatIndex(d, "l2", device, storage_dtype)
         self.ivf: IVFPQIndex | None = None
@@ -71,7 +73,7 @@ class IVFPQRefineIndex:
             x_tr = x.index_select(0, torch.randperm(n, generator=g)[:cap].to(x.device))
         else:
             x_tr = x
-        ivf = IVFPQIndex(self.d, self.nlist, self.M, 8, device=self.device)
+        ivf = IVFPQIndex(self.d, self.nlist, self.M, 8, device=self.device, rotation=self.rotation)
         ivf.nprobe = self.nprobe
         ivf.train(x_tr, seed=self.seed)
         ivf.add(x, ids=torch.arange(n, dtype=torch.long))
@@ -140,8 +142,8 @@ class IVFPQRefineIndex:
         if isinstance(data, faiss_io.RefineIndexData):
             base = data.base
             idx = cls(data.d, nlist=base.nlist, M=base.M, nprobe=base.nprobe,
-                      k_factor=max(1, int(round(data.k_factor))), device=device,
-                      **{k: v for k, v in kw.items() if k not in ("nlist", "M", "nprobe", "k_factor")})
+                      k_factor=max(1, int(round(data.k_factor))), device=device, rotation=base.rotation,
+                      **{k: v for k, v in kw.items() if k not in ("nlist", "M", "nprobe", "k_factor", "rotation")})
             idx.replace(torch.from_numpy(data.refine.xb), ivf=base)
             return idx
         if not isinstance(data, faiss_io.FlatIndexData):
@@ -161,7 +163,7 @@ def make_index(settings, d: int, device) -> object:
     if settings.index_type == "ivfpq":
         return IVFPQRefineIndex(d, nlist=settings.ivf_nlist, M=settings.pq_m, nprobe=settings.ivf_nprobe,
                                 k_factor=settings.refine_k_factor, train_min=settings.ivf_train_min,
-                                device=device)
+                                device=device, rotation=settings.pq_rotation)
     if settings.index_type != "flat":
         raise ValueError(f"INDEX_TYPE must be flat or ivfpq, got {settings.index_type!r}")
     return FlatIndex(d, "l2", device)
@@ -174,7 +176,7 @@ def load_index(settings, path, device) -> object:
     if settings.index_type == "ivfpq":
         return IVFPQRefineIndex.from_data(data, device=device, nlist=settings.ivf_nlist, M=settings.pq_m,
                                           nprobe=settings.ivf_nprobe, k_factor=settings.refine_k_factor,
-                                          train_min=settings.ivf_train_min)
+                                          train_min=settings.ivf_train_min, rotation=settings.pq_rotation)
     if isinstance(data, faiss_io.RefineIndexData):
         data = data.refine                           # an IVF snapshot read as exact flat
     idx = FlatIndex(data.d, "l2", device, capacity=max(1024, data.ntotal))

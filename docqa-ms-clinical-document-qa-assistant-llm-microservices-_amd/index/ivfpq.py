@@ -29,16 +29,39 @@ from . import faiss_io
 from .kmeans import assign, kmeans, kmeans_subspaces
 
 
+def pca_rotation(x: torch.Tensor, M: int) -> torch.Tensor:
+    """Orthogonal [d, d] pre-rotation for PQ (applied as x @ R): the principal directions of
+    ``x``, dealt to the M sub-quantizers round-robin (PCA direction r -> sub-space r % M), so
+    each sub-space gets an equal share of the variance.  L2 distances are unchanged; the
+    codebooks stop spending most of their bits on the handful of sub-spaces that would
+    otherwise hold the dominant directions (random-init sentence embeddings: one direction
+    carries ~40 % of the variance; recall@10 0.78 -> 0.93 at nprobe 64 with exact refine,
+    profiles/r3_ivfpq_rotation_probe.log)."""
+    x = x.double()
+    xc = x - x.mean(0, keepdim=True)
+    cov = xc.t() @ xc / max(1, x.shape[0] - 1)
+    _, vec = torch.linalg.eigh(cov)                        # ascending eigenvalues
+    vec = vec.flip(1)
+    d = x.shape[1]
+    order = torch.tensor([r for j in range(M) for r in range(j, d, M)], device=vec.device)
+    return vec[:, order].float().contiguous()
+
+
 class IVFPQIndex:
-    def __init__(self, d: int, nlist: int, M: int, nbits: int = 8, device="cuda"):
+    def __init__(self, d: int, nlist: int, M: int, nbits: int = 8, device="cuda", rotation: str = "none"):
         if nbits != 8:
             raise ValueError("only 8-bit PQ codes are supported")
         if d % M:
             raise ValueError("d must be divisible by M")
+        if rotation not in ("none", "pca"):
+            raise ValueError(f"unknown PQ pre-rotation {rotation!r}")
         self.d, self.nlist, self.M = d, nlist, M
         self.dsub = d // M
         self.device = torch.device(device)
         self.nprobe = 16
+        self.rotation = rotation
+        # orthogonal pre-transform R [d, d] (x -> x @ R), FAISS IndexPreTransform(LinearTransform)
+        self.rot: torch.Tensor | None = None
         self.centroids: torch.Tensor | None = None
         self.pq: torch.Tensor | None = None
         self.codes = torch.empty(0, M, dtype=torch.uint8, device=self.device)
@@ -51,8 +74,16 @@ class IVFPQIndex:
         return self.centroids is not None and self.pq is not None
 
     # ------------------------------------------------------------------ build
+    def _in(self, x) -> torch.Tensor:
+        """Vectors into the index's (rotated) space."""
+        x = torch.as_tensor(x).to(self.device, torch.float32)
+        return x @ self.rot if self.rot is not None else x
+
     def train(self, x, niter: int = 20, seed: int = 0) -> None:
         x = torch.as_tensor(x).to(self.device, torch.float32)
+        if self.rotation == "pca":
+            self.rot = pca_rotation(x, self.M).to(self.device)
+            x = x @ self.rot
         self.centroids = kmeans(x, self.nlist, niter, seed)
         _, a = assign(x, self.centroids)
         resid = x - self.centroids.index_select(0, a)
@@ -75,7 +106,7 @@ class IVFPQIndex:
         ids = torch.as_tensor(ids, dtype=torch.long).to(self.device)
         new_codes, new_lists = [], []
         for i in range(0, n, batch):
-            xb = x[i:i + batch].to(self.device, torch.float32)
+            xb = self._in(x[i:i + batch])
             _, a = assign(xb, self.centroids)
             new_codes.append(self.encode(xb, a))
             new_lists.append(a)
@@ -100,7 +131,7 @@ class IVFPQIndex:
     # ------------------------------------------------------------------ search
     def search(self, xq, k: int, nprobe: int | None = None):
         nprobe = min(nprobe or self.nprobe, self.nlist)
-        xq = torch.as_tensor(xq).to(self.device, torch.float32).contiguous()
+        xq = self._in(xq).contiguous()
         cn = (self.centroids ** 2).sum(1)
         if nprobe <= 64:
             _, probes = ops.knn(self.centroids, cn, xq, nprobe, False, 0)
@@ -136,6 +167,25 @@ class IVFPQIndex:
 
     # ------------------------------------------------------------------ FAISS IO
     def to_bytes(self) -> bytes:
+        """FAISS bytes: ``IvPQ``, wrapped as IndexPreTransform(LinearTransform) -- ``IxPT`` +
+        ``LTra`` with A = R^T, no bias -- when the index has a pre-rotation (faiss
+        index_write.cpp write_VectorTransform layout)."""
+        body = self._ivfpq_bytes()
+        if self.rot is None:
+            return body
+        w = io.BytesIO()
+        w.write(b"IxPT")
+        faiss_io.write_header(w, self.d, self.ntotal, True, faiss_io.METRIC_L2)
+        w.write(struct.pack("<i", 1))                        # chain length
+        w.write(b"LTra")
+        w.write(struct.pack("<B", 0))                        # have_bias
+        faiss_io.write_vector(w, self.rot.t().contiguous().float().cpu().numpy().reshape(-1))   # A [d_out, d_in]
+        faiss_io.write_vector(w, np.zeros(0, dtype=np.float32))                                # b
+        w.write(struct.pack("<iiB", self.d, self.d, 1))     # d_in, d_out, is_trained
+        w.write(body)
+        return w.getvalue()
+
+    def _ivfpq_bytes(self) -> bytes:
         w = io.BytesIO()
         w.write(b"IvPQ")
         faiss_io.write_header(w, self.d, self.ntotal, True, faiss_io.METRIC_L2)
@@ -174,7 +224,7 @@ class IVFPQIndex:
 
     def to(self, device) -> "IVFPQIndex":
         self.device = torch.device(device)
-        for name in ("centroids", "pq", "codes", "ids", "list_off"):
+        for name in ("rot", "centroids", "pq", "codes", "ids", "list_off"):
             t = getattr(self, name)
             if t is not None:
                 setattr(self, name, t.to(self.device))
@@ -225,3 +275,32 @@ def read_ivfpq_body(r: faiss_io.Reader) -> IVFPQIndex:
     idx.list_off = torch.from_numpy(off)
     idx.ntotal = int(ntotal)
     return idx
+
+
+def read_pretransform_body(r: faiss_io.Reader) -> IVFPQIndex:
+    """``IxPT`` (IndexPreTransform) with one orthogonal ``LTra`` (no bias) over an IVF-PQ:
+    the rotation becomes the index's pre-rotation R = A^T."""
+    read_header = faiss_io.read_header
+    d, _, _, _, _ = read_header(r)
+    nt, = r.unpack("<i")
+    if nt != 1:
+        raise ValueError("IxPT: one linear transform supported")
+    kind = r.read(4)
+    if kind not in (b"LTra", b"Pcam", b"rrot"):
+        raise ValueError(f"IxPT: unsupported vector transform {kind!r}")
+    if kind == b"Pcam":
+        raise ValueError("IxPT: PCAMatrix transforms are not supported")
+    have_bias, = r.unpack("<B")
+    A = r.vector(np.float32)
+    b = r.vector(np.float32)
+    d_in, d_out, _ = r.unpack("<iiB")
+    if have_bias and b.size and np.any(b != 0):
+        raise ValueError("IxPT: a biased linear transform is not supported")
+    if d_in != d_out or A.size != d_in * d_out:
+        raise ValueError("IxPT: only square (rotation) transforms are supported")
+    sub = faiss_io.read_index_from(r)
+    if not isinstance(sub, IVFPQIndex):
+        raise ValueError("IxPT: only an IVF-PQ sub-index is supported")
+    sub.rotation = "pca"
+    sub.rot = torch.from_numpy(A.reshape(d_out, d_in).T.copy())
+    return sub

@@ -153,24 +153,29 @@ class ShardedIVFPQIndex(ShardedIndex):
 
     @classmethod
     def build(cls, local_x, d: int, nlist: int, M: int, train_sample=None, device="cuda", group=None,
-              replicated: bool = False, niter: int = 20, seed: int = 0, max_queries: int | None = None):
+              replicated: bool = False, niter: int = 20, seed: int = 0, max_queries: int | None = None,
+              rotation: str = "none"):
         from .ivfpq import IVFPQIndex
 
         s = comm.state()
         group = group if group is not None else s.dp_group
         rank = dist.get_rank(group) if group is not None else 0
-        ivf = IVFPQIndex(d, nlist, M, 8, device=device)
+        ivf = IVFPQIndex(d, nlist, M, 8, device=device, rotation=rotation)
         if rank == 0:
             ivf.train(train_sample, niter=niter, seed=seed)
             cent, pq = ivf.centroids.contiguous(), ivf.pq.contiguous()
+            rot = ivf.rot.contiguous() if ivf.rot is not None else None
         else:
             cent = torch.empty(nlist, d, device=device)
             pq = torch.empty(M, 256, d // M, device=device)
+            rot = torch.empty(d, d, device=device) if rotation != "none" else None
         if group is not None and dist.get_world_size(group) > 1:
             src = dist.get_global_rank(group, 0)
             dist.broadcast(cent, src=src, group=group)
             dist.broadcast(pq, src=src, group=group)
-        ivf.centroids, ivf.pq = cent, pq
+            if rot is not None:         # one shared pre-rotation: every shard encodes alike
+                dist.broadcast(rot, src=src, group=group)
+        ivf.centroids, ivf.pq, ivf.rot = cent, pq, rot
         shard = _IVFShard(ivf)
         obj = cls(shard, group=group, replicated=replicated, max_queries=max_queries)
         # global ids: this shard's offset among the ranks' vector counts

@@ -200,7 +200,13 @@ class ContinuousBatcher:
             try:
                 eng.step()
             except Exception as e:  # noqa: BLE001
-                eng._fail_all(e)
+                import logging
+
+                logging.getLogger("llm-qa").error("engine step failed: %s: %s", type(e).__name__, e)
+                try:
+                    eng._fail_all(e)      # fails every running request's future first
+                except Exception as e2:  # noqa: BLE001 - the loop must survive to fail later requests
+                    logging.getLogger("llm-qa").error("engine reset failed: %s: %s", type(e2).__name__, e2)
                 _maybe_exit_on_device_error(e)
             m = self.metrics
             m.set("engine_steps", eng.steps)

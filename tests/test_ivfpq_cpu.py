@@ -70,3 +70,71 @@ def test_refine_flat_improves_recall_cpu():
     assert rec(Ir) >= rec(Ia) and rec(Ir) >= 0.8
     true_d = ((xb[Ir[:, 0]] - xq) ** 2).sum(-1)
     assert torch.allclose(Dr[:, 0], true_d, atol=1e-3)
+
+
+def _anisotropic(n=4000, d=64, seed=2, mix=False):
+    """A few dominant directions (as random-init sentence embeddings have), by default all
+    inside the first PQ sub-space's coordinates (mix: spread over random directions)."""
+    g = torch.Generator().manual_seed(seed)
+    scale = torch.ones(d)
+    scale[:3] = torch.tensor([12.0, 6.0, 3.0])
+    x = torch.randn(n, d, generator=g) * scale
+    if mix:
+        q, _ = torch.linalg.qr(torch.randn(d, d, generator=g))
+        x = x @ q.t()
+    return x
+
+
+def test_pca_rotation_orthogonal_and_balanced():
+    from docqa_amd.index.ivfpq import pca_rotation
+
+    x = _anisotropic(mix=True)
+    R = pca_rotation(x, 8)
+    torch.testing.assert_close(R.t() @ R, torch.eye(64), atol=1e-4, rtol=0)
+    # distances are unchanged by the rotation
+    a, b = x[:5], x[5:10]
+    torch.testing.assert_close(torch.cdist(a @ R, b @ R), torch.cdist(a, b), atol=1e-3, rtol=1e-4)
+    # the variance is dealt round-robin: the 3 dominant directions sit in 3 different sub-spaces
+    v = ((x - x.mean(0)) @ R).var(0).view(8, 8).sum(1)
+    assert int((v > v.median() * 1.5).sum()) == 3
+
+
+def test_pca_rotated_ivfpq_recall_and_faiss_roundtrip(tmp_path):
+    """PQ with the PCA pre-rotation ranks anisotropic data better than without, and the
+    index round-trips through FAISS's IndexPreTransform(LinearTransform) layout (IxPT/LTra),
+    also inside an IndexRefineFlat snapshot."""
+    from docqa_amd.index.hybrid import IVFPQRefineIndex
+
+    x = _anisotropic(n=4000, d=64)
+    q = x[:64] + 0.3 * torch.randn(64, 64, generator=torch.Generator().manual_seed(5))
+    f = FlatIndex(64, "l2", "cpu")
+    f.add(x)
+    _, It = f.search(q, 10)
+
+    def recall(idx):
+        _, I = idx.search(q, 10, nprobe=8)
+        return sum(len(set(I[i].tolist()) & set(It[i].tolist())) for i in range(64)) / 640
+
+    plain = IVFPQIndex(64, 16, 8, device="cpu")
+    plain.train(x, niter=6)
+    plain.add(x)
+    rot = IVFPQIndex(64, 16, 8, device="cpu", rotation="pca")
+    rot.train(x, niter=6)
+    rot.add(x)
+    assert rot.rot is not None and recall(rot) > recall(plain)
+    p = tmp_path / "r.ivfpq"
+    rot.save(p)
+    assert p.read_bytes()[:4] == b"IxPT"
+    back = faiss_io.read_index(p)
+    assert isinstance(back, IVFPQIndex) and back.rotation == "pca"
+    torch.testing.assert_close(back.rot, rot.rot)
+    assert torch.equal(back.search(q, 10, nprobe=8)[1], rot.search(q, 10, nprobe=8)[1])
+    # refine store snapshot: IxRF(IxPT(IvPQ), flat)
+    st = IVFPQRefineIndex(64, nlist=16, M=8, nprobe=8, k_factor=4, train_min=2000, device="cpu")
+    st.add(x)
+    assert st.trained and st.ivf.rot is not None
+    sp = tmp_path / "s.faiss"
+    st.save(sp)
+    st2 = IVFPQRefineIndex.load(sp, device="cpu")
+    assert st2.ivf.rotation == "pca"
+    assert torch.equal(st2.search(q, 10)[1], st.search(q, 10)[1])

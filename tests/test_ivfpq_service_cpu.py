@@ -6,6 +6,7 @@ over all vectors."""
 import os
 import socket
 
+import pytest
 import torch
 import torch.multiprocessing as mp
 
@@ -88,7 +89,7 @@ def _free_port():
     return p
 
 
-def _shard_worker(rank, world, port, path, out):
+def _shard_worker(rank, world, port, path, out, rotation="none"):
     os.environ.update({"RANK": str(rank), "WORLD_SIZE": str(world), "LOCAL_RANK": str(rank),
                        "MASTER_ADDR": "127.0.0.1", "MASTER_PORT": str(port)})
     torch.set_num_threads(1)
@@ -102,23 +103,26 @@ def _shard_worker(rank, world, port, path, out):
     n = xb.shape[0]
     lo, hi = n * rank // world, n * (rank + 1) // world
     sh = ShardedIVFPQIndex.build(xb[lo:hi], d=xb.shape[1], nlist=16, M=8, train_sample=xb[:2000] if rank == 0 else None,
-                                 device="cpu")
+                                 device="cpu", rotation=rotation)
     D, I = sh.search(xq[rank::world], 10, nprobe=8)
     torch.save({"D": D, "I": I}, f"{out}.{rank}")
     comm.destroy()
 
 
-def test_sharded_ivfpq_equals_single(tmp_path):
+@pytest.mark.parametrize("rotation", ["none", "pca"])
+def test_sharded_ivfpq_equals_single(tmp_path, rotation):
+    """Rank 0 trains the quantizers (and the PCA pre-rotation) and broadcasts them: every
+    shard encodes alike, so the merged search equals one index over all vectors."""
     from docqa_amd.index.ivfpq import IVFPQIndex
 
     xb, xq = _data(n=4000, nq=12, seed=3)
-    single = IVFPQIndex(32, 16, 8, device="cpu")
+    single = IVFPQIndex(32, 16, 8, device="cpu", rotation=rotation)
     single.train(xb[:2000])
     single.add(xb)
     path, out = tmp_path / "d.pt", tmp_path / "o"
     torch.save({"xb": xb, "xq": xq}, path)
-    mp.start_processes(_shard_worker, args=(2, _free_port(), str(path), str(out)), nprocs=2, join=True,
-                       start_method="spawn")
+    mp.start_processes(_shard_worker, args=(2, _free_port(), str(path), str(out), rotation), nprocs=2,
+                       join=True, start_method="spawn")
     for r in range(2):
         got = torch.load(f"{out}.{r}", weights_only=True)
         D, I = single.search(xq[r::2], 10, nprobe=8)
