@@ -95,13 +95,18 @@ def main():
         if cuda:
             torch.cuda.synchronize()
 
+    t_setup = time.perf_counter()
+
+    def note(msg: str) -> None:     # progress on stderr (rank 0): long TP rehearsals stay visibly alive
+        if ps.rank == 0:
+            print(f"[bench_pipeline] {msg} ({time.perf_counter() - t_setup:.0f} s)", file=sys.stderr, flush=True)
+
     def tmax(x: float) -> float:
         t = torch.tensor([x], dtype=torch.float64, device=dev)
         if dist.is_initialized():
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
         return float(t[0])
 
-    t_setup = time.perf_counter()
     enc_tok = WordPieceTokenizer()
     ner_tok = WordPieceTokenizer(max_len=256)
     encoder = ck.resolve_bert(a.embed, device=dev, seed=0)        # preset or checkpoint dir
@@ -114,6 +119,7 @@ def main():
     records = kb[ps.rank::ps.world_size]
     local.add(embed_records(encoder, enc_tok, records))
 
+    note("encoders and KB index ready")
     # ---------------------------------------------------------------- stage 1: ingest
     notes = synthetic_notes(a.notes, seed=11)
     mine = list(range(ps.rank, len(notes), ps.world_size))
@@ -154,8 +160,10 @@ def main():
     else:
         all_records, index = records, local
 
+    note(f"ingested {tot_chunks} chunks")
     # ---------------------------------------------------------------- stage 2: QA
     model = ck.resolve_llama(a.llm, device=dev, seed=0)
+    note(f"{a.llm} shard built (TP {tp})")
     llm_cfg = model.cfg
     engine = LLMEngine(model, max_batch=a.batch, max_context=a.max_context, use_graphs=cuda)
     chat_tok = ChatTokenizer(model_vocab=llm_cfg.vocab_size)
@@ -186,6 +194,7 @@ def main():
 
     run(list(range(a.warmup)))
     sync()
+    note("warm-up done")
     comm.barrier()
     sync()
     t0 = time.perf_counter()
