@@ -160,8 +160,11 @@ def run_parallel(a, opts: "StackOptions") -> None:
         model = ck.resolve_llama(opts.llm, device=opts.device)
         eng = LLMEngine(model, max_batch=opts.max_batch, max_context=opts.max_context, use_graphs=opts.use_graphs,
                         kv_mem_fraction=opts.kv_mem_fraction)
+        ce = ContinuousEngine(eng, max_running=st.max_batch, lockstep=ls)
+        if os.environ.get("DOCQA_WARM_BUCKETS", "1") == "1":
+            ce.warmup()        # the leader captures the same buckets in the same order (qa.py)
         print(f"[rank {ps.rank}] TP follower of group {ps.dp_rank} ready", flush=True)
-        ContinuousEngine(eng, max_running=st.max_batch, lockstep=ls).follow()
+        ce.follow()
         comm.destroy()
         return
     opts.qa_lockstep = ls

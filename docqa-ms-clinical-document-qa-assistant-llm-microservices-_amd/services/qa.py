@@ -22,6 +22,7 @@ from __future__ import annotations
 
 import asyncio
 import concurrent.futures as cf
+import os
 import queue
 import threading
 import time
@@ -134,6 +135,10 @@ class ContinuousBatcher:
         # lockstep: this process leads a tensor-parallel group whose other ranks mirror
         # every engine step (engine/scheduler.py Lockstep; services/launch.py --tp)
         self.engine = ContinuousEngine(pipeline.engine, max_running=settings.max_batch, lockstep=lockstep)
+        if os.environ.get("DOCQA_WARM_BUCKETS", "1") == "1":
+            # every decode bucket captured before the first request (the TP followers do
+            # the same before following, services/launch.py)
+            self.engine.warmup()
         self.q: queue.Queue = queue.Queue()
         self._stop = threading.Event()
         self._prep = threading.Thread(target=self._prep_loop, name="qa-prep", daemon=True)
