@@ -211,6 +211,11 @@ def main() -> None:
     import os
     import sys
 
+    # The HTTP front end (uvicorn thread), the QA prep thread and the engine's scheduler
+    # thread share one GIL; at CPython's 5 ms switch interval each request's few GIL hand-
+    # offs queue behind the scheduler's per-step Python, throttling admissions under load.
+    # DOCQA_GIL_SWITCH_MS (default 0.5) shortens the hand-off wait.
+    sys.setswitchinterval(float(os.environ.get("DOCQA_GIL_SWITCH_MS", "0.5")) / 1e3)
     under_torchrun = int(os.environ.get("WORLD_SIZE", "1")) > 1
     if a.gpus > 1 and not under_torchrun:
         if a.gpus % a.tp:

@@ -227,20 +227,27 @@ class ContinuousBatcher:
         asks = [it for it in items if it[0] == "ask"]
         sums = [it for it in items if it[0] == "summarize"]
         if asks:
+            tp0 = time.perf_counter()
             qs = [it[1] for it in asks]
             qemb = pipe.embed(qs)
             _, I = pipe.index.search(qemb, pipe.k)
             I = I.tolist()
             prompts = pipe.build_prompts(qs, I)
-            self.metrics.observe("ask_batch_size", len(asks))
+            te = time.perf_counter()
+            m = self.metrics
+            m.observe("ask_batch_size", len(asks))
+            m.observe("ask_prep_batch_s", te - tp0)          # embed + search + prompt assembly
             for (_, _, f, t0), ids, p in zip(asks, I, prompts):
+                m.observe("ask_queue_s", tp0 - t0)            # arrival -> its prep batch starts
                 srcs = [pipe.metadata[j].get("source") for j in ids if 0 <= j < len(pipe.metadata)]
 
                 def done(ef, f=f, t0=t0, srcs=srcs):
                     if ef.exception() is not None:
                         f.set_exception(ef.exception())
                         return
-                    self.metrics.observe("ask_latency_s", time.perf_counter() - t0)
+                    now = time.perf_counter()
+                    m.observe("ask_latency_s", now - t0)
+                    m.observe("ask_engine_s", now - te)      # engine admission + prefill + decode
                     f.set_result({"answer": pipe.chat_tok.decode(ef.result()), "sources": srcs})
 
                 self.engine.submit(p, params).add_done_callback(done)
