@@ -66,8 +66,12 @@ class KVCache:
         self.block_size = block_size
         self.num_blocks = num_blocks
         shape = (num_blocks, kv_heads, block_size, head_dim)
-        self.caches = [(torch.empty(shape, device=device, dtype=dtype),
-                        torch.empty(shape, device=device, dtype=dtype)) for _ in range(layers)]
+        # zeroed, not empty: the decode kernels stream whole 32-token tiles and mask the
+        # positions past a sequence's end with p = 0, but 0 x NaN is NaN -- a never-written
+        # slot holding a NaN bit pattern (whatever an earlier tensor of the process left
+        # there) would poison the row.  Stale finite K/V of a reused block is harmless.
+        self.caches = [(torch.zeros(shape, device=device, dtype=dtype),
+                        torch.zeros(shape, device=device, dtype=dtype)) for _ in range(layers)]
         self.allocator = make_allocator(num_blocks, block_size)
 
     @staticmethod

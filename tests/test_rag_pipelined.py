@@ -15,7 +15,12 @@ import torch
 def _stack(llm, device):
     from docqa_amd.pipeline.builder import StackConfig, build_stack
 
-    sc = StackConfig(llm=llm, n_notes=60, max_batch=8, max_context=2048)
+    # a KV pool far larger than the three batches: with a tight pool the pipelined loop,
+    # holding two batches while a third reserves, evicts cached prefixes at timing-
+    # dependent moments, and a prefix recomputed at another prefill length rounds
+    # differently (the sequential loop never holds more than one batch)
+    sc = StackConfig(llm=llm, n_notes=60, max_batch=8, max_context=2048,
+                     kv_mem_fraction=0.02 if device == "cuda" else None)
     pipe, _ = build_stack(sc, device=device, log=lambda *a: None)
     return pipe
 
