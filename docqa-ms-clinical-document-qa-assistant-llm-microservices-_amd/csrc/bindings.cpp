@@ -688,6 +688,58 @@ at::Tensor mgemm_glu(const at::Tensor& x, const at::Tensor& w, int64_t cfg) {
   return out;
 }
 
+// persistent decode-layer chain (TP = 1, 193..512 rows): attn [M, Ko] -> residual updated in
+// place twice, returns (x2 [M, H] = the next layer's normed input, the next layer's QKV
+// split-K slabs [S_q, M, Nq] or an empty tensor when w_qkv is None)
+std::tuple<at::Tensor, at::Tensor> mgemm_chain(const at::Tensor& attn, const at::Tensor& w_o, at::Tensor residual,
+                                               const at::Tensor& post_norm, const at::Tensor& w_gu,
+                                               const at::Tensor& w_down, const at::Tensor& next_norm,
+                                               const c10::optional<at::Tensor>& w_qkv, at::Tensor counters,
+                                               int64_t S_o, int64_t cfg_o, int64_t S_d, int64_t cfg_d, int64_t S_q,
+                                               int64_t cfg_q, double eps, const c10::optional<at::Tensor>& trace) {
+  for (const at::Tensor* t : {&attn, &w_o, (const at::Tensor*)&residual, &post_norm, &w_gu, &w_down, &next_norm}) {
+    CHECK_GPU(*t); CHECK_BF16(*t); CHECK_CONTIG(*t); CHECK_ALIGN16(*t);
+  }
+  CHECK_GPU(counters); CHECK_I32(counters); CHECK_CONTIG(counters);
+  TORCH_CHECK(counters.numel() >= 16, "mgemm_chain: counters need 16 int32");
+  const int Ko = attn.size(-1), M = attn.numel() / Ko, H = w_o.size(0), N2I = w_gu.size(0);
+  TORCH_CHECK(w_o.size(1) == Ko && residual.numel() == (int64_t)M * H && w_gu.size(1) == H &&
+              w_down.size(0) == H && w_down.size(1) == N2I / 2 && post_norm.numel() == H && next_norm.numel() == H,
+              "mgemm_chain: shape mismatch");
+  c10::DeviceGuard g(attn.device());
+  auto fo = attn.options().dtype(at::kFloat);
+  auto p_o = at::empty({S_o, M, H}, fo);
+  auto x1 = at::empty({M, H}, attn.options());
+  auto gl = at::empty({M, N2I / 2}, attn.options());
+  auto p_d = at::empty({S_d, M, H}, fo);
+  auto x2 = at::empty({M, H}, attn.options());
+  at::Tensor p_q;
+  const void* wq = nullptr;
+  int Nq = 0;
+  if (w_qkv.has_value()) {
+    const at::Tensor& w = *w_qkv;
+    CHECK_GPU(w); CHECK_BF16(w); CHECK_CONTIG(w); CHECK_ALIGN16(w);
+    TORCH_CHECK(w.size(1) == H, "mgemm_chain: w_qkv shape");
+    Nq = w.size(0);
+    wq = w.data_ptr();
+    p_q = at::empty({S_q, M, Nq}, fo);
+  } else {
+    p_q = at::empty({0}, fo);
+  }
+  if (trace.has_value())
+    TORCH_CHECK(trace->is_cuda() && trace->scalar_type() == at::kLong && trace->numel() >= 6 * 4096,
+                "mgemm_chain: trace needs int64 [>= 6 x 4096] on the GPU");
+  CHECK_RC(docqa_mgemm_chain(attn.data_ptr(), w_o.data_ptr(), p_o.data_ptr<float>(), residual.data_ptr(),
+                             post_norm.data_ptr(), x1.data_ptr(), w_gu.data_ptr(), gl.data_ptr(), w_down.data_ptr(),
+                             p_d.data_ptr<float>(), next_norm.data_ptr(), x2.data_ptr(), wq,
+                             wq ? p_q.data_ptr<float>() : nullptr, counters.data_ptr<int>(),
+                             trace.has_value() ? (long long*)trace->data_ptr<int64_t>() : nullptr, M, H, Ko, N2I, Nq,
+                             (int)S_o, (int)cfg_o, (int)S_d, (int)cfg_d, (int)S_q, (int)cfg_q, (float)eps,
+                             stream()),
+           "mgemm_chain");
+  return {x2, p_q};
+}
+
 // LM head + greedy pick: argmax over the first n_valid columns of bf16(x . w^T) -> int64 [M]
 at::Tensor mgemm_argmax(const at::Tensor& x, const at::Tensor& w, int64_t n_valid, int64_t cfg) {
   CHECK_GPU(x); CHECK_BF16(x); CHECK_BF16(w); CHECK_CONTIG(x); CHECK_CONTIG(w);
@@ -950,6 +1002,10 @@ TORCH_LIBRARY(docqa, m) {
   m.def("dgemm_glu(Tensor x, Tensor w) -> Tensor");
   m.def("mgemm(Tensor x, Tensor w, int splits, int cfg=0) -> Tensor");
   m.def("mgemm_glu(Tensor x, Tensor w, int cfg=0) -> Tensor");
+  m.def("mgemm_chain(Tensor attn, Tensor w_o, Tensor(a!) residual, Tensor post_norm, Tensor w_gu, Tensor w_down, "
+        "Tensor next_norm, Tensor? w_qkv, Tensor(b!) counters, int S_o, int cfg_o, int S_d, int cfg_d, int S_q, "
+        "int cfg_q, float eps, Tensor? trace=None) "
+        "-> (Tensor, Tensor)");
   m.def("mgemm_argmax(Tensor x, Tensor w, int n_valid, int cfg=0) -> Tensor");
   m.def("pgemm(Tensor x, Tensor w, int epi=0) -> Tensor");
   m.def("pgemm_partial(Tensor x, Tensor w, int splits) -> Tensor");
@@ -1013,6 +1069,7 @@ TORCH_LIBRARY_IMPL(docqa, CUDA, m) {
   m.impl("dgemm_glu", &dgemm_glu);
   m.impl("mgemm", &mgemm);
   m.impl("mgemm_glu", &mgemm_glu);
+  m.impl("mgemm_chain", &mgemm_chain);
   m.impl("mgemm_argmax", &mgemm_argmax);
   m.impl("pgemm", &pgemm);
   m.impl("pgemm_partial", &pgemm_partial);

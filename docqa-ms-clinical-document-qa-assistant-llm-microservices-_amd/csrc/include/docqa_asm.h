@@ -31,6 +31,17 @@ __device__ __forceinline__ void glds16(const void* gsrc, uint32_t dst_base) {
                  : "=&s"(keep) : "v"(gsrc), "s"(dst_base) : "memory");
 }
 
+// 16-B write-through (sc1) global store: the line is not left dirty in this XCD's L2, so a
+// consumer in another workgroup of the launch needs no release fence from the producer
+// (cdna_hip_programming.md §6 Guideline 16 R1); invisible to hipcc's waitcnt pass (drain
+// with an explicit vmcnt wait); s_nop 1 so no later VALU overwrites the data registers
+// before the store has read them (§5.7 item 1)
+__device__ __forceinline__ void store16_wt(void* p, uint4 v) {
+  typedef unsigned int u32x4_t __attribute__((ext_vector_type(4)));
+  const u32x4_t d = {v.x, v.y, v.z, v.w};
+  asm volatile("global_store_dwordx4 %0, %1, off sc1\n\ts_nop 1" ::"v"(p), "v"(d) : "memory");
+}
+
 template <int N>
 __device__ __forceinline__ void wait_vmcnt() {
   asm volatile("s_waitcnt vmcnt(%0)" :: "i"(N) : "memory");

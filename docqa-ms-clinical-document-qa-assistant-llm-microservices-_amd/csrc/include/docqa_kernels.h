@@ -123,6 +123,13 @@ int docqa_mgemm_glu(const void* X, const void* W, void* Y, int M, int N, int K, 
 int docqa_mgemm_argmax(const void* X, const void* W, int64_t* out, float* outv, float* ws_v, int* ws_i, int M,
                        int N, int K, int n_valid, int cfg, hipStream_t s);
 int docqa_mgemm_tile_n(int cfg);
+// persistent decode-layer chain (mgemm.hip): O -> add+RMSNorm -> gate|up+SwiGLU -> down ->
+// add+RMSNorm [-> next layer's QKV slabs] in one launch; counters: int32 [16], zeroed once
+int docqa_mgemm_chain(const void* attn, const void* w_o, float* p_o, void* residual, const void* post_norm,
+                      void* x1, const void* w_gu, void* g, const void* w_down, float* p_d, const void* next_norm,
+                      void* x2, const void* w_qkv, float* p_q, int* counters, long long* trace, int M, int H,
+                      int Ko, int N2I, int Nq, int S_o, int cfg_o, int S_d, int cfg_d, int S_q, int cfg_q,
+                      float eps, hipStream_t s);
 bool docqa_pgemm_ok(int M, int N, int K);
 int docqa_pgemm(const void* A, const void* W, void* C, float* P, int M, int N, int K, int S, int epi,
                 hipStream_t s);

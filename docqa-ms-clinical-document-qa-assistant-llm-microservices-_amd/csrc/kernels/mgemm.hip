@@ -31,6 +31,7 @@
 // on load and never stored).
 #include "docqa_common.h"
 #include "docqa_asm.h"
+#include "docqa_norm_row.h"
 #include <float.h>
 #include <stdlib.h>
 
@@ -57,7 +58,8 @@ __device__ __forceinline__ void better(float& bv, int& bi, float v, int i) {
 
 // Epilogue shared by the kernels: accumulators -> per-wave LDS scratch (the drained ring)
 // -> bf16 / fp32 split-K slab / fused SwiGLU / LM-head argmax partials.
-template <int EPI, int BN, int WM, int WN>
+// WT: write-through (sc1) stores, for consumers inside the same launch (the chain below)
+template <int EPI, int BN, int WM, int WN, bool WT = false>
 __device__ __forceinline__ void mgemm_epilogue(f32x4 (&acc)[BM / WM / 16][BN / WN / 16], uint16_t* smem,
                                                uint16_t* __restrict__ Y, float* __restrict__ P,
                                                float* __restrict__ pv, int* __restrict__ pi, int M, int N,
@@ -101,7 +103,12 @@ __device__ __forceinline__ void mgemm_epilogue(f32x4 (&acc)[BM / WM / 16][BN / W
         const int row = rbase + i * 16 + r, col = cbase + c;
         if (row < M) {
           if constexpr (EPI == EPI_PARTIAL) {
-            *reinterpret_cast<float4*>(P + ((size_t)slice * M + row) * N + col) = float4{v[0], v[1], v[2], v[3]};
+            float* dst = P + ((size_t)slice * M + row) * N + col;
+            if constexpr (WT)
+              store16_wt(dst, uint4{__float_as_uint(v[0]), __float_as_uint(v[1]), __float_as_uint(v[2]),
+                                    __float_as_uint(v[3])});
+            else
+              *reinterpret_cast<float4*>(dst) = float4{v[0], v[1], v[2], v[3]};
           } else if constexpr (EPI == EPI_BF16) {
             *reinterpret_cast<uint4*>(Y + (size_t)row * N + col) = pack8(v);
           } else {
@@ -112,7 +119,9 @@ __device__ __forceinline__ void mgemm_epilogue(f32x4 (&acc)[BM / WM / 16][BN / W
               const float gv = bf2f(f2bf(v[e])), uv = bf2f(f2bf(v[8 + e]));   // as the bf16 GEMM output
               o[e] = silu_f(gv) * uv;
             }
-            *reinterpret_cast<uint4*>(Y + (size_t)row * (N >> 1) + (col >> 1)) = pack8(o);
+            uint16_t* dst = Y + (size_t)row * (N >> 1) + (col >> 1);
+            if constexpr (WT) store16_wt(dst, pack8(o));
+            else *reinterpret_cast<uint4*>(dst) = pack8(o);
           }
         }
       }
@@ -173,14 +182,15 @@ __device__ __forceinline__ void mgemm_epilogue(f32x4 (&acc)[BM / WM / 16][BN / W
 // PF: fragment prefetch (stage k+1's LDS reads under stage k's MFMAs, two register sets);
 // PF = 0 reads each stage's fragments after its barrier (one register set, for the
 // 128 x 128-per-wave layout whose two sets would not fit)
-template <int EPI, int BN, int BKS, int NSR, int WM, int WN, int PF = 1>
-__global__ __launch_bounds__(WM * WN * 64) void mgemm_kernel(const uint16_t* __restrict__ X,
-                                                             const uint16_t* __restrict__ W,
-                                                             uint16_t* __restrict__ Y,
-                                                             float* __restrict__ P,
-                                                             float* __restrict__ pv, int* __restrict__ pi,
-                                                             int M, int N, int K, int Ks, int S,
-                                                             int ntiles, int remap, int n_valid) {
+// One (m-tile, weight tile, K slice) of the GEMM on the workgroup's LDS ring `smem`
+// (NSR * (BM + BN) * BKS bf16): the standalone kernel below runs one per workgroup, the
+// persistent decode-layer chain (mgemm_chain_kernel) runs them as work items.
+template <int EPI, int BN, int BKS, int NSR, int WM, int WN, int PF = 1, bool WT = false>
+__device__ __forceinline__ void mgemm_tile(uint16_t* smem, const uint16_t* __restrict__ X,
+                                           const uint16_t* __restrict__ W, uint16_t* __restrict__ Y,
+                                           float* __restrict__ P, float* __restrict__ pv,
+                                           int* __restrict__ pi, int M, int N, int K, int Ks,
+                                           int tile, int slice, int m0, int ntiles, int n_valid) {
   constexpr int WAVES = WM * WN;
   constexpr int MI = BM / WM / 16;                      // 16-row m-tiles per wave
   constexpr int CW = BN / WN;                           // output columns per wave
@@ -196,23 +206,8 @@ __global__ __launch_bounds__(WM * WN * 64) void mgemm_kernel(const uint16_t* __r
   static_assert(NSR >= 2, "ring needs >= 2 slots");
   static_assert(A_PER_WAVE * RPI * WAVES == BM && B_PER_WAVE * RPI * WAVES == BN, "DMA split");
   static_assert(NSR * SLOT * 2 <= 160 * 1024, "LDS");
-  __shared__ __attribute__((aligned(16))) uint16_t smem[NSR * SLOT];
 
-  const int L = blockIdx.x;
-  int tile, slice;
-  if (remap == 1) {            // 8 % S == 0: XCD x runs slice x % S
-    const int xcd = L & 7, j = L >> 3;
-    slice = xcd % S;
-    tile = j * (8 / S) + xcd / S;
-  } else if (remap == 2) {     // S % 8 == 0: XCD x runs slices x, x + 8, ...
-    const int xcd = L & 7, j = L >> 3, q = S / 8;
-    slice = xcd + 8 * (j % q);
-    tile = j / q;
-  } else {
-    tile = L % ntiles;
-    slice = L / ntiles;
-  }
-  const int n0 = tile * BN, m0 = blockIdx.y * BM, kbeg = slice * Ks;
+  const int n0 = tile * BN, kbeg = slice * Ks;
   const int nk = Ks / BKS;     // even, >= 2
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -368,7 +363,34 @@ __global__ __launch_bounds__(WM * WN * 64) void mgemm_kernel(const uint16_t* __r
   wait_vmcnt<0>();
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   ring_barrier();   // every wave is done reading the ring: reuse it as epilogue scratch
-  mgemm_epilogue<EPI, BN, WM, WN>(acc, smem, Y, P, pv, pi, M, N, m0, n0, slice, tile, ntiles, n_valid);
+  mgemm_epilogue<EPI, BN, WM, WN, WT>(acc, smem, Y, P, pv, pi, M, N, m0, n0, slice, tile, ntiles, n_valid);
+}
+
+template <int EPI, int BN, int BKS, int NSR, int WM, int WN, int PF = 1>
+__global__ __launch_bounds__(WM * WN * 64) void mgemm_kernel(const uint16_t* __restrict__ X,
+                                                             const uint16_t* __restrict__ W,
+                                                             uint16_t* __restrict__ Y,
+                                                             float* __restrict__ P,
+                                                             float* __restrict__ pv, int* __restrict__ pi,
+                                                             int M, int N, int K, int Ks, int S,
+                                                             int ntiles, int remap, int n_valid) {
+  __shared__ __attribute__((aligned(16))) uint16_t smem[NSR * (BM + BN) * BKS];
+  const int L = blockIdx.x;
+  int tile, slice;
+  if (remap == 1) {            // 8 % S == 0: XCD x runs slice x % S
+    const int xcd = L & 7, j = L >> 3;
+    slice = xcd % S;
+    tile = j * (8 / S) + xcd / S;
+  } else if (remap == 2) {     // S % 8 == 0: XCD x runs slices x, x + 8, ...
+    const int xcd = L & 7, j = L >> 3, q = S / 8;
+    slice = xcd + 8 * (j % q);
+    tile = j / q;
+  } else {
+    tile = L % ntiles;
+    slice = L / ntiles;
+  }
+  mgemm_tile<EPI, BN, BKS, NSR, WM, WN, PF>(smem, X, W, Y, P, pv, pi, M, N, K, Ks, tile, slice, blockIdx.y * BM,
+                                            ntiles, n_valid);
 }
 
 __global__ __launch_bounds__(64) void mgemm_argmax_merge(const float* __restrict__ pv,
@@ -500,6 +522,214 @@ int docqa_mgemm_argmax(const void* X, const void* W, int64_t* out, float* outv, 
                                         M, N, K, 1, n_valid, s);
   if (rc) return rc;
   mgemm_argmax_merge<<<M, 64, 0, s>>>(ws_v, ws_i, N / kCfg[cfg].bn, out, outv);
+  DOCQA_CHECK_LAUNCH();
+  return 0;
+}
+
+// ---------------------------------------------------------------------------------------
+// Persistent decode-layer chain: the back half of a Llama decoder layer at 193..512 decode
+// rows (TP = 1) plus the next layer's QKV projection, in ONE launch instead of six:
+//   phase 0  O projection        attn [M, Ko] . Wo^T -> fp32 split-K slabs p_o [S_o, M, H]
+//   phase 1  residual + RMSNorm  residual += bf16(sum p_o); x1 = rmsnorm(residual) * post_norm
+//   phase 2  gate|up + SwiGLU    g = silu(x1 Wg^T) * (x1 Wu^T)            (8-interleaved W)
+//   phase 3  down projection     g . Wd^T -> slabs p_d [S_d, M, H]
+//   phase 4  residual + RMSNorm  residual += bf16(sum p_d); x2 = rmsnorm(residual) * next_norm
+//   phase 5  next QKV (optional) x2 . Wqkv^T -> slabs p_q [S_q, M, Nq] (rope_cache_splitk /
+//            the grouped cascade consume them after the launch)
+// Every GEMM item is one mgemm_tile of the standalone plan (same tiles, same split, same
+// epilogues) and every norm item runs the standalone kernel's row body on each 256-thread
+// half of the workgroup (docqa_norm_row.h), so the chain's outputs equal the six-launch
+// sequence bit for bit.  What it removes: five kernel boundaries per layer -- each a grid
+// drain + fill and, behind the split-K GEMMs, the writeback of their dirty slab lines
+// (MI355X_MICROARCH.md "boundary": 1.7-1.9 us + B / 6 TB/s; "phase-in-launch": 0.85x of the
+// summed phase spans on an M = 256 block) -- and workgroups that run out of work in one
+// phase take the next phase's items and wait there, so the next phase starts on every CU
+// the moment its inputs are published.
+//
+// Scheduling (cdna_hip_programming.md §5 "Projection GEMM at M = 256" item 2 / §6 Guideline
+// 16): workgroups draw tickets from one agent-scope counter; tickets enumerate the items
+// phase by phase, so an item waits only on items with smaller tickets, which were drawn by
+// workgroups that are running -- deadlock-free whatever number of workgroups is resident.
+// Publish: every wave's stores retired (vmcnt 0) -> barrier -> lane 0 agent release fence ->
+// vmcnt 0 -> relaxed agent fetch_add of the phase counter.  Consume: lane 0 polls the
+// previous phase's counter (relaxed agent loads + s_sleep, bounded: a lost wake-up sets the
+// sticky error word and falls through instead of hanging the GPU) -> agent acquire fence ->
+// barrier.  The last workgroup out resets the counters, so a captured graph replays the
+// launch with no memset node.
+// Counters (int32, zero before the first launch): [0..5] items done per phase, [8] ticket,
+// [9] workgroups exited, [12] sticky error flag (never reset by the kernel).
+namespace {
+struct ChainArgs {
+  const uint16_t* attn;
+  const uint16_t* w_o;
+  float* p_o;
+  uint16_t* residual;
+  const uint16_t* post_norm;
+  uint16_t* x1;
+  const uint16_t* w_gu;
+  uint16_t* g;
+  const uint16_t* w_down;
+  float* p_d;
+  const uint16_t* next_norm;
+  uint16_t* x2;
+  const uint16_t* w_qkv;   // nullptr: no phase 5 (last layer)
+  float* p_q;
+  int* ctr;
+  long long* trace;        // debug: per ticket (phase, workgroup, t_ticket, t_ready, t_done, t_published)
+  int M, H, Ko, N2I, Nq;   // rows, hidden, O input width, gate|up rows (2 I), QKV rows
+  int S_o, S_d, S_q, cfg_o, cfg_d, cfg_q;
+  float eps;
+};
+
+constexpr int kChainSlot = 3 * (BM + 128) * 64;     // the cfg 2 ring (bf16 elements), >= cfg 7's
+
+__device__ __forceinline__ bool chain_wait(int* p, int target) {
+  for (int it = 0; it < (1 << 22); ++it) {
+    if (__hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= target) return true;
+    __builtin_amdgcn_s_sleep(8);
+  }
+  return false;
+}
+
+template <int NV>
+__device__ __forceinline__ void chain_norm(const float* P, int S, int M, int H, uint16_t* residual,
+                                           const uint16_t* w, uint16_t* out, float eps, int row,
+                                           int tid, float* red) {
+  const size_t slab = (size_t)M * H;
+  switch (S) {
+    case 4: add_rmsnorm_splitk_row<NV, 4, true>(P, S, slab, residual, w, out, H, eps, row, tid, red); break;
+    case 7: add_rmsnorm_splitk_row<NV, 7, true>(P, S, slab, residual, w, out, H, eps, row, tid, red); break;
+    case 8: add_rmsnorm_splitk_row<NV, 8, true>(P, S, slab, residual, w, out, H, eps, row, tid, red); break;
+    default: add_rmsnorm_splitk_row<NV, 0, true>(P, S, slab, residual, w, out, H, eps, row, tid, red); break;
+  }
+}
+
+__global__ __launch_bounds__(512) void mgemm_chain_kernel(ChainArgs a) {
+  __shared__ __attribute__((aligned(16))) uint16_t smem[kChainSlot];
+  float* red = reinterpret_cast<float*>(smem);          // norm items: 4 floats per half
+  int* tk = reinterpret_cast<int*>(smem) + 16;          // ticket broadcast
+  const int tid = threadIdx.x;
+  int* ctr = a.ctr;
+  const int mt = (a.M + BM - 1) / BM;
+  const int nt_o = a.H / (a.cfg_o == 7 ? 64 : 128), nt_gu = a.N2I / 128, nt_d = a.H / (a.cfg_d == 7 ? 64 : 128),
+            nt_q = a.Nq / (a.cfg_q == 7 ? 64 : 128);
+  const int c0 = nt_o * a.S_o * mt, c1 = a.M / 2, c2 = nt_gu * mt, c3 = nt_d * a.S_d * mt, c4 = a.M / 2,
+            c5 = a.w_qkv ? nt_q * a.S_q * mt : 0;
+  const int e0 = c0, e1 = e0 + c1, e2 = e1 + c2, e3 = e2 + c3, e4 = e3 + c4, total = e4 + c5;
+  const int I = a.N2I / 2;
+  int seen = 0;   // phases whose inputs this workgroup has acquired: items of phase <= seen may run
+  for (;;) {
+    if (tid == 0) tk[0] = __hip_atomic_fetch_add(&ctr[8], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __syncthreads();
+    int i = tk[0];
+    __syncthreads();
+    if (i >= total) break;
+    const int ticket = i;
+    long long t0 = 0, t1 = 0, t2 = 0;
+    if (a.trace && tid == 0) t0 = wall_clock64();
+    // phase of ticket i and its index within the phase; need: items in the previous phase
+    int p, need;
+    if (i < e0) { p = 0; need = 0; }
+    else if (i < e1) { p = 1; i -= e0; need = c0; }
+    else if (i < e2) { p = 2; i -= e1; need = c1; }
+    else if (i < e3) { p = 3; i -= e2; need = c2; }
+    else if (i < e4) { p = 4; i -= e3; need = c3; }
+    else { p = 5; i -= e4; need = c4; }
+    if (p > seen) {
+      if (tid == 0) {
+        if (!chain_wait(&ctr[p - 1], need))
+          __hip_atomic_store(&ctr[12], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      }
+      __syncthreads();
+      seen = p;
+    }
+    if (a.trace && tid == 0) t1 = wall_clock64();
+    if (p == 1 || p == 4) {
+      const float* P = p == 1 ? a.p_o : a.p_d;
+      const int S = p == 1 ? a.S_o : a.S_d;
+      const uint16_t* w = p == 1 ? a.post_norm : a.next_norm;
+      uint16_t* out = p == 1 ? a.x1 : a.x2;
+      const int h = tid >> 8, row = 2 * i + h;
+      if (a.H <= 2048 * 2) chain_norm<2>(P, S, a.M, a.H, a.residual, w, out, a.eps, row, tid & 255, red + 4 * h);
+      else chain_norm<4>(P, S, a.M, a.H, a.residual, w, out, a.eps, row, tid & 255, red + 4 * h);
+    } else if (p == 2) {
+      const int tile = i % nt_gu, m0 = (i / nt_gu) * BM;
+      mgemm_tile<EPI_GLU, 128, 64, 3, 4, 2, 1, true>(smem, a.x1, a.w_gu, a.g, nullptr, nullptr, nullptr, a.M, a.N2I, a.H,
+                                            a.H, tile, 0, m0, nt_gu, a.N2I);
+    } else {
+      // split-K projections (O, down, next QKV): one call site per tile width
+      const uint16_t* X = p == 0 ? a.attn : p == 3 ? a.g : a.x2;
+      const uint16_t* W = p == 0 ? a.w_o : p == 3 ? a.w_down : a.w_qkv;
+      float* P = p == 0 ? a.p_o : p == 3 ? a.p_d : a.p_q;
+      const int N = p == 5 ? a.Nq : a.H, K = p == 0 ? a.Ko : p == 3 ? I : a.H;
+      const int S = p == 0 ? a.S_o : p == 3 ? a.S_d : a.S_q;
+      const int cfg = p == 0 ? a.cfg_o : p == 3 ? a.cfg_d : a.cfg_q;
+      const int nt = N / (cfg == 7 ? 64 : 128);
+      const int slice = i % S, tile = (i / S) % nt, m0 = (i / (S * nt)) * BM;
+      if (cfg == 7)
+        mgemm_tile<EPI_PARTIAL, 64, 64, 3, 4, 2, 1, true>(smem, X, W, nullptr, P, nullptr, nullptr, a.M, N, K, K / S, tile,
+                                                 slice, m0, nt, N);
+      else
+        mgemm_tile<EPI_PARTIAL, 128, 64, 3, 4, 2, 1, true>(smem, X, W, nullptr, P, nullptr, nullptr, a.M, N, K, K / S, tile,
+                                                  slice, m0, nt, N);
+    }
+    // publish the item
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (tid == 0) {
+      if (a.trace) t2 = wall_clock64();
+      __hip_atomic_fetch_add(&ctr[p], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (a.trace) {
+        long long* tr = a.trace + (size_t)ticket * 6;
+        tr[0] = p; tr[1] = blockIdx.x | ((__builtin_amdgcn_s_getreg(20 | (3 << 11)) & 15) << 16); tr[2] = t0; tr[3] = t1; tr[4] = t2; tr[5] = wall_clock64();
+      }
+    }
+  }
+  if (tid == 0) {
+    const int old = __hip_atomic_fetch_add(&ctr[9], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (old == (int)gridDim.x - 1) {
+#pragma unroll
+      for (int j = 0; j < 10; ++j) __hip_atomic_store(&ctr[j], 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+}
+
+int chain_grid() {
+  static int n = 0;
+  if (n == 0) {
+    int dev = 0, cus = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) !=
+                                                 hipSuccess || cus <= 0)
+      cus = 256;
+    n = cus;   // one workgroup per CU (the 144 KB ring)
+  }
+  return n;
+}
+}  // namespace
+
+// Shapes: M even (rows tiled by 256); H % 128 == 0, H <= 8192; split-K tiles of cfg 2 (128
+// wide) or 7 (64 wide);
+// Ko, I = N2I / 2 and H each divisible by (split x 128); Nq % 128 == 0.
+int docqa_mgemm_chain(const void* attn, const void* w_o, float* p_o, void* residual, const void* post_norm,
+                      void* x1, const void* w_gu, void* g, const void* w_down, float* p_d, const void* next_norm,
+                      void* x2, const void* w_qkv, float* p_q, int* counters, long long* trace, int M, int H,
+                      int Ko, int N2I, int Nq, int S_o, int cfg_o, int S_d, int cfg_d, int S_q, int cfg_q,
+                      float eps, hipStream_t s) {
+  auto cfg_ok = [](int c) { return c == 2 || c == 7; };
+  if (M <= 0 || M % 2 || H > 8192 || H % 128 || N2I % 256 || !cfg_ok(cfg_o) || !cfg_ok(cfg_d)) return -1;
+  if (!shape_ok(M, H, Ko, S_o, cfg_o) || !shape_ok(M, N2I, H, 1, 2) || !shape_ok(M, H, N2I / 2, S_d, cfg_d)) return -1;
+  if (w_qkv && (!p_q || !cfg_ok(cfg_q) || !shape_ok(M, Nq, H, S_q, cfg_q))) return -1;
+  const void* ptrs[] = {attn, w_o, p_o, residual, post_norm, x1, w_gu, g, w_down, p_d, next_norm, x2};
+  for (const void* q : ptrs)
+    if (!docqa_aligned16(q)) return -1;
+  if (w_qkv && (!docqa_aligned16(w_qkv) || !docqa_aligned16(p_q))) return -1;
+  ChainArgs a{(const uint16_t*)attn, (const uint16_t*)w_o, p_o, (uint16_t*)residual, (const uint16_t*)post_norm,
+              (uint16_t*)x1, (const uint16_t*)w_gu, (uint16_t*)g, (const uint16_t*)w_down, p_d,
+              (const uint16_t*)next_norm, (uint16_t*)x2, (const uint16_t*)w_qkv, p_q, counters, trace,
+              M, H, Ko, N2I, Nq, S_o, S_d, w_qkv ? S_q : 1, cfg_o, cfg_d, w_qkv ? cfg_q : 2, eps};
+  mgemm_chain_kernel<<<chain_grid(), 512, 0, s>>>(a);
   DOCQA_CHECK_LAUNCH();
   return 0;
 }

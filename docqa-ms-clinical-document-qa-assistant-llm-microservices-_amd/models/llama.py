@@ -145,6 +145,10 @@ class LlamaModel:
         self.cos_sin = ops.rope_cos_sin(cfg.max_position, cfg.head_dim, cfg.rope_theta, self.device,
                                         scaling=cfg.rope_scaling)
         self.layers: list[dict] = []
+        # ticket / phase counters of the persistent decode-layer chain (ops.mgemm_chain), one
+        # row per layer; the kernel leaves them zeroed, so graph replays need no memset
+        self._chain_ctr = (torch.zeros(cfg.layers, 16, dtype=torch.int32, device=self.device)
+                           if self.device.type == "cuda" else None)
         if init:
             self._random_init(seed)
 
@@ -308,12 +312,23 @@ class LlamaModel:
         so, o_part = plans.get("o", (0, None))
         sd, down_part = plans.get("down", (0, None))
         cascade = decode and meta.shared_len is not None
+        # persistent decode-layer chain: O -> add+norm -> gate|up -> down -> add+norm -> next
+        # QKV in one launch (ops.chain_plan; TP = 1, mid-M plans only)
+        chain = None
+        if decode and self.tp == 1 and self.layers and self._chain_ctr is not None and x.is_cuda and sq:
+            L0 = self.layers[0]
+            chain = ops.chain_plan(M, L0["o"].shape[0], L0["o"].shape[1], L0["gate_up"].shape[0],
+                                   L0["qkv"].shape[0])
+        pq = None   # this layer's QKV slabs, already computed by the previous layer's chain
         for i, L in enumerate(self.layers):
             kc, vc = kv_caches[i]
+            if sq:
+                qkv_slabs = pq if pq is not None else qkv_part(x, L["qkv"])
+                pq = None
             if cascade:
                 # shared-prefix decode: RoPE + cache write, then prefix-once + suffix attention
                 if sq:
-                    qkv = ops.rope_cache_splitk(qkv_part(x, L["qkv"]), meta.positions,
+                    qkv = ops.rope_cache_splitk(qkv_slabs, meta.positions,
                                                 self.cos_sin, meta.slot_mapping, kc, vc, hq, hkv, D)
                     if meta.decode_groups is not None:
                         a = ops.paged_decode_cascade_grouped(qkv, kc, vc, meta.block_tables, meta.context_lens,
@@ -346,12 +361,12 @@ class LlamaModel:
                 qkv = None
             elif sq and ops.fused_decode_ok(kc, meta.block_tables):
                 # QKV partials -> RoPE + new-token cache write + attention, one launch
-                a = ops.paged_decode_fused(qkv_part(x, L["qkv"]), meta.positions, self.cos_sin,
+                a = ops.paged_decode_fused(qkv_slabs, meta.positions, self.cos_sin,
                                            meta.slot_mapping, kc, vc, meta.block_tables, meta.context_lens,
                                            hq, meta.max_context, self.scale, meta.seq_order)
                 qkv = None
             elif sq:
-                qkv = ops.rope_cache_splitk(qkv_part(x, L["qkv"]), meta.positions, self.cos_sin,
+                qkv = ops.rope_cache_splitk(qkv_slabs, meta.positions, self.cos_sin,
                                             meta.slot_mapping, kc, vc, hq, hkv, D)
             else:
                 qkv = lin(x, L["qkv"])
@@ -367,10 +382,15 @@ class LlamaModel:
             else:
                 a = ops.paged_decode(qkv, kc, vc, meta.block_tables, meta.context_lens, hq,
                                      meta.max_context, self.scale, meta.seq_order)
+            nxt = self.layers[i + 1]["in_norm"] if i + 1 < nl else self.final_norm
+            if chain is not None:
+                wq = self.layers[i + 1]["qkv"] if i + 1 < nl else None
+                x, pq = ops.mgemm_chain(a, L["o"], residual, L["post_norm"], L["gate_up"], L["down"], nxt, wq,
+                                        self._chain_ctr[i], chain, eps)
+                continue
             # row-parallel O: (TP all-reduce +) residual add + RMSNorm in one consumer
             x = comm.tp_add_rmsnorm(o_part(a, L["o"]) if so else lin(a, L["o"]), residual, L["post_norm"], eps)
             g = glu(x, L["gate_up"])
-            nxt = self.layers[i + 1]["in_norm"] if i + 1 < nl else self.final_norm
             x = comm.tp_add_rmsnorm(down_part(g, L["down"]) if sd else lin(g, L["down"]), residual, nxt, eps)
         if logits_index is not None:
             x = x.index_select(0, logits_index)

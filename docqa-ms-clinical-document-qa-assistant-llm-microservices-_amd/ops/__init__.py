@@ -280,6 +280,46 @@ def mgemm_partial(x, w, splits: int, cfg: int = 0):
     return torch.einsum("msk,nsk->smn", xs, ws).contiguous()
 
 
+_CHAIN = os.environ.get("DOCQA_DECODE_CHAIN", "0") == "1"
+
+
+def chain_plan(M: int, H: int, Ko: int, N2I: int, Nq: int) -> tuple[int, ...] | None:
+    """(S_o, cfg_o, S_d, cfg_d, S_q, cfg_q) of the persistent decode-layer chain (mgemm.hip
+    mgemm_chain_kernel) at M decode rows, or None where it does not apply: the chain runs
+    the standalone mid-M plans of the O, gate|up (fused SwiGLU, cfg 2), down and QKV
+    projections as work items of one launch, so it applies exactly where all four take the
+    mid-M GEMM (ops.mid_plan) with 128-wide (cfg 2) or 64-wide (cfg 7) tiles."""
+    if not _CHAIN or M % 2 or H > 8192 or H % 128:
+        return None
+    S_o, c_o = mid_plan(M, H, Ko)
+    S_g, c_g = mid_plan(M, N2I, H, glu=True)
+    S_d, c_d = mid_plan(M, H, N2I // 2)
+    S_q, c_q = mid_plan(M, Nq, H)
+    if not (S_o and S_g and S_d and S_q) or c_g != 2 or not {c_o, c_d, c_q} <= {2, 7}:
+        return None
+    return S_o, c_o, S_d, c_d, S_q, c_q
+
+
+def mgemm_chain(attn, w_o, residual, post_norm, w_gu, w_down, next_norm, w_qkv, counters, plan, eps: float):
+    """Back half of a decoder layer + the next layer's QKV in one persistent launch:
+    residual += O(attn); x1 = rmsnorm(residual) * post_norm; g = SwiGLU(x1 Wgu^T);
+    residual += down(g); x2 = rmsnorm(residual) * next_norm; returns (x2, the next layer's
+    QKV split-K slabs [S_q, M, Nq] or None).  Same bits as the six standalone launches."""
+    S_o, c_o, S_d, c_d, S_q, c_q = plan
+    if _gpu(attn):
+        x2, pq = _native().mgemm_chain(attn.contiguous(), w_o, residual, post_norm, w_gu, w_down, next_norm,
+                                       w_qkv, counters, S_o, c_o, S_d, c_d, S_q, c_q, eps)
+        return x2, (pq if w_qkv is not None else None)
+    def slabs(x, w, S):
+        p = mgemm_partial(x, w, S)
+        return p if S > 1 else p.float()[None]
+
+    x1 = add_rmsnorm_splitk(slabs(attn, w_o, S_o), residual, post_norm, eps)
+    g = mgemm_glu(x1, w_gu)
+    x2 = add_rmsnorm_splitk(slabs(g, w_down, S_d), residual, next_norm, eps)
+    return x2, (slabs(x2, w_qkv, S_q) if w_qkv is not None else None)
+
+
 def mgemm_glu(x, w_il, cfg: int = 0):
     """silu(x Wg^T) * (x Wu^T) for 8-interleaved gate|up weights on the mid-M decode GEMM."""
     if _gpu(x):
