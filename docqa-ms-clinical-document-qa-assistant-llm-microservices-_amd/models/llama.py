@@ -69,6 +69,13 @@ class LlamaConfig:
         if name in ("llama3-70b", "llama-3-70b", "70b"):
             return LlamaConfig(name="llama3-70b", hidden=8192, intermediate=28672, layers=80,
                                heads=64, kv_heads=8)
+        if name in ("mistral-7b", "mistral"):
+            # the reference's own generator: ChatOllama(model="mistral") (llm-qa/main.py:69)
+            # pulls Mistral-7B-Instruct v0.3 -- the Llama block with a 32768-token vocabulary,
+            # rope theta 1e6 and full causal attention (v0.1's 4096-token sliding window is
+            # gone); HF checkpoints of either version load through models/checkpoint.py
+            return LlamaConfig(name="mistral-7b", vocab_size=32768, rope_theta=1e6, max_position=32768,
+                               bos_token_id=1, eos_token_id=2)
         if name == "llama3-1b-test":  # mid-size config for kernel/engine tests on GPU
             return LlamaConfig(name=name, vocab_size=32000, hidden=2048, intermediate=8192,
                                layers=4, heads=16, kv_heads=4, max_position=4096,

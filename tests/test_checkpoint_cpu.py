@@ -228,3 +228,22 @@ def test_rope_scaled_checkpoint_round_trip(tmp_path):
     assert got.cfg.rope_scaling == cfg.rope_scaling
     want = ref.rope_cos_sin(cfg.max_position, cfg.head_dim, cfg.rope_theta, scaling=cfg.rope_scaling)
     assert torch.equal(got.cos_sin, want)
+
+
+def test_mistral_preset_matches_hf_config():
+    """The reference's generator (ChatOllama(model="mistral"), llm-qa/main.py:69) as a preset:
+    the Mistral-7B v0.3 HF config.json maps onto exactly LlamaConfig.preset("mistral-7b")."""
+    from docqa_amd.models import checkpoint as ck
+    from docqa_amd.models.llama import LlamaConfig
+
+    hf = {"architectures": ["MistralForCausalLM"], "model_type": "mistral", "vocab_size": 32768,
+          "hidden_size": 4096, "intermediate_size": 14336, "num_hidden_layers": 32, "num_attention_heads": 32,
+          "num_key_value_heads": 8, "head_dim": 128, "rope_theta": 1000000.0, "rms_norm_eps": 1e-05,
+          "max_position_embeddings": 32768, "bos_token_id": 1, "eos_token_id": 2, "sliding_window": None,
+          "hidden_act": "silu", "tie_word_embeddings": False}
+    got = ck.llama_config_from_hf(hf)
+    want = LlamaConfig.preset("mistral-7b")
+    for f in ("vocab_size", "hidden", "intermediate", "layers", "heads", "kv_heads", "head_dim", "rope_theta",
+              "rms_eps", "max_position", "bos_token_id", "eos_token_id", "sliding_window"):
+        assert getattr(got, f) == getattr(want, f), f
+    assert 7.0e9 < want.num_params() < 7.5e9
