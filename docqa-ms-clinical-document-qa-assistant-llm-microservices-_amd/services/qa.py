@@ -7,6 +7,9 @@ Contract (llm-qa/main.py:108-126 and synthese-comparative/core/llm_client.py:42-
                             in the reference; served here)
   GET  /health              {"status": "ok", "service": "llm-qa"}
   GET  /metrics             Prometheus text (requests, batch sizes, stage latencies)
+  POST /api/chat, /api/generate, GET /api/tags, /api/version
+                            the Ollama wire API the reference's ChatOllama posts to
+                            (services/ollama_api.py), served from this engine
 
 Serving model: the reference answers one blocking request at a time per process
 (llm-qa/main.py:111-117).  Here (``DOCQA_SERVING=continuous``, default) a prep thread
@@ -86,6 +89,19 @@ class DynamicBatcher:
                 self.metrics.observe("ask_batch_size", len(asks))
                 for k, v in vars(self.pipe.last_times).items():
                     self.metrics.observe(f"stage_{k}", v)
+            gens = [b for b in batch if b[0] == "gen"]
+            # Ollama-API requests: raw prompt ids with their own sampling options, one engine
+            # batch per distinct option set (no token streaming on this path)
+            groups: dict = {}
+            for b in gens:
+                p = b[1]["params"]
+                groups.setdefault((p.max_new_tokens, p.temperature, p.top_k, p.top_p, p.stop_on_eos, p.seed),
+                                  []).append(b)
+            for grp in groups.values():
+                outs = self.pipe.engine.generate([b[1]["ids"] for b in grp], grp[0][1]["params"])
+                for (_, _, f, t0), o in zip(grp, outs):
+                    self.metrics.observe("generate_latency_s", time.perf_counter() - t0)
+                    f.set_result({"ids": list(o)})
             if sums:
                 prompts = [self.pipe.chat_tok.chat_prompt(b[1]) for b in sums]
                 lim = self.pipe.max_prompt_tokens
@@ -251,6 +267,18 @@ class ContinuousBatcher:
                     f.set_result({"answer": pipe.chat_tok.decode(ef.result()), "sources": srcs})
 
                 self.engine.submit(p, params).add_done_callback(done)
+        for _, g, f, t0 in (it for it in items if it[0] == "gen"):
+            # Ollama-API requests (services/ollama_api.py): prompt ids + per-request sampling,
+            # tokens streamed through on_token as the scheduler emits them
+
+            def gdone(ef, f=f, t0=t0):
+                if ef.exception() is not None:
+                    f.set_exception(ef.exception())
+                    return
+                self.metrics.observe("generate_latency_s", time.perf_counter() - t0)
+                f.set_result({"ids": list(ef.result())})
+
+            self.engine.submit(g["ids"], g["params"], g.get("on_token")).add_done_callback(gdone)
         for _, text, f, t0 in sums:
             p = pipe.chat_tok.chat_prompt(text)
             lim = pipe.max_prompt_tokens
@@ -356,6 +384,11 @@ def create_app(pipeline=None, settings: Settings | None = None, lockstep=None,
             return await router.call("summarize", "/api/llm/summarize", {"prompt": req.prompt}, "prompt")
         fut = app.state.batcher.submit("summarize", req.prompt)
         return await asyncio.wrap_future(fut)
+
+    # the Ollama wire API the reference's llm-qa calls (ChatOllama, llm-qa/main.py:66-69,117)
+    from . import ollama_api
+
+    ollama_api.register(app, st, metrics)
 
     @app.get("/health")
     def health():

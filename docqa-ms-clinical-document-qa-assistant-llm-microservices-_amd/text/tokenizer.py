@@ -154,6 +154,20 @@ class ChatTokenizer:
         ids += self.encode("\n\n")
         return ids
 
+    def chat_messages(self, messages: list[dict]) -> list[int]:
+        """Llama-3 framing of a whole conversation (Ollama /api/chat ``messages``: role
+        system / user / assistant / tool, content) ending in the assistant header, so the
+        model continues as the assistant.  One user message (+ optional system first) gives
+        exactly :meth:`chat_prompt`'s ids."""
+        s = self.special
+        ids = [s("<|begin_of_text|>")]
+        for m in messages:
+            ids += [s("<|start_header_id|>")] + self.encode(str(m.get("role", "user"))) + [s("<|end_header_id|>")]
+            ids += self.encode("\n\n" + str(m.get("content", ""))) + [s("<|eot_id|>")]
+        ids += [s("<|start_header_id|>")] + self.encode("assistant") + [s("<|end_header_id|>")]
+        ids += self.encode("\n\n")
+        return ids
+
     def decode(self, ids: list[int]) -> str:
         keep = []
         for i in ids:

@@ -441,3 +441,59 @@ def test_tracing_spans_and_chrome_export(stack):
         assert summ["enabled"] and summ["spans"]
     finally:
         tracing.enable(False)
+
+
+@pytest.mark.parametrize("mode", ["continuous", "batch"])
+def test_ollama_api_chat_generate_stream(tmp_path, mode):
+    """The Ollama wire API the reference's ChatOllama posts to (llm-qa/main.py:66-69,117),
+    served by llm-qa from its own engine: /api/chat and /api/generate, streamed (NDJSON,
+    token by token on the continuous scheduler) and not, /api/tags, /api/version."""
+    import json as _json
+
+    from docqa_amd.services.stack import DocQAStack, StackOptions
+
+    st = Settings()
+    st.index_dir = str(tmp_path)
+    st.default_data_dir = str(tmp_path / "nodata")
+    st.database_url = "sqlite://"
+    st.max_new_tokens = 6
+    st.serving_mode = mode
+    s = DocQAStack(StackOptions(llm="tiny", embed="tiny-bert", ner="tiny-bert", device="cpu",
+                                max_batch=4, max_context=1024, use_graphs=False), st)
+    try:
+        qa = TestClient(s.qa_app)
+        msgs = [{"role": "system", "content": "Tu es un expert."}, {"role": "user", "content": "Vide de Qi ?"}]
+        r = qa.post("/api/chat", json={"model": "mistral", "messages": msgs, "stream": False,
+                                       "options": {"temperature": 0, "num_predict": 5}})
+        assert r.status_code == 200
+        j = r.json()
+        assert j["model"] == "mistral" and j["done"] is True and j["message"]["role"] == "assistant"
+        assert isinstance(j["message"]["content"], str) and 1 <= j["eval_count"] <= 5
+        assert j["done_reason"] in ("stop", "length") and j["prompt_eval_count"] > 10
+        # the same request streamed: the pieces concatenate to the non-streamed answer
+        r2 = qa.post("/api/chat", json={"model": "mistral", "messages": msgs, "options": {"num_predict": 5}})
+        assert r2.status_code == 200 and r2.headers["content-type"].startswith("application/x-ndjson")
+        lines = [_json.loads(x) for x in r2.text.splitlines() if x.strip()]
+        assert lines[-1]["done"] is True and all(not x["done"] for x in lines[:-1])
+        assert "".join(x["message"]["content"] for x in lines[:-1]) == j["message"]["content"]
+        assert lines[-1]["eval_count"] == j["eval_count"]
+        g = qa.post("/api/generate", json={"model": "m", "prompt": "Résume.", "stream": False,
+                                           "options": {"num_predict": 3}}).json()
+        assert g["done"] is True and isinstance(g["response"], str) and g["eval_count"] <= 3
+        graw = qa.post("/api/generate", json={"prompt": "abc", "raw": True, "stream": False}).json()
+        assert graw["prompt_eval_count"] == len(s.pipeline.chat_tok.encode("abc"))
+        tags = qa.get("/api/tags").json()["models"]
+        assert len(tags) == 1 and tags[0]["details"]["quantization_level"] == "BF16"
+        assert "version" in qa.get("/api/version").json()
+        assert "llm_qa_ollama_chat_requests" in qa.get("/metrics").text
+    finally:
+        s.close()
+
+
+def test_chat_messages_framing_matches_chat_prompt():
+    from docqa_amd.text.tokenizer import ChatTokenizer
+
+    t = ChatTokenizer()
+    assert t.chat_messages([{"role": "user", "content": "Bonjour"}]) == t.chat_prompt("Bonjour")
+    assert (t.chat_messages([{"role": "system", "content": "Sys"}, {"role": "user", "content": "Q"}])
+            == t.chat_prompt("Q", system="Sys"))
