@@ -146,7 +146,8 @@ def run_launch(a, mode: str) -> list[dict]:
             results = []
             for ri, rate in enumerate(a.rates):
                 batch_q = qs[a.warmup + ri * a.requests:a.warmup + (ri + 1) * a.requests]
-                lat, lags, errors, empty, retried = [], [], 0, 0, 0
+                lat, lags, dones, errors, empty, retried = [], [], [], 0, 0, 0
+                sched = _arrivals(a.requests, rate)
                 c0 = _engine_counters(await metrics_text())
                 t0 = time.perf_counter()
 
@@ -170,6 +171,7 @@ def run_launch(a, mode: str) -> list[dict]:
                     elif not body.get("answer"):
                         empty += 1       # greedy random-init model: EOS as the first token
                     lat.append(time.perf_counter() - (t0 + at))
+                    dones.append(time.perf_counter() - t0)
 
                 async def progress():
                     # a line every 15 s: a live run is visibly alive (and a wedged one visibly stuck)
@@ -181,7 +183,7 @@ def run_launch(a, mode: str) -> list[dict]:
                 pt = asyncio.create_task(progress())
                 try:
                     await asyncio.wait_for(
-                        asyncio.gather(*[one(at, q) for at, q in zip(_arrivals(a.requests, rate), batch_q)]),
+                        asyncio.gather(*[one(at, q) for at, q in zip(sched, batch_q)]),
                         timeout=a.run_timeout)
                 finally:
                     pt.cancel()
@@ -189,7 +191,13 @@ def run_launch(a, mode: str) -> list[dict]:
                 mtext = await metrics_text()
                 c1 = _engine_counters(mtext)
                 lags.sort()
-                results.append({"rate": rate, "lat": lat, "wall": wall, "errors": errors,
+                # steady state: completions between the first completion and the last
+                # scheduled arrival (the ramp before the first answer and the drain after the
+                # last arrival excluded), per second of that window
+                w0, w1 = min(dones), sched[-1]
+                steady = (round(sum(w0 <= d <= w1 for d in dones) / (w1 - w0), 2) if w1 - w0 > 1.0 else None)
+                results.append({"rate": rate, "lat": lat, "wall": wall, "errors": errors, "steady": steady,
+                                "steady_window_s": round(max(0.0, w1 - w0), 2),
                                 "empty_answers": empty, "retried_connections": retried,
                                 "send_lag_ms_p50": round(1e3 * lags[len(lags) // 2], 2),
                                 "send_lag_ms_max": round(1e3 * lags[-1], 2),
@@ -212,7 +220,8 @@ def run_launch(a, mode: str) -> list[dict]:
         shutil.rmtree(work, ignore_errors=True)
     return [{"metric": "serving_qa_queries_per_sec", "entry": "services.launch (HTTP POST /ask/)",
              "mode": mode, "offered_rate": res["rate"], "value": round(a.requests / res["wall"], 2),
-             "unit": "queries/s", **_pcts(res["lat"]), "errors": res["errors"],
+             "unit": "queries/s", "steady_state_qps": res["steady"], "steady_window_s": res["steady_window_s"],
+             **_pcts(res["lat"]), "errors": res["errors"],
              "empty_answers": res["empty_answers"], "retried_connections": res["retried_connections"],
              "server_split_p50": res["server"], "send_lag_ms_p50": res["send_lag_ms_p50"],
              "send_lag_ms_max": res["send_lag_ms_max"],

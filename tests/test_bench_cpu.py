@@ -101,3 +101,4 @@ def test_serving_bench_through_service_launcher():
     out = json.loads(r.stdout.strip().splitlines()[-1])
     assert out["errors"] == 0 and out["requests"] == 16 and out["tp"] == 2
     assert out["entry"].startswith("services.launch") and out["p50_latency_ms"] > 0
+    assert "steady_state_qps" in out and out["steady_window_s"] >= 0
