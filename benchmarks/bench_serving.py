@@ -99,6 +99,10 @@ def run_launch(a, mode: str) -> list[dict]:
            "--kv-mem-fraction", str(a.kv_mem_fraction)]
     if a.tiny:
         cmd.append("--tiny")
+    if a.launch_prefix:        # e.g. a rocprofv3 kernel trace of the service process
+        import shlex
+
+        cmd = shlex.split(a.launch_prefix) + cmd
     log = open(a.server_log, "w") if a.server_log else subprocess.DEVNULL
     proc = subprocess.Popen(cmd, cwd=str(ROOT), env=env, stdout=log, stderr=subprocess.STDOUT,
                             start_new_session=True)
@@ -254,6 +258,8 @@ def main():
     ap.add_argument("--run-timeout", type=float, default=600.0, help="launch entry: seconds per offered rate")
     ap.add_argument("--tiny", action="store_true", help="tiny random models (CPU functional run)")
     ap.add_argument("--server-log", default="", help="file for the launcher's output")
+    ap.add_argument("--launch-prefix", default="", help="launch entry: command prepended to the service "
+                    "launcher (e.g. 'rocprofv3 --kernel-trace -d DIR -o run --output-format csv --')")
     a = ap.parse_args()
     a.rates = [float(x) for x in a.rate.split(",")]
     a.rate = a.rates[0]

@@ -271,7 +271,10 @@ class LLMEngine:
         self.kv = KVCache(self.cfg.layers, num_blocks, model.hkv, self.cfg.head_dim, block_size,
                           self.device, model.dtype)
         self.use_graphs = use_graphs and self.device.type == "cuda"
-        self.tune_decode_gemms = os.environ.get("DOCQA_TUNE_DECODE", "1") == "1"
+        # TunableOp search for the decode buckets' library GEMMs (only the LM head below the
+        # mid-M rows is left on hipBLASLt): off by default -- ~28 s of service start-up for no
+        # measurable step time (docs/CONFIG.md)
+        self.tune_decode_gemms = os.environ.get("DOCQA_TUNE_DECODE", "0") == "1"
         # reuse KV blocks of shared prompt prefixes (the fixed RAG instruction template)
         self.prefix_cache = prefix_cache and os.environ.get("DOCQA_PREFIX_CACHE", "1") == "1"
         # cascade decode attention (csrc/include/docqa_cascade.h): when every sequence of a
@@ -487,6 +490,12 @@ class LLMEngine:
         # Prefill shapes vary per batch and keep the default heuristics.
         tune = self.tune_decode_gemms
         tunable = getattr(torch.cuda, "tunable", None)
+        import logging
+        import threading
+
+        logging.getLogger("docqa.engine").info("decode graph capture: bucket %d cascade %s greedy %s (thread %s)",
+                                               g.bp, getattr(g, "cascade", None), getattr(g, "greedy", None),
+                                               threading.current_thread().name)
         if tune and tunable is not None:
             tunable.enable(True)
             tunable.tuning_enable(True)
