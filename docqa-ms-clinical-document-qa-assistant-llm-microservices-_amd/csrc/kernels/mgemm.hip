@@ -554,8 +554,9 @@ int docqa_mgemm_argmax(const void* X, const void* W, int64_t* out, float* outv, 
 // vmcnt 0 -> relaxed agent fetch_add of the phase counter.  Consume: lane 0 polls the
 // previous phase's counter (relaxed agent loads + s_sleep, bounded: a lost wake-up sets the
 // sticky error word and falls through instead of hanging the GPU) -> agent acquire fence ->
-// barrier.  The launcher zeroes the ticket / phase words with a memset node before every
-// launch (§6 Guideline 16 "Re-initialise every call"); the last workgroup out resets them too.
+// barrier.  The last workgroup out resets the ticket / phase words, so a captured graph
+// replays the launch with no memset node (a 48-byte memset node captured ahead of the kernel
+// left the words garbled after replays on ROCm 7.2 -- tests/test_chain_gpu.py).
 // Counters (int32, zero before the first launch): [0..5] items done per phase, [8] ticket,
 // [9] workgroups exited, [12] sticky error flag (never reset by the kernel).
 namespace {
@@ -729,9 +730,6 @@ int docqa_mgemm_chain(const void* attn, const void* w_o, float* p_o, void* resid
               (uint16_t*)x1, (const uint16_t*)w_gu, (uint16_t*)g, (const uint16_t*)w_down, p_d,
               (const uint16_t*)next_norm, (uint16_t*)x2, (const uint16_t*)w_qkv, p_q, counters, trace,
               M, H, Ko, N2I, Nq, S_o, S_d, w_qkv ? S_q : 1, cfg_o, cfg_d, w_qkv ? cfg_q : 2, eps};
-  // zero the ticket / phase words every call (a memset node under capture): the kernel's own
-  // reset at exit is then only belt and braces, and an aborted launch cannot poison the next
-  if (hipMemsetAsync(counters, 0, 12 * sizeof(int), s) != hipSuccess) return -1;
   mgemm_chain_kernel<<<chain_grid(), 512, 0, s>>>(a);
   DOCQA_CHECK_LAUNCH();
   return 0;

@@ -497,3 +497,19 @@ def test_chat_messages_framing_matches_chat_prompt():
     assert t.chat_messages([{"role": "user", "content": "Bonjour"}]) == t.chat_prompt("Bonjour")
     assert (t.chat_messages([{"role": "system", "content": "Sys"}, {"role": "user", "content": "Q"}])
             == t.chat_prompt("Q", system="Sys"))
+
+
+def test_ollama_options_mapping():
+    """Ollama ``options`` -> SamplingParams: num_predict caps (and -1 fills) the context
+    room, temperature defaults to the service's (0 = the reference's ChatOllama setting)."""
+    from docqa_amd.services.ollama_api import sampling_from_options
+
+    st = Settings()
+    st.max_new_tokens, st.temperature = 128, 0.0
+    p = sampling_from_options(None, st, max_context=1024, prompt_len=100)
+    assert p.max_new_tokens == 128 and p.temperature == 0.0 and p.stop_on_eos
+    p = sampling_from_options({"num_predict": -1, "temperature": 0.7, "top_k": 40, "top_p": 0.9, "seed": 7},
+                              st, max_context=1024, prompt_len=1000)
+    assert p.max_new_tokens == 24 and p.temperature == 0.7 and p.top_k == 40 and p.top_p == 0.9 and p.seed == 7
+    assert sampling_from_options({"num_predict": 5000}, st, 1024, 100).max_new_tokens == 924
+    assert sampling_from_options({"num_predict": 0}, st, 1024, 100).max_new_tokens == 1
