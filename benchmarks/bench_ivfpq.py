@@ -179,8 +179,12 @@ def bench_bge_indexer(a):
                           "type": "patient_file", "patient_id": note["patient_id"]})
         i += 1
         if len(batch) >= 8192 or n_chunks + len(batch) >= a.n:
+            before = n_chunks
             n_chunks += idx.add_records(batch[: a.n - n_chunks], log=False)
             batch = []
+            if n_chunks // 500_000 != before // 500_000:   # a live line every ~25 s at scale
+                print(f"[bench_ivfpq] {n_chunks} chunks indexed, {time.perf_counter() - t:.0f} s",
+                      file=sys.stderr, flush=True)
     torch.cuda.synchronize()
     build_s = time.perf_counter() - t
     store = idx.index
