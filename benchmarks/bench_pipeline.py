@@ -47,6 +47,8 @@ def main():
     ap.add_argument("--max-new-tokens", type=int, default=128)
     ap.add_argument("--max-context", type=int, default=2048)
     ap.add_argument("--k", type=int, default=3)
+    ap.add_argument("--kv-mem-fraction", type=float, default=0.85,
+                    help="KV pool = this fraction of the HBM free after the weights (0: max_batch full contexts)")
     ap.add_argument("--pipelined", action="store_true",
                     help="overlap batch i+1's embed/search with batch i's decode tail")
     ap.add_argument("--device", default="cuda")
@@ -165,7 +167,10 @@ def main():
     model = ck.resolve_llama(a.llm, device=dev, seed=0)
     note(f"{a.llm} shard built (TP {tp})")
     llm_cfg = model.cfg
-    engine = LLMEngine(model, max_batch=a.batch, max_context=a.max_context, use_graphs=cuda)
+    # KV pool from the HBM left after the weights (the Llama-3-70B weights alone are 141 GB:
+    # max_batch full contexts no longer fit beside them at batch 256)
+    engine = LLMEngine(model, max_batch=a.batch, max_context=a.max_context, use_graphs=cuda,
+                       kv_mem_fraction=(a.kv_mem_fraction or None) if cuda else None)
     chat_tok = ChatTokenizer(model_vocab=llm_cfg.vocab_size)
     pipe = RAGPipeline(encoder, enc_tok, index, all_records, engine, chat_tok, k=a.k,
                        max_prompt_tokens=a.max_context - a.max_new_tokens - 64)
