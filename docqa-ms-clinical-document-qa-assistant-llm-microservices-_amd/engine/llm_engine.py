@@ -266,7 +266,19 @@ class LLMEngine:
             if kv_mem_fraction is None and os.environ.get("DOCQA_KV_MEM_FRACTION"):
                 kv_mem_fraction = float(os.environ["DOCQA_KV_MEM_FRACTION"])
             if kv_mem_fraction and self.device.type == "cuda":
-                num_blocks = max(num_blocks, self._blocks_from_free_memory(model, block_size, kv_mem_fraction))
+                # the HBM budget decides; when even max_batch full contexts do not fit beside the
+                # weights (Llama-3-70B at batch 256: 8193 blocks = 164 GB next to 141 GB) the pool
+                # is the budget: blocks are reserved per actual prompt + generation, admission
+                # waits / the scheduler preempts when it runs out -- it must hold at least one
+                # full-context sequence
+                fb = self._blocks_from_free_memory(model, block_size, kv_mem_fraction)
+                if num_blocks <= self._blocks_from_free_memory(model, block_size, 0.95):
+                    num_blocks = max(num_blocks, fb)       # the full-context pool fits: never less
+                elif fb >= self.max_blocks_per_seq + 1:
+                    num_blocks = fb
+                else:
+                    raise MemoryError(f"KV pool: {fb} blocks fit in {kv_mem_fraction:.2f} of the free HBM, "
+                                      f"one {self.max_context}-token sequence needs {self.max_blocks_per_seq + 1}")
         num_blocks = self._agree_across_tp(model, num_blocks)
         self.kv = KVCache(self.cfg.layers, num_blocks, model.hkv, self.cfg.head_dim, block_size,
                           self.device, model.dtype)
