@@ -68,6 +68,11 @@ def init_distributed(tp_size: int = 1, backend: str | None = None, timeout_s: in
         backend = "nccl" if torch.cuda.is_available() else "gloo"
     os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
     os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    if os.environ["MASTER_ADDR"] in ("127.0.0.1", "localhost") and os.path.exists("/sys/class/net/lo"):
+        # single node: gloo (the process group of CPU / shared-GPU runs and the side groups
+        # of RCCL runs) otherwise binds the interface the hostname resolves to, which in a
+        # container may be unreachable -- a rank then joins the mesh with 0 peers
+        os.environ.setdefault("GLOO_SOCKET_IFNAME", "lo")
     if backend == "nccl":
         torch.cuda.set_device(local_rank)
     if not dist.is_initialized():
