@@ -52,7 +52,13 @@ def test_tp_matches_tp1(tmp_path, preset, tp):
            "--master-addr", "127.0.0.1", "--master-port", str(_port()), str(ROOT / "tests" / "tp_gpu_worker.py"),
            str(sd_path), str(out_path), preset, str(tp)]
     r = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=600, env=env)
-    assert r.returncode == 0, (r.stdout[-2000:], r.stderr[-4000:])
+    if r.returncode != 0:
+        # the workers' tracebacks sit in the middle of torchrun's output: keep all of it
+        dump = ROOT / "gpurun_out" / f"tp_gpu_worker_{preset}_{tp}.log"
+        dump.parent.mkdir(exist_ok=True)
+        dump.write_text(r.stdout + "\n---- stderr ----\n" + r.stderr)
+        errs = [ln for ln in r.stderr.splitlines() if "Error" in ln or "error" in ln]
+        raise AssertionError(f"torchrun rc {r.returncode}; error lines: {errs[:12]}; full log: {dump}")
     out = torch.load(out_path, weights_only=True)
     assert _rel(out["prefill"], p1.float().cpu()) < 0.03
     assert _rel(out["decode"], d1.float().cpu()) < 0.03
