@@ -51,6 +51,24 @@ def test_bench_two_ranks_gloo_sharded_index():
     assert d["n_gpus"] == 2 and d["config"]["global_batch"] == 6 and d["config"]["parallelism"] == "dp2"
 
 
+def test_bench_eight_ranks_gloo_sharded_index():
+    """The driver's 8-GPU scaling command shape (torchrun --nproc-per-node 8 bench.py --gpus 8)
+    rehearsed on gloo: 8 data-parallel ranks, the index sharded x8 (all-gather of queries and
+    top-k), MAX-over-ranks timing, one JSON line with the whole-job aggregate."""
+    env = dict(os.environ)
+    for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
+        env.pop(k, None)
+    env["OMP_NUM_THREADS"] = "1"
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "8",
+           "--master-addr", "127.0.0.1", "--master-port", str(_port()), str(ROOT / "bench.py"),
+           "--gpus", "8", *ARGS]
+    r = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=900, env=env)
+    assert r.returncode == 0, r.stderr[-3000:]
+    d = _last_json(r.stdout)
+    assert d["n_gpus"] == 8 and d["config"]["global_batch"] == 24 and d["config"]["parallelism"] == "dp8"
+    assert d["value"] > 0 and d["workload"]["unique_question_frac"] == 1.0
+
+
 def test_pipeline_bench_tp2_gloo_sharded_index():
     """Config-5 pipeline benchmark (ingest -> deid -> embed -> sharded kNN -> TP generate)
     as 2 gloo ranks: TP=2 generator, index sharded over both ranks with replicated queries."""
