@@ -87,6 +87,10 @@ class Settings:
     # synthese
     semantic_indexer_url: str = field(default_factory=lambda: os.getenv("SEMANTIC_INDEXER_URL", "http://semantic-indexer:8003"))
     llm_qa_url: str = field(default_factory=lambda: os.getenv("LLM_QA_URL", "http://llm-qa:8004"))
+    # clinical UI back ends (the reference UI's hard-coded localhost ports; containers set
+    # the service names, deploy/docker-compose.yml)
+    ui_ingest_url: str = field(default_factory=lambda: os.getenv("DOC_INGESTOR_URL", "http://127.0.0.1:8000"))
+    ui_qa_url: str = field(default_factory=lambda: os.getenv("UI_LLM_QA_URL", "http://127.0.0.1:8001"))
     use_fake_retrieval: bool = field(default_factory=lambda: env_bool("USE_FAKE_RETRIEVAL", "true"))
     use_fake_llm: bool = field(default_factory=lambda: env_bool("USE_FAKE_LLM", "true"))
     fake_max_chars: int = 1200

@@ -41,7 +41,10 @@ using namespace docqa;
 namespace {
 constexpr int kMaxRanks = 8;
 constexpr int kMaxWG = 256;
-constexpr unsigned kSpinLimit = 1u << 24;
+// bounded wait for a peer (~2^27 x s_sleep 2 = ~7 s at 2.4 GHz): ~1 s (2^24) was hit by a
+// 4-rank TP test sharing ONE GPU, whose processes' queues the scheduler time-slices, while
+// every peer was alive; one process per GPU (deployment) arrives within microseconds
+constexpr unsigned kSpinLimit = 1u << 27;
 constexpr size_t kFlagBytes = (size_t)2 * kMaxWG * kMaxRanks * sizeof(unsigned);
 
 enum { ONESHOT = 0, TWOSHOT = 1, GATHER = 2 };

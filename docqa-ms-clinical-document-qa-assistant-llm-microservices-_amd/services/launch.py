@@ -190,7 +190,7 @@ def run_parallel(a, opts: "StackOptions") -> None:
     comm.destroy()
 
 
-def main() -> None:
+def build_parser() -> argparse.ArgumentParser:
     ap = argparse.ArgumentParser()
     ap.add_argument("--device", default="cuda")
     ap.add_argument("--host", default="127.0.0.1")
@@ -207,7 +207,11 @@ def main() -> None:
     ap.add_argument("--preload-notes", type=int, default=0,
                     help="index this many synthetic clinical notes at start (serving benchmarks, demos)")
     ap.add_argument("--kv-mem-fraction", type=float, default=0.8, help="KV pool share of free HBM")
-    a = ap.parse_args()
+    return ap
+
+
+def main() -> None:
+    a = build_parser().parse_args()
     import os
     import sys
 

@@ -147,7 +147,7 @@ class DocQAStack:
             else:   # FAKE / REAL-over-HTTP per USE_FAKE_* and the service URLs (reference behaviour)
                 self.synthese_app = synthese.create_app(self.st)
         if "ui" in svc:
-            self.ui_app = ui.create_app()
+            self.ui_app = ui.create_app(self.st.ui_ingest_url, self.st.ui_qa_url)
 
     def close(self) -> None:
         if self.deid is not None:
