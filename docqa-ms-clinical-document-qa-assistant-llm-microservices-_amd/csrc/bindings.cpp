@@ -775,6 +775,92 @@ std::tuple<at::Tensor, at::Tensor> mgemm_argmax_val(const at::Tensor& x, const a
   return {out, outv};
 }
 
+// mid-M decode GEMM, weights in VGPRs (wgemm.hip): splits == 1 -> bf16 [.., N]; splits > 1 ->
+// fp32 split-K slabs [S, M, N]
+at::Tensor wgemm(const at::Tensor& x, const at::Tensor& w, int64_t splits, int64_t cfg) {
+  CHECK_GPU(x); CHECK_BF16(x); CHECK_BF16(w); CHECK_CONTIG(x); CHECK_CONTIG(w);
+  CHECK_ALIGN16(x); CHECK_ALIGN16(w);
+  const int K = x.size(-1), N = w.size(0);
+  TORCH_CHECK(w.size(1) == K, "wgemm: K mismatch");
+  const int M = x.numel() / K;
+  TORCH_CHECK(splits >= 1, "wgemm: splits >= 1");
+  TORCH_CHECK((int64_t)std::max(M, N) * K < (1LL << 30), "wgemm: 32-bit byte offsets");
+  c10::DeviceGuard g(x.device());
+  at::Tensor out;
+  if (splits == 1) {
+    auto sizes = x.sizes().vec();
+    sizes.back() = N;
+    out = at::empty(sizes, x.options());
+    CHECK_RC(docqa_wgemm(x.data_ptr(), w.data_ptr(), out.data_ptr(), nullptr, M, N, K, 1, (int)cfg, stream()),
+             "wgemm");
+  } else {
+    out = at::empty({splits, M, N}, x.options().dtype(at::kFloat));
+    CHECK_RC(docqa_wgemm(x.data_ptr(), w.data_ptr(), nullptr, out.data_ptr<float>(), M, N, K, (int)splits,
+                         (int)cfg, stream()), "wgemm");
+  }
+  return out;
+}
+
+int64_t wgemm_tile_n(int64_t cfg) { return docqa_wgemm_tile_n((int)cfg); }
+
+// gate|up + SwiGLU: x [M, K], w [2I, K] (8-interleaved) -> [M, I]; splits 2 needs the
+// hand-off workspace: ws fp32 [m-tiles x N x 256] partial tiles, tick int32 [2 T + 1]
+// (T = m-tiles x N / tile_n tickets, then the sticky error word), tickets zeroed once and
+// re-armed by the kernel
+at::Tensor wgemm_glu(const at::Tensor& x, const at::Tensor& w, int64_t splits, int64_t cfg,
+                     const c10::optional<at::Tensor>& ws, const c10::optional<at::Tensor>& tick) {
+  CHECK_GPU(x); CHECK_BF16(x); CHECK_BF16(w); CHECK_CONTIG(x); CHECK_CONTIG(w);
+  CHECK_ALIGN16(x); CHECK_ALIGN16(w);
+  const int K = x.size(-1), N = w.size(0);
+  TORCH_CHECK(w.size(1) == K && N % 16 == 0, "wgemm_glu: shape mismatch");
+  const int M = x.numel() / K;
+  TORCH_CHECK((int64_t)std::max(M, N) * K < (1LL << 30), "wgemm_glu: 32-bit byte offsets");
+  TORCH_CHECK(splits == 1 || splits == 2, "wgemm_glu: splits 1 or 2");
+  float* wsp = nullptr;
+  int* tk = nullptr;
+  int* err = nullptr;
+  if (splits == 2) {
+    TORCH_CHECK(ws.has_value() && tick.has_value(), "wgemm_glu: splits 2 needs ws and tick");
+    CHECK_GPU(*ws); CHECK_GPU(*tick); CHECK_I32(*tick); CHECK_CONTIG(*ws); CHECK_CONTIG(*tick);
+    TORCH_CHECK(ws->scalar_type() == at::kFloat, "wgemm_glu: ws must be fp32");
+    const int bn = docqa_wgemm_tile_n((int)cfg);
+    TORCH_CHECK(bn > 0 && N % bn == 0, "wgemm_glu: N must be a multiple of the tile");
+    const int64_t tiles = ((M + 255) / 256) * (N / bn);
+    TORCH_CHECK(ws->numel() >= docqa_wgemm_glu_ws_floats(M, N, (int)cfg) && tick->numel() >= 2 * tiles + 1,
+                "wgemm_glu: workspace too small");
+    wsp = ws->data_ptr<float>();
+    tk = tick->data_ptr<int>();
+    err = tk + 2 * tiles;
+  }
+  auto sizes = x.sizes().vec();
+  sizes.back() = N / 2;
+  c10::DeviceGuard g(x.device());
+  auto out = at::empty(sizes, x.options());
+  CHECK_RC(docqa_wgemm_glu(x.data_ptr(), w.data_ptr(), out.data_ptr(), wsp, tk, err, M, N, K, (int)splits, (int)cfg,
+                           stream()), "wgemm_glu");
+  return out;
+}
+
+// LM head + greedy pick on wgemm: argmax over the first n_valid columns of bf16(x . w^T)
+std::tuple<at::Tensor, at::Tensor> wgemm_argmax_val(const at::Tensor& x, const at::Tensor& w, int64_t n_valid,
+                                                    int64_t cfg) {
+  CHECK_GPU(x); CHECK_BF16(x); CHECK_BF16(w); CHECK_CONTIG(x); CHECK_CONTIG(w);
+  CHECK_ALIGN16(x); CHECK_ALIGN16(w);
+  const int K = x.size(-1), N = w.size(0), bn = docqa_wgemm_tile_n((int)cfg);
+  TORCH_CHECK(w.size(1) == K && bn > 0 && N % bn == 0, "wgemm_argmax: shape mismatch");
+  const int M = x.numel() / K;
+  TORCH_CHECK((int64_t)std::max(M, N) * K < (1LL << 30), "wgemm_argmax: 32-bit byte offsets");
+  c10::DeviceGuard g(x.device());
+  auto out = at::empty({M}, x.options().dtype(at::kLong));
+  auto outv = at::empty({M}, x.options().dtype(at::kFloat));
+  auto ws_v = at::empty({M, N / bn}, x.options().dtype(at::kFloat));
+  auto ws_i = at::empty({M, N / bn}, x.options().dtype(at::kInt));
+  CHECK_RC(docqa_wgemm_argmax(x.data_ptr(), w.data_ptr(), out.data_ptr<int64_t>(), outv.data_ptr<float>(),
+                              ws_v.data_ptr<float>(), ws_i.data_ptr<int>(), M, N, K, (int)n_valid, (int)cfg, stream()),
+           "wgemm_argmax");
+  return {out, outv};
+}
+
 // prefill GEMM (pgemm.hip, 256 x 256 tiles): epi 0 -> x . w^T bf16 [.., N]; epi 1 -> fused
 // SwiGLU over 8-interleaved gate|up rows -> [.., N / 2]
 at::Tensor pgemm(const at::Tensor& x, const at::Tensor& w, int64_t epi) {
@@ -926,10 +1012,10 @@ void ar_ipc_close(int64_t ptr) { TORCH_CHECK(docqa_ar_ipc_close((void*)(uintptr_
 // else the all-reduced sum.  mode 0 one-shot, 1 two-shot (kernels/allreduce.hip).
 at::Tensor ar_run(const at::Tensor& x, bool slabs, const c10::optional<at::Tensor>& residual,
                   const c10::optional<at::Tensor>& w, double eps, int64_t rank, std::vector<int64_t> regions,
-                  int64_t max_elems, int64_t mode, at::Tensor ctr, at::Tensor err) {
+                  int64_t max_elems, int64_t mode, at::Tensor ctr, at::Tensor err, int64_t timeout_us) {
   CHECK_GPU(x); CHECK_CONTIG(x); CHECK_ALIGN16(x);
-  TORCH_CHECK(ctr.scalar_type() == at::kInt && ctr.numel() >= 2 && err.scalar_type() == at::kInt,
-              "ctr int32[2] / err int32[1]");
+  TORCH_CHECK(ctr.scalar_type() == at::kInt && ctr.numel() >= 4 && err.scalar_type() == at::kInt,
+              "ctr int32[4] / err int32[1]");
   TORCH_CHECK(regions.size() >= 1 && regions.size() <= 8, "1..8 ranks");
   const int H = x.size(-1);
   int S = 0, M;
@@ -962,7 +1048,7 @@ at::Tensor ar_run(const at::Tensor& x, bool slabs, const c10::optional<at::Tenso
   CHECK_RC(docqa_ar_run(x.data_ptr(), S, out.data_ptr(), fused ? residual->data_ptr() : nullptr,
                         fused ? w->data_ptr() : nullptr, (float)eps, M, H, (int)rank, (int)regions.size(),
                         ptrs.data(), (size_t)max_elems, (int)mode, (unsigned*)ctr.data_ptr(),
-                        (unsigned*)err.data_ptr(), stream()), "ar_run");
+                        (unsigned*)err.data_ptr(), (long long)timeout_us, stream()), "ar_run");
   return out;
 }
 
@@ -1007,11 +1093,15 @@ TORCH_LIBRARY(docqa, m) {
         "int cfg_q, float eps, Tensor? trace=None) "
         "-> (Tensor, Tensor)");
   m.def("mgemm_argmax(Tensor x, Tensor w, int n_valid, int cfg=0) -> Tensor");
+  m.def("wgemm(Tensor x, Tensor w, int splits, int cfg=0) -> Tensor");
+  m.def("wgemm_glu(Tensor x, Tensor w, int splits, int cfg=0, Tensor? ws=None, Tensor? tick=None) -> Tensor");
+  m.def("wgemm_argmax_val(Tensor x, Tensor w, int n_valid, int cfg=0) -> (Tensor, Tensor)");
   m.def("pgemm(Tensor x, Tensor w, int epi=0) -> Tensor");
   m.def("pgemm_partial(Tensor x, Tensor w, int splits) -> Tensor");
   m.def("mgemm_argmax_val(Tensor x, Tensor w, int n_valid, int cfg=0) -> (Tensor, Tensor)");
   m.def("pgemm_ok(int M, int N, int K) -> bool", &pgemm_ok);
   m.def("group_persist_bins(int cap, int Hkv) -> int", &group_persist_bins);
+  m.def("wgemm_tile_n(int cfg) -> int", &wgemm_tile_n);
   m.def("paged_decode_cascade(Tensor q, Tensor k_cache, Tensor v_cache, Tensor block_tables, "
         "Tensor context_lens, int Hq, int max_context, float scale, Tensor prefix_table, Tensor prefix_len, "
         "int nchunk, Tensor? order=None) -> Tensor");
@@ -1030,7 +1120,7 @@ TORCH_LIBRARY(docqa, m) {
         "Tensor(a!) k_cache, Tensor(b!) v_cache, Tensor block_tables, Tensor context_lens, int Hq, "
         "int max_context, float scale, Tensor? order=None) -> Tensor");
   m.def("ar_run(Tensor x, bool slabs, Tensor(r!)? residual, Tensor? w, float eps, int rank, int[] regions, "
-        "int max_elems, int mode, Tensor(a!) ctr, Tensor(b!) err) -> Tensor");
+        "int max_elems, int mode, Tensor(a!) ctr, Tensor(b!) err, int timeout_us=500000) -> Tensor");
   m.def("ar_region_bytes(int max_elems) -> int", &ar_region_bytes);
   m.def("ar_alloc(int bytes) -> int", &ar_alloc);
   m.def("ar_free(int ptr) -> ()", &ar_free);
@@ -1074,6 +1164,9 @@ TORCH_LIBRARY_IMPL(docqa, CUDA, m) {
   m.impl("pgemm", &pgemm);
   m.impl("pgemm_partial", &pgemm_partial);
   m.impl("mgemm_argmax_val", &mgemm_argmax_val);
+  m.impl("wgemm", &wgemm);
+  m.impl("wgemm_glu", &wgemm_glu);
+  m.impl("wgemm_argmax_val", &wgemm_argmax_val);
   m.impl("paged_decode_fused", &paged_decode_fused);
   m.impl("paged_decode_cascade", &paged_decode_cascade);
   m.impl("paged_decode_cascade_rope", &paged_decode_cascade_rope);

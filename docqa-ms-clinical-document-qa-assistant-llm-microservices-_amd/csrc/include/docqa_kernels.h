@@ -105,7 +105,7 @@ int docqa_ar_ipc_open(const void* handle, void** ptr);
 int docqa_ar_ipc_close(void* ptr);
 int docqa_ar_run(const void* in, int S, void* out, void* residual, const void* w, float eps, int M, int H,
                  int rank, int nranks, void* const* regions, size_t max_elems, int mode, unsigned* ctr,
-                 unsigned* err, hipStream_t s);
+                 unsigned* err, long long timeout_us, hipStream_t s);
 int docqa_paged_decode_fused(const float* P, int S, const int* positions, const float* cos_sin,
                              const int* slot_mapping, void* k_cache, void* v_cache,
                              const int* block_tables, int maxb, const int* context_lens, void* out,
@@ -123,6 +123,17 @@ int docqa_mgemm_glu(const void* X, const void* W, void* Y, int M, int N, int K, 
 int docqa_mgemm_argmax(const void* X, const void* W, int64_t* out, float* outv, float* ws_v, int* ws_i, int M,
                        int N, int K, int n_valid, int cfg, hipStream_t s);
 int docqa_mgemm_tile_n(int cfg);
+// mid-M decode GEMM with the weights streamed into VGPRs (wgemm.hip): X-only LDS ring,
+// 256 x 256 tiles; split-K slabs / bf16 / fused SwiGLU (S = 1, or 2 with an in-launch
+// K-half hand-off through ws + tick) / fused LM-head argmax
+int docqa_wgemm(const void* X, const void* W, void* Y, float* P, int M, int N, int K, int S, int cfg,
+                hipStream_t s);
+long long docqa_wgemm_glu_ws_floats(int M, int N, int cfg);
+int docqa_wgemm_glu(const void* X, const void* W, void* Y, float* ws, int* tick, int* err, int M, int N, int K,
+                    int S, int cfg, hipStream_t s);
+int docqa_wgemm_argmax(const void* X, const void* W, int64_t* out, float* outv, float* ws_v, int* ws_i, int M, int N,
+                       int K, int n_valid, int cfg, hipStream_t s);
+int docqa_wgemm_tile_n(int cfg);
 // persistent decode-layer chain (mgemm.hip): O -> add+RMSNorm -> gate|up+SwiGLU -> down ->
 // add+RMSNorm [-> next layer's QKV slabs] in one launch; counters: int32 [16], zeroed once
 int docqa_mgemm_chain(const void* attn, const void* w_o, float* p_o, void* residual, const void* post_norm,

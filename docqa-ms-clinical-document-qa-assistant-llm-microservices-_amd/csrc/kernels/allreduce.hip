@@ -31,8 +31,11 @@
 // previous kernel -- all its reads of that half -- has completed.  Staging and flags are
 // allocated uncached (hipDeviceMallocUncached): remote reads and writes over xGMI bypass
 // the caches; flag stores / loads are system-scope release / acquire atomics.  Spins give
-// up after a bound and set an error word instead of hanging the GPU (every grid is
-// <= 256 workgroups of 256 threads: all resident).
+// up after a wall-clock bound (``timeout``, host-set: sub-second in deployment) and record
+// WHICH peer was late in the error word instead of hanging the GPU (every grid is <= 256
+// workgroups of 256 threads: all resident); the longest wait of the call is kept in ctr[2]
+// (us) for skew diagnostics.  The host reads the word once per engine step
+// (parallel/custom_ar.py) and fails the step loudly.
 #include "docqa_common.h"
 #include <cstring>
 
@@ -41,10 +44,6 @@ using namespace docqa;
 namespace {
 constexpr int kMaxRanks = 8;
 constexpr int kMaxWG = 256;
-// bounded wait for a peer (~2^27 x s_sleep 2 = ~7 s at 2.4 GHz): ~1 s (2^24) was hit by a
-// 4-rank TP test sharing ONE GPU, whose processes' queues the scheduler time-slices, while
-// every peer was alive; one process per GPU (deployment) arrives within microseconds
-constexpr unsigned kSpinLimit = 1u << 27;
 constexpr size_t kFlagBytes = (size_t)2 * kMaxWG * kMaxRanks * sizeof(unsigned);
 
 enum { ONESHOT = 0, TWOSHOT = 1, GATHER = 2 };
@@ -64,8 +63,10 @@ struct ArArgs {
   float eps;
   int M, H, rank, nranks;
   size_t half_elems;              // elements of one [in | result] area
-  unsigned* ctr;                  // [0] epoch of the last call, [1] finished workgroups
-  unsigned* err;
+  unsigned* ctr;                  // [0] epoch of the last call, [1] finished workgroups, [2] max wait (us)
+  unsigned* err;                  // first error: 1 | late peer << 1 | phase << 4 | (epoch & 0xffffff) << 8
+  unsigned long long timeout;     // wall-clock ticks a workgroup waits for a peer before giving up
+  unsigned ticks_per_us;
 };
 
 __device__ __forceinline__ void publish(const ArPeers& peers, int phase, int wg, int rank, int nranks,
@@ -78,17 +79,21 @@ __device__ __forceinline__ void publish(const ArPeers& peers, int phase, int wg,
 }
 
 __device__ __forceinline__ void wait_peers(const ArPeers& peers, int phase, int wg, int rank, int nranks,
-                                           unsigned epoch, unsigned* err) {
+                                           unsigned epoch, const ArArgs& a) {
   if ((int)threadIdx.x < nranks) {
     const unsigned* slot = peers.flags[rank] + ((size_t)phase * kMaxWG + wg) * kMaxRanks + threadIdx.x;
-    unsigned spins = 0;
+    const unsigned long long t0 = wall_clock64();
+    unsigned long long t = t0;
     while ((int)(__hip_atomic_load(slot, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) - epoch) < 0) {
       __builtin_amdgcn_s_sleep(2);
-      if (++spins > kSpinLimit) {
-        atomicOr(err, 1u);
+      t = wall_clock64();
+      if (t - t0 > a.timeout) {
+        // keep the FIRST failure's detail: which peer (threadIdx.x), which phase, which call
+        atomicCAS(a.err, 0u, 1u | (threadIdx.x << 1) | ((unsigned)phase << 4) | ((epoch & 0xffffffu) << 8));
         break;
       }
     }
+    if (t != t0) atomicMax(a.ctr + 2, (unsigned)((t - t0) / a.ticks_per_us));
   }
   __syncthreads();
   __atomic_thread_fence(__ATOMIC_ACQUIRE);   // system scope: no stale peer lines below
@@ -152,7 +157,7 @@ __global__ __launch_bounds__(256) void allreduce_kernel(ArArgs a, ArPeers peers)
     }
   }
   publish(peers, 0, wg, a.rank, a.nranks, epoch);
-  wait_peers(peers, 0, wg, a.rank, a.nranks, epoch, a.err);
+  wait_peers(peers, 0, wg, a.rank, a.nranks, epoch, a);
 
   if constexpr (MODE == GATHER) {
     // all-gather of raw 16-B words: out[p] <- rank p's rows (bit-exact copies)
@@ -176,8 +181,15 @@ __global__ __launch_bounds__(256) void allreduce_kernel(ArArgs a, ArPeers peers)
 #pragma unroll
           for (int e = 0; e < 8; ++e) v[e] += x[e];
         }
-        if constexpr (FUSED) ss += fused_add(a, off, v);
-        else *reinterpret_cast<uint4*>(a.out + off) = pack8(v);
+        if constexpr (FUSED) {
+          // round the cross-rank sum to bf16 first, as the two-shot path (its reduced chunk
+          // is stored bf16), the RCCL fallback and TP = 1 do: bf16(bf16(sum) + residual)
+#pragma unroll
+          for (int e = 0; e < 8; ++e) v[e] = bf2f(f2bf(v[e]));
+          ss += fused_add(a, off, v);
+        } else {
+          *reinterpret_cast<uint4*>(a.out + off) = pack8(v);
+        }
       }
       if constexpr (FUSED) {
         ss = wave_sum(ss);
@@ -202,7 +214,7 @@ __global__ __launch_bounds__(256) void allreduce_kernel(ArArgs a, ArPeers peers)
       }
     }
     publish(peers, 1, wg, a.rank, a.nranks, epoch);
-    wait_peers(peers, 1, wg, a.rank, a.nranks, epoch, a.err);
+    wait_peers(peers, 1, wg, a.rank, a.nranks, epoch, a);
     // 3'. all-gather of the reduced chunks -> epilogue
     for (int row = r0 + wave; row < r1; row += 4) {
       float ss = 0.f;
@@ -271,10 +283,11 @@ int docqa_ar_ipc_close(void* ptr) { return hipIpcCloseMemHandle(ptr) == hipSucce
 // as mapped in this process).  in: bf16 [M, H] (S == 0) or fp32 split-K slabs [S, M, H];
 // residual / w given: fused add + RMSNorm epilogue (residual updated in place, out = the
 // normed rows), else out = the sum.  mode 0 one-shot, 1 two-shot, 2 gather.  ctr: int32 [2]
-// zeroed once, err: int32 [1].
+// zeroed once (+ [2] the longest peer wait in us, [3] spare), err: int32 [1]; timeout_us: how
+// long a workgroup waits for a peer before it records the error and gives up.
 int docqa_ar_run(const void* in, int S, void* out, void* residual, const void* w, float eps, int M, int H,
                  int rank, int nranks, void* const* regions, size_t max_elems, int mode, unsigned* ctr,
-                 unsigned* err, hipStream_t s) {
+                 unsigned* err, long long timeout_us, hipStream_t s) {
   if (M == 0) return 0;
   if (nranks < 1 || nranks > kMaxRanks || rank < 0 || rank >= nranks || H % 8 != 0 || M < 0) return -1;
   if ((size_t)M * H > max_elems) return -1;
@@ -287,8 +300,17 @@ int docqa_ar_run(const void* in, int S, void* out, void* residual, const void* w
     peers.flags[r] = (unsigned*)regions[r];
     peers.data[r] = (uint16_t*)((char*)regions[r] + kFlagBytes);
   }
+  static int khz = 0;   // the constant wall clock behind wall_clock64() (100 MHz on MI355X)
+  if (khz == 0) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, dev) !=
+                                                 hipSuccess || khz <= 0)
+      khz = 100000;
+  }
+  if (timeout_us <= 0) timeout_us = 500000;
+  const unsigned tpu = (unsigned)(khz / 1000 > 0 ? khz / 1000 : 1);
   ArArgs a{in, S, (uint16_t*)out, (uint16_t*)residual, (const uint16_t*)w, eps, M, H, rank, nranks,
-           max_elems, ctr, err};
+           max_elems, ctr, err, (unsigned long long)timeout_us * tpu, tpu};
   // workgroups: one per few rows (4 waves, one row each at a time), <= kMaxWG, all resident;
   // the same count on every rank (a function of M only)
   int G = (M + 3) / 4;

@@ -27,6 +27,7 @@ import numpy as np
 import torch
 
 from .. import ops
+from ..parallel import comm
 from ..utils import tracing
 from ..models.llama import AttnMeta, LlamaModel
 from .kv_cache import KVCache, TailCache, chain_keys
@@ -69,6 +70,8 @@ class Launched:
     params: "SamplingParams"
     t0: float
     t1: float
+    # pinned copy of the TP all-reduce's error word behind the batch's kernels (None at TP 1)
+    ar_err: torch.Tensor | None = None
 
     @property
     def done_event(self):
@@ -775,15 +778,17 @@ class LLMEngine:
             if cuda:
                 host = torch.empty(gen.shape, dtype=gen.dtype, pin_memory=True)
                 host.copy_(gen, non_blocking=True)
-                ev[2].record()
             else:
                 host = gen
+            ar_err = comm.collective_error_snapshot()
+            if cuda:
+                ev[2].record()
         except BaseException:
             self.release(r)
             raise
         self.stats.prompt_tokens += sum(lens)
         self.stats.generated_tokens += B * params.max_new_tokens
-        return Launched(r, host, ev, params, t0, t1)
+        return Launched(r, host, ev, params, t0, t1, ar_err)
 
     def collect(self, h: "Launched") -> list[list[int]]:
         """Wait for a :meth:`launch`ed batch, free its KV blocks and return its tokens."""
@@ -800,6 +805,8 @@ class LLMEngine:
                 t2 = time.perf_counter()
                 self.stats.prefill_s += h.t1 - h.t0
                 self.stats.decode_s += t2 - h.t1
+            # a TP peer that never arrived leaves garbage tokens: fail, never return them
+            comm.raise_on_collective_error(h.ar_err)
             result = h.host.tolist()
         finally:
             self.release(h.reservation)

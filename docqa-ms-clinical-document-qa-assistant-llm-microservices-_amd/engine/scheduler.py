@@ -42,6 +42,8 @@ from dataclasses import dataclass, field
 import torch
 
 from .. import ops
+from ..parallel import comm
+from ..parallel.custom_ar import CollectiveError
 from ..utils import tracing
 from .llm_engine import LLMEngine, SamplingParams, _bucket, _DecodeGraph
 
@@ -203,8 +205,32 @@ class ContinuousEngine:
                     continue
             try:
                 self.step()
+            except CollectiveError as e:
+                # the TP group's state is undefined: fail the requests, then hand the process
+                # to the collective-failure path (parallel/health.py: exit 71, relaunch)
+                self._fail_all(e)
+                self._reset_followers()
+                self.on_collective_error(e)
+                return
             except Exception as e:  # noqa: BLE001 - fail the affected requests, keep serving
                 self._fail_all(e)
+                self._reset_followers()
+
+    def on_collective_error(self, e: Exception) -> None:
+        from ..parallel import health
+
+        health.collective_failure(str(e))
+
+    def _reset_followers(self) -> None:
+        """Lockstep leader after a failed step: tell the followers to drop their running set
+        too, so every rank's next step has the same batch composition (the mirror invariant
+        the TP collectives rely on)."""
+        ls = self.lockstep
+        if ls is not None and ls.leader:
+            try:
+                ls.exchange(("reset",))
+            except Exception:  # noqa: BLE001 - a dead follower: its own exit path handles it
+                pass
 
     def _fail_all(self, e: Exception) -> None:
         self._pending = None
@@ -228,7 +254,10 @@ class ContinuousEngine:
                 new, self._unsynced = self._unsynced, []
                 self.waiting.extend(new)
             decision = self._admission_due()
-            self.lockstep.exchange(("step", [(r.prompt, r.params) for r in new], decision))
+            try:
+                self.lockstep.exchange(("step", [(r.prompt, r.params) for r in new], decision))
+            except Exception as e:  # noqa: BLE001 - a follower is gone: the TP group is broken
+                raise CollectiveError(f"lockstep broadcast failed: {e!r}") from e
         self._step(decision)
 
     def _step(self, decision) -> None:
@@ -252,19 +281,34 @@ class ContinuousEngine:
 
     @torch.inference_mode()
     def follow(self) -> None:
-        """Lockstep follower loop: mirror every step the leader broadcasts until "stop"."""
+        """Lockstep follower loop: mirror every step the leader broadcasts until "stop";
+        "reset" (the leader's step failed) drops the running set as the leader did.  A step
+        that fails HERE cannot be mirrored back, so the follower exits non-zero: the
+        leader's next broadcast then errors instead of its TP collectives hanging."""
         ls = self.lockstep
         while True:
             msg = ls.exchange()
             if msg[0] == "stop":
                 return
+            if msg[0] == "reset":
+                self._fail_all(RuntimeError("leader step failed"))
+                continue
             if msg[0] != "step":
                 continue
             _, specs, decision = msg
             for prompt, params in specs:
                 self.waiting.append(Request(next(self._ids), list(prompt), params, cf.Future(),
                                             t_arrival=time.perf_counter()))
-            self._step(decision)
+            try:
+                self._step(decision)
+            except Exception as e:  # noqa: BLE001
+                self.on_follower_failure(e)
+                return
+
+    def on_follower_failure(self, e: Exception) -> None:
+        from ..parallel import health
+
+        health.collective_failure(f"lockstep follower step failed: {e!r}")
 
     def _take_waiting(self) -> list[Request]:
         eng, alloc = self.eng, self.eng.kv.allocator
@@ -334,7 +378,15 @@ class ContinuousEngine:
                 greedy = all(r.params.temperature <= 0 for r in adm)
                 out = eng._prefill([r.prompt for r in adm], [r.blocks for r in adm], [r.cached for r in adm],
                                    greedy=greedy)
+                err = comm.collective_error_snapshot()
                 first = out.tolist() if greedy else self._sample_rows(out, [r.params for r in adm])
+                comm.raise_on_collective_error(err)
+        except CollectiveError:
+            for r in adm:
+                eng.release(r.res)
+                alloc.free(r.blocks)
+                r.future.set_exception(RuntimeError("TP collective failed during prefill"))
+            raise
         except Exception as e:  # noqa: BLE001
             for r in adm:
                 eng.release(r.res)
@@ -512,19 +564,21 @@ class ContinuousEngine:
             host = self._host[self._flip]
             self._flip ^= 1
             host[:n].copy_(g.out[:n], non_blocking=True)
+            err = comm.collective_error_snapshot()
             ev = torch.cuda.Event()
             ev.record()
-            prev, self._pending = self._pending, (ev, host, snap)
+            prev, self._pending = self._pending, (ev, host, snap, err)
             if prev is not None:
                 self._process(prev)          # step t-1's tokens while step t runs
         else:
-            self._process((None, g.out[:n].clone(), snap))
+            self._process((None, g.out[:n].clone(), snap, comm.collective_error_snapshot()))
         eng.stats.decode_s += time.perf_counter() - t0
 
     def _process(self, pending) -> None:
-        ev, host, snap = pending
+        ev, host, snap, err = pending
         if ev is not None:
             ev.synchronize()
+        comm.raise_on_collective_error(err)
         toks = host[:len(snap)].tolist()
         finished = []
         for r, t in zip(snap, toks):

@@ -147,6 +147,20 @@ def custom_all_reduce():
     return _CUSTOM_AR
 
 
+def collective_error_snapshot():
+    """Non-blocking, stream-ordered copy of the IPC all-reduce's error word (None when the
+    custom all-reduce is not in use).  Take it right after a step's kernels are enqueued and
+    pass it to :func:`raise_on_collective_error` after the step's own host sync."""
+    return _CUSTOM_AR.snapshot() if _CUSTOM_AR is not None else None
+
+
+def raise_on_collective_error(snap) -> None:
+    """Raise ``CollectiveError`` when the snapshot says a peer never arrived: the step's
+    outputs are garbage, and the caller must not hand them out."""
+    if snap is not None and _CUSTOM_AR is not None:
+        _CUSTOM_AR.raise_if(snap)
+
+
 def tp_all_reduce(t: torch.Tensor) -> torch.Tensor:
     s = _STATE
     if s.tp_size > 1:

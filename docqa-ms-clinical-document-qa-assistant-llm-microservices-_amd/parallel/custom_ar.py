@@ -30,6 +30,20 @@ import torch.distributed as dist
 ONESHOT, TWOSHOT, GATHER = 0, 1, 2
 
 
+class CollectiveError(RuntimeError):
+    """A TP collective did not complete (a peer was late past the bound or dead): every
+    output of the step is garbage.  The serving loop treats it as fatal for the process
+    (parallel/health.py, EXIT_COLLECTIVE_HANG) -- the launcher re-forms the group."""
+
+
+def _agree(ok: bool, group, device) -> bool:
+    """True only if ``ok`` on every rank of ``group`` (MIN all-reduce: a collective decision)."""
+    on_gpu = dist.get_backend(group) != "gloo"
+    flag = torch.tensor([1 if ok else 0], dtype=torch.int32, device=device if on_gpu else "cpu")
+    dist.all_reduce(flag, op=dist.ReduceOp.MIN, group=group)
+    return bool(flag.item())
+
+
 class CustomAllReduce:
     def __init__(self, group=None, max_bytes: int = 64 << 20, device=None,
                  oneshot_max_bytes: int | None = None):
@@ -47,21 +61,40 @@ class CustomAllReduce:
         if oneshot_max_bytes is None:
             oneshot_max_bytes = int(os.environ.get("DOCQA_AR_ONESHOT_MAX", str(256 << 10)))
         self.oneshot_max_bytes = oneshot_max_bytes
-        self.own = self.nat.ar_alloc(self.nat.ar_region_bytes(self.max_elems))
-        handle = self.nat.ar_ipc_handle(self.own)
+        # how long a workgroup waits for a late peer before it records which one and gives up
+        # (the step then fails loudly: check() / raise_if()).  One process per GPU arrives
+        # within microseconds; processes time-sliced on ONE GPU (tests, --share-gpu) need more
+        self.timeout_us = int(float(os.environ.get("DOCQA_AR_TIMEOUT_MS", "500")) * 1000)
+        # every rank runs the same collective sequence whatever fails locally, so a failure
+        # on one rank becomes the same decision on all of them (no rank left in a barrier)
+        self.own, self.regions, self._opened = 0, [], []
+        err: Exception | None = None
+        handle = None
+        try:
+            self.own = self.nat.ar_alloc(self.nat.ar_region_bytes(self.max_elems))
+            handle = self.nat.ar_ipc_handle(self.own).tolist()
+        except Exception as e:  # noqa: BLE001 - reported collectively below
+            err = e
         handles = [None] * self.world
-        dist.all_gather_object(handles, handle.tolist(), group=group)
-        self.regions, self._opened = [], []
-        for r, h in enumerate(handles):
-            if r == self.rank:
-                self.regions.append(self.own)
-            else:
-                p = self.nat.ar_ipc_open(torch.tensor(h, dtype=torch.uint8))
-                self._opened.append(p)
-                self.regions.append(p)
-        self.ctr = torch.zeros(2, dtype=torch.int32, device=self.device)
+        dist.all_gather_object(handles, handle, group=group)
+        if err is None:
+            try:
+                if any(h is None for h in handles):
+                    raise RuntimeError("a peer could not export its IPC handle")
+                for r, h in enumerate(handles):
+                    if r == self.rank:
+                        self.regions.append(self.own)
+                    else:
+                        p = self.nat.ar_ipc_open(torch.tensor(h, dtype=torch.uint8))
+                        self._opened.append(p)
+                        self.regions.append(p)
+            except Exception as e:  # noqa: BLE001
+                err = e
+        self.ctr = torch.zeros(4, dtype=torch.int32, device=self.device)
         self.err = torch.zeros(1, dtype=torch.int32, device=self.device)
-        dist.barrier(group=group)
+        if not _agree(err is None, group, self.device):
+            self.close()
+            raise RuntimeError(f"custom all-reduce setup failed on {'this rank' if err else 'a peer'}: {err}")
 
     # ------------------------------------------------------------------ capability
     def _fits(self, M: int, H: int, mode: int) -> bool:
@@ -91,7 +124,7 @@ class CustomAllReduce:
         M = t.shape[1] if slabs else t.numel() // H
         mode = self.mode_for(M, H) if mode is None else mode
         return self.nat.ar_run(t, slabs, None, None, 0.0, self.rank, self.regions, self.max_elems, mode,
-                               self.ctr, self.err)
+                               self.ctr, self.err, self.timeout_us)
 
     def reduce_add_rmsnorm(self, t: torch.Tensor, residual: torch.Tensor, w: torch.Tensor, eps: float,
                            mode: int | None = None) -> torch.Tensor:
@@ -102,7 +135,7 @@ class CustomAllReduce:
         M = t.shape[1] if slabs else t.numel() // H
         mode = self.mode_for(M, H) if mode is None else mode
         return self.nat.ar_run(t, slabs, residual, w, float(eps), self.rank, self.regions, self.max_elems,
-                               mode, self.ctr, self.err)
+                               mode, self.ctr, self.err, self.timeout_us)
 
     def all_gather_raw(self, t: torch.Tensor) -> torch.Tensor:
         """All-gather of any contiguous GPU tensor whose byte size is a multiple of 16:
@@ -113,7 +146,7 @@ class CustomAllReduce:
             raise ValueError("all_gather_raw: payload must be a multiple of 16 bytes and fit the staging area")
         words = t.contiguous().view(torch.bfloat16).view(1, nb // 2)
         out = self.nat.ar_run(words, False, None, None, 0.0, self.rank, self.regions, self.max_elems, GATHER,
-                              self.ctr, self.err)
+                              self.ctr, self.err, self.timeout_us)
         return out.view(t.dtype).view(self.world, *t.shape)
 
     def self_test(self) -> bool:
@@ -131,17 +164,39 @@ class CustomAllReduce:
         ok = ok and bool(torch.equal(gat.cpu(), torch.arange(4).repeat(self.world, 1)
                                      + 1000 * torch.arange(self.world)[:, None]))
         ok = ok and int(self.err.item()) == 0
-        on_gpu = dist.get_backend(self.group) != "gloo"
-        flag = torch.tensor([1 if ok else 0], dtype=torch.int32, device=self.device if on_gpu else "cpu")
-        dist.all_reduce(flag, op=dist.ReduceOp.MIN, group=self.group)
-        return bool(flag.item())
+        return _agree(ok, self.group, self.device)
+
+    # ------------------------------------------------------------------ failure surfacing
+    def snapshot(self) -> torch.Tensor:
+        """Stream-ordered, non-blocking copy of the error word into pinned host memory:
+        taken behind a step's kernels and read (``raise_if``) after the step's existing host
+        sync, so surfacing a late or dead peer costs no extra synchronisation."""
+        h = torch.empty(1, dtype=torch.int32, pin_memory=True)
+        h.copy_(self.err, non_blocking=True)
+        return h
+
+    @staticmethod
+    def describe(word: int) -> str:
+        word &= 0xFFFFFFFF
+        return (f"custom all-reduce: rank {(word >> 1) & 7} never arrived (phase {(word >> 4) & 1}, "
+                f"call epoch {word >> 8}); the step's results are invalid")
+
+    def raise_if(self, snap: torch.Tensor | None) -> None:
+        if snap is not None and int(snap[0]):
+            raise CollectiveError(self.describe(int(snap[0])))
 
     def check(self) -> None:
-        if int(self.err.item()):
-            raise RuntimeError("custom all-reduce: a peer never arrived (spin limit hit)")
+        """Synchronous form (tests, between requests)."""
+        w = int(self.err.item())
+        if w:
+            raise CollectiveError(self.describe(w))
+
+    def max_wait_us(self) -> int:
+        """Longest time any workgroup waited for a peer since the counters were zeroed."""
+        return int(self.ctr[2].item())
 
     def close(self) -> None:
-        for p in self._opened:
+        for p in getattr(self, "_opened", []):
             self.nat.ar_ipc_close(p)
         self._opened = []
         if self.own:

@@ -66,6 +66,17 @@ def probe(group=None, timeout_s: float = 10.0) -> bool:
         return False
 
 
+def collective_failure(reason: str) -> None:
+    """A TP collective failed or a lockstep peer cannot mirror a step: the process's group
+    state is undefined, so the process is the unit of recovery -- exit with
+    ``EXIT_COLLECTIVE_HANG`` for the launcher (torchrun --max-restarts / launch --supervise)
+    to re-form the group.  Tests replace it via ``DOCQA_COLLECTIVE_FAILURE=raise``."""
+    log.error("collective failure: %s -- exiting (%d)", reason, EXIT_COLLECTIVE_HANG)
+    if os.environ.get("DOCQA_COLLECTIVE_FAILURE", "exit") == "raise":
+        raise SystemExit(EXIT_COLLECTIVE_HANG)
+    os._exit(EXIT_COLLECTIVE_HANG)
+
+
 def _exit_handler(stalled_s: float) -> None:
     log.error("no engine step completed for %.1f s: collective presumed hung, exiting (%d)",
               stalled_s, EXIT_COLLECTIVE_HANG)

@@ -18,6 +18,7 @@ If ``TIKA_URL`` is set the file is PUT to that Tika server instead, as in the re
 from __future__ import annotations
 
 import io
+import bisect
 import re
 import zipfile
 import zlib
@@ -61,10 +62,20 @@ def extract_docx(data: bytes) -> str:
 # most generated PDFs), else WinAnsi (cp1252) for simple fonts -- literal and hex
 # strings, TJ arrays with kerning gaps as spaces.  Files it cannot parse that way fall
 # back to scanning every content stream with latin-1 decoding (the round-1 behaviour).
-_OBJ = re.compile(rb"(?<![0-9])(\d+)\s+(\d+)\s+obj\b(.*?)\bendobj", re.S)
-_STREAM = re.compile(rb"stream\r?\n(.*)\r?\nendstream\s*$", re.S)
+#
+# Uploads are untrusted, so the reader is bounded: objects are found by one
+# linear scan of "N G obj" headers paired with the next "endobj" (no backtracking regex over
+# the body); streams are kept compressed and inflated lazily, only the ones text
+# extraction touches (page contents, ToUnicode CMaps, object streams), each capped at
+# MAX_STREAM_BYTES of output and the document at MAX_INFLATE_BYTES in all, so a small
+# deflate bomb or a file of images costs nothing.
+_OBJ_HEAD = re.compile(rb"(?<![0-9])(\d+)\s+(\d+)\s+obj\b")
+_ENDOBJ = re.compile(rb"\bendobj")
+_STREAM_KW = re.compile(rb"(?<![A-Za-z])stream\r?\n")
 _REF = re.compile(rb"(\d+)\s+(\d+)\s+R")
-_PDF_STREAM = re.compile(rb"<<(.*?)>>\s*stream\r?\n(.*?)\r?\nendstream", re.S)
+MAX_STREAM_BYTES = 16 << 20
+MAX_INFLATE_BYTES = 128 << 20
+MAX_OBJECTS = 200_000
 _ESC = {b"n": b"\n", b"r": b"\r", b"t": b"\t", b"b": b"\b", b"f": b"\f", b"(": b"(", b")": b")", b"\\": b"\\"}
 
 
@@ -113,40 +124,101 @@ def _hex_string(buf: bytes, i: int) -> tuple[bytes, int]:
         return b"", j + 1
 
 
-def _decompress(head: bytes, body: bytes) -> bytes | None:
+def _inflate(body: bytes, cap: int) -> bytes | None:
+    d = zlib.decompressobj()
+    try:
+        out = d.decompress(body, cap)
+    except zlib.error:
+        return None
+    return out
+
+
+def _decompress(head: bytes, body: bytes, cap: int = MAX_STREAM_BYTES) -> bytes | None:
     if b"/FlateDecode" in head or b"/Fl " in head or head.rstrip().endswith(b"/Fl"):
-        try:
-            return zlib.decompress(body)
-        except zlib.error:
-            try:
-                return zlib.decompressobj().decompress(body)
-            except zlib.error:
-                return None
+        return _inflate(body, cap)
     if b"/Filter" in head:
         return None          # images / unsupported filters
-    return body
+    return body[:cap]
+
+
+def _split_stream(body: bytes) -> tuple[bytes, bytes | None]:
+    """(dictionary part, raw stream bytes or None) of one object's body."""
+    sm = _STREAM_KW.search(body)
+    if not sm:
+        return body, None
+    end = body.rfind(b"endstream")
+    if end < sm.end():
+        return body, None
+    raw = body[sm.end():end]
+    if raw.endswith(b"\r\n"):
+        raw = raw[:-2]
+    elif raw.endswith((b"\n", b"\r")):
+        raw = raw[:-1]
+    return body[:sm.start()], raw
+
+
+class _Objects(dict):
+    """num -> (dictionary, decoded stream | None); streams inflate on first access."""
+
+    def __init__(self, pdf: "_Pdf"):
+        super().__init__()
+        self._pdf = pdf
+
+    def __getitem__(self, num):
+        head, raw = super().__getitem__(num)
+        return head, self._pdf._stream(num, head, raw)
+
+    def get(self, num, default=None):
+        return self[num] if num in self else default
+
+    def heads(self):
+        """(num, dictionary) of every object, without inflating anything."""
+        return ((k, dict.__getitem__(self, k)[0]) for k in sorted(self.keys()))
 
 
 class _Pdf:
     def __init__(self, data: bytes):
-        self.objs: dict[int, tuple[bytes, bytes | None]] = {}
-        for m in _OBJ.finditer(data):
-            body = m.group(3)
-            sm = _STREAM.search(body)
-            if sm:
-                head = body[:sm.start()]
-                self.objs[int(m.group(1))] = (head, _decompress(head, sm.group(1)))
-            else:
-                self.objs[int(m.group(1))] = (body, None)
-        for num, (head, stream) in list(self.objs.items()):   # compressed object streams
-            if b"/ObjStm" in head and stream:
+        self.objs = _Objects(self)
+        self._inflated: dict[int, bytes | None] = {}
+        self._budget = MAX_INFLATE_BYTES
+        heads = []
+        for m in _OBJ_HEAD.finditer(data):
+            heads.append((m.start(), m.end(), int(m.group(1))))
+            if len(heads) >= MAX_OBJECTS:
+                break
+        ends = [m.start() for m in _ENDOBJ.finditer(data)]
+        for k, (_, hend, num) in enumerate(heads):
+            nxt = heads[k + 1][0] if k + 1 < len(heads) else len(data)
+            j = bisect.bisect_left(ends, hend)
+            stop = ends[j] if j < len(ends) and ends[j] < nxt else nxt
+            dict.__setitem__(self.objs, num, _split_stream(data[hend:stop]))
+        for num, head in list(self.objs.heads()):   # compressed object streams
+            if b"/ObjStm" not in head:
+                continue
+            stream = self.objs[num][1]
+            if not stream:
+                continue
+            try:
                 n = int(re.search(rb"/N\s+(\d+)", head).group(1))
                 first = int(re.search(rb"/First\s+(\d+)", head).group(1))
                 nums = [int(x) for x in stream[:first].split()]
-                offs = [(nums[2 * k], first + nums[2 * k + 1]) for k in range(min(n, len(nums) // 2))]
-                for k, (on, off) in enumerate(offs):
-                    end = offs[k + 1][1] if k + 1 < len(offs) else len(stream)
-                    self.objs.setdefault(on, (stream[off:end], None))
+            except (AttributeError, ValueError):
+                continue
+            offs = [(nums[2 * k], first + nums[2 * k + 1]) for k in range(min(n, len(nums) // 2))]
+            for k, (on, off) in enumerate(offs):
+                end = offs[k + 1][1] if k + 1 < len(offs) else len(stream)
+                if on not in self.objs:
+                    dict.__setitem__(self.objs, on, (stream[off:end], None))
+
+    def _stream(self, num: int, head: bytes, raw: bytes | None) -> bytes | None:
+        if raw is None:
+            return None
+        if num in self._inflated:
+            return self._inflated[num]
+        out = _decompress(head, raw, min(MAX_STREAM_BYTES, max(0, self._budget)))
+        self._budget -= len(out or b"")
+        self._inflated[num] = out
+        return out
 
     def get(self, ref: bytes | int | None):
         if ref is None:
@@ -344,10 +416,9 @@ def _page_fonts(pdf: _Pdf, page_head: bytes, cache: dict) -> dict:
 
 def extract_pdf(data: bytes) -> str:
     pdf = _Pdf(data)
-    pages = [(num, o) for num, o in sorted(pdf.objs.items())
-             if re.search(rb"/Type\s*/Page(?![s\w])", o[0])]
+    pages = [(num, head) for num, head in pdf.objs.heads() if re.search(rb"/Type\s*/Page(?![s\w])", head)]
     texts, cache = [], {}
-    for _, (head, _) in pages:
+    for _, head in pages:
         fonts = _page_fonts(pdf, head, cache)
         cont = _Pdf.entry(head, b"Contents")
         refs = _REF.findall(cont) if cont else []
@@ -357,9 +428,17 @@ def extract_pdf(data: bytes) -> str:
     out = "\n".join(t for t in texts if t.strip())
     if out.strip():
         return out
-    # no page tree recovered: every text-bearing stream, latin-1 strings
-    for m in _PDF_STREAM.finditer(data):
-        body = _decompress(m.group(1), m.group(2))
+    # no page tree recovered: every text-bearing stream, latin-1 strings (a linear scan of
+    # "stream" keywords, each dictionary taken from the 4 KB before it; same inflate budget)
+    budget = MAX_INFLATE_BYTES
+    for m in _STREAM_KW.finditer(data):
+        end = data.find(b"endstream", m.end())
+        if end < 0 or budget <= 0:
+            break
+        d0 = data.rfind(b"<<", max(0, m.start() - 4096), m.start())
+        head = data[d0:m.start()] if d0 >= 0 else b""
+        body = _decompress(head, data[m.end():end].rstrip(b"\r\n"), min(MAX_STREAM_BYTES, budget))
+        budget -= len(body or b"")
         if body and b"BT" in body:
             texts.append(_content_text(body, {}))
     return "\n".join(t for t in texts if t.strip())

@@ -89,3 +89,29 @@ def test_generated_pdf_roundtrip_and_multipage_order():
             5: b"<< /Type /Page /Parent 2 0 R /Contents 6 0 R >>", 6: page(b"page two"),
             7: b"<< /Type /Font /Subtype /Type1 /BaseFont /Helvetica >>"}
     assert extract_pdf(_assemble(objs)).split("\n") == ["page one", "page two"]
+
+
+def test_untrusted_pdf_is_bounded():
+    """a deflate bomb is capped, image streams are never inflated, and a file of
+    'N 0 obj' markers with no endobj parses in linear time."""
+    import time
+    import zlib
+
+    from docqa_amd.text import extraction as ex
+
+    bomb = zlib.compress(b"\0" * (256 << 20), 9)             # 256 MB of zeros in ~250 KB
+    pdf = (b"%PDF-1.4\n1 0 obj\n<< /Type /Page /Contents 2 0 R >>\nendobj\n"
+           + b"2 0 obj\n<< /Length " + str(len(bomb)).encode() + b" /Filter /FlateDecode >>\nstream\n" + bomb +
+           b"\nendstream\nendobj\n3 0 obj\n<< /Subtype /Image /Filter /FlateDecode >>\nstream\n" + bomb +
+           b"\nendstream\nendobj\n%%EOF")
+    t = time.perf_counter()
+    p = ex._Pdf(pdf)
+    assert 3 not in p._inflated                             # the image is never touched
+    body = p.objs[2][1]
+    assert body is not None and len(body) <= ex.MAX_STREAM_BYTES
+    ex.extract_pdf(pdf)
+    assert time.perf_counter() - t < 20
+    spam = b"%PDF-1.4\n" + b"1 0 obj << /A 1 >> " * 200_000    # no endobj anywhere
+    t = time.perf_counter()
+    ex.extract_pdf(spam)
+    assert time.perf_counter() - t < 10
