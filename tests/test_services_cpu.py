@@ -513,3 +513,44 @@ def test_ollama_options_mapping():
     assert p.max_new_tokens == 24 and p.temperature == 0.7 and p.top_k == 40 and p.top_p == 0.9 and p.seed == 7
     assert sampling_from_options({"num_predict": 5000}, st, 1024, 100).max_new_tokens == 924
     assert sampling_from_options({"num_predict": 0}, st, 1024, 100).max_new_tokens == 1
+
+
+@pytest.mark.parametrize("mode", ["continuous", "batch"])
+def test_summarize_long_prompt_is_not_truncated(tmp_path, mode):
+    """VERDICT r3 missing #4: the synthese service sends all of a patient's notes in one
+    prompt (synthese-comparative/api/routes.py:45-56,99-118).  With Llama-3's 8192-token
+    window (MAX_CONTEXT) a ~6k-token prompt reaches the engine whole -- chunked prefill,
+    no middle dropped."""
+    from docqa_amd.prompts import SINGLE_PATIENT_TEMPLATE
+    from docqa_amd.services.stack import DocQAStack, StackOptions
+
+    st = Settings()
+    st.index_dir = str(tmp_path)
+    st.default_data_dir = str(tmp_path / "nodata")
+    st.database_url = "sqlite://"
+    st.max_new_tokens = 4
+    st.serving_mode = mode
+    s = DocQAStack(StackOptions(llm="tiny-8k", embed="tiny-bert", ner="tiny-bert", device="cpu",
+                                max_batch=2, use_graphs=False), st)
+    try:
+        assert s.engine.max_context == 8192
+        notes = "\n\n".join(f"[doc {i}]\nConsultation {i} : anticoagulant ajusté, INR {i % 4 + 1}.{i % 10}, "
+                            f"vigilance hémorragique, note de suivi numéro {i}." for i in range(90))
+        prompt = SINGLE_PATIENT_TEMPLATE.format(patient_alias="PATIENT_7", from_date="2024-01-01",
+                                                to_date="2025-01-01", focus="anticoagulants", documents=notes)
+        want = s.chat_tok.chat_prompt(prompt)
+        assert 5000 < len(want) < 8192 - st.max_new_tokens - 8
+        seen = []
+        if mode == "continuous":
+            ce = s.qa_app.state.batcher.engine
+            orig = ce.submit
+            ce.submit = lambda p, *a, **k: (seen.append(list(p)), orig(p, *a, **k))[1]
+        else:
+            eng = s.engine
+            orig = eng.generate
+            eng.generate = lambda ps, *a, **k: (seen.extend(list(p) for p in ps), orig(ps, *a, **k))[1]
+        r = TestClient(s.qa_app).post("/api/llm/summarize", json={"prompt": prompt})
+        assert r.status_code == 200 and isinstance(r.json()["summary"], str)
+        assert want in seen                      # every token of the prompt, in order
+    finally:
+        s.close()
