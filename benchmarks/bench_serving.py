@@ -89,7 +89,7 @@ def run_launch(a, mode: str) -> list[dict]:
     work = tempfile.mkdtemp(prefix="docqa_serving_bench_")   # fresh index / documents DB per run
     env = dict(os.environ, INDEX_DIR=work, DATABASE_URL=f"sqlite:///{work}/documents.db", UPLOAD_DIR=work,
                MAX_NEW_TOKENS=str(a.max_new_tokens), MAX_BATCH=str(a.max_batch), DOCQA_SERVING=mode,
-               TEMPERATURE="0", HSA_ENABLE_IPC_MODE_LEGACY="0",
+               TEMPERATURE="0", HSA_ENABLE_IPC_MODE_LEGACY="0", STOP_ON_EOS="0" if a.ignore_eos else "1",
                # the server log must survive a crash of the service (no block-buffered stdout)
                PYTHONUNBUFFERED="1", PYTHONFAULTHANDLER="1")
     env.setdefault("PYTHONPATH", str(ROOT))
@@ -230,6 +230,8 @@ def run_launch(a, mode: str) -> list[dict]:
              "server_split_p50": res["server"], "send_lag_ms_p50": res["send_lag_ms_p50"],
              "send_lag_ms_max": res["send_lag_ms_max"],
              "requests": a.requests, "max_new_tokens": a.max_new_tokens, "max_batch": a.max_batch,
+             "ignore_eos": a.ignore_eos,
+             "gen_tokens_per_s": (round(a.requests * a.max_new_tokens / res["wall"], 1) if a.ignore_eos else None),
              "gpus": a.gpus, "tp": a.tp, "llm": "tiny" if a.tiny else a.llm, "notes": a.notes,
              "questions": a.questions, "dtype": "bf16" if a.device != "cpu" else "fp32",
              "data": "synthetic questions and notes, random-init weights", "wall_s": round(res["wall"], 2),
@@ -257,6 +259,9 @@ def main():
     ap.add_argument("--start-timeout", type=float, default=900.0)
     ap.add_argument("--run-timeout", type=float, default=600.0, help="launch entry: seconds per offered rate")
     ap.add_argument("--tiny", action="store_true", help="tiny random models (CPU functional run)")
+    ap.add_argument("--ignore-eos", action="store_true",
+                    help="decode every answer to --max-new-tokens (STOP_ON_EOS=0), as bench.py does: random "
+                         "weights otherwise end ~13 %% of answers at the first token")
     ap.add_argument("--server-log", default="", help="file for the launcher's output")
     ap.add_argument("--launch-prefix", default="", help="launch entry: command prepended to the service "
                     "launcher (e.g. 'rocprofv3 --kernel-trace -d DIR -o run --output-format csv --')")
@@ -288,6 +293,7 @@ def main():
         st.max_new_tokens = a.max_new_tokens
         st.max_batch = a.max_batch
         st.temperature = 0.0
+        st.stop_on_eos = not a.ignore_eos
         cls = ContinuousBatcher if mode == "continuous" else DynamicBatcher
         b = cls(pipe, st, Metrics("bench"))
         # warm-up: capture graphs / tune for the buckets this load will hit
@@ -319,6 +325,8 @@ def main():
                "offered_rate": a.rate, "value": round(a.requests / (t_end - t0), 2), "unit": "queries/s",
                **_pcts(lat), "questions": a.questions,
                "requests": a.requests, "max_new_tokens": a.max_new_tokens, "max_batch": a.max_batch,
+               "ignore_eos": a.ignore_eos,
+               "gen_tokens_per_s": (round(a.requests * a.max_new_tokens / (t_end - t0), 1) if a.ignore_eos else None),
                "llm": a.llm, "dtype": "bf16", "data": "synthetic questions, random-init weights",
                "engine_prefill_s": round(s1[0] - s0[0], 2), "engine_decode_s": round(s1[1] - s0[1], 2),
                "decode_steps": s1[3] - s0[3], "wall_s": round(t_end - t0, 2),

@@ -14,6 +14,11 @@ the MI355X knobs of this framework.
 | SEMANTIC_INDEXER_URL | http://semantic-indexer:8003 | synthese-comparative/core/config.py:10-13 |
 | LLM_QA_URL | http://llm-qa:8004 | synthese-comparative/core/config.py:16-19 |
 | USE_FAKE_RETRIEVAL / USE_FAKE_LLM | true / true | synthese-comparative/core/config.py:22-23 |
+| DEID_NER | auto | the spaCy NER of deid-service/anonymizer.py:29,41-45: "auto" runs the token classifier when NER_CHECKPOINT names one, "1" always (random-init weights when none), "0" never |
+| NER_CHECKPOINT | (empty) | Hugging Face BERT token-classification checkpoint directory for DEID_NER |
+| DEID_BATCH_DOCS | 32 | raw messages the deid worker drains into one packed NER forward |
+| MAX_CONTEXT | 8192 | llm-qa engine context (prompt + generation); Llama-3's window |
+| QA_TEMPLATE | reference | llm-qa prompt: the verbatim reference text (llm-qa/main.py:71-93) or cache_friendly |
 """
 from __future__ import annotations
 
@@ -46,6 +51,10 @@ class Settings:
     raw_queue: str = field(default_factory=lambda: os.getenv("INPUT_QUEUE", "raw_documents_queue"))
     clean_queue: str = field(default_factory=lambda: os.getenv("OUTPUT_QUEUE", "clean_documents_queue"))
     nlp_lang: str = field(default_factory=lambda: os.getenv("NLP_LANG", "en"))
+    # de-identification: NER token classifier in the loop (auto: when a checkpoint is set)
+    deid_ner: str = field(default_factory=lambda: os.getenv("DEID_NER", "auto").lower())
+    ner_checkpoint: str = field(default_factory=lambda: os.getenv("NER_CHECKPOINT", ""))
+    deid_batch_docs: int = field(default_factory=lambda: env_int("DEID_BATCH_DOCS", 32))
     tika_url: str = field(default_factory=lambda: os.getenv("TIKA_URL", ""))  # empty: native extractors
     upload_dir: str = field(default_factory=lambda: os.getenv("UPLOAD_DIR", "temp_uploads"))
     # indexer
@@ -77,7 +86,13 @@ class Settings:
     top_k: int = field(default_factory=lambda: env_int("TOP_K", 3))
     max_new_tokens: int = field(default_factory=lambda: env_int("MAX_NEW_TOKENS", 256))
     temperature: float = field(default_factory=lambda: float(os.getenv("TEMPERATURE", "0")))
+    # stop a generation at EOS (the reference's behaviour); STOP_ON_EOS=0 decodes every
+    # answer to MAX_NEW_TOKENS (serving benchmarks: random weights emit EOS at random)
+    stop_on_eos: bool = field(default_factory=lambda: env_bool("STOP_ON_EOS", "true"))
     max_batch: int = field(default_factory=lambda: env_int("MAX_BATCH", 64))
+    # engine context window (prompt + generation): long synthese prompts are prefilled in
+    # chunks up to it and truncated only beyond it
+    max_context: int = field(default_factory=lambda: env_int("MAX_CONTEXT", 8192))
     batch_window_ms: int = field(default_factory=lambda: env_int("BATCH_WINDOW_MS", 5))
     # llm-qa scheduling: "continuous" (requests join/leave the decode batch every step,
     # engine/scheduler.py) or "batch" (static batches, one prefill + decode loop each)
@@ -96,6 +111,14 @@ class Settings:
     fake_max_chars: int = 1200
     llm_timeout_s: float = 60.0
     retrieval_timeout_s: float = 30.0
+
+    def ner_enabled(self) -> bool:
+        """Whether the deid worker runs the NER model (DEID_NER auto / 1 / 0)."""
+        if self.deid_ner in ("1", "true", "yes", "y", "on"):
+            return True
+        if self.deid_ner in ("0", "false", "no", "n", "off"):
+            return False
+        return bool(self.ner_checkpoint)
 
     def resolved_device(self) -> str:
         if self.device != "auto":

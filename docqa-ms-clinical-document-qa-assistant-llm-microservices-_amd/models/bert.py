@@ -206,11 +206,12 @@ class BertTokenClassifier(BertEncoder):
     def predict_packed(self, ids, cu_seqlens, max_len) -> torch.Tensor:
         h = self.hidden_states(ids, cu_seqlens, max_len)
         if (self.cls_w.shape[0] <= 32 and h.dtype == torch.bfloat16
-                and os.environ.get("DOCQA_NER_FUSED", "0") == "1"
+                and os.environ.get("DOCQA_NER_FUSED", "1") == "1"
                 and h.data_ptr() % 16 == 0 and h.stride(0) % 8 == 0):
             # fused head + argmax (embed_sample.hip): the [T, labels] logits never hit HBM.
-            # Opt-in: measured at parity with hipBLASLt + argmax on clinical-bert (batch 256:
-            # 14.60 vs 14.46-14.51 ms, profiles/r1_bench_deid_fused_ab.json)
+            # Default: at parity with hipBLASLt + argmax on clinical-bert (batch 256: 14.60
+            # vs 14.46-14.51 ms, profiles/r1_bench_deid_fused_ab.json), and the whole NER
+            # forward then runs on the hand-written kernels; DOCQA_NER_FUSED=0 for the library head
             return ops.token_cls_argmax(h, self.cls_w, self.cls_b, len(self.labels))
         logits = F.linear(h, self.cls_w, self.cls_b)
         return ops.argmax(logits)  # [T] label ids

@@ -91,6 +91,10 @@ class LlamaConfig:
             return LlamaConfig(name="tiny", vocab_size=4096, hidden=256, intermediate=512,
                                layers=2, heads=4, kv_heads=2, head_dim=128, max_position=2048,
                                bos_token_id=1, eos_token_id=2)
+        if name == "tiny-8k":   # tiny with Llama-3's 8192-token window (long-prompt service tests)
+            return LlamaConfig(name="tiny-8k", vocab_size=4096, hidden=256, intermediate=512,
+                               layers=2, heads=4, kv_heads=2, head_dim=128, max_position=8192,
+                               bos_token_id=1, eos_token_id=2)
         raise ValueError(f"unknown llama preset {name}")
 
     def num_params(self) -> int:

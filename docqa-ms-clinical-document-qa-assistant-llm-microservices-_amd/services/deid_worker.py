@@ -8,8 +8,13 @@ Reference (deid-service/anonymizer.py:50-110):
   * invalid JSON or processing error -> ``nack(requeue=False)`` (here: dead-lettered to
     ``<queue>.dlq`` instead of lost);
   * ``prefetch_count=1``; reconnect every 5 s while the broker is unavailable.
-Batching: :meth:`DeidWorker.process_messages` de-identifies a list of raw messages with
-one packed NER forward on the GPU (used by the batched path and the config-3 bench).
+Batching (the MI355X part): the consumer's prefetch window is ``DEID_BATCH_DOCS`` and,
+while more raw messages are already queued, the callback only collects them; the batch is
+then de-identified by ONE packed NER forward (:meth:`process_messages`: every window of
+every document in one varlen encoder pass + the fused token-classification argmax),
+published and acked together.  An idle queue flushes at once, so a single document is
+not delayed.  A batch whose forward fails is retried one message at a time, so only a
+poison message is dead-lettered.
 """
 from __future__ import annotations
 
@@ -36,6 +41,10 @@ class DeidWorker:
         self._thread: threading.Thread | None = None
         self._ch = None
         self.processed = 0
+        self.batches = 0
+        self.batch_docs = max(1, int(getattr(self.st, "deid_batch_docs", 1)))
+        self._pending: list = []
+        self._depth = getattr(self.broker, "depth", None)
 
     def clean_message(self, message: dict, masked: str) -> dict:
         return {"doc_id": message.get("doc_id", "UNKNOWN"), "original_text_masked": masked,
@@ -46,24 +55,53 @@ class DeidWorker:
         return [self.clean_message(m, t) for m, t in zip(messages, masked)]
 
     def callback(self, ch, method, properties, body):
+        """Queue consumer: collect while more raw messages are waiting (up to
+        ``batch_docs``), then de-identify the batch in one packed forward."""
+        self._pending.append((ch, method, body))
+        waiting = self._depth(self.in_q) if self._depth is not None else 0
+        if waiting > 0 and len(self._pending) < self.batch_docs:
+            return
+        batch, self._pending = self._pending, []
+        self._flush(batch)
+
+    def _flush(self, batch: list) -> None:
+        good = []
+        for ch, method, body in batch:
+            try:
+                message = json.loads(body)
+                if not isinstance(message, dict):
+                    raise json.JSONDecodeError("not an object", str(body)[:40], 0)
+                good.append((ch, method, message, body))
+            except json.JSONDecodeError:
+                logger.error("invalid message (not JSON)")
+                ch.basic_nack(delivery_tag=method.delivery_tag, requeue=False)
+        if not good:
+            return
+        for _, _, m, _ in good:
+            logger.info("[->] doc %s (%d chars)", m.get("doc_id", "UNKNOWN"), len(m.get("text", "") or ""))
         try:
-            message = json.loads(body)
-            doc_id = message.get("doc_id", "UNKNOWN")
-            raw = message.get("text", "") or ""
-            logger.info("[->] doc %s (%d chars)", doc_id, len(raw))
-            out = self.clean_message(message, self.engine.process_text_anonymization(raw))
-            ch.queue_declare(queue=self.out_q, durable=True)
-            ch.basic_publish(exchange="", routing_key=self.out_q, body=json.dumps(out),
-                             properties=self.broker.persistent_properties())
-            ch.basic_ack(delivery_tag=method.delivery_tag)
-            self.processed += 1
-            logger.info("[<-] doc %s anonymised -> %s", doc_id, self.out_q)
-        except json.JSONDecodeError:
-            logger.error("invalid message (not JSON)")
-            ch.basic_nack(delivery_tag=method.delivery_tag, requeue=False)
-        except Exception as e:  # noqa: BLE001
-            logger.error("processing error: %s", e)
-            ch.basic_nack(delivery_tag=method.delivery_tag, requeue=False)
+            outs = self.process_messages([m for _, _, m, _ in good])
+        except Exception as e:  # noqa: BLE001 - isolate the poison message: one at a time
+            if len(good) == 1:
+                ch, method, _, _ = good[0]
+                logger.error("processing error: %s", e)
+                ch.basic_nack(delivery_tag=method.delivery_tag, requeue=False)
+                return
+            for ch, method, _, body in good:
+                self._flush([(ch, method, body)])
+            return
+        self.batches += 1
+        for (ch, method, m, _), out in zip(good, outs):
+            try:
+                ch.queue_declare(queue=self.out_q, durable=True)
+                ch.basic_publish(exchange="", routing_key=self.out_q, body=json.dumps(out),
+                                 properties=self.broker.persistent_properties())
+                ch.basic_ack(delivery_tag=method.delivery_tag)
+                self.processed += 1
+                logger.info("[<-] doc %s anonymised -> %s", m.get("doc_id", "UNKNOWN"), self.out_q)
+            except Exception as e:  # noqa: BLE001
+                logger.error("processing error: %s", e)
+                ch.basic_nack(delivery_tag=method.delivery_tag, requeue=False)
 
     def run_forever(self, retry_s: float = 5.0) -> None:
         while True:
@@ -72,7 +110,9 @@ class DeidWorker:
                 ch = self.broker.channel()
                 self._ch = ch
                 ch.queue_declare(queue=self.in_q, durable=True)
-                ch.basic_qos(prefetch_count=1)
+                # the reference's prefetch 1 unless this broker can report queue depth (then
+                # a window of batch_docs lets the callback drain a burst into one forward)
+                ch.basic_qos(prefetch_count=self.batch_docs if self._depth is not None else 1)
                 ch.basic_consume(queue=self.in_q, on_message_callback=self.callback)
                 logger.info("DeID worker consuming %s", self.in_q)
                 ch.start_consuming()

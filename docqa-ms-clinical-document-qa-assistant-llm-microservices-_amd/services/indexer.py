@@ -49,6 +49,39 @@ from ..text.kb import kb_records_from_dir, synthetic_kb_records
 logger = logging.getLogger("semantic-indexer")
 
 
+class PatientIndex:
+    """patient key -> its patient-file row ids, kept beside the append-only metadata list.
+
+    ``/api/search/patient-snippets`` (the contract of synthese-comparative/core/
+    retrieval_client.py:72-91) used to scan every metadata row under the index lock; at the
+    10M-chunk scale of config 2 that stalls every search for seconds.  The map is updated
+    by every ``add_records`` / WAL replay and rebuilt once from a loaded snapshot, so a
+    lookup costs O(rows of that patient).  A row is reachable by its ``patient_id`` and by
+    its ``doc_id`` (the reference keys patient chunks by document id)."""
+
+    def __init__(self):
+        self._rows: dict[str, list[int]] = {}
+        self.n = 0          # metadata rows covered so far
+
+    def extend(self, metadata: list[dict], start: int | None = None) -> None:
+        start = self.n if start is None else start
+        for i in range(start, len(metadata)):
+            m = metadata[i]
+            if m.get("type") != "patient_file":
+                continue
+            keys = {str(m.get("patient_id")), str(m.get("doc_id"))}
+            for k in keys:
+                self._rows.setdefault(k, []).append(i)
+        self.n = max(self.n, len(metadata))
+
+    def rebuild(self, metadata: list[dict]) -> None:
+        self._rows, self.n = {}, 0
+        self.extend(metadata, 0)
+
+    def rows(self, key: str) -> list[int]:
+        return list(self._rows.get(str(key), ()))
+
+
 class SemanticIndexer:
     def __init__(self, encoder, tokenizer, settings: Settings | None = None, index: FlatIndex | None = None,
                  metadata: list | None = None, device: str = "cuda", on_indexed=None):
@@ -58,6 +91,8 @@ class SemanticIndexer:
         self.device = device
         self.index = index
         self.metadata: list[dict] = metadata if metadata is not None else []
+        self.patients = PatientIndex()
+        self.patients.rebuild(self.metadata)
         self.lock = threading.RLock()
         self.on_indexed = on_indexed  # callback(doc_id) e.g. docs DB status -> INDEXED
         self._ch = None
@@ -88,6 +123,7 @@ class SemanticIndexer:
             if self.index_path.exists() and self.meta_path.exists():
                 self.index = load_index(self.st, self.index_path, self.device)
                 self.metadata = metadata_io.read_metadata(self.meta_path)
+                self.patients.rebuild(self.metadata)
                 if len(self.metadata) != self.index.ntotal:
                     raise RuntimeError(f"index/metadata mismatch: {self.index.ntotal} vs {len(self.metadata)}")
                 covered = read_snapshot_marker(self.marker_path)["wal_seq"]
@@ -95,6 +131,7 @@ class SemanticIndexer:
             else:
                 self.index = make_index(self.st, self.encoder.cfg.hidden, self.device)
                 self.metadata = []
+                self.patients.rebuild(self.metadata)
                 if build_if_missing:
                     recs = kb_records_from_dir(self.st.default_data_dir) or synthetic_kb_records()
                     self.add_records(recs, log=False)
@@ -104,6 +141,7 @@ class SemanticIndexer:
                 for _, recs, vecs in self.wal.replay(after_seq=covered):
                     self.index.add(torch.from_numpy(vecs.copy()))
                     self.metadata.extend(recs)
+                    self.patients.extend(self.metadata)
                     replayed += len(recs)
                 if replayed:
                     logger.info("replayed %d vectors from the write-ahead log", replayed)
@@ -145,6 +183,7 @@ class SemanticIndexer:
                 self.wal.append(recs, emb.float().cpu().numpy())
             self.index.add(emb)
             self.metadata.extend(recs)
+            self.patients.extend(self.metadata)
             self.version += 1
         return len(recs)
 
@@ -241,10 +280,10 @@ class SemanticIndexer:
         the ``focus`` text."""
         pid = str(patient_id)
         lo, hi = parse_date(from_date), parse_date(to_date)
-        with self.lock:
-            rows = [(i, m) for i, m in enumerate(self.metadata)
-                    if m.get("type") == "patient_file" and (str(m.get("patient_id")) == pid or str(m.get("doc_id")) == pid)
-                    and in_window(m.get("note_date"), lo, hi)]
+        with self.lock:   # O(rows of this patient): the per-patient map, never a metadata scan
+            ids = self.patients.rows(pid)
+            meta = self.metadata
+        rows = [(i, meta[i]) for i in ids if in_window(meta[i].get("note_date"), lo, hi)]
         if focus and rows:
             q = self.encoder.encode(self.tok.encode_batch([focus]))
             ids = torch.tensor([i for i, _ in rows], device=self.index.xb.device)

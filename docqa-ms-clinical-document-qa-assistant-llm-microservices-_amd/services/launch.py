@@ -158,7 +158,8 @@ def run_parallel(a, opts: "StackOptions") -> None:
         signal.signal(signal.SIGINT, signal.SIG_IGN)
         ck.use_checkpoint_tokenizers(opts.llm, opts.embed)
         model = ck.resolve_llama(opts.llm, device=opts.device)
-        eng = LLMEngine(model, max_batch=opts.max_batch, max_context=opts.max_context, use_graphs=opts.use_graphs,
+        ctx = min(opts.max_context or st.max_context, model.cfg.max_position)
+        eng = LLMEngine(model, max_batch=opts.max_batch, max_context=ctx, use_graphs=opts.use_graphs,
                         kv_mem_fraction=opts.kv_mem_fraction)
         ce = ContinuousEngine(eng, max_running=st.max_batch, lockstep=ls)
         if os.environ.get("DOCQA_WARM_BUCKETS", "1") == "1":
@@ -207,6 +208,10 @@ def build_parser() -> argparse.ArgumentParser:
     ap.add_argument("--preload-notes", type=int, default=0,
                     help="index this many synthetic clinical notes at start (serving benchmarks, demos)")
     ap.add_argument("--kv-mem-fraction", type=float, default=0.8, help="KV pool share of free HBM")
+    ap.add_argument("--deid-ner", choices=("auto", "on", "off"), default=None,
+                    help="NER token classifier in the deid worker (default: env DEID_NER, auto = when "
+                         "NER_CHECKPOINT names a checkpoint)")
+    ap.add_argument("--ner-checkpoint", default=None, help="BERT token-classification checkpoint (NER_CHECKPOINT)")
     return ap
 
 
@@ -234,9 +239,13 @@ def main() -> None:
         supervise([g for g in a.supervise.split(";") if g], argv)
         return
     logging.basicConfig(level=logging.INFO)
+    if a.deid_ner is not None:
+        os.environ["DEID_NER"] = {"on": "1", "off": "0"}.get(a.deid_ner, "auto")
+    if a.ner_checkpoint:
+        os.environ["NER_CHECKPOINT"] = a.ner_checkpoint
     opts = StackOptions(llm="tiny" if a.tiny else a.llm, embed="tiny-bert" if a.tiny else a.embed,
                         ner="tiny-bert" if a.tiny else "clinical-bert", device=a.device,
-                        use_graphs=a.device != "cpu", max_context=2048 if a.tiny else 4096,
+                        use_graphs=a.device != "cpu", max_context=2048 if a.tiny else None,
                         real_synthese=a.real_synthese,
                         services=tuple(x for x in a.services.split(",") if x),
                         max_batch=Settings().max_batch, preload_notes=a.preload_notes,

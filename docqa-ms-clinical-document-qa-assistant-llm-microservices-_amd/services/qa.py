@@ -57,7 +57,7 @@ class DynamicBatcher:
 
     def _params(self) -> SamplingParams:
         return SamplingParams(max_new_tokens=self.st.max_new_tokens, temperature=self.st.temperature,
-                              stop_on_eos=True)
+                              stop_on_eos=self.st.stop_on_eos)
 
     def _loop(self) -> None:
         while not self._stop.is_set():
@@ -170,7 +170,7 @@ class ContinuousBatcher:
 
     def _params(self) -> SamplingParams:
         return SamplingParams(max_new_tokens=self.st.max_new_tokens, temperature=self.st.temperature,
-                              stop_on_eos=True)
+                              stop_on_eos=self.st.stop_on_eos)
 
     def _drain(self) -> list:
         """Everything queued now; while the engine is busy, also what arrives within

@@ -36,9 +36,11 @@ class StackOptions:
     ner: str = "clinical-bert"
     device: str = "cuda"
     max_batch: int = 64
-    max_context: int = 4096
+    max_context: int | None = None   # None: Settings.max_context (MAX_CONTEXT, 8192) capped by the model
     use_graphs: bool = True
-    ner_in_loop: bool = False     # run the (random-init) NER model inside de-identification
+    # NER token classifier inside de-identification (reference: spaCy NER on every message,
+    # deid-service/anonymizer.py:29,41-45); None: Settings.ner_enabled() (DEID_NER / NER_CHECKPOINT)
+    ner_in_loop: bool | None = None
     real_synthese: bool = False
     services: tuple = ()          # subset of ALL_SERVICES hosted by this process (empty: all)
     qa_lockstep: object = None    # llm-qa leads a tensor-parallel group (services/launch.py --tp)
@@ -105,11 +107,15 @@ class DocQAStack:
         self.ingest_app = self.qa_app = self.indexer_app = self.synthese_app = self.ui_app = None
         if "deid" in svc:
             ner_model = None
-            if opts.ner_in_loop:
-                ner_model = (ck.load_bert_token_classifier(opts.ner, NER_LABELS, device=dev)
-                             if ck.is_checkpoint(opts.ner)
-                             else BertTokenClassifier(BertConfig.preset(opts.ner), NER_LABELS, device=dev))
-            self.deid_engine = DeidEngine(ner_model, self.enc_tok, use_model=opts.ner_in_loop)
+            use_ner = self.st.ner_enabled() if opts.ner_in_loop is None else opts.ner_in_loop
+            if use_ner:
+                src = self.st.ner_checkpoint or opts.ner
+                ner_model = (ck.load_bert_token_classifier(src, NER_LABELS, device=dev)
+                             if ck.is_checkpoint(src)
+                             else BertTokenClassifier(BertConfig.preset(src), NER_LABELS, device=dev))
+                log.info("deid: NER token classifier %s in the loop (batches of <= %d docs)", src,
+                         self.st.deid_batch_docs)
+            self.deid_engine = DeidEngine(ner_model, self.enc_tok, use_model=use_ner)
             self.deid = deid_worker.DeidWorker(self.deid_engine, self.st, self.broker).start()
         if "indexer" in svc:
             db = self.db
@@ -131,11 +137,12 @@ class DocQAStack:
                                               d=self.encoder.cfg.hidden, device=dev, settings=self.st).start()
                 index, metadata = self.follower.index, self.follower.metadata
             self.model = ck.resolve_llama(opts.llm, device=dev)
-            self.engine = LLMEngine(self.model, max_batch=opts.max_batch, max_context=opts.max_context,
+            ctx = min(opts.max_context or self.st.max_context, self.model.cfg.max_position)
+            self.engine = LLMEngine(self.model, max_batch=opts.max_batch, max_context=ctx,
                                     use_graphs=opts.use_graphs, kv_mem_fraction=opts.kv_mem_fraction)
             self.pipeline = RAGPipeline(self.encoder, self.enc_tok, index, metadata,
                                         self.engine, self.chat_tok, k=self.st.top_k,
-                                        max_prompt_tokens=opts.max_context - self.st.max_new_tokens - 8)
+                                        max_prompt_tokens=ctx - self.st.max_new_tokens - 8)
             self.qa_app = qa.create_app(self.pipeline, self.st, lockstep=opts.qa_lockstep,
                                         replicas=list(opts.qa_replicas) or None)
         if "ingest" in svc:
