@@ -928,6 +928,27 @@ std::tuple<at::Tensor, at::Tensor> knn(const at::Tensor& xb, const at::Tensor& x
   return {out_d, out_i};
 }
 
+// IVF coarse quantizer, wide probes: int64 [nq, nprobe] nearest centroids (ascending, ties
+// to the lower id) for nprobe <= 512
+at::Tensor coarse_probes(const at::Tensor& xq, const at::Tensor& cent, const at::Tensor& cnorm, int64_t nprobe) {
+  CHECK_GPU(xq); CHECK_GPU(cent); CHECK_GPU(cnorm);
+  CHECK_CONTIG(xq); CHECK_CONTIG(cent); CHECK_CONTIG(cnorm);
+  TORCH_CHECK(xq.scalar_type() == at::kFloat && cent.scalar_type() == at::kFloat && cnorm.scalar_type() == at::kFloat,
+              "coarse_probes: fp32 operands");
+  TORCH_CHECK(xq.dim() == 2 && cent.dim() == 2 && xq.size(1) == cent.size(1) && cnorm.numel() == cent.size(0),
+              "coarse_probes: shape mismatch");
+  const int nq = xq.size(0), d = xq.size(1), nlist = cent.size(0);
+  TORCH_CHECK(nprobe >= 1 && nprobe <= 512 && nprobe <= nlist, "coarse_probes: 1 <= nprobe <= min(512, nlist)");
+  TORCH_CHECK(d % 8 == 0 && (size_t)32 * d * 4 <= 160 * 1024, "coarse_probes: d % 8 == 0, d <= 1280");
+  c10::DeviceGuard g(xq.device());
+  auto ws = at::empty({nq, nlist}, xq.options());
+  auto probes = at::empty({nq, nprobe}, xq.options().dtype(at::kLong));
+  CHECK_RC(docqa_coarse_probes(cent.data_ptr<float>(), cnorm.data_ptr<float>(), nlist, d, xq.data_ptr<float>(), nq,
+                               (int)nprobe, ws.data_ptr<float>(), probes.data_ptr<int64_t>(), stream()),
+           "coarse_probes");
+  return probes;
+}
+
 at::Tensor pool_l2(const at::Tensor& h, const at::Tensor& cu_seqlens, bool mean, bool normalize) {
   CHECK_GPU(h); CHECK_BF16(h); CHECK_CONTIG(h); CHECK_I32(cu_seqlens);
   const int H = h.size(-1);
@@ -1077,6 +1098,7 @@ TORCH_LIBRARY(docqa, m) {
   m.def("knn(Tensor xb, Tensor xb_norms, Tensor xq, int k, bool inner_product, int id_offset) "
         "-> (Tensor, Tensor)");
   m.def("pool_l2(Tensor h, Tensor cu_seqlens, bool mean, bool normalize) -> Tensor");
+  m.def("coarse_probes(Tensor xq, Tensor cent, Tensor cnorm, int nprobe) -> Tensor");
   m.def("ivfpq_search(Tensor xq, Tensor centroids, Tensor pq, Tensor codes, Tensor ids, "
         "Tensor list_off, Tensor probes, int k) -> (Tensor, Tensor)");
   m.def("pq_encode(Tensor x, Tensor centroids, Tensor assign, Tensor pq) -> Tensor");
@@ -1165,6 +1187,7 @@ TORCH_LIBRARY_IMPL(docqa, CUDA, m) {
   m.impl("pgemm_partial", &pgemm_partial);
   m.impl("mgemm_argmax_val", &mgemm_argmax_val);
   m.impl("wgemm", &wgemm);
+  m.impl("coarse_probes", &coarse_probes);
   m.impl("wgemm_glu", &wgemm_glu);
   m.impl("wgemm_argmax_val", &wgemm_argmax_val);
   m.impl("paged_decode_fused", &paged_decode_fused);

@@ -123,6 +123,9 @@ int docqa_mgemm_glu(const void* X, const void* W, void* Y, int M, int N, int K, 
 int docqa_mgemm_argmax(const void* X, const void* W, int64_t* out, float* outv, float* ws_v, int* ws_i, int M,
                        int N, int K, int n_valid, int cfg, hipStream_t s);
 int docqa_mgemm_tile_n(int cfg);
+// IVF coarse quantizer for wide probes (coarse.hip): nprobe <= 512 nearest centroids per query
+int docqa_coarse_probes(const float* cent, const float* cnorm, int nlist, int d, const float* xq, int nq,
+                        int nprobe, float* ws, int64_t* probes, hipStream_t s);
 // mid-M decode GEMM with the weights streamed into VGPRs (wgemm.hip): X-only LDS ring,
 // 256 x 256 tiles; split-K slabs / bf16 / fused SwiGLU (S = 1, or 2 with an in-launch
 // K-half hand-off through ws + tick) / fused LM-head argmax

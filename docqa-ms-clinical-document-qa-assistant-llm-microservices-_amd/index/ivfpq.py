@@ -133,10 +133,10 @@ class IVFPQIndex:
         nprobe = min(nprobe or self.nprobe, self.nlist)
         xq = self._in(xq).contiguous()
         cn = (self.centroids ** 2).sum(1)
-        if nprobe <= 64:
+        if nprobe <= 64 and self.device.type == "cuda":
             _, probes = ops.knn(self.centroids, cn, xq, nprobe, False, 0)
-        else:   # wide probes (recall sweeps): the coarse distances are a small GEMM
-            probes = torch.topk(cn[None, :] - 2 * xq @ self.centroids.t(), nprobe, dim=1, largest=False).indices
+        else:   # wide probes (the 10M operating points: nprobe 128..512): coarse.hip
+            probes = ops.coarse_probes(xq, self.centroids, cn, nprobe)
         if self.device.type == "cuda":
             return ops._native().ivfpq_search(xq, self.centroids, self.pq, self.codes, self.ids,
                                               self.list_off, probes.contiguous(), k)

@@ -789,6 +789,15 @@ def knn(xb, xb_norms, xq, k: int, inner_product: bool = False, id_offset: int = 
     return ref.knn(xb, xb_norms, xq, k, inner_product, id_offset)
 
 
+def coarse_probes(xq, centroids, cnorm, nprobe: int):
+    """IVF coarse quantizer: int64 [nq, nprobe] nearest centroids by squared L2, ascending,
+    ties to the lower centroid id.  GPU: csrc/kernels/coarse.hip (MFMA fp32 distances +
+    radix select, nprobe <= 512); nprobe <= 64 may also use :func:`knn`."""
+    if _gpu(xq):
+        return _native().coarse_probes(xq.float().contiguous(), centroids, cnorm, int(nprobe))
+    return ref.coarse_probes(xq, centroids, cnorm, nprobe)
+
+
 # ----------------------------------------------------------------------------- pooling
 def pool_l2(h, cu_seqlens, mean: bool = True, normalize: bool = True):
     if _gpu(h):

@@ -331,3 +331,11 @@ def decode_advance(nxt, out, tokens, positions, context_lens, valid) -> None:
     tokens.copy_(nxt.int())
     positions.add_(valid)
     context_lens.add_(valid)
+
+
+def coarse_probes(xq, centroids, cnorm, nprobe: int):
+    """fp32 reference of csrc/kernels/coarse.hip: ||c||^2 - 2 q.c per (query, centroid),
+    the nprobe smallest in ascending order, ties to the lower centroid id (stable sort)."""
+    d = cnorm.float()[None, :] - 2.0 * (xq.float() @ centroids.float().t())
+    order = torch.sort(d, dim=1, stable=True).indices
+    return order[:, :nprobe].contiguous()
