@@ -688,6 +688,43 @@ at::Tensor mgemm_glu(const at::Tensor& x, const at::Tensor& w, int64_t cfg) {
   return out;
 }
 
+// the same with the K range split over S = 1 / 2 workgroups per tile meeting in the launch
+// (mgemm.hip glu_meet); ws fp32 [m-tiles x N x 256], tick int32 [2 T + 1] (T = m-tiles x
+// N / tile_n, then the sticky error word), tickets zeroed once and re-armed by the kernel
+at::Tensor mgemm_glu_split(const at::Tensor& x, const at::Tensor& w, int64_t splits, int64_t cfg,
+                           const c10::optional<at::Tensor>& ws, const c10::optional<at::Tensor>& tick) {
+  CHECK_GPU(x); CHECK_BF16(x); CHECK_BF16(w); CHECK_CONTIG(x); CHECK_CONTIG(w);
+  CHECK_ALIGN16(x); CHECK_ALIGN16(w);
+  const int K = x.size(-1), N = w.size(0);
+  TORCH_CHECK(w.size(1) == K && N % 16 == 0, "mgemm_glu_split: shape mismatch");
+  TORCH_CHECK(splits == 1 || splits == 2, "mgemm_glu_split: splits 1 or 2");
+  const int M = x.numel() / K;
+  float* wsp = nullptr;
+  int* tk = nullptr;
+  int* err = nullptr;
+  if (splits == 2) {
+    TORCH_CHECK(ws.has_value() && tick.has_value(), "mgemm_glu_split: splits 2 needs ws and tick");
+    CHECK_GPU(*ws); CHECK_GPU(*tick); CHECK_I32(*tick); CHECK_CONTIG(*ws); CHECK_CONTIG(*tick);
+    TORCH_CHECK(ws->scalar_type() == at::kFloat, "mgemm_glu_split: ws must be fp32");
+    const int bn = docqa_mgemm_tile_n((int)cfg);
+    TORCH_CHECK(bn > 0 && N % bn == 0, "mgemm_glu_split: N must be a multiple of the tile");
+    const int64_t mt = (M + 255) / 256, tiles = mt * (N / bn);
+    TORCH_CHECK(ws->numel() >= mt * N * 256 && tick->numel() >= 2 * tiles + 1, "mgemm_glu_split: workspace too small");
+    wsp = ws->data_ptr<float>();
+    tk = tick->data_ptr<int>();
+    err = tk + 2 * tiles;
+  }
+  auto sizes = x.sizes().vec();
+  sizes.back() = N / 2;
+  c10::DeviceGuard g(x.device());
+  auto out = at::empty(sizes, x.options());
+  CHECK_RC(docqa_mgemm_glu_split(x.data_ptr(), w.data_ptr(), out.data_ptr(), wsp, tk, err, M, N, K, (int)splits,
+                                 (int)cfg, stream()), "mgemm_glu_split");
+  return out;
+}
+
+int64_t mgemm_tile_n(int64_t cfg) { return docqa_mgemm_tile_n((int)cfg); }
+
 // persistent decode-layer chain (TP = 1, 193..512 rows): attn [M, Ko] -> residual updated in
 // place twice, returns (x2 [M, H] = the next layer's normed input, the next layer's QKV
 // split-K slabs [S_q, M, Nq] or an empty tensor when w_qkv is None)
@@ -1110,6 +1147,8 @@ TORCH_LIBRARY(docqa, m) {
   m.def("dgemm_glu(Tensor x, Tensor w) -> Tensor");
   m.def("mgemm(Tensor x, Tensor w, int splits, int cfg=0) -> Tensor");
   m.def("mgemm_glu(Tensor x, Tensor w, int cfg=0) -> Tensor");
+  m.def("mgemm_glu_split(Tensor x, Tensor w, int splits, int cfg=0, Tensor? ws=None, Tensor? tick=None) -> Tensor");
+  m.def("mgemm_tile_n(int cfg) -> int", &mgemm_tile_n);
   m.def("mgemm_chain(Tensor attn, Tensor w_o, Tensor(a!) residual, Tensor post_norm, Tensor w_gu, Tensor w_down, "
         "Tensor next_norm, Tensor? w_qkv, Tensor(b!) counters, int S_o, int cfg_o, int S_d, int cfg_d, int S_q, "
         "int cfg_q, float eps, Tensor? trace=None) "
@@ -1181,6 +1220,7 @@ TORCH_LIBRARY_IMPL(docqa, CUDA, m) {
   m.impl("dgemm_glu", &dgemm_glu);
   m.impl("mgemm", &mgemm);
   m.impl("mgemm_glu", &mgemm_glu);
+  m.impl("mgemm_glu_split", &mgemm_glu_split);
   m.impl("mgemm_chain", &mgemm_chain);
   m.impl("mgemm_argmax", &mgemm_argmax);
   m.impl("pgemm", &pgemm);

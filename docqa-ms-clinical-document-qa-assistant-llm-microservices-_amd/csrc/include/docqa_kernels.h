@@ -120,6 +120,8 @@ int docqa_gemm(const void* A, const void* W, const void* bias, const void* res, 
 int docqa_mgemm(const void* X, const void* W, void* Y, float* P, int M, int N, int K, int S, int cfg,
                 hipStream_t s);
 int docqa_mgemm_glu(const void* X, const void* W, void* Y, int M, int N, int K, int cfg, hipStream_t s);
+int docqa_mgemm_glu_split(const void* X, const void* W, void* Y, float* ws, int* tick, int* err, int M, int N, int K,
+                          int S, int cfg, hipStream_t s);
 int docqa_mgemm_argmax(const void* X, const void* W, int64_t* out, float* outv, float* ws_v, int* ws_i, int M,
                        int N, int K, int n_valid, int cfg, hipStream_t s);
 int docqa_mgemm_tile_n(int cfg);

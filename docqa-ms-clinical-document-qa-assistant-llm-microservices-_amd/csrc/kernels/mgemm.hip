@@ -185,12 +185,72 @@ __device__ __forceinline__ void mgemm_epilogue(f32x4 (&acc)[BM / WM / 16][BN / W
 // One (m-tile, weight tile, K slice) of the GEMM on the workgroup's LDS ring `smem`
 // (NSR * (BM + BN) * BKS bf16): the standalone kernel below runs one per workgroup, the
 // persistent decode-layer chain (mgemm_chain_kernel) runs them as work items.
+// 2-way split-K meeting of a fused-SwiGLU tile (wgemm.hip has the same protocol): the first
+// K half to finish parks its fp32 accumulators in ws (write-through, acc-native layout: 16 B
+// per lane, fully coalesced) and raises tick[2 tix + 1]; the second adds them and runs the
+// epilogue.  The second only waits on a half that already drew its ticket, i.e. is
+// resident: no deadlock for any residency; fp32 a + b == b + a keeps the bits independent
+// of the arrival order.  Returns true when this workgroup runs the epilogue.
+template <int MI, int NJ, int WAVES>
+__device__ __forceinline__ bool glu_meet(f32x4 (&acc)[MI][NJ], uint16_t* smem, float* __restrict__ ws,
+                                         int* __restrict__ tick, int* __restrict__ err, int tix) {
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  int* tk = reinterpret_cast<int*>(smem);
+  if (tid == 0) tk[0] = __hip_atomic_fetch_add(&tick[2 * tix], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __syncthreads();
+  const bool first = tk[0] == 0;
+  __syncthreads();          // every wave read the ticket before the epilogue reuses smem
+  float* slab = ws + ((size_t)tix * WAVES + wave) * (MI * NJ * 256) + lane * 4;
+  if (first) {
+#pragma unroll
+    for (int i = 0; i < MI; ++i)
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) {
+        const f32x4 v = acc[i][j];
+        store16_wt(slab + (i * NJ + j) * 256,
+                   uint4{__float_as_uint(v[0]), __float_as_uint(v[1]), __float_as_uint(v[2]), __float_as_uint(v[3])});
+      }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (tid == 0) __hip_atomic_store(&tick[2 * tix + 1], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return false;
+  }
+  if (tid == 0) {
+    int it = 0;
+    while (__hip_atomic_load(&tick[2 * tix + 1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0) {
+      if (++it > (1 << 24)) {   // a lost hand-off: report, never hang the GPU
+        __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        break;
+      }
+      __builtin_amdgcn_s_sleep(2);
+    }
+  }
+  __syncthreads();
+#pragma unroll
+  for (int i = 0; i < MI; ++i)
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) {
+      f32x4 d;
+      asm volatile("global_load_dwordx4 %0, %1, off sc1\n\ts_waitcnt vmcnt(0)" : "=v"(d) : "v"(slab + (i * NJ + j) * 256)
+                   : "memory");
+      acc[i][j] += d;
+    }
+  if (tid == 0) {   // both halves are past every use of the words: re-arm for the next launch
+    __hip_atomic_store(&tick[2 * tix], 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(&tick[2 * tix + 1], 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  return true;
+}
+
 template <int EPI, int BN, int BKS, int NSR, int WM, int WN, int PF = 1, bool WT = false>
 __device__ __forceinline__ void mgemm_tile(uint16_t* smem, const uint16_t* __restrict__ X,
                                            const uint16_t* __restrict__ W, uint16_t* __restrict__ Y,
                                            float* __restrict__ P, float* __restrict__ pv,
                                            int* __restrict__ pi, int M, int N, int K, int Ks,
-                                           int tile, int slice, int m0, int ntiles, int n_valid) {
+                                           int tile, int slice, int m0, int ntiles, int n_valid,
+                                           float* __restrict__ ws = nullptr, int* __restrict__ tick = nullptr,
+                                           int* __restrict__ err = nullptr, int S = 1) {
   constexpr int WAVES = WM * WN;
   constexpr int MI = BM / WM / 16;                      // 16-row m-tiles per wave
   constexpr int CW = BN / WN;                           // output columns per wave
@@ -363,6 +423,9 @@ __device__ __forceinline__ void mgemm_tile(uint16_t* smem, const uint16_t* __res
   wait_vmcnt<0>();
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   ring_barrier();   // every wave is done reading the ring: reuse it as epilogue scratch
+  if constexpr (EPI == EPI_GLU) {
+    if (S == 2 && !glu_meet<MI, NJ, WAVES>(acc, smem, ws, tick, err, (m0 / BM) * ntiles + tile)) return;
+  }
   mgemm_epilogue<EPI, BN, WM, WN, WT>(acc, smem, Y, P, pv, pi, M, N, m0, n0, slice, tile, ntiles, n_valid);
 }
 
@@ -373,7 +436,9 @@ __global__ __launch_bounds__(WM * WN * 64) void mgemm_kernel(const uint16_t* __r
                                                              float* __restrict__ P,
                                                              float* __restrict__ pv, int* __restrict__ pi,
                                                              int M, int N, int K, int Ks, int S,
-                                                             int ntiles, int remap, int n_valid) {
+                                                             int ntiles, int remap, int n_valid,
+                                                             float* __restrict__ ws, int* __restrict__ tick,
+                                                             int* __restrict__ err) {
   __shared__ __attribute__((aligned(16))) uint16_t smem[NSR * (BM + BN) * BKS];
   const int L = blockIdx.x;
   int tile, slice;
@@ -390,7 +455,7 @@ __global__ __launch_bounds__(WM * WN * 64) void mgemm_kernel(const uint16_t* __r
     slice = L / ntiles;
   }
   mgemm_tile<EPI, BN, BKS, NSR, WM, WN, PF>(smem, X, W, Y, P, pv, pi, M, N, K, Ks, tile, slice, blockIdx.y * BM,
-                                            ntiles, n_valid);
+                                            ntiles, n_valid, ws, tick, err, S);
 }
 
 __global__ __launch_bounds__(64) void mgemm_argmax_merge(const float* __restrict__ pv,
@@ -442,7 +507,8 @@ constexpr Cfg kCfg[kNumCfg + 1] = {{0, 0}, {128, 64}, {128, 64}, {256, 32}, {256
 
 template <int EPI, int BN, int BKS, int NSR, int WM, int WN, int PF = 1>
 int launch(const uint16_t* x, const uint16_t* w, uint16_t* y, float* p, float* pv, int* pi, int M,
-           int N, int K, int S, int n_valid, hipStream_t s) {
+           int N, int K, int S, int n_valid, hipStream_t s, float* ws = nullptr, int* tick = nullptr,
+           int* err = nullptr) {
   // the epilogue sweeps 16-row slices with (columns per wave) / (columns per lane) lanes per
   // row: the SwiGLU epilogue (16 columns per lane) needs >= 64 columns per wave
   if constexpr (EPI == EPI_GLU && BN / WN < 64) {
@@ -454,7 +520,7 @@ int launch(const uint16_t* x, const uint16_t* w, uint16_t* y, float* p, float* p
   else if (S > 8 && S % 8 == 0) remap = 2;
   dim3 grid(ntiles * S, (M + BM - 1) / BM);
   mgemm_kernel<EPI, BN, BKS, NSR, WM, WN, PF><<<grid, WM * WN * 64, 0, s>>>(x, w, y, p, pv, pi, M, N, K, Ks, S,
-                                                                      ntiles, remap, n_valid);
+                                                                      ntiles, remap, n_valid, ws, tick, err);
   DOCQA_CHECK_LAUNCH();
   return 0;
   }
@@ -462,15 +528,16 @@ int launch(const uint16_t* x, const uint16_t* w, uint16_t* y, float* p, float* p
 
 template <int EPI>
 int launch_cfg(int cfg, const uint16_t* x, const uint16_t* w, uint16_t* y, float* p, float* pv, int* pi,
-               int M, int N, int K, int S, int n_valid, hipStream_t s) {
+               int M, int N, int K, int S, int n_valid, hipStream_t s, float* ws = nullptr, int* tick = nullptr,
+               int* err = nullptr) {
   switch (cfg) {
-    case 1: return launch<EPI, 128, 64, 3, 2, 2>(x, w, y, p, pv, pi, M, N, K, S, n_valid, s);
-    case 2: return launch<EPI, 128, 64, 3, 4, 2>(x, w, y, p, pv, pi, M, N, K, S, n_valid, s);
-    case 3: return launch<EPI, 256, 32, 4, 2, 4>(x, w, y, p, pv, pi, M, N, K, S, n_valid, s);
-    case 4: return launch<EPI, 256, 32, 4, 2, 2>(x, w, y, p, pv, pi, M, N, K, S, n_valid, s);
-    case 5: return launch<EPI, 256, 64, 2, 2, 2, 0>(x, w, y, p, pv, pi, M, N, K, S, n_valid, s);
-    case 6: return launch<EPI, 256, 64, 2, 2, 4, 0>(x, w, y, p, pv, pi, M, N, K, S, n_valid, s);
-    case 7: return launch<EPI, 64, 64, 3, 4, 2>(x, w, y, p, pv, pi, M, N, K, S, n_valid, s);
+    case 1: return launch<EPI, 128, 64, 3, 2, 2>(x, w, y, p, pv, pi, M, N, K, S, n_valid, s, ws, tick, err);
+    case 2: return launch<EPI, 128, 64, 3, 4, 2>(x, w, y, p, pv, pi, M, N, K, S, n_valid, s, ws, tick, err);
+    case 3: return launch<EPI, 256, 32, 4, 2, 4>(x, w, y, p, pv, pi, M, N, K, S, n_valid, s, ws, tick, err);
+    case 4: return launch<EPI, 256, 32, 4, 2, 2>(x, w, y, p, pv, pi, M, N, K, S, n_valid, s, ws, tick, err);
+    case 5: return launch<EPI, 256, 64, 2, 2, 2, 0>(x, w, y, p, pv, pi, M, N, K, S, n_valid, s, ws, tick, err);
+    case 6: return launch<EPI, 256, 64, 2, 2, 4, 0>(x, w, y, p, pv, pi, M, N, K, S, n_valid, s, ws, tick, err);
+    case 7: return launch<EPI, 64, 64, 3, 4, 2>(x, w, y, p, pv, pi, M, N, K, S, n_valid, s, ws, tick, err);
     default: return -1;
   }
 }
@@ -501,13 +568,25 @@ int docqa_mgemm(const void* X, const void* W, void* Y, float* P, int M, int N, i
   return launch_cfg<EPI_BF16>(cfg, x, w, (uint16_t*)Y, nullptr, nullptr, nullptr, M, N, K, 1, N, s);
 }
 
+int docqa_mgemm_glu_split(const void* X, const void* W, void* Y, float* ws, int* tick, int* err, int M, int N, int K,
+                          int S, int cfg, hipStream_t s);
+
 // Y[M, N/2] = silu(gate) * up for the 8-interleaved gate|up weight W [N, K] (N = 2 I)
 int docqa_mgemm_glu(const void* X, const void* W, void* Y, int M, int N, int K, int cfg, hipStream_t s) {
+  return docqa_mgemm_glu_split(X, W, Y, nullptr, nullptr, nullptr, M, N, K, 1, cfg, s);
+}
+
+// the same with the K range split over S = 1 or 2 workgroups per tile that meet in the
+// launch (glu_meet): ws fp32 [m-tiles x N x 256], tick int32 [2 x m-tiles x N / tile_n]
+// zeroed once (re-armed by the kernel), err: sticky int32 error word
+int docqa_mgemm_glu_split(const void* X, const void* W, void* Y, float* ws, int* tick, int* err, int M, int N, int K,
+                          int S, int cfg, hipStream_t s) {
   if (cfg == 0) cfg = kDefaultCfg;
   if (M == 0) return 0;
-  if (!shape_ok(M, N, K, 1, cfg) || !docqa_aligned16(X) || !docqa_aligned16(W) || !docqa_aligned16(Y)) return -1;
+  if ((S != 1 && S != 2) || (S == 2 && (!ws || !tick || !err || !docqa_aligned16(ws)))) return -1;
+  if (!shape_ok(M, N, K, S, cfg) || !docqa_aligned16(X) || !docqa_aligned16(W) || !docqa_aligned16(Y)) return -1;
   return launch_cfg<EPI_GLU>(cfg, (const uint16_t*)X, (const uint16_t*)W, (uint16_t*)Y, nullptr, nullptr, nullptr,
-                             M, N, K, 1, N, s);
+                             M, N, K, S, N, s, ws, tick, err);
 }
 
 // out[M] = argmax over the first n_valid columns of bf16(X . W^T) (LM head + greedy pick),

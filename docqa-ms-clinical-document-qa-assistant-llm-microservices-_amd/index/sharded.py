@@ -9,8 +9,11 @@ each), searched with two collectives per query batch over RCCL/xGMI:
      and merge to the global top-k; every rank keeps the rows of its own queries.
 
 Payloads are tiny (queries: nq x d fp32; results: nq x k x 12 B), so the collectives are
-latency-bound and a single ring step per link is all xGMI has to carry.  Shards may be
-any size (the all-gather carries explicit counts).
+latency-bound.  On the GPU both all-gathers run on the IPC peer-memory kernel
+(parallel/custom_ar.py GATHER mode: every rank reads its peers' staging buffers over all
+xGMI links at once, graph-capturable, off RCCL) when ``enable_ipc`` succeeded; RCCL /
+gloo ``all_gather`` is the fallback (CPU, or a node without IPC).  Shards may be any size
+(the count-exchange path carries explicit counts).
 
 Reference parity: no distributed index exists in the reference (one FAISS file,
 semantic-indexer/indexer.py:17-18); this is the config-5 "index sharded across 8 GPUs".
@@ -45,7 +48,33 @@ class ShardedIndex:
             self.group = s.dp_group
         self._offset = 0
         self._ntotal = local.ntotal
+        self._ipc = None
         self.refresh()
+
+    def enable_ipc(self, max_bytes: int = 16 << 20) -> bool:
+        """Route the per-batch all-gathers through the IPC peer-memory kernel (collective:
+        every rank of the group calls it; all fall back to RCCL together on failure)."""
+        if self.world == 1 or self._ipc is not None or self.local.device.type != "cuda":
+            return self._ipc is not None
+        from ..parallel.custom_ar import CustomAllReduce
+
+        try:
+            self._ipc = CustomAllReduce(group=self.group, max_bytes=max_bytes, device=self.local.device)
+        except Exception as e:  # noqa: BLE001 - collective decision inside the constructor
+            print(f"[sharded] IPC all-gather unavailable ({e}); using the process group", flush=True)
+            self._ipc = None
+        return self._ipc is not None
+
+    def _all_gather(self, t: torch.Tensor) -> torch.Tensor:
+        """[world, *t.shape] -- IPC peer-memory gather when enabled, else the process group."""
+        t = t.contiguous()
+        if self._ipc is not None and t.is_cuda:
+            nb = t.numel() * t.element_size()
+            if nb % 16 == 0 and nb // 2 <= self._ipc.max_elems:
+                return self._ipc.all_gather_raw(t)
+        parts = [torch.empty_like(t) for _ in range(self.world)]
+        dist.all_gather(parts, t, group=self.group)
+        return torch.stack(parts)
 
     @property
     def d(self) -> int:
@@ -85,9 +114,8 @@ class ShardedIndex:
             mx = self.max_queries
             pad = torch.zeros(mx, self.d, device=dev, dtype=torch.float32)
             pad[:nq] = xq
-            allq = [torch.empty_like(pad) for _ in range(self.world)]
-            dist.all_gather(allq, pad, group=self.group)
-            D, I = self.local.search(torch.cat(allq, 0), k, id_offset=self._offset, **kw)
+            allq = self._all_gather(pad)
+            D, I = self.local.search(allq.view(self.world * mx, self.d), k, id_offset=self._offset, **kw)
             return self._merge(D, I, k, self.rank * mx, nq)
         cnt = torch.tensor([nq], dtype=torch.long, device=dev)
         cnts = [torch.empty_like(cnt) for _ in range(self.world)]
@@ -105,12 +133,19 @@ class ShardedIndex:
     def _merge(self, D, I, k: int, start: int, nq: int):
         """all-gather every shard's top-k (dist, id) and keep the global top-k of rows
         [start, start + nq)."""
-        allD = [torch.empty_like(D) for _ in range(self.world)]
-        allI = [torch.empty_like(I) for _ in range(self.world)]
-        dist.all_gather(allD, D.contiguous(), group=self.group)
-        dist.all_gather(allI, I.contiguous(), group=self.group)
-        Dc = torch.cat(allD, 1)  # [tot, W*k]
-        Ic = torch.cat(allI, 1)
+        rows = D.shape[0]
+        # one payload per batch: fp32 distances and int64 ids side by side as int32 words
+        pack = torch.cat([D.float().contiguous().view(torch.int32), I.to(torch.int64).contiguous().view(torch.int32)], 1)
+        if (pack.numel() * 4) % 16:
+            pad = torch.zeros(4 - pack.numel() % 4, dtype=torch.int32, device=pack.device)
+            flat = torch.cat([pack.view(-1), pad])
+            allp = self._all_gather(flat)[:, : pack.numel()].reshape(self.world, rows, 3 * k)
+        else:
+            allp = self._all_gather(pack)
+        allD = allp[:, :, :k].contiguous().view(torch.float32)               # [W, rows, k]
+        allI = allp[:, :, k:].contiguous().view(torch.int64)
+        Dc = allD.permute(1, 0, 2).reshape(rows, self.world * k)   # [tot, W*k]
+        Ic = allI.permute(1, 0, 2).reshape(rows, self.world * k)
         largest = self.local.metric == "ip"
         vals, pos = torch.topk(Dc, k, dim=1, largest=largest)
         ids = torch.gather(Ic, 1, pos)

@@ -1,6 +1,7 @@
 """Assemble the QA stack (encoder + index + generator) for services, bench and smoke."""
 from __future__ import annotations
 
+import os
 import time
 from dataclasses import dataclass
 
@@ -51,6 +52,9 @@ def build_stack(sc: StackConfig, device="cuda", log=print) -> tuple[RAGPipeline,
     local.add(emb)
     # queries padded to the static batch size: no per-search count exchange / host sync
     index = ShardedFlatIndex(local, max_queries=sc.max_batch) if s.dp_size > 1 else local
+    if s.dp_size > 1 and os.environ.get("DOCQA_SHARD_IPC", "1") == "1":
+        # per-batch query / top-k all-gathers on the IPC peer-memory kernel (off RCCL)
+        index.enable_ipc()
     if device != "cpu" and torch.device(device).type == "cuda":
         torch.cuda.synchronize()
     info["index_build_s"] = time.perf_counter() - t0

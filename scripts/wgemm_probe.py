@@ -33,6 +33,11 @@ for (name, N, K) in [("qkv", 6144, 4096), ("o", 4096, 4096), ("gate_up", 28672, 
         row["hipblaslt"] = t(lambda w: F.linear(x, w))
         if name == "gate_up":
             row["mgemm_glu_c2"] = t(lambda w: nat.mgemm_glu(x, w, 2))
+            mt = (M + 255) // 256
+            for c in (3, 5, 6):
+                wsb = torch.empty(mt * N * 256, device="cuda", dtype=torch.float32)
+                tick = torch.zeros(2 * mt * (N // nat.mgemm_tile_n(c)) + 1, device="cuda", dtype=torch.int32)
+                row[f"mgemm_glu_c{c}_S2"] = t(lambda w: nat.mgemm_glu_split(x, w, 2, c, wsb, tick))
         elif name == "lm_head":
             row["mgemm_argmax_c6"] = t(lambda w: nat.mgemm_argmax(x, w, N, 6))
         else:

@@ -112,3 +112,28 @@ def test_mgemm_argmax_ties(native):
     w[700:] = 0.75
     w[1500] = 1.0
     assert (torch.ops.docqa.mgemm_argmax(x, w, N, 4) == 1500).all()
+
+
+@pytest.mark.parametrize("M", [200, 256, 333])
+@pytest.mark.parametrize("cfg", [2, 3, 5, 6])
+def test_mgemm_glu_split2(native, M, cfg):
+    """Fused SwiGLU with the K range split over two workgroups per tile that meet in the
+    launch (mgemm.hip glu_meet): same result as the reference, bitwise identical across
+    launches whichever half arrives first, tickets re-armed."""
+    from docqa_amd.ops import reference as R
+
+    N, K = 28672, 4096
+    x = torch.randn(M, K, device="cuda", dtype=torch.bfloat16)
+    w = (torch.randn(N, K, device="cuda") / K ** 0.5).bfloat16()
+    ref = R.silu_mul((x.float() @ w.float().T).bfloat16(), interleaved=True)
+    bn = torch.ops.docqa.mgemm_tile_n(cfg)
+    mt = (M + 255) // 256
+    ws = torch.empty(mt * N * 256, device="cuda", dtype=torch.float32)
+    tick = torch.zeros(2 * mt * (N // bn) + 1, device="cuda", dtype=torch.int32)
+    outs = [torch.ops.docqa.mgemm_glu_split(x, w, 2, cfg, ws, tick) for _ in range(3)]
+    for o in outs:
+        _close(o, ref, 2e-2, 1e-2)
+        assert torch.equal(o, outs[0])
+    assert int(tick.abs().sum()) == 0
+    one = torch.ops.docqa.mgemm_glu_split(x, w, 1, cfg)
+    _close(one, ref, 2e-2, 1e-2)
