@@ -898,6 +898,24 @@ std::tuple<at::Tensor, at::Tensor> wgemm_argmax_val(const at::Tensor& x, const a
   return {out, outv};
 }
 
+// LM head + greedy pick at <= 192 rows on the skinny decode GEMM (dgemm.hip EPI_ARGMAX)
+std::tuple<at::Tensor, at::Tensor> dgemm_argmax_val(const at::Tensor& x, const at::Tensor& w, int64_t n_valid) {
+  CHECK_GPU(x); CHECK_BF16(x); CHECK_BF16(w); CHECK_CONTIG(x); CHECK_CONTIG(w);
+  const int K = x.size(-1), N = w.size(0);
+  TORCH_CHECK(w.size(1) == K && N % 64 == 0 && K % 512 == 0, "dgemm_argmax: N % 64, K % 512");
+  const int M = x.numel() / K;
+  TORCH_CHECK(M <= 192, "dgemm_argmax: at most 192 rows");
+  c10::DeviceGuard g(x.device());
+  auto out = at::empty({M}, x.options().dtype(at::kLong));
+  auto outv = at::empty({M}, x.options().dtype(at::kFloat));
+  auto ws_v = at::empty({M, N / 64}, x.options().dtype(at::kFloat));
+  auto ws_i = at::empty({M, N / 64}, x.options().dtype(at::kInt));
+  CHECK_RC(docqa_dgemm_argmax(x.data_ptr(), w.data_ptr(), out.data_ptr<int64_t>(), outv.data_ptr<float>(),
+                              ws_v.data_ptr<float>(), ws_i.data_ptr<int>(), M, N, K, (int)n_valid, stream()),
+           "dgemm_argmax");
+  return {out, outv};
+}
+
 // prefill GEMM (pgemm.hip, 256 x 256 tiles): epi 0 -> x . w^T bf16 [.., N]; epi 1 -> fused
 // SwiGLU over 8-interleaved gate|up rows -> [.., N / 2]
 at::Tensor pgemm(const at::Tensor& x, const at::Tensor& w, int64_t epi) {
@@ -1157,6 +1175,7 @@ TORCH_LIBRARY(docqa, m) {
   m.def("wgemm(Tensor x, Tensor w, int splits, int cfg=0) -> Tensor");
   m.def("wgemm_glu(Tensor x, Tensor w, int splits, int cfg=0, Tensor? ws=None, Tensor? tick=None) -> Tensor");
   m.def("wgemm_argmax_val(Tensor x, Tensor w, int n_valid, int cfg=0) -> (Tensor, Tensor)");
+  m.def("dgemm_argmax_val(Tensor x, Tensor w, int n_valid) -> (Tensor, Tensor)");
   m.def("pgemm(Tensor x, Tensor w, int epi=0) -> Tensor");
   m.def("pgemm_partial(Tensor x, Tensor w, int splits) -> Tensor");
   m.def("mgemm_argmax_val(Tensor x, Tensor w, int n_valid, int cfg=0) -> (Tensor, Tensor)");
@@ -1230,6 +1249,7 @@ TORCH_LIBRARY_IMPL(docqa, CUDA, m) {
   m.impl("coarse_probes", &coarse_probes);
   m.impl("wgemm_glu", &wgemm_glu);
   m.impl("wgemm_argmax_val", &wgemm_argmax_val);
+  m.impl("dgemm_argmax_val", &dgemm_argmax_val);
   m.impl("paged_decode_fused", &paged_decode_fused);
   m.impl("paged_decode_cascade", &paged_decode_cascade);
   m.impl("paged_decode_cascade_rope", &paged_decode_cascade_rope);

@@ -113,6 +113,8 @@ int docqa_paged_decode_fused(const float* P, int S, const int* positions, const 
                              int BS, int max_parts, float scale, const int* order, hipStream_t s);
 int docqa_dgemm_splits(int N, int K);
 int docqa_dgemm_glu(const void* X, const void* W, void* Y, int M, int N, int K, hipStream_t s);
+int docqa_dgemm_argmax(const void* X, const void* W, int64_t* out, float* outv, float* ws_v, int* ws_i, int M,
+                       int N, int K, int n_valid, hipStream_t s);
 int docqa_dgemm(const void* X, const void* W, void* Y, float* partial, int M, int N, int K, int S,
                 hipStream_t s);
 int docqa_gemm(const void* A, const void* W, const void* bias, const void* res, void* C, int M,

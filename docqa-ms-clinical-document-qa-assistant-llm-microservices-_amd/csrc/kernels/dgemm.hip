@@ -30,6 +30,7 @@
 // (M <= 192 with 64-row weight tiles: three m-tiles per wave, no fused SwiGLU).
 #include "docqa_common.h"
 #include "docqa_asm.h"
+#include "docqa_argmax.h"
 #include <stdlib.h>
 
 using namespace docqa;
@@ -37,7 +38,7 @@ using namespace docqa;
 namespace {
 constexpr int BN = 64, BKD = 128, NS = 4, MR = 192;   // NS: default ring slots, K granule 4 stages
 constexpr int KSTEPS = BKD / 32;               // 16x16x32 k-steps per stage
-enum { EPI_BF16 = 0, EPI_PARTIAL = 1, EPI_GLU = 2 };
+enum { EPI_BF16 = 0, EPI_PARTIAL = 1, EPI_GLU = 2, EPI_ARGMAX = 3 };
 typedef __attribute__((address_space(3))) void lds_void;
 
 // The ring's DMA / X loads are inline asm (docqa_asm.h): the counted waits below are the
@@ -96,7 +97,8 @@ __global__ __launch_bounds__(256) void dgemm_kernel(const uint16_t* __restrict__
                                                     const uint16_t* __restrict__ W,
                                                     uint16_t* __restrict__ Y,
                                                     float* __restrict__ P, int M, int N, int K,
-                                                    int Ks, int xcd_remap) {
+                                                    int Ks, int xcd_remap, float* __restrict__ pv = nullptr,
+                                                    int* __restrict__ pi = nullptr, int n_valid = 0) {
   constexpr int MPW = MT > 4 ? MT / 4 : 1;       // m-tiles per wave
   constexpr int MTW = MT > 4 ? 4 : MT;           // wave groups along m
   constexpr int KW = 4 / MTW, SPW = KSTEPS / KW;
@@ -243,6 +245,58 @@ __global__ __launch_bounds__(256) void dgemm_kernel(const uint16_t* __restrict__
     const float gb = bf2f(f2bf(g)), ub = bf2f(f2bf(u));   // as the unfused bf16 GEMM output
     Y[(size_t)row * (N >> 1) + ((col >> 4) << 3) + (col & 7)] = f2bf(silu_f(gb) * ub);
   };
+  if constexpr (EPI == EPI_ARGMAX) {
+    // LM head + greedy pick: the [rows, 64] logit tile through LDS (past the k-group
+    // reduction area), 4 lanes per row -> one (value, id) partial per (row, tile)
+    constexpr int TP = NT * 16 + 1;
+    __syncthreads();                                  // every wave done reading the ring
+    float* tl = reinterpret_cast<float*>(sw) + (KW == 1 ? 0 : 4 * NT * 64 * 4);
+    if constexpr (KW == 1) {
+#pragma unroll
+      for (int mi = 0; mi < MPW; ++mi)
+#pragma unroll
+        for (int nt = 0; nt < NT; ++nt)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) tl[((mt * MPW + mi) * 16 + fq * 4 + r) * TP + nt * 16 + fr] = acc[mi][nt][r];
+    } else {
+      f32x4* red = reinterpret_cast<f32x4*>(sw);      // [wave][nt][lane] = one slot
+#pragma unroll
+      for (int nt = 0; nt < NT; ++nt) red[(wave * NT + nt) * 64 + lane] = acc[0][nt];
+      __syncthreads();
+      const float* rf = reinterpret_cast<const float*>(sw);
+      for (int idx = tid; idx < MT * NT * 256; idx += 256) {
+        const int r = idx & 3, ln = (idx >> 2) & 63, q = idx >> 8;
+        const int nt = q % NT, m = q / NT;
+        float v = 0.f;
+#pragma unroll
+        for (int g = 0; g < KW; ++g) v += rf[(((g * MT + m) * NT + nt) * 64 + ln) * 4 + r];
+        tl[(m * 16 + (ln >> 4) * 4 + r) * TP + nt * 16 + (ln & 15)] = v;
+      }
+    }
+    __syncthreads();
+    const int ntiles = N / (NT * 16);
+    for (int rr = tid >> 2; rr < MT * 16; rr += 64) {
+      float bv = -FLT_MAX;
+      int bi = 0x7fffffff;
+      const int c0 = (tid & 3) * (NT * 4);
+#pragma unroll 4
+      for (int c = c0; c < c0 + NT * 4; ++c) {
+        const int col = n0 + c;
+        if (col < n_valid) argmax_better(bv, bi, bf2f(f2bf(tl[rr * TP + c])), col);
+      }
+#pragma unroll
+      for (int o = 1; o <= 2; o <<= 1) {
+        const float ov = __shfl_xor(bv, o, 64);
+        const int oi = __shfl_xor(bi, o, 64);
+        argmax_better(bv, bi, ov, oi);
+      }
+      if ((tid & 3) == 0 && rr < M) {
+        pv[(size_t)rr * ntiles + tile] = bv;
+        pi[(size_t)rr * ntiles + tile] = bi;
+      }
+    }
+    return;
+  }
   if constexpr (KW == 1) {
 #pragma unroll
     for (int mi = 0; mi < MPW; ++mi)
@@ -331,22 +385,24 @@ static int xcd_knob() {   // XCD-aware slice placement (A/B experiments): 1 on, 
 
 template <int EPI, int NT, int NSR = NS>
 static void launch_mt(int mt, dim3 grid, hipStream_t s, const uint16_t* x, const uint16_t* w,
-                      uint16_t* y, float* p, int M, int N, int K, int Ks) {
+                      uint16_t* y, float* p, int M, int N, int K, int Ks, float* pv = nullptr,
+                      int* pi = nullptr, int nv = 0) {
   const int S = grid.y;
   const int xr = (xcd_knob() && S > 1 && 8 % S == 0 && (grid.x * S) % 8 == 0) ? 1 : 0;
-  if (mt == 1) dgemm_kernel<EPI, 1, NT, NSR><<<grid, 256, 0, s>>>(x, w, y, p, M, N, K, Ks, xr);
-  else if (mt == 2) dgemm_kernel<EPI, 2, NT, NSR><<<grid, 256, 0, s>>>(x, w, y, p, M, N, K, Ks, xr);
-  else if (mt <= 4) dgemm_kernel<EPI, 4, NT, NSR><<<grid, 256, 0, s>>>(x, w, y, p, M, N, K, Ks, xr);
+  if (mt == 1) dgemm_kernel<EPI, 1, NT, NSR><<<grid, 256, 0, s>>>(x, w, y, p, M, N, K, Ks, xr, pv, pi, nv);
+  else if (mt == 2) dgemm_kernel<EPI, 2, NT, NSR><<<grid, 256, 0, s>>>(x, w, y, p, M, N, K, Ks, xr, pv, pi, nv);
+  else if (mt <= 4) dgemm_kernel<EPI, 4, NT, NSR><<<grid, 256, 0, s>>>(x, w, y, p, M, N, K, Ks, xr, pv, pi, nv);
   else if (mt <= 8) {
     if constexpr (NSR == 4) {
-      if (xa_knob() == 3) dgemm_kernel<EPI, 8, NT, NSR, 3><<<grid, 256, 0, s>>>(x, w, y, p, M, N, K, Ks, xr);
-      else dgemm_kernel<EPI, 8, NT, NSR><<<grid, 256, 0, s>>>(x, w, y, p, M, N, K, Ks, xr);
+      if (xa_knob() == 3)
+        dgemm_kernel<EPI, 8, NT, NSR, 3><<<grid, 256, 0, s>>>(x, w, y, p, M, N, K, Ks, xr, pv, pi, nv);
+      else dgemm_kernel<EPI, 8, NT, NSR><<<grid, 256, 0, s>>>(x, w, y, p, M, N, K, Ks, xr, pv, pi, nv);
     } else {
-      dgemm_kernel<EPI, 8, NT, NSR><<<grid, 256, 0, s>>>(x, w, y, p, M, N, K, Ks, xr);
+      dgemm_kernel<EPI, 8, NT, NSR><<<grid, 256, 0, s>>>(x, w, y, p, M, N, K, Ks, xr, pv, pi, nv);
     }
   } else if constexpr (NT <= 8 && EPI != EPI_GLU) {
     // 129-192 rows: three m-tiles per wave
-    dgemm_kernel<EPI, 12, NT, NSR><<<grid, 256, 0, s>>>(x, w, y, p, M, N, K, Ks, xr);
+    dgemm_kernel<EPI, 12, NT, NSR><<<grid, 256, 0, s>>>(x, w, y, p, M, N, K, Ks, xr, pv, pi, nv);
   }
 }
 
@@ -416,6 +472,21 @@ int docqa_dgemm_glu(const void* X, const void* W, void* Y, int M, int N, int K, 
   } else {
     return -1;
   }
+  DOCQA_CHECK_LAUNCH();
+  return 0;
+}
+
+// LM head + greedy pick at <= 192 rows (batch-1 decode included): out[M] = argmax over the
+// first n_valid columns of bf16(X . W^T), outv[M] (optional) the picked value; ws_v / ws_i:
+// [M, N / 64] per-tile partials.  The [M, vocab] logits never reach HBM.
+int docqa_dgemm_argmax(const void* X, const void* W, int64_t* out, float* outv, float* ws_v, int* ws_i, int M,
+                       int N, int K, int n_valid, hipStream_t s) {
+  if (M == 0) return 0;
+  if (!shape_ok(M, N, K, 1, BN) || n_valid <= 0 || n_valid > N) return -1;
+  const int mt = (M + 15) / 16;
+  launch_mt<EPI_ARGMAX, 4>(mt, dim3(N / BN), s, (const uint16_t*)X, (const uint16_t*)W, nullptr, nullptr, M, N, K,
+                           K, ws_v, ws_i, n_valid);
+  argmax_merge_kernel<<<M, 64, 0, s>>>(ws_v, ws_i, N / BN, out, outv);
   DOCQA_CHECK_LAUNCH();
   return 0;
 }

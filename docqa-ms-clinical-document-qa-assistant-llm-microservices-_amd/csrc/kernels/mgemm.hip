@@ -32,6 +32,7 @@
 #include "docqa_common.h"
 #include "docqa_asm.h"
 #include "docqa_norm_row.h"
+#include "docqa_argmax.h"
 #include <float.h>
 #include <stdlib.h>
 
@@ -458,26 +459,6 @@ __global__ __launch_bounds__(WM * WN * 64) void mgemm_kernel(const uint16_t* __r
                                             ntiles, n_valid, ws, tick, err, S);
 }
 
-__global__ __launch_bounds__(64) void mgemm_argmax_merge(const float* __restrict__ pv,
-                                                         const int* __restrict__ pi, int parts,
-                                                         int64_t* __restrict__ out, float* __restrict__ outv) {
-  const int row = blockIdx.x;
-  float bv = -FLT_MAX;
-  int bi = 0x7fffffff;
-  for (int s = threadIdx.x; s < parts; s += 64)
-    better(bv, bi, pv[(size_t)row * parts + s], pi[(size_t)row * parts + s]);
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) {
-    const float ov = __shfl_xor(bv, o, 64);
-    const int oi = __shfl_xor(bi, o, 64);
-    better(bv, bi, ov, oi);
-  }
-  if (threadIdx.x == 0) {
-    out[row] = bi == 0x7fffffff ? 0 : bi;   // all-NaN row: a valid id
-    if (outv) outv[row] = bv;               // the row's best (bf16-rounded) logit, for TP picks
-  }
-}
-
 // Variants (``cfg``): the tile width and wave layout
 //   1: BN 128, 64-deep stages x 3, waves 2 x 2 (128 x 64 each, 1 wave / SIMD)
 //   2: BN 128, 64-deep stages x 3, waves 4 x 2 ( 64 x 64 each, 2 waves / SIMD)
@@ -600,7 +581,7 @@ int docqa_mgemm_argmax(const void* X, const void* W, int64_t* out, float* outv, 
   const int rc = launch_cfg<EPI_ARGMAX>(cfg, (const uint16_t*)X, (const uint16_t*)W, nullptr, nullptr, ws_v, ws_i,
                                         M, N, K, 1, n_valid, s);
   if (rc) return rc;
-  mgemm_argmax_merge<<<M, 64, 0, s>>>(ws_v, ws_i, N / kCfg[cfg].bn, out, outv);
+  argmax_merge_kernel<<<M, 64, 0, s>>>(ws_v, ws_i, N / kCfg[cfg].bn, out, outv);
   DOCQA_CHECK_LAUNCH();
   return 0;
 }

@@ -32,6 +32,7 @@
 // any M (rows tiled by 256, tail rows clamped on load and never stored).
 #include "docqa_common.h"
 #include "docqa_asm.h"
+#include "docqa_argmax.h"
 #include <float.h>
 
 using namespace docqa;
@@ -346,25 +347,6 @@ __global__ __launch_bounds__(NW * 64) void wgemm_kernel(const uint16_t* __restri
   }
 }
 
-__global__ __launch_bounds__(64) void wgemm_argmax_merge(const float* __restrict__ pv, const int* __restrict__ pi,
-                                                         int parts, int64_t* __restrict__ out,
-                                                         float* __restrict__ outv) {
-  const int row = blockIdx.x;
-  float bv = -FLT_MAX;
-  int bi = 0x7fffffff;
-  for (int s = threadIdx.x; s < parts; s += 64) better(bv, bi, pv[(size_t)row * parts + s], pi[(size_t)row * parts + s]);
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) {
-    const float ov = __shfl_xor(bv, o, 64);
-    const int oi = __shfl_xor(bi, o, 64);
-    better(bv, bi, ov, oi);
-  }
-  if (threadIdx.x == 0) {
-    out[row] = bi == 0x7fffffff ? 0 : bi;   // all-NaN row: a valid id
-    if (outv) outv[row] = bv;
-  }
-}
-
 // Variants (``cfg``), weight loads default-policy / non-temporal (cfg + 8):
 //   1: 8 waves x 32 columns (BN 256, 2 waves / SIMD, 128 accumulator registers), 2 stages ahead
 //   2: 8 waves x 16 columns (BN 128), 3 stages ahead
@@ -460,7 +442,7 @@ int docqa_wgemm_argmax(const void* X, const void* W, int64_t* out, float* outv, 
   const int rc = launch_cfg<EPI_ARGMAX>(cfg, (const uint16_t*)X, (const uint16_t*)W, nullptr, nullptr, ws_v, ws_i,
                                         nullptr, nullptr, nullptr, M, N, K, 1, n_valid, s);
   if (rc) return rc;
-  wgemm_argmax_merge<<<M, 64, 0, s>>>(ws_v, ws_i, N / tile_n(cfg), out, outv);
+  argmax_merge_kernel<<<M, 64, 0, s>>>(ws_v, ws_i, N / tile_n(cfg), out, outv);
   DOCQA_CHECK_LAUNCH();
   return 0;
 }

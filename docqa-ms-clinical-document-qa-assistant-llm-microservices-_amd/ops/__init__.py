@@ -378,6 +378,12 @@ def lm_head_argmax(x, w, n_valid: int, cfg: int = -1, with_values: bool = False)
     fused (mgemm.hip EPI_ARGMAX): the [M, vocab] logits never reach HBM.  ``with_values``:
     (ids, picked logit fp32) -- a vocab-parallel shard's candidates for comm.tp_argmax."""
     if _gpu(x):
+        N, K = w.shape
+        if x.numel() // K <= 192 and N % 64 == 0 and K % 512 == 0:
+            # <= 192 rows (batch-1 decode included): the skinny weight-streaming kernel with the
+            # argmax in its epilogue (dgemm.hip EPI_ARGMAX)
+            ids, vals = _native().dgemm_argmax_val(x.contiguous(), w, int(n_valid))
+            return (ids, vals) if with_values else ids
         if cfg < 0:
             cfg = _LM_CFG if w.shape[0] % 256 == 0 else _MID_CFG
         if with_values:
@@ -395,8 +401,11 @@ def lm_head_argmax_shape_ok(N: int, K: int) -> bool:
 
 
 def lm_head_argmax_ok(M: int, N: int, K: int) -> bool:
-    # from 193 rows (below, hipBLASLt + the argmax kernel is faster: 250 vs 274 us at M=128)
-    return not _MID_OFF and 193 <= M <= MID_M_MAX and N % 128 == 0 and K % 128 == 0
+    """Fused LM head + argmax at every decode bucket: dgemm.hip below 193 rows, mgemm.hip
+    from 193 to 512 (no [M, vocab] logits, no library GEMM)."""
+    if M <= 192:
+        return M > 0 and N % 64 == 0 and K % 512 == 0
+    return not _MID_OFF and M <= MID_M_MAX and N % 128 == 0 and K % 128 == 0
 
 
 def add_rmsnorm_splitk(P, residual, w, eps: float):

@@ -21,11 +21,11 @@ import torch
 
 from ..utils import tracing
 from ..engine.llm_engine import LLMEngine, SamplingParams
-from ..prompts import CACHE_FRIENDLY_QA_TEMPLATE, qa_template
+from ..prompts import REFERENCE_QA_TEMPLATE, qa_template
 
-# QA prompt: the cache-friendly reordering of the reference's QA_CHAIN_PROMPT by default,
-# the verbatim reference text with QA_TEMPLATE=reference (docqa_amd/prompts.py)
-DEFAULT_TEMPLATE = CACHE_FRIENDLY_QA_TEMPLATE
+# QA prompt: the verbatim reference QA_CHAIN_PROMPT (llm-qa/main.py:71-93) by default, the
+# cache-friendly reordering with QA_TEMPLATE=cache_friendly (docqa_amd/prompts.py)
+DEFAULT_TEMPLATE = REFERENCE_QA_TEMPLATE
 
 
 @dataclass

@@ -6,8 +6,9 @@
 * ``CACHE_FRIENDLY_QA_TEMPLATE`` -- the same slots and instructions with every fixed
   line moved in front of ``{context}``, so all requests share a long token prefix that
   the engine's prefix cache serves from HBM (with the reference order, prompts diverge
-  after ~60 tokens).  The default of the QA pipeline; ``QA_TEMPLATE=reference`` selects
-  the verbatim reference text instead (``qa_template``).
+  after ~60 tokens).  Opt-in with ``QA_TEMPLATE=cache_friendly``; the llm-qa service
+  asks the verbatim reference text by default, as the reference does (``qa_template``).
+  ``bench.py`` names the template it measures in its JSON line (``workload.template``).
 * ``SINGLE_PATIENT_TEMPLATE`` / ``MULTI_PATIENT_TEMPLATE`` -- the synthese-comparative
   templates, verbatim (synthese-comparative/core/prompts.py:3-45); the synthese service
   uses them as they are.
@@ -73,10 +74,13 @@ RÉPONSE DE L'EXPERT :
 QA_TEMPLATES = {"reference": REFERENCE_QA_TEMPLATE, "cache_friendly": CACHE_FRIENDLY_QA_TEMPLATE}
 
 
+DEFAULT_QA_TEMPLATE = "reference"
+
+
 def qa_template(name: str | None = None) -> str:
-    """The QA prompt template named ``name`` (default: env ``QA_TEMPLATE``, else
-    ``cache_friendly``)."""
-    name = name or os.environ.get("QA_TEMPLATE", "cache_friendly")
+    """The QA prompt template named ``name`` (default: env ``QA_TEMPLATE``, else the
+    verbatim reference prompt)."""
+    name = name or os.environ.get("QA_TEMPLATE", DEFAULT_QA_TEMPLATE)
     try:
         return QA_TEMPLATES[name]
     except KeyError:

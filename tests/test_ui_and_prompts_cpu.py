@@ -89,9 +89,14 @@ def test_synthese_templates_have_the_reference_slots():
 
 
 def test_rag_template_puts_fixed_text_first_for_the_prefix_cache():
-    """Two questions with different contexts share every token up to the context slot."""
-    from docqa_amd.pipeline.rag import DEFAULT_TEMPLATE
+    """The cache-friendly template: two questions with different contexts share every
+    token up to the context slot.  (The service default is the verbatim reference text.)"""
+    from docqa_amd import prompts
+    from docqa_amd.pipeline.rag import DEFAULT_TEMPLATE as SERVICE_DEFAULT
     from docqa_amd.text.tokenizer import ChatTokenizer
+
+    assert SERVICE_DEFAULT is prompts.REFERENCE_QA_TEMPLATE
+    DEFAULT_TEMPLATE = prompts.CACHE_FRIENDLY_QA_TEMPLATE
 
     assert DEFAULT_TEMPLATE.index("{context}") < DEFAULT_TEMPLATE.index("{question}")
     head = DEFAULT_TEMPLATE.split("{context}")[0]
