@@ -25,17 +25,22 @@ def _port():
     return p
 
 
-def test_bench_dp2_shared_gpu():
-    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0")
+@pytest.mark.parametrize("world", [2, 8])
+def test_bench_dp_shared_gpu(world):
+    """bench.py's DP path (the driver's --gpus N command) with every rank on cuda:0: the
+    sharded index's per-batch all-gathers run on the IPC peer-memory gather."""
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0",
+               DOCQA_AR_TIMEOUT_MS=os.environ.get("DOCQA_AR_TIMEOUT_MS", "30000"))   # ranks share one GPU
     for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK"):
         env.pop(k, None)
-    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(world),
            "--master-addr", "127.0.0.1", "--master-port", str(_port()), str(ROOT / "bench.py"),
-           "--gpus", "2", "--share-gpu", "--llm", "llama3-1b-test", "--batch", "16", "--max-new-tokens", "8",
+           "--gpus", str(world), "--share-gpu", "--llm", "llama3-1b-test", "--batch", "16", "--max-new-tokens", "8",
            "--steps", "2", "--warmup", "1", "--notes", "200", "--kv-mem-fraction", "0.02"]
-    r = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=300, env=env)
+    r = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=420, env=env)
     assert r.returncode == 0, (r.stdout[-2000:], r.stderr[-4000:])
     out = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])
-    assert out["n_gpus"] == 2 and out["config"]["parallelism"] == "dp2"
-    assert out["config"]["global_batch"] == 32 and out["value"] > 0
+    assert out["n_gpus"] == world and out["config"]["parallelism"] == f"dp{world}"
+    assert out["config"]["global_batch"] == 16 * world and out["value"] > 0
+    assert "IPC all-gather unavailable" not in r.stdout + r.stderr
     assert out["workload"]["unique_question_frac"] == 1.0

@@ -45,7 +45,10 @@ def test_tp_matches_tp1(tmp_path, preset, tp):
     d1 = _decode_logits(m, kv, prompts, tables, [5, 6, 7], 64)
     del m, kv
     torch.cuda.empty_cache()
-    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0")
+    # every rank shares cuda:0: the processes' queues are time-sliced, so a peer can be
+    # late by far more than on one-GPU-per-rank xGMI (the deployment default is 500 ms)
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0",
+               DOCQA_AR_TIMEOUT_MS=os.environ.get("DOCQA_AR_TIMEOUT_MS", "30000"))
     for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK"):
         env.pop(k, None)
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(tp),
@@ -62,6 +65,8 @@ def test_tp_matches_tp1(tmp_path, preset, tp):
     out = torch.load(out_path, weights_only=True)
     assert _rel(out["prefill"], p1.float().cpu()) < 0.03
     assert _rel(out["decode"], d1.float().cpu()) < 0.03
+    waits = [int(Path(f"{out_path}.wait{r}").read_text()) for r in range(tp)]
+    print(f"[tp{tp} {preset}] longest peer wait per rank (us): {waits}", flush=True)
     toks = [torch.load(f"{out_path}.tok{r}", weights_only=True) for r in range(tp)]
     assert all(t == toks[0] for t in toks[1:])
     assert all(0 <= x < cfg.vocab_size for row in toks[0] for x in row)

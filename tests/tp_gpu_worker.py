@@ -41,6 +41,9 @@ def main():
     gen_prompts = [torch.randint(0, cfg.vocab_size, (n,), generator=g).tolist() for n in (5, 17, 64, 100, 33, 8)]
     toks = eng.generate(gen_prompts, SamplingParams(max_new_tokens=8, stop_on_eos=False))
     torch.cuda.synchronize()
+    # the longest any workgroup waited for a peer: ranks time-sliced on ONE GPU arrive far
+    # apart (a peer's queue may not be mapped while this rank spins); printed for the log
+    Path(f"{out_path}.wait{ps.rank}").write_text(str(car.max_wait_us()))
     car.check()
     torch.save(toks, f"{out_path}.tok{ps.rank}")
     if ps.rank == 0:
