@@ -83,7 +83,7 @@ __device__ __forceinline__ f32x4 load16_sc1(const float* p) {
   return d;
 }
 
-template <int EPI, int NW, int NJ, bool NT, int LD>
+template <int EPI, int NW, int NJ, bool NT, int LD, bool PK = false>
 __global__ __launch_bounds__(NW * 64) void wgemm_kernel(const uint16_t* __restrict__ X,
                                                         const uint16_t* __restrict__ W,
                                                         uint16_t* __restrict__ Y, float* __restrict__ P,
@@ -131,13 +131,13 @@ __global__ __launch_bounds__(NW * 64) void wgemm_kernel(const uint16_t* __restri
   auto issue = [&](int t, WSet& wb) {
     const uint32_t slot = base + (uint32_t)((t % NSR) * SLOT * 2);
     const uint16_t* xb = xbase + t * BKS;
-    const uint16_t* wb_ = wbase + t * BKS;
+    const uint16_t* wb_ = wbase + t * (PK ? 2 * 512 : BKS);
 #pragma unroll
     for (int q = 0; q < XI; ++q) glds16s(xb, xoff[q], slot + (uint32_t)((q * NW + wave) * 1024));
 #pragma unroll
     for (int j = 0; j < NJ; ++j) {
       wload16<NT, 0>(wb[0][j], wb_, woff[j]);
-      wload16<NT, 64>(wb[1][j], wb_, woff[j]);
+      wload16<NT, PK ? 1024 : 64>(wb[1][j], wb_, woff[j]);
     }
   };
 
@@ -347,7 +347,8 @@ __global__ __launch_bounds__(NW * 64) void wgemm_kernel(const uint16_t* __restri
   }
 }
 
-// Variants (``cfg``), weight loads default-policy / non-temporal (cfg + 8):
+// Variants (``cfg``), weight loads default-policy / non-temporal (cfg + 8); + 16: W in the
+// fragment-major layout (pack_fragments; 17, 18, 20, 25 instantiated):
 //   1: 8 waves x 32 columns (BN 256, 2 waves / SIMD, 128 accumulator registers), 2 stages ahead
 //   2: 8 waves x 16 columns (BN 128), 3 stages ahead
 //   3: 8 waves x 32 columns (BN 256), 3 stages ahead
@@ -355,12 +356,12 @@ __global__ __launch_bounds__(NW * 64) void wgemm_kernel(const uint16_t* __restri
 constexpr int kNumCfg = 4;
 constexpr int kBN[kNumCfg + 1] = {0, 256, 128, 256, 128};
 
-template <int EPI, int NW, int NJ, bool NT, int LD>
+template <int EPI, int NW, int NJ, bool NT, int LD, bool PK = false>
 int launch(const uint16_t* x, const uint16_t* w, uint16_t* y, float* p, float* pv, int* pi, float* ws, int* tick,
            int* err, int M, int N, int K, int S, int n_valid, hipStream_t s) {
   constexpr int BN = NW * NJ * 16;
   dim3 grid((N / BN) * S, (M + BM - 1) / BM);
-  wgemm_kernel<EPI, NW, NJ, NT, LD><<<grid, NW * 64, 0, s>>>(x, w, y, p, pv, pi, ws, tick, err, M, N, K, K / S, S,
+  wgemm_kernel<EPI, NW, NJ, NT, LD, PK><<<grid, NW * 64, 0, s>>>(x, w, y, p, pv, pi, ws, tick, err, M, N, K, K / S, S,
                                                          n_valid);
   DOCQA_CHECK_LAUNCH();
   return 0;
@@ -374,6 +375,10 @@ int launch_cfg(int cfg, const uint16_t* x, const uint16_t* w, uint16_t* y, float
     case 2: return launch<EPI, 8, 1, false, 3>(x, w, y, p, pv, pi, ws, tick, err, M, N, K, S, n_valid, s);
     case 3: return launch<EPI, 8, 2, false, 3>(x, w, y, p, pv, pi, ws, tick, err, M, N, K, S, n_valid, s);
     case 4: return launch<EPI, 4, 2, false, 3>(x, w, y, p, pv, pi, ws, tick, err, M, N, K, S, n_valid, s);
+    case 17: return launch<EPI, 8, 2, false, 2, true>(x, w, y, p, pv, pi, ws, tick, err, M, N, K, S, n_valid, s);
+    case 18: return launch<EPI, 8, 1, false, 3, true>(x, w, y, p, pv, pi, ws, tick, err, M, N, K, S, n_valid, s);
+    case 20: return launch<EPI, 4, 2, false, 3, true>(x, w, y, p, pv, pi, ws, tick, err, M, N, K, S, n_valid, s);
+    case 25: return launch<EPI, 8, 2, true, 2, true>(x, w, y, p, pv, pi, ws, tick, err, M, N, K, S, n_valid, s);
     case 9: return launch<EPI, 8, 2, true, 2>(x, w, y, p, pv, pi, ws, tick, err, M, N, K, S, n_valid, s);
     case 10: return launch<EPI, 8, 1, true, 3>(x, w, y, p, pv, pi, ws, tick, err, M, N, K, S, n_valid, s);
     case 11: return launch<EPI, 8, 2, true, 3>(x, w, y, p, pv, pi, ws, tick, err, M, N, K, S, n_valid, s);
@@ -383,7 +388,7 @@ int launch_cfg(int cfg, const uint16_t* x, const uint16_t* w, uint16_t* y, float
 }
 
 int tile_n(int cfg) {
-  const int c = cfg > 8 ? cfg - 8 : cfg;
+  const int c = cfg % 8 == 0 ? 0 : cfg % 8;
   return c >= 1 && c <= kNumCfg ? kBN[c] : 0;
 }
 

@@ -267,6 +267,15 @@ def mid_plan(M: int, N: int, K: int, glu: bool = False) -> tuple[int, int]:
     return S, _MID_CFG
 
 
+def pack_fragments(w: torch.Tensor) -> torch.Tensor:
+    """[N, K] row-major weights -> the MFMA fragment-major layout [N/16, K/32, 64, 8] of
+    wgemm.hip's packed variants (cfg + 16): the 16 x 32 B fragment of (n-tile, k-step) is
+    one contiguous 1 KiB block, lane l = 16 (k-chunk) + row, so every weight load of the
+    decode GEMM is a fully coalesced wave-instruction."""
+    N, K = w.shape
+    return w.reshape(N // 16, 16, K // 32, 4, 8).permute(0, 2, 3, 1, 4).contiguous().view(N, K)
+
+
 def mgemm_partial(x, w, splits: int, cfg: int = 0):
     """Split-K partial slabs [S, M, N] fp32 of x @ w^T on the mid-M decode GEMM (S = 1:
     the bf16 product [M, N])."""

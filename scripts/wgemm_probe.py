@@ -44,7 +44,16 @@ for (name, N, K) in [("qkv", 6144, 4096), ("o", 4096, 4096), ("gate_up", 28672, 
             S, c = ops.mid_plan(M, N, K)
             if S:
                 row[f"mgemm_c{c}_S{S}"] = t(lambda w: nat.mgemm(x, w, S, c))
+        wsp = None
         for cfg in CFGS:
+            if cfg >= 16 and wsp is None:     # fragment-major packed copies of the rotation
+                wsp = [ops.pack_fragments(w) for w in ws]
+            wl = wsp if cfg >= 16 else ws
+
+            def t(fn, wl=wl):
+                it = iter(range(1 << 30))
+                return round(timeit(lambda: fn(wl[next(it) % copies]), iters=4 * copies), 1)
+
             bn = nat.wgemm_tile_n(cfg)
             if N % bn:
                 continue
@@ -57,7 +66,7 @@ for (name, N, K) in [("qkv", 6144, 4096), ("o", 4096, 4096), ("gate_up", 28672, 
                     row[f"w{cfg}_glu_S{S}"] = t(lambda w: nat.wgemm_glu(x, w, S, cfg, wsb, tick))
                 assert int(tick.sum()) == 0
                 ref = ops.reference.silu_mul((x.float() @ ws[0].float().T).bfloat16(), interleaved=True)
-                got = nat.wgemm_glu(x, ws[0], 2, cfg, wsb, tick)
+                got = nat.wgemm_glu(x, wl[0], 2, cfg, wsb, tick)
                 row[f"w{cfg}_glu_err"] = round(float((got.float() - ref).abs().max()), 4)
             elif name == "lm_head":
                 row[f"w{cfg}_argmax"] = t(lambda w: nat.wgemm_argmax_val(x, w, N, cfg))
@@ -67,3 +76,4 @@ for (name, N, K) in [("qkv", 6144, 4096), ("o", 4096, 4096), ("gate_up", 28672, 
                         continue
                     row[f"w{cfg}_S{S}"] = t(lambda w: nat.wgemm(x, w, S, cfg))
         print(json.dumps(row), flush=True)
+        del wsp

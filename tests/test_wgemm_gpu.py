@@ -123,3 +123,39 @@ def test_wgemm_argmax(native, M, cfg):
     assert torch.equal(got_v, logits.gather(1, want[:, None])[:, 0])
     assert torch.equal(vals, got_v)
     assert int(ids.max()) < n_valid
+
+
+@pytest.mark.parametrize("cfg", [17, 18, 20, 25])
+@pytest.mark.parametrize("N,K,S", [(6144, 4096, 8), (4096, 14336, 14), (1024, 1024, 2)])
+def test_wgemm_packed_weights(native, cfg, N, K, S):
+    """Fragment-major packed weights (ops.pack_fragments): same product as row-major."""
+    from docqa_amd import ops
+
+    bn = torch.ops.docqa.wgemm_tile_n(cfg)
+    if N % bn:
+        pytest.skip("N not a multiple of the tile")
+    M = 256
+    x = torch.randn(M, K, device="cuda", dtype=torch.bfloat16)
+    w = (torch.randn(N, K, device="cuda") / K ** 0.5).bfloat16()
+    wp = ops.pack_fragments(w)
+    ref = x.float() @ w.float().T
+    _close(torch.ops.docqa.wgemm(x, wp, S, cfg).sum(0), ref, 2e-3, 1e-3)
+    _close(torch.ops.docqa.wgemm(x, wp, 1, cfg), ref, 2e-2, 1e-2)
+
+
+@pytest.mark.parametrize("cfg", [17, 18])
+def test_wgemm_packed_glu_and_argmax(native, cfg):
+    from docqa_amd import ops
+    from docqa_amd.ops import reference as R
+
+    M, N, K = 256, 28672, 4096
+    x = torch.randn(M, K, device="cuda", dtype=torch.bfloat16)
+    w = (torch.randn(N, K, device="cuda") / K ** 0.5).bfloat16()
+    wp = ops.pack_fragments(w)
+    ref = R.silu_mul((x.float() @ w.float().T).bfloat16(), interleaved=True)
+    ws, tick = _glu_ws(M, N, cfg)
+    for S in (1, 2):
+        _close(torch.ops.docqa.wgemm_glu(x, wp, S, cfg, ws, tick), ref, 2e-2, 1e-2)
+    logits = (x.float() @ w.float().T).bfloat16().float()
+    ids, vals = torch.ops.docqa.wgemm_argmax_val(x, wp, N, cfg)
+    assert torch.equal(logits.gather(1, ids[:, None])[:, 0], logits.max(1).values)
