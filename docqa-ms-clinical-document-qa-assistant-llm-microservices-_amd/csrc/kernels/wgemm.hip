@@ -119,12 +119,18 @@ __global__ __launch_bounds__(NW * 64) void wgemm_kernel(const uint16_t* __restri
     xoff[q] = (uint32_t)(min(m0 + r, M - 1) * K + ((pc ^ ((r >> 1) & 7)) << 3)) * 2u;
   }
   // weight sources: B fragment (16 rows x 32 k) of n-tile j at k-step ks: lane (fr, fq)
-  // holds row c0 + 16 j + fr, k chunk 4 ks + fq (ks: +64 B immediate)
+  // holds row c0 + 16 j + fr, k chunk 4 ks + fq (ks: +64 B immediate).  PK: W in the MFMA
+  // fragment-major layout of ops.pack_fragments -- [N/16][K/32][64 lanes][8]: the fragment
+  // of (n-tile, k-step) is 1 KiB contiguous, so every weight load is one fully coalesced
+  // wave-instruction (row-major: 16 rows x 64 B, half lines; ks: +1 KiB immediate)
   uint32_t woff[NJ];
 #pragma unroll
-  for (int j = 0; j < NJ; ++j) woff[j] = (uint32_t)((c0 + j * 16 + fr) * K + fq * 8) * 2u;
+  for (int j = 0; j < NJ; ++j) {
+    if constexpr (PK) woff[j] = (uint32_t)((((c0 >> 4) + j) * (K >> 5) + (kbeg >> 5)) * 512 + lane * 8) * 2u;
+    else woff[j] = (uint32_t)((c0 + j * 16 + fr) * K + fq * 8) * 2u;
+  }
   const uint16_t* xbase = X + kbeg;
-  const uint16_t* wbase = W + kbeg;
+  const uint16_t* wbase = PK ? W : W + kbeg;
 
   const uint32_t base = lds_u32(smem);
   typedef bf16x8 WSet[2][NJ];

@@ -2,8 +2,10 @@
 
 MI355X-first layout:
   * fused projections: one [(Hq + 2*Hkv)*D, H] QKV GEMM and one [2I, H] gate|up GEMM
-    per layer (fewer, larger hipBLASLt launches; the GEMM output is consumed in place by
-    the fused RoPE+KV-cache kernel and the SwiGLU kernel);
+    per layer, all on the hand-written MFMA GEMMs (prefill: pgemm.hip 256 x 256 with SwiGLU
+    in the gate|up epilogue; decode: dgemm.hip <= 192 rows, mgemm.hip 193..512 rows, split-K
+    fp32 slabs consumed by the fused RoPE + KV-cache write and residual + RMSNorm kernels;
+    the LM head with the greedy argmax fused in at every bucket);
   * the residual stream is updated inside the fused add+RMSNorm kernel, so each layer
     costs 2 GEMM-epilogue-free passes over the hidden state instead of 4;
   * attention reads Q/K/V straight out of the packed QKV buffer (prefill: MFMA flash
