@@ -39,9 +39,10 @@ def main() -> None:
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
-    # 256: the largest power-of-two batch whose p50 answer latency (~1.52 s) stays below the
-    # measured reference-equivalent p50 (1.62 s); 128 gives ~117 q/s at
-    # ~1.16 s p50, 192 ~146 q/s at ~1.35 s (profiles/r1_bench_batch_sweep.log)
+    # 256 questions per rank per step: round 3 measured 153 q/s at p50 1.71 s with unique
+    # questions (BENCH_r03; the reference-equivalent serial stack: 0.615 q/s, p50 1.62 s,
+    # BASELINE.md).  Smaller batches trade throughput for latency: 128 gave ~117 q/s at
+    # ~1.16 s p50 in round 1 (profiles/r1_bench_batch_sweep.log, repeated questions)
     ap.add_argument("--batch", type=int, default=256, help="questions per data-parallel rank per step")
     ap.add_argument("--max-new-tokens", type=int, default=128)
     ap.add_argument("--llm", default="llama3-8b")
