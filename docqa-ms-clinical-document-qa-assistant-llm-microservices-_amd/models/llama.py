@@ -162,6 +162,10 @@ class LlamaModel:
         # row per layer; the kernel leaves them zeroed, so graph replays need no memset
         self._chain_ctr = (torch.zeros(cfg.layers, 16, dtype=torch.int32, device=self.device)
                            if self.device.type == "cuda" else None)
+        # hand-off workspace of the 2-way split-K fused SwiGLU (ops.glu_split_plan): one
+        # shared by every layer (they run in stream order); tickets zeroed once here, never
+        # inside a captured graph, and re-armed by the kernel itself
+        self._glu_ws = None
         if init:
             self._random_init(seed)
 
@@ -312,7 +316,12 @@ class LlamaModel:
                     S, t = ops.decode_plan(M, *L0[k].shape)
                     plans[k] = (S, lambda a, w, S=S, t=t: ops.dgemm_partial(a, w, S, t))
             Sg, cg = ops.mid_plan(M, *L0["gate_up"].shape, glu=True)
-            glu = (lambda a, w: ops.mgemm_glu(a, w, cg)) if Sg else ops.glu_linear
+            sp = ops.glu_split_plan(M, *L0["gate_up"].shape) if x.is_cuda else None
+            if sp is not None:
+                ws = self._glu_workspace(*L0["gate_up"].shape)
+                glu = lambda a, w, sp=sp, ws=ws: ops.mgemm_glu_split(a, w, sp[0], sp[1], ws)
+            else:
+                glu = (lambda a, w: ops.mgemm_glu(a, w, cg)) if Sg else ops.glu_linear
         else:
             glu = ops.prefill_glu
         if self.tp > 1 and not x.is_cuda:
@@ -410,6 +419,11 @@ class LlamaModel:
         if greedy_ids:
             return self.greedy_ids(x)
         return ops.prefill_linear(x, self.lm_head) if x.shape[0] > 512 else F.linear(x, self.lm_head)
+
+    def _glu_workspace(self, N: int, K: int):
+        if self._glu_ws is None:
+            self._glu_ws = ops.glu_split_workspace(ops.MID_M_MAX, N, self.device)
+        return self._glu_ws
 
     def greedy_ids(self, x: torch.Tensor) -> torch.Tensor:
         """Greedy token ids int64 [R] of the final normed hidden rows ``x``: the LM-head GEMM

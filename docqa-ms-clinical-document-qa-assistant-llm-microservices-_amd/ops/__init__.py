@@ -329,6 +329,37 @@ def mgemm_chain(attn, w_o, residual, post_norm, w_gu, w_down, next_norm, w_qkv, 
     return x2, (slabs(x2, w_qkv, S_q) if w_qkv is not None else None)
 
 
+_GLU_SPLIT = os.environ.get("DOCQA_GLU_SPLIT", "0") == "1"
+_GLU_SPLIT_CFG = int(os.environ.get("DOCQA_GLU_SPLIT_CFG", "6"))
+
+
+def glu_split_plan(M: int, N: int, K: int):
+    """(splits, cfg) of the fused-SwiGLU gate|up decode GEMM with the K range split over two
+    workgroups per 256-wide tile that meet in the launch (mgemm.hip glu_meet), or None.
+    256-wide tiles halve the X bytes each CU pulls per weight byte, and the 2-way split
+    gives them a full round of workgroups (Llama-3-8B: 112 tiles x 2)."""
+    if not _GLU_SPLIT or _MID_OFF or not (65 <= M <= MID_M_MAX) or N < 16384 or N % 256 or K % (2 * 64 * 2):
+        return None
+    return 2, _GLU_SPLIT_CFG
+
+
+def glu_split_workspace(max_m: int, N: int, device):
+    """(ws fp32, tick int32) for :func:`mgemm_glu_split` up to ``max_m`` rows and N."""
+    mt = (max_m + 255) // 256
+    ws = torch.empty(mt * N * 256, dtype=torch.float32, device=device)
+    tick = torch.zeros(2 * mt * (N // 128) + 1, dtype=torch.int32, device=device)
+    return ws, tick
+
+
+def mgemm_glu_split(x, w_il, splits: int, cfg: int, workspace):
+    """silu(x Wg^T) * (x Wu^T) with the K range split over ``splits`` workgroups per tile
+    meeting in the launch; ``workspace`` from :func:`glu_split_workspace`."""
+    if _gpu(x):
+        ws, tick = workspace
+        return _native().mgemm_glu_split(x.contiguous(), w_il, splits, cfg, ws, tick)
+    return silu_mul(torch.nn.functional.linear(x, w_il), interleaved=True)
+
+
 def mgemm_glu(x, w_il, cfg: int = 0):
     """silu(x Wg^T) * (x Wu^T) for 8-interleaved gate|up weights on the mid-M decode GEMM."""
     if _gpu(x):
