@@ -125,11 +125,14 @@ glu_interleave, glu_split = ref.glu_interleave, ref.glu_split
 
 
 def glu_linear(x, w_il):
-    """silu(x Wg^T) * (x Wu^T) for 8-interleaved gate|up weights: the fused SwiGLU decode
-    GEMM for <= 64 rows, else hipBLASLt + the interleaved silu_mul kernel."""
+    """silu(x Wg^T) * (x Wu^T) for 8-interleaved gate|up weights at <= 128 decode rows: the
+    skinny fused-SwiGLU decode GEMM (dgemm.hip); 129..512 rows take the mid-M kernel
+    (:func:`mid_plan`), so no decode bucket runs the library GEMM.  Measured vs hipBLASLt +
+    silu_mul at M = 64 / 96 / 128: 50.9 / 60.0 / 63.1 us vs 56.4 / 57.6 / 59.7
+    (profiles/r4_lm_head_probe.log)."""
     if _gpu(x):
         N, K = w_il.shape
-        if x.numel() // K <= 64 and N % 64 == 0 and K % 512 == 0:
+        if x.numel() // K <= 128 and N % 64 == 0 and K % 512 == 0:
             return _native().dgemm_glu(x.contiguous(), w_il)
     return silu_mul(torch.nn.functional.linear(x, w_il), interleaved=True)
 
@@ -249,11 +252,10 @@ def mid_plan(M: int, N: int, K: int, glu: bool = False) -> tuple[int, int]:
     S=1 75.4 vs 67.8 + a 5.9 us silu_mul + a [M, 2I] round trip."""
     if _MID_OFF or not (MID_M_MIN <= M <= MID_M_MAX) or N % 128 or K % 128:
         return 0, 0
-    if M <= 192 and N >= 16384:
-        # 129..192 rows: the wide gate|up stays on hipBLASLt + silu_mul (56-62 us vs the
-        # fused 66-70 at M = 128-192); QKV / O / down gain (QKV 21.4 vs 33.7 at M = 192,
-        # down 38.5 vs dgemm 54.2; profiles/r2_mgemm_probe_m128_192.log)
-        return 0, 0
+    # 129..192 rows: QKV / O / down gain over the skinny kernel and hipBLASLt (QKV 20.2-20.8
+    # vs 27.7-33.4 us; profiles/r4_lm_head_probe.log, r2_mgemm_probe_m128_192.log); the wide
+    # gate|up with fused SwiGLU is at parity with hipBLASLt + silu_mul (62.3 / 64.7 vs
+    # 62.4 / 66.5 us at M = 160 / 192) and takes it too
     tiles = (N // 128) * ((M + 255) // 256)
     kb = K // 128
     S = max(s for s in range(1, kb + 1) if kb % s == 0 and (s == 1 or tiles * s <= _MID_WG_CAP))
@@ -419,9 +421,11 @@ def lm_head_argmax(x, w, n_valid: int, cfg: int = -1, with_values: bool = False)
     (ids, picked logit fp32) -- a vocab-parallel shard's candidates for comm.tp_argmax."""
     if _gpu(x):
         N, K = w.shape
-        if x.numel() // K <= 192 and N % 64 == 0 and K % 512 == 0:
-            # <= 192 rows (batch-1 decode included): the skinny weight-streaming kernel with the
-            # argmax in its epilogue (dgemm.hip EPI_ARGMAX)
+        if x.numel() // K <= 32 and N % 64 == 0 and K % 512 == 0:
+            # <= 32 rows (batch-1 decode included): the skinny weight-streaming kernel with
+            # the argmax in its epilogue (dgemm.hip EPI_ARGMAX) -- 197.6 / 203.4 us at M = 1 /
+            # 32 vs hipBLASLt + argmax 190.1 / 201.3; from 33 rows the mid-M kernel's 256-row
+            # tiles stream the vocab once (256-275 us flat; profiles/r4_lm_head_probe.log)
             ids, vals = _native().dgemm_argmax_val(x.contiguous(), w, int(n_valid))
             return (ids, vals) if with_values else ids
         if cfg < 0:
@@ -441,11 +445,11 @@ def lm_head_argmax_shape_ok(N: int, K: int) -> bool:
 
 
 def lm_head_argmax_ok(M: int, N: int, K: int) -> bool:
-    """Fused LM head + argmax at every decode bucket: dgemm.hip below 193 rows, mgemm.hip
-    from 193 to 512 (no [M, vocab] logits, no library GEMM)."""
-    if M <= 192:
-        return M > 0 and N % 64 == 0 and K % 512 == 0
-    return not _MID_OFF and M <= MID_M_MAX and N % 128 == 0 and K % 128 == 0
+    """Fused LM head + argmax at every decode bucket: dgemm.hip up to 32 rows, mgemm.hip
+    from 33 to 512 (no [M, vocab] logits, no library GEMM)."""
+    if M <= 32 and N % 64 == 0 and K % 512 == 0:
+        return M > 0
+    return not _MID_OFF and 0 < M <= MID_M_MAX and N % 128 == 0 and K % 128 == 0
 
 
 def add_rmsnorm_splitk(P, residual, w, eps: float):
