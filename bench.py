@@ -32,6 +32,11 @@ os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
 # kernel arguments in device memory: +0.3-0.5 % on the decode loop's ~330 launches per step
 # (profiles/r2_ab_dev_kernarg.log); read by the HIP runtime at init, so set before torch
 os.environ.setdefault("HIP_FORCE_DEV_KERNARG", "1")
+if "--share-gpu" in sys.argv:
+    # N ranks on ONE GPU: one hardware queue per process keeps every rank's queue resident,
+    # so a collective kernel never spins on a rank whose queue the scheduler left unmapped
+    # (parallel/custom_ar.py; profiles/r4_ar_skew_*); read at HIP init, so set before torch
+    os.environ.setdefault("GPU_MAX_HW_QUEUES", "1")
 
 
 def main() -> None:

@@ -36,6 +36,14 @@
 // workgroups of 256 threads: all resident); the longest wait of the call is kept in ctr[2]
 // (us) for skew diagnostics.  The host reads the word once per engine step
 // (parallel/custom_ar.py) and fails the step loudly.
+// Root cause of round 3's spin-limit hits (4 ranks sharing ONE GPU in the tests): with
+// HIP's default 4 hardware queues per process the 4 processes oversubscribe the GPU's queue
+// slots; the scheduler left one rank's queue unmapped while the other ranks' kernels spun
+// on its flags, so it "never arrived" (> 30 s, rank 0 at the first call:
+// profiles/r4_ar_skew_default_hwq_tp4_fail.txt).  With one hardware queue per process
+// (GPU_MAX_HW_QUEUES=1, set by the shared-GPU tests and bench.py --share-gpu) the longest
+// peer wait is ~35 ms (profiles/r4_ar_skew_hwq1_tp.log).  One process per GPU -- the
+// deployment -- never shares a queue slot pool with its peers.
 #include "docqa_common.h"
 #include <cstring>
 

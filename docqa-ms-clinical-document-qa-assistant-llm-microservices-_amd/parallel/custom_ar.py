@@ -63,7 +63,9 @@ class CustomAllReduce:
         self.oneshot_max_bytes = oneshot_max_bytes
         # how long a workgroup waits for a late peer before it records which one and gives up
         # (the step then fails loudly: check() / raise_if()).  One process per GPU arrives
-        # within microseconds; processes time-sliced on ONE GPU (tests, --share-gpu) need more
+        # within microseconds; several processes on ONE GPU (tests, --share-gpu) must run
+        # with GPU_MAX_HW_QUEUES=1 or a rank's queue may stay unmapped while the others spin
+        # (allreduce.hip header; profiles/r4_ar_skew_*)
         self.timeout_us = int(float(os.environ.get("DOCQA_AR_TIMEOUT_MS", "500")) * 1000)
         # every rank runs the same collective sequence whatever fails locally, so a failure
         # on one rank becomes the same decision on all of them (no rank left in a barrier)

@@ -45,10 +45,14 @@ def test_tp_matches_tp1(tmp_path, preset, tp):
     d1 = _decode_logits(m, kv, prompts, tables, [5, 6, 7], 64)
     del m, kv
     torch.cuda.empty_cache()
-    # every rank shares cuda:0: the processes' queues are time-sliced, so a peer can be
-    # late by far more than on one-GPU-per-rank xGMI (the deployment default is 500 ms)
-    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0",
-               DOCQA_AR_TIMEOUT_MS=os.environ.get("DOCQA_AR_TIMEOUT_MS", "30000"))
+    # every rank shares cuda:0.  With HIP's default 4 hardware queues per process, 4 ranks
+    # oversubscribe the GPU's queue slots: the scheduler leaves a rank's queue unmapped while
+    # the others' all-reduce kernels spin on it, so that rank "never arrives" (round 3's
+    # spin-limit hits; round 4: rank 0 absent > 30 s at the first call, profiles/
+    # r4_ar_skew_default_hwq_tp4_fail.txt).  One queue per process keeps every rank resident:
+    # the longest peer wait drops to ~35 ms (profiles/r4_ar_skew_hwq1_tp.log).
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0", GPU_MAX_HW_QUEUES="1",
+               DOCQA_AR_TIMEOUT_MS=os.environ.get("DOCQA_AR_TIMEOUT_MS", "2000"))
     for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK"):
         env.pop(k, None)
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(tp),
