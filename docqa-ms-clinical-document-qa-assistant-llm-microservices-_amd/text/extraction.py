@@ -319,20 +319,33 @@ class _Font:
         return s.decode("cp1252", errors="replace")
 
 
+# content-stream lexing: whitespace / comment runs and runs of bytes that start no token are
+# skipped in one regex step each, so a hostile stream (16 MB of NULs, say) costs C-speed
+# scanning, not one Python iteration per byte; MAX_CONTENT_TOKENS bounds the token loop
+_CS_SKIP = re.compile(rb"(?:[ \t\r\n\f\x00]+|%[^\n]*)+")
+_CS_JUNK = re.compile(rb"[^ \t\r\n\f\x00%(<\[/\-0-9.A-Za-z'\"*>{}]+")
+_CS_TOK = re.compile(rb"/[^\s/<>\[\]()]+|-?\d*\.?\d+|[A-Za-z'\"*]+|<<|>>|\{|\}")
+_CS_NUM = re.compile(rb"-?\d*\.?\d+")
+MAX_CONTENT_TOKENS = 4_000_000
+
+
 def _content_text(content: bytes, fonts: dict) -> str:
     parts: list[str] = []
     font = None
     i, n = 0, len(content)
     operands: list = []
-    while i < n:
+    budget = MAX_CONTENT_TOKENS
+    while i < n and budget > 0:
+        budget -= 1
+        m = _CS_SKIP.match(content, i)
+        if m:
+            i = m.end()
+            continue
+        m = _CS_JUNK.match(content, i)
+        if m:
+            i = m.end()
+            continue
         c = content[i:i + 1]
-        if c in b" \t\r\n\f\x00":
-            i += 1
-            continue
-        if c == b"%":
-            j = content.find(b"\n", i)
-            i = n if j < 0 else j
-            continue
         if c == b"(":
             s, i = _pdf_string(content, i)
             operands.append(s)
@@ -344,7 +357,12 @@ def _content_text(content: bytes, fonts: dict) -> str:
         if c == b"[":
             # TJ array: strings and kerning numbers
             j, arr = i + 1, []
-            while j < n and content[j:j + 1] != b"]":
+            while j < n and content[j:j + 1] != b"]" and budget > 0:
+                budget -= 1
+                m = _CS_SKIP.match(content, j) or _CS_JUNK.match(content, j)
+                if m:
+                    j = m.end()
+                    continue
                 cj = content[j:j + 1]
                 if cj == b"(":
                     s, j = _pdf_string(content, j)
@@ -353,7 +371,7 @@ def _content_text(content: bytes, fonts: dict) -> str:
                     s, j = _hex_string(content, j)
                     arr.append(s)
                 else:
-                    m = re.match(rb"-?\d*\.?\d+", content[j:j + 32])
+                    m = _CS_NUM.match(content, j)
                     if m:
                         arr.append(float(m.group(0)))
                         j += len(m.group(0))
@@ -362,7 +380,7 @@ def _content_text(content: bytes, fonts: dict) -> str:
             operands.append(arr)
             i = j + 1
             continue
-        m = re.match(rb"/[^\s/<>\[\]()]+|-?\d*\.?\d+|[A-Za-z'\"*]+|<<|>>|\{|\}", content[i:i + 64])
+        m = _CS_TOK.match(content, i)
         if not m:
             i += 1
             continue
