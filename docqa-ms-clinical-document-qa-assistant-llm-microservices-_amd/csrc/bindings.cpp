@@ -509,7 +509,7 @@ at::Tensor paged_decode_fused(const at::Tensor& P, const at::Tensor& positions, 
                               const at::Tensor& slot_mapping, at::Tensor k_cache, at::Tensor v_cache,
                               const at::Tensor& block_tables, const at::Tensor& context_lens,
                               int64_t Hq, int64_t max_context, double scale,
-                              const c10::optional<at::Tensor>& order) {
+                              const c10::optional<at::Tensor>& order, const c10::optional<at::Tensor>& tick) {
   CHECK_GPU(P); CHECK_CONTIG(P); CHECK_BF16(k_cache); CHECK_BF16(v_cache);
   CHECK_I32(positions); CHECK_I32(slot_mapping); CHECK_I32(block_tables); CHECK_I32(context_lens);
   CHECK_CONTIG(block_tables);
@@ -523,12 +523,20 @@ at::Tensor paged_decode_fused(const at::Tensor& P, const at::Tensor& positions, 
   auto out = at::empty({B, Hq * D}, P.options().dtype(at::kBFloat16));
   auto tmp_out = at::empty({B, Hq, max_parts, D}, P.options());
   auto tmp_ml = at::empty({B, Hq, max_parts, 2}, P.options());
+  // tick: zeroed int32 [>= B * Hkv] owned by the caller (the kernel re-arms it): the split
+  // partitions are merged by their last workgroup instead of a second launch
+  int* tick_ptr = nullptr;
+  if (tick && tick->defined()) {
+    CHECK_GPU((*tick)); CHECK_I32((*tick));
+    TORCH_CHECK(tick->numel() >= (int64_t)B * Hkv, "paged_decode_fused: tick needs B * Hkv entries");
+    tick_ptr = tick->data_ptr<int>();
+  }
   CHECK_RC(docqa_paged_decode_fused(P.data_ptr<float>(), P.size(0), positions.data_ptr<int>(),
                                     cos_sin.data_ptr<float>(), slot_mapping.data_ptr<int>(),
                                     k_cache.data_ptr(), v_cache.data_ptr(), block_tables.data_ptr<int>(),
                                     block_tables.size(1), context_lens.data_ptr<int>(), out.data_ptr(),
                                     Hq * D, tmp_out.data_ptr<float>(), tmp_ml.data_ptr<float>(), B, Hq,
-                                    Hkv, BS, max_parts, (float)scale, order_ptr(order, B), stream()),
+                                    Hkv, BS, max_parts, (float)scale, order_ptr(order, B), stream(), tick_ptr),
            "paged_decode_fused");
   return out;
 }
@@ -624,6 +632,26 @@ at::Tensor dgemm_partial(const at::Tensor& x, const at::Tensor& w, int64_t split
   CHECK_RC(docqa_dgemm_partial(x.data_ptr(), w.data_ptr(), part.data_ptr<float>(), M, N, K, (int)splits,
                                (int)tile_rows, stream()), "dgemm_partial");
   return part;
+}
+
+// few-row split-K projection + residual add + RMSNorm in one launch (last-arriver epilogue):
+// residual <- residual + bf16(x w^T); returns rmsnorm(residual) * gamma
+at::Tensor dgemm_add_rmsnorm(const at::Tensor& x, const at::Tensor& w, int64_t splits, at::Tensor residual,
+                             const at::Tensor& gamma, double eps, at::Tensor tick) {
+  CHECK_GPU(x); CHECK_BF16(x); CHECK_BF16(w); CHECK_CONTIG(x); CHECK_CONTIG(w);
+  CHECK_BF16(residual); CHECK_CONTIG(residual); CHECK_BF16(gamma); CHECK_I32(tick); CHECK_GPU(tick);
+  const int K = x.size(-1), N = w.size(0);
+  TORCH_CHECK(w.size(1) == K, "dgemm_add_rmsnorm: K mismatch");
+  const int M = x.numel() / K;
+  TORCH_CHECK(residual.numel() == (int64_t)M * N && gamma.numel() == N && tick.numel() >= 1,
+              "dgemm_add_rmsnorm: residual [M, N], gamma [N], one ticket word");
+  c10::DeviceGuard g(x.device());
+  auto part = at::empty({splits, M, N}, x.options().dtype(at::kFloat));
+  auto out = at::empty_like(residual);
+  CHECK_RC(docqa_dgemm_add_rmsnorm(x.data_ptr(), w.data_ptr(), part.data_ptr<float>(), M, N, K, (int)splits,
+                                   residual.data_ptr(), gamma.data_ptr(), out.data_ptr(), (float)eps,
+                                   tick.data_ptr<int>(), stream()), "dgemm_add_rmsnorm");
+  return out;
 }
 
 at::Tensor dgemm(const at::Tensor& x, const at::Tensor& w, int64_t splits) {
@@ -1162,6 +1190,8 @@ TORCH_LIBRARY(docqa, m) {
         "float scale, Tensor k_cache, Tensor v_cache, Tensor block_tables, Tensor ctx_start) -> Tensor");
   m.def("dgemm(Tensor x, Tensor w, int splits) -> Tensor");
   m.def("dgemm_partial(Tensor x, Tensor w, int splits, int tile_rows=64) -> Tensor");
+  m.def("dgemm_add_rmsnorm(Tensor x, Tensor w, int splits, Tensor(a!) residual, Tensor gamma, float eps, "
+        "Tensor(t!) tick) -> Tensor");
   m.def("dgemm_glu(Tensor x, Tensor w) -> Tensor");
   m.def("mgemm(Tensor x, Tensor w, int splits, int cfg=0) -> Tensor");
   m.def("mgemm_glu(Tensor x, Tensor w, int cfg=0) -> Tensor");
@@ -1198,7 +1228,7 @@ TORCH_LIBRARY(docqa, m) {
         "Tensor? order=None) -> Tensor");
   m.def("paged_decode_fused(Tensor P, Tensor positions, Tensor cos_sin, Tensor slot_mapping, "
         "Tensor(a!) k_cache, Tensor(b!) v_cache, Tensor block_tables, Tensor context_lens, int Hq, "
-        "int max_context, float scale, Tensor? order=None) -> Tensor");
+        "int max_context, float scale, Tensor? order=None, Tensor(t!)? tick=None) -> Tensor");
   m.def("ar_run(Tensor x, bool slabs, Tensor(r!)? residual, Tensor? w, float eps, int rank, int[] regions, "
         "int max_elems, int mode, Tensor(a!) ctr, Tensor(b!) err, int timeout_us=500000) -> Tensor");
   m.def("ar_region_bytes(int max_elems) -> int", &ar_region_bytes);
@@ -1236,6 +1266,7 @@ TORCH_LIBRARY_IMPL(docqa, CUDA, m) {
   m.impl("flash_prefill_paged", &flash_prefill_paged);
   m.impl("dgemm", &dgemm);
   m.impl("dgemm_partial", &dgemm_partial);
+  m.impl("dgemm_add_rmsnorm", &dgemm_add_rmsnorm);
   m.impl("dgemm_glu", &dgemm_glu);
   m.impl("mgemm", &mgemm);
   m.impl("mgemm_glu", &mgemm_glu);

@@ -110,9 +110,12 @@ int docqa_paged_decode_fused(const float* P, int S, const int* positions, const 
                              const int* slot_mapping, void* k_cache, void* v_cache,
                              const int* block_tables, int maxb, const int* context_lens, void* out,
                              int out_stride, float* tmp_out, float* tmp_ml, int B, int Hq, int Hkv,
-                             int BS, int max_parts, float scale, const int* order, hipStream_t s);
+                             int BS, int max_parts, float scale, const int* order, hipStream_t s,
+                             int* tick = nullptr);
 int docqa_dgemm_splits(int N, int K);
 int docqa_dgemm_glu(const void* X, const void* W, void* Y, int M, int N, int K, hipStream_t s);
+int docqa_dgemm_add_rmsnorm(const void* X, const void* W, float* P, int M, int N, int K, int S, void* residual,
+                            const void* gamma, void* out, float eps, int* tick, hipStream_t s);
 int docqa_dgemm_argmax(const void* X, const void* W, int64_t* out, float* outv, float* ws_v, int* ws_i, int M,
                        int N, int K, int n_valid, hipStream_t s);
 int docqa_dgemm(const void* X, const void* W, void* Y, float* partial, int M, int N, int K, int S,

@@ -17,8 +17,24 @@
 
 namespace docqa {
 
+// 16 B of fp32 slab; COH: agent-scope loads (sc1: past this XCD's L2) of slabs written by
+// other workgroups of the same launch
+template <bool COH>
+__device__ __forceinline__ float4 slab_load4(const float* p) {
+  if constexpr (COH) {
+    const unsigned long long* q = reinterpret_cast<const unsigned long long*>(p);
+    const unsigned long long lo = __hip_atomic_load(q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const unsigned long long hi = __hip_atomic_load(q + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return float4{__uint_as_float((unsigned)lo), __uint_as_float((unsigned)(lo >> 32)),
+                  __uint_as_float((unsigned)hi), __uint_as_float((unsigned)(hi >> 32))};
+  } else {
+    return *reinterpret_cast<const float4*>(p);
+  }
+}
+
 // WT: write-through (sc1) stores of the residual and the output, for in-launch consumers
-template <int NV, int NS, bool WT = false>
+// COH: the slabs come from the same launch (slab_load4)
+template <int NV, int NS, bool WT = false, bool COH = false>
 __device__ __forceinline__ void add_rmsnorm_splitk_row(const float* __restrict__ P, int S, size_t slab,
                                                        uint16_t* __restrict__ residual,
                                                        const uint16_t* __restrict__ w,
@@ -48,8 +64,8 @@ __device__ __forceinline__ void add_rmsnorm_splitk_row(const float* __restrict__
         float4 pa[NS], pb[NS];
 #pragma unroll
         for (int sl = 0; sl < NS; ++sl) {
-          pa[sl] = *reinterpret_cast<const float4*>(pr + sl * slab);
-          pb[sl] = *reinterpret_cast<const float4*>(pr + sl * slab + 4);
+          pa[sl] = slab_load4<COH>(pr + sl * slab);
+          pb[sl] = slab_load4<COH>(pr + sl * slab + 4);
         }
         a = pa[0];
         b = pb[0];
@@ -59,11 +75,11 @@ __device__ __forceinline__ void add_rmsnorm_splitk_row(const float* __restrict__
           b.x += pb[sl].x; b.y += pb[sl].y; b.z += pb[sl].z; b.w += pb[sl].w;
         }
       } else {
-        a = *reinterpret_cast<const float4*>(pr);
-        b = *reinterpret_cast<const float4*>(pr + 4);
+        a = slab_load4<COH>(pr);
+        b = slab_load4<COH>(pr + 4);
         for (int sl = 1; sl < S; ++sl) {
-          const float4 a2 = *reinterpret_cast<const float4*>(pr + sl * slab);
-          const float4 b2 = *reinterpret_cast<const float4*>(pr + sl * slab + 4);
+          const float4 a2 = slab_load4<COH>(pr + sl * slab);
+          const float4 b2 = slab_load4<COH>(pr + sl * slab + 4);
           a.x += a2.x; a.y += a2.y; a.z += a2.z; a.w += a2.w;
           b.x += b2.x; b.y += b2.y; b.z += b2.z; b.w += b2.w;
         }

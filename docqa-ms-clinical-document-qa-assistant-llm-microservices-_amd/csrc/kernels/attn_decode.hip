@@ -149,7 +149,9 @@ __device__ __forceinline__ void attend_rows(const uint4 (&kr)[U], const uint4 (&
 // Merge the 16 lane-group streams of a workgroup (4 per wave via xor-shuffles, 4 waves
 // through LDS) and write the partition result: normalised bf16 output (DIRECT) or the
 // un-normalised accumulator + (max, sum) for the merge kernel.
-template <int G, int D, bool DIRECT>
+// COH: the partition result is written through to the device-coherent level (agent-scope
+// relaxed atomic stores = global_store ... sc1) for a merge inside the same launch
+template <int G, int D, bool DIRECT, bool COH = false>
 __device__ __forceinline__ void finish_partition(
     float (&m)[G], float (&l)[G], float (&acc)[G][8], float (*s_acc)[G][D], float (*s_m)[G],
     float (*s_l)[G], int tid, int wave, int tg, int chunk, int b, int kvh, int part, int Hkv,
@@ -226,13 +228,113 @@ __device__ __forceinline__ void finish_partition(
       out[(size_t)b * out_stride + (size_t)h * D + d] = f2bf(lsum > 0.f ? v / lsum : 0.f);
     } else {
       const size_t o = ((size_t)b * (Hkv * G) + h) * max_parts + part;
-      tmp_out[o * D + d] = v;
-      if (d == 0) {
-        tmp_ml[o * 2 + 0] = M;
-        tmp_ml[o * 2 + 1] = lsum;
+      if constexpr (COH) {
+        __hip_atomic_store(tmp_out + o * D + d, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (d == 0) {
+          __hip_atomic_store(tmp_ml + o * 2 + 0, M, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          __hip_atomic_store(tmp_ml + o * 2 + 1, lsum, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+      } else {
+        tmp_out[o * D + d] = v;
+        if (d == 0) {
+          tmp_ml[o * 2 + 0] = M;
+          tmp_ml[o * 2 + 1] = lsum;
+        }
       }
     }
   }
+}
+
+// Partition merge by the LAST workgroup of a (sequence, KV head) to finish (LAST mode of the
+// ring kernel): replaces the paged_decode_reduce launch -- at batch 1 a 6 us kernel on the
+// critical path of every layer (profiles/r4_batch1_kernel_stats.txt) -- with one ticket
+// atomic and a merge of the G heads by a workgroup that is already resident.
+//   * every workgroup writes its partition with write-through stores (finish_partition COH),
+//     waits for them, then draws a ticket tick[b Hkv + kvh]; the one drawing np - 1 merges
+//     and re-arms the ticket for the next launch (graph replays need no memset);
+//   * the merge reads the partitions with agent-scope loads (sc1: past this XCD's L2, so a
+//     partition written on another XCD is seen), the (max, sum) pairs through LDS, and the
+//     accumulators 8 partitions per round with every load issued before the first use.
+// Same arithmetic as paged_decode_reduce (fp32, partitions in index order), so the two
+// modes agree bit for bit.
+template <int G, int D>
+__device__ __forceinline__ bool last_arriver_merge(const float* __restrict__ tmp_out, const float* __restrict__ tmp_ml,
+                                                   int* __restrict__ tick, int b, int kvh, int Hkv, int max_parts,
+                                                   int Lr, int P, const CascadeIn& ci, uint16_t* __restrict__ out,
+                                                   int out_stride) {
+  constexpr int MAXP = 64;
+  __shared__ int s_last;
+  __shared__ float s_w[G][MAXP + kCascadeMaxChunks];
+  __shared__ float s_inv[G];
+  const int tid = threadIdx.x;
+  const int chunk = split_chunk(Lr, max_parts);
+  const int np = min(max_parts, (Lr + chunk - 1) / chunk);
+  const int nc = ci.plen ? cascade_parts(P, ci.nchunk) : 0;
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this workgroup's partition has landed
+  __syncthreads();
+  if (tid == 0) {
+    int* t = tick + (size_t)b * Hkv + kvh;
+    const int old = __hip_atomic_fetch_add(t, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    s_last = old == np - 1;
+    if (s_last) __hip_atomic_store(t, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  __syncthreads();
+  if (!s_last) return false;
+  const int Hq = Hkv * G;
+  const size_t B = gridDim.y;
+  // (max, sum) of every partition (and cascade chunk) -> LDS
+  float* s_pm = &s_w[0][0];                           // reuse: [G][np + nc] maxima first
+  __shared__ float s_pl[G][MAXP + kCascadeMaxChunks];
+  const int ne = np + nc;
+  for (int i = tid; i < G * ne; i += 256) {
+    const int g = i / ne, p = i - g * ne, h = kvh * G + g;
+    float pm, pl;
+    if (p < np) {
+      const float* ml = tmp_ml + (((size_t)b * Hq + h) * max_parts + p) * 2;
+      pm = __hip_atomic_load(ml, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      pl = __hip_atomic_load(ml + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    } else {
+      const size_t r = ((size_t)(p - np) * B + b) * Hq + h;
+      pm = ci.ml[r * 2];
+      pl = ci.ml[r * 2 + 1];
+    }
+    s_pm[g * (MAXP + kCascadeMaxChunks) + p] = pm;
+    s_pl[g][p] = pl;
+  }
+  __syncthreads();
+  if (tid < G) {
+    const int g = tid;
+    float M = -FLT_MAX;
+    for (int p = 0; p < ne; ++p) M = fmaxf(M, s_w[g][p]);
+    float den = 0.f;
+    for (int p = 0; p < ne; ++p) {
+      const float pm = s_w[g][p];
+      // partitions: exp2(m - M) as paged_decode_reduce; cascade chunks may be empty
+      const float w = (p >= np && pm == -FLT_MAX) ? 0.f : exp2f(pm - M);
+      s_w[g][p] = w;
+      den += w * s_pl[g][p];
+    }
+    s_inv[g] = den;
+  }
+  __syncthreads();
+  for (int i = tid; i < G * D; i += 256) {
+    const int g = i / D, d = i - g * D, h = kvh * G + g;
+    const float* src = tmp_out + ((size_t)b * Hq + h) * max_parts * D + d;
+    float num = 0.f;
+    for (int p0 = 0; p0 < np; p0 += 8) {
+      float v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u)
+        v[u] = __hip_atomic_load(src + (size_t)min(p0 + u, np - 1) * D, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#pragma unroll
+      for (int u = 0; u < 8; ++u)
+        if (p0 + u < np) num += s_w[g][p0 + u] * v[u];
+    }
+    for (int c = 0; c < nc; ++c) num += s_w[g][np + c] * ci.acc[(((size_t)c * B + b) * Hq + h) * D + d];
+    const float den = s_inv[g];
+    out[(size_t)b * out_stride + (size_t)h * D + d] = f2bf(den > 0.f ? num / den : 0.f);
+  }
+  return true;
 }
 
 // DIRECT (one partition per sequence, the batch-64 serving case): the workgroup already
@@ -366,6 +468,27 @@ __device__ __forceinline__ void fused_row8(const FusedQKV& fz, int b, int W, siz
 // sum of the S slabs of 8 consecutive values, rounded to bf16 like the unfused path
 __device__ __forceinline__ void sum_slabs8(const float* p, int S, size_t slab, float (&x)[8]) {
   float4 a = *reinterpret_cast<const float4*>(p), b = *reinterpret_cast<const float4*>(p + 4);
+  if (S <= 4) {
+    // up to 4 slabs (the decode plans' splits): every load issued before the first add --
+    // one memory latency instead of S dependent ones; clamped slabs are loaded, not added
+    float4 c[3], d[3];
+#pragma unroll
+    for (int sl = 1; sl < 4; ++sl) {
+      const float* q = p + (size_t)min(sl, S - 1) * slab;
+      c[sl - 1] = *reinterpret_cast<const float4*>(q);
+      d[sl - 1] = *reinterpret_cast<const float4*>(q + 4);
+    }
+#pragma unroll
+    for (int sl = 1; sl < 4; ++sl)
+      if (sl < S) {
+        a.x += c[sl - 1].x; a.y += c[sl - 1].y; a.z += c[sl - 1].z; a.w += c[sl - 1].w;
+        b.x += d[sl - 1].x; b.y += d[sl - 1].y; b.z += d[sl - 1].z; b.w += d[sl - 1].w;
+      }
+    const float v[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+#pragma unroll
+    for (int j = 0; j < 8; ++j) x[j] = bf2f(f2bf(v[j]));
+    return;
+  }
   for (int sl = 1; sl < S; ++sl) {
     const float4 c = *reinterpret_cast<const float4*>(p + sl * slab);
     const float4 d = *reinterpret_cast<const float4*>(p + sl * slab + 4);
@@ -404,13 +527,16 @@ __device__ __forceinline__ void rope8(float (&x)[8], int c, const float* cs) {
 // merge scratch aliased onto the drained ring: 3 workgroups/CU -- the same bytes in flight
 // per CU spread over more workgroups, so one workgroup's prologue / epilogue overlaps
 // the others' streaming and a batch-192 step needs two launch rounds instead of three).
-template <int G, bool DIRECT, bool FUSED = false, int NSR = 4>
+// LAST (split partitions only): the last workgroup of each (sequence, KV head) merges the
+// partitions itself (last_arriver_merge; tick: zeroed int32 [B, Hkv]) -- no reduce launch.
+template <int G, bool DIRECT, bool FUSED = false, int NSR = 4, bool LAST = false>
 __global__ __launch_bounds__(256) void paged_decode_ring_kernel(
     const uint16_t* __restrict__ q, int q_stride, uint16_t* __restrict__ k_cache,
     uint16_t* __restrict__ v_cache, const int* __restrict__ block_tables, int maxb,
     const int* __restrict__ context_lens, float* __restrict__ tmp_out,
     float* __restrict__ tmp_ml, int Hkv, int max_parts, float scale,
-    uint16_t* __restrict__ out, int out_stride, FusedQKV fz, CascadeIn ci) {
+    uint16_t* __restrict__ out, int out_stride, FusedQKV fz, CascadeIn ci, int* __restrict__ tick = nullptr) {
+  static_assert(!(LAST && DIRECT), "LAST merges split partitions");
   constexpr int D = 128, TT = 32, U = 2;
   static_assert(NSR >= 2 && NSR <= 4, "ring of 2..4 slots");
   constexpr int TILE = TT * D;                   // elements of one K (or V) tile: 8 KB
@@ -433,7 +559,7 @@ __global__ __launch_bounds__(256) void paged_decode_ring_kernel(
   if (start >= L) {
     // a row with no keys of its own (a padded decode slot, L = 0) still gets a defined
     // output: zeros, so nothing downstream ever consumes uninitialised memory
-    if (DIRECT && L <= P)
+    if ((DIRECT || LAST) && L <= P && part == 0)
       for (int i = threadIdx.x; i < G * D; i += 256) out[(size_t)b * out_stride + (size_t)kvh * G * D + i] = 0;
     return;
   }
@@ -560,8 +686,10 @@ __global__ __launch_bounds__(256) void paged_decode_ring_kernel(
   wait_vmcnt<0>();                               // drain the clamped tail DMAs
   if constexpr (ALIAS) __syncthreads();          // every wave done with the ring
 
-  finish_partition<G, D, DIRECT>(m, l, acc, s_acc, s_m, s_l, tid, wave, tg, chunk, b, kvh, part,
-                                 Hkv, max_parts, tmp_out, tmp_ml, out, out_stride, ci);
+  finish_partition<G, D, DIRECT, LAST>(m, l, acc, s_acc, s_m, s_l, tid, wave, tg, chunk, b, kvh, part,
+                                       Hkv, max_parts, tmp_out, tmp_ml, out, out_stride, ci);
+  if constexpr (LAST)
+    last_arriver_merge<G, D>(tmp_out, tmp_ml, tick, b, kvh, Hkv, max_parts, L - P, P, ci, out, out_stride);
 }
 
 // ---------------------------------------------------------------------------------------
@@ -1825,7 +1953,8 @@ int docqa_paged_decode_fused(const float* P, int S, const int* positions, const 
                              const int* slot_mapping, void* k_cache, void* v_cache,
                              const int* block_tables, int maxb, const int* context_lens, void* out,
                              int out_stride, float* tmp_out, float* tmp_ml, int B, int Hq, int Hkv,
-                             int BS, int max_parts, float scale, const int* order, hipStream_t s) {
+                             int BS, int max_parts, float scale, const int* order, hipStream_t s,
+                             int* tick) {
   if (B == 0) return 0;
   if (BS != 64 || maxb > 256 || Hq % Hkv != 0 || S < 1) return -1;
   CascadeIn oi{};
@@ -1834,9 +1963,15 @@ int docqa_paged_decode_fused(const float* P, int S, const int* positions, const 
   dim3 grid(Hkv, B, max_parts);   // partitions slowest: see kDecodeGridNote
   const bool direct = max_parts == 1;
   FusedQKV fz{P, S, positions, cos_sin, slot_mapping, Hq};
+  const bool last = tick && !direct && max_parts <= 64;
 #define DFUSED(GG)                                                                            \
   do {                                                                                        \
-    if (direct)                                                                               \
+    if (last)                                                                                 \
+      paged_decode_ring_kernel<GG, false, true, 4, true><<<grid, 256, 0, s>>>(                \
+          nullptr, 0, (uint16_t*)k_cache, (uint16_t*)v_cache, block_tables, maxb,             \
+          context_lens, tmp_out, tmp_ml, Hkv, max_parts, scale, (uint16_t*)out, out_stride, fz, oi, \
+          tick);                                                                              \
+    else if (direct)                                                                          \
       paged_decode_ring_kernel<GG, true, true><<<grid, 256, 0, s>>>(                          \
           nullptr, 0, (uint16_t*)k_cache, (uint16_t*)v_cache, block_tables, maxb,             \
           context_lens, tmp_out, tmp_ml, Hkv, max_parts, scale, (uint16_t*)out, out_stride, fz, oi); \
@@ -1853,7 +1988,7 @@ int docqa_paged_decode_fused(const float* P, int S, const int* positions, const 
     default: return -1;
   }
 #undef DFUSED
-  if (!direct)
+  if (!direct && !last)
     paged_decode_reduce<128><<<dim3(Hq, B), 128, 0, s>>>(tmp_out, tmp_ml, context_lens,
                                                          (uint16_t*)out, out_stride, Hq, max_parts);
   DOCQA_CHECK_LAUNCH();

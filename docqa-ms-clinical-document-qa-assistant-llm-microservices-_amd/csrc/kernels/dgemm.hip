@@ -31,6 +31,7 @@
 #include "docqa_common.h"
 #include "docqa_asm.h"
 #include "docqa_argmax.h"
+#include "docqa_norm_row.h"
 #include <stdlib.h>
 
 using namespace docqa;
@@ -92,13 +93,28 @@ __device__ __forceinline__ float row_swap8(float v) {
 // the W stage in LDS (NT 16-row n-tiles) is shared by all of them; KW = 4 / MT k-groups
 // are summed through LDS at the end.  MT = 8: wave w owns m-tiles 2w, 2w+1 (MPW = 2) over
 // the whole k-block (KW = 1).
-template <int EPI, int MT, int NT, int NSR, int XA = 2>
+// NormArgs (EPI_PARTIAL, few rows): the split-K slabs go out write-through and the LAST
+// workgroup of the grid to finish (one ticket word, re-armed by it) runs the residual add +
+// RMSNorm over them (docqa_norm_row.h, the add_rmsnorm_splitk arithmetic) -- the batch-1
+// O / down projection then needs no add_rmsnorm_splitk launch (4.6 us each at M = 1,
+// profiles/r4_batch1_kernel_stats.txt).
+struct NormArgs {
+  int* tick = nullptr;             // null: plain partial slabs
+  uint16_t* residual = nullptr;    // [M, N] bf16, updated in place
+  const uint16_t* gamma = nullptr; // [N]
+  uint16_t* out = nullptr;         // [M, N] bf16 normed rows
+  float eps = 0.f;
+};
+
+template <int EPI, int MT, int NT, int NSR, int XA = 2, bool NORM = false>
 __global__ __launch_bounds__(256) void dgemm_kernel(const uint16_t* __restrict__ X,
                                                     const uint16_t* __restrict__ W,
                                                     uint16_t* __restrict__ Y,
                                                     float* __restrict__ P, int M, int N, int K,
                                                     int Ks, int xcd_remap, float* __restrict__ pv = nullptr,
-                                                    int* __restrict__ pi = nullptr, int n_valid = 0) {
+                                                    int* __restrict__ pi = nullptr, int n_valid = 0,
+                                                    NormArgs na = NormArgs{}) {
+  static_assert(!NORM || EPI == EPI_PARTIAL, "the fused norm consumes split-K slabs");
   constexpr int MPW = MT > 4 ? MT / 4 : 1;       // m-tiles per wave
   constexpr int MTW = MT > 4 ? 4 : MT;           // wave groups along m
   constexpr int KW = 4 / MTW, SPW = KSTEPS / KW;
@@ -237,7 +253,9 @@ __global__ __launch_bounds__(256) void dgemm_kernel(const uint16_t* __restrict__
 
   // C/D map of 16x16x32: col = lane & 15 (weight row), row = 4 * (lane >> 4) + r (X row)
   auto store = [&](int row, int col, float v) {
-    if constexpr (EPI == EPI_PARTIAL) P[((size_t)slice * M + row) * N + col] = v;
+    if constexpr (NORM)
+      __hip_atomic_store(P + ((size_t)slice * M + row) * N + col, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    else if constexpr (EPI == EPI_PARTIAL) P[((size_t)slice * M + row) * N + col] = v;
     else Y[(size_t)row * N + col] = f2bf(v);
   };
   // SwiGLU pair: gate value at an 8-block's low half, up value 8 columns later
@@ -338,6 +356,29 @@ __global__ __launch_bounds__(256) void dgemm_kernel(const uint16_t* __restrict__
       } else {
         store(row, col, sum_k(m, nt, ln, r));
       }
+    }
+  }
+  if constexpr (NORM) {
+    __shared__ int s_last;
+    __shared__ float red[4];
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this workgroup's slab pieces landed
+    __syncthreads();
+    if (tid == 0) {
+      const int old = __hip_atomic_fetch_add(na.tick, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      s_last = old == (int)(gridDim.x * gridDim.y) - 1;
+      if (s_last) __hip_atomic_store(na.tick, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    __syncthreads();
+    if (!s_last) return;
+    const int S = gridDim.y;
+    for (int row = 0; row < M; ++row) {
+      if (S == 4)
+        add_rmsnorm_splitk_row<4, 4, false, true>(P, S, (size_t)M * N, na.residual, na.gamma, na.out, N, na.eps,
+                                                  row, tid, red);
+      else
+        add_rmsnorm_splitk_row<4, 0, false, true>(P, S, (size_t)M * N, na.residual, na.gamma, na.out, N, na.eps,
+                                                  row, tid, red);
+      __syncthreads();   // red reused by the next row
     }
   }
 }
@@ -450,6 +491,23 @@ int docqa_dgemm_partial(const void* X, const void* W, float* P, int M, int N, in
     launch_mt<EPI_PARTIAL, 4, 8>(mt, dim3(N / 64, S), s, x, w, nullptr, P, M, N, K, K / S);
   else
     launch_mt<EPI_PARTIAL, 4>(mt, dim3(N / 64, S), s, x, w, nullptr, P, M, N, K, K / S);
+  DOCQA_CHECK_LAUNCH();
+  return 0;
+}
+
+// Few-row split-K projection with the residual add + RMSNorm fused in (NormArgs): P [S, M, N]
+// fp32 slabs (scratch), residual [M, N] updated, out [M, N] = rmsnorm(residual) * gamma.
+// M <= kNormRows, N <= 8192 (4 chunks of 8 per lane), 64-row weight tiles.
+constexpr int kNormRows = 4;
+int docqa_dgemm_add_rmsnorm(const void* X, const void* W, float* P, int M, int N, int K, int S, void* residual,
+                            const void* gamma, void* out, float eps, int* tick, hipStream_t s) {
+  if (M == 0) return 0;
+  if (M > kNormRows || N > 8192 || N % 8 || !tick || !P || !shape_ok(M, N, K, S, BN)) return -1;
+  NormArgs na{tick, (uint16_t*)residual, (const uint16_t*)gamma, (uint16_t*)out, eps};
+  const dim3 grid(N / BN, S);
+  const int xr = (xcd_knob() && S > 1 && 8 % S == 0 && (grid.x * S) % 8 == 0) ? 1 : 0;
+  dgemm_kernel<EPI_PARTIAL, 1, 4, NS, 2, true><<<grid, 256, 0, s>>>((const uint16_t*)X, (const uint16_t*)W, nullptr,
+                                                                    P, M, N, K, K / S, xr, nullptr, nullptr, 0, na);
   DOCQA_CHECK_LAUNCH();
   return 0;
 }

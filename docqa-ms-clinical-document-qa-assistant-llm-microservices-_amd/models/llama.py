@@ -41,6 +41,8 @@ from ..parallel import comm
 # default: measured 2.5 % slower per decode step at batch 256 than the separate rope_cache
 # launch (the ring's fused preamble delays its K/V stream; profiles/r1_cascade_rope_ab.log)
 _CASCADE_ROPE = os.environ.get("DOCQA_CASCADE_ROPE", "0") == "1"
+# short prefills (<= ops.MID_M_MAX tokens) on the decode projection plans (forward())
+_PREFILL_MID = os.environ.get("DOCQA_PREFILL_MID", "1") != "0"
 
 
 @dataclass
@@ -166,6 +168,8 @@ class LlamaModel:
         # shared by every layer (they run in stream order); tickets zeroed once here, never
         # inside a captured graph, and re-armed by the kernel itself
         self._glu_ws = None
+        self._tick = None      # decode attention's last-arriver merge tickets (ops.decode_ticket)
+        self._ntick = None     # fused projection + add + RMSNorm ticket word (ops.dgemm_add_rmsnorm)
         if init:
             self._random_init(seed)
 
@@ -305,7 +309,11 @@ class LlamaModel:
         lin = ops.decode_linear if decode else ops.prefill_linear
         M = x.shape[0]
         plans = {}
-        if decode and self.layers:
+        # a short prefill (<= ops.MID_M_MAX prompt tokens: batch-1 serving) has the decode
+        # step's shape -- too few rows for the 256 x 256 prefill GEMM's tiles -- so it takes
+        # the same split-K projection plans and fused consumers (RoPE + KV write, add + norm)
+        small = (not decode and x.is_cuda and _PREFILL_MID and M <= ops.MID_M_MAX)
+        if (decode or small) and self.layers:
             L0 = self.layers[0]
             for k in ("qkv", "o", "down"):
                 S, c = ops.mid_plan(M, *L0[k].shape)
@@ -320,6 +328,8 @@ class LlamaModel:
             if sp is not None:
                 ws = self._glu_workspace(*L0["gate_up"].shape)
                 glu = lambda a, w, sp=sp, ws=ws: ops.mgemm_glu_split(a, w, sp[0], sp[1], ws)
+            elif small and ops.pgemm_ok(M, *L0["gate_up"].shape):
+                glu = ops.prefill_glu     # 256 x 256 tiles with SwiGLU: 104 vs 141 us at M = 512
             else:
                 glu = (lambda a, w: ops.mgemm_glu(a, w, cg)) if Sg else ops.glu_linear
         else:
@@ -330,6 +340,17 @@ class LlamaModel:
             for k in ("o", "down"):
                 if not plans.get(k, (0, None))[0]:
                     plans[k] = (1, lambda a, w: F.linear(a.float(), w.float())[None])
+        # batch 1 (<= ops.NORM_FUSE_ROWS rows, TP = 1): O / down with the residual add + RMSNorm
+        # in the projection's own last workgroup -- no add_rmsnorm_splitk launch
+        nf = {}
+        if decode and self.tp == 1 and self.layers and x.is_cuda:
+            L0 = self.layers[0]
+            for k in ("o", "down"):
+                S = ops.dgemm_norm_plan(M, *L0[k].shape)
+                if S:
+                    nf[k] = S
+            if nf and self._ntick is None:
+                self._ntick = torch.zeros(1, dtype=torch.int32, device=self.device)
         sq, qkv_part = plans.get("qkv", (0, None))
         so, o_part = plans.get("o", (0, None))
         sd, down_part = plans.get("down", (0, None))
@@ -381,11 +402,12 @@ class LlamaModel:
                                                       meta.shared_table, meta.shared_len,
                                                       meta.cascade_chunks, meta.seq_order)
                 qkv = None
-            elif sq and ops.fused_decode_ok(kc, meta.block_tables):
+            elif decode and sq and ops.fused_decode_ok(kc, meta.block_tables):
                 # QKV partials -> RoPE + new-token cache write + attention, one launch
                 a = ops.paged_decode_fused(qkv_slabs, meta.positions, self.cos_sin,
                                            meta.slot_mapping, kc, vc, meta.block_tables, meta.context_lens,
-                                           hq, meta.max_context, self.scale, meta.seq_order)
+                                           hq, meta.max_context, self.scale, meta.seq_order,
+                                           self._decode_tick(M) if x.is_cuda else None)
                 qkv = None
             elif sq:
                 qkv = ops.rope_cache_splitk(qkv_slabs, meta.positions, self.cos_sin,
@@ -411,14 +433,27 @@ class LlamaModel:
                                         self._chain_ctr[i], chain, eps)
                 continue
             # row-parallel O: (TP all-reduce +) residual add + RMSNorm in one consumer
-            x = comm.tp_add_rmsnorm(o_part(a, L["o"]) if so else lin(a, L["o"]), residual, L["post_norm"], eps)
+            if "o" in nf:
+                x = ops.dgemm_add_rmsnorm(a, L["o"], nf["o"], residual, L["post_norm"], eps, self._ntick)
+            else:
+                x = comm.tp_add_rmsnorm(o_part(a, L["o"]) if so else lin(a, L["o"]), residual, L["post_norm"], eps)
             g = glu(x, L["gate_up"])
-            x = comm.tp_add_rmsnorm(down_part(g, L["down"]) if sd else lin(g, L["down"]), residual, nxt, eps)
+            if "down" in nf:
+                x = ops.dgemm_add_rmsnorm(g, L["down"], nf["down"], residual, nxt, eps, self._ntick)
+            else:
+                x = comm.tp_add_rmsnorm(down_part(g, L["down"]) if sd else lin(g, L["down"]), residual, nxt, eps)
         if logits_index is not None:
             x = x.index_select(0, logits_index)
         if greedy_ids:
             return self.greedy_ids(x)
         return ops.prefill_linear(x, self.lm_head) if x.shape[0] > 512 else F.linear(x, self.lm_head)
+
+    def _decode_tick(self, B: int):
+        """Ticket words for the fused decode attention's in-kernel partition merge, shared
+        by every layer (the launches are stream-ordered and each re-arms its words)."""
+        if self._tick is None or self._tick.numel() < B * self.hkv:
+            self._tick = ops.decode_ticket(max(B, 512) * self.hkv, self.device)
+        return self._tick
 
     def _glu_workspace(self, N: int, K: int):
         if self._glu_ws is None:

@@ -161,11 +161,11 @@ def linear_fused(x, w, bias=None, residual=None, epi: int = EPI_BIAS):
     return ref.linear_fused(x, w, bias, residual, epi)
 
 
-def _splits_for(N: int, K: int, tile: int) -> int:
-    """Smallest split-K count giving >= 192 workgroups of ``tile`` weight rows (whole
-    512-deep ring turns per slice)."""
+def _splits_for(N: int, K: int, tile: int, min_wgs: int = 192) -> int:
+    """Smallest split-K count giving >= ``min_wgs`` workgroups of ``tile`` weight rows
+    (whole 512-deep ring turns per slice)."""
     tiles, S = N // tile, 1
-    while tiles * S < 192 and K % (2 * S) == 0 and (K // (2 * S)) % 512 == 0:
+    while tiles * S < min_wgs and K % (2 * S) == 0 and (K // (2 * S)) % 512 == 0:
         S *= 2
     return S if K % S == 0 and (K // S) % 512 == 0 else 0
 
@@ -190,6 +190,11 @@ def decode_plan(M: int, N: int, K: int) -> tuple[int, int]:
         # (profiles/r1_dgemm_m192_sweep.log)
         S = _splits_for(N, K, 64)
         return (S, 64) if S and (N // 64) * S >= 256 else (0, 64)
+    if M <= 16:
+        # batch 1 and a few rows: a full round of 256 workgroups or more -- QKV S=4 (384)
+        # 11.6 us vs S=2 (192) 13.4 at M = 1; O / down stay S=4 (256) (graph-timed,
+        # profiles/r4_b1_probe.log)
+        return _splits_for(N, K, 64, 256), 64
     if M <= 64:
         return _splits_for(N, K, 64), 64
     S64 = _splits_for(N, K, 64)
@@ -452,6 +457,33 @@ def lm_head_argmax_ok(M: int, N: int, K: int) -> bool:
     return not _MID_OFF and 0 < M <= MID_M_MAX and N % 128 == 0 and K % 128 == 0
 
 
+NORM_FUSE_ROWS = 4
+# off by default: the last-workgroup add + RMSNorm tail (one workgroup reading every slab at
+# agent scope) costs more than the add_rmsnorm_splitk launch it replaces -- batch-1 p50
+# 511.5 ms with it vs 492.0 without (profiles/r4_b1_ab.log)
+_NORM_FUSE = os.environ.get("DOCQA_DGEMM_NORM", "0") == "1"
+
+
+def dgemm_norm_plan(M: int, N: int, K: int) -> int:
+    """Split count of the few-row projection with the residual add + RMSNorm fused into its
+    last workgroup (dgemm.hip NormArgs), 0 where it does not apply (more than
+    NORM_FUSE_ROWS rows, N > 8192, no skinny-kernel plan, DOCQA_DGEMM_NORM=0)."""
+    if not _NORM_FUSE or not (0 < M <= NORM_FUSE_ROWS) or N > 8192 or N % 64:
+        return 0
+    S, t = decode_plan(M, N, K)
+    return S if t == 64 else 0
+
+
+def dgemm_add_rmsnorm(x, w, splits: int, residual, gamma, eps: float, tick):
+    """residual <- residual + bf16(x @ w^T); returns rmsnorm(residual) * gamma -- the
+    split-K projection and the add + norm in one launch (few rows, :func:`dgemm_norm_plan`).
+    ``tick``: one zeroed int32 word (the kernel re-arms it)."""
+    if _gpu(x):
+        return _native().dgemm_add_rmsnorm(x.contiguous(), w, int(splits), residual, gamma, float(eps), tick)
+    y = torch.nn.functional.linear(x.float(), w.float()).to(residual.dtype)
+    return ref.add_rmsnorm(y, residual, gamma, eps)
+
+
 def add_rmsnorm_splitk(P, residual, w, eps: float):
     """residual <- residual + bf16(sum_s P[s]); returns rmsnorm(residual) * w."""
     if _gpu(P):
@@ -460,16 +492,31 @@ def add_rmsnorm_splitk(P, residual, w, eps: float):
 
 
 def paged_decode_fused(P, positions, cos_sin, slot_mapping, k_cache, v_cache, block_tables,
-                       context_lens, Hq, max_context, scale, order=None):
+                       context_lens, Hq, max_context, scale, order=None, tick=None):
     """Decode attention straight from the QKV projection's split-K partial slabs: RoPE,
     paged-cache write of the new token and attention in one launch (attn_decode.hip ring
-    kernel, FUSED mode).  Same result as rope_cache_splitk + paged_decode."""
+    kernel, FUSED mode).  Same result as rope_cache_splitk + paged_decode.
+    ``tick``: a zeroed int32 buffer of >= B x Hkv entries (:func:`decode_ticket`) -- split
+    context partitions are then merged by their last workgroup, no second launch."""
     if _gpu(P):
         return _native().paged_decode_fused(P, positions, cos_sin, slot_mapping, k_cache, v_cache,
-                                            block_tables, context_lens, Hq, max_context, scale, order)
+                                            block_tables, context_lens, Hq, max_context, scale, order,
+                                            tick)
     Hkv, D = k_cache.shape[1], k_cache.shape[3]
     qkv = rope_cache_splitk(P, positions, cos_sin, slot_mapping, k_cache, v_cache, Hq, Hkv, D)
     return ref.paged_decode(qkv, k_cache, v_cache, block_tables, context_lens, Hq, max_context, scale)
+
+
+_LAST_MERGE = os.environ.get("DOCQA_DECODE_LAST_MERGE", "1") != "0"
+
+
+def decode_ticket(n: int, device) -> torch.Tensor | None:
+    """Zeroed int32 ticket words for the last-arriver partition merge of the decode
+    attention kernels (one per sequence x KV head; the kernel re-arms them).  None when
+    DOCQA_DECODE_LAST_MERGE=0 (separate reduce launch)."""
+    if not _LAST_MERGE:
+        return None
+    return torch.zeros(n, dtype=torch.int32, device=device)
 
 
 def fused_decode_ok(k_cache, block_tables) -> bool:

@@ -414,6 +414,79 @@ def test_paged_decode_fused(native, B, Hkv, S):
     _close(o1[valid], o2[valid], 2e-2, 1e-2)
 
 
+@pytest.mark.parametrize("B,S,max_context", [(1, 2, 2048), (1, 4, 8192), (3, 1, 1024), (64, 2, 2048)])
+def test_paged_decode_fused_last_merge(native, B, S, max_context):
+    """In-kernel last-arriver partition merge (tick buffer) == the separate reduce launch (to
+    bf16 rounding), over repeated launches (the kernel re-arms its tickets), a padded row
+    (context 0) included; and both == the fp32 reference attention."""
+    from docqa_amd.ops import reference as R
+
+    G, Hkv, D, BS = 4, 8, 128, 64
+    maxb = max_context // BS
+    Hq = G * Hkv
+    W = (Hq + 2 * Hkv) * D
+    torch.manual_seed(B * 7 + S)
+    P = torch.randn(S, B, W, device="cuda") * 0.5
+    pos = torch.randint(0, max_context - 1, (B,), device="cuda", dtype=torch.int32)
+    pos[0] = min(830, max_context - 2)                  # the batch-1 bench's context length
+    bt = torch.randperm(B * maxb, device="cuda").int().view(B, maxb)
+    slots = (bt.gather(1, (pos // BS).long()[:, None])[:, 0] * BS + pos % BS).int()
+    cl = pos + 1
+    if B > 2:
+        cl[B // 2] = 0                                  # padded decode slot
+        slots[B // 2] = -1
+    kc = torch.randn(B * maxb, Hkv, BS, D, device="cuda", dtype=torch.bfloat16)
+    vc = torch.randn_like(kc)
+    cs = R.rope_cos_sin(max_context, D, 500000.0, "cuda")
+    scale = 1 / math.sqrt(D)
+    tick = torch.zeros(B * Hkv, device="cuda", dtype=torch.int32)
+    kc0, vc0 = kc.clone(), vc.clone()
+    base = native.paged_decode_fused(P, pos, cs, slots, kc0, vc0, bt, cl, Hq, max_context, scale)
+    for _ in range(3):
+        kc1, vc1 = kc.clone(), vc.clone()
+        o = native.paged_decode_fused(P, pos, cs, slots, kc1, vc1, bt, cl, Hq, max_context, scale, None, tick)
+        torch.cuda.synchronize()
+        # same arithmetic as the reduce launch; the two kernel instantiations may contract a
+        # multiply-add differently, so allow bf16 rounding-level differences only
+        d = (o.float() - base.float()).abs().max().item()
+        print(f"last-merge vs reduce max |diff| {d:.3g}, bit-equal {torch.equal(o, base)}")
+        _close(o, base, 8e-3, 8e-3)
+        assert int(tick.abs().sum()) == 0
+        assert torch.equal(kc1, kc0) and torch.equal(vc1, vc0)
+    ref = R.paged_decode(native.rope_cache_splitk(P, pos, cs, slots, kc.clone(), vc.clone(), Hq, Hkv, D).float(),
+                         kc0.float(), vc0.float(), bt, cl, Hq, max_context, scale)
+    valid = cl > 0
+    _close(base[valid], ref.to(base.dtype)[valid], 2e-2, 1e-2)
+    if B > 2:
+        assert int(base[B // 2].abs().sum()) == 0
+
+
+@pytest.mark.parametrize("M", [1, 2, 4])
+@pytest.mark.parametrize("N,K,S", [(4096, 4096, 4), (4096, 14336, 4), (8192, 1024, 2), (1024, 2048, 1)])
+def test_dgemm_add_rmsnorm_fused(native, M, N, K, S):
+    """Projection + residual add + RMSNorm in one launch (last-workgroup epilogue) == the
+    split-K projection + add_rmsnorm_splitk, bit for bit (outputs and residual), over
+    repeated launches with one ticket word (re-armed by the kernel); and == fp32 reference."""
+    from docqa_amd.ops import reference as R
+
+    x = torch.randn(M, K, device="cuda", dtype=torch.bfloat16)
+    w = (torch.randn(N, K, device="cuda") / K ** 0.5).bfloat16()
+    g = (1 + 0.1 * torch.randn(N, device="cuda")).bfloat16()
+    r0 = torch.randn(M, N, device="cuda", dtype=torch.bfloat16)
+    r_ref = r0.clone()
+    o_ref = native.add_rmsnorm_splitk(native.dgemm_partial(x, w, S, 64), r_ref, g, 1e-5)
+    tick = torch.zeros(1, device="cuda", dtype=torch.int32)
+    for _ in range(3):
+        r = r0.clone()
+        o = native.dgemm_add_rmsnorm(x, w, S, r, g, 1e-5, tick)
+        torch.cuda.synchronize()
+        assert torch.equal(o, o_ref) and torch.equal(r, r_ref)
+        assert int(tick.item()) == 0
+    r32 = r0.clone()
+    o32 = R.add_rmsnorm((x.float() @ w.float().T).bfloat16(), r32, g, 1e-5)
+    _close(o, o32, 3e-2, 3e-2)
+
+
 @pytest.mark.parametrize("M", [48, 256])
 def test_dgemm_asymmetric_identity(native, M):
     """X = I rows against an asymmetric W: Y must be W's columns, catches transposed writes
