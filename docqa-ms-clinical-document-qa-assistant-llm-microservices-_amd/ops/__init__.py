@@ -190,11 +190,9 @@ def decode_plan(M: int, N: int, K: int) -> tuple[int, int]:
         # (profiles/r1_dgemm_m192_sweep.log)
         S = _splits_for(N, K, 64)
         return (S, 64) if S and (N // 64) * S >= 256 else (0, 64)
-    if M <= 16:
-        # batch 1 and a few rows: a full round of 256 workgroups or more -- QKV S=4 (384)
-        # 11.6 us vs S=2 (192) 13.4 at M = 1; O / down stay S=4 (256) (graph-timed,
-        # profiles/r4_b1_probe.log)
-        return _splits_for(N, K, 64, 256), 64
+    # (QKV at S=4 times 11.6 vs 13.4 us alone at M = 1, profiles/r4_b1_decode_gemm_split_probe.log,
+    # but the fused attention then sums twice the slabs: batch-1 decode 471-473 vs 468-470 ms
+    # per query, profiles/r4_b1_ab.log -- S=2 stays)
     if M <= 64:
         return _splits_for(N, K, 64), 64
     S64 = _splits_for(N, K, 64)
