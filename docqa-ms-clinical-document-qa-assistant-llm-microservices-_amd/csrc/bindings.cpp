@@ -202,6 +202,22 @@ at::Tensor embedding(const at::Tensor& ids, const at::Tensor& table) {
   return out;
 }
 
+// (h, x): h = table[ids] (residual stream), x = rmsnorm(h) * w
+std::tuple<at::Tensor, at::Tensor> embed_rmsnorm(const at::Tensor& ids, const at::Tensor& table, const at::Tensor& w,
+                                                 double eps) {
+  CHECK_GPU(ids); CHECK_I32(ids); CHECK_CONTIG(ids); CHECK_BF16(table); CHECK_CONTIG(table); CHECK_BF16(w);
+  const int H = table.size(1);
+  TORCH_CHECK(w.numel() == H, "embed_rmsnorm: weight of H");
+  auto sizes = ids.sizes().vec();
+  sizes.push_back(H);
+  c10::DeviceGuard g(ids.device());
+  auto h = at::empty(sizes, table.options());
+  auto x = at::empty(sizes, table.options());
+  CHECK_RC(docqa_embed_rmsnorm(ids.data_ptr<int>(), table.data_ptr(), w.data_ptr(), h.data_ptr(), x.data_ptr(),
+                               ids.numel(), H, (int)table.size(0), (float)eps, stream()), "embed_rmsnorm");
+  return {h, x};
+}
+
 at::Tensor bert_embed_ln(const at::Tensor& ids, const at::Tensor& pos,
                          const c10::optional<at::Tensor>& token_type, const at::Tensor& wte,
                          const at::Tensor& wpe, const at::Tensor& wtt, const at::Tensor& gamma,
@@ -651,6 +667,43 @@ at::Tensor dgemm_add_rmsnorm(const at::Tensor& x, const at::Tensor& w, int64_t s
   CHECK_RC(docqa_dgemm_add_rmsnorm(x.data_ptr(), w.data_ptr(), part.data_ptr<float>(), M, N, K, (int)splits,
                                    residual.data_ptr(), gamma.data_ptr(), out.data_ptr(), (float)eps,
                                    tick.data_ptr<int>(), stream()), "dgemm_add_rmsnorm");
+  return out;
+}
+
+// batch-1 projection whose input row is built in-kernel from the previous projection's slabs:
+// x = rmsnorm(res_in + bf16(sum Pin)) * gamma, res_out <- res_in + bf16(sum Pin)
+static void check_xn(const at::Tensor& Pin, const at::Tensor& res_in, const at::Tensor& res_out,
+                     const at::Tensor& gamma, const at::Tensor& w) {
+  CHECK_GPU(Pin); CHECK_CONTIG(Pin); CHECK_BF16(res_in); CHECK_BF16(res_out); CHECK_BF16(gamma); CHECK_BF16(w);
+  CHECK_CONTIG(res_in); CHECK_CONTIG(res_out); CHECK_CONTIG(w);
+  TORCH_CHECK(Pin.scalar_type() == at::kFloat && Pin.dim() == 3 && Pin.size(1) == 1, "xn: slabs fp32 [S, 1, K]");
+  const int64_t K = w.size(1);
+  TORCH_CHECK(Pin.size(2) == K && res_in.numel() == K && res_out.numel() == K && gamma.numel() == K,
+              "xn: one row of K");
+  TORCH_CHECK(res_in.data_ptr() != res_out.data_ptr(), "xn: res_out must be a second buffer");
+}
+
+at::Tensor dgemm_partial_xn(const at::Tensor& Pin, const at::Tensor& res_in, at::Tensor res_out,
+                            const at::Tensor& gamma, double eps, const at::Tensor& w, int64_t splits) {
+  check_xn(Pin, res_in, res_out, gamma, w);
+  const int N = w.size(0), K = w.size(1);
+  c10::DeviceGuard g(Pin.device());
+  auto part = at::empty({splits, 1, N}, Pin.options());
+  CHECK_RC(docqa_dgemm_partial_xn(Pin.data_ptr<float>(), Pin.size(0), res_in.data_ptr(), res_out.data_ptr(),
+                                  gamma.data_ptr(), (float)eps, w.data_ptr(), part.data_ptr<float>(), N, K,
+                                  (int)splits, stream()), "dgemm_partial_xn");
+  return part;
+}
+
+at::Tensor dgemm_glu_xn(const at::Tensor& Pin, const at::Tensor& res_in, at::Tensor res_out, const at::Tensor& gamma,
+                        double eps, const at::Tensor& w) {
+  check_xn(Pin, res_in, res_out, gamma, w);
+  const int N = w.size(0), K = w.size(1);
+  c10::DeviceGuard g(Pin.device());
+  auto out = at::empty({1, N / 2}, res_in.options());
+  CHECK_RC(docqa_dgemm_glu_xn(Pin.data_ptr<float>(), Pin.size(0), res_in.data_ptr(), res_out.data_ptr(),
+                              gamma.data_ptr(), (float)eps, w.data_ptr(), out.data_ptr(), N, K, stream()),
+           "dgemm_glu_xn");
   return out;
 }
 
@@ -1190,6 +1243,10 @@ TORCH_LIBRARY(docqa, m) {
         "float scale, Tensor k_cache, Tensor v_cache, Tensor block_tables, Tensor ctx_start) -> Tensor");
   m.def("dgemm(Tensor x, Tensor w, int splits) -> Tensor");
   m.def("dgemm_partial(Tensor x, Tensor w, int splits, int tile_rows=64) -> Tensor");
+  m.def("embed_rmsnorm(Tensor ids, Tensor table, Tensor w, float eps) -> (Tensor, Tensor)");
+  m.def("dgemm_partial_xn(Tensor Pin, Tensor res_in, Tensor(a!) res_out, Tensor gamma, float eps, Tensor w, "
+        "int splits) -> Tensor");
+  m.def("dgemm_glu_xn(Tensor Pin, Tensor res_in, Tensor(a!) res_out, Tensor gamma, float eps, Tensor w) -> Tensor");
   m.def("dgemm_add_rmsnorm(Tensor x, Tensor w, int splits, Tensor(a!) residual, Tensor gamma, float eps, "
         "Tensor(t!) tick) -> Tensor");
   m.def("dgemm_glu(Tensor x, Tensor w) -> Tensor");
@@ -1266,6 +1323,9 @@ TORCH_LIBRARY_IMPL(docqa, CUDA, m) {
   m.impl("flash_prefill_paged", &flash_prefill_paged);
   m.impl("dgemm", &dgemm);
   m.impl("dgemm_partial", &dgemm_partial);
+  m.impl("embed_rmsnorm", &embed_rmsnorm);
+  m.impl("dgemm_partial_xn", &dgemm_partial_xn);
+  m.impl("dgemm_glu_xn", &dgemm_glu_xn);
   m.impl("dgemm_add_rmsnorm", &dgemm_add_rmsnorm);
   m.impl("dgemm_glu", &dgemm_glu);
   m.impl("mgemm", &mgemm);

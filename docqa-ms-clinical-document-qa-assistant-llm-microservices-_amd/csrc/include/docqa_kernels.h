@@ -116,6 +116,12 @@ int docqa_dgemm_splits(int N, int K);
 int docqa_dgemm_glu(const void* X, const void* W, void* Y, int M, int N, int K, hipStream_t s);
 int docqa_dgemm_add_rmsnorm(const void* X, const void* W, float* P, int M, int N, int K, int S, void* residual,
                             const void* gamma, void* out, float eps, int* tick, hipStream_t s);
+int docqa_dgemm_partial_xn(const float* Pin, int Sin, const void* res_in, void* res_out, const void* gamma,
+                           float eps, const void* W, float* P, int N, int K, int S, hipStream_t s);
+int docqa_dgemm_glu_xn(const float* Pin, int Sin, const void* res_in, void* res_out, const void* gamma, float eps,
+                       const void* W, void* Y, int N, int K, hipStream_t s);
+int docqa_embed_rmsnorm(const int* ids, const void* table, const void* w, void* h, void* x, int T, int H, int V,
+                        float eps, hipStream_t s);
 int docqa_dgemm_argmax(const void* X, const void* W, int64_t* out, float* outv, float* ws_v, int* ws_i, int M,
                        int N, int K, int n_valid, hipStream_t s);
 int docqa_dgemm(const void* X, const void* W, void* Y, float* partial, int M, int N, int K, int S,

@@ -106,23 +106,118 @@ struct NormArgs {
   float eps = 0.f;
 };
 
-template <int EPI, int MT, int NT, int NSR, int XA = 2, bool NORM = false>
+// XNormIn (batch 1, XN mode): the projection's input row is not read from X but built by
+// the workgroup itself from the PREVIOUS projection's split-K slabs -- residual add + RMSNorm
+// (the add_rmsnorm_splitk arithmetic, same thread -> chunk map, so the same bits) into LDS,
+// while the first weight stages are already streaming.  One workgroup writes the updated
+// residual to res_out (a second buffer: the others still read res_in), so the norm launch
+// between two decode projections disappears.
+struct XNormIn {
+  const float* P = nullptr;          // [S, 1, K] fp32 slabs of the previous projection
+  int S = 0;                         // 1..64 (up to 4 loaded in parallel)
+  const uint16_t* res_in = nullptr;  // [1, K]
+  uint16_t* res_out = nullptr;       // [1, K] = res_in + bf16(sum P)
+  const uint16_t* gamma = nullptr;   // [K]
+  float eps = 0.f;
+};
+constexpr int kXnMaxK = 4096;
+
+// residual add + RMSNorm of the one input row into sx[0 .. Ks) (k slice [kbeg, kbeg + Ks))
+__device__ __forceinline__ void xnorm_prologue(const XNormIn& xn, int K, int kbeg, int Ks, bool writer,
+                                               uint16_t* sx, float* red) {
+  constexpr int NV = kXnMaxK / 8 / 256;
+  const int tid = threadIdx.x, nchunk = K >> 3;
+  const uint4* rr = reinterpret_cast<const uint4*>(xn.res_in);
+  const uint4* wr = reinterpret_cast<const uint4*>(xn.gamma);
+  float v[NV][8];
+  uint4 rres[NV], wres[NV];
+  float4 pa[NV][4], pb[NV][4];
+  // every load (residual, gamma, up to 4 slabs; clamped slabs loaded, not added) before the
+  // first use: one memory latency, overlapped with the weight stages issued before
+#pragma unroll
+  for (int i = 0; i < NV; ++i) {
+    const int c = min(tid + 256 * i, nchunk - 1);
+    rres[i] = rr[c];
+    wres[i] = wr[c];
+#pragma unroll
+    for (int sl = 0; sl < 4; ++sl) {
+      const float* q = xn.P + (size_t)min(sl, xn.S - 1) * K + c * 8;
+      pa[i][sl] = *reinterpret_cast<const float4*>(q);
+      pb[i][sl] = *reinterpret_cast<const float4*>(q + 4);
+    }
+  }
+  float ss = 0.f;
+#pragma unroll
+  for (int i = 0; i < NV; ++i) {
+    const int c = tid + 256 * i;
+    if (c < nchunk) {
+      float4 a = pa[i][0], b = pb[i][0];
+#pragma unroll
+      for (int sl = 1; sl < 4; ++sl)
+        if (sl < xn.S) {
+          a.x += pa[i][sl].x; a.y += pa[i][sl].y; a.z += pa[i][sl].z; a.w += pa[i][sl].w;
+          b.x += pb[i][sl].x; b.y += pb[i][sl].y; b.z += pb[i][sl].z; b.w += pb[i][sl].w;
+        }
+      for (int sl = 4; sl < xn.S; ++sl) {   // more than 4 slabs (small models): in order, serial
+        const float* q = xn.P + (size_t)sl * K + c * 8;
+        const float4 a2 = *reinterpret_cast<const float4*>(q), b2 = *reinterpret_cast<const float4*>(q + 4);
+        a.x += a2.x; a.y += a2.y; a.z += a2.z; a.w += a2.w;
+        b.x += b2.x; b.y += b2.y; b.z += b2.z; b.w += b2.w;
+      }
+      const float x8[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+      float r[8];
+      unpack8(rres[i], r);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[i][j] = bf2f(f2bf(bf2f(f2bf(x8[j])) + r[j]));
+      if (writer) reinterpret_cast<uint4*>(xn.res_out)[c] = pack8(v[i]);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) ss += v[i][j] * v[i][j];
+    }
+  }
+  ss = wave_sum(ss);
+  if ((tid & 63) == 0) red[tid >> 6] = ss;
+  __syncthreads();
+  ss = red[0] + red[1] + red[2] + red[3];
+  const float inv = rsqrtf(ss / (float)K + xn.eps);
+#pragma unroll
+  for (int i = 0; i < NV; ++i) {
+    const int c = tid + 256 * i;
+    if (c < nchunk && c * 8 >= kbeg && c * 8 < kbeg + Ks) {
+      float g[8], o[8];
+      unpack8(wres[i], g);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) o[j] = v[i][j] * inv * g[j];
+      *reinterpret_cast<uint4*>(sx + c * 8 - kbeg) = pack8(o);
+    }
+  }
+  __syncthreads();
+}
+
+template <int EPI, int MT, int NT, int NSR, int XA = 2, bool NORM = false, bool XN = false>
 __global__ __launch_bounds__(256) void dgemm_kernel(const uint16_t* __restrict__ X,
                                                     const uint16_t* __restrict__ W,
                                                     uint16_t* __restrict__ Y,
                                                     float* __restrict__ P, int M, int N, int K,
                                                     int Ks, int xcd_remap, float* __restrict__ pv = nullptr,
                                                     int* __restrict__ pi = nullptr, int n_valid = 0,
-                                                    NormArgs na = NormArgs{}) {
+                                                    NormArgs na = NormArgs{}, XNormIn xn = XNormIn{}) {
   static_assert(!NORM || EPI == EPI_PARTIAL, "the fused norm consumes split-K slabs");
+  static_assert(!XN || (MT == 1 && XA == 2), "the in-LDS input row is the one-row (batch-1) case");
   constexpr int MPW = MT > 4 ? MT / 4 : 1;       // m-tiles per wave
   constexpr int MTW = MT > 4 ? 4 : MT;           // wave groups along m
   constexpr int KW = 4 / MTW, SPW = KSTEPS / KW;
   constexpr int XR = MPW * SPW;                  // X fragments per wave per stage
+  constexpr int XV = XN ? 0 : XR;                // ... of them vector-memory loads
+  // vector-memory ops allowed in flight at the top of a step: XN counts exactly the NSR - 2
+  // weight stages issued after this step's (deeper XN rings hide the input-row prologue);
+  // the X-streaming variants keep the tuned 4-slot count
+  constexpr int VW = XN ? (NSR - 2) * NT : 2 * NT + XV;
   constexpr int STAGE = NT * 16 * BKD;           // elements of one W stage (NT x 4 KB)
   static_assert(NSR >= 4, "ring needs >= 4 slots");
   static_assert(MT <= 4 || MT == 8 || MT == 12, "MT in {1, 2, 4, 8, 12}");
   __shared__ __attribute__((aligned(16))) uint16_t sw[NSR * STAGE];   // W ring
+  __shared__ __attribute__((aligned(16))) uint16_t sx[XN ? kXnMaxK : 8];  // XN: the input row slice
+  __shared__ float xred[4];
   // XCD-aware split-K placement: workgroups are dealt to the 8 XCDs round-robin by linear
   // id, so with the plain (tile, slice) grid every XCD sees every K slice and its 4 MB L2
   // must hold all of X next to the weight stream.  Remapped, XCD x only runs slice x % S:
@@ -176,6 +271,10 @@ __global__ __launch_bounds__(256) void dgemm_kernel(const uint16_t* __restrict__
     for (int i = 0; i < NT; ++i) glds16<true>(wsrc[i] + koff, dst + (uint32_t)((i * 4 + wave) * 1024));
   };
   auto load_x = [&](bf16x8 (&x)[XR], int j) {
+    if constexpr (XN) {   // one row, from the prologue's LDS slice (a broadcast read)
+      x[0] = *reinterpret_cast<const bf16x8*>(sx + min(j, nkb - 1) * BKD + kg * SPW * 32 + fq * 8);
+      return;
+    }
 #pragma unroll
     for (int mi = 0; mi < MPW; ++mi) {
       const uint16_t* src = xrow[mi] + min(j, nkb - 1) * BKD;
@@ -211,19 +310,29 @@ __global__ __launch_bounds__(256) void dgemm_kernel(const uint16_t* __restrict__
   stage_w((I) + NSR - 1);                                                               \
   mma(XC, I);
   if constexpr (XA == 2) {
+    if constexpr (XN) {
+      // weight stages first, then the input row (its loads overlap theirs; waiting for them
+      // retires the stages too -- vmcnt is in order), then the first two X fragments
 #pragma unroll
-    for (int j = 0; j <= NSR - 4; ++j) stage_w(j);
-    load_x(x0, 0);
-    stage_w(NSR - 3);
-    load_x(x1, 1);
-    stage_w(NSR - 2);
+      for (int j = 0; j <= NSR - 2; ++j) stage_w(j);
+      xnorm_prologue(xn, K, kbeg, Ks, blockIdx.x == 0 && blockIdx.y == 0, sx, xred);
+      load_x(x0, 0);
+      load_x(x1, 1);
+    } else {
+#pragma unroll
+      for (int j = 0; j <= NSR - 4; ++j) stage_w(j);
+      load_x(x0, 0);
+      stage_w(NSR - 3);
+      load_x(x1, 1);
+      stage_w(NSR - 2);
+    }
     // nkb % 4 == 0: a break-free 4-step body keeps each X buffer in one register set (an
     // early exit makes hipcc merge buffers with register copies that read in-flight data)
     for (int i = 0; i < nkb; i += 4) {
-      RING_STEP(i, x0, x2, 2 * NT + XR)
-      RING_STEP(i + 1, x1, x3, 2 * NT + XR)
-      RING_STEP(i + 2, x2, x0, 2 * NT + XR)
-      RING_STEP(i + 3, x3, x1, 2 * NT + XR)
+      RING_STEP(i, x0, x2, VW)
+      RING_STEP(i + 1, x1, x3, VW)
+      RING_STEP(i + 2, x2, x0, VW)
+      RING_STEP(i + 3, x3, x1, VW)
     }
   } else {
     // X three k-blocks ahead (the 65-128-row case, where X -- not W -- is the longer
@@ -512,6 +621,43 @@ int docqa_dgemm_add_rmsnorm(const void* X, const void* W, float* P, int M, int N
   return 0;
 }
 
+// Batch-1 projections whose input row is rmsnorm(res_in + bf16(sum of the previous
+// projection's slabs)) * gamma, built in LDS by each workgroup (XNormIn): split-K slabs out
+// (the next layer's QKV) or the fused SwiGLU (gate|up).  res_out <- res_in + bf16(sum Pin).
+static bool xn_ok(int N, int K, int S, int bn, const XNormIn& xn) {
+  return K <= kXnMaxK && xn.S >= 1 && xn.S <= 64 && xn.P && xn.res_in && xn.res_out &&
+         xn.gamma && xn.res_in != xn.res_out && shape_ok(1, N, K, S, bn);
+}
+
+int docqa_dgemm_partial_xn(const float* Pin, int Sin, const void* res_in, void* res_out, const void* gamma,
+                           float eps, const void* W, float* P, int N, int K, int S, hipStream_t s) {
+  const XNormIn xn{Pin, Sin, (const uint16_t*)res_in, (uint16_t*)res_out, (const uint16_t*)gamma, eps};
+  if (!P || !xn_ok(N, K, S, BN, xn)) return -1;
+  const dim3 grid(N / BN, S);
+  const int xr = (xcd_knob() && S > 1 && 8 % S == 0 && (grid.x * S) % 8 == 0) ? 1 : 0;
+  // (an 8-slot ring to stream on under the input-row prologue measured slower: QKV 17.7 vs
+  // 16.4 us, profiles/r4_b1_ab.log)
+  dgemm_kernel<EPI_PARTIAL, 1, 4, NS, 2, false, true><<<grid, 256, 0, s>>>(
+      nullptr, (const uint16_t*)W, nullptr, P, 1, N, K, K / S, xr, nullptr, nullptr, 0, NormArgs{}, xn);
+  DOCQA_CHECK_LAUNCH();
+  return 0;
+}
+
+int docqa_dgemm_glu_xn(const float* Pin, int Sin, const void* res_in, void* res_out, const void* gamma, float eps,
+                       const void* W, void* Y, int N, int K, hipStream_t s) {
+  const XNormIn xn{Pin, Sin, (const uint16_t*)res_in, (uint16_t*)res_out, (const uint16_t*)gamma, eps};
+  if (xn_ok(N, K, 1, 112, xn) && N / 112 >= 192)
+    dgemm_kernel<EPI_GLU, 1, 7, NS, 2, false, true><<<dim3(N / 112), 256, 0, s>>>(
+        nullptr, (const uint16_t*)W, (uint16_t*)Y, nullptr, 1, N, K, K, 0, nullptr, nullptr, 0, NormArgs{}, xn);
+  else if (xn_ok(N, K, 1, 64, xn))
+    dgemm_kernel<EPI_GLU, 1, 4, NS, 2, false, true><<<dim3(N / 64), 256, 0, s>>>(
+        nullptr, (const uint16_t*)W, (uint16_t*)Y, nullptr, 1, N, K, K, 0, nullptr, nullptr, 0, NormArgs{}, xn);
+  else
+    return -1;
+  DOCQA_CHECK_LAUNCH();
+  return 0;
+}
+
 // Y[M, N/2] = silu(gate) * up for the 8-interleaved gate|up weight W [N, K] (N = 2 I)
 int docqa_dgemm_glu(const void* X, const void* W, void* Y, int M, int N, int K, hipStream_t s) {
   if (M == 0) return 0;
@@ -544,7 +690,7 @@ int docqa_dgemm_argmax(const void* X, const void* W, int64_t* out, float* outv, 
   const int mt = (M + 15) / 16;
   launch_mt<EPI_ARGMAX, 4>(mt, dim3(N / BN), s, (const uint16_t*)X, (const uint16_t*)W, nullptr, nullptr, M, N, K,
                            K, ws_v, ws_i, n_valid);
-  argmax_merge_kernel<<<M, 64, 0, s>>>(ws_v, ws_i, N / BN, out, outv);
+  argmax_merge_kernel<<<M, 256, 0, s>>>(ws_v, ws_i, N / BN, out, outv);
   DOCQA_CHECK_LAUNCH();
   return 0;
 }

@@ -25,6 +25,53 @@ __global__ __launch_bounds__(256) void embedding_gather_kernel(const int* __rest
   for (int c = threadIdx.x; c < (H >> 3); c += blockDim.x) dst[c] = src[c];
 }
 
+// Llama input: h = table[id] (the residual stream) and x = rmsnorm(h) * w for the first
+// layer in one launch, one workgroup per token (decode: one kernel and one boundary fewer
+// per step).  Same thread -> chunk map and arithmetic as norm.hip rmsnorm_row_kernel.
+template <int NV>
+__global__ __launch_bounds__(256) void embed_rmsnorm_kernel(const int* __restrict__ ids,
+                                                            const uint16_t* __restrict__ table,
+                                                            const uint16_t* __restrict__ w,
+                                                            uint16_t* __restrict__ h, uint16_t* __restrict__ x,
+                                                            int H, int V, float eps) {
+  __shared__ float red[4];
+  const int t = blockIdx.x, tid = threadIdx.x, nchunk = H >> 3;
+  const int id = (unsigned)ids[t] < (unsigned)V ? ids[t] : 0;
+  const uint4* src = reinterpret_cast<const uint4*>(table + (size_t)id * H);
+  uint4* hr = reinterpret_cast<uint4*>(h + (size_t)t * H);
+  float v[NV][8];
+  float ss = 0.f;
+#pragma unroll
+  for (int i = 0; i < NV; ++i) {
+    const int c = tid + 256 * i;
+    if (c < nchunk) {
+      const uint4 q = src[c];
+      hr[c] = q;
+      unpack8(q, v[i]);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) ss += v[i][j] * v[i][j];
+    }
+  }
+  ss = wave_sum(ss);
+  if ((tid & 63) == 0) red[tid >> 6] = ss;
+  __syncthreads();
+  ss = red[0] + red[1] + red[2] + red[3];
+  const float inv = rsqrtf(ss / (float)H + eps);
+  const uint4* wr = reinterpret_cast<const uint4*>(w);
+  uint4* xr = reinterpret_cast<uint4*>(x + (size_t)t * H);
+#pragma unroll
+  for (int i = 0; i < NV; ++i) {
+    const int c = tid + 256 * i;
+    if (c < nchunk) {
+      float g[8], o[8];
+      unpack8(wr[c], g);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) o[j] = v[i][j] * inv * g[j];
+      xr[c] = pack8(o);
+    }
+  }
+}
+
 template <int NV>
 __global__ __launch_bounds__(256) void bert_embed_ln_kernel(
     const int* __restrict__ ids, const int* __restrict__ pos, const int* __restrict__ tt,
@@ -260,6 +307,25 @@ int docqa_embedding(const int* ids, const void* table, void* out, int T, int H, 
   if (T == 0) return 0;
   if (H % 8 != 0 || !docqa_aligned16(table) || !docqa_aligned16(out)) return -1;
   embedding_gather_kernel<<<T, 256, 0, s>>>(ids, (const uint16_t*)table, (uint16_t*)out, H, V);
+  DOCQA_CHECK_LAUNCH();
+  return 0;
+}
+
+int docqa_embed_rmsnorm(const int* ids, const void* table, const void* w, void* h, void* x, int T, int H, int V,
+                        float eps, hipStream_t s) {
+  if (T == 0) return 0;
+  if (H % 8 != 0 || H > 8192 || !docqa_aligned16(table) || !docqa_aligned16(w) || !docqa_aligned16(h) ||
+      !docqa_aligned16(x)) return -1;
+  const int nv = (H / 8 + 255) / 256;
+  if (nv <= 1)
+    embed_rmsnorm_kernel<1><<<T, 256, 0, s>>>(ids, (const uint16_t*)table, (const uint16_t*)w, (uint16_t*)h,
+                                              (uint16_t*)x, H, V, eps);
+  else if (nv == 2)
+    embed_rmsnorm_kernel<2><<<T, 256, 0, s>>>(ids, (const uint16_t*)table, (const uint16_t*)w, (uint16_t*)h,
+                                              (uint16_t*)x, H, V, eps);
+  else
+    embed_rmsnorm_kernel<4><<<T, 256, 0, s>>>(ids, (const uint16_t*)table, (const uint16_t*)w, (uint16_t*)h,
+                                              (uint16_t*)x, H, V, eps);
   DOCQA_CHECK_LAUNCH();
   return 0;
 }

@@ -453,7 +453,7 @@ int docqa_wgemm_argmax(const void* X, const void* W, int64_t* out, float* outv, 
   const int rc = launch_cfg<EPI_ARGMAX>(cfg, (const uint16_t*)X, (const uint16_t*)W, nullptr, nullptr, ws_v, ws_i,
                                         nullptr, nullptr, nullptr, M, N, K, 1, n_valid, s);
   if (rc) return rc;
-  argmax_merge_kernel<<<M, 64, 0, s>>>(ws_v, ws_i, N / tile_n(cfg), out, outv);
+  argmax_merge_kernel<<<M, 256, 0, s>>>(ws_v, ws_i, N / tile_n(cfg), out, outv);
   DOCQA_CHECK_LAUNCH();
   return 0;
 }

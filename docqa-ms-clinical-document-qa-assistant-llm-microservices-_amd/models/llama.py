@@ -294,9 +294,8 @@ class LlamaModel:
         is fused into its GEMM where :func:`ops.lm_head_argmax_ok`)."""
         cfg = self.cfg
         D, hq, hkv, eps = cfg.head_dim, self.hq, self.hkv, cfg.rms_eps
-        h = ops.embedding(input_ids, self.embed)
+        h, x = ops.embed_rmsnorm(input_ids, self.embed, self.layers[0]["in_norm"], eps)
         residual = h
-        x = ops.rmsnorm(h, self.layers[0]["in_norm"], eps)
         nl = len(self.layers)
         # decode steps stream every weight once: per projection the mid-M MFMA GEMM
         # (mgemm.hip, 129..512 rows where it wins -- ops.mid_plan) or the skinny
@@ -363,10 +362,25 @@ class LlamaModel:
             chain = ops.chain_plan(M, L0["o"].shape[0], L0["o"].shape[1], L0["gate_up"].shape[0],
                                    L0["qkv"].shape[0])
         pq = None   # this layer's QKV slabs, already computed by the previous layer's chain
+        # batch 1 (one row, TP = 1, skinny-kernel plans): the gate|up and the next layer's QKV
+        # projection build their input row themselves -- residual add + RMSNorm of the previous
+        # projection's slabs, in LDS, under their first weight stages (dgemm.hip XNormIn) --
+        # so no add_rmsnorm launch runs between projections; the residual ping-pongs between
+        # two buffers (one workgroup writes the new one while the others read the old)
+        xn = (decode and self.tp == 1 and chain is None and not nf and x.is_cuda and sq and so and sd
+              and self.layers and ops.xn_ok(M, self.cfg.hidden)
+              and not ops.mid_plan(M, *self.layers[0]["gate_up"].shape, glu=True)[0]
+              and ops.glu_split_plan(M, *self.layers[0]["gate_up"].shape) is None)
+        res2 = torch.empty_like(residual) if xn else None
+        pd = None   # XN: the previous layer's down-projection slabs
         for i, L in enumerate(self.layers):
             kc, vc = kv_caches[i]
             if sq:
-                qkv_slabs = pq if pq is not None else qkv_part(x, L["qkv"])
+                if xn and pd is not None:
+                    qkv_slabs = ops.dgemm_partial_xn(pd, residual, res2, L["in_norm"], eps, L["qkv"], sq)
+                    residual, res2 = res2, residual
+                else:
+                    qkv_slabs = pq if pq is not None else qkv_part(x, L["qkv"])
                 pq = None
             if cascade:
                 # shared-prefix decode: RoPE + cache write, then prefix-once + suffix attention
@@ -431,6 +445,13 @@ class LlamaModel:
                 wq = self.layers[i + 1]["qkv"] if i + 1 < nl else None
                 x, pq = ops.mgemm_chain(a, L["o"], residual, L["post_norm"], L["gate_up"], L["down"], nxt, wq,
                                         self._chain_ctr[i], chain, eps)
+                continue
+            if xn:
+                g = ops.dgemm_glu_xn(o_part(a, L["o"]), residual, res2, L["post_norm"], eps, L["gate_up"])
+                residual, res2 = res2, residual
+                pd = down_part(g, L["down"])
+                if i + 1 == nl:
+                    x = ops.add_rmsnorm_splitk(pd, residual, nxt, eps)
                 continue
             # row-parallel O: (TP all-reduce +) residual add + RMSNorm in one consumer
             if "o" in nf:

@@ -455,6 +455,45 @@ def lm_head_argmax_ok(M: int, N: int, K: int) -> bool:
     return not _MID_OFF and 0 < M <= MID_M_MAX and N % 128 == 0 and K % 128 == 0
 
 
+def embed_rmsnorm(ids, table, w, eps: float):
+    """(h, x): h = table[ids] (the residual stream), x = rmsnorm(h) * w -- the Llama input
+    embedding and the first layer's norm in one launch."""
+    if _gpu(table):
+        return _native().embed_rmsnorm(ids.contiguous(), table, w, float(eps))
+    h = embedding(ids, table)
+    return h, rmsnorm(h, w, eps)
+
+
+_XN = os.environ.get("DOCQA_DECODE_XN", "1") != "0"
+
+
+def xn_ok(M: int, K: int) -> bool:
+    """Batch-1 projections that build their own input row (residual add + RMSNorm of the
+    previous projection's slabs, in LDS) -- :func:`dgemm_partial_xn`, :func:`dgemm_glu_xn`."""
+    return _XN and M == 1 and K <= 4096 and K % 512 == 0
+
+
+def dgemm_partial_xn(Pin, res_in, res_out, gamma, eps: float, w, splits: int):
+    """Split-K slabs of x @ w^T for the one row x = rmsnorm(res_in + bf16(sum Pin)) * gamma,
+    built inside the projection (no add_rmsnorm launch); res_out <- res_in + bf16(sum Pin)
+    (a second buffer -- every workgroup still reads res_in)."""
+    if _gpu(Pin):
+        return _native().dgemm_partial_xn(Pin, res_in, res_out, gamma, float(eps), w, int(splits))
+    res_out.copy_(res_in)
+    x = ref.add_rmsnorm(Pin.sum(0).to(res_out.dtype).view_as(res_out), res_out, gamma, eps)
+    return torch.nn.functional.linear(x.float(), w.float())[None].reshape(1, 1, -1).expand(splits, 1, -1) / splits
+
+
+def dgemm_glu_xn(Pin, res_in, res_out, gamma, eps: float, w_il):
+    """silu(x Wg^T) * (x Wu^T) for x = rmsnorm(res_in + bf16(sum Pin)) * gamma (one row, built
+    in-kernel); res_out <- res_in + bf16(sum Pin)."""
+    if _gpu(Pin):
+        return _native().dgemm_glu_xn(Pin, res_in, res_out, gamma, float(eps), w_il)
+    res_out.copy_(res_in)
+    x = ref.add_rmsnorm(Pin.sum(0).to(res_out.dtype).view_as(res_out), res_out, gamma, eps)
+    return silu_mul(torch.nn.functional.linear(x, w_il), interleaved=True)
+
+
 NORM_FUSE_ROWS = 4
 # off by default: the last-workgroup add + RMSNorm tail (one workgroup reading every slab at
 # agent scope) costs more than the add_rmsnorm_splitk launch it replaces -- batch-1 p50

@@ -109,6 +109,34 @@ def test_embedding_and_bert_embed(native):
            R.bert_embed_ln(ids, pos, None, wte, wpe, wtt, g, bb, 1e-12), 6e-2, 1e-2)
 
 
+@pytest.mark.parametrize("T,H", [(1, 4096), (7, 2048), (300, 4096), (3, 8192), (2, 256)])
+def test_embed_rmsnorm(native, T, H):
+    """Fused Llama input (embedding gather + first RMSNorm) == embedding + rmsnorm, bit for
+    bit; out-of-range ids read row 0 like the plain gather."""
+    table = torch.randn(1000, H, device="cuda", dtype=torch.bfloat16)
+    w = (torch.rand(H, device="cuda") + 0.5).bfloat16()
+    ids = torch.randint(0, 1000, (T,), device="cuda", dtype=torch.int32)
+    ids[0] = 5000 if T > 1 else ids[0]
+    h, x = torch.ops.docqa.embed_rmsnorm(ids, table, w, 1e-5)
+    h2 = native.embedding(ids, table)
+    assert torch.equal(h, h2)
+    assert torch.equal(x, native.rmsnorm(h2, w, 1e-5))
+
+
+@pytest.mark.parametrize("parts", [1, 63, 2004, 4100])
+def test_argmax_merge_partials(native, parts):
+    """LM-head argmax partial merge (256-thread rounds) picks the best (value, lowest id)."""
+    M, K = 3, 512
+    N = parts * 64
+    x = torch.randn(M, K, device="cuda", dtype=torch.bfloat16)
+    w = (torch.randn(N, K, device="cuda") / K ** 0.5).bfloat16()
+    ids, vals = torch.ops.docqa.dgemm_argmax_val(x, w, N)
+    logits = (x.float() @ w.float().T).bfloat16().float()
+    best = logits.max(1).values
+    assert torch.equal(vals.cpu(), best.cpu())
+    assert torch.equal(logits.gather(1, ids[:, None])[:, 0].cpu(), best.cpu())
+
+
 @pytest.mark.parametrize("V,dtype", [(128256, torch.bfloat16), (32000, torch.float32), (1000, torch.bfloat16)])
 def test_argmax(native, V, dtype):
     x = torch.randn(13, V, device="cuda").to(dtype)
@@ -485,6 +513,31 @@ def test_dgemm_add_rmsnorm_fused(native, M, N, K, S):
     r32 = r0.clone()
     o32 = R.add_rmsnorm((x.float() @ w.float().T).bfloat16(), r32, g, 1e-5)
     _close(o, o32, 3e-2, 3e-2)
+
+
+@pytest.mark.parametrize("K,N,Sin,S", [(4096, 6144, 4, 2), (4096, 28672, 4, 0), (2048, 1024, 2, 1),
+                                       (1024, 4096, 1, 0), (4096, 4096, 3, 4)])
+def test_dgemm_xn_input_row(native, K, N, Sin, S):
+    """Batch-1 projection building its own input row (XNormIn: residual add + RMSNorm of the
+    previous projection's slabs in LDS) == add_rmsnorm_splitk + the plain projection, bit for
+    bit -- split-K slabs (S > 0) or fused SwiGLU (S == 0); res_out == the updated residual,
+    res_in untouched."""
+    Pin = torch.randn(Sin, 1, K, device="cuda")
+    r0 = torch.randn(1, K, device="cuda", dtype=torch.bfloat16)
+    gam = (1 + 0.1 * torch.randn(K, device="cuda")).bfloat16()
+    w = (torch.randn(N, K, device="cuda") / K ** 0.5).bfloat16()
+    r_ref = r0.clone()
+    x = native.add_rmsnorm_splitk(Pin, r_ref, gam, 1e-5)
+    ref = native.dgemm_partial(x, w, S, 64) if S else torch.ops.docqa.dgemm_glu(x, w)
+    for _ in range(2):
+        r_in, r_out = r0.clone(), torch.empty_like(r0)
+        if S:
+            got = native.dgemm_partial_xn(Pin, r_in, r_out, gam, 1e-5, w, S)
+        else:
+            got = native.dgemm_glu_xn(Pin, r_in, r_out, gam, 1e-5, w)
+        torch.cuda.synchronize()
+        assert torch.equal(r_in, r0) and torch.equal(r_out, r_ref)
+        assert torch.equal(got, ref), (got.float() - ref.float()).abs().max().item()
 
 
 @pytest.mark.parametrize("M", [48, 256])

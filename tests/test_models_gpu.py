@@ -183,6 +183,35 @@ def test_llama_batch_invariance_logits(native):
         assert _rel(ds[0], db[i]) < 0.02
 
 
+@pytest.mark.parametrize("preset", ["llama3-1b-test"])
+def test_llama_batch1_decode_xn(native, monkeypatch, preset):
+    """Batch-1 decode with the gate|up and next-QKV projections building their own input row
+    (residual add + RMSNorm in-kernel, ping-pong residual) == the same step with separate
+    add_rmsnorm launches, bit for bit; both track the fp32 reference."""
+    from docqa_amd import ops
+    from docqa_amd.engine.kv_cache import KVCache
+    from docqa_amd.models.llama import LlamaConfig, LlamaModel
+
+    m = LlamaModel(LlamaConfig.preset(preset), device="cuda", seed=11)
+    assert ops.xn_ok(1, m.cfg.hidden)
+    g = torch.Generator().manual_seed(6)
+    V = m.cfg.vocab_size
+    prompt = [torch.randint(0, V, (300,), generator=g).tolist()]
+    BS = 64
+    out = {}
+    for xn in (True, False):
+        monkeypatch.setattr(ops, "_XN", xn)
+        kv = KVCache(m.cfg.layers, 16, m.hkv, m.cfg.head_dim, BS).caches
+        _, tb = _prefill_logits(m, kv, prompt, BS)
+        out[xn] = _decode_logits(m, kv, prompt, tb, [7], BS)
+    assert torch.equal(out[True], out[False])
+    with native.use_reference():
+        kv = KVCache(m.cfg.layers, 16, m.hkv, m.cfg.head_dim, BS).caches
+        _, tb = _prefill_logits(m, kv, prompt, BS)
+        ref = _decode_logits(m, kv, prompt, tb, [7], BS)
+    assert _rel(out[True], ref) < 0.03
+
+
 def test_engine_greedy_matches_argmax_of_logits(native):
     """The engine's first generated token is the argmax of the prefill logits."""
     from docqa_amd.engine.llm_engine import LLMEngine, SamplingParams
