@@ -13,6 +13,7 @@ The reference serves one request at a time; here every stage is batched.
 """
 from __future__ import annotations
 
+import math
 import os
 import time
 from dataclasses import dataclass, field
@@ -218,13 +219,22 @@ class RAGPipeline:
         import concurrent.futures as cf
 
         params = params or SamplingParams(stop_on_eos=True)
-        if lead_steps is None:
-            # embed + kNN (side stream) + prompt assembly + KV reservation of batch i+1 should
-            # finish before batch i's last decode step, so batch i+1's prefill is queued right
-            # behind it (launch-before-collect below); an earlier start only adds latency
-            # (measured: lead 4 / 8 / 16 steps -> 205.1 / 204.8 / 204.4 q/s, p50 1264 / 1301 /
-            # 1370 ms; profiles/r2_ab_pipeline_lead.log)
-            lead_steps = int(os.environ.get("DOCQA_PIPELINE_LEAD", "4"))
+        # embed + kNN (side stream) + prompt assembly + KV reservation of batch i+1 should
+        # finish before batch i's last decode step, so batch i+1's prefill is queued right
+        # behind it (launch-before-collect below); an earlier start only adds latency
+        # (measured: lead 4 / 8 / 16 steps -> 205.1 / 204.8 / 204.4 q/s, p50 1264 / 1301 /
+        # 1370 ms; profiles/r2_ab_pipeline_lead.log).  Adaptive (no argument, no env): after
+        # the first batch the lead is the measured preparation time over the measured decode
+        # step time, x1.5 -- 1 step at batch 1 (1.5 ms of preparation vs 3.6 ms steps; a
+        # fixed 4 put 11 ms of waiting into every answer's latency), 4 at batch 256
+        env_lead = os.environ.get("DOCQA_PIPELINE_LEAD")
+        adaptive = lead_steps is None and env_lead is None
+        lead = [lead_steps if lead_steps is not None else int(env_lead or 4)]
+        est = {"prep": None, "step": None}
+
+        def adapt():
+            if adaptive and est["prep"] is not None and est["step"]:
+                lead[0] = max(1, min(16, math.ceil(1.5 * est["prep"] / est["step"])))
         eng = self.engine
         cuda = eng.device.type == "cuda"
         stream = torch.cuda.Stream() if cuda else None
@@ -247,6 +257,8 @@ class RAGPipeline:
                 gen_s = h.start_event.elapsed_time(h.done_event) / 1e3
             else:
                 latency, gen_s = t4 - t0, t4 - t3
+            est["step"] = gen_s / max(1, params.max_new_tokens)
+            adapt()
             st = stage_times(tm, t0, t1, t2, gen_s)
             self.last_times = st
             with tracing.span("rag.detokenise", n=len(outs)):
@@ -267,6 +279,12 @@ class RAGPipeline:
                 for i in range(len(batches)):
                     questions, I, prompts, reserved, tm, t0, t1, t2 = fut.result()
                     fut = None
+                    # preparation cost, not the wait for the gate: GPU embed + search time (side
+                    # stream events, complete once the host has the hits) + host prompt assembly
+                    evs = tm[0] if tm is not None else None
+                    est["prep"] = ((evs[0].elapsed_time(evs[2]) / 1e3 + (t2 - t1)) if evs is not None
+                                   else t2 - t0)
+                    adapt()
                     nxt = batches[i + 1] if i + 1 < len(batches) else None
 
                     def on_step(step, total, nxt=nxt):
@@ -274,7 +292,7 @@ class RAGPipeline:
                         if pending is not None and fin is None:
                             p, pending = pending, None
                             fin = col.submit(finish, p)
-                        if nxt is not None and fut is None and step >= max(1, total - lead_steps):
+                        if nxt is not None and fut is None and step >= max(1, total - lead[0]):
                             gate = None
                             if cuda:
                                 gate = torch.cuda.Event()
