@@ -173,7 +173,10 @@ def run_launch(a, mode: str) -> list[dict]:
                     if st != 200:
                         errors += 1
                     elif not body.get("answer"):
-                        empty += 1       # greedy random-init model: EOS as the first token
+                        # no text: EOS first (stop_on_eos), or -- with --ignore-eos, every answer
+                        # decoding max_new_tokens (engine counters below) -- a random-init model's
+                        # tokens that all detokenise to nothing (ids past the tokenizer's vocab)
+                        empty += 1
                     lat.append(time.perf_counter() - (t0 + at))
                     dones.append(time.perf_counter() - t0)
 
@@ -231,7 +234,13 @@ def run_launch(a, mode: str) -> list[dict]:
              "send_lag_ms_max": res["send_lag_ms_max"],
              "requests": a.requests, "max_new_tokens": a.max_new_tokens, "max_batch": a.max_batch,
              "ignore_eos": a.ignore_eos,
-             "gen_tokens_per_s": (round(a.requests * a.max_new_tokens / res["wall"], 1) if a.ignore_eos else None),
+             # measured by the engine: tokens emitted, and answers that stopped before
+             # max_new_tokens (0 with --ignore-eos: every answer decodes the full length)
+             "gen_tokens_per_s": (round(res["engine"].get("generated_tokens", 0) / res["wall"], 1)
+                                  if "generated_tokens" in res["engine"] else None),
+             "tokens_per_answer": (round(res["engine"]["generated_tokens"] / max(1, res["engine"].get("completed", 0)), 2)
+                                   if "generated_tokens" in res["engine"] else None),
+             "answers_short_of_max_new_tokens": res["engine"].get("completed_short"),
              "gpus": a.gpus, "tp": a.tp, "llm": "tiny" if a.tiny else a.llm, "notes": a.notes,
              "questions": a.questions, "dtype": "bf16" if a.device != "cpu" else "fp32",
              "data": "synthetic questions and notes, random-init weights", "wall_s": round(res["wall"], 2),

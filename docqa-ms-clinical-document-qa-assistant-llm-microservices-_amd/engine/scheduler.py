@@ -132,6 +132,9 @@ class ContinuousEngine:
         self.reserve_ahead = int(os.environ.get("DOCQA_RESERVE_AHEAD", str(engine.block_size)))
         self.preempted = 0
         self.kv_blocked = 0       # admissions deferred because the KV pool was out of blocks
+        self.generated = 0        # tokens emitted to requests
+        self.completed = 0        # requests finished
+        self.completed_short = 0  # ... of them before max_new_tokens (EOS)
 
     # ------------------------------------------------------------------ client side
     def submit(self, prompt: list[int], params: SamplingParams | None = None, on_token=None) -> cf.Future:
@@ -597,6 +600,7 @@ class ContinuousEngine:
 
     def _emit(self, r: Request, tok: int) -> None:
         r.out.append(int(tok))
+        self.generated += 1
         if r.on_token is not None:
             try:
                 r.on_token(r.rid, int(tok))
@@ -609,6 +613,8 @@ class ContinuousEngine:
         return r.params.stop_on_eos and r.out[-1] == self.eng.cfg.eos_token_id
 
     def _retire(self, r: Request) -> None:
+        self.completed += 1
+        self.completed_short += len(r.out) < r.params.max_new_tokens
         self.eng.kv.allocator.free(r.blocks)
         r.blocks = []
         if not r.future.done():

@@ -243,6 +243,9 @@ class ContinuousBatcher:
             m.set("engine_steps", eng.steps)
             m.set("engine_preemptions", eng.preempted)
             m.set("engine_kv_admission_blocked", eng.kv_blocked)
+            m.set("engine_generated_tokens", eng.generated)
+            m.set("engine_completed", eng.completed)
+            m.set("engine_completed_short", eng.completed_short)
             if wd:
                 wd.beat()
         if wd:
