@@ -433,7 +433,7 @@ at::Tensor paged_decode_cascade_split(const at::Tensor& q, at::Tensor k_cache, a
                                       const at::Tensor& block_tables, const at::Tensor& context_lens,
                                       int64_t Hq, double scale, const at::Tensor& prefix_table,
                                       const at::Tensor& prefix_len, int64_t nchunk, const at::Tensor& plan,
-                                      bool defer) {
+                                      bool defer, const c10::optional<at::Tensor>& tick) {
   CHECK_GPU(q); CHECK_BF16(q); CHECK_BF16(k_cache); CHECK_BF16(v_cache);
   CHECK_I32(block_tables); CHECK_I32(context_lens); CHECK_CONTIG(block_tables);
   CHECK_I32(prefix_table); CHECK_I32(prefix_len); CHECK_CONTIG(prefix_table);
@@ -456,6 +456,12 @@ at::Tensor paged_decode_cascade_split(const at::Tensor& q, at::Tensor k_cache, a
   auto ws_acc = at::empty({cap, Hkv, 16, D}, f32);
   auto ws_ml = at::empty({cap, Hkv, 16, 2}, f32);
   const int* pp = plan.data_ptr<int>();
+  int* tick_ptr = nullptr;   // split groups merged by their last item (zeroed int32 [cap * Hkv])
+  if (tick && tick->defined()) {
+    CHECK_GPU((*tick)); CHECK_I32((*tick));
+    TORCH_CHECK(tick->numel() >= (int64_t)cap * Hkv, "split decode: tick needs cap * Hkv entries");
+    tick_ptr = tick->data_ptr<int>();
+  }
   if (plan.size(0) == 3) {
     CHECK_RC(docqa_paged_decode_cascade_persist(q.data_ptr(), q.stride(0), k_cache.data_ptr(), v_cache.data_ptr(),
                                                 block_tables.data_ptr<int>(), block_tables.size(1),
@@ -473,7 +479,7 @@ at::Tensor paged_decode_cascade_split(const at::Tensor& q, at::Tensor k_cache, a
                                             BS, (float)scale, prefix_table.data_ptr<int>(),
                                             prefix_len.data_ptr<int>(), (int)nchunk, pacc.data_ptr<float>(),
                                             pml.data_ptr<float>(), pp, pp + 8 * cap, cap, ws_acc.data_ptr<float>(),
-                                            ws_ml.data_ptr<float>(), defer ? 1 : 0, stream()),
+                                            ws_ml.data_ptr<float>(), defer ? 1 : 0, stream(), tick_ptr),
            "paged_decode_cascade_split");
   return out;
 }
@@ -1278,7 +1284,7 @@ TORCH_LIBRARY(docqa, m) {
   m.def("kv_copy_rows(Tensor caches, Tensor tab, int num_blocks, int Hkv, int BS, int D) -> ()");
   m.def("paged_decode_cascade_split(Tensor q, Tensor k_cache, Tensor v_cache, Tensor block_tables, "
         "Tensor context_lens, int Hq, float scale, Tensor prefix_table, Tensor prefix_len, int nchunk, "
-        "Tensor plan, bool defer=False) -> Tensor");
+        "Tensor plan, bool defer=False, Tensor(t!)? tick=None) -> Tensor");
   m.def("paged_decode_cascade_rope(Tensor(a!) qkv, Tensor positions, Tensor cos_sin, Tensor slot_mapping, "
         "Tensor(b!) k_cache, Tensor(c!) v_cache, Tensor block_tables, Tensor context_lens, int Hq, "
         "int max_context, float scale, Tensor prefix_table, Tensor prefix_len, int nchunk, "

@@ -28,6 +28,7 @@
 #include "docqa_common.h"
 #include "docqa_asm.h"
 #include "docqa_cascade.h"
+#include "docqa_norm_row.h"
 #include <float.h>
 #include <stdlib.h>
 
@@ -84,6 +85,32 @@ static bool mfma_decode_on(int G) {
   return v == 1 || (v < 0 && G >= 8);
 }
 constexpr float kLog2e = 1.4426950408889634f;
+
+// write-through (agent-scope relaxed = global_store ... sc1) stores and agent-scope loads of
+// partials that a last-arriving workgroup of the same launch merges
+__device__ __forceinline__ void store4_coh(float* p, const f32x4& v) {
+  unsigned long long* q = reinterpret_cast<unsigned long long*>(p);
+  __hip_atomic_store(q, (unsigned long long)__float_as_uint(v[0]) | ((unsigned long long)__float_as_uint(v[1]) << 32),
+                     __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __hip_atomic_store(q + 1, (unsigned long long)__float_as_uint(v[2]) | ((unsigned long long)__float_as_uint(v[3]) << 32),
+                     __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void store2_coh(float* p, float a, float b) {
+  __hip_atomic_store(reinterpret_cast<unsigned long long*>(p),
+                     (unsigned long long)__float_as_uint(a) | ((unsigned long long)__float_as_uint(b) << 32),
+                     __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ float4 load2_coh(const float* p) {
+  const unsigned long long v =
+      __hip_atomic_load(reinterpret_cast<const unsigned long long*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  return float4{__uint_as_float((unsigned)v), __uint_as_float((unsigned)(v >> 32)), 0.f, 0.f};
+}
+template <bool COH>
+__device__ __forceinline__ void group_merge_body(const int* __restrict__ mg, const float* __restrict__ ws_acc,
+                                                 const float* __restrict__ ws_ml,
+                                                 const int* __restrict__ context_lens, int B, int Hkv,
+                                                 uint16_t* __restrict__ out, int out_stride, const CascadeIn& ci,
+                                                 int kvh, int t);
 
 // Adaptive split: the grid has a fixed number of splits per (sequence, kv head) --
 // fixed so a HIP graph captured once serves every step -- and each sequence's context
@@ -967,7 +994,8 @@ __global__ __launch_bounds__(256) void paged_decode_group_kernel(
     const uint16_t* __restrict__ v_cache, const int* __restrict__ block_tables, int maxb,
     const int* __restrict__ context_lens, int B, int Hkv, float scale,
     uint16_t* __restrict__ out, int out_stride, const int* __restrict__ groups, CascadeIn ci,
-    float* __restrict__ ws_acc = nullptr, float* __restrict__ ws_ml = nullptr) {
+    float* __restrict__ ws_acc = nullptr, float* __restrict__ ws_ml = nullptr,
+    const int* __restrict__ merges = nullptr, int* __restrict__ tick = nullptr) {
   constexpr int G = 4, R = 4, D = 128, TT = 32, MAXT = kGroupMaxPos * 8;
   constexpr int TILE = TT * D;                   // elements of one K (or V) tile: 8 KB
   __shared__ __attribute__((aligned(16))) uint16_t ring[NSR * 2 * TILE];
@@ -1142,17 +1170,42 @@ __global__ __launch_bounds__(256) void paged_decode_group_kernel(
   wait_vmcnt<0>();                               // drain the clamped tail DMAs
 
   // ---- epilogue: lane holds O^T[dim 16 dt + 4 lg + r][column hl], dt = 2 wave + dd
-  if (crow < 0) return;
   if constexpr (SPLIT) {
     if (part >= 0) {   // one partial of a split group: (m, l) + un-normalised O^T
       const size_t cidx = ((size_t)part * Hkv + kvh) * 16 + hl;
+      if (crow >= 0) {
+        if (tick) {    // merged inside this launch: write-through (sc1) for the last arriver
 #pragma unroll
-      for (int dd = 0; dd < 2; ++dd)
-        *reinterpret_cast<f32x4*>(ws_acc + cidx * D + 16 * (2 * wave + dd) + 4 * lg) = acc[dd];
-      if (wave == 0 && lg == 0) *reinterpret_cast<float2*>(ws_ml + cidx * 2) = make_float2(m, l);
+          for (int dd = 0; dd < 2; ++dd) store4_coh(ws_acc + cidx * D + 16 * (2 * wave + dd) + 4 * lg, acc[dd]);
+          if (wave == 0 && lg == 0) store2_coh(ws_ml + cidx * 2, m, l);
+        } else {
+#pragma unroll
+          for (int dd = 0; dd < 2; ++dd)
+            *reinterpret_cast<f32x4*>(ws_acc + cidx * D + 16 * (2 * wave + dd) + 4 * lg) = acc[dd];
+          if (wave == 0 && lg == 0) *reinterpret_cast<float2*>(ws_ml + cidx * 2) = make_float2(m, l);
+        }
+      }
+      if (tick) {
+        // last-arriver merge (no group_split_merge launch): the item drawing the group's
+        // last ticket folds its partials and the cascade-prefix chunks, and re-arms it
+        __shared__ int s_last;
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        const int mi = gp[7];
+        if (tid == 0) {
+          int* t = tick + (size_t)mi * Hkv + kvh;
+          const int old = __hip_atomic_fetch_add(t, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          s_last = old == merges[8 * mi + 5] - 1;
+          if (s_last) __hip_atomic_store(t, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        __syncthreads();
+        if (s_last) group_merge_body<true>(merges + 8 * mi, ws_acc, ws_ml, context_lens, B, Hkv, out, out_stride, ci,
+                                           kvh, tid);
+      }
       return;
     }
   }
+  if (crow < 0) return;
   const int h = kvh * G + (hl & 3);
   uint16_t* op = out + (size_t)crow * out_stride + (size_t)h * D;
   if (cL <= P) {                                 // a padded decode slot: defined zeros
@@ -1223,18 +1276,17 @@ __global__ __launch_bounds__(256) void paged_decode_group_kernel(
 // Combines the partials of every split group (merges [cap, 8] = (4 row ids, first slot,
 // slots, 0, 0); slots 0: nothing to merge) with the cascade prefix partials of each column's
 // row, then normalises: thread = (column, 8 dims).
-__global__ __launch_bounds__(256) void group_split_merge_kernel(const int* __restrict__ merges,
-                                                                const float* __restrict__ ws_acc,
-                                                                const float* __restrict__ ws_ml,
-                                                                const int* __restrict__ context_lens, int B,
-                                                                int Hkv, uint16_t* __restrict__ out,
-                                                                int out_stride, CascadeIn ci) {
+// COH: the split partials were written in this launch (write-through) -- agent-scope loads
+template <bool COH>
+__device__ __forceinline__ void group_merge_body(const int* __restrict__ mg, const float* __restrict__ ws_acc,
+                                                 const float* __restrict__ ws_ml,
+                                                 const int* __restrict__ context_lens, int B, int Hkv,
+                                                 uint16_t* __restrict__ out, int out_stride, const CascadeIn& ci,
+                                                 int kvh, int t) {
   constexpr int D = 128;
-  const int kvh = blockIdx.x;
-  const int* mg = merges + 8 * blockIdx.y;
   const int first = mg[4], np = mg[5];
   if (np <= 0) return;
-  const int t = threadIdx.x, col = t >> 4, d0 = (t & 15) * 8;
+  const int col = t >> 4, d0 = (t & 15) * 8;
   const int row = mg[col >> 2];
   if (row < 0 || row >= B) return;
   const int Hq = Hkv * 4, h = kvh * 4 + (col & 3);
@@ -1263,6 +1315,13 @@ __global__ __launch_bounds__(256) void group_split_merge_kernel(const int* __res
         const size_t c2 = ((size_t)(first + s) * Hkv + kvh) * 16 + col;
         pml = ws_ml + c2 * 2;
         pa = ws_acc + c2 * D + d0;
+        if constexpr (COH) {
+          const float4 m4 = load2_coh(pml);
+          ml[j] = make_float2(m4.x, m4.y);
+          a0[j] = slab_load4<true>(pa);
+          a1[j] = slab_load4<true>(pa + 4);
+          continue;
+        }
       } else {
         const size_t r = ((size_t)(s - np) * B + row) * Hq + h;
         pml = ci.ml + r * 2;
@@ -1293,6 +1352,16 @@ __global__ __launch_bounds__(256) void group_split_merge_kernel(const int* __res
 #pragma unroll
   for (int e = 0; e < 8; ++e) num[e] *= inv;
   *reinterpret_cast<uint4*>(op) = pack8(num);
+}
+
+__global__ __launch_bounds__(256) void group_split_merge_kernel(const int* __restrict__ merges,
+                                                                const float* __restrict__ ws_acc,
+                                                                const float* __restrict__ ws_ml,
+                                                                const int* __restrict__ context_lens, int B,
+                                                                int Hkv, uint16_t* __restrict__ out,
+                                                                int out_stride, CascadeIn ci) {
+  group_merge_body<false>(merges + 8 * blockIdx.y, ws_acc, ws_ml, context_lens, B, Hkv, out, out_stride, ci,
+                          blockIdx.x, threadIdx.x);
 }
 
 // ---------------------------------------------------------------------------------------
@@ -1691,7 +1760,7 @@ int docqa_paged_decode_cascade_split(const void* q, int q_stride, void* k_cache,
                                      void* out, int out_stride, int B, int Hq, int Hkv, int BS,
                                      float scale, const int* prefix_table, const int* plen, int nchunk,
                                      float* pacc, float* pml, const int* items, const int* merges, int cap,
-                                     float* ws_acc, float* ws_ml, int defer, hipStream_t s) {
+                                     float* ws_acc, float* ws_ml, int defer, hipStream_t s, int* tick) {
   if (B == 0) return 0;
   if (BS != 64 || maxb > kGroupMaxPos || Hq != 4 * Hkv || nchunk < 1 || nchunk > kCascadeMaxChunks || cap < 1)
     return -1;
@@ -1717,15 +1786,20 @@ int docqa_paged_decode_cascade_split(const void* q, int q_stride, void* k_cache,
     const char* e = getenv("DOCQA_GROUP_NSR");
     return e && atoi(e) == 4 ? 4 : 3;
   }();
+  // tick (non-deferred plans: the prefix partials are complete before the group kernel):
+  // split groups merged by their last item, no merge launch (int32 [cap, Hkv] zeroed,
+  // items carry their merge row in column 7)
+  int* tk = (tick && !defer) ? tick : nullptr;
   if (nsr == 4)
     paged_decode_group_kernel<4, true><<<dim3(Hkv, cap), 256, 0, s>>>(
         (const uint16_t*)q, q_stride, (const uint16_t*)k_cache, (const uint16_t*)v_cache, block_tables, maxb,
-        context_lens, B, Hkv, scale, (uint16_t*)out, out_stride, items, ci, ws_acc, ws_ml);
+        context_lens, B, Hkv, scale, (uint16_t*)out, out_stride, items, ci, ws_acc, ws_ml, merges, tk);
   else
     paged_decode_group_kernel<3, true><<<dim3(Hkv, cap), 256, 0, s>>>(
         (const uint16_t*)q, q_stride, (const uint16_t*)k_cache, (const uint16_t*)v_cache, block_tables, maxb,
-        context_lens, B, Hkv, scale, (uint16_t*)out, out_stride, items, ci, ws_acc, ws_ml);
+        context_lens, B, Hkv, scale, (uint16_t*)out, out_stride, items, ci, ws_acc, ws_ml, merges, tk);
   DOCQA_CHECK_LAUNCH();
+  if (tk) return 0;
   if (ev_join && hipStreamWaitEvent(s, ev_join, 0) != hipSuccess) return -3;
   // merge rows: at most (cap + 1) / 2 (ops.split_decode_groups guarantees it), so half the
   // grid -- the empty workgroups of the unused merge rows are not free; deferred: one per group

@@ -170,6 +170,7 @@ def _identity_groups(bp: int, dev, hkv: int = 8) -> torch.Tensor:
             if all_partial:
                 g[0, i, 4] = 0
                 g[0, i, 6] = i
+                g[0, i, 7] = i          # merge row of the item (last-arriver merge)
                 g[1, i, :len(q)] = torch.tensor(q, dtype=torch.int32)
                 g[1, i, 4], g[1, i, 5] = i, 1
             else:

@@ -391,7 +391,8 @@ class LlamaModel:
                         a = ops.paged_decode_cascade_grouped(qkv, kc, vc, meta.block_tables, meta.context_lens,
                                                              hq, self.scale, meta.shared_table, meta.shared_len,
                                                              meta.cascade_chunks, meta.decode_groups,
-                                                             meta.decode_defer)
+                                                             meta.decode_defer,
+                                                             self._decode_tick(M) if x.is_cuda else None)
                     else:
                         a = ops.paged_decode_cascade(qkv, kc, vc, meta.block_tables, meta.context_lens, hq,
                                                      meta.max_context, self.scale, meta.shared_table,
@@ -403,7 +404,8 @@ class LlamaModel:
                         a = ops.paged_decode_cascade_grouped(qkv, kc, vc, meta.block_tables, meta.context_lens,
                                                              hq, self.scale, meta.shared_table, meta.shared_len,
                                                              meta.cascade_chunks, meta.decode_groups,
-                                                             meta.decode_defer)
+                                                             meta.decode_defer,
+                                                             self._decode_tick(M) if x.is_cuda else None)
                     else:
                         a = ops.paged_decode_cascade(qkv, kc, vc, meta.block_tables, meta.context_lens, hq,
                                                      meta.max_context, self.scale, meta.shared_table,

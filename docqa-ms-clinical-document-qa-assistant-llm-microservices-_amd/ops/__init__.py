@@ -673,7 +673,8 @@ def paged_decode_cascade(q, k_cache, v_cache, block_tables, context_lens, Hq, ma
 
 
 def paged_decode_cascade_grouped(q, k_cache, v_cache, block_tables, context_lens, Hq, scale,
-                                 prefix_table, prefix_len, nchunk: int, groups, defer: bool = False):
+                                 prefix_table, prefix_len, nchunk: int, groups, defer: bool = False,
+                                 tick=None):
     """Cascade decode with the suffix attention of rows that share prefix-cache KV blocks
     done together (csrc/kernels/attn_decode.hip paged_decode_group_kernel): ``groups``
     int32 [ngroups * 4] packs every row into one group of <= 4 (-1 = empty slot), and a
@@ -681,12 +682,14 @@ def paged_decode_cascade_grouped(q, k_cache, v_cache, block_tables, context_lens
     :func:`paged_decode_cascade` for any packing.  ``groups`` may also be a split plan
     int32 [2, cap, 8] from :func:`split_decode_groups` (long groups over several
     workgroups, partials merged by log-sum-exp); ``defer``: that plan was built with
-    ``split_decode_groups(defer=True)`` (the prefix kernel then runs on a side stream)."""
+    ``split_decode_groups(defer=True)`` (the prefix kernel then runs on a side stream).
+    ``tick``: zeroed int32 ticket words (>= cap x Hkv, :func:`decode_ticket`) -- a split
+    plan's groups are then merged by their last work item instead of a merge launch."""
     if _gpu(q):
         if groups.dim() == 3:
             return _native().paged_decode_cascade_split(q, k_cache, v_cache, block_tables, context_lens, Hq,
                                                         scale, prefix_table, prefix_len, nchunk, groups,
-                                                        defer and groups.shape[0] == 2)
+                                                        defer and groups.shape[0] == 2, tick)
         return _native().paged_decode_cascade_grouped(q, k_cache, v_cache, block_tables, context_lens, Hq,
                                                       scale, prefix_table, prefix_len, nchunk, groups)
     max_context = block_tables.shape[1] * k_cache.shape[2]
@@ -850,17 +853,19 @@ def split_decode_groups(quads: list[list[int]], tables: list[list[int]], lens: l
                 acc += t
             end = max((lens[r] + block_size - 1) // block_size for r in qd)
             cuts.append((start, max(end, start + 1), acc))
+            # an item of a merged group carries its merge row (column 7) for the
+            # last-arriver merge inside the group kernel
             if all_partial:
                 merges.append(rows4 + [nslot, len(cuts), 0, 0])
                 for lo, hi, t in cuts:
-                    items.append((t, rows4 + [lo, hi, nslot, 0]))
+                    items.append((t, rows4 + [lo, hi, nslot, len(merges) - 1]))
                     nslot += 1
             elif len(cuts) == 1:
                 items.append((cuts[0][2], rows4 + [skip, 1 << 20, -1, 0]))
             else:
                 merges.append(rows4 + [nslot, len(cuts), 0, 0])
                 for lo, hi, t in cuts:
-                    items.append((t, rows4 + [lo, hi, nslot, 0]))
+                    items.append((t, rows4 + [lo, hi, nslot, len(merges) - 1]))
                     nslot += 1
         fits = len(items) <= cap and len(merges) <= (cap if all_partial else (cap + 1) // 2)
         if fits and bins:
