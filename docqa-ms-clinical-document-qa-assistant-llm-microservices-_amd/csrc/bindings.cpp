@@ -1072,6 +1072,19 @@ std::tuple<at::Tensor, at::Tensor> knn(const at::Tensor& xb, const at::Tensor& x
 
 // IVF coarse quantizer, wide probes: int64 [nq, nprobe] nearest centroids (ascending, ties
 // to the lower id) for nprobe <= 512
+// exact fp32 x @ w^T on the coarse quantizer's MFMA tiles (the IVF-PQ query pre-rotation)
+at::Tensor fp32_gemm_nt(const at::Tensor& x, const at::Tensor& w) {
+  CHECK_GPU(x); CHECK_GPU(w); CHECK_CONTIG(x); CHECK_CONTIG(w);
+  TORCH_CHECK(x.scalar_type() == at::kFloat && w.scalar_type() == at::kFloat && x.dim() == 2 && w.dim() == 2 &&
+              x.size(1) == w.size(1), "fp32_gemm_nt: fp32 [M, K] x [N, K]");
+  TORCH_CHECK(x.size(1) % 8 == 0 && (size_t)32 * x.size(1) * 4 <= 160 * 1024, "fp32_gemm_nt: K % 8 == 0, K <= 1280");
+  c10::DeviceGuard g(x.device());
+  auto out = at::empty({x.size(0), w.size(0)}, x.options());
+  CHECK_RC(docqa_fp32_gemm_nt(x.data_ptr<float>(), x.size(0), x.size(1), w.data_ptr<float>(), w.size(0),
+                              out.data_ptr<float>(), stream()), "fp32_gemm_nt");
+  return out;
+}
+
 at::Tensor coarse_probes(const at::Tensor& xq, const at::Tensor& cent, const at::Tensor& cnorm, int64_t nprobe) {
   CHECK_GPU(xq); CHECK_GPU(cent); CHECK_GPU(cnorm);
   CHECK_CONTIG(xq); CHECK_CONTIG(cent); CHECK_CONTIG(cnorm);
@@ -1241,6 +1254,7 @@ TORCH_LIBRARY(docqa, m) {
         "-> (Tensor, Tensor)");
   m.def("pool_l2(Tensor h, Tensor cu_seqlens, bool mean, bool normalize) -> Tensor");
   m.def("coarse_probes(Tensor xq, Tensor cent, Tensor cnorm, int nprobe) -> Tensor");
+  m.def("fp32_gemm_nt(Tensor x, Tensor w) -> Tensor");
   m.def("ivfpq_search(Tensor xq, Tensor centroids, Tensor pq, Tensor codes, Tensor ids, "
         "Tensor list_off, Tensor probes, int k) -> (Tensor, Tensor)");
   m.def("pq_encode(Tensor x, Tensor centroids, Tensor assign, Tensor pq) -> Tensor");
@@ -1344,6 +1358,7 @@ TORCH_LIBRARY_IMPL(docqa, CUDA, m) {
   m.impl("mgemm_argmax_val", &mgemm_argmax_val);
   m.impl("wgemm", &wgemm);
   m.impl("coarse_probes", &coarse_probes);
+  m.impl("fp32_gemm_nt", &fp32_gemm_nt);
   m.impl("wgemm_glu", &wgemm_glu);
   m.impl("wgemm_argmax_val", &wgemm_argmax_val);
   m.impl("dgemm_argmax_val", &dgemm_argmax_val);

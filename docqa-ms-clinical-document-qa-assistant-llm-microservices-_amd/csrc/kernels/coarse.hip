@@ -61,7 +61,8 @@ __global__ __launch_bounds__(256) void coarse_dist_kernel(const float* __restric
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const int row = tile + (r & 3) + 8 * (r >> 2) + 4 * hh;
-        if (row < row_end) D[(size_t)q * nlist + row] = cnorm[row] - 2.f * acc[r];
+        // cnorm null: the plain product (fp32 x @ W^T -- the PQ pre-rotation)
+        if (row < row_end) D[(size_t)q * nlist + row] = cnorm ? cnorm[row] - 2.f * acc[r] : acc[r];
       }
     }
   }
@@ -154,6 +155,23 @@ __global__ __launch_bounds__(256) void coarse_select_kernel(const float* __restr
 }
 
 }  // namespace
+
+// out[nq, n] = x[nq, d] @ w[n, d]^T in exact fp32 on the same MFMA tiles (d % 8 == 0): the
+// IVF-PQ query pre-rotation x @ R with w = R^T, so the search path runs no library GEMM.
+int docqa_fp32_gemm_nt(const float* x, int nq, int d, const float* w, int n, float* out, hipStream_t s) {
+  if (nq == 0) return 0;
+  if (d % 8 != 0 || n <= 0 || !docqa_aligned16(x) || !docqa_aligned16(w)) return -1;
+  const size_t lds = (size_t)32 * d * 4;
+  if (lds > 160 * 1024) return -2;
+  int nblk = (n + 511) / 512;
+  if (nblk > 256) nblk = 256;
+  int rpb = (n + nblk - 1) / nblk;
+  rpb = (rpb + 127) / 128 * 128;
+  nblk = (n + rpb - 1) / rpb;
+  coarse_dist_kernel<<<dim3(nblk, (nq + 31) / 32), 256, lds, s>>>(w, nullptr, n, d, x, nq, rpb, out);
+  DOCQA_CHECK_LAUNCH();
+  return 0;
+}
 
 // Workspace: fp32 [nq, nlist].  cent fp32 [nlist, d] (d % 8 == 0), cnorm fp32 [nlist],
 // xq fp32 [nq, d] -> probes int64 [nq, nprobe] ascending by distance (ties: lower id).

@@ -77,7 +77,13 @@ class IVFPQIndex:
     def _in(self, x) -> torch.Tensor:
         """Vectors into the index's (rotated) space."""
         x = torch.as_tensor(x).to(self.device, torch.float32)
-        return x @ self.rot if self.rot is not None else x
+        if self.rot is None:
+            return x
+        # x @ R as x @ (R^T)^T on the fp32 MFMA tiles of coarse.hip (no library GEMM on the
+        # search path); R^T cached per rotation tensor
+        if getattr(self, "_rot_src", None) is not self.rot:
+            self._rot_t, self._rot_src = self.rot.t().contiguous(), self.rot
+        return ops.fp32_matmul_nt(x, self._rot_t)
 
     def train(self, x, niter: int = 20, seed: int = 0) -> None:
         x = torch.as_tensor(x).to(self.device, torch.float32)

@@ -931,6 +931,14 @@ def knn(xb, xb_norms, xq, k: int, inner_product: bool = False, id_offset: int = 
     return ref.knn(xb, xb_norms, xq, k, inner_product, id_offset)
 
 
+def fp32_matmul_nt(x, w):
+    """Exact fp32 ``x @ w.T`` on the coarse quantizer's MFMA tiles (coarse.hip) -- the IVF-PQ
+    query pre-rotation on the GPU without a library GEMM; torch on the CPU."""
+    if _gpu(x) and x.shape[1] % 8 == 0 and x.shape[1] <= 1280:
+        return _native().fp32_gemm_nt(x.float().contiguous(), w.float().contiguous())
+    return x.float() @ w.float().t()
+
+
 def coarse_probes(xq, centroids, cnorm, nprobe: int):
     """IVF coarse quantizer: int64 [nq, nprobe] nearest centroids by squared L2, ascending,
     ties to the lower centroid id.  GPU: csrc/kernels/coarse.hip (MFMA fp32 distances +

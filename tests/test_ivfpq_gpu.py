@@ -125,3 +125,18 @@ def test_ivfpq_wide_probe_search_has_no_library_path(monkeypatch):
     monkeypatch.setattr(torch, "topk", boom)
     D, I = idx.search(q, 10, nprobe=128)
     assert (I[:, 0].cpu() == torch.arange(50)).float().mean() > 0.9
+
+
+@pytest.mark.parametrize("nq,d,n", [(1, 768, 768), (256, 768, 768), (37, 96, 200), (300, 1280, 64)])
+def test_fp32_gemm_nt_matches_fp32(nq, d, n):
+    """The IVF-PQ query pre-rotation on the coarse quantizer's fp32 MFMA tiles == the fp32
+    matmul (exact fp32 products, a different summation order)."""
+    from docqa_amd import ops
+
+    assert ops.load_native()
+    x = torch.randn(nq, d, device="cuda")
+    w = torch.randn(n, d, device="cuda")
+    got = ops.fp32_matmul_nt(x, w)
+    ref = (x.double() @ w.double().t()).float()
+    assert got.shape == ref.shape
+    assert (got - ref).abs().max().item() <= 1e-4 * ref.abs().max().item()
