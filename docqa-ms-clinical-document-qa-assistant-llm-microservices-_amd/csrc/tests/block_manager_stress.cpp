@@ -102,6 +102,19 @@ int main(int argc, char** argv) {
     return 1;
   } catch (const std::runtime_error&) {
   }
+  // exhaustion, deterministically (the threaded phase hits it only when threads overlap):
+  // a request for more than the pool throws and leaves every block where it was
+  try {
+    auto all = bm.alloc(NB + 1);
+    fprintf(stderr, "allocation past the pool not refused\n");
+    return 1;
+  } catch (const std::runtime_error&) {
+  }
+  auto st2 = bm.stats();
+  if (st2[0] + st2[1] != NB) {
+    fprintf(stderr, "refused allocation leaked blocks\n");
+    return 1;
+  }
   puts("OK");
   return 0;
 }
