@@ -433,7 +433,7 @@ at::Tensor paged_decode_cascade_split(const at::Tensor& q, at::Tensor k_cache, a
                                       const at::Tensor& block_tables, const at::Tensor& context_lens,
                                       int64_t Hq, double scale, const at::Tensor& prefix_table,
                                       const at::Tensor& prefix_len, int64_t nchunk, const at::Tensor& plan,
-                                      bool defer, const c10::optional<at::Tensor>& tick) {
+                                      bool defer, const c10::optional<at::Tensor>& tick, bool inline_prefix) {
   CHECK_GPU(q); CHECK_BF16(q); CHECK_BF16(k_cache); CHECK_BF16(v_cache);
   CHECK_I32(block_tables); CHECK_I32(context_lens); CHECK_CONTIG(block_tables);
   CHECK_I32(prefix_table); CHECK_I32(prefix_len); CHECK_CONTIG(prefix_table);
@@ -479,7 +479,8 @@ at::Tensor paged_decode_cascade_split(const at::Tensor& q, at::Tensor k_cache, a
                                             BS, (float)scale, prefix_table.data_ptr<int>(),
                                             prefix_len.data_ptr<int>(), (int)nchunk, pacc.data_ptr<float>(),
                                             pml.data_ptr<float>(), pp, pp + 8 * cap, cap, ws_acc.data_ptr<float>(),
-                                            ws_ml.data_ptr<float>(), defer ? 1 : 0, stream(), tick_ptr),
+                                            ws_ml.data_ptr<float>(), defer ? 1 : 0, stream(), tick_ptr,
+                                            inline_prefix ? 1 : 0),
            "paged_decode_cascade_split");
   return out;
 }
@@ -1298,7 +1299,7 @@ TORCH_LIBRARY(docqa, m) {
   m.def("kv_copy_rows(Tensor caches, Tensor tab, int num_blocks, int Hkv, int BS, int D) -> ()");
   m.def("paged_decode_cascade_split(Tensor q, Tensor k_cache, Tensor v_cache, Tensor block_tables, "
         "Tensor context_lens, int Hq, float scale, Tensor prefix_table, Tensor prefix_len, int nchunk, "
-        "Tensor plan, bool defer=False, Tensor(t!)? tick=None) -> Tensor");
+        "Tensor plan, bool defer=False, Tensor(t!)? tick=None, bool inline_prefix=False) -> Tensor");
   m.def("paged_decode_cascade_rope(Tensor(a!) qkv, Tensor positions, Tensor cos_sin, Tensor slot_mapping, "
         "Tensor(b!) k_cache, Tensor(c!) v_cache, Tensor block_tables, Tensor context_lens, int Hq, "
         "int max_context, float scale, Tensor prefix_table, Tensor prefix_len, int nchunk, "

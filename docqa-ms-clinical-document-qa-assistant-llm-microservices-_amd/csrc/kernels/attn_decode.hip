@@ -1760,16 +1760,14 @@ int docqa_paged_decode_cascade_split(const void* q, int q_stride, void* k_cache,
                                      void* out, int out_stride, int B, int Hq, int Hkv, int BS,
                                      float scale, const int* prefix_table, const int* plen, int nchunk,
                                      float* pacc, float* pml, const int* items, const int* merges, int cap,
-                                     float* ws_acc, float* ws_ml, int defer, hipStream_t s, int* tick) {
+                                     float* ws_acc, float* ws_ml, int defer, hipStream_t s, int* tick,
+                                     int inline_prefix) {
   if (B == 0) return 0;
   if (BS != 64 || maxb > kGroupMaxPos || Hq != 4 * Hkv || nchunk < 1 || nchunk > kCascadeMaxChunks || cap < 1)
     return -1;
-  // DOCQA_GROUP_INLINE_PREFIX=1: no prefix kernel -- the plan's items start at block 0, so
-  // every group streams the shared template blocks itself (L2 hits after the first group)
-  static const bool inline_prefix = [] {
-    const char* e = getenv("DOCQA_GROUP_INLINE_PREFIX");
-    return e && atoi(e) == 1;
-  }();
+  // inline_prefix: no prefix kernel -- the plan's items start at block 0 (built with skip 0),
+  // so every group streams the shared template blocks itself (L2 hits after the first group)
+  if (inline_prefix && defer) return -1;
   // defer (a plan from ops.split_decode_groups(defer=True)): every item writes a partial
   // and every group has a merge row, so no item reads the prefix partials and the prefix
   // kernel is forked onto a side stream beside the group kernel

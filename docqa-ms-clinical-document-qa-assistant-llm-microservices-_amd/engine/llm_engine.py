@@ -143,6 +143,13 @@ def _persist_groups_on() -> bool:
     return _split_groups_on() and os.environ.get("DOCQA_GROUP_PERSIST", "0") == "1"
 
 
+def _inline_prefix_on() -> bool:
+    """Split plans whose items start at block 0: every group attends the shared cascade prefix
+    itself (L2 hits after the first group) instead of a separate prefix kernel + merge --
+    decode 1113-1116 vs 1140-1150 ms per 256-question batch (profiles/r4_inline_prefix_ab.log)."""
+    return _split_groups_on() and os.environ.get("DOCQA_GROUP_INLINE_PREFIX", "1") == "1"
+
+
 def _defer_groups_on() -> bool:
     """Split plan with every group merged by the merge kernel (ops.split_decode_groups
     defer=True): the cascade-prefix kernel then runs on a side stream beside the group
@@ -409,6 +416,8 @@ class LLMEngine:
             if self.group_decode and ops.grouped_decode_ok(self.kv.caches[0][0], g.block_tables, self.model.hq):
                 meta.decode_groups = g.groups
                 meta.decode_defer = g.groups.dim() == 3 and _defer_groups_on()
+                meta.decode_inline = (g.groups.dim() == 3 and g.groups.shape[0] == 2 and _inline_prefix_on()
+                                      and not _defer_groups_on())
         if g.greedy:
             # greedy: the LM head's argmax is fused into its GEMM (no [B, vocab] logits)
             nxt = self.model.forward(g.tokens, meta, self.kv.caches, greedy_ids=True)
@@ -456,7 +465,7 @@ class LLMEngine:
         if g.groups.dim() == 3:   # split plan: long groups over several workgroups
             cap = g.groups.shape[1]
             quads = ops.pack_decode_groups(tables, lens, skip, self.block_size, (g.bp + 1) // 2)
-            if os.environ.get("DOCQA_GROUP_INLINE_PREFIX", "0") == "1":
+            if _inline_prefix_on() and not _defer_groups_on() and g.groups.shape[0] == 2:
                 skip = 0   # the kernel attends the shared prefix inside each group
             plan = ops.split_decode_groups(quads, tables, lens, skip, self.block_size, cap,
                                            int(os.environ.get("DOCQA_GROUP_TILES", "12")),

@@ -132,6 +132,8 @@ class AttnMeta:
     decode_groups: torch.Tensor | None = None
     # decode_groups is a deferred split plan (ops.split_decode_groups(defer=True))
     decode_defer: bool = False
+    # ... a split plan whose items start at block 0 (the groups attend the shared prefix)
+    decode_inline: bool = False
 
 
 class LlamaModel:
@@ -392,7 +394,8 @@ class LlamaModel:
                                                              hq, self.scale, meta.shared_table, meta.shared_len,
                                                              meta.cascade_chunks, meta.decode_groups,
                                                              meta.decode_defer,
-                                                             self._decode_tick(M) if x.is_cuda else None)
+                                                             self._decode_tick(M) if x.is_cuda else None,
+                                                             meta.decode_inline)
                     else:
                         a = ops.paged_decode_cascade(qkv, kc, vc, meta.block_tables, meta.context_lens, hq,
                                                      meta.max_context, self.scale, meta.shared_table,
@@ -405,7 +408,8 @@ class LlamaModel:
                                                              hq, self.scale, meta.shared_table, meta.shared_len,
                                                              meta.cascade_chunks, meta.decode_groups,
                                                              meta.decode_defer,
-                                                             self._decode_tick(M) if x.is_cuda else None)
+                                                             self._decode_tick(M) if x.is_cuda else None,
+                                                             meta.decode_inline)
                     else:
                         a = ops.paged_decode_cascade(qkv, kc, vc, meta.block_tables, meta.context_lens, hq,
                                                      meta.max_context, self.scale, meta.shared_table,

@@ -674,7 +674,7 @@ def paged_decode_cascade(q, k_cache, v_cache, block_tables, context_lens, Hq, ma
 
 def paged_decode_cascade_grouped(q, k_cache, v_cache, block_tables, context_lens, Hq, scale,
                                  prefix_table, prefix_len, nchunk: int, groups, defer: bool = False,
-                                 tick=None):
+                                 tick=None, inline_prefix: bool = False):
     """Cascade decode with the suffix attention of rows that share prefix-cache KV blocks
     done together (csrc/kernels/attn_decode.hip paged_decode_group_kernel): ``groups``
     int32 [ngroups * 4] packs every row into one group of <= 4 (-1 = empty slot), and a
@@ -684,12 +684,15 @@ def paged_decode_cascade_grouped(q, k_cache, v_cache, block_tables, context_lens
     workgroups, partials merged by log-sum-exp); ``defer``: that plan was built with
     ``split_decode_groups(defer=True)`` (the prefix kernel then runs on a side stream).
     ``tick``: zeroed int32 ticket words (>= cap x Hkv, :func:`decode_ticket`) -- a split
-    plan's groups are then merged by their last work item instead of a merge launch."""
+    plan's groups are then merged by their last work item instead of a merge launch.
+    ``inline_prefix``: the split plan's items start at block 0 (built with skip 0), so the
+    groups attend the shared prefix themselves -- no prefix kernel."""
     if _gpu(q):
         if groups.dim() == 3:
             return _native().paged_decode_cascade_split(q, k_cache, v_cache, block_tables, context_lens, Hq,
                                                         scale, prefix_table, prefix_len, nchunk, groups,
-                                                        defer and groups.shape[0] == 2, tick)
+                                                        defer and groups.shape[0] == 2, tick,
+                                                        bool(inline_prefix) and groups.shape[0] == 2)
         return _native().paged_decode_cascade_grouped(q, k_cache, v_cache, block_tables, context_lens, Hq,
                                                       scale, prefix_table, prefix_len, nchunk, groups)
     max_context = block_tables.shape[1] * k_cache.shape[2]

@@ -20,6 +20,10 @@ from dataclasses import dataclass, field
 
 import torch
 
+# safety factor of the adaptive pipeline lead (answer_pipelined): preparation cost x this,
+# over the decode step time
+_LEAD_MARGIN = float(os.environ.get("DOCQA_PIPELINE_LEAD_MARGIN", "1.5"))
+
 from ..utils import tracing
 from ..engine.llm_engine import LLMEngine, SamplingParams
 from ..prompts import REFERENCE_QA_TEMPLATE, qa_template
@@ -234,7 +238,7 @@ class RAGPipeline:
 
         def adapt():
             if adaptive and est["prep"] is not None and est["step"]:
-                lead[0] = max(1, min(16, math.ceil(1.5 * est["prep"] / est["step"])))
+                lead[0] = max(1, min(16, math.ceil(_LEAD_MARGIN * est["prep"] / est["step"])))
         eng = self.engine
         cuda = eng.device.type == "cuda"
         stream = torch.cuda.Stream() if cuda else None

@@ -132,6 +132,14 @@ def test_split_grouped_cascade_matches_per_row(native, B, Hkv, seed, tiles, defe
     err32 = (out.float() - ref32.float()).abs().max().item()
     assert err32 < 3e-2, err32
     if not defer:
+        # inline prefix: items from block 0 (plan built with skip 0), the groups attend the
+        # shared prefix themselves -- no prefix kernel -- same attention
+        quads0 = native.pack_decode_groups(tables, end_lens, Pb, BS, (B + 1) // 2)
+        plan0 = native.split_decode_groups(quads0, tables, end_lens, 0, BS, max(B, 4), tiles)
+        o0 = native.paged_decode_cascade_grouped(q, kc, vc, bt, cl, Hq, scale, pt, plen, 4, plan0.cuda(), False,
+                                                 None, True)
+        err0 = (o0.float() - ref32.float()).abs().max().item()
+        assert err0 < 3e-2, err0
         # split groups merged by their last item (ticket words, no merge launch) == the
         # merge kernel, with the tickets re-armed after every launch
         tick = torch.zeros(plan.shape[1] * Hkv, dtype=torch.int32, device="cuda")
