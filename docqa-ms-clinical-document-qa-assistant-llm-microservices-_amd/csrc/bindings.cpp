@@ -429,6 +429,50 @@ at::Tensor paged_decode_cascade_grouped(const at::Tensor& q, at::Tensor k_cache,
 // grouped cascade decode with long groups split over several workgroups: plan [2, cap, 8]
 // int32 = work items (4 row ids, first / end block position, partial slot or -1, 0) and
 // merges (4 row ids, first slot, slots, 0, 0) -- ops.split_decode_groups
+// grouped decode straight from the QKV projection's split-K slabs P [S, B, (Hq + 2 Hkv) 128]:
+// RoPE + the new token's cache write inside the group kernel (split plan from block 0)
+at::Tensor paged_decode_grouped_fused(const at::Tensor& P, const at::Tensor& positions, const at::Tensor& cos_sin,
+                                      const at::Tensor& slot_mapping, at::Tensor k_cache, at::Tensor v_cache,
+                                      const at::Tensor& block_tables, const at::Tensor& context_lens, int64_t Hq,
+                                      double scale, const at::Tensor& prefix_table, const at::Tensor& prefix_len,
+                                      int64_t nchunk, const at::Tensor& plan, const c10::optional<at::Tensor>& tick) {
+  CHECK_GPU(P); CHECK_CONTIG(P); CHECK_BF16(k_cache); CHECK_BF16(v_cache);
+  CHECK_I32(positions); CHECK_I32(slot_mapping); CHECK_I32(block_tables); CHECK_I32(context_lens);
+  CHECK_CONTIG(block_tables); CHECK_I32(prefix_table); CHECK_I32(prefix_len); CHECK_I32(plan); CHECK_CONTIG(plan);
+  TORCH_CHECK(P.scalar_type() == at::kFloat && P.dim() == 3, "fused grouped decode: slabs fp32 [S, B, width]");
+  TORCH_CHECK(cos_sin.scalar_type() == at::kFloat, "cos_sin must be fp32");
+  const int B = P.size(1);
+  const int Hkv = k_cache.size(1), BS = k_cache.size(2), D = k_cache.size(3);
+  TORCH_CHECK(D == 128 && BS == 64 && Hq == 4 * Hkv && P.size(2) == (Hq + 2 * Hkv) * D,
+              "fused grouped decode: head_dim 128, 64-token blocks, GQA 4, packed QKV width");
+  TORCH_CHECK(block_tables.size(1) <= 64 && context_lens.numel() == B && block_tables.size(0) >= B &&
+              positions.numel() >= B && slot_mapping.numel() >= B, "fused grouped decode: B rows, <= 64 blocks");
+  TORCH_CHECK(plan.dim() == 3 && plan.size(0) == 2 && plan.size(2) == 8, "fused grouped decode: split plan [2, cap, 8]");
+  const int cap = plan.size(1);
+  c10::DeviceGuard g(P.device());
+  auto out = at::empty({B, Hq * D}, P.options().dtype(at::kBFloat16));
+  auto f32 = P.options();
+  auto ws_acc = at::empty({cap, Hkv, 16, D}, f32);
+  auto ws_ml = at::empty({cap, Hkv, 16, 2}, f32);
+  int* tick_ptr = nullptr;
+  if (tick && tick->defined()) {
+    CHECK_GPU((*tick)); CHECK_I32((*tick));
+    TORCH_CHECK(tick->numel() >= (int64_t)cap * Hkv, "fused grouped decode: tick needs cap * Hkv entries");
+    tick_ptr = tick->data_ptr<int>();
+  }
+  const int* pp = plan.data_ptr<int>();
+  CHECK_RC(docqa_paged_decode_cascade_split(nullptr, 0, k_cache.data_ptr(), v_cache.data_ptr(),
+                                            block_tables.data_ptr<int>(), block_tables.size(1),
+                                            context_lens.data_ptr<int>(), out.data_ptr(), Hq * D, B, Hq, Hkv, BS,
+                                            (float)scale, prefix_table.data_ptr<int>(), prefix_len.data_ptr<int>(),
+                                            (int)nchunk, nullptr, nullptr, pp, pp + 8 * cap, cap,
+                                            ws_acc.data_ptr<float>(), ws_ml.data_ptr<float>(), 0, stream(), tick_ptr, 1,
+                                            P.data_ptr<float>(), P.size(0), positions.data_ptr<int>(),
+                                            cos_sin.data_ptr<float>(), slot_mapping.data_ptr<int>()),
+           "paged_decode_grouped_fused");
+  return out;
+}
+
 at::Tensor paged_decode_cascade_split(const at::Tensor& q, at::Tensor k_cache, at::Tensor v_cache,
                                       const at::Tensor& block_tables, const at::Tensor& context_lens,
                                       int64_t Hq, double scale, const at::Tensor& prefix_table,
@@ -1300,6 +1344,9 @@ TORCH_LIBRARY(docqa, m) {
   m.def("paged_decode_cascade_split(Tensor q, Tensor k_cache, Tensor v_cache, Tensor block_tables, "
         "Tensor context_lens, int Hq, float scale, Tensor prefix_table, Tensor prefix_len, int nchunk, "
         "Tensor plan, bool defer=False, Tensor(t!)? tick=None, bool inline_prefix=False) -> Tensor");
+  m.def("paged_decode_grouped_fused(Tensor P, Tensor positions, Tensor cos_sin, Tensor slot_mapping, "
+        "Tensor(a!) k_cache, Tensor(b!) v_cache, Tensor block_tables, Tensor context_lens, int Hq, float scale, "
+        "Tensor prefix_table, Tensor prefix_len, int nchunk, Tensor plan, Tensor(t!)? tick=None) -> Tensor");
   m.def("paged_decode_cascade_rope(Tensor(a!) qkv, Tensor positions, Tensor cos_sin, Tensor slot_mapping, "
         "Tensor(b!) k_cache, Tensor(c!) v_cache, Tensor block_tables, Tensor context_lens, int Hq, "
         "int max_context, float scale, Tensor prefix_table, Tensor prefix_len, int nchunk, "
@@ -1368,6 +1415,7 @@ TORCH_LIBRARY_IMPL(docqa, CUDA, m) {
   m.impl("paged_decode_cascade_rope", &paged_decode_cascade_rope);
   m.impl("paged_decode_cascade_grouped", &paged_decode_cascade_grouped);
   m.impl("paged_decode_cascade_split", &paged_decode_cascade_split);
+  m.impl("paged_decode_grouped_fused", &paged_decode_grouped_fused);
   m.impl("kv_copy_rows", &kv_copy_rows);
   m.impl("ar_run", &ar_run);
   m.impl("add_rmsnorm_splitk", &add_rmsnorm_splitk);

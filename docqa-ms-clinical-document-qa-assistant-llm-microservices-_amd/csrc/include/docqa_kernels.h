@@ -62,7 +62,9 @@ int docqa_paged_decode_cascade_split(const void* q, int q_stride, void* k_cache,
                                      float scale, const int* prefix_table, const int* plen, int nchunk,
                                      float* pacc, float* pml, const int* items, const int* merges, int cap,
                                      float* ws_acc, float* ws_ml, int defer,
-                                     hipStream_t s, int* tick = nullptr, int inline_prefix = 0);
+                                     hipStream_t s, int* tick = nullptr, int inline_prefix = 0,
+                                     const float* fP = nullptr, int fS = 0, const int* positions = nullptr,
+                                     const float* cos_sin = nullptr, const int* slot_mapping = nullptr);
 int docqa_paged_decode_cascade_persist(const void* q, int q_stride, void* k_cache, void* v_cache,
                                        const int* block_tables, int maxb, const int* context_lens,
                                        void* out, int out_stride, int B, int Hq, int Hkv, int BS,

@@ -988,14 +988,20 @@ constexpr int kGroupMaxPos = 64;     // block positions beyond the cascade prefi
 // several items (workgroups), each writing an un-normalised partial (m, l, O) for its 16
 // columns to ws_ml / ws_acc[slot] that group_split_merge_kernel combines; an item of an
 // unsplit group (slot -1) finishes as the plain kernel does.
-template <int NSR = 3, bool SPLIT = false>
+// FUSE (split plans from block 0, no prefix kernel): the step's packed QKV arrives as the
+// projection's fp32 split-K slabs (FusedQKV, q null) -- each workgroup sums and rotates the
+// query rows it needs (RoPE partner chunk c ^ 8 is the same lane's ks ^ 2 fragment), and the
+// item whose block range holds a row's new token writes that token's rotated K and V into
+// the paged cache before any tile is staged: the rope_cache_splitk launch and the bf16 QKV
+// round trip disappear.  Same arithmetic as rope_cache_splitk (bf16-rounded slab sums).
+template <int NSR = 3, bool SPLIT = false, bool FUSE = false>
 __global__ __launch_bounds__(256) void paged_decode_group_kernel(
     const uint16_t* __restrict__ q, int q_stride, const uint16_t* __restrict__ k_cache,
     const uint16_t* __restrict__ v_cache, const int* __restrict__ block_tables, int maxb,
     const int* __restrict__ context_lens, int B, int Hkv, float scale,
     uint16_t* __restrict__ out, int out_stride, const int* __restrict__ groups, CascadeIn ci,
     float* __restrict__ ws_acc = nullptr, float* __restrict__ ws_ml = nullptr,
-    const int* __restrict__ merges = nullptr, int* __restrict__ tick = nullptr) {
+    const int* __restrict__ merges = nullptr, int* __restrict__ tick = nullptr, FusedQKV fz = FusedQKV{}) {
   constexpr int G = 4, R = 4, D = 128, TT = 32, MAXT = kGroupMaxPos * 8;
   constexpr int TILE = TT * D;                   // elements of one K (or V) tile: 8 KB
   __shared__ __attribute__((aligned(16))) uint16_t ring[NSR * 2 * TILE];
@@ -1021,6 +1027,28 @@ __global__ __launch_bounds__(256) void paged_decode_group_kernel(
     lo = gp[4];
     hi = min(gp[5], maxb);
     part = gp[6];
+  }
+  const int Wq = (fz.Hq + 2 * Hkv) * D;          // FUSE: packed QKV row width
+  const size_t fslab = (size_t)B * Wq;            // FUSE: slab stride
+  if constexpr (FUSE) {
+    // new tokens first: wave 0 the rotated K, wave 1 the V of the group's rows whose last
+    // position falls in this item's block range (lane = row slot x 16 + 8-dim chunk)
+    if (wave < 2) {
+      const int rs = lane >> 4, c = lane & 15;
+      const int row = rows[rs], L = Ls[rs];
+      const bool mine = row >= 0 && L > 0 && ((L - 1) >> 6) >= lo && ((L - 1) >> 6) < hi;
+      const float* src = fz.P + (size_t)max(row, 0) * Wq + (size_t)(fz.Hq + (wave ? Hkv : 0) + kvh) * D + c * 8;
+      float x[8];
+      sum_slabs8(src, fz.S, fslab, x);
+      if (wave == 0) rope8(x, c, fz.cos_sin + (size_t)(row >= 0 ? fz.positions[row] : 0) * D);
+      const int slot = row >= 0 ? fz.slot_mapping[row] : -1;
+      if (mine && slot >= 0) {
+        uint16_t* dst = const_cast<uint16_t*>(wave ? v_cache : k_cache) +
+                        (((size_t)(slot >> 6) * Hkv + kvh) * 64 + (slot & 63)) * D + c * 8;
+        *reinterpret_cast<uint4*>(dst) = pack8(x);
+      }
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // landed before any tile is staged
+    }
   }
 
   // ---- tile list: lane j of wave 0 owns block position max(P/64, lo) + j
@@ -1065,7 +1093,28 @@ __global__ __launch_bounds__(256) void paged_decode_group_kernel(
   // Q^T fragments: column hl = row slot hl / 4, head hl % 4
   const int crow = rows[hl >> 2], cL = Ls[hl >> 2], cbit = 1 << (hl >> 2);
   bf16x8 qf[4];
-  {
+  if constexpr (FUSE) {
+    // fragment ks holds dims 8 (4 ks + lg) ..: ks and ks + 2 are a rotate-half pair
+    const float* qb = fz.P + (size_t)max(crow, 0) * Wq + (size_t)(kvh * G + (hl & 3)) * D + lg * 8;
+    const float* cs = fz.cos_sin + (size_t)(crow >= 0 ? fz.positions[crow] : 0) * D;
+#pragma unroll
+    for (int pr = 0; pr < 2; ++pr) {
+      float x1[8], x2[8], o1[8], o2[8];
+      sum_slabs8(qb + pr * 32, fz.S, fslab, x1);
+      sum_slabs8(qb + (pr + 2) * 32, fz.S, fslab, x2);
+      const int i0 = (4 * pr + lg) * 8;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float co = cs[i0 + j], si = cs[64 + i0 + j];
+        o1[j] = x1[j] * co - x2[j] * si;
+        o2[j] = x2[j] * co + x1[j] * si;
+      }
+      const uint4 a = crow >= 0 ? pack8(o1) : make_uint4(0, 0, 0, 0);
+      const uint4 b = crow >= 0 ? pack8(o2) : make_uint4(0, 0, 0, 0);
+      qf[pr] = __builtin_bit_cast(bf16x8, a);
+      qf[pr + 2] = __builtin_bit_cast(bf16x8, b);
+    }
+  } else {
     const uint16_t* qp = q + (size_t)max(crow, 0) * q_stride + (size_t)(kvh * G + (hl & 3)) * D + lg * 8;
 #pragma unroll
     for (int ks = 0; ks < 4; ++ks) {
@@ -1761,7 +1810,8 @@ int docqa_paged_decode_cascade_split(const void* q, int q_stride, void* k_cache,
                                      float scale, const int* prefix_table, const int* plen, int nchunk,
                                      float* pacc, float* pml, const int* items, const int* merges, int cap,
                                      float* ws_acc, float* ws_ml, int defer, hipStream_t s, int* tick,
-                                     int inline_prefix) {
+                                     int inline_prefix, const float* fP, int fS, const int* positions,
+                                     const float* cos_sin, const int* slot_mapping) {
   if (B == 0) return 0;
   if (BS != 64 || maxb > kGroupMaxPos || Hq != 4 * Hkv || nchunk < 1 || nchunk > kCascadeMaxChunks || cap < 1)
     return -1;
@@ -1788,7 +1838,15 @@ int docqa_paged_decode_cascade_split(const void* q, int q_stride, void* k_cache,
   // split groups merged by their last item, no merge launch (int32 [cap, Hkv] zeroed,
   // items carry their merge row in column 7)
   int* tk = (tick && !defer) ? tick : nullptr;
-  if (nsr == 4)
+  if (fP) {   // QKV slabs straight in: RoPE + new-token cache write in the group kernel
+    if (!inline_prefix || defer || fS < 1 || !positions || !cos_sin || !slot_mapping) return -1;
+    const FusedQKV fz{fP, fS, positions, cos_sin, slot_mapping, Hq};
+    paged_decode_group_kernel<3, true, true><<<dim3(Hkv, cap), 256, 0, s>>>(
+        nullptr, 0, (const uint16_t*)k_cache, (const uint16_t*)v_cache, block_tables, maxb, context_lens, B, Hkv,
+        scale, (uint16_t*)out, out_stride, items, ci, ws_acc, ws_ml, merges, tk, fz);
+    DOCQA_CHECK_LAUNCH();
+    if (tk) return 0;
+  } else if (nsr == 4)
     paged_decode_group_kernel<4, true><<<dim3(Hkv, cap), 256, 0, s>>>(
         (const uint16_t*)q, q_stride, (const uint16_t*)k_cache, (const uint16_t*)v_cache, block_tables, maxb,
         context_lens, B, Hkv, scale, (uint16_t*)out, out_stride, items, ci, ws_acc, ws_ml, merges, tk);

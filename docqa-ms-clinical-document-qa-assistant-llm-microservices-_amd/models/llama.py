@@ -41,6 +41,11 @@ from ..parallel import comm
 # default: measured 2.5 % slower per decode step at batch 256 than the separate rope_cache
 # launch (the ring's fused preamble delays its K/V stream; profiles/r1_cascade_rope_ab.log)
 _CASCADE_ROPE = os.environ.get("DOCQA_CASCADE_ROPE", "0") == "1"
+# grouped decode reading the QKV slabs itself (ops.paged_decode_grouped_fused): off -- every
+# group workgroup's slab loads + new-token write ahead of its first K/V stage cost more than the
+# rope_cache_splitk launch saved (decode 1148-1151 vs 1120-1122 ms per batch same-box,
+# profiles/r4_group_fused_ab.log)
+_GROUP_FUSED = os.environ.get("DOCQA_GROUP_FUSED", "0") == "1"
 # short prefills (<= ops.MID_M_MAX tokens) on the decode projection plans (forward())
 _PREFILL_MID = os.environ.get("DOCQA_PREFILL_MID", "1") != "0"
 
@@ -386,7 +391,14 @@ class LlamaModel:
                 pq = None
             if cascade:
                 # shared-prefix decode: RoPE + cache write, then prefix-once + suffix attention
-                if sq:
+                if (sq and meta.decode_groups is not None and meta.decode_inline and x.is_cuda
+                        and _GROUP_FUSED and meta.slot_mapping is not None):
+                    # the group kernel reads the QKV slabs itself (RoPE + new-token cache write)
+                    a = ops.paged_decode_grouped_fused(qkv_slabs, meta.positions, self.cos_sin, meta.slot_mapping,
+                                                       kc, vc, meta.block_tables, meta.context_lens, hq,
+                                                       self.scale, meta.shared_table, meta.shared_len,
+                                                       meta.cascade_chunks, meta.decode_groups, self._decode_tick(M))
+                elif sq:
                     qkv = ops.rope_cache_splitk(qkv_slabs, meta.positions,
                                                 self.cos_sin, meta.slot_mapping, kc, vc, hq, hkv, D)
                     if meta.decode_groups is not None:

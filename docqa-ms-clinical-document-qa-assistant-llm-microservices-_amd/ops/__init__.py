@@ -700,6 +700,23 @@ def paged_decode_cascade_grouped(q, k_cache, v_cache, block_tables, context_lens
                                     scale, prefix_table, prefix_len, nchunk)
 
 
+def paged_decode_grouped_fused(P, positions, cos_sin, slot_mapping, k_cache, v_cache, block_tables, context_lens,
+                               Hq, scale, prefix_table, prefix_len, nchunk: int, plan, tick=None):
+    """Grouped decode attention straight from the QKV projection's split-K slabs (split plan
+    built from block 0, no prefix kernel): each workgroup rotates the query rows it needs and
+    the item holding a row's new token writes its rotated K / V to the paged cache first --
+    the same result as :func:`rope_cache_splitk` + :func:`paged_decode_cascade_grouped`
+    (``inline_prefix``), one launch and the bf16 QKV round trip fewer."""
+    if _gpu(P):
+        return _native().paged_decode_grouped_fused(P, positions, cos_sin, slot_mapping, k_cache, v_cache,
+                                                    block_tables, context_lens, Hq, scale, prefix_table,
+                                                    prefix_len, nchunk, plan, tick)
+    Hkv, D = k_cache.shape[1], k_cache.shape[3]
+    qkv = rope_cache_splitk(P, positions, cos_sin, slot_mapping, k_cache, v_cache, Hq, Hkv, D)
+    return paged_decode_cascade_grouped(qkv, k_cache, v_cache, block_tables, context_lens, Hq, scale, prefix_table,
+                                        prefix_len, nchunk, plan, False, tick, True)
+
+
 def grouped_decode_ok(k_cache, block_tables, Hq: int) -> bool:
     """Shapes the grouped cascade kernel supports (cascade shapes, <= 64 blocks per row)."""
     return cascade_ok(k_cache, block_tables, Hq) and block_tables.shape[1] <= 64

@@ -156,6 +156,44 @@ def test_split_grouped_cascade_matches_per_row(native, B, Hkv, seed, tiles, defe
             assert int(tick.abs().sum()) == 0
 
 
+@pytest.mark.parametrize("B,Hkv,seed,S", [(37, 8, 0, 4), (256, 8, 3, 4), (9, 2, 5, 1), (64, 8, 6, 2)])
+@pytest.mark.parametrize("tiles", [3, 12])
+def test_grouped_fused_matches_unfused(native, B, Hkv, seed, S, tiles):
+    """Grouped decode straight from QKV split-K slabs (RoPE + new-token cache write inside the
+    group kernel) == rope_cache_splitk + the inline-prefix grouped kernel: same output and
+    the same cache contents."""
+    Hq, D, BS, Pb, maxb = 4 * Hkv, 128, 64, 3, 12
+    tables, lens, nblk = _trie_batch(B, Pb, maxb, seed)
+    lens = [max(L, 1) for L in lens]
+    kc = torch.randn(nblk, Hkv, BS, D, device="cuda", dtype=torch.bfloat16)
+    vc = torch.randn_like(kc)
+    bt = torch.tensor(tables, dtype=torch.int32, device="cuda")
+    cl = torch.tensor(lens, dtype=torch.int32, device="cuda")
+    pos = cl - 1
+    slots = (bt.gather(1, (pos // BS).long()[:, None])[:, 0] * BS + pos % BS).int()
+    if B > 4:
+        slots[3] = -1                       # a row without a cache write
+    P = torch.randn(S, B, (Hq + 2 * Hkv) * D, device="cuda") * 0.5
+    cs = native.reference.rope_cos_sin(maxb * BS, D, 500000.0, "cuda")
+    pt = torch.zeros(maxb, dtype=torch.int32, device="cuda")
+    pt[:Pb] = bt[0, :Pb]
+    plen = torch.tensor([Pb * BS], dtype=torch.int32, device="cuda")
+    scale = 1 / math.sqrt(D)
+    end_lens = [min(L + 128, maxb * BS) for L in lens]
+    quads = native.pack_decode_groups(tables, end_lens, Pb, BS, (B + 1) // 2)
+    plan = native.split_decode_groups(quads, tables, end_lens, 0, BS, max(B, 4), tiles).cuda()
+    kc1, vc1, kc2, vc2 = kc.clone(), vc.clone(), kc.clone(), vc.clone()
+    qkv = native.rope_cache_splitk(P, pos, cs, slots, kc1, vc1, Hq, Hkv, D)
+    ref = native.paged_decode_cascade_grouped(qkv, kc1, vc1, bt, cl, Hq, scale, pt, plen, 4, plan, False, None, True)
+    tick = torch.zeros(plan.shape[1] * Hkv, dtype=torch.int32, device="cuda")
+    got = native.paged_decode_grouped_fused(P, pos, cs, slots, kc2, vc2, bt, cl, Hq, scale, pt, plen, 4, plan, tick)
+    torch.cuda.synchronize()
+    assert torch.equal(kc2, kc1) and torch.equal(vc2, vc1)
+    d = (got.float() - ref.float()).abs().max().item()
+    assert d <= 2e-3 + 1e-2 * ref.float().abs().max().item(), d
+    assert int(tick.abs().sum()) == 0
+
+
 def test_split_grouped_cascade_padded_rows_zero(native):
     Hkv, D, BS, Pb, maxb = 2, 128, 64, 2, 6
     Hq, B = 4 * Hkv, 6
