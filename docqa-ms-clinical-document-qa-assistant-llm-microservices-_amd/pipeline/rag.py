@@ -232,7 +232,11 @@ class RAGPipeline:
         # step time, x1.5 -- 1 step at batch 1 (1.5 ms of preparation vs 3.6 ms steps; a
         # fixed 4 put 11 ms of waiting into every answer's latency), 4 at batch 256
         env_lead = os.environ.get("DOCQA_PIPELINE_LEAD")
-        adaptive = lead_steps is None and env_lead is None
+        # data-parallel ranks keep the fixed lead: their batch preparation meets in the
+        # sharded index's all-gather, so every rank must release it at the same step
+        dp = torch.distributed.is_available() and torch.distributed.is_initialized() and \
+            torch.distributed.get_world_size() > 1
+        adaptive = lead_steps is None and env_lead is None and not dp
         lead = [lead_steps if lead_steps is not None else int(env_lead or 4)]
         est = {"prep": None, "step": None}
 
