@@ -329,6 +329,13 @@ class LlamaModel:
                 else:
                     S, t = ops.decode_plan(M, *L0[k].shape)
                     plans[k] = (S, lambda a, w, S=S, t=t: ops.dgemm_partial(a, w, S, t))
+            if small and M > 256 and "down" in plans:
+                # a 257..512-token prefill: the down projection at S=4 (256 workgroups) --
+                # 75.7 vs 102.6 us at 512 rows with the add+norm consumer
+                # (profiles/r4_prefill_mid_probe.log); decode buckets keep their plan
+                N, K = L0["down"].shape
+                if ops.mid_plan(M, N, K)[0] and (K // 128) % 4 == 0 and N % 128 == 0:
+                    plans["down"] = (4, lambda a, w: ops.mgemm_partial(a, w, 4, 2))
             Sg, cg = ops.mid_plan(M, *L0["gate_up"].shape, glu=True)
             sp = ops.glu_split_plan(M, *L0["gate_up"].shape) if x.is_cuda else None
             if sp is not None:
@@ -340,6 +347,13 @@ class LlamaModel:
                 glu = (lambda a, w: ops.mgemm_glu(a, w, cg)) if Sg else ops.glu_linear
         else:
             glu = ops.prefill_glu
+            if self.layers and x.is_cuda and not decode:
+                # 513..2048-token prefills: split-K slab plans where they win with the consumer
+                L0 = self.layers[0]
+                for k in ("qkv", "o", "down"):
+                    S, c = ops.prefill_plan(M, *L0[k].shape)
+                    if S >= 2:
+                        plans[k] = (S, lambda a, w, S=S, c=c: ops.mgemm_partial(a, w, S, c))
         if self.tp > 1 and not x.is_cuda:
             # CPU TP rehearsal: row-parallel partials as fp32 slabs, all-reduced before the one
             # bf16 rounding (comm.tp_add_rmsnorm), so TP = N tracks TP = 1's rounding

@@ -386,13 +386,38 @@ def pgemm_ok(M: int, N: int, K: int) -> bool:
             and max(M, N) * K * 2 < (1 << 32) and ((M + 255) // 256) * (N // 256) >= _PGEMM_MIN_TILES)
 
 
+PREFILL_MID_MAX = 2048
+_PREFILL_PLANS = os.environ.get("DOCQA_PREFILL_PLANS", "1") != "0"
+
+
+def prefill_plan(M: int, N: int, K: int) -> tuple[int, int]:
+    """(split-K count, mgemm cfg) of a 513..2048-row prefill projection, (0, 0) for the
+    256 x 256 / 128 x 128 kernels.  S >= 2: fp32 slabs into the split-K consumers (RoPE +
+    KV write, add + RMSNorm); S == 1: the bf16 product.  Measured with the consumer on the
+    Llama-3-8B shapes (profiles/r4_prefill_mid_probe.log; hipBLASLt + consumer in brackets):
+    QKV 768 / 1024 rows cfg 2 S=1 60.9 / 65.4 us (56.3 / 60.6; the 128-tile kernel it
+    replaces 71.2 / 83.0), O S=2 42.3 / 47.9 (40.8 / 48.7), down S=2 111.8 / 131.8
+    (116.5 / 145.3); 1025..2048 rows: O and down S=1, QKV the 256 x 256 kernel."""
+    if not _PREFILL_PLANS or _MID_OFF or not (MID_M_MAX < M <= PREFILL_MID_MAX) or N % 128 or K % 128:
+        return 0, 0
+    if N >= 6144 and K <= 4096:          # QKV-like: wide N
+        return (1, 2) if M <= 1024 else (0, 0)
+    if M <= 1024 and (K // 128) % 2 == 0:
+        return 2, 2
+    return 1, 2
+
+
 def prefill_linear(x, w):
     """x @ w^T for the prefill projections (M = packed prompt tokens) on the hand-written
-    MFMA GEMMs: the 256 x 256 8-phase kernel (pgemm.hip) where it has enough tiles, else
-    the 128 x 128 kernel (gemm.hip); hipBLASLt only for shapes neither takes."""
+    MFMA GEMMs: the mid-M kernel's bf16 product where :func:`prefill_plan` says so, the
+    256 x 256 8-phase kernel (pgemm.hip) where it has enough tiles, else the 128 x 128
+    kernel (gemm.hip); hipBLASLt only for shapes none takes."""
     if _gpu(x):
         N, K = w.shape
         M = x.numel() // K
+        S, cfg = prefill_plan(M, N, K)
+        if S == 1:
+            return _native().mgemm(x.contiguous(), w, 1, cfg)
         if pgemm_ok(M, N, K):
             return _native().pgemm(x.contiguous(), w, 0)
         if N % 128 == 0 and K % 64 == 0:

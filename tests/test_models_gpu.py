@@ -99,6 +99,28 @@ def test_llama_prefill_decode_logits_native_vs_reference(native):
     assert _rel(d1, d2) < 0.03
 
 
+@pytest.mark.parametrize("lens", [(300, 200), (700, 300), (900, 800, 100)])
+def test_llama_mid_prefill_plans_vs_reference(native, lens):
+    """Prefills of 257..2048 tokens on the mid-M split-K plans (ops.prefill_plan and the short
+    prefill's decode plans) track the fp32 reference forward."""
+    from docqa_amd.engine.kv_cache import KVCache
+    from docqa_amd.models.llama import LlamaConfig, LlamaModel
+
+    m = LlamaModel(LlamaConfig.preset("llama3-1b-test"), device="cuda", seed=8)
+    g = torch.Generator().manual_seed(9)
+    prompts = [torch.randint(0, 32000, (n,), generator=g).tolist() for n in lens]
+    BS = 64
+    kv1 = KVCache(m.cfg.layers, 64, m.hkv, m.cfg.head_dim, BS).caches
+    kv2 = KVCache(m.cfg.layers, 64, m.hkv, m.cfg.head_dim, BS).caches
+    p1, tables = _prefill_logits(m, kv1, prompts, BS)
+    d1 = _decode_logits(m, kv1, prompts, tables, [3] * len(prompts), BS)
+    with native.use_reference():
+        p2, _ = _prefill_logits(m, kv2, prompts, BS)
+        d2 = _decode_logits(m, kv2, prompts, tables, [3] * len(prompts), BS)
+    assert _rel(p1, p2) < 0.03
+    assert _rel(d1, d2) < 0.03
+
+
 def test_llama_mid_batch_decode_native_vs_reference(native):
     """A 256-row decode step (the mid-M GEMM path: split-K QKV / O / down slabs, fused
     SwiGLU, fused LM-head argmax) against the same step on the fp32 reference ops."""
