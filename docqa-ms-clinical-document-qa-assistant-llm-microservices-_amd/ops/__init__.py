@@ -400,6 +400,10 @@ def prefill_plan(M: int, N: int, K: int) -> tuple[int, int]:
     (116.5 / 145.3); 1025..2048 rows: O and down S=1, QKV the 256 x 256 kernel."""
     if not _PREFILL_PLANS or _MID_OFF or not (MID_M_MAX < M <= PREFILL_MID_MAX) or N % 128 or K % 128:
         return 0, 0
+    if N < 4096:
+        # narrow N (the 70B TP-8 QKV shard, N 1280 x K 8192): the mid-M kernel's few 128-wide
+        # tiles lose to the 256 x 256 kernel's split-K (profiles/r4_pgemm_mid_probe.log)
+        return 0, 0
     if N >= 6144 and K <= 4096:          # QKV-like: wide N
         return (1, 2) if M <= 1024 else (0, 0)
     if M <= 1024 and (K // 128) % 2 == 0:
