@@ -41,6 +41,8 @@ from ..parallel import comm
 # default: measured 2.5 % slower per decode step at batch 256 than the separate rope_cache
 # launch (the ring's fused preamble delays its K/V stream; profiles/r1_cascade_rope_ab.log)
 _CASCADE_ROPE = os.environ.get("DOCQA_CASCADE_ROPE", "0") == "1"
+# last prefill layer on the logits rows only (forward(): trim)
+_PREFILL_TRIM = os.environ.get("DOCQA_PREFILL_TRIM", "1") != "0"
 # grouped decode reading the QKV slabs itself (ops.paged_decode_grouped_fused): off -- every
 # group workgroup's slab loads + new-token write ahead of its first K/V stage cost more than the
 # rope_cache_splitk launch saved (decode 1148-1151 vs 1120-1122 ms per batch same-box,
@@ -383,6 +385,9 @@ class LlamaModel:
             chain = ops.chain_plan(M, L0["o"].shape[0], L0["o"].shape[1], L0["gate_up"].shape[0],
                                    L0["qkv"].shape[0])
         pq = None   # this layer's QKV slabs, already computed by the previous layer's chain
+        trim = (not decode and _PREFILL_TRIM and x.is_cuda and logits_index is not None and self.layers
+                and meta.block_tables is not None and meta.prefix_lens is not None
+                and logits_index.numel() == meta.block_tables.shape[0] and M > logits_index.numel())
         # batch 1 (one row, TP = 1, skinny-kernel plans): the gate|up and the next layer's QKV
         # projection build their input row themselves -- residual add + RMSNorm of the previous
         # projection's slabs, in LDS, under their first weight stages (dgemm.hip XNormIn) --
@@ -461,6 +466,18 @@ class LlamaModel:
             else:
                 qkv = lin(x, L["qkv"])
                 ops.rope_cache(qkv, meta.positions, self.cos_sin, meta.slot_mapping, kc, vc, hq, hkv, D)
+            if trim and i == nl - 1 and qkv is not None:
+                # last layer of a prefill whose logits are wanted for a few rows only: every
+                # token's K/V is in the cache now; only the selected rows go on through
+                # attention, O and the MLP (their outputs are the only ones anything reads)
+                # -- each selected row is its sequence's last token, so its attention over
+                # the paged cache is exactly the decode attention at that context length
+                ctx = meta.prefix_lens + (meta.cu_seqlens[1:] - meta.cu_seqlens[:-1])
+                a = ops.paged_decode(qkv.index_select(0, logits_index).contiguous(), kc, vc, meta.block_tables,
+                                     ctx, hq, meta.block_tables.shape[1] * kc.shape[2], self.scale)
+                residual = residual.index_select(0, logits_index)
+                logits_index = None
+                qkv = None
             if qkv is None:
                 pass
             elif meta.prefill and meta.prefix_lens is not None:

@@ -121,6 +121,52 @@ def test_llama_mid_prefill_plans_vs_reference(native, lens):
     assert _rel(d1, d2) < 0.03
 
 
+def test_llama_prefill_trim_last_layer(native, monkeypatch):
+    """Prefill over a cached prefix with logits for each prompt's last token: the last layer
+    run on those rows only (attention as decode attention over the paged cache) == the full
+    last layer, and the KV cache written identically."""
+    from docqa_amd.engine.kv_cache import KVCache
+    from docqa_amd.models import llama as LM
+
+    m = LM.LlamaModel(LM.LlamaConfig.preset("llama3-1b-test"), device="cuda", seed=12)
+    g = torch.Generator().manual_seed(13)
+    BS, P = 64, 128
+    shared = torch.randint(0, 32000, (P,), generator=g).tolist()
+    suffixes = [torch.randint(0, 32000, (n,), generator=g).tolist() for n in (37, 300, 5, 900)]
+    out = {}
+    for trim in (True, False):
+        monkeypatch.setattr(LM, "_PREFILL_TRIM", trim)
+        kv = KVCache(m.cfg.layers, 128, m.hkv, m.cfg.head_dim, BS).caches
+        _prefill_logits(m, kv, [shared], BS)                # blocks 0, 1 (+ spare) hold the prefix
+        nb, tables, ids, pos, slots, cu = 3, [], [], [], [], [0]
+        for sfx in suffixes:
+            own = list(range(nb, nb + (len(sfx) + BS - 1) // BS + 1))
+            nb += len(own)
+            tb = [0, 1] + own
+            tables.append(tb)
+            for t in range(P, P + len(sfx)):
+                pos.append(t)
+                slots.append(tb[t // BS] * BS + t % BS)
+            ids += sfx
+            cu.append(cu[-1] + len(sfx))
+        maxb = max(len(t) for t in tables)
+        bt = torch.zeros(len(tables), maxb, dtype=torch.int32)
+        for r, t in enumerate(tables):
+            bt[r, :len(t)] = torch.tensor(t)
+        meta = LM.AttnMeta(prefill=True, positions=torch.tensor(pos, dtype=torch.int32, device="cuda"),
+                           slot_mapping=torch.tensor(slots, dtype=torch.int32, device="cuda"),
+                           cu_seqlens=torch.tensor(cu, dtype=torch.int32, device="cuda"),
+                           max_len=max(len(x) for x in suffixes))
+        meta.block_tables = bt.cuda()
+        meta.prefix_lens = torch.full((len(suffixes),), P, dtype=torch.int32, device="cuda")
+        last = torch.tensor(cu[1:], device="cuda") - 1
+        logits = m.forward(torch.tensor(ids, dtype=torch.int32, device="cuda"), meta, kv, last)
+        out[trim] = (logits.float(), [c.clone() for pair in kv for c in pair])
+    assert _rel(out[True][0], out[False][0]) < 0.02
+    for a, b in zip(out[True][1], out[False][1]):
+        assert torch.equal(a, b)
+
+
 def test_llama_mid_batch_decode_native_vs_reference(native):
     """A 256-row decode step (the mid-M GEMM path: split-K QKV / O / down slabs, fused
     SwiGLU, fused LM-head argmax) against the same step on the fp32 reference ops."""
