@@ -27,7 +27,7 @@ def _port():
 def test_custom_all_reduce(world):
     env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0",
                GPU_MAX_HW_QUEUES="1",   # ranks share one GPU: keep every rank's queue resident
-               DOCQA_AR_TIMEOUT_MS=os.environ.get("DOCQA_AR_TIMEOUT_MS", "2000"))
+               DOCQA_AR_TIMEOUT_MS=os.environ.get("DOCQA_AR_TIMEOUT_MS", "20000"))
     for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK"):
         env.pop(k, None)
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(world),

@@ -31,7 +31,7 @@ def test_bench_dp_shared_gpu(world):
     sharded index's per-batch all-gathers run on the IPC peer-memory gather."""
     env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0",
                GPU_MAX_HW_QUEUES="1",   # ranks share one GPU: keep every rank's queue resident
-               DOCQA_AR_TIMEOUT_MS=os.environ.get("DOCQA_AR_TIMEOUT_MS", "2000"))
+               DOCQA_AR_TIMEOUT_MS=os.environ.get("DOCQA_AR_TIMEOUT_MS", "20000"))
     for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK"):
         env.pop(k, None)
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(world),

@@ -50,9 +50,11 @@ def test_tp_matches_tp1(tmp_path, preset, tp):
     # the others' all-reduce kernels spin on it, so that rank "never arrives" (round 3's
     # spin-limit hits; round 4: rank 0 absent > 30 s at the first call, profiles/
     # r4_ar_skew_default_hwq_tp4_fail.txt).  One queue per process keeps every rank resident:
-    # the longest peer wait drops to ~35 ms (profiles/r4_ar_skew_hwq1_tp.log).
+    # the longest peer wait drops to ~35 ms (profiles/r4_ar_skew_hwq1_tp.log).  Rarely a
+    # shared-GPU rank still stalls for > 2 s (one failure in five suites, rank 0 at its 4th
+    # call), so the bound here is 20 s; one process per GPU keeps the 500 ms default.
     env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0", GPU_MAX_HW_QUEUES="1",
-               DOCQA_AR_TIMEOUT_MS=os.environ.get("DOCQA_AR_TIMEOUT_MS", "2000"))
+               DOCQA_AR_TIMEOUT_MS=os.environ.get("DOCQA_AR_TIMEOUT_MS", "20000"))
     for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK"):
         env.pop(k, None)
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(tp),
