@@ -37,6 +37,8 @@ if "--share-gpu" in sys.argv:
     # so a collective kernel never spins on a rank whose queue the scheduler left unmapped
     # (parallel/custom_ar.py; profiles/r4_ar_skew_*); read at HIP init, so set before torch
     os.environ.setdefault("GPU_MAX_HW_QUEUES", "1")
+    # and the IPC collectives' waiting workgroups must leave CUs free for a late rank's kernels
+    os.environ.setdefault("DOCQA_AR_MAX_WG", "32")
 
 
 def main() -> None:

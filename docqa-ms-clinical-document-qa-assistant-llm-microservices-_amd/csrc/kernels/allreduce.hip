@@ -45,6 +45,7 @@
 // peer wait is ~35 ms (profiles/r4_ar_skew_hwq1_tp.log).  One process per GPU -- the
 // deployment -- never shares a queue slot pool with its peers.
 #include "docqa_common.h"
+#include <stdlib.h>
 #include <cstring>
 
 using namespace docqa;
@@ -321,8 +322,17 @@ int docqa_ar_run(const void* in, int S, void* out, void* residual, const void* w
            max_elems, ctr, err, (unsigned long long)timeout_us * tpu, tpu};
   // workgroups: one per few rows (4 waves, one row each at a time), <= kMaxWG, all resident;
   // the same count on every rank (a function of M only)
+  // DOCQA_AR_MAX_WG (ranks sharing ONE GPU: tests, --share-gpu): fewer workgroups, so the
+  // waiting ranks' spinning workgroups never sit on every CU -- a late rank's next kernel
+  // (a 512-register attention wave needs a whole SIMD) would otherwise find no CU to run on
+  // until the waiters time out.  Read once; every rank sets the same value.
+  static const int max_wg = [] {
+    const char* e = getenv("DOCQA_AR_MAX_WG");
+    const int v = e ? atoi(e) : 0;
+    return v > 0 && v < kMaxWG ? v : kMaxWG;
+  }();
   int G = (M + 3) / 4;
-  if (G > kMaxWG) G = kMaxWG;
+  if (G > max_wg) G = max_wg;
   if (G < 1) G = 1;
   const bool fused = residual != nullptr;
   const int src = S > 0 ? SRC_F32 : SRC_BF16;

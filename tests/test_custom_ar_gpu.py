@@ -26,7 +26,7 @@ def _port():
 @pytest.mark.parametrize("world", [2, 4])
 def test_custom_all_reduce(world):
     env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0",
-               GPU_MAX_HW_QUEUES="1",   # ranks share one GPU: keep every rank's queue resident
+               GPU_MAX_HW_QUEUES="1", DOCQA_AR_MAX_WG="32",   # ranks share one GPU: keep every rank's queue resident
                DOCQA_AR_TIMEOUT_MS=os.environ.get("DOCQA_AR_TIMEOUT_MS", "20000"))
     for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK"):
         env.pop(k, None)

@@ -30,7 +30,7 @@ def test_bench_dp_shared_gpu(world):
     """bench.py's DP path (the driver's --gpus N command) with every rank on cuda:0: the
     sharded index's per-batch all-gathers run on the IPC peer-memory gather."""
     env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0",
-               GPU_MAX_HW_QUEUES="1",   # ranks share one GPU: keep every rank's queue resident
+               GPU_MAX_HW_QUEUES="1", DOCQA_AR_MAX_WG="32",   # ranks share one GPU: keep every rank's queue resident
                DOCQA_AR_TIMEOUT_MS=os.environ.get("DOCQA_AR_TIMEOUT_MS", "20000"))
     for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK"):
         env.pop(k, None)

@@ -53,7 +53,7 @@ def test_tp_matches_tp1(tmp_path, preset, tp):
     # the longest peer wait drops to ~35 ms (profiles/r4_ar_skew_hwq1_tp.log).  Rarely a
     # shared-GPU rank still stalls for > 2 s (one failure in five suites, rank 0 at its 4th
     # call), so the bound here is 20 s; one process per GPU keeps the 500 ms default.
-    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0", GPU_MAX_HW_QUEUES="1",
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0", GPU_MAX_HW_QUEUES="1", DOCQA_AR_MAX_WG="32",
                DOCQA_AR_TIMEOUT_MS=os.environ.get("DOCQA_AR_TIMEOUT_MS", "20000"))
     for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK"):
         env.pop(k, None)
