@@ -212,6 +212,10 @@ def main() -> None:
                 "distinct_chunks_rank0": len(chunks),
             },
         }
+        if cuda:   # the box: CU count and clocks differ between pool machines
+            pr = torch.cuda.get_device_properties(local_rank)
+            out["device"] = {"name": pr.name, "cus": pr.multi_processor_count,
+                             "gcn_arch": getattr(pr, "gcnArchName", "")}
         print(json.dumps(out), flush=True)
     comm.destroy()
 

@@ -1056,10 +1056,15 @@ __global__ __launch_bounds__(256) void paged_decode_group_kernel(
     const int pos = max(P >> 6, lo) + lane;
     int ids[R];
     bool alive[R];
+    // the table entries are loaded on the row id alone (in bounds: pos < hi <= maxb), not
+    // behind the context length: both loads fly together, one dependent latency fewer
+    // before the first tile's DMA
+#pragma unroll
+    for (int r = 0; r < R; ++r) ids[r] = rows[r] >= 0 && pos < hi ? block_tables[(size_t)rows[r] * maxb + pos] : -1;
 #pragma unroll
     for (int r = 0; r < R; ++r) {
       alive[r] = pos < hi && 64 * pos < Ls[r];
-      ids[r] = alive[r] ? block_tables[(size_t)rows[r] * maxb + pos] : -1;
+      ids[r] = alive[r] ? ids[r] : -1;
     }
     int2 ent[2 * R];
     int cnt = 0;

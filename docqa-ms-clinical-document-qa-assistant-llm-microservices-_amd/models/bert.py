@@ -78,13 +78,16 @@ class BertEncoder:
 
     def _random_init(self, seed: int) -> None:
         cfg, dev, dt = self.cfg, self.device, self.dtype
-        g = torch.Generator(device=dev)
+        # drawn on the CPU and moved: the GPU generator's stream depends on the launch grid
+        # (the device's CU count), so GPU-drawn weights -- and with them the retrieved chunks
+        # and every prompt of the bench workload -- differed from box to box
+        g = torch.Generator()
         g.manual_seed(seed + 1234)
 
         def w(*shape, s=0.02):
-            t = torch.empty(*shape, device=dev, dtype=dt)
+            t = torch.empty(*shape, dtype=dt)
             t.normal_(0.0, s, generator=g)
-            return t
+            return t.to(dev)
 
         def ones(n):
             return torch.ones(n, device=dev, dtype=dt)
@@ -192,13 +195,14 @@ class BertTokenClassifier(BertEncoder):
                  seed: int = 0):
         super().__init__(cfg, device, dtype, seed)
         self.labels = list(labels)
-        g = torch.Generator(device=self.device)
+        g = torch.Generator()       # CPU draw, as the encoder's (box-independent weights)
         g.manual_seed(seed + 99)
         n = len(self.labels)
         # 8/16/32 label rows: the shapes the fused head+argmax kernel is compiled for
         npad = next((c for c in (8, 16, 32) if n <= c), (n + 7) // 8 * 8)
-        self.cls_w = torch.zeros(npad, cfg.hidden, device=self.device, dtype=dtype)
-        self.cls_w[:n].normal_(0.0, 0.02, generator=g)
+        cls_w = torch.zeros(npad, cfg.hidden, dtype=dtype)
+        cls_w[:n].normal_(0.0, 0.02, generator=g)
+        self.cls_w = cls_w.to(self.device)
         self.cls_b = torch.zeros(npad, device=self.device, dtype=dtype)
         self.cls_b[n:] = -1e4  # padded label columns never win the argmax
 

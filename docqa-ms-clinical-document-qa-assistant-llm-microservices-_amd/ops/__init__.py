@@ -17,7 +17,8 @@ import torch
 
 from . import reference as ref
 
-_LIB_PATH = Path(__file__).resolve().parent / "_docqa_C.so"
+# DOCQA_NATIVE_LIB: load another build of the extension (same-box A/B of two kernel builds)
+_LIB_PATH = Path(os.environ.get("DOCQA_NATIVE_LIB") or Path(__file__).resolve().parent / "_docqa_C.so")
 _lock = threading.Lock()
 _loaded = False
 _load_error: str | None = None
