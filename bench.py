@@ -210,6 +210,7 @@ def main() -> None:
                 "unique_question_frac": round(len(set(timed_q)) / max(1, len(timed_q)), 4),
                 "repeat_of_earlier_frac": round(repeats / max(1, len(timed_q)), 4),
                 "distinct_chunks_rank0": len(chunks),
+                "context_order": pipe.context_order,
             },
         }
         if cuda:   # the box: CU count and clocks differ between pool machines

@@ -22,6 +22,10 @@ from pathlib import Path
 from tokenizers import Tokenizer, decoders, models, normalizers, pre_tokenizers, processors, trainers
 
 _CACHE = Path(__file__).resolve().parents[2] / "build" / "tokenizers"
+# trained vocabularies shipped with the package: the WordPiece trainer is not deterministic
+# across processes (tie order), so a box that trained its own vocabulary tokenised -- and
+# retrieved, and prompted -- differently from the next; every box now loads these
+_ASSETS = Path(__file__).resolve().parent / "assets"
 _lock = threading.Lock()
 _instances: dict = {}
 
@@ -66,6 +70,8 @@ def _cached(name: str, env: str, train, vocab_size: int) -> Tokenizer:
         path = os.environ.get(env)
         if path and Path(path).exists():
             tok = Tokenizer.from_file(path)
+        elif (_ASSETS / f"{name}-{vocab_size}.json").exists():
+            tok = Tokenizer.from_file(str(_ASSETS / f"{name}-{vocab_size}.json"))
         else:
             f = _CACHE / f"{name}-{vocab_size}.json"
             if f.exists():

@@ -135,6 +135,36 @@ def test_prompt_pieces_identical_to_full_tokenisation(monkeypatch):
     assert tok.encode_batch_chat([qs[0]]) == [tok.chat_prompt(qs[0])]
 
 
+def test_shared_context_order():
+    """context_order="shared": each prompt holds the same chunks, the batch's most
+    retrieved first (ties by id), so prompts with a common chunk share a token prefix;
+    "relevance" keeps the retrieval order."""
+    import torch
+
+    from docqa_amd.pipeline.rag import RAGPipeline
+    from docqa_amd.text.tokenizer import ChatTokenizer
+
+    tok = ChatTokenizer(model_vocab=128256)
+    meta = [{"text_content": f"Note {i} : toux, fatigue ; Ren Shen (score {i % 10}).", "source": f"s{i}"}
+            for i in range(10)]
+
+    class _Eng:
+        device = torch.device("cpu")
+
+    I = [[3, 7, 1], [9, 7, 2], [7, 5, 3]]
+    rel = RAGPipeline(None, None, None, meta, _Eng(), tok, context_order="relevance")
+    sh = RAGPipeline(None, None, None, meta, _Eng(), tok, context_order="shared")
+    assert rel._ordered(I) == I
+    assert sh._ordered(I) == [[7, 3, 1], [7, 2, 9], [7, 3, 5]]
+    a, b = sh.build_prompts(["q1", "q2"], [[3, 7, 1], [9, 7, 2]])
+    ra, rb = rel.build_prompts(["q1", "q2"], [[3, 7, 1], [9, 7, 2]])
+    common = lambda x, y: next(i for i, (u, v) in enumerate(zip(x, y)) if u != v)   # noqa: E731
+    assert common(a, b) > common(ra, rb) + 10           # chunk 7 is shared in the new order
+    assert sorted(a) == sorted(ra)                      # same tokens, other order
+    with pytest.raises(ValueError):
+        RAGPipeline(None, None, None, meta, _Eng(), tok, context_order="random")
+
+
 REF = Path("/root/reference")
 
 
