@@ -161,6 +161,8 @@ int docqa_mgemm_chain(const void* attn, const void* w_o, float* p_o, void* resid
                       int Ko, int N2I, int Nq, int S_o, int cfg_o, int S_d, int cfg_d, int S_q, int cfg_q,
                       float eps, hipStream_t s);
 bool docqa_pgemm_ok(int M, int N, int K);
+int docqa_pgemm_argmax(const void* A, const void* W, int64_t* out, float* outv, float* ws_v, int* ws_i, int M, int N,
+                       int K, int n_valid, hipStream_t s);
 int docqa_pgemm(const void* A, const void* W, void* C, float* P, int M, int N, int K, int S, int epi,
                 hipStream_t s);
 

@@ -531,8 +531,13 @@ bool shape_ok(int M, int N, int K, int S, int cfg) {
 }  // namespace
 
 constexpr int kDefaultCfg = 2;
+int docqa_pgemm_argmax(const void* A, const void* W, int64_t* out, float* outv, float* ws_v, int* ws_i, int M, int N,
+                       int K, int n_valid, hipStream_t s);
+// cfg 8 (LM head only): the argmax on pgemm.hip's 256 x 256 tiles (docqa_pgemm_argmax)
+constexpr int kPgemmArgmaxCfg = 8;
 int docqa_mgemm_tile_n(int cfg) {
   if (cfg == 0) cfg = kDefaultCfg;
+  if (cfg == kPgemmArgmaxCfg) return 256;
   return cfg >= 1 && cfg <= kNumCfg ? kCfg[cfg].bn : 0;
 }
 
@@ -576,6 +581,7 @@ int docqa_mgemm_argmax(const void* X, const void* W, int64_t* out, float* outv, 
                        int N, int K, int n_valid, int cfg, hipStream_t s) {
   if (cfg == 0) cfg = kDefaultCfg;
   if (M == 0) return 0;
+  if (cfg == kPgemmArgmaxCfg) return docqa_pgemm_argmax(X, W, out, outv, ws_v, ws_i, M, N, K, n_valid, s);
   if (!shape_ok(M, N, K, 1, cfg) || n_valid <= 0 || n_valid > N) return -1;
   if (!docqa_aligned16(X) || !docqa_aligned16(W)) return -1;
   const int rc = launch_cfg<EPI_ARGMAX>(cfg, (const uint16_t*)X, (const uint16_t*)W, nullptr, nullptr, ws_v, ws_i,

@@ -29,7 +29,7 @@ idx = FlatIndex(enc.cfg.hidden, "l2", "cpu", torch.float32, capacity=max(1024, l
 idx.add(embed_records(enc, enc_tok, recs))
 qs = synthetic_unique_questions(nb * bs, seed=123)
 res = {}
-for order in ("relevance", "shared"):
+for order in (sys.argv[3].split(",") if len(sys.argv) > 3 else ("relevance", "shared", "trie")):
     pipe = RAGPipeline(enc, enc_tok, idx, recs, None, chat_tok, k=3, max_prompt_tokens=2048 - 256,
                        context_order=order)
     trie, tot, hit = set(), 0, 0

@@ -71,9 +71,10 @@ def test_mgemm_glu(native, M, bn):
 
 
 @pytest.mark.parametrize("M", [1, 256, 300])
-@pytest.mark.parametrize("bn", [1, 2, 3, 4, 5, 6])
+@pytest.mark.parametrize("bn", [1, 2, 3, 4, 5, 6, 8])
 def test_mgemm_argmax(native, M, bn):
-    """LM head + greedy pick == argmax of the bf16 logits (ties: lowest id)."""
+    """LM head + greedy pick == argmax of the bf16 logits (ties: lowest id).  cfg 8: the
+    argmax epilogue on pgemm.hip's 256 x 256 tiles."""
     N, K = 128256, 4096
     x = torch.randn(M, K, device="cuda", dtype=torch.bfloat16)
     w = (torch.randn(N, K, device="cuda") / K ** 0.5).bfloat16()
@@ -109,9 +110,15 @@ def test_mgemm_argmax_ties(native):
     x = torch.ones(M, K, device="cuda", dtype=torch.bfloat16)
     w = torch.full((N, K), 0.5, device="cuda", dtype=torch.bfloat16)
     assert (torch.ops.docqa.mgemm_argmax(x, w, N, 2) == 0).all()
+    assert (torch.ops.docqa.mgemm_argmax(x, w, N, 8) == 0).all()
     w[700:] = 0.75
     w[1500] = 1.0
     assert (torch.ops.docqa.mgemm_argmax(x, w, N, 4) == 1500).all()
+    assert (torch.ops.docqa.mgemm_argmax(x, w, N, 8) == 1500).all()
+    w[1500] = 0.75
+    w[1999] = 1.0       # the best id in the last 256-column tile, beside the n_valid mask
+    assert (torch.ops.docqa.mgemm_argmax(x, w, N, 8) == 1999).all()
+    assert (torch.ops.docqa.mgemm_argmax(x, w, 1999, 8) == 700).all()
 
 
 @pytest.mark.parametrize("M", [200, 256, 333])
