@@ -228,15 +228,28 @@ __device__ __forceinline__ bool glu_meet(f32x4 (&acc)[MI][NJ], uint16_t* smem, f
     }
   }
   __syncthreads();
+  // the partner's accumulators: 8 write-through (sc1) loads in flight per wait -- one
+  // memory latency per 8 fragments, not per fragment (32 serial latencies at cfg 6 made
+  // the 2-way split slower than the unsplit kernel).  The wait names the 8 registers, so
+  // no add can be scheduled above it.
+  constexpr int NF = MI * NJ;
 #pragma unroll
-  for (int i = 0; i < MI; ++i)
+  for (int c = 0; c < NF; c += 8) {
+    f32x4 d[8];
 #pragma unroll
-    for (int j = 0; j < NJ; ++j) {
-      f32x4 d;
-      asm volatile("global_load_dwordx4 %0, %1, off sc1\n\ts_waitcnt vmcnt(0)" : "=v"(d) : "v"(slab + (i * NJ + j) * 256)
-                   : "memory");
-      acc[i][j] += d;
-    }
+    for (int q = 0; q < 8; ++q)
+      if (c + q < NF)
+        asm volatile("global_load_dwordx4 %0, %1, off sc1" : "=v"(d[q]) : "v"(slab + (c + q) * 256) : "memory");
+      else
+        d[q] = f32x4{0.f, 0.f, 0.f, 0.f};
+    asm volatile("s_waitcnt vmcnt(0)"
+                 : "+v"(d[0]), "+v"(d[1]), "+v"(d[2]), "+v"(d[3]), "+v"(d[4]), "+v"(d[5]), "+v"(d[6]), "+v"(d[7])
+                 :
+                 : "memory");
+#pragma unroll
+    for (int q = 0; q < 8; ++q)
+      if (c + q < NF) acc[(c + q) / NJ][(c + q) % NJ] += d[q];
+  }
   if (tid == 0) {   // both halves are past every use of the words: re-arm for the next launch
     __hip_atomic_store(&tick[2 * tix], 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     __hip_atomic_store(&tick[2 * tix + 1], 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
