@@ -224,3 +224,50 @@ def test_unique_questions_are_distinct():
     assert len(set(qs)) == 6400
     assert synthetic_unique_questions(50, seed=123) == qs[:50]
     assert len(set(synthetic_questions(6400, seed=123))) < 1000   # the cache-hot grid
+
+
+def test_trie_context_order_reuses_earlier_orders():
+    """context_order="trie": a prompt whose chunk set has a leading order an earlier prompt
+    already used (same or earlier batch) takes that order; otherwise popularity order."""
+    import torch
+
+    from docqa_amd.pipeline.rag import RAGPipeline
+    from docqa_amd.text.tokenizer import ChatTokenizer
+
+    tok = ChatTokenizer(model_vocab=128256)
+    meta = [{"text_content": f"Note {i}.", "source": f"s{i}"} for i in range(10)]
+
+    class _Eng:
+        device = torch.device("cpu")
+
+    p = RAGPipeline(None, None, None, meta, _Eng(), tok, context_order="trie")
+    assert p._ordered([[3, 7, 1]]) == [[1, 3, 7]]              # no history: popularity, ids
+    # batch popularity (5 and 8 twice) leads; the second prompt shares the pair (5, 8)
+    assert p._ordered([[5, 8, 2], [8, 6, 5]]) == [[5, 8, 2], [5, 8, 6]]
+    # a later batch: id / popularity order would be (2, 5, 8); the order an earlier prompt
+    # used -- whose KV the prefix cache holds -- wins
+    assert p._ordered([[2, 8, 5]]) == [[5, 8, 2]]
+    assert p._ordered([[1, 9, 3]]) == [[1, 3, 9]]              # longest known prefix (1, 3)
+    rel = RAGPipeline(None, None, None, meta, _Eng(), tok)     # reference template default
+    assert rel.context_order == "relevance"
+
+
+def test_shipped_tokenizer_vocabularies(monkeypatch, tmp_path):
+    """The trained vocabularies ship with the package and are loaded in preference to a
+    training run, so every machine tokenises (and retrieves, and prompts) identically."""
+    import json
+
+    from docqa_amd.text import tokenizer as T
+
+    for name in ("wordpiece-30522.json", "chatbpe-32000.json"):
+        f = T._ASSETS / name
+        assert f.exists(), f
+        json.loads(f.read_text())
+    monkeypatch.setattr(T, "_CACHE", tmp_path / "none")        # no build-dir cache to fall back on
+    monkeypatch.setattr(T, "_instances", {})
+    monkeypatch.delenv("DOCQA_WORDPIECE_JSON", raising=False)
+    trained = []
+    monkeypatch.setattr(T, "_train_wordpiece", lambda v: trained.append(v))
+    wp = T.WordPieceTokenizer()
+    assert not trained and wp.vocab_size > 1000
+    assert wp.tok.to_str() == T.Tokenizer.from_file(str(T._ASSETS / "wordpiece-30522.json")).to_str()
