@@ -166,7 +166,10 @@ def _identity_groups(bp: int, dev, hkv: int = 8) -> torch.Tensor:
         # persistent / deferred plans: every quad writes a partial that the merge kernel
         # folds with the prefix (nothing may read the forked prefix kernel's partials)
         all_partial = persist or _defer_groups_on()
-        g = torch.full((3 if persist else 2, max(bp, 1), 8), -1, dtype=torch.int32)
+        # plan rows (work items): DOCQA_GROUP_CAP_MULT x the bucket; a plan that does not fit
+        # doubles its tiles per item (ops.split_decode_groups)
+        rows = max(bp, 1) * max(1, int(os.environ.get("DOCQA_GROUP_CAP_MULT", "1")))
+        g = torch.full((3 if persist else 2, rows, 8), -1, dtype=torch.int32)
         g[:2, :, 4:] = 0
         g[0, :, 6] = -1
         nq = (bp + 3) // 4
@@ -473,6 +476,9 @@ class LLMEngine:
                                            defer=_defer_groups_on())
             _upload(g.groups, plan)
             g.groups_key = key
+            if os.environ.get("DOCQA_GROUP_PLAN_LOG", "0") == "1":
+                used = int((plan[0, :, :4] >= 0).any(1).sum())
+                print(f"[group plan] bp {g.bp} groups {len(quads)} items {used} cap {cap}", flush=True)
             return
         cap = g.groups.numel() // 4
         quads = ops.pack_decode_groups(tables, lens, skip, self.block_size, cap)
