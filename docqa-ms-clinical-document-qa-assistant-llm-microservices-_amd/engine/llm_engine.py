@@ -471,7 +471,10 @@ class LLMEngine:
             if _inline_prefix_on() and not _defer_groups_on() and g.groups.shape[0] == 2:
                 skip = 0   # the kernel attends the shared prefix inside each group
             plan = ops.split_decode_groups(quads, tables, lens, skip, self.block_size, cap,
-                                           int(os.environ.get("DOCQA_GROUP_TILES", "12")),
+                                           # 40: ~130 items per KV head at the bench's batch 256 (12
+                                           # overflowed the 256-item plan and doubled to 24 tiles, ~200
+                                           # items: 1.5 % fewer q/s, profiles/r4_group_plan_tiles_sweep.log)
+                                           int(os.environ.get("DOCQA_GROUP_TILES", "40")),
                                            bins=ops.persist_bins(cap, self.model.hkv) if g.groups.shape[0] == 3 else 0,
                                            defer=_defer_groups_on())
             _upload(g.groups, plan)
