@@ -470,13 +470,34 @@ class LLMEngine:
             quads = ops.pack_decode_groups(tables, lens, skip, self.block_size, (g.bp + 1) // 2)
             if _inline_prefix_on() and not _defer_groups_on() and g.groups.shape[0] == 2:
                 skip = 0   # the kernel attends the shared prefix inside each group
-            plan = ops.split_decode_groups(quads, tables, lens, skip, self.block_size, cap,
-                                           # 40: ~130 items per KV head at the bench's batch 256 (12
-                                           # overflowed the 256-item plan and doubled to 24 tiles, ~200
-                                           # items: 1.5 % fewer q/s, profiles/r4_group_plan_tiles_sweep.log)
-                                           int(os.environ.get("DOCQA_GROUP_TILES", "40")),
-                                           bins=ops.persist_bins(cap, self.model.hkv) if g.groups.shape[0] == 3 else 0,
-                                           defer=_defer_groups_on())
+            bins = ops.persist_bins(cap, self.model.hkv) if g.groups.shape[0] == 3 else 0
+
+            def split(tiles):
+                return ops.split_decode_groups(quads, tables, lens, skip, self.block_size, cap, tiles,
+                                               bins=bins, defer=_defer_groups_on())
+
+            tiles = os.environ.get("DOCQA_GROUP_TILES", "auto")
+            if tiles == "auto":
+                # the tiles-per-item budget whose plan has the most items, at most
+                # DOCQA_GROUP_ITEMS per KV head: ~1.4 rounds of the chip's 96 workgroup slots per head.  At the bench's
+                # batch 256 that is 40 tiles, ~130 items (12 -- which overflowed the plan into
+                # 24-tile items, ~200 -- ran 1.5 % fewer q/s; 20-32 and 56 slower too:
+                # profiles/r4_group_plan_tiles_sweep.log); smaller buckets keep smaller items,
+                # so their few groups still fill the chip
+                # (a budget whose plan overflows the rows comes back doubled, so take the plan
+                # with the MOST items within the target rather than the first that fits:
+                # batch 64 / 128 run best at 54 / 106 items, 12 tiles)
+                target = int(os.environ.get("DOCQA_GROUP_ITEMS", "132"))
+                plan, best = None, -1
+                for budget in (8, 12, 16, 24, 32, 40, 48, 64, 96, 128):
+                    p = split(budget)
+                    n = int((p[0, :, :4] >= 0).any(1).sum())
+                    if n <= target and n > best:
+                        plan, best = p, n
+                if plan is None:
+                    plan = split(128)
+            else:
+                plan = split(int(tiles))
             _upload(g.groups, plan)
             g.groups_key = key
             if os.environ.get("DOCQA_GROUP_PLAN_LOG", "0") == "1":
