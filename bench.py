@@ -71,6 +71,9 @@ def main() -> None:
     ap.add_argument("--template", choices=("cache_friendly", "reference"), default=None,
                     help="QA prompt template (docqa_amd/prompts.py; default: env QA_TEMPLATE, else "
                          "cache_friendly: the headline workload of rounds 2-4, named in the JSON line)")
+    ap.add_argument("--check-retrieval", action="store_true",
+                    help="after the timed region, check every rank's sharded top-k against an unsharded "
+                         "flat search over the whole corpus (exit 3 on a mismatch); untimed")
     a = ap.parse_args()
     os.environ["QA_TEMPLATE"] = a.template or os.environ.get("QA_TEMPLATE", "cache_friendly")
 
@@ -148,6 +151,8 @@ def main() -> None:
     sync()
     elapsed = time.perf_counter() - t0
 
+    retrieval = check_retrieval(pipe, batch_for(a.warmup), sync) if a.check_retrieval else None
+
     t = torch.tensor([elapsed] + step_times, dtype=torch.float64, device=dev)
     if dist.is_initialized():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -213,12 +218,54 @@ def main() -> None:
                 "context_order": pipe.context_order,
             },
         }
+        if retrieval is not None:
+            out["retrieval_check"] = retrieval
         if cuda:   # the box: CU count and clocks differ between pool machines
             pr = torch.cuda.get_device_properties(local_rank)
             out["device"] = {"name": pr.name, "cus": pr.multi_processor_count,
                              "gcn_arch": getattr(pr, "gcnArchName", "")}
         print(json.dumps(out), flush=True)
     comm.destroy()
+    if retrieval is not None and retrieval["bad_rows_max_over_ranks"]:
+        sys.exit(3)
+
+
+def check_retrieval(pipe, questions: list[str], sync) -> dict:
+    """The sharded search (IPC gathers + merge, whatever the world size) against ONE exact
+    flat L2 index over every record, on the same questions: each row's k distances must
+    match, and each returned id's true distance must equal its reported one (duplicated
+    KB rows make ids of equal distance interchangeable, so ids are checked by distance).
+    Collective: every rank calls it.  Reference: the k=3 retrieval of llm-qa/main.py:101."""
+    import torch
+    import torch.distributed as dist
+
+    from docqa_amd.index.flat import FlatIndex
+    from docqa_amd.pipeline.corpus import embed_records
+
+    k = pipe.k
+    dev = pipe.engine.device
+    full_x = embed_records(pipe.encoder, pipe.enc_tok, pipe.metadata).float()
+    full = FlatIndex(full_x.shape[1], "l2", dev, torch.float32, capacity=max(1024, full_x.shape[0]))
+    full.add(full_x)
+    q = pipe.embed(questions).float()
+    Ds, Is = pipe.index.search(q, k)
+    ids = pipe._host_ids(Is)                     # raises on a failed IPC gather
+    Df, _ = full.search(q, k)
+    sync()
+    Ds, Df = Ds.float().cpu(), Df.float().cpu()
+    xs = full_x.cpu()
+    qc = q.cpu()
+    bad = 0
+    for r, row in enumerate(ids):
+        true = torch.stack([((qc[r] - xs[i]) ** 2).sum() if 0 <= i < xs.shape[0] else torch.tensor(float("inf"))
+                            for i in row])
+        tol = 1e-3 * (1.0 + Df[r].abs().max())
+        if not (torch.allclose(Ds[r], Df[r], atol=tol) and torch.allclose(true, Ds[r], atol=tol)):
+            bad += 1
+    t = torch.tensor([bad], dtype=torch.int64, device=dev)
+    if dist.is_initialized():
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return {"rows": len(ids), "k": k, "bad_rows_max_over_ranks": int(t.item())}
 
 
 if __name__ == "__main__":

@@ -61,6 +61,7 @@ class InProcChannel:
         self._consumers: list[tuple[str, Callable]] = []
         self._stop = threading.Event()
         self._lock = threading.Condition()
+        self._timers: list[tuple[float, Callable]] = []
 
     # --- pika-shaped API
     def queue_declare(self, queue: str, durable: bool = True, **_):
@@ -95,11 +96,26 @@ class InProcChannel:
             self.broker._journal_ack(q, mid)
             self.broker.publish(q + ".dlq", body)
 
+    def call_later(self, delay: float, fn: Callable) -> None:
+        """Run ``fn()`` on the consuming thread after ``delay`` seconds (pika's
+        ``BlockingConnection.call_later``): consumer-side timers need no locking."""
+        self._timers.append((time.monotonic() + delay, fn))
+
+    def _run_timers(self) -> None:
+        if not self._timers:
+            return
+        now = time.monotonic()
+        due = [t for t in self._timers if t[0] <= now]
+        if due:
+            self._timers = [t for t in self._timers if t[0] > now]
+            for _, fn in due:
+                fn()
+
     def start_consuming(self):
         """Blocking dispatch loop (one thread per channel, like pika's BlockingChannel)."""
         while not self._stop.is_set():
-            if not self._dispatch_one(timeout=0.05):
-                continue
+            self._dispatch_one(timeout=0.02 if self._timers else 0.05)
+            self._run_timers()
 
     def stop_consuming(self):
         self._stop.set()
@@ -375,6 +391,10 @@ class _AmqpChannel:
 
     def __getattr__(self, name):
         return getattr(self._ch, name)
+
+    def call_later(self, delay: float, fn):  # pragma: no cover - needs a broker
+        """Timer on the connection's own thread (runs inside ``start_consuming``)."""
+        self._conn.call_later(delay, fn)
 
     def close(self):  # pragma: no cover - needs a broker
         try:

@@ -15,6 +15,15 @@ xGMI links at once, graph-capturable, off RCCL) when ``enable_ipc`` succeeded; R
 gloo ``all_gather`` is the fallback (CPU, or a node without IPC).  Shards may be any size
 (the count-exchange path carries explicit counts).
 
+Failure surfacing: the IPC gather gives up on a peer after a bounded wait and records it
+in a sticky error word instead of hanging the GPU; its results are then stale.  Every
+search through the IPC path snapshots that word behind its kernels (no extra sync) and
+``check_gather()`` -- called by the pipeline right after its existing host sync on the
+hits -- raises :class:`CollectiveError`, so a late or dead rank can never turn into
+silently wrong retrieval.  Data-parallel ranks are not in lockstep (EOS-dependent batch
+lengths, the pipelined lead, first-call setup), so the shard gathers wait up to
+``DOCQA_SHARD_GATHER_TIMEOUT_MS`` (default 60 s) rather than the TP all-reduce's 500 ms.
+
 Reference parity: no distributed index exists in the reference (one FAISS file,
 semantic-indexer/indexer.py:17-18); this is the config-5 "index sharded across 8 GPUs".
 """
@@ -49,6 +58,7 @@ class ShardedIndex:
         self._offset = 0
         self._ntotal = local.ntotal
         self._ipc = None
+        self._snap = None          # error-word snapshot of the last IPC search
         self.refresh()
 
     def enable_ipc(self, max_bytes: int = 16 << 20) -> bool:
@@ -58,8 +68,12 @@ class ShardedIndex:
             return self._ipc is not None
         from ..parallel.custom_ar import CustomAllReduce
 
+        import os
+
+        timeout_ms = float(os.environ.get("DOCQA_SHARD_GATHER_TIMEOUT_MS", "60000"))
         try:
-            self._ipc = CustomAllReduce(group=self.group, max_bytes=max_bytes, device=self.local.device)
+            self._ipc = CustomAllReduce(group=self.group, max_bytes=max_bytes, device=self.local.device,
+                                        timeout_ms=timeout_ms)
         except Exception as e:  # noqa: BLE001 - collective decision inside the constructor
             print(f"[sharded] IPC all-gather unavailable ({e}); using the process group", flush=True)
             self._ipc = None
@@ -71,6 +85,7 @@ class ShardedIndex:
         if self._ipc is not None and t.is_cuda:
             nb = t.numel() * t.element_size()
             if nb % 16 == 0 and nb // 2 <= self._ipc.max_elems:
+                self._used_ipc = True
                 return self._ipc.all_gather_raw(t)
         parts = [torch.empty_like(t) for _ in range(self.world)]
         dist.all_gather(parts, t, group=self.group)
@@ -100,10 +115,27 @@ class ShardedIndex:
     def id_offset(self) -> int:
         return self._offset
 
+    def check_gather(self) -> None:
+        """Raise :class:`~docqa_amd.parallel.custom_ar.CollectiveError` if a peer never
+        arrived at the last search's IPC gathers.  Call after a host sync that covers the
+        search (e.g. ``I.tolist()`` on the search's stream): the snapshot copy was queued
+        behind the gathers, so it is complete by then and reading it costs nothing."""
+        snap, self._snap = self._snap, None
+        if snap is not None and self._ipc is not None:
+            self._ipc.raise_if(snap)
+
     def search(self, xq: torch.Tensor, k: int, **kw):
         xq = xq.to(self.local.device, dtype=torch.float32)
         if self.world == 1:
             return self.local.search(xq, k, **kw)
+        self._used_ipc = False
+        D, I = self._search(xq, k, **kw)
+        if self._used_ipc:
+            # stream-ordered copy of the sticky error word behind this search's gathers
+            self._snap = self._ipc.snapshot()
+        return D, I
+
+    def _search(self, xq: torch.Tensor, k: int, **kw):
         nq = xq.shape[0]
         dev = xq.device
         if self.replicated:

@@ -520,9 +520,20 @@ class LlamaModel:
 
     def _decode_tick(self, B: int):
         """Ticket words for the fused decode attention's in-kernel partition merge, shared
-        by every layer (the launches are stream-ordered and each re-arms its words)."""
-        if self._tick is None or self._tick.numel() < B * self.hkv:
-            self._tick = ops.decode_ticket(max(B, 512) * self.hkv, self.device)
+        by every layer (the launches are stream-ordered and each re-arms its words).  The
+        grouped kernel indexes them by plan row, and a plan holds up to
+        bucket x DOCQA_GROUP_CAP_MULT rows (engine/llm_engine.py), so the buffer is sized for
+        the largest bucket x that multiple ONCE, before any graph is captured, and never
+        reallocated: a captured graph keeps pointing at it."""
+        import os
+
+        mult = max(1, int(os.environ.get("DOCQA_GROUP_CAP_MULT", "1")))
+        need = max(B, 1) * mult * self.hkv
+        if self._tick is None:
+            self._tick = ops.decode_ticket(max(B, 4096) * mult * self.hkv, self.device)
+        if self._tick.numel() < need:
+            raise RuntimeError(f"decode ticket buffer holds {self._tick.numel()} words, a {B}-row bucket "
+                               f"needs {need}: raise the first bucket size (buffers are never regrown)")
         return self._tick
 
     def _glu_workspace(self, N: int, K: int):

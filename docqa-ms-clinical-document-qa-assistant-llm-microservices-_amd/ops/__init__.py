@@ -992,9 +992,13 @@ def fp32_matmul_nt(x, w):
 def coarse_probes(xq, centroids, cnorm, nprobe: int):
     """IVF coarse quantizer: int64 [nq, nprobe] nearest centroids by squared L2, ascending,
     ties to the lower centroid id.  GPU: csrc/kernels/coarse.hip (MFMA fp32 distances +
-    radix select, nprobe <= 512); nprobe <= 64 may also use :func:`knn`."""
-    if _gpu(xq):
-        return _native().coarse_probes(xq.float().contiguous(), centroids, cnorm, int(nprobe))
+    radix select, nprobe <= 512); nprobe <= 64 may also use :func:`knn`.  Shapes outside
+    the kernel's envelope (nprobe > 512, d > 1280 or d % 8 != 0 -- recall sweeps, wide
+    embeddings) take the fp32 reference on the same device instead of failing."""
+    d = int(centroids.shape[1])
+    nprobe = int(min(int(nprobe), int(centroids.shape[0])))
+    if _gpu(xq) and nprobe <= 512 and d % 8 == 0 and d <= 1280:
+        return _native().coarse_probes(xq.float().contiguous(), centroids, cnorm, nprobe)
     return ref.coarse_probes(xq, centroids, cnorm, nprobe)
 
 

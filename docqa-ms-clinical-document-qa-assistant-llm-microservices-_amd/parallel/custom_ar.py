@@ -46,7 +46,7 @@ def _agree(ok: bool, group, device) -> bool:
 
 class CustomAllReduce:
     def __init__(self, group=None, max_bytes: int = 64 << 20, device=None,
-                 oneshot_max_bytes: int | None = None):
+                 oneshot_max_bytes: int | None = None, timeout_ms: float | None = None):
         from .. import ops
 
         ops.load_native()
@@ -66,7 +66,11 @@ class CustomAllReduce:
         # within microseconds; several processes on ONE GPU (tests, --share-gpu) must run
         # with GPU_MAX_HW_QUEUES=1 or a rank's queue may stay unmapped while the others spin
         # (allreduce.hip header; profiles/r4_ar_skew_*)
-        self.timeout_us = int(float(os.environ.get("DOCQA_AR_TIMEOUT_MS", "500")) * 1000)
+        # ``timeout_ms`` overrides it per instance: the data-parallel shard gathers
+        # (index/sharded.py) meet ranks that are NOT in lockstep and wait much longer
+        if timeout_ms is None:
+            timeout_ms = float(os.environ.get("DOCQA_AR_TIMEOUT_MS", "500"))
+        self.timeout_us = int(float(timeout_ms) * 1000)
         # every rank runs the same collective sequence whatever fails locally, so a failure
         # on one rank becomes the same decision on all of them (no rank left in a barrier)
         self.own, self.regions, self._opened = 0, [], []

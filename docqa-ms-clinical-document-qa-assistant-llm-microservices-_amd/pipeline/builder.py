@@ -65,5 +65,11 @@ def build_stack(sc: StackConfig, device="cuda", log=print) -> tuple[RAGPipeline,
     info["kv_blocks"] = engine.kv.allocator.num_blocks if hasattr(engine.kv.allocator, "num_blocks") else None
     pipe = RAGPipeline(encoder, enc_tok, index, records, engine, chat_tok, k=sc.k,
                        max_prompt_tokens=sc.max_context - 256)
+    if s.dp_size > 1:
+        # every rank has finished its (seconds-long, rank-skewed) weight init and KV pool
+        # before any rank enters the first search: the shard gathers start aligned
+        if device != "cpu" and torch.device(device).type == "cuda":
+            torch.cuda.synchronize()
+        comm.barrier()
     info["setup_s"] = time.perf_counter() - t0
     return pipe, info

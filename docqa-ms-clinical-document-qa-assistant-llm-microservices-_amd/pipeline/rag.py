@@ -100,6 +100,16 @@ class RAGPipeline:
     def embed(self, texts: list[str]) -> torch.Tensor:
         return self.encoder.encode(self.enc_tok.encode_batch(texts))
 
+    def _host_ids(self, I: torch.Tensor) -> list[list[int]]:
+        """Hits to the host (the batch's one sync on the search stream), then surface a
+        failed cross-rank gather of a sharded index (index/sharded.py) as an exception
+        instead of serving stale peer rows."""
+        ids = I.tolist()
+        check = getattr(self.index, "check_gather", None)
+        if check is not None:
+            check()
+        return ids
+
     def retrieve(self, questions: list[str]):
         q = self.embed(questions)
         D, I = self.index.search(q, self.k)
@@ -194,7 +204,7 @@ class RAGPipeline:
         t1 = time.perf_counter()
         with tracing.span("rag.search", n=len(questions), k=self.k):
             D, I = self.index.search(qemb, self.k)
-            I = I.tolist()  # host needs ids to assemble the prompts
+            I = self._host_ids(I)  # host needs ids to assemble the prompts
         t2 = time.perf_counter()
         with tracing.span("rag.prompt", n=len(questions)):
             prompts = self.build_prompts(questions, I)
@@ -235,13 +245,13 @@ class RAGPipeline:
                 evs[1].record(stream)
                 _, I = self.index.search(qemb, self.k)
                 evs[2].record(stream)
-                I = I.tolist()       # waits for this side stream only
+                I = self._host_ids(I)       # waits for this side stream only
             host = None
         else:
             qemb = self.embed(questions)
             tm = time.perf_counter()
             _, I = self.index.search(qemb, self.k)
-            I = I.tolist()
+            I = self._host_ids(I)
             host = (tm - t0, time.perf_counter() - tm)
         t1 = time.perf_counter()
         with tracing.span("rag.prompts", n=len(questions)):

@@ -13,13 +13,18 @@ while more raw messages are already queued, the callback only collects them; the
 then de-identified by ONE packed NER forward (:meth:`process_messages`: every window of
 every document in one varlen encoder pass + the fused token-classification argmax),
 published and acked together.  An idle queue flushes at once, so a single document is
-not delayed.  A batch whose forward fails is retried one message at a time, so only a
-poison message is dead-lettered.
+not delayed, and a partial batch held while others were queued is flushed by a timer on
+the consuming thread after ``DEID_FLUSH_MS`` (default 50 ms) even if no further delivery
+arrives (a competing consumer took the rest).  Held messages belong to one channel: a
+reconnect drops them (the broker redelivers the unacked ones) rather than acking or
+publishing on a dead channel.  A batch whose forward fails is retried one message at a
+time, so only a poison message is dead-lettered.
 """
 from __future__ import annotations
 
 import json
 import logging
+import os
 import threading
 import time
 
@@ -44,6 +49,9 @@ class DeidWorker:
         self.batches = 0
         self.batch_docs = max(1, int(getattr(self.st, "deid_batch_docs", 1)))
         self._pending: list = []
+        self._pending_t0 = 0.0
+        self._timer_armed = False
+        self.flush_s = float(os.environ.get("DEID_FLUSH_MS", "50")) / 1e3
         self._depth = getattr(self.broker, "depth", None)
 
     def clean_message(self, message: dict, masked: str) -> dict:
@@ -57,12 +65,34 @@ class DeidWorker:
     def callback(self, ch, method, properties, body):
         """Queue consumer: collect while more raw messages are waiting (up to
         ``batch_docs``), then de-identify the batch in one packed forward."""
+        if self._pending and self._pending[0][0] is not ch:
+            self._pending = []          # held on a channel that is gone: redelivered by the broker
+        if not self._pending:
+            self._pending_t0 = time.monotonic()
         self._pending.append((ch, method, body))
         waiting = self._depth(self.in_q) if self._depth is not None else 0
         if waiting > 0 and len(self._pending) < self.batch_docs:
+            if not self._timer_armed and hasattr(ch, "call_later"):
+                self._timer_armed = True
+                ch.call_later(self.flush_s, self._flush_stale)
             return
         batch, self._pending = self._pending, []
         self._flush(batch)
+
+    def _flush_stale(self) -> None:
+        """Timer (consuming thread): flush a partial batch that has waited ``flush_s``;
+        re-arm while a younger one is still being collected."""
+        self._timer_armed = False
+        if not self._pending:
+            return
+        age = time.monotonic() - self._pending_t0
+        ch = self._pending[0][0]
+        if age >= self.flush_s * 0.999:
+            batch, self._pending = self._pending, []
+            self._flush(batch)
+        elif hasattr(ch, "call_later"):
+            self._timer_armed = True
+            ch.call_later(self.flush_s - age, self._flush_stale)
 
     def _flush(self, batch: list) -> None:
         good = []
@@ -109,6 +139,9 @@ class DeidWorker:
             try:
                 ch = self.broker.channel()
                 self._ch = ch
+                # messages held on the previous channel are unacked there: the broker
+                # redelivers them, so never ack / publish them through a dead channel
+                self._pending, self._timer_armed = [], False
                 ch.queue_declare(queue=self.in_q, durable=True)
                 # the reference's prefetch 1 unless this broker can report queue depth (then
                 # a window of batch_docs lets the callback drain a burst into one forward)

@@ -260,7 +260,7 @@ class ContinuousBatcher:
             qs = [it[1] for it in asks]
             qemb = pipe.embed(qs)
             _, I = pipe.index.search(qemb, pipe.k)
-            I = I.tolist()
+            I = pipe._host_ids(I)
             prompts = pipe.build_prompts(qs, I)
             te = time.perf_counter()
             m = self.metrics

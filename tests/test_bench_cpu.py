@@ -44,11 +44,12 @@ def test_bench_two_ranks_gloo_sharded_index():
         env.pop(k, None)
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
            "--master-addr", "127.0.0.1", "--master-port", str(_port()), str(ROOT / "bench.py"),
-           "--gpus", "2", *ARGS]
+           "--gpus", "2", *ARGS, "--check-retrieval"]
     r = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=900, env=env)
     assert r.returncode == 0, r.stderr[-3000:]
     d = _last_json(r.stdout)
     assert d["n_gpus"] == 2 and d["config"]["global_batch"] == 6 and d["config"]["parallelism"] == "dp2"
+    assert d["retrieval_check"] == {"rows": 3, "k": 3, "bad_rows_max_over_ranks": 0}
 
 
 def test_bench_eight_ranks_gloo_sharded_index():
@@ -61,12 +62,13 @@ def test_bench_eight_ranks_gloo_sharded_index():
     env["OMP_NUM_THREADS"] = "1"
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "8",
            "--master-addr", "127.0.0.1", "--master-port", str(_port()), str(ROOT / "bench.py"),
-           "--gpus", "8", *ARGS]
+           "--gpus", "8", *ARGS, "--check-retrieval"]
     r = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=900, env=env)
     assert r.returncode == 0, r.stderr[-3000:]
     d = _last_json(r.stdout)
     assert d["n_gpus"] == 8 and d["config"]["global_batch"] == 24 and d["config"]["parallelism"] == "dp8"
     assert d["value"] > 0 and d["workload"]["unique_question_frac"] == 1.0
+    assert d["retrieval_check"]["bad_rows_max_over_ranks"] == 0
 
 
 def test_pipeline_bench_tp2_gloo_sharded_index():

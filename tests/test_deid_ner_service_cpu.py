@@ -104,3 +104,33 @@ def test_settings_ner_switch(monkeypatch):
     monkeypatch.setenv("DEID_NER", "1")
     monkeypatch.delenv("NER_CHECKPOINT")
     assert Settings().ner_enabled() is True             # forced on (random-init weights)
+
+
+def test_deid_worker_partial_batch_flushed_by_timer():
+    """a message held because others were queued must not wait for a delivery
+    that never comes (a competing consumer took the rest): the consuming thread's timer
+    flushes it after DEID_FLUSH_MS.  A reconnect drops messages held on the old channel."""
+    st = Settings()
+    st.deid_batch_docs = 8
+    broker = InProcBroker()
+    w = DeidWorker(DeidEngine(), st, broker)
+    w.flush_s = 0.05
+    broker.publish(st.raw_queue, json.dumps({"doc_id": 1, "text": "Appeler le 06 12 34 56 78"}).encode())
+    broker.publish(st.raw_queue, json.dumps({"doc_id": 2, "text": "x"}).encode())
+    ch = broker.channel()
+    ch.basic_qos(prefetch_count=8)
+    ch.queue_declare(st.raw_queue)
+    ch.basic_consume(queue=st.raw_queue, on_message_callback=w.callback)
+    assert ch._dispatch_one(timeout=0.5)          # doc 1 arrives while doc 2 is still queued
+    assert len(w._pending) == 1 and w._timer_armed
+    assert broker._get(st.raw_queue, timeout=0.5) is not None   # a competing consumer takes doc 2
+    time.sleep(0.08)
+    ch._run_timers()
+    assert w._pending == [] and w.processed == 1
+    out = _drain(broker, st.clean_queue, 1, timeout=5)
+    assert out[0]["doc_id"] == 1 and "<PHONE_NUMBER>" in out[0]["original_text_masked"]
+    # held on a channel that then went away: the next delivery (new channel) drops it
+    w._pending = [(object(), None, b"{}")]
+    broker.publish(st.raw_queue, json.dumps({"doc_id": 3, "text": "y"}).encode())
+    assert ch._dispatch_one(timeout=0.5)
+    assert w.processed == 2 and w._pending == []

@@ -93,6 +93,26 @@ def test_coarse_probes_match_cpu_order(nlist, d, nq, nprobe):
     assert exact > 0.99
 
 
+@pytest.mark.parametrize("nlist,d,nprobe", [(2048, 64, 1024), (512, 1536, 16), (300, 100, 8)])
+def test_coarse_probes_outside_kernel_envelope(nlist, d, nprobe):
+    """nprobe > 512, d > 1280 or d % 8 != 0 fall back to the fp32 reference on
+    the device instead of tripping the binding's TORCH_CHECK; the probe sets match."""
+    from docqa_amd import ops
+    from docqa_amd.ops import reference as R
+
+    assert ops.load_native()
+    g = torch.Generator().manual_seed(nlist + d)
+    cent = torch.randn(nlist, d, generator=g)
+    xq = torch.randn(7, d, generator=g)
+    cn = (cent ** 2).sum(1)
+    got = ops.coarse_probes(xq.cuda(), cent.cuda(), cn.cuda(), nprobe)
+    assert got.is_cuda and got.shape == (7, nprobe)
+    want = R.coarse_probes(xq.double(), cent.double(), cn.double(), nprobe)
+    for q in range(7):
+        inter = len(set(got[q].cpu().tolist()) & set(want[q].tolist()))
+        assert inter >= nprobe - 2
+
+
 def test_coarse_probes_ties_to_lower_id():
     from docqa_amd import ops
 
