@@ -820,94 +820,7 @@ at::Tensor mgemm_glu(const at::Tensor& x, const at::Tensor& w, int64_t cfg) {
   return out;
 }
 
-// the same with the K range split over S = 1 / 2 workgroups per tile meeting in the launch
-// (mgemm.hip glu_meet); ws fp32 [m-tiles x N x 256], tick int32 [2 T + 1] (T = m-tiles x
-// N / tile_n, then the sticky error word), tickets zeroed once and re-armed by the kernel
-at::Tensor mgemm_glu_split(const at::Tensor& x, const at::Tensor& w, int64_t splits, int64_t cfg,
-                           const c10::optional<at::Tensor>& ws, const c10::optional<at::Tensor>& tick) {
-  CHECK_GPU(x); CHECK_BF16(x); CHECK_BF16(w); CHECK_CONTIG(x); CHECK_CONTIG(w);
-  CHECK_ALIGN16(x); CHECK_ALIGN16(w);
-  const int K = x.size(-1), N = w.size(0);
-  TORCH_CHECK(w.size(1) == K && N % 16 == 0, "mgemm_glu_split: shape mismatch");
-  TORCH_CHECK(splits == 1 || splits == 2, "mgemm_glu_split: splits 1 or 2");
-  const int M = x.numel() / K;
-  float* wsp = nullptr;
-  int* tk = nullptr;
-  int* err = nullptr;
-  if (splits == 2) {
-    TORCH_CHECK(ws.has_value() && tick.has_value(), "mgemm_glu_split: splits 2 needs ws and tick");
-    CHECK_GPU(*ws); CHECK_GPU(*tick); CHECK_I32(*tick); CHECK_CONTIG(*ws); CHECK_CONTIG(*tick);
-    TORCH_CHECK(ws->scalar_type() == at::kFloat, "mgemm_glu_split: ws must be fp32");
-    const int bn = docqa_mgemm_tile_n((int)cfg);
-    TORCH_CHECK(bn > 0 && N % bn == 0, "mgemm_glu_split: N must be a multiple of the tile");
-    const int64_t mt = (M + 255) / 256, tiles = mt * (N / bn);
-    TORCH_CHECK(ws->numel() >= mt * N * 256 && tick->numel() >= 2 * tiles + 1, "mgemm_glu_split: workspace too small");
-    wsp = ws->data_ptr<float>();
-    tk = tick->data_ptr<int>();
-    err = tk + 2 * tiles;
-  }
-  auto sizes = x.sizes().vec();
-  sizes.back() = N / 2;
-  c10::DeviceGuard g(x.device());
-  auto out = at::empty(sizes, x.options());
-  CHECK_RC(docqa_mgemm_glu_split(x.data_ptr(), w.data_ptr(), out.data_ptr(), wsp, tk, err, M, N, K, (int)splits,
-                                 (int)cfg, stream()), "mgemm_glu_split");
-  return out;
-}
-
 int64_t mgemm_tile_n(int64_t cfg) { return docqa_mgemm_tile_n((int)cfg); }
-
-// persistent decode-layer chain (TP = 1, 193..512 rows): attn [M, Ko] -> residual updated in
-// place twice, returns (x2 [M, H] = the next layer's normed input, the next layer's QKV
-// split-K slabs [S_q, M, Nq] or an empty tensor when w_qkv is None)
-std::tuple<at::Tensor, at::Tensor> mgemm_chain(const at::Tensor& attn, const at::Tensor& w_o, at::Tensor residual,
-                                               const at::Tensor& post_norm, const at::Tensor& w_gu,
-                                               const at::Tensor& w_down, const at::Tensor& next_norm,
-                                               const c10::optional<at::Tensor>& w_qkv, at::Tensor counters,
-                                               int64_t S_o, int64_t cfg_o, int64_t S_d, int64_t cfg_d, int64_t S_q,
-                                               int64_t cfg_q, double eps, const c10::optional<at::Tensor>& trace) {
-  for (const at::Tensor* t : {&attn, &w_o, (const at::Tensor*)&residual, &post_norm, &w_gu, &w_down, &next_norm}) {
-    CHECK_GPU(*t); CHECK_BF16(*t); CHECK_CONTIG(*t); CHECK_ALIGN16(*t);
-  }
-  CHECK_GPU(counters); CHECK_I32(counters); CHECK_CONTIG(counters);
-  TORCH_CHECK(counters.numel() >= 16, "mgemm_chain: counters need 16 int32");
-  const int Ko = attn.size(-1), M = attn.numel() / Ko, H = w_o.size(0), N2I = w_gu.size(0);
-  TORCH_CHECK(w_o.size(1) == Ko && residual.numel() == (int64_t)M * H && w_gu.size(1) == H &&
-              w_down.size(0) == H && w_down.size(1) == N2I / 2 && post_norm.numel() == H && next_norm.numel() == H,
-              "mgemm_chain: shape mismatch");
-  c10::DeviceGuard g(attn.device());
-  auto fo = attn.options().dtype(at::kFloat);
-  auto p_o = at::empty({S_o, M, H}, fo);
-  auto x1 = at::empty({M, H}, attn.options());
-  auto gl = at::empty({M, N2I / 2}, attn.options());
-  auto p_d = at::empty({S_d, M, H}, fo);
-  auto x2 = at::empty({M, H}, attn.options());
-  at::Tensor p_q;
-  const void* wq = nullptr;
-  int Nq = 0;
-  if (w_qkv.has_value()) {
-    const at::Tensor& w = *w_qkv;
-    CHECK_GPU(w); CHECK_BF16(w); CHECK_CONTIG(w); CHECK_ALIGN16(w);
-    TORCH_CHECK(w.size(1) == H, "mgemm_chain: w_qkv shape");
-    Nq = w.size(0);
-    wq = w.data_ptr();
-    p_q = at::empty({S_q, M, Nq}, fo);
-  } else {
-    p_q = at::empty({0}, fo);
-  }
-  if (trace.has_value())
-    TORCH_CHECK(trace->is_cuda() && trace->scalar_type() == at::kLong && trace->numel() >= 6 * 4096,
-                "mgemm_chain: trace needs int64 [>= 6 x 4096] on the GPU");
-  CHECK_RC(docqa_mgemm_chain(attn.data_ptr(), w_o.data_ptr(), p_o.data_ptr<float>(), residual.data_ptr(),
-                             post_norm.data_ptr(), x1.data_ptr(), w_gu.data_ptr(), gl.data_ptr(), w_down.data_ptr(),
-                             p_d.data_ptr<float>(), next_norm.data_ptr(), x2.data_ptr(), wq,
-                             wq ? p_q.data_ptr<float>() : nullptr, counters.data_ptr<int>(),
-                             trace.has_value() ? (long long*)trace->data_ptr<int64_t>() : nullptr, M, H, Ko, N2I, Nq,
-                             (int)S_o, (int)cfg_o, (int)S_d, (int)cfg_d, (int)S_q, (int)cfg_q, (float)eps,
-                             stream()),
-           "mgemm_chain");
-  return {x2, p_q};
-}
 
 // LM head + greedy pick: argmax over the first n_valid columns of bf16(x . w^T) -> int64 [M]
 at::Tensor mgemm_argmax(const at::Tensor& x, const at::Tensor& w, int64_t n_valid, int64_t cfg) {
@@ -941,92 +854,6 @@ std::tuple<at::Tensor, at::Tensor> mgemm_argmax_val(const at::Tensor& x, const a
   CHECK_RC(docqa_mgemm_argmax(x.data_ptr(), w.data_ptr(), out.data_ptr<int64_t>(), outv.data_ptr<float>(),
                               ws_v.data_ptr<float>(), ws_i.data_ptr<int>(), M, N, K, (int)n_valid, (int)cfg,
                               stream()), "mgemm_argmax_val");
-  return {out, outv};
-}
-
-// mid-M decode GEMM, weights in VGPRs (wgemm.hip): splits == 1 -> bf16 [.., N]; splits > 1 ->
-// fp32 split-K slabs [S, M, N]
-at::Tensor wgemm(const at::Tensor& x, const at::Tensor& w, int64_t splits, int64_t cfg) {
-  CHECK_GPU(x); CHECK_BF16(x); CHECK_BF16(w); CHECK_CONTIG(x); CHECK_CONTIG(w);
-  CHECK_ALIGN16(x); CHECK_ALIGN16(w);
-  const int K = x.size(-1), N = w.size(0);
-  TORCH_CHECK(w.size(1) == K, "wgemm: K mismatch");
-  const int M = x.numel() / K;
-  TORCH_CHECK(splits >= 1, "wgemm: splits >= 1");
-  TORCH_CHECK((int64_t)std::max(M, N) * K < (1LL << 30), "wgemm: 32-bit byte offsets");
-  c10::DeviceGuard g(x.device());
-  at::Tensor out;
-  if (splits == 1) {
-    auto sizes = x.sizes().vec();
-    sizes.back() = N;
-    out = at::empty(sizes, x.options());
-    CHECK_RC(docqa_wgemm(x.data_ptr(), w.data_ptr(), out.data_ptr(), nullptr, M, N, K, 1, (int)cfg, stream()),
-             "wgemm");
-  } else {
-    out = at::empty({splits, M, N}, x.options().dtype(at::kFloat));
-    CHECK_RC(docqa_wgemm(x.data_ptr(), w.data_ptr(), nullptr, out.data_ptr<float>(), M, N, K, (int)splits,
-                         (int)cfg, stream()), "wgemm");
-  }
-  return out;
-}
-
-int64_t wgemm_tile_n(int64_t cfg) { return docqa_wgemm_tile_n((int)cfg); }
-
-// gate|up + SwiGLU: x [M, K], w [2I, K] (8-interleaved) -> [M, I]; splits 2 needs the
-// hand-off workspace: ws fp32 [m-tiles x N x 256] partial tiles, tick int32 [2 T + 1]
-// (T = m-tiles x N / tile_n tickets, then the sticky error word), tickets zeroed once and
-// re-armed by the kernel
-at::Tensor wgemm_glu(const at::Tensor& x, const at::Tensor& w, int64_t splits, int64_t cfg,
-                     const c10::optional<at::Tensor>& ws, const c10::optional<at::Tensor>& tick) {
-  CHECK_GPU(x); CHECK_BF16(x); CHECK_BF16(w); CHECK_CONTIG(x); CHECK_CONTIG(w);
-  CHECK_ALIGN16(x); CHECK_ALIGN16(w);
-  const int K = x.size(-1), N = w.size(0);
-  TORCH_CHECK(w.size(1) == K && N % 16 == 0, "wgemm_glu: shape mismatch");
-  const int M = x.numel() / K;
-  TORCH_CHECK((int64_t)std::max(M, N) * K < (1LL << 30), "wgemm_glu: 32-bit byte offsets");
-  TORCH_CHECK(splits == 1 || splits == 2, "wgemm_glu: splits 1 or 2");
-  float* wsp = nullptr;
-  int* tk = nullptr;
-  int* err = nullptr;
-  if (splits == 2) {
-    TORCH_CHECK(ws.has_value() && tick.has_value(), "wgemm_glu: splits 2 needs ws and tick");
-    CHECK_GPU(*ws); CHECK_GPU(*tick); CHECK_I32(*tick); CHECK_CONTIG(*ws); CHECK_CONTIG(*tick);
-    TORCH_CHECK(ws->scalar_type() == at::kFloat, "wgemm_glu: ws must be fp32");
-    const int bn = docqa_wgemm_tile_n((int)cfg);
-    TORCH_CHECK(bn > 0 && N % bn == 0, "wgemm_glu: N must be a multiple of the tile");
-    const int64_t tiles = ((M + 255) / 256) * (N / bn);
-    TORCH_CHECK(ws->numel() >= docqa_wgemm_glu_ws_floats(M, N, (int)cfg) && tick->numel() >= 2 * tiles + 1,
-                "wgemm_glu: workspace too small");
-    wsp = ws->data_ptr<float>();
-    tk = tick->data_ptr<int>();
-    err = tk + 2 * tiles;
-  }
-  auto sizes = x.sizes().vec();
-  sizes.back() = N / 2;
-  c10::DeviceGuard g(x.device());
-  auto out = at::empty(sizes, x.options());
-  CHECK_RC(docqa_wgemm_glu(x.data_ptr(), w.data_ptr(), out.data_ptr(), wsp, tk, err, M, N, K, (int)splits, (int)cfg,
-                           stream()), "wgemm_glu");
-  return out;
-}
-
-// LM head + greedy pick on wgemm: argmax over the first n_valid columns of bf16(x . w^T)
-std::tuple<at::Tensor, at::Tensor> wgemm_argmax_val(const at::Tensor& x, const at::Tensor& w, int64_t n_valid,
-                                                    int64_t cfg) {
-  CHECK_GPU(x); CHECK_BF16(x); CHECK_BF16(w); CHECK_CONTIG(x); CHECK_CONTIG(w);
-  CHECK_ALIGN16(x); CHECK_ALIGN16(w);
-  const int K = x.size(-1), N = w.size(0), bn = docqa_wgemm_tile_n((int)cfg);
-  TORCH_CHECK(w.size(1) == K && bn > 0 && N % bn == 0, "wgemm_argmax: shape mismatch");
-  const int M = x.numel() / K;
-  TORCH_CHECK((int64_t)std::max(M, N) * K < (1LL << 30), "wgemm_argmax: 32-bit byte offsets");
-  c10::DeviceGuard g(x.device());
-  auto out = at::empty({M}, x.options().dtype(at::kLong));
-  auto outv = at::empty({M}, x.options().dtype(at::kFloat));
-  auto ws_v = at::empty({M, N / bn}, x.options().dtype(at::kFloat));
-  auto ws_i = at::empty({M, N / bn}, x.options().dtype(at::kInt));
-  CHECK_RC(docqa_wgemm_argmax(x.data_ptr(), w.data_ptr(), out.data_ptr<int64_t>(), outv.data_ptr<float>(),
-                              ws_v.data_ptr<float>(), ws_i.data_ptr<int>(), M, N, K, (int)n_valid, (int)cfg, stream()),
-           "wgemm_argmax");
   return {out, outv};
 }
 
@@ -1317,23 +1144,14 @@ TORCH_LIBRARY(docqa, m) {
   m.def("dgemm_glu(Tensor x, Tensor w) -> Tensor");
   m.def("mgemm(Tensor x, Tensor w, int splits, int cfg=0) -> Tensor");
   m.def("mgemm_glu(Tensor x, Tensor w, int cfg=0) -> Tensor");
-  m.def("mgemm_glu_split(Tensor x, Tensor w, int splits, int cfg=0, Tensor? ws=None, Tensor? tick=None) -> Tensor");
   m.def("mgemm_tile_n(int cfg) -> int", &mgemm_tile_n);
-  m.def("mgemm_chain(Tensor attn, Tensor w_o, Tensor(a!) residual, Tensor post_norm, Tensor w_gu, Tensor w_down, "
-        "Tensor next_norm, Tensor? w_qkv, Tensor(b!) counters, int S_o, int cfg_o, int S_d, int cfg_d, int S_q, "
-        "int cfg_q, float eps, Tensor? trace=None) "
-        "-> (Tensor, Tensor)");
   m.def("mgemm_argmax(Tensor x, Tensor w, int n_valid, int cfg=0) -> Tensor");
-  m.def("wgemm(Tensor x, Tensor w, int splits, int cfg=0) -> Tensor");
-  m.def("wgemm_glu(Tensor x, Tensor w, int splits, int cfg=0, Tensor? ws=None, Tensor? tick=None) -> Tensor");
-  m.def("wgemm_argmax_val(Tensor x, Tensor w, int n_valid, int cfg=0) -> (Tensor, Tensor)");
   m.def("dgemm_argmax_val(Tensor x, Tensor w, int n_valid) -> (Tensor, Tensor)");
   m.def("pgemm(Tensor x, Tensor w, int epi=0) -> Tensor");
   m.def("pgemm_partial(Tensor x, Tensor w, int splits) -> Tensor");
   m.def("mgemm_argmax_val(Tensor x, Tensor w, int n_valid, int cfg=0) -> (Tensor, Tensor)");
   m.def("pgemm_ok(int M, int N, int K) -> bool", &pgemm_ok);
   m.def("group_persist_bins(int cap, int Hkv) -> int", &group_persist_bins);
-  m.def("wgemm_tile_n(int cfg) -> int", &wgemm_tile_n);
   m.def("paged_decode_cascade(Tensor q, Tensor k_cache, Tensor v_cache, Tensor block_tables, "
         "Tensor context_lens, int Hq, int max_context, float scale, Tensor prefix_table, Tensor prefix_len, "
         "int nchunk, Tensor? order=None) -> Tensor");
@@ -1398,17 +1216,12 @@ TORCH_LIBRARY_IMPL(docqa, CUDA, m) {
   m.impl("dgemm_glu", &dgemm_glu);
   m.impl("mgemm", &mgemm);
   m.impl("mgemm_glu", &mgemm_glu);
-  m.impl("mgemm_glu_split", &mgemm_glu_split);
-  m.impl("mgemm_chain", &mgemm_chain);
   m.impl("mgemm_argmax", &mgemm_argmax);
   m.impl("pgemm", &pgemm);
   m.impl("pgemm_partial", &pgemm_partial);
   m.impl("mgemm_argmax_val", &mgemm_argmax_val);
-  m.impl("wgemm", &wgemm);
   m.impl("coarse_probes", &coarse_probes);
   m.impl("fp32_gemm_nt", &fp32_gemm_nt);
-  m.impl("wgemm_glu", &wgemm_glu);
-  m.impl("wgemm_argmax_val", &wgemm_argmax_val);
   m.impl("dgemm_argmax_val", &dgemm_argmax_val);
   m.impl("paged_decode_fused", &paged_decode_fused);
   m.impl("paged_decode_cascade", &paged_decode_cascade);

@@ -134,35 +134,13 @@ int docqa_gemm(const void* A, const void* W, const void* bias, const void* res, 
 int docqa_mgemm(const void* X, const void* W, void* Y, float* P, int M, int N, int K, int S, int cfg,
                 hipStream_t s);
 int docqa_mgemm_glu(const void* X, const void* W, void* Y, int M, int N, int K, int cfg, hipStream_t s);
-int docqa_mgemm_glu_split(const void* X, const void* W, void* Y, float* ws, int* tick, int* err, int M, int N, int K,
-                          int S, int cfg, hipStream_t s);
 int docqa_mgemm_argmax(const void* X, const void* W, int64_t* out, float* outv, float* ws_v, int* ws_i, int M,
                        int N, int K, int n_valid, int cfg, hipStream_t s);
 int docqa_mgemm_tile_n(int cfg);
 // IVF coarse quantizer for wide probes (coarse.hip): nprobe <= 512 nearest centroids per query
 int docqa_coarse_probes(const float* cent, const float* cnorm, int nlist, int d, const float* xq, int nq,
                         int nprobe, float* ws, int64_t* probes, hipStream_t s);
-// mid-M decode GEMM with the weights streamed into VGPRs (wgemm.hip): X-only LDS ring,
-// 256 x 256 tiles; split-K slabs / bf16 / fused SwiGLU (S = 1, or 2 with an in-launch
-// K-half hand-off through ws + tick) / fused LM-head argmax
-int docqa_wgemm(const void* X, const void* W, void* Y, float* P, int M, int N, int K, int S, int cfg,
-                hipStream_t s);
-long long docqa_wgemm_glu_ws_floats(int M, int N, int cfg);
-int docqa_wgemm_glu(const void* X, const void* W, void* Y, float* ws, int* tick, int* err, int M, int N, int K,
-                    int S, int cfg, hipStream_t s);
-int docqa_wgemm_argmax(const void* X, const void* W, int64_t* out, float* outv, float* ws_v, int* ws_i, int M, int N,
-                       int K, int n_valid, int cfg, hipStream_t s);
-int docqa_wgemm_tile_n(int cfg);
-// persistent decode-layer chain (mgemm.hip): O -> add+RMSNorm -> gate|up+SwiGLU -> down ->
-// add+RMSNorm [-> next layer's QKV slabs] in one launch; counters: int32 [16], zeroed once
-int docqa_mgemm_chain(const void* attn, const void* w_o, float* p_o, void* residual, const void* post_norm,
-                      void* x1, const void* w_gu, void* g, const void* w_down, float* p_d, const void* next_norm,
-                      void* x2, const void* w_qkv, float* p_q, int* counters, long long* trace, int M, int H,
-                      int Ko, int N2I, int Nq, int S_o, int cfg_o, int S_d, int cfg_d, int S_q, int cfg_q,
-                      float eps, hipStream_t s);
 bool docqa_pgemm_ok(int M, int N, int K);
-int docqa_pgemm_argmax(const void* A, const void* W, int64_t* out, float* outv, float* ws_v, int* ws_i, int M, int N,
-                       int K, int n_valid, hipStream_t s);
 int docqa_pgemm(const void* A, const void* W, void* C, float* P, int M, int N, int K, int S, int epi,
                 hipStream_t s);
 

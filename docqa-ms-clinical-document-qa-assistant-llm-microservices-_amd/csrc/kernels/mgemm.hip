@@ -59,8 +59,7 @@ __device__ __forceinline__ void better(float& bv, int& bi, float v, int i) {
 
 // Epilogue shared by the kernels: accumulators -> per-wave LDS scratch (the drained ring)
 // -> bf16 / fp32 split-K slab / fused SwiGLU / LM-head argmax partials.
-// WT: write-through (sc1) stores, for consumers inside the same launch (the chain below)
-template <int EPI, int BN, int WM, int WN, bool WT = false>
+template <int EPI, int BN, int WM, int WN>
 __device__ __forceinline__ void mgemm_epilogue(f32x4 (&acc)[BM / WM / 16][BN / WN / 16], uint16_t* smem,
                                                uint16_t* __restrict__ Y, float* __restrict__ P,
                                                float* __restrict__ pv, int* __restrict__ pi, int M, int N,
@@ -105,11 +104,7 @@ __device__ __forceinline__ void mgemm_epilogue(f32x4 (&acc)[BM / WM / 16][BN / W
         if (row < M) {
           if constexpr (EPI == EPI_PARTIAL) {
             float* dst = P + ((size_t)slice * M + row) * N + col;
-            if constexpr (WT)
-              store16_wt(dst, uint4{__float_as_uint(v[0]), __float_as_uint(v[1]), __float_as_uint(v[2]),
-                                    __float_as_uint(v[3])});
-            else
-              *reinterpret_cast<float4*>(dst) = float4{v[0], v[1], v[2], v[3]};
+            *reinterpret_cast<float4*>(dst) = float4{v[0], v[1], v[2], v[3]};
           } else if constexpr (EPI == EPI_BF16) {
             *reinterpret_cast<uint4*>(Y + (size_t)row * N + col) = pack8(v);
           } else {
@@ -121,8 +116,7 @@ __device__ __forceinline__ void mgemm_epilogue(f32x4 (&acc)[BM / WM / 16][BN / W
               o[e] = silu_f(gv) * uv;
             }
             uint16_t* dst = Y + (size_t)row * (N >> 1) + (col >> 1);
-            if constexpr (WT) store16_wt(dst, pack8(o));
-            else *reinterpret_cast<uint4*>(dst) = pack8(o);
+            *reinterpret_cast<uint4*>(dst) = pack8(o);
           }
         }
       }
@@ -184,87 +178,13 @@ __device__ __forceinline__ void mgemm_epilogue(f32x4 (&acc)[BM / WM / 16][BN / W
 // PF = 0 reads each stage's fragments after its barrier (one register set, for the
 // 128 x 128-per-wave layout whose two sets would not fit)
 // One (m-tile, weight tile, K slice) of the GEMM on the workgroup's LDS ring `smem`
-// (NSR * (BM + BN) * BKS bf16): the standalone kernel below runs one per workgroup, the
-// persistent decode-layer chain (mgemm_chain_kernel) runs them as work items.
-// 2-way split-K meeting of a fused-SwiGLU tile (wgemm.hip has the same protocol): the first
-// K half to finish parks its fp32 accumulators in ws (write-through, acc-native layout: 16 B
-// per lane, fully coalesced) and raises tick[2 tix + 1]; the second adds them and runs the
-// epilogue.  The second only waits on a half that already drew its ticket, i.e. is
-// resident: no deadlock for any residency; fp32 a + b == b + a keeps the bits independent
-// of the arrival order.  Returns true when this workgroup runs the epilogue.
-template <int MI, int NJ, int WAVES>
-__device__ __forceinline__ bool glu_meet(f32x4 (&acc)[MI][NJ], uint16_t* smem, float* __restrict__ ws,
-                                         int* __restrict__ tick, int* __restrict__ err, int tix) {
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  int* tk = reinterpret_cast<int*>(smem);
-  if (tid == 0) tk[0] = __hip_atomic_fetch_add(&tick[2 * tix], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  __syncthreads();
-  const bool first = tk[0] == 0;
-  __syncthreads();          // every wave read the ticket before the epilogue reuses smem
-  float* slab = ws + ((size_t)tix * WAVES + wave) * (MI * NJ * 256) + lane * 4;
-  if (first) {
-#pragma unroll
-    for (int i = 0; i < MI; ++i)
-#pragma unroll
-      for (int j = 0; j < NJ; ++j) {
-        const f32x4 v = acc[i][j];
-        store16_wt(slab + (i * NJ + j) * 256,
-                   uint4{__float_as_uint(v[0]), __float_as_uint(v[1]), __float_as_uint(v[2]), __float_as_uint(v[3])});
-      }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (tid == 0) __hip_atomic_store(&tick[2 * tix + 1], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    return false;
-  }
-  if (tid == 0) {
-    int it = 0;
-    while (__hip_atomic_load(&tick[2 * tix + 1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0) {
-      if (++it > (1 << 24)) {   // a lost hand-off: report, never hang the GPU
-        __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        break;
-      }
-      __builtin_amdgcn_s_sleep(2);
-    }
-  }
-  __syncthreads();
-  // the partner's accumulators: 8 write-through (sc1) loads in flight per wait -- one
-  // memory latency per 8 fragments, not per fragment (32 serial latencies at cfg 6 made
-  // the 2-way split slower than the unsplit kernel).  The wait names the 8 registers, so
-  // no add can be scheduled above it.
-  constexpr int NF = MI * NJ;
-#pragma unroll
-  for (int c = 0; c < NF; c += 8) {
-    f32x4 d[8];
-#pragma unroll
-    for (int q = 0; q < 8; ++q)
-      if (c + q < NF)
-        asm volatile("global_load_dwordx4 %0, %1, off sc1" : "=v"(d[q]) : "v"(slab + (c + q) * 256) : "memory");
-      else
-        d[q] = f32x4{0.f, 0.f, 0.f, 0.f};
-    asm volatile("s_waitcnt vmcnt(0)"
-                 : "+v"(d[0]), "+v"(d[1]), "+v"(d[2]), "+v"(d[3]), "+v"(d[4]), "+v"(d[5]), "+v"(d[6]), "+v"(d[7])
-                 :
-                 : "memory");
-#pragma unroll
-    for (int q = 0; q < 8; ++q)
-      if (c + q < NF) acc[(c + q) / NJ][(c + q) % NJ] += d[q];
-  }
-  if (tid == 0) {   // both halves are past every use of the words: re-arm for the next launch
-    __hip_atomic_store(&tick[2 * tix], 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __hip_atomic_store(&tick[2 * tix + 1], 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  }
-  return true;
-}
-
-template <int EPI, int BN, int BKS, int NSR, int WM, int WN, int PF = 1, bool WT = false>
+// (NSR * (BM + BN) * BKS bf16): the kernel below runs one per workgroup.
+template <int EPI, int BN, int BKS, int NSR, int WM, int WN, int PF = 1>
 __device__ __forceinline__ void mgemm_tile(uint16_t* smem, const uint16_t* __restrict__ X,
                                            const uint16_t* __restrict__ W, uint16_t* __restrict__ Y,
                                            float* __restrict__ P, float* __restrict__ pv,
                                            int* __restrict__ pi, int M, int N, int K, int Ks,
-                                           int tile, int slice, int m0, int ntiles, int n_valid,
-                                           float* __restrict__ ws = nullptr, int* __restrict__ tick = nullptr,
-                                           int* __restrict__ err = nullptr, int S = 1) {
+                                           int tile, int slice, int m0, int ntiles, int n_valid) {
   constexpr int WAVES = WM * WN;
   constexpr int MI = BM / WM / 16;                      // 16-row m-tiles per wave
   constexpr int CW = BN / WN;                           // output columns per wave
@@ -437,10 +357,7 @@ __device__ __forceinline__ void mgemm_tile(uint16_t* smem, const uint16_t* __res
   wait_vmcnt<0>();
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   ring_barrier();   // every wave is done reading the ring: reuse it as epilogue scratch
-  if constexpr (EPI == EPI_GLU) {
-    if (S == 2 && !glu_meet<MI, NJ, WAVES>(acc, smem, ws, tick, err, (m0 / BM) * ntiles + tile)) return;
-  }
-  mgemm_epilogue<EPI, BN, WM, WN, WT>(acc, smem, Y, P, pv, pi, M, N, m0, n0, slice, tile, ntiles, n_valid);
+  mgemm_epilogue<EPI, BN, WM, WN>(acc, smem, Y, P, pv, pi, M, N, m0, n0, slice, tile, ntiles, n_valid);
 }
 
 template <int EPI, int BN, int BKS, int NSR, int WM, int WN, int PF = 1>
@@ -450,9 +367,7 @@ __global__ __launch_bounds__(WM * WN * 64) void mgemm_kernel(const uint16_t* __r
                                                              float* __restrict__ P,
                                                              float* __restrict__ pv, int* __restrict__ pi,
                                                              int M, int N, int K, int Ks, int S,
-                                                             int ntiles, int remap, int n_valid,
-                                                             float* __restrict__ ws, int* __restrict__ tick,
-                                                             int* __restrict__ err) {
+                                                             int ntiles, int remap, int n_valid) {
   __shared__ __attribute__((aligned(16))) uint16_t smem[NSR * (BM + BN) * BKS];
   const int L = blockIdx.x;
   int tile, slice;
@@ -469,7 +384,7 @@ __global__ __launch_bounds__(WM * WN * 64) void mgemm_kernel(const uint16_t* __r
     slice = L / ntiles;
   }
   mgemm_tile<EPI, BN, BKS, NSR, WM, WN, PF>(smem, X, W, Y, P, pv, pi, M, N, K, Ks, tile, slice, blockIdx.y * BM,
-                                            ntiles, n_valid, ws, tick, err, S);
+                                            ntiles, n_valid);
 }
 
 // Variants (``cfg``): the tile width and wave layout
@@ -501,8 +416,7 @@ constexpr Cfg kCfg[kNumCfg + 1] = {{0, 0}, {128, 64}, {128, 64}, {256, 32}, {256
 
 template <int EPI, int BN, int BKS, int NSR, int WM, int WN, int PF = 1>
 int launch(const uint16_t* x, const uint16_t* w, uint16_t* y, float* p, float* pv, int* pi, int M,
-           int N, int K, int S, int n_valid, hipStream_t s, float* ws = nullptr, int* tick = nullptr,
-           int* err = nullptr) {
+           int N, int K, int S, int n_valid, hipStream_t s) {
   // the epilogue sweeps 16-row slices with (columns per wave) / (columns per lane) lanes per
   // row: the SwiGLU epilogue (16 columns per lane) needs >= 64 columns per wave
   if constexpr (EPI == EPI_GLU && BN / WN < 64) {
@@ -514,7 +428,7 @@ int launch(const uint16_t* x, const uint16_t* w, uint16_t* y, float* p, float* p
   else if (S > 8 && S % 8 == 0) remap = 2;
   dim3 grid(ntiles * S, (M + BM - 1) / BM);
   mgemm_kernel<EPI, BN, BKS, NSR, WM, WN, PF><<<grid, WM * WN * 64, 0, s>>>(x, w, y, p, pv, pi, M, N, K, Ks, S,
-                                                                      ntiles, remap, n_valid, ws, tick, err);
+                                                                      ntiles, remap, n_valid);
   DOCQA_CHECK_LAUNCH();
   return 0;
   }
@@ -522,16 +436,15 @@ int launch(const uint16_t* x, const uint16_t* w, uint16_t* y, float* p, float* p
 
 template <int EPI>
 int launch_cfg(int cfg, const uint16_t* x, const uint16_t* w, uint16_t* y, float* p, float* pv, int* pi,
-               int M, int N, int K, int S, int n_valid, hipStream_t s, float* ws = nullptr, int* tick = nullptr,
-               int* err = nullptr) {
+               int M, int N, int K, int S, int n_valid, hipStream_t s) {
   switch (cfg) {
-    case 1: return launch<EPI, 128, 64, 3, 2, 2>(x, w, y, p, pv, pi, M, N, K, S, n_valid, s, ws, tick, err);
-    case 2: return launch<EPI, 128, 64, 3, 4, 2>(x, w, y, p, pv, pi, M, N, K, S, n_valid, s, ws, tick, err);
-    case 3: return launch<EPI, 256, 32, 4, 2, 4>(x, w, y, p, pv, pi, M, N, K, S, n_valid, s, ws, tick, err);
-    case 4: return launch<EPI, 256, 32, 4, 2, 2>(x, w, y, p, pv, pi, M, N, K, S, n_valid, s, ws, tick, err);
-    case 5: return launch<EPI, 256, 64, 2, 2, 2, 0>(x, w, y, p, pv, pi, M, N, K, S, n_valid, s, ws, tick, err);
-    case 6: return launch<EPI, 256, 64, 2, 2, 4, 0>(x, w, y, p, pv, pi, M, N, K, S, n_valid, s, ws, tick, err);
-    case 7: return launch<EPI, 64, 64, 3, 4, 2>(x, w, y, p, pv, pi, M, N, K, S, n_valid, s, ws, tick, err);
+    case 1: return launch<EPI, 128, 64, 3, 2, 2>(x, w, y, p, pv, pi, M, N, K, S, n_valid, s);
+    case 2: return launch<EPI, 128, 64, 3, 4, 2>(x, w, y, p, pv, pi, M, N, K, S, n_valid, s);
+    case 3: return launch<EPI, 256, 32, 4, 2, 4>(x, w, y, p, pv, pi, M, N, K, S, n_valid, s);
+    case 4: return launch<EPI, 256, 32, 4, 2, 2>(x, w, y, p, pv, pi, M, N, K, S, n_valid, s);
+    case 5: return launch<EPI, 256, 64, 2, 2, 2, 0>(x, w, y, p, pv, pi, M, N, K, S, n_valid, s);
+    case 6: return launch<EPI, 256, 64, 2, 2, 4, 0>(x, w, y, p, pv, pi, M, N, K, S, n_valid, s);
+    case 7: return launch<EPI, 64, 64, 3, 4, 2>(x, w, y, p, pv, pi, M, N, K, S, n_valid, s);
     default: return -1;
   }
 }
@@ -544,13 +457,8 @@ bool shape_ok(int M, int N, int K, int S, int cfg) {
 }  // namespace
 
 constexpr int kDefaultCfg = 2;
-int docqa_pgemm_argmax(const void* A, const void* W, int64_t* out, float* outv, float* ws_v, int* ws_i, int M, int N,
-                       int K, int n_valid, hipStream_t s);
-// cfg 8 (LM head only): the argmax on pgemm.hip's 256 x 256 tiles (docqa_pgemm_argmax)
-constexpr int kPgemmArgmaxCfg = 8;
 int docqa_mgemm_tile_n(int cfg) {
   if (cfg == 0) cfg = kDefaultCfg;
-  if (cfg == kPgemmArgmaxCfg) return 256;
   return cfg >= 1 && cfg <= kNumCfg ? kCfg[cfg].bn : 0;
 }
 
@@ -567,25 +475,13 @@ int docqa_mgemm(const void* X, const void* W, void* Y, float* P, int M, int N, i
   return launch_cfg<EPI_BF16>(cfg, x, w, (uint16_t*)Y, nullptr, nullptr, nullptr, M, N, K, 1, N, s);
 }
 
-int docqa_mgemm_glu_split(const void* X, const void* W, void* Y, float* ws, int* tick, int* err, int M, int N, int K,
-                          int S, int cfg, hipStream_t s);
-
 // Y[M, N/2] = silu(gate) * up for the 8-interleaved gate|up weight W [N, K] (N = 2 I)
 int docqa_mgemm_glu(const void* X, const void* W, void* Y, int M, int N, int K, int cfg, hipStream_t s) {
-  return docqa_mgemm_glu_split(X, W, Y, nullptr, nullptr, nullptr, M, N, K, 1, cfg, s);
-}
-
-// the same with the K range split over S = 1 or 2 workgroups per tile that meet in the
-// launch (glu_meet): ws fp32 [m-tiles x N x 256], tick int32 [2 x m-tiles x N / tile_n]
-// zeroed once (re-armed by the kernel), err: sticky int32 error word
-int docqa_mgemm_glu_split(const void* X, const void* W, void* Y, float* ws, int* tick, int* err, int M, int N, int K,
-                          int S, int cfg, hipStream_t s) {
   if (cfg == 0) cfg = kDefaultCfg;
   if (M == 0) return 0;
-  if ((S != 1 && S != 2) || (S == 2 && (!ws || !tick || !err || !docqa_aligned16(ws)))) return -1;
-  if (!shape_ok(M, N, K, S, cfg) || !docqa_aligned16(X) || !docqa_aligned16(W) || !docqa_aligned16(Y)) return -1;
+  if (!shape_ok(M, N, K, 1, cfg) || !docqa_aligned16(X) || !docqa_aligned16(W) || !docqa_aligned16(Y)) return -1;
   return launch_cfg<EPI_GLU>(cfg, (const uint16_t*)X, (const uint16_t*)W, (uint16_t*)Y, nullptr, nullptr, nullptr,
-                             M, N, K, S, N, s, ws, tick, err);
+                             M, N, K, 1, N, s);
 }
 
 // out[M] = argmax over the first n_valid columns of bf16(X . W^T) (LM head + greedy pick),
@@ -594,222 +490,12 @@ int docqa_mgemm_argmax(const void* X, const void* W, int64_t* out, float* outv, 
                        int N, int K, int n_valid, int cfg, hipStream_t s) {
   if (cfg == 0) cfg = kDefaultCfg;
   if (M == 0) return 0;
-  if (cfg == kPgemmArgmaxCfg) return docqa_pgemm_argmax(X, W, out, outv, ws_v, ws_i, M, N, K, n_valid, s);
   if (!shape_ok(M, N, K, 1, cfg) || n_valid <= 0 || n_valid > N) return -1;
   if (!docqa_aligned16(X) || !docqa_aligned16(W)) return -1;
   const int rc = launch_cfg<EPI_ARGMAX>(cfg, (const uint16_t*)X, (const uint16_t*)W, nullptr, nullptr, ws_v, ws_i,
                                         M, N, K, 1, n_valid, s);
   if (rc) return rc;
   argmax_merge_kernel<<<M, 256, 0, s>>>(ws_v, ws_i, N / kCfg[cfg].bn, out, outv);
-  DOCQA_CHECK_LAUNCH();
-  return 0;
-}
-
-// ---------------------------------------------------------------------------------------
-// Persistent decode-layer chain: the back half of a Llama decoder layer at 193..512 decode
-// rows (TP = 1) plus the next layer's QKV projection, in ONE launch instead of six:
-//   phase 0  O projection        attn [M, Ko] . Wo^T -> fp32 split-K slabs p_o [S_o, M, H]
-//   phase 1  residual + RMSNorm  residual += bf16(sum p_o); x1 = rmsnorm(residual) * post_norm
-//   phase 2  gate|up + SwiGLU    g = silu(x1 Wg^T) * (x1 Wu^T)            (8-interleaved W)
-//   phase 3  down projection     g . Wd^T -> slabs p_d [S_d, M, H]
-//   phase 4  residual + RMSNorm  residual += bf16(sum p_d); x2 = rmsnorm(residual) * next_norm
-//   phase 5  next QKV (optional) x2 . Wqkv^T -> slabs p_q [S_q, M, Nq] (rope_cache_splitk /
-//            the grouped cascade consume them after the launch)
-// Every GEMM item is one mgemm_tile of the standalone plan (same tiles, same split, same
-// epilogues) and every norm item runs the standalone kernel's row body on each 256-thread
-// half of the workgroup (docqa_norm_row.h), so the chain's outputs equal the six-launch
-// sequence bit for bit.  What it removes: five kernel boundaries per layer -- each a grid
-// drain + fill and, behind the split-K GEMMs, the writeback of their dirty slab lines
-// (MI355X_MICROARCH.md "boundary": 1.7-1.9 us + B / 6 TB/s; "phase-in-launch": 0.85x of the
-// summed phase spans on an M = 256 block) -- and workgroups that run out of work in one
-// phase take the next phase's items and wait there, so the next phase starts on every CU
-// the moment its inputs are published.
-//
-// Scheduling (cdna_hip_programming.md §5 "Projection GEMM at M = 256" item 2 / §6 Guideline
-// 16): workgroups draw tickets from one agent-scope counter; tickets enumerate the items
-// phase by phase, so an item waits only on items with smaller tickets, which were drawn by
-// workgroups that are running -- deadlock-free whatever number of workgroups is resident.
-// Publish: every wave's stores retired (vmcnt 0) -> barrier -> lane 0 agent release fence ->
-// vmcnt 0 -> relaxed agent fetch_add of the phase counter.  Consume: lane 0 polls the
-// previous phase's counter (relaxed agent loads + s_sleep, bounded: a lost wake-up sets the
-// sticky error word and falls through instead of hanging the GPU) -> agent acquire fence ->
-// barrier.  The last workgroup out resets the ticket / phase words, so a captured graph
-// replays the launch with no memset node (a 48-byte memset node captured ahead of the kernel
-// left the words garbled after replays on ROCm 7.2 -- tests/test_chain_gpu.py).
-// Counters (int32, zero before the first launch): [0..5] items done per phase, [8] ticket,
-// [9] workgroups exited, [12] sticky error flag (never reset by the kernel).
-namespace {
-struct ChainArgs {
-  const uint16_t* attn;
-  const uint16_t* w_o;
-  float* p_o;
-  uint16_t* residual;
-  const uint16_t* post_norm;
-  uint16_t* x1;
-  const uint16_t* w_gu;
-  uint16_t* g;
-  const uint16_t* w_down;
-  float* p_d;
-  const uint16_t* next_norm;
-  uint16_t* x2;
-  const uint16_t* w_qkv;   // nullptr: no phase 5 (last layer)
-  float* p_q;
-  int* ctr;
-  long long* trace;        // debug: per ticket (phase, workgroup, t_ticket, t_ready, t_done, t_published)
-  int M, H, Ko, N2I, Nq;   // rows, hidden, O input width, gate|up rows (2 I), QKV rows
-  int S_o, S_d, S_q, cfg_o, cfg_d, cfg_q;
-  float eps;
-};
-
-constexpr int kChainSlot = 3 * (BM + 128) * 64;     // the cfg 2 ring (bf16 elements), >= cfg 7's
-
-__device__ __forceinline__ bool chain_wait(int* p, int target) {
-  for (int it = 0; it < (1 << 22); ++it) {
-    if (__hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= target) return true;
-    __builtin_amdgcn_s_sleep(8);
-  }
-  return false;
-}
-
-template <int NV>
-__device__ __forceinline__ void chain_norm(const float* P, int S, int M, int H, uint16_t* residual,
-                                           const uint16_t* w, uint16_t* out, float eps, int row,
-                                           int tid, float* red) {
-  const size_t slab = (size_t)M * H;
-  switch (S) {
-    case 4: add_rmsnorm_splitk_row<NV, 4, true>(P, S, slab, residual, w, out, H, eps, row, tid, red); break;
-    case 7: add_rmsnorm_splitk_row<NV, 7, true>(P, S, slab, residual, w, out, H, eps, row, tid, red); break;
-    case 8: add_rmsnorm_splitk_row<NV, 8, true>(P, S, slab, residual, w, out, H, eps, row, tid, red); break;
-    default: add_rmsnorm_splitk_row<NV, 0, true>(P, S, slab, residual, w, out, H, eps, row, tid, red); break;
-  }
-}
-
-__global__ __launch_bounds__(512) void mgemm_chain_kernel(ChainArgs a) {
-  __shared__ __attribute__((aligned(16))) uint16_t smem[kChainSlot];
-  float* red = reinterpret_cast<float*>(smem);          // norm items: 4 floats per half
-  int* tk = reinterpret_cast<int*>(smem) + 16;          // ticket broadcast
-  const int tid = threadIdx.x;
-  int* ctr = a.ctr;
-  const int mt = (a.M + BM - 1) / BM;
-  const int nt_o = a.H / (a.cfg_o == 7 ? 64 : 128), nt_gu = a.N2I / 128, nt_d = a.H / (a.cfg_d == 7 ? 64 : 128),
-            nt_q = a.Nq / (a.cfg_q == 7 ? 64 : 128);
-  const int c0 = nt_o * a.S_o * mt, c1 = a.M / 2, c2 = nt_gu * mt, c3 = nt_d * a.S_d * mt, c4 = a.M / 2,
-            c5 = a.w_qkv ? nt_q * a.S_q * mt : 0;
-  const int e0 = c0, e1 = e0 + c1, e2 = e1 + c2, e3 = e2 + c3, e4 = e3 + c4, total = e4 + c5;
-  const int I = a.N2I / 2;
-  int seen = 0;   // phases whose inputs this workgroup has acquired: items of phase <= seen may run
-  for (;;) {
-    if (tid == 0) tk[0] = __hip_atomic_fetch_add(&ctr[8], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __syncthreads();
-    int i = tk[0];
-    __syncthreads();
-    if (i >= total) break;
-    const int ticket = i;
-    long long t0 = 0, t1 = 0, t2 = 0;
-    if (a.trace && tid == 0) t0 = wall_clock64();
-    // phase of ticket i and its index within the phase; need: items in the previous phase
-    int p, need;
-    if (i < e0) { p = 0; need = 0; }
-    else if (i < e1) { p = 1; i -= e0; need = c0; }
-    else if (i < e2) { p = 2; i -= e1; need = c1; }
-    else if (i < e3) { p = 3; i -= e2; need = c2; }
-    else if (i < e4) { p = 4; i -= e3; need = c3; }
-    else { p = 5; i -= e4; need = c4; }
-    if (p > seen) {
-      if (tid == 0) {
-        if (!chain_wait(&ctr[p - 1], need))
-          __hip_atomic_store(&ctr[12], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      }
-      __syncthreads();
-      seen = p;
-    }
-    if (a.trace && tid == 0) t1 = wall_clock64();
-    if (p == 1 || p == 4) {
-      const float* P = p == 1 ? a.p_o : a.p_d;
-      const int S = p == 1 ? a.S_o : a.S_d;
-      const uint16_t* w = p == 1 ? a.post_norm : a.next_norm;
-      uint16_t* out = p == 1 ? a.x1 : a.x2;
-      const int h = tid >> 8, row = 2 * i + h;
-      if (a.H <= 2048 * 2) chain_norm<2>(P, S, a.M, a.H, a.residual, w, out, a.eps, row, tid & 255, red + 4 * h);
-      else chain_norm<4>(P, S, a.M, a.H, a.residual, w, out, a.eps, row, tid & 255, red + 4 * h);
-    } else if (p == 2) {
-      const int tile = i % nt_gu, m0 = (i / nt_gu) * BM;
-      mgemm_tile<EPI_GLU, 128, 64, 3, 4, 2, 1, true>(smem, a.x1, a.w_gu, a.g, nullptr, nullptr, nullptr, a.M, a.N2I, a.H,
-                                            a.H, tile, 0, m0, nt_gu, a.N2I);
-    } else {
-      // split-K projections (O, down, next QKV): one call site per tile width
-      const uint16_t* X = p == 0 ? a.attn : p == 3 ? a.g : a.x2;
-      const uint16_t* W = p == 0 ? a.w_o : p == 3 ? a.w_down : a.w_qkv;
-      float* P = p == 0 ? a.p_o : p == 3 ? a.p_d : a.p_q;
-      const int N = p == 5 ? a.Nq : a.H, K = p == 0 ? a.Ko : p == 3 ? I : a.H;
-      const int S = p == 0 ? a.S_o : p == 3 ? a.S_d : a.S_q;
-      const int cfg = p == 0 ? a.cfg_o : p == 3 ? a.cfg_d : a.cfg_q;
-      const int nt = N / (cfg == 7 ? 64 : 128);
-      const int slice = i % S, tile = (i / S) % nt, m0 = (i / (S * nt)) * BM;
-      if (cfg == 7)
-        mgemm_tile<EPI_PARTIAL, 64, 64, 3, 4, 2, 1, true>(smem, X, W, nullptr, P, nullptr, nullptr, a.M, N, K, K / S, tile,
-                                                 slice, m0, nt, N);
-      else
-        mgemm_tile<EPI_PARTIAL, 128, 64, 3, 4, 2, 1, true>(smem, X, W, nullptr, P, nullptr, nullptr, a.M, N, K, K / S, tile,
-                                                  slice, m0, nt, N);
-    }
-    // publish the item
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (tid == 0) {
-      if (a.trace) t2 = wall_clock64();
-      __hip_atomic_fetch_add(&ctr[p], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      if (a.trace) {
-        long long* tr = a.trace + (size_t)ticket * 6;
-        tr[0] = p; tr[1] = blockIdx.x | ((__builtin_amdgcn_s_getreg(20 | (3 << 11)) & 15) << 16); tr[2] = t0; tr[3] = t1; tr[4] = t2; tr[5] = wall_clock64();
-      }
-    }
-  }
-  if (tid == 0) {
-    const int old = __hip_atomic_fetch_add(&ctr[9], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (old == (int)gridDim.x - 1) {
-#pragma unroll
-      for (int j = 0; j < 10; ++j) __hip_atomic_store(&ctr[j], 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-  }
-}
-
-int chain_grid() {
-  static int n = 0;
-  if (n == 0) {
-    int dev = 0, cus = 0;
-    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) !=
-                                                 hipSuccess || cus <= 0)
-      cus = 256;
-    n = cus;   // one workgroup per CU (the 144 KB ring)
-  }
-  return n;
-}
-}  // namespace
-
-// Shapes: M even (rows tiled by 256); H % 128 == 0, H <= 8192; split-K tiles of cfg 2 (128
-// wide) or 7 (64 wide);
-// Ko, I = N2I / 2 and H each divisible by (split x 128); Nq % 128 == 0.
-int docqa_mgemm_chain(const void* attn, const void* w_o, float* p_o, void* residual, const void* post_norm,
-                      void* x1, const void* w_gu, void* g, const void* w_down, float* p_d, const void* next_norm,
-                      void* x2, const void* w_qkv, float* p_q, int* counters, long long* trace, int M, int H,
-                      int Ko, int N2I, int Nq, int S_o, int cfg_o, int S_d, int cfg_d, int S_q, int cfg_q,
-                      float eps, hipStream_t s) {
-  auto cfg_ok = [](int c) { return c == 2 || c == 7; };
-  if (M <= 0 || M % 2 || H > 8192 || H % 128 || N2I % 256 || !cfg_ok(cfg_o) || !cfg_ok(cfg_d)) return -1;
-  if (!shape_ok(M, H, Ko, S_o, cfg_o) || !shape_ok(M, N2I, H, 1, 2) || !shape_ok(M, H, N2I / 2, S_d, cfg_d)) return -1;
-  if (w_qkv && (!p_q || !cfg_ok(cfg_q) || !shape_ok(M, Nq, H, S_q, cfg_q))) return -1;
-  const void* ptrs[] = {attn, w_o, p_o, residual, post_norm, x1, w_gu, g, w_down, p_d, next_norm, x2};
-  for (const void* q : ptrs)
-    if (!docqa_aligned16(q)) return -1;
-  if (w_qkv && (!docqa_aligned16(w_qkv) || !docqa_aligned16(p_q))) return -1;
-  ChainArgs a{(const uint16_t*)attn, (const uint16_t*)w_o, p_o, (uint16_t*)residual, (const uint16_t*)post_norm,
-              (uint16_t*)x1, (const uint16_t*)w_gu, (uint16_t*)g, (const uint16_t*)w_down, p_d,
-              (const uint16_t*)next_norm, (uint16_t*)x2, (const uint16_t*)w_qkv, p_q, counters, trace,
-              M, H, Ko, N2I, Nq, S_o, S_d, w_qkv ? S_q : 1, cfg_o, cfg_d, w_qkv ? cfg_q : 2, eps};
-  mgemm_chain_kernel<<<chain_grid(), 512, 0, s>>>(a);
   DOCQA_CHECK_LAUNCH();
   return 0;
 }

@@ -36,7 +36,6 @@
 // byte offsets of A and W rows must fit 32 bits (saddr + voffset addressing).
 #include "docqa_common.h"
 #include "docqa_asm.h"
-#include "docqa_argmax.h"
 #include <float.h>
 
 using namespace docqa;
@@ -48,7 +47,7 @@ constexpr int BUF_B = 4 * HALF_B;        // bytes of one K-tile buffer (64 KiB)
 constexpr int SCR_PITCH = 72;            // epilogue scratch row pitch (bf16), 144 B
 constexpr int LDS_B = (2 * BUF_B > 8 * 128 * SCR_PITCH * 2) ? 2 * BUF_B : 8 * 128 * SCR_PITCH * 2;
 enum { HA0 = 0, HA1 = 1, HB0 = 2, HB1 = 3 };
-enum { EPI_BF16 = 0, EPI_GLU = 1, EPI_PARTIAL = 2, EPI_ARGMAX = 3 };
+enum { EPI_BF16 = 0, EPI_GLU = 1, EPI_PARTIAL = 2 };
 
 // byte offset of logical 16-B chunk `ch` of `row` inside a [128][64] bf16 half-tile
 __device__ __forceinline__ uint32_t swz(int row, int ch) {
@@ -91,9 +90,7 @@ template <int EPI>
 __global__ __launch_bounds__(512, 2) void pgemm_kernel(const uint16_t* __restrict__ A,
                                                       const uint16_t* __restrict__ W,
                                                       uint16_t* __restrict__ C, float* __restrict__ P,
-                                                      int M, int N, int K, int ntm, int ntn, int S, int Ks,
-                                                      float* __restrict__ pv = nullptr, int* __restrict__ pi = nullptr,
-                                                      int n_valid = 0) {
+                                                      int M, int N, int K, int ntm, int ntn, int S, int Ks) {
   __shared__ __attribute__((aligned(16))) char smem[LDS_B];
   const int nwg = ntm * ntn;
   // split-K (decode-sized M): workgroup -> (tile, K slice).  With S | 8 and whole rounds of
@@ -286,56 +283,6 @@ __global__ __launch_bounds__(512, 2) void pgemm_kernel(const uint16_t* __restric
       const uint4 v = *reinterpret_cast<const uint4*>(scr + r * SCR_PITCH + c);
       if (row < M) *reinterpret_cast<uint4*>(C + (size_t)row * N + n0 + wc * 64 + c) = v;
     }
-  } else if constexpr (EPI == EPI_ARGMAX) {
-    // LM head + greedy pick: per row, the best (bf16-rounded value, lowest id on ties, as
-    // torch.argmax over the bf16 logits) over this tile's first-n_valid columns -> one
-    // partial per (row, n-tile) for argmax_merge_kernel; the logits never reach HBM.
-    // Lane (fk, fr) holds rows .. + fk * 4 + r at columns .. + fr: reduce over the 4 column
-    // fragments in registers, then over fr (16 lanes, xor 1..8), then the 4 column waves
-    // through LDS
-    float* rv = reinterpret_cast<float*>(smem);            // [256 rows][4 wave columns]
-    int* ri = reinterpret_cast<int*>(smem) + BM * 4;
-#pragma unroll
-    for (int mh = 0; mh < 2; ++mh)
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          float bv = -FLT_MAX;
-          int bi = 0x7fffffff;
-#pragma unroll
-          for (int nh = 0; nh < 2; ++nh)
-#pragma unroll
-            for (int j = 0; j < 2; ++j) {
-              const int col = n0 + wc * 64 + nh * 32 + j * 16 + fr;
-              const float v = bf2f(f2bf(acc[mh][i][nh][j][r]));
-              if (col < n_valid && (v > bv || (v == bv && col < bi))) { bv = v; bi = col; }
-            }
-#pragma unroll
-          for (int o = 1; o < 16; o <<= 1) {
-            const float ov = __shfl_xor(bv, o, 64);
-            const int oi = __shfl_xor(bi, o, 64);
-            if (ov > bv || (ov == bv && oi < bi)) { bv = ov; bi = oi; }
-          }
-          if (fr == 0) {
-            const int lr = wr * 128 + mh * 64 + i * 16 + fk * 4 + r;
-            rv[lr * 4 + wc] = bv;
-            ri[lr * 4 + wc] = bi;
-          }
-        }
-    __syncthreads();
-    if (tid < BM && m0 + tid < M) {
-      float bv = rv[tid * 4];
-      int bi = ri[tid * 4];
-#pragma unroll
-      for (int w = 1; w < 4; ++w) {
-        const float ov = rv[tid * 4 + w];
-        const int oi = ri[tid * 4 + w];
-        if (ov > bv || (ov == bv && oi < bi)) { bv = ov; bi = oi; }
-      }
-      pv[(size_t)(m0 + tid) * ntn + bn] = bv;
-      pi[(size_t)(m0 + tid) * ntn + bn] = bi;
-    }
   } else if constexpr (EPI == EPI_PARTIAL) {
     // fp32 split-K slab P[slice][row][col] (combined by the consumer kernel): each wave's
     // 64-row halves through its own LDS scratch [64][68] so stores are whole 256-B row runs
@@ -400,23 +347,6 @@ bool docqa_pgemm_ok(int M, int N, int K) {
   // 32-bit per-lane byte offsets: (rows - 1) * K * 2 + 128 must fit
   const uint64_t rows = (uint64_t)(M > N ? M : N);
   return rows * (uint64_t)K * 2ull < (1ull << 32);
-}
-
-// out[M] = argmax over the first n_valid columns of bf16(A . W^T) (LM head + greedy pick on
-// the 256 x 256 prefill tiles: 501 workgroups stream the 128256-row vocab once per 256 rows),
-// outv[M] (optional) its value; ws_v / ws_i: [M, N / 256] partials
-int docqa_pgemm_argmax(const void* A, const void* W, int64_t* out, float* outv, float* ws_v, int* ws_i, int M, int N,
-                       int K, int n_valid, hipStream_t s) {
-  if (M == 0) return 0;
-  if (!docqa_pgemm_ok(M, N, K) || n_valid <= 0 || n_valid > N || !ws_v || !ws_i || !out) return -1;
-  if (!docqa_aligned16(A) || !docqa_aligned16(W)) return -1;
-  const int ntm = (M + BM - 1) / BM, ntn = N / BN;
-  pgemm_kernel<EPI_ARGMAX><<<ntm * ntn, 512, 0, s>>>((const uint16_t*)A, (const uint16_t*)W, nullptr, nullptr, M, N,
-                                                     K, ntm, ntn, 1, K, ws_v, ws_i, n_valid);
-  DOCQA_CHECK_LAUNCH();
-  argmax_merge_kernel<<<M, 256, 0, s>>>(ws_v, ws_i, ntn, out, outv);
-  DOCQA_CHECK_LAUNCH();
-  return 0;
 }
 
 // epi 0: C [M, N] bf16; epi 1: C [M, N / 2] = silu(gate) * up (8-interleaved gate|up W);

@@ -169,14 +169,6 @@ class LlamaModel:
         self.cos_sin = ops.rope_cos_sin(cfg.max_position, cfg.head_dim, cfg.rope_theta, self.device,
                                         scaling=cfg.rope_scaling)
         self.layers: list[dict] = []
-        # ticket / phase counters of the persistent decode-layer chain (ops.mgemm_chain), one
-        # row per layer; the kernel leaves them zeroed, so graph replays need no memset
-        self._chain_ctr = (torch.zeros(cfg.layers, 16, dtype=torch.int32, device=self.device)
-                           if self.device.type == "cuda" else None)
-        # hand-off workspace of the 2-way split-K fused SwiGLU (ops.glu_split_plan): one
-        # shared by every layer (they run in stream order); tickets zeroed once here, never
-        # inside a captured graph, and re-armed by the kernel itself
-        self._glu_ws = None
         self._tick = None      # decode attention's last-arriver merge tickets (ops.decode_ticket)
         self._ntick = None     # fused projection + add + RMSNorm ticket word (ops.dgemm_add_rmsnorm)
         if init:
@@ -339,11 +331,7 @@ class LlamaModel:
                 if ops.mid_plan(M, N, K)[0] and (K // 128) % 4 == 0 and N % 128 == 0:
                     plans["down"] = (4, lambda a, w: ops.mgemm_partial(a, w, 4, 2))
             Sg, cg = ops.mid_plan(M, *L0["gate_up"].shape, glu=True)
-            sp = ops.glu_split_plan(M, *L0["gate_up"].shape) if x.is_cuda else None
-            if sp is not None:
-                ws = self._glu_workspace(*L0["gate_up"].shape)
-                glu = lambda a, w, sp=sp, ws=ws: ops.mgemm_glu_split(a, w, sp[0], sp[1], ws)
-            elif small and ops.pgemm_ok(M, *L0["gate_up"].shape):
+            if small and ops.pgemm_ok(M, *L0["gate_up"].shape):
                 glu = ops.prefill_glu     # 256 x 256 tiles with SwiGLU: 104 vs 141 us at M = 512
             else:
                 glu = (lambda a, w: ops.mgemm_glu(a, w, cg)) if Sg else ops.glu_linear
@@ -377,14 +365,6 @@ class LlamaModel:
         so, o_part = plans.get("o", (0, None))
         sd, down_part = plans.get("down", (0, None))
         cascade = decode and meta.shared_len is not None
-        # persistent decode-layer chain: O -> add+norm -> gate|up -> down -> add+norm -> next
-        # QKV in one launch (ops.chain_plan; TP = 1, mid-M plans only)
-        chain = None
-        if decode and self.tp == 1 and self.layers and self._chain_ctr is not None and x.is_cuda and sq:
-            L0 = self.layers[0]
-            chain = ops.chain_plan(M, L0["o"].shape[0], L0["o"].shape[1], L0["gate_up"].shape[0],
-                                   L0["qkv"].shape[0])
-        pq = None   # this layer's QKV slabs, already computed by the previous layer's chain
         trim = (not decode and _PREFILL_TRIM and x.is_cuda and logits_index is not None and self.layers
                 and meta.block_tables is not None and meta.prefix_lens is not None
                 and logits_index.numel() == meta.block_tables.shape[0] and M > logits_index.numel())
@@ -393,10 +373,9 @@ class LlamaModel:
         # projection's slabs, in LDS, under their first weight stages (dgemm.hip XNormIn) --
         # so no add_rmsnorm launch runs between projections; the residual ping-pongs between
         # two buffers (one workgroup writes the new one while the others read the old)
-        xn = (decode and self.tp == 1 and chain is None and not nf and x.is_cuda and sq and so and sd
+        xn = (decode and self.tp == 1 and not nf and x.is_cuda and sq and so and sd
               and self.layers and ops.xn_ok(M, self.cfg.hidden)
-              and not ops.mid_plan(M, *self.layers[0]["gate_up"].shape, glu=True)[0]
-              and ops.glu_split_plan(M, *self.layers[0]["gate_up"].shape) is None)
+              and not ops.mid_plan(M, *self.layers[0]["gate_up"].shape, glu=True)[0])
         res2 = torch.empty_like(residual) if xn else None
         pd = None   # XN: the previous layer's down-projection slabs
         for i, L in enumerate(self.layers):
@@ -406,8 +385,7 @@ class LlamaModel:
                     qkv_slabs = ops.dgemm_partial_xn(pd, residual, res2, L["in_norm"], eps, L["qkv"], sq)
                     residual, res2 = res2, residual
                 else:
-                    qkv_slabs = pq if pq is not None else qkv_part(x, L["qkv"])
-                pq = None
+                    qkv_slabs = qkv_part(x, L["qkv"])
             if cascade:
                 # shared-prefix decode: RoPE + cache write, then prefix-once + suffix attention
                 if (sq and meta.decode_groups is not None and meta.decode_inline and x.is_cuda
@@ -490,11 +468,6 @@ class LlamaModel:
                 a = ops.paged_decode(qkv, kc, vc, meta.block_tables, meta.context_lens, hq,
                                      meta.max_context, self.scale, meta.seq_order)
             nxt = self.layers[i + 1]["in_norm"] if i + 1 < nl else self.final_norm
-            if chain is not None:
-                wq = self.layers[i + 1]["qkv"] if i + 1 < nl else None
-                x, pq = ops.mgemm_chain(a, L["o"], residual, L["post_norm"], L["gate_up"], L["down"], nxt, wq,
-                                        self._chain_ctr[i], chain, eps)
-                continue
             if xn:
                 g = ops.dgemm_glu_xn(o_part(a, L["o"]), residual, res2, L["post_norm"], eps, L["gate_up"])
                 residual, res2 = res2, residual
@@ -535,11 +508,6 @@ class LlamaModel:
             raise RuntimeError(f"decode ticket buffer holds {self._tick.numel()} words, a {B}-row bucket "
                                f"needs {need}: raise the first bucket size (buffers are never regrown)")
         return self._tick
-
-    def _glu_workspace(self, N: int, K: int):
-        if self._glu_ws is None:
-            self._glu_ws = ops.glu_split_workspace(ops.MID_M_MAX, N, self.device)
-        return self._glu_ws
 
     def greedy_ids(self, x: torch.Tensor) -> torch.Tensor:
         """Greedy token ids int64 [R] of the final normed hidden rows ``x``: the LM-head GEMM

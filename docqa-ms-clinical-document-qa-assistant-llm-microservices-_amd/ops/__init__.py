@@ -273,15 +273,6 @@ def mid_plan(M: int, N: int, K: int, glu: bool = False) -> tuple[int, int]:
     return S, _MID_CFG
 
 
-def pack_fragments(w: torch.Tensor) -> torch.Tensor:
-    """[N, K] row-major weights -> the MFMA fragment-major layout [N/16, K/32, 64, 8] of
-    wgemm.hip's packed variants (cfg + 16): the 16 x 32 B fragment of (n-tile, k-step) is
-    one contiguous 1 KiB block, lane l = 16 (k-chunk) + row, so every weight load of the
-    decode GEMM is a fully coalesced wave-instruction."""
-    N, K = w.shape
-    return w.reshape(N // 16, 16, K // 32, 4, 8).permute(0, 2, 3, 1, 4).contiguous().view(N, K)
-
-
 def mgemm_partial(x, w, splits: int, cfg: int = 0):
     """Split-K partial slabs [S, M, N] fp32 of x @ w^T on the mid-M decode GEMM (S = 1:
     the bf16 product [M, N])."""
@@ -293,77 +284,6 @@ def mgemm_partial(x, w, splits: int, cfg: int = 0):
     xs = x.float().reshape(-1, splits, K // splits)
     ws = w.float().reshape(-1, splits, K // splits)
     return torch.einsum("msk,nsk->smn", xs, ws).contiguous()
-
-
-_CHAIN = os.environ.get("DOCQA_DECODE_CHAIN", "0") == "1"
-
-
-def chain_plan(M: int, H: int, Ko: int, N2I: int, Nq: int) -> tuple[int, ...] | None:
-    """(S_o, cfg_o, S_d, cfg_d, S_q, cfg_q) of the persistent decode-layer chain (mgemm.hip
-    mgemm_chain_kernel) at M decode rows, or None where it does not apply: the chain runs
-    the standalone mid-M plans of the O, gate|up (fused SwiGLU, cfg 2), down and QKV
-    projections as work items of one launch, so it applies exactly where all four take the
-    mid-M GEMM (ops.mid_plan) with 128-wide (cfg 2) or 64-wide (cfg 7) tiles."""
-    if not _CHAIN or M % 2 or H > 8192 or H % 128:
-        return None
-    S_o, c_o = mid_plan(M, H, Ko)
-    S_g, c_g = mid_plan(M, N2I, H, glu=True)
-    S_d, c_d = mid_plan(M, H, N2I // 2)
-    S_q, c_q = mid_plan(M, Nq, H)
-    if not (S_o and S_g and S_d and S_q) or c_g != 2 or not {c_o, c_d, c_q} <= {2, 7}:
-        return None
-    return S_o, c_o, S_d, c_d, S_q, c_q
-
-
-def mgemm_chain(attn, w_o, residual, post_norm, w_gu, w_down, next_norm, w_qkv, counters, plan, eps: float):
-    """Back half of a decoder layer + the next layer's QKV in one persistent launch:
-    residual += O(attn); x1 = rmsnorm(residual) * post_norm; g = SwiGLU(x1 Wgu^T);
-    residual += down(g); x2 = rmsnorm(residual) * next_norm; returns (x2, the next layer's
-    QKV split-K slabs [S_q, M, Nq] or None).  Same bits as the six standalone launches."""
-    S_o, c_o, S_d, c_d, S_q, c_q = plan
-    if _gpu(attn):
-        x2, pq = _native().mgemm_chain(attn.contiguous(), w_o, residual, post_norm, w_gu, w_down, next_norm,
-                                       w_qkv, counters, S_o, c_o, S_d, c_d, S_q, c_q, eps)
-        return x2, (pq if w_qkv is not None else None)
-    def slabs(x, w, S):
-        p = mgemm_partial(x, w, S)
-        return p if S > 1 else p.float()[None]
-
-    x1 = add_rmsnorm_splitk(slabs(attn, w_o, S_o), residual, post_norm, eps)
-    g = mgemm_glu(x1, w_gu)
-    x2 = add_rmsnorm_splitk(slabs(g, w_down, S_d), residual, next_norm, eps)
-    return x2, (slabs(x2, w_qkv, S_q) if w_qkv is not None else None)
-
-
-_GLU_SPLIT = os.environ.get("DOCQA_GLU_SPLIT", "0") == "1"
-_GLU_SPLIT_CFG = int(os.environ.get("DOCQA_GLU_SPLIT_CFG", "6"))
-
-
-def glu_split_plan(M: int, N: int, K: int):
-    """(splits, cfg) of the fused-SwiGLU gate|up decode GEMM with the K range split over two
-    workgroups per 256-wide tile that meet in the launch (mgemm.hip glu_meet), or None.
-    256-wide tiles halve the X bytes each CU pulls per weight byte, and the 2-way split
-    gives them a full round of workgroups (Llama-3-8B: 112 tiles x 2)."""
-    if not _GLU_SPLIT or _MID_OFF or not (65 <= M <= MID_M_MAX) or N < 16384 or N % 256 or K % (2 * 64 * 2):
-        return None
-    return 2, _GLU_SPLIT_CFG
-
-
-def glu_split_workspace(max_m: int, N: int, device):
-    """(ws fp32, tick int32) for :func:`mgemm_glu_split` up to ``max_m`` rows and N."""
-    mt = (max_m + 255) // 256
-    ws = torch.empty(mt * N * 256, dtype=torch.float32, device=device)
-    tick = torch.zeros(2 * mt * (N // 128) + 1, dtype=torch.int32, device=device)
-    return ws, tick
-
-
-def mgemm_glu_split(x, w_il, splits: int, cfg: int, workspace):
-    """silu(x Wg^T) * (x Wu^T) with the K range split over ``splits`` workgroups per tile
-    meeting in the launch; ``workspace`` from :func:`glu_split_workspace`."""
-    if _gpu(x):
-        ws, tick = workspace
-        return _native().mgemm_glu_split(x.contiguous(), w_il, splits, cfg, ws, tick)
-    return silu_mul(torch.nn.functional.linear(x, w_il), interleaved=True)
 
 
 def mgemm_glu(x, w_il, cfg: int = 0):

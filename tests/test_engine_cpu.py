@@ -432,35 +432,6 @@ def test_mid_plan_glu_never_picks_narrow_tiles():
         assert S2 >= 1 or cfg2 == 0
 
 
-def test_chain_plan_and_cpu_path(monkeypatch):
-    """The persistent decode-layer chain applies where every projection takes the mid-M
-    GEMM (Llama-3-8B at 256 / 512 rows, odd buckets excluded), and its CPU rehearsal equals
-    the six standalone ops."""
-    import torch
-
-    from docqa_amd import ops
-
-    monkeypatch.setattr(ops, "_CHAIN", True)
-    assert ops.chain_plan(256, 4096, 4096, 28672, 6144) == (4, 7, 7, 2, 4, 2)
-    assert ops.chain_plan(512, 4096, 4096, 28672, 6144) is not None
-    assert ops.chain_plan(255, 4096, 4096, 28672, 6144) is None       # odd rows
-    assert ops.chain_plan(64, 4096, 4096, 28672, 6144) is None        # skinny regime
-    monkeypatch.setattr(ops, "_CHAIN", False)
-    assert ops.chain_plan(256, 4096, 4096, 28672, 6144) is None
-    torch.manual_seed(0)
-    M, H, inter, Nq = 8, 256, 512, 384
-    w = lambda n, k: (torch.randn(n, k) / k ** 0.5).bfloat16()   # noqa: E731
-    wo, wgu, wd, wq = w(H, H), w(2 * inter, H), w(H, inter), w(Nq, H)
-    post, nxt = torch.ones(H).bfloat16(), torch.ones(H).bfloat16()
-    a, r0 = torch.randn(M, H).bfloat16(), torch.randn(M, H).bfloat16()
-    r1, r2 = r0.clone(), r0.clone()
-    x2, pq = ops.mgemm_chain(a, wo, r1, post, wgu, wd, nxt, wq, None, (2, 2, 4, 2, 2, 2), 1e-5)
-    x1 = ops.add_rmsnorm_splitk(ops.mgemm_partial(a, wo, 2), r2, post, 1e-5)
-    x2r = ops.add_rmsnorm_splitk(ops.mgemm_partial(ops.mgemm_glu(x1, wgu), wd, 4), r2, nxt, 1e-5)
-    assert torch.equal(x2, x2r) and torch.equal(r1, r2)
-    assert torch.equal(pq, ops.mgemm_partial(x2r, wq, 2))
-
-
 def test_reserve_rolls_back_without_prefix_cache():
     """a batch that does not fit frees what it had reserved (prefix cache off)."""
     m = _model()
