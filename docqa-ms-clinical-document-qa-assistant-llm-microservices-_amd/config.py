@@ -17,6 +17,7 @@ the MI355X knobs of this framework.
 | DEID_NER | auto | the spaCy NER of deid-service/anonymizer.py:29,41-45: "auto" runs the token classifier when NER_CHECKPOINT names one, "1" always (random-init weights when none), "0" never |
 | NER_CHECKPOINT | (empty) | Hugging Face BERT token-classification checkpoint directory for DEID_NER |
 | DEID_BATCH_DOCS | 32 | raw messages the deid worker drains into one packed NER forward |
+| MAX_BATCH | 256 on a GPU, 64 on CPU | llm-qa decode slots (the measured batch) |
 | MAX_CONTEXT | 8192 | llm-qa engine context (prompt + generation); Llama-3's window |
 | QA_TEMPLATE | reference | llm-qa prompt: the verbatim reference text (llm-qa/main.py:71-93) or cache_friendly |
 """
@@ -89,7 +90,9 @@ class Settings:
     # stop a generation at EOS (the reference's behaviour); STOP_ON_EOS=0 decodes every
     # answer to MAX_NEW_TOKENS (serving benchmarks: random weights emit EOS at random)
     stop_on_eos: bool = field(default_factory=lambda: env_bool("STOP_ON_EOS", "true"))
-    max_batch: int = field(default_factory=lambda: env_int("MAX_BATCH", 64))
+    # decode slots: MAX_BATCH, else 256 on a GPU -- the batch every throughput number in
+    # profiles/ and BENCH_r*.json is measured at -- and 64 on CPU
+    max_batch: int = field(default_factory=lambda: _default_max_batch())
     # engine context window (prompt + generation): long synthese prompts are prefilled in
     # chunks up to it and truncated only beyond it
     max_context: int = field(default_factory=lambda: env_int("MAX_CONTEXT", 8192))
@@ -129,6 +132,20 @@ class Settings:
             return "cuda" if torch.cuda.is_available() else "cpu"
         except Exception:
             return "cpu"
+
+
+def _default_max_batch() -> int:
+    if os.environ.get("MAX_BATCH"):
+        return env_int("MAX_BATCH", 256)
+    dev = os.environ.get("DOCQA_DEVICE", "auto")
+    if dev == "auto":
+        try:
+            import torch
+
+            dev = "cuda" if torch.cuda.is_available() else "cpu"
+        except Exception:  # noqa: BLE001
+            dev = "cpu"
+    return 256 if dev.startswith("cuda") else 64
 
 
 def settings() -> Settings:

@@ -911,6 +911,18 @@ at::Tensor pgemm_partial(const at::Tensor& x, const at::Tensor& w, int64_t split
 
 int64_t group_persist_bins(int64_t cap, int64_t Hkv) { return docqa_group_persist_bins((int)cap, (int)Hkv); }
 
+// diagnostics: per-workgroup timeline of the grouped decode kernel into buf (int64
+// [>= workgroups x 8], see attn_decode.hip g_group_trace); None turns it off
+void set_decode_trace(const c10::optional<at::Tensor>& buf) {
+  long long* p = nullptr;
+  if (buf.has_value()) {
+    CHECK_GPU(*buf); CHECK_CONTIG(*buf);
+    TORCH_CHECK(buf->scalar_type() == at::kLong, "set_decode_trace: int64 buffer");
+    p = (long long*)buf->data_ptr<int64_t>();
+  }
+  CHECK_RC(docqa_set_decode_trace(p), "set_decode_trace");
+}
+
 bool pgemm_ok(int64_t M, int64_t N, int64_t K) { return docqa_pgemm_ok((int)M, (int)N, (int)K); }
 
 std::tuple<at::Tensor, at::Tensor> knn(const at::Tensor& xb, const at::Tensor& xb_norms,
@@ -1152,6 +1164,7 @@ TORCH_LIBRARY(docqa, m) {
   m.def("mgemm_argmax_val(Tensor x, Tensor w, int n_valid, int cfg=0) -> (Tensor, Tensor)");
   m.def("pgemm_ok(int M, int N, int K) -> bool", &pgemm_ok);
   m.def("group_persist_bins(int cap, int Hkv) -> int", &group_persist_bins);
+  m.def("set_decode_trace(Tensor? buf) -> ()", &set_decode_trace);
   m.def("paged_decode_cascade(Tensor q, Tensor k_cache, Tensor v_cache, Tensor block_tables, "
         "Tensor context_lens, int Hq, int max_context, float scale, Tensor prefix_table, Tensor prefix_len, "
         "int nchunk, Tensor? order=None) -> Tensor");

@@ -72,6 +72,7 @@ int docqa_paged_decode_cascade_persist(const void* q, int q_stride, void* k_cach
                                        float* pacc, float* pml, const int* items, const int* merges,
                                        const int* bins, int cap, float* ws_acc, float* ws_ml, hipStream_t s);
 int docqa_group_persist_bins(int cap, int Hkv);
+int docqa_set_decode_trace(long long* buf);
 int docqa_paged_decode_cascade_rope(void* qkv, int q_stride, const int* positions,
                                     const float* cos_sin, const int* slot_mapping, void* k_cache,
                                     void* v_cache, const int* block_tables, int maxb,

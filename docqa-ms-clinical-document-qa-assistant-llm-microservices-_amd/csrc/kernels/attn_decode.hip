@@ -983,6 +983,12 @@ __global__ __launch_bounds__(256) void paged_decode_mfma_kernel(
 // (P: the cascade prefix, attended by the prefix kernel and merged here).
 constexpr int kGroupMaxPos = 64;     // block positions beyond the cascade prefix (4096 tokens)
 
+// Diagnostic timeline of the group kernel (off unless docqa_set_decode_trace set a buffer):
+// per workgroup 8 int64 -- entry, tile list + Q ready, first tile landed, loop end, exit
+// (wall_clock64 ticks, 100 MHz), tiles streamed, HW_ID, XCC_ID.  One scalar load of a null
+// pointer per workgroup when off.
+__device__ long long* g_group_trace = nullptr;
+
 // SPLIT: `groups` is a work-item list [cap, 8] = (4 row ids, first block position, end
 // block position, partial slot or -1, 0): a long group's block positions are split over
 // several items (workgroups), each writing an un-normalised partial (m, l, O) for its 16
@@ -1012,6 +1018,9 @@ __global__ __launch_bounds__(256) void paged_decode_group_kernel(
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int hl = lane & 15, lg = lane >> 4;      // MFMA column (row slot x head) / lane group
+  long long* trace = g_group_trace;
+  long long tr0 = 0, tr1 = 0, tr2 = 0, tr3 = 0;
+  if (trace && tid == 0) tr0 = wall_clock64();
   const int P = ci.plen ? *ci.plen : 0;          // multiple of 64
   const int* gp = groups + (SPLIT ? 8 : R) * grp;
   int rows[R], Ls[R];
@@ -1129,6 +1138,15 @@ __global__ __launch_bounds__(256) void paged_decode_group_kernel(
   }
   __syncthreads();
   const int nt = s_nt;
+  if (trace && tid == 0) tr1 = wall_clock64();
+  auto trace_out = [&]() {
+    if (trace && tid == 0) {
+      long long* t = trace + ((size_t)blockIdx.y * gridDim.x + blockIdx.x) * 8;
+      t[0] = tr0; t[1] = tr1; t[2] = tr2; t[3] = tr3; t[4] = wall_clock64(); t[5] = nt;
+      t[6] = __builtin_amdgcn_s_getreg((31 << 11) | 4);
+      t[7] = __builtin_amdgcn_s_getreg(20 | (3 << 11)) & 15;
+    }
+  };
 
   const float qs = scale * kLog2e;
   const uint32_t ring_base = lds_u32(ring);
@@ -1158,6 +1176,7 @@ __global__ __launch_bounds__(256) void paged_decode_group_kernel(
   for (int jt = 0; jt < nt; ++jt) {
     wait_vmcnt<4 * (NSR - 2)>();                 // the next NSR-2 tiles (4 DMAs each) may fly
     ring_barrier();                              // tile jt visible; slot (jt-1) % NSR free
+    if (trace && tid == 0 && jt == 0) tr2 = wall_clock64();
     stage(jt + NSR - 1);
     const int2 e = s_tl[jt];
     const bool mine = (e.y & cbit) != 0;         // this column's row reads this block
@@ -1222,6 +1241,7 @@ __global__ __launch_bounds__(256) void paged_decode_group_kernel(
     }
   }
   wait_vmcnt<0>();                               // drain the clamped tail DMAs
+  if (trace && tid == 0) tr3 = wall_clock64();
 
   // ---- epilogue: lane holds O^T[dim 16 dt + 4 lg + r][column hl], dt = 2 wave + dd
   if constexpr (SPLIT) {
@@ -1256,9 +1276,11 @@ __global__ __launch_bounds__(256) void paged_decode_group_kernel(
         if (s_last) group_merge_body<true>(merges + 8 * mi, ws_acc, ws_ml, context_lens, B, Hkv, out, out_stride, ci,
                                            kvh, tid);
       }
+      trace_out();
       return;
     }
   }
+  trace_out();
   if (crow < 0) return;
   const int h = kvh * G + (hl & 3);
   uint16_t* op = out + (size_t)crow * out_stride + (size_t)h * D;
@@ -1902,6 +1924,12 @@ int docqa_paged_decode_cascade_persist(const void* q, int q_stride, void* k_cach
 }
 
 int docqa_group_persist_bins(int cap, int Hkv) { return group_persist_bins(cap, Hkv); }
+
+// diagnostics: route the group kernel's per-workgroup timeline into `buf` (int64 [wgs x 8]),
+// nullptr turns it off
+int docqa_set_decode_trace(long long* buf) {
+  return hipMemcpyToSymbol(HIP_SYMBOL(g_group_trace), &buf, sizeof(buf)) == hipSuccess ? 0 : -1;
+}
 
 // log-sum-exp merge of a sequence's context partitions (and, cascade, of the shared-prefix
 // chunk partials) -> normalised bf16 output

@@ -34,6 +34,10 @@ from .kv_cache import KVCache, TailCache, chain_keys
 
 _PREFILL_LOG = os.environ.get("DOCQA_PREFILL_LOG") == "1"   # one JSON line per prefill chunk
 _PREFILL_DUMP = os.environ.get("DOCQA_PREFILL_DUMP", "")       # dir: save paged-prefill shapes for replay
+# dir: save one cascade decode batch's tables / lengths / group plan for kernel replay
+# (scripts/decode_replay_probe.py); the first DOCQA_DECODE_DUMP_SKIP batches are skipped
+_DECODE_DUMP = os.environ.get("DOCQA_DECODE_DUMP", "")
+_DECODE_DUMP_SKIP = [int(os.environ.get("DOCQA_DECODE_DUMP_SKIP", "1"))]
 
 
 @dataclass
@@ -787,6 +791,8 @@ class LLMEngine:
             self.set_order(g, lens)
             if nshared:
                 self.set_groups(g, tables, [n + params.max_new_tokens for n in lens], nshared)
+                if _DECODE_DUMP:
+                    self._dump_decode(g, tables, lens, nshared, params)
             if not greedy:
                 g.inv_temp.fill_(1.0 / params.temperature)
                 g.top_k.fill_(params.top_k)
@@ -831,6 +837,22 @@ class LLMEngine:
         self.stats.prompt_tokens += sum(lens)
         self.stats.generated_tokens += B * params.max_new_tokens
         return Launched(r, host, ev, params, t0, t1, ar_err)
+
+    def _dump_decode(self, g: _DecodeGraph, tables, lens, nshared: int, params: SamplingParams) -> None:
+        """Diagnostics: the decode attention inputs of one cascade batch, for replaying the
+        grouped kernel on its real block layout outside the engine."""
+        if _DECODE_DUMP_SKIP[0] > 0:
+            _DECODE_DUMP_SKIP[0] -= 1
+            return
+        _DECODE_DUMP_SKIP[0] = 1 << 30
+        os.makedirs(_DECODE_DUMP, exist_ok=True)
+        torch.save({"tables": tables, "lens": lens, "nshared": nshared, "bp": g.bp,
+                    "groups": g.groups.cpu(), "max_new_tokens": params.max_new_tokens,
+                    "block_size": self.block_size, "num_blocks": self.kv.caches[0][0].shape[0],
+                    "max_blocks_per_seq": self.max_blocks_per_seq, "hq": self.model.hq, "hkv": self.model.hkv,
+                    "head_dim": self.cfg.head_dim, "cascade_chunks": self._cascade_chunks(g.bp),
+                    "inline": _inline_prefix_on() and not _defer_groups_on()},
+                   os.path.join(_DECODE_DUMP, "decode_batch.pt"))
 
     def collect(self, h: "Launched") -> list[list[int]]:
         """Wait for a :meth:`launch`ed batch, free its KV blocks and return its tokens."""

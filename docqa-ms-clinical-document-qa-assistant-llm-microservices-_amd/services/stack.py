@@ -12,7 +12,7 @@ from __future__ import annotations
 
 import logging
 import tempfile
-from dataclasses import dataclass
+from dataclasses import dataclass, field
 
 from ..bus.broker import InProcBroker, get_broker
 from ..index.follower import IndexFollower
@@ -35,7 +35,7 @@ class StackOptions:
     embed: str = "minilm-l6"
     ner: str = "clinical-bert"
     device: str = "cuda"
-    max_batch: int = 64
+    max_batch: int = field(default_factory=lambda: Settings().max_batch)   # MAX_BATCH: 256 on a GPU
     max_context: int | None = None   # None: Settings.max_context (MAX_CONTEXT, 8192) capped by the model
     use_graphs: bool = True
     # NER token classifier inside de-identification (reference: spaCy NER on every message,

@@ -11,6 +11,7 @@
 #   bench[:<bench.py args>]         python bench.py ... ; the JSON line is echoed
 #   py:<script> [args]              any python script (probes, micro-benchmarks; 600 s)
 #   prof:<tag>:<script> [args]      rocprofv3 --kernel-trace --stats -> gpurun_out/prof_<tag>/
+#   env:NAME=VALUE                  export NAME for the steps after it (A/B knobs)
 #   pmc:<tag>:<counters>:<script> [args]
 #                                   rocprofv3 --pmc <counters> --kernel-trace --stats (one pass;
 #                                   counters space-separated inside the step, keep within the
@@ -30,6 +31,8 @@ for step in "$@"; do
   log="gpurun_out/${n}_${kind}.log"
   t0=$(date +%s)
   case "$kind" in
+    env)
+      export "$arg"; echo "[gpu.sh] export $arg"; continue ;;
     suite)
       timeout -k 10 "${STEP_TIMEOUT:-900}" python -u -m pytest tests -m gpu -x -q --timeout 300 \
         --timeout-method thread $arg > "$log" 2>&1 ;;
