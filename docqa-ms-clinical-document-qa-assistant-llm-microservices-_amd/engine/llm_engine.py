@@ -415,6 +415,17 @@ class LLMEngine:
 
     # ------------------------------------------------------------------ decode step
     def _step_body(self, g: _DecodeGraph) -> None:
+        meta = self._decode_meta(g)
+        if g.greedy:
+            # greedy: the LM head's argmax is fused into its GEMM (no [B, vocab] logits)
+            nxt = self.model.forward(g.tokens, meta, self.kv.caches, greedy_ids=True)
+        else:
+            nxt = self._select(self.model.forward(g.tokens, meta, self.kv.caches), g)
+        ops.decode_advance(nxt.long().contiguous(), g.out, g.tokens, g.positions, g.context_lens, g.valid)
+
+    def _decode_meta(self, g: _DecodeGraph) -> AttnMeta:
+        """Attention metadata of one decode step of bucket ``g`` (slots of the new tokens,
+        cascade prefix and row groups when the step attends a shared prefix)."""
         slots = ops.decode_slots(g.block_tables, g.positions, g.valid, self.block_size)
         meta = AttnMeta(prefill=False, positions=g.positions, slot_mapping=slots,
                         block_tables=g.block_tables, context_lens=g.context_lens,
@@ -427,12 +438,7 @@ class LLMEngine:
                 meta.decode_defer = g.groups.dim() == 3 and _defer_groups_on()
                 meta.decode_inline = (g.groups.dim() == 3 and g.groups.shape[0] == 2 and _inline_prefix_on()
                                       and not _defer_groups_on())
-        if g.greedy:
-            # greedy: the LM head's argmax is fused into its GEMM (no [B, vocab] logits)
-            nxt = self.model.forward(g.tokens, meta, self.kv.caches, greedy_ids=True)
-        else:
-            nxt = self._select(self.model.forward(g.tokens, meta, self.kv.caches), g)
-        ops.decode_advance(nxt.long().contiguous(), g.out, g.tokens, g.positions, g.context_lens, g.valid)
+        return meta
 
     def _select(self, logits, g: _DecodeGraph):
         from .. import ops

@@ -21,10 +21,18 @@ requests join and leave between steps:
   * lagged readback: step t's tokens are copied to pinned host memory and read while
     step t+1 already runs, so the GPU never idles on the host's bookkeeping (a finished
     request rides one extra step inside its reserved blocks and that token is dropped);
-  * admission batching: under load, requests are admitted in groups (>= ``admit_min``
-    that can join -- waiting AND free slots -- or ``admit_wait_s`` after the first could),
-    so one prefill pass over the weights serves several new requests instead of stalling
-    every decode step.
+  * stall-free admission (mixed steps, DOCQA_MIXED_PREFILL=1, the default): while
+    requests decode, new prompts are prefilled in token-budgeted chunks
+    (DOCQA_CHUNK_TOKENS) that ride INSIDE the decode step's forward
+    (LlamaModel.forward_mixed): every projection makes one weight pass over the decode
+    rows and the chunk's tokens together, only attention is split by row kind.  A
+    running request never waits for a separate prefill pass and arrivals are admitted the
+    step they come (no hold to batch prefills); a prompt longer than the budget is spread
+    over several steps, its first token sampled when its last chunk has run;
+  * admission batching (mixed steps off): under load, requests are admitted in groups
+    (>= ``admit_min`` that can join -- waiting AND free slots -- or ``admit_wait_s``
+    after the first could), so one prefill pass over the weights serves several new
+    requests instead of stalling every decode step.
 
 Reference parity: the reference serves one blocking request at a time
 (llm-qa/main.py:111-117); its generator (Ollama) schedules requests internally.
@@ -45,7 +53,7 @@ from .. import ops
 from ..parallel import comm
 from ..parallel.custom_ar import CollectiveError
 from ..utils import tracing
-from .llm_engine import LLMEngine, SamplingParams, _bucket, _DecodeGraph
+from .llm_engine import LLMEngine, SamplingParams, _bucket, _DecodeGraph, _prefill_inputs
 
 
 @dataclass
@@ -68,6 +76,7 @@ class Request:
     orig_len: int = -1
     pos: int = 0
     preemptions: int = 0
+    filled: int = 0      # mixed steps: prompt tokens already in the KV cache
 
 
 class Lockstep:
@@ -135,6 +144,11 @@ class ContinuousEngine:
         self.generated = 0        # tokens emitted to requests
         self.completed = 0        # requests finished
         self.completed_short = 0  # ... of them before max_new_tokens (EOS)
+        # stall-free admission: prompt chunks ride in the decode step (module docstring)
+        self.mixed = os.environ.get("DOCQA_MIXED_PREFILL", "1") == "1"
+        self.chunk_tokens = max(engine.block_size, int(os.environ.get("DOCQA_CHUNK_TOKENS", "2048")))
+        self.prefilling: list[Request] = []   # admitted, prompt partly in the KV cache
+        self.mixed_steps = 0
 
     # ------------------------------------------------------------------ client side
     def submit(self, prompt: list[int], params: SamplingParams | None = None, on_token=None) -> cf.Future:
@@ -153,7 +167,7 @@ class ContinuousEngine:
         return fut
 
     def has_work(self) -> bool:
-        return bool(self.waiting or self.running or self._pending or self._unsynced)
+        return bool(self.waiting or self.running or self.prefilling or self._pending or self._unsynced)
 
     def generate(self, prompts: list[list[int]], params: SamplingParams | None = None) -> list[list[int]]:
         """Submit all prompts and drive the scheduler in this thread until they finish."""
@@ -237,11 +251,12 @@ class ContinuousEngine:
 
     def _fail_all(self, e: Exception) -> None:
         self._pending = None
-        for r in self.running:
+        for r in self.running + self.prefilling:
             self.eng.kv.allocator.free(r.blocks)
             if not r.future.done():
                 r.future.set_exception(e)
         self.running = []
+        self.prefilling = []
         self._version += 1
         self._master.valid.zero_()
         self._master.context_lens.zero_()
@@ -264,6 +279,9 @@ class ContinuousEngine:
         self._step(decision)
 
     def _step(self, decision) -> None:
+        if self._mixed_due():
+            self._mixed_step(decision)
+            return
         self._admit(decision)
         if self.running:
             self._decode()
@@ -313,12 +331,17 @@ class ContinuousEngine:
 
         health.collective_failure(f"lockstep follower step failed: {e!r}")
 
-    def _take_waiting(self) -> list[Request]:
+    def _take_waiting(self, mixed: bool = False, token_cap: int | None = None) -> list[Request]:
+        """Reserve KV blocks for waiting requests while slots are free.  ``mixed``: for the
+        chunked-prefill queue -- greedy requests only (a sampled one waits for a plain
+        admission), and stop once ``token_cap`` prompt tokens are taken."""
         eng, alloc = self.eng, self.eng.kv.allocator
         admitted, budget = [], 0
         with self._cv:
-            while self.waiting and len(self.running) + len(admitted) < self.max_running:
+            while self.waiting and len(self.running) + len(self.prefilling) + len(admitted) < self.max_running:
                 r = self.waiting[0]
+                if mixed and (r.params.temperature > 0 or (token_cap is not None and budget >= token_cap)):
+                    break
                 if r.orig_len < 0:
                     r.orig_len = len(r.prompt)
                 remaining = r.params.max_new_tokens - r.gen_base
@@ -345,6 +368,9 @@ class ContinuousEngine:
     def _admission_due(self) -> bool:
         """Whether the waiting requests are admitted at this step (the timing-dependent
         half of admission; a lockstep leader broadcasts it)."""
+        if self.mixed and self.running and self.waiting:
+            # chunks ride in the decode steps: admit as soon as a slot is free, no hold
+            return len(self.running) + len(self.prefilling) < self.max_running
         if self.running and self.waiting:
             # gather a group -- one prefill pass over the weights for several requests --
             # until admit_min requests can join or the first of them has waited
@@ -414,6 +440,136 @@ class ContinuousEngine:
         if joined:
             self._place(joined)
         self._update_shared()
+
+    # ------------------------------------------------------------------ mixed steps
+    def _mixed_due(self) -> bool:
+        """A mixed step runs while prompt chunks are pending, or when greedy requests wait
+        beside a greedy running batch (sampled decode rows keep the separate prefill)."""
+        if not self.mixed:
+            return False
+        if self.prefilling:
+            return True
+        return bool(self.running and self.waiting and self.waiting[0].params.temperature <= 0
+                    and all(r.params.temperature <= 0 for r in self.running))
+
+    def _mixed_step(self, decision) -> None:
+        """One forward over every running slot's next token AND up to ``chunk_tokens`` of
+        the pending prompts (LlamaModel.forward_mixed).  Synchronous: the chunk's first
+        tokens are needed on the host to place the completed prompts, so the previous
+        step's lagged readback is folded in first and this step's tokens are read here."""
+        eng, BS = self.eng, self.eng.block_size
+        if self._pending is not None:
+            p, self._pending = self._pending, None
+            self._process(p)
+        if decision is None:
+            decision = self._admission_due()
+        if decision and self.waiting:
+            pend = sum(len(r.prompt) - r.filled for r in self.prefilling)
+            cap = 2 * self.chunk_tokens - pend
+            if cap > 0:
+                for r in self._take_waiting(mixed=True, token_cap=cap):
+                    eng.queue_prefix_copies(r.res)
+                    r.filled = r.cached
+                    self.prefilling.append(r)
+        if not self.prefilling:
+            if self.running:
+                self._decode()
+            return
+        self._grow_tables()
+        t0 = time.perf_counter()
+        pieces, budget = [], self.chunk_tokens
+        for r in self.prefilling:
+            if budget <= 0:
+                break
+            start = min(r.filled, len(r.prompt) - 1)    # >= 1 token: its logits pick the first
+            end = min(len(r.prompt), start + budget)
+            pieces.append((r, start, end))
+            budget -= end - start
+        n = len(self.running)
+        dev = eng.device
+        g, bp, dmeta = None, 0, None
+        if n:
+            bp = _bucket(n, eng.max_batch) if self.pad_buckets else n
+            g = self._graph(bp, True, self._nshared > 0)
+            if eng.lpt:
+                eng.set_order(g, [len(r.prompt) + len(r.out) for r in self.running], key=self._version)
+            if self._nshared > 0:
+                eng.set_groups(g, [r.blocks for r in self.running],
+                               [len(r.prompt) + r.params.max_new_tokens for r in self.running], self._nshared,
+                               key=(self._version, self._nshared))
+            dmeta = eng._decode_meta(g)
+        from ..models.llama import AttnMeta
+
+        ids, pos, slots, cu = _prefill_inputs([r.prompt[:e] for r, _, e in pieces], [r.blocks for r, _, _ in pieces],
+                                              [s_ for _, s_, _ in pieces], BS)
+        maxb = max(len(r.blocks) for r, _, _ in pieces)
+        btab = torch.zeros(len(pieces), maxb, dtype=torch.int32)
+        for i, (r, _, _) in enumerate(pieces):
+            btab[i, :len(r.blocks)] = torch.tensor(r.blocks, dtype=torch.int32)
+        pmeta = AttnMeta(prefill=True, positions=torch.from_numpy(pos).to(dev), slot_mapping=torch.from_numpy(slots).to(dev),
+                         cu_seqlens=torch.from_numpy(cu).to(dev), max_len=max(e - s_ for _, s_, e in pieces),
+                         block_tables=btab.to(dev),
+                         prefix_lens=torch.tensor([s_ for _, s_, _ in pieces], dtype=torch.int32).to(dev))
+        done = [i for i, (r, _, e) in enumerate(pieces) if e == len(r.prompt)]
+        rows = list(range(bp)) + [bp + int(cu[i + 1]) - 1 for i in done]
+        chunk_ids = torch.from_numpy(ids).to(dev)
+        input_ids = torch.cat([g.tokens, chunk_ids]) if bp else chunk_ids
+        with tracing.span("sched.mixed", running=n, bucket=bp, chunk_tokens=int(cu[-1]), completes=len(done)):
+            nxt = eng.model.forward_mixed(input_ids, bp, dmeta, pmeta, eng.kv.caches,
+                                          torch.tensor(rows, dtype=torch.long).to(dev))
+            if bp:
+                ops.decode_advance(nxt[:bp].long().contiguous(), g.out, g.tokens, g.positions, g.context_lens,
+                                   g.valid)
+            err = comm.collective_error_snapshot()
+            toks = nxt.tolist()
+            comm.raise_on_collective_error(err)
+        self.steps += 1
+        self.mixed_steps += 1
+        now = time.perf_counter()
+        # decode rows: the same bookkeeping as a plain step (_decode + _process)
+        if n:
+            eng.stats.generated_tokens += n
+            snap = list(self.running)
+            for r in snap:
+                r.pos += 1
+            finished = []
+            for r, t in zip(snap, toks[:n]):
+                if r.done:
+                    continue
+                self._emit(r, t)
+                if self._finished(r):
+                    r.done = True
+                    finished.append(r)
+            if finished:
+                for r in finished:
+                    self._retire(r)
+                self._compact([i for i, r in enumerate(self.running) if not r.done])
+        # prompt chunks: progress, and first tokens of the prompts whose last chunk ran
+        joined, completed = [], []
+        for r, _, e in pieces:
+            r.filled = e
+        for i, t in zip(done, toks[bp:]):
+            completed.append((pieces[i][0], t))
+        if completed:
+            gone = {id(r) for r, _ in completed}
+            self.prefilling = [r for r in self.prefilling if id(r) not in gone]
+            reqs = [r for r, _ in completed]
+            eng.register_prefixes([r.prompt for r in reqs], [r.blocks for r in reqs],
+                                  [r.res.keys[0] if r.res is not None and r.res.keys else None for r in reqs])
+            eng.stats.prompt_tokens += sum(len(r.prompt) for r in reqs)
+            eng.stats.cached_tokens += sum(r.cached for r in reqs)
+            for r, t in completed:
+                r.t_first = now
+                self._emit(r, t)
+                if self._finished(r):
+                    r.done = True
+                    self._retire(r)
+                else:
+                    joined.append(r)
+        if joined:
+            self._place(joined)
+        self._update_shared()
+        eng.stats.decode_s += now - t0
 
     def _place(self, reqs: list[Request]) -> None:
         """Write the decode state of newly joined requests into slots [n, n + k)."""

@@ -491,6 +491,62 @@ class LlamaModel:
             return self.greedy_ids(x)
         return ops.prefill_linear(x, self.lm_head) if x.shape[0] > 512 else F.linear(x, self.lm_head)
 
+    def forward_mixed(self, input_ids: torch.Tensor, n_dec: int, dmeta: AttnMeta, pmeta: AttnMeta,
+                      kv_caches: list, logits_index: torch.Tensor) -> torch.Tensor:
+        """One forward over decode rows AND a prefill chunk (continuous batching without the
+        prefill stall): rows [0, n_dec) are decode slots (one new token each, paged decode
+        attention over their cache -- ``dmeta``, the decode step's metadata), rows
+        [n_dec, T) are prompt-chunk tokens (``pmeta``: positions / slots / cu_seqlens /
+        block_tables / prefix_lens of the chunk; attention over cached prefix + chunk).
+        Every projection runs ONCE over all T rows -- the decode rows ride in the prefill
+        GEMMs' weight pass -- and only attention is split by row kind.  Returns the greedy
+        ids of the rows in ``logits_index``.
+        Reference parity: the service loop the reference runs one request at a time
+        (llm-qa/main.py:111-117)."""
+        cfg = self.cfg
+        D, hq, hkv, eps = cfg.head_dim, self.hq, self.hkv, cfg.rms_eps
+        h, x = ops.embed_rmsnorm(input_ids, self.embed, self.layers[0]["in_norm"], eps)
+        residual = h
+        positions = torch.cat([dmeta.positions, pmeta.positions]) if n_dec else pmeta.positions
+        slots = torch.cat([dmeta.slot_mapping, pmeta.slot_mapping]) if n_dec else pmeta.slot_mapping
+        nl = len(self.layers)
+        M = x.shape[0]
+        for i, L in enumerate(self.layers):
+            kc, vc = kv_caches[i]
+            qkv = ops.prefill_linear(x, L["qkv"])
+            ops.rope_cache(qkv, positions, self.cos_sin, slots, kc, vc, hq, hkv, D)
+            parts = []
+            if n_dec:
+                parts.append(self._attend_decode(qkv[:n_dec], dmeta, kc, vc, n_dec))
+            parts.append(ops.flash_prefill_paged(qkv[n_dec:], pmeta.cu_seqlens, pmeta.max_len, hq, hkv, D,
+                                                 self.scale, kc, vc, pmeta.block_tables, pmeta.prefix_lens))
+            a = torch.cat(parts) if len(parts) > 1 else parts[0]
+            nxt = self.layers[i + 1]["in_norm"] if i + 1 < nl else self.final_norm
+            x = comm.tp_add_rmsnorm(ops.prefill_linear(a, L["o"]), residual, L["post_norm"], eps)
+            g = ops.prefill_glu(x, L["gate_up"])
+            x = comm.tp_add_rmsnorm(ops.prefill_linear(g, L["down"]), residual, nxt, eps)
+        assert x.shape[0] == M
+        return self.greedy_ids(x.index_select(0, logits_index))
+
+    def _attend_decode(self, qkv: torch.Tensor, meta: AttnMeta, kc, vc, M: int) -> torch.Tensor:
+        """Decode attention of post-RoPE bf16 QKV rows whose new K/V are already in the
+        cache: the grouped / plain cascade kernels when the step attends a shared prefix,
+        else per-row paged decode (the same dispatch as :meth:`forward`'s library-GEMM
+        branch)."""
+        hq = self.hq
+        if meta.shared_len is not None:
+            if meta.decode_groups is not None:
+                return ops.paged_decode_cascade_grouped(qkv, kc, vc, meta.block_tables, meta.context_lens, hq,
+                                                        self.scale, meta.shared_table, meta.shared_len,
+                                                        meta.cascade_chunks, meta.decode_groups, meta.decode_defer,
+                                                        self._decode_tick(M) if qkv.is_cuda else None,
+                                                        meta.decode_inline)
+            return ops.paged_decode_cascade(qkv, kc, vc, meta.block_tables, meta.context_lens, hq,
+                                            meta.max_context, self.scale, meta.shared_table, meta.shared_len,
+                                            meta.cascade_chunks, meta.seq_order)
+        return ops.paged_decode(qkv, kc, vc, meta.block_tables, meta.context_lens, hq, meta.max_context,
+                                self.scale, meta.seq_order)
+
     def _decode_tick(self, B: int):
         """Ticket words for the fused decode attention's in-kernel partition merge, shared
         by every layer (the launches are stream-ordered and each re-arms its words).  The
