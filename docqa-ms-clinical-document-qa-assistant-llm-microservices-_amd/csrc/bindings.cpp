@@ -4,6 +4,8 @@
 // current HIP stream, so they run under torch.cuda.graph capture (HIP graphs) and on
 // the side streams the pipeline uses for embed/search/generate overlap.
 #include <torch/library.h>
+#include <algorithm>
+#include <tuple>
 #include <ATen/ATen.h>
 #include <c10/hip/HIPStream.h>
 #include <c10/core/DeviceGuard.h>
@@ -473,6 +475,35 @@ at::Tensor paged_decode_grouped_fused(const at::Tensor& P, const at::Tensor& pos
   return out;
 }
 
+// deep-ring grouped decode variant (DOCQA_GROUP_DEEP_VARIANT: 0 = 7-tile ring, 4 items per
+// bin, 1 workgroup / CU; 1 = 3-tile ring, 2 / CU; 2 = 5-tile ring, 8 items per bin)
+static int group_deep_variant() {
+  static const int v = [] {
+    const char* e = getenv("DOCQA_GROUP_DEEP_VARIANT");
+    return e ? atoi(e) : 0;
+  }();
+  return v;
+}
+
+static int device_cus(int dev) {
+  static int cus[16] = {0};
+  if (dev < 0 || dev >= 16) return 256;
+  if (cus[dev] == 0) {
+    int n = 0;
+    if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0) n = 256;
+    cus[dev] = n;
+  }
+  return cus[dev];
+}
+
+// (bins per KV head, items per bin) the deep grouped decode plan must be built with
+std::tuple<int64_t, int64_t> group_deep_shape(int64_t Hkv) {
+  int nit = 0, dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) dev = 0;
+  const int nb = docqa_group_deep_shape(group_deep_variant(), (int)Hkv, device_cus(dev), &nit);
+  return {nb, nit};
+}
+
 at::Tensor paged_decode_cascade_split(const at::Tensor& q, at::Tensor k_cache, at::Tensor v_cache,
                                       const at::Tensor& block_tables, const at::Tensor& context_lens,
                                       int64_t Hq, double scale, const at::Tensor& prefix_table,
@@ -488,8 +519,8 @@ at::Tensor paged_decode_cascade_split(const at::Tensor& q, at::Tensor k_cache, a
   TORCH_CHECK(D == 128 && BS == 64 && Hq == 4 * Hkv, "split decode: head_dim 128, 64-token blocks, GQA 4");
   TORCH_CHECK(block_tables.size(1) <= 64, "split decode: <= 64 blocks per sequence");
   TORCH_CHECK(context_lens.numel() == B && block_tables.size(0) >= B, "split decode: B rows");
-  TORCH_CHECK(plan.dim() == 3 && (plan.size(0) == 2 || plan.size(0) == 3) && plan.size(2) == 8 &&
-              plan.size(1) >= 1, "plan: [2, cap, 8] (split) or [3, cap, 8] (persistent bins)");
+  TORCH_CHECK(plan.dim() == 3 && plan.size(0) >= 2 && plan.size(0) <= 4 && plan.size(2) == 8 && plan.size(1) >= 1,
+              "plan: [2, cap, 8] (split), [3, cap, 8] (persistent bins) or [4, cap, 8] (deep-ring bins)");
   TORCH_CHECK(prefix_table.numel() >= 1 && prefix_len.numel() == 1, "cascade decode: prefix table / length");
   const int cap = plan.size(1);
   c10::DeviceGuard g(q.device());
@@ -505,6 +536,21 @@ at::Tensor paged_decode_cascade_split(const at::Tensor& q, at::Tensor k_cache, a
     CHECK_GPU((*tick)); CHECK_I32((*tick));
     TORCH_CHECK(tick->numel() >= (int64_t)cap * Hkv, "split decode: tick needs cap * Hkv entries");
     tick_ptr = tick->data_ptr<int>();
+  }
+  if (plan.size(0) == 4) {
+    // deep-ring persistent bins (inline prefix, split groups merged by their last item)
+    TORCH_CHECK(tick_ptr && inline_prefix && !defer, "deep grouped decode: needs tick words and an inline-prefix plan");
+    int nit = 0;
+    const int nb = std::min(docqa_group_deep_shape(group_deep_variant(), Hkv, device_cus(q.device().index()), &nit),
+                            cap);
+    CHECK_RC(docqa_paged_decode_group_deep(q.data_ptr(), q.stride(0), k_cache.data_ptr(), v_cache.data_ptr(),
+                                           block_tables.data_ptr<int>(), block_tables.size(1),
+                                           context_lens.data_ptr<int>(), out.data_ptr(), Hq * D, B, Hq, Hkv, BS,
+                                           (float)scale, pp, pp + 8 * cap, pp + 16 * cap, nb,
+                                           ws_acc.data_ptr<float>(), ws_ml.data_ptr<float>(), tick_ptr,
+                                           group_deep_variant(), stream()),
+             "paged_decode_group_deep");
+    return out;
   }
   if (plan.size(0) == 3) {
     CHECK_RC(docqa_paged_decode_cascade_persist(q.data_ptr(), q.stride(0), k_cache.data_ptr(), v_cache.data_ptr(),
@@ -1165,6 +1211,7 @@ TORCH_LIBRARY(docqa, m) {
   m.def("pgemm_ok(int M, int N, int K) -> bool", &pgemm_ok);
   m.def("group_persist_bins(int cap, int Hkv) -> int", &group_persist_bins);
   m.def("set_decode_trace(Tensor? buf) -> ()", &set_decode_trace);
+  m.def("group_deep_shape(int Hkv) -> (int, int)", &group_deep_shape);
   m.def("paged_decode_cascade(Tensor q, Tensor k_cache, Tensor v_cache, Tensor block_tables, "
         "Tensor context_lens, int Hq, int max_context, float scale, Tensor prefix_table, Tensor prefix_len, "
         "int nchunk, Tensor? order=None) -> Tensor");

@@ -73,6 +73,11 @@ int docqa_paged_decode_cascade_persist(const void* q, int q_stride, void* k_cach
                                        const int* bins, int cap, float* ws_acc, float* ws_ml, hipStream_t s);
 int docqa_group_persist_bins(int cap, int Hkv);
 int docqa_set_decode_trace(long long* buf);
+int docqa_paged_decode_group_deep(const void* q, int q_stride, void* k_cache, void* v_cache, const int* block_tables,
+                                  int maxb, const int* context_lens, void* out, int out_stride, int B, int Hq, int Hkv,
+                                  int BS, float scale, const int* items, const int* merges, const int* bins,
+                                  int nbins, float* ws_acc, float* ws_ml, int* tick, int variant, hipStream_t s);
+int docqa_group_deep_shape(int variant, int Hkv, int cus, int* items_per_bin);
 int docqa_paged_decode_cascade_rope(void* qkv, int q_stride, const int* positions,
                                     const float* cos_sin, const int* slot_mapping, void* k_cache,
                                     void* v_cache, const int* block_tables, int maxb,

@@ -239,6 +239,7 @@ _MID_OFF = os.environ.get("DOCQA_MID_GEMM", "1") == "0"
 _MID_CFG = int(os.environ.get("DOCQA_MID_CFG", "2"))
 _MID_NARROW = os.environ.get("DOCQA_MID_NARROW", "1") == "1"
 _MID_WG_CAP = int(os.environ.get("DOCQA_MID_WG_CAP", "224"))
+_L2_XCD_BYTES = 4 << 20          # one XCD's L2 (MI355X_MICROARCH.md)
 
 
 def mid_plan(M: int, N: int, K: int, glu: bool = False) -> tuple[int, int]:
@@ -265,6 +266,12 @@ def mid_plan(M: int, N: int, K: int, glu: bool = False) -> tuple[int, int]:
     S = max(s for s in range(1, kb + 1) if kb % s == 0 and (s == 1 or tiles * s <= _MID_WG_CAP))
     if glu:
         return S, _MID_CFG
+    if _MID_CFG == 2 and M * K * 2 > _L2_XCD_BYTES and kb % 8 == 0 and tiles * 8 <= 256 and S < 8:
+        # activations larger than one XCD's L2 (down: 256 x 14336 bf16 = 7.3 MB): 8 slices,
+        # one per XCD (mgemm.hip remap 1), so each L2 holds only its 0.9 MB slice of X --
+        # down S=8 40.5 vs S=7 44.1 us, 46.4 vs 48.8 with the add+norm consumer
+        # (profiles/r5_mid_consumer_probe.log)
+        return 8, _MID_CFG
     if _MID_CFG == 2 and _MID_NARROW and S > 1 and tiles * S <= 128 and N % 64 == 0:
         # the split left half the chip idle (O: 32 tiles x S=4): 64-wide tiles (cfg 7) at
         # the same split fill it with the same slab bytes -- O 17.5 vs 20.7 us
@@ -642,7 +649,7 @@ def paged_decode_cascade_grouped(q, k_cache, v_cache, block_tables, context_lens
             return _native().paged_decode_cascade_split(q, k_cache, v_cache, block_tables, context_lens, Hq,
                                                         scale, prefix_table, prefix_len, nchunk, groups,
                                                         defer and groups.shape[0] == 2, tick,
-                                                        bool(inline_prefix) and groups.shape[0] == 2)
+                                                        bool(inline_prefix) and groups.shape[0] in (2, 4))
         return _native().paged_decode_cascade_grouped(q, k_cache, v_cache, block_tables, context_lens, Hq,
                                                       scale, prefix_table, prefix_len, nchunk, groups)
     max_context = block_tables.shape[1] * k_cache.shape[2]
@@ -786,9 +793,17 @@ def persist_bins(cap: int, Hkv: int) -> int:
 BIN_ITEMS, BIN_MAX_TILES = 8, 512    # attn_decode.hip kBinItems / kBinMaxTiles
 
 
+def group_deep_shape(Hkv: int) -> tuple[int, int]:
+    """(bins per KV head, items per bin) of the deep-ring persistent grouped decode
+    (attn_decode.hip paged_decode_group_deep_kernel, DOCQA_GROUP_DEEP_VARIANT): one bin per
+    resident workgroup, so a plan built with it never needs a second launch round."""
+    nb, nit = _native().group_deep_shape(int(Hkv))
+    return int(nb), int(nit)
+
+
 def split_decode_groups(quads: list[list[int]], tables: list[list[int]], lens: list[int], skip: int,
                         block_size: int, cap: int, tiles_per_item: int = 12, bins: int = 0,
-                        defer: bool = False) -> torch.Tensor:
+                        defer: bool = False, deep: tuple[int, int] | None = None) -> torch.Tensor:
     """Split plan for the grouped cascade decode (``paged_decode_cascade_grouped`` with a
     [2, cap, 8] int32 ``groups``): every group of :func:`pack_decode_groups` is cut at block
     positions into work items of about ``tiles_per_item`` K/V tiles (``lens``: the lengths
@@ -807,7 +822,12 @@ def split_decode_groups(quads: list[list[int]], tables: list[list[int]], lens: l
 
     ``defer``: every item writes a partial and every group has a merge row (at most ``cap``),
     as in the persistent plan, so no item reads the cascade-prefix partials and the prefix
-    kernel runs on a side stream beside the group kernel (attn_decode.hip, DOCQA_GROUP_DEFER)."""
+    kernel runs on a side stream beside the group kernel (attn_decode.hip, DOCQA_GROUP_DEFER).
+
+    ``deep`` = (bins, items per bin): the DEEP-RING plan [4, cap, 8] -- plan[0] / plan[1] as
+    the split plan (unsplit groups finish in their item, split groups are merged by their
+    last item's workgroup), plan[2] the items packed longest-first onto the least-loaded of
+    ``bins`` bins (<= items per bin, <= 512 tiles each; dense from bin 0), plan[3] unused."""
     budget = max(1, tiles_per_item)
     all_partial = bool(bins) or defer
     while True:
@@ -841,11 +861,38 @@ def split_decode_groups(quads: list[list[int]], tables: list[list[int]], lens: l
         if fits and bins:
             nb = min(bins, cap)
             fits = len(items) <= nb * BIN_ITEMS and all(t <= BIN_MAX_TILES for t, _ in items)
+        if fits and deep:
+            nb = min(deep[0], cap)
+            fits = len(items) <= nb * deep[1] and all(t <= BIN_MAX_TILES for t, _ in items)
         if fits:
             break
         if budget > 1 << 20:
             raise ValueError(f"split_decode_groups: {len(quads)} groups exceed the plan capacity {cap}")
         budget *= 2
+    if deep:
+        items.sort(key=lambda it: -it[0])
+        nb, nit = min(deep[0], cap), deep[1]
+        load, members = [0] * nb, [[] for _ in range(nb)]
+        for i, (t, _) in enumerate(items):                # longest first (sorted above)
+            best = min((b for b in range(nb) if len(members[b]) < nit and load[b] + t <= BIN_MAX_TILES),
+                       key=lambda b: (load[b], len(members[b])), default=None)
+            if best is None:
+                raise ValueError("split_decode_groups: items exceed the deep bins")
+            members[best].append(i)
+            load[best] += t
+        members.sort(key=lambda mem: -len(mem))           # dense: used bins first
+        plan = torch.full((4, cap, 8), -1, dtype=torch.int32)
+        plan[:2, :, 4:] = 0
+        plan[0, len(items):, 6] = -1
+        plan[3] = 0
+        if items:
+            plan[0, :len(items)] = torch.tensor([it[1] for it in items], dtype=torch.int32)
+        if merges:
+            plan[1, :len(merges)] = torch.tensor(merges, dtype=torch.int32)
+        for b, mem in enumerate(members):
+            for j, i in enumerate(mem):
+                plan[2, b, j] = i
+        return plan
     if not bins:
         items.sort(key=lambda it: -it[0])
         plan = torch.full((2, cap, 8), -1, dtype=torch.int32)

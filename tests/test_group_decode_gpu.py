@@ -282,3 +282,67 @@ def test_identity_plan_matches_per_row(native, monkeypatch, mode):
     out = native.paged_decode_cascade_grouped(q, kc, vc, bt, cl, Hq, scale, pt, plen, 4, plan,
                                               _defer_groups_on())
     assert (out.float() - ref.float()).abs().max().item() < 2e-2
+
+
+@pytest.mark.parametrize("B,Hkv,seed", [(37, 8, 0), (256, 8, 3), (9, 2, 5), (512, 8, 4)])
+@pytest.mark.parametrize("tiles", [1, 3, 12, 1000])
+def test_deep_grouped_cascade_matches_per_row(native, B, Hkv, seed, tiles):
+    """Deep-ring persistent plan (items LPT-packed into one bin per resident workgroup, one
+    ring across item boundaries, unsplit groups finished in their item, split groups merged
+    by their last item) == per-row cascade and the fp32 reference, tickets re-armed; END-of-
+    decode planning lengths, so some items have no live keys yet."""
+    Hq, D, BS, Pb, maxb = 4 * Hkv, 128, 64, 3, 12
+    tables, lens, nblk = _trie_batch(B, Pb, maxb, seed)
+    kc = torch.randn(nblk, Hkv, BS, D, device="cuda", dtype=torch.bfloat16)
+    vc = torch.randn_like(kc)
+    bt = torch.tensor(tables, dtype=torch.int32, device="cuda")
+    cl = torch.tensor(lens, dtype=torch.int32, device="cuda")
+    q = torch.randn(B, (Hq + 2 * Hkv) * D, device="cuda", dtype=torch.bfloat16)
+    pt = torch.zeros(maxb, dtype=torch.int32, device="cuda")
+    pt[:Pb] = bt[0, :Pb]
+    plen = torch.tensor([Pb * BS], dtype=torch.int32, device="cuda")
+    scale = 1 / math.sqrt(D)
+    with native.use_reference():
+        ref32 = native.paged_decode_cascade(q, kc, vc, bt, cl, Hq, maxb * BS, scale, pt, plen, 4)
+    end_lens = [min(L + 128, maxb * BS) for L in lens]
+    cap = max(B, 4)
+    quads = native.pack_decode_groups(tables, end_lens, Pb, BS, (B + 1) // 2)
+    deep = native.group_deep_shape(Hkv)
+    assert deep[0] >= 1 and deep[1] >= 4
+    plan = native.split_decode_groups(quads, tables, end_lens, 0, BS, cap, tiles, deep=deep)
+    assert plan.shape == (4, cap, 8)
+    used = plan[2][plan[2] >= 0]
+    nitems = int((plan[0, :, :4] >= 0).any(1).sum())
+    assert sorted(used.tolist()) == list(range(nitems))             # every item in exactly one bin
+    tick = torch.zeros(cap * Hkv, dtype=torch.int32, device="cuda")
+    for _ in range(2):
+        out = native.paged_decode_cascade_grouped(q, kc, vc, bt, cl, Hq, scale, pt, plen, 4, plan.cuda(), False,
+                                                  tick, True)
+        torch.cuda.synchronize()
+        err32 = (out.float() - ref32.float()).abs().max().item()
+        assert err32 < 3e-2, err32
+        assert int(tick.abs().sum()) == 0
+
+
+def test_deep_plan_balances_bins(native):
+    """The deep plan's bins carry about the same number of tiles (LPT onto the least-loaded
+    bin), and every bin index the kernel launches exists in the plan."""
+    Hkv, BS, Pb, maxb = 8, 64, 5, 32
+    B = 256
+    tables, lens, _ = _trie_batch(B, Pb, maxb, 11)
+    end_lens = [min(L + 128, maxb * BS) for L in lens]
+    quads = native.pack_decode_groups(tables, end_lens, Pb, BS, (B + 1) // 2)
+    deep = native.group_deep_shape(Hkv)
+    plan = native.split_decode_groups(quads, tables, end_lens, 0, BS, B, 40, deep=deep)
+    loads = []
+    items = plan[0]
+    for b in range(min(deep[0], B)):
+        mem = [int(i) for i in plan[2, b] if i >= 0]
+        t = 0
+        for i in mem:
+            rows = [int(r) for r in items[i, :4] if r >= 0]
+            lo, hi = int(items[i, 4]), int(items[i, 5])
+            t += sum(tt for pos, tt in native.group_tiles_by_position(tables, end_lens, rows, 0, BS) if lo <= pos < hi)
+        loads.append(t)
+    busy = [x for x in loads if x > 0]
+    assert busy and max(busy) <= 1.6 * (sum(busy) / len(busy)) + 40, loads
