@@ -475,35 +475,6 @@ at::Tensor paged_decode_grouped_fused(const at::Tensor& P, const at::Tensor& pos
   return out;
 }
 
-// deep-ring grouped decode variant (DOCQA_GROUP_DEEP_VARIANT: 0 = 7-tile ring, 4 items per
-// bin, 1 workgroup / CU; 1 = 3-tile ring, 2 / CU; 2 = 5-tile ring, 8 items per bin)
-static int group_deep_variant() {
-  static const int v = [] {
-    const char* e = getenv("DOCQA_GROUP_DEEP_VARIANT");
-    return e ? atoi(e) : 0;
-  }();
-  return v;
-}
-
-static int device_cus(int dev) {
-  static int cus[16] = {0};
-  if (dev < 0 || dev >= 16) return 256;
-  if (cus[dev] == 0) {
-    int n = 0;
-    if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0) n = 256;
-    cus[dev] = n;
-  }
-  return cus[dev];
-}
-
-// (bins per KV head, items per bin) the deep grouped decode plan must be built with
-std::tuple<int64_t, int64_t> group_deep_shape(int64_t Hkv) {
-  int nit = 0, dev = 0;
-  if (hipGetDevice(&dev) != hipSuccess) dev = 0;
-  const int nb = docqa_group_deep_shape(group_deep_variant(), (int)Hkv, device_cus(dev), &nit);
-  return {nb, nit};
-}
-
 at::Tensor paged_decode_cascade_split(const at::Tensor& q, at::Tensor k_cache, at::Tensor v_cache,
                                       const at::Tensor& block_tables, const at::Tensor& context_lens,
                                       int64_t Hq, double scale, const at::Tensor& prefix_table,
@@ -519,8 +490,8 @@ at::Tensor paged_decode_cascade_split(const at::Tensor& q, at::Tensor k_cache, a
   TORCH_CHECK(D == 128 && BS == 64 && Hq == 4 * Hkv, "split decode: head_dim 128, 64-token blocks, GQA 4");
   TORCH_CHECK(block_tables.size(1) <= 64, "split decode: <= 64 blocks per sequence");
   TORCH_CHECK(context_lens.numel() == B && block_tables.size(0) >= B, "split decode: B rows");
-  TORCH_CHECK(plan.dim() == 3 && plan.size(0) >= 2 && plan.size(0) <= 4 && plan.size(2) == 8 && plan.size(1) >= 1,
-              "plan: [2, cap, 8] (split), [3, cap, 8] (persistent bins) or [4, cap, 8] (deep-ring bins)");
+  TORCH_CHECK(plan.dim() == 3 && plan.size(0) >= 2 && plan.size(0) <= 3 && plan.size(2) == 8 && plan.size(1) >= 1,
+              "plan: [2, cap, 8] (split) or [3, cap, 8] (persistent bins)");
   TORCH_CHECK(prefix_table.numel() >= 1 && prefix_len.numel() == 1, "cascade decode: prefix table / length");
   const int cap = plan.size(1);
   c10::DeviceGuard g(q.device());
@@ -536,21 +507,6 @@ at::Tensor paged_decode_cascade_split(const at::Tensor& q, at::Tensor k_cache, a
     CHECK_GPU((*tick)); CHECK_I32((*tick));
     TORCH_CHECK(tick->numel() >= (int64_t)cap * Hkv, "split decode: tick needs cap * Hkv entries");
     tick_ptr = tick->data_ptr<int>();
-  }
-  if (plan.size(0) == 4) {
-    // deep-ring persistent bins (inline prefix, split groups merged by their last item)
-    TORCH_CHECK(tick_ptr && inline_prefix && !defer, "deep grouped decode: needs tick words and an inline-prefix plan");
-    int nit = 0;
-    const int nb = std::min(docqa_group_deep_shape(group_deep_variant(), Hkv, device_cus(q.device().index()), &nit),
-                            cap);
-    CHECK_RC(docqa_paged_decode_group_deep(q.data_ptr(), q.stride(0), k_cache.data_ptr(), v_cache.data_ptr(),
-                                           block_tables.data_ptr<int>(), block_tables.size(1),
-                                           context_lens.data_ptr<int>(), out.data_ptr(), Hq * D, B, Hq, Hkv, BS,
-                                           (float)scale, pp, pp + 8 * cap, pp + 16 * cap, nb,
-                                           ws_acc.data_ptr<float>(), ws_ml.data_ptr<float>(), tick_ptr,
-                                           group_deep_variant(), stream()),
-             "paged_decode_group_deep");
-    return out;
   }
   if (plan.size(0) == 3) {
     CHECK_RC(docqa_paged_decode_cascade_persist(q.data_ptr(), q.stride(0), k_cache.data_ptr(), v_cache.data_ptr(),
@@ -969,6 +925,10 @@ void set_decode_trace(const c10::optional<at::Tensor>& buf) {
   CHECK_RC(docqa_set_decode_trace(p), "set_decode_trace");
 }
 
+// grouped decode kernel choice for split plans: 1 = wave-parallel, 0 = cooperative, -1 =
+// query; returns the previous setting
+int64_t set_group_wave(int64_t on) { return docqa_set_group_wave((int)on); }
+
 bool pgemm_ok(int64_t M, int64_t N, int64_t K) { return docqa_pgemm_ok((int)M, (int)N, (int)K); }
 
 std::tuple<at::Tensor, at::Tensor> knn(const at::Tensor& xb, const at::Tensor& xb_norms,
@@ -1071,6 +1031,65 @@ std::tuple<at::Tensor, at::Tensor> ivfpq_search(const at::Tensor& xq, const at::
                               list_off.data_ptr<int64_t>(), probes.data_ptr<int64_t>(), nq, nprobe, d,
                               M, k, ws_d.data_ptr<float>(), ws_i.data_ptr<int>(),
                               out_d.data_ptr<float>(), out_i.data_ptr<int64_t>(), stream()), "ivfpq_search");
+  return {out_d, out_i};
+}
+
+std::tuple<at::Tensor, at::Tensor> ivfpq_search_pt(const at::Tensor& xq, const at::Tensor& centroids,
+                                                   const at::Tensor& pq, const at::Tensor& codes,
+                                                   const at::Tensor& norms, const at::Tensor& ids,
+                                                   const at::Tensor& list_off, const at::Tensor& probes, int64_t k,
+                                                   int64_t pc) {
+  CHECK_GPU(xq); CHECK_CONTIG(xq); CHECK_CONTIG(centroids); CHECK_CONTIG(pq); CHECK_CONTIG(codes);
+  CHECK_CONTIG(probes); CHECK_CONTIG(norms); CHECK_CONTIG(ids); CHECK_CONTIG(list_off);
+  TORCH_CHECK(xq.scalar_type() == at::kFloat && centroids.scalar_type() == at::kFloat &&
+              pq.scalar_type() == at::kFloat && norms.scalar_type() == at::kFloat,
+              "ivfpq_pt: fp32 queries / centroids / codebook / norms");
+  TORCH_CHECK(codes.scalar_type() == at::kByte, "codes must be uint8");
+  TORCH_CHECK(ids.scalar_type() == at::kLong && list_off.scalar_type() == at::kLong &&
+              probes.scalar_type() == at::kLong, "ids / list offsets / probes must be int64");
+  const int nq = xq.size(0), d = xq.size(1), nprobe = probes.size(1), M = pq.size(0);
+  TORCH_CHECK(pq.size(1) == 256 && pq.size(2) * M == d, "pq codebook must be [M, 256, d/M]");
+  TORCH_CHECK(codes.size(1) == M && norms.size(0) == codes.size(0) && ids.size(0) == codes.size(0),
+              "codes [N, M], norms [N], ids [N]");
+  TORCH_CHECK(centroids.size(1) == d && list_off.size(0) == centroids.size(0) + 1, "centroids / list offsets");
+  TORCH_CHECK(probes.size(0) == nq, "probes must be [nq, nprobe]");
+  TORCH_CHECK(M % 4 == 0 && (size_t)M * 512 + 1024 * 8 + 272 * 4 <= 160 * 1024, "ivfpq_pt: M % 4 == 0, M <= 300");
+  TORCH_CHECK(k >= 1 && k <= 64, "k must be in [1, 64]");
+  TORCH_CHECK(pc >= 1, "probes per workgroup must be >= 1");
+  const int kp = k <= 8 ? 8 : k <= 16 ? 16 : k <= 32 ? 32 : 64;
+  const int nchunk = (nprobe + (int)pc - 1) / (int)pc;
+  c10::DeviceGuard g(xq.device());
+  auto out_d = at::empty({nq, k}, xq.options());
+  auto out_i = at::empty({nq, k}, xq.options().dtype(at::kLong));
+  auto lut = at::empty({nq, M, 256}, xq.options().dtype(at::kHalf));
+  auto base = at::empty({nq, nprobe}, xq.options());
+  auto ws_d = at::empty({nq, nchunk, kp}, xq.options());
+  auto ws_i = at::empty({nq, nchunk, kp}, xq.options().dtype(at::kInt));
+  CHECK_RC(docqa_ivfpq_search_pt(xq.data_ptr<float>(), centroids.data_ptr<float>(), pq.data_ptr<float>(),
+                                 codes.data_ptr<uint8_t>(), norms.data_ptr<float>(), ids.data_ptr<int64_t>(),
+                                 list_off.data_ptr<int64_t>(), probes.data_ptr<int64_t>(), nq, nprobe, d, M, k,
+                                 (int)pc, lut.data_ptr(), base.data_ptr<float>(), ws_d.data_ptr<float>(),
+                                 ws_i.data_ptr<int>(), out_d.data_ptr<float>(), out_i.data_ptr<int64_t>(), stream()),
+           "ivfpq_search_pt");
+  return {out_d, out_i};
+}
+
+std::tuple<at::Tensor, at::Tensor> refine_flat(const at::Tensor& xb, const at::Tensor& xq, const at::Tensor& cand,
+                                               int64_t k, bool ip) {
+  CHECK_GPU(xb); CHECK_CONTIG(xb); CHECK_CONTIG(xq); CHECK_CONTIG(cand);
+  TORCH_CHECK(xb.scalar_type() == at::kFloat || xb.scalar_type() == at::kBFloat16, "refine: fp32 / bf16 vectors");
+  TORCH_CHECK(xq.scalar_type() == at::kFloat && cand.scalar_type() == at::kLong, "refine: fp32 queries, int64 ids");
+  TORCH_CHECK(xb.dim() == 2 && xq.dim() == 2 && xq.size(1) == xb.size(1) && cand.size(0) == xq.size(0),
+              "refine: xb [N, d], xq [nq, d], cand [nq, kc]");
+  TORCH_CHECK(cand.size(1) >= 1 && cand.size(1) <= 64 && k >= 1, "refine: 1..64 candidates per query");
+  const int nq = xq.size(0), d = xq.size(1);
+  c10::DeviceGuard g(xq.device());
+  auto out_d = at::empty({nq, k}, xq.options());
+  auto out_i = at::empty({nq, k}, xq.options().dtype(at::kLong));
+  CHECK_RC(docqa_refine_flat(xb.data_ptr(), xb.scalar_type() == at::kBFloat16 ? 1 : 0, xb.size(0),
+                             xq.data_ptr<float>(), cand.data_ptr<int64_t>(), nq, cand.size(1), d, k, ip ? 1 : 0,
+                             out_d.data_ptr<float>(), out_i.data_ptr<int64_t>(), stream()),
+           "refine_flat");
   return {out_d, out_i};
 }
 
@@ -1187,6 +1206,9 @@ TORCH_LIBRARY(docqa, m) {
   m.def("fp32_gemm_nt(Tensor x, Tensor w) -> Tensor");
   m.def("ivfpq_search(Tensor xq, Tensor centroids, Tensor pq, Tensor codes, Tensor ids, "
         "Tensor list_off, Tensor probes, int k) -> (Tensor, Tensor)");
+  m.def("ivfpq_search_pt(Tensor xq, Tensor centroids, Tensor pq, Tensor codes, Tensor norms, Tensor ids, "
+        "Tensor list_off, Tensor probes, int k, int pc) -> (Tensor, Tensor)");
+  m.def("refine_flat(Tensor xb, Tensor xq, Tensor cand, int k, bool ip) -> (Tensor, Tensor)");
   m.def("pq_encode(Tensor x, Tensor centroids, Tensor assign, Tensor pq) -> Tensor");
   m.def("gemm(Tensor a, Tensor w, Tensor? bias, Tensor? residual, int epi) -> Tensor");
   m.def("flash_prefill_paged(Tensor qkv, Tensor cu_seqlens, int max_len, int Hq, int Hkv, int D, "
@@ -1211,7 +1233,7 @@ TORCH_LIBRARY(docqa, m) {
   m.def("pgemm_ok(int M, int N, int K) -> bool", &pgemm_ok);
   m.def("group_persist_bins(int cap, int Hkv) -> int", &group_persist_bins);
   m.def("set_decode_trace(Tensor? buf) -> ()", &set_decode_trace);
-  m.def("group_deep_shape(int Hkv) -> (int, int)", &group_deep_shape);
+  m.def("set_group_wave(int on) -> int", &set_group_wave);
   m.def("paged_decode_cascade(Tensor q, Tensor k_cache, Tensor v_cache, Tensor block_tables, "
         "Tensor context_lens, int Hq, int max_context, float scale, Tensor prefix_table, Tensor prefix_len, "
         "int nchunk, Tensor? order=None) -> Tensor");
@@ -1264,6 +1286,8 @@ TORCH_LIBRARY_IMPL(docqa, CUDA, m) {
   m.impl("knn", &knn);
   m.impl("pool_l2", &pool_l2);
   m.impl("ivfpq_search", &ivfpq_search);
+  m.impl("ivfpq_search_pt", &ivfpq_search_pt);
+  m.impl("refine_flat", &refine_flat);
   m.impl("pq_encode", &pq_encode);
   m.impl("gemm", &gemm);
   m.impl("flash_prefill_paged", &flash_prefill_paged);

@@ -73,11 +73,7 @@ int docqa_paged_decode_cascade_persist(const void* q, int q_stride, void* k_cach
                                        const int* bins, int cap, float* ws_acc, float* ws_ml, hipStream_t s);
 int docqa_group_persist_bins(int cap, int Hkv);
 int docqa_set_decode_trace(long long* buf);
-int docqa_paged_decode_group_deep(const void* q, int q_stride, void* k_cache, void* v_cache, const int* block_tables,
-                                  int maxb, const int* context_lens, void* out, int out_stride, int B, int Hq, int Hkv,
-                                  int BS, float scale, const int* items, const int* merges, const int* bins,
-                                  int nbins, float* ws_acc, float* ws_ml, int* tick, int variant, hipStream_t s);
-int docqa_group_deep_shape(int variant, int Hkv, int cus, int* items_per_bin);
+int docqa_set_group_wave(int on);   // -1: query only; returns the previous setting
 int docqa_paged_decode_cascade_rope(void* qkv, int q_stride, const int* positions,
                                     const float* cos_sin, const int* slot_mapping, void* k_cache,
                                     void* v_cache, const int* block_tables, int maxb,
@@ -160,6 +156,15 @@ int docqa_ivfpq_search(const float* xq, const float* centroids, const float* pq,
                        const uint8_t* codes, const int64_t* ids, const int64_t* list_off,
                        const int64_t* probes, int nq, int nprobe, int d, int M, int k,
                        float* ws_d, int* ws_i, float* out_d, int64_t* out_i, hipStream_t s);
+// precomputed-table scan: norms [N] = ||c_list + r^||^2; lut_ws >= nq*M*256 halves, base_ws >=
+// nq*nprobe floats, ws_d / ws_i >= nq*ceil(nprobe/pc)*kpad (kpad = k rounded up to 8/16/32/64)
+int docqa_ivfpq_search_pt(const float* xq, const float* centroids, const float* pq, const uint8_t* codes,
+                          const float* norms, const int64_t* ids, const int64_t* list_off, const int64_t* probes,
+                          int nq, int nprobe, int d, int M, int k, int pc, void* lut_ws, float* base_ws,
+                          float* ws_d, int* ws_i, float* out_d, int64_t* out_i, hipStream_t s);
+// exact re-rank of <= 64 candidate ids per query against stored vectors (fp32 or bf16 rows)
+int docqa_refine_flat(const void* xb, int xb_bf16, int64_t ntotal, const float* xq, const int64_t* cand, int nq,
+                      int kc, int d, int k, int ip, float* out_d, int64_t* out_i, hipStream_t s);
 int docqa_pq_encode(const float* x, const float* centroids, const int64_t* assign, const float* pq,
                     int n, int d, int M, uint8_t* codes, hipStream_t s);
 

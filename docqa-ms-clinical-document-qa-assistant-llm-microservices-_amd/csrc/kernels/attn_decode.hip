@@ -989,6 +989,124 @@ constexpr int kGroupMaxPos = 64;     // block positions beyond the cascade prefi
 // pointer per workgroup when off.
 __device__ long long* g_group_trace = nullptr;
 
+// Epilogue of one grouped-decode work item (paged_decode_group_kernel, paged_decode_group_wave_
+// kernel): lane holds O^T[dim 16 dt + 4 lg + r][column hl], dt = 2 wave + dd, with the
+// column's running (m, l).  SPLIT items with a partial slot store it (write-through when the
+// launch merges by ticket, the last arriver then merging the group); otherwise the column's
+// row is normalised -- folding the cascade-prefix partials when a prefix kernel ran -- and
+// stored as bf16.
+template <bool SPLIT>
+__device__ __forceinline__ void group_item_finish(float m, float l, const f32x4 (&acc)[2], int part, int crow, int cL,
+                                                  int hl, int lg, int wave, int tid, const int* __restrict__ gp,
+                                                  const int* __restrict__ merges, int* __restrict__ tick,
+                                                  float* __restrict__ ws_acc, float* __restrict__ ws_ml,
+                                                  const CascadeIn& ci, const int* __restrict__ context_lens, int B,
+                                                  int Hkv, uint16_t* __restrict__ out, int out_stride, int kvh,
+                                                  int P) {
+  constexpr int G = 4, D = 128;
+  if constexpr (SPLIT) {
+    if (part >= 0) {   // one partial of a split group: (m, l) + un-normalised O^T
+      const size_t cidx = ((size_t)part * Hkv + kvh) * 16 + hl;
+      if (crow >= 0) {
+        if (tick) {    // merged inside this launch: write-through (sc1) for the last arriver
+#pragma unroll
+          for (int dd = 0; dd < 2; ++dd) store4_coh(ws_acc + cidx * D + 16 * (2 * wave + dd) + 4 * lg, acc[dd]);
+          if (wave == 0 && lg == 0) store2_coh(ws_ml + cidx * 2, m, l);
+        } else {
+#pragma unroll
+          for (int dd = 0; dd < 2; ++dd)
+            *reinterpret_cast<f32x4*>(ws_acc + cidx * D + 16 * (2 * wave + dd) + 4 * lg) = acc[dd];
+          if (wave == 0 && lg == 0) *reinterpret_cast<float2*>(ws_ml + cidx * 2) = make_float2(m, l);
+        }
+      }
+      if (tick) {
+        // last-arriver merge (no group_split_merge launch): the item drawing the group's
+        // last ticket folds its partials and the cascade-prefix chunks, and re-arms it
+        __shared__ int s_last;
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        const int mi = gp[7];
+        if (tid == 0) {
+          int* t = tick + (size_t)mi * Hkv + kvh;
+          const int old = __hip_atomic_fetch_add(t, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          s_last = old == merges[8 * mi + 5] - 1;
+          if (s_last) __hip_atomic_store(t, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        __syncthreads();
+        if (s_last) group_merge_body<true>(merges + 8 * mi, ws_acc, ws_ml, context_lens, B, Hkv, out, out_stride, ci,
+                                           kvh, tid);
+      }
+      return;
+    }
+  }
+  if (crow < 0) return;
+  const int h = kvh * G + (hl & 3);
+  uint16_t* op = out + (size_t)crow * out_stride + (size_t)h * D;
+  if (cL <= P) {                                 // a padded decode slot: defined zeros
+#pragma unroll
+    for (int dd = 0; dd < 2; ++dd) *reinterpret_cast<uint2*>(op + 16 * (2 * wave + dd) + 4 * lg) = make_uint2(0, 0);
+    return;
+  }
+  float den = l;
+  float o[2][4];
+#pragma unroll
+  for (int dd = 0; dd < 2; ++dd)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) o[dd][r] = acc[dd][r];
+  const int np = ci.plen ? cascade_parts(P, ci.nchunk) : 0;
+  if (np > 0) {   // cascade: fold in the shared-prefix chunk partials of this column's row
+    const size_t Hq = (size_t)Hkv * G;
+    float pm[kCascadeMaxChunks], pl[kCascadeMaxChunks];
+#pragma unroll
+    for (int c = 0; c < kCascadeMaxChunks; ++c) {
+      const size_t r = ((size_t)min(c, np - 1) * B + crow) * Hq + h;
+      const float2 mlv = *reinterpret_cast<const float2*>(ci.ml + r * 2);
+      pm[c] = c < np ? mlv.x : -FLT_MAX;
+      pl[c] = mlv.y;
+    }
+    float M2 = m;
+#pragma unroll
+    for (int c = 0; c < kCascadeMaxChunks; ++c) M2 = fmaxf(M2, pm[c]);
+    const float f0 = m == -FLT_MAX ? 0.f : exp2f(m - M2);
+    den = l * f0;
+#pragma unroll
+    for (int dd = 0; dd < 2; ++dd)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) o[dd][r] *= f0;
+    for (int c0 = 0; c0 < np; c0 += 4) {
+      f32x4 pa[4][2];
+#pragma unroll
+      for (int cc = 0; cc < 4; ++cc) {
+        const size_t r = ((size_t)min(c0 + cc, np - 1) * B + crow) * Hq + h;
+#pragma unroll
+        for (int dd = 0; dd < 2; ++dd)
+          pa[cc][dd] = *reinterpret_cast<const f32x4*>(ci.acc + r * D + 16 * (2 * wave + dd) + 4 * lg);
+      }
+#pragma unroll
+      for (int cc = 0; cc < 4; ++cc) {
+        float pmc = -FLT_MAX, plc = 0.f;
+#pragma unroll
+        for (int c = 0; c < kCascadeMaxChunks; ++c)
+          if (c == c0 + cc) { pmc = pm[c]; plc = pl[c]; }
+        const float f = pmc == -FLT_MAX ? 0.f : exp2f(pmc - M2);
+        den += f * plc;
+#pragma unroll
+        for (int dd = 0; dd < 2; ++dd)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) o[dd][r] += f * pa[cc][dd][r];
+      }
+    }
+  }
+  const float inv = den > 0.f ? 1.f / den : 0.f;
+#pragma unroll
+  for (int dd = 0; dd < 2; ++dd) {
+    uint2 v;
+    v.x = pack2(o[dd][0] * inv, o[dd][1] * inv);
+    v.y = pack2(o[dd][2] * inv, o[dd][3] * inv);
+    *reinterpret_cast<uint2*>(op + 16 * (2 * wave + dd) + 4 * lg) = v;
+  }
+}
+
 // SPLIT: `groups` is a work-item list [cap, 8] = (4 row ids, first block position, end
 // block position, partial slot or -1, 0): a long group's block positions are split over
 // several items (workgroups), each writing an un-normalised partial (m, l, O) for its 16
@@ -1243,110 +1361,237 @@ __global__ __launch_bounds__(256) void paged_decode_group_kernel(
   wait_vmcnt<0>();                               // drain the clamped tail DMAs
   if (trace && tid == 0) tr3 = wall_clock64();
 
-  // ---- epilogue: lane holds O^T[dim 16 dt + 4 lg + r][column hl], dt = 2 wave + dd
-  if constexpr (SPLIT) {
-    if (part >= 0) {   // one partial of a split group: (m, l) + un-normalised O^T
-      const size_t cidx = ((size_t)part * Hkv + kvh) * 16 + hl;
-      if (crow >= 0) {
-        if (tick) {    // merged inside this launch: write-through (sc1) for the last arriver
-#pragma unroll
-          for (int dd = 0; dd < 2; ++dd) store4_coh(ws_acc + cidx * D + 16 * (2 * wave + dd) + 4 * lg, acc[dd]);
-          if (wave == 0 && lg == 0) store2_coh(ws_ml + cidx * 2, m, l);
-        } else {
-#pragma unroll
-          for (int dd = 0; dd < 2; ++dd)
-            *reinterpret_cast<f32x4*>(ws_acc + cidx * D + 16 * (2 * wave + dd) + 4 * lg) = acc[dd];
-          if (wave == 0 && lg == 0) *reinterpret_cast<float2*>(ws_ml + cidx * 2) = make_float2(m, l);
-        }
-      }
-      if (tick) {
-        // last-arriver merge (no group_split_merge launch): the item drawing the group's
-        // last ticket folds its partials and the cascade-prefix chunks, and re-arms it
-        __shared__ int s_last;
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __syncthreads();
-        const int mi = gp[7];
-        if (tid == 0) {
-          int* t = tick + (size_t)mi * Hkv + kvh;
-          const int old = __hip_atomic_fetch_add(t, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          s_last = old == merges[8 * mi + 5] - 1;
-          if (s_last) __hip_atomic_store(t, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
-        __syncthreads();
-        if (s_last) group_merge_body<true>(merges + 8 * mi, ws_acc, ws_ml, context_lens, B, Hkv, out, out_stride, ci,
-                                           kvh, tid);
-      }
-      trace_out();
-      return;
-    }
-  }
   trace_out();
-  if (crow < 0) return;
-  const int h = kvh * G + (hl & 3);
-  uint16_t* op = out + (size_t)crow * out_stride + (size_t)h * D;
-  if (cL <= P) {                                 // a padded decode slot: defined zeros
+  group_item_finish<SPLIT>(m, l, acc, part, crow, cL, hl, lg, wave, tid, gp, merges, tick, ws_acc, ws_ml, ci,
+                           context_lens, B, Hkv, out, out_stride, kvh, P);
+}
+
+// Wave-parallel grouped decode (split plans): the same work items as paged_decode_group_
+// kernel<NSR, SPLIT = true>, but the four waves of a workgroup stream DIFFERENT 16-token
+// quarter tiles of the item (tile j to wave j % 4), each through a private LDS ring of NSRW
+// slots fed by its own LDS-DMA and its own counted vmcnt -- no workgroup barrier per tile.
+// Why (profiles/r5_group_deep_ab.log, the per-workgroup timeline of the cooperative kernel on
+// a real batch-256 step): all four waves of the cooperative kernel compute the SAME 32-token
+// Q K^T (8 MFMAs and 8 KB of LDS reads each, 4x redundant), its online softmax, then PV for
+// their 32 dims, behind one barrier per tile -- a serial chain of ~2 us per tile per
+// workgroup that neither a deeper ring (deep variants: 7 tiles in flight, 1.0 us/tile, but
+// one workgroup per CU) nor more workgroups hides.  Here a tile costs one wave 4 Q K^T MFMAs,
+// its softmax and 8 PV MFMAs over 4 + 4 KB of LDS; the four per-wave states (m, l, O^T) are
+// combined once at the end through LDS, after which every wave owns 32 dims exactly as in
+// the cooperative kernel and the shared epilogue (group_item_finish) runs unchanged.
+// LDS: 4 waves x NSRW x 8 KB + the 8 KB tile list -> two workgroups per CU at NSRW = 2.
+template <int NSRW>
+__global__ __launch_bounds__(256) void paged_decode_group_wave_kernel(
+    const uint16_t* __restrict__ q, int q_stride, const uint16_t* __restrict__ k_cache,
+    const uint16_t* __restrict__ v_cache, const int* __restrict__ block_tables, int maxb,
+    const int* __restrict__ context_lens, int B, int Hkv, float scale,
+    uint16_t* __restrict__ out, int out_stride, const int* __restrict__ groups, CascadeIn ci,
+    float* __restrict__ ws_acc, float* __restrict__ ws_ml, const int* __restrict__ merges, int* __restrict__ tick) {
+  constexpr int G = 4, R = 4, D = 128, TQ = 16, MAXT = kGroupMaxPos * 16;
+  constexpr int TILE = TQ * D;                   // elements of one K (or V) quarter tile: 4 KB
+  constexpr int WSLOT = 2 * TILE;                // K + V of one ring slot
+  static_assert(4 * NSRW * WSLOT * 2 >= 4 * 8 * 64 * 16 + 4 * 16 * 2 * 4, "ring reused by the wave merge");
+  __shared__ __attribute__((aligned(16))) uint16_t ring[4 * NSRW * WSLOT];
+  __shared__ int2 s_tl[MAXT];                    // (block id, pos << 8 | quarter << 4 | row mask)
+  __shared__ int s_nt;
+
+  const int kvh = blockIdx.x, grp = blockIdx.y;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int hl = lane & 15, lg = lane >> 4;
+  long long* trace = g_group_trace;
+  long long tr0 = 0, tr1 = 0, tr2 = 0, tr3 = 0;
+  if (trace && tid == 0) tr0 = wall_clock64();
+  const int P = ci.plen ? *ci.plen : 0;
+  const int* gp = groups + 8 * grp;
+  int rows[R], Ls[R];
 #pragma unroll
-    for (int dd = 0; dd < 2; ++dd) *reinterpret_cast<uint2*>(op + 16 * (2 * wave + dd) + 4 * lg) = make_uint2(0, 0);
-    return;
+  for (int r = 0; r < R; ++r) {
+    const int row = gp[r];
+    rows[r] = row >= 0 && row < B ? row : -1;
+    Ls[r] = rows[r] >= 0 ? context_lens[rows[r]] : 0;
   }
-  float den = l;
-  float o[2][4];
+  if (rows[0] < 0 && rows[1] < 0 && rows[2] < 0 && rows[3] < 0) return;   // unused item
+  const int lo = gp[4], hi = min(gp[5], maxb), part = gp[6];
+
+  // ---- tile list: lane j of wave 0 owns block position max(P/64, lo) + j; a distinct block
+  // yields the quarters any of its rows reaches
+  if (wave == 0) {
+    const int pos = max(P >> 6, lo) + lane;
+    int ids[R], nq[R], mk[R];
 #pragma unroll
-  for (int dd = 0; dd < 2; ++dd)
+    for (int r = 0; r < R; ++r) ids[r] = rows[r] >= 0 && pos < hi ? block_tables[(size_t)rows[r] * maxb + pos] : -1;
+    bool alive[R];
 #pragma unroll
-    for (int r = 0; r < 4; ++r) o[dd][r] = acc[dd][r];
-  const int np = ci.plen ? cascade_parts(P, ci.nchunk) : 0;
-  if (np > 0) {   // cascade: fold in the shared-prefix chunk partials of this column's row
-    const size_t Hq = (size_t)Hkv * G;
-    float pm[kCascadeMaxChunks], pl[kCascadeMaxChunks];
-#pragma unroll
-    for (int c = 0; c < kCascadeMaxChunks; ++c) {
-      const size_t r = ((size_t)min(c, np - 1) * B + crow) * Hq + h;
-      const float2 mlv = *reinterpret_cast<const float2*>(ci.ml + r * 2);
-      pm[c] = c < np ? mlv.x : -FLT_MAX;
-      pl[c] = mlv.y;
+    for (int r = 0; r < R; ++r) {
+      alive[r] = pos < hi && 64 * pos < Ls[r];
+      ids[r] = alive[r] ? ids[r] : -1;
     }
-    float M2 = m;
+    int cnt = 0;
 #pragma unroll
-    for (int c = 0; c < kCascadeMaxChunks; ++c) M2 = fmaxf(M2, pm[c]);
-    const float f0 = m == -FLT_MAX ? 0.f : exp2f(m - M2);
-    den = l * f0;
+    for (int r = 0; r < R; ++r) {
+      bool first = alive[r];
 #pragma unroll
-    for (int dd = 0; dd < 2; ++dd)
+      for (int r2 = 0; r2 < r; ++r2) first = first && !(alive[r2] && ids[r2] == ids[r]);
+      int mask = 0, need = 0;
+      if (first) {
 #pragma unroll
-      for (int r = 0; r < 4; ++r) o[dd][r] *= f0;
-    for (int c0 = 0; c0 < np; c0 += 4) {
-      f32x4 pa[4][2];
-#pragma unroll
-      for (int cc = 0; cc < 4; ++cc) {
-        const size_t r = ((size_t)min(c0 + cc, np - 1) * B + crow) * Hq + h;
-#pragma unroll
-        for (int dd = 0; dd < 2; ++dd)
-          pa[cc][dd] = *reinterpret_cast<const f32x4*>(ci.acc + r * D + 16 * (2 * wave + dd) + 4 * lg);
+        for (int r2 = 0; r2 < R; ++r2)
+          if (alive[r2] && ids[r2] == ids[r]) {
+            mask |= 1 << r2;
+            need = max(need, min(4, (Ls[r2] - 64 * pos + TQ - 1) / TQ));
+          }
       }
+      nq[r] = need;
+      mk[r] = mask;
+      cnt += need;
+    }
+    int off = cnt;
 #pragma unroll
-      for (int cc = 0; cc < 4; ++cc) {
-        float pmc = -FLT_MAX, plc = 0.f;
+    for (int o = 1; o < 64; o <<= 1) {
+      const int v = __shfl_up(off, o, 64);
+      if (lane >= o) off += v;
+    }
+    const int total = __shfl(off, 63, 64);
+    off -= cnt;
 #pragma unroll
-        for (int c = 0; c < kCascadeMaxChunks; ++c)
-          if (c == c0 + cc) { pmc = pm[c]; plc = pl[c]; }
-        const float f = pmc == -FLT_MAX ? 0.f : exp2f(pmc - M2);
-        den += f * plc;
+    for (int r = 0; r < R; ++r)
+      for (int h = 0; h < nq[r]; ++h) s_tl[off++] = make_int2(ids[r], (pos << 8) | (h << 4) | mk[r]);
+    if (lane == 0) s_nt = total;
+  }
+  const int crow = rows[hl >> 2], cL = Ls[hl >> 2], cbit = 1 << (hl >> 2);
+  bf16x8 qf[4];
+  {
+    const uint16_t* qp = q + (size_t)max(crow, 0) * q_stride + (size_t)(kvh * G + (hl & 3)) * D + lg * 8;
 #pragma unroll
-        for (int dd = 0; dd < 2; ++dd)
-#pragma unroll
-          for (int r = 0; r < 4; ++r) o[dd][r] += f * pa[cc][dd][r];
-      }
+    for (int ks = 0; ks < 4; ++ks) {
+      const uint4 v = crow >= 0 ? *reinterpret_cast<const uint4*>(qp + ks * 32) : make_uint4(0, 0, 0, 0);
+      qf[ks] = __builtin_bit_cast(bf16x8, v);
     }
   }
-  const float inv = den > 0.f ? 1.f / den : 0.f;
+  __syncthreads();                               // tile list + Q landed (fence drains vmcnt)
+  const int nt = s_nt;
+  if (trace && tid == 0) tr1 = wall_clock64();
+
+  const float qs = scale * kLog2e;
+  const uint32_t wbase = lds_u32(ring) + (uint32_t)(wave * NSRW * WSLOT * 2);
+  const int prow = lane >> 4, pslot = lane & 15;
+  const int mine_nt = nt > wave ? (nt - wave + 3) >> 2 : 0;   // this wave's tiles: wave + 4 i
+  auto stage = [&](int i) {
+    const int2 e = s_tl[wave + 4 * i];
+    const size_t row0 = ((size_t)e.x * Hkv + kvh) * 64 + ((e.y >> 4) & 3) * TQ;
+    const uint16_t* kp = k_cache + row0 * D;
+    const uint16_t* vp = v_cache + row0 * D;
+    const uint32_t dst = wbase + (uint32_t)((i % NSRW) * WSLOT * 2);
 #pragma unroll
-  for (int dd = 0; dd < 2; ++dd) {
-    uint2 v;
-    v.x = pack2(o[dd][0] * inv, o[dd][1] * inv);
-    v.y = pack2(o[dd][2] * inv, o[dd][3] * inv);
-    *reinterpret_cast<uint2*>(op + 16 * (2 * wave + dd) + 4 * lg) = v;
+    for (int c = 0; c < 4; ++c) {                // 1 KB piece = tile rows 4c .. 4c+3
+      const int t = 4 * c + prow;
+      glds16<true>(kp + t * D + ((pslot ^ t) << 3), dst + c * 1024);
+      glds16<true>(vp + t * D + ((pslot ^ vswz(t)) << 3), dst + TILE * 2 + c * 1024);
+    }
+  };
+#pragma unroll
+  for (int i = 0; i < NSRW - 1; ++i)
+    if (i < mine_nt) stage(i);
+  float m = -FLT_MAX, l = 0.f;
+  f32x4 o8[8];
+#pragma unroll
+  for (int dt = 0; dt < 8; ++dt) o8[dt] = f32x4{0.f, 0.f, 0.f, 0.f};
+  for (int i = 0; i < mine_nt; ++i) {
+    if (i + NSRW - 1 < mine_nt) {
+      stage(i + NSRW - 1);
+      wait_vmcnt<8 * (NSRW - 1)>();              // tile i landed; the next NSRW - 1 may fly
+    } else {
+      wait_vmcnt<0>();
+    }
+    if (trace && tid == 0 && i == 0) tr2 = wall_clock64();
+    const int2 e = s_tl[wave + 4 * i];
+    const bool mine = (e.y & cbit) != 0;
+    const int base = (e.y >> 8) * 64 + ((e.y >> 4) & 3) * TQ;
+    const uint16_t* kt = ring + (wave * NSRW + i % NSRW) * WSLOT;
+    const uint16_t* vt = kt + TILE;
+    f32x4 x = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) {
+      const bf16x8 a = *reinterpret_cast<const bf16x8*>(kt + hl * D + (((4 * ks + lg) ^ hl) << 3));
+      x = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, qf[ks], x, 0, 0, 0);
+    }
+    // ---- per-column online softmax: lane = tokens 4 lg + r of column hl
+    float mx = -FLT_MAX;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int tok = base + 4 * lg + r;
+      const float v = (mine && tok < cL) ? x[r] * qs : -FLT_MAX;
+      x[r] = v;
+      mx = fmaxf(mx, v);
+    }
+    mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
+    mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+    const float m_new = fmaxf(m, mx);
+    const float alpha = m_new == -FLT_MAX ? 1.f : exp2f(m - m_new);
+    float ps = 0.f;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const float p = x[r] == -FLT_MAX ? 0.f : exp2f(x[r] - m_new);
+      x[r] = p;
+      ps += p;
+    }
+    ps += __shfl_xor(ps, 16, 64);
+    ps += __shfl_xor(ps, 32, 64);
+    l = l * alpha + ps;
+    m = m_new;
+    // ---- O^T += V^T P^T over all 128 dims (8 x 16)
+    i16x4 pb;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) pb[r] = (short)f2bf(x[r]);
+    const int row = 4 * lg + (hl >> 2), pp = hl & 3;
+#pragma unroll
+    for (int dt = 0; dt < 8; ++dt) {
+      o8[dt] *= alpha;
+      const int ch = 2 * dt + (pp >> 1);
+      const uint16_t* va = vt + row * D + ((ch ^ vswz(row)) << 3) + 4 * (pp & 1);
+      const i16x4 a = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_i16x4*)va);
+      o8[dt] = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(a, pb, o8[dt], 0, 0, 0);
+    }
   }
+  if (trace && tid == 0) tr3 = wall_clock64();
+
+  // ---- combine the four waves' states through LDS (the ring is free once every wave is
+  // done): wave w then owns dims 16 (2 w + dd) + 4 lg + r, as in the cooperative kernel
+  __syncthreads();
+  f32x4* s_o = reinterpret_cast<f32x4*>(ring);                       // [wave][dt][lane]
+  float* s_ml = reinterpret_cast<float*>(ring) + 4 * 8 * 64 * 4;     // [wave][column][2]
+#pragma unroll
+  for (int dt = 0; dt < 8; ++dt) s_o[(wave * 8 + dt) * 64 + lane] = o8[dt];
+  if (lg == 0) {
+    s_ml[(wave * 16 + hl) * 2] = m;
+    s_ml[(wave * 16 + hl) * 2 + 1] = l;
+  }
+  __syncthreads();
+  float mw[4], lw[4], M = -FLT_MAX;
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    mw[u] = s_ml[(u * 16 + hl) * 2];
+    lw[u] = s_ml[(u * 16 + hl) * 2 + 1];
+    M = fmaxf(M, mw[u]);
+  }
+  f32x4 acc[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
+  float L = 0.f;
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    const float f = mw[u] == -FLT_MAX ? 0.f : exp2f(mw[u] - M);
+    L += f * lw[u];
+#pragma unroll
+    for (int dd = 0; dd < 2; ++dd) acc[dd] += f * s_o[(u * 8 + 2 * wave + dd) * 64 + lane];
+  }
+  if (trace && tid == 0) {
+    long long* t = trace + ((size_t)blockIdx.y * gridDim.x + blockIdx.x) * 8;
+    t[0] = tr0; t[1] = tr1; t[2] = tr2; t[3] = tr3; t[4] = wall_clock64(); t[5] = nt;
+    t[6] = __builtin_amdgcn_s_getreg((31 << 11) | 4);
+    t[7] = __builtin_amdgcn_s_getreg(20 | (3 << 11)) & 15;
+  }
+  group_item_finish<true>(M, L, acc, part, crow, cL, hl, lg, wave, tid, gp, merges, tick, ws_acc, ws_ml, ci,
+                          context_lens, B, Hkv, out, out_stride, kvh, P);
 }
 
 // Combines the partials of every split group (merges [cap, 8] = (4 row ids, first slot,
@@ -1740,358 +1985,6 @@ __global__ __launch_bounds__(256) void paged_decode_group_persist_kernel(
   wait_vmcnt<0>();                               // drain the clamped tail DMAs
 }
 
-// ---------------------------------------------------------------------------------------
-// Deep-ring persistent grouped decode (plan [4, cap, 8]: items and merges exactly as the
-// inline-prefix split plan -- unsplit groups finish in their item, split groups write
-// write-through partials merged by their last item -- plus plan[2] = bins of <= NIT item
-// indices, LPT-packed by the host so every workgroup streams ~total / bins tiles).
-// Why (profiles/r5_decode_replay_trace.log, the per-workgroup timeline of the one-item-per-
-// workgroup kernel above on a real batch-256 step): every workgroup streams at the same
-// latency-bound rate (~2 us per 16 KB tile with two in flight, HBM queues full), so the
-// launch ends when its LONGEST item does -- concurrency falls from 768 to < 300 workgroups
-// over the last ~20 % of the kernel -- and each of the ~1.4 rounds of workgroups pays a
-// ~5 us tile-list prologue and a ~3 us epilogue in front of / behind its stream.  Here one
-// workgroup per CU owns a balanced bin: one prologue (every item's tile list and Q
-// fragments, into LDS), then ONE ring of NSR 16-KB tiles (NSR - 2 in flight) that runs
-// across item boundaries, unsplit items normalised and stored the moment their last tile is
-// folded, split items' partials stored write-through without waiting; the tickets of the
-// split items are drawn after the stream drains and the last arriver of a group merges it.
-// Inline prefix only (items start at block 0, the shared template blocks are L2 hits after
-// the first group), G = 4 query heads per KV head, 64-token blocks.
-template <int NSR, int NIT>
-__global__ __launch_bounds__(256) void paged_decode_group_deep_kernel(
-    const uint16_t* __restrict__ q, int q_stride, const uint16_t* __restrict__ k_cache,
-    const uint16_t* __restrict__ v_cache, const int* __restrict__ block_tables, int maxb,
-    const int* __restrict__ context_lens, int B, int Hkv, float scale, uint16_t* __restrict__ out,
-    int out_stride, const int* __restrict__ items, const int* __restrict__ merges,
-    const int* __restrict__ bins, float* __restrict__ ws_acc, float* __restrict__ ws_ml,
-    int* __restrict__ tick) {
-  constexpr int G = 4, R = 4, D = 128, TT = 32;
-  constexpr int TILE = TT * D;
-  static_assert(NIT <= 8 && NSR >= 3, "bin / ring shape");
-  __shared__ __attribute__((aligned(16))) uint16_t ring[NSR * 2 * TILE];
-  __shared__ __attribute__((aligned(16))) uint16_t s_q[NIT][16][D];   // Q^T columns of every item
-  __shared__ int2 s_tl[kBinMaxTiles];           // (block id, item << 16 | pos << 8 | half << 4 | mask)
-  __shared__ int s_it[NIT][8];                  // rows[4], lo, hi, slot, merge row
-  __shared__ int s_L[NIT][4];
-  __shared__ int s_cnt[NIT];
-  __shared__ int s_last[NIT];
-
-  const int kvh = blockIdx.x, bin = blockIdx.y;
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int hl = lane & 15, lg = lane >> 4;
-  long long* trace = g_group_trace;
-  long long tr0 = 0, tr1 = 0, tr2 = 0, tr3 = 0;
-  if (trace && tid == 0) tr0 = wall_clock64();
-
-  if (tid < NIT * 8) {                           // the bin's items -> LDS
-    const int j = tid >> 3, f = tid & 7;
-    const int it = bins[bin * 8 + j];
-    int v = it >= 0 ? items[it * 8 + f] : -1;
-    if (f < 4) {
-      v = (v >= 0 && v < B) ? v : -1;
-      s_L[j][f] = v >= 0 ? context_lens[v] : 0;
-    }
-    s_it[j][f] = it < 0 ? -1 : v;
-    if (f == 0) s_last[j] = 0;
-  }
-  __syncthreads();
-  int nit = 0;
-#pragma unroll
-  for (int j = 0; j < NIT; ++j) nit += (s_it[j][0] >= 0 || s_it[j][1] >= 0 || s_it[j][2] >= 0 || s_it[j][3] >= 0) ? 1 : 0;
-  if (nit == 0) return;                          // unused bin (uniform): the host packs bins densely
-
-  // ---- Q^T columns of every item (column c = row slot c / 4, head c % 4) -> LDS
-  for (int e = tid; e < nit * 16 * 16; e += 256) {
-    const int j = e >> 8, c = (e >> 4) & 15, k = e & 15;
-    const int row = s_it[j][c >> 2];
-    const uint4 v = row >= 0 ? *reinterpret_cast<const uint4*>(q + (size_t)row * q_stride +
-                                                                (size_t)(kvh * G + (c & 3)) * D + k * 8)
-                             : make_uint4(0, 0, 0, 0);
-    *reinterpret_cast<uint4*>(&s_q[j][c][k * 8]) = v;
-  }
-  // ---- tile lists of items wave and wave + 4: lane = one block position of the item
-  int2 ent[2][2 * R];
-  int cnt[2], off[2];
-#pragma unroll
-  for (int u = 0; u < 2; ++u) {
-    const int j = wave + 4 * u;
-    cnt[u] = 0;
-    off[u] = 0;
-    if (j < nit) {
-      const int lo = s_it[j][4], hi = min(s_it[j][5], maxb);
-      const int pos = lo + lane;
-      int ids[R];
-      bool alive[R];
-#pragma unroll
-      for (int r = 0; r < R; ++r) {
-        const int row = s_it[j][r];
-        alive[r] = row >= 0 && pos < hi && 64 * pos < s_L[j][r];
-        ids[r] = alive[r] ? block_tables[(size_t)row * maxb + pos] : -1;
-      }
-#pragma unroll
-      for (int r = 0; r < R; ++r) {
-        bool first = alive[r];
-#pragma unroll
-        for (int r2 = 0; r2 < r; ++r2) first = first && !(alive[r2] && ids[r2] == ids[r]);
-        if (first) {
-          int mask = 0, two = 0;
-#pragma unroll
-          for (int r2 = 0; r2 < R; ++r2)
-            if (alive[r2] && ids[r2] == ids[r]) { mask |= 1 << r2; two |= s_L[j][r2] > 64 * pos + 32; }
-#pragma unroll
-          for (int h = 0; h < 2; ++h)
-            if (h == 0 || two) {
-              const int y = (j << 16) | (pos << 8) | (h << 4) | mask;
-#pragma unroll
-              for (int e = 0; e < 2 * R; ++e)
-                if (e == cnt[u]) ent[u][e] = make_int2(ids[r], y);
-              cnt[u]++;
-            }
-        }
-      }
-      int o = cnt[u];                            // exclusive prefix sum over the lanes
-#pragma unroll
-      for (int d = 1; d < 64; d <<= 1) {
-        const int v = __shfl_up(o, d, 64);
-        if (lane >= d) o += v;
-      }
-      if (lane == 63) s_cnt[j] = o;
-      off[u] = o - cnt[u];
-    }
-  }
-  __syncthreads();
-  int base[NIT], NT = 0;
-#pragma unroll
-  for (int j = 0; j < NIT; ++j) {
-    base[j] = NT;
-    NT += j < nit ? s_cnt[j] : 0;
-  }
-  NT = min(NT, kBinMaxTiles);                    // the host plans <= kBinMaxTiles per bin
-#pragma unroll
-  for (int u = 0; u < 2; ++u) {
-    const int j = wave + 4 * u;
-    if (j < nit) {
-      int b0 = 0;
-#pragma unroll
-      for (int jj = 0; jj < NIT; ++jj)
-        if (jj == j) b0 = base[jj];
-#pragma unroll
-      for (int e = 0; e < 2 * R; ++e)
-        if (e < cnt[u] && b0 + off[u] + e < kBinMaxTiles) s_tl[b0 + off[u] + e] = ent[u][e];
-    }
-  }
-  __syncthreads();
-  if (trace && tid == 0) tr1 = wall_clock64();
-
-  const float qs = scale * kLog2e;
-  const uint32_t ring_base = lds_u32(ring);
-  const int prow = lane >> 4, pslot = lane & 15;  // DMA piece geometry: 4 rows x 16 slots
-  auto stage = [&](int jt) {
-    const int2 e = s_tl[min(jt, NT - 1)];
-    const int tok0 = ((e.y >> 4) & 1) * TT;
-    const size_t row0 = ((size_t)e.x * Hkv + kvh) * 64 + tok0;
-    const uint16_t* kp = k_cache + row0 * D;
-    const uint16_t* vp = v_cache + row0 * D;
-    const uint32_t dst = ring_base + (uint32_t)((jt % NSR) * 2 * TILE * 2);
-#pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      const int c = i * 4 + wave;                // 1 KB piece = tile rows 4c .. 4c+3
-      const int t = 4 * c + prow;
-      glds16<true>(kp + t * D + ((pslot ^ (t & 15)) << 3), dst + c * 1024);
-      glds16<true>(vp + t * D + ((pslot ^ vswz(t)) << 3), dst + TILE * 2 + c * 1024);
-    }
-  };
-  if (NT > 0) {
-#pragma unroll
-    for (int j = 0; j < NSR - 1; ++j) stage(j);
-  }
-  // item state: the online softmax of this lane's column over the item's tiles
-  float m = -FLT_MAX, l = 0.f;
-  f32x4 acc[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
-  // finish item j: unsplit -> normalised bf16 output of this lane's column; split -> the
-  // un-normalised partial, write-through for the group's last-arriving item
-  auto finish = [&](int j) {
-    const int crow = s_it[j][hl >> 2];
-    const int slot = s_it[j][6];
-    if (slot >= 0) {
-      const size_t cidx = ((size_t)slot * Hkv + kvh) * 16 + hl;
-      if (crow >= 0) {
-#pragma unroll
-        for (int dd = 0; dd < 2; ++dd) store4_coh(ws_acc + cidx * D + 16 * (2 * wave + dd) + 4 * lg, acc[dd]);
-        if (wave == 0 && lg == 0) store2_coh(ws_ml + cidx * 2, m, l);
-      }
-      return;
-    }
-    if (crow < 0) return;
-    uint16_t* op = out + (size_t)crow * out_stride + (size_t)(kvh * G + (hl & 3)) * D;
-    const float inv = (s_L[j][hl >> 2] > 0 && l > 0.f) ? 1.f / l : 0.f;
-#pragma unroll
-    for (int dd = 0; dd < 2; ++dd) {
-      uint2 v;
-      v.x = pack2(acc[dd][0] * inv, acc[dd][1] * inv);
-      v.y = pack2(acc[dd][2] * inv, acc[dd][3] * inv);
-      *reinterpret_cast<uint2*>(op + 16 * (2 * wave + dd) + 4 * lg) = v;
-    }
-  };
-  // items without a live tile finish with the empty state (zeros / an empty partial)
-  for (int j = 0; j < nit; ++j)
-    if (s_cnt[j] == 0) finish(j);
-
-  int cur = -1, cL = 0;
-  bf16x8 qf[4];
-  const int cbit = 1 << (hl >> 2);
-  for (int jt = 0; jt < NT; ++jt) {
-    wait_vmcnt<4 * (NSR - 2)>();                 // tile jt landed; the next NSR-2 may fly
-    ring_barrier();                              // tile jt visible; slot (jt-1) % NSR free
-    if (trace && tid == 0 && jt == 0) tr2 = wall_clock64();
-    const int2 e = s_tl[jt];
-    const int it = __builtin_amdgcn_readfirstlane((e.y >> 16) & 7);
-    if (it != cur) {                             // item boundary (uniform): finish, switch
-      if (cur >= 0) finish(cur);
-      cur = it;
-#pragma unroll
-      for (int ks = 0; ks < 4; ++ks) qf[ks] = *reinterpret_cast<const bf16x8*>(&s_q[cur][hl][(4 * ks + lg) * 8]);
-      cL = s_L[cur][hl >> 2];
-      m = -FLT_MAX;
-      l = 0.f;
-      acc[0] = f32x4{0.f, 0.f, 0.f, 0.f};
-      acc[1] = f32x4{0.f, 0.f, 0.f, 0.f};
-    }
-    stage(jt + NSR - 1);
-    const bool mine = (e.y & cbit) != 0;         // this column's row reads this block
-    const int tbase = ((e.y >> 8) & 0xff) * 64 + ((e.y >> 4) & 1) * TT;   // position of token 0
-    const uint16_t* kt = ring + (jt % NSR) * 2 * TILE;
-    const uint16_t* vt = kt + TILE;
-    f32x4 x[2];
-#pragma unroll
-    for (int c = 0; c < 2; ++c) {
-      x[c] = f32x4{0.f, 0.f, 0.f, 0.f};
-      const int t = 16 * c + hl;
-#pragma unroll
-      for (int ks = 0; ks < 4; ++ks) {
-        const bf16x8 a = *reinterpret_cast<const bf16x8*>(kt + t * D + (((4 * ks + lg) ^ (t & 15)) << 3));
-        x[c] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, qf[ks], x[c], 0, 0, 0);
-      }
-    }
-    float mx = -FLT_MAX;
-#pragma unroll
-    for (int c = 0; c < 2; ++c)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int tok = tbase + 16 * c + 4 * lg + r;
-        const float v = (mine && tok < cL) ? x[c][r] * qs : -FLT_MAX;
-        x[c][r] = v;
-        mx = fmaxf(mx, v);
-      }
-    mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
-    mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
-    const float m_new = fmaxf(m, mx);
-    const float alpha = m_new == -FLT_MAX ? 1.f : exp2f(m - m_new);
-    float ps = 0.f;
-#pragma unroll
-    for (int c = 0; c < 2; ++c)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const float p = x[c][r] == -FLT_MAX ? 0.f : exp2f(x[c][r] - m_new);
-        x[c][r] = p;
-        ps += p;
-      }
-    ps += __shfl_xor(ps, 16, 64);
-    ps += __shfl_xor(ps, 32, 64);
-    l = l * alpha + ps;
-    m = m_new;
-#pragma unroll
-    for (int dd = 0; dd < 2; ++dd) acc[dd] *= alpha;
-#pragma unroll
-    for (int c = 0; c < 2; ++c) {
-      i16x4 pb;
-#pragma unroll
-      for (int r = 0; r < 4; ++r) pb[r] = (short)f2bf(x[c][r]);
-      const int row = 16 * c + 4 * lg + (hl >> 2), pp = hl & 3;
-#pragma unroll
-      for (int dd = 0; dd < 2; ++dd) {
-        const int ch = 2 * (2 * wave + dd) + (pp >> 1);
-        const uint16_t* va = vt + row * D + ((ch ^ vswz(row)) << 3) + 4 * (pp & 1);
-        const i16x4 a = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_i16x4*)va);
-        acc[dd] = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(a, pb, acc[dd], 0, 0, 0);
-      }
-    }
-  }
-  if (cur >= 0) finish(cur);
-  wait_vmcnt<0>();                               // the clamped tail DMAs and every partial store
-  if (trace && tid == 0) tr3 = wall_clock64();
-  __syncthreads();
-  // split items: draw the group tickets now that every partial of this bin is stored; the
-  // item drawing a group's last ticket merges it (and re-arms the word for the next launch)
-  if (tid < nit) {
-    const int slot = s_it[tid][6], mi = s_it[tid][7];
-    if (slot >= 0 && mi >= 0) {
-      int* t = tick + (size_t)mi * Hkv + kvh;
-      const int old = __hip_atomic_fetch_add(t, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      const bool last = old == merges[8 * mi + 5] - 1;
-      if (last) __hip_atomic_store(t, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      s_last[tid] = last ? 1 : 0;
-    }
-  }
-  __syncthreads();
-  const CascadeIn none{nullptr, nullptr, nullptr, 1, nullptr};
-  for (int j = 0; j < nit; ++j)
-    if (s_last[j]) group_merge_body<true>(merges + 8 * s_it[j][7], ws_acc, ws_ml, context_lens, B, Hkv, out, out_stride,
-                                          none, kvh, tid);
-  if (trace && tid == 0) {
-    long long* t = trace + ((size_t)blockIdx.y * gridDim.x + blockIdx.x) * 8;
-    t[0] = tr0; t[1] = tr1; t[2] = tr2; t[3] = tr3; t[4] = wall_clock64(); t[5] = NT;
-    t[6] = __builtin_amdgcn_s_getreg((31 << 11) | 4);
-    t[7] = __builtin_amdgcn_s_getreg(20 | (3 << 11)) & 15;
-  }
-}
-
-// LDS of the deep kernel -> bins per KV head so every workgroup of the grid is resident
-template <int NSR, int NIT>
-constexpr int deep_lds_bytes() {
-  return NSR * 2 * 32 * 128 * 2 + NIT * 16 * 128 * 2 + kBinMaxTiles * 8 + NIT * (8 + 4 + 2) * 4;
-}
-
-// Deep-ring persistent grouped decode (inline prefix): plan [4, cap, 8] (items, merges,
-// bins of <= nit items, unused), `nbins` bins per KV head (docqa_group_deep_bins), tick
-// int32 [cap, Hkv] zeroed (re-armed by the kernel), ws_acc / ws_ml: split partials.
-int docqa_paged_decode_group_deep(const void* q, int q_stride, void* k_cache, void* v_cache, const int* block_tables,
-                                  int maxb, const int* context_lens, void* out, int out_stride, int B, int Hq, int Hkv,
-                                  int BS, float scale, const int* items, const int* merges, const int* bins,
-                                  int nbins, float* ws_acc, float* ws_ml, int* tick, int variant, hipStream_t s) {
-  if (B == 0) return 0;
-  if (BS != 64 || maxb > kGroupMaxPos || Hq != 4 * Hkv || nbins < 1 || !tick) return -1;
-  const dim3 grid(Hkv, nbins);
-  if (variant == 1)
-    paged_decode_group_deep_kernel<3, 4><<<grid, 256, 0, s>>>(
-        (const uint16_t*)q, q_stride, (const uint16_t*)k_cache, (const uint16_t*)v_cache, block_tables, maxb,
-        context_lens, B, Hkv, scale, (uint16_t*)out, out_stride, items, merges, bins, ws_acc, ws_ml, tick);
-  else if (variant == 2)
-    paged_decode_group_deep_kernel<5, 8><<<grid, 256, 0, s>>>(
-        (const uint16_t*)q, q_stride, (const uint16_t*)k_cache, (const uint16_t*)v_cache, block_tables, maxb,
-        context_lens, B, Hkv, scale, (uint16_t*)out, out_stride, items, merges, bins, ws_acc, ws_ml, tick);
-  else
-    paged_decode_group_deep_kernel<7, 4><<<grid, 256, 0, s>>>(
-        (const uint16_t*)q, q_stride, (const uint16_t*)k_cache, (const uint16_t*)v_cache, block_tables, maxb,
-        context_lens, B, Hkv, scale, (uint16_t*)out, out_stride, items, merges, bins, ws_acc, ws_ml, tick);
-  DOCQA_CHECK_LAUNCH();
-  return 0;
-}
-
-// (bins per KV head, items per bin) of a deep variant: every workgroup resident at once
-// (LDS-limited workgroups per CU x the CU count), so the bins never wait for a second round
-int docqa_group_deep_shape(int variant, int Hkv, int cus, int* items_per_bin) {
-  int lds, nit;
-  if (variant == 1) { lds = deep_lds_bytes<3, 4>(); nit = 4; }
-  else if (variant == 2) { lds = deep_lds_bytes<5, 8>(); nit = 8; }
-  else { lds = deep_lds_bytes<7, 4>(); nit = 4; }
-  const int per_cu = (160 * 1024) / lds;
-  if (items_per_bin) *items_per_bin = nit;
-  return (per_cu < 1 ? 1 : per_cu) * cus / (Hkv > 0 ? Hkv : 1);
-}
-
 // forward declaration (defined below with the other cascade launchers)
 int docqa_cascade_prefix(const void* qkv, int row_stride, int rows, int Hq, int Hkv, float scale,
                          const void* k_cache, const void* v_cache, const int* prefix_table,
@@ -2183,6 +2076,23 @@ static int cascade_prefix_forked(const void* q, int q_stride, int B, int Hq, int
 // Grouped cascade decode with long groups split over several workgroups: items [cap, 8]
 // (see paged_decode_group_kernel SPLIT), merges [cap, 8] (group_split_merge_kernel),
 // ws_acc [slots, Hkv, 16, 128] / ws_ml [slots, Hkv, 16, 2] fp32 partials.
+// wave-parallel split kernel (paged_decode_group_wave_kernel): DOCQA_GROUP_WAVE=1, or
+// docqa_set_group_wave (tests and probes A/B both kernels in one process)
+static int g_group_wave = -1;
+static bool group_wave_on() {
+  if (g_group_wave < 0) {
+    const char* e = getenv("DOCQA_GROUP_WAVE");
+    g_group_wave = e && atoi(e) == 1 ? 1 : 0;
+  }
+  return g_group_wave == 1;
+}
+
+int docqa_set_group_wave(int on) {
+  const int was = group_wave_on() ? 1 : 0;
+  if (on >= 0) g_group_wave = on ? 1 : 0;
+  return was;
+}
+
 int docqa_paged_decode_cascade_split(const void* q, int q_stride, void* k_cache, void* v_cache,
                                      const int* block_tables, int maxb, const int* context_lens,
                                      void* out, int out_stride, int B, int Hq, int Hkv, int BS,
@@ -2225,7 +2135,11 @@ int docqa_paged_decode_cascade_split(const void* q, int q_stride, void* k_cache,
         scale, (uint16_t*)out, out_stride, items, ci, ws_acc, ws_ml, merges, tk, fz);
     DOCQA_CHECK_LAUNCH();
     if (tk) return 0;
-  } else if (nsr == 4)
+  } else if (group_wave_on())
+    paged_decode_group_wave_kernel<2><<<dim3(Hkv, cap), 256, 0, s>>>(
+        (const uint16_t*)q, q_stride, (const uint16_t*)k_cache, (const uint16_t*)v_cache, block_tables, maxb,
+        context_lens, B, Hkv, scale, (uint16_t*)out, out_stride, items, ci, ws_acc, ws_ml, merges, tk);
+  else if (nsr == 4)
     paged_decode_group_kernel<4, true><<<dim3(Hkv, cap), 256, 0, s>>>(
         (const uint16_t*)q, q_stride, (const uint16_t*)k_cache, (const uint16_t*)v_cache, block_tables, maxb,
         context_lens, B, Hkv, scale, (uint16_t*)out, out_stride, items, ci, ws_acc, ws_ml, merges, tk);

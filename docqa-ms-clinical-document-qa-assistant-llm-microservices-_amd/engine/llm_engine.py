@@ -154,15 +154,6 @@ def _inline_prefix_on() -> bool:
     return _split_groups_on() and os.environ.get("DOCQA_GROUP_INLINE_PREFIX", "1") == "1"
 
 
-def _deep_groups_on() -> bool:
-    """Deep-ring persistent grouped decode (plan [4, cap, 8], attn_decode.hip
-    paged_decode_group_deep_kernel): one balanced bin of work items per resident workgroup,
-    one LDS ring across item boundaries -- no launch tail, one prologue per workgroup
-    (DOCQA_GROUP_DEEP=1; inline prefix only)."""
-    return (_split_groups_on() and _inline_prefix_on() and not _persist_groups_on()
-            and os.environ.get("DOCQA_GROUP_DEEP", "0") == "1" and torch.cuda.is_available())
-
-
 def _defer_groups_on() -> bool:
     """Split plan with every group merged by the merge kernel (ops.split_decode_groups
     defer=True): the cascade-prefix kernel then runs on a side stream beside the group
@@ -172,22 +163,6 @@ def _defer_groups_on() -> bool:
 
 def _identity_groups(bp: int, dev, hkv: int = 8) -> torch.Tensor:
     cap = (bp + 1) // 2
-    if _deep_groups_on() and torch.device(dev).type == "cuda":
-        # deep plan [4, bp, 8]: consecutive unsplit quads, dealt round-robin onto the bins
-        nb, nit = ops.group_deep_shape(hkv)
-        rows = max(bp, 1)
-        nb = min(nb, rows)
-        nq = (bp + 3) // 4
-        if nq <= nb * nit:
-            g = torch.full((4, rows, 8), -1, dtype=torch.int32)
-            g[:2, :, 4:] = 0
-            g[3] = 0
-            for i in range(nq):
-                q = list(range(4 * i, min(4 * i + 4, bp)))
-                g[0, i, :len(q)] = torch.tensor(q, dtype=torch.int32)
-                g[0, i, 4], g[0, i, 5], g[0, i, 6], g[0, i, 7] = 0, 1 << 20, -1, 0
-                g[2, i % nb, i // nb] = i
-            return g.to(dev)
     if _split_groups_on():
         # split plan [2, bp, 8] (persistent: [3, bp, 8]): consecutive unsplit quads until
         # set_groups runs
@@ -461,7 +436,7 @@ class LLMEngine:
             if self.group_decode and ops.grouped_decode_ok(self.kv.caches[0][0], g.block_tables, self.model.hq):
                 meta.decode_groups = g.groups
                 meta.decode_defer = g.groups.dim() == 3 and _defer_groups_on()
-                meta.decode_inline = (g.groups.dim() == 3 and g.groups.shape[0] in (2, 4) and _inline_prefix_on()
+                meta.decode_inline = (g.groups.dim() == 3 and g.groups.shape[0] == 2 and _inline_prefix_on()
                                       and not _defer_groups_on())
         return meta
 
@@ -505,14 +480,13 @@ class LLMEngine:
         if g.groups.dim() == 3:   # split plan: long groups over several workgroups
             cap = g.groups.shape[1]
             quads = ops.pack_decode_groups(tables, lens, skip, self.block_size, (g.bp + 1) // 2)
-            deep = ops.group_deep_shape(self.model.hkv) if g.groups.shape[0] == 4 else None
-            if _inline_prefix_on() and not _defer_groups_on() and g.groups.shape[0] in (2, 4):
+            if _inline_prefix_on() and not _defer_groups_on() and g.groups.shape[0] == 2:
                 skip = 0   # the kernel attends the shared prefix inside each group
             bins = ops.persist_bins(cap, self.model.hkv) if g.groups.shape[0] == 3 else 0
 
             def split(tiles):
                 return ops.split_decode_groups(quads, tables, lens, skip, self.block_size, cap, tiles,
-                                               bins=bins, defer=_defer_groups_on(), deep=deep)
+                                               bins=bins, defer=_defer_groups_on())
 
             tiles = os.environ.get("DOCQA_GROUP_TILES", "auto")
             if tiles == "auto":
@@ -526,8 +500,6 @@ class LLMEngine:
                 # with the MOST items within the target rather than the first that fits:
                 # batch 64 / 128 run best at 54 / 106 items, 12 tiles)
                 target = int(os.environ.get("DOCQA_GROUP_ITEMS", "132"))
-                if deep:   # a deep plan holds bins x items-per-bin items
-                    target = min(target, min(deep[0], cap) * deep[1])
                 plan, best = None, -1
                 for budget in (8, 12, 16, 24, 32, 40, 48, 64, 96, 128):
                     p = split(budget)

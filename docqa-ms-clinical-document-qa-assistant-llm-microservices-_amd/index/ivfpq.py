@@ -6,8 +6,13 @@ codes of all lists concatenated and sorted by list [N, M] uint8 with list offset
 [nlist + 1] int64 and stored ids [N] int64.  At 10M x 768-d with M=64 the codes take
 640 MB -- a fraction of one MI355X's 288 GB, so an 8-GPU node holds 3.5B vectors.
 
-Search = coarse flat kNN (q vs centroids, top-nprobe; MFMA kernel) + one ADC scan
-launch over (query, list) work items + one merge launch (``ivfpq.hip``).
+Search = coarse flat kNN (q vs centroids, top-nprobe; MFMA kernel) + the precomputed-table
+ADC scan (``ivfpq.hip`` ivfpq_scan_pt_kernel): ||q - c_l - r^||^2 splits into ||q||^2 -
+2<q, c_l> (one dot product per probe), ||c_l + r^||^2 (``norms``, stored per vector at add
+time) and -2 sum_m <q_m, pq[m][code_m]> (one fp16 LUT per QUERY, shared by all its probes),
+so no per-(query, list) table is rebuilt; candidates pass an LDS threshold buffer with
+radix-select compaction, then one merge launch maps positions to ids.
+``DOCQA_IVFPQ_SCAN=lut`` keeps the per-item-LUT kernel (exact fp32 ADC, no norms needed).
 Training = GPU k-means (coarse) + per-subspace k-means (PQ); encoding = one kernel.
 
 FAISS file format (``IvPQ``) read/write: header + nlist/nprobe + flat quantizer +
@@ -19,6 +24,7 @@ parity with FAISS itself is "parity unpinned" (round-trip tested only).
 from __future__ import annotations
 
 import io
+import os
 import struct
 
 import numpy as np
@@ -47,6 +53,17 @@ def pca_rotation(x: torch.Tensor, M: int) -> torch.Tensor:
     return vec[:, order].float().contiguous()
 
 
+def probes_per_workgroup(nq: int, nprobe: int) -> int:
+    """Probed lists per scan workgroup: enough workgroups to fill the chip several times
+    over (~4096: two 57 KB-LDS workgroups per CU x 256 CUs x 8 rounds) without re-loading
+    each query's 48 KB LUT for only a list or two (DOCQA_IVFPQ_PC overrides)."""
+    env = os.environ.get("DOCQA_IVFPQ_PC")
+    if env:
+        return max(1, int(env))
+    chunks = max(1, min(nprobe, -(-4096 // max(1, nq))))
+    return -(-nprobe // chunks)
+
+
 class IVFPQIndex:
     def __init__(self, d: int, nlist: int, M: int, nbits: int = 8, device="cuda", rotation: str = "none"):
         if nbits != 8:
@@ -67,6 +84,9 @@ class IVFPQIndex:
         self.codes = torch.empty(0, M, dtype=torch.uint8, device=self.device)
         self.ids = torch.empty(0, dtype=torch.long, device=self.device)
         self.list_off = torch.zeros(nlist + 1, dtype=torch.long, device=self.device)
+        # ||c_list + r^_i||^2 per stored vector (list-major like codes); rebuilt lazily after
+        # a FAISS load, which stores no such term
+        self.norms: torch.Tensor | None = torch.empty(0, dtype=torch.float32, device=self.device)
         self.ntotal = 0
 
     @property
@@ -116,12 +136,15 @@ class IVFPQIndex:
             _, a = assign(xb, self.centroids)
             new_codes.append(self.encode(xb, a))
             new_lists.append(a)
+        new_norms = [self.recon_norms(c, a) for c, a in zip(new_codes, new_lists)]
+        old_norms = [self._norms()] if self.ntotal else []
         codes = torch.cat([self._list_major_codes(), *new_codes]) if self.ntotal else torch.cat(new_codes)
         lists = torch.cat([self._row_lists(), *new_lists]) if self.ntotal else torch.cat(new_lists)
         allids = torch.cat([self.ids, ids]) if self.ntotal else ids
         order = torch.argsort(lists, stable=True)
         self.codes = codes.index_select(0, order).contiguous()
         self.ids = allids.index_select(0, order).contiguous()
+        self.norms = torch.cat([*old_norms, *new_norms]).index_select(0, order).contiguous()
         counts = torch.bincount(lists, minlength=self.nlist)
         self.list_off = torch.zeros(self.nlist + 1, dtype=torch.long, device=self.device)
         self.list_off[1:] = torch.cumsum(counts, 0)
@@ -129,6 +152,23 @@ class IVFPQIndex:
 
     def _list_major_codes(self):
         return self.codes
+
+    def recon_norms(self, codes: torch.Tensor, lists: torch.Tensor, batch: int = 1 << 18) -> torch.Tensor:
+        """||c_list + r^||^2 of encoded vectors (r^ = the PQ reconstruction of the residual):
+        the per-vector term of the precomputed-table distance."""
+        out = torch.empty(codes.shape[0], dtype=torch.float32, device=codes.device)
+        m_idx = torch.arange(self.M, device=codes.device)
+        for i in range(0, codes.shape[0], batch):
+            c = codes[i:i + batch].long()
+            r = self.pq[m_idx[None, :], c].reshape(c.shape[0], self.d)      # [n, d]
+            x = r + self.centroids.index_select(0, lists[i:i + batch])
+            out[i:i + batch] = (x * x).sum(1)
+        return out
+
+    def _norms(self) -> torch.Tensor:
+        if self.norms is None or self.norms.shape[0] != self.codes.shape[0]:
+            self.norms = self.recon_norms(self.codes, self._row_lists()).contiguous()
+        return self.norms
 
     def _row_lists(self):
         counts = self.list_off[1:] - self.list_off[:-1]
@@ -144,8 +184,12 @@ class IVFPQIndex:
         else:   # wide probes (the 10M operating points: nprobe 128..512): coarse.hip
             probes = ops.coarse_probes(xq, self.centroids, cn, nprobe)
         if self.device.type == "cuda":
-            return ops._native().ivfpq_search(xq, self.centroids, self.pq, self.codes, self.ids,
-                                              self.list_off, probes.contiguous(), k)
+            if os.environ.get("DOCQA_IVFPQ_SCAN", "pt") == "lut":
+                return ops._native().ivfpq_search(xq, self.centroids, self.pq, self.codes, self.ids,
+                                                  self.list_off, probes.contiguous(), k)
+            return ops._native().ivfpq_search_pt(xq, self.centroids, self.pq, self.codes, self._norms(),
+                                                 self.ids, self.list_off, probes.contiguous(), k,
+                                                 probes_per_workgroup(xq.shape[0], probes.shape[1]))
         return self._search_reference(xq, probes, k)
 
     def _search_reference(self, xq, probes, k):
@@ -230,7 +274,7 @@ class IVFPQIndex:
 
     def to(self, device) -> "IVFPQIndex":
         self.device = torch.device(device)
-        for name in ("rot", "centroids", "pq", "codes", "ids", "list_off"):
+        for name in ("rot", "centroids", "pq", "codes", "ids", "list_off", "norms"):
             t = getattr(self, name)
             if t is not None:
                 setattr(self, name, t.to(self.device))

@@ -5,8 +5,9 @@ whose nearest neighbours are nearly equidistant that ordering is noisy.  The ref
 asks the base index for ``k * k_factor`` candidates (the scan kernel keeps up to 32 per
 query) and re-ranks them with exact L2 / inner-product distances against the stored
 full-precision vectors -- the same vectors a FlatIndex already keeps in HBM, shared, not
-copied.  Gather + batched dot product run as device tensor ops (the candidate set is
-tiny: nq x <=32 rows); no host round trip.
+copied.  On the GPU one kernel (ivfpq.hip refine_l2_kernel: a workgroup per query, a wave
+per candidate row, rank-counting top-k of <= 64) replaces the gather + einsum + topk
+chain; the tensor-op path stays as the CPU implementation and the test oracle.
 
 Reference parity: the reference only has IndexFlatL2 (semantic-indexer/indexer.py:21-22);
 the 10M-vector IVF-PQ configuration is BASELINE.json config 2, where FAISS users pair
@@ -15,6 +16,8 @@ IVF-PQ with IndexRefineFlat for recall.
 from __future__ import annotations
 
 import torch
+
+from .. import ops
 
 
 class RefineFlat:
@@ -34,6 +37,13 @@ class RefineFlat:
         xq = torch.as_tensor(xq).to(self.xb.device, torch.float32).contiguous()
         _, cand = self.base.search(xq, kc, **base_kw)
         cand = cand.to(self.xb.device)
+        if self.xb.is_cuda and self.xb.dtype in (torch.float32, torch.bfloat16) and kc <= 64:
+            return ops._native().refine_flat(self.xb.contiguous(), xq, cand.contiguous(), k, self.metric == "ip")
+        return self.rerank(xq, cand, k)
+
+    def rerank(self, xq: torch.Tensor, cand: torch.Tensor, k: int):
+        """Tensor-op exact re-rank (CPU path / oracle of the native kernel)."""
+        kc = cand.shape[1]
         valid = cand >= 0
         rows = self.xb[cand.clamp_min(0)].float()              # [nq, kc, d]
         ip = torch.einsum("qcd,qd->qc", rows, xq)

@@ -649,7 +649,7 @@ def paged_decode_cascade_grouped(q, k_cache, v_cache, block_tables, context_lens
             return _native().paged_decode_cascade_split(q, k_cache, v_cache, block_tables, context_lens, Hq,
                                                         scale, prefix_table, prefix_len, nchunk, groups,
                                                         defer and groups.shape[0] == 2, tick,
-                                                        bool(inline_prefix) and groups.shape[0] in (2, 4))
+                                                        bool(inline_prefix) and groups.shape[0] == 2)
         return _native().paged_decode_cascade_grouped(q, k_cache, v_cache, block_tables, context_lens, Hq,
                                                       scale, prefix_table, prefix_len, nchunk, groups)
     max_context = block_tables.shape[1] * k_cache.shape[2]
@@ -793,17 +793,9 @@ def persist_bins(cap: int, Hkv: int) -> int:
 BIN_ITEMS, BIN_MAX_TILES = 8, 512    # attn_decode.hip kBinItems / kBinMaxTiles
 
 
-def group_deep_shape(Hkv: int) -> tuple[int, int]:
-    """(bins per KV head, items per bin) of the deep-ring persistent grouped decode
-    (attn_decode.hip paged_decode_group_deep_kernel, DOCQA_GROUP_DEEP_VARIANT): one bin per
-    resident workgroup, so a plan built with it never needs a second launch round."""
-    nb, nit = _native().group_deep_shape(int(Hkv))
-    return int(nb), int(nit)
-
-
 def split_decode_groups(quads: list[list[int]], tables: list[list[int]], lens: list[int], skip: int,
                         block_size: int, cap: int, tiles_per_item: int = 12, bins: int = 0,
-                        defer: bool = False, deep: tuple[int, int] | None = None) -> torch.Tensor:
+                        defer: bool = False) -> torch.Tensor:
     """Split plan for the grouped cascade decode (``paged_decode_cascade_grouped`` with a
     [2, cap, 8] int32 ``groups``): every group of :func:`pack_decode_groups` is cut at block
     positions into work items of about ``tiles_per_item`` K/V tiles (``lens``: the lengths
@@ -822,12 +814,7 @@ def split_decode_groups(quads: list[list[int]], tables: list[list[int]], lens: l
 
     ``defer``: every item writes a partial and every group has a merge row (at most ``cap``),
     as in the persistent plan, so no item reads the cascade-prefix partials and the prefix
-    kernel runs on a side stream beside the group kernel (attn_decode.hip, DOCQA_GROUP_DEFER).
-
-    ``deep`` = (bins, items per bin): the DEEP-RING plan [4, cap, 8] -- plan[0] / plan[1] as
-    the split plan (unsplit groups finish in their item, split groups are merged by their
-    last item's workgroup), plan[2] the items packed longest-first onto the least-loaded of
-    ``bins`` bins (<= items per bin, <= 512 tiles each; dense from bin 0), plan[3] unused."""
+    kernel runs on a side stream beside the group kernel (attn_decode.hip, DOCQA_GROUP_DEFER)."""
     budget = max(1, tiles_per_item)
     all_partial = bool(bins) or defer
     while True:
@@ -861,38 +848,11 @@ def split_decode_groups(quads: list[list[int]], tables: list[list[int]], lens: l
         if fits and bins:
             nb = min(bins, cap)
             fits = len(items) <= nb * BIN_ITEMS and all(t <= BIN_MAX_TILES for t, _ in items)
-        if fits and deep:
-            nb = min(deep[0], cap)
-            fits = len(items) <= nb * deep[1] and all(t <= BIN_MAX_TILES for t, _ in items)
         if fits:
             break
         if budget > 1 << 20:
             raise ValueError(f"split_decode_groups: {len(quads)} groups exceed the plan capacity {cap}")
         budget *= 2
-    if deep:
-        items.sort(key=lambda it: -it[0])
-        nb, nit = min(deep[0], cap), deep[1]
-        load, members = [0] * nb, [[] for _ in range(nb)]
-        for i, (t, _) in enumerate(items):                # longest first (sorted above)
-            best = min((b for b in range(nb) if len(members[b]) < nit and load[b] + t <= BIN_MAX_TILES),
-                       key=lambda b: (load[b], len(members[b])), default=None)
-            if best is None:
-                raise ValueError("split_decode_groups: items exceed the deep bins")
-            members[best].append(i)
-            load[best] += t
-        members.sort(key=lambda mem: -len(mem))           # dense: used bins first
-        plan = torch.full((4, cap, 8), -1, dtype=torch.int32)
-        plan[:2, :, 4:] = 0
-        plan[0, len(items):, 6] = -1
-        plan[3] = 0
-        if items:
-            plan[0, :len(items)] = torch.tensor([it[1] for it in items], dtype=torch.int32)
-        if merges:
-            plan[1, :len(merges)] = torch.tensor(merges, dtype=torch.int32)
-        for b, mem in enumerate(members):
-            for j, i in enumerate(mem):
-                plan[2, b, j] = i
-        return plan
     if not bins:
         items.sort(key=lambda it: -it[0])
         plan = torch.full((2, cap, 8), -1, dtype=torch.int32)

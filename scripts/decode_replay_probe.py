@@ -68,21 +68,6 @@ def main():
     st = st.cuda()
     sl = torch.tensor([ns * BS], dtype=torch.int32, device="cuda")
     groups = d["groups"].cuda()
-    if os.environ.get("DOCQA_REPLAY_DEEP", "0") == "1":
-        # the engine's deep-ring plan for the same batch (llm_engine.set_groups): END lengths,
-        # groups packed by shared blocks, items from block 0, the tiles budget giving the most
-        # items the bins hold
-        end = [n + d["max_new_tokens"] for n in lens]
-        quads = ops.pack_decode_groups(tables, end, d["nshared"], BS, (bp + 1) // 2)
-        deep = ops.group_deep_shape(Hkv)
-        target = min(int(os.environ.get("DOCQA_GROUP_ITEMS", "132")), min(deep[0], bp) * deep[1])
-        plan, best = None, -1
-        for budget in (8, 12, 16, 24, 32, 40, 48, 64, 96, 128):
-            p = ops.split_decode_groups(quads, tables, end, 0, BS, bp, budget, deep=deep)
-            n = int((p[0, :, :4] >= 0).any(1).sum())
-            if n <= target and n > best:
-                plan, best = p, n
-        groups = plan.cuda()
     tick = ops.decode_ticket(max(bp, 4096) * Hkv, "cuda")
     scale = 1 / math.sqrt(D)
     nchunk = d["cascade_chunks"]
@@ -96,21 +81,12 @@ def main():
     distinct = len({b for t, L in zip(tables, cl[:B].tolist()) for b in t[:(L + BS - 1) // BS]})
     kv_bytes = distinct * Hkv * BS * D * 2 * 2
     us = graph_time(run, copies)
-    if groups.dim() == 3 and groups.shape[0] == 4:
-        ref = ops.paged_decode_cascade_grouped(q, caches[0][0], caches[0][1], bt, cl, Hq, scale, st, sl, nchunk,
-                                               d["groups"].cuda(), False, tick, inline)
-        got = run(0)
-        torch.cuda.synchronize()
-        err = (got.float() - ref.float()).abs().max().item()
-        assert err < 2e-2, f"deep plan output differs from the split plan: {err}"
     out = {"B": B, "bp": bp, "t_off": t_off, "distinct_blocks": distinct, "kv_MB": round(kv_bytes / 1e6, 1),
            "us": round(us, 1), "TBps": round(kv_bytes / us / 1e6, 2), "nshared": ns, "copies": copies,
            "items": int((groups[0, :, :4] >= 0).any(1).sum()) if groups.dim() == 3 else None,
            "env": {k: v for k, v in os.environ.items() if k.startswith("DOCQA_GROUP")}}
     # timeline
     nwg = Hkv * (groups.shape[1] if groups.dim() == 3 else groups.numel() // 4)
-    if groups.dim() == 3 and groups.shape[0] == 4:
-        out["deep"] = list(ops.group_deep_shape(Hkv))
     buf = torch.zeros(nwg * 8, dtype=torch.int64, device="cuda")
     torch.ops.docqa.set_decode_trace(buf)
     run(0)

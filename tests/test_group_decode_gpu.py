@@ -284,15 +284,19 @@ def test_identity_plan_matches_per_row(native, monkeypatch, mode):
     assert (out.float() - ref.float()).abs().max().item() < 2e-2
 
 
-@pytest.mark.parametrize("B,Hkv,seed", [(37, 8, 0), (256, 8, 3), (9, 2, 5), (512, 8, 4)])
+@pytest.mark.parametrize("B,Hkv,seed,maxb", [(37, 8, 0, 12), (256, 8, 3, 12), (9, 2, 5, 12), (12, 8, 7, 64)])
 @pytest.mark.parametrize("tiles", [1, 3, 12, 1000])
-def test_deep_grouped_cascade_matches_per_row(native, B, Hkv, seed, tiles):
-    """Deep-ring persistent plan (items LPT-packed into one bin per resident workgroup, one
-    ring across item boundaries, unsplit groups finished in their item, split groups merged
-    by their last item) == per-row cascade and the fp32 reference, tickets re-armed; END-of-
-    decode planning lengths, so some items have no live keys yet."""
-    Hq, D, BS, Pb, maxb = 4 * Hkv, 128, 64, 3, 12
+@pytest.mark.parametrize("inline", [False, True])
+def test_wave_kernel_matches_cooperative(native, B, Hkv, seed, maxb, tiles, inline):
+    """attn_decode.hip paged_decode_group_wave_kernel (each wave streams its own 16-token
+    quarter tiles through a private ring; per-wave states combined once) == the cooperative
+    split kernel and the fp32 reference: cascade prefix kernel or inline prefix, ticket merges
+    re-armed, END-of-decode planning lengths, up to 64 block positions per row."""
+    Hq, D, BS, Pb = 4 * Hkv, 128, 64, 3
     tables, lens, nblk = _trie_batch(B, Pb, maxb, seed)
+    if maxb == 64:   # long rows: most of the 64 block positions live
+        rnd = random.Random(seed)
+        lens = [min(64 * maxb - 128, L + 64 * rnd.randint(20, 58)) for L in lens]
     kc = torch.randn(nblk, Hkv, BS, D, device="cuda", dtype=torch.bfloat16)
     vc = torch.randn_like(kc)
     bt = torch.tensor(tables, dtype=torch.int32, device="cuda")
@@ -305,44 +309,22 @@ def test_deep_grouped_cascade_matches_per_row(native, B, Hkv, seed, tiles):
     with native.use_reference():
         ref32 = native.paged_decode_cascade(q, kc, vc, bt, cl, Hq, maxb * BS, scale, pt, plen, 4)
     end_lens = [min(L + 128, maxb * BS) for L in lens]
-    cap = max(B, 4)
     quads = native.pack_decode_groups(tables, end_lens, Pb, BS, (B + 1) // 2)
-    deep = native.group_deep_shape(Hkv)
-    assert deep[0] >= 1 and deep[1] >= 4
-    plan = native.split_decode_groups(quads, tables, end_lens, 0, BS, cap, tiles, deep=deep)
-    assert plan.shape == (4, cap, 8)
-    used = plan[2][plan[2] >= 0]
-    nitems = int((plan[0, :, :4] >= 0).any(1).sum())
-    assert sorted(used.tolist()) == list(range(nitems))             # every item in exactly one bin
-    tick = torch.zeros(cap * Hkv, dtype=torch.int32, device="cuda")
-    for _ in range(2):
-        out = native.paged_decode_cascade_grouped(q, kc, vc, bt, cl, Hq, scale, pt, plen, 4, plan.cuda(), False,
-                                                  tick, True)
-        torch.cuda.synchronize()
-        err32 = (out.float() - ref32.float()).abs().max().item()
-        assert err32 < 3e-2, err32
-        assert int(tick.abs().sum()) == 0
-
-
-def test_deep_plan_balances_bins(native):
-    """The deep plan's bins carry about the same number of tiles (LPT onto the least-loaded
-    bin), and every bin index the kernel launches exists in the plan."""
-    Hkv, BS, Pb, maxb = 8, 64, 5, 32
-    B = 256
-    tables, lens, _ = _trie_batch(B, Pb, maxb, 11)
-    end_lens = [min(L + 128, maxb * BS) for L in lens]
-    quads = native.pack_decode_groups(tables, end_lens, Pb, BS, (B + 1) // 2)
-    deep = native.group_deep_shape(Hkv)
-    plan = native.split_decode_groups(quads, tables, end_lens, 0, BS, B, 40, deep=deep)
-    loads = []
-    items = plan[0]
-    for b in range(min(deep[0], B)):
-        mem = [int(i) for i in plan[2, b] if i >= 0]
-        t = 0
-        for i in mem:
-            rows = [int(r) for r in items[i, :4] if r >= 0]
-            lo, hi = int(items[i, 4]), int(items[i, 5])
-            t += sum(tt for pos, tt in native.group_tiles_by_position(tables, end_lens, rows, 0, BS) if lo <= pos < hi)
-        loads.append(t)
-    busy = [x for x in loads if x > 0]
-    assert busy and max(busy) <= 1.6 * (sum(busy) / len(busy)) + 40, loads
+    plan = native.split_decode_groups(quads, tables, end_lens, 0 if inline else Pb, BS, max(B, 4), tiles).cuda()
+    tick = torch.zeros(plan.shape[1] * Hkv, dtype=torch.int32, device="cuda")
+    was = torch.ops.docqa.set_group_wave(0)
+    try:
+        coop = native.paged_decode_cascade_grouped(q, kc, vc, bt, cl, Hq, scale, pt, plen, 4, plan, False, tick,
+                                                   inline)
+        torch.ops.docqa.set_group_wave(1)
+        for _ in range(2):
+            wave = native.paged_decode_cascade_grouped(q, kc, vc, bt, cl, Hq, scale, pt, plen, 4, plan, False,
+                                                       tick, inline)
+            torch.cuda.synchronize()
+            assert int(tick.abs().sum()) == 0
+            err32 = (wave.float() - ref32.float()).abs().max().item()
+            assert err32 < 3e-2, err32
+            d = (wave.float() - coop.float()).abs().max().item()
+            assert d < 2e-2, d
+    finally:
+        torch.ops.docqa.set_group_wave(was)

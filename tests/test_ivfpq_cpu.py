@@ -138,3 +138,38 @@ def test_pca_rotated_ivfpq_recall_and_faiss_roundtrip(tmp_path):
     st2 = IVFPQRefineIndex.load(sp, device="cpu")
     assert st2.ivf.rotation == "pca"
     assert torch.equal(st2.search(q, 10)[1], st.search(q, 10)[1])
+
+
+def test_precomputed_table_decomposition_cpu():
+    """The precomputed-table scan's terms (ivfpq.hip ivfpq_scan_pt_kernel): ||q||^2 -
+    2<q, c_l> + ||c_l + r^_i||^2 - 2 sum_m <q_m, pq[m][code_m]> == the per-item-LUT ADC
+    distance ||q - c_l - r^_i||^2, with the stored norms kept in list order through
+    incremental adds."""
+    x = _data(3000, 64, 3)
+    idx = IVFPQIndex(64, 16, 16, device="cpu")
+    idx.train(x, niter=4)
+    idx.add(x[:1700])
+    idx.add(x[1700:])
+    lists = idx._row_lists()
+    assert idx.norms.shape == (3000,)
+    torch.testing.assert_close(idx.norms, idx.recon_norms(idx.codes, lists))
+    q = x[:3] + 0.1
+    m = torch.arange(idx.M)
+    recon = idx.pq[m[None], idx.codes.long()].reshape(-1, 64)          # r^ per stored vector
+    cent = idx.centroids[lists]
+    adc = ((q[:, None] - cent[None] - recon[None]) ** 2).sum(-1)        # [3, N]
+    lut = -2 * torch.einsum("qmd,mkd->qmk", q.view(3, idx.M, -1), idx.pq)   # [3, M, 256]
+    cross = lut[:, m[None], idx.codes.long()].sum(-1)                  # [3, N]
+    pt = (q * q).sum(1, keepdim=True) - 2 * q @ cent.t() + idx.norms[None] + cross
+    torch.testing.assert_close(pt, adc, rtol=1e-4, atol=1e-2)
+
+
+def test_probes_per_workgroup_fills_chip(monkeypatch):
+    from docqa_amd.index.ivfpq import probes_per_workgroup
+
+    monkeypatch.delenv("DOCQA_IVFPQ_PC", raising=False)
+    assert probes_per_workgroup(256, 256) == 16          # 16 chunks x 256 queries = 4096 WGs
+    assert probes_per_workgroup(1, 64) == 1              # one query: a workgroup per probe
+    assert probes_per_workgroup(4096, 128) == 128        # a big batch fills the chip alone
+    monkeypatch.setenv("DOCQA_IVFPQ_PC", "3")
+    assert probes_per_workgroup(256, 256) == 3

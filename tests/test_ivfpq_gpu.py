@@ -32,9 +32,22 @@ def test_ivfpq_gpu_matches_reference(d, M, k):
     cn = (idx.centroids ** 2).sum(1)
     _, probes = ops.knn(idx.centroids, cn, q, 8, False, 0)
     D2, I2 = _ref(idx, q, probes, k)
-    torch.testing.assert_close(D.cpu(), D2, rtol=1e-3, atol=1e-3)
-    assert (I.cpu() == I2).float().mean() > 0.97
+    _close_pt(D.cpu(), D2, q.cpu())
+    same = sum(len(set(a) & set(b)) for a, b in zip(I.cpu().tolist(), I2.tolist()))
+    assert same / I.numel() > 0.95
     assert (I[:, 0].cpu() == torch.arange(40)).float().mean() > 0.9
+
+
+def _close_pt(D, Dref, q):
+    """The precomputed-table scan sums fp16 LUT terms -2 <q_m, pq[m][k]> that scale with
+    ||q||, not with the (much smaller) residual distance: its error bound is a fraction of
+    ||q||^2 + D (FAISS's fp16 GPU tables have the same trade-off; exact re-rank follows)."""
+    qn = (q.double() ** 2).sum(1, keepdim=True)
+    tol = 1e-3 * (qn + Dref.double().abs()) + 1e-3
+    fin = torch.isfinite(Dref)
+    assert torch.equal(fin, torch.isfinite(D))
+    err = (D.double() - Dref.double()).abs()
+    assert bool((err[fin] <= tol.expand_as(err)[fin]).all()), float((err - tol).max())
 
 
 def _ref(idx, q, probes, k):
@@ -62,7 +75,7 @@ def test_ivfpq_wide_probe_matches_knn_probe_order():
     cn = (idx.centroids ** 2).sum(1)
     probes = torch.topk(cn[None] - 2 * q @ idx.centroids.t(), 128, dim=1, largest=False).indices
     D2, I2 = _ref(idx, q, probes, 10)
-    torch.testing.assert_close(D.cpu(), D2, rtol=1e-3, atol=1e-3)
+    _close_pt(D.cpu(), D2, q.cpu())
 
 
 @pytest.mark.parametrize("nlist,d,nq,nprobe", [(8192, 768, 64, 128), (8192, 768, 300, 512), (1000, 96, 33, 257),
@@ -160,3 +173,160 @@ def test_fp32_gemm_nt_matches_fp32(nq, d, n):
     ref = (x.double() @ w.double().t()).float()
     assert got.shape == ref.shape
     assert (got - ref).abs().max().item() <= 1e-4 * ref.abs().max().item()
+
+
+def _built(d, M, nlist=64, n=20000, seed=0):
+    from docqa_amd.index.ivfpq import IVFPQIndex
+
+    g = torch.Generator().manual_seed(seed)
+    c = torch.randn(nlist, d, generator=g) * 2
+    x = c[torch.randint(0, nlist, (n,), generator=g)] + torch.randn(n, d, generator=g)
+    idx = IVFPQIndex(d, nlist, M, device="cuda")
+    idx.train(x, niter=5)
+    idx.add(x)
+    return idx, x, g
+
+
+@pytest.mark.parametrize("d,M,k,nprobe,pc", [(768, 96, 10, 8, None), (768, 96, 64, 16, 1), (96, 12, 40, 8, 3),
+                                             (64, 16, 8, 64, 1000), (768, 64, 33, 5, 2)])
+def test_precomputed_table_scan_matches_lut_scan(monkeypatch, d, M, k, nprobe, pc):
+    """the precomputed-table scan (per-query fp16 LUT, stored
+    ||c + r^||^2, LDS threshold buffer + radix select) returns the per-item-LUT kernel's
+    neighbours and distances (fp16 LUT terms: ~1e-4 relative), for chunkings from one probe
+    per workgroup to all of them and both code-row load widths (M % 16 != 0 at M = 12)."""
+    from docqa_amd import ops
+
+    assert ops.load_native()
+    idx, x, g = _built(d, M)
+    q = (x[:96] + 0.1 * torch.randn(96, d, generator=g)).cuda()
+    if pc is not None:
+        monkeypatch.setenv("DOCQA_IVFPQ_PC", str(pc))
+    monkeypatch.setenv("DOCQA_IVFPQ_SCAN", "pt")
+    D, I = idx.search(q, k, nprobe=nprobe)
+    monkeypatch.setenv("DOCQA_IVFPQ_SCAN", "lut")
+    D2, I2 = idx.search(q, k, nprobe=nprobe)
+    assert D.shape == (96, k) and I.shape == (96, k)
+    _close_pt(D.cpu(), D2.cpu(), q.cpu())
+    assert bool((D[:, 1:] >= D[:, :-1]).all())                     # merged lists come back sorted
+    same = sum(len(set(a) & set(b)) for a, b in zip(I.cpu().tolist(), I2.cpu().tolist()))
+    assert same / I.numel() > 0.97                                 # fp16 near-ties only
+    assert (I[:, 0].cpu() == torch.arange(96)).float().mean() > 0.9
+
+
+def test_precomputed_table_scan_exact_ties():
+    """3000 copies of one vector: every candidate ties at the K-th distance -- the radix
+    select keeps exactly K distinct positions per workgroup (no buffer overflow), the merge
+    returns k distinct ids."""
+    from docqa_amd import ops
+    from docqa_amd.index.ivfpq import IVFPQIndex
+
+    assert ops.load_native()
+    g = torch.Generator().manual_seed(5)
+    base = torch.randn(4000, 64, generator=g)
+    idx = IVFPQIndex(64, 16, 16, device="cuda")
+    idx.train(base, niter=4)
+    dup = base[:1].repeat(3000, 1)
+    idx.add(torch.cat([dup, base[1:]]))
+    D, I = idx.search(base[:1].cuda(), 64, nprobe=16)
+    ids = I[0].cpu().tolist()
+    assert len(set(ids)) == 64 and all(0 <= i < 3000 for i in ids)
+    assert float(D[0].max() - D[0].min()) < 1e-2
+
+
+def test_precomputed_table_norms_survive_faiss_round_trip(tmp_path):
+    """A FAISS file holds no ||c + r^||^2 term: a loaded index rebuilds it from its codes and
+    searches exactly like the index that wrote it."""
+    from docqa_amd import ops
+    from docqa_amd.index.ivfpq import IVFPQIndex
+
+    assert ops.load_native()
+    idx, x, g = _built(96, 12, nlist=32, n=6000, seed=2)
+    q = x[:20].cuda()
+    D, I = idx.search(q, 10, nprobe=8)
+    p = tmp_path / "ivfpq.faiss"
+    idx.save(p)
+    back = IVFPQIndex.load(p, device="cuda")
+    D2, I2 = back.search(q, 10, nprobe=8)
+    assert torch.equal(I.cpu(), I2.cpu())
+    torch.testing.assert_close(D, D2, rtol=1e-5, atol=1e-4)
+    torch.testing.assert_close(back.norms, idx.norms, rtol=1e-5, atol=1e-3)
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("metric", ["l2", "ip"])
+@pytest.mark.parametrize("k,kc", [(10, 30), (10, 64), (20, 8), (1, 1)])
+def test_native_refine_matches_tensor_rerank(dtype, metric, k, kc):
+    """ivfpq.hip refine_l2_kernel == RefineFlat.rerank (the tensor-op oracle): exact
+    distances of the candidates, best k, missing candidates (-1) and k > kc padded."""
+    from docqa_amd import ops
+    from docqa_amd.index.refine import RefineFlat
+
+    assert ops.load_native()
+    g = torch.Generator().manual_seed(kc + k)
+    xb = torch.randn(5000, 768, generator=g).to(dtype).cuda()
+    xq = torch.randn(33, 768, generator=g).cuda()
+    cand = torch.randint(0, 5000, (33, kc), generator=g)
+    cand[::4, -1] = -1
+    cand = cand.cuda()
+    rf = RefineFlat(None, xb, metric=metric)
+    D, I = ops._native().refine_flat(xb, xq, cand, k, metric == "ip")
+    D2, I2 = rf.rerank(xq, cand, k)
+    assert D.shape == (33, k) and I.shape == (33, k)
+    fin = torch.isfinite(D2)
+    assert torch.equal(fin, torch.isfinite(D))
+    torch.testing.assert_close(D[fin], D2[fin], rtol=1e-4, atol=1e-2)
+    assert (I == I2).float().mean() > 0.99                         # fp-order near-ties only
+    assert bool((I[~fin] == -1).all())
+
+
+def _ref_pt(idx, q, probes, k):
+    """CPU model of the precomputed-table scan with the kernel's own fp16 table values:
+    ||q||^2 - 2<q, c_l> + ||c_l + r^||^2 + sum_m fp16(-2 <q_m, pq[m][code_m]>), exact top-k."""
+    q, probes = q.cpu().double(), probes.cpu()
+    cent, pq = idx.centroids.cpu().double(), idx.pq.cpu().double()
+    codes, ids, off = idx.codes.cpu().long(), idx.ids.cpu(), idx.list_off.cpu().tolist()
+    norms = idx.norms.cpu().double()
+    M = idx.M
+    nq = q.shape[0]
+    D = torch.full((nq, k), float("inf"), dtype=torch.float64)
+    I = torch.full((nq, k), -1, dtype=torch.long)
+    m_idx = torch.arange(M)
+    for i in range(nq):
+        lut = (-2 * torch.einsum("md,mkd->mk", q[i].view(M, -1), pq)).float().half().double()
+        dd, ii = [], []
+        for l in probes[i].tolist():
+            if l < 0 or off[l] == off[l + 1]:
+                continue
+            c = codes[off[l]:off[l + 1]]
+            base = (q[i] ** 2).sum() - 2 * q[i] @ cent[l]
+            dd.append(base + norms[off[l]:off[l + 1]] + lut[m_idx[None], c].sum(1))
+            ii.append(ids[off[l]:off[l + 1]])
+        if dd:
+            d, x = torch.cat(dd), torch.cat(ii)
+            v, p = torch.topk(d, min(k, d.numel()), largest=False)
+            D[i, :v.numel()], I[i, :v.numel()] = v, x[p]
+    return D, I
+
+
+@pytest.mark.parametrize("d,M,k,nprobe,pc", [(96, 12, 40, 8, 3), (768, 96, 64, 16, 1), (64, 16, 10, 64, 1000)])
+def test_precomputed_table_scan_exact_selection(monkeypatch, d, M, k, nprobe, pc):
+    """Selection exactness of the threshold buffer + radix select: against a CPU model that
+    uses the same fp16 table values the k-th order statistics agree to fp32 summation
+    error (order statistics move by at most the largest per-element error, so a dropped or
+    duplicated candidate would show), and the id sets agree up to exact-distance ties."""
+    from docqa_amd import ops
+
+    assert ops.load_native()
+    idx, x, g = _built(d, M, n=12000)
+    q = (x[:24] + 0.1 * torch.randn(24, d, generator=g)).cuda()
+    monkeypatch.setenv("DOCQA_IVFPQ_PC", str(pc))
+    monkeypatch.setenv("DOCQA_IVFPQ_SCAN", "pt")
+    D, I = idx.search(q, k, nprobe=nprobe)
+    cn = (idx.centroids ** 2).sum(1)
+    _, probes = ops.knn(idx.centroids, cn, q, nprobe, False, 0) if nprobe <= 64 else (None, None)
+    Dm, Im = _ref_pt(idx, q, probes, k)
+    qn = (q.cpu().double() ** 2).sum(1, keepdim=True)
+    err = (D.cpu().double() - Dm).abs()
+    assert bool((err <= 1e-4 * (qn + Dm.abs()) + 1e-4).all()), float(err.max())   # + a rare fp16 rounding flip
+    same = sum(len(set(a) & set(b)) for a, b in zip(I.cpu().tolist(), Im.tolist()))
+    assert same / I.numel() > 0.99
