@@ -489,6 +489,7 @@ at::Tensor paged_decode_cascade_split(const at::Tensor& q, at::Tensor k_cache, a
   const int Hkv = k_cache.size(1), BS = k_cache.size(2), D = k_cache.size(3);
   TORCH_CHECK(D == 128 && BS == 64 && Hq == 4 * Hkv, "split decode: head_dim 128, 64-token blocks, GQA 4");
   TORCH_CHECK(block_tables.size(1) <= 64, "split decode: <= 64 blocks per sequence");
+  TORCH_CHECK(k_cache.size(0) < (1 << 20), "split decode: < 2^20 KV blocks (packed tile lists)");
   TORCH_CHECK(context_lens.numel() == B && block_tables.size(0) >= B, "split decode: B rows");
   TORCH_CHECK(plan.dim() == 3 && plan.size(0) >= 2 && plan.size(0) <= 3 && plan.size(2) == 8 && plan.size(1) >= 1,
               "plan: [2, cap, 8] (split) or [3, cap, 8] (persistent bins)");

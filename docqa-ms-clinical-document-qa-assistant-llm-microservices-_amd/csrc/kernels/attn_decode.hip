@@ -995,8 +995,8 @@ __device__ long long* g_group_trace = nullptr;
 // launch merges by ticket, the last arriver then merging the group); otherwise the column's
 // row is normalised -- folding the cascade-prefix partials when a prefix kernel ran -- and
 // stored as bf16.
-template <bool SPLIT>
-__device__ __forceinline__ void group_item_finish(float m, float l, const f32x4 (&acc)[2], int part, int crow, int cL,
+template <bool SPLIT, int NDT = 2>
+__device__ __forceinline__ void group_item_finish(float m, float l, const f32x4 (&acc)[NDT], int part, int crow, int cL,
                                                   int hl, int lg, int wave, int tid, const int* __restrict__ gp,
                                                   const int* __restrict__ merges, int* __restrict__ tick,
                                                   float* __restrict__ ws_acc, float* __restrict__ ws_ml,
@@ -1010,12 +1010,12 @@ __device__ __forceinline__ void group_item_finish(float m, float l, const f32x4 
       if (crow >= 0) {
         if (tick) {    // merged inside this launch: write-through (sc1) for the last arriver
 #pragma unroll
-          for (int dd = 0; dd < 2; ++dd) store4_coh(ws_acc + cidx * D + 16 * (2 * wave + dd) + 4 * lg, acc[dd]);
+          for (int dd = 0; dd < NDT; ++dd) store4_coh(ws_acc + cidx * D + 16 * (NDT * wave + dd) + 4 * lg, acc[dd]);
           if (wave == 0 && lg == 0) store2_coh(ws_ml + cidx * 2, m, l);
         } else {
 #pragma unroll
-          for (int dd = 0; dd < 2; ++dd)
-            *reinterpret_cast<f32x4*>(ws_acc + cidx * D + 16 * (2 * wave + dd) + 4 * lg) = acc[dd];
+          for (int dd = 0; dd < NDT; ++dd)
+            *reinterpret_cast<f32x4*>(ws_acc + cidx * D + 16 * (NDT * wave + dd) + 4 * lg) = acc[dd];
           if (wave == 0 && lg == 0) *reinterpret_cast<float2*>(ws_ml + cidx * 2) = make_float2(m, l);
         }
       }
@@ -1033,8 +1033,9 @@ __device__ __forceinline__ void group_item_finish(float m, float l, const f32x4 
           if (s_last) __hip_atomic_store(t, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
         __syncthreads();
-        if (s_last) group_merge_body<true>(merges + 8 * mi, ws_acc, ws_ml, context_lens, B, Hkv, out, out_stride, ci,
-                                           kvh, tid);
+        if (s_last)   // thread = (column, 8 dims): 256 of them over the workgroup's 512 / NDT threads
+          for (int t = tid; t < 256; t += 512 / NDT)
+            group_merge_body<true>(merges + 8 * mi, ws_acc, ws_ml, context_lens, B, Hkv, out, out_stride, ci, kvh, t);
       }
       return;
     }
@@ -1044,13 +1045,13 @@ __device__ __forceinline__ void group_item_finish(float m, float l, const f32x4 
   uint16_t* op = out + (size_t)crow * out_stride + (size_t)h * D;
   if (cL <= P) {                                 // a padded decode slot: defined zeros
 #pragma unroll
-    for (int dd = 0; dd < 2; ++dd) *reinterpret_cast<uint2*>(op + 16 * (2 * wave + dd) + 4 * lg) = make_uint2(0, 0);
+    for (int dd = 0; dd < NDT; ++dd) *reinterpret_cast<uint2*>(op + 16 * (NDT * wave + dd) + 4 * lg) = make_uint2(0, 0);
     return;
   }
   float den = l;
-  float o[2][4];
+  float o[NDT][4];
 #pragma unroll
-  for (int dd = 0; dd < 2; ++dd)
+  for (int dd = 0; dd < NDT; ++dd)
 #pragma unroll
     for (int r = 0; r < 4; ++r) o[dd][r] = acc[dd][r];
   const int np = ci.plen ? cascade_parts(P, ci.nchunk) : 0;
@@ -1070,17 +1071,17 @@ __device__ __forceinline__ void group_item_finish(float m, float l, const f32x4 
     const float f0 = m == -FLT_MAX ? 0.f : exp2f(m - M2);
     den = l * f0;
 #pragma unroll
-    for (int dd = 0; dd < 2; ++dd)
+    for (int dd = 0; dd < NDT; ++dd)
 #pragma unroll
       for (int r = 0; r < 4; ++r) o[dd][r] *= f0;
     for (int c0 = 0; c0 < np; c0 += 4) {
-      f32x4 pa[4][2];
+      f32x4 pa[4][NDT];
 #pragma unroll
       for (int cc = 0; cc < 4; ++cc) {
         const size_t r = ((size_t)min(c0 + cc, np - 1) * B + crow) * Hq + h;
 #pragma unroll
-        for (int dd = 0; dd < 2; ++dd)
-          pa[cc][dd] = *reinterpret_cast<const f32x4*>(ci.acc + r * D + 16 * (2 * wave + dd) + 4 * lg);
+        for (int dd = 0; dd < NDT; ++dd)
+          pa[cc][dd] = *reinterpret_cast<const f32x4*>(ci.acc + r * D + 16 * (NDT * wave + dd) + 4 * lg);
       }
 #pragma unroll
       for (int cc = 0; cc < 4; ++cc) {
@@ -1091,7 +1092,7 @@ __device__ __forceinline__ void group_item_finish(float m, float l, const f32x4 
         const float f = pmc == -FLT_MAX ? 0.f : exp2f(pmc - M2);
         den += f * plc;
 #pragma unroll
-        for (int dd = 0; dd < 2; ++dd)
+        for (int dd = 0; dd < NDT; ++dd)
 #pragma unroll
           for (int r = 0; r < 4; ++r) o[dd][r] += f * pa[cc][dd][r];
       }
@@ -1099,11 +1100,11 @@ __device__ __forceinline__ void group_item_finish(float m, float l, const f32x4 
   }
   const float inv = den > 0.f ? 1.f / den : 0.f;
 #pragma unroll
-  for (int dd = 0; dd < 2; ++dd) {
+  for (int dd = 0; dd < NDT; ++dd) {
     uint2 v;
     v.x = pack2(o[dd][0] * inv, o[dd][1] * inv);
     v.y = pack2(o[dd][2] * inv, o[dd][3] * inv);
-    *reinterpret_cast<uint2*>(op + 16 * (2 * wave + dd) + 4 * lg) = v;
+    *reinterpret_cast<uint2*>(op + 16 * (NDT * wave + dd) + 4 * lg) = v;
   }
 }
 
@@ -1366,6 +1367,25 @@ __global__ __launch_bounds__(256) void paged_decode_group_kernel(
                            context_lens, B, Hkv, out, out_stride, kvh, P);
 }
 
+// Reductions over the four 16-lane rows of a wave (lanes l, l ^ 16, l ^ 32, l ^ 48: the
+// 4 lane groups of one MFMA output column) with the gfx950 row-swap permutes -- VALU ops,
+// no ds_bpermute round trip through the LDS unit in the softmax's dependent chain.
+typedef unsigned int u32x2_t __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ float rows4_max(float x) {
+  const u32x2_t a = __builtin_amdgcn_permlane16_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+  const float h0 = __uint_as_float(a.x), h1 = __uint_as_float(a.y);
+  const float y = h0 > h1 ? h0 : h1;
+  const u32x2_t b = __builtin_amdgcn_permlane32_swap(__float_as_uint(y), __float_as_uint(y), false, false);
+  const float g0 = __uint_as_float(b.x), g1 = __uint_as_float(b.y);
+  return g0 > g1 ? g0 : g1;
+}
+__device__ __forceinline__ float rows4_sum(float x) {
+  const u32x2_t a = __builtin_amdgcn_permlane16_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+  const float y = __uint_as_float(a.x) + __uint_as_float(a.y);
+  const u32x2_t b = __builtin_amdgcn_permlane32_swap(__float_as_uint(y), __float_as_uint(y), false, false);
+  return __uint_as_float(b.x) + __uint_as_float(b.y);
+}
+
 // Wave-parallel grouped decode (split plans): the same work items as paged_decode_group_
 // kernel<NSR, SPLIT = true>, but the four waves of a workgroup stream DIFFERENT 16-token
 // quarter tiles of the item (tile j to wave j % 4), each through a private LDS ring of NSRW
@@ -1380,8 +1400,8 @@ __global__ __launch_bounds__(256) void paged_decode_group_kernel(
 // combined once at the end through LDS, after which every wave owns 32 dims exactly as in
 // the cooperative kernel and the shared epilogue (group_item_finish) runs unchanged.
 // LDS: 4 waves x NSRW x 8 KB + the 8 KB tile list -> two workgroups per CU at NSRW = 2.
-template <int NSRW>
-__global__ __launch_bounds__(256) void paged_decode_group_wave_kernel(
+template <int WAVES, int NSRW>
+__global__ __launch_bounds__(64 * WAVES) void paged_decode_group_wave_kernel(
     const uint16_t* __restrict__ q, int q_stride, const uint16_t* __restrict__ k_cache,
     const uint16_t* __restrict__ v_cache, const int* __restrict__ block_tables, int maxb,
     const int* __restrict__ context_lens, int B, int Hkv, float scale,
@@ -1390,9 +1410,10 @@ __global__ __launch_bounds__(256) void paged_decode_group_wave_kernel(
   constexpr int G = 4, R = 4, D = 128, TQ = 16, MAXT = kGroupMaxPos * 16;
   constexpr int TILE = TQ * D;                   // elements of one K (or V) quarter tile: 4 KB
   constexpr int WSLOT = 2 * TILE;                // K + V of one ring slot
-  static_assert(4 * NSRW * WSLOT * 2 >= 4 * 8 * 64 * 16 + 4 * 16 * 2 * 4, "ring reused by the wave merge");
-  __shared__ __attribute__((aligned(16))) uint16_t ring[4 * NSRW * WSLOT];
-  __shared__ int2 s_tl[MAXT];                    // (block id, pos << 8 | quarter << 4 | row mask)
+  constexpr int NDT = 8 / WAVES;                 // 16-dim output blocks per wave after the merge
+  static_assert(WAVES * NSRW * WSLOT * 2 >= WAVES * 8 * 64 * 16 + WAVES * 16 * 2 * 4, "ring reused by the merge");
+  __shared__ __attribute__((aligned(16))) uint16_t ring[WAVES * NSRW * WSLOT];
+  __shared__ unsigned s_tl[MAXT];                // block id << 12 | pos << 6 | quarter << 4 | row mask
   __shared__ int s_nt;
 
   const int kvh = blockIdx.x, grp = blockIdx.y;
@@ -1456,7 +1477,7 @@ __global__ __launch_bounds__(256) void paged_decode_group_wave_kernel(
     off -= cnt;
 #pragma unroll
     for (int r = 0; r < R; ++r)
-      for (int h = 0; h < nq[r]; ++h) s_tl[off++] = make_int2(ids[r], (pos << 8) | (h << 4) | mk[r]);
+      for (int h = 0; h < nq[r]; ++h) s_tl[off++] = ((unsigned)ids[r] << 12) | (pos << 6) | (h << 4) | mk[r];
     if (lane == 0) s_nt = total;
   }
   const int crow = rows[hl >> 2], cL = Ls[hl >> 2], cbit = 1 << (hl >> 2);
@@ -1476,10 +1497,10 @@ __global__ __launch_bounds__(256) void paged_decode_group_wave_kernel(
   const float qs = scale * kLog2e;
   const uint32_t wbase = lds_u32(ring) + (uint32_t)(wave * NSRW * WSLOT * 2);
   const int prow = lane >> 4, pslot = lane & 15;
-  const int mine_nt = nt > wave ? (nt - wave + 3) >> 2 : 0;   // this wave's tiles: wave + 4 i
+  const int mine_nt = nt > wave ? (nt - wave + WAVES - 1) / WAVES : 0;   // this wave's tiles: wave + WAVES i
   auto stage = [&](int i) {
-    const int2 e = s_tl[wave + 4 * i];
-    const size_t row0 = ((size_t)e.x * Hkv + kvh) * 64 + ((e.y >> 4) & 3) * TQ;
+    const unsigned e = s_tl[wave + WAVES * i];
+    const size_t row0 = ((size_t)(e >> 12) * Hkv + kvh) * 64 + ((e >> 4) & 3) * TQ;
     const uint16_t* kp = k_cache + row0 * D;
     const uint16_t* vp = v_cache + row0 * D;
     const uint32_t dst = wbase + (uint32_t)((i % NSRW) * WSLOT * 2);
@@ -1505,9 +1526,9 @@ __global__ __launch_bounds__(256) void paged_decode_group_wave_kernel(
       wait_vmcnt<0>();
     }
     if (trace && tid == 0 && i == 0) tr2 = wall_clock64();
-    const int2 e = s_tl[wave + 4 * i];
-    const bool mine = (e.y & cbit) != 0;
-    const int base = (e.y >> 8) * 64 + ((e.y >> 4) & 3) * TQ;
+    const unsigned e = s_tl[wave + WAVES * i];
+    const bool mine = (e & cbit) != 0;
+    const int base = ((e >> 6) & 63) * 64 + ((e >> 4) & 3) * TQ;
     const uint16_t* kt = ring + (wave * NSRW + i % NSRW) * WSLOT;
     const uint16_t* vt = kt + TILE;
     f32x4 x = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -1525,19 +1546,17 @@ __global__ __launch_bounds__(256) void paged_decode_group_wave_kernel(
       x[r] = v;
       mx = fmaxf(mx, v);
     }
-    mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
-    mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+    mx = rows4_max(mx);
     const float m_new = fmaxf(m, mx);
-    const float alpha = m_new == -FLT_MAX ? 1.f : exp2f(m - m_new);
+    const float alpha = m_new == -FLT_MAX ? 1.f : __builtin_amdgcn_exp2f(m - m_new);
     float ps = 0.f;
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
-      const float p = x[r] == -FLT_MAX ? 0.f : exp2f(x[r] - m_new);
+      const float p = x[r] == -FLT_MAX ? 0.f : __builtin_amdgcn_exp2f(x[r] - m_new);
       x[r] = p;
       ps += p;
     }
-    ps += __shfl_xor(ps, 16, 64);
-    ps += __shfl_xor(ps, 32, 64);
+    ps = rows4_sum(ps);
     l = l * alpha + ps;
     m = m_new;
     // ---- O^T += V^T P^T over all 128 dims (8 x 16)
@@ -1556,11 +1575,12 @@ __global__ __launch_bounds__(256) void paged_decode_group_wave_kernel(
   }
   if (trace && tid == 0) tr3 = wall_clock64();
 
-  // ---- combine the four waves' states through LDS (the ring is free once every wave is
-  // done): wave w then owns dims 16 (2 w + dd) + 4 lg + r, as in the cooperative kernel
+  // ---- combine the waves' states through LDS (the ring is free once every wave is done):
+  // wave w then owns dims 16 (NDT w + dd) + 4 lg + r (NDT = 2 at four waves: as in the
+  // cooperative kernel)
   __syncthreads();
   f32x4* s_o = reinterpret_cast<f32x4*>(ring);                       // [wave][dt][lane]
-  float* s_ml = reinterpret_cast<float*>(ring) + 4 * 8 * 64 * 4;     // [wave][column][2]
+  float* s_ml = reinterpret_cast<float*>(ring) + WAVES * 8 * 64 * 4; // [wave][column][2]
 #pragma unroll
   for (int dt = 0; dt < 8; ++dt) s_o[(wave * 8 + dt) * 64 + lane] = o8[dt];
   if (lg == 0) {
@@ -1568,21 +1588,23 @@ __global__ __launch_bounds__(256) void paged_decode_group_wave_kernel(
     s_ml[(wave * 16 + hl) * 2 + 1] = l;
   }
   __syncthreads();
-  float mw[4], lw[4], M = -FLT_MAX;
+  float mw[WAVES], lw[WAVES], M = -FLT_MAX;
 #pragma unroll
-  for (int u = 0; u < 4; ++u) {
+  for (int u = 0; u < WAVES; ++u) {
     mw[u] = s_ml[(u * 16 + hl) * 2];
     lw[u] = s_ml[(u * 16 + hl) * 2 + 1];
     M = fmaxf(M, mw[u]);
   }
-  f32x4 acc[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
+  f32x4 acc[NDT];
+#pragma unroll
+  for (int dd = 0; dd < NDT; ++dd) acc[dd] = f32x4{0.f, 0.f, 0.f, 0.f};
   float L = 0.f;
 #pragma unroll
-  for (int u = 0; u < 4; ++u) {
+  for (int u = 0; u < WAVES; ++u) {
     const float f = mw[u] == -FLT_MAX ? 0.f : exp2f(mw[u] - M);
     L += f * lw[u];
 #pragma unroll
-    for (int dd = 0; dd < 2; ++dd) acc[dd] += f * s_o[(u * 8 + 2 * wave + dd) * 64 + lane];
+    for (int dd = 0; dd < NDT; ++dd) acc[dd] += f * s_o[(u * 8 + NDT * wave + dd) * 64 + lane];
   }
   if (trace && tid == 0) {
     long long* t = trace + ((size_t)blockIdx.y * gridDim.x + blockIdx.x) * 8;
@@ -1590,7 +1612,7 @@ __global__ __launch_bounds__(256) void paged_decode_group_wave_kernel(
     t[6] = __builtin_amdgcn_s_getreg((31 << 11) | 4);
     t[7] = __builtin_amdgcn_s_getreg(20 | (3 << 11)) & 15;
   }
-  group_item_finish<true>(M, L, acc, part, crow, cL, hl, lg, wave, tid, gp, merges, tick, ws_acc, ws_ml, ci,
+  group_item_finish<true, NDT>(M, L, acc, part, crow, cL, hl, lg, wave, tid, gp, merges, tick, ws_acc, ws_ml, ci,
                           context_lens, B, Hkv, out, out_stride, kvh, P);
 }
 
@@ -2078,18 +2100,24 @@ static int cascade_prefix_forked(const void* q, int q_stride, int B, int Hq, int
 // ws_acc [slots, Hkv, 16, 128] / ws_ml [slots, Hkv, 16, 2] fp32 partials.
 // wave-parallel split kernel (paged_decode_group_wave_kernel): DOCQA_GROUP_WAVE=1, or
 // docqa_set_group_wave (tests and probes A/B both kernels in one process)
+// variants (waves per workgroup x ring slots per wave): 1 = 4 x 2 (the default), 2 = 2 x 3,
+// 3 = 2 x 4, 4 = 1 x 4; 0 = the cooperative kernel.  Replayed on a real batch-256 step:
+// 69.6 / 81.2-83.7 / 81.4 / 103.7-110.5 us against the cooperative kernel's 98.4 (132
+// items) - 111.8 us (profiles/r5_group_wave_variants.log)
 static int g_group_wave = -1;
 static bool group_wave_on() {
   if (g_group_wave < 0) {
     const char* e = getenv("DOCQA_GROUP_WAVE");
-    g_group_wave = e && atoi(e) == 1 ? 1 : 0;
+    const int v = e ? atoi(e) : 1;   // default: 4 waves x 2 slots (profiles/r5_group_wave_variants.log)
+    g_group_wave = v >= 0 && v <= 4 ? v : 0;
   }
-  return g_group_wave == 1;
+  return g_group_wave > 0;
 }
 
-int docqa_set_group_wave(int on) {
-  const int was = group_wave_on() ? 1 : 0;
-  if (on >= 0) g_group_wave = on ? 1 : 0;
+int docqa_set_group_wave(int v) {
+  group_wave_on();
+  const int was = g_group_wave;
+  if (v >= 0) g_group_wave = v <= 4 ? v : 0;
   return was;
 }
 
@@ -2135,11 +2163,19 @@ int docqa_paged_decode_cascade_split(const void* q, int q_stride, void* k_cache,
         scale, (uint16_t*)out, out_stride, items, ci, ws_acc, ws_ml, merges, tk, fz);
     DOCQA_CHECK_LAUNCH();
     if (tk) return 0;
-  } else if (group_wave_on())
-    paged_decode_group_wave_kernel<2><<<dim3(Hkv, cap), 256, 0, s>>>(
-        (const uint16_t*)q, q_stride, (const uint16_t*)k_cache, (const uint16_t*)v_cache, block_tables, maxb,
-        context_lens, B, Hkv, scale, (uint16_t*)out, out_stride, items, ci, ws_acc, ws_ml, merges, tk);
-  else if (nsr == 4)
+  } else if (group_wave_on()) {
+#define DOCQA_WAVE_LAUNCH(W_, N_)                                                                                 \
+  paged_decode_group_wave_kernel<W_, N_><<<dim3(Hkv, cap), 64 * W_, 0, s>>>(                                     \
+      (const uint16_t*)q, q_stride, (const uint16_t*)k_cache, (const uint16_t*)v_cache, block_tables, maxb,       \
+      context_lens, B, Hkv, scale, (uint16_t*)out, out_stride, items, ci, ws_acc, ws_ml, merges, tk)
+    switch (g_group_wave) {
+      case 2: DOCQA_WAVE_LAUNCH(2, 3); break;
+      case 3: DOCQA_WAVE_LAUNCH(2, 4); break;
+      case 4: DOCQA_WAVE_LAUNCH(1, 4); break;
+      default: DOCQA_WAVE_LAUNCH(4, 2); break;
+    }
+#undef DOCQA_WAVE_LAUNCH
+  } else if (nsr == 4)
     paged_decode_group_kernel<4, true><<<dim3(Hkv, cap), 256, 0, s>>>(
         (const uint16_t*)q, q_stride, (const uint16_t*)k_cache, (const uint16_t*)v_cache, block_tables, maxb,
         context_lens, B, Hkv, scale, (uint16_t*)out, out_stride, items, ci, ws_acc, ws_ml, merges, tk);

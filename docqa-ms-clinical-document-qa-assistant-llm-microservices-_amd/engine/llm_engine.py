@@ -154,6 +154,15 @@ def _inline_prefix_on() -> bool:
     return _split_groups_on() and os.environ.get("DOCQA_GROUP_INLINE_PREFIX", "1") == "1"
 
 
+def _group_wave_on() -> bool:
+    """Split plans run on the wave-parallel grouped decode kernel (attn_decode.hip
+    paged_decode_group_wave_kernel, DOCQA_GROUP_WAVE=1..4, default 1; 0 = the cooperative
+    kernel).  Its best plan has fewer, longer items: 66-82 items per KV head at batch 256
+    run 69.6-69.8 us against 73.3 us at the cooperative kernel's 132
+    (profiles/r5_group_wave_variants.log)."""
+    return os.environ.get("DOCQA_GROUP_WAVE", "1") != "0"
+
+
 def _defer_groups_on() -> bool:
     """Split plan with every group merged by the merge kernel (ops.split_decode_groups
     defer=True): the cascade-prefix kernel then runs on a side stream beside the group
@@ -499,7 +508,7 @@ class LLMEngine:
                 # (a budget whose plan overflows the rows comes back doubled, so take the plan
                 # with the MOST items within the target rather than the first that fits:
                 # batch 64 / 128 run best at 54 / 106 items, 12 tiles)
-                target = int(os.environ.get("DOCQA_GROUP_ITEMS", "132"))
+                target = int(os.environ.get("DOCQA_GROUP_ITEMS", "82" if _group_wave_on() else "132"))
                 plan, best = None, -1
                 for budget in (8, 12, 16, 24, 32, 40, 48, 64, 96, 128):
                     p = split(budget)

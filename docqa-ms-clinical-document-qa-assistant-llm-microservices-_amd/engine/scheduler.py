@@ -21,15 +21,19 @@ requests join and leave between steps:
   * lagged readback: step t's tokens are copied to pinned host memory and read while
     step t+1 already runs, so the GPU never idles on the host's bookkeeping (a finished
     request rides one extra step inside its reserved blocks and that token is dropped);
-  * stall-free admission (mixed steps, DOCQA_MIXED_PREFILL=1, the default): while
+  * stall-free admission (mixed steps, DOCQA_MIXED_PREFILL=1; off by default): while
     requests decode, new prompts are prefilled in token-budgeted chunks
     (DOCQA_CHUNK_TOKENS) that ride INSIDE the decode step's forward
     (LlamaModel.forward_mixed): every projection makes one weight pass over the decode
     rows and the chunk's tokens together, only attention is split by row kind.  A
     running request never waits for a separate prefill pass and arrivals are admitted the
     step they come (no hold to batch prefills); a prompt longer than the budget is spread
-    over several steps, its first token sampled when its last chunk has run;
-  * admission batching (mixed steps off): under load, requests are admitted in groups
+    over several steps, its first token sampled when its last chunk has run.  Measured
+    SLOWER than admission batching on the GPU (profiles/r5_serving_mixed_ab.log: offered
+    60 q/s p50 2.39 s vs 1.45 s; offered 100 78 vs 91 q/s): a mixed step is an eager,
+    host-synchronised forward, so its ~20 ms of launch work does not overlap the GPU the
+    way graph-replayed decode steps and a few large admission prefills do;
+  * admission batching (mixed steps off, the default): under load, requests are admitted in groups
     (>= ``admit_min`` that can join -- waiting AND free slots -- or ``admit_wait_s``
     after the first could), so one prefill pass over the weights serves several new
     requests instead of stalling every decode step.
@@ -145,7 +149,7 @@ class ContinuousEngine:
         self.completed = 0        # requests finished
         self.completed_short = 0  # ... of them before max_new_tokens (EOS)
         # stall-free admission: prompt chunks ride in the decode step (module docstring)
-        self.mixed = os.environ.get("DOCQA_MIXED_PREFILL", "1") == "1"
+        self.mixed = os.environ.get("DOCQA_MIXED_PREFILL", "0") == "1"
         self.chunk_tokens = max(engine.block_size, int(os.environ.get("DOCQA_CHUNK_TOKENS", "2048")))
         self.prefilling: list[Request] = []   # admitted, prompt partly in the KV cache
         self.mixed_steps = 0

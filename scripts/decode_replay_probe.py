@@ -78,6 +78,34 @@ def main():
         return ops.paged_decode_cascade_grouped(q, kc, vc, bt, cl, Hq, scale, st, sl, nchunk, groups, False,
                                                 tick, inline)
 
+    sweep = os.environ.get("DOCQA_REPLAY_ITEMS", "")
+    if sweep and groups.dim() == 3 and groups.shape[0] == 2:
+        # re-plan the same batch for other item-count targets (llm_engine.set_groups' rule:
+        # END lengths, the tiles budget giving the most items within the target)
+        end = [n + d.get("max_new_tokens", 128) for n in lens]
+        skip = 0 if inline else d["nshared"]
+        quads = ops.pack_decode_groups(tables, end, d["nshared"], BS, (bp + 1) // 2)
+        for target in [int(x) for x in sweep.split(",")]:
+            plan, best = None, -1
+            for budget in (4, 6, 8, 12, 16, 24, 32, 40, 48, 64, 80, 96, 128, 160, 192, 256, 384, 512):
+                p = ops.split_decode_groups(quads, tables, end, skip, BS, bp, budget)
+                n_it = int((p[0, :, :4] >= 0).any(1).sum())
+                if n_it <= target and n_it > best:
+                    plan, best = p, n_it
+            if plan is None:
+                continue
+            gp = plan.cuda()
+
+            def run_p(i, gp=gp):
+                kc, vc = caches[i % copies]
+                return ops.paged_decode_cascade_grouped(q, kc, vc, bt, cl, Hq, scale, st, sl, nchunk, gp, False,
+                                                        tick, inline)
+
+            for v in [int(x) for x in os.environ.get("DOCQA_REPLAY_WAVES", "-1").split(",")]:
+                was = torch.ops.docqa.set_group_wave(v)
+                print(json.dumps({"sweep_target": target, "items": best, "us": round(graph_time(run_p, copies), 1),
+                                  "wave": int(torch.ops.docqa.set_group_wave(-1))}), flush=True)
+                torch.ops.docqa.set_group_wave(was)
     distinct = len({b for t, L in zip(tables, cl[:B].tolist()) for b in t[:(L + BS - 1) // BS]})
     kv_bytes = distinct * Hkv * BS * D * 2 * 2
     us = graph_time(run, copies)

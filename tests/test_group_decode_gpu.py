@@ -287,9 +287,11 @@ def test_identity_plan_matches_per_row(native, monkeypatch, mode):
 @pytest.mark.parametrize("B,Hkv,seed,maxb", [(37, 8, 0, 12), (256, 8, 3, 12), (9, 2, 5, 12), (12, 8, 7, 64)])
 @pytest.mark.parametrize("tiles", [1, 3, 12, 1000])
 @pytest.mark.parametrize("inline", [False, True])
-def test_wave_kernel_matches_cooperative(native, B, Hkv, seed, maxb, tiles, inline):
-    """attn_decode.hip paged_decode_group_wave_kernel (each wave streams its own 16-token
-    quarter tiles through a private ring; per-wave states combined once) == the cooperative
+@pytest.mark.parametrize("variant", [1, 2, 3, 4])
+def test_wave_kernel_matches_cooperative(native, B, Hkv, seed, maxb, tiles, inline, variant):
+    """attn_decode.hip paged_decode_group_wave_kernel in each shape (waves x ring slots: 4 x 2,
+    2 x 3, 2 x 4, 1 x 4; each wave streams its own 16-token quarter tiles through a private
+    ring; per-wave states combined once) == the cooperative
     split kernel and the fp32 reference: cascade prefix kernel or inline prefix, ticket merges
     re-armed, END-of-decode planning lengths, up to 64 block positions per row."""
     Hq, D, BS, Pb = 4 * Hkv, 128, 64, 3
@@ -316,7 +318,7 @@ def test_wave_kernel_matches_cooperative(native, B, Hkv, seed, maxb, tiles, inli
     try:
         coop = native.paged_decode_cascade_grouped(q, kc, vc, bt, cl, Hq, scale, pt, plen, 4, plan, False, tick,
                                                    inline)
-        torch.ops.docqa.set_group_wave(1)
+        torch.ops.docqa.set_group_wave(variant)
         for _ in range(2):
             wave = native.paged_decode_cascade_grouped(q, kc, vc, bt, cl, Hq, scale, pt, plen, 4, plan, False,
                                                        tick, inline)

@@ -219,7 +219,7 @@ def test_mixed_steps_with_shared_prefix_cascade_exact():
     eng = LLMEngine(m, max_batch=4, max_context=512, block_size=16, use_graphs=False)
     eng.cascade_min_batch = 2
     ce = ContinuousEngine(eng)
-    ce.chunk_tokens = 16
+    ce.mixed, ce.chunk_tokens = True, 16
     futs = [ce.submit(prompts[0], SamplingParams(max_new_tokens=12, stop_on_eos=False))]
     ce.step()
     ce.step()
@@ -240,6 +240,7 @@ def test_sampled_request_takes_the_plain_admission():
     m = _model(seed=9)
     eng = LLMEngine(m, max_batch=4, max_context=512, block_size=16, use_graphs=False)
     ce = ContinuousEngine(eng)
+    ce.mixed = True
     g = torch.Generator().manual_seed(5)
     p1, p2 = (torch.randint(3, 4096, (30,), generator=g).tolist() for _ in range(2))
     f1 = ce.submit(p1, SamplingParams(max_new_tokens=6, stop_on_eos=False))
