@@ -207,7 +207,11 @@ def bench_bge_indexer(a):
         return float(ok.float().mean())
 
     sweep = []
-    for nprobe in sorted({max(1, a.nprobe // 4), a.nprobe // 2, a.nprobe, 2 * a.nprobe, 4 * a.nprobe}):
+    scans = os.environ.get("BENCH_IVFPQ_SCANS", "pt").split(",")   # A/B: "pt,lut"
+    for scan, nprobe in [(sc, npb) for sc in scans
+                         for npb in sorted({max(1, a.nprobe // 4), a.nprobe // 2, a.nprobe, 2 * a.nprobe,
+                                            4 * a.nprobe})]:
+        os.environ["DOCQA_IVFPQ_SCAN"] = scan
         for kf in sorted({1, a.k_factor, 2 * a.k_factor}):
             store.k_factor = kf
             _, Ia = store.search(xq, a.k, nprobe=nprobe)
@@ -219,7 +223,7 @@ def bench_bge_indexer(a):
                 store.search(xq, a.k, nprobe=nprobe)
             torch.cuda.synchronize()
             ms = (time.perf_counter() - t) / a.iters * 1e3
-            sweep.append({"nprobe": nprobe, "k_factor": kf, "recall_at_k": round(rec, 4),
+            sweep.append({"scan": scan, "nprobe": nprobe, "k_factor": kf, "recall_at_k": round(rec, 4),
                           "recall_at_k_tie_aware": round(rec_tie, 4),
                           "ms_per_batch": round(ms, 3), "qps": round(a.nq / ms * 1e3, 1)})
     store.k_factor = a.k_factor

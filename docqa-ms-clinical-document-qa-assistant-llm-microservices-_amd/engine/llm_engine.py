@@ -480,12 +480,27 @@ class LLMEngine:
         g.order_key = key
 
     def set_groups(self, g: _DecodeGraph, tables: list[list[int]], lens: list[int], skip: int,
-                   key=None) -> None:
+                   key=None, ids: list | None = None) -> None:
         """Pack the active rows of bucket ``g`` into groups of <= 4 that share prefix-cache
         blocks beyond the ``skip`` cascade-prefix blocks (ops.pack_decode_groups); padded
-        rows take no group.  Static while the batch composition is unchanged (``key``)."""
+        rows take no group.  Static while the batch composition is unchanged (``key``).
+
+        ``ids`` (a request id per row): when the rows are a subset of the rows the current
+        split plan was built for -- requests only RETIRED and the survivors were compacted
+        -- the plan's row ids are remapped instead of re-planned (a retired row's columns
+        go empty; an item whose rows all retired exits at once, and since every item of a
+        group carries the same rows, no group's merge ticket is left half-drawn).  A full
+        re-plan runs on any admission, or once a quarter of the planned rows is gone."""
         if not self.group_decode or (key is not None and g.groups_key == key):
             return
+        skip_in = skip
+        if (ids is not None and g.groups.dim() == 3 and getattr(g, "plan_ids", None) is not None
+                and g.plan_skip == skip_in and len(ids) * 4 >= len(g.plan_ids) * 3):
+            plan = ops.remap_plan_rows(g.plan_host, g.plan_ids, ids)
+            if plan is not None:
+                _upload(g.groups, plan)
+                g.groups_key = key
+                return
         if g.groups.dim() == 3:   # split plan: long groups over several workgroups
             cap = g.groups.shape[1]
             quads = ops.pack_decode_groups(tables, lens, skip, self.block_size, (g.bp + 1) // 2)
@@ -493,9 +508,13 @@ class LLMEngine:
                 skip = 0   # the kernel attends the shared prefix inside each group
             bins = ops.persist_bins(cap, self.model.hkv) if g.groups.shape[0] == 3 else 0
 
+            # the per-quad tile lists do not depend on the budget: computed once for every
+            # budget the auto search tries (38 -> ~6 ms of host planning per 256-row replan)
+            per_quad = [ops.group_tiles_by_position(tables, lens, list(qd), skip, self.block_size) for qd in quads]
+
             def split(tiles):
                 return ops.split_decode_groups(quads, tables, lens, skip, self.block_size, cap, tiles,
-                                               bins=bins, defer=_defer_groups_on())
+                                               bins=bins, defer=_defer_groups_on(), per_quad=per_quad)
 
             tiles = os.environ.get("DOCQA_GROUP_TILES", "auto")
             if tiles == "auto":
@@ -509,18 +528,23 @@ class LLMEngine:
                 # with the MOST items within the target rather than the first that fits:
                 # batch 64 / 128 run best at 54 / 106 items, 12 tiles)
                 target = int(os.environ.get("DOCQA_GROUP_ITEMS", "82" if _group_wave_on() else "132"))
-                plan, best = None, -1
+                # items fall as the budget grows: the first budget within the target gives
+                # the plan with the most items (the search stops there -- host time per
+                # replan matters when serving retires rows every few steps)
+                plan = None
                 for budget in (8, 12, 16, 24, 32, 40, 48, 64, 96, 128):
                     p = split(budget)
-                    n = int((p[0, :, :4] >= 0).any(1).sum())
-                    if n <= target and n > best:
-                        plan, best = p, n
+                    if int((p[0, :, :4] >= 0).any(1).sum()) <= target:
+                        plan = p
+                        break
                 if plan is None:
                     plan = split(128)
             else:
                 plan = split(int(tiles))
             _upload(g.groups, plan)
             g.groups_key = key
+            g.plan_ids = list(ids) if ids is not None else None
+            g.plan_host, g.plan_skip = plan, skip_in
             if os.environ.get("DOCQA_GROUP_PLAN_LOG", "0") == "1":
                 used = int((plan[0, :, :4] >= 0).any(1).sum())
                 print(f"[group plan] bp {g.bp} groups {len(quads)} items {used} cap {cap}", flush=True)

@@ -500,7 +500,7 @@ class ContinuousEngine:
             if self._nshared > 0:
                 eng.set_groups(g, [r.blocks for r in self.running],
                                [len(r.prompt) + r.params.max_new_tokens for r in self.running], self._nshared,
-                               key=(self._version, self._nshared))
+                               key=(self._version, self._nshared), ids=[r.rid for r in self.running])
             dmeta = eng._decode_meta(g)
         from ..models.llama import AttnMeta
 
@@ -705,7 +705,7 @@ class ContinuousEngine:
         if self._nshared > 0:
             eng.set_groups(g, [r.blocks for r in self.running],
                            [len(r.prompt) + r.params.max_new_tokens for r in self.running], self._nshared,
-                           key=(self._version, self._nshared))
+                           key=(self._version, self._nshared), ids=[r.rid for r in self.running])
         t0 = time.perf_counter()
         with tracing.span("sched.decode", running=n, bucket=bp, cascade=self._nshared > 0):
             if eng.use_graphs:

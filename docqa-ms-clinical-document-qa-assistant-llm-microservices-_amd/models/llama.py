@@ -344,6 +344,11 @@ class LlamaModel:
                     S, c = ops.prefill_plan(M, *L0[k].shape)
                     if S >= 2:
                         plans[k] = (S, lambda a, w, S=S, c=c: ops.mgemm_partial(a, w, S, c))
+                    elif not S:
+                        # narrow tensor-parallel shards: the 256 x 256 tiles split over K
+                        Sp = ops.prefill_split_plan(M, *L0[k].shape)
+                        if Sp:
+                            plans[k] = (Sp, lambda a, w, S=Sp: ops.pgemm_partial(a, w, S))
         if self.tp > 1 and not x.is_cuda:
             # CPU TP rehearsal: row-parallel partials as fp32 slabs, all-reduced before the one
             # bf16 rounding (comm.tp_add_rmsnorm), so TP = N tracks TP = 1's rounding

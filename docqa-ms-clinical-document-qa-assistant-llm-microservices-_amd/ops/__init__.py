@@ -293,6 +293,16 @@ def mgemm_partial(x, w, splits: int, cfg: int = 0):
     return torch.einsum("msk,nsk->smn", xs, ws).contiguous()
 
 
+def pgemm_partial(x, w, splits: int):
+    """Split-K partial slabs [S, M, N] fp32 of x @ w^T on the 256 x 256 prefill GEMM."""
+    if _gpu(x):
+        return _native().pgemm_partial(x.contiguous(), w, splits)
+    K = w.shape[1]
+    xs = x.float().reshape(-1, splits, K // splits)
+    ws = w.float().reshape(-1, splits, K // splits)
+    return torch.einsum("msk,nsk->smn", xs, ws).contiguous()
+
+
 def mgemm_glu(x, w_il, cfg: int = 0):
     """silu(x Wg^T) * (x Wu^T) for 8-interleaved gate|up weights on the mid-M decode GEMM."""
     if _gpu(x):
@@ -337,6 +347,27 @@ def prefill_plan(M: int, N: int, K: int) -> tuple[int, int]:
     if M <= 1024 and (K // 128) % 2 == 0:
         return 2, 2
     return 1, 2
+
+
+def prefill_split_plan(M: int, N: int, K: int) -> int:
+    """Split-K count for a prefill projection whose 256 x 256 tiles cannot fill the chip:
+    the narrow column-parallel shards of tensor parallelism (the 70B TP-8 QKV shard, N 1280 x
+    K 8192: 10 tiles at 512 rows, 0.41x hipBLASLt unsplit, profiles/r4_pgemm_mid_probe.log).
+    The fp32 slabs [S, M, N] go straight into the split-K consumers that run anyway (RoPE +
+    KV write, (TP all-reduce +) add + RMSNorm).  0: no split (enough tiles, or not a pgemm
+    shape).  DOCQA_PREFILL_SPLIT=0 disables."""
+    if (not _PREFILL_SPLIT or _PGEMM_OFF or N >= 4096 or M <= 0 or N % 256 or K % 256
+            or max(M, N) * K * 2 >= (1 << 32)):
+        return 0
+    tiles = ((M + 255) // 256) * (N // 256)
+    S = 1
+    while S < _PREFILL_SPLIT_MAX and tiles * S * 2 <= 256 and K % (128 * S * 2) == 0 and K // (S * 2) >= 512:
+        S *= 2
+    return S if S >= 2 else 0
+
+
+_PREFILL_SPLIT = os.environ.get("DOCQA_PREFILL_SPLIT", "1") != "0"
+_PREFILL_SPLIT_MAX = int(os.environ.get("DOCQA_PREFILL_SPLIT_MAX", "8"))
 
 
 def prefill_linear(x, w):
@@ -783,6 +814,28 @@ def group_tiles_by_position(tables: list[list[int]], lens: list[int], rows: list
     return out
 
 
+def remap_plan_rows(plan: torch.Tensor, plan_ids: list, ids: list) -> torch.Tensor | None:
+    """A split plan (:func:`split_decode_groups`, [2 or 3, cap, 8]) built for rows with
+    request ids ``plan_ids``, re-targeted at rows ``ids`` after requests RETIRED and the
+    survivors were compacted: each row id in columns 0..3 of the items and merges becomes
+    the survivor's new index, or -1 if it retired.  None if ``ids`` holds a request the plan
+    does not know (an admission: re-plan).  Positions and split points stay valid -- they
+    depend only on each survivor's blocks and END length -- and every item of a group
+    carries the group's rows, so a fully retired group's items all exit before drawing a
+    merge ticket."""
+    pos = {rid: i for i, rid in enumerate(plan_ids)}
+    if not all(rid in pos for rid in ids):
+        return None
+    n = len(plan_ids)
+    m = torch.full((n + 1,), -1, dtype=torch.int32)
+    if ids:
+        m[torch.tensor([pos[rid] for rid in ids], dtype=torch.long)] = torch.arange(len(ids), dtype=torch.int32)
+    out = plan.clone()
+    cols = plan[:2, :, :4].long()
+    out[:2, :, :4] = torch.where(cols >= 0, m[cols.clamp(min=0, max=n)], torch.full_like(plan[:2, :, :4], -1))
+    return out
+
+
 def persist_bins(cap: int, Hkv: int) -> int:
     """Workgroups per KV head of the persistent grouped decode (attn_decode.hip
     group_persist_bins): ~3 per CU chip-wide, at least one per quad of ``cap`` rows."""
@@ -795,7 +848,7 @@ BIN_ITEMS, BIN_MAX_TILES = 8, 512    # attn_decode.hip kBinItems / kBinMaxTiles
 
 def split_decode_groups(quads: list[list[int]], tables: list[list[int]], lens: list[int], skip: int,
                         block_size: int, cap: int, tiles_per_item: int = 12, bins: int = 0,
-                        defer: bool = False) -> torch.Tensor:
+                        defer: bool = False, per_quad: list | None = None) -> torch.Tensor:
     """Split plan for the grouped cascade decode (``paged_decode_cascade_grouped`` with a
     [2, cap, 8] int32 ``groups``): every group of :func:`pack_decode_groups` is cut at block
     positions into work items of about ``tiles_per_item`` K/V tiles (``lens``: the lengths
@@ -814,14 +867,18 @@ def split_decode_groups(quads: list[list[int]], tables: list[list[int]], lens: l
 
     ``defer``: every item writes a partial and every group has a merge row (at most ``cap``),
     as in the persistent plan, so no item reads the cascade-prefix partials and the prefix
-    kernel runs on a side stream beside the group kernel (attn_decode.hip, DOCQA_GROUP_DEFER)."""
+    kernel runs on a side stream beside the group kernel (attn_decode.hip, DOCQA_GROUP_DEFER).
+
+    ``per_quad``: :func:`group_tiles_by_position` of each quad, precomputed (a caller that
+    tries several budgets for one batch computes them once -- they do not depend on it)."""
     budget = max(1, tiles_per_item)
     all_partial = bool(bins) or defer
+    if per_quad is None:
+        per_quad = [group_tiles_by_position(tables, lens, list(qd), skip, block_size) for qd in quads]
     while True:
         items, merges, nslot = [], [], 0
-        for qd in quads:
+        for qd, per in zip(quads, per_quad):
             rows4 = (list(qd) + [-1] * 4)[:4]
-            per = group_tiles_by_position(tables, lens, list(qd), skip, block_size)
             cuts, acc, start = [], 0, skip
             for pos, t in per:
                 if acc and acc + t > budget:

@@ -8,6 +8,7 @@ of interleaved rounds:
              split-K consumer would pay)
 Usage: python scripts/pgemm_mid_probe.py [M ...]   -> one JSON line per (M, projection)"""
 import json
+import os
 import statistics
 import sys
 
@@ -40,7 +41,10 @@ def main():
     nat = torch.ops.docqa
     Ms = [int(a) for a in sys.argv[1:]] or [512, 1024, 2048, 4096]
     for M in Ms:
+        only = os.environ.get("PROBE_PROJ", "")
         for name, (N, K, epi) in PROJ.items():
+            if only and name not in only.split(","):
+                continue
             x = (torch.rand(M, K, device="cuda") * 2 - 1).to(torch.bfloat16)
             w = ((torch.rand(N, K, device="cuda") * 2 - 1) / K ** 0.5).to(torch.bfloat16)
             c = {}
@@ -54,7 +58,10 @@ def main():
                 c["hipblaslt"] = lambda: F.linear(x, w)
                 if N % 256 == 0:
                     c["pgemm"] = lambda: nat.pgemm(x, w, 0)
-                    c["pgS2"] = lambda: nat.pgemm_partial(x, w, 2).sum(0)
+                    for S in (2, 4, 8, 16):
+                        if K % (128 * S) == 0 and (S == 2 or N < 4096):
+                            c[f"pgS{S}"] = (lambda S=S: nat.pgemm_partial(x, w, S).sum(0))
+                            c[f"pgS{S}_only"] = (lambda S=S: nat.pgemm_partial(x, w, S))
                 c["gemm128"] = lambda: nat.gemm(x, w, None, None, 0)
                 for cfg in (2, 6, 7):
                     if N % nat.mgemm_tile_n(cfg) == 0:
@@ -65,7 +72,10 @@ def main():
             errs = {}
             for k, fn in c.items():
                 try:
-                    errs[k] = round((fn().float() - r).abs().max().item() / max(1e-6, r.abs().max().item()), 5)
+                    y = fn().float()
+                    if k.endswith("_only"):
+                        y = y.sum(0)
+                    errs[k] = round((y - r).abs().max().item() / max(1e-6, r.abs().max().item()), 5)
                 except Exception as e:  # noqa: BLE001 -- a shape a candidate does not take
                     errs[k] = f"n/a: {str(e).splitlines()[0][:60]}"
             t = {k: [] for k in c if not isinstance(errs[k], str)}
@@ -78,7 +88,7 @@ def main():
                 med = statistics.median(v)
                 out[k + "_us"] = round(med, 1)
                 out[k + "_TF"] = round(flops / med / 1e6, 1)
-            best = min((k for k in t if k != "hipblaslt"), key=lambda k: out[k + "_us"])
+            best = min((k for k in t if k != "hipblaslt" and not k.endswith("_only")), key=lambda k: out[k + "_us"])
             out["best"] = best
             out["best_vs_lib"] = round(out["hipblaslt_us"] / out[best + "_us"], 3)
             out["errs"] = errs

@@ -330,3 +330,49 @@ def test_wave_kernel_matches_cooperative(native, B, Hkv, seed, maxb, tiles, inli
             assert d < 2e-2, d
     finally:
         torch.ops.docqa.set_group_wave(was)
+
+
+@pytest.mark.parametrize("variant", [0, 1])
+def test_remapped_plan_after_retirement_matches_per_row(native, variant):
+    """Requests retire and the survivors are compacted: the plan re-targeted by
+    ops.remap_plan_rows (no re-plan) still gives the per-row attention of the survivors,
+    with the merge tickets left re-armed (fully retired groups draw none)."""
+    Hkv, D, BS, Pb, maxb, B = 8, 128, 64, 3, 12, 96
+    Hq = 4 * Hkv
+    tables, lens, nblk = _trie_batch(B, Pb, maxb, 21)
+    end_lens = [min(L + 128, maxb * BS) for L in lens]
+    quads = native.pack_decode_groups(tables, end_lens, Pb, BS, (B + 1) // 2)
+    plan = native.split_decode_groups(quads, tables, end_lens, 0, BS, B, 3)
+    ids = list(range(1000, 1000 + B))
+    rnd = random.Random(3)
+    keep = sorted(rnd.sample(range(B), 80))
+    for qd in quads[:3]:                         # retire three whole groups too
+        keep = [i for i in keep if i not in qd]
+    new_plan = native.remap_plan_rows(plan, ids, [ids[i] for i in keep])
+    assert new_plan is not None
+    assert native.remap_plan_rows(plan, ids, [ids[i] for i in keep] + [7]) is None   # an admission
+    tables2, lens2 = [tables[i] for i in keep], [lens[i] for i in keep]
+    n = len(keep)
+    kc = torch.randn(nblk, Hkv, BS, D, device="cuda", dtype=torch.bfloat16)
+    vc = torch.randn_like(kc)
+    bt = torch.tensor(tables2, dtype=torch.int32, device="cuda")
+    cl = torch.tensor(lens2, dtype=torch.int32, device="cuda")
+    q = torch.randn(n, (Hq + 2 * Hkv) * D, device="cuda", dtype=torch.bfloat16)
+    pt = torch.zeros(maxb, dtype=torch.int32, device="cuda")
+    pt[:Pb] = bt[0, :Pb]
+    plen = torch.tensor([Pb * BS], dtype=torch.int32, device="cuda")
+    scale = 1 / math.sqrt(D)
+    with native.use_reference():
+        ref32 = native.paged_decode_cascade(q, kc, vc, bt, cl, Hq, maxb * BS, scale, pt, plen, 4)
+    tick = torch.zeros(B * Hkv, dtype=torch.int32, device="cuda")
+    was = torch.ops.docqa.set_group_wave(variant)
+    try:
+        for _ in range(2):
+            out = native.paged_decode_cascade_grouped(q, kc, vc, bt, cl, Hq, scale, pt, plen, 4, new_plan.cuda(),
+                                                      False, tick, True)
+            torch.cuda.synchronize()
+            assert int(tick.abs().sum()) == 0
+            err = (out.float() - ref32.float()).abs().max().item()
+            assert err < 3e-2, err
+    finally:
+        torch.ops.docqa.set_group_wave(was)

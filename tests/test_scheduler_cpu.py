@@ -250,3 +250,24 @@ def test_sampled_request_takes_the_plain_admission():
     while ce.has_work():
         ce.step()
     assert f1.result() == _alone(m, p1, 6) and len(f2.result()) == 5
+
+
+def test_remap_plan_rows_semantics():
+    """ops.remap_plan_rows: survivors take their compacted index, retired rows -1, plan
+    geometry (positions, slots, merge rows) untouched; an unknown id means re-plan."""
+    from docqa_amd import ops
+
+    plan = torch.full((2, 6, 8), -1, dtype=torch.int32)
+    plan[:, :, 4:] = 0
+    plan[0, 0] = torch.tensor([0, 1, 2, -1, 0, 5, 0, 0], dtype=torch.int32)
+    plan[0, 1] = torch.tensor([0, 1, 2, -1, 5, 9, 1, 0], dtype=torch.int32)
+    plan[0, 2] = torch.tensor([3, 4, -1, -1, 0, 1 << 20, -1, 0], dtype=torch.int32)
+    plan[1, 0] = torch.tensor([0, 1, 2, -1, 0, 2, 0, 0], dtype=torch.int32)
+    ids = [10, 11, 12, 13, 14]
+    out = ops.remap_plan_rows(plan, ids, [11, 13, 14])          # 10 and 12 retired
+    assert out[0, 0].tolist() == [-1, 0, -1, -1, 0, 5, 0, 0]
+    assert out[0, 1].tolist() == [-1, 0, -1, -1, 5, 9, 1, 0]
+    assert out[0, 2].tolist() == [1, 2, -1, -1, 0, 1 << 20, -1, 0]
+    assert out[1, 0].tolist() == [-1, 0, -1, -1, 0, 2, 0, 0]
+    assert torch.equal(out[:, 3:], plan[:, 3:])
+    assert ops.remap_plan_rows(plan, ids, [11, 99]) is None
