@@ -657,8 +657,9 @@ at::Tensor gemm(const at::Tensor& a, const at::Tensor& w, const c10::optional<at
   const void* rp = nullptr;
   if (bias.has_value()) { CHECK_BF16(*bias); TORCH_CHECK(bias->numel() == N, "bias size"); bp = bias->data_ptr(); }
   if (residual.has_value()) { CHECK_BF16(*residual); CHECK_CONTIG(*residual); rp = residual->data_ptr(); }
+  TORCH_CHECK(epi != 4 || N % 128 == 0, "gemm: the SwiGLU epilogue needs 8-interleaved gate|up rows, N % 128");
   auto sizes = a.sizes().vec();
-  sizes.back() = N;
+  sizes.back() = epi == 4 ? N / 2 : N;   // 4: SwiGLU over 8-interleaved gate|up -> [.., N / 2]
   c10::DeviceGuard g(a.device());
   auto out = at::empty(sizes, a.options());
   CHECK_RC(docqa_gemm(a.data_ptr(), w.data_ptr(), bp, rp, out.data_ptr(), M, N, K, (int)epi, stream()), "gemm");

@@ -1,7 +1,8 @@
 // gemm.hip -- bf16 MFMA GEMM with fused epilogues for the encoder stacks
 //   C[M, N] = act(A[M, K] . W[N, K]^T + bias[N]) (+ residual[M, N])
 // (nn.Linear layout: weights stored [out, in]).  Epilogues: none, bias, bias+GELU(erf),
-// bias+residual.  Used by the BERT encoders (MiniLM / bge / clinical-BERT): the FFN-up
+// bias+residual, and the Llama SwiGLU over 8-interleaved gate|up rows (prefill shapes whose
+// 256 x 256 tiles cannot fill the chip: the 70B TP-8 gate|up shard at <= 1k tokens).  Used by the BERT encoders (MiniLM / bge / clinical-BERT): the FFN-up
 // GEMM with its bias+GELU, the QKV and output projections with their biases, so no
 // separate element-wise pass re-reads the [tokens, 4H] activations from HBM.
 //
@@ -26,7 +27,7 @@ namespace {
 constexpr int BM = 128, BN = 128, BK = 64;
 typedef short i16x8 __attribute__((ext_vector_type(8)));
 
-enum Epi { EPI_NONE = 0, EPI_BIAS = 1, EPI_BIAS_GELU = 2, EPI_BIAS_RES = 3 };
+enum Epi { EPI_NONE = 0, EPI_BIAS = 1, EPI_BIAS_GELU = 2, EPI_BIAS_RES = 3, EPI_GLU = 4 };
 
 __device__ __forceinline__ int sw_off(int row, int ch) {  // element offset in a [128][64] tile
   return row * BK + ((ch ^ ((row >> 1) & 7)) << 3);
@@ -120,6 +121,27 @@ __global__ __launch_bounds__(256) void gemm_kernel(const uint16_t* __restrict__ 
       for (int r = 0; r < 4; ++r)
         st[(i * 16 + fk * 4 + r) * 65 + j * 16 + fr] = acc[i][j][r];
   __syncthreads();
+  if constexpr (EPI == EPI_GLU) {
+    // Llama gate|up in the 8-interleaved row layout (decode GEMMs' layout): output columns
+    // [16 p, 16 p + 8) are gate, [16 p + 8, 16 p + 16) up; C is [M, N / 2] =
+    // silu(gate) * up, each input rounded to bf16 first (as the unfused bf16 GEMM output
+    // would be).  Lane -> (row, pair p of the wave's 4)
+    for (int it = 0; it < 4; ++it) {
+      const int rloc = it * 16 + (lane >> 2), p = lane & 3;
+      const int gr = row0 + wr * 64 + rloc;
+      if (gr < M) {
+        float o[8];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const float g = bf2f(f2bf(st[rloc * 65 + p * 16 + e]));
+          const float u = bf2f(f2bf(st[rloc * 65 + p * 16 + 8 + e]));
+          o[e] = g / (1.f + __expf(-g)) * u;
+        }
+        *reinterpret_cast<uint4*>(C + (size_t)gr * (N >> 1) + ((col0 + wc * 64) >> 1) + p * 8) = pack8(o);
+      }
+    }
+    return;
+  }
   // each wave writes its own 64 rows x 64 cols: lane -> (row group, 8-col chunk)
   for (int it = 0; it < 8; ++it) {
     const int rloc = it * 8 + (lane >> 3);
@@ -156,7 +178,7 @@ int docqa_gemm(const void* A, const void* W, const void* bias, const void* res, 
                int N, int K, int epi, hipStream_t s) {
   if (M == 0) return 0;
   if (N % BN != 0 || K % BK != 0) return -1;
-  if (epi != EPI_NONE && bias == nullptr) return -1;
+  if (epi != EPI_NONE && epi != EPI_GLU && bias == nullptr) return -1;
   if (epi == EPI_BIAS_RES && res == nullptr) return -1;
   const int nwg = (N / BN) * ((M + BM - 1) / BM);
   const uint16_t *a = (const uint16_t*)A, *w = (const uint16_t*)W, *b = (const uint16_t*)bias,
@@ -167,6 +189,7 @@ int docqa_gemm(const void* A, const void* W, const void* bias, const void* res, 
     case EPI_BIAS: gemm_kernel<EPI_BIAS><<<nwg, 256, 0, s>>>(a, w, b, r, c, M, N, K); break;
     case EPI_BIAS_GELU: gemm_kernel<EPI_BIAS_GELU><<<nwg, 256, 0, s>>>(a, w, b, r, c, M, N, K); break;
     case EPI_BIAS_RES: gemm_kernel<EPI_BIAS_RES><<<nwg, 256, 0, s>>>(a, w, b, r, c, M, N, K); break;
+    case EPI_GLU: gemm_kernel<EPI_GLU><<<nwg, 256, 0, s>>>(a, w, b, r, c, M, N, K); break;
     default: return -1;
   }
   DOCQA_CHECK_LAUNCH();

@@ -145,7 +145,7 @@ def bias_act(x, bias, residual=None, gelu: bool = False):
 
 
 # ----------------------------------------------------------------------------- fused GEMM
-EPI_NONE, EPI_BIAS, EPI_BIAS_GELU, EPI_BIAS_RES = 0, 1, 2, 3
+EPI_NONE, EPI_BIAS, EPI_BIAS_GELU, EPI_BIAS_RES, EPI_GLU = 0, 1, 2, 3, 4
 
 
 def linear_fused(x, w, bias=None, residual=None, epi: int = EPI_BIAS):
@@ -388,6 +388,9 @@ def prefill_linear(x, w):
     return torch.nn.functional.linear(x, w)
 
 
+_GLU128 = os.environ.get("DOCQA_GLU128", "1") != "0"
+
+
 def prefill_glu(x, w_il):
     """silu(x Wg^T) * (x Wu^T) for 8-interleaved gate|up weights at prefill sizes: SwiGLU
     fused into the 256 x 256 GEMM's epilogue (no [M, 2I] round trip through HBM)."""
@@ -396,6 +399,11 @@ def prefill_glu(x, w_il):
         M = x.numel() // K
         if pgemm_ok(M, N, K):
             return _native().pgemm(x.contiguous(), w_il, 1)
+        if (_GLU128 and N % 128 == 0 and K % 64 == 0 and ((M + 255) // 256) * (N // 128) < 256
+                and ((M + 127) // 128) * (N // 128) >= 192):
+            # too few 256 x 256 tiles, and the 256 x 128 kernel would leave CUs idle: the
+            # 128 x 128 tiles with the SwiGLU epilogue (gemm.hip EPI_GLU; the 70B TP-8 shard)
+            return _native().gemm(x.contiguous(), w_il, None, None, EPI_GLU)
         if N % 128 == 0 and K % 128 == 0:
             return _native().mgemm_glu(x.contiguous(), w_il, 2)
     return silu_mul(prefill_linear(x, w_il), interleaved=True)

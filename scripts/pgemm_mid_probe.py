@@ -53,6 +53,7 @@ def main():
                 if N % 256 == 0:
                     c["pgemm"] = lambda: nat.pgemm(x, w, 1)
                 c["mgemm_2"] = lambda: nat.mgemm_glu(x, w, 2)
+                c["gemm128"] = lambda: nat.gemm(x, w, None, None, 4)
                 c["mgemm_6"] = lambda: nat.mgemm_glu(x, w, 6)
             else:
                 c["hipblaslt"] = lambda: F.linear(x, w)

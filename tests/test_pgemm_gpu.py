@@ -81,3 +81,31 @@ def test_pgemm_splitk_slabs(M, N, K, S):
     Ks = K // S
     r0 = x[:, :Ks].float() @ w[:, :Ks].float().t()
     assert (P[0] - r0).abs().max().item() <= 2e-3 * r0.abs().max().item() + 1e-3
+
+
+@pytest.mark.parametrize("M,N,K", [(512, 7168, 8192), (1000, 7168, 1024), (77, 256, 128)])
+def test_gemm128_swiglu_epilogue(M, N, K):
+    """gemm.hip EPI_GLU (128 x 128 tiles, SwiGLU over 8-interleaved gate|up rows, inputs
+    rounded to bf16 like the unfused GEMM's output) == the fp32 reference; the prefill
+    dispatch takes it where the 256-wide tiles leave the chip idle (70B TP-8 gate|up)."""
+    x, w = _data(M, N, K, seed=7)
+    y = torch.ops.docqa.gemm(x, w, None, None, ops.EPI_GLU)
+    r = ref.silu_mul((x.float() @ w.float().t()), interleaved=True).float()
+    assert y.shape == (M, N // 2)
+    err = (y.float() - r).abs().max().item()
+    assert err <= 2e-2 * r.abs().max().item() + 1e-3, err
+    y2 = ops.prefill_glu(x, w)
+    assert (y2.float() - r).abs().max().item() <= 2e-2 * r.abs().max().item() + 1e-3
+
+
+def test_prefill_split_plan_slabs_feed_the_consumers():
+    """The narrow-N prefill split (ops.prefill_split_plan, the 70B TP-8 QKV shard) picks
+    S with tiles x S <= 256 and K % (128 S) == 0; its slabs sum to the product."""
+    assert ops.prefill_split_plan(512, 1280, 8192) == 8
+    assert ops.prefill_split_plan(4096, 1280, 8192) == 2
+    assert ops.prefill_split_plan(512, 6144, 4096) == 0           # wide N: no split
+    x, w = _data(700, 1280, 8192, seed=8)
+    S = ops.prefill_split_plan(700, 1280, 8192)
+    P = ops.pgemm_partial(x, w, S)
+    r = x.float() @ w.float().t()
+    assert (P.sum(0) - r).abs().max().item() <= 2e-3 * r.abs().max().item() + 1e-3
