@@ -135,6 +135,10 @@ def _upload(dst: torch.Tensor, src: torch.Tensor) -> None:
         dst.copy_(src)
 
 
+_GROUP_NOPREFIX = os.environ.get("DOCQA_GROUP_NOPREFIX", "1") == "1"
+_GROUP_NOPREFIX_MIN = int(os.environ.get("DOCQA_GROUP_NOPREFIX_MIN_BATCH", "32"))
+
+
 def _split_groups_on() -> bool:
     return os.environ.get("DOCQA_GROUP_SPLIT", "1") == "1"
 
@@ -557,6 +561,20 @@ class LLMEngine:
         _upload(g.groups, flat)
         g.groups_key = key
 
+    def group_without_prefix(self, B: int) -> bool:
+        """The grouped split-plan decode with the prefix attended inline needs no prefix
+        shared by EVERY row: its items start at block 0 and rows are grouped by whatever
+        prefix-cache blocks they share (retrieved chunks).  So batches without a common
+        template prefix -- the reference QA template puts the context first -- take the
+        wave-parallel grouped kernel too instead of the per-row ring kernel (round 5: 162 us
+        vs ~70 us per layer at batch 256, profiles/r5_head_kernel_stats.txt).
+        DOCQA_GROUP_NOPREFIX=0 disables; from DOCQA_GROUP_NOPREFIX_MIN_BATCH rows (32)."""
+        return (B >= _GROUP_NOPREFIX_MIN and _GROUP_NOPREFIX and self.group_decode and self.cascade
+                and self.device.type == "cuda" and _split_groups_on() and _inline_prefix_on()
+                and not _defer_groups_on() and not _persist_groups_on()
+                and ops.grouped_decode_ok(self.kv.caches[0][0], torch.empty(0, self.max_blocks_per_seq),
+                                          self.model.hq))
+
     def _cascade_chunks(self, bp: int) -> int:
         """Key chunks of the shared-prefix kernel: about 256 workgroups of (64 rows, KV
         head, chunk) in total, 1..16 chunks (DOCQA_CASCADE_CHUNKS overrides)."""
@@ -809,7 +827,10 @@ class LLMEngine:
             nshared = self._shared_prefix_blocks(tables, cached)
             self.stats.attn_kv_blocks += nshared + len({b for t in tables for b in t[nshared:]})
             self.stats.attn_batches += 1
-            g = self._get_graph(_bucket(B, self.max_batch) if self.use_graphs else B, greedy, nshared > 0)
+            grouped = nshared > 0 or self.group_without_prefix(B)
+            g = self._get_graph(_bucket(B, self.max_batch) if self.use_graphs else B, greedy, grouped)
+            if grouped:
+                g.shared_len.fill_(0)
             if nshared:
                 st = torch.zeros(self.max_blocks_per_seq, dtype=torch.int32)
                 st[:nshared] = torch.tensor(tables[0][:nshared], dtype=torch.int32)
@@ -828,7 +849,7 @@ class LLMEngine:
             _upload(g.positions, pos)
             _upload(g.context_lens, pos + vl)
             self.set_order(g, lens)
-            if nshared:
+            if grouped:
                 self.set_groups(g, tables, [n + params.max_new_tokens for n in lens], nshared)
                 if _DECODE_DUMP:
                     self._dump_decode(g, tables, lens, nshared, params)

@@ -134,6 +134,11 @@ class ContinuousEngine:
         self._pending = None               # (event, pinned host tokens, slot -> request) of the last step
         self._host = None
         self._flip = 0
+        self._mhost = None   # mixed steps' pinned token buffers (decode rows + first tokens)
+        self._mflip = 0
+        # CPU runs read each step's tokens at once; True: lag them by one step as on a GPU
+        # (the tests exercise the GPU's readback order on the CPU this way)
+        self.lag_cpu = False
         self._version = 0                  # bumped whenever the running set changes
         # KV blocks on demand: admission reserves the prompt + ``reserve_ahead`` generated
         # tokens (not all max_new_tokens), tables grow a block at a time as decode reaches
@@ -254,8 +259,9 @@ class ContinuousEngine:
                 pass
 
     def _fail_all(self, e: Exception) -> None:
+        lagged = list(self._pending[4]) if self._pending is not None and isinstance(self._pending[0], str) else []
         self._pending = None
-        for r in self.running + self.prefilling:
+        for r in self.running + self.prefilling + lagged:
             self.eng.kv.allocator.free(r.blocks)
             if not r.future.done():
                 r.future.set_exception(e)
@@ -342,7 +348,7 @@ class ContinuousEngine:
         eng, alloc = self.eng, self.eng.kv.allocator
         admitted, budget = [], 0
         with self._cv:
-            while self.waiting and len(self.running) + len(self.prefilling) + len(admitted) < self.max_running:
+            while self.waiting and self._occupied() + len(admitted) < self.max_running:
                 r = self.waiting[0]
                 if mixed and (r.params.temperature > 0 or (token_cap is not None and budget >= token_cap)):
                     break
@@ -369,12 +375,19 @@ class ContinuousEngine:
                     break
         return admitted
 
+    def _occupied(self) -> int:
+        """Decode slots taken or promised: running rows, prompts being chunk-prefilled, and
+        prompts whose last chunk ran in the step whose tokens are still to be read (they
+        join the running rows when that lagged readback is processed)."""
+        lag = len(self._pending[4]) if self._pending is not None and isinstance(self._pending[0], str) else 0
+        return len(self.running) + len(self.prefilling) + lag
+
     def _admission_due(self) -> bool:
         """Whether the waiting requests are admitted at this step (the timing-dependent
         half of admission; a lockstep leader broadcasts it)."""
         if self.mixed and self.running and self.waiting:
             # chunks ride in the decode steps: admit as soon as a slot is free, no hold
-            return len(self.running) + len(self.prefilling) < self.max_running
+            return self._occupied() < self.max_running
         if self.running and self.waiting:
             # gather a group -- one prefill pass over the weights for several requests --
             # until admit_min requests can join or the first of them has waited
@@ -382,7 +395,7 @@ class ContinuousEngine:
             # free up one or two per step as requests finish, and admitting them as they
             # appear ran a near-empty prefill pass every step or two (continuous 114.6 vs
             # static 118.9 q/s at Poisson 140, prefill 29 % of the wall time).
-            free = self.max_running - len(self.running)
+            free = self.max_running - self._occupied()
             now = time.perf_counter()
             if free <= 0:
                 self._free_t = None
@@ -458,13 +471,14 @@ class ContinuousEngine:
 
     def _mixed_step(self, decision) -> None:
         """One forward over every running slot's next token AND up to ``chunk_tokens`` of
-        the pending prompts (LlamaModel.forward_mixed).  Synchronous: the chunk's first
-        tokens are needed on the host to place the completed prompts, so the previous
-        step's lagged readback is folded in first and this step's tokens are read here."""
+        the pending prompts (LlamaModel.forward_mixed).  Asynchronous like a plain decode
+        step: this step's tokens (decode rows + the first tokens of the prompts whose last
+        chunk ran) are copied to pinned host memory and read while the NEXT step runs, so
+        the eager forward's launch work overlaps the GPU instead of serialising with it
+        (the synchronous version lost to admission batching, profiles/r5_serving_mixed_ab.log).
+        A prompt that completes here joins the decode slots when its tokens are processed,
+        one step later."""
         eng, BS = self.eng, self.eng.block_size
-        if self._pending is not None:
-            p, self._pending = self._pending, None
-            self._process(p)
         if decision is None:
             decision = self._admission_due()
         if decision and self.waiting:
@@ -478,6 +492,9 @@ class ContinuousEngine:
         if not self.prefilling:
             if self.running:
                 self._decode()
+            elif self._pending is not None:
+                p, self._pending = self._pending, None
+                self._process(p)
             return
         self._grow_tables()
         t0 = time.perf_counter()
@@ -494,10 +511,11 @@ class ContinuousEngine:
         g, bp, dmeta = None, 0, None
         if n:
             bp = _bucket(n, eng.max_batch) if self.pad_buckets else n
-            g = self._graph(bp, True, self._nshared > 0)
+            grouped = self._nshared > 0 or eng.group_without_prefix(n)
+            g = self._graph(bp, True, grouped)
             if eng.lpt:
                 eng.set_order(g, [len(r.prompt) + len(r.out) for r in self.running], key=self._version)
-            if self._nshared > 0:
+            if grouped:
                 eng.set_groups(g, [r.blocks for r in self.running],
                                [len(r.prompt) + r.params.max_new_tokens for r in self.running], self._nshared,
                                key=(self._version, self._nshared), ids=[r.rid for r in self.running])
@@ -524,45 +542,70 @@ class ContinuousEngine:
             if bp:
                 ops.decode_advance(nxt[:bp].long().contiguous(), g.out, g.tokens, g.positions, g.context_lens,
                                    g.valid)
-            err = comm.collective_error_snapshot()
-            toks = nxt.tolist()
-            comm.raise_on_collective_error(err)
+        # launch-time bookkeeping: everything that does not need the tokens
         self.steps += 1
         self.mixed_steps += 1
-        now = time.perf_counter()
-        # decode rows: the same bookkeeping as a plain step (_decode + _process)
-        if n:
-            eng.stats.generated_tokens += n
-            snap = list(self.running)
-            for r in snap:
-                r.pos += 1
-            finished = []
-            for r, t in zip(snap, toks[:n]):
-                if r.done:
-                    continue
-                self._emit(r, t)
-                if self._finished(r):
-                    r.done = True
-                    finished.append(r)
-            if finished:
-                for r in finished:
-                    self._retire(r)
-                self._compact([i for i, r in enumerate(self.running) if not r.done])
-        # prompt chunks: progress, and first tokens of the prompts whose last chunk ran
-        joined, completed = [], []
+        eng.stats.generated_tokens += n
+        snap = list(self.running)
+        for r in snap:
+            r.pos += 1
         for r, _, e in pieces:
             r.filled = e
-        for i, t in zip(done, toks[bp:]):
-            completed.append((pieces[i][0], t))
-        if completed:
-            gone = {id(r) for r, _ in completed}
+        completing = [pieces[i][0] for i in done]
+        if completing:
+            gone = {id(r) for r in completing}
             self.prefilling = [r for r in self.prefilling if id(r) not in gone]
-            reqs = [r for r, _ in completed]
-            eng.register_prefixes([r.prompt for r in reqs], [r.blocks for r in reqs],
-                                  [r.res.keys[0] if r.res is not None and r.res.keys else None for r in reqs])
-            eng.stats.prompt_tokens += sum(len(r.prompt) for r in reqs)
-            eng.stats.cached_tokens += sum(r.cached for r in reqs)
-            for r, t in completed:
+        k = len(rows)
+        if nxt.device.type == "cuda":
+            if self._mhost is None or self._mhost[0].dtype != nxt.dtype or self._mhost[0].numel() < k:
+                size = max(k, eng.max_batch + self.chunk_tokens)
+                self._mhost = [torch.empty(size, dtype=nxt.dtype, pin_memory=True) for _ in range(2)]
+            host = self._mhost[self._mflip]
+            self._mflip ^= 1
+            host[:k].copy_(nxt[:k], non_blocking=True)
+            ev = torch.cuda.Event()
+            ev.record()
+        else:
+            host, ev = nxt[:k].clone(), None
+        pend = ("mixed", ev, host, snap, completing, bp, comm.collective_error_snapshot())
+        prev, self._pending = self._pending, pend
+        if prev is not None:
+            self._process(prev)              # step t-1's tokens while step t runs
+        if ev is None and not self.lag_cpu:
+            p, self._pending = self._pending, None
+            self._process(p)
+        eng.stats.decode_s += time.perf_counter() - t0
+
+    def _process_mixed(self, pending) -> None:
+        """The lagged readback of a mixed step: decode rows as in :meth:`_process`, then
+        the prompts whose last chunk ran -- prefix registration, first token, a decode
+        slot (or retirement)."""
+        _, ev, host, snap, completing, bp, err = pending
+        if ev is not None:
+            ev.synchronize()
+        comm.raise_on_collective_error(err)
+        toks = host[:bp + len(completing)].tolist()
+        finished = []
+        for r, t in zip(snap, toks[:len(snap)]):
+            if r.done:
+                continue                      # the extra lagged step of a finished request
+            self._emit(r, t)
+            if self._finished(r):
+                r.done = True
+                finished.append(r)
+        if finished:
+            for r in finished:
+                self._retire(r)
+            self._compact([i for i, r in enumerate(self.running) if not r.done])
+        if completing:
+            eng = self.eng
+            eng.register_prefixes([r.prompt for r in completing], [r.blocks for r in completing],
+                                  [r.res.keys[0] if r.res is not None and r.res.keys else None for r in completing])
+            eng.stats.prompt_tokens += sum(len(r.prompt) for r in completing)
+            eng.stats.cached_tokens += sum(r.cached for r in completing)
+            now = time.perf_counter()
+            joined = []
+            for r, t in zip(completing, toks[bp:]):
                 r.t_first = now
                 self._emit(r, t)
                 if self._finished(r):
@@ -570,10 +613,9 @@ class ContinuousEngine:
                     self._retire(r)
                 else:
                     joined.append(r)
-        if joined:
-            self._place(joined)
+            if joined:
+                self._place(joined)
         self._update_shared()
-        eng.stats.decode_s += now - t0
 
     def _place(self, reqs: list[Request]) -> None:
         """Write the decode state of newly joined requests into slots [n, n + k)."""
@@ -698,11 +740,12 @@ class ContinuousEngine:
             return
         bp = _bucket(n, eng.max_batch) if self.pad_buckets else n
         greedy = all(r.params.temperature <= 0 for r in self.running)
-        g = self._graph(bp, greedy, self._nshared > 0)
+        grouped = self._nshared > 0 or eng.group_without_prefix(n)
+        g = self._graph(bp, greedy, grouped)
         if eng.lpt:
             # re-rank only when the running set changed (admission / retirement)
             eng.set_order(g, [len(r.prompt) + len(r.out) for r in self.running], key=self._version)
-        if self._nshared > 0:
+        if grouped:
             eng.set_groups(g, [r.blocks for r in self.running],
                            [len(r.prompt) + r.params.max_new_tokens for r in self.running], self._nshared,
                            key=(self._version, self._nshared), ids=[r.rid for r in self.running])
@@ -721,15 +764,18 @@ class ContinuousEngine:
         for r in self.running:
             r.pos += 1
         snap = list(self.running)
-        if g.out.device.type == "cuda":
-            if self._host is None:
-                self._host = [torch.empty(eng.max_batch, dtype=torch.long, pin_memory=True) for _ in range(2)]
-            host = self._host[self._flip]
-            self._flip ^= 1
-            host[:n].copy_(g.out[:n], non_blocking=True)
-            err = comm.collective_error_snapshot()
-            ev = torch.cuda.Event()
-            ev.record()
+        if g.out.device.type == "cuda" or self.lag_cpu:
+            if g.out.device.type == "cuda":
+                if self._host is None:
+                    self._host = [torch.empty(eng.max_batch, dtype=torch.long, pin_memory=True) for _ in range(2)]
+                host = self._host[self._flip]
+                self._flip ^= 1
+                host[:n].copy_(g.out[:n], non_blocking=True)
+                err = comm.collective_error_snapshot()
+                ev = torch.cuda.Event()
+                ev.record()
+            else:
+                host, err, ev = g.out[:n].clone(), comm.collective_error_snapshot(), None
             prev, self._pending = self._pending, (ev, host, snap, err)
             if prev is not None:
                 self._process(prev)          # step t-1's tokens while step t runs
@@ -738,6 +784,9 @@ class ContinuousEngine:
         eng.stats.decode_s += time.perf_counter() - t0
 
     def _process(self, pending) -> None:
+        if isinstance(pending[0], str):      # ("mixed", ...): a mixed step's readback
+            self._process_mixed(pending)
+            return
         ev, host, snap, err = pending
         if ev is not None:
             ev.synchronize()

@@ -399,10 +399,12 @@ def prefill_glu(x, w_il):
         M = x.numel() // K
         if pgemm_ok(M, N, K):
             return _native().pgemm(x.contiguous(), w_il, 1)
-        if (_GLU128 and N % 128 == 0 and K % 64 == 0 and ((M + 255) // 256) * (N // 128) < 256
+        if (_GLU128 and N % 128 == 0 and K % 64 == 0 and ((M + 255) // 256) * (N // 128) < 128
                 and ((M + 127) // 128) * (N // 128) >= 192):
-            # too few 256 x 256 tiles, and the 256 x 128 kernel would leave CUs idle: the
-            # 128 x 128 tiles with the SwiGLU epilogue (gemm.hip EPI_GLU; the 70B TP-8 shard)
+            # too few 256 x 256 tiles, and the 256 x 128 kernel would leave half the CUs idle:
+            # the 128 x 128 tiles with the SwiGLU epilogue (gemm.hip EPI_GLU) -- 70B TP-8
+            # gate|up shard at 512 rows 90.8 us vs 106.1 (256 x 128) and 132.7 (256 x 256);
+            # hipBLASLt + silu_mul 64.6 (profiles/r5_pgemm_70b_split_probe.log)
             return _native().gemm(x.contiguous(), w_il, None, None, EPI_GLU)
         if N % 128 == 0 and K % 128 == 0:
             return _native().mgemm_glu(x.contiguous(), w_il, 2)
