@@ -28,11 +28,15 @@ requests join and leave between steps:
     rows and the chunk's tokens together, only attention is split by row kind.  A
     running request never waits for a separate prefill pass and arrivals are admitted the
     step they come (no hold to batch prefills); a prompt longer than the budget is spread
-    over several steps, its first token sampled when its last chunk has run.  Measured
-    SLOWER than admission batching on the GPU (profiles/r5_serving_mixed_ab.log: offered
-    60 q/s p50 2.39 s vs 1.45 s; offered 100 78 vs 91 q/s): a mixed step is an eager,
-    host-synchronised forward, so its ~20 ms of launch work does not overlap the GPU the
-    way graph-replayed decode steps and a few large admission prefills do;
+    over several steps, its first token sampled when its last chunk has run.  Mixed steps
+    read their tokens one step late like plain steps, so the eager forward's launch work
+    overlaps the GPU.  Still measured SLOWER than admission batching over HTTP
+    (profiles/r5_serving_async_mixed_ab.log: offered 60 q/s p50 2.05 s vs 1.38 s, offered
+    100 79 vs 92 q/s; the synchronous first version: 2.39 s / 78 q/s,
+    profiles/r5_serving_mixed_ab.log): every step that carries a chunk is an eager
+    ~500-launch forward instead of a graph replay, and a chunk of 2048 tokens holds every
+    decode row for its whole prefill, which admission batching amortises over fewer,
+    larger passes;
   * admission batching (mixed steps off, the default): under load, requests are admitted in groups
     (>= ``admit_min`` that can join -- waiting AND free slots -- or ``admit_wait_s``
     after the first could), so one prefill pass over the weights serves several new
