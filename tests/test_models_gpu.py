@@ -366,3 +366,30 @@ def test_token_classifier_fused_head_matches_unfused(native, monkeypatch):
     assert got.shape == (ids.numel(),)
     assert torch.equal(got[clear].cpu(), logits.argmax(-1)[clear].cpu())
     assert clear.float().mean().item() > 0.95
+
+
+def test_grouped_decode_without_common_prefix(native, monkeypatch):
+    """Batches whose rows share no prompt prefix (the reference QA template) take the
+    grouped split-plan decode with the prefix attended inline (LLMEngine.group_without_prefix)
+    instead of the per-row ring kernel: same generations up to fp summation-order near-ties."""
+    from docqa_amd.engine.llm_engine import LLMEngine, SamplingParams
+    from docqa_amd.models.llama import LlamaConfig, LlamaModel
+
+    m = LlamaModel(LlamaConfig.preset("llama3-1b-test"), device="cuda", seed=31)
+    g = torch.Generator().manual_seed(8)
+    shared = [torch.randint(3, 32000, (int(n),), generator=g).tolist() for n in (70, 150)]
+    prompts = []
+    for i in range(40):      # some rows share a retrieved "chunk" after a unique head, none share a prefix
+        head = torch.randint(3, 32000, (5 + i % 7,), generator=g).tolist()
+        prompts.append(head + shared[i % 2] + torch.randint(3, 32000, (20 + 3 * i,), generator=g).tolist())
+    sp = SamplingParams(max_new_tokens=10, stop_on_eos=False)
+    outs = {}
+    for flag in (False, True):
+        eng = LLMEngine(m, max_batch=64, max_context=512, use_graphs=True)
+        eng.group_without_prefix = (lambda B, f=flag, e=eng, orig=LLMEngine.group_without_prefix:
+                                    f and orig(e, B))
+        assert LLMEngine.group_without_prefix(eng, 40) or not flag
+        outs[flag] = eng.generate(prompts, sp)
+    same = sum(a == b for a, b in zip(outs[False], outs[True]))
+    assert same >= 0.8 * len(prompts), same
+    assert all(len(o) == 10 for o in outs[True])
