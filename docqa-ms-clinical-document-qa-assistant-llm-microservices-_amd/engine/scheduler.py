@@ -159,6 +159,7 @@ class ContinuousEngine:
         self.completed_short = 0  # ... of them before max_new_tokens (EOS)
         # stall-free admission: prompt chunks ride in the decode step (module docstring)
         self.mixed = os.environ.get("DOCQA_MIXED_PREFILL", "0") == "1"
+        self.mixed_hold = os.environ.get("DOCQA_MIXED_HOLD", "0") == "1"
         self.chunk_tokens = max(engine.block_size, int(os.environ.get("DOCQA_CHUNK_TOKENS", "2048")))
         self.prefilling: list[Request] = []   # admitted, prompt partly in the KV cache
         self.mixed_steps = 0
@@ -293,7 +294,7 @@ class ContinuousEngine:
         self._step(decision)
 
     def _step(self, decision) -> None:
-        if self._mixed_due():
+        if self._mixed_due(decision):
             self._mixed_step(decision)
             return
         self._admit(decision)
@@ -389,7 +390,7 @@ class ContinuousEngine:
     def _admission_due(self) -> bool:
         """Whether the waiting requests are admitted at this step (the timing-dependent
         half of admission; a lockstep leader broadcasts it)."""
-        if self.mixed and self.running and self.waiting:
+        if self.mixed and not self.mixed_hold and self.running and self.waiting:
             # chunks ride in the decode steps: admit as soon as a slot is free, no hold
             return self._occupied() < self.max_running
         if self.running and self.waiting:
@@ -463,15 +464,21 @@ class ContinuousEngine:
         self._update_shared()
 
     # ------------------------------------------------------------------ mixed steps
-    def _mixed_due(self) -> bool:
+    def _mixed_due(self, decision=None) -> bool:
         """A mixed step runs while prompt chunks are pending, or when greedy requests wait
-        beside a greedy running batch (sampled decode rows keep the separate prefill)."""
+        beside a greedy running batch (sampled decode rows keep the separate prefill).
+        ``mixed_hold``: new prompts wait for the admission-batching decision (``decision``,
+        the leader's in lockstep) as with mixed steps off, so prompts are prefilled in a
+        few large chunks that ride in one decode step each, read back one step late."""
         if not self.mixed:
             return False
         if self.prefilling:
             return True
-        return bool(self.running and self.waiting and self.waiting[0].params.temperature <= 0
-                    and all(r.params.temperature <= 0 for r in self.running))
+        due = bool(self.running and self.waiting and self.waiting[0].params.temperature <= 0
+                   and all(r.params.temperature <= 0 for r in self.running))
+        if due and self.mixed_hold:
+            due = self._admission_due() if decision is None else bool(decision)
+        return due
 
     def _mixed_step(self, decision) -> None:
         """One forward over every running slot's next token AND up to ``chunk_tokens`` of

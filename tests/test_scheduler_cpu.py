@@ -186,11 +186,15 @@ def test_mixed_steps_chunk_prompts_into_decode_steps_token_exact():
     prompts = [torch.randint(3, 4096, (int(n),), generator=g).tolist() for n in (40, 70, 23, 95, 12, 57)]
     lens = [9, 4, 12, 6, 10, 7]
     results = {}
-    for mixed, lag in ((True, False), (True, True), (False, False), (False, True)):
+    for mixed, lag, hold in ((True, False, False), (True, True, False), (False, False, False),
+                             (False, True, False), (True, True, True)):
         eng = LLMEngine(m, max_batch=4, max_context=512, block_size=16, use_graphs=False)
         ce = ContinuousEngine(eng)
         ce.mixed, ce.chunk_tokens = mixed, 32
         ce.lag_cpu = lag          # the GPU's one-step-lagged readback order, on the CPU
+        ce.mixed_hold = hold      # admission batching decides when prompts join mixed steps
+        if hold:
+            ce.admit_wait_s = 0.0
         futs = []
         for i, (p, n) in enumerate(zip(prompts, lens)):
             futs.append(ce.submit(p, SamplingParams(max_new_tokens=n, stop_on_eos=False)))
@@ -198,7 +202,7 @@ def test_mixed_steps_chunk_prompts_into_decode_steps_token_exact():
                 ce.step()
         while ce.has_work():
             ce.step()
-        results[(mixed, lag)] = [f.result() for f in futs]
+        results[(mixed, lag, hold)] = [f.result() for f in futs]
         if mixed:
             assert ce.mixed_steps >= 3, ce.mixed_steps       # the 95-token prompt alone needs 3 chunks
             assert not ce.prefilling
@@ -206,7 +210,7 @@ def test_mixed_steps_chunk_prompts_into_decode_steps_token_exact():
             eng.tail.clear()
         st = eng.kv.allocator.stats()
         assert st["free"] + st["evictable"] == eng.kv.num_blocks
-    for p, n, o in zip(prompts, lens, results[(True, False)]):
+    for p, n, o in zip(prompts, lens, results[(True, False, False)]):
         assert o == _alone(m, p, n)
     assert len({tuple(map(tuple, v)) for v in results.values()}) == 1
 
