@@ -36,6 +36,7 @@ using namespace docqa;
 namespace {
 constexpr int QB = 128;   // query rows per workgroup
 constexpr int KB = 64;    // keys per tile
+constexpr int kPrefillMaxBT = 512;   // block ids of a paged sequence staged in LDS (else read per tile)
 constexpr float kLog2e = 1.4426950408889634f;
 
 typedef __attribute__((address_space(3))) i16x4 lds_i16x4;
@@ -78,6 +79,10 @@ __global__ __launch_bounds__(64 * G * WPH) void flash_prefill_kernel(
   constexpr int NT = 64 * G * WPH;              // threads
   constexpr int QBW = 32 * WPH;                 // query rows per workgroup
   __shared__ __attribute__((aligned(16))) uint16_t smem[2 * KB * D];
+  // PAGED: the sequence's block ids, read once into LDS -- the per-tile block-table load
+  // was a dependent global round trip ahead of every tile's K/V loads (RAG shapes: 458 ->
+  // 442 us; an LDS-DMA ring for the tiles was slower still, profiles/r5_prefill_attn_ring_ab.log)
+  __shared__ int s_bt[PAGED ? kPrefillMaxBT : 1];
   uint16_t* sK = smem;
   uint16_t* sV = smem + KB * D;
 
@@ -166,6 +171,17 @@ __global__ __launch_bounds__(64 * G * WPH) void flash_prefill_kernel(
 
   // staging: KB rows x NCH chunks per tensor, CPT per thread per tensor
   uint4 rk[CPT], rv[CPT];
+  // block ids the keys [0, Lk) need; PFX: the shared prefix table (row 0, pk.maxb unset),
+  // whose first ceil(Lk / BS) entries all exist (Lk <= the prefix length)
+  const int nb_need = PAGED ? (Lk + pk.BS - 1) >> pk.log2BS : 0;
+  const bool bt_lds = PAGED && nb_need <= kPrefillMaxBT && (PFX || nb_need <= pk.maxb);
+  if constexpr (PAGED) {
+    if (bt_lds) {
+      const int* btr = pk.block_tables + (size_t)(PFX ? 0 : b) * pk.maxb;
+      for (int i = tid; i < nb_need; i += NT) s_bt[i] = btr[i];
+      __syncthreads();
+    }
+  }
   auto load_tile = [&](int t) {
 #pragma unroll
     for (int i = 0; i < CPT; ++i) {
@@ -174,7 +190,8 @@ __global__ __launch_bounds__(64 * G * WPH) void flash_prefill_kernel(
       const int key = t * KB + row;
       if (idx < KB * NCH && key < Lk) {
         if constexpr (PAGED) {
-          const int blk = pk.block_tables[(size_t)(PFX ? 0 : b) * pk.maxb + (key >> pk.log2BS)];
+          const int blk = bt_lds ? s_bt[key >> pk.log2BS]
+                                 : pk.block_tables[(size_t)(PFX ? 0 : b) * pk.maxb + (key >> pk.log2BS)];
           const size_t off = (((size_t)blk * Hkv + kvh) * pk.BS + (key & (pk.BS - 1))) * D + ch * 8;
           rk[i] = *reinterpret_cast<const uint4*>(pk.k + off);
           rv[i] = *reinterpret_cast<const uint4*>(pk.v + off);
