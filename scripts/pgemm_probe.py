@@ -5,6 +5,7 @@ rounds in one process (cdna_hip_programming.md §5.4 rule 24), uniform random op
 Usage: python scripts/pgemm_probe.py [M ...]   -> one JSON line per (M, projection)
 """
 import json
+import os
 import statistics
 import sys
 
@@ -17,7 +18,9 @@ from docqa_amd import ops  # noqa: E402
 PROJ = {  # name: (N, K, epi) for Llama-3-8B (TP=1) and 70B at TP=8
     "qkv": (6144, 4096, 0), "o": (4096, 4096, 0), "gate_up": (28672, 4096, 1), "down": (4096, 14336, 0),
     "70b_qkv": (1280, 8192, 0), "70b_o": (8192, 1024, 0), "70b_gate_up": (7168, 8192, 1), "70b_down": (8192, 3584, 0),
+    "lm_head": (128256, 4096, 0),
 }
+ONLY = [p for p in os.environ.get("PROBE_PROJ", "").split(",") if p]   # default: all but lm_head
 
 
 def timeit(fn, reps=10):
@@ -37,6 +40,8 @@ def main():
     Ms = [int(a) for a in sys.argv[1:]] or [16384, 4096, 1024]
     for M in Ms:
         for name, (N, K, epi) in PROJ.items():
+            if (ONLY and name not in ONLY) or (not ONLY and name == "lm_head"):
+                continue
             x = (torch.rand(M, K, device="cuda") * 2 - 1).to(torch.bfloat16)
             w = ((torch.rand(N, K, device="cuda") * 2 - 1) / K ** 0.5).to(torch.bfloat16)
             if epi:
