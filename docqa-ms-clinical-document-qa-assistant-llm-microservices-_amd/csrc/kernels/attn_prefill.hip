@@ -71,8 +71,11 @@ struct PagedKV {
 // (blockIdx.y) of the prompt prefix they all share, read through the shared block table
 // (row 0 of pk.block_tables), no causal mask; the epilogue writes the un-normalised
 // accumulator and (max, sum) of the chunk instead of normalised bf16 rows.
+// G = 4, WPH = 1 (32-row tiles, 4 waves): at most 256 VGPRs so that two workgroups share a
+// CU and one's prologue (Q, block ids, first K/V tile: three dependent round trips) runs
+// under the other's main loop -- unbounded, hipcc spends ~300 and keeps one per CU
 template <int D, bool CAUSAL, bool PAGED, int G, int WPH, bool PFX = false>
-__global__ __launch_bounds__(64 * G * WPH) void flash_prefill_kernel(
+__global__ __launch_bounds__(64 * G * WPH, (G == 4 && WPH == 1) ? 2 : 1) void flash_prefill_kernel(
     const uint16_t* __restrict__ qkv, int row_stride, const int* __restrict__ cu_seqlens,
     uint16_t* __restrict__ out, int o_stride, int Hq, int Hkv, float scale, PagedKV pk,
     CascadeOut co) {
@@ -374,13 +377,25 @@ static void launch_prefill(dim3 grid, hipStream_t s, int causal, const void* qkv
   }
 }
 
-// G = 4 query heads per KV head (Llama-3 GQA): one workgroup per (64 query rows, KV head)
-// with 8 waves; otherwise one workgroup per (128 rows, query head) with 4 waves
+// G = 4 query heads per KV head (Llama-3 GQA): one workgroup per (32 query rows, KV head)
+// with 4 waves (DOCQA_PREFILL_WPH=2: 64 rows, 8 waves); otherwise one workgroup per (128
+// rows, query head) with 4 waves
 static int prefill_dispatch(hipStream_t s, int B, int max_len, int head_dim, int causal, const void* qkv,
                             int row_stride, const int* cu, void* out, int o_stride, int Hq, int Hkv,
                             float scale, const PagedKV& pk) {
   const bool gqa4 = head_dim == 128 && Hq == 4 * Hkv;
-  if (gqa4) {
+  // waves per query head: 1 (default; 32-row tiles, 4 waves, two workgroups per CU) or 2
+  // (64-row tiles, 8 waves, one per CU).  RAG shapes: 443 -> 401 us on the bench mix, 134 ->
+  // 84 us at 16 new tokens per prompt, bench prefill 428.7 -> 423.0 ms per batch
+  // (profiles/r5_prefill_attn_wph_ab.log)
+  static const int wph = [] {
+    const char* e = getenv("DOCQA_PREFILL_WPH");
+    return e && atoi(e) == 2 ? 2 : 1;
+  }();
+  if (gqa4 && wph == 1) {
+    dim3 grid(Hkv, B, (max_len + 31) / 32);
+    launch_prefill<128, 4, 1>(grid, s, causal, qkv, row_stride, cu, out, o_stride, Hq, Hkv, scale, pk);
+  } else if (gqa4) {
     dim3 grid(Hkv, B, (max_len + 63) / 64);
     launch_prefill<128, 4, 2>(grid, s, causal, qkv, row_stride, cu, out, o_stride, Hq, Hkv, scale, pk);
   } else {

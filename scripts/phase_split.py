@@ -3,7 +3,8 @@ batch, the wall span and the kernel-busy time of its prefill (first prefill GEMM
 first decode attention launch) and of its decode loop, and the GPU gap between batches.
 Kernel-busy < wall inside a phase means the GPU waited on the host there.
 
-Usage: python scripts/phase_split.py <run_kernel_trace.csv> [--last N]
+Usage: python scripts/phase_split.py <run_kernel_trace.csv> [--last N] [--kernels]
+(--kernels: per-kernel calls / busy ms / share inside the last batch's prefill phase)
 """
 import argparse
 import csv
@@ -21,6 +22,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("trace")
     ap.add_argument("--last", type=int, default=4)
+    ap.add_argument("--kernels", action="store_true")
     a = ap.parse_args()
     rows = []
     with open(a.trace) as f:
@@ -36,7 +38,7 @@ def main():
             seen_decode = False
         elif k == "D":
             seen_decode = True
-    out = []
+    out, pres = [], []
     for bi, si in enumerate(starts):
         ei = starts[bi + 1] if bi + 1 < len(starts) else len(rows)
         seg = rows[si:ei]
@@ -47,6 +49,7 @@ def main():
         # preamble; decode = the rest up to the last decode-kind kernel
         dl = max(j for j, r in enumerate(seg) if kind(r[2]) == "D")
         pre, dec = seg[:d0], seg[d0:dl + 1]
+        pres.append(pre)
 
         def busy(xs):
             return sum(e - s for s, e, _ in xs) / 1e6
@@ -59,6 +62,19 @@ def main():
                     "decode_kernels": len(dec), "gap_to_next_batch_ms": None if gap is None else round(gap, 2)})
     for o in out[-a.last:]:
         print(o)
+    # the longest prefill phase among the last N batches (a pipelined batch's prefill can be
+    # queued behind the previous decode, which splits a short preamble off as its own phase)
+    last_pre = max(pres[-a.last:], key=lambda p: sum(e - s for s, e, _ in p)) if pres else None
+    if a.kernels and last_pre:
+        tot = sum(e - s for s, e, _ in last_pre)
+        agg = {}
+        for s, e, n in last_pre:
+            c = agg.setdefault(n[:120], [0, 0])
+            c[0] += 1
+            c[1] += e - s
+        print(f"# longest recent prefill phase: {len(last_pre)} kernels, busy {tot / 1e6:.2f} ms")
+        for n, (c, t) in sorted(agg.items(), key=lambda kv: -kv[1][1]):
+            print(f"{t / 1e6:9.2f} ms {c:6d} {100 * t / tot:5.1f}%  {n}")
 
 
 if __name__ == "__main__":
