@@ -316,6 +316,8 @@ class LlamaModel:
         if (decode or small) and self.layers:
             L0 = self.layers[0]
             for k in ("qkv", "o", "down"):
+                if small and ops.lib_route(M, *L0[k].shape):
+                    continue          # prefill_linear takes hipBLASLt for this shape
                 S, c = ops.mid_plan(M, *L0[k].shape)
                 if S:
                     plans[k] = (S, lambda a, w, S=S, c=c: (ops.mgemm_partial(a, w, S, c) if S > 1
@@ -328,10 +330,10 @@ class LlamaModel:
                 # 75.7 vs 102.6 us at 512 rows with the add+norm consumer
                 # (profiles/r4_prefill_mid_probe.log); decode buckets keep their plan
                 N, K = L0["down"].shape
-                if ops.mid_plan(M, N, K)[0] and (K // 128) % 4 == 0 and N % 128 == 0:
+                if ops.mid_plan(M, N, K)[0] and (K // 128) % 4 == 0 and N % 128 == 0 and not ops.lib_route(M, N, K):
                     plans["down"] = (4, lambda a, w: ops.mgemm_partial(a, w, 4, 2))
             Sg, cg = ops.mid_plan(M, *L0["gate_up"].shape, glu=True)
-            if small and ops.pgemm_ok(M, *L0["gate_up"].shape):
+            if small and (ops.pgemm_ok(M, *L0["gate_up"].shape) or ops.lib_route(M, *L0["gate_up"].shape, glu=True)):
                 glu = ops.prefill_glu     # 256 x 256 tiles with SwiGLU: 104 vs 141 us at M = 512
             else:
                 glu = (lambda a, w: ops.mgemm_glu(a, w, cg)) if Sg else ops.glu_linear

@@ -325,6 +325,28 @@ def pgemm_ok(M: int, N: int, K: int) -> bool:
 
 
 PREFILL_MID_MAX = 2048
+_LIB_ROUTES_ON = os.environ.get("DOCQA_LIB_ROUTES", "1") != "0"
+# Prefill projection shapes where hipBLASLt beats what the hand-written path runs there
+# (the plain-GEMM library path, plus a silu_mul launch for gate|up): (N, K, glu) -> row
+# ranges.  Measured per route, split-K plans counted by their slabs alone
+# (scripts/pgemm_mid_probe.py "routed" column; profiles/r5_prefill_lib_routes.log): the 70B
+# TP-8 gate|up / down shards at <= 768 rows (0.71x / 0.82x before), and the 8B projections
+# at the mid sizes where the 256-row tiles leave the chip half idle -- QKV 513..1024 (0.77x
+# / 0.85x), O 513..768 and 1025..1536 (0.89x / 0.83x), gate|up 513..768 (0.89x), down
+# 513..768 and 1025..2048 (0.89x / 0.88x).
+_LIB_ROUTES = {
+    (7168, 8192, True): ((1, 768),), (8192, 3584, False): ((1, 768),),
+    (6144, 4096, False): ((513, 1024),), (4096, 4096, False): ((513, 768), (1025, 1536)),
+    (28672, 4096, True): ((513, 768),), (4096, 14336, False): ((513, 768), (1025, 2048)),
+}
+
+
+def lib_route(M: int, N: int, K: int, glu: bool = False) -> bool:
+    """True when a prefill projection of M rows should take hipBLASLt (measured table
+    above; DOCQA_LIB_ROUTES=0 disables)."""
+    ranges = _LIB_ROUTES.get((int(N), int(K), bool(glu)), ())
+    return _LIB_ROUTES_ON and any(lo <= M <= hi for lo, hi in ranges)
+
 _PREFILL_PLANS = os.environ.get("DOCQA_PREFILL_PLANS", "1") != "0"
 
 
@@ -337,6 +359,8 @@ def prefill_plan(M: int, N: int, K: int) -> tuple[int, int]:
     replaces 71.2 / 83.0), O S=2 42.3 / 47.9 (40.8 / 48.7), down S=2 111.8 / 131.8
     (116.5 / 145.3); 1025..2048 rows: O and down S=1, QKV the 256 x 256 kernel."""
     if not _PREFILL_PLANS or _MID_OFF or not (MID_M_MAX < M <= PREFILL_MID_MAX) or N % 128 or K % 128:
+        return 0, 0
+    if lib_route(M, N, K):
         return 0, 0
     if N < 4096:
         # narrow N (the 70B TP-8 QKV shard, N 1280 x K 8192): the mid-M kernel's few 128-wide
@@ -357,7 +381,7 @@ def prefill_split_plan(M: int, N: int, K: int) -> int:
     KV write, (TP all-reduce +) add + RMSNorm).  0: no split (enough tiles, or not a pgemm
     shape).  DOCQA_PREFILL_SPLIT=0 disables."""
     if (not _PREFILL_SPLIT or _PGEMM_OFF or N >= 4096 or M <= 0 or N % 256 or K % 256
-            or max(M, N) * K * 2 >= (1 << 32)):
+            or max(M, N) * K * 2 >= (1 << 32) or lib_route(M, N, K)):
         return 0
     tiles = ((M + 255) // 256) * (N // 256)
     S = 1
@@ -378,6 +402,8 @@ def prefill_linear(x, w):
     if _gpu(x):
         N, K = w.shape
         M = x.numel() // K
+        if lib_route(M, N, K):
+            return torch.nn.functional.linear(x, w)
         S, cfg = prefill_plan(M, N, K)
         if S == 1:
             return _native().mgemm(x.contiguous(), w, 1, cfg)
@@ -386,6 +412,38 @@ def prefill_linear(x, w):
         if N % 128 == 0 and K % 64 == 0:
             return _native().gemm(x.contiguous(), w, None, None, EPI_NONE)
     return torch.nn.functional.linear(x, w)
+
+
+def prefill_route(M: int, N: int, K: int, glu: bool = False, down: bool = False):
+    """(label, fn(x, w)) of what a prefill projection of M rows runs in models/llama.py
+    (its per-forward plan logic, mirrored here for probes): split-K slab plans return the
+    fp32 slabs [S, M, N] their consumer sums; ``down``: the 257..512-row down override."""
+    nat = _native
+    if glu:
+        if M <= MID_M_MAX and not (pgemm_ok(M, N, K) or lib_route(M, N, K, glu=True)):
+            Sg, cg = mid_plan(M, N, K, glu=True)
+            if Sg:
+                return f"mgemm_glu c{cg}", lambda x, w: nat().mgemm_glu(x.contiguous(), w, cg)
+            return "glu_linear", glu_linear
+        return ("hipblaslt+silu" if lib_route(M, N, K, glu=True) else "prefill_glu"), prefill_glu
+    if lib_route(M, N, K):
+        return "hipblaslt", lambda x, w: torch.nn.functional.linear(x, w)
+    if M <= MID_M_MAX:
+        if down and M > 256 and mid_plan(M, N, K)[0] and (K // 128) % 4 == 0 and N % 128 == 0:
+            return "mgemm S4 c2", lambda x, w: nat().mgemm(x.contiguous(), w, 4, 2)
+        S, c = mid_plan(M, N, K)
+        if S:
+            return f"mgemm S{S} c{c}", lambda x, w: nat().mgemm(x.contiguous(), w, S, c)
+        S, t = decode_plan(M, N, K)
+        return f"dgemm S{S} t{t}", lambda x, w: dgemm_partial(x, w, S, t)
+    S, c = prefill_plan(M, N, K)
+    if S >= 2:
+        return f"mgemm S{S} c{c}", lambda x, w: nat().mgemm(x.contiguous(), w, S, c)
+    if not S:
+        Sp = prefill_split_plan(M, N, K)
+        if Sp:
+            return f"pgemm S{Sp}", lambda x, w: nat().pgemm_partial(x.contiguous(), w, Sp)
+    return "prefill_linear", prefill_linear
 
 
 _GLU128 = os.environ.get("DOCQA_GLU128", "1") != "0"
@@ -397,6 +455,8 @@ def prefill_glu(x, w_il):
     if _gpu(x):
         N, K = w_il.shape
         M = x.numel() // K
+        if lib_route(M, N, K, glu=True):
+            return silu_mul(torch.nn.functional.linear(x, w_il), interleaved=True)
         if pgemm_ok(M, N, K):
             return _native().pgemm(x.contiguous(), w_il, 1)
         if (_GLU128 and N % 128 == 0 and K % 64 == 0 and ((M + 255) // 256) * (N // 128) < 128

@@ -6,6 +6,10 @@ of interleaved rounds:
   mgemm_c -- 256-row m-tiles x (128 | 256 | 64)-row weight tiles, K unsplit (mgemm.hip cfg c)
   pgS     -- pgemm split-K slabs (pgemm_partial, S = 2) + the fp32 slab sum (what a fused
              split-K consumer would pay)
+  routed  -- what the prefill forward runs for the projection (ops.prefill_route, the plan
+             logic of models/llama.py: split-K plans timed as their slabs alone, since the
+             RoPE / add+RMSNorm consumer that sums them runs either way; hipBLASLt on the
+             measured library routes, ops.lib_route); "route" names it
 Usage: python scripts/pgemm_mid_probe.py [M ...]   -> one JSON line per (M, projection)"""
 import json
 import os
@@ -48,6 +52,8 @@ def main():
             x = (torch.rand(M, K, device="cuda") * 2 - 1).to(torch.bfloat16)
             w = ((torch.rand(N, K, device="cuda") * 2 - 1) / K ** 0.5).to(torch.bfloat16)
             c = {}
+            route, rfn = ops.prefill_route(M, N, K, glu=bool(epi), down=name.endswith("down"))
+            c["routed"] = lambda: rfn(x, w)
             if epi:
                 c["hipblaslt"] = lambda: ops.silu_mul(F.linear(x, w), interleaved=True)
                 if N % 256 == 0:
@@ -74,7 +80,7 @@ def main():
             for k, fn in c.items():
                 try:
                     y = fn().float()
-                    if k.endswith("_only"):
+                    if k.endswith("_only") or (k == "routed" and y.dim() == 3):
                         y = y.sum(0)
                     errs[k] = round((y - r).abs().max().item() / max(1e-6, r.abs().max().item()), 5)
                 except Exception as e:  # noqa: BLE001 -- a shape a candidate does not take
@@ -89,9 +95,13 @@ def main():
                 med = statistics.median(v)
                 out[k + "_us"] = round(med, 1)
                 out[k + "_TF"] = round(flops / med / 1e6, 1)
-            best = min((k for k in t if k != "hipblaslt" and not k.endswith("_only")), key=lambda k: out[k + "_us"])
+            hand = [k for k in t if k not in ("hipblaslt", "routed") and not k.endswith("_only")]
+            best = min(hand, key=lambda k: out[k + "_us"])
             out["best"] = best
             out["best_vs_lib"] = round(out["hipblaslt_us"] / out[best + "_us"], 3)
+            out["route"] = route
+            if "routed" in t:
+                out["routed_vs_lib"] = round(out["hipblaslt_us"] / out["routed_us"], 3)
             out["errs"] = errs
             print(json.dumps(out), flush=True)
             del x, w, r

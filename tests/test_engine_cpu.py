@@ -432,6 +432,29 @@ def test_mid_plan_glu_never_picks_narrow_tiles():
         assert S2 >= 1 or cfg2 == 0
 
 
+def test_prefill_library_routes():
+    """Measured library routes (ops._LIB_ROUTES): listed (shape, row range) pairs take
+    hipBLASLt, get no split-K plan that would bypass the route, and prefill_route names the
+    library for them; the headline's large prefills (> 2048 rows) and decode stay hand-written."""
+    from docqa_amd import ops
+
+    assert ops.lib_route(512, 7168, 8192, glu=True) and ops.lib_route(768, 7168, 8192, glu=True)
+    assert not ops.lib_route(1024, 7168, 8192, glu=True)
+    assert not ops.lib_route(512, 7168, 8192)                 # same shape, no SwiGLU: not measured
+    assert ops.lib_route(600, 8192, 3584) and not ops.lib_route(1024, 8192, 3584)
+    assert ops.lib_route(1536, 4096, 14336) and not ops.lib_route(1024, 4096, 14336)
+    assert ops.lib_route(700, 4096, 4096) and not ops.lib_route(1024, 4096, 4096) and ops.lib_route(1200, 4096, 4096)
+    assert not ops.lib_route(512, 6144, 4096) and ops.lib_route(1024, 6144, 4096)
+    for N, K, glu in [(6144, 4096, False), (4096, 4096, False), (28672, 4096, True), (4096, 14336, False)]:
+        assert not ops.lib_route(4096, N, K, glu) and not ops.lib_route(256, N, K, glu)
+    assert ops.prefill_plan(600, 8192, 3584) == (0, 0) and ops.prefill_plan(1536, 4096, 14336) == (0, 0)
+    assert ops.prefill_plan(1024, 4096, 14336) != (0, 0)
+    assert ops.prefill_split_plan(600, 8192, 3584) == 0
+    assert ops.prefill_route(600, 8192, 3584)[0] == "hipblaslt"
+    assert ops.prefill_route(600, 7168, 8192, glu=True)[0] == "hipblaslt+silu"
+    assert ops.prefill_route(4096, 4096, 14336)[0] == "prefill_linear"
+
+
 def test_reserve_rolls_back_without_prefix_cache():
     """a batch that does not fit frees what it had reserved (prefix cache off)."""
     m = _model()
