@@ -392,7 +392,18 @@ static int prefill_dispatch(hipStream_t s, int B, int max_len, int head_dim, int
     const char* e = getenv("DOCQA_PREFILL_WPH");
     return e && atoi(e) == 2 ? 2 : 1;
   }();
-  if (gqa4 && wph == 1) {
+  // G = 8 (Llama-3-70B: 64 query heads over 8 KV heads; its TP-8 shard: 8 over 1): one
+  // 8-wave workgroup per (32 rows, KV head), every K/V tile staged once for all 8 heads --
+  // the per-query-head path below re-streamed each tile 8 times
+  static const bool gqa8_on = [] {
+    const char* e = getenv("DOCQA_PREFILL_GQA8");
+    return !(e && atoi(e) == 0);
+  }();
+  const bool gqa8 = gqa8_on && head_dim == 128 && Hq == 8 * Hkv;
+  if (gqa8) {
+    dim3 grid(Hkv, B, (max_len + 31) / 32);
+    launch_prefill<128, 8, 1>(grid, s, causal, qkv, row_stride, cu, out, o_stride, Hq, Hkv, scale, pk);
+  } else if (gqa4 && wph == 1) {
     dim3 grid(Hkv, B, (max_len + 31) / 32);
     launch_prefill<128, 4, 1>(grid, s, causal, qkv, row_stride, cu, out, o_stride, Hq, Hkv, scale, pk);
   } else if (gqa4) {

@@ -2,6 +2,7 @@
 contiguous kernel, to locate the prefill-attention cost seen in the bench profile."""
 import json
 import math
+import os
 import sys
 from pathlib import Path
 
@@ -15,7 +16,9 @@ from docqa_amd import ops
 def main():
     assert ops.load_native()
     nat = torch.ops.docqa
-    Hq, Hkv, D, BS = 32, 8, 128, 64
+    # PROBE_HEADS=64,8: the Llama-3-70B head layout (8 query heads per KV head)
+    Hq, Hkv = (int(v) for v in os.environ.get("PROBE_HEADS", "32,8").split(","))
+    D, BS = 128, 64
     scale = 1 / math.sqrt(D)
     for B, new, pre in [(128, 130, 448), (128, 130, 0), (64, 130, 448), (16, 600, 0), (128, 16, 448)]:
         W = (Hq + 2 * Hkv) * D

@@ -264,6 +264,32 @@ def test_flash_prefill(native, D, causal):
     _close(o1, o2, 3e-2, 1e-2)
 
 
+@pytest.mark.parametrize("Hq,Hkv", [(16, 2), (8, 1)])
+@pytest.mark.parametrize("causal", [True, False])
+def test_flash_prefill_gqa8(native, Hq, Hkv, causal):
+    """8 query heads per KV head (Llama-3-70B and its TP-8 shard): one 8-wave workgroup per
+    (32 rows, KV head) sharing every K/V tile -- plain and prefix-cached (paged) prefill."""
+    from docqa_amd.ops import reference as R
+
+    D, BS = 128, 64
+    lens = [1, 130, 257, 64, 500]
+    cu = torch.tensor([0] + list(torch.tensor(lens).cumsum(0)), device="cuda", dtype=torch.int32)
+    qkv = torch.randn(sum(lens), (Hq + 2 * Hkv) * D, device="cuda", dtype=torch.bfloat16)
+    scale = 1 / math.sqrt(D)
+    o1 = native.flash_prefill(qkv, cu, max(lens), Hq, Hkv, D, scale, causal)
+    o2 = R.flash_prefill(qkv, cu, max(lens), Hq, Hkv, D, scale, causal)
+    _close(o1, o2, 3e-2, 1e-2)
+    if causal:
+        B, maxb = len(lens), 16
+        kc = torch.randn(B * maxb, Hkv, BS, D, device="cuda", dtype=torch.bfloat16)
+        vc = torch.randn_like(kc)
+        bt = torch.randperm(B * maxb, device="cuda").int().view(B, maxb)
+        cs = torch.tensor([0, 64, 320, 128, 448], device="cuda", dtype=torch.int32)
+        o1 = native.flash_prefill_paged(qkv, cu, max(lens), Hq, Hkv, D, scale, kc, vc, bt, cs)
+        o2 = R.flash_prefill_paged(qkv, cu, max(lens), Hq, Hkv, D, scale, kc, vc, bt, cs)
+        _close(o1, o2, 3e-2, 1e-2)
+
+
 @pytest.mark.parametrize("prefix", [[0, 64, 128, 320], [256, 0, 64, 1000]])
 def test_flash_prefill_paged(native, prefix):
     """Prefix-cached prefill: keys = cached prefix + new tokens, read via block tables."""
