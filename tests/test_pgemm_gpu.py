@@ -109,3 +109,24 @@ def test_prefill_split_plan_slabs_feed_the_consumers():
     P = ops.pgemm_partial(x, w, S)
     r = x.float() @ w.float().t()
     assert (P.sum(0) - r).abs().max().item() <= 2e-3 * r.abs().max().item() + 1e-3
+
+
+@pytest.mark.parametrize("M,N,K,glu", [(512, 7168, 8192, True), (600, 8192, 3584, False), (768, 6144, 4096, False),
+                                       (1200, 4096, 4096, False), (1024, 4096, 14336, False), (512, 1280, 8192, False),
+                                       (300, 4096, 14336, False), (2048, 7168, 8192, True), (700, 28672, 4096, True)])
+def test_prefill_route_products(M, N, K, glu):
+    """Every route the prefill forward can take (ops.prefill_route: hand-written tiles, split-K
+    slabs, the measured hipBLASLt routes) computes the projection: fp32 slabs summed, bf16
+    products and SwiGLU outputs against the fp32 reference."""
+    x, w = _data(M, N, K, seed=3)
+    label, fn = ops.prefill_route(M, N, K, glu=glu, down=(K == 14336 or K == 3584))
+    y = fn(x, w)
+    if y.dim() == 3:
+        y = y.sum(0)
+    r = x.float() @ w.float().t()
+    if glu:
+        r = ref.silu_mul(r.bfloat16(), interleaved=True).float()
+    err = (y.float() - r).abs().max().item() / max(1e-6, r.abs().max().item())
+    assert y.shape == r.shape, label
+    assert err < 2e-2, (label, err)
+    assert ops.lib_route(M, N, K, glu) == label.startswith("hipblaslt")
