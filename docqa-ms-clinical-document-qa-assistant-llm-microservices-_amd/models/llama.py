@@ -312,6 +312,8 @@ class LlamaModel:
         # a short prefill (<= ops.MID_M_MAX prompt tokens: batch-1 serving) has the decode
         # step's shape -- too few rows for the 256 x 256 prefill GEMM's tiles -- so it takes
         # the same split-K projection plans and fused consumers (RoPE + KV write, add + norm)
+        # (ops.prefill_route mirrors the prefill plan choices below for the GEMM probes and
+        # tests/test_pgemm_gpu.py::test_prefill_route_products -- keep the two in step)
         small = (not decode and x.is_cuda and _PREFILL_MID and M <= ops.MID_M_MAX)
         if (decode or small) and self.layers:
             L0 = self.layers[0]
