@@ -134,18 +134,21 @@ class Settings:
             return "cpu"
 
 
-def _default_max_batch() -> int:
+def default_max_batch(device: str | None = None) -> int:
+    """MAX_BATCH, else by device: 256 decode slots on a GPU, 64 on the CPU.  ``device``:
+    the device the engine will run on (``StackOptions.device``); None reads DOCQA_DEVICE,
+    and ``auto`` looks for the GPU driver node WITHOUT initialising the HIP runtime (a
+    settings read in a CPU-only service process must not start it -- ADVICE r5)."""
     if os.environ.get("MAX_BATCH"):
         return env_int("MAX_BATCH", 256)
-    dev = os.environ.get("DOCQA_DEVICE", "auto")
+    dev = device if device is not None else os.environ.get("DOCQA_DEVICE", "auto")
     if dev == "auto":
-        try:
-            import torch
+        dev = "cuda" if os.path.exists("/dev/kfd") else "cpu"
+    return 256 if str(dev).startswith("cuda") else 64
 
-            dev = "cuda" if torch.cuda.is_available() else "cpu"
-        except Exception:  # noqa: BLE001
-            dev = "cpu"
-    return 256 if dev.startswith("cuda") else 64
+
+def _default_max_batch() -> int:
+    return default_max_batch()
 
 
 def settings() -> Settings:

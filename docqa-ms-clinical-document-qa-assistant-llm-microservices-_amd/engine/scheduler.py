@@ -136,6 +136,7 @@ class ContinuousEngine:
         self._free_t = None                # when a slot last became free with the batch full before
         self._pool = None
         self._pending = None               # (event, pinned host tokens, slot -> request) of the last step
+        self._processing = None            # the readback being processed (see _process)
         self._host = None
         self._flip = 0
         self._mhost = None   # mixed steps' pinned token buffers (decode rows + first tokens)
@@ -264,10 +265,18 @@ class ContinuousEngine:
                 pass
 
     def _fail_all(self, e: Exception) -> None:
-        lagged = list(self._pending[4]) if self._pending is not None and isinstance(self._pending[0], str) else []
-        self._pending = None
+        lagged = []
+        for p in (self._pending, self._processing):
+            if p is not None and isinstance(p[0], str):
+                lagged += list(p[4])         # a mixed step's completing prompts
+        self._pending = self._processing = None
+        seen = set()
         for r in self.running + self.prefilling + lagged:
+            if id(r) in seen:                # a completing prompt already placed in a slot
+                continue
+            seen.add(id(r))
             self.eng.kv.allocator.free(r.blocks)
+            r.blocks = []
             if not r.future.done():
                 r.future.set_exception(e)
         self.running = []
@@ -365,7 +374,9 @@ class ContinuousEngine:
                     # prefix-cache hits (whole blocks + token-granular rows), fresh blocks
                     res = eng.reserve([r.prompt], r.params, gen_tokens=gen)
                 except MemoryError:
-                    if not self.running and not admitted:   # can never fit: fail, don't stall
+                    # can never fit: nothing else holds KV (running rows, prompts being
+                    # chunk-prefilled, lagged completions) to free -- fail, don't stall
+                    if self._occupied() == 0 and not admitted:
                         need = eng.kv.blocks_for(len(r.prompt) + gen)
                         self.waiting.popleft().future.set_exception(MemoryError(
                             f"request needs {need} KV blocks, the cache has {alloc.num_free()} free"))
@@ -508,6 +519,11 @@ class ContinuousEngine:
                 self._process(p)
             return
         self._grow_tables()
+        if not self.prefilling:
+            # KV pressure re-queued every prefilling prompt (_preempt_youngest): a plain step
+            if self.running:
+                self._decode()
+            return
         t0 = time.perf_counter()
         pieces, budget = [], self.chunk_tokens
         for r in self.prefilling:
@@ -718,6 +734,19 @@ class ContinuousEngine:
         if self._pending is not None:       # every issued step's tokens reach the host first
             p, self._pending = self._pending, None
             self._process(p)
+        if self.prefilling:
+            # mixed steps: prompts being chunk-prefilled hold their whole prompt's blocks and
+            # have produced no token yet -- re-queue the latest of them first (the
+            # last running row used to fail while prefilling prompts held the blocks it needed)
+            v = max(self.prefilling, key=lambda r: (r.t_arrival, r.rid))
+            self.eng.kv.allocator.free(v.blocks)
+            v.blocks, v.res, v.cached, v.filled = [], None, 0, 0
+            self.prefilling = [r for r in self.prefilling if r is not v]
+            v.preemptions += 1
+            self.preempted += 1
+            with self._cv:
+                self.waiting.appendleft(v)
+            return
         if not self.running:
             return
         v = max(self.running, key=lambda r: (r.t_arrival, r.rid))   # the latest arrival
@@ -795,6 +824,15 @@ class ContinuousEngine:
         eng.stats.decode_s += time.perf_counter() - t0
 
     def _process(self, pending) -> None:
+        # a readback taken out of ``_pending`` stays reachable while it is processed: if it
+        # raises (a collective-error snapshot, register_prefixes, _place), _fail_all still
+        # frees the KV blocks and resolves the futures of a mixed step's completing prompts,
+        # which are in neither ``running`` nor ``prefilling`` yet
+        self._processing = pending
+        self._process_one(pending)
+        self._processing = None
+
+    def _process_one(self, pending) -> None:
         if isinstance(pending[0], str):      # ("mixed", ...): a mixed step's readback
             self._process_mixed(pending)
             return

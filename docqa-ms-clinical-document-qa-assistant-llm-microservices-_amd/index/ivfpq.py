@@ -107,6 +107,9 @@ class IVFPQIndex:
 
     def train(self, x, niter: int = 20, seed: int = 0) -> None:
         x = torch.as_tensor(x).to(self.device, torch.float32)
+        # stored ||c + r^||^2 belong to the old quantizers: rebuilt from the codes on the next
+        # precomputed-table search (they were rebuilt only on a row-count change)
+        self.norms = None
         if self.rotation == "pca":
             self.rot = pca_rotation(x, self.M).to(self.device)
             x = x @ self.rot

@@ -29,6 +29,8 @@ semantic-indexer/indexer.py:17-18); this is the config-5 "index sharded across 8
 """
 from __future__ import annotations
 
+import threading
+
 import torch
 import torch.distributed as dist
 
@@ -58,26 +60,76 @@ class ShardedIndex:
         self._offset = 0
         self._ntotal = local.ntotal
         self._ipc = None
-        self._snap = None          # error-word snapshot of the last IPC search
+        # per-thread search state: the error-word snapshot of this thread's last IPC search
+        # (a serving front end searches from its prep thread while the indexer searches from
+        # request threads; one instance-wide slot let one thread's search overwrite
+        # another's snapshot before it was checked -- ADVICE r5)
+        self._tls = threading.local()
         self.refresh()
 
-    def enable_ipc(self, max_bytes: int = 16 << 20) -> bool:
+    def enable_ipc(self, max_bytes: int = 16 << 20, factory=None) -> bool:
         """Route the per-batch all-gathers through the IPC peer-memory kernel (collective:
-        every rank of the group calls it; all fall back to RCCL together on failure)."""
+        every rank of the group calls it; all fall back to RCCL together if the kernel cannot
+        be set up).  Once set up, a handshake gather (:meth:`_handshake`) must return every
+        peer's row exactly, else the run fails with :class:`CollectiveError` before the
+        first search.  ``factory``: the gather's constructor (tests)."""
         if self.world == 1 or self._ipc is not None or self.local.device.type != "cuda":
             return self._ipc is not None
-        from ..parallel.custom_ar import CustomAllReduce
-
         import os
+
+        if factory is None:
+            from ..parallel.custom_ar import CustomAllReduce as factory
 
         timeout_ms = float(os.environ.get("DOCQA_SHARD_GATHER_TIMEOUT_MS", "60000"))
         try:
-            self._ipc = CustomAllReduce(group=self.group, max_bytes=max_bytes, device=self.local.device,
-                                        timeout_ms=timeout_ms)
+            self._ipc = factory(group=self.group, max_bytes=max_bytes, device=self.local.device,
+                                timeout_ms=timeout_ms)
         except Exception as e:  # noqa: BLE001 - collective decision inside the constructor
             print(f"[sharded] IPC all-gather unavailable ({e}); using the process group", flush=True)
             self._ipc = None
+        if self._ipc is not None:
+            self._handshake()
         return self._ipc is not None
+
+    def _handshake(self) -> None:
+        """One gather through the IPC path of a row every rank can predict for every peer --
+        (rank, world, shard offset, shard size, magic) -- checked word for word: a peer
+        mapping that reads the wrong buffer, a stale staging row or a rank that never
+        arrives fails the run here (all ranks agree on the outcome over the process group),
+        not as silently wrong top-k later.  The offsets / sizes come from :meth:`refresh`'s
+        process-group exchange, independent of the IPC path.  Reference: the k = 3 retrieval
+        of llm-qa/main.py:101, which must not silently change."""
+        from ..parallel.custom_ar import CollectiveError, _agree
+
+        magic = 0x5D0C0A11
+        sizes = self._shard_sizes()
+        offs = [sum(sizes[:r]) for r in range(self.world)]
+
+        def row(r: int) -> list[int]:
+            return [r, self.world, offs[r], sizes[r], magic, r ^ magic, 0, 0]
+
+        dev = getattr(self._ipc, "device", self.local.device)
+        mine = torch.tensor(row(self.rank), dtype=torch.int32, device=dev)
+        got = self._ipc.all_gather_raw(mine).view(self.world, -1).cpu()
+        want = torch.tensor([row(r) for r in range(self.world)], dtype=torch.int32)
+        ok = bool(torch.equal(got, want))
+        try:
+            self._ipc.check()
+        except Exception:  # noqa: BLE001 - a peer that never arrived
+            ok = False
+        if dist.is_initialized():
+            ok = _agree(ok, self.group, dev)
+        if not ok:
+            bad = [r for r in range(self.world) if not torch.equal(got[r], want[r])]
+            raise CollectiveError(f"sharded index: IPC handshake gather returned wrong peer rows "
+                                  f"{bad or '(on another rank)'}; refusing to serve sharded retrieval")
+
+    def _shard_sizes(self) -> list[int]:
+        """Every rank's shard size (the counts :meth:`refresh` exchanged)."""
+        sizes = getattr(self, "_sizes", None)
+        if sizes is None or len(sizes) != self.world:
+            raise RuntimeError("shard sizes unknown: call refresh() first")
+        return list(sizes)
 
     def _all_gather(self, t: torch.Tensor) -> torch.Tensor:
         """[world, *t.shape] -- IPC peer-memory gather when enabled, else the process group."""
@@ -85,7 +137,7 @@ class ShardedIndex:
         if self._ipc is not None and t.is_cuda:
             nb = t.numel() * t.element_size()
             if nb % 16 == 0 and nb // 2 <= self._ipc.max_elems:
-                self._used_ipc = True
+                self._tls.used_ipc = True
                 return self._ipc.all_gather_raw(t)
         parts = [torch.empty_like(t) for _ in range(self.world)]
         dist.all_gather(parts, t, group=self.group)
@@ -103,11 +155,13 @@ class ShardedIndex:
         """Recompute global id offsets after local adds (collective)."""
         if self.world == 1:
             self._offset, self._ntotal = 0, self.local.ntotal
+            self._sizes = [self.local.ntotal]
             return
         n = torch.tensor([self.local.ntotal], dtype=torch.long, device=self.local.device)
         parts = [torch.empty_like(n) for _ in range(self.world)]
         dist.all_gather(parts, n, group=self.group)
         counts = [int(p.item()) for p in parts]
+        self._sizes = counts
         self._offset = sum(counts[: self.rank])
         self._ntotal = sum(counts)
 
@@ -120,7 +174,8 @@ class ShardedIndex:
         arrived at the last search's IPC gathers.  Call after a host sync that covers the
         search (e.g. ``I.tolist()`` on the search's stream): the snapshot copy was queued
         behind the gathers, so it is complete by then and reading it costs nothing."""
-        snap, self._snap = self._snap, None
+        snap = getattr(self._tls, "snap", None)
+        self._tls.snap = None
         if snap is not None and self._ipc is not None:
             self._ipc.raise_if(snap)
 
@@ -128,11 +183,12 @@ class ShardedIndex:
         xq = xq.to(self.local.device, dtype=torch.float32)
         if self.world == 1:
             return self.local.search(xq, k, **kw)
-        self._used_ipc = False
+        self._tls.used_ipc = False
         D, I = self._search(xq, k, **kw)
-        if self._used_ipc:
+        if self._tls.used_ipc:
             # stream-ordered copy of the sticky error word behind this search's gathers
-            self._snap = self._ipc.snapshot()
+            # (this thread's: check_gather() of the same thread reads it)
+            self._tls.snap = self._ipc.snapshot()
         return D, I
 
     def _search(self, xq: torch.Tensor, k: int, **kw):
@@ -257,6 +313,7 @@ class ShardedIVFPQIndex(ShardedIndex):
         start = sum(offs[: obj.rank])
         ivf.add(local_x, ids=torch.arange(start, start + n, dtype=torch.long))
         obj._offset, obj._ntotal = 0, sum(offs)
+        obj._sizes = offs
         return obj
 
     def refresh(self) -> None:   # ids are global from build time

@@ -111,8 +111,13 @@ class RAGPipeline:
         return ids
 
     def retrieve(self, questions: list[str]):
+        """(D, I) of the questions' top-k.  On a sharded index the hits are checked for a
+        failed cross-rank gather here (one host sync on the search's ids) so no caller can
+        use stale peer rows unchecked."""
         q = self.embed(questions)
         D, I = self.index.search(q, self.k)
+        if getattr(self.index, "check_gather", None) is not None:
+            self._host_ids(I)
         return D, I
 
     def _piece_prompt(self, qtext: str, ids: list[int], qids: list[int] | None = None) -> list[int]:

@@ -266,8 +266,14 @@ class SemanticIndexer:
         q = self.encoder.encode(self.tok.encode_batch([query]))
         with self.lock:
             D, I = self.index.search(q, k)
+            dl, il = D[0].tolist(), I[0].tolist()
+            # a sharded index: surface a failed cross-rank gather (stale peer rows) after the
+            # host sync above instead of serving it (index/sharded.py check_gather)
+            check = getattr(self.index, "check_gather", None)
+            if check is not None:
+                check()
             out = []
-            for d, i in zip(D[0].tolist(), I[0].tolist()):
+            for d, i in zip(dl, il):
                 if 0 <= i < len(self.metadata):
                     m = self.metadata[i]
                     out.append({"id": i, "score": d, "text": m.get("text_content", ""), "source": m.get("source"),

@@ -35,7 +35,7 @@ class StackOptions:
     embed: str = "minilm-l6"
     ner: str = "clinical-bert"
     device: str = "cuda"
-    max_batch: int = field(default_factory=lambda: Settings().max_batch)   # MAX_BATCH: 256 on a GPU
+    max_batch: int | None = None     # None: MAX_BATCH, else 256 on a GPU / 64 on the CPU (this device)
     max_context: int | None = None   # None: Settings.max_context (MAX_CONTEXT, 8192) capped by the model
     use_graphs: bool = True
     # NER token classifier inside de-identification (reference: spaCy NER on every message,
@@ -47,6 +47,12 @@ class StackOptions:
     qa_replicas: tuple = ()       # llm-qa front-end over these data-parallel replica URLs
     kv_mem_fraction: float | None = 0.8   # KV pool from free HBM (GPU only; LLMEngine)
     preload_notes: int = 0        # index this many synthetic clinical notes at start (benchmarks / demos)
+
+    def __post_init__(self):
+        if self.max_batch is None:
+            from ..config import default_max_batch
+
+            self.max_batch = default_max_batch(self.device)
 
 
 class _LocalRetrieval(synthese.RetrievalClient):

@@ -36,6 +36,7 @@ def test_bench_single_process_cpu():
     assert r.returncode == 0, r.stderr[-3000:]
     d = _last_json(r.stdout)
     assert KEYS <= set(d) and d["n_gpus"] == 1 and d["value"] > 0
+    assert "retrieval_check" not in d          # one GPU: no sharded index to verify
 
 
 def test_bench_two_ranks_gloo_sharded_index():
@@ -44,7 +45,7 @@ def test_bench_two_ranks_gloo_sharded_index():
         env.pop(k, None)
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
            "--master-addr", "127.0.0.1", "--master-port", str(_port()), str(ROOT / "bench.py"),
-           "--gpus", "2", *ARGS, "--check-retrieval"]
+           "--gpus", "2", *ARGS]            # WORLD_SIZE > 1: the retrieval check runs by default
     r = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=900, env=env)
     assert r.returncode == 0, r.stderr[-3000:]
     d = _last_json(r.stdout)
@@ -62,13 +63,14 @@ def test_bench_eight_ranks_gloo_sharded_index():
     env["OMP_NUM_THREADS"] = "1"
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "8",
            "--master-addr", "127.0.0.1", "--master-port", str(_port()), str(ROOT / "bench.py"),
-           "--gpus", "8", *ARGS, "--check-retrieval"]
+           "--gpus", "8", *ARGS]            # the driver's exact command: self-verifying by default
     r = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=900, env=env)
     assert r.returncode == 0, r.stderr[-3000:]
     d = _last_json(r.stdout)
     assert d["n_gpus"] == 8 and d["config"]["global_batch"] == 24 and d["config"]["parallelism"] == "dp8"
     assert d["value"] > 0 and d["workload"]["unique_question_frac"] == 1.0
     assert d["retrieval_check"]["bad_rows_max_over_ranks"] == 0
+    assert d["retrieval_check"]["rows"] == 3
 
 
 def test_pipeline_bench_tp2_gloo_sharded_index():

@@ -213,6 +213,51 @@ def test_precomputed_table_scan_matches_lut_scan(monkeypatch, d, M, k, nprobe, p
     assert (I[:, 0].cpu() == torch.arange(96)).float().mean() > 0.9
 
 
+def test_precomputed_table_scan_unnormalised_offset_vectors(monkeypatch):
+    """the precomputed-table decomposition ||q||^2 - 2<q, c> + ||c + r^||^2 -
+    2 sum_m <q_m, pq> cancels large terms when the vectors are far from the origin (not
+    unit-norm embeddings); the fp16 LUT must still give the exact-fp32 'lut' kernel's
+    candidates.  Also: train() again after add() drops the stored norms (they belong to the
+    old quantizers) instead of reusing them."""
+    from docqa_amd import ops
+    from docqa_amd.index.ivfpq import IVFPQIndex
+
+    assert ops.load_native()
+    g = torch.Generator().manual_seed(11)
+    d, M, nlist, n = 128, 16, 32, 12000
+    c = torch.randn(nlist, d, generator=g) * 2 + 20.0           # ||x|| ~ 230: far from unit norm
+    x = c[torch.randint(0, nlist, (n,), generator=g)] + torch.randn(n, d, generator=g)
+    idx = IVFPQIndex(d, nlist, M, device="cuda")
+    idx.train(x, niter=5)
+    idx.add(x)
+    q = (x[:64] + 0.1 * torch.randn(64, d, generator=g)).cuda()
+
+    def both():
+        monkeypatch.setenv("DOCQA_IVFPQ_SCAN", "pt")
+        D, I = idx.search(q, 16, nprobe=8)
+        monkeypatch.setenv("DOCQA_IVFPQ_SCAN", "lut")
+        D2, I2 = idx.search(q, 16, nprobe=8)
+        same = sum(len(set(a) & set(b)) for a, b in zip(I.cpu().tolist(), I2.cpu().tolist()))
+        return D.cpu(), D2.cpu(), same / I.numel()
+
+    D, D2, overlap = both()
+    assert overlap > 0.95, overlap
+    scale = float(D2.abs().max())
+    assert float((D - D2).abs().max()) <= 2e-3 * scale + 1e-2
+    # re-train on the same data: new quantizers, the stored norms must be rebuilt from the codes
+    idx.train(x, niter=3, seed=7)
+    assert idx.norms is None
+    # and a fresh index on those quantizers searches pt == lut (norms built at add time)
+    idx2 = IVFPQIndex(d, nlist, M, device="cuda")
+    idx2.train(x, niter=3, seed=7)
+    idx2.add(x)
+    monkeypatch.setenv("DOCQA_IVFPQ_SCAN", "pt")
+    Da, _ = idx2.search(q, 8, nprobe=8)
+    monkeypatch.setenv("DOCQA_IVFPQ_SCAN", "lut")
+    Db, _ = idx2.search(q, 8, nprobe=8)
+    assert float((Da.cpu() - Db.cpu()).abs().max()) <= 2e-3 * float(Db.abs().max()) + 1e-2
+
+
 def test_precomputed_table_scan_exact_ties():
     """3000 copies of one vector: every candidate ties at the K-th distance -- the radix
     select keeps exactly K distinct positions per workgroup (no buffer overflow), the merge

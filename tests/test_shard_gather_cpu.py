@@ -4,6 +4,9 @@ whose staging rows are then stale -- turns into CollectiveError at the pipeline'
 instead of silently wrong retrieval.  The IPC kernel itself is exercised on the GPU
 (tests/test_custom_ar_gpu.py, tests/test_dp_share_gpu.py); here a stand-in with the same
 snapshot / raise_if contract drives the Python path."""
+import threading
+import time
+
 import pytest
 import torch
 
@@ -33,15 +36,24 @@ class FakeIPC:
     raise_if = CustomAllReduce.raise_if
 
 
-def _sharded(word: int) -> ShardedIndex:
-    local = FlatIndex(8, "l2", "cpu", torch.float32, capacity=64)
-    local.add(torch.randn(16, 8))
+def _bare(local=None) -> ShardedIndex:
+    """A 2-rank ShardedIndex (rank 0) without a process group: shards of 16 rows each."""
+    if local is None:
+        local = FlatIndex(8, "l2", "cpu", torch.float32, capacity=64)
+        local.add(torch.randn(16, 8))
     s = ShardedIndex.__new__(ShardedIndex)
     s.local, s.group, s.replicated, s.max_queries = local, None, False, 4
-    s.world, s.rank, s._offset, s._ntotal, s._snap = 2, 0, 0, 32, None
+    s.world, s.rank, s._offset, s._ntotal, s._sizes = 2, 0, 0, 32, [16, 16]
+    s._tls = threading.local()
+    s._ipc = None
+    return s
+
+
+def _sharded(word: int) -> ShardedIndex:
+    s = _bare()
     s._ipc = FakeIPC(word)
     # the stand-in "is_cuda" check: route every gather through the fake IPC kernel
-    s._all_gather = lambda t: (setattr(s, "_used_ipc", True), s._ipc.all_gather_raw(t.contiguous()))[1]
+    s._all_gather = lambda t: (setattr(s._tls, "used_ipc", True), s._ipc.all_gather_raw(t.contiguous()))[1]
     return s
 
 
@@ -77,10 +89,110 @@ def test_pipeline_host_sync_surfaces_the_error():
     assert len(pipe._host_ids(I)) == 2
 
 
-def test_gather_timeout_is_per_instance(monkeypatch):
-    """The shard gathers get their own, longer bound than the TP all-reduce's 500 ms."""
-    import inspect
+class BoundedPeerIPC:
+    """Stand-in for the IPC gather kernel's bounded peer wait (allreduce.hip GATHER mode):
+    each call waits for the peer at most ``timeout_ms`` -- the bound enable_ipc passes in --
+    and, if the peer is later than that, records "rank 1 never arrived" in the sticky error
+    word and returns (stale rows) instead of hanging.  ``peer_delay_s``: when the peer
+    arrives at the next call; ``corrupt``: peer row words to flip (a wrong mapping)."""
 
-    src = inspect.getsource(ShardedIndex.enable_ipc)
-    assert "DOCQA_SHARD_GATHER_TIMEOUT_MS" in src and "timeout_ms=" in src
-    assert "timeout_ms" in inspect.signature(CustomAllReduce.__init__).parameters
+    max_elems = 1 << 20
+
+    def __init__(self, group=None, max_bytes=0, device=None, timeout_ms=500.0):
+        self.timeout_ms = timeout_ms
+        self.device = torch.device("cpu")
+        self.err = torch.zeros(1, dtype=torch.int32)
+        self.peer_delay_s = 0.0
+        self.corrupt = False
+        self.calls = 0
+
+    def all_gather_raw(self, t):
+        self.calls += 1
+        peer = t.clone()
+        if t.dtype == torch.int32 and t.numel() >= 4:
+            peer[0] = 1                               # the peer's row, as rank 1 builds it
+            peer[2], peer[3] = 16, 16                 # its shard offset / size
+            peer[5] = 1 ^ 0x5D0C0A11
+        if self.corrupt:
+            peer[3] += 1
+        bound = self.timeout_ms / 1e3
+        time.sleep(min(self.peer_delay_s, bound))
+        if self.peer_delay_s > bound:
+            self.err[0] = 1 | (1 << 1) | (self.calls << 8)    # rank 1 never arrived
+        return torch.stack([t, peer])
+
+    def snapshot(self):
+        return self.err.clone()
+
+    def check(self):
+        if int(self.err[0]):
+            raise CollectiveError(self.describe(int(self.err[0])))
+
+    describe = staticmethod(CustomAllReduce.describe)
+    raise_if = CustomAllReduce.raise_if
+
+
+class _CudaShard:
+    """Rank 0's shard as enable_ipc sees it (a GPU shard); searches run on the CPU copy."""
+
+    def __init__(self, flat):
+        self.flat, self.device, self.d, self.ntotal, self.metric = flat, torch.device("cuda"), flat.d, flat.ntotal, "l2"
+
+
+def _ipc_index(monkeypatch, timeout_ms: str):
+    monkeypatch.setenv("DOCQA_SHARD_GATHER_TIMEOUT_MS", timeout_ms)
+    flat = FlatIndex(8, "l2", "cpu", torch.float32, capacity=64)
+    flat.add(torch.randn(16, 8))
+    s = _bare(_CudaShard(flat))
+    made = []
+
+    def factory(**kw):
+        made.append(BoundedPeerIPC(**kw))
+        return made[-1]
+    return s, flat, made, factory
+
+
+def test_gather_wait_bound_expires_on_delayed_peer(monkeypatch):
+    """The shard gathers' own wait bound (DOCQA_SHARD_GATHER_TIMEOUT_MS, not the TP
+    all-reduce's 500 ms) reaches the gather: a peer later than the bound ends the gather at
+    the bound with the error word set, and the search's check raises -- no hang, no silent
+    stale rows; a peer within the bound passes."""
+    s, flat, made, factory = _ipc_index(monkeypatch, "50")
+    assert s.enable_ipc(factory=factory) and made[0].timeout_ms == 50.0
+    s.local = flat                                     # searches on the CPU copy of the shard
+    s._all_gather = lambda t: (setattr(s._tls, "used_ipc", True), s._ipc.all_gather_raw(t.contiguous()))[1]
+    made[0].peer_delay_s = 0.005                       # on time
+    s.search(torch.randn(2, 8), 3)
+    s.check_gather()
+    made[0].peer_delay_s = 5.0                         # far past the bound
+    t0 = time.perf_counter()
+    s.search(torch.randn(2, 8), 3)
+    assert time.perf_counter() - t0 < 2.0              # gave up at ~the 50 ms bound
+    with pytest.raises(CollectiveError, match="rank 1 never arrived"):
+        s.check_gather()
+
+
+def test_ipc_handshake_rejects_a_corrupted_peer_row(monkeypatch):
+    """enable_ipc's handshake gather must return every peer's (rank, world, offset, size,
+    magic) row exactly; one wrong word fails the run before the first search."""
+    s, _, made, factory = _ipc_index(monkeypatch, "100")
+
+    def corrupting(**kw):
+        ipc = factory(**kw)
+        ipc.corrupt = True
+        return ipc
+    with pytest.raises(CollectiveError, match=r"wrong peer rows \[1\]"):
+        s.enable_ipc(factory=corrupting)
+    s2, _, made2, factory2 = _ipc_index(monkeypatch, "100")
+    assert s2.enable_ipc(factory=factory2) and made2[0].calls == 1      # the clean handshake
+
+
+def test_ipc_handshake_rejects_a_peer_that_never_arrives(monkeypatch):
+    s, _, made, factory = _ipc_index(monkeypatch, "20")
+
+    def late(**kw):
+        ipc = factory(**kw)
+        ipc.peer_delay_s = 1.0
+        return ipc
+    with pytest.raises(CollectiveError):
+        s.enable_ipc(factory=late)
