@@ -826,6 +826,32 @@ at::Tensor mgemm_glu(const at::Tensor& x, const at::Tensor& w, int64_t cfg) {
 
 int64_t mgemm_tile_n(int64_t cfg) { return docqa_mgemm_tile_n((int)cfg); }
 
+// layout probe: x [M, K] / w [N, K] views with row strides >= K (stride(1) == 1); glu: the
+// SwiGLU epilogue over 8-interleaved gate|up rows -> [M, N / 2]; else splits >= 2 -> fp32
+// slabs [S, M, N], splits == 1 -> bf16 [M, N]
+at::Tensor mgemm_ld(const at::Tensor& x, const at::Tensor& w, int64_t splits, int64_t cfg, bool glu) {
+  CHECK_GPU(x); CHECK_BF16(x); CHECK_BF16(w);
+  TORCH_CHECK(x.dim() == 2 && w.dim() == 2 && x.stride(1) == 1 && w.stride(1) == 1, "mgemm_ld: 2-D row views");
+  const int M = x.size(0), K = x.size(1), N = w.size(0);
+  TORCH_CHECK(w.size(1) == K && splits >= 1, "mgemm_ld: shape");
+  c10::DeviceGuard g(x.device());
+  at::Tensor out;
+  if (glu) {
+    out = at::empty({M, N / 2}, x.options());
+    CHECK_RC(docqa_mgemm_ld(x.data_ptr(), (int)x.stride(0), w.data_ptr(), (int)w.stride(0), out.data_ptr(), nullptr,
+                            M, N, K, 1, (int)cfg, 1, stream()), "mgemm_ld");
+  } else if (splits == 1) {
+    out = at::empty({M, N}, x.options());
+    CHECK_RC(docqa_mgemm_ld(x.data_ptr(), (int)x.stride(0), w.data_ptr(), (int)w.stride(0), out.data_ptr(), nullptr,
+                            M, N, K, 1, (int)cfg, 0, stream()), "mgemm_ld");
+  } else {
+    out = at::empty({splits, M, N}, x.options().dtype(at::kFloat));
+    CHECK_RC(docqa_mgemm_ld(x.data_ptr(), (int)x.stride(0), w.data_ptr(), (int)w.stride(0), nullptr,
+                            out.data_ptr<float>(), M, N, K, (int)splits, (int)cfg, 0, stream()), "mgemm_ld");
+  }
+  return out;
+}
+
 // LM head + greedy pick: argmax over the first n_valid columns of bf16(x . w^T) -> int64 [M]
 at::Tensor mgemm_argmax(const at::Tensor& x, const at::Tensor& w, int64_t n_valid, int64_t cfg) {
   CHECK_GPU(x); CHECK_BF16(x); CHECK_BF16(w); CHECK_CONTIG(x); CHECK_CONTIG(w);
@@ -1233,6 +1259,7 @@ TORCH_LIBRARY(docqa, m) {
   m.def("pgemm_partial(Tensor x, Tensor w, int splits) -> Tensor");
   m.def("mgemm_argmax_val(Tensor x, Tensor w, int n_valid, int cfg=0) -> (Tensor, Tensor)");
   m.def("pgemm_ok(int M, int N, int K) -> bool", &pgemm_ok);
+  m.def("mgemm_ld(Tensor x, Tensor w, int splits, int cfg, bool glu) -> Tensor");
   m.def("group_persist_bins(int cap, int Hkv) -> int", &group_persist_bins);
   m.def("set_decode_trace(Tensor? buf) -> ()", &set_decode_trace);
   m.def("set_group_wave(int on) -> int", &set_group_wave);
@@ -1304,6 +1331,7 @@ TORCH_LIBRARY_IMPL(docqa, CUDA, m) {
   m.impl("mgemm_glu", &mgemm_glu);
   m.impl("mgemm_argmax", &mgemm_argmax);
   m.impl("pgemm", &pgemm);
+  m.impl("mgemm_ld", &mgemm_ld);
   m.impl("pgemm_partial", &pgemm_partial);
   m.impl("mgemm_argmax_val", &mgemm_argmax_val);
   m.impl("coarse_probes", &coarse_probes);

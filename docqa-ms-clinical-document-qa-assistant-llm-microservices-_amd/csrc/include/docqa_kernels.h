@@ -139,6 +139,8 @@ int docqa_mgemm_glu(const void* X, const void* W, void* Y, int M, int N, int K, 
 int docqa_mgemm_argmax(const void* X, const void* W, int64_t* out, float* outv, float* ws_v, int* ws_i, int M,
                        int N, int K, int n_valid, int cfg, hipStream_t s);
 int docqa_mgemm_tile_n(int cfg);
+int docqa_mgemm_ld(const void* X, int ldx, const void* W, int ldw, void* Y, float* P, int M, int N, int K, int S,
+                   int cfg, int glu, hipStream_t s);
 // IVF coarse quantizer for wide probes (coarse.hip): nprobe <= 512 nearest centroids per query
 int docqa_coarse_probes(const float* cent, const float* cnorm, int nlist, int d, const float* xq, int nq,
                         int nprobe, float* ws, int64_t* probes, hipStream_t s);

@@ -184,7 +184,8 @@ __device__ __forceinline__ void mgemm_tile(uint16_t* smem, const uint16_t* __res
                                            const uint16_t* __restrict__ W, uint16_t* __restrict__ Y,
                                            float* __restrict__ P, float* __restrict__ pv,
                                            int* __restrict__ pi, int M, int N, int K, int Ks,
-                                           int tile, int slice, int m0, int ntiles, int n_valid) {
+                                           int tile, int slice, int m0, int ntiles, int n_valid, int ldx,
+                                           int ldw) {
   constexpr int WAVES = WM * WN;
   constexpr int MI = BM / WM / 16;                      // 16-row m-tiles per wave
   constexpr int CW = BN / WN;                           // output columns per wave
@@ -220,12 +221,12 @@ __device__ __forceinline__ void mgemm_tile(uint16_t* smem, const uint16_t* __res
 #pragma unroll
   for (int i = 0; i < A_PER_WAVE; ++i) {
     const int p = (i * WAVES + wave) * 64 + lane, r = p / CPR;
-    asrc[i] = X + (size_t)min(m0 + r, M - 1) * K + kbeg + lchunk(r, p % CPR) * 8;
+    asrc[i] = X + (size_t)min(m0 + r, M - 1) * ldx + kbeg + lchunk(r, p % CPR) * 8;
   }
 #pragma unroll
   for (int i = 0; i < B_PER_WAVE; ++i) {
     const int p = (i * WAVES + wave) * 64 + lane, r = p / CPR;
-    bsrc[i] = W + (size_t)(n0 + r) * K + kbeg + lchunk(r, p % CPR) * 8;
+    bsrc[i] = W + (size_t)(n0 + r) * ldw + kbeg + lchunk(r, p % CPR) * 8;
   }
   const uint32_t base = lds_u32(smem);
   auto stage = [&](int kt) {
@@ -367,7 +368,8 @@ __global__ __launch_bounds__(WM * WN * 64) void mgemm_kernel(const uint16_t* __r
                                                              float* __restrict__ P,
                                                              float* __restrict__ pv, int* __restrict__ pi,
                                                              int M, int N, int K, int Ks, int S,
-                                                             int ntiles, int remap, int n_valid) {
+                                                             int ntiles, int remap, int n_valid, int ldx,
+                                                             int ldw) {
   __shared__ __attribute__((aligned(16))) uint16_t smem[NSR * (BM + BN) * BKS];
   const int L = blockIdx.x;
   int tile, slice;
@@ -384,7 +386,7 @@ __global__ __launch_bounds__(WM * WN * 64) void mgemm_kernel(const uint16_t* __r
     slice = L / ntiles;
   }
   mgemm_tile<EPI, BN, BKS, NSR, WM, WN, PF>(smem, X, W, Y, P, pv, pi, M, N, K, Ks, tile, slice, blockIdx.y * BM,
-                                            ntiles, n_valid);
+                                            ntiles, n_valid, ldx, ldw);
 }
 
 // Variants (``cfg``): the tile width and wave layout
@@ -416,7 +418,7 @@ constexpr Cfg kCfg[kNumCfg + 1] = {{0, 0}, {128, 64}, {128, 64}, {256, 32}, {256
 
 template <int EPI, int BN, int BKS, int NSR, int WM, int WN, int PF = 1>
 int launch(const uint16_t* x, const uint16_t* w, uint16_t* y, float* p, float* pv, int* pi, int M,
-           int N, int K, int S, int n_valid, hipStream_t s) {
+           int N, int K, int S, int n_valid, hipStream_t s, int ldx, int ldw) {
   // the epilogue sweeps 16-row slices with (columns per wave) / (columns per lane) lanes per
   // row: the SwiGLU epilogue (16 columns per lane) needs >= 64 columns per wave
   if constexpr (EPI == EPI_GLU && BN / WN < 64) {
@@ -428,7 +430,7 @@ int launch(const uint16_t* x, const uint16_t* w, uint16_t* y, float* p, float* p
   else if (S > 8 && S % 8 == 0) remap = 2;
   dim3 grid(ntiles * S, (M + BM - 1) / BM);
   mgemm_kernel<EPI, BN, BKS, NSR, WM, WN, PF><<<grid, WM * WN * 64, 0, s>>>(x, w, y, p, pv, pi, M, N, K, Ks, S,
-                                                                      ntiles, remap, n_valid);
+                                                                      ntiles, remap, n_valid, ldx, ldw);
   DOCQA_CHECK_LAUNCH();
   return 0;
   }
@@ -436,15 +438,17 @@ int launch(const uint16_t* x, const uint16_t* w, uint16_t* y, float* p, float* p
 
 template <int EPI>
 int launch_cfg(int cfg, const uint16_t* x, const uint16_t* w, uint16_t* y, float* p, float* pv, int* pi,
-               int M, int N, int K, int S, int n_valid, hipStream_t s) {
+               int M, int N, int K, int S, int n_valid, hipStream_t s, int ldx = 0, int ldw = 0) {
+  if (ldx <= 0) ldx = K;
+  if (ldw <= 0) ldw = K;
   switch (cfg) {
-    case 1: return launch<EPI, 128, 64, 3, 2, 2>(x, w, y, p, pv, pi, M, N, K, S, n_valid, s);
-    case 2: return launch<EPI, 128, 64, 3, 4, 2>(x, w, y, p, pv, pi, M, N, K, S, n_valid, s);
-    case 3: return launch<EPI, 256, 32, 4, 2, 4>(x, w, y, p, pv, pi, M, N, K, S, n_valid, s);
-    case 4: return launch<EPI, 256, 32, 4, 2, 2>(x, w, y, p, pv, pi, M, N, K, S, n_valid, s);
-    case 5: return launch<EPI, 256, 64, 2, 2, 2, 0>(x, w, y, p, pv, pi, M, N, K, S, n_valid, s);
-    case 6: return launch<EPI, 256, 64, 2, 2, 4, 0>(x, w, y, p, pv, pi, M, N, K, S, n_valid, s);
-    case 7: return launch<EPI, 64, 64, 3, 4, 2>(x, w, y, p, pv, pi, M, N, K, S, n_valid, s);
+    case 1: return launch<EPI, 128, 64, 3, 2, 2>(x, w, y, p, pv, pi, M, N, K, S, n_valid, s, ldx, ldw);
+    case 2: return launch<EPI, 128, 64, 3, 4, 2>(x, w, y, p, pv, pi, M, N, K, S, n_valid, s, ldx, ldw);
+    case 3: return launch<EPI, 256, 32, 4, 2, 4>(x, w, y, p, pv, pi, M, N, K, S, n_valid, s, ldx, ldw);
+    case 4: return launch<EPI, 256, 32, 4, 2, 2>(x, w, y, p, pv, pi, M, N, K, S, n_valid, s, ldx, ldw);
+    case 5: return launch<EPI, 256, 64, 2, 2, 2, 0>(x, w, y, p, pv, pi, M, N, K, S, n_valid, s, ldx, ldw);
+    case 6: return launch<EPI, 256, 64, 2, 2, 4, 0>(x, w, y, p, pv, pi, M, N, K, S, n_valid, s, ldx, ldw);
+    case 7: return launch<EPI, 64, 64, 3, 4, 2>(x, w, y, p, pv, pi, M, N, K, S, n_valid, s, ldx, ldw);
     default: return -1;
   }
 }
@@ -498,4 +502,18 @@ int docqa_mgemm_argmax(const void* X, const void* W, int64_t* out, float* outv, 
   argmax_merge_kernel<<<M, 256, 0, s>>>(ws_v, ws_i, N / kCfg[cfg].bn, out, outv);
   DOCQA_CHECK_LAUNCH();
   return 0;
+}
+
+// strided operands (row strides ldx / ldw elements, multiples of 8): the layout probe of the
+// decode GEMMs (power-of-two row strides put every row of a stage on one L2 channel?)
+int docqa_mgemm_ld(const void* X, int ldx, const void* W, int ldw, void* Y, float* P, int M, int N, int K, int S,
+                   int cfg, int glu, hipStream_t s) {
+  if (cfg == 0) cfg = kDefaultCfg;
+  if (M == 0) return 0;
+  if (!shape_ok(M, N, K, S, cfg) || ldx < K || ldw < K || ldx % 8 || ldw % 8) return -1;
+  if (!docqa_aligned16(X) || !docqa_aligned16(W)) return -1;
+  const uint16_t *x = (const uint16_t*)X, *w = (const uint16_t*)W;
+  if (glu) return launch_cfg<EPI_GLU>(cfg, x, w, (uint16_t*)Y, nullptr, nullptr, nullptr, M, N, K, 1, N, s, ldx, ldw);
+  if (P) return launch_cfg<EPI_PARTIAL>(cfg, x, w, nullptr, P, nullptr, nullptr, M, N, K, S, N, s, ldx, ldw);
+  return launch_cfg<EPI_BF16>(cfg, x, w, (uint16_t*)Y, nullptr, nullptr, nullptr, M, N, K, 1, N, s, ldx, ldw);
 }

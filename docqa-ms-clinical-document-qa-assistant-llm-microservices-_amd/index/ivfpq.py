@@ -64,6 +64,10 @@ def probes_per_workgroup(nq: int, nprobe: int) -> int:
     return -(-nprobe // chunks)
 
 
+# auto scan: above this E||c||^2 / E||r^||^2 the exact-fp32 LUT kernel is used
+_PT_MAX_RATIO = float(os.environ.get("DOCQA_IVFPQ_PT_MAX_RATIO", "32"))
+
+
 class IVFPQIndex:
     def __init__(self, d: int, nlist: int, M: int, nbits: int = 8, device="cuda", rotation: str = "none"):
         if nbits != 8:
@@ -187,13 +191,32 @@ class IVFPQIndex:
         else:   # wide probes (the 10M operating points: nprobe 128..512): coarse.hip
             probes = ops.coarse_probes(xq, self.centroids, cn, nprobe)
         if self.device.type == "cuda":
-            if os.environ.get("DOCQA_IVFPQ_SCAN", "pt") == "lut":
+            if self.scan_mode() == "lut":
                 return ops._native().ivfpq_search(xq, self.centroids, self.pq, self.codes, self.ids,
                                                   self.list_off, probes.contiguous(), k)
             return ops._native().ivfpq_search_pt(xq, self.centroids, self.pq, self.codes, self._norms(),
                                                  self.ids, self.list_off, probes.contiguous(), k,
                                                  probes_per_workgroup(xq.shape[0], probes.shape[1]))
         return self._search_reference(xq, probes, k)
+
+    def scan_mode(self) -> str:
+        """``pt`` (precomputed tables: fp16 per-query LUT + stored norms) or ``lut`` (exact
+        fp32 per-(query, list) LUT).  DOCQA_IVFPQ_SCAN=pt|lut forces one; ``auto`` (default)
+        takes ``pt`` unless the vectors sit far from the origin relative to their residual
+        spread: the pt decomposition ||q||^2 - 2<q, c> + ||c + r^||^2 - 2 sum <q_m, pq>
+        cancels terms of size ||x||^2 down to a distance of size ||r||^2, so its fp16 LUT
+        error grows with that ratio (unit-norm embeddings sit at ~2-4, an offset
+        cloud at 400 measured 2.4e-3 relative distance error,
+        tests/test_ivfpq_gpu.py::test_precomputed_table_scan_unnormalised_offset_vectors)."""
+        mode = os.environ.get("DOCQA_IVFPQ_SCAN", "auto")
+        if mode in ("pt", "lut"):
+            return mode
+        if getattr(self, "_auto_src", None) is not (self.centroids, self.pq):
+            cn = float((self.centroids.float() ** 2).sum(1).mean())
+            rn = float((self.pq.float() ** 2).sum(-1).mean(1).sum())      # E||r^||^2 over the M sub-spaces
+            self._auto_mode = "lut" if cn > _PT_MAX_RATIO * max(rn, 1e-30) else "pt"
+            self._auto_src = (self.centroids, self.pq)
+        return self._auto_mode
 
     def _search_reference(self, xq, probes, k):
         nq = xq.shape[0]
