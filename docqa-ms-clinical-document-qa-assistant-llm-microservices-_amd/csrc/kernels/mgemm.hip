@@ -53,6 +53,7 @@ __device__ __forceinline__ int swz(int row, int ch) {
 
 __device__ __forceinline__ float silu_f(float x) { return x / (1.f + __expf(-x)); }
 
+
 __device__ __forceinline__ void better(float& bv, int& bi, float v, int i) {
   if (v > bv || (v == bv && i < bi)) { bv = v; bi = i; }
 }
@@ -177,15 +178,20 @@ __device__ __forceinline__ void mgemm_epilogue(f32x4 (&acc)[BM / WM / 16][BN / W
 // PF: fragment prefetch (stage k+1's LDS reads under stage k's MFMAs, two register sets);
 // PF = 0 reads each stage's fragments after its barrier (one register set, for the
 // 128 x 128-per-wave layout whose two sets would not fit)
-// One (m-tile, weight tile, K slice) of the GEMM on the workgroup's LDS ring `smem`
-// (NSR * (BM + BN) * BKS bf16): the kernel below runs one per workgroup.
-template <int EPI, int BN, int BKS, int NSR, int WM, int WN, int PF = 1>
-__device__ __forceinline__ void mgemm_tile(uint16_t* smem, const uint16_t* __restrict__ X,
-                                           const uint16_t* __restrict__ W, uint16_t* __restrict__ Y,
-                                           float* __restrict__ P, float* __restrict__ pv,
-                                           int* __restrict__ pi, int M, int N, int K, int Ks,
-                                           int tile, int slice, int m0, int ntiles, int n_valid, int ldx,
-                                           int ldw) {
+// The K loop of one (m-tile, weight tile) over K-stages [kbeg / BKS, kbeg / BKS + nk)
+// (nk even, >= 2), accumulating into `acc`; ends with the ring drained and a barrier, so the
+// caller may reuse the LDS (epilogue scratch, or the next tile's ring).
+template <int BN, int BKS, int NSR, int WM, int WN, int PF>
+__device__ __forceinline__ void mgemm_mainloop(uint16_t* smem, const uint16_t* __restrict__ X,
+                                               const uint16_t* __restrict__ W, int M, int kbeg, int nk, int m0,
+                                               int n0, int ldx, int ldw,
+                                               f32x4 (&acc)[BM / WM / 16][BN / WN / 16]) {
+  // PF bits 0-1: 1 = fragment prefetch, 0 = none, 2 / 3 = probe-only (no MFMAs / no MFMAs
+  // and no fragment reads); bit 2: W stored stage-tiled -- [N / BN][K / BKS][BN][BKS], so a
+  // stage's weight tile is one contiguous 16 KiB run instead of BN rows x 128 B at a K x 2 B
+  // stride (the DRAM-page probe, scripts/mgemm_floor_probe.py)
+  constexpr int MODE = PF & 3;
+  constexpr bool WTILE = (PF & 4) != 0;
   constexpr int WAVES = WM * WN;
   constexpr int MI = BM / WM / 16;                      // 16-row m-tiles per wave
   constexpr int CW = BN / WN;                           // output columns per wave
@@ -197,13 +203,10 @@ __device__ __forceinline__ void mgemm_tile(uint16_t* smem, const uint16_t* __res
   constexpr int B_PER_WAVE = BN / RPI / WAVES;
   constexpr int PER_STAGE = A_PER_WAVE + B_PER_WAVE;
   constexpr int SLOT = (BM + BN) * BKS;                 // elements per ring slot
-  constexpr int SCR = CW + 4;                           // scratch row pitch (floats)
   static_assert(NSR >= 2, "ring needs >= 2 slots");
   static_assert(A_PER_WAVE * RPI * WAVES == BM && B_PER_WAVE * RPI * WAVES == BN, "DMA split");
   static_assert(NSR * SLOT * 2 <= 160 * 1024, "LDS");
 
-  const int n0 = tile * BN, kbeg = slice * Ks;
-  const int nk = Ks / BKS;     // even, >= 2
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int fr = lane & 15, fq = lane >> 4;
@@ -226,9 +229,16 @@ __device__ __forceinline__ void mgemm_tile(uint16_t* smem, const uint16_t* __res
 #pragma unroll
   for (int i = 0; i < B_PER_WAVE; ++i) {
     const int p = (i * WAVES + wave) * 64 + lane, r = p / CPR;
-    bsrc[i] = W + (size_t)(n0 + r) * ldw + kbeg + lchunk(r, p % CPR) * 8;
+    if constexpr (WTILE)
+      bsrc[i] = W + ((size_t)(n0 / BN) * (size_t)(ldw / BKS) + (size_t)(kbeg / BKS)) * (BN * BKS) + r * BKS +
+                lchunk(r, p % CPR) * 8;
+    else
+      bsrc[i] = W + (size_t)(n0 + r) * ldw + kbeg + lchunk(r, p % CPR) * 8;
   }
   const uint32_t base = lds_u32(smem);
+  // the ring's counted waits below must count only its own DMAs: retire anything hipcc left
+  // in flight before the first one (the stream-K loop spills around its fixup)
+  wait_vmcnt<0>();
   auto stage = [&](int kt) {
     const uint32_t slot = base + (uint32_t)((kt % NSR) * SLOT * 2);
     const int ko = kt * BKS;
@@ -237,14 +247,8 @@ __device__ __forceinline__ void mgemm_tile(uint16_t* smem, const uint16_t* __res
       glds16<false>(asrc[i] + ko, slot + (uint32_t)((i * WAVES + wave) * 1024));
 #pragma unroll
     for (int i = 0; i < B_PER_WAVE; ++i)
-      glds16<true>(bsrc[i] + ko, slot + (uint32_t)(BM * BKS * 2 + (i * WAVES + wave) * 1024));
+      glds16<true>(bsrc[i] + (WTILE ? (size_t)kt * (BN * BKS) : (size_t)ko), slot + (uint32_t)(BM * BKS * 2 + (i * WAVES + wave) * 1024));
   };
-
-  f32x4 acc[MI][NJ];
-#pragma unroll
-  for (int i = 0; i < MI; ++i)
-#pragma unroll
-    for (int j = 0; j < NJ; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   // fragments of one stage: [k-step][m-tile] A, [k-step][n-tile] B.  They are read by
   // inline-asm ds_read_b128 (invisible to hipcc's waitcnt pass, which otherwise drains
@@ -305,8 +309,8 @@ __device__ __forceinline__ void mgemm_tile(uint16_t* smem, const uint16_t* __res
     else wait_vmcnt<0>();
     ring_barrier();
     if (kt + NSR < nk) stage(kt + NSR);
-    load_frags(nxt, kt + 1);
-    mma(cur);
+    if constexpr (MODE != 3) load_frags(nxt, kt + 1);
+    if constexpr (MODE == 1) mma(cur);
     // keep this stage's MFMAs above the next stage's publish wait (hipcc otherwise sinks
     // some of them below it, where they wait for the whole prefetch)
     __builtin_amdgcn_sched_barrier(0);
@@ -314,7 +318,9 @@ __device__ __forceinline__ void mgemm_tile(uint16_t* smem, const uint16_t* __res
 #pragma unroll
   for (int j = 0; j < NSR; ++j)
     if (j < nk) stage(j);
-  if constexpr (PF) {
+  // PF 2 / 3: probe-only variants (cfg 8-10) -- the same ring without the MFMAs (2), and
+  // without the fragment reads too (3): the transfer floor of the schedule
+  if constexpr (MODE != 0) {
     Frag f0, f1;
     if (nk >= NSR) wait_vmcnt<(NSR - 1) * PER_STAGE>();
     else wait_vmcnt<0>();
@@ -358,6 +364,25 @@ __device__ __forceinline__ void mgemm_tile(uint16_t* smem, const uint16_t* __res
   wait_vmcnt<0>();
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   ring_barrier();   // every wave is done reading the ring: reuse it as epilogue scratch
+}
+
+// One (m-tile, weight tile, K slice) of the GEMM on the workgroup's LDS ring `smem`
+// (NSR * (BM + BN) * BKS bf16): the kernel below runs one per workgroup.
+template <int EPI, int BN, int BKS, int NSR, int WM, int WN, int PF = 1>
+__device__ __forceinline__ void mgemm_tile(uint16_t* smem, const uint16_t* __restrict__ X,
+                                           const uint16_t* __restrict__ W, uint16_t* __restrict__ Y,
+                                           float* __restrict__ P, float* __restrict__ pv,
+                                           int* __restrict__ pi, int M, int N, int K, int Ks,
+                                           int tile, int slice, int m0, int ntiles, int n_valid, int ldx,
+                                           int ldw) {
+  constexpr int MI = BM / WM / 16, NJ = BN / WN / 16;
+  f32x4 acc[MI][NJ];
+#pragma unroll
+  for (int i = 0; i < MI; ++i)
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const int n0 = tile * BN;
+  mgemm_mainloop<BN, BKS, NSR, WM, WN, PF>(smem, X, W, M, slice * Ks, Ks / BKS, m0, n0, ldx, ldw, acc);
   mgemm_epilogue<EPI, BN, WM, WN>(acc, smem, Y, P, pv, pi, M, N, m0, n0, slice, tile, ntiles, n_valid);
 }
 
@@ -389,6 +414,161 @@ __global__ __launch_bounds__(WM * WN * 64) void mgemm_kernel(const uint16_t* __r
                                             ntiles, n_valid, ldx, ldw);
 }
 
+// ------------------------------------------------------------------------------ stream-K
+// The same tile body with the work split evenly over a persistent grid of G <= CU-count
+// workgroups (stream-K): the (tile, 128-deep K unit) iterations are dealt out in one
+// contiguous range per workgroup, so a grid whose tile count is not a multiple of the CU
+// count -- 144 tiles at 768 prefill rows of the 8B QKV, 224 at the batch-256 gate|up --
+// still keeps every CU busy to the end.  A tile whose K range is cut between workgroups is
+// finished in-launch: each piece draws an arrival ticket (agent-scope atomic); every piece
+// but the last arriver stores its fp32 accumulators write-through (sc1, lane-major: one
+// 1-KiB run per wave instruction) into its workgroup's slot and counts itself done; the last
+// arriver waits for those (they hold a ticket, so they are past their K loop: the wait is a
+// store's latency, never a dependency on unscheduled work), reads them with sc1 loads and
+// sums the pieces IN K ORDER with its own registers in its place -- the result does not
+// depend on which piece arrived last -- then runs the ordinary epilogue (bf16 / SwiGLU /
+// fp32 slab).  It re-arms the tile's two counters for the next launch (zeroed once at
+// allocation).  Hand-off form: cdna_hip_programming.md §6 Guideline 16 / MI355X_MICROARCH.md
+// table row "one lane of each storing workgroup ... agent-scope atomic add", sc1 both sides.
+// Reference: the prefill + generate of llm-qa/main.py:69,117 (served by Ollama there).
+// The hand-off's stores and loads are compiler-visible 8-byte agent-scope atomics
+// (global_store / global_load_dwordx2 ... sc1): the segment loop's register pressure makes
+// hipcc spill around the fixup, and a spill reload counted by hipcc's own vmcnt next to
+// inline-asm memory ops it cannot see reads its register too early (a wild address: the
+// first version of this kernel faulted).  The ring's inline-asm DMA is drained before.
+__device__ __forceinline__ void st16_wt(float* p, const f32x4& v) {
+  unsigned long long* q = reinterpret_cast<unsigned long long*>(p);
+  __hip_atomic_store(q, (unsigned long long)__float_as_uint(v[0]) | ((unsigned long long)__float_as_uint(v[1]) << 32),
+                     __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __hip_atomic_store(q + 1, (unsigned long long)__float_as_uint(v[2]) | ((unsigned long long)__float_as_uint(v[3]) << 32),
+                     __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ f32x4 ld16_sc1(const float* p) {
+  const unsigned long long* q = reinterpret_cast<const unsigned long long*>(p);
+  const unsigned long long a = __hip_atomic_load(q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  const unsigned long long b = __hip_atomic_load(q + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  return f32x4{__uint_as_float((unsigned)a), __uint_as_float((unsigned)(a >> 32)), __uint_as_float((unsigned)b),
+               __uint_as_float((unsigned)(b >> 32))};
+}
+
+constexpr int kSkMaxPieces = 5;      // host-side grid choice bounds a tile to <= 5 pieces
+
+// first workgroup whose unit range [ub, ue) holds unit u (ub(l) = l U / G)
+__device__ __forceinline__ int sk_owner(long long u, long long U, int G) {
+  int l = (int)((u * G) / U);
+  while (l + 1 < G && ((long long)(l + 1) * U) / G <= u) ++l;
+  while (l > 0 && ((long long)l * U) / G > u) --l;
+  return l;
+}
+
+template <int BN, int WM, int WN>
+__device__ __forceinline__ bool sk_fixup(f32x4 (&acc)[BM / WM / 16][BN / WN / 16], uint16_t* smem,
+                                         float* __restrict__ part, int* __restrict__ cnt, int t, int units,
+                                         long long U, int G, int l, int slot) {
+  constexpr int MI = BM / WM / 16, NJ = BN / WN / 16, Q = MI * NJ, NT = WM * WN * 64;
+  constexpr int QB = 2;
+  static_assert(Q % QB == 0, "fixup batches");
+  const int tid = threadIdx.x;
+  const long long t0 = (long long)t * units, t1 = t0 + units;
+  const int lf = sk_owner(t0, U, G), ll = sk_owner(t1 - 1, U, G);
+  const int n = ll - lf + 1, me = l - lf;
+  int* flag = reinterpret_cast<int*>(smem);        // the ring is drained: LDS is free
+  if (tid == 0) flag[0] = __hip_atomic_fetch_add(cnt + 2 * t, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __syncthreads();
+  const int ticket = flag[0];
+  auto slot_of = [&](int lw) {                      // a partial piece: its workgroup's first or last
+    const long long ubw = ((long long)lw * U) / G;
+    return (size_t)(lw * 2 + (ubw >= t0 ? 0 : 1)) * (size_t)(Q * NT) * 4;
+  };
+  if (ticket < n - 1) {
+    float* dst = part + (size_t)(l * 2 + slot) * (size_t)(Q * NT) * 4;
+#pragma unroll
+    for (int i = 0; i < MI; ++i)
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) st16_wt(dst + ((size_t)(i * NJ + j) * NT + tid) * 4, acc[i][j]);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (tid == 0) __hip_atomic_fetch_add(cnt + 2 * t + 1, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return false;
+  }
+  // last arriver: the other n - 1 pieces hold tickets; wait until all are stored (bounded:
+  // a counter left dirty by an aborted launch must not hang the GPU -- the tile is then wrong)
+  if (tid == 0) {
+    int spins = 0;
+    while (__hip_atomic_load(cnt + 2 * t + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < n - 1 &&
+           ++spins < (1 << 22))
+      __builtin_amdgcn_s_sleep(2);
+    __hip_atomic_store(cnt + 2 * t, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(cnt + 2 * t + 1, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  __syncthreads();
+  size_t off[kSkMaxPieces];
+#pragma unroll
+  for (int p = 0; p < kSkMaxPieces; ++p) off[p] = (p < n && p != me) ? slot_of(lf + p) : 0;
+#pragma unroll
+  for (int qb = 0; qb < Q / QB; ++qb) {
+    f32x4 buf[kSkMaxPieces][QB];
+#pragma unroll
+    for (int p = 0; p < kSkMaxPieces; ++p) {
+      if (p < n && p != me) {
+#pragma unroll
+        for (int qq = 0; qq < QB; ++qq)
+          buf[p][qq] = ld16_sc1(part + off[p] + ((size_t)(qb * QB + qq) * NT + tid) * 4);
+      }
+    }
+#pragma unroll
+    for (int qq = 0; qq < QB; ++qq) {
+      const int q = qb * QB + qq, i = q / NJ, j = q % NJ;
+      // K order: (((p0 + p1) + p2) ...), this workgroup's registers at position `me`
+      const f32x4 v = acc[i][j];
+      f32x4 sum = me == 0 ? v : buf[0][qq];
+#pragma unroll
+      for (int p = 1; p < kSkMaxPieces; ++p)
+        if (p < n) sum += (p == me ? v : buf[p][qq]);
+      acc[i][j] = sum;
+    }
+  }
+  return true;
+}
+
+template <int EPI, int BN, int BKS, int NSR, int WM, int WN>
+__global__ __launch_bounds__(WM * WN * 64) void mgemm_sk_kernel(const uint16_t* __restrict__ X,
+                                                                const uint16_t* __restrict__ W,
+                                                                uint16_t* __restrict__ Y, float* __restrict__ P,
+                                                                float* __restrict__ part, int* __restrict__ cnt,
+                                                                int M, int N, int K, int ntm, int ntn, int units,
+                                                                int G, int ldx, int ldw) {
+  __shared__ __attribute__((aligned(16))) uint16_t smem[NSR * (BM + BN) * BKS];
+  constexpr int MI = BM / WM / 16, NJ = BN / WN / 16;
+  // consecutive logical ids on one XCD: its workgroups share the W columns of neighbouring
+  // tiles (m-tiles fastest) in that XCD's L2
+  const int l = xcd_remap(blockIdx.x, G);
+  const long long U = (long long)ntm * ntn * units;
+  const long long ub = ((long long)l * U) / G, ue = ((long long)(l + 1) * U) / G;
+  long long u = ub;
+  int slot = 0;
+  while (u < ue) {
+    const int t = (int)(u / units);
+    const int kb = (int)(u - (long long)t * units);
+    const int ke = (int)min((long long)units, ue - (long long)t * units);
+    const int m0 = (t % ntm) * BM, n0 = (t / ntm) * BN;
+    f32x4 acc[MI][NJ];
+#pragma unroll
+    for (int i = 0; i < MI; ++i)
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    mgemm_mainloop<BN, BKS, NSR, WM, WN, 1>(smem, X, W, M, kb * 2 * BKS, (ke - kb) * 2, m0, n0, ldx, ldw, acc);
+    bool mine = true;
+    if (kb != 0 || ke != units) mine = sk_fixup<BN, WM, WN>(acc, smem, part, cnt, t, units, U, G, l, slot);
+    if (mine) mgemm_epilogue<EPI, BN, WM, WN>(acc, smem, Y, P, nullptr, nullptr, M, N, m0, n0, 0, 0, 0, N);
+    // every wave is done with the epilogue scratch / ticket word before the next ring fill
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    __syncthreads();
+    u = (long long)t * units + ke;
+    slot = 1;
+  }
+}
+
 // Variants (``cfg``): the tile width and wave layout
 //   1: BN 128, 64-deep stages x 3, waves 2 x 2 (128 x 64 each, 1 wave / SIMD)
 //   2: BN 128, 64-deep stages x 3, waves 4 x 2 ( 64 x 64 each, 2 waves / SIMD)
@@ -412,9 +592,15 @@ struct Cfg { int bn, bks; };
 // (Raising the wave priority over each stage's MFMA burst (s_setprio 1 / 0 around mma):
 // 3-7 % slower per projection, 1.3 % slower end to end; profiles/r2_mgemm_probe_setprio.log,
 // profiles/r2_ab_mid_setprio.log.)
-constexpr int kNumCfg = 7;
+// Probe-only (scripts/mgemm_floor_probe.py): 8 = cfg 2 without MFMAs, 9 = cfg 2 without
+// MFMAs and fragment reads (DMA ring + waits + barriers alone), 10 = BN 128 x 32-deep x 6
+// slots, DMA alone (5 stages / 120 KB in flight instead of 2 / 96 KB)
+// 11 / 12 / 13 / 14 = cfg 2 / 9 / 7 / 6 reading a stage-tiled weight copy (WTILE above:
+// [N / BN][K / 64][BN][64])
+constexpr int kNumCfg = 14;
 constexpr Cfg kCfg[kNumCfg + 1] = {{0, 0}, {128, 64}, {128, 64}, {256, 32}, {256, 32}, {256, 64}, {256, 64},
-                                   {64, 64}};
+                                   {64, 64}, {128, 64}, {128, 64}, {128, 32}, {128, 64}, {128, 64}, {64, 64},
+                                   {256, 64}};
 
 template <int EPI, int BN, int BKS, int NSR, int WM, int WN, int PF = 1>
 int launch(const uint16_t* x, const uint16_t* w, uint16_t* y, float* p, float* pv, int* pi, int M,
@@ -449,6 +635,13 @@ int launch_cfg(int cfg, const uint16_t* x, const uint16_t* w, uint16_t* y, float
     case 5: return launch<EPI, 256, 64, 2, 2, 2, 0>(x, w, y, p, pv, pi, M, N, K, S, n_valid, s, ldx, ldw);
     case 6: return launch<EPI, 256, 64, 2, 2, 4, 0>(x, w, y, p, pv, pi, M, N, K, S, n_valid, s, ldx, ldw);
     case 7: return launch<EPI, 64, 64, 3, 4, 2>(x, w, y, p, pv, pi, M, N, K, S, n_valid, s, ldx, ldw);
+    case 8: return launch<EPI, 128, 64, 3, 4, 2, 2>(x, w, y, p, pv, pi, M, N, K, S, n_valid, s, ldx, ldw);
+    case 9: return launch<EPI, 128, 64, 3, 4, 2, 3>(x, w, y, p, pv, pi, M, N, K, S, n_valid, s, ldx, ldw);
+    case 10: return launch<EPI, 128, 32, 6, 4, 2, 3>(x, w, y, p, pv, pi, M, N, K, S, n_valid, s, ldx, ldw);
+    case 11: return launch<EPI, 128, 64, 3, 4, 2, 5>(x, w, y, p, pv, pi, M, N, K, S, n_valid, s, ldx, ldw);
+    case 12: return launch<EPI, 128, 64, 3, 4, 2, 7>(x, w, y, p, pv, pi, M, N, K, S, n_valid, s, ldx, ldw);
+    case 13: return launch<EPI, 64, 64, 3, 4, 2, 5>(x, w, y, p, pv, pi, M, N, K, S, n_valid, s, ldx, ldw);
+    case 14: return launch<EPI, 256, 64, 2, 2, 4, 4>(x, w, y, p, pv, pi, M, N, K, S, n_valid, s, ldx, ldw);
     default: return -1;
   }
 }
@@ -516,4 +709,47 @@ int docqa_mgemm_ld(const void* X, int ldx, const void* W, int ldw, void* Y, floa
   if (glu) return launch_cfg<EPI_GLU>(cfg, x, w, (uint16_t*)Y, nullptr, nullptr, nullptr, M, N, K, 1, N, s, ldx, ldw);
   if (P) return launch_cfg<EPI_PARTIAL>(cfg, x, w, nullptr, P, nullptr, nullptr, M, N, K, S, N, s, ldx, ldw);
   return launch_cfg<EPI_BF16>(cfg, x, w, (uint16_t*)Y, nullptr, nullptr, nullptr, M, N, K, 1, N, s, ldx, ldw);
+}
+
+// stream-K over a persistent grid (mgemm_sk_kernel): epi 0 bf16 Y [M, N], 1 SwiGLU Y [M, N/2]
+// over 8-interleaved gate|up rows, 2 one fp32 slab P [1, M, N] (the split-K consumers with
+// S = 1).  part: >= docqa_mgemm_sk_part_floats(grid) floats; cnt: >= 2 * tiles ints, zero
+// before the first launch (each launch leaves them zero).  grid: the CU count (the host
+// shrinks it so no tile is cut into more than kSkMaxPieces pieces).
+int docqa_mgemm_sk_grid(int M, int N, int K, int cus) {
+  constexpr int BN = 128, BKS = 64;
+  if (M <= 0 || N % BN || K % (2 * BKS) || cus <= 0) return 0;
+  const long long units = K / (2 * BKS), T = (long long)((M + BM - 1) / BM) * (N / BN), U = T * units;
+  long long G = cus < U ? cus : U;
+  const long long per_min = (units + kSkMaxPieces - 2) / (kSkMaxPieces - 1);   // >= ceil(units / 4)
+  if (U / G < per_min) G = U / per_min;
+  return (int)(G < 1 ? 1 : G);
+}
+size_t docqa_mgemm_sk_part_floats(int grid) { return (size_t)grid * 2 * BM * 128; }
+int docqa_mgemm_sk_tiles(int M, int N) { return ((M + BM - 1) / BM) * (N / 128); }
+
+int docqa_mgemm_sk(const void* X, const void* W, void* Y, float* P, float* part, int* cnt, int M, int N, int K,
+                   int epi, int grid, hipStream_t s) {
+  constexpr int BN = 128, BKS = 64, NSR = 3, WM = 4, WN = 2;
+  if (M == 0) return 0;
+  if (M < 0 || N % BN || K % (2 * BKS) || grid <= 0 || part == nullptr || cnt == nullptr) return -1;
+  if (grid > docqa_mgemm_sk_grid(M, N, K, grid)) return -1;     // keeps pieces per tile bounded
+  if (!docqa_aligned16(X) || !docqa_aligned16(W) || !docqa_aligned16(part)) return -1;
+  if (epi == 2 ? !docqa_aligned16(P) : (Y == nullptr || !docqa_aligned16(Y))) return -1;
+  const int ntm = (M + BM - 1) / BM, ntn = N / BN, units = K / (2 * BKS);
+  const uint16_t *x = (const uint16_t*)X, *w = (const uint16_t*)W;
+  uint16_t* y = (uint16_t*)Y;
+  if (epi == 0)
+    mgemm_sk_kernel<EPI_BF16, BN, BKS, NSR, WM, WN><<<grid, WM * WN * 64, 0, s>>>(x, w, y, nullptr, part, cnt, M, N, K,
+                                                                               ntm, ntn, units, grid, K, K);
+  else if (epi == 1)
+    mgemm_sk_kernel<EPI_GLU, BN, BKS, NSR, WM, WN><<<grid, WM * WN * 64, 0, s>>>(x, w, y, nullptr, part, cnt, M, N, K,
+                                                                              ntm, ntn, units, grid, K, K);
+  else if (epi == 2)
+    mgemm_sk_kernel<EPI_PARTIAL, BN, BKS, NSR, WM, WN><<<grid, WM * WN * 64, 0, s>>>(x, w, nullptr, P, part, cnt, M, N,
+                                                                                  K, ntm, ntn, units, grid, K, K);
+  else
+    return -1;
+  DOCQA_CHECK_LAUNCH();
+  return 0;
 }
