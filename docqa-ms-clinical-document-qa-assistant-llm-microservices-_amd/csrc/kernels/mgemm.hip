@@ -418,39 +418,18 @@ __global__ __launch_bounds__(WM * WN * 64) void mgemm_kernel(const uint16_t* __r
 // The same tile body with the work split evenly over a persistent grid of G <= CU-count
 // workgroups (stream-K): the (tile, 128-deep K unit) iterations are dealt out in one
 // contiguous range per workgroup, so a grid whose tile count is not a multiple of the CU
-// count -- 144 tiles at 768 prefill rows of the 8B QKV, 224 at the batch-256 gate|up --
-// still keeps every CU busy to the end.  A tile whose K range is cut between workgroups is
-// finished in-launch: each piece draws an arrival ticket (agent-scope atomic); every piece
-// but the last arriver stores its fp32 accumulators write-through (sc1, lane-major: one
-// 1-KiB run per wave instruction) into its workgroup's slot and counts itself done; the last
-// arriver waits for those (they hold a ticket, so they are past their K loop: the wait is a
-// store's latency, never a dependency on unscheduled work), reads them with sc1 loads and
-// sums the pieces IN K ORDER with its own registers in its place -- the result does not
-// depend on which piece arrived last -- then runs the ordinary epilogue (bf16 / SwiGLU /
-// fp32 slab).  It re-arms the tile's two counters for the next launch (zeroed once at
-// allocation).  Hand-off form: cdna_hip_programming.md §6 Guideline 16 / MI355X_MICROARCH.md
-// table row "one lane of each storing workgroup ... agent-scope atomic add", sc1 both sides.
-// Reference: the prefill + generate of llm-qa/main.py:69,117 (served by Ollama there).
-// The hand-off's stores and loads are compiler-visible 8-byte agent-scope atomics
-// (global_store / global_load_dwordx2 ... sc1): the segment loop's register pressure makes
-// hipcc spill around the fixup, and a spill reload counted by hipcc's own vmcnt next to
-// inline-asm memory ops it cannot see reads its register too early (a wild address: the
-// first version of this kernel faulted).  The ring's inline-asm DMA is drained before.
-__device__ __forceinline__ void st16_wt(float* p, const f32x4& v) {
-  unsigned long long* q = reinterpret_cast<unsigned long long*>(p);
-  __hip_atomic_store(q, (unsigned long long)__float_as_uint(v[0]) | ((unsigned long long)__float_as_uint(v[1]) << 32),
-                     __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  __hip_atomic_store(q + 1, (unsigned long long)__float_as_uint(v[2]) | ((unsigned long long)__float_as_uint(v[3]) << 32),
-                     __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ f32x4 ld16_sc1(const float* p) {
-  const unsigned long long* q = reinterpret_cast<const unsigned long long*>(p);
-  const unsigned long long a = __hip_atomic_load(q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  const unsigned long long b = __hip_atomic_load(q + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  return f32x4{__uint_as_float((unsigned)a), __uint_as_float((unsigned)(a >> 32)), __uint_as_float((unsigned)b),
-               __uint_as_float((unsigned)(b >> 32))};
-}
-
+// count -- 144 tiles at 768 prefill rows of the 8B QKV, 48 of the O projection -- still keeps
+// every CU busy to the end.  Two launches, no inter-workgroup waits:
+//   * mgemm_sk_kernel: each workgroup walks its range; a tile it covers whole gets the
+//     ordinary epilogue (bf16 / SwiGLU / fp32 slab), a piece of a cut tile stores its fp32
+//     accumulators lane-major (one 1-KiB run per wave instruction) into its slot;
+//   * mgemm_sk_fixup_kernel: one workgroup per cut tile rebuilds the accumulators by
+//     summing the pieces IN K ORDER (bit-for-bit repeatable whatever the timing) and runs
+//     the same epilogue.
+// (A one-launch version -- tickets, the last arriving piece finishing the tile -- kept the
+// whole fixup in the segment loop's registers: hipcc spilled 130-330 VGPRs around it and the
+// loop lost to the plain grid; profiles/r6_mgemm_floor_probe.log "streamK".)
+// Reference: the prefill + generate of llm-qa/main.py:69,117 (Ollama's in the reference).
 constexpr int kSkMaxPieces = 5;      // host-side grid choice bounds a tile to <= 5 pieces
 
 // first workgroup whose unit range [ub, ue) holds unit u (ub(l) = l U / G)
@@ -461,85 +440,14 @@ __device__ __forceinline__ int sk_owner(long long u, long long U, int G) {
   return l;
 }
 
-template <int BN, int WM, int WN>
-__device__ __forceinline__ bool sk_fixup(f32x4 (&acc)[BM / WM / 16][BN / WN / 16], uint16_t* smem,
-                                         float* __restrict__ part, int* __restrict__ cnt, int t, int units,
-                                         long long U, int G, int l, int slot) {
-  constexpr int MI = BM / WM / 16, NJ = BN / WN / 16, Q = MI * NJ, NT = WM * WN * 64;
-  constexpr int QB = 2;
-  static_assert(Q % QB == 0, "fixup batches");
-  const int tid = threadIdx.x;
-  const long long t0 = (long long)t * units, t1 = t0 + units;
-  const int lf = sk_owner(t0, U, G), ll = sk_owner(t1 - 1, U, G);
-  const int n = ll - lf + 1, me = l - lf;
-  int* flag = reinterpret_cast<int*>(smem);        // the ring is drained: LDS is free
-  if (tid == 0) flag[0] = __hip_atomic_fetch_add(cnt + 2 * t, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  __syncthreads();
-  const int ticket = flag[0];
-  auto slot_of = [&](int lw) {                      // a partial piece: its workgroup's first or last
-    const long long ubw = ((long long)lw * U) / G;
-    return (size_t)(lw * 2 + (ubw >= t0 ? 0 : 1)) * (size_t)(Q * NT) * 4;
-  };
-  if (ticket < n - 1) {
-    float* dst = part + (size_t)(l * 2 + slot) * (size_t)(Q * NT) * 4;
-#pragma unroll
-    for (int i = 0; i < MI; ++i)
-#pragma unroll
-      for (int j = 0; j < NJ; ++j) st16_wt(dst + ((size_t)(i * NJ + j) * NT + tid) * 4, acc[i][j]);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (tid == 0) __hip_atomic_fetch_add(cnt + 2 * t + 1, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    return false;
-  }
-  // last arriver: the other n - 1 pieces hold tickets; wait until all are stored (bounded:
-  // a counter left dirty by an aborted launch must not hang the GPU -- the tile is then wrong)
-  if (tid == 0) {
-    int spins = 0;
-    while (__hip_atomic_load(cnt + 2 * t + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < n - 1 &&
-           ++spins < (1 << 22))
-      __builtin_amdgcn_s_sleep(2);
-    __hip_atomic_store(cnt + 2 * t, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __hip_atomic_store(cnt + 2 * t + 1, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  }
-  __syncthreads();
-  size_t off[kSkMaxPieces];
-#pragma unroll
-  for (int p = 0; p < kSkMaxPieces; ++p) off[p] = (p < n && p != me) ? slot_of(lf + p) : 0;
-#pragma unroll
-  for (int qb = 0; qb < Q / QB; ++qb) {
-    f32x4 buf[kSkMaxPieces][QB];
-#pragma unroll
-    for (int p = 0; p < kSkMaxPieces; ++p) {
-      if (p < n && p != me) {
-#pragma unroll
-        for (int qq = 0; qq < QB; ++qq)
-          buf[p][qq] = ld16_sc1(part + off[p] + ((size_t)(qb * QB + qq) * NT + tid) * 4);
-      }
-    }
-#pragma unroll
-    for (int qq = 0; qq < QB; ++qq) {
-      const int q = qb * QB + qq, i = q / NJ, j = q % NJ;
-      // K order: (((p0 + p1) + p2) ...), this workgroup's registers at position `me`
-      const f32x4 v = acc[i][j];
-      f32x4 sum = me == 0 ? v : buf[0][qq];
-#pragma unroll
-      for (int p = 1; p < kSkMaxPieces; ++p)
-        if (p < n) sum += (p == me ? v : buf[p][qq]);
-      acc[i][j] = sum;
-    }
-  }
-  return true;
-}
-
 template <int EPI, int BN, int BKS, int NSR, int WM, int WN>
 __global__ __launch_bounds__(WM * WN * 64) void mgemm_sk_kernel(const uint16_t* __restrict__ X,
                                                                 const uint16_t* __restrict__ W,
                                                                 uint16_t* __restrict__ Y, float* __restrict__ P,
-                                                                float* __restrict__ part, int* __restrict__ cnt,
-                                                                int M, int N, int K, int ntm, int ntn, int units,
-                                                                int G, int ldx, int ldw) {
+                                                                float* __restrict__ part, int M, int N, int K,
+                                                                int ntm, int ntn, int units, int G) {
   __shared__ __attribute__((aligned(16))) uint16_t smem[NSR * (BM + BN) * BKS];
-  constexpr int MI = BM / WM / 16, NJ = BN / WN / 16;
+  constexpr int MI = BM / WM / 16, NJ = BN / WN / 16, NT = WM * WN * 64;
   // consecutive logical ids on one XCD: its workgroups share the W columns of neighbouring
   // tiles (m-tiles fastest) in that XCD's L2
   const int l = xcd_remap(blockIdx.x, G);
@@ -557,16 +465,56 @@ __global__ __launch_bounds__(WM * WN * 64) void mgemm_sk_kernel(const uint16_t* 
     for (int i = 0; i < MI; ++i)
 #pragma unroll
       for (int j = 0; j < NJ; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-    mgemm_mainloop<BN, BKS, NSR, WM, WN, 1>(smem, X, W, M, kb * 2 * BKS, (ke - kb) * 2, m0, n0, ldx, ldw, acc);
-    bool mine = true;
-    if (kb != 0 || ke != units) mine = sk_fixup<BN, WM, WN>(acc, smem, part, cnt, t, units, U, G, l, slot);
-    if (mine) mgemm_epilogue<EPI, BN, WM, WN>(acc, smem, Y, P, nullptr, nullptr, M, N, m0, n0, 0, 0, 0, N);
-    // every wave is done with the epilogue scratch / ticket word before the next ring fill
-    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    mgemm_mainloop<BN, BKS, NSR, WM, WN, 1>(smem, X, W, M, kb * 2 * BKS, (ke - kb) * 2, m0, n0, K, K, acc);
+    if (kb == 0 && ke == units) {
+      mgemm_epilogue<EPI, BN, WM, WN>(acc, smem, Y, P, nullptr, nullptr, M, N, m0, n0, 0, 0, 0, N);
+    } else {
+      const int tid = threadIdx.x;
+      float* dst = part + (size_t)(l * 2 + slot) * (size_t)(MI * NJ * NT) * 4;
+#pragma unroll
+      for (int i = 0; i < MI; ++i)
+#pragma unroll
+        for (int j = 0; j < NJ; ++j)
+          *reinterpret_cast<f32x4*>(dst + ((size_t)(i * NJ + j) * NT + tid) * 4) = acc[i][j];
+    }
+    // every wave is done with the epilogue scratch before the next ring fill
     __syncthreads();
     u = (long long)t * units + ke;
     slot = 1;
   }
+}
+
+// one workgroup per tile (tiles the first kernel finished whole exit at once): the cut
+// tile's pieces summed in K order -> the ordinary epilogue
+template <int EPI, int BN, int WM, int WN>
+__global__ __launch_bounds__(WM * WN * 64) void mgemm_sk_fixup_kernel(const float* __restrict__ part,
+                                                                      uint16_t* __restrict__ Y,
+                                                                      float* __restrict__ P, int M, int N,
+                                                                      int ntm, int units, int G, long long U) {
+  __shared__ __attribute__((aligned(16))) uint16_t smem[8 * 16 * (BN / WN + 4) * 2];
+  constexpr int MI = BM / WM / 16, NJ = BN / WN / 16, Q = MI * NJ, NT = WM * WN * 64;
+  const int t = blockIdx.x;
+  const long long t0 = (long long)t * units;
+  const int lf = sk_owner(t0, U, G), ll = sk_owner(t0 + units - 1, U, G);
+  const int n = ll - lf + 1;
+  if (n == 1) return;                              // finished whole by one workgroup
+  const int tid = threadIdx.x;
+  f32x4 acc[MI][NJ];
+  for (int p = 0; p < n; ++p) {
+    const int lw = lf + p;
+    const long long ubw = ((long long)lw * U) / G;
+    const float* src = part + (size_t)(lw * 2 + (ubw >= t0 ? 0 : 1)) * (size_t)(Q * NT) * 4;
+    f32x4 v[Q];
+#pragma unroll
+    for (int q = 0; q < Q; ++q) v[q] = *reinterpret_cast<const f32x4*>(src + ((size_t)q * NT + tid) * 4);
+#pragma unroll
+    for (int q = 0; q < Q; ++q) {                  // K order: (((p0 + p1) + p2) ...)
+      if (p == 0) acc[q / NJ][q % NJ] = v[q];
+      else acc[q / NJ][q % NJ] += v[q];
+    }
+  }
+  const int m0 = (t % ntm) * BM, n0 = (t / ntm) * BN;
+  mgemm_epilogue<EPI, BN, WM, WN>(acc, smem, Y, P, nullptr, nullptr, M, N, m0, n0, 0, 0, 0, N);
 }
 
 // Variants (``cfg``): the tile width and wave layout
@@ -730,26 +678,34 @@ int docqa_mgemm_sk_tiles(int M, int N) { return ((M + BM - 1) / BM) * (N / 128);
 
 int docqa_mgemm_sk(const void* X, const void* W, void* Y, float* P, float* part, int* cnt, int M, int N, int K,
                    int epi, int grid, hipStream_t s) {
+  (void)cnt;
   constexpr int BN = 128, BKS = 64, NSR = 3, WM = 4, WN = 2;
   if (M == 0) return 0;
-  if (M < 0 || N % BN || K % (2 * BKS) || grid <= 0 || part == nullptr || cnt == nullptr) return -1;
+  if (M < 0 || N % BN || K % (2 * BKS) || grid <= 0 || part == nullptr) return -1;
   if (grid > docqa_mgemm_sk_grid(M, N, K, grid)) return -1;     // keeps pieces per tile bounded
   if (!docqa_aligned16(X) || !docqa_aligned16(W) || !docqa_aligned16(part)) return -1;
   if (epi == 2 ? !docqa_aligned16(P) : (Y == nullptr || !docqa_aligned16(Y))) return -1;
   const int ntm = (M + BM - 1) / BM, ntn = N / BN, units = K / (2 * BKS);
+  const long long U = (long long)ntm * ntn * units;
   const uint16_t *x = (const uint16_t*)X, *w = (const uint16_t*)W;
   uint16_t* y = (uint16_t*)Y;
-  if (epi == 0)
-    mgemm_sk_kernel<EPI_BF16, BN, BKS, NSR, WM, WN><<<grid, WM * WN * 64, 0, s>>>(x, w, y, nullptr, part, cnt, M, N, K,
-                                                                               ntm, ntn, units, grid, K, K);
-  else if (epi == 1)
-    mgemm_sk_kernel<EPI_GLU, BN, BKS, NSR, WM, WN><<<grid, WM * WN * 64, 0, s>>>(x, w, y, nullptr, part, cnt, M, N, K,
-                                                                              ntm, ntn, units, grid, K, K);
-  else if (epi == 2)
-    mgemm_sk_kernel<EPI_PARTIAL, BN, BKS, NSR, WM, WN><<<grid, WM * WN * 64, 0, s>>>(x, w, nullptr, P, part, cnt, M, N,
-                                                                                  K, ntm, ntn, units, grid, K, K);
-  else
+  const int T = ntm * ntn;
+  if (epi == 0) {
+    mgemm_sk_kernel<EPI_BF16, BN, BKS, NSR, WM, WN><<<grid, WM * WN * 64, 0, s>>>(x, w, y, nullptr, part, M, N, K,
+                                                                               ntm, ntn, units, grid);
+    mgemm_sk_fixup_kernel<EPI_BF16, BN, WM, WN><<<T, WM * WN * 64, 0, s>>>(part, y, nullptr, M, N, ntm, units, grid, U);
+  } else if (epi == 1) {
+    mgemm_sk_kernel<EPI_GLU, BN, BKS, NSR, WM, WN><<<grid, WM * WN * 64, 0, s>>>(x, w, y, nullptr, part, M, N, K,
+                                                                              ntm, ntn, units, grid);
+    mgemm_sk_fixup_kernel<EPI_GLU, BN, WM, WN><<<T, WM * WN * 64, 0, s>>>(part, y, nullptr, M, N, ntm, units, grid, U);
+  } else if (epi == 2) {
+    mgemm_sk_kernel<EPI_PARTIAL, BN, BKS, NSR, WM, WN><<<grid, WM * WN * 64, 0, s>>>(x, w, nullptr, P, part, M, N,
+                                                                                  K, ntm, ntn, units, grid);
+    mgemm_sk_fixup_kernel<EPI_PARTIAL, BN, WM, WN><<<T, WM * WN * 64, 0, s>>>(part, nullptr, P, M, N, ntm, units,
+                                                                            grid, U);
+  } else {
     return -1;
+  }
   DOCQA_CHECK_LAUNCH();
   return 0;
 }

@@ -284,7 +284,47 @@ class LlamaModel:
         n = self.embed.numel() + self.lm_head.numel() + self.final_norm.numel()
         for L in self.layers:
             n += sum(t.numel() for t in L.values())
+        for t in self._tiled_weights():
+            n += t.numel()
         return n * self.embed.element_size()
+
+    def _tiled_weights(self):
+        for w in [self.lm_head] + [L[k] for L in self.layers for k in ("qkv", "o", "gate_up", "down")]:
+            yield from getattr(w, "_docqa_tiled", {}).values()
+
+    def prepare_decode_weights(self, max_rows: int) -> int:
+        """Stage-tiled copies (ops.attach_tiled) of the projections and the LM head for the
+        mid-M decode GEMM tiles its plans use (decode buckets of up to ``max_rows`` rows -- the
+        LM head's copy only when that exceeds the skinny kernel's 32 -- and the short prefills
+        of <= ops.MID_M_MAX tokens; mgemm.hip: one
+        contiguous 16 KiB weight run per K stage instead of 128 scattered 128-B rows;
+        scripts/tiled_weight_ab.py).  The row-major weights stay for the prefill / skinny
+        kernels.  Returns the bytes added (0: off -- DOCQA_TILED_W=0, CPU, or no mid-M
+        bucket).  Call before the KV pool is sized from the free HBM."""
+        if not (self.layers and self.device.type == "cuda"):
+            return 0
+        L0 = self.layers[0]
+        # decode buckets up to max_rows, and the short prefills (<= ops.MID_M_MAX tokens) that
+        # take the same projection plans whatever the batch size
+        rows = (ops.MID_M_MIN + 64, 256, ops.MID_M_MAX)
+        bn_of = {cfg: bn for cfg, (_, bn) in ops._TILED_CFG.items()}
+        need: dict[str, set] = {k: set() for k in ("qkv", "o", "gate_up", "down")}
+        for M in rows:
+            for k in ("qkv", "o", "down"):
+                S, c = ops.mid_plan(M, *L0[k].shape)
+                if S and c in bn_of:
+                    need[k].add(bn_of[c])
+            S, c = ops.mid_plan(M, *L0["gate_up"].shape, glu=True)
+            if S and c in bn_of:
+                need["gate_up"].add(bn_of[c])
+        before = sum(t.numel() for t in self._tiled_weights())
+        for L in self.layers:
+            for k, bns in need.items():
+                for bn in bns:
+                    ops.attach_tiled(L[k], bn)
+        if self.lm_head.shape[0] % 256 == 0 and ops._LM_CFG in bn_of and max_rows > 32:
+            ops.attach_tiled(self.lm_head, bn_of[ops._LM_CFG])
+        return (sum(t.numel() for t in self._tiled_weights()) - before) * self.embed.element_size()
 
     # ------------------------------------------------------------------ forward
     def forward(self, input_ids: torch.Tensor, meta: AttnMeta, kv_caches: list,
@@ -498,7 +538,7 @@ class LlamaModel:
             x = x.index_select(0, logits_index)
         if greedy_ids:
             return self.greedy_ids(x)
-        return ops.prefill_linear(x, self.lm_head) if x.shape[0] > 512 else F.linear(x, self.lm_head)
+        return ops.lm_head_logits(x, self.lm_head)
 
     def forward_mixed(self, input_ids: torch.Tensor, n_dec: int, dmeta: AttnMeta, pmeta: AttnMeta,
                       kv_caches: list, logits_index: torch.Tensor) -> torch.Tensor:
@@ -585,11 +625,11 @@ class LlamaModel:
         if self.tp == 1:
             if fused:
                 return ops.lm_head_argmax(x, self.lm_head, self.cfg.vocab_size)
-            return self.greedy(F.linear(x, self.lm_head))
+            return self.greedy(ops.lm_head_logits(x, self.lm_head))
         if fused and self.vocab_valid > 0:
             ids, vals = ops.lm_head_argmax(x, self.lm_head, self.vocab_valid, with_values=True)
         else:
-            logits = F.linear(x, self.lm_head)[:, : max(1, self.vocab_valid)]
+            logits = ops.lm_head_logits(x, self.lm_head)[:, : max(1, self.vocab_valid)]
             ids = ops.argmax(logits)
             vals = logits.gather(1, ids[:, None])[:, 0].float()
         if self.vocab_valid == 0:
