@@ -826,43 +826,6 @@ at::Tensor mgemm_glu(const at::Tensor& x, const at::Tensor& w, int64_t cfg) {
 
 int64_t mgemm_tile_n(int64_t cfg) { return docqa_mgemm_tile_n((int)cfg); }
 
-// stream-K mid-M GEMM (mgemm.hip mgemm_sk_kernel): epi 0 bf16 [.., N], 1 SwiGLU over
-// 8-interleaved gate|up rows [.., N/2], 2 fp32 slab [1, M, N]; part / cnt: the caller's
-// workspace (ops.mgemm_sk: per device and stream, cnt zeroed once)
-at::Tensor mgemm_sk(const at::Tensor& x, const at::Tensor& w, int64_t epi, at::Tensor part, at::Tensor cnt,
-                    int64_t grid) {
-  CHECK_GPU(x); CHECK_BF16(x); CHECK_BF16(w); CHECK_CONTIG(x); CHECK_CONTIG(w);
-  CHECK_ALIGN16(x); CHECK_ALIGN16(w);
-  const int K = x.size(-1), N = w.size(0);
-  TORCH_CHECK(w.size(1) == K && N % 128 == 0 && K % 128 == 0, "mgemm_sk: N % 128, K % 128");
-  TORCH_CHECK(epi >= 0 && epi <= 2, "mgemm_sk: epi 0 (bf16), 1 (SwiGLU) or 2 (fp32 slab)");
-  const int M = x.numel() / K;
-  TORCH_CHECK(part.is_cuda() && part.scalar_type() == at::kFloat && part.is_contiguous() &&
-                  (size_t)part.numel() >= docqa_mgemm_sk_part_floats((int)grid),
-              "mgemm_sk: partial workspace too small");
-  TORCH_CHECK(cnt.is_cuda() && cnt.scalar_type() == at::kInt && cnt.is_contiguous() &&
-                  cnt.numel() >= 2 * docqa_mgemm_sk_tiles(M, N),
-              "mgemm_sk: ticket workspace too small");
-  c10::DeviceGuard g(x.device());
-  at::Tensor out;
-  if (epi == 2) {
-    out = at::empty({1, M, N}, x.options().dtype(at::kFloat));
-    CHECK_RC(docqa_mgemm_sk(x.data_ptr(), w.data_ptr(), nullptr, out.data_ptr<float>(), part.data_ptr<float>(),
-                            cnt.data_ptr<int>(), M, N, K, 2, (int)grid, stream()), "mgemm_sk");
-  } else {
-    auto sizes = x.sizes().vec();
-    sizes.back() = epi == 1 ? N / 2 : N;
-    out = at::empty(sizes, x.options());
-    CHECK_RC(docqa_mgemm_sk(x.data_ptr(), w.data_ptr(), out.data_ptr(), nullptr, part.data_ptr<float>(),
-                            cnt.data_ptr<int>(), M, N, K, (int)epi, (int)grid, stream()), "mgemm_sk");
-  }
-  return out;
-}
-
-int64_t mgemm_sk_grid(int64_t M, int64_t N, int64_t K, int64_t cus) {
-  return docqa_mgemm_sk_grid((int)M, (int)N, (int)K, (int)cus);
-}
-int64_t mgemm_sk_part_floats(int64_t grid) { return (int64_t)docqa_mgemm_sk_part_floats((int)grid); }
 
 // layout probe: x [M, K] / w [N, K] views with row strides >= K (stride(1) == 1); glu: the
 // SwiGLU epilogue over 8-interleaved gate|up rows -> [M, N / 2]; else splits >= 2 -> fp32
@@ -1297,9 +1260,6 @@ TORCH_LIBRARY(docqa, m) {
   m.def("pgemm_partial(Tensor x, Tensor w, int splits) -> Tensor");
   m.def("mgemm_argmax_val(Tensor x, Tensor w, int n_valid, int cfg=0) -> (Tensor, Tensor)");
   m.def("pgemm_ok(int M, int N, int K) -> bool", &pgemm_ok);
-  m.def("mgemm_sk(Tensor x, Tensor w, int epi, Tensor part, Tensor cnt, int grid) -> Tensor");
-  m.def("mgemm_sk_grid(int M, int N, int K, int cus) -> int", &mgemm_sk_grid);
-  m.def("mgemm_sk_part_floats(int grid) -> int", &mgemm_sk_part_floats);
   m.def("mgemm_ld(Tensor x, Tensor w, int splits, int cfg, bool glu) -> Tensor");
   m.def("group_persist_bins(int cap, int Hkv) -> int", &group_persist_bins);
   m.def("set_decode_trace(Tensor? buf) -> ()", &set_decode_trace);
@@ -1373,7 +1333,6 @@ TORCH_LIBRARY_IMPL(docqa, CUDA, m) {
   m.impl("mgemm_argmax", &mgemm_argmax);
   m.impl("pgemm", &pgemm);
   m.impl("mgemm_ld", &mgemm_ld);
-  m.impl("mgemm_sk", &mgemm_sk);
   m.impl("pgemm_partial", &pgemm_partial);
   m.impl("mgemm_argmax_val", &mgemm_argmax_val);
   m.impl("coarse_probes", &coarse_probes);

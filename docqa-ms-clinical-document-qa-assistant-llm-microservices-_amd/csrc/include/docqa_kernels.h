@@ -139,11 +139,6 @@ int docqa_mgemm_glu(const void* X, const void* W, void* Y, int M, int N, int K, 
 int docqa_mgemm_argmax(const void* X, const void* W, int64_t* out, float* outv, float* ws_v, int* ws_i, int M,
                        int N, int K, int n_valid, int cfg, hipStream_t s);
 int docqa_mgemm_tile_n(int cfg);
-int docqa_mgemm_sk_grid(int M, int N, int K, int cus);
-size_t docqa_mgemm_sk_part_floats(int grid);
-int docqa_mgemm_sk_tiles(int M, int N);
-int docqa_mgemm_sk(const void* X, const void* W, void* Y, float* P, float* part, int* cnt, int M, int N, int K,
-                   int epi, int grid, hipStream_t s);
 int docqa_mgemm_ld(const void* X, int ldx, const void* W, int ldw, void* Y, float* P, int M, int N, int K, int S,
                    int cfg, int glu, hipStream_t s);
 // IVF coarse quantizer for wide probes (coarse.hip): nprobe <= 512 nearest centroids per query

@@ -236,9 +236,6 @@ __device__ __forceinline__ void mgemm_mainloop(uint16_t* smem, const uint16_t* _
       bsrc[i] = W + (size_t)(n0 + r) * ldw + kbeg + lchunk(r, p % CPR) * 8;
   }
   const uint32_t base = lds_u32(smem);
-  // the ring's counted waits below must count only its own DMAs: retire anything hipcc left
-  // in flight before the first one (the stream-K loop spills around its fixup)
-  wait_vmcnt<0>();
   auto stage = [&](int kt) {
     const uint32_t slot = base + (uint32_t)((kt % NSR) * SLOT * 2);
     const int ko = kt * BKS;
@@ -414,109 +411,6 @@ __global__ __launch_bounds__(WM * WN * 64) void mgemm_kernel(const uint16_t* __r
                                             ntiles, n_valid, ldx, ldw);
 }
 
-// ------------------------------------------------------------------------------ stream-K
-// The same tile body with the work split evenly over a persistent grid of G <= CU-count
-// workgroups (stream-K): the (tile, 128-deep K unit) iterations are dealt out in one
-// contiguous range per workgroup, so a grid whose tile count is not a multiple of the CU
-// count -- 144 tiles at 768 prefill rows of the 8B QKV, 48 of the O projection -- still keeps
-// every CU busy to the end.  Two launches, no inter-workgroup waits:
-//   * mgemm_sk_kernel: each workgroup walks its range; a tile it covers whole gets the
-//     ordinary epilogue (bf16 / SwiGLU / fp32 slab), a piece of a cut tile stores its fp32
-//     accumulators lane-major (one 1-KiB run per wave instruction) into its slot;
-//   * mgemm_sk_fixup_kernel: one workgroup per cut tile rebuilds the accumulators by
-//     summing the pieces IN K ORDER (bit-for-bit repeatable whatever the timing) and runs
-//     the same epilogue.
-// (A one-launch version -- tickets, the last arriving piece finishing the tile -- kept the
-// whole fixup in the segment loop's registers: hipcc spilled 130-330 VGPRs around it and the
-// loop lost to the plain grid; profiles/r6_mgemm_floor_probe.log "streamK".)
-// Reference: the prefill + generate of llm-qa/main.py:69,117 (Ollama's in the reference).
-constexpr int kSkMaxPieces = 5;      // host-side grid choice bounds a tile to <= 5 pieces
-
-// first workgroup whose unit range [ub, ue) holds unit u (ub(l) = l U / G)
-__device__ __forceinline__ int sk_owner(long long u, long long U, int G) {
-  int l = (int)((u * G) / U);
-  while (l + 1 < G && ((long long)(l + 1) * U) / G <= u) ++l;
-  while (l > 0 && ((long long)l * U) / G > u) --l;
-  return l;
-}
-
-template <int EPI, int BN, int BKS, int NSR, int WM, int WN>
-__global__ __launch_bounds__(WM * WN * 64) void mgemm_sk_kernel(const uint16_t* __restrict__ X,
-                                                                const uint16_t* __restrict__ W,
-                                                                uint16_t* __restrict__ Y, float* __restrict__ P,
-                                                                float* __restrict__ part, int M, int N, int K,
-                                                                int ntm, int ntn, int units, int G) {
-  __shared__ __attribute__((aligned(16))) uint16_t smem[NSR * (BM + BN) * BKS];
-  constexpr int MI = BM / WM / 16, NJ = BN / WN / 16, NT = WM * WN * 64;
-  // consecutive logical ids on one XCD: its workgroups share the W columns of neighbouring
-  // tiles (m-tiles fastest) in that XCD's L2
-  const int l = xcd_remap(blockIdx.x, G);
-  const long long U = (long long)ntm * ntn * units;
-  const long long ub = ((long long)l * U) / G, ue = ((long long)(l + 1) * U) / G;
-  long long u = ub;
-  int slot = 0;
-  while (u < ue) {
-    const int t = (int)(u / units);
-    const int kb = (int)(u - (long long)t * units);
-    const int ke = (int)min((long long)units, ue - (long long)t * units);
-    const int m0 = (t % ntm) * BM, n0 = (t / ntm) * BN;
-    f32x4 acc[MI][NJ];
-#pragma unroll
-    for (int i = 0; i < MI; ++i)
-#pragma unroll
-      for (int j = 0; j < NJ; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-    mgemm_mainloop<BN, BKS, NSR, WM, WN, 1>(smem, X, W, M, kb * 2 * BKS, (ke - kb) * 2, m0, n0, K, K, acc);
-    if (kb == 0 && ke == units) {
-      mgemm_epilogue<EPI, BN, WM, WN>(acc, smem, Y, P, nullptr, nullptr, M, N, m0, n0, 0, 0, 0, N);
-    } else {
-      const int tid = threadIdx.x;
-      float* dst = part + (size_t)(l * 2 + slot) * (size_t)(MI * NJ * NT) * 4;
-#pragma unroll
-      for (int i = 0; i < MI; ++i)
-#pragma unroll
-        for (int j = 0; j < NJ; ++j)
-          *reinterpret_cast<f32x4*>(dst + ((size_t)(i * NJ + j) * NT + tid) * 4) = acc[i][j];
-    }
-    // every wave is done with the epilogue scratch before the next ring fill
-    __syncthreads();
-    u = (long long)t * units + ke;
-    slot = 1;
-  }
-}
-
-// one workgroup per tile (tiles the first kernel finished whole exit at once): the cut
-// tile's pieces summed in K order -> the ordinary epilogue
-template <int EPI, int BN, int WM, int WN>
-__global__ __launch_bounds__(WM * WN * 64) void mgemm_sk_fixup_kernel(const float* __restrict__ part,
-                                                                      uint16_t* __restrict__ Y,
-                                                                      float* __restrict__ P, int M, int N,
-                                                                      int ntm, int units, int G, long long U) {
-  __shared__ __attribute__((aligned(16))) uint16_t smem[8 * 16 * (BN / WN + 4) * 2];
-  constexpr int MI = BM / WM / 16, NJ = BN / WN / 16, Q = MI * NJ, NT = WM * WN * 64;
-  const int t = blockIdx.x;
-  const long long t0 = (long long)t * units;
-  const int lf = sk_owner(t0, U, G), ll = sk_owner(t0 + units - 1, U, G);
-  const int n = ll - lf + 1;
-  if (n == 1) return;                              // finished whole by one workgroup
-  const int tid = threadIdx.x;
-  f32x4 acc[MI][NJ];
-  for (int p = 0; p < n; ++p) {
-    const int lw = lf + p;
-    const long long ubw = ((long long)lw * U) / G;
-    const float* src = part + (size_t)(lw * 2 + (ubw >= t0 ? 0 : 1)) * (size_t)(Q * NT) * 4;
-    f32x4 v[Q];
-#pragma unroll
-    for (int q = 0; q < Q; ++q) v[q] = *reinterpret_cast<const f32x4*>(src + ((size_t)q * NT + tid) * 4);
-#pragma unroll
-    for (int q = 0; q < Q; ++q) {                  // K order: (((p0 + p1) + p2) ...)
-      if (p == 0) acc[q / NJ][q % NJ] = v[q];
-      else acc[q / NJ][q % NJ] += v[q];
-    }
-  }
-  const int m0 = (t % ntm) * BM, n0 = (t / ntm) * BN;
-  mgemm_epilogue<EPI, BN, WM, WN>(acc, smem, Y, P, nullptr, nullptr, M, N, m0, n0, 0, 0, 0, N);
-}
-
 // Variants (``cfg``): the tile width and wave layout
 //   1: BN 128, 64-deep stages x 3, waves 2 x 2 (128 x 64 each, 1 wave / SIMD)
 //   2: BN 128, 64-deep stages x 3, waves 4 x 2 ( 64 x 64 each, 2 waves / SIMD)
@@ -657,55 +551,4 @@ int docqa_mgemm_ld(const void* X, int ldx, const void* W, int ldw, void* Y, floa
   if (glu) return launch_cfg<EPI_GLU>(cfg, x, w, (uint16_t*)Y, nullptr, nullptr, nullptr, M, N, K, 1, N, s, ldx, ldw);
   if (P) return launch_cfg<EPI_PARTIAL>(cfg, x, w, nullptr, P, nullptr, nullptr, M, N, K, S, N, s, ldx, ldw);
   return launch_cfg<EPI_BF16>(cfg, x, w, (uint16_t*)Y, nullptr, nullptr, nullptr, M, N, K, 1, N, s, ldx, ldw);
-}
-
-// stream-K over a persistent grid (mgemm_sk_kernel): epi 0 bf16 Y [M, N], 1 SwiGLU Y [M, N/2]
-// over 8-interleaved gate|up rows, 2 one fp32 slab P [1, M, N] (the split-K consumers with
-// S = 1).  part: >= docqa_mgemm_sk_part_floats(grid) floats; cnt: >= 2 * tiles ints, zero
-// before the first launch (each launch leaves them zero).  grid: the CU count (the host
-// shrinks it so no tile is cut into more than kSkMaxPieces pieces).
-int docqa_mgemm_sk_grid(int M, int N, int K, int cus) {
-  constexpr int BN = 128, BKS = 64;
-  if (M <= 0 || N % BN || K % (2 * BKS) || cus <= 0) return 0;
-  const long long units = K / (2 * BKS), T = (long long)((M + BM - 1) / BM) * (N / BN), U = T * units;
-  long long G = cus < U ? cus : U;
-  const long long per_min = (units + kSkMaxPieces - 2) / (kSkMaxPieces - 1);   // >= ceil(units / 4)
-  if (U / G < per_min) G = U / per_min;
-  return (int)(G < 1 ? 1 : G);
-}
-size_t docqa_mgemm_sk_part_floats(int grid) { return (size_t)grid * 2 * BM * 128; }
-int docqa_mgemm_sk_tiles(int M, int N) { return ((M + BM - 1) / BM) * (N / 128); }
-
-int docqa_mgemm_sk(const void* X, const void* W, void* Y, float* P, float* part, int* cnt, int M, int N, int K,
-                   int epi, int grid, hipStream_t s) {
-  (void)cnt;
-  constexpr int BN = 128, BKS = 64, NSR = 3, WM = 4, WN = 2;
-  if (M == 0) return 0;
-  if (M < 0 || N % BN || K % (2 * BKS) || grid <= 0 || part == nullptr) return -1;
-  if (grid > docqa_mgemm_sk_grid(M, N, K, grid)) return -1;     // keeps pieces per tile bounded
-  if (!docqa_aligned16(X) || !docqa_aligned16(W) || !docqa_aligned16(part)) return -1;
-  if (epi == 2 ? !docqa_aligned16(P) : (Y == nullptr || !docqa_aligned16(Y))) return -1;
-  const int ntm = (M + BM - 1) / BM, ntn = N / BN, units = K / (2 * BKS);
-  const long long U = (long long)ntm * ntn * units;
-  const uint16_t *x = (const uint16_t*)X, *w = (const uint16_t*)W;
-  uint16_t* y = (uint16_t*)Y;
-  const int T = ntm * ntn;
-  if (epi == 0) {
-    mgemm_sk_kernel<EPI_BF16, BN, BKS, NSR, WM, WN><<<grid, WM * WN * 64, 0, s>>>(x, w, y, nullptr, part, M, N, K,
-                                                                               ntm, ntn, units, grid);
-    mgemm_sk_fixup_kernel<EPI_BF16, BN, WM, WN><<<T, WM * WN * 64, 0, s>>>(part, y, nullptr, M, N, ntm, units, grid, U);
-  } else if (epi == 1) {
-    mgemm_sk_kernel<EPI_GLU, BN, BKS, NSR, WM, WN><<<grid, WM * WN * 64, 0, s>>>(x, w, y, nullptr, part, M, N, K,
-                                                                              ntm, ntn, units, grid);
-    mgemm_sk_fixup_kernel<EPI_GLU, BN, WM, WN><<<T, WM * WN * 64, 0, s>>>(part, y, nullptr, M, N, ntm, units, grid, U);
-  } else if (epi == 2) {
-    mgemm_sk_kernel<EPI_PARTIAL, BN, BKS, NSR, WM, WN><<<grid, WM * WN * 64, 0, s>>>(x, w, nullptr, P, part, M, N,
-                                                                                  K, ntm, ntn, units, grid);
-    mgemm_sk_fixup_kernel<EPI_PARTIAL, BN, WM, WN><<<T, WM * WN * 64, 0, s>>>(part, nullptr, P, M, N, ntm, units,
-                                                                            grid, U);
-  } else {
-    return -1;
-  }
-  DOCQA_CHECK_LAUNCH();
-  return 0;
 }

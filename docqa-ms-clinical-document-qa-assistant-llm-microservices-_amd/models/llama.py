@@ -293,37 +293,20 @@ class LlamaModel:
             yield from getattr(w, "_docqa_tiled", {}).values()
 
     def prepare_decode_weights(self, max_rows: int) -> int:
-        """Stage-tiled copies (ops.attach_tiled) of the projections and the LM head for the
-        mid-M decode GEMM tiles its plans use (decode buckets of up to ``max_rows`` rows -- the
-        LM head's copy only when that exceeds the skinny kernel's 32 -- and the short prefills
-        of <= ops.MID_M_MAX tokens; mgemm.hip: one
-        contiguous 16 KiB weight run per K stage instead of 128 scattered 128-B rows;
-        scripts/tiled_weight_ab.py).  The row-major weights stay for the prefill / skinny
-        kernels.  Returns the bytes added (0: off -- DOCQA_TILED_W=0, CPU, or no mid-M
-        bucket).  Call before the KV pool is sized from the free HBM."""
-        if not (self.layers and self.device.type == "cuda"):
+        """Stage-tiled copy (ops.attach_tiled) of the LM head for the fused greedy-argmax
+        GEMM of decode buckets past the skinny kernel's 32 rows (mgemm.hip cfg 6 -> 14: one
+        contiguous 32 KiB weight run per 64-deep K stage instead of 256 scattered 128-B rows):
+        283.8 -> 264.4 us per batch-256 step, every round of the A/B
+        (profiles/r6_tiled_weight_ab_m256.log).  The projections gained nothing measurable
+        (0.97-1.02x) and keep one row-major copy.  Returns the bytes added (0: off --
+        DOCQA_TILED_W=0, CPU, <= 32 rows).  Call before the KV pool is sized from the free HBM."""
+        if not (self.layers and self.device.type == "cuda" and max_rows > 32):
             return 0
-        L0 = self.layers[0]
-        # decode buckets up to max_rows, and the short prefills (<= ops.MID_M_MAX tokens) that
-        # take the same projection plans whatever the batch size
-        rows = (ops.MID_M_MIN + 64, 256, ops.MID_M_MAX)
-        bn_of = {cfg: bn for cfg, (_, bn) in ops._TILED_CFG.items()}
-        need: dict[str, set] = {k: set() for k in ("qkv", "o", "gate_up", "down")}
-        for M in rows:
-            for k in ("qkv", "o", "down"):
-                S, c = ops.mid_plan(M, *L0[k].shape)
-                if S and c in bn_of:
-                    need[k].add(bn_of[c])
-            S, c = ops.mid_plan(M, *L0["gate_up"].shape, glu=True)
-            if S and c in bn_of:
-                need["gate_up"].add(bn_of[c])
+        bn = ops._TILED_CFG.get(ops._LM_CFG, (0, 0))[1]
+        if not bn or self.lm_head.shape[0] % bn:
+            return 0
         before = sum(t.numel() for t in self._tiled_weights())
-        for L in self.layers:
-            for k, bns in need.items():
-                for bn in bns:
-                    ops.attach_tiled(L[k], bn)
-        if self.lm_head.shape[0] % 256 == 0 and ops._LM_CFG in bn_of and max_rows > 32:
-            ops.attach_tiled(self.lm_head, bn_of[ops._LM_CFG])
+        ops.attach_tiled(self.lm_head, bn)
         return (sum(t.numel() for t in self._tiled_weights()) - before) * self.embed.element_size()
 
     # ------------------------------------------------------------------ forward

@@ -67,14 +67,6 @@ def main() -> None:
         a = nat.mgemm_glu(x, ws[0], 2) if glu else nat.mgemm(x, ws[0], S, 2)
         b = nat.mgemm_glu(x, wts[0], 11) if glu else nat.mgemm(x, wts[0], S, 11)
         res["tiledW_exact"] = bool(torch.equal(a, b))
-        # stream-K over the whole chip (one launch, bf16 / SwiGLU out)
-        cus = torch.cuda.get_device_properties(0).multi_processor_count
-        grid = nat.mgemm_sk_grid(M, N, K, cus)
-        part = torch.empty(nat.mgemm_sk_part_floats(grid), device="cuda")
-        cnt = torch.zeros(2 * ((M + 255) // 256) * (N // 128), dtype=torch.int32, device="cuda")
-        epi = 1 if glu else 0
-        t = timeit(lambda i: nat.mgemm_sk(x, ws[i % ncopy], epi, part, cnt, grid), iters)
-        res["streamK_us"], res["streamK_grid"] = round(t, 1), grid
         del wts
         print(json.dumps(res), flush=True)
         del ws
