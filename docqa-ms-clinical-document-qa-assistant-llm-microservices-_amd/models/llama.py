@@ -524,7 +524,7 @@ class LlamaModel:
         return ops.lm_head_logits(x, self.lm_head)
 
     def forward_mixed(self, input_ids: torch.Tensor, n_dec: int, dmeta: AttnMeta, pmeta: AttnMeta,
-                      kv_caches: list, logits_index: torch.Tensor) -> torch.Tensor:
+                      kv_caches: list, logits_index: torch.Tensor, return_logits: bool = False) -> torch.Tensor:
         """One forward over decode rows AND a prefill chunk (continuous batching without the
         prefill stall): rows [0, n_dec) are decode slots (one new token each, paged decode
         attention over their cache -- ``dmeta``, the decode step's metadata), rows
@@ -558,6 +558,8 @@ class LlamaModel:
             g = ops.prefill_glu(x, L["gate_up"])
             x = comm.tp_add_rmsnorm(ops.prefill_linear(g, L["down"]), residual, nxt, eps)
         assert x.shape[0] == M
+        if return_logits:          # tests: the selected rows' logits instead of their greedy ids
+            return ops.lm_head_logits(x.index_select(0, logits_index).contiguous(), self.lm_head)
         return self.greedy_ids(x.index_select(0, logits_index))
 
     def _attend_decode(self, qkv: torch.Tensor, meta: AttnMeta, kc, vc, M: int) -> torch.Tensor:

@@ -216,6 +216,95 @@ def _decode_ids(m, kv, prompts, tables, next_tok, BS):
     return m.forward(torch.tensor(next_tok, dtype=torch.int32, device="cuda"), meta, kv, greedy_ids=True)
 
 
+def _mixed_metas(prompts, tables, chunk_prompts, chunk_tables, starts, BS):
+    """(decode-step metadata of ``prompts`` -- one new token each after their prompt --,
+    prefill metadata of the chunks ``chunk_prompts[i][starts[i]:]`` over their cached heads)."""
+    from docqa_amd.models.llama import AttnMeta
+
+    B = len(prompts)
+    maxb = max(len(t) for t in tables)
+    bt = torch.zeros(B, maxb, dtype=torch.int32)
+    for i, t in enumerate(tables):
+        bt[i, :len(t)] = torch.tensor(t)
+    lens = [len(p) for p in prompts]
+    dmeta = AttnMeta(prefill=False, positions=torch.tensor(lens, dtype=torch.int32, device="cuda"),
+                     slot_mapping=torch.tensor([tables[i][lens[i] // BS] * BS + lens[i] % BS for i in range(B)],
+                                               dtype=torch.int32, device="cuda"),
+                     block_tables=bt.cuda(),
+                     context_lens=torch.tensor([n + 1 for n in lens], dtype=torch.int32, device="cuda"),
+                     max_context=maxb * BS)
+    pos, slots, cu = [], [], [0]
+    for p, t, s0 in zip(chunk_prompts, chunk_tables, starts):
+        pos += list(range(s0, len(p)))
+        slots += [t[i // BS] * BS + i % BS for i in range(s0, len(p))]
+        cu.append(cu[-1] + len(p) - s0)
+    mb = max(len(t) for t in chunk_tables)
+    cbt = torch.zeros(len(chunk_tables), mb, dtype=torch.int32)
+    for i, t in enumerate(chunk_tables):
+        cbt[i, :len(t)] = torch.tensor(t)
+    pmeta = AttnMeta(prefill=True, positions=torch.tensor(pos, dtype=torch.int32, device="cuda"),
+                     slot_mapping=torch.tensor(slots, dtype=torch.int32, device="cuda"),
+                     cu_seqlens=torch.tensor(cu, dtype=torch.int32, device="cuda"),
+                     max_len=max(len(p) - s0 for p, s0 in zip(chunk_prompts, starts)),
+                     block_tables=cbt.cuda(), prefix_lens=torch.tensor(starts, dtype=torch.int32, device="cuda"))
+    return dmeta, pmeta, cu
+
+
+def test_forward_mixed_native_vs_reference(native):
+    """a mixed step -- running decode rows AND prompt chunks in one forward
+    (LlamaModel.forward_mixed: every projection over all rows on the prefill GEMMs, attention
+    split by row kind, chunks attending their cached heads) -- on the HIP kernels against the
+    same step on the fp32 reference ops: logits of every decode row and of each chunk's last
+    token (teacher forcing), and the greedy pick wherever the reference's top-2 margin exceeds
+    the measured error."""
+    from docqa_amd.engine.kv_cache import KVCache
+    from docqa_amd.models.llama import LlamaConfig, LlamaModel
+
+    m = LlamaModel(LlamaConfig.preset("llama3-1b-test"), device="cuda", seed=12)
+    g = torch.Generator().manual_seed(13)
+    BS = 64
+    running = [torch.randint(0, 32000, (int(n),), generator=g).tolist() for n in (37, 150, 64, 201)]
+    # two new prompts: one from its start, one whose first 128 tokens are already cached
+    newp = [torch.randint(0, 32000, (n,), generator=g).tolist() for n in (90, 300)]
+    starts = [0, 128]
+    nxt = torch.randint(0, 32000, (len(running),), generator=g).tolist()
+    out = {}
+    for ref in (False, True):
+        kv = KVCache(m.cfg.layers, 64, m.hkv, m.cfg.head_dim, BS).caches
+        ctx = native.use_reference() if ref else torch.no_grad()
+        with ctx:
+            _, tables = _prefill_logits(m, kv, running, BS)
+            base = sum(len(t) for t in tables)
+            ctab = [list(range(base, base + 3)), list(range(base + 3, base + 9))]
+            # the cached head of the second new prompt
+            _prefill_into(m, kv, newp[1][:starts[1]], ctab[1], BS)
+            dmeta, pmeta, cu = _mixed_metas(running, tables, newp, ctab, starts, BS)
+            ids = torch.tensor(nxt + [t for p, s0 in zip(newp, starts) for t in p[s0:]], dtype=torch.int32,
+                               device="cuda")
+            rows = list(range(len(running))) + [len(running) + c - 1 for c in cu[1:]]
+            out[ref] = m.forward_mixed(ids, len(running), dmeta, pmeta, kv, torch.tensor(rows, device="cuda"),
+                                       return_logits=True).float()
+    a, b = out[False], out[True]
+    err = _rel(a, b)
+    assert err < 0.03, err
+    top2 = b.topk(2, dim=1).values
+    clear = (top2[:, 0] - top2[:, 1]) > 4 * err * b.abs().max()
+    assert torch.equal(a.argmax(1)[clear], b.argmax(1)[clear])
+
+
+def _prefill_into(m, kv, prompt, table, BS):
+    """Prefill one prompt into the given blocks (its K/V land in the cache)."""
+    from docqa_amd.models.llama import AttnMeta
+
+    n = len(prompt)
+    meta = AttnMeta(prefill=True, positions=torch.arange(n, dtype=torch.int32, device="cuda"),
+                    slot_mapping=torch.tensor([table[t // BS] * BS + t % BS for t in range(n)], dtype=torch.int32,
+                                              device="cuda"),
+                    cu_seqlens=torch.tensor([0, n], dtype=torch.int32, device="cuda"), max_len=n)
+    m.forward(torch.tensor(prompt, dtype=torch.int32, device="cuda"), meta, kv,
+              torch.tensor([n - 1], device="cuda"))
+
+
 def test_llama_graph_vs_eager(native, monkeypatch):
     monkeypatch.setenv("DOCQA_TUNE_DECODE", "0")  # same GEMM kernels on both paths
     from docqa_amd.engine.llm_engine import LLMEngine, SamplingParams
