@@ -273,10 +273,6 @@ class LLMEngine:
         HBM still free after the weights, minus the prefill activation headroom (the block
         prefix cache keeps every block the running batches do not need)."""
         self.model = model
-        # stage-tiled weight copies for the mid-M decode GEMM buckets, before the KV pool
-        # takes the free HBM (LlamaModel.prepare_decode_weights)
-        if hasattr(model, "prepare_decode_weights"):
-            model.prepare_decode_weights(max_batch)
         self.cfg = model.cfg
         self.device = model.device
         self.max_batch = max_batch

@@ -284,30 +284,7 @@ class LlamaModel:
         n = self.embed.numel() + self.lm_head.numel() + self.final_norm.numel()
         for L in self.layers:
             n += sum(t.numel() for t in L.values())
-        for t in self._tiled_weights():
-            n += t.numel()
         return n * self.embed.element_size()
-
-    def _tiled_weights(self):
-        for w in [self.lm_head] + [L[k] for L in self.layers for k in ("qkv", "o", "gate_up", "down")]:
-            yield from getattr(w, "_docqa_tiled", {}).values()
-
-    def prepare_decode_weights(self, max_rows: int) -> int:
-        """Stage-tiled copy (ops.attach_tiled) of the LM head for the fused greedy-argmax
-        GEMM of decode buckets past the skinny kernel's 32 rows (mgemm.hip cfg 6 -> 14: one
-        contiguous 32 KiB weight run per 64-deep K stage instead of 256 scattered 128-B rows):
-        283.8 -> 264.4 us per batch-256 step, every round of the A/B
-        (profiles/r6_tiled_weight_ab_m256.log).  The projections gained nothing measurable
-        (0.97-1.02x) and keep one row-major copy.  Returns the bytes added (0: off --
-        DOCQA_TILED_W=0, CPU, <= 32 rows).  Call before the KV pool is sized from the free HBM."""
-        if not (self.layers and self.device.type == "cuda" and max_rows > 32):
-            return 0
-        bn = ops._TILED_CFG.get(ops._LM_CFG, (0, 0))[1]
-        if not bn or self.lm_head.shape[0] % bn:
-            return 0
-        before = sum(t.numel() for t in self._tiled_weights())
-        ops.attach_tiled(self.lm_head, bn)
-        return (sum(t.numel() for t in self._tiled_weights()) - before) * self.embed.element_size()
 
     # ------------------------------------------------------------------ forward
     def forward(self, input_ids: torch.Tensor, meta: AttnMeta, kv_caches: list,

@@ -280,54 +280,11 @@ def mid_plan(M: int, N: int, K: int, glu: bool = False) -> tuple[int, int]:
     return S, _MID_CFG
 
 
-# ---------------------------------------------------------------- stage-tiled weight copies
-# mgemm.hip streams a weight tile as BN rows x 128 B per 64-deep K stage.  On row-major
-# [N, K] weights those are BN scattered 128-B pieces at a K x 2 B stride; on a stage-tiled
-# copy [N / BN][K / 64][BN][64] one contiguous BN x 128-B run (mgemm.hip WTILE; the
-# variants below are the same kernels, bit-exact).  Measured: scripts/tiled_weight_ab.py.
-# The copy hangs off the weight tensor (``_docqa_tiled[bn]``), built once by
-# :func:`attach_tiled` (LlamaModel.prepare_decode_weights) -- never inside a captured graph.
-_TILED_W = os.environ.get("DOCQA_TILED_W", "1") != "0"
-_TILED_CFG = {2: (11, 128), 7: (13, 64), 6: (14, 256)}     # row-major cfg -> (tiled cfg, BN)
-
-
-def tile_weight(w: torch.Tensor, bn: int) -> torch.Tensor:
-    """[N, K] -> the stage-tiled copy [N / BN][K / 64][BN][64], viewed as [N, K]."""
-    N, K = w.shape
-    return w.view(N // bn, bn, K // 64, 64).permute(0, 2, 1, 3).contiguous().view(N, K)
-
-
-def attach_tiled(w: torch.Tensor, bn: int) -> bool:
-    """Build (once) the stage-tiled copy of ``w`` for BN-row mgemm tiles."""
-    N, K = w.shape
-    if not (_TILED_W and w.is_cuda and N % bn == 0 and K % 64 == 0):
-        return False
-    d = getattr(w, "_docqa_tiled", None)
-    if d is None:
-        d = {}
-        w._docqa_tiled = d
-    if bn not in d:
-        d[bn] = tile_weight(w, bn)
-    return True
-
-
-def _tiled(w: torch.Tensor, cfg: int):
-    """(cfg, weight) to launch: the tiled variant when ``w`` carries its copy."""
-    if cfg == 0:
-        cfg = _MID_CFG
-    t = _TILED_CFG.get(cfg)
-    d = getattr(w, "_docqa_tiled", None)
-    if t is not None and d is not None and t[1] in d:
-        return t[0], d[t[1]]
-    return cfg, w
-
-
 def mgemm_partial(x, w, splits: int, cfg: int = 0):
     """Split-K partial slabs [S, M, N] fp32 of x @ w^T on the mid-M decode GEMM (S = 1:
     the bf16 product [M, N])."""
     if _gpu(x):
-        c, wt = _tiled(w, cfg)
-        return _native().mgemm(x.contiguous(), wt, splits, c)
+        return _native().mgemm(x.contiguous(), w, splits, cfg)
     if splits == 1:
         return torch.nn.functional.linear(x, w)
     K = w.shape[1]
@@ -349,8 +306,7 @@ def pgemm_partial(x, w, splits: int):
 def mgemm_glu(x, w_il, cfg: int = 0):
     """silu(x Wg^T) * (x Wu^T) for 8-interleaved gate|up weights on the mid-M decode GEMM."""
     if _gpu(x):
-        c, wt = _tiled(w_il, cfg)
-        return _native().mgemm_glu(x.contiguous(), wt, c)
+        return _native().mgemm_glu(x.contiguous(), w_il, cfg)
     return silu_mul(torch.nn.functional.linear(x, w_il), interleaved=True)
 
 
@@ -535,7 +491,6 @@ def lm_head_argmax(x, w, n_valid: int, cfg: int = -1, with_values: bool = False)
             return (ids, vals) if with_values else ids
         if cfg < 0:
             cfg = _LM_CFG if w.shape[0] % 256 == 0 else _MID_CFG
-        cfg, w = _tiled(w, cfg)
         if with_values:
             return _native().mgemm_argmax_val(x.contiguous(), w, int(n_valid), cfg)
         return _native().mgemm_argmax(x.contiguous(), w, int(n_valid), cfg)
@@ -550,7 +505,7 @@ def lm_head_logits(x, w):
     """bf16 logits x @ w^T of the LM head for SAMPLED rows (temperature > 0: the Ollama
     API's options), on the hand-written GEMMs at every row count: the skinny
     weight-streaming kernel up to 192 rows (dgemm.hip, one pass over the vocab), the mid-M
-    kernel with 256-wide tiles (and their stage-tiled copy) up to 512, the prefill kernels
+    kernel with 256-wide tiles up to 512, the prefill kernels
     beyond -- no library GEMM.  Greedy rows never get here: their
     argmax is fused into the GEMM (:func:`lm_head_argmax`)."""
     if _gpu(x):
@@ -560,8 +515,7 @@ def lm_head_logits(x, w):
             return _native().dgemm(x.contiguous(), w, 1)
         if 0 < M <= MID_M_MAX and N % 128 == 0 and K % 128 == 0 and not _MID_OFF:
             cfg = _LM_CFG if N % 256 == 0 else _MID_CFG
-            c, wt = _tiled(w, cfg)
-            return _native().mgemm(x.contiguous(), wt, 1, c)
+            return _native().mgemm(x.contiguous(), w, 1, cfg)
         return prefill_linear(x, w)
     return torch.nn.functional.linear(x, w)
 
