@@ -14,7 +14,7 @@ the MI355X knobs of this framework.
 | SEMANTIC_INDEXER_URL | http://semantic-indexer:8003 | synthese-comparative/core/config.py:10-13 |
 | LLM_QA_URL | http://llm-qa:8004 | synthese-comparative/core/config.py:16-19 |
 | USE_FAKE_RETRIEVAL / USE_FAKE_LLM | true / true | synthese-comparative/core/config.py:22-23 |
-| DEID_NER | auto | the spaCy NER of deid-service/anonymizer.py:29,41-45: "auto" runs the token classifier when NER_CHECKPOINT names one, "1" always (random-init weights when none), "0" never |
+| DEID_NER | auto | the spaCy NER of deid-service/anonymizer.py:29,41-45: "auto" runs the token classifier -- NER_CHECKPOINT's, else the shipped synthetic-trained one (deid/assets/ner-synthetic) --, "1" always, "0" never |
 | NER_CHECKPOINT | (empty) | Hugging Face BERT token-classification checkpoint directory for DEID_NER |
 | DEID_BATCH_DOCS | 32 | raw messages the deid worker drains into one packed NER forward |
 | MAX_BATCH | 256 on a GPU, 64 on CPU | llm-qa decode slots (the measured batch) |
@@ -121,7 +121,18 @@ class Settings:
             return True
         if self.deid_ner in ("0", "false", "no", "n", "off"):
             return False
-        return bool(self.ner_checkpoint)
+        from .deid.engine import shipped_ner
+
+        return bool(self.ner_checkpoint) or shipped_ner() is not None
+
+    def ner_source(self, fallback: str) -> str:
+        """The NER model to load: NER_CHECKPOINT, else the shipped synthetic-trained
+        checkpoint (deid/assets/ner-synthetic), else ``fallback`` (a random-init preset)."""
+        if self.ner_checkpoint:
+            return self.ner_checkpoint
+        from .deid.engine import shipped_ner
+
+        return shipped_ner() or fallback
 
     def resolved_device(self) -> str:
         if self.device != "auto":

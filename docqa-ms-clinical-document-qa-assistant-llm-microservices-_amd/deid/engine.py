@@ -21,6 +21,19 @@ from .recognizers import ENTITIES, Span, context_spans, pattern_spans, resolve_o
 
 NER_LABELS = ["O", "B-PER", "I-PER", "B-LOC", "I-LOC", "B-NRP", "I-NRP", "B-DATE", "I-DATE"]
 
+# The learned recognizer of the default deployment: a 2-layer BERT token classifier trained
+# from scratch on synthetic clinical notes with known PII spans (scripts/train_deid_ner.py;
+# held-out names / places / nationalities in ``eval.json``).  DEID_NER=auto runs it when no
+# NER_CHECKPOINT is given; a real checkpoint (NER_CHECKPOINT) replaces it.
+SHIPPED_NER = os.path.join(os.path.dirname(os.path.abspath(__file__)), "assets", "ner-synthetic")
+
+
+def shipped_ner() -> str | None:
+    """Path of the shipped NER checkpoint, or None if it is missing."""
+    ok = os.path.exists(os.path.join(SHIPPED_NER, "config.json")) and \
+        os.path.exists(os.path.join(SHIPPED_NER, "model.safetensors"))
+    return SHIPPED_NER if ok else None
+
 # Checkpoint label type -> Presidio entity (the six entities of
 # deid-service/anonymizer.py:43 plus the usual extra NER types).  Real token-classifier
 # checkpoints bring their own id2label (models/checkpoint.py:load_bert_token_classifier),

@@ -200,7 +200,7 @@ def load_bert_encoder(path, device="cuda") -> BertEncoder:
     return enc
 
 
-def load_bert_token_classifier(path, labels: list[str], device="cuda") -> BertTokenClassifier:
+def load_bert_token_classifier(path, labels: list[str], device="cuda", dtype=None) -> BertTokenClassifier:
     """BertForTokenClassification checkpoint (the NER de-identifier) ->
     :class:`BertTokenClassifier`; ``labels`` in the checkpoint's id2label order."""
     p = Path(path)
@@ -208,7 +208,9 @@ def load_bert_token_classifier(path, labels: list[str], device="cuda") -> BertTo
     cfg = bert_config_from_hf(hf, name=p.name, pooling="cls", normalize=False, max_seq_len=512)
     if "id2label" in hf:
         labels = [hf["id2label"][str(i)] for i in range(len(hf["id2label"]))]
-    clf = BertTokenClassifier(cfg, labels, device=device)
+    if dtype is None:
+        dtype = torch.bfloat16 if str(device).startswith("cuda") else torch.float32
+    clf = BertTokenClassifier(cfg, labels, device=device, dtype=dtype)
     sd = LazySafetensors(p)
     clf.load_state_dict_hf(sd, prefix=_bert_prefix(sd))
     n = len(clf.labels)

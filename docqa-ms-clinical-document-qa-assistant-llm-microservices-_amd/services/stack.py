@@ -115,7 +115,7 @@ class DocQAStack:
             ner_model = None
             use_ner = self.st.ner_enabled() if opts.ner_in_loop is None else opts.ner_in_loop
             if use_ner:
-                src = self.st.ner_checkpoint or opts.ner
+                src = self.st.ner_source(opts.ner)
                 ner_model = (ck.load_bert_token_classifier(src, NER_LABELS, device=dev)
                              if ck.is_checkpoint(src)
                              else BertTokenClassifier(BertConfig.preset(src), NER_LABELS, device=dev))

@@ -73,6 +73,12 @@ def main():
                 for cfg in (2, 6, 7):
                     if N % nat.mgemm_tile_n(cfg) == 0:
                         c[f"mgemm_{cfg}"] = (lambda cfg=cfg: nat.mgemm(x, w, 1, cfg))
+            # mid-M split-K slab plans (the consumer that sums them runs anyway: RoPE / add +
+            # RMSNorm, or for gate|up the SwiGLU of the slab sum); "_only" = the slabs alone
+            for cfg in (2, 7):
+                for S in (2, 3, 4, 8):
+                    if N % nat.mgemm_tile_n(cfg) == 0 and K % (S * 128) == 0:
+                        c[f"mS{S}c{cfg}_only"] = (lambda S=S, cfg=cfg: nat.mgemm(x, w, S, cfg))
             r = x.float() @ w.float().t()
             if epi:
                 r = ops.reference.silu_mul(r, interleaved=True).float()
@@ -82,6 +88,8 @@ def main():
                     y = fn().float()
                     if k.endswith("_only") or (k == "routed" and y.dim() == 3):
                         y = y.sum(0)
+                        if epi and y.shape[-1] == N:
+                            y = ops.reference.silu_mul(y.to(torch.bfloat16).float(), interleaved=True).float()
                     errs[k] = round((y - r).abs().max().item() / max(1e-6, r.abs().max().item()), 5)
                 except Exception as e:  # noqa: BLE001 -- a shape a candidate does not take
                     errs[k] = f"n/a: {str(e).splitlines()[0][:60]}"
@@ -99,6 +107,14 @@ def main():
             best = min(hand, key=lambda k: out[k + "_us"])
             out["best"] = best
             out["best_vs_lib"] = round(out["hipblaslt_us"] / out[best + "_us"], 3)
+            # slab plans priced with their consumer's extra slab reads (S fp32 slabs at ~5 TB/s,
+            # minus the one bf16 pass a plain consumer reads anyway)
+            slab = {k: out[k + "_us"] + (int(k[2:k.index("c")]) * 4 - 2) * M * N / 5e6
+                    for k in t if k.startswith("mS")}
+            if slab:
+                bs = min(slab, key=slab.get)
+                out["best_slab"], out["best_slab_priced_us"] = bs, round(slab[bs], 1)
+                out["best_slab_vs_lib"] = round(out["hipblaslt_us"] / slab[bs], 3)
             out["route"] = route
             if "routed" in t:
                 out["routed_vs_lib"] = round(out["hipblaslt_us"] / out["routed_us"], 3)

