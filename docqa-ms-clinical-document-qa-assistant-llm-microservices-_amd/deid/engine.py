@@ -109,6 +109,35 @@ def bio_to_spans(labels: list[str], offsets: list[tuple[int, int]], score: float
     return spans
 
 
+def word_labels(labels: list[str], word_ids: list) -> list[str]:
+    """WordPiece -> word-level BIO: every piece of a word takes its first piece's entity
+    type (I- after the first piece), so a label cannot start or stop inside a word (the
+    classifier is trained on whole-word spans; a stray piece label inside "Grenoble" or
+    "domicilié" would otherwise cut a span there)."""
+    out = list(labels)
+    prev_w, first = None, "O"
+    for i, w in enumerate(word_ids[:len(labels)]):    # a model with fewer positions labels a prefix
+        if w is not None and w == prev_w:
+            out[i] = "O" if first == "O" else "I-" + first.split("-", 1)[-1]
+        else:
+            first = labels[i]
+        prev_w = w
+    return out
+
+
+def merge_adjacent(spans: list[Span], text: str) -> list[Span]:
+    """Join consecutive model spans of one entity type separated by whitespace only (a
+    first name and a surname the classifier opened as two B- spans are one PERSON)."""
+    out: list[Span] = []
+    for sp in sorted(spans, key=lambda x: x.start):
+        if out and out[-1].entity_type == sp.entity_type and sp.start >= out[-1].end \
+                and text[out[-1].end:sp.start].isspace() and sp.start - out[-1].end <= 2:
+            out[-1] = Span(out[-1].start, sp.end, sp.entity_type, max(out[-1].score, sp.score))
+        else:
+            out.append(sp)
+    return out
+
+
 @dataclass
 class AnalyzerResult:
     entity_type: str
@@ -137,19 +166,20 @@ class DeidEngine:
             w = self.window - 2
             starts = list(range(0, max(1, n - w + self.stride), self.stride)) or [0]
             for s0 in starts:
-                windows.append((e.ids[s0:s0 + w], e.offsets[s0:s0 + w]))
+                windows.append((e.ids[s0:s0 + w], e.offsets[s0:s0 + w], e.word_ids[s0:s0 + w]))
                 owners.append(di)
                 if s0 + w >= n:
                     break
         cls = self.tok.tok.token_to_id("[CLS]") or 2
         sep = self.tok.tok.token_to_id("[SEP]") or 3
-        toks = [[cls] + ids + [sep] for ids, _ in windows]
+        toks = [[cls] + ids + [sep] for ids, _, _ in windows]
         preds = self.ner.predict(toks) if toks else []
         out: list[list[Span]] = [[] for _ in texts]
-        for (ids, offs), owner, p in zip(windows, owners, preds):
+        for (ids, offs, wids), owner, p in zip(windows, owners, preds):
             labels = [self.ner.labels[i] if i < len(self.ner.labels) else "O" for i in p[1:-1]]
+            labels = word_labels(labels, list(wids))
             out[owner] += bio_to_spans(labels, list(offs), label_map=self.label_map)
-        return out
+        return [merge_adjacent(sp, t) for sp, t in zip(out, texts)]
 
     def analyze_batch(self, texts: list[str], entities=None) -> list[list[AnalyzerResult]]:
         ents = list(entities or ENTITIES)

@@ -220,6 +220,16 @@ def make_doc(r: random.Random, P: dict) -> Doc:
         pl = r.sample(syn.PLANTS, 2)
         d.add(f"Prescription : {pl[0][0]} ({pl[0][2]}) {r.randint(3, 15)} g, {pl[1][0]} en décoction.")
 
+    def s_herbs(d):
+        # exotic NON-entity words (pinyin / Latin herb names and made-up ones): a rare-looking
+        # word is not a name by itself -- the context decides
+        pl = r.choice(syn.PLANTS)
+        herb = " ".join(_pseudo(r, 1, 2) for _ in range(r.randint(1, 3)))
+        d.add(r.choice([f"Ajout de {herb} {r.randint(3, 15)} g et {pl[2]} {r.randint(3, 15)} g.",
+                        f"Formule {herb} ({pl[1]}) : {pl[0]}, {r.randint(3, 15)} g par jour.",
+                        f"Herbs: {pl[2]}, {herb}, {r.choice(syn.MEDS)}.",
+                        f"Décoction de {herb} pendant {r.randint(2, 8)} semaines, puis {pl[2]}."]))
+
     def s_origin(d):
         d.add(r.choice(["Patient d'origine ", "Patiente de nationalité ", "Of ", "Famille "]))
         d.add(_pick(r, P, "nrp"), "NRP")
@@ -227,7 +237,7 @@ def make_doc(r: random.Random, P: dict) -> Doc:
         d.add(_pick(r, P, "city"), "LOC").add(".")
 
     bank = [s_consult, s_patient, s_motif, s_follow, s_treat, s_exam, s_family, s_ctrl, s_free, s_plants,
-            s_origin]
+            s_origin, s_origin, s_herbs, s_herbs]
     sents = [s_consult, s_patient] + r.sample(bank, r.randint(2, 6))
     for i, fn in enumerate(sents):
         if i:
@@ -332,7 +342,7 @@ class TinyBertNER(nn.Module):
         (out / "config.json").write_text(json.dumps(cfg, indent=1))
 
 
-def batches(data, bs, r, drop: float = 0.0, vocab: int = 0):
+def batches(data, bs, r, drop: float = 0.0, vocab: int = 0, ent_drop: float = 0.0):
     idx = list(range(len(data)))
     while True:
         r.shuffle(idx)
@@ -348,30 +358,32 @@ def batches(data, bs, r, drop: float = 0.0, vocab: int = 0):
                 xt = torch.tensor(x)
                 yt = torch.tensor(y)
                 if drop > 0:
-                    # entity pieces swapped for random vocabulary ids: the label must come
-                    # from the surrounding words, not from memorised pieces
-                    hit = (yt > 0) & (torch.rand(n) < drop)
-                    xt = torch.where(hit, torch.randint(5, vocab, (n,)), xt)
+                    # pieces (of any word) swapped for [UNK]: an entity's label must also come
+                    # from the surrounding words, and [UNK] alone is no entity cue
+                    hit = torch.rand(n) < torch.where(yt > 0, torch.full((n,), max(drop, ent_drop)),
+                                                      torch.full((n,), drop))
+                    xt = torch.where(hit, torch.full_like(xt, UNK_ID), xt)
                 ids[b, 1:n + 1] = xt
                 lab[b, 1:n + 1] = yt
                 mask[b, :n + 2] = True
             yield ids, lab, mask
 
 
-CLS_ID, SEP_ID = 2, 3
+CLS_ID, SEP_ID, UNK_ID = 2, 3, 1
 
 
 def span_eval(model_predict, docs, tok):
     """Span-level precision / recall / F1 per entity type: a predicted span counts when it
     covers exactly a gold span's characters (after trimming whitespace)."""
-    from docqa_amd.deid.engine import bio_to_spans
+    from docqa_amd.deid.engine import bio_to_spans, merge_adjacent, word_labels
 
     tp, fp, fn = {}, {}, {}
     for d in docs:
         e = tok.encode(d.text, add_special_tokens=False)
         pred = model_predict([[CLS_ID] + e.ids[:254] + [SEP_ID]])[0][1:-1]
-        labels = [NER_LABELS[i] for i in pred]
-        spans = {(s.start, s.end, s.entity_type) for s in bio_to_spans(labels, list(e.offsets[:254]))}
+        labels = word_labels([NER_LABELS[i] for i in pred], list(e.word_ids[:254]))
+        spans = {(s.start, s.end, s.entity_type)
+                 for s in merge_adjacent(bio_to_spans(labels, list(e.offsets[:254])), d.text)}
         ent = {"PER": "PERSON", "LOC": "LOCATION", "NRP": "NRP", "DATE": "DATE_TIME"}
         gold = {(a, b, ent[t]) for a, b, t in d.spans if b <= (e.offsets[:254][-1][1] if e.offsets else 0)}
         for g in gold:
@@ -390,7 +402,7 @@ def span_eval(model_predict, docs, tok):
 
 
 def main():
-    global CLS_ID, SEP_ID
+    global CLS_ID, SEP_ID, UNK_ID
     ap = argparse.ArgumentParser()
     ap.add_argument("--steps", type=int, default=2500)
     ap.add_argument("--docs", type=int, default=12000)
@@ -399,14 +411,16 @@ def main():
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--pseudo", type=float, default=0.6,
                     help="share of names / places / nationalities drawn as made-up words in training")
-    ap.add_argument("--tok-drop", type=float, default=0.1,
-                    help="share of entity tokens replaced by a random vocabulary token per batch")
+    ap.add_argument("--tok-drop", type=float, default=0.08,
+                    help="share of word pieces replaced by [UNK] per batch")
+    ap.add_argument("--ent-drop", type=float, default=0.25,
+                    help="share of ENTITY word pieces replaced by [UNK] (the label must come from context)")
     a = ap.parse_args()
     torch.manual_seed(a.seed)
     torch.set_num_threads(8)
     wp = WordPieceTokenizer()
     tok = wp.tok
-    CLS_ID, SEP_ID = tok.token_to_id("[CLS]"), tok.token_to_id("[SEP]")
+    CLS_ID, SEP_ID, UNK_ID = tok.token_to_id("[CLS]"), tok.token_to_id("[SEP]"), tok.token_to_id("[UNK]")
     vocab = wp.vocab_size
     train_pool, held_pool = _pools()
     train_pool["pseudo"] = a.pseudo
@@ -419,7 +433,7 @@ def main():
     opt = torch.optim.AdamW(model.parameters(), lr=2e-3, weight_decay=0.01)
     sched = torch.optim.lr_scheduler.LambdaLR(
         opt, lambda s: min(1.0, (s + 1) / 200) * max(0.05, 1 - s / a.steps))
-    it = batches(data, a.bs, random.Random(a.seed + 1), a.tok_drop, vocab)
+    it = batches(data, a.bs, random.Random(a.seed + 1), a.tok_drop, vocab, a.ent_drop)
     t0 = time.time()
     model.train()
     for step in range(a.steps):
@@ -433,6 +447,16 @@ def main():
         if step % 250 == 0 or step == a.steps - 1:
             print(f"[ner] step {step} loss {loss.item():.4f} {time.time() - t0:.0f}s", flush=True)
     model.eval()
+    # word pieces that never occurred in training keep a meaningless (decayed random)
+    # embedding: give them the [UNK] row, which training taught to mean "some word -- read
+    # the context" (a held-out nationality like 'espagnole' is one such piece)
+    seen_ids = torch.zeros(vocab, dtype=torch.bool)
+    for x, _ in data:
+        seen_ids[torch.tensor(x)] = True
+    seen_ids[[CLS_ID, SEP_ID, UNK_ID, 0]] = True
+    with torch.no_grad():
+        model.wte.weight[~seen_ids] = model.wte.weight[UNK_ID].clone()
+    print(f"[ner] {int(seen_ids.sum())} of {vocab} pieces seen in training; the rest map to [UNK]", flush=True)
 
     @torch.no_grad()
     def predict(tl):
@@ -443,7 +467,7 @@ def main():
     held = [make_doc(rh, held_pool) for _ in range(400)]
     seen = [make_doc(random.Random(778), train_pool) for _ in range(200)]
     report = {"held_out_pools": span_eval(predict, held, tok), "training_pools": span_eval(predict, seen, tok),
-              "steps": a.steps, "docs": a.docs, "pseudo": a.pseudo, "tok_drop": a.tok_drop, "windows": len(data), "train_s": round(time.time() - t0, 1),
+              "steps": a.steps, "docs": a.docs, "pseudo": a.pseudo, "tok_drop": a.tok_drop, "ent_drop": a.ent_drop, "windows": len(data), "train_s": round(time.time() - t0, 1),
               "params": sum(p.numel() for p in model.parameters())}
     print(json.dumps(report), flush=True)
     out = Path(a.out)

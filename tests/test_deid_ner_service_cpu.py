@@ -94,9 +94,14 @@ def test_deid_worker_poison_message_isolated():
 
 
 def test_settings_ner_switch(monkeypatch):
+    from docqa_amd.deid import engine as deid_engine
+
     monkeypatch.delenv("DEID_NER", raising=False)
     monkeypatch.delenv("NER_CHECKPOINT", raising=False)
-    assert Settings().ner_enabled() is False            # auto, no checkpoint: regex + context only
+    # auto: the shipped synthetic-note classifier (deid/assets/ner-synthetic) when present
+    assert Settings().ner_enabled() is (deid_engine.shipped_ner() is not None)
+    monkeypatch.setattr(deid_engine, "shipped_ner", lambda: None)
+    assert Settings().ner_enabled() is False            # auto, nothing to load: regex + context only
     monkeypatch.setenv("NER_CHECKPOINT", "/models/clinical-ner")
     assert Settings().ner_enabled() is True             # auto with a checkpoint
     monkeypatch.setenv("DEID_NER", "0")
