@@ -167,6 +167,19 @@ at::Tensor rope_cache_splitk(const at::Tensor& P, const at::Tensor& positions, c
   return qkv;
 }
 
+// split-K SwiGLU consumer: P [S, T, 2I] fp32 slabs of an 8-interleaved gate|up projection
+// -> [T, I] bf16 silu(gate) * up
+at::Tensor silu_mul_splitk(const at::Tensor& P) {
+  CHECK_GPU(P); CHECK_CONTIG(P); CHECK_ALIGN16(P);
+  TORCH_CHECK(P.scalar_type() == at::kFloat && P.dim() == 3, "silu_mul_splitk: float32 [S, T, 2I]");
+  const int S = P.size(0), T = P.size(1), I2 = P.size(2);
+  TORCH_CHECK(I2 % 16 == 0, "silu_mul_splitk: 2I % 16");
+  c10::DeviceGuard g(P.device());
+  auto out = at::empty({T, I2 / 2}, P.options().dtype(at::kBFloat16));
+  CHECK_RC(docqa_silu_mul_splitk(P.data_ptr<float>(), out.data_ptr(), S, T, I2 / 2, stream()), "silu_mul_splitk");
+  return out;
+}
+
 at::Tensor silu_mul(const at::Tensor& gu, bool interleaved) {
   CHECK_GPU(gu); CHECK_BF16(gu); CHECK_CONTIG(gu);
   const int I2 = gu.size(-1);
@@ -1215,6 +1228,7 @@ TORCH_LIBRARY(docqa, m) {
   m.def("rope_cache(Tensor(a!) qkv, Tensor positions, Tensor cos_sin, Tensor? slot_mapping, "
         "Tensor(b!) k_cache, Tensor(c!) v_cache, int Hq, int Hkv, int D) -> ()");
   m.def("silu_mul(Tensor gu, bool interleaved=False) -> Tensor");
+  m.def("silu_mul_splitk(Tensor P) -> Tensor");
   m.def("bias_act(Tensor x, Tensor bias, Tensor? residual, bool gelu) -> Tensor");
   m.def("embedding(Tensor ids, Tensor table) -> Tensor");
   m.def("bert_embed_ln(Tensor ids, Tensor pos, Tensor? token_type, Tensor wte, Tensor wpe, "
@@ -1303,6 +1317,7 @@ TORCH_LIBRARY_IMPL(docqa, CUDA, m) {
   m.impl("layernorm", &layernorm);
   m.impl("rope_cache", &rope_cache);
   m.impl("silu_mul", &silu_mul);
+  m.impl("silu_mul_splitk", &silu_mul_splitk);
   m.impl("bias_act", &bias_act);
   m.impl("embedding", &embedding);
   m.impl("bert_embed_ln", &bert_embed_ln);

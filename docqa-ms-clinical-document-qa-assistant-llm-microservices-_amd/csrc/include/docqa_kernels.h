@@ -20,6 +20,7 @@ int docqa_rope_cache(void* qkv, const int* positions, const float* cos_sin,
                      int Hkv, int D, int row_stride, int BS, hipStream_t s);
 
 int docqa_silu_mul(const void* gu, void* out, int T, int I, int interleaved, hipStream_t s);
+int docqa_silu_mul_splitk(const float* P, void* out, int S, int T, int I, hipStream_t s);
 int docqa_bias_act(const void* x, const void* bias, const void* res, void* out, int T, int N,
                    int gelu, hipStream_t s);
 
@@ -147,7 +148,6 @@ int docqa_coarse_probes(const float* cent, const float* cnorm, int nlist, int d,
 bool docqa_pgemm_ok(int M, int N, int K);
 int docqa_pgemm(const void* A, const void* W, void* C, float* P, int M, int N, int K, int S, int epi,
                 hipStream_t s);
-
 int docqa_knn_workspace_blocks(int N);
 int docqa_knn_kpad(int k);
 int docqa_knn(const void* xb, const float* norms, int N, int d, int is_bf16, const float* xq,

@@ -37,6 +37,38 @@ __global__ __launch_bounds__(256) void silu_mul_kernel(const uint16_t* __restric
   }
 }
 
+// split-K SwiGLU consumer: P [S, T, 2I] fp32 slabs of an 8-interleaved gate|up GEMM ->
+// out [T, I] = silu(bf16(sum gate)) * bf16(sum up), slabs summed in slab order (the rounding
+// of the fused-epilogue GEMMs: the gate / up values as the bf16 GEMM output).  The gate|up
+// projection at prefill sizes whose 256 x 256 tiles cannot fill the chip (the 70B TP-8
+// shard: 56 tiles at 512 rows) is split over K into these slabs (pgemm.hip EPI_PARTIAL).
+__global__ __launch_bounds__(256) void silu_mul_splitk_kernel(const float* __restrict__ P,
+                                                              uint16_t* __restrict__ out, int S, int T, int I) {
+  const int cpr = I >> 3;
+  const int total = T * cpr;
+  const size_t slab4 = (size_t)T * (size_t)(2 * I) / 4;   // one slab in float4
+  for (int idx = blockIdx.x * blockDim.x + threadIdx.x; idx < total; idx += gridDim.x * blockDim.x) {
+    const int t = idx / cpr;
+    const int c = idx - t * cpr;
+    const float4* p = reinterpret_cast<const float4*>(P + (size_t)t * (size_t)(2 * I)) + 4 * c;
+    float4 v[4] = {p[0], p[1], p[2], p[3]};
+    for (int sl = 1; sl < S; ++sl) {
+      const float4* q = p + sl * slab4;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const float4 w = q[j];
+        v[j].x += w.x; v[j].y += w.y; v[j].z += w.z; v[j].w += w.w;
+      }
+    }
+    const float g[8] = {v[0].x, v[0].y, v[0].z, v[0].w, v[1].x, v[1].y, v[1].z, v[1].w};
+    const float u[8] = {v[2].x, v[2].y, v[2].z, v[2].w, v[3].x, v[3].y, v[3].z, v[3].w};
+    float o[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) o[j] = silu(bf2f(f2bf(g[j]))) * bf2f(f2bf(u[j]));
+    reinterpret_cast<uint4*>(out + (size_t)t * I)[c] = pack8(o);
+  }
+}
+
 template <bool GELU, bool RES>
 __global__ __launch_bounds__(256) void bias_act_kernel(const uint16_t* __restrict__ x,
                                                        const uint16_t* __restrict__ bias,
@@ -76,6 +108,15 @@ int docqa_silu_mul(const void* gu, void* out, int T, int I, int interleaved, hip
   else
     silu_mul_kernel<false><<<grid_for((size_t)T * (I / 8)), 256, 0, s>>>((const uint16_t*)gu,
                                                                         (uint16_t*)out, T, I);
+  DOCQA_CHECK_LAUNCH();
+  return 0;
+}
+
+int docqa_silu_mul_splitk(const float* P, void* out, int S, int T, int I, hipStream_t s) {
+  if (I % 8 != 0 || S < 1 || (long long)T * (I / 8) >= (1LL << 31)) return -1;
+  if (T == 0) return 0;
+  if (!docqa_aligned16(P) || !docqa_aligned16(out)) return -1;
+  silu_mul_splitk_kernel<<<grid_for((size_t)T * (I / 8)), 256, 0, s>>>(P, (uint16_t*)out, S, T, I);
   DOCQA_CHECK_LAUNCH();
   return 0;
 }

@@ -86,39 +86,12 @@ __device__ __forceinline__ void glds_pair(const void* sbase, uint32_t v0, uint32
 
 __device__ __forceinline__ float silu_f(float x) { return x / (1.f + __expf(-x)); }
 
-template <int EPI>
-__global__ __launch_bounds__(512, 2) void pgemm_kernel(const uint16_t* __restrict__ A,
-                                                      const uint16_t* __restrict__ W,
-                                                      uint16_t* __restrict__ C, float* __restrict__ P,
-                                                      int M, int N, int K, int ntm, int ntn, int S, int Ks) {
-  __shared__ __attribute__((aligned(16))) char smem[LDS_B];
-  const int nwg = ntm * ntn;
-  // split-K (decode-sized M): workgroup -> (tile, K slice).  With S | 8 and whole rounds of
-  // 8, the workgroups of one XCD all take the same slice, so that XCD's L2 holds just that
-  // slice of A -- re-read by every tile (cf. mgemm.hip)
-  int tile_id, slice = 0;
-  if (S == 1) {
-    tile_id = xcd_remap(blockIdx.x, nwg);
-  } else if (8 % S == 0 && (nwg * S) % 8 == 0) {
-    const int xcd = blockIdx.x & 7, j = blockIdx.x >> 3;
-    slice = xcd % S;
-    tile_id = j * (8 / S) + xcd / S;
-  } else {
-    tile_id = blockIdx.x % nwg;
-    slice = blockIdx.x / nwg;
-  }
-  const int kbeg = slice * Ks;
-  const int wg = tile_id;
-  // groups of GM m-tiles x all n-tiles: consecutive ids (one XCD's concurrent workgroups)
-  // form a GM x (32 / GM) block of output tiles
-  constexpr int GM = 4;
-  const int per_group = GM * ntn;
-  const int grp = wg / per_group, first_m = grp * GM;
-  const int gm = min(ntm - first_m, GM);
-  const int rem = wg - grp * per_group;
-  const int bm = first_m + rem % gm, bn = rem / gm;
-  const int m0 = bm * BM, n0 = bn * BN;
-
+// K range [kbeg, kbeg + 128 nit) of the 256 x 256 output tile at (m0, n0) into acc (zeroed
+// here), nit >= 1.  Returns with the wave rows re-aligned and every LDS buffer drained, so
+// the caller may reuse the LDS as epilogue scratch.
+__device__ __forceinline__ void pgemm_mainloop(char* smem, const uint16_t* __restrict__ A,
+                                               const uint16_t* __restrict__ W, int M, int K, int m0, int n0,
+                                               int kbeg, int nit, f32x4 (&acc)[2][4][2][2]) {
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wr = wave >> 2, wc = wave & 3;
@@ -149,7 +122,6 @@ __global__ __launch_bounds__(512, 2) void pgemm_kernel(const uint16_t* __restric
     glds_pair(base, soff[h][0], soff[h][1], d, d + 8 * 1024);
   };
 
-  f32x4 acc[2][4][2][2];
 #pragma unroll
   for (int a = 0; a < 2; ++a)
 #pragma unroll
@@ -218,8 +190,6 @@ __global__ __launch_bounds__(512, 2) void pgemm_kernel(const uint16_t* __restric
   // phase 1 of j+1; E.HB1 5 -> 1 -> 2; E.HA1 6 -> 2 -> 3; O.HA0 / HB0 7 / 8 -> 4 -> 5;
   // O.HB1 1 -> 5 -> 6; O.HA1 2 -> 6 -> 7).  The last iteration issues only phases 1-2 and
   // retires with the counts that keep the same guarantees (8, 8, 8, 4, 2, 0, 0, 0).
-  const int nk = Ks / BK;
-  const int nit = nk / 2;
   // prologue: everything the steady state assumes was issued in iteration -1
   stage(HA0, 0);
   stage(HB0, 0);
@@ -258,6 +228,16 @@ __global__ __launch_bounds__(512, 2) void pgemm_kernel(const uint16_t* __restric
   vmcnt<0>();
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   sbarrier();                // every wave done with the buffers: reuse LDS as scratch
+}
+
+// the tile's epilogue through the drained LDS: bf16 tile, fused SwiGLU, or an fp32 slab
+template <int EPI>
+__device__ __forceinline__ void pgemm_store(char* smem, f32x4 (&acc)[2][4][2][2], uint16_t* __restrict__ C,
+                                            float* __restrict__ P, int M, int N, int m0, int n0, int slice) {
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wr = wave >> 2, wc = wave & 3;
+  const int fr = lane & 15, fk = lane >> 4;
 
   // ---- epilogue: the wave's 128 x 64 tile -> bf16 scratch [128][SCR_PITCH] -> row stores
   uint16_t* scr = reinterpret_cast<uint16_t*>(smem) + wave * 128 * SCR_PITCH;
@@ -339,6 +319,44 @@ __global__ __launch_bounds__(512, 2) void pgemm_kernel(const uint16_t* __restric
       if (row < M) *reinterpret_cast<uint4*>(C + (size_t)row * (N >> 1) + ((n0 + wc * 64) >> 1) + c) = v;
     }
   }
+}
+
+template <int EPI>
+__global__ __launch_bounds__(512, 2) void pgemm_kernel(const uint16_t* __restrict__ A,
+                                                      const uint16_t* __restrict__ W,
+                                                      uint16_t* __restrict__ C, float* __restrict__ P,
+                                                      int M, int N, int K, int ntm, int ntn, int S, int Ks) {
+  __shared__ __attribute__((aligned(16))) char smem[LDS_B];
+  const int nwg = ntm * ntn;
+  // split-K (decode-sized M): workgroup -> (tile, K slice).  With S | 8 and whole rounds of
+  // 8, the workgroups of one XCD all take the same slice, so that XCD's L2 holds just that
+  // slice of A -- re-read by every tile (cf. mgemm.hip)
+  int tile_id, slice = 0;
+  if (S == 1) {
+    tile_id = xcd_remap(blockIdx.x, nwg);
+  } else if (8 % S == 0 && (nwg * S) % 8 == 0) {
+    const int xcd = blockIdx.x & 7, j = blockIdx.x >> 3;
+    slice = xcd % S;
+    tile_id = j * (8 / S) + xcd / S;
+  } else {
+    tile_id = blockIdx.x % nwg;
+    slice = blockIdx.x / nwg;
+  }
+  const int kbeg = slice * Ks;
+  const int wg = tile_id;
+  // groups of GM m-tiles x all n-tiles: consecutive ids (one XCD's concurrent workgroups)
+  // form a GM x (32 / GM) block of output tiles
+  constexpr int GM = 4;
+  const int per_group = GM * ntn;
+  const int grp = wg / per_group, first_m = grp * GM;
+  const int gm = min(ntm - first_m, GM);
+  const int rem = wg - grp * per_group;
+  const int bm = first_m + rem % gm, bn = rem / gm;
+  const int m0 = bm * BM, n0 = bn * BN;
+
+  f32x4 acc[2][4][2][2];
+  pgemm_mainloop(smem, A, W, M, K, m0, n0, kbeg, Ks / (2 * BK), acc);
+  pgemm_store<EPI>(smem, acc, C, P, M, N, m0, n0, slice);
 }
 }  // namespace
 

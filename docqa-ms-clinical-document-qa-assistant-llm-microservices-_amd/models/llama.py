@@ -318,8 +318,6 @@ class LlamaModel:
         if (decode or small) and self.layers:
             L0 = self.layers[0]
             for k in ("qkv", "o", "down"):
-                if small and ops.lib_route(M, *L0[k].shape):
-                    continue          # prefill_linear takes hipBLASLt for this shape
                 S, c = ops.mid_plan(M, *L0[k].shape)
                 if S:
                     plans[k] = (S, lambda a, w, S=S, c=c: (ops.mgemm_partial(a, w, S, c) if S > 1
@@ -328,15 +326,19 @@ class LlamaModel:
                     S, t = ops.decode_plan(M, *L0[k].shape)
                     plans[k] = (S, lambda a, w, S=S, t=t: ops.dgemm_partial(a, w, S, t))
             if small and M > 256 and "down" in plans:
-                # a 257..512-token prefill: the down projection at S=4 (256 workgroups) --
-                # 75.7 vs 102.6 us at 512 rows with the add+norm consumer
-                # (profiles/r4_prefill_mid_probe.log); decode buckets keep their plan
-                N, K = L0["down"].shape
-                if ops.mid_plan(M, N, K)[0] and (K // 128) % 4 == 0 and N % 128 == 0 and not ops.lib_route(M, N, K):
-                    plans["down"] = (4, lambda a, w: ops.mgemm_partial(a, w, 4, 2))
+                # a 257..512-token prefill's down projection (decode buckets keep their plan):
+                # the 256 x 256 kernel's S=8 slabs where K is long -- 8B: 66.1 vs the mid-M
+                # kernel's S=4 77.5 and hipBLASLt's 97.4 us at 512 rows
+                # (profiles/r6_prefill_mid_plans.log); the 70B TP-8 shard keeps mid_plan's
+                Sd = ops.down_small_split(M, *L0["down"].shape)
+                if Sd:
+                    plans["down"] = (Sd, lambda a, w, S=Sd: ops.pgemm_partial(a, w, S))
             Sg, cg = ops.mid_plan(M, *L0["gate_up"].shape, glu=True)
-            if small and (ops.pgemm_ok(M, *L0["gate_up"].shape) or ops.lib_route(M, *L0["gate_up"].shape, glu=True)):
-                glu = ops.prefill_glu     # 256 x 256 tiles with SwiGLU: 104 vs 141 us at M = 512
+            if small and (ops.pgemm_ok(M, *L0["gate_up"].shape)
+                          or ops.prefill_split_plan(M, *L0["gate_up"].shape, glu=True)):
+                # 256 x 256 tiles with SwiGLU (104 vs 141 us at M = 512), or their split-K
+                # slabs into the SwiGLU consumer where too few tiles (the 70B TP-8 shard)
+                glu = ops.prefill_glu
             else:
                 glu = (lambda a, w: ops.mgemm_glu(a, w, cg)) if Sg else ops.glu_linear
         else:

@@ -277,6 +277,12 @@ def mid_plan(M: int, N: int, K: int, glu: bool = False) -> tuple[int, int]:
         # the same split fill it with the same slab bytes -- O 17.5 vs 20.7 us
         # (profiles/r2_mgemm_probe_bn64.log)
         return S, 7
+    if _MID_CFG == 2 and _MID_NARROW and S == 1 and tiles * 2 <= 256 and N % 64 == 0:
+        # no split under the cap (the 70B TP-8 O / down shards, 128 tiles at 257..512 rows):
+        # twice the workgroups -- short K (O, 1024) by 64-wide tiles, 22.6 vs 26.3 us at 512
+        # rows (hipBLASLt 23.2), long K (down, 3584) by a 2-way split, 46.5 vs 58.8 (46.1)
+        # (profiles/r6_prefill_mid_plans.log)
+        return (2, 2) if K >= 2048 and kb % 2 == 0 else (1, 7)
     return S, _MID_CFG
 
 
@@ -325,27 +331,17 @@ def pgemm_ok(M: int, N: int, K: int) -> bool:
 
 
 PREFILL_MID_MAX = 2048
-_LIB_ROUTES_ON = os.environ.get("DOCQA_LIB_ROUTES", "1") != "0"
-# Prefill projection shapes where hipBLASLt beats what the hand-written path runs there
-# (the plain-GEMM library path, plus a silu_mul launch for gate|up): (N, K, glu) -> row
-# ranges.  Measured per route, split-K plans counted by their slabs alone
-# (scripts/pgemm_mid_probe.py "routed" column; profiles/r5_prefill_lib_routes.log): the 70B
-# TP-8 gate|up / down shards at <= 768 rows (0.71x / 0.82x before), and the 8B projections
-# at the mid sizes where the 256-row tiles leave the chip half idle -- QKV 513..1024 (0.77x
-# / 0.85x), O 513..768 and 1025..1536 (0.89x / 0.83x), gate|up 513..768 (0.89x), down
-# 513..768 and 1025..2048 (0.89x / 0.88x).
-_LIB_ROUTES = {
-    (7168, 8192, True): ((1, 768),), (8192, 3584, False): ((1, 768),),
-    (6144, 4096, False): ((513, 1024),), (4096, 4096, False): ((513, 768), (1025, 1536)),
-    (28672, 4096, True): ((513, 768),), (4096, 14336, False): ((513, 768), (1025, 2048)),
-}
+# Mid-M prefill (513..2048 packed prompt tokens; the Llama-3-70B TP-8 shards from 257 rows):
+# every projection on the hand-written kernels -- no library GEMM.  Measured WITH each
+# projection's consumer and weights rotated past the MALL (scripts/prefill_mid_probe.py,
+# profiles/r6_prefill_mid_plans.log): where the 256 x 256 tiles cannot fill the 256 CUs the
+# K dimension is split into fp32 slabs (pgemm.hip EPI_PARTIAL, one K slice per XCD group)
+# that the consumer which runs anyway sums -- RoPE + KV write (QKV), residual add + RMSNorm
+# (O / down), SwiGLU (gate|up: act.hip silu_mul_splitk) -- :func:`prefill_split_plan`; a
+# few measured shapes keep the mid-M kernel (:func:`prefill_plan`).  Best hand-written /
+# hipBLASLt (+ the same consumer) there: 0.93..1.46x, 28 of 40 (shape, M) points >= 0.97x.
+_PREFILL_SPLIT_MIN_K = 1024       # K per slice below this loses to fewer slices (O at 512 rows: S=8 42.0 vs S=4 37.5 us)
 
-
-def lib_route(M: int, N: int, K: int, glu: bool = False) -> bool:
-    """True when a prefill projection of M rows should take hipBLASLt (measured table
-    above; DOCQA_LIB_ROUTES=0 disables)."""
-    ranges = _LIB_ROUTES.get((int(N), int(K), bool(glu)), ())
-    return _LIB_ROUTES_ON and any(lo <= M <= hi for lo, hi in ranges)
 
 _PREFILL_PLANS = os.environ.get("DOCQA_PREFILL_PLANS", "1") != "0"
 
@@ -360,7 +356,11 @@ def prefill_plan(M: int, N: int, K: int) -> tuple[int, int]:
     (116.5 / 145.3); 1025..2048 rows: O and down S=1, QKV the 256 x 256 kernel."""
     if not _PREFILL_PLANS or _MID_OFF or not (MID_M_MAX < M <= PREFILL_MID_MAX) or N % 128 or K % 128:
         return 0, 0
-    if lib_route(M, N, K):
+    if 769 <= M <= 1024 and (N, K) in ((4096, 4096), (8192, 3584)):
+        # the two measured points where the mid-M kernel beats the split 256 x 256 tiles:
+        # 8B O S=2 48.5 vs pgemm S=4 50.9 us, 70B TP-8 down S=1 71.9 vs pgemm S=2 75.4
+        return (2, 2) if N == 4096 else (1, 2)
+    if prefill_split_plan(M, N, K):
         return 0, 0
     if N < 4096:
         # narrow N (the 70B TP-8 QKV shard, N 1280 x K 8192): the mid-M kernel's few 128-wide
@@ -373,21 +373,42 @@ def prefill_plan(M: int, N: int, K: int) -> tuple[int, int]:
     return 1, 2
 
 
-def prefill_split_plan(M: int, N: int, K: int) -> int:
+def prefill_split_plan(M: int, N: int, K: int, glu: bool = False) -> int:
     """Split-K count for a prefill projection whose 256 x 256 tiles cannot fill the chip:
-    the narrow column-parallel shards of tensor parallelism (the 70B TP-8 QKV shard, N 1280 x
-    K 8192: 10 tiles at 512 rows, 0.41x hipBLASLt unsplit, profiles/r4_pgemm_mid_probe.log).
-    The fp32 slabs [S, M, N] go straight into the split-K consumers that run anyway (RoPE +
-    KV write, (TP all-reduce +) add + RMSNorm).  0: no split (enough tiles, or not a pgemm
-    shape).  DOCQA_PREFILL_SPLIT=0 disables."""
-    if (not _PREFILL_SPLIT or _PGEMM_OFF or N >= 4096 or M <= 0 or N % 256 or K % 256
-            or max(M, N) * K * 2 >= (1 << 32) or lib_route(M, N, K)):
+    the largest S (<= DOCQA_PREFILL_SPLIT_MAX) with tiles x S <= 256 workgroups and >= 1024
+    of K per slice.  The fp32 slabs [S, M, N] go straight into the split-K consumer that runs
+    anyway (RoPE + KV write, (TP all-reduce +) add + RMSNorm, SwiGLU).  Measured with the
+    consumer (profiles/r6_prefill_mid_plans.log): 8B down S=4 93.8 vs hipBLASLt 115.9 us at
+    768 rows, QKV S=2 55.3 vs 55.2, O S=4 42.3 vs 40.3; 70B TP-8 gate|up S=4 69.2 vs 84.2 at
+    512 rows, QKV shard S=8 32.2 vs 35.8.  0: no split (enough tiles, or not a pgemm shape).
+    ``glu``: the gate|up shard's S (consumer silu_mul_splitk), from 257 rows (measured at
+    512+; below that the decode-sized mid-M SwiGLU kernel keeps it).  DOCQA_PREFILL_SPLIT=0
+    disables."""
+    if (not _PREFILL_SPLIT or _PGEMM_OFF or M <= 0 or N % 256 or K % 256
+            or max(M, N) * K * 2 >= (1 << 32)):
+        return 0
+    if M <= MID_M_MAX and not (N < 4096 or (glu and M > 256)):
+        return 0          # decode-sized M: the mid-M kernel's plans (mid_plan)
+    tiles = ((M + 255) // 256) * (N // 256)
+    S = 1
+    while (S < _PREFILL_SPLIT_MAX and tiles * S * 2 <= 256 and K % (128 * S * 2) == 0
+           and K // (S * 2) >= _PREFILL_SPLIT_MIN_K):
+        S *= 2
+    return S if S >= 2 else 0
+
+
+def down_small_split(M: int, N: int, K: int) -> int:
+    """Split-K count of a 257..512-row prefill's down projection on the 256 x 256 kernel
+    (long K: the 8B down, 14336): S=8 slabs into add + RMSNorm, 67.5 vs 77.5 us for the mid-M
+    kernel's S=4 and 98.7 for hipBLASLt at 512 rows (profiles/r6_prefill_mid_plans.log).
+    0 where it does not apply (fewer than 4 slices of >= 1024)."""
+    if not (256 < M <= MID_M_MAX) or _PGEMM_OFF or not _PREFILL_SPLIT or N % 256 or K % 256:
         return 0
     tiles = ((M + 255) // 256) * (N // 256)
     S = 1
-    while S < _PREFILL_SPLIT_MAX and tiles * S * 2 <= 256 and K % (128 * S * 2) == 0 and K // (S * 2) >= 512:
+    while S < 8 and tiles * S * 2 <= 256 and K % (128 * S * 2) == 0 and K // (S * 2) >= _PREFILL_SPLIT_MIN_K:
         S *= 2
-    return S if S >= 2 else 0
+    return S if S >= 4 else 0
 
 
 _PREFILL_SPLIT = os.environ.get("DOCQA_PREFILL_SPLIT", "1") != "0"
@@ -402,11 +423,14 @@ def prefill_linear(x, w):
     if _gpu(x):
         N, K = w.shape
         M = x.numel() // K
-        if lib_route(M, N, K):
-            return torch.nn.functional.linear(x, w)
         S, cfg = prefill_plan(M, N, K)
         if S == 1:
             return _native().mgemm(x.contiguous(), w, 1, cfg)
+        Sp = prefill_split_plan(M, N, K)
+        if Sp:
+            # a caller without a split-K consumer (the mixed prefill/decode forward): the
+            # slabs summed here, still ahead of the 128 x 128 kernel at these shapes
+            return _native().pgemm_partial(x.contiguous(), w, Sp).sum(0).to(torch.bfloat16)
         if pgemm_ok(M, N, K):
             return _native().pgemm(x.contiguous(), w, 0)
         if N % 128 == 0 and K % 64 == 0:
@@ -420,17 +444,17 @@ def prefill_route(M: int, N: int, K: int, glu: bool = False, down: bool = False)
     fp32 slabs [S, M, N] their consumer sums; ``down``: the 257..512-row down override."""
     nat = _native
     if glu:
-        if M <= MID_M_MAX and not (pgemm_ok(M, N, K) or lib_route(M, N, K, glu=True)):
+        if M <= MID_M_MAX and not (pgemm_ok(M, N, K) or prefill_split_plan(M, N, K, glu=True)):
             Sg, cg = mid_plan(M, N, K, glu=True)
             if Sg:
                 return f"mgemm_glu c{cg}", lambda x, w: nat().mgemm_glu(x.contiguous(), w, cg)
             return "glu_linear", glu_linear
-        return ("hipblaslt+silu" if lib_route(M, N, K, glu=True) else "prefill_glu"), prefill_glu
-    if lib_route(M, N, K):
-        return "hipblaslt", lambda x, w: torch.nn.functional.linear(x, w)
+        Sg = prefill_split_plan(M, N, K, glu=True)
+        return (f"pgemm S{Sg}+silu_splitk" if Sg else "prefill_glu"), prefill_glu
+    if down and M <= MID_M_MAX and M > 256 and down_small_split(M, N, K):
+        Sd = down_small_split(M, N, K)
+        return f"pgemm S{Sd}", lambda x, w: nat().pgemm_partial(x.contiguous(), w, Sd)
     if M <= MID_M_MAX:
-        if down and M > 256 and mid_plan(M, N, K)[0] and (K // 128) % 4 == 0 and N % 128 == 0:
-            return "mgemm S4 c2", lambda x, w: nat().mgemm(x.contiguous(), w, 4, 2)
         S, c = mid_plan(M, N, K)
         if S:
             return f"mgemm S{S} c{c}", lambda x, w: nat().mgemm(x.contiguous(), w, S, c)
@@ -455,8 +479,11 @@ def prefill_glu(x, w_il):
     if _gpu(x):
         N, K = w_il.shape
         M = x.numel() // K
-        if lib_route(M, N, K, glu=True):
-            return silu_mul(torch.nn.functional.linear(x, w_il), interleaved=True)
+        S = prefill_split_plan(M, N, K, glu=True)
+        if S:
+            # too few 256 x 256 tiles (the 70B TP-8 shard: 56 at 512 rows): K split into fp32
+            # slabs, summed by the SwiGLU consumer -- 69.2 vs hipBLASLt + silu_mul 84.2 us
+            return _native().silu_mul_splitk(_native().pgemm_partial(x.contiguous(), w_il, S))
         if pgemm_ok(M, N, K):
             return _native().pgemm(x.contiguous(), w_il, 1)
         if (_GLU128 and N % 128 == 0 and K % 64 == 0 and ((M + 255) // 256) * (N // 128) < 128

@@ -9,7 +9,7 @@ of interleaved rounds:
   routed  -- what the prefill forward runs for the projection (ops.prefill_route, the plan
              logic of models/llama.py: split-K plans timed as their slabs alone, since the
              RoPE / add+RMSNorm consumer that sums them runs either way; hipBLASLt on the
-             measured library routes, ops.lib_route); "route" names it
+             split-K slab plans into the consumers); "route" names it
 Usage: python scripts/pgemm_mid_probe.py [M ...]   -> one JSON line per (M, projection)"""
 import json
 import os

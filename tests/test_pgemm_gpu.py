@@ -116,7 +116,7 @@ def test_prefill_split_plan_slabs_feed_the_consumers():
                                        (300, 4096, 14336, False), (2048, 7168, 8192, True), (700, 28672, 4096, True)])
 def test_prefill_route_products(M, N, K, glu):
     """Every route the prefill forward can take (ops.prefill_route: hand-written tiles, split-K
-    slabs, the measured hipBLASLt routes) computes the projection: fp32 slabs summed, bf16
+    slabs into the consumers, the SwiGLU split-K consumer) computes the projection: fp32 slabs summed, bf16
     products and SwiGLU outputs against the fp32 reference."""
     x, w = _data(M, N, K, seed=3)
     label, fn = ops.prefill_route(M, N, K, glu=glu, down=(K == 14336 or K == 3584))
@@ -129,4 +129,27 @@ def test_prefill_route_products(M, N, K, glu):
     err = (y.float() - r).abs().max().item() / max(1e-6, r.abs().max().item())
     assert y.shape == r.shape, label
     assert err < 2e-2, (label, err)
-    assert ops.lib_route(M, N, K, glu) == label.startswith("hipblaslt")
+    assert "hipblaslt" not in label
+
+
+@pytest.mark.parametrize("S,M,I", [(1, 7, 64), (2, 300, 3584), (4, 512, 3584), (8, 33, 128)])
+def test_silu_mul_splitk_matches_reference(S, M, I):
+    """The SwiGLU split-K consumer (act.hip silu_mul_splitk): fp32 slabs of an 8-interleaved
+    gate|up projection summed in slab order, rounded as the bf16 GEMM output, silu(gate) * up."""
+    g = torch.Generator(device="cuda").manual_seed(S * 1000 + M)
+    P = torch.randn(S, M, 2 * I, device="cuda", generator=g)
+    got = torch.ops.docqa.silu_mul_splitk(P)
+    want = ref.silu_mul(P.sum(0).to(torch.bfloat16), interleaved=True).float()
+    assert got.shape == (M, I) and got.dtype == torch.bfloat16
+    assert (got.float() - want).abs().max().item() <= 2e-2 * want.abs().max().item() + 1e-3
+
+
+def test_70b_gate_up_split_route_matches_fused_epilogue():
+    """The 70B TP-8 gate|up shard at 512 rows takes K-split slabs + silu_mul_splitk (no
+    library GEMM): same values as the 256 x 256 kernel's fused SwiGLU epilogue up to the
+    K-split summation order."""
+    x, w = _data(512, 7168, 8192, seed=11)
+    assert ops.prefill_split_plan(512, 7168, 8192, glu=True) == 4
+    a = ops.prefill_glu(x, w).float()
+    b = torch.ops.docqa.pgemm(x, w, 1).float()
+    assert (a - b).abs().max().item() <= 2e-2 * b.abs().max().item() + 1e-3
