@@ -338,8 +338,9 @@ PREFILL_MID_MAX = 2048
 # K dimension is split into fp32 slabs (pgemm.hip EPI_PARTIAL, one K slice per XCD group)
 # that the consumer which runs anyway sums -- RoPE + KV write (QKV), residual add + RMSNorm
 # (O / down), SwiGLU (gate|up: act.hip silu_mul_splitk) -- :func:`prefill_split_plan`; a
-# few measured shapes keep the mid-M kernel (:func:`prefill_plan`).  Best hand-written /
-# hipBLASLt (+ the same consumer) there: 0.93..1.46x, 28 of 40 (shape, M) points >= 0.97x.
+# few measured shapes keep the mid-M kernel (:func:`prefill_plan`).  What the forward runs
+# (:func:`prefill_route`) against hipBLASLt + the same consumer at 512..2048 rows: 0.93..1.47x,
+# 36 of 40 (shape, M) points >= 0.95x.
 _PREFILL_SPLIT_MIN_K = 1024       # K per slice below this loses to fewer slices (O at 512 rows: S=8 42.0 vs S=4 37.5 us)
 
 
@@ -347,13 +348,13 @@ _PREFILL_PLANS = os.environ.get("DOCQA_PREFILL_PLANS", "1") != "0"
 
 
 def prefill_plan(M: int, N: int, K: int) -> tuple[int, int]:
-    """(split-K count, mgemm cfg) of a 513..2048-row prefill projection, (0, 0) for the
-    256 x 256 / 128 x 128 kernels.  S >= 2: fp32 slabs into the split-K consumers (RoPE +
-    KV write, add + RMSNorm); S == 1: the bf16 product.  Measured with the consumer on the
-    Llama-3-8B shapes (profiles/r4_prefill_mid_probe.log; hipBLASLt + consumer in brackets):
-    QKV 768 / 1024 rows cfg 2 S=1 60.9 / 65.4 us (56.3 / 60.6; the 128-tile kernel it
-    replaces 71.2 / 83.0), O S=2 42.3 / 47.9 (40.8 / 48.7), down S=2 111.8 / 131.8
-    (116.5 / 145.3); 1025..2048 rows: O and down S=1, QKV the 256 x 256 kernel."""
+    """(split-K count, mgemm cfg) of a 513..2048-row prefill projection on the mid-M kernel,
+    (0, 0) for the 256 x 256 kernel (split-K slabs where :func:`prefill_split_plan` says so,
+    else bf16 tiles).  S >= 2: fp32 slabs into the split-K consumers (RoPE + KV write, add +
+    RMSNorm); S == 1: the bf16 product.  Since round 6 the 256 x 256 split plans take every
+    shape they apply to except the two points measured faster here (8B O and the 70B TP-8
+    down shard at 769..1024 rows, profiles/r6_prefill_mid_plans.log); the remaining rules
+    are round 4's (profiles/r4_prefill_mid_probe.log) for shapes no split plan takes."""
     if not _PREFILL_PLANS or _MID_OFF or not (MID_M_MAX < M <= PREFILL_MID_MAX) or N % 128 or K % 128:
         return 0, 0
     if 769 <= M <= 1024 and (N, K) in ((4096, 4096), (8192, 3584)):
