@@ -938,23 +938,6 @@ at::Tensor pgemm(const at::Tensor& x, const at::Tensor& w, int64_t epi) {
   return out;
 }
 
-// A/B entry: the prefill GEMM with an explicit MFMA shape (mf32 1: 32x32x16, 0: 16x16x32)
-at::Tensor pgemm_mf(const at::Tensor& x, const at::Tensor& w, int64_t epi, int64_t mf32) {
-  CHECK_GPU(x); CHECK_BF16(x); CHECK_BF16(w); CHECK_CONTIG(x); CHECK_CONTIG(w);
-  CHECK_ALIGN16(x); CHECK_ALIGN16(w);
-  const int K = x.size(-1), N = w.size(0);
-  TORCH_CHECK(w.size(1) == K && (epi == 0 || epi == 1), "pgemm_mf: K mismatch / epi");
-  const int M = x.numel() / K;
-  TORCH_CHECK(M == 0 || docqa_pgemm_ok(M, N, K), "pgemm_mf: unsupported shape");
-  auto sizes = x.sizes().vec();
-  sizes.back() = epi == 1 ? N / 2 : N;
-  c10::DeviceGuard g(x.device());
-  auto out = at::empty(sizes, x.options());
-  CHECK_RC(docqa_pgemm_mf(x.data_ptr(), w.data_ptr(), out.data_ptr(), M, N, K, (int)epi, (int)mf32, stream()),
-           "pgemm_mf");
-  return out;
-}
-
 // split-K fp32 slabs [S, M, N] of x . w^T on the 256 x 256 kernel (decode-sized M)
 at::Tensor pgemm_partial(const at::Tensor& x, const at::Tensor& w, int64_t splits) {
   CHECK_GPU(x); CHECK_BF16(x); CHECK_BF16(w); CHECK_CONTIG(x); CHECK_CONTIG(w);
@@ -1289,7 +1272,6 @@ TORCH_LIBRARY(docqa, m) {
   m.def("dgemm_argmax_val(Tensor x, Tensor w, int n_valid) -> (Tensor, Tensor)");
   m.def("pgemm(Tensor x, Tensor w, int epi=0) -> Tensor");
   m.def("pgemm_partial(Tensor x, Tensor w, int splits) -> Tensor");
-  m.def("pgemm_mf(Tensor x, Tensor w, int epi, int mf32) -> Tensor");
   m.def("mgemm_argmax_val(Tensor x, Tensor w, int n_valid, int cfg=0) -> (Tensor, Tensor)");
   m.def("pgemm_ok(int M, int N, int K) -> bool", &pgemm_ok);
   m.def("mgemm_ld(Tensor x, Tensor w, int splits, int cfg, bool glu) -> Tensor");
@@ -1367,7 +1349,6 @@ TORCH_LIBRARY_IMPL(docqa, CUDA, m) {
   m.impl("pgemm", &pgemm);
   m.impl("mgemm_ld", &mgemm_ld);
   m.impl("pgemm_partial", &pgemm_partial);
-  m.impl("pgemm_mf", &pgemm_mf);
   m.impl("mgemm_argmax_val", &mgemm_argmax_val);
   m.impl("coarse_probes", &coarse_probes);
   m.impl("fp32_gemm_nt", &fp32_gemm_nt);

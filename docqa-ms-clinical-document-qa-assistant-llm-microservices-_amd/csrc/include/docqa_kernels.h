@@ -148,7 +148,6 @@ int docqa_coarse_probes(const float* cent, const float* cnorm, int nlist, int d,
 bool docqa_pgemm_ok(int M, int N, int K);
 int docqa_pgemm(const void* A, const void* W, void* C, float* P, int M, int N, int K, int S, int epi,
                 hipStream_t s);
-int docqa_pgemm_mf(const void* A, const void* W, void* C, int M, int N, int K, int epi, int mf32, hipStream_t s);
 int docqa_knn_workspace_blocks(int N);
 int docqa_knn_kpad(int k);
 int docqa_knn(const void* xb, const float* norms, int N, int d, int is_bf16, const float* xq,

@@ -36,7 +36,6 @@
 // byte offsets of A and W rows must fit 32 bits (saddr + voffset addressing).
 #include "docqa_common.h"
 #include "docqa_asm.h"
-#include <stdlib.h>
 #include <float.h>
 
 using namespace docqa;
@@ -87,29 +86,12 @@ __device__ __forceinline__ void glds_pair(const void* sbase, uint32_t v0, uint32
 
 __device__ __forceinline__ float silu_f(float x) { return x / (1.f + __expf(-x)); }
 
-// MFMA shape of a wave's 128 x 64 tile (per K-tile of 64: 64 x 16x16x32 or 32 x 32x32x16,
-// the same FLOPs from the same LDS fragment bytes -- the 32x32x16 form reads half the
-// operand registers per FLOP).  Acc: the wave's accumulators; FA / FB: the fragments of one
-// m-half / both n-halves of a K-tile.
-template <bool MF32> struct Tile;
-template <> struct Tile<false> {
-  typedef f32x4 Acc[2][4][2][2];   // [m-half][16-row block][n-half][16-col block]
-  typedef bf16x8 FA[2][4];         // [k-step of 32][16-row block]
-  typedef bf16x8 FB[2][2][2];      // [n-half][k-step][16-col block]
-};
-template <> struct Tile<true> {
-  typedef f32x16 Acc[2][2][2];     // [m-half][32-row block][n-half]
-  typedef bf16x8 FA[4][2];         // [k-step of 16][32-row block]
-  typedef bf16x8 FB[2][4];         // [n-half][k-step]
-};
-
 // K range [kbeg, kbeg + 128 nit) of the 256 x 256 output tile at (m0, n0) into acc (zeroed
 // here), nit >= 1.  Returns with the wave rows re-aligned and every LDS buffer drained, so
 // the caller may reuse the LDS as epilogue scratch.
-template <bool MF32>
 __device__ __forceinline__ void pgemm_mainloop(char* smem, const uint16_t* __restrict__ A,
                                                const uint16_t* __restrict__ W, int M, int K, int m0, int n0,
-                                               int kbeg, int nit, typename Tile<MF32>::Acc& acc) {
+                                               int kbeg, int nit, f32x4 (&acc)[2][4][2][2]) {
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wr = wave >> 2, wc = wave & 3;
@@ -140,66 +122,45 @@ __device__ __forceinline__ void pgemm_mainloop(char* smem, const uint16_t* __res
     glds_pair(base, soff[h][0], soff[h][1], d, d + 8 * 1024);
   };
 
-  {
-    float* az = reinterpret_cast<float*>(&acc);
 #pragma unroll
-    for (int e = 0; e < 128; ++e) az[e] = 0.f;
-  }
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int b = 0; b < 2; ++b)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) acc[a][i][b][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  typename Tile<MF32>::FA fa;   // fragments of the current m-half
-  typename Tile<MF32>::FB fb;   // fragments of both n-halves
+  bf16x8 fa[2][4];       // [k-step][m-tile] of the current m-half
+  bf16x8 fb[2][2][2];    // [n-half][k-step][n-tile]
   const char* sm = smem;
-  // 32x32x16: lane = (row l & 31, 8-wide K chunk l >> 5) of a 32-row block per k-step of 16
-  const int r32 = lane & 31, k32 = lane >> 5;
 
   auto read_a = [&](int buf, int mh) {
     const char* h = sm + buf * BUF_B + (HA0 + mh) * HALF_B;
-    if constexpr (MF32) {
 #pragma unroll
-      for (int ks = 0; ks < 4; ++ks)
+    for (int ks = 0; ks < 2; ++ks)
 #pragma unroll
-        for (int i = 0; i < 2; ++i)
-          fa[ks][i] = *reinterpret_cast<const bf16x8*>(h + swz(wr * 64 + i * 32 + r32, ks * 2 + k32));
-    } else {
-#pragma unroll
-      for (int ks = 0; ks < 2; ++ks)
-#pragma unroll
-        for (int i = 0; i < 4; ++i)
-          fa[ks][i] = *reinterpret_cast<const bf16x8*>(h + swz(wr * 64 + i * 16 + fr, ks * 4 + fk));
-    }
+      for (int i = 0; i < 4; ++i)
+        fa[ks][i] = *reinterpret_cast<const bf16x8*>(h + swz(wr * 64 + i * 16 + fr, ks * 4 + fk));
   };
   auto read_b = [&](int buf, int nh) {
     const char* h = sm + buf * BUF_B + (HB0 + nh) * HALF_B;
-    if constexpr (MF32) {
 #pragma unroll
-      for (int ks = 0; ks < 4; ++ks)
-        fb[nh][ks] = *reinterpret_cast<const bf16x8*>(h + swz(wc * 32 + r32, ks * 2 + k32));
-    } else {
+    for (int ks = 0; ks < 2; ++ks)
 #pragma unroll
-      for (int ks = 0; ks < 2; ++ks)
-#pragma unroll
-        for (int j = 0; j < 2; ++j)
-          fb[nh][ks][j] = *reinterpret_cast<const bf16x8*>(h + swz(wc * 32 + j * 16 + fr, ks * 4 + fk));
-    }
+      for (int j = 0; j < 2; ++j)
+        fb[nh][ks][j] = *reinterpret_cast<const bf16x8*>(h + swz(wc * 32 + j * 16 + fr, ks * 4 + fk));
   };
   auto mma = [&](int mh, int nh) {
     __builtin_amdgcn_s_setprio(1);
-    if constexpr (MF32) {
 #pragma unroll
-      for (int ks = 0; ks < 4; ++ks)
+    for (int ks = 0; ks < 2; ++ks)
 #pragma unroll
-        for (int i = 0; i < 2; ++i)
-          acc[mh][i][nh] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[ks][i], fb[nh][ks], acc[mh][i][nh], 0, 0, 0);
-    } else {
+      for (int i = 0; i < 4; ++i)
 #pragma unroll
-      for (int ks = 0; ks < 2; ++ks)
-#pragma unroll
-        for (int i = 0; i < 4; ++i)
-#pragma unroll
-          for (int j = 0; j < 2; ++j)
-            acc[mh][i][nh][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[ks][i], fb[nh][ks][j],
-                                                                        acc[mh][i][nh][j], 0, 0, 0);
-    }
+        for (int j = 0; j < 2; ++j)
+          acc[mh][i][nh][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[ks][i], fb[nh][ks][j],
+                                                                      acc[mh][i][nh][j], 0, 0, 0);
     __builtin_amdgcn_s_setprio(0);
   };
 
@@ -269,27 +230,20 @@ __device__ __forceinline__ void pgemm_mainloop(char* smem, const uint16_t* __res
   sbarrier();                // every wave done with the buffers: reuse LDS as scratch
 }
 
-// the tile's epilogue through the drained LDS: bf16 tile, fused SwiGLU, or an fp32 slab.
-// EACH(fn): fn(mh, row in the m-half 0..63, nh, col in the n-half 0..31, value) over the
-// wave's accumulators in either MFMA layout (16x16: row 16 i + 4 (lane >> 4) + r, col
-// 16 j + (lane & 15); 32x32: row 32 i + 8 (r >> 2) + 4 (lane >> 5) + (r & 3), col lane & 31)
-template <int EPI, bool MF32>
-__device__ __forceinline__ void pgemm_store(char* smem, typename Tile<MF32>::Acc& acc, uint16_t* __restrict__ C,
+// the tile's epilogue through the drained LDS: bf16 tile, fused SwiGLU, or an fp32 slab
+template <int EPI>
+__device__ __forceinline__ void pgemm_store(char* smem, f32x4 (&acc)[2][4][2][2], uint16_t* __restrict__ C,
                                             float* __restrict__ P, int M, int N, int m0, int n0, int slice) {
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wr = wave >> 2, wc = wave & 3;
   const int fr = lane & 15, fk = lane >> 4;
-  auto each_half = [&](int mh, auto&& fn) {
-    if constexpr (MF32) {
+
+  // ---- epilogue: the wave's 128 x 64 tile -> bf16 scratch [128][SCR_PITCH] -> row stores
+  uint16_t* scr = reinterpret_cast<uint16_t*>(smem) + wave * 128 * SCR_PITCH;
+  if constexpr (EPI == EPI_BF16) {
 #pragma unroll
-      for (int i = 0; i < 2; ++i)
-#pragma unroll
-        for (int nh = 0; nh < 2; ++nh)
-#pragma unroll
-          for (int r = 0; r < 16; ++r)
-            fn(i * 32 + 8 * (r >> 2) + 4 * (lane >> 5) + (r & 3), nh, lane & 31, acc[mh][i][nh][r]);
-    } else {
+    for (int mh = 0; mh < 2; ++mh)
 #pragma unroll
       for (int i = 0; i < 4; ++i)
 #pragma unroll
@@ -297,18 +251,9 @@ __device__ __forceinline__ void pgemm_store(char* smem, typename Tile<MF32>::Acc
 #pragma unroll
           for (int j = 0; j < 2; ++j)
 #pragma unroll
-            for (int r = 0; r < 4; ++r) fn(i * 16 + fk * 4 + r, nh, j * 16 + fr, acc[mh][i][nh][j][r]);
-    }
-  };
-
-  // ---- epilogue: the wave's 128 x 64 tile -> bf16 scratch [128][SCR_PITCH] -> row stores
-  uint16_t* scr = reinterpret_cast<uint16_t*>(smem) + wave * 128 * SCR_PITCH;
-  if constexpr (EPI == EPI_BF16) {
-#pragma unroll
-    for (int mh = 0; mh < 2; ++mh)
-      each_half(mh, [&](int row, int nh, int col, float v) {
-        scr[(mh * 64 + row) * SCR_PITCH + nh * 32 + col] = f2bf(v);
-      });
+            for (int r = 0; r < 4; ++r)
+              scr[(mh * 64 + i * 16 + fk * 4 + r) * SCR_PITCH + nh * 32 + j * 16 + fr] =
+                  f2bf(acc[mh][i][nh][j][r]);
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     // 8 lanes per 128-B row segment, 8 rows per sweep
 #pragma unroll 4
@@ -325,7 +270,15 @@ __device__ __forceinline__ void pgemm_store(char* smem, typename Tile<MF32>::Acc
     float* Ps = P + (size_t)slice * M * N;
 #pragma unroll
     for (int mh = 0; mh < 2; ++mh) {
-      each_half(mh, [&](int row, int nh, int col, float v) { fs[row * 68 + nh * 32 + col] = v; });
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int nh = 0; nh < 2; ++nh)
+#pragma unroll
+          for (int j = 0; j < 2; ++j)
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+              fs[(i * 16 + fk * 4 + r) * 68 + nh * 32 + j * 16 + fr] = acc[mh][i][nh][j][r];
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
 #pragma unroll 4
       for (int it = 0; it < 16; ++it) {
@@ -341,13 +294,21 @@ __device__ __forceinline__ void pgemm_store(char* smem, typename Tile<MF32>::Acc
     // lane fr + 8 the matching up (DPP row rotate by 8 pairs them); 32 outputs per wave row
 #pragma unroll
     for (int mh = 0; mh < 2; ++mh)
-      each_half(mh, [&](int row, int nh, int col, float v) {
-        const float u = row_ror<8>(v);
-        if (fr < 8) {   // col % 16 < 8: a gate column; its up value sits 8 lanes (columns) on
-          const float gv = bf2f(f2bf(v)), uv = bf2f(f2bf(u));   // as the bf16 GEMM output
-          scr[(mh * 64 + row) * SCR_PITCH + nh * 16 + (col >> 4) * 8 + (col & 7)] = f2bf(silu_f(gv) * uv);
-        }
-      });
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int nh = 0; nh < 2; ++nh)
+#pragma unroll
+          for (int j = 0; j < 2; ++j)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              const float v = acc[mh][i][nh][j][r];
+              const float u = row_ror<8>(v);
+              if (fr < 8) {
+                const float gv = bf2f(f2bf(v)), uv = bf2f(f2bf(u));   // as the bf16 GEMM output
+                scr[(mh * 64 + i * 16 + fk * 4 + r) * SCR_PITCH + nh * 16 + j * 8 + fr] = f2bf(silu_f(gv) * uv);
+              }
+            }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     // 32 outputs (64 B) per row: 4 lanes per row, 16 rows per sweep
 #pragma unroll 4
@@ -360,7 +321,7 @@ __device__ __forceinline__ void pgemm_store(char* smem, typename Tile<MF32>::Acc
   }
 }
 
-template <int EPI, bool MF32>
+template <int EPI>
 __global__ __launch_bounds__(512, 2) void pgemm_kernel(const uint16_t* __restrict__ A,
                                                       const uint16_t* __restrict__ W,
                                                       uint16_t* __restrict__ C, float* __restrict__ P,
@@ -393,45 +354,17 @@ __global__ __launch_bounds__(512, 2) void pgemm_kernel(const uint16_t* __restric
   const int bm = first_m + rem % gm, bn = rem / gm;
   const int m0 = bm * BM, n0 = bn * BN;
 
-  typename Tile<MF32>::Acc acc;
-  pgemm_mainloop<MF32>(smem, A, W, M, K, m0, n0, kbeg, Ks / (2 * BK), acc);
-  pgemm_store<EPI, MF32>(smem, acc, C, P, M, N, m0, n0, slice);
+  f32x4 acc[2][4][2][2];
+  pgemm_mainloop(smem, A, W, M, K, m0, n0, kbeg, Ks / (2 * BK), acc);
+  pgemm_store<EPI>(smem, acc, C, P, M, N, m0, n0, slice);
 }
 }  // namespace
-
-// MFMA shape of the tiles (DOCQA_PGEMM_MFMA32=1: 32x32x16, else 16x16x32); read once
-static bool pgemm_mfma32() {
-  static const bool v = [] {
-    const char* e = getenv("DOCQA_PGEMM_MFMA32");
-    return e && atoi(e) == 1;
-  }();
-  return v;
-}
 
 bool docqa_pgemm_ok(int M, int N, int K) {
   if (M <= 0 || N % BN != 0 || K % (2 * BK) != 0) return false;
   // 32-bit per-lane byte offsets: (rows - 1) * K * 2 + 128 must fit
   const uint64_t rows = (uint64_t)(M > N ? M : N);
   return rows * (uint64_t)K * 2ull < (1ull << 32);
-}
-
-// A/B entry for the probes: the kernel with an explicit MFMA shape (mf32 0 / 1)
-int docqa_pgemm_mf(const void* A, const void* W, void* C, int M, int N, int K, int epi, int mf32, hipStream_t s) {
-  if (M == 0) return 0;
-  if (!docqa_pgemm_ok(M, N, K) || (epi != EPI_BF16 && epi != EPI_GLU) || C == nullptr) return -1;
-  if (!docqa_aligned16(A) || !docqa_aligned16(W) || !docqa_aligned16(C)) return -1;
-  const int ntm = (M + BM - 1) / BM, ntn = N / BN, grid = ntm * ntn;
-  const uint16_t *a = (const uint16_t*)A, *w = (const uint16_t*)W;
-  uint16_t* c = (uint16_t*)C;
-  if (mf32) {
-    if (epi == EPI_BF16) pgemm_kernel<EPI_BF16, true><<<grid, 512, 0, s>>>(a, w, c, nullptr, M, N, K, ntm, ntn, 1, K);
-    else pgemm_kernel<EPI_GLU, true><<<grid, 512, 0, s>>>(a, w, c, nullptr, M, N, K, ntm, ntn, 1, K);
-  } else {
-    if (epi == EPI_BF16) pgemm_kernel<EPI_BF16, false><<<grid, 512, 0, s>>>(a, w, c, nullptr, M, N, K, ntm, ntn, 1, K);
-    else pgemm_kernel<EPI_GLU, false><<<grid, 512, 0, s>>>(a, w, c, nullptr, M, N, K, ntm, ntn, 1, K);
-  }
-  DOCQA_CHECK_LAUNCH();
-  return 0;
 }
 
 // epi 0: C [M, N] bf16; epi 1: C [M, N / 2] = silu(gate) * up (8-interleaved gate|up W);
@@ -447,21 +380,12 @@ int docqa_pgemm(const void* A, const void* W, void* C, float* P, int M, int N, i
   const uint16_t *a = (const uint16_t*)A, *w = (const uint16_t*)W;
   uint16_t* c = (uint16_t*)C;
   const int grid = ntm * ntn * S, Ks = K / S;
-  if (pgemm_mfma32()) {
-    if (epi == EPI_BF16)
-      pgemm_kernel<EPI_BF16, true><<<grid, 512, 0, s>>>(a, w, c, P, M, N, K, ntm, ntn, S, Ks);
-    else if (epi == EPI_GLU)
-      pgemm_kernel<EPI_GLU, true><<<grid, 512, 0, s>>>(a, w, c, P, M, N, K, ntm, ntn, S, Ks);
-    else
-      pgemm_kernel<EPI_PARTIAL, true><<<grid, 512, 0, s>>>(a, w, c, P, M, N, K, ntm, ntn, S, Ks);
-  } else {
-    if (epi == EPI_BF16)
-      pgemm_kernel<EPI_BF16, false><<<grid, 512, 0, s>>>(a, w, c, P, M, N, K, ntm, ntn, S, Ks);
-    else if (epi == EPI_GLU)
-      pgemm_kernel<EPI_GLU, false><<<grid, 512, 0, s>>>(a, w, c, P, M, N, K, ntm, ntn, S, Ks);
-    else
-      pgemm_kernel<EPI_PARTIAL, false><<<grid, 512, 0, s>>>(a, w, c, P, M, N, K, ntm, ntn, S, Ks);
-  }
+  if (epi == EPI_BF16)
+    pgemm_kernel<EPI_BF16><<<grid, 512, 0, s>>>(a, w, c, P, M, N, K, ntm, ntn, S, Ks);
+  else if (epi == EPI_GLU)
+    pgemm_kernel<EPI_GLU><<<grid, 512, 0, s>>>(a, w, c, P, M, N, K, ntm, ntn, S, Ks);
+  else
+    pgemm_kernel<EPI_PARTIAL><<<grid, 512, 0, s>>>(a, w, c, P, M, N, K, ntm, ntn, S, Ks);
   DOCQA_CHECK_LAUNCH();
   return 0;
 }
