@@ -8,8 +8,8 @@ of interleaved rounds:
              split-K consumer would pay)
   routed  -- what the prefill forward runs for the projection (ops.prefill_route, the plan
              logic of models/llama.py: split-K plans timed as their slabs alone, since the
-             RoPE / add+RMSNorm consumer that sums them runs either way; hipBLASLt on the
-             split-K slab plans into the consumers); "route" names it
+             RoPE / add+RMSNorm consumer that sums them runs either way); "route" names it
+             (scripts/prefill_mid_probe.py times the same WITH the consumers)
 Usage: python scripts/pgemm_mid_probe.py [M ...]   -> one JSON line per (M, projection)"""
 import json
 import os
