@@ -242,6 +242,9 @@ class _DecodeGraph:
         self.greedy = True
         self.graph = None
         self.hkv = eng.model.hkv
+        # the rows this graph serves reach <= ops.GROUP_MAX_BLOCKS blocks (the grouped decode
+        # kernels' window): always true when the block table itself is that narrow
+        self.groups_fit = eng.max_blocks_per_seq <= ops.GROUP_MAX_BLOCKS
 
     @classmethod
     def view_of(cls, master: "_DecodeGraph", bp: int) -> "_DecodeGraph":
@@ -259,6 +262,7 @@ class _DecodeGraph:
         g.groups = _identity_groups(bp, master.tokens.device, master.hkv)
         g.groups_key = None
         g.cascade, g.greedy, g.graph = False, True, None
+        g.groups_fit = master.groups_fit
         g.hkv = master.hkv
         return g
 
@@ -446,7 +450,8 @@ class LLMEngine:
         if g.cascade:
             meta.shared_table, meta.shared_len = g.shared_table, g.shared_len
             meta.cascade_chunks = self._cascade_chunks(g.bp)
-            if self.group_decode and ops.grouped_decode_ok(self.kv.caches[0][0], g.block_tables, self.model.hq):
+            if self.group_decode and g.groups_fit and ops.grouped_decode_ok(
+                    self.kv.caches[0][0], g.block_tables, self.model.hq, max_blocks=ops.GROUP_MAX_BLOCKS):
                 meta.decode_groups = g.groups
                 meta.decode_defer = g.groups.dim() == 3 and _defer_groups_on()
                 meta.decode_inline = (g.groups.dim() == 3 and g.groups.shape[0] == 2 and _inline_prefix_on()
@@ -462,15 +467,28 @@ class LLMEngine:
         u = torch.rand(full.shape[0], device=full.device)
         return ops.sample(full, g.inv_temp, g.top_k, g.top_p, u)
 
-    def _get_graph(self, bp: int, greedy: bool, cascade: bool = False) -> _DecodeGraph:
-        key = (bp, greedy, cascade)
+    def _get_graph(self, bp: int, greedy: bool, cascade: bool = False, fit: bool = True) -> _DecodeGraph:
+        fit = fit or self.max_blocks_per_seq <= ops.GROUP_MAX_BLOCKS
+        key = (bp, greedy, cascade, fit)
         g = self._graphs.get(key)
         if g is None:
             g = _DecodeGraph(self, bp)
             g.greedy = greedy
             g.cascade = cascade
+            g.groups_fit = fit
             self._graphs[key] = g
         return g
+
+    def groups_fit(self, end_lens: list[int]) -> bool:
+        """Whether every row of a decode batch -- at ``end_lens`` tokens by the end of its
+        decode -- stays within the grouped decode kernels' window (ops.GROUP_MAX_BLOCKS
+        blocks, 4096 tokens).  The block table is sized for MAX_CONTEXT (8192 in the llm-qa
+        service: 128 blocks), but RAG prompts of ~1k tokens fit, so they take the grouped
+        kernels (~70 us per layer at batch 256) instead of the per-row ring kernel (~160)."""
+        if self.max_blocks_per_seq <= ops.GROUP_MAX_BLOCKS:
+            return True
+        BS = self.block_size
+        return all((n + BS - 1) // BS <= ops.GROUP_MAX_BLOCKS for n in end_lens)
 
     def set_order(self, g: _DecodeGraph, lens: list[int], key=None) -> None:
         """Dispatch order of bucket ``g``'s decode rows: active rows [0, len(lens)) by
@@ -561,19 +579,20 @@ class LLMEngine:
         _upload(g.groups, flat)
         g.groups_key = key
 
-    def group_without_prefix(self, B: int) -> bool:
+    def group_without_prefix(self, B: int, fit: bool = True) -> bool:
         """The grouped split-plan decode with the prefix attended inline needs no prefix
         shared by EVERY row: its items start at block 0 and rows are grouped by whatever
         prefix-cache blocks they share (retrieved chunks).  So batches without a common
         template prefix -- the reference QA template puts the context first -- take the
         wave-parallel grouped kernel too instead of the per-row ring kernel (round 5: 162 us
         vs ~70 us per layer at batch 256, profiles/r5_head_kernel_stats.txt).
-        DOCQA_GROUP_NOPREFIX=0 disables; from DOCQA_GROUP_NOPREFIX_MIN_BATCH rows (32)."""
-        return (B >= _GROUP_NOPREFIX_MIN and _GROUP_NOPREFIX and self.group_decode and self.cascade
+        DOCQA_GROUP_NOPREFIX=0 disables; from DOCQA_GROUP_NOPREFIX_MIN_BATCH rows (32).
+        ``fit``: :meth:`groups_fit` of the batch's rows."""
+        return (B >= _GROUP_NOPREFIX_MIN and _GROUP_NOPREFIX and self.group_decode and self.cascade and fit
                 and self.device.type == "cuda" and _split_groups_on() and _inline_prefix_on()
                 and not _defer_groups_on() and not _persist_groups_on()
                 and ops.grouped_decode_ok(self.kv.caches[0][0], torch.empty(0, self.max_blocks_per_seq),
-                                          self.model.hq))
+                                          self.model.hq, max_blocks=ops.GROUP_MAX_BLOCKS))
 
     def _cascade_chunks(self, bp: int) -> int:
         """Key chunks of the shared-prefix kernel: about 256 workgroups of (64 rows, KV
@@ -827,8 +846,9 @@ class LLMEngine:
             nshared = self._shared_prefix_blocks(tables, cached)
             self.stats.attn_kv_blocks += nshared + len({b for t in tables for b in t[nshared:]})
             self.stats.attn_batches += 1
-            grouped = nshared > 0 or self.group_without_prefix(B)
-            g = self._get_graph(_bucket(B, self.max_batch) if self.use_graphs else B, greedy, grouped)
+            fit = self.groups_fit([n + params.max_new_tokens for n in lens])
+            grouped = nshared > 0 or self.group_without_prefix(B, fit)
+            g = self._get_graph(_bucket(B, self.max_batch) if self.use_graphs else B, greedy, grouped, fit)
             if grouped:
                 g.shared_len.fill_(0)
             if nshared:
@@ -849,7 +869,7 @@ class LLMEngine:
             _upload(g.positions, pos)
             _upload(g.context_lens, pos + vl)
             self.set_order(g, lens)
-            if grouped:
+            if grouped and g.groups_fit:
                 self.set_groups(g, tables, [n + params.max_new_tokens for n in lens], nshared)
                 if _DECODE_DUMP:
                     self._dump_decode(g, tables, lens, nshared, params)

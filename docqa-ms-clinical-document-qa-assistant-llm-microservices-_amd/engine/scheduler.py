@@ -538,11 +538,12 @@ class ContinuousEngine:
         g, bp, dmeta = None, 0, None
         if n:
             bp = _bucket(n, eng.max_batch) if self.pad_buckets else n
-            grouped = self._nshared > 0 or eng.group_without_prefix(n)
-            g = self._graph(bp, True, grouped)
+            fit = self._groups_fit()
+            grouped = self._nshared > 0 or eng.group_without_prefix(n, fit)
+            g = self._graph(bp, True, grouped, fit)
             if eng.lpt:
                 eng.set_order(g, [len(r.prompt) + len(r.out) for r in self.running], key=self._version)
-            if grouped:
+            if grouped and g.groups_fit:
                 eng.set_groups(g, [r.blocks for r in self.running],
                                [len(r.prompt) + r.params.max_new_tokens for r in self.running], self._nshared,
                                key=(self._version, self._nshared), ids=[r.rid for r in self.running])
@@ -690,14 +691,20 @@ class ContinuousEngine:
         u = torch.rand(full.shape[0], device=dev)
         return ops.sample(full, it, tk, tp, u).tolist()
 
-    def _graph(self, bp: int, greedy: bool, cascade: bool) -> _DecodeGraph:
-        key = (bp, greedy, cascade)
+    def _graph(self, bp: int, greedy: bool, cascade: bool, fit: bool = True) -> _DecodeGraph:
+        fit = fit or self._master.groups_fit
+        key = (bp, greedy, cascade, fit)
         g = self._graphs.get(key)
         if g is None:
             g = _DecodeGraph.view_of(self._master, bp)
-            g.greedy, g.cascade = greedy, cascade
+            g.greedy, g.cascade, g.groups_fit = greedy, cascade, fit
             self._graphs[key] = g
         return g
+
+    def _groups_fit(self) -> bool:
+        """The running rows stay within the grouped decode kernels' window by the end of
+        their decode (LLMEngine.groups_fit)."""
+        return self.eng.groups_fit([len(r.prompt) + r.params.max_new_tokens for r in self.running])
 
     # ------------------------------------------------------------------ KV on demand
     def _grow_tables(self) -> None:
@@ -780,12 +787,13 @@ class ContinuousEngine:
             return
         bp = _bucket(n, eng.max_batch) if self.pad_buckets else n
         greedy = all(r.params.temperature <= 0 for r in self.running)
-        grouped = self._nshared > 0 or eng.group_without_prefix(n)
-        g = self._graph(bp, greedy, grouped)
+        fit = self._groups_fit()
+        grouped = self._nshared > 0 or eng.group_without_prefix(n, fit)
+        g = self._graph(bp, greedy, grouped, fit)
         if eng.lpt:
             # re-rank only when the running set changed (admission / retirement)
             eng.set_order(g, [len(r.prompt) + len(r.out) for r in self.running], key=self._version)
-        if grouped:
+        if grouped and g.groups_fit:
             eng.set_groups(g, [r.blocks for r in self.running],
                            [len(r.prompt) + r.params.max_new_tokens for r in self.running], self._nshared,
                            key=(self._version, self._nshared), ids=[r.rid for r in self.running])

@@ -822,9 +822,15 @@ def paged_decode_grouped_fused(P, positions, cos_sin, slot_mapping, k_cache, v_c
                                         prefix_len, nchunk, plan, False, tick, True)
 
 
-def grouped_decode_ok(k_cache, block_tables, Hq: int) -> bool:
-    """Shapes the grouped cascade kernel supports (cascade shapes, <= 64 blocks per row)."""
-    return cascade_ok(k_cache, block_tables, Hq) and block_tables.shape[1] <= 64
+GROUP_MAX_BLOCKS = 64   # block positions one grouped-decode work item covers (attn_decode.hip kGroupMaxPos)
+
+
+def grouped_decode_ok(k_cache, block_tables, Hq: int, max_blocks: int | None = None) -> bool:
+    """Shapes the grouped cascade kernel supports: cascade shapes and rows of <= 64 blocks --
+    ``max_blocks``, the most any row of the batch reaches by the end of its decode, or else
+    the block table's width (its capacity)."""
+    nb = block_tables.shape[1] if max_blocks is None else max_blocks
+    return cascade_ok(k_cache, block_tables, Hq) and nb <= GROUP_MAX_BLOCKS
 
 
 def pack_decode_groups(tables: list[list[int]], lens: list[int], skip: int, block_size: int,

@@ -473,3 +473,24 @@ def test_reserve_rolls_back_without_prefix_cache():
     with pytest.raises(MemoryError):
         eng.reserve(prompts, SamplingParams(max_new_tokens=16))
     assert eng.kv.allocator.num_free() == free0
+
+
+def test_grouped_decode_window_follows_the_rows_not_the_table():
+    """The grouped decode kernels cover ops.GROUP_MAX_BLOCKS block positions per work item.
+    With a block table sized for a long MAX_CONTEXT (the llm-qa service: 8192 tokens) the
+    decision follows the rows' own end lengths -- RAG prompts of ~1k tokens keep the grouped
+    kernels -- and a graph built for rows that do not fit never gets decode groups."""
+    from docqa_amd import ops
+    from docqa_amd.engine.llm_engine import LLMEngine
+
+    m = _model()
+    short = LLMEngine(m, max_batch=4, max_context=128, block_size=16, use_graphs=False)
+    assert short.max_blocks_per_seq <= ops.GROUP_MAX_BLOCKS and short.groups_fit([10 ** 6])
+    long_ = LLMEngine(m, max_batch=4, max_context=2048, block_size=16, use_graphs=False)
+    assert long_.max_blocks_per_seq > ops.GROUP_MAX_BLOCKS
+    assert long_.groups_fit([900, 1024]) and not long_.groups_fit([900, 1025])
+    g_fit = long_._get_graph(4, True, True, True)
+    g_long = long_._get_graph(4, True, True, False)
+    assert g_fit is not g_long and g_fit.groups_fit and not g_long.groups_fit
+    assert short._get_graph(4, True, True, False).groups_fit      # a narrow table always fits
+    assert not long_.group_without_prefix(64, fit=False)
