@@ -421,7 +421,7 @@ at::Tensor paged_decode_cascade_grouped(const at::Tensor& q, at::Tensor k_cache,
   const int B = q.size(0);
   const int Hkv = k_cache.size(1), BS = k_cache.size(2), D = k_cache.size(3);
   TORCH_CHECK(D == 128 && BS == 64 && Hq == 4 * Hkv, "grouped decode: head_dim 128, 64-token blocks, GQA 4");
-  TORCH_CHECK(block_tables.size(1) <= 64, "grouped decode: <= 64 blocks per sequence");
+  TORCH_CHECK(block_tables.size(1) <= 256, "grouped decode: block table <= 256 wide (rows <= 64 blocks: the caller)");
   TORCH_CHECK(context_lens.numel() == B && block_tables.size(0) >= B, "grouped decode: B rows");
   TORCH_CHECK(groups.numel() % 4 == 0 && groups.numel() >= 4, "groups: [ngroups, 4]");
   TORCH_CHECK(prefix_table.numel() >= 1 && prefix_len.numel() == 1, "cascade decode: prefix table / length");
@@ -460,8 +460,8 @@ at::Tensor paged_decode_grouped_fused(const at::Tensor& P, const at::Tensor& pos
   const int Hkv = k_cache.size(1), BS = k_cache.size(2), D = k_cache.size(3);
   TORCH_CHECK(D == 128 && BS == 64 && Hq == 4 * Hkv && P.size(2) == (Hq + 2 * Hkv) * D,
               "fused grouped decode: head_dim 128, 64-token blocks, GQA 4, packed QKV width");
-  TORCH_CHECK(block_tables.size(1) <= 64 && context_lens.numel() == B && block_tables.size(0) >= B &&
-              positions.numel() >= B && slot_mapping.numel() >= B, "fused grouped decode: B rows, <= 64 blocks");
+  TORCH_CHECK(block_tables.size(1) <= 256 && context_lens.numel() == B && block_tables.size(0) >= B &&
+              positions.numel() >= B && slot_mapping.numel() >= B, "fused grouped decode: B rows, block table <= 256 wide");
   TORCH_CHECK(plan.dim() == 3 && plan.size(0) == 2 && plan.size(2) == 8, "fused grouped decode: split plan [2, cap, 8]");
   const int cap = plan.size(1);
   c10::DeviceGuard g(P.device());
@@ -501,7 +501,7 @@ at::Tensor paged_decode_cascade_split(const at::Tensor& q, at::Tensor k_cache, a
   const int B = q.size(0);
   const int Hkv = k_cache.size(1), BS = k_cache.size(2), D = k_cache.size(3);
   TORCH_CHECK(D == 128 && BS == 64 && Hq == 4 * Hkv, "split decode: head_dim 128, 64-token blocks, GQA 4");
-  TORCH_CHECK(block_tables.size(1) <= 64, "split decode: <= 64 blocks per sequence");
+  TORCH_CHECK(block_tables.size(1) <= 256, "split decode: block table <= 256 wide (rows <= 64 blocks: the caller)");
   TORCH_CHECK(k_cache.size(0) < (1 << 20), "split decode: < 2^20 KV blocks (packed tile lists)");
   TORCH_CHECK(context_lens.numel() == B && block_tables.size(0) >= B, "split decode: B rows");
   TORCH_CHECK(plan.dim() == 3 && plan.size(0) >= 2 && plan.size(0) <= 3 && plan.size(2) == 8 && plan.size(1) >= 1,

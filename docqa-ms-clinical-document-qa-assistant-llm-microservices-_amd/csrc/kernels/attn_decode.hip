@@ -982,6 +982,11 @@ __global__ __launch_bounds__(256) void paged_decode_mfma_kernel(
 // then streamed through the same LDS-DMA ring as the MFMA kernel.  Keys [P, L) per row
 // (P: the cascade prefix, attended by the prefix kernel and merged here).
 constexpr int kGroupMaxPos = 64;     // block positions beyond the cascade prefix (4096 tokens)
+// Block-table WIDTH the grouped kernels accept (a table sized for an 8192-token MAX_CONTEXT
+// is 128 wide); every ROW must still end within kGroupMaxPos positions of its window start,
+// which the caller guarantees (LLMEngine.groups_fit: rows of <= 64 blocks by the end of
+// their decode) -- positions past the window would not be attended
+constexpr int kGroupMaxTable = 256;
 
 // Diagnostic timeline of the group kernel (off unless docqa_set_decode_trace set a buffer):
 // per workgroup 8 int64 -- entry, tile list + Q ready, first tile landed, loop end, exit
@@ -2023,7 +2028,7 @@ int docqa_paged_decode_cascade_grouped(const void* q, int q_stride, void* k_cach
                                        float* pacc, float* pml, const int* groups, int ngroups,
                                        hipStream_t s) {
   if (B == 0) return 0;
-  if (BS != 64 || maxb > kGroupMaxPos || Hq != 4 * Hkv || nchunk < 1 || nchunk > kCascadeMaxChunks ||
+  if (BS != 64 || maxb > kGroupMaxTable || Hq != 4 * Hkv || nchunk < 1 || nchunk > kCascadeMaxChunks ||
       ngroups < 1)
     return -1;
   int rc = docqa_cascade_prefix(q, q_stride, B, Hq, Hkv, scale, k_cache, v_cache, prefix_table, plen, BS,
@@ -2130,7 +2135,7 @@ int docqa_paged_decode_cascade_split(const void* q, int q_stride, void* k_cache,
                                      int inline_prefix, const float* fP, int fS, const int* positions,
                                      const float* cos_sin, const int* slot_mapping) {
   if (B == 0) return 0;
-  if (BS != 64 || maxb > kGroupMaxPos || Hq != 4 * Hkv || nchunk < 1 || nchunk > kCascadeMaxChunks || cap < 1)
+  if (BS != 64 || maxb > kGroupMaxTable || Hq != 4 * Hkv || nchunk < 1 || nchunk > kCascadeMaxChunks || cap < 1)
     return -1;
   // inline_prefix: no prefix kernel -- the plan's items start at block 0 (built with skip 0),
   // so every group streams the shared template blocks itself (L2 hits after the first group)
@@ -2204,7 +2209,7 @@ int docqa_paged_decode_cascade_persist(const void* q, int q_stride, void* k_cach
                                        float* pacc, float* pml, const int* items, const int* merges,
                                        const int* bins, int cap, float* ws_acc, float* ws_ml, hipStream_t s) {
   if (B == 0) return 0;
-  if (BS != 64 || maxb > kGroupMaxPos || Hq != 4 * Hkv || nchunk < 1 || nchunk > kCascadeMaxChunks || cap < 1)
+  if (BS != 64 || maxb > kGroupMaxTable || Hq != 4 * Hkv || nchunk < 1 || nchunk > kCascadeMaxChunks || cap < 1)
     return -1;
   // The group kernel no longer reads the prefix partials (the merge does), so the shared-
   // prefix kernel runs on a side stream beside it (cascade_prefix_forked).

@@ -376,3 +376,42 @@ def test_remapped_plan_after_retirement_matches_per_row(native, variant):
             assert err < 3e-2, err
     finally:
         torch.ops.docqa.set_group_wave(was)
+
+
+@pytest.mark.parametrize("B,Hkv,seed", [(37, 8, 0), (256, 8, 3)])
+@pytest.mark.parametrize("inline", [False, True])
+def test_wave_kernel_on_a_wide_block_table(native, B, Hkv, seed, inline):
+    """A block table sized for a long MAX_CONTEXT (128 wide: the llm-qa service's 8192
+    tokens) with rows that end within 64 blocks (LLMEngine.groups_fit) -- the grouped wave
+    kernel gives the result it gives on the same rows in a 64-wide table and matches the
+    fp32 reference."""
+    Hq, D, BS, Pb, maxb = 4 * Hkv, 128, 64, 3, 12
+    tables, lens, nblk = _trie_batch(B, Pb, maxb, seed)
+    kc = torch.randn(nblk, Hkv, BS, D, device="cuda", dtype=torch.bfloat16)
+    vc = torch.randn_like(kc)
+    narrow = torch.tensor([t + [0] * (64 - len(t)) for t in tables], dtype=torch.int32, device="cuda")
+    wide = torch.zeros(B, 128, dtype=torch.int32, device="cuda")
+    wide[:, :64] = narrow
+    wide[:, 64:] = 0              # past every row's end: attending these would change the result
+    cl = torch.tensor(lens, dtype=torch.int32, device="cuda")
+    q = torch.randn(B, (Hq + 2 * Hkv) * D, device="cuda", dtype=torch.bfloat16)
+    plen = torch.tensor([Pb * BS], dtype=torch.int32, device="cuda")
+    scale = 1 / math.sqrt(D)
+    end_lens = [L + 128 for L in lens]
+    quads = native.pack_decode_groups(tables, end_lens, Pb, BS, (B + 1) // 2)
+    plan = native.split_decode_groups(quads, tables, end_lens, 0 if inline else Pb, BS, max(B, 4), 12).cuda()
+    outs = []
+    for bt in (narrow, wide):
+        pt = torch.zeros(bt.shape[1], dtype=torch.int32, device="cuda")
+        pt[:Pb] = bt[0, :Pb]
+        tick = torch.zeros(plan.shape[1] * Hkv, dtype=torch.int32, device="cuda")
+        outs.append(native.paged_decode_cascade_grouped(q, kc, vc, bt, cl, Hq, scale, pt, plen, 4, plan, False,
+                                                        tick, inline))
+        torch.cuda.synchronize()
+        assert int(tick.abs().sum()) == 0
+    with native.use_reference():
+        pt = torch.zeros(64, dtype=torch.int32, device="cuda")
+        pt[:Pb] = narrow[0, :Pb]
+        ref32 = native.paged_decode_cascade(q, kc, vc, narrow, cl, Hq, 64 * BS, scale, pt, plen, 4)
+    assert torch.equal(outs[0], outs[1])
+    assert (outs[1].float() - ref32.float()).abs().max().item() < 3e-2
