@@ -775,6 +775,35 @@ at::Tensor dgemm_glu_xn(const at::Tensor& Pin, const at::Tensor& res_in, at::Ten
   return out;
 }
 
+// batch-1 GEMV (dgemm.hip gemv_kernel: weight rows streamed straight into VGPRs): fp32
+// slabs [S, 1, N] of x . w^T (rows weight rows per workgroup), or with glu the SwiGLU row
+// [1, N / 2] of an 8-interleaved gate|up weight
+at::Tensor gemv(const at::Tensor& x, const at::Tensor& w, int64_t splits, int64_t rows, bool glu) {
+  CHECK_GPU(x); CHECK_BF16(x); CHECK_BF16(w); CHECK_CONTIG(x); CHECK_CONTIG(w); CHECK_ALIGN16(x); CHECK_ALIGN16(w);
+  const int K = x.size(-1), N = w.size(0);
+  TORCH_CHECK(w.size(1) == K && x.numel() == K, "gemv: one row, K mismatch");
+  c10::DeviceGuard g(x.device());
+  at::Tensor out = glu ? at::empty({1, N / 2}, x.options()) : at::empty({splits, 1, N}, x.options().dtype(at::kFloat));
+  CHECK_RC(docqa_gemv(x.data_ptr(), w.data_ptr(), glu ? out.data_ptr() : nullptr,
+                      glu ? nullptr : out.data_ptr<float>(), N, K, (int)splits, (int)rows, glu ? 1 : 0, nullptr, 0,
+                      nullptr, nullptr, nullptr, 0.f, stream()), "gemv");
+  return out;
+}
+
+// batch-1 GEMV whose input row is rmsnorm(res_in + bf16(sum Pin)) * gamma built in LDS
+// (XNormIn); res_out <- res_in + bf16(sum Pin)
+at::Tensor gemv_xn(const at::Tensor& Pin, const at::Tensor& res_in, at::Tensor res_out, const at::Tensor& gamma,
+                   double eps, const at::Tensor& w, int64_t splits, int64_t rows, bool glu) {
+  check_xn(Pin, res_in, res_out, gamma, w);
+  const int N = w.size(0), K = w.size(1);
+  c10::DeviceGuard g(Pin.device());
+  at::Tensor out = glu ? at::empty({1, N / 2}, res_in.options()) : at::empty({splits, 1, N}, Pin.options());
+  CHECK_RC(docqa_gemv(nullptr, w.data_ptr(), glu ? out.data_ptr() : nullptr, glu ? nullptr : out.data_ptr<float>(),
+                      N, K, (int)splits, (int)rows, glu ? 1 : 0, Pin.data_ptr<float>(), Pin.size(0), res_in.data_ptr(),
+                      res_out.data_ptr(), gamma.data_ptr(), (float)eps, stream()), "gemv_xn");
+  return out;
+}
+
 at::Tensor dgemm(const at::Tensor& x, const at::Tensor& w, int64_t splits) {
   CHECK_GPU(x); CHECK_BF16(x); CHECK_BF16(w); CHECK_CONTIG(x); CHECK_CONTIG(w);
   const int K = x.size(-1), N = w.size(0);
@@ -1262,6 +1291,8 @@ TORCH_LIBRARY(docqa, m) {
   m.def("dgemm_partial_xn(Tensor Pin, Tensor res_in, Tensor(a!) res_out, Tensor gamma, float eps, Tensor w, "
         "int splits) -> Tensor");
   m.def("dgemm_glu_xn(Tensor Pin, Tensor res_in, Tensor(a!) res_out, Tensor gamma, float eps, Tensor w) -> Tensor");
+  m.def("gemv(Tensor x, Tensor w, int splits=1, int rows=16, bool glu=False) -> Tensor");
+  m.def("gemv_xn(Tensor Pin, Tensor res_in, Tensor(a!) res_out, Tensor gamma, float eps, Tensor w, int splits=1, int rows=16, bool glu=False) -> Tensor");
   m.def("dgemm_add_rmsnorm(Tensor x, Tensor w, int splits, Tensor(a!) residual, Tensor gamma, float eps, "
         "Tensor(t!) tick) -> Tensor");
   m.def("dgemm_glu(Tensor x, Tensor w) -> Tensor");
@@ -1341,6 +1372,8 @@ TORCH_LIBRARY_IMPL(docqa, CUDA, m) {
   m.impl("embed_rmsnorm", &embed_rmsnorm);
   m.impl("dgemm_partial_xn", &dgemm_partial_xn);
   m.impl("dgemm_glu_xn", &dgemm_glu_xn);
+  m.impl("gemv", &gemv);
+  m.impl("gemv_xn", &gemv_xn);
   m.impl("dgemm_add_rmsnorm", &dgemm_add_rmsnorm);
   m.impl("dgemm_glu", &dgemm_glu);
   m.impl("mgemm", &mgemm);

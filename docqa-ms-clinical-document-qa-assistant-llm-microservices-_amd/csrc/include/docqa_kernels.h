@@ -125,6 +125,11 @@ int docqa_dgemm_partial_xn(const float* Pin, int Sin, const void* res_in, void* 
                            float eps, const void* W, float* P, int N, int K, int S, hipStream_t s);
 int docqa_dgemm_glu_xn(const float* Pin, int Sin, const void* res_in, void* res_out, const void* gamma, float eps,
                        const void* W, void* Y, int N, int K, hipStream_t s);
+// batch-1 GEMV (dgemm.hip gemv_kernel): epi 0 fp32 slabs P [S, 1, N], epi 1 SwiGLU Y [1, N / 2];
+// Pin != null: the input row from the previous projection's slabs (XNormIn)
+int docqa_gemv(const void* X, const void* W, void* Y, float* P, int N, int K, int S, int R, int epi,
+               const float* Pin, int Sin, const void* res_in, void* res_out, const void* gamma, float eps,
+               hipStream_t s);
 int docqa_embed_rmsnorm(const int* ids, const void* table, const void* w, void* h, void* x, int T, int H, int V,
                         float eps, hipStream_t s);
 int docqa_fp32_gemm_nt(const float* x, int nq, int d, const float* w, int n, float* out, hipStream_t s);

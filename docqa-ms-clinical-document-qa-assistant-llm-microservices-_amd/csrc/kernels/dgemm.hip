@@ -33,6 +33,7 @@
 #include "docqa_argmax.h"
 #include "docqa_norm_row.h"
 #include <stdlib.h>
+#include <type_traits>
 
 using namespace docqa;
 
@@ -691,6 +692,147 @@ int docqa_dgemm_argmax(const void* X, const void* W, int64_t* out, float* outv, 
   launch_mt<EPI_ARGMAX, 4>(mt, dim3(N / BN), s, (const uint16_t*)X, (const uint16_t*)W, nullptr, nullptr, M, N, K,
                            K, ws_v, ws_i, n_valid);
   argmax_merge_kernel<<<M, 256, 0, s>>>(ws_v, ws_i, N / BN, out, outv);
+  DOCQA_CHECK_LAUNCH();
+  return 0;
+}
+
+// ---------------------------------------------------------------------------------------
+// Batch-1 GEMV (one decode row): y[N] = x[K] . W[N, K]^T with NO MFMA and NO LDS ring.  At
+// M = 1 the projection is a pure weight stream, and the ring kernel above tops out at
+// ~4.3 TB/s there (profiles/r4_b1_decode_gemm_split_probe.log) with two 16-KB stages in
+// flight per workgroup.  Here every lane issues ALL of its weight loads at once, straight
+// into VGPRs (R weight rows x C 16-B chunks: 32 loads = 128 KB per 256-thread workgroup in
+// flight for the 4096-wide projections), then retires them row by row in issue order
+// (vmcnt counts loads back in order) into v_dot2_f32_bf16 dot products against the input
+// row; the 4 waves split K and meet in LDS.  Workgroup = R output rows x one K slice.
+//   * EPI_PARTIAL: fp32 slab P[slice][n] for the split-K consumers (same layout as dgemm);
+//   * EPI_GLU: R = 16 rows = one 8-interleaved gate|up group -> 8 SwiGLU outputs, bf16;
+//   * XN: the input row is built in LDS from the previous projection's slabs (XNormIn),
+//     its loads queued behind the weight loads (the stream is already in flight).
+// Shapes: N % R == 0, Ks = K / S with Ks % 2048 == 0 (C = Ks / 2048 chunks per lane), and
+// R x C <= 32 loads per lane (the 6-bit vmcnt counter holds at most 63 outstanding).
+template <int I, int N, typename F>
+__device__ __forceinline__ void static_for(F&& f) {
+  if constexpr (I < N) {
+    f(std::integral_constant<int, I>{});
+    static_for<I + 1, N>(f);
+  }
+}
+
+template <int R, int C, int EPI, bool XN>
+__global__ __launch_bounds__(256) void gemv_kernel(const uint16_t* __restrict__ X, const uint16_t* __restrict__ W,
+                                                   uint16_t* __restrict__ Y, float* __restrict__ P, int N, int K,
+                                                   int Ks, XNormIn xn) {
+  static_assert(EPI == EPI_PARTIAL || (EPI == EPI_GLU && R == 16), "GLU: one 16-row gate|up group");
+  static_assert(R * C <= 32, "loads in flight per lane must fit the vmcnt counter");
+  __shared__ __attribute__((aligned(16))) uint16_t sx[XN ? kXnMaxK : 8];
+  __shared__ float red[4][R];
+  __shared__ float xred[4];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int n0 = blockIdx.x * R, slice = blockIdx.y, kbeg = slice * Ks;
+  const int kq = Ks >> 2;                         // k per wave
+  const int kw = kbeg + wave * kq;                // this wave's k range
+  // weight chunk (r, c) of this lane: row n0 + r, k = kw + c * 512 + lane * 8
+  bf16x8 w[R][C];
+  const uint16_t* wb = W + (size_t)n0 * K + kw + lane * 8;
+#pragma unroll
+  for (int r = 0; r < R; ++r)
+#pragma unroll
+    for (int c = 0; c < C; ++c) gload16<0>(w[r][c], wb + (size_t)r * K + c * 512);
+  bf16x8 x[C];
+  if constexpr (XN) {
+    xnorm_prologue(xn, K, kbeg, Ks, blockIdx.x == 0 && blockIdx.y == 0, sx, xred);
+#pragma unroll
+    for (int c = 0; c < C; ++c) x[c] = *reinterpret_cast<const bf16x8*>(sx + (kw - kbeg) + c * 512 + lane * 8);
+  } else {
+#pragma unroll
+    for (int c = 0; c < C; ++c) x[c] = *reinterpret_cast<const bf16x8*>(X + kw + c * 512 + lane * 8);
+  }
+  float acc[R];
+  static_for<0, R>([&](auto rc) {
+    constexpr int r = decltype(rc)::value;
+    // row r's chunks landed: everything issued after them is the later rows' C chunks each
+    constexpr int LEFT = (R - 1 - r) * C;
+    if constexpr (C == 1) wait_vm_n<LEFT, 1>(*reinterpret_cast<bf16x8(*)[1]>(&w[r][0]));
+    else if constexpr (C == 2) wait_vm_n<LEFT, 2>(*reinterpret_cast<bf16x8(*)[2]>(&w[r][0]));
+    else if constexpr (C == 4) wait_vm_n<LEFT, 4>(*reinterpret_cast<bf16x8(*)[4]>(&w[r][0]));
+    else {
+      static_assert(C == 7, "C in {1, 2, 4, 7}");
+      asm volatile("s_waitcnt vmcnt(%7)" : "+v"(w[r][0]), "+v"(w[r][1]), "+v"(w[r][2]), "+v"(w[r][3]), "+v"(w[r][4]),
+                   "+v"(w[r][5]), "+v"(w[r][6]) : "i"(LEFT) : "memory");
+    }
+    float a = 0.f;
+#pragma unroll
+    for (int c = 0; c < C; ++c) {
+      const bf16x8 wv = w[r][c], xv = x[c];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const bf16x2 wa = {wv[2 * j], wv[2 * j + 1]}, xa = {xv[2 * j], xv[2 * j + 1]};
+        a = __builtin_amdgcn_fdot2_f32_bf16(wa, xa, a, false);
+      }
+    }
+    acc[r] = wave_sum(a);
+  });
+  if (lane == 0) {
+#pragma unroll
+    for (int r = 0; r < R; ++r) red[wave][r] = acc[r];
+  }
+  __syncthreads();
+  if constexpr (EPI == EPI_PARTIAL) {
+    if (tid < R) P[(size_t)slice * N + n0 + tid] = red[0][tid] + red[1][tid] + red[2][tid] + red[3][tid];
+  } else {
+    // gate rows n0 .. n0 + 7, up rows n0 + 8 .. n0 + 15 -> outputs n0 / 2 .. n0 / 2 + 7
+    if (tid < 8) {
+      const float g = red[0][tid] + red[1][tid] + red[2][tid] + red[3][tid];
+      const float u = red[0][tid + 8] + red[1][tid + 8] + red[2][tid + 8] + red[3][tid + 8];
+      const float gv = bf2f(f2bf(g)), uv = bf2f(f2bf(u));   // as the bf16 GEMM output
+      Y[(n0 >> 1) + tid] = f2bf(silu_f(gv) * uv);
+    }
+  }
+}
+
+template <int EPI, bool XN>
+static int launch_gemv(int R, int C, dim3 grid, hipStream_t s, const uint16_t* x, const uint16_t* w, uint16_t* y,
+                       float* p, int N, int K, int Ks, const XNormIn& xn) {
+#define GEMV_CASE(RR, CC)                                                                                    \
+  if (R == RR && C == CC) {                                                                                  \
+    gemv_kernel<RR, CC, EPI, XN><<<grid, 256, 0, s>>>(x, w, y, p, N, K, Ks, xn);                             \
+    return 0;                                                                                                \
+  }
+  if constexpr (EPI == EPI_GLU) {
+    GEMV_CASE(16, 1) GEMV_CASE(16, 2)
+  } else {
+    GEMV_CASE(16, 1) GEMV_CASE(16, 2) GEMV_CASE(8, 2) GEMV_CASE(8, 4) GEMV_CASE(4, 4) GEMV_CASE(4, 7)
+    GEMV_CASE(8, 1) GEMV_CASE(4, 2) GEMV_CASE(4, 1)
+  }
+#undef GEMV_CASE
+  return -1;
+}
+
+// Batch-1 GEMV (see gemv_kernel).  epi 0: fp32 slabs P [S, 1, N]; epi 1: SwiGLU Y [1, N / 2]
+// (R = 16, S = 1).  xn (nullable): the input row from the previous projection's slabs.
+int docqa_gemv(const void* X, const void* W, void* Y, float* P, int N, int K, int S, int R, int epi,
+               const float* Pin, int Sin, const void* res_in, void* res_out, const void* gamma, float eps,
+               hipStream_t s) {
+  if (S < 1 || K % S || (K / S) % 2048 || N % R || R < 1) return -1;
+  const int Ks = K / S, C = Ks / 2048;
+  const bool xnm = Pin != nullptr;
+  const XNormIn xn{Pin, Sin, (const uint16_t*)res_in, (uint16_t*)res_out, (const uint16_t*)gamma, eps};
+  if (xnm && !xn_ok(N, K, 1, R, xn)) return -1;
+  if (!xnm && !X) return -1;
+  if (epi == 1 ? (R != 16 || S != 1 || !Y) : !P) return -1;
+  const dim3 grid(N / R, S);
+  const uint16_t* x = (const uint16_t*)X;
+  const uint16_t* w = (const uint16_t*)W;
+  int rc;
+  if (epi == 1)
+    rc = xnm ? launch_gemv<EPI_GLU, true>(R, C, grid, s, x, w, (uint16_t*)Y, nullptr, N, K, Ks, xn)
+             : launch_gemv<EPI_GLU, false>(R, C, grid, s, x, w, (uint16_t*)Y, nullptr, N, K, Ks, xn);
+  else
+    rc = xnm ? launch_gemv<EPI_PARTIAL, true>(R, C, grid, s, x, w, nullptr, P, N, K, Ks, xn)
+             : launch_gemv<EPI_PARTIAL, false>(R, C, grid, s, x, w, nullptr, P, N, K, Ks, xn);
+  if (rc) return rc;
   DOCQA_CHECK_LAUNCH();
   return 0;
 }

@@ -318,6 +318,11 @@ class LlamaModel:
         if (decode or small) and self.layers:
             L0 = self.layers[0]
             for k in ("qkv", "o", "down"):
+                Sg, R = ops.gemv_plan(M, *L0[k].shape) if x.is_cuda else (0, 0)
+                if Sg:
+                    # one row: the register-streaming GEMV (no LDS ring) -- QKV / O
+                    plans[k] = (Sg, lambda a, w, S=Sg, R=R: ops.gemv_partial(a, w, S, R))
+                    continue
                 S, c = ops.mid_plan(M, *L0[k].shape)
                 if S:
                     plans[k] = (S, lambda a, w, S=S, c=c: (ops.mgemm_partial(a, w, S, c) if S > 1
@@ -334,7 +339,9 @@ class LlamaModel:
                 if Sd:
                     plans["down"] = (Sd, lambda a, w, S=Sd: ops.pgemm_partial(a, w, S))
             Sg, cg = ops.mid_plan(M, *L0["gate_up"].shape, glu=True)
-            if small and (ops.pgemm_ok(M, *L0["gate_up"].shape)
+            if decode and x.is_cuda and ops.gemv_glu_ok(M, *L0["gate_up"].shape):
+                glu = ops.gemv_glu        # one row: the register-streaming GEMV with SwiGLU
+            elif small and (ops.pgemm_ok(M, *L0["gate_up"].shape)
                           or ops.prefill_split_plan(M, *L0["gate_up"].shape, glu=True)):
                 # 256 x 256 tiles with SwiGLU (104 vs 141 us at M = 512), or their split-K
                 # slabs into the SwiGLU consumer where too few tiles (the 70B TP-8 shard)
@@ -393,7 +400,11 @@ class LlamaModel:
             kc, vc = kv_caches[i]
             if sq:
                 if xn and pd is not None:
-                    qkv_slabs = ops.dgemm_partial_xn(pd, residual, res2, L["in_norm"], eps, L["qkv"], sq)
+                    Sg, R = ops.gemv_plan(M, *L["qkv"].shape)
+                    if Sg == sq:
+                        qkv_slabs = ops.gemv_partial_xn(pd, residual, res2, L["in_norm"], eps, L["qkv"], sq, R)
+                    else:
+                        qkv_slabs = ops.dgemm_partial_xn(pd, residual, res2, L["in_norm"], eps, L["qkv"], sq)
                     residual, res2 = res2, residual
                 else:
                     qkv_slabs = qkv_part(x, L["qkv"])
@@ -480,7 +491,10 @@ class LlamaModel:
                                      meta.max_context, self.scale, meta.seq_order)
             nxt = self.layers[i + 1]["in_norm"] if i + 1 < nl else self.final_norm
             if xn:
-                g = ops.dgemm_glu_xn(o_part(a, L["o"]), residual, res2, L["post_norm"], eps, L["gate_up"])
+                if ops.gemv_glu_ok(M, *L["gate_up"].shape):
+                    g = ops.gemv_glu_xn(o_part(a, L["o"]), residual, res2, L["post_norm"], eps, L["gate_up"])
+                else:
+                    g = ops.dgemm_glu_xn(o_part(a, L["o"]), residual, res2, L["post_norm"], eps, L["gate_up"])
                 residual, res2 = res2, residual
                 pd = down_part(g, L["down"])
                 if i + 1 == nl:

@@ -599,6 +599,57 @@ def dgemm_glu_xn(Pin, res_in, res_out, gamma, eps: float, w_il):
     return silu_mul(torch.nn.functional.linear(x, w_il), interleaved=True)
 
 
+_GEMV = os.environ.get("DOCQA_GEMV", "1") != "0"
+
+
+def gemv_plan(M: int, N: int, K: int) -> tuple[int, int]:
+    """(split-K count, weight rows per workgroup) of the batch-1 register-streaming GEMV
+    (dgemm.hip gemv_kernel: every lane issues all its weight loads at once, no LDS ring)
+    for a one-row projection; (0, 0) where the ring kernel stays.  Measured at M = 1 on the
+    Llama-3-8B projections, weights rotated past the MALL (profiles/r6_gemv_probe.log): O
+    7.8 vs 8.8 us for the ring kernel's plan; the QKV with its input row built in-kernel
+    (XNormIn: every workgroup runs that prologue, so few wide workgroups win) 13.3 vs 15.4
+    at 8 rows per workgroup, no split (17.9 at 4 rows x 2 slices); the down projection
+    (K 14336) stays on the ring (21.3 vs 20.9).  DOCQA_GEMV=0 disables."""
+    if not _GEMV or M != 1 or N % 8 or K > 8192 or K % 2048:
+        return 0, 0
+    return (1, 8) if K <= 4096 else ((2, 8) if K % 4096 == 0 else (0, 0))
+
+
+def gemv_glu_ok(M: int, N: int, K: int) -> bool:
+    """The batch-1 gate|up projection with SwiGLU on the GEMV (one 16-row gate|up group per
+    workgroup): 41.1 vs 47.6 us for the ring kernel at Llama-3-8B (profiles/r6_gemv_probe.log)."""
+    return _GEMV and M == 1 and N % 16 == 0 and K % 2048 == 0 and (K // 2048) in (1, 2)
+
+
+def gemv_glu(x, w_il):
+    """silu(x Wg^T) * (x Wu^T) for one row on the batch-1 GEMV (:func:`gemv_glu_ok`)."""
+    if _gpu(x):
+        return _native().gemv(x.contiguous(), w_il, 1, 16, True)
+    return glu_linear(x, w_il)
+
+
+def gemv_partial(x, w, splits: int, rows: int):
+    """fp32 slabs [S, 1, N] of one row x @ w^T on the batch-1 GEMV (:func:`gemv_plan`)."""
+    if _gpu(x):
+        return _native().gemv(x.contiguous(), w, int(splits), int(rows), False)
+    return dgemm_partial(x, w, splits, 64)
+
+
+def gemv_partial_xn(Pin, res_in, res_out, gamma, eps: float, w, splits: int, rows: int):
+    """:func:`dgemm_partial_xn` (input row built in-kernel) on the batch-1 GEMV."""
+    if _gpu(Pin):
+        return _native().gemv_xn(Pin, res_in, res_out, gamma, float(eps), w, int(splits), int(rows), False)
+    return dgemm_partial_xn(Pin, res_in, res_out, gamma, eps, w, splits)
+
+
+def gemv_glu_xn(Pin, res_in, res_out, gamma, eps: float, w_il):
+    """:func:`dgemm_glu_xn` (input row built in-kernel, SwiGLU epilogue) on the batch-1 GEMV."""
+    if _gpu(Pin):
+        return _native().gemv_xn(Pin, res_in, res_out, gamma, float(eps), w_il, 1, 16, True)
+    return dgemm_glu_xn(Pin, res_in, res_out, gamma, eps, w_il)
+
+
 NORM_FUSE_ROWS = 4
 # off by default: the last-workgroup add + RMSNorm tail (one workgroup reading every slab at
 # agent scope) costs more than the add_rmsnorm_splitk launch it replaces -- batch-1 p50
