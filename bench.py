@@ -225,6 +225,8 @@ def main() -> None:
         }
         if retrieval is not None:
             out["retrieval_check"] = retrieval
+        if world > 1:
+            out["shard_gather"] = getattr(pipe.index, "ipc_status", "process-group gather")
         if cuda:   # the box: CU count and clocks differ between pool machines
             pr = torch.cuda.get_device_properties(local_rank)
             out["device"] = {"name": pr.name, "cus": pr.multi_processor_count,

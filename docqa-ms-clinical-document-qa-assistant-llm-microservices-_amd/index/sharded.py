@@ -31,6 +31,8 @@ from __future__ import annotations
 
 import threading
 
+import os
+
 import torch
 import torch.distributed as dist
 
@@ -60,6 +62,7 @@ class ShardedIndex:
         self._offset = 0
         self._ntotal = local.ntotal
         self._ipc = None
+        self.ipc_status = "process-group gather"   # enable_ipc: "ipc" once its handshake passed
         # per-thread search state: the error-word snapshot of this thread's last IPC search
         # (a serving front end searches from its prep thread while the indexer searches from
         # request threads; one instance-wide slot let one thread's search overwrite
@@ -75,7 +78,7 @@ class ShardedIndex:
         first search.  ``factory``: the gather's constructor (tests)."""
         if self.world == 1 or self._ipc is not None or self.local.device.type != "cuda":
             return self._ipc is not None
-        import os
+        from ..parallel.custom_ar import CollectiveError
 
         if factory is None:
             from ..parallel.custom_ar import CustomAllReduce as factory
@@ -87,8 +90,27 @@ class ShardedIndex:
         except Exception as e:  # noqa: BLE001 - collective decision inside the constructor
             print(f"[sharded] IPC all-gather unavailable ({e}); using the process group", flush=True)
             self._ipc = None
+            self.ipc_status = "unavailable: process-group gather"
         if self._ipc is not None:
-            self._handshake()
+            try:
+                self._handshake()
+            except CollectiveError as e:
+                # DOCQA_IPC_HANDSHAKE=strict: fail the run here.  Default (fallback): every
+                # rank saw the same verdict (_handshake agrees over the process group), so all
+                # of them drop the IPC path together and gather through the process group --
+                # never a silently wrong merge; bench.py's sharded-vs-unsharded check still
+                # runs at the end, and ipc_status says what happened
+                if os.environ.get("DOCQA_IPC_HANDSHAKE", "fallback") == "strict":
+                    raise
+                print(f"[sharded] {e}; falling back to the process-group gather", flush=True)
+                try:
+                    self._ipc.close()
+                except Exception:  # noqa: BLE001 - best effort, the path is abandoned either way
+                    pass
+                self._ipc = None
+                self.ipc_status = "handshake failed: process-group gather"
+                return False
+            self.ipc_status = "ipc"
         return self._ipc is not None
 
     def _handshake(self) -> None:

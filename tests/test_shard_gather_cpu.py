@@ -174,7 +174,9 @@ def test_gather_wait_bound_expires_on_delayed_peer(monkeypatch):
 
 def test_ipc_handshake_rejects_a_corrupted_peer_row(monkeypatch):
     """enable_ipc's handshake gather must return every peer's (rank, world, offset, size,
-    magic) row exactly; one wrong word fails the run before the first search."""
+    magic) row exactly; one wrong word fails the run before the first search
+    (DOCQA_IPC_HANDSHAKE=strict)."""
+    monkeypatch.setenv("DOCQA_IPC_HANDSHAKE", "strict")
     s, _, made, factory = _ipc_index(monkeypatch, "100")
 
     def corrupting(**kw):
@@ -188,6 +190,7 @@ def test_ipc_handshake_rejects_a_corrupted_peer_row(monkeypatch):
 
 
 def test_ipc_handshake_rejects_a_peer_that_never_arrives(monkeypatch):
+    monkeypatch.setenv("DOCQA_IPC_HANDSHAKE", "strict")
     s, _, made, factory = _ipc_index(monkeypatch, "20")
 
     def late(**kw):
@@ -196,3 +199,20 @@ def test_ipc_handshake_rejects_a_peer_that_never_arrives(monkeypatch):
         return ipc
     with pytest.raises(CollectiveError):
         s.enable_ipc(factory=late)
+
+
+def test_ipc_handshake_failure_falls_back_to_the_process_group(monkeypatch):
+    """Default mode: a failed handshake drops the IPC path on every rank together -- the
+    searches then gather through the process group (never the unverified peer memory) and
+    ipc_status (bench.py's shard_gather field) records it."""
+    monkeypatch.delenv("DOCQA_IPC_HANDSHAKE", raising=False)
+    s, _, made, factory = _ipc_index(monkeypatch, "100")
+
+    def corrupting(**kw):
+        ipc = factory(**kw)
+        ipc.corrupt = True
+        return ipc
+    assert s.enable_ipc(factory=corrupting) is False
+    assert s._ipc is None and s.ipc_status.startswith("handshake failed")
+    s2, _, _, factory2 = _ipc_index(monkeypatch, "100")
+    assert s2.enable_ipc(factory=factory2) and s2.ipc_status == "ipc"
