@@ -53,6 +53,13 @@ __device__ __forceinline__ void gload16(bf16x8& d, const void* p) {
 
 // wait until at most N vector-memory ops are outstanding, naming the registers that
 // become valid so nothing reading them is scheduled above the wait
+// the same with the non-temporal hint: once-read weight streams (nt: aux = 2,
+// MI355X_MICROARCH.md nt-weights) do not displace the L2 lines the next launch re-reads
+template <int OFF>
+__device__ __forceinline__ void gload16_nt(bf16x8& d, const void* p) {
+  asm volatile("global_load_dwordx4 %0, %1, off offset:%2 nt" : "=v"(d) : "v"(p), "i"(OFF) : "memory");
+}
+
 template <int N, int SPW>
 __device__ __forceinline__ void wait_vm_n(bf16x8 (&x)[SPW]) {
   if constexpr (SPW == 1)
@@ -719,7 +726,7 @@ __device__ __forceinline__ void static_for(F&& f) {
   }
 }
 
-template <int R, int C, int EPI, bool XN>
+template <int R, int C, int EPI, bool XN, bool NTW>
 __global__ __launch_bounds__(256) void gemv_kernel(const uint16_t* __restrict__ X, const uint16_t* __restrict__ W,
                                                    uint16_t* __restrict__ Y, float* __restrict__ P, int N, int K,
                                                    int Ks, XNormIn xn) {
@@ -739,7 +746,10 @@ __global__ __launch_bounds__(256) void gemv_kernel(const uint16_t* __restrict__ 
 #pragma unroll
   for (int r = 0; r < R; ++r)
 #pragma unroll
-    for (int c = 0; c < C; ++c) gload16<0>(w[r][c], wb + (size_t)r * K + c * 512);
+    for (int c = 0; c < C; ++c) {
+      if constexpr (NTW) gload16_nt<0>(w[r][c], wb + (size_t)r * K + c * 512);
+      else gload16<0>(w[r][c], wb + (size_t)r * K + c * 512);
+    }
   bf16x8 x[C];
   if constexpr (XN) {
     xnorm_prologue(xn, K, kbeg, Ks, blockIdx.x == 0 && blockIdx.y == 0, sx, xred);
@@ -792,12 +802,24 @@ __global__ __launch_bounds__(256) void gemv_kernel(const uint16_t* __restrict__ 
   }
 }
 
+// weight-load policy: nt by default (batch-1 p50 454 -> 439 ms, profiles/r6_b1_nt_down_ab.log);
+// DOCQA_GEMV_NT=0 for the default policy
+static bool gemv_nt() {
+  static const bool v = [] {
+    const char* e = getenv("DOCQA_GEMV_NT");
+    return e ? atoi(e) != 0 : true;
+  }();
+  return v;
+}
+
 template <int EPI, bool XN>
 static int launch_gemv(int R, int C, dim3 grid, hipStream_t s, const uint16_t* x, const uint16_t* w, uint16_t* y,
                        float* p, int N, int K, int Ks, const XNormIn& xn) {
+  const bool nt = gemv_nt();
 #define GEMV_CASE(RR, CC)                                                                                    \
   if (R == RR && C == CC) {                                                                                  \
-    gemv_kernel<RR, CC, EPI, XN><<<grid, 256, 0, s>>>(x, w, y, p, N, K, Ks, xn);                             \
+    if (nt) gemv_kernel<RR, CC, EPI, XN, true><<<grid, 256, 0, s>>>(x, w, y, p, N, K, Ks, xn);               \
+    else gemv_kernel<RR, CC, EPI, XN, false><<<grid, 256, 0, s>>>(x, w, y, p, N, K, Ks, xn);                 \
     return 0;                                                                                                \
   }
   if constexpr (EPI == EPI_GLU) {

@@ -602,6 +602,9 @@ def dgemm_glu_xn(Pin, res_in, res_out, gamma, eps: float, w_il):
 _GEMV = os.environ.get("DOCQA_GEMV", "1") != "0"
 
 
+_GEMV_DOWN = os.environ.get("DOCQA_GEMV_DOWN", "1") == "1"
+
+
 def gemv_plan(M: int, N: int, K: int) -> tuple[int, int]:
     """(split-K count, weight rows per workgroup) of the batch-1 register-streaming GEMV
     (dgemm.hip gemv_kernel: every lane issues all its weight loads at once, no LDS ring)
@@ -609,10 +612,16 @@ def gemv_plan(M: int, N: int, K: int) -> tuple[int, int]:
     Llama-3-8B projections, weights rotated past the MALL (profiles/r6_gemv_probe.log): O
     7.8 vs 8.8 us for the ring kernel's plan; the QKV with its input row built in-kernel
     (XNormIn: every workgroup runs that prologue, so few wide workgroups win) 13.3 vs 15.4
-    at 8 rows per workgroup, no split (17.9 at 4 rows x 2 slices); the down projection
-    (K 14336) stays on the ring (21.3 vs 20.9).  DOCQA_GEMV=0 disables."""
-    if not _GEMV or M != 1 or N % 8 or K > 8192 or K % 2048:
+    at 8 rows per workgroup, no split (17.9 at 4 rows x 2 slices).  The down projection
+    (K 14336) alone is 21.3 vs the ring's 20.9 us, but on the GEMV (4 rows, no split) it
+    hands the next QKV ONE slab to build its input row from instead of four: with the
+    non-temporal weight loads, batch-1 p50 454 -> 431 ms (profiles/r6_b1_nt_down_ab.log;
+    DOCQA_GEMV_DOWN=0 keeps the ring).  DOCQA_GEMV=0 disables."""
+    if not _GEMV or M != 1 or N % 8 or K % 2048:
         return 0, 0
+    if K > 8192:
+        # one slab for the next QKV's in-kernel input row instead of the ring's four
+        return (1, 4) if _GEMV_DOWN and K // 2048 == 7 else (0, 0)
     return (1, 8) if K <= 4096 else ((2, 8) if K % 4096 == 0 else (0, 0))
 
 
