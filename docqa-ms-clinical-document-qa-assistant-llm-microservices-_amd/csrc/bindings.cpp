@@ -948,6 +948,23 @@ std::tuple<at::Tensor, at::Tensor> dgemm_argmax_val(const at::Tensor& x, const a
   return {out, outv};
 }
 
+// batch-1 LM head + greedy pick on the register-streaming GEMV (dgemm.hip EPI_ARGMAX)
+std::tuple<at::Tensor, at::Tensor> gemv_argmax_val(const at::Tensor& x, const at::Tensor& w, int64_t n_valid) {
+  CHECK_GPU(x); CHECK_BF16(x); CHECK_BF16(w); CHECK_CONTIG(x); CHECK_CONTIG(w);
+  const int K = x.size(-1), N = w.size(0);
+  TORCH_CHECK(x.numel() == K && w.size(1) == K, "gemv_argmax: one row");
+  TORCH_CHECK(N % 16 == 0 && K % 2048 == 0 && K / 2048 <= 2, "gemv_argmax: N % 16, K 2048 or 4096");
+  c10::DeviceGuard g(x.device());
+  auto out = at::empty({1}, x.options().dtype(at::kLong));
+  auto outv = at::empty({1}, x.options().dtype(at::kFloat));
+  auto ws_v = at::empty({N / 16}, x.options().dtype(at::kFloat));
+  auto ws_i = at::empty({N / 16}, x.options().dtype(at::kInt));
+  CHECK_RC(docqa_gemv_argmax(x.data_ptr(), w.data_ptr(), out.data_ptr<int64_t>(), outv.data_ptr<float>(),
+                             ws_v.data_ptr<float>(), ws_i.data_ptr<int>(), N, K, (int)n_valid, stream()),
+           "gemv_argmax");
+  return {out, outv};
+}
+
 // prefill GEMM (pgemm.hip, 256 x 256 tiles): epi 0 -> x . w^T bf16 [.., N]; epi 1 -> fused
 // SwiGLU over 8-interleaved gate|up rows -> [.., N / 2]
 at::Tensor pgemm(const at::Tensor& x, const at::Tensor& w, int64_t epi) {
@@ -1301,6 +1318,7 @@ TORCH_LIBRARY(docqa, m) {
   m.def("mgemm_tile_n(int cfg) -> int", &mgemm_tile_n);
   m.def("mgemm_argmax(Tensor x, Tensor w, int n_valid, int cfg=0) -> Tensor");
   m.def("dgemm_argmax_val(Tensor x, Tensor w, int n_valid) -> (Tensor, Tensor)");
+  m.def("gemv_argmax_val(Tensor x, Tensor w, int n_valid) -> (Tensor, Tensor)");
   m.def("pgemm(Tensor x, Tensor w, int epi=0) -> Tensor");
   m.def("pgemm_partial(Tensor x, Tensor w, int splits) -> Tensor");
   m.def("mgemm_argmax_val(Tensor x, Tensor w, int n_valid, int cfg=0) -> (Tensor, Tensor)");
@@ -1386,6 +1404,7 @@ TORCH_LIBRARY_IMPL(docqa, CUDA, m) {
   m.impl("coarse_probes", &coarse_probes);
   m.impl("fp32_gemm_nt", &fp32_gemm_nt);
   m.impl("dgemm_argmax_val", &dgemm_argmax_val);
+  m.impl("gemv_argmax_val", &gemv_argmax_val);
   m.impl("paged_decode_fused", &paged_decode_fused);
   m.impl("paged_decode_cascade", &paged_decode_cascade);
   m.impl("paged_decode_cascade_rope", &paged_decode_cascade_rope);

@@ -133,6 +133,8 @@ int docqa_gemv(const void* X, const void* W, void* Y, float* P, int N, int K, in
 int docqa_embed_rmsnorm(const int* ids, const void* table, const void* w, void* h, void* x, int T, int H, int V,
                         float eps, hipStream_t s);
 int docqa_fp32_gemm_nt(const float* x, int nq, int d, const float* w, int n, float* out, hipStream_t s);
+int docqa_gemv_argmax(const void* X, const void* W, int64_t* out, float* outv, float* ws_v, int* ws_i, int N, int K,
+                      int n_valid, hipStream_t s);
 int docqa_dgemm_argmax(const void* X, const void* W, int64_t* out, float* outv, float* ws_v, int* ws_i, int M,
                        int N, int K, int n_valid, hipStream_t s);
 int docqa_dgemm(const void* X, const void* W, void* Y, float* partial, int M, int N, int K, int S,

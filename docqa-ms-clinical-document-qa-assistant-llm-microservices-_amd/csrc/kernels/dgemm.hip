@@ -729,8 +729,10 @@ __device__ __forceinline__ void static_for(F&& f) {
 template <int R, int C, int EPI, bool XN, bool NTW>
 __global__ __launch_bounds__(256) void gemv_kernel(const uint16_t* __restrict__ X, const uint16_t* __restrict__ W,
                                                    uint16_t* __restrict__ Y, float* __restrict__ P, int N, int K,
-                                                   int Ks, XNormIn xn) {
-  static_assert(EPI == EPI_PARTIAL || (EPI == EPI_GLU && R == 16), "GLU: one 16-row gate|up group");
+                                                   int Ks, XNormIn xn, int* __restrict__ pi = nullptr,
+                                                   int n_valid = 0) {
+  static_assert(EPI == EPI_PARTIAL || (EPI == EPI_GLU && R == 16) || (EPI == EPI_ARGMAX && R == 16),
+                "GLU: one 16-row gate|up group; ARGMAX: 16 logits per workgroup");
   static_assert(R * C <= 32, "loads in flight per lane must fit the vmcnt counter");
   __shared__ __attribute__((aligned(16))) uint16_t sx[XN ? kXnMaxK : 8];
   __shared__ float red[4][R];
@@ -791,6 +793,27 @@ __global__ __launch_bounds__(256) void gemv_kernel(const uint16_t* __restrict__ 
   __syncthreads();
   if constexpr (EPI == EPI_PARTIAL) {
     if (tid < R) P[(size_t)slice * N + n0 + tid] = red[0][tid] + red[1][tid] + red[2][tid] + red[3][tid];
+  } else if constexpr (EPI == EPI_ARGMAX) {
+    // LM head + greedy pick: the 16 logits (bf16-rounded, as the unfused logits) -> one
+    // (value, id) partial per workgroup at P / pi [blockIdx.x] for argmax_merge_kernel
+    if (tid < 64) {
+      float bv = -FLT_MAX;
+      int bi = 0x7fffffff;
+      if (tid < R && n0 + tid < n_valid) {
+        bv = bf2f(f2bf(red[0][tid] + red[1][tid] + red[2][tid] + red[3][tid]));
+        bi = n0 + tid;
+      }
+#pragma unroll
+      for (int o = 1; o < R; o <<= 1) {
+        const float ov = __shfl_xor(bv, o, 64);
+        const int oi = __shfl_xor(bi, o, 64);
+        argmax_better(bv, bi, ov, oi);
+      }
+      if (tid == 0) {
+        P[blockIdx.x] = bv;
+        pi[blockIdx.x] = bi;
+      }
+    }
   } else {
     // gate rows n0 .. n0 + 7, up rows n0 + 8 .. n0 + 15 -> outputs n0 / 2 .. n0 / 2 + 7
     if (tid < 8) {
@@ -824,6 +847,8 @@ static int launch_gemv(int R, int C, dim3 grid, hipStream_t s, const uint16_t* x
   }
   if constexpr (EPI == EPI_GLU) {
     GEMV_CASE(16, 1) GEMV_CASE(16, 2)
+  } else if constexpr (EPI == EPI_ARGMAX) {
+    return -1;   // docqa_gemv_argmax launches its own instantiations
   } else {
     GEMV_CASE(16, 1) GEMV_CASE(16, 2) GEMV_CASE(8, 2) GEMV_CASE(8, 4) GEMV_CASE(4, 4) GEMV_CASE(4, 7)
     GEMV_CASE(8, 1) GEMV_CASE(4, 2) GEMV_CASE(4, 1)
@@ -855,6 +880,25 @@ int docqa_gemv(const void* X, const void* W, void* Y, float* P, int N, int K, in
     rc = xnm ? launch_gemv<EPI_PARTIAL, true>(R, C, grid, s, x, w, nullptr, P, N, K, Ks, xn)
              : launch_gemv<EPI_PARTIAL, false>(R, C, grid, s, x, w, nullptr, P, N, K, Ks, xn);
   if (rc) return rc;
+  DOCQA_CHECK_LAUNCH();
+  return 0;
+}
+
+// Batch-1 LM head + greedy pick on the GEMV: 16 vocabulary rows per workgroup (C = K / 2048
+// chunks per lane, nt weight loads), one (value, id) partial each, merged by
+// argmax_merge_kernel.  ws_v / ws_i: N / 16 entries.
+int docqa_gemv_argmax(const void* X, const void* W, int64_t* out, float* outv, float* ws_v, int* ws_i, int N, int K,
+                      int n_valid, hipStream_t s) {
+  if (N % 16 || K % 2048 || K / 2048 > 2 || n_valid <= 0 || n_valid > N) return -1;
+  const dim3 grid(N / 16);
+  const XNormIn xn{};
+  const uint16_t* x = (const uint16_t*)X;
+  const uint16_t* w = (const uint16_t*)W;
+  if (K == 2048)
+    gemv_kernel<16, 1, EPI_ARGMAX, false, true><<<grid, 256, 0, s>>>(x, w, nullptr, ws_v, N, K, K, xn, ws_i, n_valid);
+  else
+    gemv_kernel<16, 2, EPI_ARGMAX, false, true><<<grid, 256, 0, s>>>(x, w, nullptr, ws_v, N, K, K, xn, ws_i, n_valid);
+  argmax_merge_kernel<<<1, 256, 0, s>>>(ws_v, ws_i, N / 16, out, outv);
   DOCQA_CHECK_LAUNCH();
   return 0;
 }

@@ -502,6 +502,7 @@ def prefill_glu(x, w_il):
 # LM head: 256-wide tiles (mgemm.hip cfg 6) halve the X re-reads of the 1002-tile vocab
 # sweep -- 281 vs 326 us with the argmax fused at M = 256 (profiles/r2_mgemm_probe_m256_v6.log)
 _LM_CFG = int(os.environ.get("DOCQA_LM_HEAD_CFG", "6"))
+_GEMV_LM = os.environ.get("DOCQA_GEMV_LM", "1") != "0"
 
 
 def lm_head_argmax(x, w, n_valid: int, cfg: int = -1, with_values: bool = False):
@@ -510,6 +511,12 @@ def lm_head_argmax(x, w, n_valid: int, cfg: int = -1, with_values: bool = False)
     (ids, picked logit fp32) -- a vocab-parallel shard's candidates for comm.tp_argmax."""
     if _gpu(x):
         N, K = w.shape
+        if (_GEMV_LM and x.numel() == K and N % 16 == 0 and K % 2048 == 0 and K // 2048 <= 2
+                and n_valid > 0):
+            # one row: the register-streaming GEMV with the argmax in its epilogue
+            # (profiles/r6_b1_lm_head_gemv_ab.log)
+            ids, vals = _native().gemv_argmax_val(x.contiguous(), w, int(n_valid))
+            return (ids, vals) if with_values else ids
         if x.numel() // K <= 32 and N % 64 == 0 and K % 512 == 0:
             # <= 32 rows (batch-1 decode included): the skinny weight-streaming kernel with
             # the argmax in its epilogue (dgemm.hip EPI_ARGMAX) -- 197.6 / 203.4 us at M = 1 /

@@ -88,3 +88,20 @@ def test_llama_batch1_decode_on_gemv_plans(native):
         _prefill_logits(m, kv2, prompts, BS)
         d2 = _decode_logits(m, kv2, prompts, tables, [4], BS)
     assert _rel(d1, d2) < 0.03
+
+
+@pytest.mark.parametrize("N,K,n_valid", [(128256, 4096, 128256), (32000, 2048, 31990), (4096, 4096, 1000)])
+def test_gemv_argmax_matches_bf16_logits(N, K, n_valid):
+    """Batch-1 LM head + greedy pick on the GEMV == argmax of the bf16 fp32-accumulated
+    logits over the valid vocabulary (ties to the lowest id), planted winner included."""
+    assert ops.load_native()
+    x = (torch.rand(1, K, device="cuda") * 2 - 1).to(torch.bfloat16)
+    w = _w(N, K, 5)
+    w[n_valid - 1] = (x.float() * 4).to(torch.bfloat16)[0]     # a clear winner at the last valid id
+    if n_valid < N:
+        w[n_valid] = (x.float() * 8).to(torch.bfloat16)[0]     # past n_valid: must be ignored
+    ids, vals = torch.ops.docqa.gemv_argmax_val(x, w, n_valid)
+    logits = (x.float() @ w[:n_valid].float().t()).bfloat16().float()
+    assert int(ids[0]) == int(logits.argmax(1)[0]) == n_valid - 1
+    assert abs(float(vals[0]) - float(logits.max())) <= 1e-2 * abs(float(logits.max()))
+    assert int(ops.lm_head_argmax(x, w, n_valid)[0]) == n_valid - 1
