@@ -284,6 +284,8 @@ __device__ __forceinline__ void finish_partition(
 //     accumulators 8 partitions per round with every load issued before the first use.
 // Same arithmetic as paged_decode_reduce (fp32, partitions in index order), so the two
 // modes agree bit for bit.
+constexpr int kFastMergeParts = 16;
+
 template <int G, int D>
 __device__ __forceinline__ bool last_arriver_merge(const float* __restrict__ tmp_out, const float* __restrict__ tmp_ml,
                                                    int* __restrict__ tick, int b, int kvh, int Hkv, int max_parts,
@@ -309,6 +311,49 @@ __device__ __forceinline__ bool last_arriver_merge(const float* __restrict__ tmp
   if (!s_last) return false;
   const int Hq = Hkv * G;
   const size_t B = gridDim.y;
+  if constexpr (G * D <= 512) {
+    if (nc == 0 && np <= kFastMergeParts) {
+      // up to 16 partitions, no cascade (batch-1 decode at <= 1k tokens): ONE memory round
+      // trip -- every (max, sum) pair and accumulator this thread's outputs need is loaded
+      // before the first is used; the general path below takes two (pairs into LDS, then
+      // the accumulators).  Same fp32 arithmetic in the same partition order.
+      constexpr int EPT = (G * D + 255) / 256;
+      float pm[EPT][kFastMergeParts], pl[EPT][kFastMergeParts], pa[EPT][kFastMergeParts];
+#pragma unroll
+      for (int e = 0; e < EPT; ++e) {
+        const int i = min(tid + 256 * e, G * D - 1), g = i / D, d = i - g * D, h = kvh * G + g;
+        const size_t row = ((size_t)b * Hq + h) * max_parts;
+#pragma unroll
+        for (int p = 0; p < kFastMergeParts; ++p) {
+          const int pp = min(p, np - 1);
+          const float4 ml = load2_coh(tmp_ml + (row + pp) * 2);
+          pm[e][p] = ml.x;
+          pl[e][p] = ml.y;
+          pa[e][p] = __hip_atomic_load(tmp_out + (row + pp) * D + d, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+      }
+#pragma unroll
+      for (int e = 0; e < EPT; ++e) {
+        const int i = tid + 256 * e;
+        if (i >= G * D) break;
+        const int g = i / D, d = i - g * D, h = kvh * G + g;
+        float M = -FLT_MAX;
+#pragma unroll
+        for (int p = 0; p < kFastMergeParts; ++p)
+          if (p < np) M = fmaxf(M, pm[e][p]);
+        float den = 0.f, num = 0.f;
+#pragma unroll
+        for (int p = 0; p < kFastMergeParts; ++p)
+          if (p < np) {
+            const float w = exp2f(pm[e][p] - M);
+            den += w * pl[e][p];
+            num += w * pa[e][p];
+          }
+        out[(size_t)b * out_stride + (size_t)h * D + d] = f2bf(den > 0.f ? num / den : 0.f);
+      }
+      return true;
+    }
+  }
   // (max, sum) of every partition (and cascade chunk) -> LDS
   float* s_pm = &s_w[0][0];                           // reuse: [G][np + nc] maxima first
   __shared__ float s_pl[G][MAXP + kCascadeMaxChunks];
