@@ -610,6 +610,7 @@ _GEMV = os.environ.get("DOCQA_GEMV", "1") != "0"
 
 
 _GEMV_DOWN = os.environ.get("DOCQA_GEMV_DOWN", "1") == "1"
+_GEMV_R = int(os.environ.get("DOCQA_GEMV_R", "8"))   # rows per workgroup, K <= 4096 (A/B knob)
 
 
 def gemv_plan(M: int, N: int, K: int) -> tuple[int, int]:
@@ -629,7 +630,7 @@ def gemv_plan(M: int, N: int, K: int) -> tuple[int, int]:
     if K > 8192:
         # one slab for the next QKV's in-kernel input row instead of the ring's four
         return (1, 4) if _GEMV_DOWN and K // 2048 == 7 else (0, 0)
-    return (1, 8) if K <= 4096 else ((2, 8) if K % 4096 == 0 else (0, 0))
+    return (1, _GEMV_R) if K <= 4096 else ((2, 8) if K % 4096 == 0 else (0, 0))
 
 
 def gemv_glu_ok(M: int, N: int, K: int) -> bool:
