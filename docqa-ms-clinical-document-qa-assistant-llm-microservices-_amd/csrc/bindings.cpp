@@ -130,14 +130,20 @@ void kv_copy_rows(const at::Tensor& caches, const at::Tensor& tab, int64_t num_b
 // split-K partial slabs P [S, rows, H] fp32 -> residual += bf16(sum P); rmsnorm(residual) * w
 at::Tensor add_rmsnorm_splitk(const at::Tensor& P, at::Tensor residual, const at::Tensor& w, double eps) {
   CHECK_GPU(P); CHECK_CONTIG(P); CHECK_BF16(residual); CHECK_CONTIG(residual); CHECK_BF16(w);
-  TORCH_CHECK(P.scalar_type() == at::kFloat && P.dim() == 3, "partials must be fp32 [S, rows, H]");
+  TORCH_CHECK((P.scalar_type() == at::kFloat || P.scalar_type() == at::kBFloat16) && P.dim() == 3,
+              "partials must be fp32 or bf16 [S, rows, H]");
   TORCH_CHECK(P.size(1) * P.size(2) == residual.numel() && P.size(2) == residual.size(-1),
               "add_rmsnorm_splitk shape mismatch");
   c10::DeviceGuard g(P.device());
   auto out = at::empty_like(residual);
-  CHECK_RC(docqa_add_rmsnorm_splitk(P.data_ptr<float>(), P.size(0), residual.data_ptr(), w.data_ptr(),
-                                    out.data_ptr(), P.size(1), P.size(2), (float)eps, stream()),
-           "add_rmsnorm_splitk");
+  if (P.scalar_type() == at::kBFloat16)
+    CHECK_RC(docqa_add_rmsnorm_splitk16(P.data_ptr(), P.size(0), residual.data_ptr(), w.data_ptr(),
+                                        out.data_ptr(), P.size(1), P.size(2), (float)eps, stream()),
+             "add_rmsnorm_splitk");
+  else
+    CHECK_RC(docqa_add_rmsnorm_splitk(P.data_ptr<float>(), P.size(0), residual.data_ptr(), w.data_ptr(),
+                                      out.data_ptr(), P.size(1), P.size(2), (float)eps, stream()),
+             "add_rmsnorm_splitk");
   return out;
 }
 
@@ -146,7 +152,8 @@ at::Tensor rope_cache_splitk(const at::Tensor& P, const at::Tensor& positions, c
                              const c10::optional<at::Tensor>& slot_mapping, at::Tensor k_cache,
                              at::Tensor v_cache, int64_t Hq, int64_t Hkv, int64_t D) {
   CHECK_GPU(P); CHECK_CONTIG(P); CHECK_I32(positions);
-  TORCH_CHECK(P.scalar_type() == at::kFloat && P.dim() == 3, "partials must be fp32 [S, T, width]");
+  TORCH_CHECK((P.scalar_type() == at::kFloat || P.scalar_type() == at::kBFloat16) && P.dim() == 3,
+              "partials must be fp32 or bf16 [S, T, width]");
   TORCH_CHECK(cos_sin.scalar_type() == at::kFloat, "cos_sin must be fp32");
   TORCH_CHECK(P.size(2) == (Hq + 2 * Hkv) * D, "qkv width mismatch");
   const int T = P.size(1);
@@ -160,10 +167,16 @@ at::Tensor rope_cache_splitk(const at::Tensor& P, const at::Tensor& positions, c
   }
   c10::DeviceGuard g(P.device());
   auto qkv = at::empty({T, P.size(2)}, P.options().dtype(at::kBFloat16));
-  CHECK_RC(docqa_rope_cache_splitk(P.data_ptr<float>(), P.size(0), qkv.data_ptr(), positions.data_ptr<int>(),
-                                   cos_sin.data_ptr<float>(), sm, sm ? k_cache.data_ptr() : nullptr,
-                                   sm ? v_cache.data_ptr() : nullptr, T, Hq, Hkv, D, P.size(2), BS,
-                                   stream()), "rope_cache_splitk");
+  if (P.scalar_type() == at::kBFloat16)
+    CHECK_RC(docqa_rope_cache_splitk16(P.data_ptr(), P.size(0), qkv.data_ptr(), positions.data_ptr<int>(),
+                                       cos_sin.data_ptr<float>(), sm, sm ? k_cache.data_ptr() : nullptr,
+                                       sm ? v_cache.data_ptr() : nullptr, T, Hq, Hkv, D, P.size(2), BS,
+                                       stream()), "rope_cache_splitk");
+  else
+    CHECK_RC(docqa_rope_cache_splitk(P.data_ptr<float>(), P.size(0), qkv.data_ptr(), positions.data_ptr<int>(),
+                                     cos_sin.data_ptr<float>(), sm, sm ? k_cache.data_ptr() : nullptr,
+                                     sm ? v_cache.data_ptr() : nullptr, T, Hq, Hkv, D, P.size(2), BS,
+                                     stream()), "rope_cache_splitk");
   return qkv;
 }
 
@@ -851,6 +864,21 @@ at::Tensor mgemm(const at::Tensor& x, const at::Tensor& w, int64_t splits, int64
   return out;
 }
 
+// mid-M decode GEMM -> bf16 split-K slabs [S, M, N] (the bf16-slab consumers)
+at::Tensor mgemm_slab16(const at::Tensor& x, const at::Tensor& w, int64_t splits, int64_t cfg) {
+  CHECK_GPU(x); CHECK_BF16(x); CHECK_BF16(w); CHECK_CONTIG(x); CHECK_CONTIG(w);
+  CHECK_ALIGN16(x); CHECK_ALIGN16(w);
+  const int K = x.size(-1), N = w.size(0);
+  TORCH_CHECK(w.size(1) == K, "mgemm_slab16: K mismatch");
+  const int M = x.numel() / K;
+  TORCH_CHECK(splits >= 1, "mgemm_slab16: splits >= 1");
+  c10::DeviceGuard g(x.device());
+  auto out = at::empty({splits, M, N}, x.options());
+  CHECK_RC(docqa_mgemm_slab16(x.data_ptr(), w.data_ptr(), out.data_ptr(), M, N, K, (int)splits, (int)cfg,
+                              stream()), "mgemm_slab16");
+  return out;
+}
+
 // mid-M gate|up projection with fused SwiGLU: x [M, K], w [2I, K] (8-interleaved) -> [M, I]
 at::Tensor mgemm_glu(const at::Tensor& x, const at::Tensor& w, int64_t cfg) {
   CHECK_GPU(x); CHECK_BF16(x); CHECK_BF16(w); CHECK_CONTIG(x); CHECK_CONTIG(w);
@@ -1314,6 +1342,7 @@ TORCH_LIBRARY(docqa, m) {
         "Tensor(t!) tick) -> Tensor");
   m.def("dgemm_glu(Tensor x, Tensor w) -> Tensor");
   m.def("mgemm(Tensor x, Tensor w, int splits, int cfg=0) -> Tensor");
+  m.def("mgemm_slab16(Tensor x, Tensor w, int splits, int cfg=0) -> Tensor");
   m.def("mgemm_glu(Tensor x, Tensor w, int cfg=0) -> Tensor");
   m.def("mgemm_tile_n(int cfg) -> int", &mgemm_tile_n);
   m.def("mgemm_argmax(Tensor x, Tensor w, int n_valid, int cfg=0) -> Tensor");
@@ -1395,6 +1424,7 @@ TORCH_LIBRARY_IMPL(docqa, CUDA, m) {
   m.impl("dgemm_add_rmsnorm", &dgemm_add_rmsnorm);
   m.impl("dgemm_glu", &dgemm_glu);
   m.impl("mgemm", &mgemm);
+  m.impl("mgemm_slab16", &mgemm_slab16);
   m.impl("mgemm_glu", &mgemm_glu);
   m.impl("mgemm_argmax", &mgemm_argmax);
   m.impl("pgemm", &pgemm);

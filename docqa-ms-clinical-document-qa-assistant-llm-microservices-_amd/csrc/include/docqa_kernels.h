@@ -102,6 +102,12 @@ int docqa_rope_cache_splitk(const float* P, int S, void* qkv_out, const int* pos
                             const float* cos_sin, const int* slot_mapping, void* k_cache,
                             void* v_cache, int T, int Hq, int Hkv, int D, int row_stride, int BS,
                             hipStream_t s);
+int docqa_add_rmsnorm_splitk16(const void* P, int S, void* residual, const void* w, void* out,
+                               int rows, int H, float eps, hipStream_t s);
+int docqa_rope_cache_splitk16(const void* P, int S, void* qkv_out, const int* positions,
+                              const float* cos_sin, const int* slot_mapping, void* k_cache,
+                              void* v_cache, int T, int Hq, int Hkv, int D, int row_stride, int BS,
+                              hipStream_t s);
 size_t docqa_ar_region_bytes(size_t max_elems);
 int docqa_ar_alloc(size_t bytes, void** ptr);
 int docqa_ar_free(void* ptr);
@@ -143,6 +149,8 @@ int docqa_gemm(const void* A, const void* W, const void* bias, const void* res, 
                int N, int K, int epi, hipStream_t s);
 int docqa_mgemm(const void* X, const void* W, void* Y, float* P, int M, int N, int K, int S, int cfg,
                 hipStream_t s);
+int docqa_mgemm_slab16(const void* X, const void* W, void* Y, int M, int N, int K, int S, int cfg,
+                       hipStream_t s);
 int docqa_mgemm_glu(const void* X, const void* W, void* Y, int M, int N, int K, int cfg, hipStream_t s);
 int docqa_mgemm_argmax(const void* X, const void* W, int64_t* out, float* outv, float* ws_v, int* ws_i, int M,
                        int N, int K, int n_valid, int cfg, hipStream_t s);

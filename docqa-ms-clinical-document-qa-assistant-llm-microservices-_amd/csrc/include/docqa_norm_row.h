@@ -32,10 +32,28 @@ __device__ __forceinline__ float4 slab_load4(const float* p) {
   }
 }
 
+// 8 consecutive slab values at p as two float4: fp32 slabs (two 16-B loads), or bf16 slabs
+// (mgemm.hip EPI_PARTIAL16: one 16-B load)
+template <bool COH>
+__device__ __forceinline__ void slab_load8(const float* p, float4& a, float4& b) {
+  a = slab_load4<COH>(p);
+  b = slab_load4<COH>(p + 4);
+}
+template <bool COH>
+__device__ __forceinline__ void slab_load8(const uint16_t* p, float4& a, float4& b) {
+  static_assert(!COH, "bf16 slabs come from an earlier launch");
+  const uint4 u = *reinterpret_cast<const uint4*>(p);
+  a = float4{__uint_as_float(u.x << 16), __uint_as_float(u.x & 0xffff0000u), __uint_as_float(u.y << 16),
+             __uint_as_float(u.y & 0xffff0000u)};
+  b = float4{__uint_as_float(u.z << 16), __uint_as_float(u.z & 0xffff0000u), __uint_as_float(u.w << 16),
+             __uint_as_float(u.w & 0xffff0000u)};
+}
+
 // WT: write-through (sc1) stores of the residual and the output, for in-launch consumers
 // COH: the slabs come from the same launch (slab_load4)
-template <int NV, int NS, bool WT = false, bool COH = false>
-__device__ __forceinline__ void add_rmsnorm_splitk_row(const float* __restrict__ P, int S, size_t slab,
+// PT: the slab element type (float, or uint16_t for bf16 slabs)
+template <int NV, int NS, bool WT = false, bool COH = false, typename PT = float>
+__device__ __forceinline__ void add_rmsnorm_splitk_row(const PT* __restrict__ P, int S, size_t slab,
                                                        uint16_t* __restrict__ residual,
                                                        const uint16_t* __restrict__ w,
                                                        uint16_t* __restrict__ out, int H, float eps,
@@ -58,15 +76,12 @@ __device__ __forceinline__ void add_rmsnorm_splitk_row(const float* __restrict__
   for (int i = 0; i < NV; ++i) {
     const int c = tid + 256 * i;
     if (c < nchunk) {
-      const float* pr = P + (size_t)row * H + c * 8;
+      const PT* pr = P + (size_t)row * H + c * 8;
       float4 a, b;
       if constexpr (NS > 0) {
         float4 pa[NS], pb[NS];
 #pragma unroll
-        for (int sl = 0; sl < NS; ++sl) {
-          pa[sl] = slab_load4<COH>(pr + sl * slab);
-          pb[sl] = slab_load4<COH>(pr + sl * slab + 4);
-        }
+        for (int sl = 0; sl < NS; ++sl) slab_load8<COH>(pr + sl * slab, pa[sl], pb[sl]);
         a = pa[0];
         b = pb[0];
 #pragma unroll
@@ -75,11 +90,10 @@ __device__ __forceinline__ void add_rmsnorm_splitk_row(const float* __restrict__
           b.x += pb[sl].x; b.y += pb[sl].y; b.z += pb[sl].z; b.w += pb[sl].w;
         }
       } else {
-        a = slab_load4<COH>(pr);
-        b = slab_load4<COH>(pr + 4);
+        slab_load8<COH>(pr, a, b);
         for (int sl = 1; sl < S; ++sl) {
-          const float4 a2 = slab_load4<COH>(pr + sl * slab);
-          const float4 b2 = slab_load4<COH>(pr + sl * slab + 4);
+          float4 a2, b2;
+          slab_load8<COH>(pr + sl * slab, a2, b2);
           a.x += a2.x; a.y += a2.y; a.z += a2.z; a.w += a2.w;
           b.x += b2.x; b.y += b2.y; b.z += b2.z; b.w += b2.w;
         }

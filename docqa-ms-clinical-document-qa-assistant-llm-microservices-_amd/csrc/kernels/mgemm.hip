@@ -40,7 +40,9 @@ using namespace docqa;
 
 namespace {
 constexpr int BM = 256;
-enum { EPI_BF16 = 0, EPI_PARTIAL = 1, EPI_GLU = 2, EPI_ARGMAX = 3 };
+// EPI_PARTIAL16: the split-K slabs [S, M, N] stored as bf16 (half the slab bytes the GEMM
+// writes and its consumer reads; each partial rounded once before the consumer's fp32 sum)
+enum { EPI_BF16 = 0, EPI_PARTIAL = 1, EPI_GLU = 2, EPI_ARGMAX = 3, EPI_PARTIAL16 = 4 };
 
 // element offset of 16-B chunk `ch` of `row` in a [rows][BKS] bf16 tile: the XOR spreads
 // the 16 rows of a fragment read over all 64 banks (128-B rows: pairs of rows share a
@@ -89,7 +91,7 @@ __device__ __forceinline__ void mgemm_epilogue(f32x4 (&acc)[BM / WM / 16][BN / W
       for (int r = 0; r < 4; ++r) scr[(fq * 4 + r) * SCR + j * 16 + fr] = acc[i][j][r];
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     // EPC: output columns per lane (fp32 slab 4, bf16 8, SwiGLU 16 inputs -> 8 outputs)
-    constexpr int EPC = EPI == EPI_PARTIAL ? 4 : EPI == EPI_BF16 ? 8 : 16;
+    constexpr int EPC = EPI == EPI_PARTIAL ? 4 : (EPI == EPI_BF16 || EPI == EPI_PARTIAL16) ? 8 : 16;
     constexpr int LPR = CW / EPC, RPS = 64 / LPR;          // lanes per row, rows per sweep
     if constexpr (EPI != EPI_ARGMAX) {
 #pragma unroll
@@ -108,6 +110,8 @@ __device__ __forceinline__ void mgemm_epilogue(f32x4 (&acc)[BM / WM / 16][BN / W
             *reinterpret_cast<float4*>(dst) = float4{v[0], v[1], v[2], v[3]};
           } else if constexpr (EPI == EPI_BF16) {
             *reinterpret_cast<uint4*>(Y + (size_t)row * N + col) = pack8(v);
+          } else if constexpr (EPI == EPI_PARTIAL16) {
+            *reinterpret_cast<uint4*>(Y + ((size_t)slice * M + row) * N + col) = pack8(v);
           } else {
             // 16 consecutive columns = one (gate 8, up 8) interleave group
             float o[8];
@@ -512,6 +516,17 @@ int docqa_mgemm(const void* X, const void* W, void* Y, float* P, int M, int N, i
   const uint16_t *x = (const uint16_t*)X, *w = (const uint16_t*)W;
   if (P) return launch_cfg<EPI_PARTIAL>(cfg, x, w, nullptr, P, nullptr, nullptr, M, N, K, S, N, s);
   return launch_cfg<EPI_BF16>(cfg, x, w, (uint16_t*)Y, nullptr, nullptr, nullptr, M, N, K, 1, N, s);
+}
+
+// bf16 split-K slabs Y [S, M, N] (S >= 1) for the bf16-slab consumers
+int docqa_mgemm_slab16(const void* X, const void* W, void* Y, int M, int N, int K, int S, int cfg,
+                       hipStream_t s) {
+  if (cfg == 0) cfg = kDefaultCfg;
+  if (M == 0) return 0;
+  if (!shape_ok(M, N, K, S, cfg) || Y == nullptr) return -1;
+  if (!docqa_aligned16(X) || !docqa_aligned16(W) || !docqa_aligned16(Y)) return -1;
+  return launch_cfg<EPI_PARTIAL16>(cfg, (const uint16_t*)X, (const uint16_t*)W, (uint16_t*)Y, nullptr, nullptr,
+                                   nullptr, M, N, K, S, N, s);
 }
 
 // Y[M, N/2] = silu(gate) * up for the 8-interleaved gate|up weight W [N, K] (N = 2 I)

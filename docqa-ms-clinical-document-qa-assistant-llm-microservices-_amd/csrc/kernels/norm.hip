@@ -123,8 +123,8 @@ __global__ __launch_bounds__(256) void rmsnorm_row_kernel(const uint16_t* __rest
 // NS > 0: S == NS at compile time -- every slab, the residual and the weight chunk are
 // loaded before the first add, so the row costs one memory latency instead of S + 2
 // dependent ones (at 128 decode rows this kernel is latency-bound, not bandwidth-bound).
-template <int NV, int NS>
-__global__ __launch_bounds__(256) void add_rmsnorm_splitk_kernel(const float* __restrict__ P,
+template <int NV, int NS, typename PT>
+__global__ __launch_bounds__(256) void add_rmsnorm_splitk_kernel(const PT* __restrict__ P,
                                                                  int S, size_t slab,
                                                                  uint16_t* __restrict__ residual,
                                                                  const uint16_t* __restrict__ w,
@@ -234,10 +234,10 @@ int docqa_add_rmsnorm(const void* x, void* residual, const void* w, void* out, i
   return launch_rms<true>(x, residual, w, out, rows, H, eps, s);
 }
 
-template <int NV>
-static void launch_arns(const float* P, int S, size_t slab, uint16_t* rp, const uint16_t* wp,
+template <int NV, typename PT>
+static void launch_arns(const PT* P, int S, size_t slab, uint16_t* rp, const uint16_t* wp,
                         uint16_t* op, int rows, int H, float eps, hipStream_t s) {
-#define DOCQA_ARNS(NS_) add_rmsnorm_splitk_kernel<NV, NS_><<<rows, 256, 0, s>>>(P, S, slab, rp, wp, op, H, eps)
+#define DOCQA_ARNS(NS_) add_rmsnorm_splitk_kernel<NV, NS_, PT><<<rows, 256, 0, s>>>(P, S, slab, rp, wp, op, H, eps)
   switch (S) {
     case 1: DOCQA_ARNS(1); break;
     case 2: DOCQA_ARNS(2); break;
@@ -252,8 +252,9 @@ static void launch_arns(const float* P, int S, size_t slab, uint16_t* rp, const 
 #undef DOCQA_ARNS
 }
 
-int docqa_add_rmsnorm_splitk(const float* P, int S, void* residual, const void* w, void* out,
-                             int rows, int H, float eps, hipStream_t s) {
+template <typename PT>
+static int add_rmsnorm_splitk_any(const PT* P, int S, void* residual, const void* w, void* out, int rows, int H,
+                                  float eps, hipStream_t s) {
   if (rows == 0) return 0;
   if (H % 8 != 0 || S < 1) return -1;
   const size_t slab = (size_t)rows * H;
@@ -266,6 +267,17 @@ int docqa_add_rmsnorm_splitk(const float* P, int S, void* residual, const void* 
   else launch_arns<4>(P, S, slab, rp, wp, op, rows, H, eps, s);
   DOCQA_CHECK_LAUNCH();
   return 0;
+}
+
+int docqa_add_rmsnorm_splitk(const float* P, int S, void* residual, const void* w, void* out,
+                             int rows, int H, float eps, hipStream_t s) {
+  return add_rmsnorm_splitk_any(P, S, residual, w, out, rows, H, eps, s);
+}
+
+// bf16 slabs (mgemm.hip EPI_PARTIAL16), summed in fp32 in slab order like the fp32 form
+int docqa_add_rmsnorm_splitk16(const void* P, int S, void* residual, const void* w, void* out,
+                               int rows, int H, float eps, hipStream_t s) {
+  return add_rmsnorm_splitk_any((const uint16_t*)P, S, residual, w, out, rows, H, eps, s);
 }
 
 int docqa_layernorm(const void* x, const void* residual, const void* g, const void* b, void* out,

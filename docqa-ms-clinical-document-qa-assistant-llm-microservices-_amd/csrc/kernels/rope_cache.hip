@@ -24,15 +24,34 @@ using namespace docqa;
 // compile time, so every slab load is issued before the first add (one memory latency
 // instead of S dependent ones -- the decode consumers are latency-bound at 128 rows);
 // NS == 0: runtime S.  Summation order is slab 0, 1, 2, ... either way.
-template <int N, int NS>
-__device__ __forceinline__ void load_partials(const float* P, int S, size_t slab, size_t off, float* x) {
+// 4 / 8 slab values at p as float4s: fp32 slabs, or bf16 slabs (mgemm.hip EPI_PARTIAL16)
+template <int N>
+__device__ __forceinline__ void slab_vals(const float* p, float4* a) {
+#pragma unroll
+  for (int j = 0; j < N / 4; ++j) a[j] = *reinterpret_cast<const float4*>(p + 4 * j);
+}
+template <int N>
+__device__ __forceinline__ void slab_vals(const uint16_t* p, float4* a) {
+  if constexpr (N == 4) {
+    const uint2 u = *reinterpret_cast<const uint2*>(p);
+    a[0] = float4{__uint_as_float(u.x << 16), __uint_as_float(u.x & 0xffff0000u), __uint_as_float(u.y << 16),
+                  __uint_as_float(u.y & 0xffff0000u)};
+  } else {
+    const uint4 u = *reinterpret_cast<const uint4*>(p);
+    a[0] = float4{__uint_as_float(u.x << 16), __uint_as_float(u.x & 0xffff0000u), __uint_as_float(u.y << 16),
+                  __uint_as_float(u.y & 0xffff0000u)};
+    a[1] = float4{__uint_as_float(u.z << 16), __uint_as_float(u.z & 0xffff0000u), __uint_as_float(u.w << 16),
+                  __uint_as_float(u.w & 0xffff0000u)};
+  }
+}
+
+template <int N, int NS, typename PT>
+__device__ __forceinline__ void load_partials(const PT* P, int S, size_t slab, size_t off, float* x) {
   float4 a[N / 4];
   if constexpr (NS > 0) {
     float4 p[NS][N / 4];
 #pragma unroll
-    for (int sl = 0; sl < NS; ++sl)
-#pragma unroll
-      for (int j = 0; j < N / 4; ++j) p[sl][j] = *reinterpret_cast<const float4*>(P + sl * slab + off + 4 * j);
+    for (int sl = 0; sl < NS; ++sl) slab_vals<N>(P + sl * slab + off, p[sl]);
 #pragma unroll
     for (int j = 0; j < N / 4; ++j) {
       a[j] = p[0][j];
@@ -42,12 +61,13 @@ __device__ __forceinline__ void load_partials(const float* P, int S, size_t slab
       }
     }
   } else {
+    slab_vals<N>(P + off, a);
+    for (int sl = 1; sl < S; ++sl) {
+      float4 b[N / 4];
+      slab_vals<N>(P + sl * slab + off, b);
 #pragma unroll
-    for (int j = 0; j < N / 4; ++j) {
-      a[j] = *reinterpret_cast<const float4*>(P + off + 4 * j);
-      for (int sl = 1; sl < S; ++sl) {
-        const float4 b = *reinterpret_cast<const float4*>(P + sl * slab + off + 4 * j);
-        a[j].x += b.x; a[j].y += b.y; a[j].z += b.z; a[j].w += b.w;
+      for (int j = 0; j < N / 4; ++j) {
+        a[j].x += b[j].x; a[j].y += b[j].y; a[j].z += b[j].z; a[j].w += b[j].w;
       }
     }
   }
@@ -63,12 +83,12 @@ __device__ __forceinline__ void load_partials(const float* P, int S, size_t slab
 // Grid (T, ceil(heads / heads-per-workgroup)): one head slice per thread and no loop, so
 // a 128-token decode batch is 384 workgroups (Llama-3-8B: 48 heads / 16 per workgroup)
 // instead of 128 workgroups each walking three passes.
-template <bool SPLIT, int NS>
+template <bool SPLIT, int NS, typename PT = float>
 __global__ __launch_bounds__(256) void rope_cache_kernel(
     uint16_t* __restrict__ qkv, const int* __restrict__ positions,
     const float* __restrict__ cos_sin, const int* __restrict__ slot_mapping,
     uint16_t* __restrict__ k_cache, uint16_t* __restrict__ v_cache, int Hq, int Hkv, int D,
-    int row_stride, int BS, const float* __restrict__ P, int S, size_t slab) {
+    int row_stride, int BS, const PT* __restrict__ P, int S, size_t slab) {
   const int t = blockIdx.x;
   const int tph = D >> 3;                 // threads per head
   const int heads_per_pass = 256 / tph;
@@ -147,26 +167,25 @@ int docqa_rope_cache(void* qkv, const int* positions, const float* cos_sin,
                      int Hkv, int D, int row_stride, int BS, hipStream_t s) {
   if (T == 0) return 0;
   if (D % 8 != 0 || (256 % (D / 8)) != 0) return -1;
-  rope_cache_kernel<false, 0><<<rope_grid(T, Hq, Hkv, D), 256, 0, s>>>(
+  rope_cache_kernel<false, 0, float><<<rope_grid(T, Hq, Hkv, D), 256, 0, s>>>(
       (uint16_t*)qkv, positions, cos_sin, slot_mapping, (uint16_t*)k_cache, (uint16_t*)v_cache,
       Hq, Hkv, D, row_stride, BS, nullptr, 0, 0);
   DOCQA_CHECK_LAUNCH();
   return 0;
 }
 
-// qkv_out [T, row_stride] bf16 <- rope(sum_s P[s]) ; P: [S, T, row_stride] fp32
-int docqa_rope_cache_splitk(const float* P, int S, void* qkv_out, const int* positions,
-                            const float* cos_sin, const int* slot_mapping, void* k_cache,
-                            void* v_cache, int T, int Hq, int Hkv, int D, int row_stride, int BS,
-                            hipStream_t s) {
+template <typename PT>
+static int rope_cache_splitk_any(const PT* P, int S, void* qkv_out, const int* positions, const float* cos_sin,
+                                 const int* slot_mapping, void* k_cache, void* v_cache, int T, int Hq, int Hkv,
+                                 int D, int row_stride, int BS, hipStream_t s) {
   if (T == 0) return 0;
   if (D % 8 != 0 || (256 % (D / 8)) != 0 || S < 1 || row_stride % 4 != 0) return -1;
   const dim3 grid = rope_grid(T, Hq, Hkv, D);
   const size_t slab = (size_t)T * row_stride;
   uint16_t *q = (uint16_t*)qkv_out, *kc = (uint16_t*)k_cache, *vc = (uint16_t*)v_cache;
-#define DOCQA_ROPE_SPLIT(NS_)                                                                  \
-  rope_cache_kernel<true, NS_><<<grid, 256, 0, s>>>(q, positions, cos_sin, slot_mapping, kc, vc, \
-                                                    Hq, Hkv, D, row_stride, BS, P, S, slab)
+#define DOCQA_ROPE_SPLIT(NS_)                                                                      \
+  rope_cache_kernel<true, NS_, PT><<<grid, 256, 0, s>>>(q, positions, cos_sin, slot_mapping, kc, vc, \
+                                                        Hq, Hkv, D, row_stride, BS, P, S, slab)
   switch (S) {
     case 1: DOCQA_ROPE_SPLIT(1); break;
     case 2: DOCQA_ROPE_SPLIT(2); break;
@@ -181,6 +200,24 @@ int docqa_rope_cache_splitk(const float* P, int S, void* qkv_out, const int* pos
 #undef DOCQA_ROPE_SPLIT
   DOCQA_CHECK_LAUNCH();
   return 0;
+}
+
+// qkv_out [T, row_stride] bf16 <- rope(sum_s P[s]) ; P: [S, T, row_stride] fp32
+int docqa_rope_cache_splitk(const float* P, int S, void* qkv_out, const int* positions,
+                            const float* cos_sin, const int* slot_mapping, void* k_cache,
+                            void* v_cache, int T, int Hq, int Hkv, int D, int row_stride, int BS,
+                            hipStream_t s) {
+  return rope_cache_splitk_any(P, S, qkv_out, positions, cos_sin, slot_mapping, k_cache, v_cache, T, Hq, Hkv, D,
+                               row_stride, BS, s);
+}
+
+// the same from bf16 slabs (mgemm.hip EPI_PARTIAL16)
+int docqa_rope_cache_splitk16(const void* P, int S, void* qkv_out, const int* positions,
+                              const float* cos_sin, const int* slot_mapping, void* k_cache,
+                              void* v_cache, int T, int Hq, int Hkv, int D, int row_stride, int BS,
+                              hipStream_t s) {
+  return rope_cache_splitk_any((const uint16_t*)P, S, qkv_out, positions, cos_sin, slot_mapping, k_cache, v_cache,
+                               T, Hq, Hkv, D, row_stride, BS, s);
 }
 
 // Token-granular prefix reuse (engine/kv_cache.py TailCache): copy K/V rows [0, m) of a

@@ -317,6 +317,16 @@ class LlamaModel:
         small = (not decode and x.is_cuda and _PREFILL_MID and M <= ops.MID_M_MAX)
         if (decode or small) and self.layers:
             L0 = self.layers[0]
+            cascade = decode and meta.shared_len is not None
+            # bf16 split-K slabs (ops.SLAB_BF16) where the consumer is the RoPE + cache-write
+            # kernel (QKV) or the TP = 1 add + RMSNorm (O / down); the fused attention kernels
+            # that read QKV slabs themselves take fp32 only
+            s16 = decode and x.is_cuda and self.tp == 1 and ops.SLAB_BF16
+            qkv_rope = (not (meta.decode_groups is not None and meta.decode_inline and _GROUP_FUSED
+                             and meta.slot_mapping is not None) if cascade
+                        else not (meta.block_tables is not None and kv_caches
+                                  and ops.fused_decode_ok(kv_caches[0][0], meta.block_tables)))
+            b16 = {"qkv": s16 and qkv_rope, "o": s16, "down": s16}
             for k in ("qkv", "o", "down"):
                 Sg, R = ops.gemv_plan(M, *L0[k].shape) if x.is_cuda else (0, 0)
                 if Sg:
@@ -324,7 +334,9 @@ class LlamaModel:
                     plans[k] = (Sg, lambda a, w, S=Sg, R=R: ops.gemv_partial(a, w, S, R))
                     continue
                 S, c = ops.mid_plan(M, *L0[k].shape)
-                if S:
+                if S and b16[k] and S > 1:
+                    plans[k] = (S, lambda a, w, S=S, c=c: ops.mgemm_partial(a, w, S, c, bf16=True))
+                elif S:
                     plans[k] = (S, lambda a, w, S=S, c=c: (ops.mgemm_partial(a, w, S, c) if S > 1
                                                           else ops.mgemm_partial(a, w, 1, c).float()[None]))
                 else:

@@ -286,17 +286,27 @@ def mid_plan(M: int, N: int, K: int, glu: bool = False) -> tuple[int, int]:
     return S, _MID_CFG
 
 
-def mgemm_partial(x, w, splits: int, cfg: int = 0):
-    """Split-K partial slabs [S, M, N] fp32 of x @ w^T on the mid-M decode GEMM (S = 1:
-    the bf16 product [M, N])."""
+# bf16 split-K slabs for the mid-M decode GEMM's fused consumers (RoPE + cache write, add +
+# RMSNorm) at TP = 1: half the slab bytes the GEMM writes and its consumer reads; each
+# partial is rounded to bf16 once before the consumer's fp32 sum (as a bf16 all-reduce
+# rounds each rank's partial)
+SLAB_BF16 = os.environ.get("DOCQA_SLAB_BF16", "1") == "1"
+
+
+def mgemm_partial(x, w, splits: int, cfg: int = 0, bf16: bool = False):
+    """Split-K partial slabs [S, M, N] fp32 (``bf16``: bf16) of x @ w^T on the mid-M decode
+    GEMM (S = 1 without ``bf16``: the bf16 product [M, N])."""
     if _gpu(x):
+        if bf16:
+            return _native().mgemm_slab16(x.contiguous(), w, splits, cfg)
         return _native().mgemm(x.contiguous(), w, splits, cfg)
-    if splits == 1:
+    if splits == 1 and not bf16:
         return torch.nn.functional.linear(x, w)
     K = w.shape[1]
     xs = x.float().reshape(-1, splits, K // splits)
     ws = w.float().reshape(-1, splits, K // splits)
-    return torch.einsum("msk,nsk->smn", xs, ws).contiguous()
+    out = torch.einsum("msk,nsk->smn", xs, ws).contiguous()
+    return out.to(torch.bfloat16) if bf16 else out
 
 
 def pgemm_partial(x, w, splits: int):
@@ -698,7 +708,7 @@ def add_rmsnorm_splitk(P, residual, w, eps: float):
     """residual <- residual + bf16(sum_s P[s]); returns rmsnorm(residual) * w."""
     if _gpu(P):
         return _native().add_rmsnorm_splitk(P, residual, w, eps)
-    return ref.add_rmsnorm(P.sum(0).to(residual.dtype).view_as(residual), residual, w, eps)
+    return ref.add_rmsnorm(P.float().sum(0).to(residual.dtype).view_as(residual), residual, w, eps)
 
 
 def paged_decode_fused(P, positions, cos_sin, slot_mapping, k_cache, v_cache, block_tables,
@@ -742,7 +752,7 @@ def rope_cache_splitk(P, positions, cos_sin, slot_mapping, k_cache, v_cache, Hq,
             k_cache = v_cache = P
         return _native().rope_cache_splitk(P, positions, cos_sin, slot_mapping, k_cache, v_cache, Hq, Hkv, D)
     # the model dtype: bf16 on the GPU path, fp32 for CPU reference models
-    qkv = P.sum(0).to(k_cache.dtype if slot_mapping is not None else torch.bfloat16)
+    qkv = P.float().sum(0).to(k_cache.dtype if slot_mapping is not None else torch.bfloat16)
     ref.rope_cache(qkv, positions, cos_sin, slot_mapping, k_cache, v_cache, Hq, Hkv, D)
     return qkv
 

@@ -186,7 +186,7 @@ def tp_add_rmsnorm(x: torch.Tensor, residual: torch.Tensor, w: torch.Tensor, eps
         return _CUSTOM_AR.reduce_add_rmsnorm(x, residual, w, eps)
     # fp32 slabs are summed across the group in fp32 and rounded once, as the TP = 1 GEMM
     # rounds its fp32 accumulator once (rounding each rank's partial first flips bf16 ties)
-    y = x.sum(0) if slabs else x.contiguous()
+    y = x.float().sum(0) if slabs else x.contiguous()
     dist.all_reduce(y, group=s.tp_group)
     return ops.add_rmsnorm(y.to(residual.dtype), residual, w, eps)
 

@@ -494,3 +494,24 @@ def test_grouped_decode_window_follows_the_rows_not_the_table():
     assert g_fit is not g_long and g_fit.groups_fit and not g_long.groups_fit
     assert short._get_graph(4, True, True, False).groups_fit      # a narrow table always fits
     assert not long_.group_without_prefix(64, fit=False)
+
+
+def test_mgemm_partial_bf16_slabs_cpu():
+    """bf16 split-K slabs (ops.SLAB_BF16): each slab is the fp32 slab rounded once, and the
+    consumers sum them in fp32."""
+    import torch
+    from docqa_amd import ops
+
+    g = torch.Generator().manual_seed(0)
+    x = torch.randn(8, 256, generator=g).bfloat16()
+    w = (torch.randn(64, 256, generator=g) / 16).bfloat16()
+    P32 = ops.mgemm_partial(x, w, 4)
+    P16 = ops.mgemm_partial(x, w, 4, bf16=True)
+    assert P16.dtype == torch.bfloat16 and P16.shape == (4, 8, 64)
+    assert torch.equal(P16, P32.bfloat16())
+    res = torch.randn(8, 64, generator=g).bfloat16()
+    gam = torch.ones(64).bfloat16()
+    r1, r2 = res.clone(), res.clone()
+    o16 = ops.add_rmsnorm_splitk(P16, r1, gam, 1e-5)
+    o32 = ops.add_rmsnorm_splitk(P16.float(), r2, gam, 1e-5)
+    assert torch.equal(o16, o32) and torch.equal(r1, r2)

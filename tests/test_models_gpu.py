@@ -167,11 +167,15 @@ def test_llama_prefill_trim_last_layer(native, monkeypatch):
         assert torch.equal(a, b)
 
 
-def test_llama_mid_batch_decode_native_vs_reference(native):
-    """A 256-row decode step (the mid-M GEMM path: split-K QKV / O / down slabs, fused
-    SwiGLU, fused LM-head argmax) against the same step on the fp32 reference ops."""
+@pytest.mark.parametrize("slab16", [False, True])
+def test_llama_mid_batch_decode_native_vs_reference(native, monkeypatch, slab16):
+    """A 256-row decode step (the mid-M GEMM path: split-K QKV / O / down slabs -- fp32, or
+    bf16 with ``slab16`` (ops.SLAB_BF16) -- fused SwiGLU, fused LM-head argmax) against the
+    same step on the fp32 reference ops."""
     from docqa_amd.engine.kv_cache import KVCache
     from docqa_amd.models.llama import LlamaConfig, LlamaModel
+
+    monkeypatch.setattr(native, "SLAB_BF16", slab16)
 
     m = LlamaModel(LlamaConfig.preset("llama3-1b-test"), device="cuda", seed=5)
     assert native.mid_plan(256, *m.layers[0]["qkv"].shape)[0] > 0
