@@ -321,11 +321,12 @@ class LlamaModel:
             # bf16 split-K slabs (ops.SLAB_BF16) where the consumer is the RoPE + cache-write
             # kernel (QKV) or the TP = 1 add + RMSNorm (O / down); the fused attention kernels
             # that read QKV slabs themselves take fp32 only
-            s16 = decode and x.is_cuda and self.tp == 1 and ops.SLAB_BF16
-            qkv_rope = (not (meta.decode_groups is not None and meta.decode_inline and _GROUP_FUSED
-                             and meta.slot_mapping is not None) if cascade
-                        else not (meta.block_tables is not None and kv_caches
-                                  and ops.fused_decode_ok(kv_caches[0][0], meta.block_tables)))
+            s16 = x.is_cuda and self.tp == 1 and ops.SLAB_BF16
+            qkv_rope = (not decode or
+                        (not (meta.decode_groups is not None and meta.decode_inline and _GROUP_FUSED
+                              and meta.slot_mapping is not None) if cascade
+                         else not (meta.block_tables is not None and kv_caches
+                                   and ops.fused_decode_ok(kv_caches[0][0], meta.block_tables))))
             b16 = {"qkv": s16 and qkv_rope, "o": s16, "down": s16}
             for k in ("qkv", "o", "down"):
                 Sg, R = ops.gemv_plan(M, *L0[k].shape) if x.is_cuda else (0, 0)
@@ -365,10 +366,11 @@ class LlamaModel:
             if self.layers and x.is_cuda and not decode:
                 # 513..2048-token prefills: split-K slab plans where they win with the consumer
                 L0 = self.layers[0]
+                s16 = self.tp == 1 and ops.SLAB_BF16      # bf16 slabs: see the decode plans above
                 for k in ("qkv", "o", "down"):
                     S, c = ops.prefill_plan(M, *L0[k].shape)
                     if S >= 2:
-                        plans[k] = (S, lambda a, w, S=S, c=c: ops.mgemm_partial(a, w, S, c))
+                        plans[k] = (S, lambda a, w, S=S, c=c, b=s16: ops.mgemm_partial(a, w, S, c, bf16=b))
                     elif not S:
                         # narrow tensor-parallel shards: the 256 x 256 tiles split over K
                         Sp = ops.prefill_split_plan(M, *L0[k].shape)
