@@ -184,12 +184,16 @@ at::Tensor rope_cache_splitk(const at::Tensor& P, const at::Tensor& positions, c
 // -> [T, I] bf16 silu(gate) * up
 at::Tensor silu_mul_splitk(const at::Tensor& P) {
   CHECK_GPU(P); CHECK_CONTIG(P); CHECK_ALIGN16(P);
-  TORCH_CHECK(P.scalar_type() == at::kFloat && P.dim() == 3, "silu_mul_splitk: float32 [S, T, 2I]");
+  TORCH_CHECK((P.scalar_type() == at::kFloat || P.scalar_type() == at::kBFloat16) && P.dim() == 3,
+              "silu_mul_splitk: float32 or bf16 [S, T, 2I]");
   const int S = P.size(0), T = P.size(1), I2 = P.size(2);
   TORCH_CHECK(I2 % 16 == 0, "silu_mul_splitk: 2I % 16");
   c10::DeviceGuard g(P.device());
   auto out = at::empty({T, I2 / 2}, P.options().dtype(at::kBFloat16));
-  CHECK_RC(docqa_silu_mul_splitk(P.data_ptr<float>(), out.data_ptr(), S, T, I2 / 2, stream()), "silu_mul_splitk");
+  if (P.scalar_type() == at::kBFloat16)
+    CHECK_RC(docqa_silu_mul_splitk16(P.data_ptr(), out.data_ptr(), S, T, I2 / 2, stream()), "silu_mul_splitk");
+  else
+    CHECK_RC(docqa_silu_mul_splitk(P.data_ptr<float>(), out.data_ptr(), S, T, I2 / 2, stream()), "silu_mul_splitk");
   return out;
 }
 

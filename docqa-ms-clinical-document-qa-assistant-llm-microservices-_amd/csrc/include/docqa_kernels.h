@@ -20,6 +20,7 @@ int docqa_rope_cache(void* qkv, const int* positions, const float* cos_sin,
                      int Hkv, int D, int row_stride, int BS, hipStream_t s);
 
 int docqa_silu_mul(const void* gu, void* out, int T, int I, int interleaved, hipStream_t s);
+int docqa_silu_mul_splitk16(const void* P, void* out, int S, int T, int I, hipStream_t s);
 int docqa_silu_mul_splitk(const float* P, void* out, int S, int T, int I, hipStream_t s);
 int docqa_bias_act(const void* x, const void* bias, const void* res, void* out, int T, int N,
                    int gelu, hipStream_t s);

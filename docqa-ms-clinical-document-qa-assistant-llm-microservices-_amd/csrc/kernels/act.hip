@@ -69,6 +69,56 @@ __global__ __launch_bounds__(256) void silu_mul_splitk_kernel(const float* __res
   }
 }
 
+// the same from bf16 slabs (mgemm.hip EPI_PARTIAL16: the batch-256 decode gate|up on 256-wide
+// tiles split over K, X re-read half as often as the fused-SwiGLU 128-wide tiles).  NS > 0:
+// S known at compile time, every slab load in flight before the first add; sum in fp32 in
+// slab order.
+template <int NS>
+__global__ __launch_bounds__(256) void silu_mul_splitk16_kernel(const uint16_t* __restrict__ P,
+                                                                uint16_t* __restrict__ out, int S, int T, int I) {
+  const int cpr = I >> 3;
+  const int total = T * cpr;
+  const size_t slab8 = (size_t)T * (size_t)(2 * I) / 8;   // one slab in uint4
+  for (int idx = blockIdx.x * blockDim.x + threadIdx.x; idx < total; idx += gridDim.x * blockDim.x) {
+    const int t = idx / cpr;
+    const int c = idx - t * cpr;
+    const uint4* p = reinterpret_cast<const uint4*>(P + (size_t)t * (size_t)(2 * I)) + 2 * c;
+    float g[8], u[8];
+    if constexpr (NS > 0) {
+      uint4 a[NS], b[NS];
+#pragma unroll
+      for (int sl = 0; sl < NS; ++sl) {
+        a[sl] = p[sl * slab8];
+        b[sl] = p[sl * slab8 + 1];
+      }
+      unpack8(a[0], g);
+      unpack8(b[0], u);
+#pragma unroll
+      for (int sl = 1; sl < NS; ++sl) {
+        float g2[8], u2[8];
+        unpack8(a[sl], g2);
+        unpack8(b[sl], u2);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) { g[j] += g2[j]; u[j] += u2[j]; }
+      }
+    } else {
+      unpack8(p[0], g);
+      unpack8(p[1], u);
+      for (int sl = 1; sl < S; ++sl) {
+        float g2[8], u2[8];
+        unpack8(p[sl * slab8], g2);
+        unpack8(p[sl * slab8 + 1], u2);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) { g[j] += g2[j]; u[j] += u2[j]; }
+      }
+    }
+    float o[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) o[j] = silu(bf2f(f2bf(g[j]))) * bf2f(f2bf(u[j]));
+    reinterpret_cast<uint4*>(out + (size_t)t * I)[c] = pack8(o);
+  }
+}
+
 template <bool GELU, bool RES>
 __global__ __launch_bounds__(256) void bias_act_kernel(const uint16_t* __restrict__ x,
                                                        const uint16_t* __restrict__ bias,
@@ -117,6 +167,22 @@ int docqa_silu_mul_splitk(const float* P, void* out, int S, int T, int I, hipStr
   if (T == 0) return 0;
   if (!docqa_aligned16(P) || !docqa_aligned16(out)) return -1;
   silu_mul_splitk_kernel<<<grid_for((size_t)T * (I / 8)), 256, 0, s>>>(P, (uint16_t*)out, S, T, I);
+  DOCQA_CHECK_LAUNCH();
+  return 0;
+}
+
+int docqa_silu_mul_splitk16(const void* P, void* out, int S, int T, int I, hipStream_t s) {
+  if (I % 8 != 0 || S < 1 || (long long)T * (I / 8) >= (1LL << 31)) return -1;
+  if (T == 0) return 0;
+  if (!docqa_aligned16(P) || !docqa_aligned16(out)) return -1;
+  const uint16_t* p = (const uint16_t*)P;
+  uint16_t* o = (uint16_t*)out;
+  const dim3 g = grid_for((size_t)T * (I / 8));
+  switch (S) {
+    case 2: silu_mul_splitk16_kernel<2><<<g, 256, 0, s>>>(p, o, S, T, I); break;
+    case 4: silu_mul_splitk16_kernel<4><<<g, 256, 0, s>>>(p, o, S, T, I); break;
+    default: silu_mul_splitk16_kernel<0><<<g, 256, 0, s>>>(p, o, S, T, I); break;
+  }
   DOCQA_CHECK_LAUNCH();
   return 0;
 }

@@ -359,6 +359,9 @@ class LlamaModel:
                 # 256 x 256 tiles with SwiGLU (104 vs 141 us at M = 512), or their split-K
                 # slabs into the SwiGLU consumer where too few tiles (the 70B TP-8 shard)
                 glu = ops.prefill_glu
+            elif decode and s16 and ops.glu_split16_plan(M, *L0["gate_up"].shape)[0]:
+                S2, c2 = ops.glu_split16_plan(M, *L0["gate_up"].shape)
+                glu = lambda a, w, S=S2, c=c2: ops.glu_split16(a, w, S, c)  # noqa: E731
             else:
                 glu = (lambda a, w: ops.mgemm_glu(a, w, cg)) if Sg else ops.glu_linear
         else:

@@ -326,6 +326,31 @@ def mgemm_glu(x, w_il, cfg: int = 0):
     return silu_mul(torch.nn.functional.linear(x, w_il), interleaved=True)
 
 
+# batch-256 decode gate|up as 256-wide tiles split over K into bf16 slabs + the split-K
+# SwiGLU consumer (act.hip silu_mul_splitk16) instead of the fused-SwiGLU 128-wide tiles: X
+# is re-read from L2 112 instead of 224 times (scripts/gateup_split_probe.py, cold weights:
+# GEMM 64.3 us at cfg 6 S=2 vs 78.8 us fused)
+_GLU_SPLIT16 = os.environ.get("DOCQA_GLU_SPLIT16", "0") == "1"
+
+
+def glu_split16_plan(M: int, N: int, K: int) -> tuple[int, int]:
+    """(S, cfg) of the split bf16-slab gate|up (:func:`glu_split16`) for an [M, K] x [N, K]^T
+    gate|up at TP = 1, or (0, 0): one 256-row m-tile (193..256 rows), 256-wide tiles, two K
+    slices -- (N / 256) x 2 workgroups must fit one round of the chip."""
+    if not (SLAB_BF16 and _GLU_SPLIT16) or not (193 <= M <= 256):
+        return 0, 0
+    if N % 256 or K % 256 or (N // 256) * 2 > 256:
+        return 0, 0
+    return 2, 6
+
+
+def glu_split16(x, w_il, S: int, cfg: int):
+    """silu(x Wg^T) * (x Wu^T) from S bf16 split-K slabs (mgemm cfg ``cfg``)."""
+    if _gpu(x):
+        return _native().silu_mul_splitk(_native().mgemm_slab16(x.contiguous(), w_il, S, cfg))
+    return silu_mul(torch.nn.functional.linear(x, w_il), interleaved=True)
+
+
 # ----------------------------------------------------------------------------- prefill GEMM
 _PGEMM_OFF = os.environ.get("DOCQA_PGEMM", "1") == "0"
 # below this many 256 x 256 tiles the 128 x 128 encoder GEMM (gemm.hip, 4x the workgroups)

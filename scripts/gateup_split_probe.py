@@ -2,9 +2,13 @@
 fused-SwiGLU mid-M GEMM (mgemm cfg 2, S = 1, 224 workgroups, X re-read 224 times) against
 256-wide tiles split over K into bf16 slabs (X re-read 112 times; the SwiGLU moves to a
 split-K consumer).  Weights rotate over 4 copies (past the 256 MB MALL).  GPU only."""
-import torch
+import sys
+from pathlib import Path
 
-from docqa_amd import ops
+sys.path.insert(0, str(Path(__file__).resolve().parents[1]))
+import torch  # noqa: E402
+
+from docqa_amd import ops  # noqa: E402
 
 assert ops.load_native()
 nat = torch.ops.docqa

@@ -167,8 +167,8 @@ def test_llama_prefill_trim_last_layer(native, monkeypatch):
         assert torch.equal(a, b)
 
 
-@pytest.mark.parametrize("slab16", [False, True])
-def test_llama_mid_batch_decode_native_vs_reference(native, monkeypatch, slab16):
+@pytest.mark.parametrize("slab16,glu16", [(False, False), (True, False), (True, True)])
+def test_llama_mid_batch_decode_native_vs_reference(native, monkeypatch, slab16, glu16):
     """A 256-row decode step (the mid-M GEMM path: split-K QKV / O / down slabs -- fp32, or
     bf16 with ``slab16`` (ops.SLAB_BF16) -- fused SwiGLU, fused LM-head argmax) against the
     same step on the fp32 reference ops."""
@@ -176,6 +176,7 @@ def test_llama_mid_batch_decode_native_vs_reference(native, monkeypatch, slab16)
     from docqa_amd.models.llama import LlamaConfig, LlamaModel
 
     monkeypatch.setattr(native, "SLAB_BF16", slab16)
+    monkeypatch.setattr(native, "_GLU_SPLIT16", glu16)
 
     m = LlamaModel(LlamaConfig.preset("llama3-1b-test"), device="cuda", seed=5)
     assert native.mid_plan(256, *m.layers[0]["qkv"].shape)[0] > 0

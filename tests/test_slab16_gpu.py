@@ -74,3 +74,22 @@ def test_rope_cache_splitk16(native):
     rot = torch.cat([x1 * c - x2 * s, x2 * c + x1 * s], -1)
     assert (q16.float().view(T, -1, D)[:, : Hq + Hkv] - rot).abs().max().item() < 5e-2
     assert torch.equal(q16.view(T, -1, D)[:, Hq + Hkv:].float(), x[:, Hq + Hkv:])
+
+
+@pytest.mark.parametrize("M", [193, 256])
+def test_glu_split16(native, M):
+    """Batch-256 gate|up on 256-wide tiles split over K into bf16 slabs + the bf16 split-K
+    SwiGLU consumer, against the fp32 reference and bit-exact against the fp32-slab consumer
+    fed the same bf16 partials."""
+    K, I = 4096, 14336
+    x = torch.randn(M, K, device="cuda").bfloat16()
+    w = (torch.randn(2 * I, K, device="cuda") / K ** 0.5).bfloat16()
+    P16 = torch.ops.docqa.mgemm_slab16(x, w, 2, 6)
+    o16 = torch.ops.docqa.silu_mul_splitk(P16)
+    o32 = torch.ops.docqa.silu_mul_splitk(P16.float())
+    assert torch.equal(o16, o32)
+    assert torch.equal(native.glu_split16(x, w, 2, 6), o16)
+    gu = (x.float() @ w.float().T).view(M, -1, 2, 8)
+    ref = (torch.nn.functional.silu(gu[:, :, 0]) * gu[:, :, 1]).reshape(M, I)
+    err = (o16.float() - ref).abs().max().item()
+    assert err <= 3e-2 + 2e-2 * ref.abs().max().item()
